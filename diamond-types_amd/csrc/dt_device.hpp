@@ -1,0 +1,58 @@
+// dt_device.hpp -- host/device shared layout of a staged batch (see dt_replay.hip).
+#pragma once
+#include <stdint.h>
+
+#include "dt_host.hpp"
+
+namespace dtgpu {
+
+// Per-document descriptor (device resident).  Offsets index the batch arenas.
+struct DocDesc {
+    uint64_t cmd_off;       // into cmds (Cmd units)
+    uint64_t lv_off;        // into per-LV arenas (cbyte, st, blk, slot, aux, orr)
+    uint64_t content_off;   // into content (bytes)
+    uint64_t arun_off;      // into aruns (uint32 units)
+    uint64_t blk_off;       // into items (blocks of 64 uint32)
+    uint64_t out_off;       // into out (bytes)
+    uint64_t gidx_off;      // into gidx (bytes), large-document tier only
+    uint32_t ncmd, n_lv, n_aruns, max_blocks, out_cap, content_len;
+};
+
+struct DocResult {
+    uint32_t status, out_len;
+    uint64_t hash;
+    uint32_t n_items, n_blocks;
+};
+
+struct BatchParams {
+    const Cmd *cmds;
+    const uint32_t *cbyte;
+    const uint8_t *content;
+    const uint32_t *aruns;
+    uint8_t *st;
+    uint32_t *blk;
+    uint8_t *slot;
+    uint32_t *aux;
+    uint32_t *orr;
+    uint32_t *items;
+    uint8_t *out;
+    uint8_t *gidx;
+    const DocDesc *docs;
+    const uint32_t *doc_list;
+    uint32_t n_list;
+    uint32_t lds_blocks;    // block-index capacity held in LDS (small tier)
+    uint32_t *counter;      // work-queue head, zeroed before each launch
+    DocResult *results;
+};
+
+// Bytes of a block index for `mb` blocks (mvis, mlive: u64; ord, opos: u32; bcnt: u8; per
+// superblock svis, scnt: u32), 16-byte aligned.
+inline uint64_t index_bytes(uint64_t mb) {
+    const uint64_t nsb = (mb + 63) / 64;
+    return ((24 * mb + 8 * nsb + mb) + 15) & ~uint64_t(15);
+}
+
+// Launch both tiers on `stream` (hipStream_t).  small/large lists index docs[].
+int launch_replay(const BatchParams &small, const BatchParams &large, void *stream, int n_cu);
+
+}  // namespace dtgpu

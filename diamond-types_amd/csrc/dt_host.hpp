@@ -1,0 +1,95 @@
+// dt_host.hpp -- host-side model of a diamond-types list oplog for the MI355X engine:
+// the `.dt` decoder and the causal-graph walk planner that feed the device replay.
+//
+// The oplog is kept as SoA runs (not the reference's RleVec<KVPair<..>> trees):
+//   OpRun     <- ListOpMetrics runs   (src/list/op_metrics.rs:22-42), split at graph-entry
+//                boundaries so that every run is a linear chain of LVs
+//   AgentRun  <- client_with_localtime (src/causalgraph/agent_assignment/mod.rs:29-45)
+//   GraphEntry<- GraphEntryInternal   (src/causalgraph/graph/mod.rs:25-53)
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace dtgpu {
+
+enum Status : int {
+    OK = 0, InvalidMagic = 1, UnsupportedProtocolVersion = 2, DocIdMismatch = 3, BaseVersionUnknown = 4,
+    UnknownChunk = 5, LZ4DecoderNeeded = 6, LZ4DecompressionError = 7, CompressedDataMissing = 8,
+    InvalidChunkHeader = 9, MissingChunk = 10, InvalidLength = 11, UnexpectedEOF = 12, InvalidUTF8 = 13,
+    InvalidRemoteID = 14, InvalidVarInt = 15, InvalidContent = 16, GenericInvalidData = 17,
+    ChecksumFailed = 18, DataMissing = 19,
+    ErrCheckout = 64, ErrCapacity = 65, ErrHip = 66, ErrArg = 67, ErrNoDevice = 68,
+};
+
+struct OpRun {            // a run of LVs [lv, lv+len) of one kind inside one graph entry
+    uint64_t lv, len;
+    uint64_t pos;         // Ins: position of the first char. Del fwd: start. Del rev: span start
+    uint8_t kind;         // 0 Ins, 1 Del
+    uint8_t fwd;          // Del only: 1 forward, 0 reversed (backspace)
+};
+
+struct AgentRun { uint64_t lv, len; uint32_t agent; uint64_t seq; };
+struct SeqRun { uint64_t seq, lv, len; };
+
+struct GraphEntry {
+    uint64_t start, end, shadow;
+    std::vector<uint64_t> parents;   // sorted
+};
+
+struct Graph {
+    std::vector<GraphEntry> entries;
+    int64_t find_idx(uint64_t lv) const;
+    void push(const std::vector<uint64_t> &parents, uint64_t start, uint64_t end);
+    // Graph::diff_rev (src/causalgraph/graph/tools.rs:176-292); spans descending.
+    void diff_rev(const std::vector<uint64_t> &a, const std::vector<uint64_t> &b,
+                  std::vector<std::pair<uint64_t, uint64_t>> &only_a,
+                  std::vector<std::pair<uint64_t, uint64_t>> &only_b) const;
+};
+
+struct HostOpLog {
+    std::vector<std::string> agent_names;
+    std::vector<std::vector<SeqRun>> agent_seqs;   // per agent, seq -> LV
+    std::vector<AgentRun> agent_runs;              // LV order
+    std::vector<OpRun> ops;                        // LV order, contiguous, split at entries
+    std::vector<uint8_t> ins_content;              // UTF-8 of inserted chars in LV order
+    std::vector<uint32_t> ins_cbyte;               // per LV: byte offset of its char (Ins), else ~0
+    bool content_complete = true;                  // every insert has known content
+    Graph graph;
+    std::vector<uint64_t> version;                 // cg.version (frontier)
+    uint64_t n_lv = 0;
+
+    int32_t agent_id(const char *name, size_t len);          // get_or_create_agent_id
+    uint64_t next_seq(uint32_t agent) const;
+    int64_t seq_to_lv(uint32_t agent, uint64_t seq) const;
+    void assign(uint32_t agent, uint64_t seq, uint64_t lv, uint64_t len);
+    void push_ins(uint64_t pos, const uint8_t *utf8, size_t nbytes, uint64_t nchars, bool known);
+    void push_del(uint64_t pos, uint64_t len, bool fwd);
+    void add_span(uint32_t agent, std::vector<uint64_t> parents, uint64_t start, uint64_t end);
+    void finish();                                 // split op runs at graph-entry boundaries
+};
+
+// ListOpLog::load_from (src/list/encoding/decode_oplog.rs:447-960)
+Status decode_dt(const uint8_t *data, size_t len, bool ignore_crc, HostOpLog &out);
+uint32_t crc32c(const uint8_t *d, size_t n);
+bool lz4_block_decompress(const uint8_t *src, size_t n, uint8_t *dst, size_t out_len);
+bool utf8_valid(const uint8_t *s, size_t n);
+inline uint32_t utf8_len(uint8_t c) { return c < 0x80 ? 1 : (c & 0xE0) == 0xC0 ? 2 : (c & 0xF0) == 0xE0 ? 3 : 4; }
+
+// Device command stream (consumed by dt_replay.hip).  One command = 16 bytes.
+enum CmdOp : uint32_t { CMD_INS = 0, CMD_DEL = 1, CMD_ADV_INS = 2, CMD_ADV_DEL = 3, CMD_RET_INS = 4, CMD_RET_DEL = 5 };
+struct Cmd { uint32_t op; uint32_t lv; uint32_t len; uint32_t pos; };   // op: bits 0-3 opcode, bit 4 fwd
+
+struct Plan {
+    std::vector<Cmd> cmds;
+    std::vector<uint32_t> agent_runs;   // triples (lv_start, name_rank, seq_start) for YjsMod tie-breaks
+    uint64_t n_steps = 0, n_retreat = 0, n_advance = 0;
+};
+
+// SpanningTreeWalker over the whole graph from ROOT (src/listmerge/txn_trace.rs:114-333) turned
+// into the device command stream (retreat / advance / apply, src/listmerge/merge.rs:564-581).
+Status build_plan(const HostOpLog &o, Plan &plan);
+
+uint64_t text_hash(const uint8_t *t, size_t n);
+
+}  // namespace dtgpu

@@ -1,0 +1,425 @@
+// dtgpu_api.cpp -- C ABI of libdtgpu (include/dtgpu.h): oplog handles, batch staging in HBM,
+// device checkout.  There is no CPU checkout path: without a HIP device every checkout call
+// returns DTGPU_ERR_NO_DEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <memory>
+#include <thread>
+#include <vector>
+
+#include "../../include/dtgpu.h"
+#include "dt_device.hpp"
+#include "dt_host.hpp"
+
+using namespace dtgpu;
+
+struct dtgpu_oplog {
+    HostOpLog o;
+};
+
+namespace {
+
+template <typename T>
+struct DevBuf {
+    T *p = nullptr;
+    size_t n = 0;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+    hipError_t alloc(size_t count) {
+        n = count;
+        return hipMalloc(reinterpret_cast<void **>(&p), std::max<size_t>(count, 1) * sizeof(T));
+    }
+    hipError_t upload(const std::vector<T> &v, hipStream_t s) {
+        hipError_t e = alloc(v.size());
+        if (e != hipSuccess || v.empty()) return e;
+        return hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s);
+    }
+};
+
+// Number of documents whose block index fits the LDS tier: up to 64 KiB of index per wave.
+constexpr uint64_t kLdsIndexBudget = 64 * 1024;
+
+}  // namespace
+
+struct dtgpu_batch {
+    int device = 0;
+    int n_cu = 256;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    size_t n = 0;
+    std::vector<uint32_t> host_status;   // decode / plan status per doc
+    std::vector<uint64_t> n_lv;
+    std::vector<DocDesc> docs;
+    std::vector<uint32_t> small_list, large_list;
+    uint32_t lds_blocks = 0;
+    uint64_t alg_bytes = 0, total_lv = 0;
+
+    DevBuf<Cmd> d_cmds;
+    DevBuf<uint32_t> d_cbyte, d_aruns, d_blk, d_aux, d_orr, d_items, d_lists, d_counter;
+    DevBuf<uint8_t> d_content, d_st, d_slot, d_out, d_gidx;
+    DevBuf<DocDesc> d_docs;
+    DevBuf<DocResult> d_results;
+    BatchParams small{}, large{};
+
+    ~dtgpu_batch() {
+        if (ev0) (void)hipEventDestroy(ev0);
+        if (ev1) (void)hipEventDestroy(ev1);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+namespace {
+
+struct Prepared {
+    Status status = OK;
+    HostOpLog log;
+    Plan plan;
+};
+
+void prepare_from_oplog(const HostOpLog &src, Prepared &p) {
+    p.log = src;
+    p.log.finish();
+    p.status = build_plan(p.log, p.plan);
+}
+
+int threads_for(const dtgpu_batch_opts *opts, size_t n) {
+    int t = opts && opts->host_threads > 0 ? opts->host_threads : int(std::thread::hardware_concurrency());
+    if (t < 1) t = 1;
+    if (size_t(t) > n) t = int(std::max<size_t>(n, 1));
+    return t;
+}
+
+template <typename F>
+void parallel_for(size_t n, int threads, F f) {
+    std::atomic<size_t> next{0};
+    std::vector<std::thread> pool;
+    for (int t = 0; t < threads; t++)
+        pool.emplace_back([&] { for (size_t i; (i = next.fetch_add(1)) < n;) f(i); });
+    for (auto &th : pool) th.join();
+}
+
+dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dtgpu_batch **out) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return DTGPU_ERR_NO_DEVICE;
+    auto B = std::make_unique<dtgpu_batch>();
+    B->device = opts ? opts->device : 0;
+    if (hipSetDevice(B->device) != hipSuccess) return DTGPU_ERR_HIP;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, B->device) == hipSuccess && prop.multiProcessorCount > 0)
+        B->n_cu = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&B->stream, hipStreamNonBlocking) != hipSuccess) return DTGPU_ERR_HIP;
+    if (hipEventCreate(&B->ev0) != hipSuccess || hipEventCreate(&B->ev1) != hipSuccess) return DTGPU_ERR_HIP;
+
+    const size_t n = prep.size();
+    B->n = n;
+    B->host_status.resize(n);
+    B->n_lv.resize(n);
+    B->docs.resize(n);
+    std::vector<Cmd> cmds;
+    std::vector<uint32_t> cbyte, aruns;
+    std::vector<uint8_t> content;
+    uint64_t lv_total = 0, blk_total = 0, out_total = 0, gidx_total = 0;
+    for (size_t i = 0; i < n; i++) {
+        Prepared &p = prep[i];
+        B->host_status[i] = p.status;
+        B->n_lv[i] = p.log.n_lv;
+        B->total_lv += p.log.n_lv;
+        DocDesc &d = B->docs[i];
+        std::memset(&d, 0, sizeof d);
+        if (p.status != OK) continue;
+        uint64_t n_ins = 0;
+        for (const OpRun &r : p.log.ops) if (r.kind == 0) n_ins += r.len;
+        d.cmd_off = cmds.size();
+        d.ncmd = uint32_t(p.plan.cmds.size());
+        d.lv_off = lv_total;
+        d.n_lv = uint32_t(p.log.n_lv);
+        d.content_off = content.size();
+        d.content_len = uint32_t(p.log.ins_content.size());
+        d.arun_off = aruns.size();
+        d.n_aruns = uint32_t(p.plan.agent_runs.size() / 3);
+        d.max_blocks = uint32_t(n_ins / 32 + 2);
+        d.blk_off = blk_total;
+        d.out_off = out_total;
+        d.out_cap = uint32_t(p.log.ins_content.size());
+        cmds.insert(cmds.end(), p.plan.cmds.begin(), p.plan.cmds.end());
+        cbyte.insert(cbyte.end(), p.log.ins_cbyte.begin(), p.log.ins_cbyte.end());
+        content.insert(content.end(), p.log.ins_content.begin(), p.log.ins_content.end());
+        aruns.insert(aruns.end(), p.plan.agent_runs.begin(), p.plan.agent_runs.end());
+        lv_total += p.log.n_lv;
+        blk_total += d.max_blocks;
+        out_total += d.out_cap;
+        // compulsory bytes: command stream + agent runs + per-LV content offsets + content
+        // read at materialisation + text written
+        B->alg_bytes += uint64_t(d.ncmd) * sizeof(Cmd) + uint64_t(p.plan.agent_runs.size()) * 4 +
+                        uint64_t(p.log.n_lv) * 4 + 2ull * d.content_len;
+        if (index_bytes(d.max_blocks) <= kLdsIndexBudget) {
+            B->small_list.push_back(uint32_t(i));
+            B->lds_blocks = std::max(B->lds_blocks, d.max_blocks);
+        } else {
+            d.gidx_off = gidx_total;
+            gidx_total += index_bytes(d.max_blocks);
+            B->large_list.push_back(uint32_t(i));
+        }
+    }
+    hipStream_t s = B->stream;
+#define CK(x) do { if ((x) != hipSuccess) return DTGPU_ERR_HIP; } while (0)
+    CK(B->d_cmds.upload(cmds, s));
+    CK(B->d_cbyte.upload(cbyte, s));
+    CK(B->d_aruns.upload(aruns, s));
+    CK(B->d_content.upload(content, s));
+    CK(B->d_docs.upload(B->docs, s));
+    std::vector<uint32_t> lists(B->small_list);
+    lists.insert(lists.end(), B->large_list.begin(), B->large_list.end());
+    CK(B->d_lists.upload(lists, s));
+    CK(B->d_st.alloc(lv_total));
+    CK(B->d_blk.alloc(lv_total));
+    CK(B->d_slot.alloc(lv_total));
+    CK(B->d_aux.alloc(lv_total));
+    CK(B->d_orr.alloc(lv_total));
+    CK(B->d_items.alloc(blk_total * 64));
+    CK(B->d_out.alloc(out_total));
+    CK(B->d_gidx.alloc(gidx_total));
+    CK(B->d_counter.alloc(2));
+    CK(B->d_results.alloc(n));
+    CK(hipMemsetAsync(B->d_results.p, 0, std::max<size_t>(n, 1) * sizeof(DocResult), s));
+    CK(hipStreamSynchronize(s));
+#undef CK
+    BatchParams base{};
+    base.cmds = B->d_cmds.p;
+    base.cbyte = B->d_cbyte.p;
+    base.content = B->d_content.p;
+    base.aruns = B->d_aruns.p;
+    base.st = B->d_st.p;
+    base.blk = B->d_blk.p;
+    base.slot = B->d_slot.p;
+    base.aux = B->d_aux.p;
+    base.orr = B->d_orr.p;
+    base.items = B->d_items.p;
+    base.out = B->d_out.p;
+    base.gidx = B->d_gidx.p;
+    base.docs = B->d_docs.p;
+    base.results = B->d_results.p;
+    B->small = base;
+    B->small.doc_list = B->d_lists.p;
+    B->small.n_list = uint32_t(B->small_list.size());
+    B->small.lds_blocks = B->lds_blocks;
+    B->small.counter = B->d_counter.p;
+    B->large = base;
+    B->large.doc_list = B->d_lists.p + B->small_list.size();
+    B->large.n_list = uint32_t(B->large_list.size());
+    B->large.counter = B->d_counter.p + 1;
+    *out = B.release();
+    return DTGPU_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+// ---- oplog ----------------------------------------------------------------------------------
+dtgpu_status dtgpu_oplog_load(const uint8_t *bytes, size_t len, int ignore_crc, dtgpu_oplog **out) {
+    if (!out || (!bytes && len)) return DTGPU_ERR_ARG;
+    auto h = std::make_unique<dtgpu_oplog>();
+    Status s = decode_dt(bytes, len, ignore_crc != 0, h->o);
+    if (s != OK) { *out = nullptr; return dtgpu_status(s); }
+    *out = h.release();
+    return DTGPU_OK;
+}
+dtgpu_oplog *dtgpu_oplog_new(void) { return new dtgpu_oplog(); }
+void dtgpu_oplog_free(dtgpu_oplog *o) { delete o; }
+int32_t dtgpu_oplog_get_or_create_agent_id(dtgpu_oplog *o, const char *name, size_t len) {
+    if (!o || (!name && len)) return -1;
+    return o->o.agent_id(name, len);
+}
+static bool parents_ok(const HostOpLog &o, const uint64_t *parents, size_t np) {
+    for (size_t i = 0; i < np; i++) if (parents[i] >= o.n_lv) return false;
+    return true;
+}
+int64_t dtgpu_oplog_add_insert_at(dtgpu_oplog *h, int32_t agent, const uint64_t *parents, size_t np,
+                                  uint64_t pos, const char *utf8, size_t nbytes) {
+    if (!h || agent < 0 || size_t(agent) >= h->o.agent_names.size() || !parents_ok(h->o, parents, np)) return -1;
+    const uint8_t *s = reinterpret_cast<const uint8_t *>(utf8);
+    if (nbytes && !utf8_valid(s, nbytes)) return -1;
+    uint64_t nchars = 0;
+    for (size_t i = 0; i < nbytes; i += utf8_len(s[i])) nchars++;
+    const uint64_t start = h->o.n_lv;
+    if (!nchars) return int64_t(start) - 1;
+    h->o.push_ins(pos, s, nbytes, nchars, true);
+    h->o.add_span(uint32_t(agent), std::vector<uint64_t>(parents, parents + np), start, start + nchars);
+    return int64_t(start + nchars - 1);
+}
+int64_t dtgpu_oplog_add_delete_at(dtgpu_oplog *h, int32_t agent, const uint64_t *parents, size_t np,
+                                  uint64_t del_start, uint64_t del_end) {
+    if (!h || agent < 0 || size_t(agent) >= h->o.agent_names.size() || !parents_ok(h->o, parents, np)) return -1;
+    const uint64_t start = h->o.n_lv;
+    if (del_end <= del_start) return int64_t(start) - 1;
+    h->o.push_del(del_start, del_end - del_start, true);
+    h->o.add_span(uint32_t(agent), std::vector<uint64_t>(parents, parents + np), start, start + (del_end - del_start));
+    return int64_t(h->o.n_lv - 1);
+}
+int64_t dtgpu_oplog_add_insert(dtgpu_oplog *h, int32_t agent, uint64_t pos, const char *utf8, size_t nbytes) {
+    if (!h) return -1;
+    std::vector<uint64_t> v = h->o.version;
+    return dtgpu_oplog_add_insert_at(h, agent, v.data(), v.size(), pos, utf8, nbytes);
+}
+int64_t dtgpu_oplog_add_delete_without_content(dtgpu_oplog *h, int32_t agent, uint64_t s, uint64_t e) {
+    if (!h) return -1;
+    std::vector<uint64_t> v = h->o.version;
+    return dtgpu_oplog_add_delete_at(h, agent, v.data(), v.size(), s, e);
+}
+size_t dtgpu_oplog_len(const dtgpu_oplog *h) { return h ? size_t(h->o.n_lv) : 0; }
+size_t dtgpu_oplog_local_frontier(const dtgpu_oplog *h, uint64_t *out, size_t cap) {
+    if (!h) return 0;
+    for (size_t i = 0; i < h->o.version.size() && i < cap; i++) out[i] = h->o.version[i];
+    return h->o.version.size();
+}
+
+dtgpu_status dtgpu_oplog_plan_stats(const dtgpu_oplog *h, uint64_t out[4]) {
+    if (!h || !out) return DTGPU_ERR_ARG;
+    Prepared p;
+    prepare_from_oplog(h->o, p);
+    if (p.status != OK) return dtgpu_status(p.status);
+    out[0] = p.plan.n_steps;
+    out[1] = p.plan.n_retreat;
+    out[2] = p.plan.n_advance;
+    out[3] = p.plan.cmds.size();
+    return DTGPU_OK;
+}
+
+// ---- batch ----------------------------------------------------------------------------------
+dtgpu_status dtgpu_batch_create(const uint8_t *const *docs, const size_t *lens, size_t n,
+                                const dtgpu_batch_opts *opts, dtgpu_batch **out) {
+    if (!out || (n && (!docs || !lens))) return DTGPU_ERR_ARG;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return DTGPU_ERR_NO_DEVICE;
+    std::vector<Prepared> prep(n);
+    const bool ignore_crc = opts && opts->ignore_crc;
+    parallel_for(n, threads_for(opts, n), [&](size_t i) {
+        Prepared &p = prep[i];
+        p.status = decode_dt(docs[i], lens[i], ignore_crc, p.log);
+        if (p.status == OK) p.status = build_plan(p.log, p.plan);
+    });
+    return stage(prep, opts, out);
+}
+dtgpu_status dtgpu_batch_create_from_oplogs(const dtgpu_oplog *const *oplogs, size_t n,
+                                            const dtgpu_batch_opts *opts, dtgpu_batch **out) {
+    if (!out || (n && !oplogs)) return DTGPU_ERR_ARG;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return DTGPU_ERR_NO_DEVICE;
+    std::vector<Prepared> prep(n);
+    parallel_for(n, threads_for(opts, n), [&](size_t i) { prepare_from_oplog(oplogs[i]->o, prep[i]); });
+    return stage(prep, opts, out);
+}
+dtgpu_status dtgpu_batch_run(dtgpu_batch *B, void *stream) {
+    if (!B) return DTGPU_ERR_ARG;
+    if (hipSetDevice(B->device) != hipSuccess) return DTGPU_ERR_HIP;
+    void *s = stream ? stream : reinterpret_cast<void *>(B->stream);
+    return dtgpu_status(launch_replay(B->small, B->large, s, B->n_cu));
+}
+dtgpu_status dtgpu_batch_run_timed(dtgpu_batch *B, float *ms) {
+    if (!B) return DTGPU_ERR_ARG;
+    if (hipSetDevice(B->device) != hipSuccess) return DTGPU_ERR_HIP;
+    if (hipEventRecord(B->ev0, B->stream) != hipSuccess) return DTGPU_ERR_HIP;
+    int s = launch_replay(B->small, B->large, B->stream, B->n_cu);
+    if (s) return dtgpu_status(s);
+    if (hipEventRecord(B->ev1, B->stream) != hipSuccess) return DTGPU_ERR_HIP;
+    if (hipEventSynchronize(B->ev1) != hipSuccess) return DTGPU_ERR_HIP;
+    float t = 0;
+    if (hipEventElapsedTime(&t, B->ev0, B->ev1) != hipSuccess) return DTGPU_ERR_HIP;
+    if (ms) *ms = t;
+    return DTGPU_OK;
+}
+dtgpu_status dtgpu_batch_sync(dtgpu_batch *B) {
+    if (!B) return DTGPU_ERR_ARG;
+    return hipStreamSynchronize(B->stream) == hipSuccess ? DTGPU_OK : DTGPU_ERR_HIP;
+}
+size_t dtgpu_batch_size(const dtgpu_batch *B) { return B ? B->n : 0; }
+uint64_t dtgpu_batch_algorithmic_bytes(const dtgpu_batch *B) { return B ? B->alg_bytes : 0; }
+uint64_t dtgpu_batch_total_lv(const dtgpu_batch *B) { return B ? B->total_lv : 0; }
+
+dtgpu_status dtgpu_batch_results(dtgpu_batch *B, dtgpu_doc_result *res) {
+    if (!B || (!res && B->n)) return DTGPU_ERR_ARG;
+    std::vector<DocResult> dr(B->n);
+    if (B->n && hipMemcpyAsync(dr.data(), B->d_results.p, B->n * sizeof(DocResult), hipMemcpyDeviceToHost, B->stream) != hipSuccess)
+        return DTGPU_ERR_HIP;
+    if (hipStreamSynchronize(B->stream) != hipSuccess) return DTGPU_ERR_HIP;
+    for (size_t i = 0; i < B->n; i++) {
+        res[i].status = B->host_status[i] != OK ? B->host_status[i] : dr[i].status;
+        res[i].reserved = 0;
+        res[i].text_len = res[i].status == OK ? dr[i].out_len : 0;
+        res[i].text_hash = res[i].status == OK ? dr[i].hash : 0;
+        res[i].n_lv = B->n_lv[i];
+    }
+    return DTGPU_OK;
+}
+dtgpu_status dtgpu_batch_text(dtgpu_batch *B, size_t i, uint8_t *out, size_t cap, size_t *out_len) {
+    if (!B || i >= B->n) return DTGPU_ERR_ARG;
+    if (B->host_status[i] != OK) return dtgpu_status(B->host_status[i]);
+    DocResult r;
+    if (hipMemcpyAsync(&r, B->d_results.p + i, sizeof r, hipMemcpyDeviceToHost, B->stream) != hipSuccess ||
+        hipStreamSynchronize(B->stream) != hipSuccess)
+        return DTGPU_ERR_HIP;
+    if (r.status != OK) return dtgpu_status(r.status);
+    if (out_len) *out_len = r.out_len;
+    if (!out) return DTGPU_OK;
+    if (cap < r.out_len) return DTGPU_ERR_ARG;
+    if (r.out_len && (hipMemcpyAsync(out, B->d_out.p + B->docs[i].out_off, r.out_len, hipMemcpyDeviceToHost, B->stream) != hipSuccess ||
+                      hipStreamSynchronize(B->stream) != hipSuccess))
+        return DTGPU_ERR_HIP;
+    return DTGPU_OK;
+}
+void dtgpu_batch_free(dtgpu_batch *B) { delete B; }
+
+dtgpu_status dtgpu_batch_checkout(const uint8_t *const *docs, const size_t *lens, size_t n,
+                                  const dtgpu_batch_opts *opts, dtgpu_doc_result *results) {
+    dtgpu_batch *B = nullptr;
+    dtgpu_status s = dtgpu_batch_create(docs, lens, n, opts, &B);
+    if (s) return s;
+    s = dtgpu_batch_run(B, nullptr);
+    if (!s) s = dtgpu_batch_results(B, results);
+    dtgpu_batch_free(B);
+    return s;
+}
+
+dtgpu_status dtgpu_checkout_tip(const dtgpu_oplog *h, uint8_t *out, size_t cap, size_t *out_len) {
+    if (!h) return DTGPU_ERR_ARG;
+    dtgpu_batch *B = nullptr;
+    dtgpu_status s = dtgpu_batch_create_from_oplogs(&h, 1, nullptr, &B);
+    if (s) return s;
+    s = dtgpu_batch_run(B, nullptr);
+    size_t len = 0;
+    if (!s) s = dtgpu_batch_text(B, 0, nullptr, 0, &len);
+    if (!s) {
+        if (out_len) *out_len = len;
+        if (out) s = cap < len ? DTGPU_ERR_ARG : dtgpu_batch_text(B, 0, out, cap, &len);
+    }
+    dtgpu_batch_free(B);
+    return s;
+}
+
+uint64_t dtgpu_text_hash(const uint8_t *t, size_t n) { return text_hash(t, n); }
+int dtgpu_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+const char *dtgpu_status_str(dtgpu_status s) {
+    static const char *names[] = {"OK", "InvalidMagic", "UnsupportedProtocolVersion", "DocIdMismatch",
+                                  "BaseVersionUnknown", "UnknownChunk", "LZ4DecoderNeeded", "LZ4DecompressionError",
+                                  "CompressedDataMissing", "InvalidChunkHeader", "MissingChunk", "InvalidLength",
+                                  "UnexpectedEOF", "InvalidUTF8", "InvalidRemoteID", "InvalidVarInt", "InvalidContent",
+                                  "GenericInvalidData", "ChecksumFailed", "DataMissing"};
+    if (int(s) >= 0 && int(s) < 20) return names[s];
+    switch (s) {
+        case DTGPU_ERR_CHECKOUT: return "ErrCheckout";
+        case DTGPU_ERR_CAPACITY: return "ErrCapacity";
+        case DTGPU_ERR_HIP: return "ErrHip";
+        case DTGPU_ERR_ARG: return "ErrArg";
+        case DTGPU_ERR_NO_DEVICE: return "ErrNoDevice";
+        default: return "Unknown";
+    }
+}
+
+}  // extern "C"

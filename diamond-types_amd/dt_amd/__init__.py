@@ -1,0 +1,291 @@
+"""dt_amd -- Python mirror of diamond-types' `ListOpLog` / `ListBranch` checkout surface,
+backed by libdtgpu (hand-written HIP kernels for MI355X, C ABI in include/dtgpu.h).
+
+Mirrors (reference paths under jarrodhroberson/diamond-types):
+  ListOpLog.load_from          src/list/encoding/decode_oplog.rs:447
+  ListOpLog.checkout_tip       src/list/oplog.rs:38  (device replay: dt_replay.hip)
+  ListOpLog.add_insert_at ...  src/list/oplog.rs:221-300
+  ListBranch.content / len     src/list/branch.rs:38-63
+  batch_checkout               SURVEY.md §8b batch entry
+
+There is no CPU fallback: every checkout runs the HIP kernels, and a missing library or a
+missing GPU raises immediately.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libdtgpu.so")
+
+STATUS_NAMES = {
+    0: "OK", 1: "InvalidMagic", 2: "UnsupportedProtocolVersion", 3: "DocIdMismatch", 4: "BaseVersionUnknown",
+    5: "UnknownChunk", 6: "LZ4DecoderNeeded", 7: "LZ4DecompressionError", 8: "CompressedDataMissing",
+    9: "InvalidChunkHeader", 10: "MissingChunk", 11: "InvalidLength", 12: "UnexpectedEOF", 13: "InvalidUTF8",
+    14: "InvalidRemoteID", 15: "InvalidVarInt", 16: "InvalidContent", 17: "GenericInvalidData",
+    18: "ChecksumFailed", 19: "DataMissing", 64: "ErrCheckout", 65: "ErrCapacity", 66: "ErrHip", 67: "ErrArg",
+    68: "ErrNoDevice",
+}
+
+
+class ParseError(Exception):
+    """Mirror of `ParseError` (src/encoding/parseerror.rs:14-48) plus engine statuses."""
+
+    def __init__(self, code):
+        self.code = code
+        self.name = STATUS_NAMES.get(code, str(code))
+        super().__init__(f"{self.name} ({code})")
+
+
+class DocResult(ctypes.Structure):
+    _fields_ = [("status", ctypes.c_uint32), ("reserved", ctypes.c_uint32), ("text_len", ctypes.c_uint64),
+                ("text_hash", ctypes.c_uint64), ("n_lv", ctypes.c_uint64)]
+
+
+class BatchOpts(ctypes.Structure):
+    _fields_ = [("ignore_crc", ctypes.c_int), ("host_threads", ctypes.c_int), ("device", ctypes.c_int)]
+
+
+_lib = None
+
+
+def lib():
+    """Load libdtgpu.so (fails loudly when it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libdtgpu.so not built at {LIB_PATH}; run `make -C diamond-types_amd`")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, sz, u64, i64, c = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int
+    pu64 = ctypes.POINTER(ctypes.c_uint64)
+    L.dtgpu_oplog_load.argtypes = [ctypes.c_char_p, sz, c, ctypes.POINTER(vp)]
+    L.dtgpu_oplog_new.restype = vp
+    L.dtgpu_oplog_free.argtypes = [vp]
+    L.dtgpu_oplog_get_or_create_agent_id.argtypes = [vp, ctypes.c_char_p, sz]
+    L.dtgpu_oplog_get_or_create_agent_id.restype = ctypes.c_int32
+    L.dtgpu_oplog_add_insert_at.argtypes = [vp, ctypes.c_int32, pu64, sz, u64, ctypes.c_char_p, sz]
+    L.dtgpu_oplog_add_insert_at.restype = i64
+    L.dtgpu_oplog_add_delete_at.argtypes = [vp, ctypes.c_int32, pu64, sz, u64, u64]
+    L.dtgpu_oplog_add_delete_at.restype = i64
+    L.dtgpu_oplog_add_insert.argtypes = [vp, ctypes.c_int32, u64, ctypes.c_char_p, sz]
+    L.dtgpu_oplog_add_insert.restype = i64
+    L.dtgpu_oplog_add_delete_without_content.argtypes = [vp, ctypes.c_int32, u64, u64]
+    L.dtgpu_oplog_add_delete_without_content.restype = i64
+    L.dtgpu_oplog_len.argtypes = [vp]
+    L.dtgpu_oplog_len.restype = sz
+    L.dtgpu_oplog_local_frontier.argtypes = [vp, pu64, sz]
+    L.dtgpu_oplog_local_frontier.restype = sz
+    L.dtgpu_oplog_plan_stats.argtypes = [vp, pu64]
+    L.dtgpu_checkout_tip.argtypes = [vp, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
+    L.dtgpu_batch_create.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz), sz,
+                                     ctypes.POINTER(BatchOpts), ctypes.POINTER(vp)]
+    L.dtgpu_batch_create_from_oplogs.argtypes = [ctypes.POINTER(vp), sz, ctypes.POINTER(BatchOpts), ctypes.POINTER(vp)]
+    L.dtgpu_batch_run.argtypes = [vp, vp]
+    L.dtgpu_batch_run_timed.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
+    L.dtgpu_batch_sync.argtypes = [vp]
+    L.dtgpu_batch_size.argtypes = [vp]
+    L.dtgpu_batch_size.restype = sz
+    L.dtgpu_batch_results.argtypes = [vp, ctypes.POINTER(DocResult)]
+    L.dtgpu_batch_text.argtypes = [vp, sz, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
+    L.dtgpu_batch_algorithmic_bytes.argtypes = [vp]
+    L.dtgpu_batch_algorithmic_bytes.restype = u64
+    L.dtgpu_batch_total_lv.argtypes = [vp]
+    L.dtgpu_batch_total_lv.restype = u64
+    L.dtgpu_batch_free.argtypes = [vp]
+    L.dtgpu_batch_checkout.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz), sz,
+                                       ctypes.POINTER(BatchOpts), ctypes.POINTER(DocResult)]
+    L.dtgpu_text_hash.argtypes = [ctypes.c_char_p, sz]
+    L.dtgpu_text_hash.restype = u64
+    L.dtgpu_device_count.restype = c
+    L.dtgpu_status_str.argtypes = [c]
+    L.dtgpu_status_str.restype = ctypes.c_char_p
+    _lib = L
+    return L
+
+
+def _check(code):
+    if code:
+        raise ParseError(code)
+
+
+def _u64s(xs):
+    return (ctypes.c_uint64 * max(1, len(xs)))(*xs), len(xs)
+
+
+def text_hash(data: bytes) -> int:
+    return lib().dtgpu_text_hash(data, len(data))
+
+
+class ListBranch:
+    """Result of a checkout: `ListBranch` (src/list/mod.rs:65-76) content + version."""
+
+    def __init__(self, content: bytes, version):
+        self._content = content
+        self.version = list(version)
+
+    def content(self) -> str:
+        return self._content.decode("utf-8")
+
+    def content_bytes(self) -> bytes:
+        return self._content
+
+    def __len__(self):
+        return len(self.content())
+
+    def len(self):
+        return len(self)
+
+    def local_frontier(self):
+        return list(self.version)
+
+
+class ListOpLog:
+    """Mirror of `ListOpLog` (src/list/mod.rs:103-126) for the checkout path."""
+
+    def __init__(self, _handle=None):
+        self._h = _handle if _handle is not None else lib().dtgpu_oplog_new()
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            lib().dtgpu_oplog_free(h)
+            self._h = None
+
+    @classmethod
+    def load_from(cls, data: bytes, ignore_crc: bool = False) -> "ListOpLog":
+        out = ctypes.c_void_p()
+        _check(lib().dtgpu_oplog_load(data, len(data), int(ignore_crc), ctypes.byref(out)))
+        return cls(out.value)
+
+    def __len__(self):
+        return lib().dtgpu_oplog_len(self._h)
+
+    def get_or_create_agent_id(self, name: str) -> int:
+        b = name.encode()
+        a = lib().dtgpu_oplog_get_or_create_agent_id(self._h, b, len(b))
+        if a < 0:
+            raise ValueError(f"invalid agent name {name!r}")
+        return a
+
+    def add_insert_at(self, agent: int, parents, pos: int, content: str) -> int:
+        p, n = _u64s(parents)
+        b = content.encode()
+        return lib().dtgpu_oplog_add_insert_at(self._h, agent, p, n, pos, b, len(b))
+
+    def add_delete_at(self, agent: int, parents, start: int, end: int) -> int:
+        p, n = _u64s(parents)
+        return lib().dtgpu_oplog_add_delete_at(self._h, agent, p, n, start, end)
+
+    def add_insert(self, agent: int, pos: int, content: str) -> int:
+        b = content.encode()
+        return lib().dtgpu_oplog_add_insert(self._h, agent, pos, b, len(b))
+
+    def add_delete_without_content(self, agent: int, start: int, end: int) -> int:
+        return lib().dtgpu_oplog_add_delete_without_content(self._h, agent, start, end)
+
+    def local_frontier(self):
+        buf = (ctypes.c_uint64 * 64)()
+        n = lib().dtgpu_oplog_local_frontier(self._h, buf, 64)
+        if n > 64:
+            buf = (ctypes.c_uint64 * n)()
+            lib().dtgpu_oplog_local_frontier(self._h, buf, n)
+        return list(buf[:n])
+
+    def plan_stats(self):
+        out = (ctypes.c_uint64 * 4)()
+        _check(lib().dtgpu_oplog_plan_stats(self._h, out))
+        return dict(steps=out[0], retreat=out[1], advance=out[2], commands=out[3])
+
+    def checkout_tip_bytes(self) -> bytes:
+        n = ctypes.c_size_t()
+        _check(lib().dtgpu_checkout_tip(self._h, None, 0, ctypes.byref(n)))
+        buf = ctypes.create_string_buffer(max(1, n.value))
+        _check(lib().dtgpu_checkout_tip(self._h, buf, n.value, ctypes.byref(n)))
+        return buf.raw[:n.value]
+
+    def checkout_tip(self) -> ListBranch:
+        return ListBranch(self.checkout_tip_bytes(), self.local_frontier())
+
+
+def oplog_from_trace(txns, agent_name="jeremy") -> ListOpLog:
+    """crates/bench/src/utils.rs:25-44 apply_edits_push_merge (delete then insert per patch)."""
+    o = ListOpLog()
+    a = o.get_or_create_agent_id(agent_name)
+    for txn in txns:
+        for pos, dl, ins in txn["patches"]:
+            if dl > 0:
+                o.add_delete_without_content(a, pos, pos + dl)
+            if ins:
+                o.add_insert(a, pos, ins)
+    return o
+
+
+class Batch:
+    """A batch staged in HBM (decode + plan on host threads, replay on the GPU)."""
+
+    def __init__(self, docs=None, oplogs=None, ignore_crc=False, host_threads=0, device=0):
+        L = lib()
+        opts = BatchOpts(int(ignore_crc), int(host_threads), int(device))
+        out = ctypes.c_void_p()
+        if oplogs is not None:
+            arr = (ctypes.c_void_p * max(1, len(oplogs)))(*[o._h for o in oplogs])
+            self._keep = oplogs
+            _check(L.dtgpu_batch_create_from_oplogs(arr, len(oplogs), ctypes.byref(opts), ctypes.byref(out)))
+            self.n = len(oplogs)
+        else:
+            self._keep = list(docs)
+            ptrs = (ctypes.c_char_p * max(1, len(self._keep)))(*self._keep)
+            lens = (ctypes.c_size_t * max(1, len(self._keep)))(*[len(d) for d in self._keep])
+            _check(L.dtgpu_batch_create(ptrs, lens, len(self._keep), ctypes.byref(opts), ctypes.byref(out)))
+            self.n = len(self._keep)
+        self._h = out.value
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            lib().dtgpu_batch_free(h)
+            self._h = None
+
+    def run(self, stream=None):
+        _check(lib().dtgpu_batch_run(self._h, stream))
+
+    def run_timed(self) -> float:
+        ms = ctypes.c_float()
+        _check(lib().dtgpu_batch_run_timed(self._h, ctypes.byref(ms)))
+        return ms.value
+
+    def sync(self):
+        _check(lib().dtgpu_batch_sync(self._h))
+
+    def results(self):
+        arr = (DocResult * max(1, self.n))()
+        _check(lib().dtgpu_batch_results(self._h, arr))
+        return [dict(status=r.status, text_len=r.text_len, text_hash=r.text_hash, n_lv=r.n_lv) for r in arr[:self.n]]
+
+    def text(self, i) -> bytes:
+        n = ctypes.c_size_t()
+        _check(lib().dtgpu_batch_text(self._h, i, None, 0, ctypes.byref(n)))
+        buf = ctypes.create_string_buffer(max(1, n.value))
+        _check(lib().dtgpu_batch_text(self._h, i, buf, n.value, ctypes.byref(n)))
+        return buf.raw[:n.value]
+
+    @property
+    def algorithmic_bytes(self):
+        return lib().dtgpu_batch_algorithmic_bytes(self._h)
+
+    @property
+    def total_lv(self):
+        return lib().dtgpu_batch_total_lv(self._h)
+
+
+def batch_checkout(docs, **kw):
+    """Checkout every `.dt` document in `docs`; returns (results, texts)."""
+    b = Batch(docs=docs, **kw)
+    b.run()
+    b.sync()
+    res = b.results()
+    return res, [b.text(i) if r["status"] == 0 else None for i, r in enumerate(res)]
+
+
+def device_count() -> int:
+    return lib().dtgpu_device_count()

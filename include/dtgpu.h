@@ -1,0 +1,157 @@
+/*
+ * dtgpu.h -- C ABI of the MI355X-native batch checkout engine for diamond-types oplogs.
+ *
+ * Drop-in boundary for the reference's `ListOpLog` -> `checkout_tip()` / `ListBranch::merge()`
+ * path.  Every entry point names the reference interface it replaces
+ * (paths under jarrodhroberson/diamond-types).  Plain pointers and sizes only; no torch or HIP
+ * types appear in the signatures (streams are passed as `void*` = hipStream_t).
+ *
+ * Ownership: an oplog handle is immutable once loaded except through the add_* calls; the
+ * caller owns every output buffer.  Batch handles own their device memory.  No call aborts the
+ * process: conditions on which the reference panics become DTGPU_ERR_CHECKOUT.
+ */
+#ifndef DTGPU_H
+#define DTGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Status codes.  1..19 mirror `ParseError` in declaration order
+ * (src/encoding/parseerror.rs:14-48); the rest are engine statuses. */
+typedef enum dtgpu_status {
+    DTGPU_OK = 0,
+    DTGPU_INVALID_MAGIC = 1,
+    DTGPU_UNSUPPORTED_PROTOCOL_VERSION = 2,
+    DTGPU_DOC_ID_MISMATCH = 3,
+    DTGPU_BASE_VERSION_UNKNOWN = 4,
+    DTGPU_UNKNOWN_CHUNK = 5,
+    DTGPU_LZ4_DECODER_NEEDED = 6,
+    DTGPU_LZ4_DECOMPRESSION_ERROR = 7,
+    DTGPU_COMPRESSED_DATA_MISSING = 8,
+    DTGPU_INVALID_CHUNK_HEADER = 9,
+    DTGPU_MISSING_CHUNK = 10,
+    DTGPU_INVALID_LENGTH = 11,
+    DTGPU_UNEXPECTED_EOF = 12,
+    DTGPU_INVALID_UTF8 = 13,
+    DTGPU_INVALID_REMOTE_ID = 14,
+    DTGPU_INVALID_VARINT = 15,
+    DTGPU_INVALID_CONTENT = 16,
+    DTGPU_GENERIC_INVALID_DATA = 17,
+    DTGPU_CHECKSUM_FAILED = 18,
+    DTGPU_DATA_MISSING = 19,
+    DTGPU_ERR_CHECKOUT = 64,    /* the reference would panic (merge.rs:384,489; yjsspan.rs:49-90) */
+    DTGPU_ERR_CAPACITY = 65,    /* a device-side structure overflowed its reservation */
+    DTGPU_ERR_HIP = 66,         /* HIP runtime error (no GPU, OOM, launch failure) */
+    DTGPU_ERR_ARG = 67,         /* invalid argument / buffer too small */
+    DTGPU_ERR_NO_DEVICE = 68,   /* no HIP device: the engine has no CPU fallback */
+} dtgpu_status;
+
+typedef struct dtgpu_oplog dtgpu_oplog;
+typedef struct dtgpu_batch dtgpu_batch;
+
+/* ---- ListOpLog construction -------------------------------------------------------------- */
+
+/* ListOpLog::load_from(&[u8]) -> Result<ListOpLog, ParseError>
+ * (src/list/encoding/decode_oplog.rs:447-451).  CRC-32C is verified unless ignore_crc
+ * (DecodeOptions::ignore_crc, decode_oplog.rs:428-444). */
+dtgpu_status dtgpu_oplog_load(const uint8_t *bytes, size_t len, int ignore_crc, dtgpu_oplog **out);
+
+/* ListOpLog::new() (src/list/oplog.rs:22-30) */
+dtgpu_oplog *dtgpu_oplog_new(void);
+void dtgpu_oplog_free(dtgpu_oplog *oplog);
+
+/* ListOpLog::get_or_create_agent_id (src/list/oplog.rs:44-46).  Returns -1 on a reserved or
+ * over-long name (the reference panics: agent_assignment/mod.rs:88-91). */
+int32_t dtgpu_oplog_get_or_create_agent_id(dtgpu_oplog *oplog, const char *name, size_t name_len);
+
+/* ListOpLog::add_insert_at / add_delete_at (src/list/oplog.rs:221-246).  Return the last LV
+ * of the new span (`end - 1`), or -1 on an invalid argument. */
+int64_t dtgpu_oplog_add_insert_at(dtgpu_oplog *oplog, int32_t agent, const uint64_t *parents, size_t n_parents,
+                                  uint64_t pos, const char *utf8, size_t n_bytes);
+int64_t dtgpu_oplog_add_delete_at(dtgpu_oplog *oplog, int32_t agent, const uint64_t *parents, size_t n_parents,
+                                  uint64_t del_start, uint64_t del_end);
+/* ListOpLog::add_insert / add_delete_without_content at the current version (oplog.rs:273-300) */
+int64_t dtgpu_oplog_add_insert(dtgpu_oplog *oplog, int32_t agent, uint64_t pos, const char *utf8, size_t n_bytes);
+int64_t dtgpu_oplog_add_delete_without_content(dtgpu_oplog *oplog, int32_t agent, uint64_t del_start, uint64_t del_end);
+
+/* ListOpLog::len() (src/list/oplog.rs:89-91) */
+size_t dtgpu_oplog_len(const dtgpu_oplog *oplog);
+/* ListOpLog::local_frontier() (src/list/oplog.rs:329-331).  Returns the frontier length;
+ * writes min(len, cap) LVs. */
+size_t dtgpu_oplog_local_frontier(const dtgpu_oplog *oplog, uint64_t *out, size_t cap);
+
+/* Host-side walk plan of checkout_tip for this oplog (SpanningTreeWalker over all LVs,
+ * src/listmerge/txn_trace.rs:114-333): out[0] walk steps, out[1] retreated LVs, out[2]
+ * advanced LVs, out[3] device commands.  Pure host code; usable without a GPU. */
+dtgpu_status dtgpu_oplog_plan_stats(const dtgpu_oplog *oplog, uint64_t out[4]);
+
+/* ---- checkout ------------------------------------------------------------------------------ */
+
+/* ListOpLog::checkout_tip() -> ListBranch, then ListBranch::content().to_string()
+ * (src/list/oplog.rs:38-42, src/list/merge.rs:63-95, src/list/branch.rs:38-63).
+ * Runs on the GPU.  out == NULL (or cap too small) returns the required length in *out_len
+ * (with DTGPU_ERR_ARG when a non-NULL buffer was too small). */
+dtgpu_status dtgpu_checkout_tip(const dtgpu_oplog *oplog, uint8_t *out, size_t cap, size_t *out_len);
+
+/* ---- batch checkout (SURVEY.md §8b "batch entry") ------------------------------------------ */
+
+typedef struct dtgpu_batch_opts {
+    int ignore_crc;          /* DecodeOptions::ignore_crc */
+    int host_threads;        /* decode/plan worker threads, 0 = hardware concurrency */
+    int device;              /* HIP device ordinal */
+} dtgpu_batch_opts;
+
+typedef struct dtgpu_doc_result {
+    uint32_t status;         /* dtgpu_status of this document */
+    uint32_t reserved;
+    uint64_t text_len;       /* bytes of checkout_tip().content() */
+    uint64_t text_hash;      /* dtgpu_text_hash of the content (see below) */
+    uint64_t n_lv;           /* ListOpLog::len() = merged ops of this document */
+} dtgpu_doc_result;
+
+/* Decode + plan every document on host threads and stage the batch in HBM.  Documents are
+ * `.dt` byte buffers (decode_oplog.rs:447).  Per-document failures are reported in the
+ * results, never abort the batch. */
+dtgpu_status dtgpu_batch_create(const uint8_t *const *docs, const size_t *lens, size_t n_docs,
+                                const dtgpu_batch_opts *opts, dtgpu_batch **out);
+/* Same, from already-built oplog handles (e.g. JSON traces built with add_*). */
+dtgpu_status dtgpu_batch_create_from_oplogs(const dtgpu_oplog *const *oplogs, size_t n_docs,
+                                            const dtgpu_batch_opts *opts, dtgpu_batch **out);
+/* Enqueue the device checkout of the whole batch on `stream` (hipStream_t, NULL = the batch's
+ * own stream).  Asynchronous; inputs are already resident in HBM. */
+dtgpu_status dtgpu_batch_run(dtgpu_batch *batch, void *stream);
+/* Run once, synchronously, and report device time of the replay kernels (hipEvents on the
+ * launch stream) in *kernel_ms. */
+dtgpu_status dtgpu_batch_run_timed(dtgpu_batch *batch, float *kernel_ms);
+dtgpu_status dtgpu_batch_sync(dtgpu_batch *batch);
+size_t dtgpu_batch_size(const dtgpu_batch *batch);
+/* Copy per-document results (n_docs entries) to host. */
+dtgpu_status dtgpu_batch_results(dtgpu_batch *batch, dtgpu_doc_result *results);
+/* Copy one document's merged text to host. */
+dtgpu_status dtgpu_batch_text(dtgpu_batch *batch, size_t doc, uint8_t *out, size_t cap, size_t *out_len);
+/* Bytes the replay reads + writes per run by construction (the roofline numerator). */
+uint64_t dtgpu_batch_algorithmic_bytes(const dtgpu_batch *batch);
+/* Total merged ops (sum of ListOpLog::len()) in the batch. */
+uint64_t dtgpu_batch_total_lv(const dtgpu_batch *batch);
+void dtgpu_batch_free(dtgpu_batch *batch);
+
+/* One-shot batch checkout: create + run + sync + results. */
+dtgpu_status dtgpu_batch_checkout(const uint8_t *const *docs, const size_t *lens, size_t n_docs,
+                                  const dtgpu_batch_opts *opts, dtgpu_doc_result *results);
+
+/* Order-sensitive 64-bit hash of a text: sum over byte i of splitmix64((i << 8) | byte_i),
+ * wrapping.  Computed on device for the RCCL length/hash gather; exported for checking. */
+uint64_t dtgpu_text_hash(const uint8_t *text, size_t len);
+
+/* Number of HIP devices visible (0 when there is no GPU). */
+int dtgpu_device_count(void);
+const char *dtgpu_status_str(dtgpu_status status);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DTGPU_H */

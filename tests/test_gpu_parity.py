@@ -1,0 +1,118 @@
+"""GPU parity: libdtgpu's device checkout vs the CPU oracle and the reference's golden texts.
+
+Every test calls through the C ABI (dt_amd -> libdtgpu.so -> HIP kernels).  Bit-exact bar:
+the merged text must equal the oracle's / golden bytes exactly.
+"""
+import hashlib
+
+import pytest
+
+import golden_data as G
+from oracle.oracle import OpLog as OracleOpLog, oplog_from_trace as oracle_from_trace
+
+pytestmark = pytest.mark.gpu
+
+import dt_amd  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if dt_amd.device_count() < 1:
+        pytest.fail("no HIP device visible: the engine has no CPU fallback")
+
+
+def test_friendsforever_golden():
+    o = dt_amd.ListOpLog.load_from(G.dt_bytes("friendsforever"))
+    assert len(o) == 26078
+    br = o.checkout_tip()
+    assert br.content() == G.trace("friendsforever_flat")["endContent"]
+    assert br.local_frontier() == [26077]
+
+
+@pytest.mark.parametrize("vec", [G.COMPAT_SIMPLE_1, G.COMPAT_SIMPLE_2, G.COMPAT_SIMPLE_LZ4])
+def test_compat_simple(vec):
+    assert dt_amd.ListOpLog.load_from(vec).checkout_tip().content() == "hi me"
+
+
+@pytest.mark.parametrize("vec", [G.COMPAT_EMPTY_1, G.COMPAT_EMPTY_2])
+def test_compat_empty(vec):
+    assert dt_amd.ListOpLog.load_from(vec).checkout_tip().content() == ""
+
+
+@pytest.mark.parametrize("name", ["git-makefile", "node_nodecc"])
+def test_large_docs_vs_oracle(name):
+    data = G.dt_bytes(name)
+    want = OracleOpLog.load_from(data).checkout_tip_bytes()
+    got = dt_amd.ListOpLog.load_from(data).checkout_tip_bytes()
+    assert len(got) == len(want)
+    assert hashlib.sha256(got).hexdigest() == hashlib.sha256(want).hexdigest()
+
+
+@pytest.mark.parametrize("name", G.JSON_TRACES)
+def test_json_traces_golden(name):
+    t = G.trace(name)
+    o = dt_amd.oplog_from_trace(t["txns"])
+    assert o.checkout_tip().content() == t["endContent"]
+
+
+def test_batch_friendsforever_copies():
+    data = G.dt_bytes("friendsforever")
+    want = G.trace("friendsforever_flat")["endContent"].encode()
+    b = dt_amd.Batch(docs=[bytes(data) for _ in range(300)])
+    b.run()
+    b.sync()
+    res = b.results()
+    h = dt_amd.text_hash(want)
+    assert all(r["status"] == 0 and r["text_len"] == len(want) and r["text_hash"] == h for r in res)
+    assert b.text(0) == want and b.text(299) == want
+
+
+def test_batch_mixed_and_errors():
+    docs = [G.dt_bytes("friendsforever"), b"not a dt file", G.COMPAT_SIMPLE_LZ4, G.dt_bytes("git-makefile"),
+            G.COMPAT_EMPTY_2]
+    bad = bytearray(G.COMPAT_SIMPLE_1)
+    bad[-1] ^= 0xFF
+    docs.append(bytes(bad))
+    res, texts = dt_amd.batch_checkout(docs)
+    assert [r["status"] for r in res] == [0, 1, 0, 0, 0, 18]
+    assert texts[0].decode() == G.trace("friendsforever_flat")["endContent"]
+    assert texts[2] == b"hi me" and texts[4] == b""
+    assert texts[3] == OracleOpLog.load_from(G.dt_bytes("git-makefile")).checkout_tip_bytes()
+
+
+def _kat(build):
+    g = dt_amd.ListOpLog()
+    o = OracleOpLog()
+    build(g, o)
+    return g.checkout_tip().content(), o.checkout_tip()
+
+
+def test_merge_kats():
+    def b1(g, o):
+        for x in (g, o):
+            ag = x.get_or_create_agent_id if x is g else x.agent
+            a, b = ag("a"), ag("b")
+            x.add_insert_at(a, [], 0, "aaa")
+            x.add_insert_at(b, [], 0, "bbb")
+            x.add_insert_at(a, [2, 5], 0, "ccc")
+    got, want = _kat(b1)
+    assert got == want == "cccaaabbb"
+
+    def b2(g, o):
+        for x in (g, o):
+            ag = x.get_or_create_agent_id if x is g else x.agent
+            a, b = ag("a"), ag("b")
+            t = x.add_insert_at(a, [], 0, "aaa")
+            x.add_delete_at(a, [t], 1, 2)
+            x.add_delete_at(b, [t], 0, 3)
+    got, want = _kat(b2)
+    assert got == want == ""
+
+
+def test_unicode():
+    g = dt_amd.ListOpLog()
+    s = g.get_or_create_agent_id("seph")
+    g.add_insert(s, 0, "héllo 𝄞 wörld")
+    g.add_delete_without_content(s, 1, 2)
+    g.add_insert(s, 6, "✓")
+    assert g.checkout_tip().content() == "hllo 𝄞✓ wörld"
