@@ -42,6 +42,7 @@ struct BatchParams {
     uint32_t n_list;
     uint32_t lds_blocks;    // block-index capacity held in LDS (small tier)
     uint32_t *counter;      // work-queue head, zeroed before each launch
+    uint32_t debug;         // DTGPU_DEBUG: device printf tracing
     DocResult *results;
 };
 

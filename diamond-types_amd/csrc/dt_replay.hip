@@ -38,6 +38,13 @@ DEV uint32_t lane_id() { return __lane_id(); }
 DEV void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); __builtin_amdgcn_wave_barrier(); }
 DEV uint32_t bcast(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
 DEV uint32_t first_lane(u64 m) { return uint32_t(__ffsll((long long)m) - 1); }
+// Wave-uniform values are pinned to scalar registers: control flow that depends on them is
+// scalar (no exec-mask loops), which is both what the algorithm means and what keeps hipcc
+// from treating the sequential replay as divergent.
+DEV uint32_t U(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+DEV u64 U64(u64 v) {
+    return (u64(__builtin_amdgcn_readfirstlane(uint32_t(v >> 32))) << 32) | __builtin_amdgcn_readfirstlane(uint32_t(v));
+}
 
 // inclusive wave prefix sum (64 lanes)
 DEV uint32_t wave_scan(uint32_t v) {
@@ -98,6 +105,7 @@ struct Doc {
     uint32_t nb;
     uint32_t err;
     uint32_t n_items;
+    uint32_t debug;
 };
 
 struct Cursor { uint32_t b, s; };
@@ -134,7 +142,7 @@ DEV bool find_vis(Doc &D, uint32_t p, Cursor &out) {
     const uint32_t fl = first_lane(m);
     const uint32_t bb = bcast(b, fl);
     const uint32_t off = p - base - bcast(inc - v, fl);
-    const u64 mv = D.mvis[bb];
+    const u64 mv = U64(D.mvis[bb]);
     const bool set = (mv >> l) & 1ull;
     const uint32_t before = uint32_t(__popcll(mv & ((1ull << l) - 1ull)));
     const u64 m2 = __ballot(set && before == off);
@@ -147,9 +155,9 @@ DEV bool find_vis(Doc &D, uint32_t p, Cursor &out) {
 // Document index of an item (number of items before it in list order).
 DEV uint64_t rank_of(Doc &D, uint32_t item) {
     const uint32_t l = lane_id();
-    uint32_t b = D.blk[item], s = D.slot[item];
+    uint32_t b = U(D.blk[item]), s = U(D.slot[item]);
     if (b >= D.nb) { D.err = ErrCheckout; b = 0; s = 0; }
-    const uint32_t p = D.opos[b], sb = p / SB;
+    const uint32_t p = U(D.opos[b]), sb = p / SB;
     uint32_t acc = 0;
     for (uint32_t c = 0; c < sb; c += 64) {
         const uint32_t i = c + l;
@@ -164,10 +172,10 @@ DEV uint64_t rank_of(Doc &D, uint32_t item) {
 
 // Move a cursor at the end of a block to the start of the next block in order.
 DEV void normalize(Doc &D, Cursor &c) {
-    while (c.s >= D.bcnt[c.b]) {
-        const uint32_t p = D.opos[c.b] + 1;
+    while (c.s >= U(D.bcnt[c.b])) {
+        const uint32_t p = U(D.opos[c.b]) + 1;
         if (p >= D.nb) return;   // end of document
-        c.b = D.ord[p];
+        c.b = U(D.ord[p]);
         c.s = 0;
     }
 }
@@ -175,16 +183,16 @@ DEV void normalize(Doc &D, Cursor &c) {
 // First item at/after c that is not NIY (origin_right search, merge.rs:405-423).
 DEV bool next_live(Doc &D, Cursor c, Cursor &out) {
     const uint32_t l = lane_id();
-    const u64 ml = c.s >= 64 ? 0ull : (D.mlive[c.b] & (~0ull << c.s));
+    const u64 ml = c.s >= 64 ? 0ull : (U64(D.mlive[c.b]) & (~0ull << c.s));
     if (ml) { out.b = c.b; out.s = first_lane(ml); return true; }
-    for (uint32_t p0 = D.opos[c.b] + 1; p0 < D.nb; p0 += 64) {
+    for (uint32_t p0 = U(D.opos[c.b]) + 1; p0 < D.nb; p0 += 64) {
         const uint32_t i = p0 + l;
         const uint32_t b = i < D.nb ? D.ord[i] : 0;
         const u64 m = __ballot(i < D.nb && D.mlive[b] != 0ull);
         if (m) {
             const uint32_t fl = first_lane(m);
             out.b = bcast(b, fl);
-            out.s = first_lane(D.mlive[out.b]);
+            out.s = first_lane(U64(D.mlive[out.b]));
             return true;
         }
     }
@@ -220,7 +228,7 @@ DEV uint32_t split_block(Doc &D, uint32_t b) {
         D.blk[v] = b2;
         D.slot[v] = uint8_t(l - BLK / 2);
     }
-    const uint32_t p = D.opos[b] + 1;
+    const uint32_t p = U(D.opos[b]) + 1;
     // shift ord[p .. nb) right by one, highest chunk first
     for (int c = int(D.nb) - 1; c >= int(p); c -= 64) {
         const int i = c - int(l);
@@ -257,7 +265,7 @@ DEV void insert_run(Doc &D, Cursor c, uint32_t lv, uint32_t k, uint32_t ol, uint
     }
     uint32_t b = c.b, s = c.s;
     while (k > 0) {
-        const uint32_t cnt = D.bcnt[b];
+        const uint32_t cnt = U(D.bcnt[b]);
         if (cnt == BLK) {
             const uint32_t b2 = split_block(D, b);
             if (D.err) return;
@@ -300,10 +308,10 @@ DEV void agent_of(const Doc &D, uint32_t lv, uint32_t &rank, uint32_t &seq) {
     uint32_t lo = 0, hi = D.n_aruns;   // last run with start <= lv
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) / 2;
-        if (D.aruns[3 * mid] <= lv) lo = mid; else hi = mid;
+        if (U(D.aruns[3 * mid]) <= lv) lo = mid; else hi = mid;
     }
-    rank = D.aruns[3 * lo + 1];
-    seq = D.aruns[3 * lo + 2] + (lv - D.aruns[3 * lo]);
+    rank = U(D.aruns[3 * lo + 1]);
+    seq = U(D.aruns[3 * lo + 2]) + (lv - U(D.aruns[3 * lo]));
 }
 
 DEV uint64_t rank_left(Doc &D, uint32_t ol) { return ol == ROOT_ID ? 0 : rank_of(D, ol) + 1; }
@@ -316,20 +324,20 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
     uint32_t ol;
     if (pos == 0) {
         ol = ROOT_ID;
-        cur.b = D.ord[0];
+        cur.b = U(D.ord[0]);
         cur.s = 0;
     } else {
         Cursor c;
         if (!find_vis(D, pos - 1, c)) { D.err = ErrCheckout; return; }
-        ol = D.items[size_t(c.b) * BLK + c.s];
+        ol = U(D.items[size_t(c.b) * BLK + c.s]);
         cur.b = c.b;
         cur.s = c.s + 1;
     }
     normalize(D, cur);
     Cursor rc;
     const bool has_r = next_live(D, cur, rc);
-    const uint32_t orr = has_r ? D.items[size_t(rc.b) * BLK + rc.s] : END_ID;
-    const bool at_end = cur.s >= D.bcnt[cur.b];
+    const uint32_t orr = has_r ? U(D.items[size_t(rc.b) * BLK + rc.s]) : END_ID;
+    const bool at_end = cur.s >= U(D.bcnt[cur.b]);
     const bool direct = has_r ? (rc.b == cur.b && rc.s == cur.s) : at_end;
     if (!direct) {
         // concurrent NIY items between cursor and origin_right: YjsMod scan
@@ -339,13 +347,13 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
         bool scanning = false;
         Cursor scan_start = cur, c = cur;
         for (;;) {
-            if (c.s >= D.bcnt[c.b]) break;   // reached the end of the document
-            const uint32_t o = D.items[size_t(c.b) * BLK + c.s];
+            if (c.s >= U(D.bcnt[c.b])) break;   // reached the end of the document
+            const uint32_t o = U(D.items[size_t(c.b) * BLK + c.s]);
             if (o == orr) break;
-            const uint64_t ol_o = rank_left(D, D.aux[o]);
+            const uint64_t ol_o = rank_left(D, U(D.aux[o]));
             if (ol_o < my_l) break;
             if (ol_o == my_l) {
-                const uint32_t orr_o = D.orr[o];
+                const uint32_t orr_o = U(D.orr[o]);
                 if (orr_o == orr) {
                     uint32_t r2, s2;
                     agent_of(D, o, r2, s2);
@@ -375,7 +383,7 @@ DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
     while (j0 < n) {
         Cursor c;
         if (!find_vis(D, pos, c)) { D.err = ErrCheckout; return; }
-        const u64 vm = D.mvis[c.b] & (~0ull << c.s);
+        const u64 vm = U64(D.mvis[c.b]) & (~0ull << c.s);
         const uint32_t avail = uint32_t(__popcll(vm));
         const uint32_t take = min(avail, n - j0);
         const uint32_t r = uint32_t(__popcll(vm & ((1ull << l) - 1ull)));
@@ -459,8 +467,8 @@ DEV void materialise(Doc &D, uint8_t *out, uint32_t cap, uint32_t &len_out, u64 
     uint32_t total = 0;
     u64 h = 0;
     for (uint32_t i = 0; i < D.nb; i++) {
-        const uint32_t b = D.ord[i];
-        const uint32_t cnt = D.bcnt[b];
+        const uint32_t b = U(D.ord[i]);
+        const uint32_t cnt = U(D.bcnt[b]);
         uint32_t cb = 0, n = 0;
         if (l < cnt) {
             const uint32_t it = D.items[size_t(b) * BLK + l];
@@ -495,7 +503,8 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
     D.err = 0;
     D.n_items = 0;
     for (uint32_t ci = 0; ci < D.ncmd && !D.err; ci++) {
-        const Cmd c = D.cmds[ci];
+        Cmd c = D.cmds[ci];
+        c.op = U(c.op); c.lv = U(c.lv); c.len = U(c.len); c.pos = U(c.pos);
         const uint32_t op = c.op & 15u;
         if (c.len == 0 || c.lv >= D.n_lv || c.len > D.n_lv - c.lv) { D.err = ErrCheckout; break; }
         switch (op) {
@@ -541,11 +550,12 @@ __global__ __launch_bounds__(64) void replay_kernel(BatchParams P) {
     for (;;) {
         uint32_t di = 0;
         if (l == 0) di = atomicAdd(P.counter, 1u);
-        di = __shfl(di, 0, 64);
+        di = U(__shfl(di, 0, 64));
         if (di >= P.n_list) break;
         const uint32_t d = P.doc_list[di];
         const DocDesc dd = P.docs[d];
         Doc D;
+        D.debug = P.debug;
         D.cmds = P.cmds + dd.cmd_off;
         D.ncmd = dd.ncmd;
         D.n_lv = dd.n_lv;

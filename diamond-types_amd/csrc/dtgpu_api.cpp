@@ -5,6 +5,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <thread>
@@ -187,6 +189,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     CK(hipStreamSynchronize(s));
 #undef CK
     BatchParams base{};
+    base.debug = getenv("DTGPU_DEBUG") ? 1u : 0u;
     base.cmds = B->d_cmds.p;
     base.cbyte = B->d_cbyte.p;
     base.content = B->d_content.p;
@@ -316,7 +319,14 @@ dtgpu_status dtgpu_batch_run(dtgpu_batch *B, void *stream) {
     if (!B) return DTGPU_ERR_ARG;
     if (hipSetDevice(B->device) != hipSuccess) return DTGPU_ERR_HIP;
     void *s = stream ? stream : reinterpret_cast<void *>(B->stream);
-    return dtgpu_status(launch_replay(B->small, B->large, s, B->n_cu));
+    if (B->small.debug) fprintf(stderr, "[dtgpu] launch small=%u large=%u lds_blocks=%u\n", B->small.n_list, B->large.n_list, B->lds_blocks);
+    dtgpu_status st = dtgpu_status(launch_replay(B->small, B->large, s, B->n_cu));
+    if (B->small.debug) {
+        fprintf(stderr, "[dtgpu] launched status %d\n", int(st));
+        hipError_t e = hipStreamSynchronize(reinterpret_cast<hipStream_t>(s));
+        fprintf(stderr, "[dtgpu] synced %d\n", int(e));
+    }
+    return st;
 }
 dtgpu_status dtgpu_batch_run_timed(dtgpu_batch *B, float *ms) {
     if (!B) return DTGPU_ERR_ARG;
