@@ -81,10 +81,15 @@ def main():
         dist.init_process_group("nccl")
 
     import dt_amd
+    from dt_amd.shard import doc_cost, gather_results, lpt_assign, max_over_ranks
     data = open(os.path.join(ROOT, "tests", "golden", "benchmark_data", args.workload + ".dt"), "rb").read()
+    n_total = args.docs * world
+    # weak scaling: the global batch is docs x world copies; LPT gives every rank its shard
+    mine = lpt_assign([doc_cost(data)] * n_total, world)[rank]
+    dev = f"cuda:{local_rank}" if dist is not None else None
 
     t0 = time.perf_counter()
-    batch = dt_amd.Batch(docs=[data] * args.docs, device=local_rank if world > 1 else 0)
+    batch = dt_amd.Batch(docs=[bytes(data) for _ in mine], device=local_rank if world > 1 else 0)
     host_stage_s = time.perf_counter() - t0
 
     for _ in range(args.warmup):
@@ -102,15 +107,10 @@ def main():
     h = dt_amd.text_hash(want)
     bad = sum(1 for r in res if r["status"] != 0 or r["text_hash"] != h or r["text_len"] != len(want))
     assert bad == 0, f"{bad} documents differ"
-
-    if dist is not None:
-        import torch
-        recs = torch.tensor([[r["text_len"], r["text_hash"] & 0x7FFFFFFFFFFFFFFF] for r in res],
-                            dtype=torch.int64, device="cuda")
-        gathered = [torch.empty_like(recs) for _ in range(world)]
-        dist.all_gather(gathered, recs)
-        allrec = torch.cat(gathered)
-        assert bool((allrec[:, 0] == len(want)).all()), "RCCL gather: length mismatch on some rank"
+    if dist is not None:   # RCCL all-gather of per-document (len, hash) records
+        table = gather_results([(g, r["status"], r["text_len"], r["text_hash"]) for g, r in zip(mine, res)],
+                               n_total, dist, device=dev)
+        assert all(row is not None and row[1] == 0 and row[2] == len(want) for row in table), "gather mismatch"
         dist.barrier()
 
     # timed region: K device passes over the resident batch
@@ -124,14 +124,11 @@ def main():
     batch.sync()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = max_over_ranks(elapsed, dist, device=dev)
         dist.barrier()
-        elapsed = float(t.item())
 
     lv_per_doc = res[0]["n_lv"]
-    total_lv = lv_per_doc * args.docs * world
+    total_lv = lv_per_doc * n_total
     ms_per_step = elapsed * 1000.0 / args.steps
     value = total_lv * args.steps / elapsed
     avg_kernel_ms = statistics.mean(kernel_ms)
@@ -155,7 +152,7 @@ def main():
                    "docs_per_gpu": args.docs, "merged_ops_per_doc": lv_per_doc,
                    "timed": "device replay + materialisation of the whole batch (plan resident in HBM)",
                    "parallelism": f"dp{world} (documents sharded, no data-path collective)"},
-        "docs_per_sec": args.docs * world * args.steps / elapsed,
+        "docs_per_sec": n_total * args.steps / elapsed,
         "host_stage_s": host_stage_s,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,

@@ -22,6 +22,8 @@ struct DocResult {
     uint32_t status, out_len;
     uint64_t hash;
     uint32_t n_items, n_blocks;
+    uint32_t fail_cmd, fail_site;   // diagnostics: command index and code site of the first error
+    uint32_t dbg[10];               // DTGPU_DEBUG invariant-failure detail
 };
 
 struct BatchParams {

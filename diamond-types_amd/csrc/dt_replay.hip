@@ -36,14 +36,14 @@ typedef unsigned long long u64;
 
 DEV uint32_t lane_id() { return __lane_id(); }
 DEV void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); __builtin_amdgcn_wave_barrier(); }
-DEV uint32_t bcast(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
+DEV uint32_t bcast(uint32_t v, uint32_t l) { return uint32_t(__builtin_amdgcn_readlane(int(v), int(l))); }
 DEV uint32_t first_lane(u64 m) { return uint32_t(__ffsll((long long)m) - 1); }
 // Wave-uniform values are pinned to scalar registers: control flow that depends on them is
 // scalar (no exec-mask loops), which is both what the algorithm means and what keeps hipcc
 // from treating the sequential replay as divergent.
-DEV uint32_t U(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-DEV u64 U64(u64 v) {
-    return (u64(__builtin_amdgcn_readfirstlane(uint32_t(v >> 32))) << 32) | __builtin_amdgcn_readfirstlane(uint32_t(v));
+DEV uint32_t U(uint32_t v) { return uint32_t(__builtin_amdgcn_readfirstlane(int(v))); }
+DEV u64 U64(u64 v) {   // (readfirstlane returns int: keep both halves unsigned)
+    return (u64(U(uint32_t(v >> 32))) << 32) | u64(U(uint32_t(v)));
 }
 
 // inclusive wave prefix sum (64 lanes)
@@ -106,7 +106,20 @@ struct Doc {
     uint32_t err;
     uint32_t n_items;
     uint32_t debug;
+    uint32_t site, ci;
+    uint64_t steps, step_limit;   // watchdog: every loop iteration is charged; a bound
+                                  // violation ends the document with ErrCapacity
 };
+
+// Charge one loop iteration; returns false (and flags the document) past the budget, so every
+// loop in the replay provably terminates whatever the input.
+DEV void fail(Doc &D, uint32_t code, uint32_t site) {
+    if (!D.err) { D.err = code; D.site = site; }
+}
+DEV bool charge(Doc &D) {
+    if (++D.steps > D.step_limit) { fail(D, ErrCapacity, 1); return false; }
+    return true;
+}
 
 struct Cursor { uint32_t b, s; };
 
@@ -156,7 +169,7 @@ DEV bool find_vis(Doc &D, uint32_t p, Cursor &out) {
 DEV uint64_t rank_of(Doc &D, uint32_t item) {
     const uint32_t l = lane_id();
     uint32_t b = U(D.blk[item]), s = U(D.slot[item]);
-    if (b >= D.nb) { D.err = ErrCheckout; b = 0; s = 0; }
+    if (b >= D.nb) { fail(D, ErrCheckout, 11); b = 0; s = 0; }
     const uint32_t p = U(D.opos[b]), sb = p / SB;
     uint32_t acc = 0;
     for (uint32_t c = 0; c < sb; c += 64) {
@@ -173,6 +186,7 @@ DEV uint64_t rank_of(Doc &D, uint32_t item) {
 // Move a cursor at the end of a block to the start of the next block in order.
 DEV void normalize(Doc &D, Cursor &c) {
     while (c.s >= U(D.bcnt[c.b])) {
+        if (!charge(D)) return;
         const uint32_t p = U(D.opos[c.b]) + 1;
         if (p >= D.nb) return;   // end of document
         c.b = U(D.ord[p]);
@@ -218,7 +232,7 @@ DEV void recompute_sb(Doc &D, uint32_t from_sb) {
 // Split a full block: its upper half moves to a new block placed right after it in order.
 DEV uint32_t split_block(Doc &D, uint32_t b) {
     const uint32_t l = lane_id();
-    if (D.nb >= D.max_blocks) { D.err = ErrCapacity; return 0; }
+    if (D.nb >= D.max_blocks) { fail(D, ErrCapacity, 12); return 0; }
     const uint32_t b2 = D.nb;
     uint32_t *src = D.items + size_t(b) * BLK;
     uint32_t *dst = D.items + size_t(b2) * BLK;
@@ -265,6 +279,7 @@ DEV void insert_run(Doc &D, Cursor c, uint32_t lv, uint32_t k, uint32_t ol, uint
     }
     uint32_t b = c.b, s = c.s;
     while (k > 0) {
+        if (!charge(D)) return;
         const uint32_t cnt = U(D.bcnt[b]);
         if (cnt == BLK) {
             const uint32_t b2 = split_block(D, b);
@@ -328,7 +343,7 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
         cur.s = 0;
     } else {
         Cursor c;
-        if (!find_vis(D, pos - 1, c)) { D.err = ErrCheckout; return; }
+        if (!find_vis(D, pos - 1, c)) { fail(D, ErrCheckout, 13); return; }
         ol = U(D.items[size_t(c.b) * BLK + c.s]);
         cur.b = c.b;
         cur.s = c.s + 1;
@@ -347,6 +362,7 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
         bool scanning = false;
         Cursor scan_start = cur, c = cur;
         for (;;) {
+            if (!charge(D)) return;
             if (c.s >= U(D.bcnt[c.b])) break;   // reached the end of the document
             const uint32_t o = U(D.items[size_t(c.b) * BLK + c.s]);
             if (o == orr) break;
@@ -381,8 +397,9 @@ DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
     const uint32_t l = lane_id();
     uint32_t j0 = 0;
     while (j0 < n) {
+        if (!charge(D)) return;
         Cursor c;
-        if (!find_vis(D, pos, c)) { D.err = ErrCheckout; return; }
+        if (!find_vis(D, pos, c)) { fail(D, ErrCheckout, 14); return; }
         const u64 vm = U64(D.mvis[c.b]) & (~0ull << c.s);
         const uint32_t avail = uint32_t(__popcll(vm));
         const uint32_t take = min(avail, n - j0);
@@ -399,7 +416,7 @@ DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
             D.st[item] = DEL_BIT | 2;
             D.aux[dlv] = item;
         }
-        if (__ballot(bad)) { D.err = ErrCheckout; return; }
+        if (__ballot(bad)) { fail(D, ErrCheckout, 15); return; }
         if (l == 0) {
             D.mvis[c.b] &= ~selm;
             D.svis[D.opos[c.b] / SB] -= take;
@@ -456,7 +473,7 @@ DEV void toggle_run(Doc &D, uint32_t lv, uint32_t n) {
                 }
             }
         }
-        if (__ballot(bad)) { D.err = ErrCheckout; return; }
+        if (__ballot(bad)) { fail(D, ErrCheckout, 16); return; }
         wave_fence();
     }
 }
@@ -490,6 +507,52 @@ DEV void materialise(Doc &D, uint8_t *out, uint32_t cap, uint32_t &len_out, u64 
     hash_out = wave_sum64(h);
 }
 
+// Debug-mode consistency check of the whole structure (DTGPU_DEBUG): returns 0 or a code.
+DEV uint32_t check_invariants(Doc &D, DocResult *res) {
+    const uint32_t l = lane_id();
+    uint32_t code = 0;
+    for (uint32_t i = 0; i < D.nb; i++) {
+        const uint32_t b = U(D.ord[i]);
+        if (U(D.opos[b]) != i) return 201;
+        const uint32_t cnt = U(D.bcnt[b]);
+        const u64 mv = U64(D.mvis[b]), ml = U64(D.mlive[b]);
+        bool bad = false;
+        if (l < cnt) {
+            const uint32_t it = D.items[size_t(b) * BLK + l];
+            if (it >= D.n_lv) bad = true;
+            else {
+                const uint32_t st = D.st[it] & 0x7F;
+                if (((mv >> l) & 1) != (st == 1 ? 1u : 0u)) bad = true;
+                if (((ml >> l) & 1) != (st != 0 ? 1u : 0u)) bad = true;
+                if (D.blk[it] != b || D.slot[it] != l) bad = true;
+            }
+        } else if (((mv | ml) >> l) & 1) bad = true;
+        const u64 bm = __ballot(bad);
+        if (bm) {
+            const uint32_t fl = first_lane(bm);
+            if (l == fl) {
+                const uint32_t it = l < cnt ? D.items[size_t(b) * BLK + l] : 0xFFFFFFFFu;
+                res->dbg[0] = b; res->dbg[1] = l; res->dbg[2] = cnt; res->dbg[3] = it;
+                res->dbg[4] = it < D.n_lv ? D.st[it] : 999; res->dbg[5] = it < D.n_lv ? D.blk[it] : 999;
+                res->dbg[6] = it < D.n_lv ? D.slot[it] : 999;
+                res->dbg[7] = uint32_t(mv); res->dbg[8] = uint32_t(mv >> 32); res->dbg[9] = uint32_t(ml);
+            }
+            return 202;
+        }
+    }
+    const uint32_t nsb = (D.nb + SB - 1) / SB;
+    for (uint32_t s = 0; s < nsb; s++) {
+        const uint32_t i = s * SB + l;
+        const uint32_t b = i < D.nb ? D.ord[i] : 0;
+        const uint32_t v = i < D.nb ? uint32_t(__popcll(D.mvis[b])) : 0;
+        const uint32_t c = i < D.nb ? uint32_t(D.bcnt[b]) : 0;
+        if (U(wave_sum(v)) != U(D.svis[s])) code = 203;
+        if (U(wave_sum(c)) != U(D.scnt[s])) code = 204;
+        if (code) return code;
+    }
+    return 0;
+}
+
 DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
     const uint32_t l = lane_id();
     // fresh tracker: one empty block, every LV not-inserted-yet
@@ -502,11 +565,16 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
     D.nb = 1;
     D.err = 0;
     D.n_items = 0;
+    D.steps = 0;
+    D.step_limit = 64ull * (uint64_t(D.ncmd) + D.n_lv) + 4096;
+    D.site = 0;
     for (uint32_t ci = 0; ci < D.ncmd && !D.err; ci++) {
+        D.ci = ci;
         Cmd c = D.cmds[ci];
         c.op = U(c.op); c.lv = U(c.lv); c.len = U(c.len); c.pos = U(c.pos);
         const uint32_t op = c.op & 15u;
-        if (c.len == 0 || c.lv >= D.n_lv || c.len > D.n_lv - c.lv) { D.err = ErrCheckout; break; }
+        if (c.len == 0 || c.lv >= D.n_lv || c.len > D.n_lv - c.lv) { fail(D, ErrCheckout, 17); break; }
+        if (!charge(D)) break;
         switch (op) {
             case CMD_INS: do_insert(D, c.lv, c.len, c.pos); break;
             case CMD_DEL: do_delete(D, c.lv, c.len, c.pos, (c.op & 16u) != 0); break;
@@ -514,7 +582,11 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
             case CMD_ADV_DEL: toggle_run<true, true>(D, c.lv, c.len); break;
             case CMD_RET_INS: toggle_run<false, false>(D, c.lv, c.len); break;
             case CMD_RET_DEL: toggle_run<false, true>(D, c.lv, c.len); break;
-            default: D.err = ErrCheckout; break;
+            default: fail(D, ErrCheckout, 18); break;
+        }
+        if (D.debug && !D.err) {
+            const uint32_t code = check_invariants(D, res);
+            if (code) fail(D, ErrCheckout, code);
         }
     }
     uint32_t len = 0;
@@ -526,6 +598,8 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
         res->hash = h;
         res->n_items = D.n_items;
         res->n_blocks = D.nb;
+        res->fail_cmd = D.err ? D.ci : 0;
+        res->fail_site = D.err ? D.site : 0;
     }
 }
 
@@ -541,43 +615,38 @@ DEV void bind_index(Doc &D, uint8_t *base, uint32_t mb) {
     D.bcnt = reinterpret_cast<uint8_t *>(D.scnt + nsb);
 }
 
-// Persistent work-queue kernel: each 64-lane workgroup pulls documents until the list is
-// drained (every wave reaches the exit when the counter passes n_list).
+// One 64-lane workgroup per document of the list (the hardware dispatcher is the work queue;
+// LDS per workgroup bounds how many documents share a CU).
 template <bool LDS_INDEX>
 __global__ __launch_bounds__(64) void replay_kernel(BatchParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const uint32_t l = lane_id();
-    for (;;) {
-        uint32_t di = 0;
-        if (l == 0) di = atomicAdd(P.counter, 1u);
-        di = U(__shfl(di, 0, 64));
-        if (di >= P.n_list) break;
-        const uint32_t d = P.doc_list[di];
-        const DocDesc dd = P.docs[d];
-        Doc D;
-        D.debug = P.debug;
-        D.cmds = P.cmds + dd.cmd_off;
-        D.ncmd = dd.ncmd;
-        D.n_lv = dd.n_lv;
-        D.cbyte = P.cbyte + dd.lv_off;
-        D.content = P.content + dd.content_off;
-        D.aruns = P.aruns + dd.arun_off;
-        D.n_aruns = dd.n_aruns;
-        D.st = P.st + dd.lv_off;
-        D.blk = P.blk + dd.lv_off;
-        D.slot = P.slot + dd.lv_off;
-        D.aux = P.aux + dd.lv_off;
-        D.orr = P.orr + dd.lv_off;
-        D.items = P.items + dd.blk_off * BLK;
-        D.max_blocks = dd.max_blocks;
-        if (LDS_INDEX) {
-            bind_index(D, smem, P.lds_blocks);
-            if (D.max_blocks > P.lds_blocks) D.max_blocks = P.lds_blocks;
-        } else {
-            bind_index(D, P.gidx + dd.gidx_off, dd.max_blocks);
-        }
-        run_doc(D, P.out + dd.out_off, dd.out_cap, &P.results[d]);
+    const uint32_t di = U(blockIdx.x);
+    if (di >= P.n_list) return;
+    const uint32_t d = U(P.doc_list[di]);
+    const DocDesc dd = P.docs[d];
+    Doc D;
+    D.debug = P.debug;
+    D.cmds = P.cmds + dd.cmd_off;
+    D.ncmd = U(dd.ncmd);
+    D.n_lv = U(dd.n_lv);
+    D.cbyte = P.cbyte + dd.lv_off;
+    D.content = P.content + dd.content_off;
+    D.aruns = P.aruns + dd.arun_off;
+    D.n_aruns = U(dd.n_aruns);
+    D.st = P.st + dd.lv_off;
+    D.blk = P.blk + dd.lv_off;
+    D.slot = P.slot + dd.lv_off;
+    D.aux = P.aux + dd.lv_off;
+    D.orr = P.orr + dd.lv_off;
+    D.items = P.items + dd.blk_off * BLK;
+    D.max_blocks = U(dd.max_blocks);
+    if (LDS_INDEX) {
+        bind_index(D, smem, P.lds_blocks);
+        if (D.max_blocks > P.lds_blocks) D.max_blocks = P.lds_blocks;
+    } else {
+        bind_index(D, P.gidx + dd.gidx_off, D.max_blocks);
     }
+    run_doc(D, P.out + dd.out_off, U(dd.out_cap), &P.results[d]);
 }
 
 }  // namespace dev
@@ -586,20 +655,11 @@ int launch_replay(const BatchParams &small, const BatchParams &large, void *stre
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (small.n_list) {
         const size_t lds = size_t(index_bytes(small.lds_blocks));
-        int per_cu = int((160u * 1024u) / (lds ? lds : 1));
-        if (per_cu > 16) per_cu = 16;
-        if (per_cu < 1) per_cu = 1;
-        uint32_t grid = uint32_t(n_cu * per_cu);
-        if (grid > small.n_list) grid = small.n_list;
-        if (hipMemsetAsync(small.counter, 0, sizeof(uint32_t), s) != hipSuccess) return ErrHip;
-        hipLaunchKernelGGL(dev::replay_kernel<true>, dim3(grid), dim3(64), lds, s, small);
+        hipLaunchKernelGGL(dev::replay_kernel<true>, dim3(small.n_list), dim3(64), lds, s, small);
         if (hipGetLastError() != hipSuccess) return ErrHip;
     }
     if (large.n_list) {
-        uint32_t grid = uint32_t(n_cu * 8);
-        if (grid > large.n_list) grid = large.n_list;
-        if (hipMemsetAsync(large.counter, 0, sizeof(uint32_t), s) != hipSuccess) return ErrHip;
-        hipLaunchKernelGGL(dev::replay_kernel<false>, dim3(grid), dim3(64), 0, s, large);
+        hipLaunchKernelGGL(dev::replay_kernel<false>, dim3(large.n_list), dim3(64), 0, s, large);
         if (hipGetLastError() != hipSuccess) return ErrHip;
     }
     return OK;

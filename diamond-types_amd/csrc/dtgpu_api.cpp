@@ -291,6 +291,41 @@ dtgpu_status dtgpu_oplog_plan_stats(const dtgpu_oplog *h, uint64_t out[4]) {
     return DTGPU_OK;
 }
 
+size_t dtgpu_oplog_plan_commands(const dtgpu_oplog *h, uint32_t *cmds, size_t cap) {
+    if (!h) return 0;
+    Prepared p;
+    prepare_from_oplog(h->o, p);
+    if (p.status != OK) return 0;
+    for (size_t i = 0; i < p.plan.cmds.size() && i < cap; i++) {
+        cmds[4 * i] = p.plan.cmds[i].op;
+        cmds[4 * i + 1] = p.plan.cmds[i].lv;
+        cmds[4 * i + 2] = p.plan.cmds[i].len;
+        cmds[4 * i + 3] = p.plan.cmds[i].pos;
+    }
+    return p.plan.cmds.size();
+}
+
+size_t dtgpu_oplog_ins_content(const dtgpu_oplog *h, uint8_t *out, size_t cap) {
+    if (!h) return 0;
+    const auto &c = h->o.ins_content;
+    if (out) std::memcpy(out, c.data(), std::min(cap, c.size()));
+    return c.size();
+}
+size_t dtgpu_oplog_char_offsets(const dtgpu_oplog *h, uint32_t *out, size_t cap) {
+    if (!h) return 0;
+    const auto &c = h->o.ins_cbyte;
+    if (out) std::memcpy(out, c.data(), std::min(cap, c.size()) * sizeof(uint32_t));
+    return c.size();
+}
+size_t dtgpu_oplog_agent_runs(const dtgpu_oplog *h, uint32_t *out, size_t cap) {
+    if (!h) return 0;
+    Prepared p;
+    prepare_from_oplog(h->o, p);
+    const auto &a = p.plan.agent_runs;
+    if (out) std::memcpy(out, a.data(), std::min(cap, a.size()) * sizeof(uint32_t));
+    return a.size();
+}
+
 // ---- batch ----------------------------------------------------------------------------------
 dtgpu_status dtgpu_batch_create(const uint8_t *const *docs, const size_t *lens, size_t n,
                                 const dtgpu_batch_opts *opts, dtgpu_batch **out) {
@@ -371,7 +406,13 @@ dtgpu_status dtgpu_batch_text(dtgpu_batch *B, size_t i, uint8_t *out, size_t cap
     if (hipMemcpyAsync(&r, B->d_results.p + i, sizeof r, hipMemcpyDeviceToHost, B->stream) != hipSuccess ||
         hipStreamSynchronize(B->stream) != hipSuccess)
         return DTGPU_ERR_HIP;
-    if (r.status != OK) return dtgpu_status(r.status);
+    if (r.status != OK) {
+        if (B->small.debug)
+            fprintf(stderr, "[dtgpu] doc %zu status %u fail_cmd %u fail_site %u items %u blocks %u dbg %u %u %u %u %u %u %u %x %x %x\n", i, r.status,
+                    r.fail_cmd, r.fail_site, r.n_items, r.n_blocks, r.dbg[0], r.dbg[1], r.dbg[2], r.dbg[3], r.dbg[4],
+                    r.dbg[5], r.dbg[6], r.dbg[7], r.dbg[8], r.dbg[9]);
+        return dtgpu_status(r.status);
+    }
     if (out_len) *out_len = r.out_len;
     if (!out) return DTGPU_OK;
     if (cap < r.out_len) return DTGPU_ERR_ARG;

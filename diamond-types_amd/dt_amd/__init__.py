@@ -76,6 +76,14 @@ def lib():
     L.dtgpu_oplog_local_frontier.argtypes = [vp, pu64, sz]
     L.dtgpu_oplog_local_frontier.restype = sz
     L.dtgpu_oplog_plan_stats.argtypes = [vp, pu64]
+    L.dtgpu_oplog_plan_commands.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32), sz]
+    L.dtgpu_oplog_plan_commands.restype = sz
+    L.dtgpu_oplog_ins_content.argtypes = [vp, ctypes.c_char_p, sz]
+    L.dtgpu_oplog_ins_content.restype = sz
+    L.dtgpu_oplog_char_offsets.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32), sz]
+    L.dtgpu_oplog_char_offsets.restype = sz
+    L.dtgpu_oplog_agent_runs.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32), sz]
+    L.dtgpu_oplog_agent_runs.restype = sz
     L.dtgpu_checkout_tip.argtypes = [vp, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
     L.dtgpu_batch_create.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz), sz,
                                      ctypes.POINTER(BatchOpts), ctypes.POINTER(vp)]
@@ -195,6 +203,30 @@ class ListOpLog:
         out = (ctypes.c_uint64 * 4)()
         _check(lib().dtgpu_oplog_plan_stats(self._h, out))
         return dict(steps=out[0], retreat=out[1], advance=out[2], commands=out[3])
+
+    def plan_commands(self):
+        n = lib().dtgpu_oplog_plan_commands(self._h, None, 0)
+        buf = (ctypes.c_uint32 * max(4, 4 * n))()
+        lib().dtgpu_oplog_plan_commands(self._h, buf, n)
+        return [tuple(buf[4 * i:4 * i + 4]) for i in range(n)]
+
+    def ins_content(self) -> bytes:
+        n = lib().dtgpu_oplog_ins_content(self._h, None, 0)
+        buf = ctypes.create_string_buffer(max(1, n))
+        lib().dtgpu_oplog_ins_content(self._h, buf, n)
+        return buf.raw[:n]
+
+    def char_offsets(self):
+        n = lib().dtgpu_oplog_char_offsets(self._h, None, 0)
+        buf = (ctypes.c_uint32 * max(1, n))()
+        lib().dtgpu_oplog_char_offsets(self._h, buf, n)
+        return list(buf[:n])
+
+    def agent_runs(self):
+        n = lib().dtgpu_oplog_agent_runs(self._h, None, 0)
+        buf = (ctypes.c_uint32 * max(1, n))()
+        lib().dtgpu_oplog_agent_runs(self._h, buf, n)
+        return list(buf[:n])
 
     def checkout_tip_bytes(self) -> bytes:
         n = ctypes.c_size_t()

@@ -89,6 +89,18 @@ size_t dtgpu_oplog_local_frontier(const dtgpu_oplog *oplog, uint64_t *out, size_
  * advanced LVs, out[3] device commands.  Pure host code; usable without a GPU. */
 dtgpu_status dtgpu_oplog_plan_stats(const dtgpu_oplog *oplog, uint64_t out[4]);
 
+/* The device command stream of that plan (16 B per command: op | fwd<<4, lv, len, pos) and
+ * the tie-break agent runs (lv, name rank, seq).  Returns the command count; writes at most
+ * cap commands.  Introspection for tests and tools. */
+size_t dtgpu_oplog_plan_commands(const dtgpu_oplog *oplog, uint32_t *cmds, size_t cap);
+
+/* Inserted-content arena (UTF-8, LV order; the text every checkout draws from) and the byte
+ * offset of each LV's char (~0 for deletes).  Return the full sizes; copy at most cap. */
+size_t dtgpu_oplog_ins_content(const dtgpu_oplog *oplog, uint8_t *out, size_t cap);
+size_t dtgpu_oplog_char_offsets(const dtgpu_oplog *oplog, uint32_t *out, size_t cap);
+/* Tie-break agent runs of the plan: triples (first LV, agent-name rank, first seq). */
+size_t dtgpu_oplog_agent_runs(const dtgpu_oplog *oplog, uint32_t *out, size_t cap);
+
 /* ---- checkout ------------------------------------------------------------------------------ */
 
 /* ListOpLog::checkout_tip() -> ListBranch, then ListBranch::content().to_string()

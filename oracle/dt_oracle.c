@@ -802,7 +802,7 @@ EXPORT int dto_load(const u8 *bytes, size_t len, int ignore_crc, dto_oplog **out
 /* ------------------------------------------------------------------------------------------ */
 /* SpanningTreeWalker (txn_trace.rs:114-333), full walk from ROOT                              */
 /* ------------------------------------------------------------------------------------------ */
-typedef struct { i64 start, end; int np; const i64 *parents; VecI64 pidx, cidx; int visited; } VisitEntry;
+typedef struct { i64 start, end; int np; const i64 *parents; i64 p1; int own_p1; VecI64 pidx, cidx; int visited; } VisitEntry;
 typedef struct { VecRange retreat, advance_rev; Range consume; } WalkStep;
 
 typedef struct {
@@ -815,15 +815,29 @@ static i64 find_input(const Walker *w, i64 t) {
         if (t < e->start) hi = m - 1; else if (t >= e->end) lo = m + 1; else return m; }
     return -1;
 }
-static void walker_init(Walker *w, const Graph *g) {
+/* SpanningTreeWalker::new (txn_trace.rs:114-182): ascending input spans split per graph entry;
+ * parents outside the input are ignored. */
+static void walker_init(Walker *w, const Graph *g, const Range *spans, i64 nspans) {
     memset(w, 0, sizeof *w); w->g = g;
-    for (i64 i = 0; i < g->e.n; i++) {
-        const GEntry *ge = &g->e.v[i];
-        VisitEntry ve; memset(&ve, 0, sizeof ve);
-        ve.start = ge->start; ve.end = ge->end; ve.np = ge->np; ve.parents = ge->parents;
-        for (int k = 0; k < ge->np; k++) { i64 pi = find_input(w, ge->parents[k]); if (pi >= 0) VPUSH(ve.pidx, pi); }
-        if (ve.pidx.n == 0) VPUSH(w->todo, w->in.n);
-        VPUSH(w->in, ve);
+    for (i64 si = 0; si < nspans; si++) {
+        i64 s = spans[si].start, e = spans[si].end;
+        i64 gi = graph_find_idx(g, s);
+        while (s < e) {
+            const GEntry *ge = &g->e.v[gi];
+            i64 pe = ge->end < e ? ge->end : e;
+            VisitEntry ve; memset(&ve, 0, sizeof ve);
+            ve.start = s; ve.end = pe;
+            if (s > ge->start) { ve.p1 = s - 1; ve.own_p1 = 1; ve.np = 1; }   /* clone_parents_at_version */
+            else { ve.np = ge->np; ve.parents = ge->parents; }
+            VPUSH(w->in, ve);
+            s = pe; gi++;
+        }
+    }
+    for (i64 i = 0; i < w->in.n; i++) {
+        VisitEntry *ve = &w->in.v[i];
+        if (ve->own_p1) ve->parents = &ve->p1;   /* stable now that the vector is built */
+        for (int k = 0; k < ve->np; k++) { i64 pi = find_input(w, ve->parents[k]); if (pi >= 0) VPUSH(ve->pidx, pi); }
+        if (ve->pidx.n == 0) VPUSH(w->todo, i);
     }
     for (i64 i = 0; i < w->in.n; i++)
         for (i64 k = 0; k < w->in.v[i].pidx.n; k++) VPUSH(w->in.v[w->in.v[i].pidx.v[k]].cidx, i);
@@ -1018,11 +1032,17 @@ static void inorder(Tracker *T, int x, const dto_oplog *o, u8 *out, size_t *n) {
     free(stack);
 }
 
-/* checkout_tip -> text.  order: 0 = spanning-tree walk (the reference's), 1 = plain LV order
- * (a second topological order, for the convergence check of SURVEY.md §8c). */
-EXPORT int dto_checkout_tip(const dto_oplog *o, int order, u8 **out, size_t *out_len, dto_stats *stats) {
+/* ListOpLog::checkout(version) -> text (src/list/oplog.rs:32-36; checkout_tip = version
+ * cg.version).  order: 0 = spanning-tree walk (the reference's), 1 = plain LV order (a second
+ * topological order, for the convergence check of SURVEY.md §8c). */
+EXPORT int dto_checkout(const dto_oplog *o, const i64 *version, int nv, int order, u8 **out, size_t *out_len, dto_stats *stats) {
     i64 n = o->kind.n;
-    for (i64 i = 0; i < n; i++) if (o->kind.v[i] == 0 && o->cbyte.v[i] < 0) return E_CheckoutPanic;  /* content.unwrap() */
+    VecRange hist = {0}, none = {0};
+    graph_diff_rev(&o->g, version, nv, NULL, 0, &hist, &none);   /* Hist(version), descending */
+    for (i64 i = 0, j = hist.n - 1; i < j; i++, j--) { Range t = hist.v[i]; hist.v[i] = hist.v[j]; hist.v[j] = t; }
+    for (i64 i = 0; i < hist.n; i++)
+        for (i64 v = hist.v[i].start; v < hist.v[i].end; v++)
+            if (o->kind.v[v] == 0 && o->cbyte.v[v] < 0) { VFREE(hist); VFREE(none); return E_CheckoutPanic; }  /* content.unwrap() */
     Tracker T; memset(&T, 0, sizeof T);
     T.o = o; T.root = -1; T.rng = 0x9E3779B97F4A7C15ull;
     T.t = malloc(sizeof(TNode) * (size_t)(n + 1));
@@ -1031,21 +1051,20 @@ EXPORT int dto_checkout_tip(const dto_oplog *o, int order, u8 **out, size_t *out
     T.ol = malloc(sizeof(i64) * (size_t)(n + 1)); T.orr = malloc(sizeof(i64) * (size_t)(n + 1));
     T.del_target = malloc(sizeof(i64) * (size_t)(n + 1));
     Walker w; WalkStep st; memset(&st, 0, sizeof st);
-    if (order == 0) walker_init(&w, &o->g);
+    walker_init(&w, &o->g, hist.v, hist.n);
     VecI64 cur = {0};       /* for order 1 */
     i64 next_entry = 0;
     for (;;) {
-        Range consume; const i64 *par; int np;
+        Range consume;
         if (order == 0) {
             if (!walker_next(&w, &st)) break;
             consume = st.consume;
         } else {
-            if (next_entry >= o->g.e.n) break;
-            const GEntry *ge = &o->g.e.v[next_entry++];
-            par = ge->parents; np = ge->np;
-            graph_diff_rev(&o->g, cur.v, (int)cur.n, par, np, &st.retreat, &st.advance_rev);
-            consume.start = ge->start; consume.end = ge->end;
-            cur.n = 0; VPUSH(cur, ge->end - 1);
+            if (next_entry >= w.in.n) break;
+            const VisitEntry *ve = &w.in.v[next_entry++];
+            graph_diff_rev(&o->g, cur.v, (int)cur.n, ve->parents, ve->np, &st.retreat, &st.advance_rev);
+            consume.start = ve->start; consume.end = ve->end;
+            cur.n = 0; VPUSH(cur, ve->end - 1);
         }
         T.n_steps++;
         for (i64 i = 0; i < st.retreat.n && !T.err; i++)
@@ -1066,10 +1085,13 @@ EXPORT int dto_checkout_tip(const dto_oplog *o, int order, u8 **out, size_t *out
     }
     if (stats) { stats->n_steps = T.n_steps; stats->n_retreat = T.n_retreat; stats->n_advance = T.n_advance;
                  stats->n_scans = T.n_scans; stats->n_items = T.n_items; }
-    if (order == 0) walker_free(&w);
-    VFREE(st.retreat); VFREE(st.advance_rev); VFREE(cur);
+    walker_free(&w);
+    VFREE(st.retreat); VFREE(st.advance_rev); VFREE(cur); VFREE(hist); VFREE(none);
     free(T.t); free(T.state); free(T.ever_deleted); free(T.ol); free(T.orr); free(T.del_target);
     return err;
+}
+EXPORT int dto_checkout_tip(const dto_oplog *o, int order, u8 **out, size_t *out_len, dto_stats *stats) {
+    return dto_checkout(o, o->version.v, (int)o->version.n, order, out, out_len, stats);
 }
 EXPORT void dto_free_buf(u8 *p) { free(p); }
 
