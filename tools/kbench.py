@@ -1,0 +1,33 @@
+"""Kernel-time micro-benchmark: stage N copies of a document and time device passes."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "diamond-types_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def main():
+    import dt_amd
+    import golden_data as G
+    name = sys.argv[1]
+    counts = [int(x) for x in sys.argv[2].split(",")]
+    reps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+    data = G.dt_bytes(name)
+    for n in counts:
+        t = time.time()
+        b = dt_amd.Batch(docs=[data] * n)
+        stage = time.time() - t
+        b.run(); b.sync()
+        ms = [b.run_timed() for _ in range(reps)]
+        res = b.results()
+        ok = all(r["status"] == 0 for r in res)
+        lv = sum(r["n_lv"] for r in res)
+        best = min(ms)
+        print(f"{name} docs={n} stage={stage:.2f}s kernel_ms={best:.2f} (all {['%.2f' % m for m in ms]}) "
+              f"ok={ok} Mops/s={lv / best / 1e3:.1f} alg_GB/s={b.algorithmic_bytes / best / 1e6:.1f}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
