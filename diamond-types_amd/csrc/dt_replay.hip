@@ -46,21 +46,19 @@ DEV u64 U64(u64 v) {   // (readfirstlane returns int: keep both halves unsigned)
     return (u64(U(uint32_t(v >> 32))) << 32) | u64(U(uint32_t(v)));
 }
 
-// inclusive wave prefix sum (64 lanes)
-DEV uint32_t wave_scan(uint32_t v) {
-    const uint32_t l = lane_id();
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t t = __shfl_up(v, d, 64);
-        if (l >= uint32_t(d)) v += t;
-    }
-    return v;
+// Inclusive wave prefix sum over 64 lanes with DPP: Hillis-Steele inside each 16-lane row
+// (row_shr 1/2/4/8), then row_bcast:15 and row_bcast:31 carry the row totals forward.
+// Validated against a sequential prefix sum by tools/scan_probe.hip.
+DEV uint32_t wave_scan(uint32_t x) {
+    x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x111, 0xF, 0xF, false));
+    x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x112, 0xF, 0xF, false));
+    x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x114, 0xF, 0xF, false));
+    x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x118, 0xF, 0xF, false));
+    x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x142, 0xA, 0xF, false));
+    x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x143, 0xC, 0xF, false));
+    return x;
 }
-DEV uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-    return v;
-}
+DEV uint32_t wave_sum(uint32_t v) { return uint32_t(__builtin_amdgcn_readlane(int(wave_scan(v)), 63)); }
 DEV u64 wave_sum64(u64 v) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
@@ -271,12 +269,7 @@ DEV uint32_t split_block(Doc &D, uint32_t b) {
 // Insert the run [lv, lv+k) at cursor c (all new items visible).
 DEV void insert_run(Doc &D, Cursor c, uint32_t lv, uint32_t k, uint32_t ol, uint32_t orr) {
     const uint32_t l = lane_id();
-    for (uint32_t j = l; j < k; j += 64) {
-        const uint32_t it = lv + j;
-        D.st[it] = 1;
-        D.aux[it] = j == 0 ? ol : it - 1;
-        D.orr[it] = orr;
-    }
+    const uint32_t lv0 = lv, k0 = k;
     uint32_t b = c.b, s = c.s;
     while (k > 0) {
         if (!charge(D)) return;
@@ -316,6 +309,13 @@ DEV void insert_run(Doc &D, Cursor c, uint32_t lv, uint32_t k, uint32_t ol, uint
         k -= m;
         s += m;
     }
+    // per-item metadata last: origin loads issued before the block work have landed by now
+    for (uint32_t j = l; j < k0; j += 64) {
+        const uint32_t it = lv0 + j;
+        D.st[it] = 1;
+        D.aux[it] = j == 0 ? ol : it - 1;
+        D.orr[it] = orr;
+    }
 }
 
 // YjsMod tie-break by agent name rank then seq (merge.rs:199-218).
@@ -344,19 +344,21 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
     } else {
         Cursor c;
         if (!find_vis(D, pos - 1, c)) { fail(D, ErrCheckout, 13); return; }
-        ol = U(D.items[size_t(c.b) * BLK + c.s]);
+        ol = D.items[size_t(c.b) * BLK + c.s];   // same value in every lane; consumed late
         cur.b = c.b;
         cur.s = c.s + 1;
     }
     normalize(D, cur);
     Cursor rc;
     const bool has_r = next_live(D, cur, rc);
-    const uint32_t orr = has_r ? U(D.items[size_t(rc.b) * BLK + rc.s]) : END_ID;
+    const uint32_t orr = has_r ? D.items[size_t(rc.b) * BLK + rc.s] : END_ID;
     const bool at_end = cur.s >= U(D.bcnt[cur.b]);
     const bool direct = has_r ? (rc.b == cur.b && rc.s == cur.s) : at_end;
     if (!direct) {
         // concurrent NIY items between cursor and origin_right: YjsMod scan
-        const uint64_t my_l = rank_left(D, ol), my_r = rank_right(D, orr);
+        ol = U(ol);
+        const uint32_t orr_u = U(orr);
+        const uint64_t my_l = rank_left(D, ol), my_r = rank_right(D, orr_u);
         uint32_t new_rank = 0, new_seq = 0;
         agent_of(D, lv, new_rank, new_seq);
         bool scanning = false;
@@ -365,12 +367,12 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
             if (!charge(D)) return;
             if (c.s >= U(D.bcnt[c.b])) break;   // reached the end of the document
             const uint32_t o = U(D.items[size_t(c.b) * BLK + c.s]);
-            if (o == orr) break;
+            if (o == orr_u) break;
             const uint64_t ol_o = rank_left(D, U(D.aux[o]));
             if (ol_o < my_l) break;
             if (ol_o == my_l) {
                 const uint32_t orr_o = U(D.orr[o]);
-                if (orr_o == orr) {
+                if (orr_o == orr_u) {
                     uint32_t r2, s2;
                     agent_of(D, o, r2, s2);
                     const bool ins_here = new_rank < r2 || (new_rank == r2 && new_seq < s2);
@@ -568,25 +570,32 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
     D.steps = 0;
     D.step_limit = 64ull * (uint64_t(D.ncmd) + D.n_lv) + 4096;
     D.site = 0;
-    for (uint32_t ci = 0; ci < D.ncmd && !D.err; ci++) {
-        D.ci = ci;
-        Cmd c = D.cmds[ci];
-        c.op = U(c.op); c.lv = U(c.lv); c.len = U(c.len); c.pos = U(c.pos);
-        const uint32_t op = c.op & 15u;
-        if (c.len == 0 || c.lv >= D.n_lv || c.len > D.n_lv - c.lv) { fail(D, ErrCheckout, 17); break; }
-        if (!charge(D)) break;
-        switch (op) {
-            case CMD_INS: do_insert(D, c.lv, c.len, c.pos); break;
-            case CMD_DEL: do_delete(D, c.lv, c.len, c.pos, (c.op & 16u) != 0); break;
-            case CMD_ADV_INS: toggle_run<true, false>(D, c.lv, c.len); break;
-            case CMD_ADV_DEL: toggle_run<true, true>(D, c.lv, c.len); break;
-            case CMD_RET_INS: toggle_run<false, false>(D, c.lv, c.len); break;
-            case CMD_RET_DEL: toggle_run<false, true>(D, c.lv, c.len); break;
-            default: fail(D, ErrCheckout, 18); break;
-        }
-        if (D.debug && !D.err) {
-            const uint32_t code = check_invariants(D, res);
-            if (code) fail(D, ErrCheckout, code);
+    // commands are fetched 64 at a time (one per lane) and broadcast with readlane
+    for (uint32_t base = 0; base < D.ncmd && !D.err; base += 64) {
+        const uint32_t n_here = min(64u, D.ncmd - base);
+        Cmd pre = {0, 0, 0, 0};
+        if (l < n_here) pre = D.cmds[base + l];
+        for (uint32_t j = 0; j < n_here && !D.err; j++) {
+            const uint32_t ci = base + j;
+            D.ci = ci;
+            Cmd c;
+            c.op = bcast(pre.op, j); c.lv = bcast(pre.lv, j); c.len = bcast(pre.len, j); c.pos = bcast(pre.pos, j);
+            const uint32_t op = c.op & 15u;
+            if (c.len == 0 || c.lv >= D.n_lv || c.len > D.n_lv - c.lv) { fail(D, ErrCheckout, 17); break; }
+            if (!charge(D)) break;
+            switch (op) {
+                case CMD_INS: do_insert(D, c.lv, c.len, c.pos); break;
+                case CMD_DEL: do_delete(D, c.lv, c.len, c.pos, (c.op & 16u) != 0); break;
+                case CMD_ADV_INS: toggle_run<true, false>(D, c.lv, c.len); break;
+                case CMD_ADV_DEL: toggle_run<true, true>(D, c.lv, c.len); break;
+                case CMD_RET_INS: toggle_run<false, false>(D, c.lv, c.len); break;
+                case CMD_RET_DEL: toggle_run<false, true>(D, c.lv, c.len); break;
+                default: fail(D, ErrCheckout, 18); break;
+            }
+            if (D.debug && !D.err) {
+                const uint32_t code = check_invariants(D, res);
+                if (code) fail(D, ErrCheckout, code);
+            }
         }
     }
     uint32_t len = 0;
