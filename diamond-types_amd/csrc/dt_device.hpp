@@ -15,7 +15,10 @@ struct DocDesc {
     uint64_t blk_off;       // into items (blocks of 64 uint32)
     uint64_t out_off;       // into out (bytes)
     uint64_t gidx_off;      // into gidx (bytes), large-document tier only
+    uint64_t tlist_off;     // into tlist (uint32 units)
     uint32_t ncmd, n_lv, n_aruns, max_blocks, out_cap, content_len;
+    uint32_t ascii;         // every inserted char is one byte
+    uint32_t pad;
 };
 
 struct DocResult {
@@ -23,17 +26,22 @@ struct DocResult {
     uint64_t hash;
     uint32_t n_items, n_blocks;
     uint32_t fail_cmd, fail_site;   // diagnostics: command index and code site of the first error
-    uint32_t dbg[10];               // DTGPU_DEBUG invariant-failure detail
+    uint32_t dbg[16];               // DTGPU_DEBUG invariant-failure detail / cycle profile
 };
+
+// Packed per-item location word (dt_replay.hip): count | block | slot.
+constexpr uint32_t LOC_CNT_SHIFT = 24;
+constexpr uint32_t LOC_BLK_SHIFT = 6;
+constexpr uint32_t LOC_BLK_MASK = 0x3FFFF;
+constexpr uint32_t LOC_MAX_BLOCKS = LOC_BLK_MASK + 1;
 
 struct BatchParams {
     const Cmd *cmds;
+    const uint32_t *tlist;
     const uint32_t *cbyte;
     const uint8_t *content;
     const uint32_t *aruns;
-    uint8_t *st;
-    uint32_t *blk;
-    uint8_t *slot;
+    uint32_t *loc;
     uint32_t *aux;
     uint32_t *orr;
     uint32_t *items;
@@ -44,7 +52,7 @@ struct BatchParams {
     uint32_t n_list;
     uint32_t lds_blocks;    // block-index capacity held in LDS (small tier)
     uint32_t *counter;      // work-queue head, zeroed before each launch
-    uint32_t debug;         // DTGPU_DEBUG: device printf tracing
+    uint32_t debug;         // DTGPU_DEBUG: bit 0 invariant checks, bit 1 cycle profile
     DocResult *results;
 };
 

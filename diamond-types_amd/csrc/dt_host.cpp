@@ -700,8 +700,9 @@ Status decode_dt(const uint8_t *data, size_t len, bool ignore_crc, HostOpLog &o)
 // ------------------------------------------------------------------------------------------
 Status build_plan(const HostOpLog &o, Plan &plan) {
     plan.cmds.clear();
+    plan.tlist.clear();
     plan.agent_runs.clear();
-    if (o.n_lv >= 0xFFFFFFF0ull) return ErrCapacity;
+    if (o.n_lv >= MAX_PLAN_LV) return ErrCapacity;
     if (!o.content_complete) return ErrCheckout;   // content.unwrap() in apply_to (merge.rs:329)
 
     // agent name ranks for the YjsMod tie-break (byte-wise name order, merge.rs:199-218)
@@ -734,32 +735,21 @@ Status build_plan(const HostOpLog &o, Plan &plan) {
         auto it = std::upper_bound(ops.begin(), ops.end(), lv, [](uint64_t v, const OpRun &r) { return v < r.lv + r.len; });
         return size_t(it - ops.begin());
     };
+    // retreat / advance entries of one walk step, labelled Ins/Del per op run
     auto emit_state = [&](uint64_t s, uint64_t e, bool retreat) {
         if (s >= e) return;
-        if (retreat) {
-            size_t ri = run_of(e - 1);
-            uint64_t hi = e;
-            while (hi > s) {
-                const OpRun &r = ops[ri];
-                const uint64_t lo = std::max(s, r.lv);
-                plan.cmds.push_back(Cmd{r.kind ? uint32_t(CMD_RET_DEL) : uint32_t(CMD_RET_INS), uint32_t(lo), uint32_t(hi - lo), 0});
-                plan.n_retreat += hi - lo;
-                hi = lo;
-                if (ri == 0) break;
-                ri--;
-            }
-        } else {
-            size_t ri = run_of(s);
-            uint64_t lo = s;
-            while (lo < e) {
-                const OpRun &r = ops[ri];
-                const uint64_t hi = std::min(e, r.lv + r.len);
-                plan.cmds.push_back(Cmd{r.kind ? uint32_t(CMD_ADV_DEL) : uint32_t(CMD_ADV_INS), uint32_t(lo), uint32_t(hi - lo), 0});
-                plan.n_advance += hi - lo;
-                lo = hi;
-                ri++;
-            }
+        size_t ri = run_of(s);
+        for (uint64_t lo = s; lo < e; ri++) {
+            const OpRun &r = ops[ri];
+            const uint64_t hi = std::min(e, r.lv + r.len);
+            const uint32_t tag = (r.kind ? TL_DEL : 0u) | (retreat ? 0u : TL_ADV);
+            for (uint64_t v = lo; v < hi; v++) plan.tlist.push_back(uint32_t(v) | tag);
+            lo = hi;
         }
+    };
+    auto flush_step = [&](size_t from) {
+        if (plan.tlist.size() > from)
+            plan.cmds.push_back(Cmd{CMD_TOG, uint32_t(from), uint32_t(plan.tlist.size() - from), 0});
     };
     auto emit_apply = [&](uint64_t s, uint64_t e) {
         size_t ri = run_of(s);
@@ -790,8 +780,10 @@ Status build_plan(const HostOpLog &o, Plan &plan) {
         visited[idx] = 1;
         const GraphEntry &e = E[idx];
         o.graph.diff_rev(frontier, e.parents, only_a, only_b);
-        for (auto &rg : only_a) emit_state(rg.first, rg.second, true);                   // descending
-        for (auto it = only_b.rbegin(); it != only_b.rend(); ++it) emit_state(it->first, it->second, false);
+        const size_t t0 = plan.tlist.size();
+        for (auto &rg : only_a) { emit_state(rg.first, rg.second, true); plan.n_retreat += rg.second - rg.first; }
+        for (auto &rg : only_b) { emit_state(rg.first, rg.second, false); plan.n_advance += rg.second - rg.first; }
+        flush_step(t0);
         emit_apply(e.start, e.end);
         frontier.assign(1, e.end - 1);
         plan.n_steps++;
@@ -802,6 +794,13 @@ Status build_plan(const HostOpLog &o, Plan &plan) {
             if (ok) todo.push_back(c);
         }
     }
+    // advance to the tip: the tracker's visible set is then the checkout (list/merge.rs:63-95)
+    o.graph.diff_rev(frontier, o.version, only_a, only_b);
+    if (!only_a.empty()) return ErrCheckout;   // the tip contains every LV
+    const size_t t0 = plan.tlist.size();
+    for (auto &rg : only_b) { emit_state(rg.first, rg.second, false); plan.n_tip_advance += rg.second - rg.first; }
+    flush_step(t0);
+    if (plan.tlist.size() >= 0xFFFFFFFFull) return ErrCapacity;
     return OK;
 }
 

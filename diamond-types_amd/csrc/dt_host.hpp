@@ -77,13 +77,20 @@ bool utf8_valid(const uint8_t *s, size_t n);
 inline uint32_t utf8_len(uint8_t c) { return c < 0x80 ? 1 : (c & 0xE0) == 0xC0 ? 2 : (c & 0xF0) == 0xE0 ? 3 : 4; }
 
 // Device command stream (consumed by dt_replay.hip).  One command = 16 bytes.
-enum CmdOp : uint32_t { CMD_INS = 0, CMD_DEL = 1, CMD_ADV_INS = 2, CMD_ADV_DEL = 3, CMD_RET_INS = 4, CMD_RET_DEL = 5 };
+//   INS {lv, len, pos}          apply an insert run at visible position pos
+//   DEL {lv, len, pos} (+fwd)   apply a delete run (op bit 4: forward; clear: backspace run)
+//   TOG {off, n}                one walk step's retreat + advance set: n tlist entries from off
+enum CmdOp : uint32_t { CMD_INS = 0, CMD_DEL = 1, CMD_TOG = 2 };
 struct Cmd { uint32_t op; uint32_t lv; uint32_t len; uint32_t pos; };   // op: bits 0-3 opcode, bit 4 fwd
+// tlist entry: LV | is_del << 30 | advance << 31
+constexpr uint32_t TL_DEL = 1u << 30, TL_ADV = 1u << 31;
+constexpr uint64_t MAX_PLAN_LV = 1ull << 30;
 
 struct Plan {
     std::vector<Cmd> cmds;
+    std::vector<uint32_t> tlist;
     std::vector<uint32_t> agent_runs;   // triples (lv_start, name_rank, seq_start) for YjsMod tie-breaks
-    uint64_t n_steps = 0, n_retreat = 0, n_advance = 0;
+    uint64_t n_steps = 0, n_retreat = 0, n_advance = 0, n_tip_advance = 0;
 };
 
 // SpanningTreeWalker over the whole graph from ROOT (src/listmerge/txn_trace.rs:114-333) turned

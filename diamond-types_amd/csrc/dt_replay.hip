@@ -9,19 +9,25 @@
 //   block idx  per block: visible mask, live (non-NIY) mask, item count, order position;
 //              per 64 blocks (superblock): visible / item totals.  In LDS for documents
 //              whose block count fits the LDS budget, in HBM otherwise (same code).
-//   per-LV     state (0 NIY, 1 inserted, k>=2 deleted k-1 times; bit7 = ever_deleted),
-//              block id, slot, origin_left or delete target, origin_right (HBM).
+//   loc[lv]    one packed word per inserted LV: count (8 bits: 0 NIY, 1 inserted, k>=2
+//              deleted k-1 times) | block (18 bits) | slot (6 bits).  Every access is an
+//              L2-coherent (sc1) atomic or load, so the returning atomic of a retreat/advance
+//              hands back the item's position and its old state in one round trip.
+//   aux[lv]    Ins: origin_left; Del: the item it deleted.   orr[lv]: origin_right.
 //
-// Positional lookups are wave-parallel: a 64-lane prefix scan over superblock totals, a
-// second over the 64 blocks of the chosen superblock, then a ballot select of the k-th set
-// bit inside the block's visible mask.  Retreat/advance commands are lane-parallel over the
-// LVs of one run (distinct items by construction), with LDS atomics on the masks.
-// Materialisation walks blocks in order and stream-compacts never-deleted chars (prefix
-// scan), writing UTF-8 bytes and an order-sensitive hash.
+// Commands: INS / DEL apply one op run; TOG applies one walk step's whole retreat + advance
+// set in one lane-parallel pass.  Counters make that legal: a retreat subtracts one, an advance
+// adds one, visibility (count == 1) and liveness (count >= 1) flip by XOR whenever the returned
+// old count crosses the boundary, and XOR / add commute, so the pass ends in the state the
+// reference reaches by retreating in descending LV order and then advancing
+// (advance_retreat.rs:58-153).  Intermediate counts never go negative: the retreat set is
+// contained in the current version.
 //
-// Memory ordering: every cross-lane hand-off stays inside one wavefront; a wavefront-scope
-// fence (compiler barrier) separates the phases (AMDGPU memory model: no cache maintenance is
-// needed between lanes of one wavefront).
+// The plan ends with a TOG that advances to the tip, so the final visible set is the checkout:
+// materialisation stream-compacts visible items in document order (list/merge.rs:63-95).
+//
+// Document order is a total order on (order position of the block, slot): YjsMod compares
+// those keys directly (merge.rs:154-278) instead of counting items.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -38,12 +44,16 @@ DEV uint32_t lane_id() { return __lane_id(); }
 DEV void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); __builtin_amdgcn_wave_barrier(); }
 DEV uint32_t bcast(uint32_t v, uint32_t l) { return uint32_t(__builtin_amdgcn_readlane(int(v), int(l))); }
 DEV uint32_t first_lane(u64 m) { return uint32_t(__ffsll((long long)m) - 1); }
+DEV uint32_t last_lane(u64 m) { return 63u - uint32_t(__clzll((long long)m)); }
 // Wave-uniform values are pinned to scalar registers: control flow that depends on them is
 // scalar (no exec-mask loops), which is both what the algorithm means and what keeps hipcc
 // from treating the sequential replay as divergent.
 DEV uint32_t U(uint32_t v) { return uint32_t(__builtin_amdgcn_readfirstlane(int(v))); }
 DEV u64 U64(u64 v) {   // (readfirstlane returns int: keep both halves unsigned)
     return (u64(U(uint32_t(v >> 32))) << 32) | u64(U(uint32_t(v)));
+}
+DEV uint32_t shfl(uint32_t v, uint32_t src) {
+    return uint32_t(__builtin_amdgcn_ds_bpermute(int(src << 2), int(v)));
 }
 
 // Inclusive wave prefix sum over 64 lanes with DPP: Hillis-Steele inside each 16-lane row
@@ -76,20 +86,45 @@ constexpr uint32_t BLK = 64;   // slots per block
 constexpr uint32_t SB = 64;    // blocks per superblock
 constexpr uint32_t ROOT_ID = 0xFFFFFFFFu;
 constexpr uint32_t END_ID = 0xFFFFFFFEu;
-constexpr uint8_t DEL_BIT = 0x80;
+constexpr uint32_t NO_BLOCK = 0xFFFFFFFFu;
+constexpr uint32_t CNT_ONE = 1u << LOC_CNT_SHIFT;
+
+DEV uint32_t loc_blk(uint32_t w) { return (w >> LOC_BLK_SHIFT) & LOC_BLK_MASK; }
+DEV uint32_t loc_slot(uint32_t w) { return w & 63u; }
+DEV uint32_t loc_cnt(uint32_t w) { return w >> LOC_CNT_SHIFT; }
+
+// loc words: L2-coherent accesses only (returning atomics and plain loads must not meet a
+// stale L1 line).
+DEV uint32_t loc_load(const uint32_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+DEV void loc_store(uint32_t *p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+DEV uint32_t loc_add(uint32_t *p, uint32_t d) { return __hip_atomic_fetch_add(p, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// Block-index accessors.  LDS tier: plain LDS (one wave owns the workgroup).  HBM tier: every
+// index word touched by an atomic is read L2-coherently.
+template <bool L> DEV uint32_t ix_ld(const uint32_t *p) {
+    if (L) return *p;
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <bool L> DEV u64 ix_ld64(const u64 *p) {
+    if (L) return *p;
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <bool L> DEV uint32_t ix_ld8(const uint8_t *p) { return *p; }
+
+enum ProfSlot { P_INS = 0, P_DEL, P_TOG, P_MAT, P_YJS, P_SPLIT, P_FIND, P_BLOAD, P_ORR, P_RUN, P_N_YJS, P_N_SPLIT, P_N };
 
 struct Doc {
     // inputs
     const Cmd *cmds;
     uint32_t ncmd, n_lv;
+    const uint32_t *tlist;
     const uint32_t *cbyte;
     const uint8_t *content;
     const uint32_t *aruns;
     uint32_t n_aruns;
+    uint32_t ascii;
     // per-LV state
-    uint8_t *st;
-    uint32_t *blk;
-    uint8_t *slot;
+    uint32_t *loc;
     uint32_t *aux;
     uint32_t *orr;
     // blocks
@@ -107,31 +142,32 @@ struct Doc {
     uint32_t site, ci;
     uint64_t steps, step_limit;   // watchdog: every loop iteration is charged; a bound
                                   // violation ends the document with ErrCapacity
+    uint64_t prof[P_N];
 };
 
-// Charge one loop iteration; returns false (and flags the document) past the budget, so every
-// loop in the replay provably terminates whatever the input.
 DEV void fail(Doc &D, uint32_t code, uint32_t site) {
     if (!D.err) { D.err = code; D.site = site; }
 }
+// Charge one loop iteration; returns false (and flags the document) past the budget, so every
+// loop in the replay provably terminates whatever the input.
 DEV bool charge(Doc &D) {
     if (++D.steps > D.step_limit) { fail(D, ErrCapacity, 1); return false; }
     return true;
 }
-
-struct Cursor { uint32_t b, s; };
+template <bool PROF> DEV uint64_t tick() { return PROF ? __builtin_amdgcn_s_memtime() : 0; }
 
 // ---- order-statistic queries -------------------------------------------------------------
 
 // Item holding visible index p (content-tree cursor_at_content_pos, root.rs:50-89).
-DEV bool find_vis(Doc &D, uint32_t p, Cursor &out) {
+template <bool L>
+DEV bool find_vis(Doc &D, uint32_t p, uint32_t &ob, uint32_t &os) {
     const uint32_t l = lane_id();
     const uint32_t nsb = (D.nb + SB - 1) / SB;
     uint32_t base = 0, sb = 0;
     bool found = false;
     for (uint32_t c = 0; c < nsb; c += 64) {
         const uint32_t i = c + l;
-        const uint32_t v = i < nsb ? D.svis[i] : 0;
+        const uint32_t v = i < nsb ? ix_ld<L>(D.svis + i) : 0;
         const uint32_t inc = wave_scan(v);
         const u64 m = __ballot(base + inc > p);
         if (m) {
@@ -145,81 +181,56 @@ DEV bool find_vis(Doc &D, uint32_t p, Cursor &out) {
     }
     if (!found) return false;
     const uint32_t i = sb * SB + l;
-    const uint32_t b = i < D.nb ? D.ord[i] : 0;
-    const uint32_t v = i < D.nb ? uint32_t(__popcll(D.mvis[b])) : 0;
+    const uint32_t b = i < D.nb ? ix_ld<L>(D.ord + i) : 0;
+    const uint32_t v = i < D.nb ? uint32_t(__popcll(ix_ld64<L>(D.mvis + b))) : 0;
     const uint32_t inc = wave_scan(v);
     const u64 m = __ballot(base + inc > p);
     if (!m) return false;
     const uint32_t fl = first_lane(m);
-    const uint32_t bb = bcast(b, fl);
+    const uint32_t bb = U(bcast(b, fl));
     const uint32_t off = p - base - bcast(inc - v, fl);
-    const u64 mv = U64(D.mvis[bb]);
+    const u64 mv = U64(ix_ld64<L>(D.mvis + bb));
     const bool set = (mv >> l) & 1ull;
     const uint32_t before = uint32_t(__popcll(mv & ((1ull << l) - 1ull)));
     const u64 m2 = __ballot(set && before == off);
     if (!m2) return false;
-    out.b = bb;
-    out.s = first_lane(m2);
+    ob = bb;
+    os = first_lane(m2);
     return true;
 }
 
-// Document index of an item (number of items before it in list order).
-DEV uint64_t rank_of(Doc &D, uint32_t item) {
-    const uint32_t l = lane_id();
-    uint32_t b = U(D.blk[item]), s = U(D.slot[item]);
-    if (b >= D.nb) { fail(D, ErrCheckout, 11); b = 0; s = 0; }
-    const uint32_t p = U(D.opos[b]), sb = p / SB;
-    uint32_t acc = 0;
-    for (uint32_t c = 0; c < sb; c += 64) {
-        const uint32_t i = c + l;
-        acc += i < sb ? D.scnt[i] : 0;
-    }
-    {
-        const uint32_t i = sb * SB + l;
-        acc += i < p ? uint32_t(D.bcnt[D.ord[i]]) : 0;
-    }
-    return uint64_t(wave_sum(acc)) + s;
+// Document-order key of an item: (order position of its block, slot).
+template <bool L>
+DEV uint32_t key_of(const Doc &D, uint32_t item) {
+    const uint32_t w = loc_load(D.loc + item);
+    return (ix_ld<L>(D.opos + loc_blk(w)) << 6) | loc_slot(w);
 }
 
-// Move a cursor at the end of a block to the start of the next block in order.
-DEV void normalize(Doc &D, Cursor &c) {
-    while (c.s >= U(D.bcnt[c.b])) {
-        if (!charge(D)) return;
-        const uint32_t p = U(D.opos[c.b]) + 1;
-        if (p >= D.nb) return;   // end of document
-        c.b = U(D.ord[p]);
-        c.s = 0;
-    }
-}
-
-// First item at/after c that is not NIY (origin_right search, merge.rs:405-423).
-DEV bool next_live(Doc &D, Cursor c, Cursor &out) {
+// First live (non-NIY) item in a block after order position p0 (origin_right search,
+// merge.rs:405-423).  Returns NO_BLOCK when there is none.
+template <bool L>
+DEV uint32_t next_live_block(Doc &D, uint32_t p0) {
     const uint32_t l = lane_id();
-    const u64 ml = c.s >= 64 ? 0ull : (U64(D.mlive[c.b]) & (~0ull << c.s));
-    if (ml) { out.b = c.b; out.s = first_lane(ml); return true; }
-    for (uint32_t p0 = U(D.opos[c.b]) + 1; p0 < D.nb; p0 += 64) {
-        const uint32_t i = p0 + l;
-        const uint32_t b = i < D.nb ? D.ord[i] : 0;
-        const u64 m = __ballot(i < D.nb && D.mlive[b] != 0ull);
-        if (m) {
-            const uint32_t fl = first_lane(m);
-            out.b = bcast(b, fl);
-            out.s = first_lane(U64(D.mlive[out.b]));
-            return true;
-        }
+    for (uint32_t p = p0; p < D.nb; p += 64) {
+        if (!charge(D)) return NO_BLOCK;
+        const uint32_t i = p + l;
+        const uint32_t b = i < D.nb ? ix_ld<L>(D.ord + i) : 0;
+        const u64 m = __ballot(i < D.nb && ix_ld64<L>(D.mlive + b) != 0ull);
+        if (m) return U(bcast(b, first_lane(m)));
     }
-    return false;
+    return NO_BLOCK;
 }
 
 // ---- block maintenance ---------------------------------------------------------------------
 
+template <bool L>
 DEV void recompute_sb(Doc &D, uint32_t from_sb) {
     const uint32_t l = lane_id();
     const uint32_t nsb = (D.nb + SB - 1) / SB;
     for (uint32_t s = from_sb; s < nsb; s++) {
         const uint32_t i = s * SB + l;
-        const uint32_t b = i < D.nb ? D.ord[i] : 0;
-        const uint32_t v = i < D.nb ? uint32_t(__popcll(D.mvis[b])) : 0;
+        const uint32_t b = i < D.nb ? ix_ld<L>(D.ord + i) : 0;
+        const uint32_t v = i < D.nb ? uint32_t(__popcll(ix_ld64<L>(D.mvis + b))) : 0;
         const uint32_t c = i < D.nb ? uint32_t(D.bcnt[b]) : 0;
         const uint32_t tv = wave_sum(v), tc = wave_sum(c);
         if (l == 0) { D.svis[s] = tv; D.scnt[s] = tc; }
@@ -227,34 +238,34 @@ DEV void recompute_sb(Doc &D, uint32_t from_sb) {
     wave_fence();
 }
 
-// Split a full block: its upper half moves to a new block placed right after it in order.
-DEV uint32_t split_block(Doc &D, uint32_t b) {
+// Split the full block b (its items in `it` lane by lane): the upper half moves to a new block
+// placed right after b in document order.
+template <bool L>
+DEV uint32_t split_block(Doc &D, uint32_t b, uint32_t it) {
     const uint32_t l = lane_id();
     if (D.nb >= D.max_blocks) { fail(D, ErrCapacity, 12); return 0; }
     const uint32_t b2 = D.nb;
-    uint32_t *src = D.items + size_t(b) * BLK;
-    uint32_t *dst = D.items + size_t(b2) * BLK;
     if (l >= BLK / 2) {
-        const uint32_t v = src[l];
-        dst[l - BLK / 2] = v;
-        D.blk[v] = b2;
-        D.slot[v] = uint8_t(l - BLK / 2);
+        D.items[size_t(b2) * BLK + (l - BLK / 2)] = it;
+        // (b, s) -> (b2, s - 32): one field-wise delta on the packed word
+        loc_add(D.loc + it, ((b2 - b) << LOC_BLK_SHIFT) - BLK / 2);
     }
-    const uint32_t p = U(D.opos[b]) + 1;
+    const uint32_t p = ix_ld<L>(D.opos + b) + 1;
     // shift ord[p .. nb) right by one, highest chunk first
     for (int c = int(D.nb) - 1; c >= int(p); c -= 64) {
         const int i = c - int(l);
         uint32_t v = 0;
-        if (i >= int(p)) v = D.ord[i];
+        if (i >= int(p)) v = ix_ld<L>(D.ord + i);
         wave_fence();
         if (i >= int(p)) { D.ord[i + 1] = v; D.opos[v] = uint32_t(i + 1); }
         wave_fence();
     }
     if (l == 0) {
-        D.mvis[b2] = D.mvis[b] >> 32;
-        D.mvis[b] &= 0xFFFFFFFFull;
-        D.mlive[b2] = D.mlive[b] >> 32;
-        D.mlive[b] &= 0xFFFFFFFFull;
+        const u64 mv = ix_ld64<L>(D.mvis + b), ml = ix_ld64<L>(D.mlive + b);
+        D.mvis[b2] = mv >> 32;
+        D.mvis[b] = mv & 0xFFFFFFFFull;
+        D.mlive[b2] = ml >> 32;
+        D.mlive[b] = ml & 0xFFFFFFFFull;
         D.bcnt[b2] = BLK / 2;
         D.bcnt[b] = BLK / 2;
         D.ord[p] = b2;
@@ -262,282 +273,382 @@ DEV uint32_t split_block(Doc &D, uint32_t b) {
     }
     wave_fence();
     D.nb++;
-    recompute_sb(D, (p - 1) / SB);
+    recompute_sb<L>(D, (p - 1) / SB);
     return b2;
 }
 
-// Insert the run [lv, lv+k) at cursor c (all new items visible).
-DEV void insert_run(Doc &D, Cursor c, uint32_t lv, uint32_t k, uint32_t ol, uint32_t orr) {
+// Insert the run [lv, lv+k) before slot s of block b (all new items visible).  `it` holds the
+// block's items lane by lane; lanes >= the block count are don't-care.
+template <bool L, bool PROF>
+DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, uint32_t lv, uint32_t k, uint32_t ol,
+                    uint32_t orr) {
     const uint32_t l = lane_id();
     const uint32_t lv0 = lv, k0 = k;
-    uint32_t b = c.b, s = c.s;
     while (k > 0) {
         if (!charge(D)) return;
-        const uint32_t cnt = U(D.bcnt[b]);
+        const uint32_t cnt = U(ix_ld8<L>(D.bcnt + b));
         if (cnt == BLK) {
-            const uint32_t b2 = split_block(D, b);
+            const uint64_t t0 = tick<PROF>();
+            const uint32_t b2 = split_block<L>(D, b, it);
             if (D.err) return;
-            if (s > BLK / 2) { b = b2; s -= BLK / 2; }
+            if (s > BLK / 2) {
+                b = b2;
+                s -= BLK / 2;
+                it = shfl(it, (l + BLK / 2) & 63u);
+            }
+            if (PROF) { D.prof[P_SPLIT] += tick<PROF>() - t0; D.prof[P_N_SPLIT]++; }
             continue;
         }
         const uint32_t m = min(k, BLK - cnt);
         uint32_t *items = D.items + size_t(b) * BLK;
-        const uint32_t v = l < cnt ? items[l] : 0;
-        wave_fence();
-        if (l >= s && l < cnt) { items[l + m] = v; D.slot[v] = uint8_t(l + m); }
-        if (l >= s && l < s + m) {
-            const uint32_t it = lv + (l - s);
-            items[l] = it;
-            D.slot[it] = uint8_t(l);
-            D.blk[it] = b;
+        if (l >= s && l < cnt) {
+            items[l + m] = it;
+            loc_add(D.loc + it, m);   // slot += m
         }
+        if (l >= s && l < s + m) {
+            const uint32_t nit = lv + (l - s);
+            items[l] = nit;
+            loc_store(D.loc + nit, CNT_ONE | (b << LOC_BLK_SHIFT) | l);
+        }
+        const uint32_t shifted = shfl(it, l >= m ? l - m : l);
+        it = l < s ? it : (l < s + m ? lv + (l - s) : shifted);
         if (l == 0) {
             const u64 low = s == 0 ? 0ull : (~0ull >> (64 - s));
             const u64 ins = (m == 64 ? ~0ull : ((1ull << m) - 1ull)) << s;
-            const u64 mv = D.mvis[b], ml = D.mlive[b];
+            const u64 mv = ix_ld64<L>(D.mvis + b), ml = ix_ld64<L>(D.mlive + b);
             const u64 hv = m == 64 ? 0ull : ((mv & ~low) << m);
             const u64 hl = m == 64 ? 0ull : ((ml & ~low) << m);
             D.mvis[b] = (mv & low) | hv | ins;
             D.mlive[b] = (ml & low) | hl | ins;
             D.bcnt[b] = uint8_t(cnt + m);
-            const uint32_t sbi = D.opos[b] / SB;
-            D.svis[sbi] += m;
-            D.scnt[sbi] += m;
+            const uint32_t sbi = ix_ld<L>(D.opos + b) / SB;
+            D.svis[sbi] = ix_ld<L>(D.svis + sbi) + m;
+            D.scnt[sbi] = ix_ld<L>(D.scnt + sbi) + m;
         }
         wave_fence();
         lv += m;
         k -= m;
         s += m;
     }
-    // per-item metadata last: origin loads issued before the block work have landed by now
     for (uint32_t j = l; j < k0; j += 64) {
-        const uint32_t it = lv0 + j;
-        D.st[it] = 1;
-        D.aux[it] = j == 0 ? ol : it - 1;
-        D.orr[it] = orr;
+        const uint32_t nit = lv0 + j;
+        D.aux[nit] = j == 0 ? ol : nit - 1;
+        D.orr[nit] = orr;
     }
 }
 
-// YjsMod tie-break by agent name rank then seq (merge.rs:199-218).
-DEV void agent_of(const Doc &D, uint32_t lv, uint32_t &rank, uint32_t &seq) {
-    uint32_t lo = 0, hi = D.n_aruns;   // last run with start <= lv
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) / 2;
-        if (U(D.aruns[3 * mid]) <= lv) lo = mid; else hi = mid;
+// YjsMod tie-break key of an LV: (agent name rank, seq) (merge.rs:199-218).  64-ary search
+// over the agent runs; `lv` is wave-uniform.
+DEV void agent_of(Doc &D, uint32_t lv, uint32_t &rank, uint32_t &seq) {
+    const uint32_t l = lane_id();
+    uint32_t lo = 0, n = D.n_aruns;   // last run with start <= lv lies in [lo, lo+n)
+    while (n > 64) {
+        if (!charge(D)) { rank = seq = 0; return; }
+        const uint32_t stride = (n + 63) / 64;
+        const uint32_t idx = lo + l * stride;
+        const bool ok = l * stride < n && D.aruns[3 * idx] <= lv;
+        const uint32_t k = uint32_t(__popcll(__ballot(ok)));
+        const uint32_t nlo = lo + (k ? k - 1 : 0) * stride;
+        n = min(stride, lo + n - nlo);
+        lo = nlo;
     }
-    rank = U(D.aruns[3 * lo + 1]);
-    seq = U(D.aruns[3 * lo + 2]) + (lv - U(D.aruns[3 * lo]));
+    const bool ok = l < n && D.aruns[3 * (lo + l)] <= lv;
+    const uint32_t k = uint32_t(__popcll(__ballot(ok)));
+    const uint32_t j = U(lo + (k ? k - 1 : 0));
+    rank = U(D.aruns[3 * j + 1]);
+    seq = U(D.aruns[3 * j + 2]) + (lv - U(D.aruns[3 * j]));
 }
 
-DEV uint64_t rank_left(Doc &D, uint32_t ol) { return ol == ROOT_ID ? 0 : rank_of(D, ol) + 1; }
-DEV uint64_t rank_right(Doc &D, uint32_t orr) { return orr == END_ID ? ~0ull : rank_of(D, orr); }
+// YjsMod integrate (merge.rs:154-278) over the not-inserted-yet items between the cursor
+// (b, s) and origin_right (rb, rs) (rb == NO_BLOCK: END), one block of candidates at a time.
+// Every candidate's keys come in lane-parallel; the sequential scan state machine is resolved
+// with ballots: the first stopping lane ends the scan, and `scanning` is the state after the
+// last event lane before it.  Returns the insertion point in (b, s).
+template <bool L>
+DEV void yjs_scan(Doc &D, uint32_t &b, uint32_t &s, uint32_t rb, uint32_t rs, uint32_t my_l, uint32_t my_r,
+                  uint32_t orr_new, uint32_t lv) {
+    const uint32_t l = lane_id();
+    uint32_t new_rank, new_seq;
+    agent_of(D, lv, new_rank, new_seq);
+    bool scanning = false;
+    uint32_t st_b = 0, st_s = 0;
+    uint32_t cb = b, cs = s;
+    for (;;) {
+        if (!charge(D)) return;
+        const uint32_t cnt = U(ix_ld8<L>(D.bcnt + cb));
+        if (cs >= cnt) {   // next block in document order
+            const uint32_t p = ix_ld<L>(D.opos + cb) + 1;
+            if (p >= D.nb) break;   // end of document
+            cb = U(ix_ld<L>(D.ord + p));
+            cs = 0;
+            continue;
+        }
+        const uint32_t end = cb == rb ? rs : cnt;
+        if (cs >= end) break;   // reached origin_right
+        const bool inr = l >= cs && l < end;
+        const uint32_t o = l < cnt ? D.items[size_t(cb) * BLK + l] : 0;
+        uint32_t ol_o = ROOT_ID, orr_o = END_ID;
+        if (inr) { ol_o = D.aux[o]; orr_o = D.orr[o]; }
+        const uint32_t kl = ol_o == ROOT_ID ? 0u : key_of<L>(D, ol_o) + 1u;
+        const uint32_t kr = orr_o == END_ID ? 0xFFFFFFFFu : key_of<L>(D, orr_o);
+        const bool tie = inr && kl == my_l && orr_o == orr_new;
+        bool new_lt = false;
+        for (u64 mt = __ballot(tie); mt; mt &= mt - 1) {
+            const uint32_t f = first_lane(mt);
+            uint32_t r2, s2;
+            agent_of(D, U(bcast(o, f)), r2, s2);
+            const bool lt = new_rank < r2 || (new_rank == r2 && new_seq < s2);
+            if (l == f) new_lt = lt;
+        }
+        const bool stop = inr && (kl < my_l || (tie && new_lt));
+        const bool setv = inr && kl == my_l && orr_o != orr_new && kr < my_r;
+        const bool clr = inr && kl == my_l && !stop && !setv;
+        const u64 ms = __ballot(stop);
+        const uint32_t lim = ms ? first_lane(ms) : end;
+        const u64 below = lim >= 64 ? ~0ull : ((1ull << lim) - 1ull);
+        const u64 mset = __ballot(setv) & below, mclr = __ballot(clr) & below;
+        if (mset | mclr) {
+            const int lc = mclr ? int(last_lane(mclr)) : -1;
+            const int ls = mset ? int(last_lane(mset)) : -1;
+            if (ls > lc) {
+                const u64 after = lc >= 0 ? (mset & ~((2ull << lc) - 1ull)) : mset;
+                if (lc >= 0 || !scanning) { scanning = true; st_b = cb; st_s = first_lane(after); }
+            } else {
+                scanning = false;
+            }
+        }
+        cs = lim;
+        if (ms) break;
+    }
+    if (scanning) { b = st_b; s = st_s; }
+    else { b = cb; s = cs; }
+    b = U(b);
+    s = U(s);
+}
 
 // Apply an insert run at visible position pos (M2Tracker::apply Ins + integrate,
 // merge.rs:154-278, 383-455).
+template <bool L, bool PROF>
 DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
-    Cursor cur;
-    uint32_t ol;
+    const uint32_t l = lane_id();
+    uint64_t tp = tick<PROF>();
+    uint32_t b, s, s0 = 0;
     if (pos == 0) {
-        ol = ROOT_ID;
-        cur.b = U(D.ord[0]);
-        cur.s = 0;
+        b = U(ix_ld<L>(D.ord + 0));
+        s = 0;
     } else {
-        Cursor c;
-        if (!find_vis(D, pos - 1, c)) { fail(D, ErrCheckout, 13); return; }
-        ol = D.items[size_t(c.b) * BLK + c.s];   // same value in every lane; consumed late
-        cur.b = c.b;
-        cur.s = c.s + 1;
+        if (!find_vis<L>(D, pos - 1, b, s0)) { fail(D, ErrCheckout, 13); return; }
+        s = s0 + 1;
     }
-    normalize(D, cur);
-    Cursor rc;
-    const bool has_r = next_live(D, cur, rc);
-    const uint32_t orr = has_r ? D.items[size_t(rc.b) * BLK + rc.s] : END_ID;
-    const bool at_end = cur.s >= U(D.bcnt[cur.b]);
-    const bool direct = has_r ? (rc.b == cur.b && rc.s == cur.s) : at_end;
-    if (!direct) {
-        // concurrent NIY items between cursor and origin_right: YjsMod scan
-        ol = U(ol);
-        const uint32_t orr_u = U(orr);
-        const uint64_t my_l = rank_left(D, ol), my_r = rank_right(D, orr_u);
-        uint32_t new_rank = 0, new_seq = 0;
-        agent_of(D, lv, new_rank, new_seq);
-        bool scanning = false;
-        Cursor scan_start = cur, c = cur;
-        for (;;) {
-            if (!charge(D)) return;
-            if (c.s >= U(D.bcnt[c.b])) break;   // reached the end of the document
-            const uint32_t o = U(D.items[size_t(c.b) * BLK + c.s]);
-            if (o == orr_u) break;
-            const uint64_t ol_o = rank_left(D, U(D.aux[o]));
-            if (ol_o < my_l) break;
-            if (ol_o == my_l) {
-                const uint32_t orr_o = U(D.orr[o]);
-                if (orr_o == orr_u) {
-                    uint32_t r2, s2;
-                    agent_of(D, o, r2, s2);
-                    const bool ins_here = new_rank < r2 || (new_rank == r2 && new_seq < s2);
-                    if (ins_here) break;
-                    scanning = false;
-                } else {
-                    if (rank_right(D, orr_o) < my_r) {
-                        if (!scanning) { scanning = true; scan_start = c; }
-                    } else scanning = false;
-                }
-            }
-            c.s++;
-            normalize(D, c);
+    if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_FIND] += t - tp; tp = t; }
+    const uint32_t cnt = U(ix_ld8<L>(D.bcnt + b));
+    uint32_t it = l < cnt ? D.items[size_t(b) * BLK + l] : 0;
+    const uint32_t ol = pos == 0 ? ROOT_ID : U(bcast(it, s0));
+    if (PROF) { const uint32_t x = U(it); asm volatile("" :: "s"(x)); const uint64_t t = tick<PROF>(); D.prof[P_BLOAD] += t - tp; tp = t; }
+    // origin_right: first live item at or after the cursor (possibly a deleted one)
+    const u64 ml = s >= 64 ? 0ull : (U64(ix_ld64<L>(D.mlive + b)) & (~0ull << s));
+    uint32_t rb, rs, orr;
+    bool direct;
+    if (ml) {
+        rb = b;
+        rs = first_lane(ml);
+        orr = U(bcast(it, rs));
+        direct = rs == s;
+    } else {
+        const uint32_t p = ix_ld<L>(D.opos + b) + 1;
+        rb = next_live_block<L>(D, p);
+        if (D.err) return;
+        if (rb != NO_BLOCK) {
+            rs = first_lane(U64(ix_ld64<L>(D.mlive + rb)));
+            orr = U(D.items[size_t(rb) * BLK + rs]);
+        } else {
+            rs = 0;
+            orr = END_ID;
         }
-        cur = scanning ? scan_start : c;
+        // direct iff no item lies between the cursor and origin_right
+        if (s < cnt) direct = false;
+        else if (p >= D.nb) direct = true;
+        else direct = rb == U(ix_ld<L>(D.ord + p)) && rs == 0;
     }
-    insert_run(D, cur, lv, k, ol, orr);
+    if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_ORR] += t - tp; tp = t; }
+    if (!direct) {
+        const uint64_t t0 = tick<PROF>();
+        const uint32_t my_l = ol == ROOT_ID ? 0u : U(key_of<L>(D, ol)) + 1u;
+        const uint32_t my_r = orr == END_ID ? 0xFFFFFFFFu : U(key_of<L>(D, orr));
+        const uint32_t b0 = b;
+        yjs_scan<L>(D, b, s, rb, rs, my_l, my_r, orr, lv);
+        if (D.err) return;
+        if (b != b0) {
+            const uint32_t c2 = U(ix_ld8<L>(D.bcnt + b));
+            it = l < c2 ? D.items[size_t(b) * BLK + l] : 0;
+        }
+        if (PROF) { D.prof[P_YJS] += tick<PROF>() - t0; D.prof[P_N_YJS]++; }
+    }
+    if (PROF) tp = tick<PROF>();
+    const uint64_t sp0 = PROF ? D.prof[P_SPLIT] : 0;
+    insert_run<L, PROF>(D, b, s, it, lv, k, ol, orr);
+    if (PROF) D.prof[P_RUN] += tick<PROF>() - tp - (D.prof[P_SPLIT] - sp0);
     D.n_items += k;
 }
 
 // Apply a delete run: n visible items from position pos (merge.rs:457-556).  LV lv+j targets
-// the j-th item (fwd) or the (n-1-j)-th item (reversed / backspace runs).
+// the j-th item (fwd) or the (n-1-j)-th item (reversed / backspace runs, op_metrics.rs:184-202).
+template <bool L>
 DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
     const uint32_t l = lane_id();
     uint32_t j0 = 0;
     while (j0 < n) {
         if (!charge(D)) return;
-        Cursor c;
-        if (!find_vis(D, pos, c)) { fail(D, ErrCheckout, 14); return; }
-        const u64 vm = U64(D.mvis[c.b]) & (~0ull << c.s);
+        uint32_t b, s;
+        if (!find_vis<L>(D, pos, b, s)) { fail(D, ErrCheckout, 14); return; }
+        const u64 vm = U64(ix_ld64<L>(D.mvis + b)) & (~0ull << s);
         const uint32_t avail = uint32_t(__popcll(vm));
         const uint32_t take = min(avail, n - j0);
         const uint32_t r = uint32_t(__popcll(vm & ((1ull << l) - 1ull)));
         const bool sel = ((vm >> l) & 1ull) && r < take;
         const u64 selm = __ballot(sel);
-        bool bad = false;
         if (sel) {
-            const uint32_t item = D.items[size_t(c.b) * BLK + l];
+            const uint32_t item = D.items[size_t(b) * BLK + l];
             const uint32_t j = j0 + r;
             const uint32_t dlv = fwd ? lv + j : lv + n - 1 - j;
-            const uint8_t old = D.st[item];
-            if ((old & 0x7F) != 1) bad = true;
-            D.st[item] = DEL_BIT | 2;
+            loc_add(D.loc + item, CNT_ONE);   // visible (count 1) -> deleted once
             D.aux[dlv] = item;
         }
-        if (__ballot(bad)) { fail(D, ErrCheckout, 15); return; }
         if (l == 0) {
-            D.mvis[c.b] &= ~selm;
-            D.svis[D.opos[c.b] / SB] -= take;
+            D.mvis[b] = ix_ld64<L>(D.mvis + b) & ~selm;
+            const uint32_t sbi = ix_ld<L>(D.opos + b) / SB;
+            D.svis[sbi] = ix_ld<L>(D.svis + sbi) - take;
         }
         wave_fence();
         j0 += take;
     }
 }
 
-// Retreat / advance one run of LVs (advance_retreat.rs:58-153).  Items in one run are
-// distinct, so lanes proceed independently; mask and superblock updates are LDS atomics.
-template <bool ADVANCE, bool IS_DEL>
-DEV void toggle_run(Doc &D, uint32_t lv, uint32_t n) {
+// One walk step's retreat + advance set (advance_retreat.rs:58-153), lane-parallel.
+// Entry: LV | is_del << 30 | advance << 31.
+template <bool L>
+DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n) {
     const uint32_t l = lane_id();
     for (uint32_t j = 0; j < n; j += 64) {
-        const uint32_t v = lv + j + l;
+        if (!charge(D)) return;
         bool bad = false;
         if (j + l < n) {
-            const uint32_t item = IS_DEL ? D.aux[v] : v;
-            if (item >= D.n_lv) {
-                bad = true;
-            } else {
-                const uint8_t old = D.st[item];
-                const uint32_t state = old & 0x7F;
-                uint32_t b = D.blk[item], s = D.slot[item];
-                if (b >= D.nb || s >= BLK || (!IS_DEL && !ADVANCE && state == 0)) { bad = true; b = 0; s = 0; }
-                const u64 bit = 1ull << s;
-                const uint32_t sbi = D.opos[b] / SB;
-                if (bad) {
-                } else if (!IS_DEL) {
-                    if (ADVANCE) {
-                        if (state != 0) bad = true;
-                        D.st[item] = uint8_t(old | 1);
-                        atomicOr(&D.mvis[b], bit);
-                        atomicOr(&D.mlive[b], bit);
-                        atomicAdd(&D.svis[sbi], 1u);
-                    } else {
-                        if (state != 1) bad = true;
-                        D.st[item] = uint8_t(old & DEL_BIT);
-                        atomicAnd(&D.mvis[b], ~bit);
-                        atomicAnd(&D.mlive[b], ~bit);
-                        atomicSub(&D.svis[sbi], 1u);
-                    }
+            const uint32_t e = D.tlist[off + j + l];
+            const uint32_t lv = e & 0x3FFFFFFFu;
+            const bool is_del = (e >> 30) & 1u, adv = (e >> 31) != 0;
+            uint32_t item = lv;
+            if (lv >= D.n_lv) bad = true;
+            else if (is_del) item = D.aux[lv];
+            if (!bad && item >= D.n_lv) bad = true;
+            if (!bad) {
+                const uint32_t old = loc_add(D.loc + item, adv ? CNT_ONE : 0u - CNT_ONE);
+                const uint32_t oc = loc_cnt(old);
+                const uint32_t nc = adv ? oc + 1 : oc - 1;
+                const uint32_t b = loc_blk(old);
+                if ((!adv && oc == 0) || (adv && oc == 255) || b >= D.nb) {
+                    bad = true;
                 } else {
-                    if (ADVANCE) {
-                        if (state == 0 || state >= 0x7F) bad = true;
-                        D.st[item] = uint8_t(DEL_BIT | (state + 1));
-                        if (state == 1) { atomicAnd(&D.mvis[b], ~bit); atomicSub(&D.svis[sbi], 1u); }
-                    } else {
-                        if (state < 2) bad = true;
-                        D.st[item] = uint8_t((old & DEL_BIT) | (state - 1));
-                        if (state == 2) { atomicOr(&D.mvis[b], bit); atomicAdd(&D.svis[sbi], 1u); }
+                    const u64 bit = 1ull << loc_slot(old);
+                    if ((oc == 1) != (nc == 1)) {
+                        atomicXor(&D.mvis[b], bit);
+                        atomicAdd(&D.svis[ix_ld<L>(D.opos + b) / SB], nc == 1 ? 1u : 0xFFFFFFFFu);
                     }
+                    if ((oc != 0) != (nc != 0)) atomicXor(&D.mlive[b], bit);
                 }
             }
         }
         if (__ballot(bad)) { fail(D, ErrCheckout, 16); return; }
-        wave_fence();
     }
+    wave_fence();
 }
 
-// Stream-compact never-deleted chars in document order into out[] (list/merge.rs:63-95).
+// Stream-compact the visible items (the tip's content) in document order into out[]
+// (list/merge.rs:63-95).  G blocks per round keep that many dependent gathers in flight.
+template <bool L>
 DEV void materialise(Doc &D, uint8_t *out, uint32_t cap, uint32_t &len_out, u64 &hash_out) {
+    constexpr uint32_t G = 4;
     const uint32_t l = lane_id();
     uint32_t total = 0;
     u64 h = 0;
-    for (uint32_t i = 0; i < D.nb; i++) {
-        const uint32_t b = U(D.ord[i]);
-        const uint32_t cnt = U(D.bcnt[b]);
-        uint32_t cb = 0, n = 0;
-        if (l < cnt) {
-            const uint32_t it = D.items[size_t(b) * BLK + l];
-            if (!(D.st[it] & DEL_BIT)) {
-                cb = D.cbyte[it];
-                n = utf8_len(D.content[cb]);
+    for (uint32_t i = 0; i < D.nb; i += G) {
+        uint32_t it[G], cb[G];
+        bool vis[G];
+#pragma unroll
+        for (uint32_t g = 0; g < G; g++) {
+            const uint32_t p = i + g;
+            vis[g] = false;
+            it[g] = 0;
+            if (p < D.nb) {
+                const uint32_t b = U(ix_ld<L>(D.ord + p));
+                const u64 mv = U64(ix_ld64<L>(D.mvis + b));
+                vis[g] = (mv >> l) & 1ull;
+                if (vis[g]) it[g] = D.items[size_t(b) * BLK + l];
             }
         }
-        const uint32_t inc = wave_scan(n);
-        const uint32_t at = total + inc - n;
-        for (uint32_t k = 0; k < n; k++) {
-            const uint8_t byte = D.content[cb + k];
-            if (at + k < cap) out[at + k] = byte;
-            h += splitmix((u64(at + k) << 8) | byte);
+#pragma unroll
+        for (uint32_t g = 0; g < G; g++) cb[g] = vis[g] ? D.cbyte[it[g]] : 0;
+        if (D.ascii) {
+            uint8_t by[G];
+#pragma unroll
+            for (uint32_t g = 0; g < G; g++) by[g] = vis[g] ? D.content[cb[g]] : 0;
+#pragma unroll
+            for (uint32_t g = 0; g < G; g++) {
+                const uint32_t n = vis[g] ? 1u : 0u;
+                const uint32_t inc = wave_scan(n);
+                const uint32_t at = total + inc - n;
+                if (n) {
+                    if (at < cap) out[at] = by[g];
+                    h += splitmix((u64(at) << 8) | by[g]);
+                }
+                total += bcast(inc, 63);
+            }
+        } else {
+#pragma unroll
+            for (uint32_t g = 0; g < G; g++) {
+                const uint32_t n = vis[g] ? utf8_len(D.content[cb[g]]) : 0u;
+                const uint32_t inc = wave_scan(n);
+                const uint32_t at = total + inc - n;
+                for (uint32_t k = 0; k < n; k++) {
+                    const uint8_t byte = D.content[cb[g] + k];
+                    if (at + k < cap) out[at + k] = byte;
+                    h += splitmix((u64(at + k) << 8) | byte);
+                }
+                total += bcast(inc, 63);
+            }
         }
-        total += bcast(inc, 63);
     }
     len_out = total;
     hash_out = wave_sum64(h);
 }
 
 // Debug-mode consistency check of the whole structure (DTGPU_DEBUG): returns 0 or a code.
+template <bool L>
 DEV uint32_t check_invariants(Doc &D, DocResult *res) {
     const uint32_t l = lane_id();
-    uint32_t code = 0;
     for (uint32_t i = 0; i < D.nb; i++) {
-        const uint32_t b = U(D.ord[i]);
-        if (U(D.opos[b]) != i) return 201;
-        const uint32_t cnt = U(D.bcnt[b]);
-        const u64 mv = U64(D.mvis[b]), ml = U64(D.mlive[b]);
+        const uint32_t b = U(ix_ld<L>(D.ord + i));
+        if (U(ix_ld<L>(D.opos + b)) != i) return 201;
+        const uint32_t cnt = U(ix_ld8<L>(D.bcnt + b));
+        const u64 mv = U64(ix_ld64<L>(D.mvis + b)), ml = U64(ix_ld64<L>(D.mlive + b));
         bool bad = false;
+        uint32_t w = 0, it = 0xFFFFFFFFu;
         if (l < cnt) {
-            const uint32_t it = D.items[size_t(b) * BLK + l];
+            it = D.items[size_t(b) * BLK + l];
             if (it >= D.n_lv) bad = true;
             else {
-                const uint32_t st = D.st[it] & 0x7F;
-                if (((mv >> l) & 1) != (st == 1 ? 1u : 0u)) bad = true;
-                if (((ml >> l) & 1) != (st != 0 ? 1u : 0u)) bad = true;
-                if (D.blk[it] != b || D.slot[it] != l) bad = true;
+                w = loc_load(D.loc + it);
+                const uint32_t c = loc_cnt(w);
+                if (((mv >> l) & 1) != (c == 1 ? 1u : 0u)) bad = true;
+                if (((ml >> l) & 1) != (c != 0 ? 1u : 0u)) bad = true;
+                if (loc_blk(w) != b || loc_slot(w) != l) bad = true;
             }
         } else if (((mv | ml) >> l) & 1) bad = true;
         const u64 bm = __ballot(bad);
         if (bm) {
-            const uint32_t fl = first_lane(bm);
-            if (l == fl) {
-                const uint32_t it = l < cnt ? D.items[size_t(b) * BLK + l] : 0xFFFFFFFFu;
-                res->dbg[0] = b; res->dbg[1] = l; res->dbg[2] = cnt; res->dbg[3] = it;
-                res->dbg[4] = it < D.n_lv ? D.st[it] : 999; res->dbg[5] = it < D.n_lv ? D.blk[it] : 999;
-                res->dbg[6] = it < D.n_lv ? D.slot[it] : 999;
-                res->dbg[7] = uint32_t(mv); res->dbg[8] = uint32_t(mv >> 32); res->dbg[9] = uint32_t(ml);
+            if (l == first_lane(bm)) {
+                res->dbg[0] = b; res->dbg[1] = l; res->dbg[2] = cnt; res->dbg[3] = it; res->dbg[4] = w;
+                res->dbg[5] = uint32_t(mv); res->dbg[6] = uint32_t(mv >> 32);
+                res->dbg[7] = uint32_t(ml); res->dbg[8] = uint32_t(ml >> 32);
             }
             return 202;
         }
@@ -545,20 +656,19 @@ DEV uint32_t check_invariants(Doc &D, DocResult *res) {
     const uint32_t nsb = (D.nb + SB - 1) / SB;
     for (uint32_t s = 0; s < nsb; s++) {
         const uint32_t i = s * SB + l;
-        const uint32_t b = i < D.nb ? D.ord[i] : 0;
-        const uint32_t v = i < D.nb ? uint32_t(__popcll(D.mvis[b])) : 0;
+        const uint32_t b = i < D.nb ? ix_ld<L>(D.ord + i) : 0;
+        const uint32_t v = i < D.nb ? uint32_t(__popcll(ix_ld64<L>(D.mvis + b))) : 0;
         const uint32_t c = i < D.nb ? uint32_t(D.bcnt[b]) : 0;
-        if (U(wave_sum(v)) != U(D.svis[s])) code = 203;
-        if (U(wave_sum(c)) != U(D.scnt[s])) code = 204;
-        if (code) return code;
+        if (U(wave_sum(v)) != U(ix_ld<L>(D.svis + s))) return 203;
+        if (U(wave_sum(c)) != U(ix_ld<L>(D.scnt + s))) return 204;
     }
     return 0;
 }
 
+template <bool L, bool PROF>
 DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
     const uint32_t l = lane_id();
-    // fresh tracker: one empty block, every LV not-inserted-yet
-    for (uint32_t i = l; i < D.n_lv; i += 64) D.st[i] = 0;
+    // fresh tracker: one empty block (loc words are written when their item is inserted)
     if (l == 0) {
         D.ord[0] = 0; D.opos[0] = 0; D.bcnt[0] = 0; D.mvis[0] = 0; D.mlive[0] = 0;
         D.svis[0] = 0; D.scnt[0] = 0;
@@ -570,37 +680,47 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
     D.steps = 0;
     D.step_limit = 64ull * (uint64_t(D.ncmd) + D.n_lv) + 4096;
     D.site = 0;
+    D.ci = 0;
+    if (PROF) for (int i = 0; i < P_N; i++) D.prof[i] = 0;
+    const uint64_t t_start = tick<PROF>();
     // commands are fetched 64 at a time (one per lane) and broadcast with readlane
     for (uint32_t base = 0; base < D.ncmd && !D.err; base += 64) {
         const uint32_t n_here = min(64u, D.ncmd - base);
         Cmd pre = {0, 0, 0, 0};
         if (l < n_here) pre = D.cmds[base + l];
         for (uint32_t j = 0; j < n_here && !D.err; j++) {
-            const uint32_t ci = base + j;
-            D.ci = ci;
-            Cmd c;
-            c.op = bcast(pre.op, j); c.lv = bcast(pre.lv, j); c.len = bcast(pre.len, j); c.pos = bcast(pre.pos, j);
-            const uint32_t op = c.op & 15u;
-            if (c.len == 0 || c.lv >= D.n_lv || c.len > D.n_lv - c.lv) { fail(D, ErrCheckout, 17); break; }
+            D.ci = base + j;
+            const uint32_t op = U(bcast(pre.op, j)), a = U(bcast(pre.lv, j)), n = U(bcast(pre.len, j)),
+                           pos = U(bcast(pre.pos, j));
             if (!charge(D)) break;
-            switch (op) {
-                case CMD_INS: do_insert(D, c.lv, c.len, c.pos); break;
-                case CMD_DEL: do_delete(D, c.lv, c.len, c.pos, (c.op & 16u) != 0); break;
-                case CMD_ADV_INS: toggle_run<true, false>(D, c.lv, c.len); break;
-                case CMD_ADV_DEL: toggle_run<true, true>(D, c.lv, c.len); break;
-                case CMD_RET_INS: toggle_run<false, false>(D, c.lv, c.len); break;
-                case CMD_RET_DEL: toggle_run<false, true>(D, c.lv, c.len); break;
+            const uint64_t t0 = tick<PROF>();
+            switch (op & 15u) {
+                case CMD_INS:
+                    if (n == 0 || a >= D.n_lv || n > D.n_lv - a) { fail(D, ErrCheckout, 17); break; }
+                    do_insert<L, PROF>(D, a, n, pos);
+                    if (PROF) D.prof[P_INS] += tick<PROF>() - t0;
+                    break;
+                case CMD_DEL:
+                    if (n == 0 || a >= D.n_lv || n > D.n_lv - a) { fail(D, ErrCheckout, 17); break; }
+                    do_delete<L>(D, a, n, pos, (op & 16u) != 0);
+                    if (PROF) D.prof[P_DEL] += tick<PROF>() - t0;
+                    break;
+                case CMD_TOG:
+                    toggle_pass<L>(D, a, n);
+                    if (PROF) D.prof[P_TOG] += tick<PROF>() - t0;
+                    break;
                 default: fail(D, ErrCheckout, 18); break;
             }
             if (D.debug && !D.err) {
-                const uint32_t code = check_invariants(D, res);
+                const uint32_t code = check_invariants<L>(D, res);
                 if (code) fail(D, ErrCheckout, code);
             }
         }
     }
     uint32_t len = 0;
     u64 h = 0;
-    if (!D.err) materialise(D, out, cap, len, h);
+    const uint64_t t_mat = tick<PROF>();
+    if (!D.err) materialise<L>(D, out, cap, len, h);
     if (l == 0) {
         res->status = D.err;
         res->out_len = len;
@@ -609,6 +729,11 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
         res->n_blocks = D.nb;
         res->fail_cmd = D.err ? D.ci : 0;
         res->fail_site = D.err ? D.site : 0;
+        if (PROF) {
+            D.prof[P_MAT] = tick<PROF>() - t_mat;
+            for (int i = 0; i < P_N; i++) res->dbg[i] = uint32_t(D.prof[i] >> (i < P_N_YJS ? 4 : 0));
+            res->dbg[P_N] = uint32_t((tick<PROF>() - t_start) >> 4);
+        }
     }
 }
 
@@ -626,7 +751,7 @@ DEV void bind_index(Doc &D, uint8_t *base, uint32_t mb) {
 
 // One 64-lane workgroup per document of the list (the hardware dispatcher is the work queue;
 // LDS per workgroup bounds how many documents share a CU).
-template <bool LDS_INDEX>
+template <bool LDS_INDEX, bool PROF>
 __global__ __launch_bounds__(64) void replay_kernel(BatchParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t di = U(blockIdx.x);
@@ -634,17 +759,17 @@ __global__ __launch_bounds__(64) void replay_kernel(BatchParams P) {
     const uint32_t d = U(P.doc_list[di]);
     const DocDesc dd = P.docs[d];
     Doc D;
-    D.debug = P.debug;
+    D.debug = P.debug & 1u;
     D.cmds = P.cmds + dd.cmd_off;
     D.ncmd = U(dd.ncmd);
     D.n_lv = U(dd.n_lv);
+    D.tlist = P.tlist + dd.tlist_off;
     D.cbyte = P.cbyte + dd.lv_off;
     D.content = P.content + dd.content_off;
     D.aruns = P.aruns + dd.arun_off;
     D.n_aruns = U(dd.n_aruns);
-    D.st = P.st + dd.lv_off;
-    D.blk = P.blk + dd.lv_off;
-    D.slot = P.slot + dd.lv_off;
+    D.ascii = U(dd.ascii);
+    D.loc = P.loc + dd.lv_off;
     D.aux = P.aux + dd.lv_off;
     D.orr = P.orr + dd.lv_off;
     D.items = P.items + dd.blk_off * BLK;
@@ -655,20 +780,23 @@ __global__ __launch_bounds__(64) void replay_kernel(BatchParams P) {
     } else {
         bind_index(D, P.gidx + dd.gidx_off, D.max_blocks);
     }
-    run_doc(D, P.out + dd.out_off, U(dd.out_cap), &P.results[d]);
+    run_doc<LDS_INDEX, PROF>(D, P.out + dd.out_off, U(dd.out_cap), &P.results[d]);
 }
 
 }  // namespace dev
 
 int launch_replay(const BatchParams &small, const BatchParams &large, void *stream, int n_cu) {
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const bool prof = (small.debug | large.debug) & 2u;
     if (small.n_list) {
         const size_t lds = size_t(index_bytes(small.lds_blocks));
-        hipLaunchKernelGGL(dev::replay_kernel<true>, dim3(small.n_list), dim3(64), lds, s, small);
+        if (prof) hipLaunchKernelGGL((dev::replay_kernel<true, true>), dim3(small.n_list), dim3(64), lds, s, small);
+        else hipLaunchKernelGGL((dev::replay_kernel<true, false>), dim3(small.n_list), dim3(64), lds, s, small);
         if (hipGetLastError() != hipSuccess) return ErrHip;
     }
     if (large.n_list) {
-        hipLaunchKernelGGL(dev::replay_kernel<false>, dim3(large.n_list), dim3(64), 0, s, large);
+        if (prof) hipLaunchKernelGGL((dev::replay_kernel<false, true>), dim3(large.n_list), dim3(64), 0, s, large);
+        else hipLaunchKernelGGL((dev::replay_kernel<false, false>), dim3(large.n_list), dim3(64), 0, s, large);
         if (hipGetLastError() != hipSuccess) return ErrHip;
     }
     return OK;

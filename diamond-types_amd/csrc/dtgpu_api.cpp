@@ -56,11 +56,11 @@ struct dtgpu_batch {
     std::vector<DocDesc> docs;
     std::vector<uint32_t> small_list, large_list;
     uint32_t lds_blocks = 0;
-    uint64_t alg_bytes = 0, total_lv = 0;
+    uint64_t alg_in_bytes = 0, total_lv = 0;
 
     DevBuf<Cmd> d_cmds;
-    DevBuf<uint32_t> d_cbyte, d_aruns, d_blk, d_aux, d_orr, d_items, d_lists, d_counter;
-    DevBuf<uint8_t> d_content, d_st, d_slot, d_out, d_gidx;
+    DevBuf<uint32_t> d_tlist, d_cbyte, d_aruns, d_loc, d_aux, d_orr, d_items, d_lists, d_counter;
+    DevBuf<uint8_t> d_content, d_out, d_gidx;
     DevBuf<DocDesc> d_docs;
     DevBuf<DocResult> d_results;
     BatchParams small{}, large{};
@@ -120,7 +120,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     B->n_lv.resize(n);
     B->docs.resize(n);
     std::vector<Cmd> cmds;
-    std::vector<uint32_t> cbyte, aruns;
+    std::vector<uint32_t> tlist, cbyte, aruns;
     std::vector<uint8_t> content;
     uint64_t lv_total = 0, blk_total = 0, out_total = 0, gidx_total = 0;
     for (size_t i = 0; i < n; i++) {
@@ -133,7 +133,10 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         if (p.status != OK) continue;
         uint64_t n_ins = 0;
         for (const OpRun &r : p.log.ops) if (r.kind == 0) n_ins += r.len;
+        if (n_ins / 32 + 2 > LOC_MAX_BLOCKS) { B->host_status[i] = ErrCapacity; continue; }
         d.cmd_off = cmds.size();
+        d.tlist_off = tlist.size();
+        d.ascii = p.log.ins_content.size() == n_ins ? 1u : 0u;
         d.ncmd = uint32_t(p.plan.cmds.size());
         d.lv_off = lv_total;
         d.n_lv = uint32_t(p.log.n_lv);
@@ -146,16 +149,20 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         d.out_off = out_total;
         d.out_cap = uint32_t(p.log.ins_content.size());
         cmds.insert(cmds.end(), p.plan.cmds.begin(), p.plan.cmds.end());
+        tlist.insert(tlist.end(), p.plan.tlist.begin(), p.plan.tlist.end());
         cbyte.insert(cbyte.end(), p.log.ins_cbyte.begin(), p.log.ins_cbyte.end());
         content.insert(content.end(), p.log.ins_content.begin(), p.log.ins_content.end());
         aruns.insert(aruns.end(), p.plan.agent_runs.begin(), p.plan.agent_runs.end());
         lv_total += p.log.n_lv;
         blk_total += d.max_blocks;
         out_total += d.out_cap;
-        // compulsory bytes: command stream + agent runs + per-LV content offsets + content
-        // read at materialisation + text written
-        B->alg_bytes += uint64_t(d.ncmd) * sizeof(Cmd) + uint64_t(p.plan.agent_runs.size()) * 4 +
-                        uint64_t(p.log.n_lv) * 4 + 2ull * d.content_len;
+        // compulsory input bytes of the decoded oplog (SURVEY.md §8d merge-only formula):
+        // 16 per op run + (8 + 4 per parent) per graph entry + 12 per agent run + inserted
+        // bytes; the text written is added from the results (dtgpu_batch_algorithmic_bytes)
+        uint64_t parents = 0;
+        for (const GraphEntry &g : p.log.graph.entries) parents += g.parents.size();
+        B->alg_in_bytes += 16ull * p.log.ops.size() + 8ull * p.log.graph.entries.size() + 4ull * parents +
+                           12ull * p.log.agent_runs.size() + d.content_len;
         if (index_bytes(d.max_blocks) <= kLdsIndexBudget) {
             B->small_list.push_back(uint32_t(i));
             B->lds_blocks = std::max(B->lds_blocks, d.max_blocks);
@@ -168,6 +175,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     hipStream_t s = B->stream;
 #define CK(x) do { if ((x) != hipSuccess) return DTGPU_ERR_HIP; } while (0)
     CK(B->d_cmds.upload(cmds, s));
+    CK(B->d_tlist.upload(tlist, s));
     CK(B->d_cbyte.upload(cbyte, s));
     CK(B->d_aruns.upload(aruns, s));
     CK(B->d_content.upload(content, s));
@@ -175,9 +183,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     std::vector<uint32_t> lists(B->small_list);
     lists.insert(lists.end(), B->large_list.begin(), B->large_list.end());
     CK(B->d_lists.upload(lists, s));
-    CK(B->d_st.alloc(lv_total));
-    CK(B->d_blk.alloc(lv_total));
-    CK(B->d_slot.alloc(lv_total));
+    CK(B->d_loc.alloc(lv_total));
     CK(B->d_aux.alloc(lv_total));
     CK(B->d_orr.alloc(lv_total));
     CK(B->d_items.alloc(blk_total * 64));
@@ -189,14 +195,13 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     CK(hipStreamSynchronize(s));
 #undef CK
     BatchParams base{};
-    base.debug = getenv("DTGPU_DEBUG") ? 1u : 0u;
+    if (const char *dbg = getenv("DTGPU_DEBUG")) base.debug = uint32_t(atoi(dbg) ? atoi(dbg) : 1);
     base.cmds = B->d_cmds.p;
+    base.tlist = B->d_tlist.p;
     base.cbyte = B->d_cbyte.p;
     base.content = B->d_content.p;
     base.aruns = B->d_aruns.p;
-    base.st = B->d_st.p;
-    base.blk = B->d_blk.p;
-    base.slot = B->d_slot.p;
+    base.loc = B->d_loc.p;
     base.aux = B->d_aux.p;
     base.orr = B->d_orr.p;
     base.items = B->d_items.p;
@@ -381,7 +386,25 @@ dtgpu_status dtgpu_batch_sync(dtgpu_batch *B) {
     return hipStreamSynchronize(B->stream) == hipSuccess ? DTGPU_OK : DTGPU_ERR_HIP;
 }
 size_t dtgpu_batch_size(const dtgpu_batch *B) { return B ? B->n : 0; }
-uint64_t dtgpu_batch_algorithmic_bytes(const dtgpu_batch *B) { return B ? B->alg_bytes : 0; }
+uint64_t dtgpu_batch_algorithmic_bytes(dtgpu_batch *B) {
+    if (!B) return 0;
+    std::vector<dtgpu_doc_result> r(B->n);
+    if (B->n && dtgpu_batch_results(B, r.data()) != DTGPU_OK) return 0;
+    uint64_t out = 0;
+    for (const auto &x : r) out += x.text_len;
+    return B->alg_in_bytes + out;
+}
+dtgpu_status dtgpu_batch_doc_stats(dtgpu_batch *B, size_t i, uint32_t out[22]) {
+    if (!B || i >= B->n || !out) return DTGPU_ERR_ARG;
+    DocResult r;
+    if (hipMemcpyAsync(&r, B->d_results.p + i, sizeof r, hipMemcpyDeviceToHost, B->stream) != hipSuccess ||
+        hipStreamSynchronize(B->stream) != hipSuccess)
+        return DTGPU_ERR_HIP;
+    out[0] = r.n_items; out[1] = r.n_blocks; out[2] = r.fail_cmd; out[3] = r.fail_site;
+    out[4] = B->docs[i].ncmd; out[5] = B->docs[i].max_blocks;
+    for (int k = 0; k < 16; k++) out[6 + k] = r.dbg[k];
+    return DTGPU_OK;
+}
 uint64_t dtgpu_batch_total_lv(const dtgpu_batch *B) { return B ? B->total_lv : 0; }
 
 dtgpu_status dtgpu_batch_results(dtgpu_batch *B, dtgpu_doc_result *res) {

@@ -97,6 +97,7 @@ def lib():
     L.dtgpu_batch_text.argtypes = [vp, sz, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
     L.dtgpu_batch_algorithmic_bytes.argtypes = [vp]
     L.dtgpu_batch_algorithmic_bytes.restype = u64
+    L.dtgpu_batch_doc_stats.argtypes = [vp, sz, ctypes.POINTER(ctypes.c_uint32)]
     L.dtgpu_batch_total_lv.argtypes = [vp]
     L.dtgpu_batch_total_lv.restype = u64
     L.dtgpu_batch_free.argtypes = [vp]
@@ -300,6 +301,15 @@ class Batch:
         buf = ctypes.create_string_buffer(max(1, n.value))
         _check(lib().dtgpu_batch_text(self._h, i, buf, n.value, ctypes.byref(n)))
         return buf.raw[:n.value]
+
+    def doc_stats(self, i):
+        """Diagnostics of document i after a run (see dtgpu_batch_doc_stats)."""
+        out = (ctypes.c_uint32 * 22)()
+        _check(lib().dtgpu_batch_doc_stats(self._h, i, out))
+        keys = ["n_items", "n_blocks", "fail_cmd", "fail_site", "n_cmds", "max_blocks",
+                "cyc_ins", "cyc_del", "cyc_tog", "cyc_mat", "cyc_yjs", "cyc_split", "cyc_find", "cyc_bload",
+                "cyc_orr", "cyc_run", "n_yjs", "n_split", "cyc_total"]
+        return dict(zip(keys, list(out)))
 
     @property
     def algorithmic_bytes(self):

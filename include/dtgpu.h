@@ -145,8 +145,16 @@ size_t dtgpu_batch_size(const dtgpu_batch *batch);
 dtgpu_status dtgpu_batch_results(dtgpu_batch *batch, dtgpu_doc_result *results);
 /* Copy one document's merged text to host. */
 dtgpu_status dtgpu_batch_text(dtgpu_batch *batch, size_t doc, uint8_t *out, size_t cap, size_t *out_len);
-/* Bytes the replay reads + writes per run by construction (the roofline numerator). */
-uint64_t dtgpu_batch_algorithmic_bytes(const dtgpu_batch *batch);
+/* Compulsory bytes of one run (the roofline numerator, SURVEY.md §8d merge-only formula):
+ * 16 per op run + (8 + 4 per parent) per graph entry + 12 per agent run + inserted bytes, plus
+ * the text written.  Reads the results of the last run. */
+uint64_t dtgpu_batch_algorithmic_bytes(dtgpu_batch *batch);
+/* Diagnostics of one document from the last run: out[0] items, [1] blocks used, [2] failing
+ * command, [3] failing site, [4] commands, [5] block capacity, [6..21] profile / debug words
+ * (DTGPU_DEBUG=2: cycles/16 in insert, delete, retreat+advance, materialise, YjsMod scans,
+ * splits, and the insert phases find / block load / origin_right / run; scan and split
+ * counts; total cycles/16). */
+dtgpu_status dtgpu_batch_doc_stats(dtgpu_batch *batch, size_t doc, uint32_t out[22]);
 /* Total merged ops (sum of ListOpLog::len()) in the batch. */
 uint64_t dtgpu_batch_total_lv(const dtgpu_batch *batch);
 void dtgpu_batch_free(dtgpu_batch *batch);
