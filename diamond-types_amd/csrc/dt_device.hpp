@@ -45,6 +45,7 @@ struct BatchParams {
     uint32_t *aux;
     uint32_t *orr;
     uint32_t *items;
+    unsigned long long *mvis, *mlive;   // per block: visible / live slot masks
     uint8_t *out;
     uint8_t *gidx;
     const DocDesc *docs;
@@ -56,12 +57,17 @@ struct BatchParams {
     DocResult *results;
 };
 
-// Bytes of a block index for `mb` blocks (mvis, mlive: u64; ord, opos: u32; bcnt: u8; per
-// superblock svis, scnt: u32), 16-byte aligned.
-inline uint64_t index_bytes(uint64_t mb) {
-    const uint64_t nsb = (mb + 63) / 64;
-    return ((24 * mb + 8 * nsb + mb) + 15) & ~uint64_t(15);
+// Superblock capacity for an index of `mb` blocks: every superblock but the first holds >= 32
+// blocks (they split 64 -> 32 + 32).
+__host__ __device__ inline uint32_t sb_capacity(uint32_t mb) { return mb / 32 + 2; }
+// Bytes of a block index for `mb` blocks (dt_replay.hip bind_index): per block the packed
+// counts and the (superblock, index) position (u32 each); per superblock visible / live totals,
+// list length, top position, top order (u32 each) and a 64-entry u16 block list.
+__host__ __device__ inline uint64_t index_bytes(uint64_t mb) {
+    const uint64_t ms = sb_capacity(uint32_t(mb));
+    return ((8 * mb + 20 * ms + 128 * ms) + 15) & ~uint64_t(15);
 }
+constexpr uint32_t MAX_DOC_BLOCKS = 65535;   // block ids are u16 in the superblock lists
 
 // Launch both tiers on `stream` (hipStream_t).  small/large lists index docs[].
 int launch_replay(const BatchParams &small, const BatchParams &large, void *stream, int n_cu);

@@ -3,17 +3,23 @@
 // One wavefront (64 lanes) replays one document's command stream (built on the host from the
 // spanning-tree walk, dt_host.cpp::build_plan).  This is the checkout-from-ROOT per-item
 // formulation of the reference's M2Tracker (src/listmerge/merge.rs:89-581,
-// advance_retreat.rs:58-153, yjsspan.rs:13-228):
+// advance_retreat.rs:58-153, yjsspan.rs:13-228).
 //
-//   items      one per inserted char, kept in document order in 64-slot blocks (HBM);
-//   block idx  per block: visible mask, live (non-NIY) mask, item count, order position;
-//              per 64 blocks (superblock): visible / item totals.  In LDS for documents
-//              whose block count fits the LDS budget, in HBM otherwise (same code).
-//   loc[lv]    one packed word per inserted LV: count (8 bits: 0 NIY, 1 inserted, k>=2
-//              deleted k-1 times) | block (18 bits) | slot (6 bits).  Every access is an
-//              L2-coherent (sc1) atomic or load, so the returning atomic of a retreat/advance
-//              hands back the item's position and its old state in one round trip.
-//   aux[lv]    Ins: origin_left; Del: the item it deleted.   orr[lv]: origin_right.
+// Document = a 3-level order-statistic tree of inserted chars (items):
+//   block        64 item slots in document order; items[] (LV ids), and the visible / live
+//                (non-NIY) bit masks mvis[] / mlive[]: HBM.
+//   superblock   an ordered list of <= 64 block ids (sbl) with visible / live totals.
+//   top          the ordered list of superblocks (sbord).
+//   The block and superblock index (packed per-block counts: visible | live << 8 | items << 16;
+//   block -> (superblock, index) opos; the superblock lists and totals) lives in LDS for
+//   documents whose index fits the LDS budget and in HBM otherwise (same code).  A full block
+//   splits 64 -> 32 + 32 and a full superblock 64 -> 32 + 32, so a split costs O(64) work.
+//   loc[lv]      one packed word per inserted LV: count (8 bits: 0 NIY, 1 inserted, k >= 2
+//                deleted k-1 times) | block (18 bits) | slot (6 bits).  All loc and mask
+//                accesses are L2-coherent (sc1) atomics / loads / stores, so the returning
+//                atomic of a retreat/advance hands back the item's position and old state in
+//                one round trip.
+//   aux[lv]      Ins: origin_left; Del: the item it deleted.   orr[lv]: origin_right.
 //
 // Commands: INS / DEL apply one op run; TOG applies one walk step's whole retreat + advance
 // set in one lane-parallel pass.  Counters make that legal: a retreat subtracts one, an advance
@@ -26,8 +32,8 @@
 // The plan ends with a TOG that advances to the tip, so the final visible set is the checkout:
 // materialisation stream-compacts visible items in document order (list/merge.rs:63-95).
 //
-// Document order is a total order on (order position of the block, slot): YjsMod compares
-// those keys directly (merge.rs:154-278) instead of counting items.
+// Document order is the lexicographic order of (top position, index in superblock, slot):
+// YjsMod compares those keys directly (merge.rs:154-278) instead of counting items.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -43,6 +49,9 @@ typedef unsigned long long u64;
 DEV uint32_t lane_id() { return __lane_id(); }
 DEV void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); __builtin_amdgcn_wave_barrier(); }
 DEV uint32_t bcast(uint32_t v, uint32_t l) { return uint32_t(__builtin_amdgcn_readlane(int(v), int(l))); }
+DEV u64 bcast64(u64 v, uint32_t l) {
+    return (u64(bcast(uint32_t(v >> 32), l)) << 32) | u64(bcast(uint32_t(v), l));
+}
 DEV uint32_t first_lane(u64 m) { return uint32_t(__ffsll((long long)m) - 1); }
 DEV uint32_t last_lane(u64 m) { return 63u - uint32_t(__clzll((long long)m)); }
 // Wave-uniform values are pinned to scalar registers: control flow that depends on them is
@@ -55,6 +64,7 @@ DEV u64 U64(u64 v) {   // (readfirstlane returns int: keep both halves unsigned)
 DEV uint32_t shfl(uint32_t v, uint32_t src) {
     return uint32_t(__builtin_amdgcn_ds_bpermute(int(src << 2), int(v)));
 }
+DEV u64 lanes_below(uint32_t l) { return l >= 64 ? ~0ull : ((1ull << l) - 1ull); }
 
 // Inclusive wave prefix sum over 64 lanes with DPP: Hillis-Steele inside each 16-lane row
 // (row_shr 1/2/4/8), then row_bcast:15 and row_bcast:31 carry the row totals forward.
@@ -83,35 +93,37 @@ DEV u64 splitmix(u64 z) {
 DEV uint32_t utf8_len(uint8_t c) { return c < 0x80 ? 1 : (c & 0xE0) == 0xC0 ? 2 : (c & 0xF0) == 0xE0 ? 3 : 4; }
 
 constexpr uint32_t BLK = 64;   // slots per block
-constexpr uint32_t SB = 64;    // blocks per superblock
+constexpr uint32_t SBC = 64;   // block capacity of a superblock list
 constexpr uint32_t ROOT_ID = 0xFFFFFFFFu;
 constexpr uint32_t END_ID = 0xFFFFFFFEu;
-constexpr uint32_t NO_BLOCK = 0xFFFFFFFFu;
+constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr uint32_t CNT_ONE = 1u << LOC_CNT_SHIFT;
+// packed per-block counts
+constexpr uint32_t C_VIS = 1u, C_LIVE = 1u << 8, C_ITEMS = 1u << 16;
+DEV uint32_t c_vis(uint32_t c) { return c & 0xFFu; }
+DEV uint32_t c_live(uint32_t c) { return (c >> 8) & 0xFFu; }
+DEV uint32_t c_items(uint32_t c) { return (c >> 16) & 0xFFu; }
 
 DEV uint32_t loc_blk(uint32_t w) { return (w >> LOC_BLK_SHIFT) & LOC_BLK_MASK; }
 DEV uint32_t loc_slot(uint32_t w) { return w & 63u; }
 DEV uint32_t loc_cnt(uint32_t w) { return w >> LOC_CNT_SHIFT; }
 
-// loc words: L2-coherent accesses only (returning atomics and plain loads must not meet a
-// stale L1 line).
-DEV uint32_t loc_load(const uint32_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-DEV void loc_store(uint32_t *p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-DEV uint32_t loc_add(uint32_t *p, uint32_t d) { return __hip_atomic_fetch_add(p, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+// L2-coherent accesses (returning atomics and loads must never meet a stale L1 line).
+template <typename T> DEV T ld_sc(const T *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+template <typename T> DEV void st_sc(T *p, T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+DEV uint32_t loc_add(uint32_t *p, uint32_t d) { return __hip_atomic_fetch_add(p, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+template <typename T> DEV void at_xor(T *p, T v) { __hip_atomic_fetch_xor(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+template <typename T> DEV void at_add(T *p, T v) { __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 
-// Block-index accessors.  LDS tier: plain LDS (one wave owns the workgroup).  HBM tier: every
-// index word touched by an atomic is read L2-coherently.
-template <bool L> DEV uint32_t ix_ld(const uint32_t *p) {
+// Index accessors.  LDS tier: plain LDS (one wave owns the workgroup).  HBM tier: words that
+// atomics touch are read L2-coherently.
+template <bool L> DEV uint32_t ix(const uint32_t *p) {
     if (L) return *p;
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return ld_sc(p);
 }
-template <bool L> DEV u64 ix_ld64(const u64 *p) {
-    if (L) return *p;
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <bool L> DEV uint32_t ix_ld8(const uint8_t *p) { return *p; }
+template <bool L> DEV uint32_t ix16(const uint16_t *p) { return *p; }
 
-enum ProfSlot { P_INS = 0, P_DEL, P_TOG, P_MAT, P_YJS, P_SPLIT, P_FIND, P_BLOAD, P_ORR, P_RUN, P_N_YJS, P_N_SPLIT, P_N };
+enum ProfSlot { P_INS = 0, P_DEL, P_TOG, P_MAT, P_YJS, P_SPLIT, P_FIND, P_BLOAD, P_ORR, P_RUN, P_R1, P_R2, P_R3, P_N_YJS, P_N_SPLIT, P_N };
 
 struct Doc {
     // inputs
@@ -123,19 +135,20 @@ struct Doc {
     const uint32_t *aruns;
     uint32_t n_aruns;
     uint32_t ascii;
-    // per-LV state
+    // per-LV state (HBM)
     uint32_t *loc;
     uint32_t *aux;
     uint32_t *orr;
-    // blocks
+    // blocks (HBM)
     uint32_t *items;
-    uint32_t max_blocks;
-    // block index
     u64 *mvis, *mlive;
-    uint32_t *ord, *opos, *svis, *scnt;
-    uint8_t *bcnt;
+    uint32_t max_blocks, max_sb;
+    // index (LDS or HBM)
+    uint32_t *cnt, *opos;                                // per block
+    uint32_t *svis, *slive, *sbn, *sbpos, *sbord;        // per superblock / top order
+    uint16_t *sbl;                                       // per superblock: SBC block ids
     // wave-uniform scalars
-    uint32_t nb;
+    uint32_t nb, nsb;
     uint32_t err;
     uint32_t n_items;
     uint32_t debug;
@@ -156,92 +169,151 @@ DEV bool charge(Doc &D) {
 }
 template <bool PROF> DEV uint64_t tick() { return PROF ? __builtin_amdgcn_s_memtime() : 0; }
 
-// ---- order-statistic queries -------------------------------------------------------------
+// ---- navigation ------------------------------------------------------------------------------
 
-// Item holding visible index p (content-tree cursor_at_content_pos, root.rs:50-89).
+template <bool L> DEV uint32_t first_block(const Doc &D) {
+    return U(ix16<L>(D.sbl + size_t(U(ix<L>(D.sbord))) * SBC));
+}
+// Next block in document order, or NONE.
+template <bool L> DEV uint32_t next_block(const Doc &D, uint32_t b) {
+    const uint32_t o = U(ix<L>(D.opos + b));
+    const uint32_t S = o >> 6, i = o & 63u;
+    if (i + 1 < U(ix<L>(D.sbn + S))) return U(ix16<L>(D.sbl + size_t(S) * SBC + i + 1));
+    const uint32_t p = U(ix<L>(D.sbpos + S)) + 1;
+    if (p >= D.nsb) return NONE;
+    return U(ix16<L>(D.sbl + size_t(U(ix<L>(D.sbord + p))) * SBC));
+}
+// Document-order key of (block, slot).
+template <bool L> DEV uint32_t key_at(const Doc &D, uint32_t b, uint32_t s) {
+    const uint32_t o = ix<L>(D.opos + b);
+    return (ix<L>(D.sbpos + (o >> 6)) << 12) | ((o & 63u) << 6) | s;
+}
+template <bool L> DEV uint32_t key_of(const Doc &D, uint32_t item) {
+    const uint32_t w = ld_sc(D.loc + item);
+    return key_at<L>(D, loc_blk(w), loc_slot(w));
+}
+
+// Block holding visible index p and the rank k of that item among the block's visible items
+// (content-tree cursor_at_content_pos, root.rs:50-89): prefix scans over superblock totals,
+// then over the chosen superblock's block counts.
 template <bool L>
-DEV bool find_vis(Doc &D, uint32_t p, uint32_t &ob, uint32_t &os) {
+DEV bool find_vis(Doc &D, uint32_t p, uint32_t &ob, uint32_t &ok) {
     const uint32_t l = lane_id();
-    const uint32_t nsb = (D.nb + SB - 1) / SB;
-    uint32_t base = 0, sb = 0;
-    bool found = false;
-    for (uint32_t c = 0; c < nsb; c += 64) {
+    uint32_t base = 0, S = NONE;
+    for (uint32_t c = 0; c < D.nsb; c += 64) {
         const uint32_t i = c + l;
-        const uint32_t v = i < nsb ? ix_ld<L>(D.svis + i) : 0;
+        const uint32_t s = i < D.nsb ? ix<L>(D.sbord + i) : 0;
+        const uint32_t v = i < D.nsb ? ix<L>(D.svis + s) : 0;
         const uint32_t inc = wave_scan(v);
         const u64 m = __ballot(base + inc > p);
         if (m) {
             const uint32_t fl = first_lane(m);
-            sb = c + fl;
+            S = U(bcast(s, fl));
             base += bcast(inc - v, fl);
-            found = true;
             break;
         }
         base += bcast(inc, 63);
     }
-    if (!found) return false;
-    const uint32_t i = sb * SB + l;
-    const uint32_t b = i < D.nb ? ix_ld<L>(D.ord + i) : 0;
-    const uint32_t v = i < D.nb ? uint32_t(__popcll(ix_ld64<L>(D.mvis + b))) : 0;
+    if (S == NONE) return false;
+    const uint32_t n = U(ix<L>(D.sbn + S));
+    const uint32_t b = l < n ? ix16<L>(D.sbl + size_t(S) * SBC + l) : 0;
+    const uint32_t v = l < n ? c_vis(ix<L>(D.cnt + b)) : 0;
     const uint32_t inc = wave_scan(v);
     const u64 m = __ballot(base + inc > p);
     if (!m) return false;
     const uint32_t fl = first_lane(m);
-    const uint32_t bb = U(bcast(b, fl));
-    const uint32_t off = p - base - bcast(inc - v, fl);
-    const u64 mv = U64(ix_ld64<L>(D.mvis + bb));
-    const bool set = (mv >> l) & 1ull;
-    const uint32_t before = uint32_t(__popcll(mv & ((1ull << l) - 1ull)));
-    const u64 m2 = __ballot(set && before == off);
-    if (!m2) return false;
-    ob = bb;
-    os = first_lane(m2);
+    ob = U(bcast(b, fl));
+    ok = U(p - base - bcast(inc - v, fl));
     return true;
 }
 
-// Document-order key of an item: (order position of its block, slot).
-template <bool L>
-DEV uint32_t key_of(const Doc &D, uint32_t item) {
-    const uint32_t w = loc_load(D.loc + item);
-    return (ix_ld<L>(D.opos + loc_blk(w)) << 6) | loc_slot(w);
+// Slot of the k-th set bit of a wave-uniform mask.
+DEV uint32_t select_bit(u64 m, uint32_t k) {
+    const uint32_t l = lane_id();
+    const bool set = (m >> l) & 1ull;
+    const uint32_t before = uint32_t(__popcll(m & lanes_below(l)));
+    return first_lane(__ballot(set && before == k));
 }
 
-// First live (non-NIY) item in a block after order position p0 (origin_right search,
-// merge.rs:405-423).  Returns NO_BLOCK when there is none.
+// First block after b (document order) with a live item, or NONE (origin_right search,
+// merge.rs:405-423).
 template <bool L>
-DEV uint32_t next_live_block(Doc &D, uint32_t p0) {
+DEV uint32_t next_live_block(Doc &D, uint32_t b) {
     const uint32_t l = lane_id();
-    for (uint32_t p = p0; p < D.nb; p += 64) {
-        if (!charge(D)) return NO_BLOCK;
-        const uint32_t i = p + l;
-        const uint32_t b = i < D.nb ? ix_ld<L>(D.ord + i) : 0;
-        const u64 m = __ballot(i < D.nb && ix_ld64<L>(D.mlive + b) != 0ull);
-        if (m) return U(bcast(b, first_lane(m)));
+    const uint32_t o = U(ix<L>(D.opos + b));
+    uint32_t S = o >> 6;
+    {   // rest of b's superblock
+        const uint32_t n = U(ix<L>(D.sbn + S)), i0 = (o & 63u) + 1;
+        const uint32_t bl = l < n ? ix16<L>(D.sbl + size_t(S) * SBC + l) : 0;
+        const u64 m = __ballot(l >= i0 && l < n && c_live(ix<L>(D.cnt + bl)) != 0);
+        if (m) return U(bcast(bl, first_lane(m)));
     }
-    return NO_BLOCK;
+    for (uint32_t p = U(ix<L>(D.sbpos + S)) + 1; p < D.nsb; p += 64) {
+        if (!charge(D)) return NONE;
+        const uint32_t i = p + l;
+        const uint32_t s = i < D.nsb ? ix<L>(D.sbord + i) : 0;
+        const u64 m = __ballot(i < D.nsb && ix<L>(D.slive + s) != 0);
+        if (m) {
+            S = U(bcast(s, first_lane(m)));
+            const uint32_t n = U(ix<L>(D.sbn + S));
+            const uint32_t bl = l < n ? ix16<L>(D.sbl + size_t(S) * SBC + l) : 0;
+            const u64 m2 = __ballot(l < n && c_live(ix<L>(D.cnt + bl)) != 0);
+            if (!m2) { fail(D, ErrCheckout, 19); return NONE; }
+            return U(bcast(bl, first_lane(m2)));
+        }
+    }
+    return NONE;
 }
 
 // ---- block maintenance ---------------------------------------------------------------------
 
+// Split the full superblock S (64 blocks): its upper half becomes a new superblock right after
+// it in the top order.
 template <bool L>
-DEV void recompute_sb(Doc &D, uint32_t from_sb) {
+DEV void split_sb(Doc &D, uint32_t S) {
     const uint32_t l = lane_id();
-    const uint32_t nsb = (D.nb + SB - 1) / SB;
-    for (uint32_t s = from_sb; s < nsb; s++) {
-        const uint32_t i = s * SB + l;
-        const uint32_t b = i < D.nb ? ix_ld<L>(D.ord + i) : 0;
-        const uint32_t v = i < D.nb ? uint32_t(__popcll(ix_ld64<L>(D.mvis + b))) : 0;
-        const uint32_t c = i < D.nb ? uint32_t(D.bcnt[b]) : 0;
-        const uint32_t tv = wave_sum(v), tc = wave_sum(c);
-        if (l == 0) { D.svis[s] = tv; D.scnt[s] = tc; }
+    if (D.nsb >= D.max_sb) { fail(D, ErrCapacity, 21); return; }
+    const uint32_t S2 = D.nsb;
+    uint32_t vis = 0, live = 0;
+    {
+        const uint32_t b = ix16<L>(D.sbl + size_t(S) * SBC + l);
+        const uint32_t c = ix<L>(D.cnt + b);
+        vis = c_vis(c);
+        live = c_live(c);
+        wave_fence();
+        if (l >= SBC / 2) {
+            D.sbl[size_t(S2) * SBC + (l - SBC / 2)] = uint16_t(b);
+            D.opos[b] = (S2 << 6) | (l - SBC / 2);
+        }
+    }
+    const uint32_t vh = wave_sum(l >= 32 ? vis : 0), lh = wave_sum(l >= 32 ? live : 0);
+    const uint32_t vl = wave_sum(l < 32 ? vis : 0), ll = wave_sum(l < 32 ? live : 0);
+    const uint32_t p = U(ix<L>(D.sbpos + S)) + 1;
+    // shift sbord[p .. nsb) right by one, highest chunk first
+    for (int c = int(D.nsb) - 1; c >= int(p); c -= 64) {
+        const int i = c - int(l);
+        uint32_t v = 0;
+        if (i >= int(p)) v = ix<L>(D.sbord + i);
+        wave_fence();
+        if (i >= int(p)) { D.sbord[i + 1] = v; D.sbpos[v] = uint32_t(i + 1); }
+        wave_fence();
+    }
+    if (l == 0) {
+        D.sbn[S] = SBC / 2;
+        D.sbn[S2] = SBC / 2;
+        D.svis[S] = vl; D.slive[S] = ll;
+        D.svis[S2] = vh; D.slive[S2] = lh;
+        D.sbord[p] = S2;
+        D.sbpos[S2] = p;
     }
     wave_fence();
+    D.nsb++;
 }
 
-// Split the full block b (its items in `it` lane by lane): the upper half moves to a new block
-// placed right after b in document order.
+// Split the full block b (items in `it` lane by lane, masks mv / ml): the upper half moves to
+// a new block placed right after b in its superblock.
 template <bool L>
-DEV uint32_t split_block(Doc &D, uint32_t b, uint32_t it) {
+DEV uint32_t split_block(Doc &D, uint32_t b, uint32_t it, u64 mv, u64 ml) {
     const uint32_t l = lane_id();
     if (D.nb >= D.max_blocks) { fail(D, ErrCapacity, 12); return 0; }
     const uint32_t b2 = D.nb;
@@ -250,91 +322,106 @@ DEV uint32_t split_block(Doc &D, uint32_t b, uint32_t it) {
         // (b, s) -> (b2, s - 32): one field-wise delta on the packed word
         loc_add(D.loc + it, ((b2 - b) << LOC_BLK_SHIFT) - BLK / 2);
     }
-    const uint32_t p = ix_ld<L>(D.opos + b) + 1;
-    // shift ord[p .. nb) right by one, highest chunk first
-    for (int c = int(D.nb) - 1; c >= int(p); c -= 64) {
-        const int i = c - int(l);
+    if (l == 0) {
+        st_sc(D.mvis + b2, mv >> 32);
+        st_sc(D.mvis + b, mv & 0xFFFFFFFFull);
+        st_sc(D.mlive + b2, ml >> 32);
+        st_sc(D.mlive + b, ml & 0xFFFFFFFFull);
+    }
+    const uint32_t o = U(ix<L>(D.opos + b));
+    const uint32_t S = o >> 6, i = o & 63u, n = U(ix<L>(D.sbn + S));
+    {   // shift S's list after i right by one
         uint32_t v = 0;
-        if (i >= int(p)) v = ix_ld<L>(D.ord + i);
+        const bool mv_lane = l > i && l < n;
+        if (mv_lane) v = ix16<L>(D.sbl + size_t(S) * SBC + l);
         wave_fence();
-        if (i >= int(p)) { D.ord[i + 1] = v; D.opos[v] = uint32_t(i + 1); }
-        wave_fence();
+        if (mv_lane) {
+            D.sbl[size_t(S) * SBC + l + 1] = uint16_t(v);
+            D.opos[v] = (S << 6) | (l + 1);
+        }
     }
     if (l == 0) {
-        const u64 mv = ix_ld64<L>(D.mvis + b), ml = ix_ld64<L>(D.mlive + b);
-        D.mvis[b2] = mv >> 32;
-        D.mvis[b] = mv & 0xFFFFFFFFull;
-        D.mlive[b2] = ml >> 32;
-        D.mlive[b] = ml & 0xFFFFFFFFull;
-        D.bcnt[b2] = BLK / 2;
-        D.bcnt[b] = BLK / 2;
-        D.ord[p] = b2;
-        D.opos[b2] = p;
+        D.cnt[b2] = uint32_t(__popcll(mv >> 32)) * C_VIS + uint32_t(__popcll(ml >> 32)) * C_LIVE + (BLK / 2) * C_ITEMS;
+        D.cnt[b] = uint32_t(__popcll(mv & 0xFFFFFFFFull)) * C_VIS + uint32_t(__popcll(ml & 0xFFFFFFFFull)) * C_LIVE +
+                   (BLK / 2) * C_ITEMS;
+        D.sbl[size_t(S) * SBC + i + 1] = uint16_t(b2);
+        D.opos[b2] = (S << 6) | (i + 1);
+        D.sbn[S] = n + 1;
     }
     wave_fence();
     D.nb++;
-    recompute_sb<L>(D, (p - 1) / SB);
+    if (n + 1 == SBC) split_sb<L>(D, S);
     return b2;
 }
 
 // Insert the run [lv, lv+k) before slot s of block b (all new items visible).  `it` holds the
-// block's items lane by lane; lanes >= the block count are don't-care.
+// block's items lane by lane (lanes >= the block count are don't-care); mv / ml its masks.
 template <bool L, bool PROF>
-DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, uint32_t lv, uint32_t k, uint32_t ol,
-                    uint32_t orr) {
+DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml, uint32_t lv, uint32_t k,
+                    uint32_t ol, uint32_t orr) {
     const uint32_t l = lane_id();
     const uint32_t lv0 = lv, k0 = k;
     while (k > 0) {
         if (!charge(D)) return;
-        const uint32_t cnt = U(ix_ld8<L>(D.bcnt + b));
-        if (cnt == BLK) {
+        const uint32_t c = U(ix<L>(D.cnt + b));
+        const uint32_t bc = c_items(c);
+        if (bc == BLK) {
             const uint64_t t0 = tick<PROF>();
-            const uint32_t b2 = split_block<L>(D, b, it);
+            const uint32_t b2 = split_block<L>(D, b, it, mv, ml);
             if (D.err) return;
             if (s > BLK / 2) {
                 b = b2;
                 s -= BLK / 2;
                 it = shfl(it, (l + BLK / 2) & 63u);
+                mv >>= 32;
+                ml >>= 32;
+            } else {
+                mv &= 0xFFFFFFFFull;
+                ml &= 0xFFFFFFFFull;
             }
             if (PROF) { D.prof[P_SPLIT] += tick<PROF>() - t0; D.prof[P_N_SPLIT]++; }
             continue;
         }
-        const uint32_t m = min(k, BLK - cnt);
+        uint64_t tr = tick<PROF>();
+        const uint32_t m = min(k, BLK - bc);
         uint32_t *items = D.items + size_t(b) * BLK;
-        if (l >= s && l < cnt) {
+        if (l >= s && l < bc) {
             items[l + m] = it;
             loc_add(D.loc + it, m);   // slot += m
         }
         if (l >= s && l < s + m) {
             const uint32_t nit = lv + (l - s);
             items[l] = nit;
-            loc_store(D.loc + nit, CNT_ONE | (b << LOC_BLK_SHIFT) | l);
+            st_sc(D.loc + nit, CNT_ONE | (b << LOC_BLK_SHIFT) | l);
         }
+        if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_R1] += t - tr; tr = t; }
         const uint32_t shifted = shfl(it, l >= m ? l - m : l);
         it = l < s ? it : (l < s + m ? lv + (l - s) : shifted);
+        const u64 low = lanes_below(s);
+        const u64 ins = lanes_below(m) << s;
+        mv = m == 64 ? ins : ((mv & low) | ((mv & ~low) << m) | ins);
+        ml = m == 64 ? ins : ((ml & low) | ((ml & ~low) << m) | ins);
         if (l == 0) {
-            const u64 low = s == 0 ? 0ull : (~0ull >> (64 - s));
-            const u64 ins = (m == 64 ? ~0ull : ((1ull << m) - 1ull)) << s;
-            const u64 mv = ix_ld64<L>(D.mvis + b), ml = ix_ld64<L>(D.mlive + b);
-            const u64 hv = m == 64 ? 0ull : ((mv & ~low) << m);
-            const u64 hl = m == 64 ? 0ull : ((ml & ~low) << m);
-            D.mvis[b] = (mv & low) | hv | ins;
-            D.mlive[b] = (ml & low) | hl | ins;
-            D.bcnt[b] = uint8_t(cnt + m);
-            const uint32_t sbi = ix_ld<L>(D.opos + b) / SB;
-            D.svis[sbi] = ix_ld<L>(D.svis + sbi) + m;
-            D.scnt[sbi] = ix_ld<L>(D.scnt + sbi) + m;
+            st_sc(D.mvis + b, mv);
+            st_sc(D.mlive + b, ml);
+            D.cnt[b] = c + m * (C_VIS + C_LIVE + C_ITEMS);
+            const uint32_t S = ix<L>(D.opos + b) >> 6;
+            D.svis[S] = ix<L>(D.svis + S) + m;
+            D.slive[S] = ix<L>(D.slive + S) + m;
         }
         wave_fence();
+        if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_R2] += t - tr; tr = t; }
         lv += m;
         k -= m;
         s += m;
     }
+    const uint64_t t3 = tick<PROF>();
     for (uint32_t j = l; j < k0; j += 64) {
         const uint32_t nit = lv0 + j;
         D.aux[nit] = j == 0 ? ol : nit - 1;
         D.orr[nit] = orr;
     }
+    if (PROF) D.prof[P_R3] += tick<PROF>() - t3;
 }
 
 // YjsMod tie-break key of an LV: (agent name rank, seq) (merge.rs:199-218).  64-ary search
@@ -360,7 +447,7 @@ DEV void agent_of(Doc &D, uint32_t lv, uint32_t &rank, uint32_t &seq) {
 }
 
 // YjsMod integrate (merge.rs:154-278) over the not-inserted-yet items between the cursor
-// (b, s) and origin_right (rb, rs) (rb == NO_BLOCK: END), one block of candidates at a time.
+// (b, s) and origin_right (rb, rs) (rb == NONE: END), one block of candidates at a time.
 // Every candidate's keys come in lane-parallel; the sequential scan state machine is resolved
 // with ballots: the first stopping lane ends the scan, and `scanning` is the state after the
 // last event lane before it.  Returns the insertion point in (b, s).
@@ -375,11 +462,11 @@ DEV void yjs_scan(Doc &D, uint32_t &b, uint32_t &s, uint32_t rb, uint32_t rs, ui
     uint32_t cb = b, cs = s;
     for (;;) {
         if (!charge(D)) return;
-        const uint32_t cnt = U(ix_ld8<L>(D.bcnt + cb));
+        const uint32_t cnt = c_items(U(ix<L>(D.cnt + cb)));
         if (cs >= cnt) {   // next block in document order
-            const uint32_t p = ix_ld<L>(D.opos + cb) + 1;
-            if (p >= D.nb) break;   // end of document
-            cb = U(ix_ld<L>(D.ord + p));
+            const uint32_t nx = next_block<L>(D, cb);
+            if (nx == NONE) break;   // end of document
+            cb = nx;
             cs = 0;
             continue;
         }
@@ -405,7 +492,7 @@ DEV void yjs_scan(Doc &D, uint32_t &b, uint32_t &s, uint32_t rb, uint32_t rs, ui
         const bool clr = inr && kl == my_l && !stop && !setv;
         const u64 ms = __ballot(stop);
         const uint32_t lim = ms ? first_lane(ms) : end;
-        const u64 below = lim >= 64 ? ~0ull : ((1ull << lim) - 1ull);
+        const u64 below = lanes_below(lim);
         const u64 mset = __ballot(setv) & below, mclr = __ballot(clr) & below;
         if (mset | mclr) {
             const int lc = mclr ? int(last_lane(mclr)) : -1;
@@ -426,67 +513,81 @@ DEV void yjs_scan(Doc &D, uint32_t &b, uint32_t &s, uint32_t rb, uint32_t rs, ui
     s = U(s);
 }
 
+// Items and masks of block b into registers (items lane by lane, masks wave-uniform).
+template <bool L>
+DEV void load_block(const Doc &D, uint32_t b, uint32_t bc, uint32_t &it, u64 &mv, u64 &ml) {
+    const uint32_t l = lane_id();
+    it = l < bc ? D.items[size_t(b) * BLK + l] : 0;
+    u64 x = 0;
+    if (l == 0) x = ld_sc(D.mvis + b);
+    if (l == 1) x = ld_sc(D.mlive + b);
+    mv = bcast64(x, 0);
+    ml = bcast64(x, 1);
+}
+
 // Apply an insert run at visible position pos (M2Tracker::apply Ins + integrate,
 // merge.rs:154-278, 383-455).
 template <bool L, bool PROF>
 DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
-    const uint32_t l = lane_id();
     uint64_t tp = tick<PROF>();
-    uint32_t b, s, s0 = 0;
+    uint32_t b, kk = 0;
     if (pos == 0) {
-        b = U(ix_ld<L>(D.ord + 0));
-        s = 0;
-    } else {
-        if (!find_vis<L>(D, pos - 1, b, s0)) { fail(D, ErrCheckout, 13); return; }
-        s = s0 + 1;
+        b = first_block<L>(D);
+    } else if (!find_vis<L>(D, pos - 1, b, kk)) {
+        fail(D, ErrCheckout, 13);
+        return;
     }
     if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_FIND] += t - tp; tp = t; }
-    const uint32_t cnt = U(ix_ld8<L>(D.bcnt + b));
-    uint32_t it = l < cnt ? D.items[size_t(b) * BLK + l] : 0;
-    const uint32_t ol = pos == 0 ? ROOT_ID : U(bcast(it, s0));
-    if (PROF) { const uint32_t x = U(it); asm volatile("" :: "s"(x)); const uint64_t t = tick<PROF>(); D.prof[P_BLOAD] += t - tp; tp = t; }
+    const uint32_t bc = c_items(U(ix<L>(D.cnt + b)));
+    uint32_t it;
+    u64 mv, ml;
+    load_block<L>(D, b, bc, it, mv, ml);
+    uint32_t s = 0, ol = ROOT_ID;
+    if (pos) {
+        const uint32_t s0 = select_bit(mv, kk);
+        if (s0 >= bc) { fail(D, ErrCheckout, 13); return; }
+        ol = U(bcast(it, s0));
+        s = s0 + 1;
+    }
+    if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_BLOAD] += t - tp; tp = t; }
     // origin_right: first live item at or after the cursor (possibly a deleted one)
-    const u64 ml = s >= 64 ? 0ull : (U64(ix_ld64<L>(D.mlive + b)) & (~0ull << s));
+    const u64 mlr = s >= 64 ? 0ull : (ml & (~0ull << s));
     uint32_t rb, rs, orr;
     bool direct;
-    if (ml) {
+    if (mlr) {
         rb = b;
-        rs = first_lane(ml);
+        rs = first_lane(mlr);
         orr = U(bcast(it, rs));
         direct = rs == s;
     } else {
-        const uint32_t p = ix_ld<L>(D.opos + b) + 1;
-        rb = next_live_block<L>(D, p);
+        rb = next_live_block<L>(D, b);
         if (D.err) return;
-        if (rb != NO_BLOCK) {
-            rs = first_lane(U64(ix_ld64<L>(D.mlive + rb)));
+        if (rb != NONE) {
+            rs = first_lane(U64(ld_sc(D.mlive + rb)));
             orr = U(D.items[size_t(rb) * BLK + rs]);
         } else {
             rs = 0;
             orr = END_ID;
         }
         // direct iff no item lies between the cursor and origin_right
-        if (s < cnt) direct = false;
-        else if (p >= D.nb) direct = true;
-        else direct = rb == U(ix_ld<L>(D.ord + p)) && rs == 0;
+        if (s < bc) direct = false;
+        else {
+            const uint32_t nx = next_block<L>(D, b);
+            direct = nx == NONE || (rb == nx && rs == 0);
+        }
     }
     if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_ORR] += t - tp; tp = t; }
     if (!direct) {
-        const uint64_t t0 = tick<PROF>();
         const uint32_t my_l = ol == ROOT_ID ? 0u : U(key_of<L>(D, ol)) + 1u;
         const uint32_t my_r = orr == END_ID ? 0xFFFFFFFFu : U(key_of<L>(D, orr));
         const uint32_t b0 = b;
         yjs_scan<L>(D, b, s, rb, rs, my_l, my_r, orr, lv);
         if (D.err) return;
-        if (b != b0) {
-            const uint32_t c2 = U(ix_ld8<L>(D.bcnt + b));
-            it = l < c2 ? D.items[size_t(b) * BLK + l] : 0;
-        }
-        if (PROF) { D.prof[P_YJS] += tick<PROF>() - t0; D.prof[P_N_YJS]++; }
+        if (b != b0) load_block<L>(D, b, c_items(U(ix<L>(D.cnt + b))), it, mv, ml);
+        if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_YJS] += t - tp; tp = t; D.prof[P_N_YJS]++; }
     }
-    if (PROF) tp = tick<PROF>();
     const uint64_t sp0 = PROF ? D.prof[P_SPLIT] : 0;
-    insert_run<L, PROF>(D, b, s, it, lv, k, ol, orr);
+    insert_run<L, PROF>(D, b, s, it, mv, ml, lv, k, ol, orr);
     if (PROF) D.prof[P_RUN] += tick<PROF>() - tp - (D.prof[P_SPLIT] - sp0);
     D.n_items += k;
 }
@@ -499,25 +600,29 @@ DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
     uint32_t j0 = 0;
     while (j0 < n) {
         if (!charge(D)) return;
-        uint32_t b, s;
-        if (!find_vis<L>(D, pos, b, s)) { fail(D, ErrCheckout, 14); return; }
-        const u64 vm = U64(ix_ld64<L>(D.mvis + b)) & (~0ull << s);
-        const uint32_t avail = uint32_t(__popcll(vm));
+        uint32_t b, kk;
+        if (!find_vis<L>(D, pos, b, kk)) { fail(D, ErrCheckout, 14); return; }
+        const uint32_t c = U(ix<L>(D.cnt + b));
+        uint32_t it;
+        u64 mv, ml;
+        load_block<L>(D, b, c_items(c), it, mv, ml);
+        const uint32_t avail = c_vis(c) - kk;
         const uint32_t take = min(avail, n - j0);
-        const uint32_t r = uint32_t(__popcll(vm & ((1ull << l) - 1ull)));
-        const bool sel = ((vm >> l) & 1ull) && r < take;
+        const uint32_t r = uint32_t(__popcll(mv & lanes_below(l)));
+        const bool sel = ((mv >> l) & 1ull) && r >= kk && r < kk + take;
         const u64 selm = __ballot(sel);
+        if (uint32_t(__popcll(selm)) != take || take == 0) { fail(D, ErrCheckout, 15); return; }
         if (sel) {
-            const uint32_t item = D.items[size_t(b) * BLK + l];
-            const uint32_t j = j0 + r;
+            const uint32_t j = j0 + (r - kk);
             const uint32_t dlv = fwd ? lv + j : lv + n - 1 - j;
-            loc_add(D.loc + item, CNT_ONE);   // visible (count 1) -> deleted once
-            D.aux[dlv] = item;
+            loc_add(D.loc + it, CNT_ONE);   // visible (count 1) -> deleted once
+            D.aux[dlv] = it;
         }
         if (l == 0) {
-            D.mvis[b] = ix_ld64<L>(D.mvis + b) & ~selm;
-            const uint32_t sbi = ix_ld<L>(D.opos + b) / SB;
-            D.svis[sbi] = ix_ld<L>(D.svis + sbi) - take;
+            st_sc(D.mvis + b, mv & ~selm);
+            D.cnt[b] = c - take * C_VIS;
+            const uint32_t S = ix<L>(D.opos + b) >> 6;
+            D.svis[S] = ix<L>(D.svis + S) - take;
         }
         wave_fence();
         j0 += take;
@@ -549,11 +654,24 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n) {
                     bad = true;
                 } else {
                     const u64 bit = 1ull << loc_slot(old);
-                    if ((oc == 1) != (nc == 1)) {
-                        atomicXor(&D.mvis[b], bit);
-                        atomicAdd(&D.svis[ix_ld<L>(D.opos + b) / SB], nc == 1 ? 1u : 0xFFFFFFFFu);
+                    const bool fv = (oc == 1) != (nc == 1), fl = (oc != 0) != (nc != 0);
+                    if (fv || fl) {
+                        const uint32_t S = ix<L>(D.opos + b) >> 6;
+                        uint32_t dc = 0;
+                        if (fv) {
+                            at_xor(D.mvis + b, bit);
+                            const uint32_t d = nc == 1 ? 1u : 0xFFFFFFFFu;
+                            at_add(D.svis + S, d);
+                            dc += d * C_VIS;
+                        }
+                        if (fl) {
+                            at_xor(D.mlive + b, bit);
+                            const uint32_t d = nc != 0 ? 1u : 0xFFFFFFFFu;
+                            at_add(D.slive + S, d);
+                            dc += d * C_LIVE;
+                        }
+                        at_add(D.cnt + b, dc);
                     }
-                    if ((oc != 0) != (nc != 0)) atomicXor(&D.mlive[b], bit);
                 }
             }
         }
@@ -566,54 +684,55 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n) {
 // (list/merge.rs:63-95).  G blocks per round keep that many dependent gathers in flight.
 template <bool L>
 DEV void materialise(Doc &D, uint8_t *out, uint32_t cap, uint32_t &len_out, u64 &hash_out) {
-    constexpr uint32_t G = 4;
+    constexpr uint32_t G = 8;
     const uint32_t l = lane_id();
     uint32_t total = 0;
     u64 h = 0;
-    for (uint32_t i = 0; i < D.nb; i += G) {
-        uint32_t it[G], cb[G];
-        bool vis[G];
-#pragma unroll
-        for (uint32_t g = 0; g < G; g++) {
-            const uint32_t p = i + g;
-            vis[g] = false;
-            it[g] = 0;
-            if (p < D.nb) {
-                const uint32_t b = U(ix_ld<L>(D.ord + p));
-                const u64 mv = U64(ix_ld64<L>(D.mvis + b));
-                vis[g] = (mv >> l) & 1ull;
-                if (vis[g]) it[g] = D.items[size_t(b) * BLK + l];
-            }
-        }
-#pragma unroll
-        for (uint32_t g = 0; g < G; g++) cb[g] = vis[g] ? D.cbyte[it[g]] : 0;
-        if (D.ascii) {
-            uint8_t by[G];
-#pragma unroll
-            for (uint32_t g = 0; g < G; g++) by[g] = vis[g] ? D.content[cb[g]] : 0;
+    for (uint32_t p = 0; p < D.nsb; p++) {
+        const uint32_t S = U(ix<L>(D.sbord + p));
+        const uint32_t n = U(ix<L>(D.sbn + S));
+        for (uint32_t i = 0; i < n; i += G) {
+            // lane g < G fetches block g's visible mask
+            const uint32_t bl = l < G && i + l < n ? ix16<L>(D.sbl + size_t(S) * SBC + i + l) : 0;
+            const u64 mvl = l < G && i + l < n ? ld_sc(D.mvis + bl) : 0ull;
+            uint32_t it[G], cb[G];
+            bool vis[G];
 #pragma unroll
             for (uint32_t g = 0; g < G; g++) {
-                const uint32_t n = vis[g] ? 1u : 0u;
-                const uint32_t inc = wave_scan(n);
-                const uint32_t at = total + inc - n;
-                if (n) {
-                    if (at < cap) out[at] = by[g];
-                    h += splitmix((u64(at) << 8) | by[g]);
-                }
-                total += bcast(inc, 63);
+                const uint32_t b = bcast(bl, g);
+                vis[g] = (bcast64(mvl, g) >> l) & 1ull;
+                it[g] = vis[g] ? D.items[size_t(b) * BLK + l] : 0;
             }
-        } else {
 #pragma unroll
-            for (uint32_t g = 0; g < G; g++) {
-                const uint32_t n = vis[g] ? utf8_len(D.content[cb[g]]) : 0u;
-                const uint32_t inc = wave_scan(n);
-                const uint32_t at = total + inc - n;
-                for (uint32_t k = 0; k < n; k++) {
-                    const uint8_t byte = D.content[cb[g] + k];
-                    if (at + k < cap) out[at + k] = byte;
-                    h += splitmix((u64(at + k) << 8) | byte);
+            for (uint32_t g = 0; g < G; g++) cb[g] = vis[g] ? D.cbyte[it[g]] : 0;
+            if (D.ascii) {
+                uint8_t by[G];
+#pragma unroll
+                for (uint32_t g = 0; g < G; g++) by[g] = vis[g] ? D.content[cb[g]] : 0;
+#pragma unroll
+                for (uint32_t g = 0; g < G; g++) {
+                    const uint32_t c = vis[g] ? 1u : 0u;
+                    const uint32_t inc = wave_scan(c);
+                    const uint32_t at = total + inc - c;
+                    if (c) {
+                        if (at < cap) out[at] = by[g];
+                        h += splitmix((u64(at) << 8) | by[g]);
+                    }
+                    total += bcast(inc, 63);
                 }
-                total += bcast(inc, 63);
+            } else {
+#pragma unroll
+                for (uint32_t g = 0; g < G; g++) {
+                    const uint32_t c = vis[g] ? utf8_len(D.content[cb[g]]) : 0u;
+                    const uint32_t inc = wave_scan(c);
+                    const uint32_t at = total + inc - c;
+                    for (uint32_t k = 0; k < c; k++) {
+                        const uint8_t byte = D.content[cb[g] + k];
+                        if (at + k < cap) out[at + k] = byte;
+                        h += splitmix((u64(at + k) << 8) | byte);
+                    }
+                    total += bcast(inc, 63);
+                }
             }
         }
     }
@@ -621,60 +740,71 @@ DEV void materialise(Doc &D, uint8_t *out, uint32_t cap, uint32_t &len_out, u64 
     hash_out = wave_sum64(h);
 }
 
-// Debug-mode consistency check of the whole structure (DTGPU_DEBUG): returns 0 or a code.
+// Debug-mode consistency check of the whole structure (DTGPU_DEBUG=1): returns 0 or a code.
 template <bool L>
 DEV uint32_t check_invariants(Doc &D, DocResult *res) {
     const uint32_t l = lane_id();
-    for (uint32_t i = 0; i < D.nb; i++) {
-        const uint32_t b = U(ix_ld<L>(D.ord + i));
-        if (U(ix_ld<L>(D.opos + b)) != i) return 201;
-        const uint32_t cnt = U(ix_ld8<L>(D.bcnt + b));
-        const u64 mv = U64(ix_ld64<L>(D.mvis + b)), ml = U64(ix_ld64<L>(D.mlive + b));
-        bool bad = false;
-        uint32_t w = 0, it = 0xFFFFFFFFu;
-        if (l < cnt) {
-            it = D.items[size_t(b) * BLK + l];
-            if (it >= D.n_lv) bad = true;
-            else {
-                w = loc_load(D.loc + it);
-                const uint32_t c = loc_cnt(w);
-                if (((mv >> l) & 1) != (c == 1 ? 1u : 0u)) bad = true;
-                if (((ml >> l) & 1) != (c != 0 ? 1u : 0u)) bad = true;
-                if (loc_blk(w) != b || loc_slot(w) != l) bad = true;
+    uint32_t blocks = 0;
+    for (uint32_t p = 0; p < D.nsb; p++) {
+        const uint32_t S = U(ix<L>(D.sbord + p));
+        if (U(ix<L>(D.sbpos + S)) != p) return 205;
+        const uint32_t n = U(ix<L>(D.sbn + S));
+        if (n == 0 || n >= SBC) return 206;
+        uint32_t tv = 0, tl = 0;
+        for (uint32_t i = 0; i < n; i++) {
+            const uint32_t b = U(ix16<L>(D.sbl + size_t(S) * SBC + i));
+            if (U(ix<L>(D.opos + b)) != ((S << 6) | i)) return 201;
+            const uint32_t c = U(ix<L>(D.cnt + b));
+            const uint32_t cnt = c_items(c);
+            const u64 mv = U64(ld_sc(D.mvis + b)), ml = U64(ld_sc(D.mlive + b));
+            if (uint32_t(__popcll(mv)) != c_vis(c) || uint32_t(__popcll(ml)) != c_live(c)) return 207;
+            tv += c_vis(c);
+            tl += c_live(c);
+            bool bad = false;
+            uint32_t w = 0, it = 0xFFFFFFFFu;
+            if (l < cnt) {
+                it = D.items[size_t(b) * BLK + l];
+                if (it >= D.n_lv) bad = true;
+                else {
+                    w = ld_sc(D.loc + it);
+                    const uint32_t k = loc_cnt(w);
+                    if (((mv >> l) & 1) != (k == 1 ? 1u : 0u)) bad = true;
+                    if (((ml >> l) & 1) != (k != 0 ? 1u : 0u)) bad = true;
+                    if (loc_blk(w) != b || loc_slot(w) != l) bad = true;
+                }
+            } else if (((mv | ml) >> l) & 1) bad = true;
+            const u64 bm = __ballot(bad);
+            if (bm) {
+                if (l == first_lane(bm)) {
+                    res->dbg[0] = b; res->dbg[1] = l; res->dbg[2] = cnt; res->dbg[3] = it; res->dbg[4] = w;
+                    res->dbg[5] = uint32_t(mv); res->dbg[6] = uint32_t(mv >> 32);
+                    res->dbg[7] = uint32_t(ml); res->dbg[8] = uint32_t(ml >> 32);
+                }
+                return 202;
             }
-        } else if (((mv | ml) >> l) & 1) bad = true;
-        const u64 bm = __ballot(bad);
-        if (bm) {
-            if (l == first_lane(bm)) {
-                res->dbg[0] = b; res->dbg[1] = l; res->dbg[2] = cnt; res->dbg[3] = it; res->dbg[4] = w;
-                res->dbg[5] = uint32_t(mv); res->dbg[6] = uint32_t(mv >> 32);
-                res->dbg[7] = uint32_t(ml); res->dbg[8] = uint32_t(ml >> 32);
-            }
-            return 202;
+            blocks++;
         }
+        if (tv != U(ix<L>(D.svis + S))) return 203;
+        if (tl != U(ix<L>(D.slive + S))) return 204;
     }
-    const uint32_t nsb = (D.nb + SB - 1) / SB;
-    for (uint32_t s = 0; s < nsb; s++) {
-        const uint32_t i = s * SB + l;
-        const uint32_t b = i < D.nb ? ix_ld<L>(D.ord + i) : 0;
-        const uint32_t v = i < D.nb ? uint32_t(__popcll(ix_ld64<L>(D.mvis + b))) : 0;
-        const uint32_t c = i < D.nb ? uint32_t(D.bcnt[b]) : 0;
-        if (U(wave_sum(v)) != U(ix_ld<L>(D.svis + s))) return 203;
-        if (U(wave_sum(c)) != U(ix_ld<L>(D.scnt + s))) return 204;
-    }
+    if (blocks != D.nb) return 208;
     return 0;
 }
 
 template <bool L, bool PROF>
 DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
     const uint32_t l = lane_id();
-    // fresh tracker: one empty block (loc words are written when their item is inserted)
+    // fresh tracker: one empty block in one superblock (loc words are written when their
+    // item is inserted)
     if (l == 0) {
-        D.ord[0] = 0; D.opos[0] = 0; D.bcnt[0] = 0; D.mvis[0] = 0; D.mlive[0] = 0;
-        D.svis[0] = 0; D.scnt[0] = 0;
+        D.cnt[0] = 0; D.opos[0] = 0;
+        D.sbl[0] = 0; D.sbn[0] = 1; D.svis[0] = 0; D.slive[0] = 0; D.sbpos[0] = 0; D.sbord[0] = 0;
+        st_sc(D.mvis, 0ull);
+        st_sc(D.mlive, 0ull);
     }
     wave_fence();
     D.nb = 1;
+    D.nsb = 1;
     D.err = 0;
     D.n_items = 0;
     D.steps = 0;
@@ -732,21 +862,23 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
         if (PROF) {
             D.prof[P_MAT] = tick<PROF>() - t_mat;
             for (int i = 0; i < P_N; i++) res->dbg[i] = uint32_t(D.prof[i] >> (i < P_N_YJS ? 4 : 0));
-            res->dbg[P_N] = uint32_t((tick<PROF>() - t_start) >> 4);
+            res->dbg[15] = uint32_t((tick<PROF>() - t_start) >> 4);
         }
     }
 }
 
-// Carve a block index for capacity `mb` out of `base` (LDS or HBM).
-DEV void bind_index(Doc &D, uint8_t *base, uint32_t mb) {
-    const uint32_t nsb = (mb + 63) / 64;
-    D.mvis = reinterpret_cast<u64 *>(base);
-    D.mlive = D.mvis + mb;
-    D.ord = reinterpret_cast<uint32_t *>(D.mlive + mb);
-    D.opos = D.ord + mb;
-    D.svis = D.opos + mb;
-    D.scnt = D.svis + nsb;
-    D.bcnt = reinterpret_cast<uint8_t *>(D.scnt + nsb);
+// Carve an index for `mb` blocks / `ms` superblocks out of `base` (LDS or HBM); layout must
+// match index_bytes().
+DEV void bind_index(Doc &D, uint8_t *base, uint32_t mb, uint32_t ms) {
+    uint32_t *w = reinterpret_cast<uint32_t *>(base);
+    D.cnt = w; w += mb;
+    D.opos = w; w += mb;
+    D.svis = w; w += ms;
+    D.slive = w; w += ms;
+    D.sbn = w; w += ms;
+    D.sbpos = w; w += ms;
+    D.sbord = w; w += ms;
+    D.sbl = reinterpret_cast<uint16_t *>(w);
 }
 
 // One 64-lane workgroup per document of the list (the hardware dispatcher is the work queue;
@@ -773,12 +905,16 @@ __global__ __launch_bounds__(64) void replay_kernel(BatchParams P) {
     D.aux = P.aux + dd.lv_off;
     D.orr = P.orr + dd.lv_off;
     D.items = P.items + dd.blk_off * BLK;
+    D.mvis = P.mvis + dd.blk_off;
+    D.mlive = P.mlive + dd.blk_off;
     D.max_blocks = U(dd.max_blocks);
+    D.max_sb = sb_capacity(D.max_blocks);
     if (LDS_INDEX) {
-        bind_index(D, smem, P.lds_blocks);
         if (D.max_blocks > P.lds_blocks) D.max_blocks = P.lds_blocks;
+        D.max_sb = sb_capacity(P.lds_blocks);
+        bind_index(D, smem, P.lds_blocks, D.max_sb);
     } else {
-        bind_index(D, P.gidx + dd.gidx_off, D.max_blocks);
+        bind_index(D, P.gidx + dd.gidx_off, D.max_blocks, D.max_sb);
     }
     run_doc<LDS_INDEX, PROF>(D, P.out + dd.out_off, U(dd.out_cap), &P.results[d]);
 }

@@ -60,6 +60,7 @@ struct dtgpu_batch {
 
     DevBuf<Cmd> d_cmds;
     DevBuf<uint32_t> d_tlist, d_cbyte, d_aruns, d_loc, d_aux, d_orr, d_items, d_lists, d_counter;
+    DevBuf<unsigned long long> d_mvis, d_mlive;
     DevBuf<uint8_t> d_content, d_out, d_gidx;
     DevBuf<DocDesc> d_docs;
     DevBuf<DocResult> d_results;
@@ -133,7 +134,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         if (p.status != OK) continue;
         uint64_t n_ins = 0;
         for (const OpRun &r : p.log.ops) if (r.kind == 0) n_ins += r.len;
-        if (n_ins / 32 + 2 > LOC_MAX_BLOCKS) { B->host_status[i] = ErrCapacity; continue; }
+        if (n_ins / 32 + 2 > std::min<uint64_t>(LOC_MAX_BLOCKS, MAX_DOC_BLOCKS)) { B->host_status[i] = ErrCapacity; continue; }
         d.cmd_off = cmds.size();
         d.tlist_off = tlist.size();
         d.ascii = p.log.ins_content.size() == n_ins ? 1u : 0u;
@@ -187,6 +188,8 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     CK(B->d_aux.alloc(lv_total));
     CK(B->d_orr.alloc(lv_total));
     CK(B->d_items.alloc(blk_total * 64));
+    CK(B->d_mvis.alloc(blk_total));
+    CK(B->d_mlive.alloc(blk_total));
     CK(B->d_out.alloc(out_total));
     CK(B->d_gidx.alloc(gidx_total));
     CK(B->d_counter.alloc(2));
@@ -205,6 +208,8 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     base.aux = B->d_aux.p;
     base.orr = B->d_orr.p;
     base.items = B->d_items.p;
+    base.mvis = B->d_mvis.p;
+    base.mlive = B->d_mlive.p;
     base.out = B->d_out.p;
     base.gidx = B->d_gidx.p;
     base.docs = B->d_docs.p;

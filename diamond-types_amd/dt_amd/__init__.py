@@ -308,7 +308,7 @@ class Batch:
         _check(lib().dtgpu_batch_doc_stats(self._h, i, out))
         keys = ["n_items", "n_blocks", "fail_cmd", "fail_site", "n_cmds", "max_blocks",
                 "cyc_ins", "cyc_del", "cyc_tog", "cyc_mat", "cyc_yjs", "cyc_split", "cyc_find", "cyc_bload",
-                "cyc_orr", "cyc_run", "n_yjs", "n_split", "cyc_total"]
+                "cyc_orr", "cyc_run", "cyc_r1", "cyc_r2", "cyc_r3", "n_yjs", "n_split", "cyc_total"]
         return dict(zip(keys, list(out)))
 
     @property
