@@ -53,6 +53,8 @@ struct BatchParams {
     uint32_t n_list;
     uint32_t lds_blocks;    // block-index capacity held in LDS (small tier)
     uint32_t *counter;      // work-queue head, zeroed before each launch
+    uint32_t *fb_list;      // LDS-tier documents handed to the HBM tier (capacity overflow)
+    uint32_t *fb_count;
     uint32_t debug;         // DTGPU_DEBUG: bit 0 invariant checks, bit 1 cycle profile
     DocResult *results;
 };

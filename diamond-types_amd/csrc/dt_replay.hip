@@ -9,7 +9,8 @@
 //   block        64 item slots in document order; items[] (LV ids), and the visible / live
 //                (non-NIY) bit masks mvis[] / mlive[]: HBM.
 //   superblock   an ordered list of <= 64 block ids (sbl) with visible / live totals.
-//   top          the ordered list of superblocks (sbord).
+//   top          the ordered list of superblocks: top[p] = superblock id << 16 | visible
+//                total, tlive[p] = live total, by top position p.
 //   The block and superblock index (packed per-block counts: visible | live << 8 | items << 16;
 //   block -> (superblock, index) opos; the superblock lists and totals) lives in LDS for
 //   documents whose index fits the LDS budget and in HBM otherwise (same code).  A full block
@@ -145,7 +146,8 @@ struct Doc {
     uint32_t max_blocks, max_sb;
     // index (LDS or HBM)
     uint32_t *cnt, *opos;                                // per block
-    uint32_t *svis, *slive, *sbn, *sbpos, *sbord;        // per superblock / top order
+    uint32_t *sbn, *sbpos;                               // per superblock
+    uint32_t *top, *tlive;                               // by top position
     uint16_t *sbl;                                       // per superblock: SBC block ids
     // wave-uniform scalars
     uint32_t nb, nsb;
@@ -156,6 +158,8 @@ struct Doc {
     uint64_t steps, step_limit;   // watchdog: every loop iteration is charged; a bound
                                   // violation ends the document with ErrCapacity
     uint64_t prof[P_N];
+    uint32_t doc;
+    uint32_t *fb_list, *fb_count;   // LDS tier: capacity-overflow queue for the HBM tier
 };
 
 DEV void fail(Doc &D, uint32_t code, uint32_t site) {
@@ -172,7 +176,7 @@ template <bool PROF> DEV uint64_t tick() { return PROF ? __builtin_amdgcn_s_memt
 // ---- navigation ------------------------------------------------------------------------------
 
 template <bool L> DEV uint32_t first_block(const Doc &D) {
-    return U(ix16<L>(D.sbl + size_t(U(ix<L>(D.sbord))) * SBC));
+    return U(ix16<L>(D.sbl + size_t(U(ix<L>(D.top)) >> 16) * SBC));
 }
 // Next block in document order, or NONE.
 template <bool L> DEV uint32_t next_block(const Doc &D, uint32_t b) {
@@ -181,7 +185,7 @@ template <bool L> DEV uint32_t next_block(const Doc &D, uint32_t b) {
     if (i + 1 < U(ix<L>(D.sbn + S))) return U(ix16<L>(D.sbl + size_t(S) * SBC + i + 1));
     const uint32_t p = U(ix<L>(D.sbpos + S)) + 1;
     if (p >= D.nsb) return NONE;
-    return U(ix16<L>(D.sbl + size_t(U(ix<L>(D.sbord + p))) * SBC));
+    return U(ix16<L>(D.sbl + size_t(U(ix<L>(D.top + p)) >> 16) * SBC));
 }
 // Document-order key of (block, slot).
 template <bool L> DEV uint32_t key_at(const Doc &D, uint32_t b, uint32_t s) {
@@ -196,25 +200,31 @@ template <bool L> DEV uint32_t key_of(const Doc &D, uint32_t item) {
 // Block holding visible index p and the rank k of that item among the block's visible items
 // (content-tree cursor_at_content_pos, root.rs:50-89): prefix scans over superblock totals,
 // then over the chosen superblock's block counts.
+struct Found {
+    uint32_t b, k;     // block, rank of the item among the block's visible items
+    uint32_t S, tp;    // its superblock and that superblock's top position
+};
 template <bool L>
-DEV bool find_vis(Doc &D, uint32_t p, uint32_t &ob, uint32_t &ok) {
+DEV bool find_vis(Doc &D, uint32_t p, Found &f) {
     const uint32_t l = lane_id();
     uint32_t base = 0, S = NONE;
     for (uint32_t c = 0; c < D.nsb; c += 64) {
         const uint32_t i = c + l;
-        const uint32_t s = i < D.nsb ? ix<L>(D.sbord + i) : 0;
-        const uint32_t v = i < D.nsb ? ix<L>(D.svis + s) : 0;
+        const uint32_t w = i < D.nsb ? ix<L>(D.top + i) : 0;
+        const uint32_t v = w & 0xFFFFu;
         const uint32_t inc = wave_scan(v);
         const u64 m = __ballot(base + inc > p);
         if (m) {
             const uint32_t fl = first_lane(m);
-            S = U(bcast(s, fl));
+            S = U(bcast(w, fl) >> 16);
+            f.tp = U(c + fl);
             base += bcast(inc - v, fl);
             break;
         }
         base += bcast(inc, 63);
     }
     if (S == NONE) return false;
+    f.S = S;
     const uint32_t n = U(ix<L>(D.sbn + S));
     const uint32_t b = l < n ? ix16<L>(D.sbl + size_t(S) * SBC + l) : 0;
     const uint32_t v = l < n ? c_vis(ix<L>(D.cnt + b)) : 0;
@@ -222,8 +232,8 @@ DEV bool find_vis(Doc &D, uint32_t p, uint32_t &ob, uint32_t &ok) {
     const u64 m = __ballot(base + inc > p);
     if (!m) return false;
     const uint32_t fl = first_lane(m);
-    ob = U(bcast(b, fl));
-    ok = U(p - base - bcast(inc - v, fl));
+    f.b = U(bcast(b, fl));
+    f.k = U(p - base - bcast(inc - v, fl));
     return true;
 }
 
@@ -251,10 +261,9 @@ DEV uint32_t next_live_block(Doc &D, uint32_t b) {
     for (uint32_t p = U(ix<L>(D.sbpos + S)) + 1; p < D.nsb; p += 64) {
         if (!charge(D)) return NONE;
         const uint32_t i = p + l;
-        const uint32_t s = i < D.nsb ? ix<L>(D.sbord + i) : 0;
-        const u64 m = __ballot(i < D.nsb && ix<L>(D.slive + s) != 0);
+        const u64 m = __ballot(i < D.nsb && ix<L>(D.tlive + i) != 0);
         if (m) {
-            S = U(bcast(s, first_lane(m)));
+            S = U(ix<L>(D.top + p + first_lane(m)) >> 16);
             const uint32_t n = U(ix<L>(D.sbn + S));
             const uint32_t bl = l < n ? ix16<L>(D.sbl + size_t(S) * SBC + l) : 0;
             const u64 m2 = __ballot(l < n && c_live(ix<L>(D.cnt + bl)) != 0);
@@ -289,44 +298,45 @@ DEV void split_sb(Doc &D, uint32_t S) {
     const uint32_t vh = wave_sum(l >= 32 ? vis : 0), lh = wave_sum(l >= 32 ? live : 0);
     const uint32_t vl = wave_sum(l < 32 ? vis : 0), ll = wave_sum(l < 32 ? live : 0);
     const uint32_t p = U(ix<L>(D.sbpos + S)) + 1;
-    // shift sbord[p .. nsb) right by one, highest chunk first
+    // shift top[p .. nsb) / tlive right by one, highest chunk first
     for (int c = int(D.nsb) - 1; c >= int(p); c -= 64) {
         const int i = c - int(l);
-        uint32_t v = 0;
-        if (i >= int(p)) v = ix<L>(D.sbord + i);
+        uint32_t w = 0, lv = 0;
+        if (i >= int(p)) { w = ix<L>(D.top + i); lv = ix<L>(D.tlive + i); }
         wave_fence();
-        if (i >= int(p)) { D.sbord[i + 1] = v; D.sbpos[v] = uint32_t(i + 1); }
+        if (i >= int(p)) { D.top[i + 1] = w; D.tlive[i + 1] = lv; D.sbpos[w >> 16] = uint32_t(i + 1); }
         wave_fence();
     }
     if (l == 0) {
         D.sbn[S] = SBC / 2;
         D.sbn[S2] = SBC / 2;
-        D.svis[S] = vl; D.slive[S] = ll;
-        D.svis[S2] = vh; D.slive[S2] = lh;
-        D.sbord[p] = S2;
+        D.top[p - 1] = (S << 16) | vl; D.tlive[p - 1] = ll;
+        D.top[p] = (S2 << 16) | vh; D.tlive[p] = lh;
         D.sbpos[S2] = p;
     }
     wave_fence();
     D.nsb++;
 }
 
-// Split the full block b (items in `it` lane by lane, masks mv / ml): the upper half moves to
-// a new block placed right after b in its superblock.
+// Split the full block b (items in `it` lane by lane, masks mv / ml) at slot c: items [c, 64)
+// move to a new block b2 placed right after b in its superblock.
 template <bool L>
-DEV uint32_t split_block(Doc &D, uint32_t b, uint32_t it, u64 mv, u64 ml) {
+DEV uint32_t split_block(Doc &D, uint32_t b, uint32_t c, uint32_t it, u64 mv, u64 ml) {
     const uint32_t l = lane_id();
     if (D.nb >= D.max_blocks) { fail(D, ErrCapacity, 12); return 0; }
     const uint32_t b2 = D.nb;
-    if (l >= BLK / 2) {
-        D.items[size_t(b2) * BLK + (l - BLK / 2)] = it;
-        // (b, s) -> (b2, s - 32): one field-wise delta on the packed word
-        loc_add(D.loc + it, ((b2 - b) << LOC_BLK_SHIFT) - BLK / 2);
+    if (l >= c) {
+        D.items[size_t(b2) * BLK + (l - c)] = it;
+        // (b, s) -> (b2, s - c): one field-wise delta on the packed word
+        loc_add(D.loc + it, ((b2 - b) << LOC_BLK_SHIFT) - c);
     }
+    const u64 lo = lanes_below(c);
+    const u64 mv_hi = c >= 64 ? 0ull : mv >> c, ml_hi = c >= 64 ? 0ull : ml >> c;
     if (l == 0) {
-        st_sc(D.mvis + b2, mv >> 32);
-        st_sc(D.mvis + b, mv & 0xFFFFFFFFull);
-        st_sc(D.mlive + b2, ml >> 32);
-        st_sc(D.mlive + b, ml & 0xFFFFFFFFull);
+        st_sc(D.mvis + b2, mv_hi);
+        st_sc(D.mvis + b, mv & lo);
+        st_sc(D.mlive + b2, ml_hi);
+        st_sc(D.mlive + b, ml & lo);
     }
     const uint32_t o = U(ix<L>(D.opos + b));
     const uint32_t S = o >> 6, i = o & 63u, n = U(ix<L>(D.sbn + S));
@@ -341,9 +351,8 @@ DEV uint32_t split_block(Doc &D, uint32_t b, uint32_t it, u64 mv, u64 ml) {
         }
     }
     if (l == 0) {
-        D.cnt[b2] = uint32_t(__popcll(mv >> 32)) * C_VIS + uint32_t(__popcll(ml >> 32)) * C_LIVE + (BLK / 2) * C_ITEMS;
-        D.cnt[b] = uint32_t(__popcll(mv & 0xFFFFFFFFull)) * C_VIS + uint32_t(__popcll(ml & 0xFFFFFFFFull)) * C_LIVE +
-                   (BLK / 2) * C_ITEMS;
+        D.cnt[b2] = uint32_t(__popcll(mv_hi)) * C_VIS + uint32_t(__popcll(ml_hi)) * C_LIVE + (BLK - c) * C_ITEMS;
+        D.cnt[b] = uint32_t(__popcll(mv & lo)) * C_VIS + uint32_t(__popcll(ml & lo)) * C_LIVE + c * C_ITEMS;
         D.sbl[size_t(S) * SBC + i + 1] = uint16_t(b2);
         D.opos[b2] = (S << 6) | (i + 1);
         D.sbn[S] = n + 1;
@@ -353,6 +362,15 @@ DEV uint32_t split_block(Doc &D, uint32_t b, uint32_t it, u64 mv, u64 ml) {
     if (n + 1 == SBC) split_sb<L>(D, S);
     return b2;
 }
+
+// Cut point for splitting a full block that receives an insert at slot s.  The LDS tier cuts
+// at the insert point clamped to [16, 48]: an edit inside a block leaves the text after the
+// cursor in one block and the typing room in the other, so blocks end up ~43 items full on
+// the benchmark traces instead of ~35 (tools/blocksim.py measured the policies).  Its
+// capacity is sized for that fill; a document that still outgrows it is handed to the HBM
+// tier, which always cuts at the midpoint so every block keeps >= 32 items and
+// n_ins / 32 + 2 blocks suffice.
+template <bool L> DEV uint32_t cut_point(uint32_t s) { return L ? min(max(s, 16u), 48u) : BLK / 2; }
 
 // Insert the run [lv, lv+k) before slot s of block b (all new items visible).  `it` holds the
 // block's items lane by lane (lanes >= the block count are don't-care); mv / ml its masks.
@@ -367,17 +385,18 @@ DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml,
         const uint32_t bc = c_items(c);
         if (bc == BLK) {
             const uint64_t t0 = tick<PROF>();
-            const uint32_t b2 = split_block<L>(D, b, it, mv, ml);
+            const uint32_t cut = cut_point<L>(s);
+            const uint32_t b2 = split_block<L>(D, b, cut, it, mv, ml);
             if (D.err) return;
-            if (s > BLK / 2) {
+            if (s > cut || cut == BLK) {
                 b = b2;
-                s -= BLK / 2;
-                it = shfl(it, (l + BLK / 2) & 63u);
-                mv >>= 32;
-                ml >>= 32;
+                s -= cut;
+                it = shfl(it, (l + cut) & 63u);
+                mv = cut >= 64 ? 0ull : mv >> cut;
+                ml = cut >= 64 ? 0ull : ml >> cut;
             } else {
-                mv &= 0xFFFFFFFFull;
-                ml &= 0xFFFFFFFFull;
+                mv &= lanes_below(cut);
+                ml &= lanes_below(cut);
             }
             if (PROF) { D.prof[P_SPLIT] += tick<PROF>() - t0; D.prof[P_N_SPLIT]++; }
             continue;
@@ -405,9 +424,9 @@ DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml,
             st_sc(D.mvis + b, mv);
             st_sc(D.mlive + b, ml);
             D.cnt[b] = c + m * (C_VIS + C_LIVE + C_ITEMS);
-            const uint32_t S = ix<L>(D.opos + b) >> 6;
-            D.svis[S] = ix<L>(D.svis + S) + m;
-            D.slive[S] = ix<L>(D.slive + S) + m;
+            const uint32_t tp = ix<L>(D.sbpos + (ix<L>(D.opos + b) >> 6));
+            D.top[tp] = ix<L>(D.top + tp) + m;
+            D.tlive[tp] = ix<L>(D.tlive + tp) + m;
         }
         wave_fence();
         if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_R2] += t - tr; tr = t; }
@@ -533,9 +552,11 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
     uint32_t b, kk = 0;
     if (pos == 0) {
         b = first_block<L>(D);
-    } else if (!find_vis<L>(D, pos - 1, b, kk)) {
-        fail(D, ErrCheckout, 13);
-        return;
+    } else {
+        Found f;
+        if (!find_vis<L>(D, pos - 1, f)) { fail(D, ErrCheckout, 13); return; }
+        b = f.b;
+        kk = f.k;
     }
     if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_FIND] += t - tp; tp = t; }
     const uint32_t bc = c_items(U(ix<L>(D.cnt + b)));
@@ -600,8 +621,9 @@ DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
     uint32_t j0 = 0;
     while (j0 < n) {
         if (!charge(D)) return;
-        uint32_t b, kk;
-        if (!find_vis<L>(D, pos, b, kk)) { fail(D, ErrCheckout, 14); return; }
+        Found f;
+        if (!find_vis<L>(D, pos, f)) { fail(D, ErrCheckout, 14); return; }
+        const uint32_t b = f.b, kk = f.k;
         const uint32_t c = U(ix<L>(D.cnt + b));
         uint32_t it;
         u64 mv, ml;
@@ -621,8 +643,7 @@ DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
         if (l == 0) {
             st_sc(D.mvis + b, mv & ~selm);
             D.cnt[b] = c - take * C_VIS;
-            const uint32_t S = ix<L>(D.opos + b) >> 6;
-            D.svis[S] = ix<L>(D.svis + S) - take;
+            D.top[f.tp] = ix<L>(D.top + f.tp) - take;
         }
         wave_fence();
         j0 += take;
@@ -631,14 +652,15 @@ DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
 
 // One walk step's retreat + advance set (advance_retreat.rs:58-153), lane-parallel.
 // Entry: LV | is_del << 30 | advance << 31.
+// `pre` is the first 64-entry chunk when the caller prefetched it (have_pre).
 template <bool L>
-DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n) {
+DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_pre) {
     const uint32_t l = lane_id();
     for (uint32_t j = 0; j < n; j += 64) {
         if (!charge(D)) return;
         bool bad = false;
         if (j + l < n) {
-            const uint32_t e = D.tlist[off + j + l];
+            const uint32_t e = (j == 0 && have_pre) ? pre : D.tlist[off + j + l];
             const uint32_t lv = e & 0x3FFFFFFFu;
             const bool is_del = (e >> 30) & 1u, adv = (e >> 31) != 0;
             uint32_t item = lv;
@@ -656,18 +678,18 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n) {
                     const u64 bit = 1ull << loc_slot(old);
                     const bool fv = (oc == 1) != (nc == 1), fl = (oc != 0) != (nc != 0);
                     if (fv || fl) {
-                        const uint32_t S = ix<L>(D.opos + b) >> 6;
+                        const uint32_t tp = ix<L>(D.sbpos + (ix<L>(D.opos + b) >> 6));
                         uint32_t dc = 0;
                         if (fv) {
                             at_xor(D.mvis + b, bit);
                             const uint32_t d = nc == 1 ? 1u : 0xFFFFFFFFu;
-                            at_add(D.svis + S, d);
+                            at_add(D.top + tp, d);
                             dc += d * C_VIS;
                         }
                         if (fl) {
                             at_xor(D.mlive + b, bit);
                             const uint32_t d = nc != 0 ? 1u : 0xFFFFFFFFu;
-                            at_add(D.slive + S, d);
+                            at_add(D.tlive + tp, d);
                             dc += d * C_LIVE;
                         }
                         at_add(D.cnt + b, dc);
@@ -689,7 +711,7 @@ DEV void materialise(Doc &D, uint8_t *out, uint32_t cap, uint32_t &len_out, u64 
     uint32_t total = 0;
     u64 h = 0;
     for (uint32_t p = 0; p < D.nsb; p++) {
-        const uint32_t S = U(ix<L>(D.sbord + p));
+        const uint32_t S = U(ix<L>(D.top + p)) >> 16;
         const uint32_t n = U(ix<L>(D.sbn + S));
         for (uint32_t i = 0; i < n; i += G) {
             // lane g < G fetches block g's visible mask
@@ -746,7 +768,7 @@ DEV uint32_t check_invariants(Doc &D, DocResult *res) {
     const uint32_t l = lane_id();
     uint32_t blocks = 0;
     for (uint32_t p = 0; p < D.nsb; p++) {
-        const uint32_t S = U(ix<L>(D.sbord + p));
+        const uint32_t S = U(ix<L>(D.top + p)) >> 16;
         if (U(ix<L>(D.sbpos + S)) != p) return 205;
         const uint32_t n = U(ix<L>(D.sbn + S));
         if (n == 0 || n >= SBC) return 206;
@@ -784,8 +806,8 @@ DEV uint32_t check_invariants(Doc &D, DocResult *res) {
             }
             blocks++;
         }
-        if (tv != U(ix<L>(D.svis + S))) return 203;
-        if (tl != U(ix<L>(D.slive + S))) return 204;
+        if (tv != (U(ix<L>(D.top + p)) & 0xFFFFu)) return 203;
+        if (tl != U(ix<L>(D.tlive + p))) return 204;
     }
     if (blocks != D.nb) return 208;
     return 0;
@@ -798,7 +820,7 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
     // item is inserted)
     if (l == 0) {
         D.cnt[0] = 0; D.opos[0] = 0;
-        D.sbl[0] = 0; D.sbn[0] = 1; D.svis[0] = 0; D.slive[0] = 0; D.sbpos[0] = 0; D.sbord[0] = 0;
+        D.sbl[0] = 0; D.sbn[0] = 1; D.sbpos[0] = 0; D.top[0] = 0; D.tlive[0] = 0;
         st_sc(D.mvis, 0ull);
         st_sc(D.mlive, 0ull);
     }
@@ -813,7 +835,10 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
     D.ci = 0;
     if (PROF) for (int i = 0; i < P_N; i++) D.prof[i] = 0;
     const uint64_t t_start = tick<PROF>();
-    // commands are fetched 64 at a time (one per lane) and broadcast with readlane
+    // commands are fetched 64 at a time (one per lane) and broadcast with readlane; the first
+    // tlist chunk of a TOG is fetched while the command before it runs (tlist is read-only)
+    uint32_t pf = 0;
+    bool pf_ok = false;
     for (uint32_t base = 0; base < D.ncmd && !D.err; base += 64) {
         const uint32_t n_here = min(64u, D.ncmd - base);
         Cmd pre = {0, 0, 0, 0};
@@ -823,6 +848,13 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
             const uint32_t op = U(bcast(pre.op, j)), a = U(bcast(pre.lv, j)), n = U(bcast(pre.len, j)),
                            pos = U(bcast(pre.pos, j));
             if (!charge(D)) break;
+            uint32_t nx_pf = 0;
+            bool nx_ok = false;
+            if (j + 1 < n_here && (U(bcast(pre.op, j + 1)) & 15u) == CMD_TOG) {
+                const uint32_t o2 = U(bcast(pre.lv, j + 1)), n2 = U(bcast(pre.len, j + 1));
+                if (l < n2) nx_pf = D.tlist[o2 + l];
+                nx_ok = true;
+            }
             const uint64_t t0 = tick<PROF>();
             switch (op & 15u) {
                 case CMD_INS:
@@ -836,7 +868,7 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
                     if (PROF) D.prof[P_DEL] += tick<PROF>() - t0;
                     break;
                 case CMD_TOG:
-                    toggle_pass<L>(D, a, n);
+                    toggle_pass<L>(D, a, n, pf, pf_ok);
                     if (PROF) D.prof[P_TOG] += tick<PROF>() - t0;
                     break;
                 default: fail(D, ErrCheckout, 18); break;
@@ -845,7 +877,15 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
                 const uint32_t code = check_invariants<L>(D, res);
                 if (code) fail(D, ErrCheckout, code);
             }
+            pf = nx_pf;
+            pf_ok = nx_ok;
         }
+    }
+    // an LDS-tier document that outgrew its optimistic block capacity is queued for the HBM
+    // tier, which replays it again from scratch
+    if (L && D.err == ErrCapacity && (D.site == 12 || D.site == 21) && D.fb_list) {
+        if (l == 0) D.fb_list[atomicAdd(D.fb_count, 1u)] = D.doc;
+        return;
     }
     uint32_t len = 0;
     u64 h = 0;
@@ -873,11 +913,10 @@ DEV void bind_index(Doc &D, uint8_t *base, uint32_t mb, uint32_t ms) {
     uint32_t *w = reinterpret_cast<uint32_t *>(base);
     D.cnt = w; w += mb;
     D.opos = w; w += mb;
-    D.svis = w; w += ms;
-    D.slive = w; w += ms;
+    D.top = w; w += ms;
+    D.tlive = w; w += ms;
     D.sbn = w; w += ms;
     D.sbpos = w; w += ms;
-    D.sbord = w; w += ms;
     D.sbl = reinterpret_cast<uint16_t *>(w);
 }
 
@@ -887,10 +926,20 @@ template <bool LDS_INDEX, bool PROF>
 __global__ __launch_bounds__(64) void replay_kernel(BatchParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t di = U(blockIdx.x);
-    if (di >= P.n_list) return;
-    const uint32_t d = U(P.doc_list[di]);
+    uint32_t d;
+    if (di < P.n_list) {
+        d = U(P.doc_list[di]);
+    } else {   // HBM tier: documents the LDS tier handed back
+        if (LDS_INDEX || !P.fb_count) return;
+        const uint32_t j = di - P.n_list;
+        if (j >= U(__hip_atomic_load(P.fb_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) return;
+        d = U(P.fb_list[j]);
+    }
     const DocDesc dd = P.docs[d];
     Doc D;
+    D.doc = d;
+    D.fb_list = LDS_INDEX ? P.fb_list : nullptr;
+    D.fb_count = P.fb_count;
     D.debug = P.debug & 1u;
     D.cmds = P.cmds + dd.cmd_off;
     D.ncmd = U(dd.ncmd);
@@ -925,14 +974,17 @@ int launch_replay(const BatchParams &small, const BatchParams &large, void *stre
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const bool prof = (small.debug | large.debug) & 2u;
     if (small.n_list) {
+        if (small.fb_count && hipMemsetAsync(small.fb_count, 0, sizeof(uint32_t), s) != hipSuccess) return ErrHip;
         const size_t lds = size_t(index_bytes(small.lds_blocks));
         if (prof) hipLaunchKernelGGL((dev::replay_kernel<true, true>), dim3(small.n_list), dim3(64), lds, s, small);
         else hipLaunchKernelGGL((dev::replay_kernel<true, false>), dim3(small.n_list), dim3(64), lds, s, small);
         if (hipGetLastError() != hipSuccess) return ErrHip;
     }
-    if (large.n_list) {
-        if (prof) hipLaunchKernelGGL((dev::replay_kernel<false, true>), dim3(large.n_list), dim3(64), 0, s, large);
-        else hipLaunchKernelGGL((dev::replay_kernel<false, false>), dim3(large.n_list), dim3(64), 0, s, large);
+    // HBM tier: its own list plus a slot per LDS-tier document that may be handed back
+    const uint32_t grid = large.n_list + (small.fb_list ? small.n_list : 0);
+    if (grid) {
+        if (prof) hipLaunchKernelGGL((dev::replay_kernel<false, true>), dim3(grid), dim3(64), 0, s, large);
+        else hipLaunchKernelGGL((dev::replay_kernel<false, false>), dim3(grid), dim3(64), 0, s, large);
         if (hipGetLastError() != hipSuccess) return ErrHip;
     }
     return OK;

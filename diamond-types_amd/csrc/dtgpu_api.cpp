@@ -62,6 +62,7 @@ struct dtgpu_batch {
     DevBuf<uint32_t> d_tlist, d_cbyte, d_aruns, d_loc, d_aux, d_orr, d_items, d_lists, d_counter;
     DevBuf<unsigned long long> d_mvis, d_mlive;
     DevBuf<uint8_t> d_content, d_out, d_gidx;
+    DevBuf<uint32_t> d_fb;   // [0] = count, then the handed-back documents
     DevBuf<DocDesc> d_docs;
     DevBuf<DocResult> d_results;
     BatchParams small{}, large{};
@@ -124,6 +125,10 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     std::vector<uint32_t> tlist, cbyte, aruns;
     std::vector<uint8_t> content;
     uint64_t lv_total = 0, blk_total = 0, out_total = 0, gidx_total = 0;
+    // expected items per block in the LDS tier (insert-point splits keep typing runs in full
+    // blocks); DTGPU_LDS_FILL overrides it for experiments
+    uint64_t lds_fill = 40;
+    if (const char *e = getenv("DTGPU_LDS_FILL")) lds_fill = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
     for (size_t i = 0; i < n; i++) {
         Prepared &p = prep[i];
         B->host_status[i] = p.status;
@@ -164,12 +169,15 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         for (const GraphEntry &g : p.log.graph.entries) parents += g.parents.size();
         B->alg_in_bytes += 16ull * p.log.ops.size() + 8ull * p.log.graph.entries.size() + 4ull * parents +
                            12ull * p.log.agent_runs.size() + d.content_len;
-        if (index_bytes(d.max_blocks) <= kLdsIndexBudget) {
+        // every document gets an HBM index (the LDS tier hands back documents that outgrow
+        // their optimistic LDS capacity); the LDS tier is sized from the expected block fill
+        d.gidx_off = gidx_total;
+        gidx_total += index_bytes(d.max_blocks);
+        const uint32_t est = uint32_t(std::min<uint64_t>(d.max_blocks, n_ins / lds_fill + 8));
+        if (index_bytes(est) <= kLdsIndexBudget) {
             B->small_list.push_back(uint32_t(i));
-            B->lds_blocks = std::max(B->lds_blocks, d.max_blocks);
+            B->lds_blocks = std::max(B->lds_blocks, est);
         } else {
-            d.gidx_off = gidx_total;
-            gidx_total += index_bytes(d.max_blocks);
             B->large_list.push_back(uint32_t(i));
         }
     }
@@ -192,6 +200,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     CK(B->d_mlive.alloc(blk_total));
     CK(B->d_out.alloc(out_total));
     CK(B->d_gidx.alloc(gidx_total));
+    CK(B->d_fb.alloc(B->small_list.size() + 1));
     CK(B->d_counter.alloc(2));
     CK(B->d_results.alloc(n));
     CK(hipMemsetAsync(B->d_results.p, 0, std::max<size_t>(n, 1) * sizeof(DocResult), s));
@@ -223,6 +232,12 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     B->large.doc_list = B->d_lists.p + B->small_list.size();
     B->large.n_list = uint32_t(B->large_list.size());
     B->large.counter = B->d_counter.p + 1;
+    if (!B->small_list.empty() && !getenv("DTGPU_NO_FALLBACK")) {
+        B->small.fb_count = B->d_fb.p;
+        B->small.fb_list = B->d_fb.p + 1;
+        B->large.fb_count = B->d_fb.p;
+        B->large.fb_list = B->d_fb.p + 1;
+    }
     *out = B.release();
     return DTGPU_OK;
 }

@@ -116,3 +116,45 @@ def test_unicode():
     g.add_delete_without_content(s, 1, 2)
     g.add_insert(s, 6, "✓")
     assert g.checkout_tip().content() == "hllo 𝄞✓ wörld"
+
+
+def _with_env(env, fn):
+    import os
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return fn()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def test_lds_overflow_falls_back_to_hbm_tier():
+    """An optimistic LDS capacity far too small: every document overflows in the LDS tier and is
+    replayed by the HBM tier inside the same run; texts must still be exact."""
+    data = G.dt_bytes("friendsforever")
+    want = G.trace("friendsforever_flat")["endContent"].encode()
+
+    def run():
+        b = dt_amd.Batch(docs=[data] * 70 + [G.COMPAT_SIMPLE_LZ4])
+        b.run()
+        b.sync()
+        return b.results(), b.text(0), b.text(69), b.text(70)
+
+    res, t0, t69, t70 = _with_env({"DTGPU_LDS_FILL": "400"}, run)
+    assert all(r["status"] == 0 for r in res)
+    assert t0 == want and t69 == want and t70 == b"hi me"
+
+
+def test_invariants_hold_after_every_command():
+    """DTGPU_DEBUG=1 checks the whole tree (masks vs per-item counts, block / superblock totals,
+    positions) after every command of the replay."""
+    for name in ("friendsforever",):
+        data = G.dt_bytes(name)
+        got = _with_env({"DTGPU_DEBUG": "1"}, lambda: dt_amd.ListOpLog.load_from(data).checkout_tip_bytes())
+        assert got == G.trace("friendsforever_flat")["endContent"].encode()
+    g = _with_env({"DTGPU_DEBUG": "1"}, lambda: dt_amd.ListOpLog.load_from(G.COMPAT_SIMPLE_LZ4).checkout_tip_bytes())
+    assert g == b"hi me"
