@@ -41,11 +41,11 @@ struct BatchParams {
     const uint32_t *cbyte;
     const uint8_t *content;
     const uint32_t *aruns;
-    uint32_t *loc;
-    uint32_t *aux;
-    uint32_t *orr;
+    uint32_t *pos;
+    uint32_t *cv;
+    unsigned long long *ao;
     uint32_t *items;
-    unsigned long long *mvis, *mlive;   // per block: visible / live slot masks
+    unsigned long long *m2;   // per block: visible, live slot masks
     uint8_t *out;
     uint8_t *gidx;
     const DocDesc *docs;

@@ -15,12 +15,14 @@
 //   block -> (superblock, index) opos; the superblock lists and totals) lives in LDS for
 //   documents whose index fits the LDS budget and in HBM otherwise (same code).  A full block
 //   splits 64 -> 32 + 32 and a full superblock 64 -> 32 + 32, so a split costs O(64) work.
-//   loc[lv]      one packed word per inserted LV: count (8 bits: 0 NIY, 1 inserted, k >= 2
-//                deleted k-1 times) | block (18 bits) | slot (6 bits).  All loc and mask
-//                accesses are L2-coherent (sc1) atomics / loads / stores, so the returning
-//                atomic of a retreat/advance hands back the item's position and old state in
-//                one round trip.
-//   aux[lv]      Ins: origin_left; Del: the item it deleted.   orr[lv]: origin_right.
+//   pos[lv]      inserted LV: block << 6 | slot.  Written with plain stores (an insert
+//                rewrites the positions of the items it shifts; no read-modify-write).
+//   cv[lv]       inserted LV: count (0 NIY, 1 inserted, k >= 2 deleted k-1 times); the only
+//                per-item word that needs an atomic (a retreat/advance pass may touch one item
+//                from two lanes).
+//   ao[lv]       Ins: origin_left | origin_right << 32; Del: the item it deleted.
+//   Every per-document structure is touched by its own wave only, so all atomics are
+//   workgroup-scope and stay in the CU's L2 path.
 //
 // Commands: INS / DEL apply one op run; TOG applies one walk step's whole retreat + advance
 // set in one lane-parallel pass.  Counters make that legal: a retreat subtracts one, an advance
@@ -98,21 +100,20 @@ constexpr uint32_t SBC = 64;   // block capacity of a superblock list
 constexpr uint32_t ROOT_ID = 0xFFFFFFFFu;
 constexpr uint32_t END_ID = 0xFFFFFFFEu;
 constexpr uint32_t NONE = 0xFFFFFFFFu;
-constexpr uint32_t CNT_ONE = 1u << LOC_CNT_SHIFT;
 // packed per-block counts
 constexpr uint32_t C_VIS = 1u, C_LIVE = 1u << 8, C_ITEMS = 1u << 16;
 DEV uint32_t c_vis(uint32_t c) { return c & 0xFFu; }
 DEV uint32_t c_live(uint32_t c) { return (c >> 8) & 0xFFu; }
 DEV uint32_t c_items(uint32_t c) { return (c >> 16) & 0xFFu; }
 
-DEV uint32_t loc_blk(uint32_t w) { return (w >> LOC_BLK_SHIFT) & LOC_BLK_MASK; }
-DEV uint32_t loc_slot(uint32_t w) { return w & 63u; }
-DEV uint32_t loc_cnt(uint32_t w) { return w >> LOC_CNT_SHIFT; }
+DEV uint32_t pos_blk(uint32_t w) { return w >> 6; }
+DEV uint32_t pos_slot(uint32_t w) { return w & 63u; }
+DEV uint32_t pos_of(uint32_t b, uint32_t s) { return (b << 6) | s; }
 
 // L2-coherent accesses (returning atomics and loads must never meet a stale L1 line).
 template <typename T> DEV T ld_sc(const T *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 template <typename T> DEV void st_sc(T *p, T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
-DEV uint32_t loc_add(uint32_t *p, uint32_t d) { return __hip_atomic_fetch_add(p, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+DEV uint32_t cv_add(uint32_t *p, uint32_t d) { return __hip_atomic_fetch_add(p, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 template <typename T> DEV void at_xor(T *p, T v) { __hip_atomic_fetch_xor(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 template <typename T> DEV void at_add(T *p, T v) { __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 
@@ -137,12 +138,12 @@ struct Doc {
     uint32_t n_aruns;
     uint32_t ascii;
     // per-LV state (HBM)
-    uint32_t *loc;
-    uint32_t *aux;
-    uint32_t *orr;
+    uint32_t *pos;   // inserted LV: block << 6 | slot (plain stores only)
+    uint32_t *cv;    // inserted LV: count (0 NIY, 1 inserted, k >= 2 deleted k-1 times)
+    u64 *ao;         // Ins: origin_left | origin_right << 32; Del: the item it deleted (low word)
     // blocks (HBM)
     uint32_t *items;
-    u64 *mvis, *mlive;
+    u64 *m2;         // per block: visible mask, live mask (adjacent: one wave load / store)
     uint32_t max_blocks, max_sb;
     // index (LDS or HBM)
     uint32_t *cnt, *opos;                                // per block
@@ -193,8 +194,8 @@ template <bool L> DEV uint32_t key_at(const Doc &D, uint32_t b, uint32_t s) {
     return (ix<L>(D.sbpos + (o >> 6)) << 12) | ((o & 63u) << 6) | s;
 }
 template <bool L> DEV uint32_t key_of(const Doc &D, uint32_t item) {
-    const uint32_t w = ld_sc(D.loc + item);
-    return key_at<L>(D, loc_blk(w), loc_slot(w));
+    const uint32_t w = D.pos[item];
+    return key_at<L>(D, pos_blk(w), pos_slot(w));
 }
 
 // Block holding visible index p and the rank k of that item among the block's visible items
@@ -327,16 +328,13 @@ DEV uint32_t split_block(Doc &D, uint32_t b, uint32_t c, uint32_t it, u64 mv, u6
     const uint32_t b2 = D.nb;
     if (l >= c) {
         D.items[size_t(b2) * BLK + (l - c)] = it;
-        // (b, s) -> (b2, s - c): one field-wise delta on the packed word
-        loc_add(D.loc + it, ((b2 - b) << LOC_BLK_SHIFT) - c);
+        D.pos[it] = pos_of(b2, l - c);
     }
     const u64 lo = lanes_below(c);
     const u64 mv_hi = c >= 64 ? 0ull : mv >> c, ml_hi = c >= 64 ? 0ull : ml >> c;
-    if (l == 0) {
-        st_sc(D.mvis + b2, mv_hi);
-        st_sc(D.mvis + b, mv & lo);
-        st_sc(D.mlive + b2, ml_hi);
-        st_sc(D.mlive + b, ml & lo);
+    if (l < 4) {   // both blocks' mask pairs in one store
+        const u64 v = l == 0 ? (mv & lo) : l == 1 ? (ml & lo) : l == 2 ? mv_hi : ml_hi;
+        st_sc(D.m2 + 2 * size_t(l < 2 ? b : b2) + (l & 1), v);
     }
     const uint32_t o = U(ix<L>(D.opos + b));
     const uint32_t S = o >> 6, i = o & 63u, n = U(ix<L>(D.sbn + S));
@@ -404,25 +402,22 @@ DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml,
         uint64_t tr = tick<PROF>();
         const uint32_t m = min(k, BLK - bc);
         uint32_t *items = D.items + size_t(b) * BLK;
-        if (l >= s && l < bc) {
-            items[l + m] = it;
-            loc_add(D.loc + it, m);   // slot += m
-        }
-        if (l >= s && l < s + m) {
-            const uint32_t nit = lv + (l - s);
-            items[l] = nit;
-            st_sc(D.loc + nit, CNT_ONE | (b << LOC_BLK_SHIFT) | l);
-        }
-        if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_R1] += t - tr; tr = t; }
+        // the block after the insert, lane = slot: shifted items and the new ones are written
+        // with one store each for items and positions
         const uint32_t shifted = shfl(it, l >= m ? l - m : l);
         it = l < s ? it : (l < s + m ? lv + (l - s) : shifted);
+        if (l >= s && l < bc + m) {
+            items[l] = it;
+            D.pos[it] = pos_of(b, l);
+        }
+        if (l >= s && l < s + m) st_sc(D.cv + it, 1u);   // cv: atomics elsewhere, so scoped stores
+        if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_R1] += t - tr; tr = t; }
         const u64 low = lanes_below(s);
         const u64 ins = lanes_below(m) << s;
         mv = m == 64 ? ins : ((mv & low) | ((mv & ~low) << m) | ins);
         ml = m == 64 ? ins : ((ml & low) | ((ml & ~low) << m) | ins);
+        if (l < 2) st_sc(D.m2 + 2 * size_t(b) + l, l == 0 ? mv : ml);
         if (l == 0) {
-            st_sc(D.mvis + b, mv);
-            st_sc(D.mlive + b, ml);
             D.cnt[b] = c + m * (C_VIS + C_LIVE + C_ITEMS);
             const uint32_t tp = ix<L>(D.sbpos + (ix<L>(D.opos + b) >> 6));
             D.top[tp] = ix<L>(D.top + tp) + m;
@@ -437,8 +432,7 @@ DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml,
     const uint64_t t3 = tick<PROF>();
     for (uint32_t j = l; j < k0; j += 64) {
         const uint32_t nit = lv0 + j;
-        D.aux[nit] = j == 0 ? ol : nit - 1;
-        D.orr[nit] = orr;
+        D.ao[nit] = u64(j == 0 ? ol : nit - 1) | (u64(orr) << 32);
     }
     if (PROF) D.prof[P_R3] += tick<PROF>() - t3;
 }
@@ -494,7 +488,11 @@ DEV void yjs_scan(Doc &D, uint32_t &b, uint32_t &s, uint32_t rb, uint32_t rs, ui
         const bool inr = l >= cs && l < end;
         const uint32_t o = l < cnt ? D.items[size_t(cb) * BLK + l] : 0;
         uint32_t ol_o = ROOT_ID, orr_o = END_ID;
-        if (inr) { ol_o = D.aux[o]; orr_o = D.orr[o]; }
+        if (inr) {
+            const u64 x = D.ao[o];
+            ol_o = uint32_t(x);
+            orr_o = uint32_t(x >> 32);
+        }
         const uint32_t kl = ol_o == ROOT_ID ? 0u : key_of<L>(D, ol_o) + 1u;
         const uint32_t kr = orr_o == END_ID ? 0xFFFFFFFFu : key_of<L>(D, orr_o);
         const bool tie = inr && kl == my_l && orr_o == orr_new;
@@ -538,8 +536,7 @@ DEV void load_block(const Doc &D, uint32_t b, uint32_t bc, uint32_t &it, u64 &mv
     const uint32_t l = lane_id();
     it = l < bc ? D.items[size_t(b) * BLK + l] : 0;
     u64 x = 0;
-    if (l == 0) x = ld_sc(D.mvis + b);
-    if (l == 1) x = ld_sc(D.mlive + b);
+    if (l < 2) x = ld_sc(D.m2 + 2 * size_t(b) + l);
     mv = bcast64(x, 0);
     ml = bcast64(x, 1);
 }
@@ -584,7 +581,7 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
         rb = next_live_block<L>(D, b);
         if (D.err) return;
         if (rb != NONE) {
-            rs = first_lane(U64(ld_sc(D.mlive + rb)));
+            rs = first_lane(U64(ld_sc(D.m2 + 2 * size_t(rb) + 1)));
             orr = U(D.items[size_t(rb) * BLK + rs]);
         } else {
             rs = 0;
@@ -637,11 +634,11 @@ DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
         if (sel) {
             const uint32_t j = j0 + (r - kk);
             const uint32_t dlv = fwd ? lv + j : lv + n - 1 - j;
-            loc_add(D.loc + it, CNT_ONE);   // visible (count 1) -> deleted once
-            D.aux[dlv] = it;
+            st_sc(D.cv + it, 2u);   // visible (count 1) -> deleted once
+            *reinterpret_cast<uint32_t *>(D.ao + dlv) = it;
         }
         if (l == 0) {
-            st_sc(D.mvis + b, mv & ~selm);
+            st_sc(D.m2 + 2 * size_t(b), mv & ~selm);
             D.cnt[b] = c - take * C_VIS;
             D.top[f.tp] = ix<L>(D.top + f.tp) - take;
         }
@@ -665,29 +662,29 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
             const bool is_del = (e >> 30) & 1u, adv = (e >> 31) != 0;
             uint32_t item = lv;
             if (lv >= D.n_lv) bad = true;
-            else if (is_del) item = D.aux[lv];
+            else if (is_del) item = *reinterpret_cast<const uint32_t *>(D.ao + lv);
             if (!bad && item >= D.n_lv) bad = true;
             if (!bad) {
-                const uint32_t old = loc_add(D.loc + item, adv ? CNT_ONE : 0u - CNT_ONE);
-                const uint32_t oc = loc_cnt(old);
+                const uint32_t w = D.pos[item];
+                const uint32_t oc = cv_add(D.cv + item, adv ? 1u : 0xFFFFFFFFu);
                 const uint32_t nc = adv ? oc + 1 : oc - 1;
-                const uint32_t b = loc_blk(old);
-                if ((!adv && oc == 0) || (adv && oc == 255) || b >= D.nb) {
+                const uint32_t b = pos_blk(w);
+                if ((!adv && oc == 0) || (adv && oc >= 0x7FFFFFFFu) || b >= D.nb) {
                     bad = true;
                 } else {
-                    const u64 bit = 1ull << loc_slot(old);
+                    const u64 bit = 1ull << pos_slot(w);
                     const bool fv = (oc == 1) != (nc == 1), fl = (oc != 0) != (nc != 0);
                     if (fv || fl) {
                         const uint32_t tp = ix<L>(D.sbpos + (ix<L>(D.opos + b) >> 6));
                         uint32_t dc = 0;
                         if (fv) {
-                            at_xor(D.mvis + b, bit);
+                            at_xor(D.m2 + 2 * size_t(b), bit);
                             const uint32_t d = nc == 1 ? 1u : 0xFFFFFFFFu;
                             at_add(D.top + tp, d);
                             dc += d * C_VIS;
                         }
                         if (fl) {
-                            at_xor(D.mlive + b, bit);
+                            at_xor(D.m2 + 2 * size_t(b) + 1, bit);
                             const uint32_t d = nc != 0 ? 1u : 0xFFFFFFFFu;
                             at_add(D.tlive + tp, d);
                             dc += d * C_LIVE;
@@ -716,7 +713,7 @@ DEV void materialise(Doc &D, uint8_t *out, uint32_t cap, uint32_t &len_out, u64 
         for (uint32_t i = 0; i < n; i += G) {
             // lane g < G fetches block g's visible mask
             const uint32_t bl = l < G && i + l < n ? ix16<L>(D.sbl + size_t(S) * SBC + i + l) : 0;
-            const u64 mvl = l < G && i + l < n ? ld_sc(D.mvis + bl) : 0ull;
+            const u64 mvl = l < G && i + l < n ? ld_sc(D.m2 + 2 * size_t(bl)) : 0ull;
             uint32_t it[G], cb[G];
             bool vis[G];
 #pragma unroll
@@ -778,7 +775,7 @@ DEV uint32_t check_invariants(Doc &D, DocResult *res) {
             if (U(ix<L>(D.opos + b)) != ((S << 6) | i)) return 201;
             const uint32_t c = U(ix<L>(D.cnt + b));
             const uint32_t cnt = c_items(c);
-            const u64 mv = U64(ld_sc(D.mvis + b)), ml = U64(ld_sc(D.mlive + b));
+            const u64 mv = U64(ld_sc(D.m2 + 2 * size_t(b))), ml = U64(ld_sc(D.m2 + 2 * size_t(b) + 1));
             if (uint32_t(__popcll(mv)) != c_vis(c) || uint32_t(__popcll(ml)) != c_live(c)) return 207;
             tv += c_vis(c);
             tl += c_live(c);
@@ -788,11 +785,11 @@ DEV uint32_t check_invariants(Doc &D, DocResult *res) {
                 it = D.items[size_t(b) * BLK + l];
                 if (it >= D.n_lv) bad = true;
                 else {
-                    w = ld_sc(D.loc + it);
-                    const uint32_t k = loc_cnt(w);
+                    w = D.pos[it];
+                    const uint32_t k = ld_sc(D.cv + it);
                     if (((mv >> l) & 1) != (k == 1 ? 1u : 0u)) bad = true;
                     if (((ml >> l) & 1) != (k != 0 ? 1u : 0u)) bad = true;
-                    if (loc_blk(w) != b || loc_slot(w) != l) bad = true;
+                    if (pos_blk(w) != b || pos_slot(w) != l) bad = true;
                 }
             } else if (((mv | ml) >> l) & 1) bad = true;
             const u64 bm = __ballot(bad);
@@ -816,14 +813,13 @@ DEV uint32_t check_invariants(Doc &D, DocResult *res) {
 template <bool L, bool PROF>
 DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
     const uint32_t l = lane_id();
-    // fresh tracker: one empty block in one superblock (loc words are written when their
+    // fresh tracker: one empty block in one superblock (per-LV words are written when their
     // item is inserted)
     if (l == 0) {
         D.cnt[0] = 0; D.opos[0] = 0;
         D.sbl[0] = 0; D.sbn[0] = 1; D.sbpos[0] = 0; D.top[0] = 0; D.tlive[0] = 0;
-        st_sc(D.mvis, 0ull);
-        st_sc(D.mlive, 0ull);
     }
+    if (l < 2) st_sc(D.m2 + l, 0ull);
     wave_fence();
     D.nb = 1;
     D.nsb = 1;
@@ -950,12 +946,11 @@ __global__ __launch_bounds__(64) void replay_kernel(BatchParams P) {
     D.aruns = P.aruns + dd.arun_off;
     D.n_aruns = U(dd.n_aruns);
     D.ascii = U(dd.ascii);
-    D.loc = P.loc + dd.lv_off;
-    D.aux = P.aux + dd.lv_off;
-    D.orr = P.orr + dd.lv_off;
+    D.pos = P.pos + dd.lv_off;
+    D.cv = P.cv + dd.lv_off;
+    D.ao = P.ao + dd.lv_off;
     D.items = P.items + dd.blk_off * BLK;
-    D.mvis = P.mvis + dd.blk_off;
-    D.mlive = P.mlive + dd.blk_off;
+    D.m2 = P.m2 + 2 * dd.blk_off;
     D.max_blocks = U(dd.max_blocks);
     D.max_sb = sb_capacity(D.max_blocks);
     if (LDS_INDEX) {

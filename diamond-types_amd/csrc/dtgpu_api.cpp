@@ -59,8 +59,8 @@ struct dtgpu_batch {
     uint64_t alg_in_bytes = 0, total_lv = 0;
 
     DevBuf<Cmd> d_cmds;
-    DevBuf<uint32_t> d_tlist, d_cbyte, d_aruns, d_loc, d_aux, d_orr, d_items, d_lists, d_counter;
-    DevBuf<unsigned long long> d_mvis, d_mlive;
+    DevBuf<uint32_t> d_tlist, d_cbyte, d_aruns, d_pos, d_cv, d_items, d_lists, d_counter;
+    DevBuf<unsigned long long> d_ao, d_m2;
     DevBuf<uint8_t> d_content, d_out, d_gidx;
     DevBuf<uint32_t> d_fb;   // [0] = count, then the handed-back documents
     DevBuf<DocDesc> d_docs;
@@ -192,12 +192,11 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     std::vector<uint32_t> lists(B->small_list);
     lists.insert(lists.end(), B->large_list.begin(), B->large_list.end());
     CK(B->d_lists.upload(lists, s));
-    CK(B->d_loc.alloc(lv_total));
-    CK(B->d_aux.alloc(lv_total));
-    CK(B->d_orr.alloc(lv_total));
+    CK(B->d_pos.alloc(lv_total));
+    CK(B->d_cv.alloc(lv_total));
+    CK(B->d_ao.alloc(lv_total));
     CK(B->d_items.alloc(blk_total * 64));
-    CK(B->d_mvis.alloc(blk_total));
-    CK(B->d_mlive.alloc(blk_total));
+    CK(B->d_m2.alloc(2 * blk_total));
     CK(B->d_out.alloc(out_total));
     CK(B->d_gidx.alloc(gidx_total));
     CK(B->d_fb.alloc(B->small_list.size() + 1));
@@ -213,12 +212,11 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     base.cbyte = B->d_cbyte.p;
     base.content = B->d_content.p;
     base.aruns = B->d_aruns.p;
-    base.loc = B->d_loc.p;
-    base.aux = B->d_aux.p;
-    base.orr = B->d_orr.p;
+    base.pos = B->d_pos.p;
+    base.cv = B->d_cv.p;
+    base.ao = B->d_ao.p;
     base.items = B->d_items.p;
-    base.mvis = B->d_mvis.p;
-    base.mlive = B->d_mlive.p;
+    base.m2 = B->d_m2.p;
     base.out = B->d_out.p;
     base.gidx = B->d_gidx.p;
     base.docs = B->d_docs.p;
