@@ -71,6 +71,40 @@ __host__ __device__ inline uint64_t index_bytes(uint64_t mb) {
 }
 constexpr uint32_t MAX_DOC_BLOCKS = 65535;   // block ids are u16 in the superblock lists
 
+// ---- device planner (dt_plan.hip) -------------------------------------------------------------
+constexpr uint32_t PLAN_MAX_AGENTS = 512;
+constexpr uint32_t PLAN_MAX_LDS_ENTRIES = 16384;   // u16 todo + u16 pending per entry in LDS
+enum PlanStatus : uint32_t {
+    PLAN_OK = 0, PLAN_NOT_CHAIN = 1, PLAN_TLIST_FULL = 2, PLAN_CMDS_FULL = 3, PLAN_TOO_MANY_AGENTS = 4,
+    PLAN_ERR_INTERNAL = 5,
+};
+struct PlanDesc {       // per document; offsets index the concatenated PlanInput arrays
+    uint64_t e_off;     // entries
+    uint64_t par_off;   // par / pent
+    uint64_t child_off, op_off, arun_off, tip_off;
+    uint64_t base_off;  // vv rows scratch (n_entries * n_agents)
+    uint64_t erec_off, doff_off, dense_off;
+    uint64_t cmd_off, tlist_off;
+    uint32_t ne, n_agents, n_aruns, ntip, n_lv, ccap, tcap, skip;
+};
+struct PlanResult {
+    uint32_t status, ncmd, ntlist, n_tip;
+    uint64_t n_retreat, n_advance;
+};
+struct PlanParams {
+    const uint32_t *par, *pent, *child, *aruns, *tip, *erec, *doff, *dense;
+    const Cmd *opc;
+    uint32_t *base;
+    uint32_t lds_entries;   // per-wave LDS capacity (entries) of the todo stack / pending counts
+    uint32_t max_agents;    // largest agent count among device-planned documents
+    Cmd *cmds;
+    uint32_t *tlist;
+    const PlanDesc *docs;
+    PlanResult *results;
+    uint32_t n_docs, count_only;
+};
+int launch_plan(const PlanParams &q, void *stream);
+
 // Launch both tiers on `stream` (hipStream_t).  small/large lists index docs[].
 int launch_replay(const BatchParams &small, const BatchParams &large, void *stream, int n_cu);
 

@@ -714,6 +714,7 @@ Status build_plan(const HostOpLog &o, Plan &plan) {
         plan.agent_runs.push_back(uint32_t(r.lv));
         plan.agent_runs.push_back(rank[r.agent]);
         plan.agent_runs.push_back(uint32_t(r.seq));
+        plan.agent_runs.push_back(r.agent);
     }
 
     const auto &E = o.graph.entries;
@@ -801,6 +802,144 @@ Status build_plan(const HostOpLog &o, Plan &plan) {
     for (auto &rg : only_b) { emit_state(rg.first, rg.second, false); plan.n_tip_advance += rg.second - rg.first; }
     flush_step(t0);
     if (plan.tlist.size() >= 0xFFFFFFFFull) return ErrCapacity;
+    return OK;
+}
+
+Status build_plan_input(const HostOpLog &o, PlanInput &pi) {
+    if (o.n_lv >= MAX_PLAN_LV) return ErrCapacity;
+    if (!o.content_complete) return ErrCheckout;
+    const auto &E = o.graph.entries;
+    const size_t ne = E.size();
+    pi = PlanInput();
+    pi.n_agents = uint32_t(o.agent_names.size());
+    pi.est.reserve(2 * ne);
+    pi.poff.assign(1, 0);
+    std::vector<uint32_t> ccount(ne + 1, 0);
+    for (size_t i = 0; i < ne; i++) {
+        pi.est.push_back(uint32_t(E[i].start));
+        pi.est.push_back(uint32_t(E[i].end));
+        for (uint64_t p : E[i].parents) {
+            const int64_t pe = o.graph.find_idx(p);
+            if (pe < 0) return ErrCheckout;
+            pi.par.push_back(uint32_t(p));
+            pi.pent.push_back(uint32_t(pe));
+            ccount[size_t(pe)]++;
+        }
+        pi.poff.push_back(uint32_t(pi.par.size()));
+    }
+    pi.coff.assign(ne + 1, 0);
+    for (size_t i = 0; i < ne; i++) pi.coff[i + 1] = pi.coff[i] + ccount[i];
+    pi.child.assign(pi.coff[ne], 0);
+    {
+        std::vector<uint32_t> fill(pi.coff.begin(), pi.coff.end() - 1);
+        for (size_t i = 0; i < ne; i++)
+            for (uint32_t k = pi.poff[i]; k < pi.poff[i + 1]; k++) pi.child[fill[pi.pent[k]]++] = uint32_t(i);
+    }
+    // op runs (already split at entry boundaries by finish()) as apply commands
+    pi.eop.assign(ne + 1, 0);
+    {
+        size_t ri = 0;
+        for (size_t i = 0; i < ne; i++) {
+            while (ri < o.ops.size() && o.ops[ri].lv < E[i].start) ri++;
+            pi.eop[i] = uint32_t(ri);
+        }
+        pi.eop[ne] = uint32_t(o.ops.size());
+    }
+    for (const OpRun &r : o.ops) {
+        if (r.kind == 0) pi.opc.push_back(Cmd{CMD_INS, uint32_t(r.lv), uint32_t(r.len), uint32_t(r.pos)});
+        else pi.opc.push_back(Cmd{r.fwd ? (CMD_DEL | 16u) : uint32_t(CMD_DEL), uint32_t(r.lv), uint32_t(r.len), uint32_t(r.pos)});
+    }
+    // agent assignment, both directions
+    std::vector<uint32_t> order(o.agent_names.size()), rank(o.agent_names.size());
+    for (uint32_t i = 0; i < order.size(); i++) order[i] = i;
+    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return o.agent_names[a] < o.agent_names[b]; });
+    for (uint32_t i = 0; i < order.size(); i++) rank[order[i]] = i;
+    for (const AgentRun &r : o.agent_runs) {
+        pi.aruns.push_back(uint32_t(r.lv));
+        pi.aruns.push_back(rank[r.agent]);
+        pi.aruns.push_back(uint32_t(r.seq));
+        pi.aruns.push_back(r.agent);
+    }
+    pi.ear.assign(ne, 0);
+    {
+        size_t ai = 0;
+        const auto &R = o.agent_runs;
+        for (size_t i = 0; i < ne; i++) {
+            while (ai < R.size() && R[ai].lv + R[ai].len <= E[i].start) ai++;
+            pi.ear[i] = uint32_t(ai);
+        }
+    }
+    pi.aoff.assign(1, 0);
+    for (uint32_t a = 0; a < pi.n_agents; a++) {
+        std::vector<SeqRun> v = o.agent_seqs[a];
+        std::sort(v.begin(), v.end(), [](const SeqRun &x, const SeqRun &y) { return x.seq < y.seq; });
+        for (const SeqRun &r : v) {
+            pi.aseq.push_back(uint32_t(r.seq));
+            pi.aseq.push_back(uint32_t(r.lv));
+            pi.aseq.push_back(uint32_t(r.len));
+        }
+        pi.aoff.push_back(uint32_t(pi.aseq.size() / 3));
+    }
+    pi.isdel.assign((o.n_lv + 31) / 32, 0);
+    for (const OpRun &r : o.ops)
+        if (r.kind)
+            for (uint64_t v = r.lv; v < r.lv + r.len; v++) pi.isdel[v >> 5] |= 1u << (v & 31);
+    for (uint64_t t : o.version) {
+        const int64_t te = o.graph.find_idx(t);
+        if (te < 0) return ErrCheckout;
+        pi.tip.push_back(uint32_t(t));
+        pi.tip.push_back(uint32_t(te));
+    }
+    // Chain decomposition of the graph: every entry joins the chain whose current tail entry
+    // ends at one of its parents (the first such parent), or opens a new chain.  Each chain is
+    // then a causal chain, so a version's ancestor set is a prefix of every chain and a version
+    // vector over chains describes it exactly (the device planner diffs those vectors).
+    std::vector<uint32_t> chain_of(ne), seq0(ne);
+    std::vector<uint32_t> tail;           // per chain: its last entry
+    std::vector<uint64_t> clen;           // per chain: ops so far
+    for (size_t i = 0; i < ne; i++) {
+        uint32_t c = 0xFFFFFFFFu;
+        for (uint32_t k = pi.poff[i]; k < pi.poff[i + 1] && c == 0xFFFFFFFFu; k++) {
+            const uint32_t pe = pi.pent[k];
+            const uint32_t pc = chain_of[pe];
+            if (pi.par[k] + 1 == E[pe].end && tail[pc] == pe) c = pc;
+        }
+        if (c == 0xFFFFFFFFu) {
+            c = uint32_t(tail.size());
+            tail.push_back(0);
+            clen.push_back(0);
+        }
+        chain_of[i] = c;
+        seq0[i] = uint32_t(clen[c]);
+        clen[c] += E[i].end - E[i].start;
+        tail[c] = uint32_t(i);
+    }
+    pi.n_chains = uint32_t(tail.size());
+    // entry records
+    pi.erec.assign(ne * EREC_WORDS, 0);
+    for (size_t i = 0; i < ne; i++) {
+        uint32_t *r = &pi.erec[i * EREC_WORDS];
+        r[0] = uint32_t(E[i].start);
+        r[1] = uint32_t(E[i].end);
+        r[2] = pi.poff[i];
+        r[3] = pi.poff[i + 1] - pi.poff[i];
+        r[4] = pi.eop[i];
+        r[5] = pi.eop[i + 1] - pi.eop[i];
+        r[6] = chain_of[i];
+        r[7] = seq0[i];
+        r[8] = pi.coff[i];
+        r[9] = pi.coff[i + 1] - pi.coff[i];
+        r[10] = r[3] ? pi.par[pi.poff[i]] : 0xFFFFFFFFu;
+        r[11] = r[3] ? pi.pent[pi.poff[i]] : 0xFFFFFFFFu;
+    }
+    // dense chain seq -> LV | is_del tables (the planner copies retreat/advance ranges out)
+    pi.doff.assign(pi.n_chains + 1, 0);
+    for (uint32_t c = 0; c < pi.n_chains; c++) pi.doff[c + 1] = pi.doff[c] + uint32_t(clen[c]);
+    pi.dense.assign(o.n_lv, 0);
+    for (size_t i = 0; i < ne; i++)
+        for (uint64_t lv = E[i].start; lv < E[i].end; lv++)
+            pi.dense[pi.doff[chain_of[i]] + seq0[i] + (lv - E[i].start)] =
+                uint32_t(lv) | (((pi.isdel[lv >> 5] >> (lv & 31)) & 1u) ? TL_DEL : 0u);
     return OK;
 }
 

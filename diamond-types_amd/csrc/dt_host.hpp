@@ -89,13 +89,43 @@ constexpr uint64_t MAX_PLAN_LV = 1ull << 30;
 struct Plan {
     std::vector<Cmd> cmds;
     std::vector<uint32_t> tlist;
-    std::vector<uint32_t> agent_runs;   // triples (lv_start, name_rank, seq_start) for YjsMod tie-breaks
+    std::vector<uint32_t> agent_runs;   // quads (lv_start, name_rank, seq_start, agent) for YjsMod tie-breaks
     uint64_t n_steps = 0, n_retreat = 0, n_advance = 0, n_tip_advance = 0;
 };
 
 // SpanningTreeWalker over the whole graph from ROOT (src/listmerge/txn_trace.rs:114-333) turned
 // into the device command stream (retreat / advance / apply, src/listmerge/merge.rs:564-581).
 Status build_plan(const HostOpLog &o, Plan &plan);
+
+// The decoded oplog as flat arrays for the device planner (dt_plan.hip): the same information
+// the reference's ListOpLog holds (Graph entries with parents and child indexes, the agent
+// assignment in both directions, op runs), laid out for coalesced loads.
+struct PlanInput {
+    uint32_t n_agents = 0;
+    std::vector<uint32_t> est;      // per entry: start, end
+    std::vector<uint32_t> poff;     // parents CSR (n_entries + 1)
+    std::vector<uint32_t> par;      // parent LV
+    std::vector<uint32_t> pent;     // entry index of that parent
+    std::vector<uint32_t> coff;     // children CSR (n_entries + 1), children in index order
+    std::vector<uint32_t> child;
+    std::vector<uint32_t> eop;      // first op run of each entry (n_entries + 1)
+    std::vector<uint32_t> ear;      // first agent run overlapping each entry
+    std::vector<Cmd> opc;           // op runs as INS / DEL commands (runs never cross entries)
+    std::vector<uint32_t> aruns;    // quads (lv_start, name_rank, seq_start, agent), LV order
+    std::vector<uint32_t> aoff;     // per agent: offset into aseq (n_agents + 1)
+    std::vector<uint32_t> aseq;     // triples (seq, lv, len) sorted by seq within each agent
+    std::vector<uint32_t> isdel;    // bit per LV: 1 = delete op
+    std::vector<uint32_t> tip;      // pairs (LV, entry) of cg.version
+    // per entry, 12 words: start, end, parents offset, parent count, first op run, op runs,
+    // chain, first seq in the chain, children offset, child count, first parent LV / entry
+    std::vector<uint32_t> erec;
+    uint32_t n_chains = 0;          // causal chains the entries are partitioned into
+    std::vector<uint32_t> doff;     // per chain: offset of its dense seq table (n_chains + 1)
+    std::vector<uint32_t> dense;    // per chain, by seq: LV | is_del << 30
+    bool device_ok = true;
+};
+constexpr uint32_t EREC_WORDS = 12;
+Status build_plan_input(const HostOpLog &o, PlanInput &pi);
 
 uint64_t text_hash(const uint8_t *t, size_t n);
 

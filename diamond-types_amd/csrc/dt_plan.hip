@@ -1,0 +1,413 @@
+// dt_plan.hip -- device walk planner: the decoded oplog of each document -> the replay command
+// stream (INS / DEL / TOG commands + retreat/advance entries) consumed by dt_replay.hip.
+//
+// One wavefront plans one document, walking the causal graph in the reference's spanning-tree
+// order (SpanningTreeWalker, src/listmerge/txn_trace.rs:114-333): a todo stack seeded with the
+// root entries; merge entries (>= 2 parents) wait while a non-merge entry is ready
+// (txn_trace.rs:249-266); an entry becomes ready when its last parent entry is consumed.
+//
+// Between two consumed entries the tracker moves from the previous entry's last LV to the next
+// entry's parents: retreat (ancestors of the old frontier not in the new one) then advance
+// (the converse) -- Graph::diff_rev (src/causalgraph/graph/tools.rs:176-292).  The planner gets
+// those sets from version vectors over causal chains: the host partitions the graph entries
+// into chains (each entry extends the chain whose tail is one of its parents, dt_host.cpp
+// build_plan_input), so the ancestor set of a version is a prefix of every chain,
+// { (chain, seq) : seq < vv[chain] }, and a diff is one seq range per chain, copied out of a
+// dense per-chain seq -> LV table.  (Diamond-types' agents are not chains in general: a git
+// import has one author committing on concurrent branches.)
+//
+// vv rows (one per entry: the version vector of the entry's parents) live in HBM scratch;
+// lane l keeps chains l, l + 64, ... of the current vector (K chunks: K = 1 up to 64 chains,
+// K = 8 up to 512).  The todo stack and the pending-parent counts live in LDS.  Per consumed
+// entry the wave issues one record load (as soon as the entry is picked, overlapping the
+// previous entry's emission), one batch of independent loads (its op runs and children) and,
+// when the frontier moves sideways, one gather per 64 retreat/advance entries.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dt_device.hpp"
+
+namespace dtgpu {
+namespace pdev {
+
+typedef unsigned long long u64;
+#define DEV __device__ __forceinline__
+
+DEV uint32_t lane_id() { return __lane_id(); }
+DEV uint32_t U(uint32_t v) { return uint32_t(__builtin_amdgcn_readfirstlane(int(v))); }
+DEV uint32_t bcast(uint32_t v, uint32_t l) { return uint32_t(__builtin_amdgcn_readlane(int(v), int(l))); }
+DEV uint32_t first_lane(u64 m) { return uint32_t(__ffsll((long long)m) - 1); }
+DEV void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); __builtin_amdgcn_wave_barrier(); }
+DEV uint32_t wave_scan(uint32_t x) {   // inclusive prefix sum (same DPP sequence as dt_replay.hip)
+    x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x111, 0xF, 0xF, false));
+    x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x112, 0xF, 0xF, false));
+    x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x114, 0xF, 0xF, false));
+    x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x118, 0xF, 0xF, false));
+    x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x142, 0xA, 0xF, false));
+    x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x143, 0xC, 0xF, false));
+    return x;
+}
+
+struct P {
+    // inputs (decoded oplog)
+    const uint32_t *erec, *par, *pent, *child, *doff, *dense, *tip;
+    const Cmd *opc;
+    uint32_t ne, A, ntip, n_lv;
+    // scratch: vv rows in HBM; todo stack and pending parent counts in LDS (u16)
+    uint32_t *base;
+    uint16_t *todo, *pending;
+    // outputs
+    Cmd *cmds;
+    uint32_t *tlist;
+    uint32_t ccap, tcap;
+    uint32_t count_only;   // sizing pass: count commands and entries, write nothing
+    // wave-uniform state
+    uint32_t nc, nt, err;
+    uint64_t steps, limit;
+    uint64_t n_ret, n_adv;
+};
+
+DEV void fail(P &p, uint32_t code) {
+    if (!p.err) p.err = code;
+}
+DEV bool charge(P &p) {
+    if (++p.steps > p.limit) { fail(p, PLAN_ERR_INTERNAL); return false; }
+    return true;
+}
+
+// Entry record (EREC_WORDS words) lane by lane; R(rw, k) reads word k.
+enum { R_START = 0, R_END, R_POFF, R_NP, R_OP0, R_NOP, R_CHAIN, R_SEQ0, R_CH0, R_NCH, R_PAR0, R_PENT0 };
+DEV uint32_t load_rec(const P &p, uint32_t e) {
+    const uint32_t l = lane_id();
+    return l < EREC_WORDS ? p.erec[size_t(e) * EREC_WORDS + l] : 0;
+}
+DEV uint32_t R(uint32_t rw, int k) { return U(bcast(rw, uint32_t(k))); }
+
+template <int K> struct VV { uint32_t v[K]; };
+
+template <int K> DEV void vv_zero(VV<K> &x) {
+#pragma unroll
+    for (int k = 0; k < K; k++) x.v[k] = 0;
+}
+template <int K> DEV void vv_max(VV<K> &x, const VV<K> &y) {
+#pragma unroll
+    for (int k = 0; k < K; k++) x.v[k] = max(x.v[k], y.v[k]);
+}
+template <int K> DEV bool vv_differ(const VV<K> &x, const VV<K> &y) {
+    bool d = false;
+#pragma unroll
+    for (int k = 0; k < K; k++) d |= x.v[k] != y.v[k];
+    return __ballot(d) != 0;
+}
+template <int K> DEV void load_row(const P &p, uint32_t e, VV<K> &row) {
+    const uint32_t l = lane_id();
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const uint32_t a = l + 64 * k;
+        row.v[k] = a < p.A ? p.base[size_t(e) * p.A + a] : 0;
+    }
+}
+template <int K> DEV void store_row(P &p, uint32_t e, const VV<K> &row) {
+    const uint32_t l = lane_id();
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const uint32_t a = l + 64 * k;
+        if (a < p.A) p.base[size_t(e) * p.A + a] = row.v[k];
+    }
+}
+
+// The frontier moves along entry e (chain c, first seq s0) up to LV `upto`: row[c] becomes
+// s0 + the entry's LVs so far.  check: the chain must continue exactly where row[c] stands
+// (the chain decomposition guarantees it; a mismatch means a corrupt plan input).
+template <int K>
+DEV void fold_entry(P &p, uint32_t start, uint32_t end, uint32_t upto, uint32_t c, uint32_t s0, VV<K> &row,
+                    bool check) {
+    const uint32_t l = lane_id();
+    const uint32_t hi = min(end, upto + 1);
+    if (c >= p.A || hi <= start) { fail(p, PLAN_ERR_INTERNAL); return; }
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        if (c == l + 64 * k) {
+            if (check && row.v[k] != s0) bad = true;
+            row.v[k] = check ? s0 + (hi - start) : max(row.v[k], s0 + (hi - start));
+        }
+    }
+    if (__ballot(bad)) fail(p, PLAN_NOT_CHAIN);
+}
+
+// Version vector of the version {lv} (lv inside entry e): the entry's parent vector plus the
+// entry's own LVs up to lv.
+template <int K> DEV void vv_at(P &p, uint32_t lv, uint32_t e, VV<K> &row) {
+    const uint32_t rw = load_rec(p, e);
+    load_row(p, e, row);
+    fold_entry<K>(p, R(rw, R_START), R(rw, R_END), lv, R(rw, R_CHAIN), R(rw, R_SEQ0), row, false);
+}
+
+// Emit the retreat (from has more) / advance (to has more) entries of a diff: per agent one
+// seq range of its dense seq -> (LV | is_del) table.  The ranges of one 64-agent chunk are
+// gathered together, 64 entries per load.
+template <int K>
+DEV void emit_diff(P &p, const VV<K> &from, const VV<K> &to, bool allow_retreat) {
+    const uint32_t l = lane_id();
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const uint32_t a = l + 64 * k;
+        const bool act = a < p.A && from.v[k] != to.v[k];
+        const u64 am = __ballot(act);
+        if (!am) continue;
+        if (__ballot(act && to.v[k] < from.v[k] && !allow_retreat)) { fail(p, PLAN_ERR_INTERNAL); return; }
+        const bool adv = to.v[k] > from.v[k];
+        const uint32_t s0 = adv ? from.v[k] : to.v[k];
+        const uint32_t n = act ? (adv ? to.v[k] - from.v[k] : from.v[k] - to.v[k]) : 0;
+        uint32_t d0 = 0, d1 = 0;
+        if (act) { d0 = p.doff[a]; d1 = p.doff[a + 1]; }
+        if (__ballot(act && d0 + s0 + n > d1)) { fail(p, PLAN_ERR_INTERNAL); return; }
+        const uint32_t inc = wave_scan(n);
+        const uint32_t total = bcast(inc, 63);
+        const uint32_t n_adv = bcast(wave_scan(adv ? n : 0), 63);
+        if (uint64_t(p.nt) + total > p.tcap) { fail(p, PLAN_TLIST_FULL); return; }
+        if (!p.count_only) {
+            const uint32_t src = d0 + s0, off = inc - n;   // per agent lane
+            bool bad = false;
+            for (uint32_t c = 0; c < total; c += 64) {
+                const uint32_t u = c + l;
+                uint32_t from_idx = 0, flag = 0;
+                for (u64 m = am; m; m &= m - 1) {   // the agent whose output slice holds u
+                    const uint32_t j = first_lane(m);
+                    const uint32_t o = U(bcast(off, j)), nn = U(bcast(n, j));
+                    const uint32_t sj = U(bcast(src, j)), fj = U(bcast(adv ? TL_ADV : 0u, j));
+                    if (u >= o && u < o + nn) { from_idx = sj + (u - o); flag = fj; }
+                }
+                if (u < total) {
+                    const uint32_t v = p.dense[from_idx];
+                    if (v == 0xFFFFFFFFu) bad = true;
+                    p.tlist[p.nt + u] = v | flag;
+                }
+            }
+            if (__ballot(bad)) { fail(p, PLAN_ERR_INTERNAL); return; }
+        }
+        p.nt += total;
+        p.n_adv += n_adv;
+        p.n_ret += total - n_adv;
+    }
+}
+
+DEV void push_cmd(P &p, uint32_t op, uint32_t a, uint32_t n, uint32_t pos) {
+    if (uint64_t(p.nc) >= p.ccap) { fail(p, PLAN_CMDS_FULL); return; }
+    if (lane_id() == 0 && !p.count_only) p.cmds[p.nc] = Cmd{op, a, n, pos};
+    p.nc++;
+}
+
+constexpr uint16_t MERGE_BIT = 0x8000;   // pending word: parent count | merge flag
+
+// Next entry to consume: the todo top, unless it is a merge and a non-merge is ready
+// (txn_trace.rs:249-266).  Pops it.
+DEV uint32_t pick(P &p, uint32_t &top) {
+    const uint32_t l = lane_id();
+    uint32_t idx = U(p.todo[top - 1]);
+    if (p.pending[idx] & MERGE_BIT) {
+        int found = -1;
+        for (int hi = int(top) - 1; hi >= 0 && found < 0; hi -= 64) {
+            const int i = hi - int(l);
+            const bool ok = i >= 0 && !(p.pending[p.todo[i]] & MERGE_BIT);
+            const u64 m = __ballot(ok);
+            if (m) found = hi - int(first_lane(m));
+        }
+        if (found >= 0) {
+            idx = U(p.todo[found]);
+            if (l == 0) p.todo[found] = p.todo[top - 1];
+            wave_fence();
+        }
+    }
+    top--;
+    return idx;
+}
+
+template <int K>
+DEV void plan_doc(P &p, PlanResult *res) {
+    const uint32_t l = lane_id();
+    VV<K> vf, vp;
+    vv_zero(vf);
+    // pending parent counts (+ merge flag); the todo stack holds the roots, first root on top
+    uint32_t top = 0;
+    for (uint32_t c = 0; c < p.ne; c += 64) {
+        const uint32_t e = c + l;
+        if (e < p.ne) {
+            const uint32_t np = p.erec[size_t(e) * EREC_WORDS + R_NP];
+            p.pending[e] = uint16_t(min(np, 0x7FFFu) | (np >= 2 ? MERGE_BIT : 0));
+        }
+    }
+    for (int c = int((p.ne + 63) / 64) - 1; c >= 0; c--) {
+        if (!charge(p)) break;
+        const uint32_t e = uint32_t(c) * 64 + (63 - l);   // descending entry index across lanes
+        const bool root = e < p.ne && p.erec[size_t(e) * EREC_WORDS + R_NP] == 0;
+        const u64 m = __ballot(root);
+        const uint32_t rank = uint32_t(__popcll(m & ((1ull << l) - 1ull)));
+        if (root) p.todo[top + rank] = uint16_t(e);
+        top += uint32_t(__popcll(m));
+    }
+    wave_fence();
+    uint32_t f = 0xFFFFFFFFu;   // current frontier: ROOT or one LV
+    bool have = top > 0;
+    uint32_t idx = have ? pick(p, top) : 0;
+    uint32_t rw = have ? load_rec(p, idx) : 0;
+    while (have && !p.err) {
+        if (!charge(p)) break;
+        // the entry's op runs, agent runs and children: independent loads, issued together
+        const uint32_t np = R(rw, R_NP), op0 = R(rw, R_OP0), nop = R(rw, R_NOP), ch0 = R(rw, R_CH0),
+                       nch = R(rw, R_NCH), chain = R(rw, R_CHAIN), seq0 = R(rw, R_SEQ0);
+        const uint32_t e_start = R(rw, R_START), e_end = R(rw, R_END);
+        // (four scalars, not a Cmd: a struct assigned under a branch goes through scratch)
+        const uint32_t *opw = reinterpret_cast<const uint32_t *>(p.opc);
+        uint32_t oc0 = 0, oc1 = 0, oc2 = 0, oc3 = 0;
+        if (l < nop && !p.count_only) {
+            const size_t w = 4 * size_t(op0 + l);
+            oc0 = opw[w]; oc1 = opw[w + 1]; oc2 = opw[w + 2]; oc3 = opw[w + 3];
+        }
+        const uint32_t ch = l < nch ? p.child[ch0 + l] : 0;
+        // version vector of the parents
+        if (np == 1 && R(rw, R_PAR0) == f) {
+            vp = vf;
+        } else {
+            vv_zero(vp);
+            const uint32_t po = R(rw, R_POFF);
+            for (uint32_t j = 0; j < np; j++) {
+                VV<K> t;
+                vv_at<K>(p, j == 0 ? R(rw, R_PAR0) : U(p.par[po + j]), j == 0 ? R(rw, R_PENT0) : U(p.pent[po + j]), t);
+                vv_max(vp, t);
+            }
+        }
+        store_row(p, idx, vp);
+        const VV<K> v_old = vf;
+        // the frontier moves to the entry's last LV; its runs must continue the agents' chains
+        vf = vp;
+        fold_entry<K>(p, e_start, e_end, e_end - 1, chain, seq0, vf, true);
+        if (p.err) break;
+        // children whose last parent this was become ready (pushed in child index order); the
+        // next entry is picked and its record requested before this entry's output is written
+        for (uint32_t c = 0; c < nch; c += 64) {
+            const uint32_t chv = c == 0 ? ch : (c + l < nch ? p.child[ch0 + c + l] : 0);
+            bool ready = false;
+            if (c + l < nch) {
+                const uint16_t pd = uint16_t(p.pending[chv] - 1);
+                p.pending[chv] = pd;
+                ready = (pd & 0x7FFF) == 0;
+            }
+            const u64 m = __ballot(ready);
+            const uint32_t rank = uint32_t(__popcll(m & ((1ull << l) - 1ull)));
+            if (ready) p.todo[top + rank] = uint16_t(chv);
+            top += uint32_t(__popcll(m));
+        }
+        wave_fence();
+        have = top > 0;
+        if (have) {
+            idx = pick(p, top);
+            rw = load_rec(p, idx);
+        }
+        // retreat / advance to the parents, then apply the entry's op runs
+        if (vv_differ(v_old, vp)) {
+            const uint32_t t0 = p.nt;
+            emit_diff<K>(p, v_old, vp, true);
+            if (p.err) break;
+            if (p.nt > t0) push_cmd(p, CMD_TOG, t0, p.nt - t0, 0);
+        }
+        if (uint64_t(p.nc) + nop > p.ccap) { fail(p, PLAN_CMDS_FULL); break; }
+        if (!p.count_only) {
+            if (l < nop) {
+                uint32_t *cw = reinterpret_cast<uint32_t *>(p.cmds) + 4 * size_t(p.nc + l);
+                cw[0] = oc0; cw[1] = oc1; cw[2] = oc2; cw[3] = oc3;
+            }
+            for (uint32_t j = 64 + l; j < nop; j += 64) p.cmds[p.nc + j] = p.opc[op0 + j];
+        }
+        p.nc += nop;
+        f = e_end - 1;
+    }
+    // advance to the tip (cg.version): the replay then holds the checkout
+    if (!p.err) {
+        VV<K> vt;
+        vv_zero(vt);
+        for (uint32_t j = 0; j < p.ntip; j++) {
+            VV<K> t;
+            vv_at<K>(p, U(p.tip[2 * j]), U(p.tip[2 * j + 1]), t);
+            vv_max(vt, t);
+        }
+        if (!p.err && vv_differ(vf, vt)) {
+            const uint32_t t0 = p.nt;
+            const uint64_t adv0 = p.n_adv;
+            emit_diff<K>(p, vf, vt, false);
+            if (!p.err && p.nt > t0) push_cmd(p, CMD_TOG, t0, p.nt - t0, 0);
+            res->n_tip = uint32_t(p.n_adv - adv0);
+            p.n_adv = adv0;
+        }
+    }
+    if (l == 0) {
+        res->status = p.err;
+        res->ncmd = p.nc;
+        res->ntlist = p.nt;
+        res->n_retreat = p.n_ret;
+        res->n_advance = p.n_adv;
+    }
+}
+
+// K = agent chunks per lane.  Documents with <= 64 agents run in the K = 1 instantiation, the
+// others (<= PLAN_MAX_AGENTS) in the wide one; each kernel skips the other's documents.
+template <int K>
+__global__ __launch_bounds__(64) void plan_kernel(PlanParams Q) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t lds16[];
+    const uint32_t d = U(blockIdx.x);
+    if (d >= Q.n_docs) return;
+    const PlanDesc pd = Q.docs[d];
+    PlanResult *res = Q.results + d;
+    if (pd.skip) return;   // planned on the host
+    const uint32_t A = U(pd.n_agents);
+    if (K == 1 ? A > 64 : A <= 64) return;
+    P p;
+    p.erec = Q.erec + pd.erec_off;
+    p.par = Q.par + pd.par_off;
+    p.pent = Q.pent + pd.par_off;
+    p.child = Q.child + pd.child_off;
+    p.opc = Q.opc + pd.op_off;
+    p.doff = Q.doff + pd.doff_off;
+    p.dense = Q.dense + pd.dense_off;
+    p.tip = Q.tip + pd.tip_off * 2;
+    p.ne = U(pd.ne);
+    p.A = A;
+    p.ntip = U(pd.ntip);
+    p.n_lv = U(pd.n_lv);
+    p.todo = lds16;
+    p.pending = lds16 + Q.lds_entries;
+    p.base = Q.base + pd.base_off;
+    p.cmds = Q.cmds + pd.cmd_off;
+    p.tlist = Q.tlist + pd.tlist_off;
+    p.count_only = Q.count_only;
+    p.ccap = Q.count_only ? 0xFFFFFFFFu : U(pd.ccap);
+    p.tcap = Q.count_only ? 0xFFFFFFFFu : U(pd.tcap);
+    p.nc = p.nt = p.err = 0;
+    p.steps = 0;
+    p.limit = 1024ull * (uint64_t(p.ne) + 16) + 4ull * pd.n_lv + (1u << 20);
+    p.n_ret = p.n_adv = 0;
+    res->n_tip = 0;
+    if (p.ne > Q.lds_entries) {
+        if (lane_id() == 0) res->status = PLAN_ERR_INTERNAL;
+        return;
+    }
+    plan_doc<K>(p, res);
+}
+
+}  // namespace pdev
+
+int launch_plan(const PlanParams &q, void *stream) {
+    if (!q.n_docs) return OK;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const size_t lds = size_t(q.lds_entries) * 4;   // u16 todo + u16 pending per entry
+    hipLaunchKernelGGL(pdev::plan_kernel<1>, dim3(q.n_docs), dim3(64), lds, s, q);
+    if (hipGetLastError() != hipSuccess) return ErrHip;
+    if (q.max_agents > 64) {
+        hipLaunchKernelGGL(pdev::plan_kernel<PLAN_MAX_AGENTS / 64>, dim3(q.n_docs), dim3(64), lds, s, q);
+        if (hipGetLastError() != hipSuccess) return ErrHip;
+    }
+    return OK;
+}
+
+}  // namespace dtgpu

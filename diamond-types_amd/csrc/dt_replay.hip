@@ -446,17 +446,17 @@ DEV void agent_of(Doc &D, uint32_t lv, uint32_t &rank, uint32_t &seq) {
         if (!charge(D)) { rank = seq = 0; return; }
         const uint32_t stride = (n + 63) / 64;
         const uint32_t idx = lo + l * stride;
-        const bool ok = l * stride < n && D.aruns[3 * idx] <= lv;
+        const bool ok = l * stride < n && D.aruns[4 * idx] <= lv;
         const uint32_t k = uint32_t(__popcll(__ballot(ok)));
         const uint32_t nlo = lo + (k ? k - 1 : 0) * stride;
         n = min(stride, lo + n - nlo);
         lo = nlo;
     }
-    const bool ok = l < n && D.aruns[3 * (lo + l)] <= lv;
+    const bool ok = l < n && D.aruns[4 * (lo + l)] <= lv;
     const uint32_t k = uint32_t(__popcll(__ballot(ok)));
     const uint32_t j = U(lo + (k ? k - 1 : 0));
-    rank = U(D.aruns[3 * j + 1]);
-    seq = U(D.aruns[3 * j + 2]) + (lv - U(D.aruns[3 * j]));
+    rank = U(D.aruns[4 * j + 1]);
+    seq = U(D.aruns[4 * j + 2]) + (lv - U(D.aruns[4 * j]));
 }
 
 // YjsMod integrate (merge.rs:154-278) over the not-inserted-yet items between the cursor

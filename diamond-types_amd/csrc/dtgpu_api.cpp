@@ -49,14 +49,25 @@ struct dtgpu_batch {
     int device = 0;
     int n_cu = 256;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev0 = nullptr, ev_mid = nullptr, ev1 = nullptr;
     size_t n = 0;
     std::vector<uint32_t> host_status;   // decode / plan status per doc
     std::vector<uint64_t> n_lv;
     std::vector<DocDesc> docs;
     std::vector<uint32_t> small_list, large_list;
+    std::vector<uint8_t> host_planned;   // 0: device-planned; else why the host planned it
     uint32_t lds_blocks = 0;
     uint64_t alg_in_bytes = 0, total_lv = 0;
+    float last_plan_ms = 0, last_replay_ms = 0;
+
+    // device planner inputs (the decoded oplogs) and scratch
+    DevBuf<uint32_t> p_par, p_pent, p_child, p_tip, p_erec, p_doff, p_dense;
+    DevBuf<Cmd> p_opc;
+    DevBuf<uint32_t> p_base;
+    DevBuf<PlanDesc> p_docs;
+    DevBuf<PlanResult> p_results;
+    PlanParams plan{};
+    uint32_t n_gpu_planned = 0;
 
     DevBuf<Cmd> d_cmds;
     DevBuf<uint32_t> d_tlist, d_cbyte, d_aruns, d_pos, d_cv, d_items, d_lists, d_counter;
@@ -69,6 +80,7 @@ struct dtgpu_batch {
 
     ~dtgpu_batch() {
         if (ev0) (void)hipEventDestroy(ev0);
+        if (ev_mid) (void)hipEventDestroy(ev_mid);
         if (ev1) (void)hipEventDestroy(ev1);
         if (stream) (void)hipStreamDestroy(stream);
     }
@@ -79,13 +91,19 @@ namespace {
 struct Prepared {
     Status status = OK;
     HostOpLog log;
-    Plan plan;
+    PlanInput pi;
+    Plan plan;             // host plan: only for documents the device planner declines
+    bool host_plan = false;
 };
 
 void prepare_from_oplog(const HostOpLog &src, Prepared &p) {
     p.log = src;
     p.log.finish();
     p.status = build_plan(p.log, p.plan);
+}
+// Decoded oplog -> device planner input (the walk itself runs on the GPU).
+void prepare_input(Prepared &p) {
+    if (p.status == OK) p.status = build_plan_input(p.log, p.pi);
 }
 
 int threads_for(const dtgpu_batch_opts *opts, size_t n) {
@@ -104,6 +122,9 @@ void parallel_for(size_t n, int threads, F f) {
     for (auto &th : pool) th.join();
 }
 
+template <typename T>
+void append(std::vector<T> &dst, const std::vector<T> &src) { dst.insert(dst.end(), src.begin(), src.end()); }
+
 dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dtgpu_batch **out) {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return DTGPU_ERR_NO_DEVICE;
@@ -114,16 +135,101 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     if (hipGetDeviceProperties(&prop, B->device) == hipSuccess && prop.multiProcessorCount > 0)
         B->n_cu = prop.multiProcessorCount;
     if (hipStreamCreateWithFlags(&B->stream, hipStreamNonBlocking) != hipSuccess) return DTGPU_ERR_HIP;
-    if (hipEventCreate(&B->ev0) != hipSuccess || hipEventCreate(&B->ev1) != hipSuccess) return DTGPU_ERR_HIP;
-
+    if (hipEventCreate(&B->ev0) != hipSuccess || hipEventCreate(&B->ev_mid) != hipSuccess ||
+        hipEventCreate(&B->ev1) != hipSuccess)
+        return DTGPU_ERR_HIP;
+    hipStream_t s = B->stream;
+#define CK(x) do { if ((x) != hipSuccess) return DTGPU_ERR_HIP; } while (0)
     const size_t n = prep.size();
+    const int threads = threads_for(opts, n);
     B->n = n;
     B->host_status.resize(n);
     B->n_lv.resize(n);
     B->docs.resize(n);
-    std::vector<Cmd> cmds;
-    std::vector<uint32_t> tlist, cbyte, aruns;
+    B->host_planned.assign(n, 0);
+    const bool force_host = getenv("DTGPU_HOST_PLAN") != nullptr;
+
+    // ---- 1. device planner inputs; a sizing pass of the planner gives exact stream sizes ----
+    std::vector<PlanDesc> pdesc(n);
+    {
+        std::vector<uint32_t> par, pent, child, tip, aruns, erec, doff, dense;
+        std::vector<Cmd> opc;
+        uint64_t base_total = 0, n_entries = 0;
+        uint32_t lds_entries = 0, max_agents = 0;
+        for (size_t i = 0; i < n; i++) {
+            Prepared &p = prep[i];
+            PlanDesc &q = pdesc[i];
+            std::memset(&q, 0, sizeof q);
+            q.skip = 1;
+            if (p.status != OK) continue;
+            const PlanInput &pi = p.pi;
+            const uint64_t ne = pi.est.size() / 2;
+            const bool host = force_host || !pi.device_ok || pi.n_chains > PLAN_MAX_AGENTS ||
+                              ne > PLAN_MAX_LDS_ENTRIES || ne * std::max<uint32_t>(pi.n_chains, 1) > (64ull << 20);
+            if (host) p.host_plan = true;
+            q.skip = host ? 1 : 0;
+            q.e_off = n_entries;
+            q.par_off = par.size();
+            q.child_off = child.size();
+            q.op_off = opc.size();
+            q.arun_off = aruns.size() / 4;
+            q.tip_off = tip.size() / 2;
+            q.erec_off = erec.size();
+            q.doff_off = doff.size();
+            q.dense_off = dense.size();
+            q.base_off = base_total;
+            q.ne = uint32_t(ne);
+            q.n_agents = pi.n_chains;
+            q.n_aruns = uint32_t(pi.aruns.size() / 4);
+            q.ntip = uint32_t(pi.tip.size() / 2);
+            q.n_lv = uint32_t(p.log.n_lv);
+            append(aruns, pi.aruns);   // also the replay's tie-break runs
+            if (host) continue;
+            append(par, pi.par); append(pent, pi.pent); append(child, pi.child); append(opc, pi.opc);
+            append(tip, pi.tip); append(erec, pi.erec); append(doff, pi.doff); append(dense, pi.dense);
+            base_total += ne * pi.n_chains;
+            n_entries += ne;
+            lds_entries = std::max<uint32_t>(lds_entries, uint32_t(ne));
+            max_agents = std::max<uint32_t>(max_agents, pi.n_chains);
+        }
+        CK(B->p_par.upload(par, s)); CK(B->p_pent.upload(pent, s)); CK(B->p_child.upload(child, s));
+        CK(B->p_opc.upload(opc, s)); CK(B->d_aruns.upload(aruns, s)); CK(B->p_tip.upload(tip, s));
+        CK(B->p_erec.upload(erec, s)); CK(B->p_doff.upload(doff, s)); CK(B->p_dense.upload(dense, s));
+        CK(B->p_base.alloc(base_total));
+        CK(B->p_docs.upload(pdesc, s));
+        CK(B->p_results.alloc(n));
+        CK(hipMemsetAsync(B->p_results.p, 0, std::max<size_t>(n, 1) * sizeof(PlanResult), s));
+        PlanParams &q = B->plan;
+        q.par = B->p_par.p; q.pent = B->p_pent.p; q.child = B->p_child.p; q.opc = B->p_opc.p;
+        q.aruns = B->d_aruns.p; q.tip = B->p_tip.p; q.erec = B->p_erec.p; q.doff = B->p_doff.p;
+        q.dense = B->p_dense.p; q.base = B->p_base.p;
+        q.lds_entries = (lds_entries + 7) & ~7u;
+        q.max_agents = max_agents;
+        q.docs = B->p_docs.p; q.results = B->p_results.p; q.n_docs = uint32_t(n);
+        q.count_only = 1;
+        if (launch_plan(q, s) != OK) return DTGPU_ERR_HIP;
+        q.count_only = 0;
+    }
+    std::vector<PlanResult> pres(n);
+    CK(hipMemcpyAsync(pres.data(), B->p_results.p, std::max<size_t>(n, 1) * sizeof(PlanResult), hipMemcpyDeviceToHost, s));
+    CK(hipStreamSynchronize(s));
+    // documents the device planner declined are planned on the host
+    std::vector<uint8_t> reason(n, 0);
+    for (size_t i = 0; i < n; i++) {
+        if (prep[i].status != OK) continue;
+        if (pdesc[i].skip) reason[i] = force_host ? 1 : 2;
+        else if (pres[i].status != PLAN_OK) { prep[i].host_plan = true; reason[i] = uint8_t(16 + pres[i].status); }
+    }
+    parallel_for(n, threads, [&](size_t i) {
+        Prepared &p = prep[i];
+        if (p.status == OK && p.host_plan) p.status = build_plan(p.log, p.plan);
+    });
+
+    // ---- 2. per-document layout ---------------------------------------------------------------
+    std::vector<Cmd> hcmds;     // host plans, at their documents' offsets
+    std::vector<uint32_t> htlist, cbyte;
     std::vector<uint8_t> content;
+    uint64_t cmd_total = 0, tlist_total = 0;
     uint64_t lv_total = 0, blk_total = 0, out_total = 0, gidx_total = 0;
     // expected items per block in the LDS tier (insert-point splits keep typing runs in full
     // blocks); DTGPU_LDS_FILL overrides it for experiments
@@ -136,29 +242,46 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         B->total_lv += p.log.n_lv;
         DocDesc &d = B->docs[i];
         std::memset(&d, 0, sizeof d);
-        if (p.status != OK) continue;
+        const uint64_t aq = p.pi.aruns.size() / 4;
+        d.arun_off = pdesc[i].arun_off * 4;
+        if (p.status != OK) { pdesc[i].skip = 1; continue; }
         uint64_t n_ins = 0;
         for (const OpRun &r : p.log.ops) if (r.kind == 0) n_ins += r.len;
-        if (n_ins / 32 + 2 > std::min<uint64_t>(LOC_MAX_BLOCKS, MAX_DOC_BLOCKS)) { B->host_status[i] = ErrCapacity; continue; }
-        d.cmd_off = cmds.size();
-        d.tlist_off = tlist.size();
+        if (n_ins / 32 + 2 > std::min<uint64_t>(LOC_MAX_BLOCKS, MAX_DOC_BLOCKS)) { B->host_status[i] = ErrCapacity; pdesc[i].skip = 1; continue; }
+        d.cmd_off = cmd_total;
+        d.tlist_off = tlist_total;
+        if (p.host_plan) {
+            B->host_planned[i] = reason[i] ? reason[i] : 2;
+            pdesc[i].skip = 1;
+            d.ncmd = uint32_t(p.plan.cmds.size());
+            hcmds.resize(cmd_total);
+            htlist.resize(tlist_total);
+            append(hcmds, p.plan.cmds);
+            append(htlist, p.plan.tlist);
+            cmd_total += p.plan.cmds.size();
+            tlist_total += p.plan.tlist.size();
+        } else {
+            d.ncmd = pres[i].ncmd;
+            pdesc[i].cmd_off = cmd_total;
+            pdesc[i].tlist_off = tlist_total;
+            pdesc[i].ccap = pres[i].ncmd;
+            pdesc[i].tcap = pres[i].ntlist;
+            cmd_total += pres[i].ncmd;
+            tlist_total += pres[i].ntlist;
+            B->n_gpu_planned++;
+        }
         d.ascii = p.log.ins_content.size() == n_ins ? 1u : 0u;
-        d.ncmd = uint32_t(p.plan.cmds.size());
         d.lv_off = lv_total;
         d.n_lv = uint32_t(p.log.n_lv);
         d.content_off = content.size();
         d.content_len = uint32_t(p.log.ins_content.size());
-        d.arun_off = aruns.size();
-        d.n_aruns = uint32_t(p.plan.agent_runs.size() / 3);
+        d.n_aruns = uint32_t(aq);
         d.max_blocks = uint32_t(n_ins / 32 + 2);
         d.blk_off = blk_total;
         d.out_off = out_total;
         d.out_cap = uint32_t(p.log.ins_content.size());
-        cmds.insert(cmds.end(), p.plan.cmds.begin(), p.plan.cmds.end());
-        tlist.insert(tlist.end(), p.plan.tlist.begin(), p.plan.tlist.end());
         cbyte.insert(cbyte.end(), p.log.ins_cbyte.begin(), p.log.ins_cbyte.end());
         content.insert(content.end(), p.log.ins_content.begin(), p.log.ins_content.end());
-        aruns.insert(aruns.end(), p.plan.agent_runs.begin(), p.plan.agent_runs.end());
         lv_total += p.log.n_lv;
         blk_total += d.max_blocks;
         out_total += d.out_cap;
@@ -181,12 +304,37 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
             B->large_list.push_back(uint32_t(i));
         }
     }
-    hipStream_t s = B->stream;
-#define CK(x) do { if ((x) != hipSuccess) return DTGPU_ERR_HIP; } while (0)
-    CK(B->d_cmds.upload(cmds, s));
-    CK(B->d_tlist.upload(tlist, s));
+    // host-planned documents' agent runs are not in the planner arrays: append them
+    {
+        std::vector<uint32_t> extra;
+        uint64_t base_q = B->d_aruns.n / 4;
+        for (size_t i = 0; i < n; i++) {
+            if (!B->host_planned[i]) continue;
+            B->docs[i].arun_off = (base_q + extra.size() / 4) * 4;
+            append(extra, prep[i].pi.aruns.empty() ? prep[i].plan.agent_runs : prep[i].pi.aruns);
+        }
+        if (!extra.empty()) {
+            std::vector<uint32_t> all(B->d_aruns.n);
+            if (B->d_aruns.n)
+                CK(hipMemcpyAsync(all.data(), B->d_aruns.p, all.size() * 4, hipMemcpyDeviceToHost, s));
+            CK(hipStreamSynchronize(s));
+            append(all, extra);
+            DevBuf<uint32_t> fresh;
+            CK(fresh.upload(all, s));
+            std::swap(B->d_aruns.p, fresh.p);
+            std::swap(B->d_aruns.n, fresh.n);
+            B->plan.aruns = B->d_aruns.p;
+        }
+    }
+    hcmds.resize(cmd_total);
+    htlist.resize(tlist_total);
+    CK(B->d_cmds.upload(hcmds, s));
+    CK(B->d_tlist.upload(htlist, s));
+    CK(B->p_docs.upload(pdesc, s));
+    B->plan.docs = B->p_docs.p;
+    B->plan.cmds = B->d_cmds.p;
+    B->plan.tlist = B->d_tlist.p;
     CK(B->d_cbyte.upload(cbyte, s));
-    CK(B->d_aruns.upload(aruns, s));
     CK(B->d_content.upload(content, s));
     CK(B->d_docs.upload(B->docs, s));
     std::vector<uint32_t> lists(B->small_list);
@@ -238,6 +386,15 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     }
     *out = B.release();
     return DTGPU_OK;
+}
+
+// Plan (device) then replay, on stream s.
+int launch_all(dtgpu_batch *B, hipStream_t s) {
+    if (B->n_gpu_planned) {
+        int e = launch_plan(B->plan, s);
+        if (e) return e;
+    }
+    return launch_replay(B->small, B->large, s, B->n_cu);
 }
 
 }  // namespace
@@ -328,6 +485,15 @@ size_t dtgpu_oplog_plan_commands(const dtgpu_oplog *h, uint32_t *cmds, size_t ca
     return p.plan.cmds.size();
 }
 
+size_t dtgpu_oplog_plan_tlist(const dtgpu_oplog *h, uint32_t *out, size_t cap) {
+    if (!h) return 0;
+    Prepared p;
+    prepare_from_oplog(h->o, p);
+    if (p.status != OK) return 0;
+    if (out) std::memcpy(out, p.plan.tlist.data(), std::min(cap, p.plan.tlist.size()) * sizeof(uint32_t));
+    return p.plan.tlist.size();
+}
+
 size_t dtgpu_oplog_ins_content(const dtgpu_oplog *h, uint8_t *out, size_t cap) {
     if (!h) return 0;
     const auto &c = h->o.ins_content;
@@ -360,7 +526,7 @@ dtgpu_status dtgpu_batch_create(const uint8_t *const *docs, const size_t *lens, 
     parallel_for(n, threads_for(opts, n), [&](size_t i) {
         Prepared &p = prep[i];
         p.status = decode_dt(docs[i], lens[i], ignore_crc, p.log);
-        if (p.status == OK) p.status = build_plan(p.log, p.plan);
+        prepare_input(p);
     });
     return stage(prep, opts, out);
 }
@@ -370,7 +536,11 @@ dtgpu_status dtgpu_batch_create_from_oplogs(const dtgpu_oplog *const *oplogs, si
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return DTGPU_ERR_NO_DEVICE;
     std::vector<Prepared> prep(n);
-    parallel_for(n, threads_for(opts, n), [&](size_t i) { prepare_from_oplog(oplogs[i]->o, prep[i]); });
+    parallel_for(n, threads_for(opts, n), [&](size_t i) {
+        prep[i].log = oplogs[i]->o;
+        prep[i].log.finish();
+        prepare_input(prep[i]);
+    });
     return stage(prep, opts, out);
 }
 dtgpu_status dtgpu_batch_run(dtgpu_batch *B, void *stream) {
@@ -378,7 +548,7 @@ dtgpu_status dtgpu_batch_run(dtgpu_batch *B, void *stream) {
     if (hipSetDevice(B->device) != hipSuccess) return DTGPU_ERR_HIP;
     void *s = stream ? stream : reinterpret_cast<void *>(B->stream);
     if (B->small.debug) fprintf(stderr, "[dtgpu] launch small=%u large=%u lds_blocks=%u\n", B->small.n_list, B->large.n_list, B->lds_blocks);
-    dtgpu_status st = dtgpu_status(launch_replay(B->small, B->large, s, B->n_cu));
+    dtgpu_status st = dtgpu_status(launch_all(B, reinterpret_cast<hipStream_t>(s)));
     if (B->small.debug) {
         fprintf(stderr, "[dtgpu] launched status %d\n", int(st));
         hipError_t e = hipStreamSynchronize(reinterpret_cast<hipStream_t>(s));
@@ -389,13 +559,19 @@ dtgpu_status dtgpu_batch_run(dtgpu_batch *B, void *stream) {
 dtgpu_status dtgpu_batch_run_timed(dtgpu_batch *B, float *ms) {
     if (!B) return DTGPU_ERR_ARG;
     if (hipSetDevice(B->device) != hipSuccess) return DTGPU_ERR_HIP;
+    // plan (device walk planner) + replay + materialisation, all on the batch's stream
     if (hipEventRecord(B->ev0, B->stream) != hipSuccess) return DTGPU_ERR_HIP;
+    if (B->n_gpu_planned && launch_plan(B->plan, B->stream) != OK) return DTGPU_ERR_HIP;
+    if (hipEventRecord(B->ev_mid, B->stream) != hipSuccess) return DTGPU_ERR_HIP;
     int s = launch_replay(B->small, B->large, B->stream, B->n_cu);
     if (s) return dtgpu_status(s);
     if (hipEventRecord(B->ev1, B->stream) != hipSuccess) return DTGPU_ERR_HIP;
     if (hipEventSynchronize(B->ev1) != hipSuccess) return DTGPU_ERR_HIP;
-    float t = 0;
+    float t = 0, tp = 0;
     if (hipEventElapsedTime(&t, B->ev0, B->ev1) != hipSuccess) return DTGPU_ERR_HIP;
+    if (hipEventElapsedTime(&tp, B->ev0, B->ev_mid) != hipSuccess) return DTGPU_ERR_HIP;
+    B->last_plan_ms = tp;
+    B->last_replay_ms = t - tp;
     if (ms) *ms = t;
     return DTGPU_OK;
 }
@@ -404,6 +580,44 @@ dtgpu_status dtgpu_batch_sync(dtgpu_batch *B) {
     return hipStreamSynchronize(B->stream) == hipSuccess ? DTGPU_OK : DTGPU_ERR_HIP;
 }
 size_t dtgpu_batch_size(const dtgpu_batch *B) { return B ? B->n : 0; }
+dtgpu_status dtgpu_batch_last_times(const dtgpu_batch *B, float out[2]) {
+    if (!B || !out) return DTGPU_ERR_ARG;
+    out[0] = B->last_plan_ms;
+    out[1] = B->last_replay_ms;
+    return DTGPU_OK;
+}
+size_t dtgpu_batch_host_planned(const dtgpu_batch *B, uint8_t *flags, size_t cap) {
+    if (!B) return 0;
+    if (flags) for (size_t i = 0; i < B->n && i < cap; i++) flags[i] = B->host_planned[i];
+    size_t k = 0;
+    for (uint8_t f : B->host_planned) k += f != 0;
+    return k;
+}
+dtgpu_status dtgpu_batch_plan(dtgpu_batch *B, size_t i, uint32_t *cmds, size_t cmd_cap, uint32_t *tlist,
+                              size_t tlist_cap, size_t *n_cmds, size_t *n_tlist) {
+    if (!B || i >= B->n) return DTGPU_ERR_ARG;
+    if (B->host_status[i] != OK) return dtgpu_status(B->host_status[i]);
+    const DocDesc &d = B->docs[i];
+    std::vector<Cmd> c(d.ncmd);
+    if (d.ncmd && hipMemcpyAsync(c.data(), B->d_cmds.p + d.cmd_off, d.ncmd * sizeof(Cmd), hipMemcpyDeviceToHost, B->stream) != hipSuccess)
+        return DTGPU_ERR_HIP;
+    if (hipStreamSynchronize(B->stream) != hipSuccess) return DTGPU_ERR_HIP;
+    size_t nt = 0;
+    for (const Cmd &x : c) if ((x.op & 15u) == CMD_TOG) nt = std::max<size_t>(nt, size_t(x.lv) + x.len);
+    if (n_cmds) *n_cmds = c.size();
+    if (n_tlist) *n_tlist = nt;
+    if (cmds) {
+        if (cmd_cap < c.size()) return DTGPU_ERR_ARG;
+        std::memcpy(cmds, c.data(), c.size() * sizeof(Cmd));
+    }
+    if (tlist && nt) {
+        if (tlist_cap < nt) return DTGPU_ERR_ARG;
+        if (hipMemcpyAsync(tlist, B->d_tlist.p + d.tlist_off, nt * 4, hipMemcpyDeviceToHost, B->stream) != hipSuccess ||
+            hipStreamSynchronize(B->stream) != hipSuccess)
+            return DTGPU_ERR_HIP;
+    }
+    return DTGPU_OK;
+}
 uint64_t dtgpu_batch_algorithmic_bytes(dtgpu_batch *B) {
     if (!B) return 0;
     std::vector<dtgpu_doc_result> r(B->n);

@@ -78,6 +78,13 @@ def lib():
     L.dtgpu_oplog_plan_stats.argtypes = [vp, pu64]
     L.dtgpu_oplog_plan_commands.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32), sz]
     L.dtgpu_oplog_plan_commands.restype = sz
+    L.dtgpu_oplog_plan_tlist.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32), sz]
+    L.dtgpu_oplog_plan_tlist.restype = sz
+    L.dtgpu_batch_last_times.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
+    L.dtgpu_batch_host_planned.argtypes = [vp, ctypes.POINTER(ctypes.c_uint8), sz]
+    L.dtgpu_batch_host_planned.restype = sz
+    pu32 = ctypes.POINTER(ctypes.c_uint32)
+    L.dtgpu_batch_plan.argtypes = [vp, sz, pu32, sz, pu32, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
     L.dtgpu_oplog_ins_content.argtypes = [vp, ctypes.c_char_p, sz]
     L.dtgpu_oplog_ins_content.restype = sz
     L.dtgpu_oplog_char_offsets.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32), sz]
@@ -211,6 +218,12 @@ class ListOpLog:
         lib().dtgpu_oplog_plan_commands(self._h, buf, n)
         return [tuple(buf[4 * i:4 * i + 4]) for i in range(n)]
 
+    def plan_tlist(self):
+        n = lib().dtgpu_oplog_plan_tlist(self._h, None, 0)
+        buf = (ctypes.c_uint32 * max(1, n))()
+        lib().dtgpu_oplog_plan_tlist(self._h, buf, n)
+        return list(buf[:n])
+
     def ins_content(self) -> bytes:
         n = lib().dtgpu_oplog_ins_content(self._h, None, 0)
         buf = ctypes.create_string_buffer(max(1, n))
@@ -254,7 +267,8 @@ def oplog_from_trace(txns, agent_name="jeremy") -> ListOpLog:
 
 
 class Batch:
-    """A batch staged in HBM (decode + plan on host threads, replay on the GPU)."""
+    """A batch staged in HBM: decode on host threads; walk planning (dt_plan.hip), replay and
+    materialisation (dt_replay.hip) on the GPU."""
 
     def __init__(self, docs=None, oplogs=None, ignore_crc=False, host_threads=0, device=0):
         L = lib()
@@ -272,6 +286,9 @@ class Batch:
             _check(L.dtgpu_batch_create(ptrs, lens, len(self._keep), ctypes.byref(opts), ctypes.byref(out)))
             self.n = len(self._keep)
         self._h = out.value
+
+    def __len__(self):
+        return self.n
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -301,6 +318,27 @@ class Batch:
         buf = ctypes.create_string_buffer(max(1, n.value))
         _check(lib().dtgpu_batch_text(self._h, i, buf, n.value, ctypes.byref(n)))
         return buf.raw[:n.value]
+
+    def last_times(self):
+        """(plan_ms, replay_ms) of the last run_timed()."""
+        out = (ctypes.c_float * 2)()
+        _check(lib().dtgpu_batch_last_times(self._h, out))
+        return out[0], out[1]
+
+    def host_planned(self):
+        n = len(self)
+        buf = (ctypes.c_uint8 * max(1, n))()
+        lib().dtgpu_batch_host_planned(self._h, buf, n)
+        return [int(x) for x in buf[:n]]
+
+    def plan(self, i):
+        """Command stream (op, lv, len, pos) and retreat/advance entries of document i."""
+        nc, nt = ctypes.c_size_t(), ctypes.c_size_t()
+        _check(lib().dtgpu_batch_plan(self._h, i, None, 0, None, 0, ctypes.byref(nc), ctypes.byref(nt)))
+        cb = (ctypes.c_uint32 * max(4, 4 * nc.value))()
+        tb = (ctypes.c_uint32 * max(1, nt.value))()
+        _check(lib().dtgpu_batch_plan(self._h, i, cb, nc.value, tb, nt.value, ctypes.byref(nc), ctypes.byref(nt)))
+        return [tuple(cb[4 * k:4 * k + 4]) for k in range(nc.value)], list(tb[:nt.value])
 
     def doc_stats(self, i):
         """Diagnostics of document i after a run (see dtgpu_batch_doc_stats)."""

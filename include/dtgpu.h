@@ -89,10 +89,13 @@ size_t dtgpu_oplog_local_frontier(const dtgpu_oplog *oplog, uint64_t *out, size_
  * advanced LVs, out[3] device commands.  Pure host code; usable without a GPU. */
 dtgpu_status dtgpu_oplog_plan_stats(const dtgpu_oplog *oplog, uint64_t out[4]);
 
-/* The device command stream of that plan (16 B per command: op | fwd<<4, lv, len, pos) and
- * the tie-break agent runs (lv, name rank, seq).  Returns the command count; writes at most
- * cap commands.  Introspection for tests and tools. */
+/* The device command stream of the host plan (16 B per command: op | fwd<<4, lv, len, pos;
+ * op 0 INS, 1 DEL, 2 TOG {tlist offset, count}).  Returns the command count; writes at most
+ * cap commands.  Introspection for tests and tools (the device planner, dt_plan.hip, must
+ * produce the same stream). */
 size_t dtgpu_oplog_plan_commands(const dtgpu_oplog *oplog, uint32_t *cmds, size_t cap);
+/* Retreat / advance entries of the host plan (LV | is_del << 30 | advance << 31). */
+size_t dtgpu_oplog_plan_tlist(const dtgpu_oplog *oplog, uint32_t *out, size_t cap);
 
 /* Inserted-content arena (UTF-8, LV order; the text every checkout draws from) and the byte
  * offset of each LV's char (~0 for deletes).  Return the full sizes; copy at most cap. */
@@ -136,11 +139,25 @@ dtgpu_status dtgpu_batch_create_from_oplogs(const dtgpu_oplog *const *oplogs, si
 /* Enqueue the device checkout of the whole batch on `stream` (hipStream_t, NULL = the batch's
  * own stream).  Asynchronous; inputs are already resident in HBM. */
 dtgpu_status dtgpu_batch_run(dtgpu_batch *batch, void *stream);
-/* Run once, synchronously, and report device time of the replay kernels (hipEvents on the
- * launch stream) in *kernel_ms. */
+/* Run once, synchronously, and report device time of the planner + replay kernels (hipEvents
+ * on the launch stream) in *kernel_ms. */
 dtgpu_status dtgpu_batch_run_timed(dtgpu_batch *batch, float *kernel_ms);
 dtgpu_status dtgpu_batch_sync(dtgpu_batch *batch);
 size_t dtgpu_batch_size(const dtgpu_batch *batch);
+/* Device time of the last dtgpu_batch_run_timed split into out[0] = walk planning (dt_plan.hip)
+ * and out[1] = replay + materialisation (dt_replay.hip), milliseconds. */
+dtgpu_status dtgpu_batch_last_times(const dtgpu_batch *batch, float out[2]);
+/* Documents planned on the host because the device planner declined them: returns their count
+ * and, when flags is not NULL, one code per document: 0 device-planned, 1 DTGPU_HOST_PLAN set,
+ * 2 outside the planner's limits (> 512 agents, > 16384 graph entries, sparse agent seq
+ * numbering), 16 + k the device planner stopped with status k (17: an agent whose ops are not
+ * one causal chain, e.g. one author committing on concurrent branches). */
+size_t dtgpu_batch_host_planned(const dtgpu_batch *batch, uint8_t *flags, size_t cap);
+/* The command stream of document `doc` as last planned (16-byte commands as uint32 quads
+ * {op, lv, len, pos}; TOG commands index the retreat/advance entries copied to tlist).
+ * NULL buffers query the sizes. */
+dtgpu_status dtgpu_batch_plan(dtgpu_batch *batch, size_t doc, uint32_t *cmds, size_t cmd_cap, uint32_t *tlist,
+                              size_t tlist_cap, size_t *n_cmds, size_t *n_tlist);
 /* Copy per-document results (n_docs entries) to host. */
 dtgpu_status dtgpu_batch_results(dtgpu_batch *batch, dtgpu_doc_result *results);
 /* Copy one document's merged text to host. */

@@ -158,3 +158,72 @@ def test_invariants_hold_after_every_command():
         assert got == G.trace("friendsforever_flat")["endContent"].encode()
     g = _with_env({"DTGPU_DEBUG": "1"}, lambda: dt_amd.ListOpLog.load_from(G.COMPAT_SIMPLE_LZ4).checkout_tip_bytes())
     assert g == b"hi me"
+
+
+def _host_plan(oplog):
+    return oplog.plan_commands(), oplog.plan_tlist()
+
+
+def _same_plan(gpu, host):
+    """Same command sequence; a TOG's entries compared as a multiset (the pass is commutative)."""
+    (gc, gt), (hc, ht) = gpu, host
+    assert len(gc) == len(hc)
+    for k, (a, b) in enumerate(zip(gc, hc)):
+        assert a[0] == b[0], (k, a, b)
+        if (a[0] & 15) == 2:
+            assert a[2] == b[2], (k, a, b)
+            assert sorted(gt[a[1]:a[1] + a[2]]) == sorted(ht[b[1]:b[1] + b[2]]), k
+        else:
+            assert a == b, (k, a, b)
+
+
+@pytest.mark.parametrize("name", ["friendsforever", "git-makefile", "node_nodecc"])
+def test_device_planner_matches_host_walk(name):
+    """dt_plan.hip walks the graph in the reference's spanning-tree order and derives the
+    retreat / advance sets from agent version vectors: its stream must equal the host planner's
+    (Graph::diff_rev) command for command."""
+    data = G.dt_bytes(name)
+    b = dt_amd.Batch(docs=[data])
+    assert b.host_planned() == [0]
+    b.run()
+    b.sync()
+    _same_plan(b.plan(0), _host_plan(dt_amd.ListOpLog.load_from(data)))
+
+
+def test_device_planner_on_traces_and_kats():
+    oplogs = [dt_amd.oplog_from_trace(G.trace(n)["txns"]) for n in ("sveltecomponent", "friendsforever_flat")]
+    g = dt_amd.ListOpLog()
+    a, c = g.get_or_create_agent_id("a"), g.get_or_create_agent_id("b")
+    t = g.add_insert_at(a, [], 0, "aaa")
+    g.add_insert_at(c, [], 0, "bbb")
+    g.add_delete_at(c, [t], 0, 2)
+    g.add_insert_at(a, [2, 5], 0, "ccc")
+    oplogs.append(g)
+    b = dt_amd.Batch(oplogs=oplogs)
+    assert b.host_planned() == [0] * 3
+    b.run()
+    b.sync()
+    for i, o in enumerate(oplogs):
+        _same_plan(b.plan(i), _host_plan(o))
+    assert b.text(2) == OracleOpLog_from(g).encode()
+
+
+def OracleOpLog_from(g):
+    """Rebuild the KAT oplog in the oracle and check it out there."""
+    o = OracleOpLog()
+    a, c = o.agent("a"), o.agent("b")
+    t = o.add_insert_at(a, [], 0, "aaa")
+    o.add_insert_at(c, [], 0, "bbb")
+    o.add_delete_at(c, [t], 0, 2)
+    o.add_insert_at(a, [2, 5], 0, "ccc")
+    return o.checkout_tip()
+
+
+def test_host_planner_path_still_exact():
+    data = G.dt_bytes("git-makefile")
+    want = OracleOpLog.load_from(data).checkout_tip_bytes()
+    b = _with_env({"DTGPU_HOST_PLAN": "1"}, lambda: dt_amd.Batch(docs=[data, G.dt_bytes("friendsforever")]))
+    assert b.host_planned() == [1, 1]
+    b.run()
+    b.sync()
+    assert b.text(0) == want

@@ -20,13 +20,18 @@ def main():
         b = dt_amd.Batch(docs=[data] * n)
         stage = time.time() - t
         b.run(); b.sync()
-        ms = [b.run_timed() for _ in range(reps)]
+        ms, split = [], []
+        for _ in range(reps):
+            ms.append(b.run_timed())
+            split.append(b.last_times())
         res = b.results()
         ok = all(r["status"] == 0 for r in res)
         lv = sum(r["n_lv"] for r in res)
         best = min(ms)
         print(f"{name} docs={n} stage={stage:.2f}s kernel_ms={best:.2f} (all {['%.2f' % m for m in ms]}) "
-              f"ok={ok} Mops/s={lv / best / 1e3:.1f} alg_GB/s={b.algorithmic_bytes / best / 1e6:.1f}", flush=True)
+              f"ok={ok} Mops/s={lv / best / 1e3:.1f} alg_GB/s={b.algorithmic_bytes / best / 1e6:.1f} "
+              f"plan/replay_ms={split[ms.index(best)][0]:.2f}/{split[ms.index(best)][1]:.2f} host_planned={sum(b.host_planned())}",
+              flush=True)
 
 
 if __name__ == "__main__":
