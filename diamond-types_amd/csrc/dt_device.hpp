@@ -90,13 +90,15 @@ struct PlanDesc {       // per document; offsets index the concatenated PlanInpu
 struct PlanResult {
     uint32_t status, ncmd, ntlist, n_tip;
     uint64_t n_retreat, n_advance;
+    uint64_t prof[6];   // DTGPU_PLAN_PROF: cycles in record wait, parents, children+pick, emit, ops, init
 };
 struct PlanParams {
-    const uint32_t *par, *pent, *child, *aruns, *tip, *erec, *doff, *dense;
+    const uint32_t *par, *pent, *pch, *pcnt, *child, *aruns, *tip, *erec, *doff, *dense;
     const Cmd *opc;
     uint32_t *base;
     uint32_t lds_entries;   // per-wave LDS capacity (entries) of the todo stack / pending counts
     uint32_t max_agents;    // largest agent count among device-planned documents
+    uint32_t prof;          // cycle profile into PlanResult.prof
     Cmd *cmds;
     uint32_t *tlist;
     const PlanDesc *docs;

@@ -915,6 +915,13 @@ Status build_plan_input(const HostOpLog &o, PlanInput &pi) {
         tail[c] = uint32_t(i);
     }
     pi.n_chains = uint32_t(tail.size());
+    pi.pch.resize(pi.par.size());
+    pi.pcnt.resize(pi.par.size());
+    for (size_t k = 0; k < pi.par.size(); k++) {
+        const uint32_t pe = pi.pent[k];
+        pi.pch[k] = chain_of[pe];
+        pi.pcnt[k] = seq0[pe] + (pi.par[k] - uint32_t(E[pe].start)) + 1;
+    }
     // entry records
     pi.erec.assign(ne * EREC_WORDS, 0);
     for (size_t i = 0; i < ne; i++) {
@@ -930,7 +937,14 @@ Status build_plan_input(const HostOpLog &o, PlanInput &pi) {
         r[8] = pi.coff[i];
         r[9] = pi.coff[i + 1] - pi.coff[i];
         r[10] = r[3] ? pi.par[pi.poff[i]] : 0xFFFFFFFFu;
-        r[11] = r[3] ? pi.pent[pi.poff[i]] : 0xFFFFFFFFu;
+        for (uint32_t j = 0; j < 2; j++) {
+            const bool has = r[3] > j;
+            const uint32_t k = pi.poff[i] + j;
+            r[11 + 3 * j] = has ? pi.pent[k] : 0xFFFFFFFFu;
+            r[12 + 3 * j] = has ? pi.pch[k] : 0;
+            r[13 + 3 * j] = has ? pi.pcnt[k] : 0;
+        }
+        r[17] = r[9] ? pi.child[pi.coff[i + 1] - 1] : 0xFFFFFFFFu;
     }
     // dense chain seq -> LV | is_del tables (the planner copies retreat/advance ranges out)
     pi.doff.assign(pi.n_chains + 1, 0);

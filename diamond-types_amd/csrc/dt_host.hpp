@@ -116,15 +116,17 @@ struct PlanInput {
     std::vector<uint32_t> aseq;     // triples (seq, lv, len) sorted by seq within each agent
     std::vector<uint32_t> isdel;    // bit per LV: 1 = delete op
     std::vector<uint32_t> tip;      // pairs (LV, entry) of cg.version
-    // per entry, 12 words: start, end, parents offset, parent count, first op run, op runs,
-    // chain, first seq in the chain, children offset, child count, first parent LV / entry
+    // per entry, EREC_WORDS words: start, end, parents offset, parent count, first op run, op
+    // runs, chain, first seq in the chain, children offset, child count, first parent LV, then
+    // for the first two parents (entry, chain, ops of that chain up to the parent), last child
     std::vector<uint32_t> erec;
+    std::vector<uint32_t> pch, pcnt;  // per parent slot: its chain and that chain's ops up to it
     uint32_t n_chains = 0;          // causal chains the entries are partitioned into
     std::vector<uint32_t> doff;     // per chain: offset of its dense seq table (n_chains + 1)
     std::vector<uint32_t> dense;    // per chain, by seq: LV | is_del << 30
     bool device_ok = true;
 };
-constexpr uint32_t EREC_WORDS = 12;
+constexpr uint32_t EREC_WORDS = 20;
 Status build_plan_input(const HostOpLog &o, PlanInput &pi);
 
 uint64_t text_hash(const uint8_t *t, size_t n);

@@ -50,7 +50,7 @@ DEV uint32_t wave_scan(uint32_t x) {   // inclusive prefix sum (same DPP sequenc
 
 struct P {
     // inputs (decoded oplog)
-    const uint32_t *erec, *par, *pent, *child, *doff, *dense, *tip;
+    const uint32_t *erec, *par, *pent, *pch, *pcnt, *child, *doff, *dense, *tip;
     const Cmd *opc;
     uint32_t ne, A, ntip, n_lv;
     // scratch: vv rows in HBM; todo stack and pending parent counts in LDS (u16)
@@ -65,7 +65,11 @@ struct P {
     uint32_t nc, nt, err;
     uint64_t steps, limit;
     uint64_t n_ret, n_adv;
+    uint32_t prof;
+    uint64_t pc[6];
 };
+DEV uint64_t tk(const P &p) { return p.prof ? __builtin_amdgcn_s_memtime() : 0; }
+#define PT(slot) do { if (p.prof) { const uint64_t t_ = __builtin_amdgcn_s_memtime(); p.pc[slot] += t_ - t_last; t_last = t_; } } while (0)
 
 DEV void fail(P &p, uint32_t code) {
     if (!p.err) p.err = code;
@@ -76,7 +80,10 @@ DEV bool charge(P &p) {
 }
 
 // Entry record (EREC_WORDS words) lane by lane; R(rw, k) reads word k.
-enum { R_START = 0, R_END, R_POFF, R_NP, R_OP0, R_NOP, R_CHAIN, R_SEQ0, R_CH0, R_NCH, R_PAR0, R_PENT0 };
+enum {
+    R_START = 0, R_END, R_POFF, R_NP, R_OP0, R_NOP, R_CHAIN, R_SEQ0, R_CH0, R_NCH, R_PAR0,
+    R_PENT0, R_PCH0, R_PCNT0, R_PENT1, R_PCH1, R_PCNT1, R_LASTCH
+};
 DEV uint32_t load_rec(const P &p, uint32_t e) {
     const uint32_t l = lane_id();
     return l < EREC_WORDS ? p.erec[size_t(e) * EREC_WORDS + l] : 0;
@@ -148,7 +155,7 @@ template <int K> DEV void vv_at(P &p, uint32_t lv, uint32_t e, VV<K> &row) {
 // seq range of its dense seq -> (LV | is_del) table.  The ranges of one 64-agent chunk are
 // gathered together, 64 entries per load.
 template <int K>
-DEV void emit_diff(P &p, const VV<K> &from, const VV<K> &to, bool allow_retreat) {
+DEV void emit_diff(P &p, const VV<K> &from, const VV<K> &to, const VV<K> &dlo, const VV<K> &dhi, bool allow_retreat) {
     const uint32_t l = lane_id();
 #pragma unroll
     for (int k = 0; k < K; k++) {
@@ -160,8 +167,7 @@ DEV void emit_diff(P &p, const VV<K> &from, const VV<K> &to, bool allow_retreat)
         const bool adv = to.v[k] > from.v[k];
         const uint32_t s0 = adv ? from.v[k] : to.v[k];
         const uint32_t n = act ? (adv ? to.v[k] - from.v[k] : from.v[k] - to.v[k]) : 0;
-        uint32_t d0 = 0, d1 = 0;
-        if (act) { d0 = p.doff[a]; d1 = p.doff[a + 1]; }
+        const uint32_t d0 = dlo.v[k], d1 = dhi.v[k];
         if (__ballot(act && d0 + s0 + n > d1)) { fail(p, PLAN_ERR_INTERNAL); return; }
         const uint32_t inc = wave_scan(n);
         const uint32_t total = bcast(inc, 63);
@@ -227,8 +233,15 @@ DEV uint32_t pick(P &p, uint32_t &top) {
 template <int K>
 DEV void plan_doc(P &p, PlanResult *res) {
     const uint32_t l = lane_id();
-    VV<K> vf, vp;
+    VV<K> vf, vp, dlo, dhi;
     vv_zero(vf);
+    // each chain's dense-table slice, kept in registers
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const uint32_t a = l + 64 * k;
+        dlo.v[k] = a < p.A ? p.doff[a] : 0;
+        dhi.v[k] = a < p.A ? p.doff[a + 1] : 0;
+    }
     // pending parent counts (+ merge flag); the todo stack holds the roots, first root on top
     uint32_t top = 0;
     for (uint32_t c = 0; c < p.ne; c += 64) {
@@ -248,6 +261,8 @@ DEV void plan_doc(P &p, PlanResult *res) {
         top += uint32_t(__popcll(m));
     }
     wave_fence();
+    uint64_t t_last = tk(p);
+    PT(5);
     uint32_t f = 0xFFFFFFFFu;   // current frontier: ROOT or one LV
     bool have = top > 0;
     uint32_t idx = have ? pick(p, top) : 0;
@@ -257,7 +272,11 @@ DEV void plan_doc(P &p, PlanResult *res) {
         // the entry's op runs, agent runs and children: independent loads, issued together
         const uint32_t np = R(rw, R_NP), op0 = R(rw, R_OP0), nop = R(rw, R_NOP), ch0 = R(rw, R_CH0),
                        nch = R(rw, R_NCH), chain = R(rw, R_CHAIN), seq0 = R(rw, R_SEQ0);
+        PT(0);
         const uint32_t e_start = R(rw, R_START), e_end = R(rw, R_END);
+        // speculation: the entry's last child is usually the next one consumed
+        const uint32_t spec = R(rw, R_LASTCH);
+        const uint32_t rw_spec = spec != 0xFFFFFFFFu ? load_rec(p, spec) : 0;
         // (four scalars, not a Cmd: a struct assigned under a branch goes through scratch)
         const uint32_t *opw = reinterpret_cast<const uint32_t *>(p.opc);
         uint32_t oc0 = 0, oc1 = 0, oc2 = 0, oc3 = 0;
@@ -270,15 +289,42 @@ DEV void plan_doc(P &p, PlanResult *res) {
         if (np == 1 && R(rw, R_PAR0) == f) {
             vp = vf;
         } else {
+            // parents' vectors: each parent entry's row plus its chain's ops up to the parent;
+            // up to 4 parents' rows in flight at once
             vv_zero(vp);
             const uint32_t po = R(rw, R_POFF);
-            for (uint32_t j = 0; j < np; j++) {
-                VV<K> t;
-                vv_at<K>(p, j == 0 ? R(rw, R_PAR0) : U(p.par[po + j]), j == 0 ? R(rw, R_PENT0) : U(p.pent[po + j]), t);
-                vv_max(vp, t);
+            for (uint32_t j0 = 0; j0 < np; j0 += 4) {
+                uint32_t pe[4], pc[4], pn[4];
+                VV<K> t[4];
+#pragma unroll
+                for (int jj = 0; jj < 4; jj++) {
+                    const uint32_t j = j0 + jj;
+                    pe[jj] = pc[jj] = pn[jj] = 0;
+                    if (j < np) {
+                        if (j < 2) {
+                            pe[jj] = R(rw, R_PENT0 + 3 * int(j));
+                            pc[jj] = R(rw, R_PCH0 + 3 * int(j));
+                            pn[jj] = R(rw, R_PCNT0 + 3 * int(j));
+                        } else {
+                            pe[jj] = U(p.pent[po + j]);
+                            pc[jj] = U(p.pch[po + j]);
+                            pn[jj] = U(p.pcnt[po + j]);
+                        }
+                        load_row(p, pe[jj], t[jj]);
+                    }
+                }
+#pragma unroll
+                for (int jj = 0; jj < 4; jj++) {
+                    if (j0 + jj >= np) break;
+                    vv_max(vp, t[jj]);
+#pragma unroll
+                    for (int k = 0; k < K; k++)
+                        if (pc[jj] == l + 64 * uint32_t(k)) vp.v[k] = max(vp.v[k], pn[jj]);
+                }
             }
         }
         store_row(p, idx, vp);
+        PT(1);
         const VV<K> v_old = vf;
         // the frontier moves to the entry's last LV; its runs must continue the agents' chains
         vf = vp;
@@ -303,15 +349,17 @@ DEV void plan_doc(P &p, PlanResult *res) {
         have = top > 0;
         if (have) {
             idx = pick(p, top);
-            rw = load_rec(p, idx);
+            rw = idx == spec ? rw_spec : load_rec(p, idx);
         }
+        PT(2);
         // retreat / advance to the parents, then apply the entry's op runs
         if (vv_differ(v_old, vp)) {
             const uint32_t t0 = p.nt;
-            emit_diff<K>(p, v_old, vp, true);
+            emit_diff<K>(p, v_old, vp, dlo, dhi, true);
             if (p.err) break;
             if (p.nt > t0) push_cmd(p, CMD_TOG, t0, p.nt - t0, 0);
         }
+        PT(3);
         if (uint64_t(p.nc) + nop > p.ccap) { fail(p, PLAN_CMDS_FULL); break; }
         if (!p.count_only) {
             if (l < nop) {
@@ -322,6 +370,7 @@ DEV void plan_doc(P &p, PlanResult *res) {
         }
         p.nc += nop;
         f = e_end - 1;
+        PT(4);
     }
     // advance to the tip (cg.version): the replay then holds the checkout
     if (!p.err) {
@@ -335,13 +384,14 @@ DEV void plan_doc(P &p, PlanResult *res) {
         if (!p.err && vv_differ(vf, vt)) {
             const uint32_t t0 = p.nt;
             const uint64_t adv0 = p.n_adv;
-            emit_diff<K>(p, vf, vt, false);
+            emit_diff<K>(p, vf, vt, dlo, dhi, false);
             if (!p.err && p.nt > t0) push_cmd(p, CMD_TOG, t0, p.nt - t0, 0);
             res->n_tip = uint32_t(p.n_adv - adv0);
             p.n_adv = adv0;
         }
     }
     if (l == 0) {
+        for (int i = 0; i < 6; i++) res->prof[i] = p.pc[i];
         res->status = p.err;
         res->ncmd = p.nc;
         res->ntlist = p.nt;
@@ -366,6 +416,8 @@ __global__ __launch_bounds__(64) void plan_kernel(PlanParams Q) {
     p.erec = Q.erec + pd.erec_off;
     p.par = Q.par + pd.par_off;
     p.pent = Q.pent + pd.par_off;
+    p.pch = Q.pch + pd.par_off;
+    p.pcnt = Q.pcnt + pd.par_off;
     p.child = Q.child + pd.child_off;
     p.opc = Q.opc + pd.op_off;
     p.doff = Q.doff + pd.doff_off;
@@ -387,6 +439,8 @@ __global__ __launch_bounds__(64) void plan_kernel(PlanParams Q) {
     p.steps = 0;
     p.limit = 1024ull * (uint64_t(p.ne) + 16) + 4ull * pd.n_lv + (1u << 20);
     p.n_ret = p.n_adv = 0;
+    p.prof = Q.prof;
+    for (int i = 0; i < 6; i++) p.pc[i] = 0;
     res->n_tip = 0;
     if (p.ne > Q.lds_entries) {
         if (lane_id() == 0) res->status = PLAN_ERR_INTERNAL;

@@ -61,7 +61,7 @@ struct dtgpu_batch {
     float last_plan_ms = 0, last_replay_ms = 0;
 
     // device planner inputs (the decoded oplogs) and scratch
-    DevBuf<uint32_t> p_par, p_pent, p_child, p_tip, p_erec, p_doff, p_dense;
+    DevBuf<uint32_t> p_par, p_pent, p_pch, p_pcnt, p_child, p_tip, p_erec, p_doff, p_dense;
     DevBuf<Cmd> p_opc;
     DevBuf<uint32_t> p_base;
     DevBuf<PlanDesc> p_docs;
@@ -152,7 +152,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     // ---- 1. device planner inputs; a sizing pass of the planner gives exact stream sizes ----
     std::vector<PlanDesc> pdesc(n);
     {
-        std::vector<uint32_t> par, pent, child, tip, aruns, erec, doff, dense;
+        std::vector<uint32_t> par, pent, pch, pcnt, child, tip, aruns, erec, doff, dense;
         std::vector<Cmd> opc;
         uint64_t base_total = 0, n_entries = 0;
         uint32_t lds_entries = 0, max_agents = 0;
@@ -185,7 +185,8 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
             q.n_lv = uint32_t(p.log.n_lv);
             append(aruns, pi.aruns);   // also the replay's tie-break runs
             if (host) continue;
-            append(par, pi.par); append(pent, pi.pent); append(child, pi.child); append(opc, pi.opc);
+            append(par, pi.par); append(pent, pi.pent); append(pch, pi.pch); append(pcnt, pi.pcnt);
+            append(child, pi.child); append(opc, pi.opc);
             append(tip, pi.tip); append(erec, pi.erec); append(doff, pi.doff); append(dense, pi.dense);
             base_total += ne * pi.n_chains;
             n_entries += ne;
@@ -193,6 +194,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
             max_agents = std::max<uint32_t>(max_agents, pi.n_chains);
         }
         CK(B->p_par.upload(par, s)); CK(B->p_pent.upload(pent, s)); CK(B->p_child.upload(child, s));
+        CK(B->p_pch.upload(pch, s)); CK(B->p_pcnt.upload(pcnt, s));
         CK(B->p_opc.upload(opc, s)); CK(B->d_aruns.upload(aruns, s)); CK(B->p_tip.upload(tip, s));
         CK(B->p_erec.upload(erec, s)); CK(B->p_doff.upload(doff, s)); CK(B->p_dense.upload(dense, s));
         CK(B->p_base.alloc(base_total));
@@ -200,11 +202,13 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         CK(B->p_results.alloc(n));
         CK(hipMemsetAsync(B->p_results.p, 0, std::max<size_t>(n, 1) * sizeof(PlanResult), s));
         PlanParams &q = B->plan;
-        q.par = B->p_par.p; q.pent = B->p_pent.p; q.child = B->p_child.p; q.opc = B->p_opc.p;
+        q.par = B->p_par.p; q.pent = B->p_pent.p; q.pch = B->p_pch.p; q.pcnt = B->p_pcnt.p;
+        q.child = B->p_child.p; q.opc = B->p_opc.p;
         q.aruns = B->d_aruns.p; q.tip = B->p_tip.p; q.erec = B->p_erec.p; q.doff = B->p_doff.p;
         q.dense = B->p_dense.p; q.base = B->p_base.p;
         q.lds_entries = (lds_entries + 7) & ~7u;
         q.max_agents = max_agents;
+        q.prof = getenv("DTGPU_PLAN_PROF") ? 1u : 0u;
         q.docs = B->p_docs.p; q.results = B->p_results.p; q.n_docs = uint32_t(n);
         q.count_only = 1;
         if (launch_plan(q, s) != OK) return DTGPU_ERR_HIP;
@@ -625,6 +629,17 @@ uint64_t dtgpu_batch_algorithmic_bytes(dtgpu_batch *B) {
     uint64_t out = 0;
     for (const auto &x : r) out += x.text_len;
     return B->alg_in_bytes + out;
+}
+dtgpu_status dtgpu_batch_plan_profile(dtgpu_batch *B, size_t i, uint64_t out[8]) {
+    if (!B || i >= B->n || !out) return DTGPU_ERR_ARG;
+    PlanResult r;
+    if (hipMemcpyAsync(&r, B->p_results.p + i, sizeof r, hipMemcpyDeviceToHost, B->stream) != hipSuccess ||
+        hipStreamSynchronize(B->stream) != hipSuccess)
+        return DTGPU_ERR_HIP;
+    for (int k = 0; k < 6; k++) out[k] = r.prof[k];
+    out[6] = r.ncmd;
+    out[7] = r.ntlist;
+    return DTGPU_OK;
 }
 dtgpu_status dtgpu_batch_doc_stats(dtgpu_batch *B, size_t i, uint32_t out[22]) {
     if (!B || i >= B->n || !out) return DTGPU_ERR_ARG;

@@ -105,6 +105,7 @@ def lib():
     L.dtgpu_batch_algorithmic_bytes.argtypes = [vp]
     L.dtgpu_batch_algorithmic_bytes.restype = u64
     L.dtgpu_batch_doc_stats.argtypes = [vp, sz, ctypes.POINTER(ctypes.c_uint32)]
+    L.dtgpu_batch_plan_profile.argtypes = [vp, sz, ctypes.POINTER(ctypes.c_uint64)]
     L.dtgpu_batch_total_lv.argtypes = [vp]
     L.dtgpu_batch_total_lv.restype = u64
     L.dtgpu_batch_free.argtypes = [vp]
@@ -339,6 +340,12 @@ class Batch:
         tb = (ctypes.c_uint32 * max(1, nt.value))()
         _check(lib().dtgpu_batch_plan(self._h, i, cb, nc.value, tb, nt.value, ctypes.byref(nc), ctypes.byref(nt)))
         return [tuple(cb[4 * k:4 * k + 4]) for k in range(nc.value)], list(tb[:nt.value])
+
+    def plan_profile(self, i):
+        out = (ctypes.c_uint64 * 8)()
+        _check(lib().dtgpu_batch_plan_profile(self._h, i, out))
+        keys = ["rec", "parents", "children", "emit", "ops", "init", "n_cmds", "n_tlist"]
+        return dict(zip(keys, list(out)))
 
     def doc_stats(self, i):
         """Diagnostics of document i after a run (see dtgpu_batch_doc_stats)."""

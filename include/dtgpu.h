@@ -172,6 +172,11 @@ uint64_t dtgpu_batch_algorithmic_bytes(dtgpu_batch *batch);
  * splits, and the insert phases find / block load / origin_right / run; scan and split
  * counts; total cycles/16). */
 dtgpu_status dtgpu_batch_doc_stats(dtgpu_batch *batch, size_t doc, uint32_t out[22]);
+/* Device planner cycle profile of one document (DTGPU_PLAN_PROF set at batch creation):
+ * out[0..5] cycles waiting for entry records, computing parent vectors, children + next pick,
+ * emitting retreat/advance entries, copying op runs, initialising; out[6] commands, out[7]
+ * retreat/advance entries. */
+dtgpu_status dtgpu_batch_plan_profile(dtgpu_batch *batch, size_t doc, uint64_t out[8]);
 /* Total merged ops (sum of ListOpLog::len()) in the batch. */
 uint64_t dtgpu_batch_total_lv(const dtgpu_batch *batch);
 void dtgpu_batch_free(dtgpu_batch *batch);

@@ -30,5 +30,29 @@ def main():
               flush=True)
 
 
+
+
+def plan_profile(names):
+    """Planner cycle profile (DTGPU_PLAN_PROF): python tools/kprof.py --plan friendsforever ..."""
+    os.environ["DTGPU_PLAN_PROF"] = "1"
+    import dt_amd
+    import golden_data as G
+    for a in names:
+        name, _, copies = a.partition("x")
+        copies = int(copies or 1)
+        b = dt_amd.Batch(docs=[G.dt_bytes(name)] * copies)
+        b.run_timed()
+        ms = b.last_times()
+        pr = [b.plan_profile(i) for i in range(0, copies, max(1, copies // 16))]
+        avg = {k: sum(x[k] for x in pr) / len(pr) for k in pr[0]}
+        tot = sum(avg[k] for k in ("rec", "parents", "children", "emit", "ops", "init"))
+        print(f"{a}: plan_ms={ms[0]:.2f} " + " ".join(f"{k}={avg[k] / 1e6:.2f}M({100 * avg[k] / max(tot, 1):.0f}%)"
+                                                     for k in ("rec", "parents", "children", "emit", "ops", "init"))
+              + f" cmds={avg['n_cmds']:.0f} tlist={avg['n_tlist']:.0f}", flush=True)
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:2] == ["--plan"]:
+        plan_profile(sys.argv[2:])
+    else:
+        main()
