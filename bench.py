@@ -3,8 +3,11 @@
 
 One step = one device pass of `checkout_tip()` over the whole batch resident in HBM: the
 friendsforever.dt workload (BASELINE.json configs[1]) replicated to --docs copies per GPU
-(weak scaling: every rank owns its own copies).  Host `.dt` decode + walk planning happen
-once when the batch is staged (untimed; reported separately as `host_stage_s`).
+(weak scaling: every rank owns its own copies).  The timed pass runs the walk planner
+(dt_plan.hip: spanning-tree walk + retreat/advance sets) and the replay + materialisation
+(dt_replay.hip) -- everything the reference's `checkout_tip()` does on a decoded oplog
+(crates/bench `complex/merge`).  The `.dt` decode happens once when the batch is staged
+(the reference benches it separately as `complex/decode`; reported here as `host_stage_s`).
 
 Contract: `python bench.py --gpus N --steps K --warmup W` prints ONE JSON line on rank 0.
 For N > 1 it is launched by torch.distributed.run, one process per GPU; per-rank times are
@@ -41,19 +44,21 @@ def parse():
 
 def cpu_baseline(data, budget_s, cores):
     """The CPU oracle (C restatement of the reference algorithm, one document per thread)
-    timed on a bounded sample of the same workload."""
+    timed on a bounded sample of the same workload: checkout_tip() on an already-decoded
+    oplog, as the reference's `complex/merge` bench times it."""
     from oracle.oracle import OpLog as OracleOpLog
-    t0 = time.perf_counter()
     o = OracleOpLog.load_from(data)
+    t0 = time.perf_counter()
     o.checkout_tip_bytes()
     one = time.perf_counter() - t0
     per_core = max(1, int(budget_s / max(one, 1e-4) / cores))
     n_lv = len(o)
     done = [0] * cores
+    logs = [OracleOpLog.load_from(data) for _ in range(cores)]
 
     def work(k):
         for _ in range(per_core):
-            OracleOpLog.load_from(data).checkout_tip_bytes()
+            logs[k].checkout_tip_bytes()
             done[k] += 1
 
     th = [threading.Thread(target=work, args=(k,)) for k in range(cores)]
@@ -65,7 +70,8 @@ def cpu_baseline(data, budget_s, cores):
     wall = time.perf_counter() - t0
     docs = sum(done)
     return {"value": docs * n_lv / wall, "unit": "merged ops/s", "cores": cores, "kind": "port",
-            "sample": f"{docs} x friendsforever.dt (decode+checkout_tip each) on {cores} host threads, {wall:.2f} s"}
+            "sample": f"{docs} x friendsforever.dt checkout_tip (decoded oplog, C oracle) on {cores} host threads, "
+                      f"{wall:.2f} s"}
 
 
 def main():
@@ -114,13 +120,14 @@ def main():
         dist.barrier()
 
     # timed region: K device passes over the resident batch
-    kernel_ms = []
+    kernel_ms, split = [], []
     batch.sync()
     if dist is not None:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         kernel_ms.append(batch.run_timed())
+        split.append(batch.last_times())
     batch.sync()
     elapsed = time.perf_counter() - t0
     if dist is not None:
@@ -132,8 +139,14 @@ def main():
     ms_per_step = elapsed * 1000.0 / args.steps
     value = total_lv * args.steps / elapsed
     avg_kernel_ms = statistics.mean(kernel_ms)
+    plan_ms = statistics.mean(x[0] for x in split)
+    replay_ms = statistics.mean(x[1] for x in split)
     alg_bytes = batch.algorithmic_bytes
     achieved = alg_bytes / (avg_kernel_ms / 1000.0) / 1e9
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", f"traffic_{args.workload}_{args.docs}.json")
+    if os.path.exists(tpath):   # HBM bytes per pass from a rocprofv3 PMC run of this command
+        traffic = json.load(open(tpath)).get("hbm_bytes_per_pass")
 
     out = {
         "metric": "merged ops/sec (whole node) for batched checkout",
@@ -150,13 +163,18 @@ def main():
         "data": "benchmark_data/friendsforever.dt replicated (byte-identical copies in distinct buffers)",
         "config": {"workload": f"{args.workload}.dt x {args.docs} docs per GPU (checkout_tip)",
                    "docs_per_gpu": args.docs, "merged_ops_per_doc": lv_per_doc,
-                   "timed": "device replay + materialisation of the whole batch (plan resident in HBM)",
+                   "timed": "device walk planning + replay + materialisation of the whole batch "
+                            "(decoded oplogs resident in HBM)",
                    "parallelism": f"dp{world} (documents sharded, no data-path collective)"},
         "docs_per_sec": n_total * args.steps / elapsed,
         "host_stage_s": host_stage_s,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel_ms": avg_kernel_ms, "algorithmic_bytes_per_launch": alg_bytes},
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "plan_kernel + replay_kernel (one checkout pass)",
+                     "kernel_ms": avg_kernel_ms, "plan_ms": plan_ms, "replay_ms": replay_ms,
+                     "algorithmic_bytes_per_launch": alg_bytes,
+                     "algorithmic_formula": "per doc: 16*op_runs + (8+4*parents)*graph_entries + 12*agent_runs "
+                                            "+ inserted_bytes + text_out_bytes (SURVEY.md 8d merge-only)"},
     }
     if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(data, args.cpu_seconds, args.cpu_cores)

@@ -890,31 +890,46 @@ Status build_plan_input(const HostOpLog &o, PlanInput &pi) {
         pi.tip.push_back(uint32_t(t));
         pi.tip.push_back(uint32_t(te));
     }
-    // Chain decomposition of the graph: every entry joins the chain whose current tail entry
-    // ends at one of its parents (the first such parent), or opens a new chain.  Each chain is
-    // then a causal chain, so a version's ancestor set is a prefix of every chain and a version
-    // vector over chains describes it exactly (the device planner diffs those vectors).
+    // Chain decomposition of the graph, in LV order: an entry joins a chain whose every op is
+    // already in the entry's history (the chain's length equals the entry's parent version
+    // vector at that chain), preferring its first parent's chain; with none such it opens a
+    // new chain.  Every chain is then a causal chain, so a version's ancestor set is a prefix
+    // of every chain and a version vector over chains describes it exactly (the device planner
+    // diffs those vectors).  The chain count stays near the history's concurrency width.
     std::vector<uint32_t> chain_of(ne), seq0(ne);
-    std::vector<uint32_t> tail;           // per chain: its last entry
-    std::vector<uint64_t> clen;           // per chain: ops so far
+    std::vector<uint64_t> clen;                    // per chain: ops so far
+    std::vector<std::vector<uint32_t>> prow(ne);   // per entry: parent vector over chains
     for (size_t i = 0; i < ne; i++) {
-        uint32_t c = 0xFFFFFFFFu;
-        for (uint32_t k = pi.poff[i]; k < pi.poff[i + 1] && c == 0xFFFFFFFFu; k++) {
+        std::vector<uint32_t> &row = prow[i];
+        row.assign(clen.size(), 0);
+        for (uint32_t k = pi.poff[i]; k < pi.poff[i + 1]; k++) {
             const uint32_t pe = pi.pent[k];
+            const std::vector<uint32_t> &pr = prow[pe];
+            for (size_t c = 0; c < pr.size(); c++) row[c] = std::max(row[c], pr[c]);
             const uint32_t pc = chain_of[pe];
-            if (pi.par[k] + 1 == E[pe].end && tail[pc] == pe) c = pc;
+            row[pc] = std::max<uint32_t>(row[pc], seq0[pe] + uint32_t(pi.par[k] - E[pe].start) + 1);
         }
+        uint32_t c = 0xFFFFFFFFu;
+        if (pi.poff[i + 1] > pi.poff[i]) {
+            const uint32_t pc = chain_of[pi.pent[pi.poff[i]]];
+            if (row[pc] == clen[pc]) c = pc;
+        }
+        for (size_t k = 0; k < clen.size() && c == 0xFFFFFFFFu; k++)
+            if (row[k] == clen[k]) c = uint32_t(k);
         if (c == 0xFFFFFFFFu) {
-            c = uint32_t(tail.size());
-            tail.push_back(0);
+            c = uint32_t(clen.size());
             clen.push_back(0);
+            if (clen.size() > PLAN_CHAIN_LIMIT) {   // too wide for the device planner
+                pi.device_ok = false;
+                return OK;
+            }
+            row.push_back(0);
         }
         chain_of[i] = c;
         seq0[i] = uint32_t(clen[c]);
         clen[c] += E[i].end - E[i].start;
-        tail[c] = uint32_t(i);
     }
-    pi.n_chains = uint32_t(tail.size());
+    pi.n_chains = uint32_t(clen.size());
     pi.pch.resize(pi.par.size());
     pi.pcnt.resize(pi.par.size());
     for (size_t k = 0; k < pi.par.size(); k++) {

@@ -127,6 +127,7 @@ struct PlanInput {
     bool device_ok = true;
 };
 constexpr uint32_t EREC_WORDS = 20;
+constexpr uint32_t PLAN_CHAIN_LIMIT = 512;   // = PLAN_MAX_AGENTS of the device planner
 Status build_plan_input(const HostOpLog &o, PlanInput &pi);
 
 uint64_t text_hash(const uint8_t *t, size_t n);

@@ -1,0 +1,17 @@
+#!/bin/bash
+# Round-end evidence on the GPU box: bench JSON line, rocprofv3 kernel-trace stats of the same
+# command, and FETCH_SIZE / WRITE_SIZE PMC passes (separate runs) for the roofline traffic.
+# Usage (inside gpurun): bash tools/bench_profile.sh OUTDIR [bench args...]
+OUT=$1; shift
+ARGS=("$@")
+mkdir -p "$OUT"
+timeout -k 10 400 python -u bench.py "${ARGS[@]}" > "$OUT/bench.json" 2> "$OUT/bench.err"
+echo "bench rc=$?"
+cd /tmp && export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run -f csv -- python -u bench.py "${ARGS[@]}" --no-cpu-baseline --steps 3 --warmup 1 > "$OUT/trace.log" 2>&1
+echo "trace rc=$?"
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run -f csv -- python -u bench.py "${ARGS[@]}" --no-cpu-baseline --steps 1 --warmup 0 > "$OUT/fetch.log" 2>&1
+echo "fetch rc=$?"
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run -f csv -- python -u bench.py "${ARGS[@]}" --no-cpu-baseline --steps 1 --warmup 0 > "$OUT/write.log" 2>&1
+echo "write rc=$?"
