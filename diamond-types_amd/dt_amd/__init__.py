@@ -114,6 +114,9 @@ def lib():
     L.dtgpu_text_hash.argtypes = [ctypes.c_char_p, sz]
     L.dtgpu_text_hash.restype = u64
     L.dtgpu_device_count.restype = c
+    L.dtgpu_synth_ops.argtypes = [u64, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32), sz]
+    L.dtgpu_synth_ops.restype = sz
+    L.dtgpu_synth_oplog.argtypes = [u64, ctypes.c_uint32, ctypes.POINTER(vp)]
     L.dtgpu_status_str.argtypes = [c]
     L.dtgpu_status_str.restype = ctypes.c_char_p
     _lib = L
@@ -376,3 +379,27 @@ def batch_checkout(docs, **kw):
 
 def device_count() -> int:
     return lib().dtgpu_device_count()
+
+
+def synth_ops(doc, target_ops=5000):
+    """Op list of synthetic document `doc` (dt_synth.cpp): (n_agents, [(agent, kind, pos, len,
+    text, parents)])."""
+    na = ctypes.c_uint32()
+    n = lib().dtgpu_synth_ops(doc, target_ops, ctypes.byref(na), None, 0)
+    buf = (ctypes.c_uint32 * max(1, n))()
+    lib().dtgpu_synth_ops(doc, target_ops, ctypes.byref(na), buf, n)
+    w = list(buf[:n])
+    ops, i = [], 0
+    while i < n:
+        agent, kind, pos, ln, c0, c1, np_ = w[i:i + 7]
+        text = bytes([c0, c1][:ln]).decode() if kind == 0 else ""
+        ops.append((agent, kind, pos, ln, text, w[i + 7:i + 7 + np_]))
+        i += 7 + np_
+    return na.value, ops
+
+
+def synth_oplog(doc, target_ops=5000):
+    """Synthetic document `doc` built as a ListOpLog."""
+    h = ctypes.c_void_p()
+    _check(lib().dtgpu_synth_oplog(doc, target_ops, ctypes.byref(h)))
+    return ListOpLog(h.value)

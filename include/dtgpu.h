@@ -189,6 +189,16 @@ dtgpu_status dtgpu_batch_checkout(const uint8_t *const *docs, const size_t *lens
  * wrapping.  Computed on device for the RCCL length/hash gather; exported for checking. */
 uint64_t dtgpu_text_hash(const uint8_t *text, size_t len);
 
+/* ---- synthetic concurrent documents (BASELINE.json configs[3]) ---------------------------- */
+
+/* Deterministic synthetic document `doc` (seed 0xD1A00000 + doc, 4..16 agents, epochs of
+ * concurrent edits merged at their ends, >= target_ops LVs; dt_synth.cpp).  The op list is
+ * written as variable-length uint32 records {agent, kind (0 ins, 1 del), pos, len, char0,
+ * char1, n_parents, parents...}; returns the words needed (writes only when they fit in cap). */
+size_t dtgpu_synth_ops(uint64_t doc, uint32_t target_ops, uint32_t *n_agents, uint32_t *out, size_t cap);
+/* The same document built as an oplog (agents "a0".."a15"). */
+dtgpu_status dtgpu_synth_oplog(uint64_t doc, uint32_t target_ops, dtgpu_oplog **out);
+
 /* Number of HIP devices visible (0 when there is no GPU). */
 int dtgpu_device_count(void);
 const char *dtgpu_status_str(dtgpu_status status);

@@ -227,3 +227,19 @@ def test_host_planner_path_still_exact():
     b.run()
     b.sync()
     assert b.text(0) == want
+
+
+def test_synthetic_docs_vs_oracle():
+    """Synthetic concurrent docs (4-16 agents, epochs of concurrent edits): device checkout ==
+    CPU oracle, and the device plan == the host plan."""
+    from test_synth import oracle_from_synth
+    docs = list(range(12))
+    oplogs = [dt_amd.synth_oplog(d, 5000) for d in docs]
+    b = dt_amd.Batch(oplogs=oplogs)
+    assert b.host_planned() == [0] * len(docs)
+    b.run()
+    b.sync()
+    for i, d in enumerate(docs):
+        _, _, o = oracle_from_synth(d, 5000)
+        assert b.text(i) == o.checkout_tip_bytes(), d
+        _same_plan(b.plan(i), _host_plan(oplogs[i]))

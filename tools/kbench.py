@@ -14,10 +14,18 @@ def main():
     name = sys.argv[1]
     counts = [int(x) for x in sys.argv[2].split(",")]
     reps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
-    data = G.dt_bytes(name)
+    distinct = None
+    if name.startswith("synth"):   # synth[:distinct] -- synthetic concurrent docs (dt_synth.cpp)
+        distinct = int(name.split(":")[1]) if ":" in name else 256
+        pool = [dt_amd.synth_oplog(i, 5000) for i in range(distinct)]
+    else:
+        data = G.dt_bytes(name)
     for n in counts:
         t = time.time()
-        b = dt_amd.Batch(docs=[data] * n)
+        if distinct:
+            b = dt_amd.Batch(oplogs=[pool[i % distinct] for i in range(n)])
+        else:
+            b = dt_amd.Batch(docs=[data] * n)
         stage = time.time() - t
         b.run(); b.sync()
         ms, split = [], []
