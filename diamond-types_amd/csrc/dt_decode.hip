@@ -1,0 +1,1142 @@
+// dt_decode.hip -- batched `.dt` decode on MI355X.
+//
+// One 64-lane wavefront decodes one document.  The `.dt` grammar is a sequential byte stream
+// (chunk headers, LEB128 varints, run records whose cursor depends on the previous record), so
+// the parse itself runs wave-uniformly: bytes come out of a 256-byte register window (lane i
+// holds bytes 4i..4i+3, one coalesced load per refill, `v_readlane` to extract), and every
+// parse variable lives in scalar registers.  Everything with data parallelism runs across the
+// 64 lanes: LZ4 literal and match copies (a match with offset < length is periodic, so lane k
+// copies byte `k mod offset`), UTF-8 validation (lead / continuation checks per byte, ASCII
+// chunks by one ballot), character counting inside content runs (ballot + popcount),
+// per-LV content offsets, CRC-32C (64 segment CRCs merged with the x^(8n) mod P combine), the
+// per-agent seq -> LV lookup lists and the output records (buffered one per lane, flushed as
+// coalesced 16-byte stores).
+//
+// Reference behaviour followed, by function:
+//   header / chunk reader      src/list/encoding/decode_oplog.rs:590-615, decode_tools.rs:185-268
+//   varints / zigzag           src/list/encoding/leb.rs:113-178, 305-323
+//   LZ4 block                  decode_oplog.rs:621-633 (lz4_flex::decompress, raw block)
+//   FileInfo / agent names     decode_oplog.rs:197-227, agent_assignment/mod.rs:80-100
+//   StartBranch                decode_oplog.rs:652-664, read_version :70-93
+//   PatchContent / runs        decode_oplog.rs:383-425, decode_tools.rs:133-195
+//   OpVersions                 read_next_agent_assignment, decode_oplog.rs:29-68
+//   OpTypeAndPosition          ReadPatchesIter::next_internal, decode_oplog.rs:289-337, 731-778
+//   RLE op-run append          src/list/op_metrics.rs:235-293 (push_op_internal, oplog.rs:159-175)
+//   OpParents / graph push     decode_oplog.rs:95-148, 856-913; graph/mod.rs:85-128
+//   frontier advance           src/frontier.rs:251-279
+//   CRC-32C                    decode_oplog.rs:940-955, src/encoding/tools.rs:111-115
+// The host decoder (dt_host.cpp decode_dt) is the same algorithm in sequential C++; the parity
+// tests compare the two array by array, and status by status on corrupted inputs.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dt_decode.hpp"
+
+namespace dtgpu {
+namespace ddec {
+
+enum : int {
+    S_OK = 0, InvalidMagic = 1, UnsupportedProtocolVersion = 2, BaseVersionUnknown = 4, UnknownChunk = 5,
+    LZ4DecompressionError = 7, CompressedDataMissing = 8, MissingChunk = 10, InvalidLength = 11,
+    UnexpectedEOF = 12, InvalidUTF8 = 13, InvalidVarInt = 15, InvalidContent = 16, ChecksumFailed = 18,
+    ErrCheckout = 64, ErrCapacity = 65, Defer = int(DECODE_DEFER),
+};
+
+#define TRY(x) do { const int s_ = (x); if (s_) return s_; } while (0)
+
+constexpr uint32_t CRC_POLY = 0x82F63B78u;
+constexpr uint64_t LIM31 = 1ull << 31;
+
+__device__ __forceinline__ uint32_t lane() { return __lane_id(); }
+__device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t l) {
+    return uint32_t(__builtin_amdgcn_readlane(int(v), int(l)));
+}
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ uint64_t lt_mask() { return (1ull << lane()) - 1ull; }
+__device__ __forceinline__ uint32_t popc(uint64_t m) { return uint32_t(__popcll(m)); }
+__device__ __forceinline__ uint32_t ctz(uint64_t m) { return uint32_t(__ffsll((unsigned long long)m) - 1); }
+// Stores of this wave become visible to its later loads (same CU; workgroup scope).
+__device__ __forceinline__ void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+
+// ---------------------------------------------------------------------------------------------
+// byte windows and readers
+// ---------------------------------------------------------------------------------------------
+struct Win {
+    const uint8_t *base;   // 4-B aligned, readable for 256 B past any valid offset
+    uint32_t wpos;         // window start (uniform)
+    uint32_t w;            // lane i: bytes wpos + 4i .. + 3
+};
+__device__ __forceinline__ uint32_t wbyte(Win &W, uint32_t off) {
+    uint32_t d = off - W.wpos;
+    if (d >= 256u) {
+        W.wpos = off & ~3u;
+        W.w = *reinterpret_cast<const uint32_t *>(W.base + W.wpos + 4u * lane());
+        d = off - W.wpos;
+    }
+    return (rdl(W.w, d >> 2) >> ((d & 3u) << 3)) & 0xFFu;
+}
+
+// A reader over one byte stream: source s selects the register window (the streams that the
+// main loop interleaves each keep their own): 0 document (chunk headers), 1 LZ4 buffer,
+// 2 OpVersions, 3 OpTypeAndPosition, 4 / 5 ContentIsKnown of inserts / deletes, 6 OpParents.
+struct Rd { uint32_t s, p, n; };
+enum : uint32_t { SRC_DOC = 0, SRC_LZ = 1, SRC_AV = 2, SRC_TP = 3, SRC_RUNS_INS = 4, SRC_RUNS_DEL = 5, SRC_HIST = 6 };
+
+struct Ctx {
+    Win w0, w1, w2, w3, w4, w5, w6;
+    const uint8_t *in;   // the document
+    uint8_t *lz;         // its decompressed LZ4 buffer
+    __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t off) {
+        switch (s) {
+            case SRC_LZ: return wbyte(w1, off);
+            case SRC_AV: return wbyte(w2, off);
+            case SRC_TP: return wbyte(w3, off);
+            case SRC_RUNS_INS: return wbyte(w4, off);
+            case SRC_RUNS_DEL: return wbyte(w5, off);
+            case SRC_HIST: return wbyte(w6, off);
+            default: return wbyte(w0, off);
+        }
+    }
+    __device__ __forceinline__ const uint8_t *ptr(uint32_t s) const { return s == SRC_LZ ? lz : in; }
+
+    // unsigned LEB128 (leb.rs:113-178)
+    __device__ __forceinline__ int varint_at(const Rd &r, uint64_t &v, uint32_t &used) {
+        uint64_t x = 0;
+        for (uint32_t i = 0; i < r.n; i++) {
+            if (i == 10) return InvalidVarInt;
+            const uint32_t b = byte(r.s, r.p + i);
+            if (i == 9 && (b & 0x7fu) > 1u) return InvalidVarInt;
+            x |= uint64_t(b & 0x7fu) << (7 * i);
+            if (b < 0x80u) { v = x; used = i + 1; return S_OK; }
+        }
+        return r.n >= 10 ? InvalidVarInt : UnexpectedEOF;
+    }
+    __device__ __forceinline__ int u64v(Rd &r, uint64_t &v) {
+        if (!r.n) return UnexpectedEOF;
+        uint32_t used;
+        TRY(varint_at(r, v, used));
+        r.p += used; r.n -= used;
+        return S_OK;
+    }
+    __device__ __forceinline__ int u32v(Rd &r, uint64_t &v) {
+        TRY(u64v(r, v));
+        return v >= 0xFFFFFFFFull ? InvalidVarInt : S_OK;
+    }
+    __device__ __forceinline__ int peek_u32(const Rd &r, bool &has, uint64_t &v) {
+        has = false;
+        if (!r.n) return S_OK;
+        uint32_t used;
+        TRY(varint_at(r, v, used));
+        if (v >= 0xFFFFFFFFull) return InvalidVarInt;
+        has = true;
+        return S_OK;
+    }
+    __device__ __forceinline__ int zigzag(Rd &r, int64_t &v) {   // "old" sign-magnitude zigzag (leb.rs:305-323)
+        uint64_t u;
+        TRY(u64v(r, u));
+        v = int64_t(u >> 1) * ((u & 1) ? -1 : 1);
+        return S_OK;
+    }
+    // ChunkReader (decode_tools.rs:185-268)
+    __device__ __forceinline__ static bool known_chunk(uint64_t t) {
+        return t == 1 || t == 2 || t == 3 || t == 4 || t == 5 || t == 10 || t == 11 || t == 12 || t == 13 ||
+               t == 14 || t == 20 || t == 21 || t == 22 || t == 23 || t == 24 || t == 25 || t == 27 || t == 100;
+    }
+    __device__ __forceinline__ int next_chunk(Rd &r, uint64_t &type, Rd &body) {
+        for (;;) {
+            uint64_t t, len;
+            TRY(u32v(r, t));
+            TRY(u64v(r, len));
+            if (len > r.n) return InvalidLength;
+            body = Rd{r.s, r.p, uint32_t(len)};
+            r.p += uint32_t(len); r.n -= uint32_t(len);
+            if (known_chunk(t)) { type = t; return S_OK; }
+        }
+    }
+    __device__ __forceinline__ int chunk_if(Rd &r, uint64_t want, bool &found, Rd &body) {
+        found = false;
+        bool has; uint64_t t;
+        TRY(peek_u32(r, has, t));
+        if (!has || t != want) return S_OK;
+        uint64_t tt;
+        TRY(next_chunk(r, tt, body));
+        found = true;
+        return S_OK;
+    }
+    __device__ __forceinline__ int expect_chunk(Rd &r, uint64_t want, Rd &body) {
+        uint64_t t;
+        TRY(next_chunk(r, t, body));
+        return t == want ? S_OK : MissingChunk;
+    }
+};
+
+// ---------------------------------------------------------------------------------------------
+// lane-parallel helpers
+// ---------------------------------------------------------------------------------------------
+// UTF-8 validity (std::str::from_utf8): every lead byte carries exactly its continuation bytes,
+// no overlong forms, no surrogates, <= U+10FFFF; every continuation byte lies inside the span
+// of the nearest preceding lead.  ASCII windows are cleared by one ballot.
+__device__ __forceinline__ bool utf8_ok(const uint8_t *s, uint32_t n, bool &ascii) {
+    ascii = true;
+    for (uint32_t i = 0; i < n; i += 64) {
+        const uint32_t j = i + lane();
+        const uint32_t c = j < n ? s[j] : 0u;
+        if (!ballot(c >= 0x80u)) continue;
+        ascii = false;
+        bool bad = false;
+        if (j < n && c >= 0x80u) {
+            if ((c & 0xC0u) == 0x80u) {   // continuation: covered by the nearest lead?
+                bool covered = false, found = false;
+                for (uint32_t k = 1; k <= 3 && k <= j && !found; k++) {
+                    const uint32_t b = s[j - k];
+                    if ((b & 0xC0u) == 0x80u) continue;
+                    found = true;
+                    const uint32_t L = (b & 0xE0u) == 0xC0u ? 2u : (b & 0xF0u) == 0xE0u ? 3u : (b & 0xF8u) == 0xF0u ? 4u : 0u;
+                    covered = L > k;
+                }
+                bad = !covered;
+            } else {
+                uint32_t L, cp;
+                if ((c & 0xE0u) == 0xC0u) { L = 2; cp = c & 0x1Fu; }
+                else if ((c & 0xF0u) == 0xE0u) { L = 3; cp = c & 0x0Fu; }
+                else if ((c & 0xF8u) == 0xF0u) { L = 4; cp = c & 0x07u; }
+                else { L = 0; cp = 0; bad = true; }
+                if (!bad && j + L > n) bad = true;
+                for (uint32_t k = 1; !bad && k < L; k++) {
+                    const uint32_t b = s[j + k];
+                    if ((b & 0xC0u) != 0x80u) bad = true;
+                    cp = (cp << 6) | (b & 0x3Fu);
+                }
+                if (!bad && ((L == 2 && cp < 0x80u) || (L == 3 && cp < 0x800u) || (L == 4 && cp < 0x10000u))) bad = true;
+                if (!bad && (cp > 0x10FFFFu || (cp >= 0xD800u && cp <= 0xDFFFu))) bad = true;
+            }
+        }
+        if (ballot(bad)) return false;
+    }
+    return true;
+}
+
+// Byte length of the first `want` chars of validated UTF-8 text (ContentRuns::next's walk):
+// chars = min(want, chars in text).
+__device__ __forceinline__ void walk_chars(const uint8_t *s, uint32_t n, uint64_t want, bool ascii, uint32_t &bytes, uint64_t &chars) {
+    if (ascii) {
+        chars = want < n ? want : n;
+        bytes = uint32_t(chars);
+        return;
+    }
+    uint64_t c = 0;
+    for (uint32_t i = 0; i < n; i += 64) {
+        const uint32_t j = i + lane();
+        const bool st = j < n && (s[j] & 0xC0u) != 0x80u;
+        uint64_t m = ballot(st);
+        const uint32_t k = popc(m);
+        if (c + k > want) {   // the char after the `want`-th starts in this window
+            for (uint64_t skip = want - c; skip; skip--) m &= m - 1;
+            bytes = i + ctz(m);
+            chars = want;
+            return;
+        }
+        c += k;
+    }
+    bytes = n;
+    chars = c;
+}
+
+// One output record per lane, flushed as a coalesced quad store per 64 records.
+struct Quads {
+    uint32_t a, b, c, d;   // lane k: record k of the current group
+    uint32_t n;            // records buffered (uniform)
+    uint64_t at;           // records already flushed (uniform)
+    __device__ __forceinline__ void init() { a = b = c = d = 0; n = 0; at = 0; }
+    __device__ __forceinline__ void push(uint32_t x, uint32_t y, uint32_t z, uint32_t w, uint4 *dst) {
+        const bool me = lane() == n;
+        a = me ? x : a; b = me ? y : b; c = me ? z : c; d = me ? w : d;
+        if (++n == 64) flush(dst);
+    }
+    __device__ __forceinline__ void flush(uint4 *dst) {
+        if (lane() < n) dst[at + lane()] = make_uint4(a, b, c, d);
+        at += n;
+        n = 0;
+    }
+    __device__ uint64_t count() const { return at + n; }
+};
+
+// CRC-32C combine (zlib's crc32_combine scheme over the reflected polynomial)
+__device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {
+    if (!a) return 0;
+    uint32_t m = 1u << 31, p = 0;
+    for (;;) {
+        if (a & m) {
+            p ^= b;
+            if ((a & (m - 1)) == 0) break;
+        }
+        m >>= 1;
+        b = (b & 1u) ? (b >> 1) ^ CRC_POLY : b >> 1;
+    }
+    return p;
+}
+__device__ __forceinline__ uint32_t x2nmodp(const uint32_t *x2n, uint64_t n, uint32_t k) {
+    uint32_t p = 1u << 31;
+    while (n) {
+        if (n & 1) p = multmodp(x2n[k & 31], p);
+        n >>= 1;
+        k++;
+    }
+    return p;
+}
+// CRC-32C of s[0, n): 64 lane segments (4-B aligned), merged in order.
+__device__ __forceinline__ uint32_t crc32c_par(const uint8_t *s, uint32_t n, const uint32_t *T, const uint32_t *x2n) {
+    const uint32_t S = (((n + 63) / 64) + 3) & ~3u;
+    const uint32_t b0 = lane() * S;
+    const uint32_t e0 = b0 < n ? (b0 + S < n ? b0 + S : n) : b0;
+    uint32_t c = ~0u;
+    uint32_t i = b0;
+    for (; i + 4 <= e0; i += 4) {
+        c ^= *reinterpret_cast<const uint32_t *>(s + i);
+        c = T[c & 0xFFu] ^ (c >> 8);
+        c = T[c & 0xFFu] ^ (c >> 8);
+        c = T[c & 0xFFu] ^ (c >> 8);
+        c = T[c & 0xFFu] ^ (c >> 8);
+    }
+    for (; i < e0; i++) c = T[(c ^ s[i]) & 0xFFu] ^ (c >> 8);
+    c = ~c;
+    if (e0 <= b0) c = 0;   // empty segment
+    const uint32_t op_full = x2nmodp(x2n, S, 3);
+    uint32_t crc = rdl(c, 0);
+    for (uint32_t l = 1; l < 64; l++) {
+        const uint32_t sb = l * S;
+        if (sb >= n) break;
+        const uint32_t len = sb + S <= n ? S : n - sb;
+        crc = multmodp(len == S ? op_full : x2nmodp(x2n, len, 3), crc) ^ rdl(c, l);
+    }
+    return crc;
+}
+
+// LZ4 raw block (lz4_flex::decompress; decode_oplog.rs:621-633) from the document into dst.
+__device__ __forceinline__ bool lz4_block(Ctx &C, const Rd &src, uint8_t *dst, uint32_t out_len) {
+    const uint8_t *sp = C.in + src.p;
+    const uint64_t n = src.n;
+    uint64_t ip = 0, op = 0, fenced = 0;
+    while (ip < n) {
+        const uint32_t tok = C.byte(0, src.p + uint32_t(ip++));
+        uint64_t lit = tok >> 4;
+        if (lit == 15) {
+            uint32_t b;
+            do {
+                if (ip >= n) return false;
+                b = C.byte(0, src.p + uint32_t(ip++));
+                lit += b;
+            } while (b == 255);
+        }
+        if (ip + lit > n || op + lit > out_len) return false;
+        for (uint64_t k = lane(); k < lit; k += 64) dst[op + k] = sp[ip + k];
+        ip += lit;
+        op += lit;
+        if (ip >= n) break;
+        if (ip + 2 > n) return false;
+        const uint64_t off = C.byte(0, src.p + uint32_t(ip)) | (C.byte(0, src.p + uint32_t(ip + 1)) << 8);
+        ip += 2;
+        if (off == 0 || off > op) return false;
+        uint64_t ml = tok & 15u;
+        if (ml == 15) {
+            uint32_t b;
+            do {
+                if (ip >= n) return false;
+                b = C.byte(0, src.p + uint32_t(ip++));
+                ml += b;
+            } while (b == 255);
+        }
+        ml += 4;
+        if (op + ml > out_len) return false;
+        // the match reads [op - off, op - off + min(off, ml)): make earlier stores visible
+        if (op - off + (off < ml ? off : ml) > fenced) {
+            wave_fence();
+            fenced = op;
+        }
+        if (off >= ml) {
+            for (uint64_t k = lane(); k < ml; k += 64) dst[op + k] = dst[op - off + k];
+        } else {   // overlapping match: the output repeats with period `off`
+            const uint32_t o32 = uint32_t(off);
+            for (uint32_t k = lane(); k < ml; k += 64) dst[op + k] = dst[op - off + (k % o32)];
+        }
+        op += ml;
+    }
+    wave_fence();
+    return op == out_len;
+}
+
+// ---------------------------------------------------------------------------------------------
+// the document decoder
+// ---------------------------------------------------------------------------------------------
+struct Lds {                 // per-wave tables, F = max file agents of the batch
+    uint32_t *fmap;          // file agent -> agent id
+    uint32_t *fseq;          // file agent -> next seq (the assignment cursor)
+    uint32_t *noff, *nlen;   // agent id -> name bytes in the document
+    uint32_t *acnt, *aoff;   // agent id -> lookup list (count, offset)
+    uint32_t *acur;          // agent id -> last lookup hit
+    uint32_t *amono;         // agent id -> 1 if its runs' seq ranges increase in LV order
+    uint32_t *crc;           // CRC-32C table (256)
+    uint32_t *fr;            // frontier compaction scratch (64)
+};
+
+struct CRuns {               // ContentIsKnown run iterator (ReadPatchContentIter)
+    uint32_t present, ascii;
+    Rd runs, text;
+    uint32_t t0;                 // where the text started
+    uint32_t pb, pb_known;
+    uint64_t pb_len;
+    Rd pb_s;
+};
+
+template <bool SIZE>
+__device__ __forceinline__ int content_str(Ctx &C, Rd &chunks, Rd &comp, bool has_comp, Rd &text, uint32_t &ascii) {
+    uint64_t t; Rd c;
+    TRY(C.next_chunk(chunks, t, c));
+    if (t != 13 && t != 14) return MissingChunk;
+    uint64_t dt;
+    TRY(C.u32v(c, dt));
+    if (dt != 4) return UnknownChunk;
+    bool asc = true;
+    if (t == 13) {
+        if (!SIZE && !utf8_ok(C.in + c.p, c.n, asc)) return InvalidUTF8;
+        text = c;
+        ascii = asc;
+        return S_OK;
+    }
+    uint64_t len;
+    TRY(C.u64v(c, len));
+    if (!has_comp) return CompressedDataMissing;
+    if (len > comp.n) return UnexpectedEOF;
+    text = Rd{comp.s, comp.p, uint32_t(len)};
+    comp.p += uint32_t(len); comp.n -= uint32_t(len);
+    if (!SIZE && !utf8_ok(C.lz + text.p, text.n, asc)) return InvalidUTF8;
+    ascii = asc;
+    return S_OK;
+}
+
+__device__ __forceinline__ int cruns_next(Ctx &C, CRuns &R, bool &has, uint64_t &len, bool &known, Rd &s) {
+    if (R.pb) {
+        R.pb = 0; has = true; len = R.pb_len; known = R.pb_known; s = R.pb_s;
+        return S_OK;
+    }
+    if (!R.runs.n) {
+        if (!R.text.n) { has = false; return S_OK; }
+        return UnexpectedEOF;
+    }
+    uint64_t x;
+    TRY(C.u64v(R.runs, x));
+    len = x >> 1;
+    known = x & 1;
+    s = Rd{R.text.s, R.text.p, 0};
+    if (known) {
+        uint32_t b; uint64_t c;
+        walk_chars(C.ptr(R.text.s) + R.text.p, R.text.n, len, R.ascii, b, c);
+        if (c != len) return UnexpectedEOF;
+        s.n = b;
+        R.text.p += b; R.text.n -= b;
+    }
+    has = true;
+    return S_OK;
+}
+
+struct Out {                 // this document's output arenas
+    uint4 *aruns, *pre, *ops;
+    uint32_t *alist;         // triples (seq, lv, len) per agent, as quads
+    uint2 *ent;
+    uint32_t *poff, *par, *cbyte, *ver;
+    uint2 *agents;
+    uint8_t *content;
+};
+
+// Per-agent seq -> LV lookup lists from the agent runs (agent_assignment seq_to_lv): a stable
+// counting sort by agent, so each list is in insertion order like the host's agent_seqs.  An
+// agent whose seq ranges increase along the list is marked monotone (any hit is the only one).
+__device__ __forceinline__ int build_lookup(const Out &O, const Lds &L, uint32_t n_agents, uint32_t n_aruns) {
+    for (uint32_t a = lane(); a < n_agents; a += 64) { L.acnt[a] = 0; L.acur[a] = 0; L.amono[a] = 1; }
+    __syncthreads();
+    for (uint32_t i = lane(); i < n_aruns; i += 64) {
+        const uint4 r = O.aruns[i];
+        if (r.y) atomicAdd(&L.acnt[r.z], 1u);
+    }
+    __syncthreads();
+    if (lane() == 0) {
+        uint32_t s = 0;
+        for (uint32_t a = 0; a < n_agents; a++) { L.aoff[a] = s; s += L.acnt[a]; L.acnt[a] = 0; }
+    }
+    __syncthreads();
+    for (uint32_t i0 = 0; i0 < n_aruns; i0 += 64) {
+        const uint32_t i = i0 + lane();
+        uint4 r = make_uint4(0, 0, 0xFFFFFFFFu, 0);
+        if (i < n_aruns) r = O.aruns[i];
+        bool todo = i < n_aruns && r.y != 0;
+        while (ballot(todo)) {   // one agent per round, lanes keep their LV order
+            const uint32_t lead = rdl(todo ? r.z : 0xFFFFFFFFu, ctz(ballot(todo)));
+            const uint64_t m = ballot(todo && r.z == lead);
+            if (todo && r.z == lead) {
+                const uint32_t k = L.aoff[lead] + L.acnt[lead] + popc(m & lt_mask());
+                reinterpret_cast<uint4 *>(O.alist)[k] = make_uint4(r.w, r.x, r.y, 0);
+                todo = false;
+            }
+            __syncthreads();
+            if (lane() == 0) L.acnt[lead] += popc(m);
+            __syncthreads();
+        }
+    }
+    wave_fence();
+    // an entry below its predecessor's end clears its agent's monotone flag
+    for (uint32_t a = 0; a < n_agents; a++) {
+        const uint32_t off = L.aoff[a], cnt = L.acnt[a];
+        bool bad = false;
+        for (uint32_t k = 1 + lane(); k < cnt; k += 64) {
+            const uint4 p = reinterpret_cast<const uint4 *>(O.alist)[off + k - 1];
+            const uint4 q = reinterpret_cast<const uint4 *>(O.alist)[off + k];
+            if (uint64_t(q.x) < uint64_t(p.x) + p.z) bad = true;
+        }
+        if (ballot(bad) && lane() == 0) L.amono[a] = 0;
+    }
+    __syncthreads();
+    return S_OK;
+}
+
+// seq -> LV in agent a's list (seq_to_lv: the first run in insertion order that holds seq).
+// Monotone lists: a 64-entry window from the last hit, else binary search.  Others: scan in
+// insertion order, 64 runs at a time.
+__device__ __forceinline__ int64_t lookup_lv(const Out &O, const Lds &L, uint32_t a, uint64_t seq) {
+    const uint32_t off = L.aoff[a], cnt = L.acnt[a];
+    if (!cnt || seq >= LIM31) return -1;
+    const uint4 *lst = reinterpret_cast<const uint4 *>(O.alist) + off;
+    if (!L.amono[a]) {
+        for (uint32_t k0 = 0; k0 < cnt; k0 += 64) {
+            const uint32_t k = k0 + lane();
+            uint4 e = make_uint4(0, 0, 0, 0);
+            if (k < cnt) e = lst[k];
+            const uint64_t m = ballot(k < cnt && seq >= e.x && seq < uint64_t(e.x) + e.z);
+            if (m) {
+                const uint32_t l = ctz(m);
+                return int64_t(rdl(e.y, l)) + int64_t(seq - rdl(e.x, l));
+            }
+        }
+        return -1;
+    }
+    uint32_t start = L.acur[a];
+    start = start >= 4 ? start - 4 : 0;
+    const uint32_t k = start + lane();
+    uint4 e = make_uint4(0, 0, 0, 0);
+    if (k < cnt) e = lst[k];
+    const bool hit = k < cnt && seq >= e.x && seq < uint64_t(e.x) + e.z;
+    const uint64_t m = ballot(hit);
+    if (m) {
+        const uint32_t l = ctz(m);
+        if (lane() == 0) L.acur[a] = start + l;
+        return int64_t(rdl(e.y, l)) + int64_t(seq - rdl(e.x, l));
+    }
+    uint32_t lo = 0, hi = cnt;   // first entry with seq start > seq
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        const uint32_t s = rdl(lst[mid].x, 0);
+        if (s <= seq) lo = mid + 1; else hi = mid;
+    }
+    if (!lo) return -1;
+    const uint4 f = lst[lo - 1];
+    const uint32_t fs = rdl(f.x, 0), fl = rdl(f.y, 0), fn = rdl(f.z, 0);
+    if (seq >= uint64_t(fs) + fn) return -1;
+    if (lane() == 0) L.acur[a] = lo - 1;
+    return int64_t(fl) + int64_t(seq - fs);
+}
+
+template <bool SIZE>
+__device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDesc &D, DecodeResult &R, const Lds &L) {
+    Ctx C;
+    C.in = P.in + D.in_off;
+    C.lz = P.lz + D.lz_off;
+    C.w0 = Win{C.in, 0x80000000u, 0};
+    C.w1 = Win{C.lz, 0x80000000u, 0};
+    C.w2 = C.w3 = C.w4 = C.w5 = C.w6 = C.w0;
+    const uint32_t len = D.in_len;
+    Out O;
+    O.aruns = reinterpret_cast<uint4 *>(P.aruns) + D.arun_off;
+    O.alist = P.alist + 4 * D.arun_off;
+    O.pre = reinterpret_cast<uint4 *>(P.pre) + D.pre_off;
+    O.ops = reinterpret_cast<uint4 *>(P.ops) + D.op_off;
+    O.ent = reinterpret_cast<uint2 *>(P.ent) + D.ent_off;
+    O.poff = P.poff + D.poff_off;
+    O.par = P.par + D.par_off;
+    O.cbyte = P.cbyte + D.lv_off;
+    O.ver = P.ver + D.ver_off;
+    O.agents = reinterpret_cast<uint2 *>(P.agents) + D.agent_off;
+    O.content = P.content + D.content_off;
+
+    uint64_t t_prev = __builtin_amdgcn_s_memtime();
+    auto prof_mark = [&](int k) {   // core-clock cycles per phase (DecodeResult::prof)
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        R.prof[k] += uint32_t(t - t_prev);
+        t_prev = t;
+    };
+    if (len < 8) return UnexpectedEOF;
+    {
+        const char *magic = "DMNDTYPS";
+        for (uint32_t i = 0; i < 8; i++)
+            if (C.byte(0, i) != uint32_t(uint8_t(magic[i]))) return InvalidMagic;
+    }
+    Rd r{0, 8, len - 8};
+    uint64_t pv;
+    TRY(C.u64v(r, pv));
+    if (pv != 0) return UnsupportedProtocolVersion;
+
+    Rd comp{SRC_LZ, 0, 0};
+    bool has_comp = false;
+    {
+        bool found; Rd c;
+        TRY(C.chunk_if(r, 5, found, c));
+        if (found) {
+            uint64_t ulen;
+            TRY(C.u64v(c, ulen));
+            if (ulen > (uint64_t(1) << 34)) return LZ4DecompressionError;
+            // an LZ4 block expands at most ~255x: a larger claim cannot decompress exactly
+            if (ulen > 255ull * c.n + 64) return LZ4DecompressionError;
+            if (SIZE) {
+                R.lz_len = uint32_t(ulen);
+            } else {
+                if (ulen > D.lz_cap) return ErrCapacity;
+                if (!lz4_block(C, c, C.lz, uint32_t(ulen))) return LZ4DecompressionError;
+            }
+            comp.n = uint32_t(ulen);
+            has_comp = true;
+        }
+    }
+
+    prof_mark(0);
+    uint32_t n_file = 0, n_agents = 0;
+    {   // FileInfo (decode_oplog.rs:197-227)
+        Rd fi, an, tmp;
+        bool found;
+        TRY(C.expect_chunk(r, 1, fi));
+        TRY(C.chunk_if(fi, 2, found, tmp));
+        if (found) {
+            uint64_t dt;
+            TRY(C.u32v(tmp, dt));
+            if (dt != 4) return UnknownChunk;
+            bool asc;
+            if (!SIZE && !utf8_ok(C.in + tmp.p, tmp.n, asc)) return InvalidUTF8;
+        }
+        TRY(C.expect_chunk(fi, 3, an));
+        TRY(C.chunk_if(fi, 4, found, tmp));
+        while (an.n) {
+            uint64_t nl;
+            TRY(C.u64v(an, nl));
+            if (nl > an.n) return InvalidLength;
+            const uint32_t noff = an.p, nlen = uint32_t(nl);
+            an.p += nlen; an.n -= nlen;
+            if (SIZE) { R.n_file_agents = ++n_file; continue; }
+            if (n_file >= P.max_file_agents) return Defer;
+            bool asc;
+            if (!utf8_ok(C.in + noff, nlen, asc)) return InvalidUTF8;
+            // get_or_create_agent_id: an existing name maps to its id
+            uint32_t id = 0xFFFFFFFFu;
+            for (uint32_t j0 = 0; j0 < n_agents && id == 0xFFFFFFFFu; j0 += 64) {
+                const uint32_t j = j0 + lane();
+                bool eq = false;
+                if (j < n_agents && L.nlen[j] == nlen) {
+                    eq = true;
+                    const uint32_t o2 = L.noff[j];
+                    for (uint32_t k = 0; k < nlen && eq; k++) eq = C.in[o2 + k] == C.in[noff + k];
+                }
+                const uint64_t m = ballot(eq);
+                if (m) id = j0 + ctz(m);
+            }
+            if (id == 0xFFFFFFFFu) {
+                bool root = nlen == 4 && C.byte(0, noff) == 'R' && C.byte(0, noff + 1) == 'O' &&
+                            C.byte(0, noff + 2) == 'O' && C.byte(0, noff + 3) == 'T';
+                if (root || nlen >= 50) return ErrCheckout;   // mod.rs:88-91
+                id = n_agents++;
+                if (lane() == 0) { L.noff[id] = noff; L.nlen[id] = nlen; }
+            }
+            if (lane() == 0) { L.fmap[n_file] = id; L.fseq[n_file] = 0; }
+            n_file++;
+            __syncthreads();
+        }
+    }
+    R.n_file_agents = n_file;
+    {   // StartBranch (decode_oplog.rs:652-664)
+        Rd sb, ver;
+        bool found;
+        TRY(C.expect_chunk(r, 10, sb));
+        TRY(C.chunk_if(sb, 12, found, ver));
+        if (found) {   // read_version: any named version is unknown to a fresh oplog
+            for (;;) {
+                uint64_t n, seq;
+                TRY(C.u64v(ver, n));
+                TRY(C.u64v(ver, seq));
+                if ((n >> 1) == 0) break;
+                if ((n >> 1) - 1 >= n_file) return InvalidLength;
+                return BaseVersionUnknown;
+            }
+            if (ver.n) return InvalidLength;
+        }
+        if (sb.n) {
+            Rd s; uint32_t asc;
+            TRY(content_str<SIZE>(C, sb, comp, has_comp, s, asc));
+        }
+    }
+    Rd pc;
+    TRY(C.expect_chunk(r, 20, pc));
+    CRuns ins{}, del{};
+    uint32_t cik_bytes = 0;
+    for (;;) {
+        bool found; Rd ch;
+        TRY(C.chunk_if(pc, 24, found, ch));
+        if (!found) break;
+        uint64_t tag;
+        TRY(C.u32v(ch, tag));
+        if (tag > 1) return InvalidContent;
+        CRuns it{};
+        it.present = 1;
+        TRY(content_str<SIZE>(C, ch, comp, has_comp, it.text, it.ascii));
+        TRY(C.expect_chunk(ch, 25, it.runs));
+        it.runs.s = tag == 0 ? SRC_RUNS_INS : SRC_RUNS_DEL;
+        it.t0 = it.text.p;
+        cik_bytes += it.runs.n;
+        if (tag == 0) ins = it; else del = it;
+    }
+    Rd av, tp, hist;
+    TRY(C.expect_chunk(pc, 21, av));
+    TRY(C.expect_chunk(pc, 22, tp));
+    TRY(C.expect_chunk(pc, 23, hist));
+    av.s = SRC_AV;
+    tp.s = SRC_TP;
+    hist.s = SRC_HIST;
+    prof_mark(1);
+
+    if (SIZE) {   // OpVersions: LV count and agent runs
+        uint64_t lv = 0;
+        uint32_t runs = 0;
+        R.tp_bytes = tp.n;
+        R.cik_bytes = cik_bytes;
+        R.hist_bytes = hist.n;
+        while (av.n) {
+            uint64_t n, alen;
+            int64_t jump = 0;
+            TRY(C.u64v(av, n));
+            const bool hj = n & 1;
+            TRY(C.u64v(av, alen));
+            if (hj) TRY(C.zigzag(av, jump));
+            lv += alen;
+            runs++;
+            R.raw_aruns = runs;   // partial counts size a pass that fails later
+            R.n_lv = lv;
+            if (lv >= LIM31) return Defer;
+        }
+        R.raw_aruns = runs;
+        R.n_lv = lv;
+        return S_OK;
+    }
+
+    // ---- OpVersions + OpTypeAndPosition + content runs (decode_oplog.rs:29-68, 289-337, 731-778)
+    Quads qa, qp;
+    qa.init(); qp.init();
+    uint32_t ca_valid = 0, ca_lv = 0, ca_len = 0, ca_agent = 0, ca_seq = 0;   // pending agent run
+    uint32_t cr_valid = 0, cr_lv = 0, cr_len = 0, cr_pos = 0, cr_kind = 0, cr_fwd = 0;   // pending op run
+    uint64_t n_lv = 0, next_assign = 0;
+    uint32_t ins_size = 0, complete = 1, all_ascii = 1;
+    int64_t last_cursor = 0;
+    bool have_op = false;
+    uint64_t op_len = 0;
+    int64_t op_start = 0;
+    bool op_del = false, op_fwd = true;
+
+    auto flush_arun = [&]() -> int {
+        if (!ca_valid) return S_OK;
+        if (qa.count() >= D.arun_cap) return int(ErrCapacity);
+        qa.push(ca_lv, ca_len, ca_agent, ca_seq, O.aruns);
+        return S_OK;
+    };
+    auto flush_op = [&]() -> int {
+        if (!cr_valid) return S_OK;
+        if (qp.count() >= D.pre_cap) return int(ErrCapacity);
+        qp.push(cr_lv, cr_len, cr_pos, cr_kind | (cr_fwd << 1), O.pre);
+        return S_OK;
+    };
+    auto fill_cbyte = [&](uint64_t lv0, uint64_t k, uint32_t v) {
+        for (uint64_t i = lane(); i < k; i += 64) O.cbyte[lv0 + i] = v;
+    };
+
+    while (av.n) {
+        uint64_t n, alen;
+        int64_t jump = 0;
+        TRY(C.u64v(av, n));
+        const bool has_jump = n & 1;
+        n >>= 1;
+        TRY(C.u64v(av, alen));
+        if (has_jump) TRY(C.zigzag(av, jump));
+        if (n == 0 || n - 1 >= n_file) return InvalidLength;
+        const uint32_t fa = uint32_t(n - 1);
+        const int64_t sstart = int64_t(L.fseq[fa]) + jump;
+        if (sstart < 0 || uint64_t(sstart) + alen >= LIM31 || next_assign + alen >= LIM31) return Defer;
+        __syncthreads();
+        if (lane() == 0) L.fseq[fa] = uint32_t(sstart + int64_t(alen));
+        __syncthreads();
+        const uint32_t agent = L.fmap[fa];
+        // assign (agent_runs RLE)
+        if (ca_valid && ca_agent == agent && ca_lv + ca_len == next_assign && uint64_t(ca_seq) + ca_len == uint64_t(sstart)) {
+            ca_len += uint32_t(alen);
+        } else {
+            TRY(flush_arun());
+            ca_valid = 1; ca_lv = uint32_t(next_assign); ca_len = uint32_t(alen); ca_agent = agent; ca_seq = uint32_t(sstart);
+        }
+        next_assign += alen;
+
+        uint64_t want = alen;
+        while (want) {
+            if (!have_op) {
+                if (!tp.n) return InvalidLength;
+                uint64_t x;
+                TRY(C.u64v(tp, x));
+                const bool has_length = x & 1; x >>= 1;
+                const bool diff_nz = x & 1; x >>= 1;
+                const bool is_del = x & 1; x >>= 1;
+                int64_t diff = 0;
+                bool fwd = true;
+                uint64_t l;
+                if (has_length) {
+                    if (is_del) { fwd = x & 1; x >>= 1; }
+                    if (diff_nz) TRY(C.zigzag(tp, diff));
+                    l = x;
+                } else {
+                    l = 1;
+                    diff = int64_t(x >> 1) * ((x & 1) ? -1 : 1);
+                }
+                const int64_t raw = int64_t(uint64_t(last_cursor) + uint64_t(diff));
+                int64_t st, raw_end;
+                if (!is_del) { st = raw; raw_end = raw + int64_t(l); }
+                else if (fwd) { st = raw; raw_end = raw; }
+                else { st = raw - int64_t(l); raw_end = raw - int64_t(l); }
+                last_cursor = raw_end;
+                if (l == 0) return ErrCheckout;   // assert!(max_len > 0)
+                op_len = l; op_start = st; op_del = is_del; op_fwd = fwd; have_op = true;
+            }
+            uint64_t take = want < op_len ? want : op_len;
+            CRuns ci = op_del ? del : ins;   // by value: no dynamically indexed private memory
+            bool known = false;
+            Rd cs{0, 0, 0};
+            if (ci.present) {
+                bool has, cknown; uint64_t clen;
+                TRY(cruns_next(C, ci, has, clen, cknown, cs));
+                if (!has) return InvalidLength;
+                if (clen < take) take = clen;
+                if (clen > take) {   // push the remainder back
+                    uint32_t b = 0;
+                    if (cknown) {
+                        uint64_t c2;
+                        walk_chars(C.ptr(cs.s) + cs.p, cs.n, take, ci.ascii, b, c2);
+                    }
+                    ci.pb = 1;
+                    ci.pb_len = clen - take; ci.pb_known = cknown;
+                    ci.pb_s = cknown ? Rd{cs.s, cs.p + b, cs.n - b} : Rd{cs.s, cs.p, 0};
+                    cs.n = b;
+                }
+                known = cknown;
+            }
+            if (op_del) del = ci; else ins = ci;
+            if (!take) return ErrCheckout;
+            // the piece's position; out-of-range positions are left to the host decoder
+            int64_t ppos;
+            bool pfwd = true;
+            if (!op_del) ppos = op_start;
+            else if (op_fwd) ppos = op_start;
+            else { ppos = op_start + int64_t(op_len) - int64_t(take); pfwd = false; }
+            if (ppos < 0 || uint64_t(ppos) >= LIM31) return Defer;
+            const uint32_t lv = uint32_t(n_lv);
+            if (n_lv + take > D.lv_cap) return ErrCapacity;
+            if (!op_del) {   // push_ins
+                if (known) {
+                    // the known pieces tile the insert text in order: the text is copied whole
+                    // once at the end, pieces only place their per-LV offsets
+                    const uint8_t *src = C.ptr(cs.s) + cs.p;
+                    if (ci.ascii) {
+                        for (uint64_t i = lane(); i < take; i += 64) O.cbyte[lv + i] = ins_size + uint32_t(i);
+                    } else {
+                        all_ascii = 0;
+                        uint32_t cnt = 0;
+                        for (uint32_t i = 0; i < cs.n; i += 64) {
+                            const uint32_t j = i + lane();
+                            const bool st = j < cs.n && (src[j] & 0xC0u) != 0x80u;
+                            const uint64_t m = ballot(st);
+                            if (st) O.cbyte[lv + cnt + popc(m & lt_mask())] = ins_size + j;
+                            cnt += popc(m);
+                        }
+                    }
+                    ins_size += cs.n;
+                } else {
+                    fill_cbyte(lv, take, 0xFFFFFFFFu);
+                    complete = 0;
+                }
+                n_lv += take;
+                if (cr_valid && cr_kind == 0 && cr_lv + cr_len == lv && uint64_t(cr_pos) + cr_len == uint64_t(ppos)) {
+                    cr_len += uint32_t(take);
+                } else {
+                    TRY(flush_op());
+                    cr_valid = 1; cr_lv = lv; cr_len = uint32_t(take); cr_pos = uint32_t(ppos); cr_kind = 0; cr_fwd = 1;
+                }
+                op_start += int64_t(take);
+            } else {         // push_del
+                fill_cbyte(lv, take, 0xFFFFFFFFu);
+                n_lv += take;
+                const uint32_t pos = uint32_t(ppos), ln = uint32_t(take);
+                bool merged = false;
+                if (cr_valid && cr_kind == 1 && cr_lv + cr_len == lv) {
+                    if ((cr_len == 1 || cr_fwd) && (ln == 1 || pfwd) && pos == cr_pos) {
+                        cr_len += ln; cr_fwd = 1; merged = true;
+                    } else if ((cr_len == 1 || !cr_fwd) && (ln == 1 || !pfwd) && uint64_t(pos) + ln == cr_pos) {
+                        cr_pos = pos; cr_len += ln; cr_fwd = 0; merged = true;
+                    }
+                }
+                if (!merged) {
+                    TRY(flush_op());
+                    cr_valid = 1; cr_lv = lv; cr_len = ln; cr_pos = pos; cr_kind = 1; cr_fwd = pfwd ? 1 : 0;
+                }
+            }
+            op_len -= take;
+            if (!op_len) have_op = false;
+            want -= take;
+        }
+    }
+    if (n_lv != next_assign) return InvalidLength;
+    TRY(flush_arun());
+    TRY(flush_op());
+    qa.flush(O.aruns);
+    qp.flush(O.pre);
+    const uint32_t n_aruns = uint32_t(qa.at), n_pre = uint32_t(qp.at);
+    wave_fence();
+    prof_mark(2);
+    TRY(build_lookup(O, L, n_agents, n_aruns));
+    prof_mark(3);
+
+    // ---- OpParents (decode_oplog.rs:95-148, 856-913) -----------------------------------------
+    uint64_t next_file = 0;
+    uint32_t pe_valid = 0, pe_start = 0, pe_end = 0, pe_poff = 0;   // pending graph entry
+    uint32_t n_ent = 0, n_par = 0;
+    uint32_t fr = 0, fn = 0;   // frontier: lane k holds element k (sorted)
+    while (hist.n) {
+        uint64_t hl;
+        TRY(C.u64v(hist, hl));
+        uint32_t parv = 0, np = 0;
+        bool par_bad = false;   // next_time - n underflowed (fails the range check below)
+        for (;;) {
+            uint64_t n;
+            TRY(C.u64v(hist, n));
+            const bool foreign = n & 1; n >>= 1;
+            const bool more = n & 1; n >>= 1;
+            uint64_t p;
+            if (foreign) {
+                if (n == 0) break;
+                if (n - 1 >= n_file) return InvalidLength;
+                uint64_t seq;
+                TRY(C.u64v(hist, seq));
+                const int64_t lv = lookup_lv(O, L, L.fmap[n - 1], seq);
+                if (lv < 0) return InvalidLength;
+                p = uint64_t(lv);
+            } else {
+                par_bad |= n > next_file;
+                p = next_file - n;
+            }
+            if (np == DECODE_MAX_PARENTS) return Defer;
+            parv = lane() == np ? uint32_t(p) : parv;
+            np++;
+            if (!more) break;
+        }
+        if (hl == 0 || next_file + hl > next_assign) return InvalidLength;
+        if (par_bad || ballot(lane() < np && parv >= next_file)) return InvalidLength;
+        // sort the parents: rank = smaller values + equal values at lower lanes
+        uint32_t rank = 0;
+        for (uint32_t j = 0; j < np; j++) {
+            const uint32_t pj = rdl(parv, j);
+            rank += (pj < parv || (pj == parv && j < lane())) ? 1u : 0u;
+        }
+        const uint32_t start = uint32_t(next_file), end = uint32_t(next_file + hl);
+        if (np == 1 && pe_valid && rdl(parv, 0) == pe_end - 1 && pe_end == start) {   // Graph::push extends
+            pe_end = end;
+        } else {
+            if (pe_valid) {
+                if (n_ent >= D.ent_cap) return ErrCapacity;
+                if (lane() == 0) { O.ent[n_ent] = make_uint2(pe_start, pe_end); O.poff[n_ent] = pe_poff; }
+                n_ent++;
+            }
+            if (n_par + np > D.par_cap) return ErrCapacity;
+            if (lane() < np) O.par[n_par + rank] = parv;
+            pe_valid = 1; pe_start = start; pe_end = end; pe_poff = n_par;
+            n_par += np;
+        }
+        // frontier advance (frontier.rs:251-279): drop the parents, append the span's last LV
+        bool in_par = false;
+        for (uint32_t j = 0; j < np; j++) in_par |= rdl(parv, j) == fr;
+        const bool keep = lane() < fn && !in_par;
+        const uint64_t km = ballot(keep);
+        if (keep) L.fr[popc(km & lt_mask())] = fr;
+        __syncthreads();
+        fn = popc(km);
+        if (fn >= DECODE_MAX_FRONTIER) return Defer;
+        fr = lane() < fn ? L.fr[lane()] : 0u;
+        fr = lane() == fn ? end - 1 : fr;
+        fn++;
+        __syncthreads();
+        next_file += hl;
+    }
+    if (next_file != next_assign) return InvalidLength;
+    if (pe_valid) {
+        if (n_ent >= D.ent_cap) return ErrCapacity;
+        if (lane() == 0) { O.ent[n_ent] = make_uint2(pe_start, pe_end); O.poff[n_ent] = pe_poff; }
+        n_ent++;
+    }
+    if (lane() == 0) O.poff[n_ent] = n_par;
+    prof_mark(4);
+    if (pc.n) return InvalidLength;
+    if (ins.present) {   // the content iterators must be exhausted
+        bool has, kn; uint64_t l; Rd s;
+        const int e = cruns_next(C, ins, has, l, kn, s);
+        if (e || has) return InvalidContent;
+    }
+    if (del.present) {
+        bool has, kn; uint64_t l; Rd s;
+        const int e = cruns_next(C, del, has, l, kn, s);
+        if (e || has) return InvalidContent;
+    }
+    {   // CRC (decode_oplog.rs:940-955)
+        const uint32_t reader_len = r.n;
+        bool found; Rd c;
+        TRY(C.chunk_if(r, 100, found, c));
+        if (found && !D.ignore_crc) {
+            if (c.n < 4) return UnexpectedEOF;
+            const uint32_t want = C.byte(0, c.p) | (C.byte(0, c.p + 1) << 8) | (C.byte(0, c.p + 2) << 16) |
+                                  (C.byte(0, c.p + 3) << 24);
+            if (crc32c_par(C.in, len - reader_len, L.crc, P.x2n) != want) return ChecksumFailed;
+        }
+    }
+    wave_fence();
+    prof_mark(5);
+
+    // ---- the insert text (every known piece, in order) ------------------------------------------
+    if (ins.present && ins_size) {
+        if (ins_size > D.content_cap) return ErrCapacity;
+        const uint8_t *src = C.ptr(ins.text.s) + ins.t0;
+        for (uint32_t i = 0; i < ins_size; i += 256) {
+            uint8_t b[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t j = i + 64 * u + lane();
+                b[u] = j < ins_size ? src[j] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t j = i + 64 * u + lane();
+                if (j < ins_size) O.content[j] = b[u];
+            }
+        }
+    }
+
+    // ---- split op runs at graph-entry boundaries (HostOpLog::finish) --------------------------
+    {
+        Quads qo;
+        qo.init();
+        uint32_t gi = 0;
+        uint32_t gend = 0xFFFFFFFFu;   // end of entry gi (uniform)
+        uint32_t eblk = 0xFFFFFFFFu, ew = 0;   // 64 entry ends cached in lanes
+        auto entry_end = [&](uint32_t g) -> uint32_t {
+            if (g >= n_ent) return 0xFFFFFFFFu;
+            if ((g & ~63u) != eblk) {
+                eblk = g & ~63u;
+                const uint32_t k = eblk + lane();
+                ew = k < n_ent ? O.ent[k].y : 0xFFFFFFFFu;
+            }
+            return rdl(ew, g & 63u);
+        };
+        gend = entry_end(0);
+        for (uint32_t b0 = 0; b0 < n_pre; b0 += 64) {
+            uint4 q = make_uint4(0, 0, 0, 0);
+            if (b0 + lane() < n_pre) q = O.pre[b0 + lane()];
+            const uint32_t m = n_pre - b0 < 64 ? n_pre - b0 : 64;
+            for (uint32_t k = 0; k < m; k++) {
+                uint32_t rlv = rdl(q.x, k), rlen = rdl(q.y, k), rpos = rdl(q.z, k);
+                const uint32_t kf = rdl(q.w, k);
+                const uint32_t kind = kf & 1u, fwd = kf >> 1;
+                while (rlen) {
+                    while (gi < n_ent && gend <= rlv) gend = entry_end(++gi);
+                    const uint32_t cut = gi < n_ent ? gend : rlv + rlen;
+                    const uint32_t mm = rlen < cut - rlv ? rlen : cut - rlv;
+                    uint32_t apos = rpos;
+                    if (kind == 0) rpos += mm;
+                    else if (!fwd) apos = rpos + rlen - mm;
+                    if (qo.count() >= D.op_cap) return ErrCapacity;
+                    qo.push(rlv, mm, apos, kf, O.ops);
+                    rlv += mm;
+                    rlen -= mm;
+                }
+            }
+        }
+        qo.flush(O.ops);
+        R.n_ops = uint32_t(qo.at);
+    }
+    prof_mark(6);
+    if (lane() < fn) O.ver[lane()] = fr;
+    for (uint32_t a = lane(); a < n_agents; a += 64) O.agents[a] = make_uint2(L.noff[a], L.nlen[a]);
+
+    R.n_agents = n_agents;
+    R.n_aruns = n_aruns;
+    R.n_pre = n_pre;
+    R.n_entries = n_ent;
+    R.n_parents = n_par;
+    R.n_content = ins_size;
+    R.n_version = fn;
+    R.content_complete = complete;
+    R.ascii = all_ascii;
+    R.n_lv = n_lv;
+    return S_OK;
+}
+
+template <bool SIZE>
+__global__ __launch_bounds__(64) void decode_kernel(DecodeParams P) {
+    extern __shared__ uint32_t lds[];
+    const uint32_t doc = blockIdx.x;
+    if (doc >= P.n_docs) return;
+    const DecodeDesc D = P.docs[doc];
+    Lds L;
+    const uint32_t F = P.max_file_agents;
+    L.crc = lds;
+    L.fr = lds + 256;
+    L.fmap = lds + 320;
+    L.fseq = L.fmap + F;
+    L.noff = L.fseq + F;
+    L.nlen = L.noff + F;
+    L.acnt = L.nlen + F;
+    L.aoff = L.acnt + F;
+    L.acur = L.aoff + F;
+    L.amono = L.acur + F;
+    if (!SIZE) {
+        for (uint32_t i = lane(); i < 256; i += 64) {
+            uint32_t c = i;
+            for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ CRC_POLY : c >> 1;
+            L.crc[i] = c;
+        }
+        __syncthreads();
+    }
+    DecodeResult R{};
+    int st = S_OK;
+    if (D.skip) st = Defer;
+    else st = decode_doc<SIZE>(P, D, R, L);
+    R.status = uint32_t(st);
+    if (lane() == 0) P.results[doc] = R;
+}
+
+}  // namespace ddec
+
+int launch_decode(const DecodeParams &p, void *stream) {
+    if (!p.n_docs) return 0;
+    const size_t lds = (320 + 8 * size_t(p.max_file_agents)) * 4;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (p.size_only)
+        hipLaunchKernelGGL(ddec::decode_kernel<true>, dim3(p.n_docs), dim3(64), lds, s, p);
+    else
+        hipLaunchKernelGGL(ddec::decode_kernel<false>, dim3(p.n_docs), dim3(64), lds, s, p);
+    return hipGetLastError() == hipSuccess ? 0 : 66;
+}
+
+}  // namespace dtgpu

@@ -1,0 +1,60 @@
+// dt_decode.hpp -- host/device layout of the batched `.dt` decoder (dt_decode.hip).
+//
+// One 64-lane wavefront decodes one document (ListOpLog::load_from,
+// src/list/encoding/decode_oplog.rs:447-960) into the same SoA runs the host decoder builds
+// (dt_host.hpp HostOpLog): op runs split at graph-entry boundaries, agent runs, graph entries with
+// sorted parents, inserted content with a per-LV byte offset, and the frontier.  A sizing pass
+// (size_only) reads the chunk directory and the OpVersions stream to size every arena; the full
+// pass then decodes with exact or upper-bound capacities.
+#pragma once
+#include <stdint.h>
+
+namespace dtgpu {
+
+// Arena capacities / offsets of one document.  Offsets are in elements of each arena.
+struct DecodeDesc {
+    uint64_t in_off;        // bytes; 256-B aligned with >= 256 B of readable padding after the doc
+    uint64_t lz_off;        // bytes; the decompressed LZ4 buffer (same alignment / padding)
+    uint64_t arun_off;      // quads (lv, len, agent, seq) -- also the per-agent lookup lists
+    uint64_t pre_off;       // quads: op runs before the entry split
+    uint64_t op_off;        // quads (lv, len, pos, kind | fwd << 1): the final op runs
+    uint64_t ent_off;       // pairs (start, end)
+    uint64_t poff_off;      // ent_cap + 1 words: parents CSR
+    uint64_t par_off;       // words
+    uint64_t content_off;   // bytes: inserted UTF-8 in LV order
+    uint64_t lv_off;        // words: per-LV byte offset of an inserted char (~0 otherwise)
+    uint64_t agent_off;     // pairs (name offset in the document, name length), by agent id
+    uint64_t ver_off;       // words: the frontier (cg.version), <= 64 LVs
+    uint32_t in_len, lz_cap, arun_cap, pre_cap, op_cap, ent_cap, par_cap, content_cap, lv_cap, agent_cap;
+    uint32_t ignore_crc, skip;
+};
+
+struct DecodeResult {
+    uint32_t status;        // dtgpu_status codes; DECODE_DEFER = decode this document on the host
+    uint32_t n_file_agents, n_agents, n_aruns, n_pre, n_ops, n_entries, n_parents;
+    uint32_t n_content, n_version, content_complete, ascii;
+    uint64_t n_lv;
+    // sizing pass (size_only): what the full pass needs
+    uint32_t lz_len, tp_bytes, cik_bytes, hist_bytes, raw_aruns, pad;
+    uint32_t prof[8];       // core-clock cycles per decode phase (full pass)
+};
+
+constexpr uint32_t DECODE_DEFER = 80;           // a case the device decoder hands to the host
+constexpr uint32_t DECODE_MAX_FILE_AGENTS = 2048;
+constexpr uint32_t DECODE_MAX_FRONTIER = 64;
+constexpr uint32_t DECODE_MAX_PARENTS = 64;
+
+struct DecodeParams {
+    const uint8_t *in;
+    uint8_t *lz;
+    uint32_t *aruns, *alist, *pre, *ops, *ent, *poff, *par, *cbyte, *agents, *ver;
+    uint8_t *content;
+    const DecodeDesc *docs;
+    DecodeResult *results;
+    uint32_t n_docs, size_only, max_file_agents, pad;
+    uint32_t x2n[32];       // x^(2^k) mod the CRC-32C polynomial (crc32 combine tables)
+};
+
+int launch_decode(const DecodeParams &p, void *stream);
+
+}  // namespace dtgpu

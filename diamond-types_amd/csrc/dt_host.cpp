@@ -641,8 +641,7 @@ Status decode_dt(const uint8_t *data, size_t len, bool ignore_crc, HostOpLog &o)
                 const int64_t lv = o.seq_to_lv(amap[size_t(n - 1)].agent, seq);
                 if (lv < 0) return InvalidLength;
                 p = uint64_t(lv);
-            } else {
-                if (n > next_file) return InvalidLength;
+            } else {   // next_time - n: an out-of-range value fails the range check below
                 p = next_file - n;
             }
             par.push_back(p);

@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "../../include/dtgpu.h"
+#include "dt_devbuf.hpp"
 #include "dt_device.hpp"
 #include "dt_host.hpp"
 
@@ -23,22 +24,6 @@ struct dtgpu_oplog {
 };
 
 namespace {
-
-template <typename T>
-struct DevBuf {
-    T *p = nullptr;
-    size_t n = 0;
-    ~DevBuf() { if (p) (void)hipFree(p); }
-    hipError_t alloc(size_t count) {
-        n = count;
-        return hipMalloc(reinterpret_cast<void **>(&p), std::max<size_t>(count, 1) * sizeof(T));
-    }
-    hipError_t upload(const std::vector<T> &v, hipStream_t s) {
-        hipError_t e = alloc(v.size());
-        if (e != hipSuccess || v.empty()) return e;
-        return hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s);
-    }
-};
 
 // Number of documents whose block index fits the LDS tier: up to 64 KiB of index per wave.
 constexpr uint64_t kLdsIndexBudget = 64 * 1024;
@@ -517,6 +502,55 @@ size_t dtgpu_oplog_agent_runs(const dtgpu_oplog *h, uint32_t *out, size_t cap) {
     const auto &a = p.plan.agent_runs;
     if (out) std::memcpy(out, a.data(), std::min(cap, a.size()) * sizeof(uint32_t));
     return a.size();
+}
+
+size_t dtgpu_oplog_export(const dtgpu_oplog *h, int what, void *out, size_t cap) {
+    if (!h) return 0;
+    const HostOpLog &o = h->o;
+    std::vector<uint32_t> w;
+    std::vector<uint8_t> b;
+    bool bytes = false;
+    switch (what) {
+        case DTGPU_EXPORT_OPS:
+            for (const OpRun &r : o.ops) {
+                w.push_back(uint32_t(r.lv)); w.push_back(uint32_t(r.len)); w.push_back(uint32_t(r.pos));
+                w.push_back(uint32_t(r.kind) | (uint32_t(r.fwd) << 1));
+            }
+            break;
+        case DTGPU_EXPORT_AGENT_RUNS:
+            for (const AgentRun &r : o.agent_runs) {
+                w.push_back(uint32_t(r.lv)); w.push_back(uint32_t(r.len)); w.push_back(r.agent); w.push_back(uint32_t(r.seq));
+            }
+            break;
+        case DTGPU_EXPORT_ENTRIES:
+            for (const GraphEntry &e : o.graph.entries) { w.push_back(uint32_t(e.start)); w.push_back(uint32_t(e.end)); }
+            break;
+        case DTGPU_EXPORT_PARENT_OFFSETS: {
+            uint32_t k = 0;
+            for (const GraphEntry &e : o.graph.entries) { w.push_back(k); k += uint32_t(e.parents.size()); }
+            w.push_back(k);
+            break;
+        }
+        case DTGPU_EXPORT_PARENTS:
+            for (const GraphEntry &e : o.graph.entries) for (uint64_t p : e.parents) w.push_back(uint32_t(p));
+            break;
+        case DTGPU_EXPORT_CONTENT: b = o.ins_content; bytes = true; break;
+        case DTGPU_EXPORT_CHAR_OFFSETS: w = o.ins_cbyte; break;
+        case DTGPU_EXPORT_VERSION: for (uint64_t v : o.version) w.push_back(uint32_t(v)); break;
+        case DTGPU_EXPORT_AGENT_NAMES:
+            for (const std::string &nm : o.agent_names) { b.push_back(uint8_t(nm.size())); b.insert(b.end(), nm.begin(), nm.end()); }
+            bytes = true;
+            break;
+        default: return 0;
+    }
+    const size_t per = what == DTGPU_EXPORT_OPS || what == DTGPU_EXPORT_AGENT_RUNS ? 4 : what == DTGPU_EXPORT_ENTRIES ? 2 : 1;
+    if (bytes) {
+        if (out) std::memcpy(out, b.data(), std::min(cap, b.size()));
+        return b.size();
+    }
+    const size_t count = w.size() / per;
+    if (out) std::memcpy(out, w.data(), std::min(cap, count) * per * 4);
+    return count;
 }
 
 // ---- batch ----------------------------------------------------------------------------------

@@ -117,6 +117,22 @@ def lib():
     L.dtgpu_synth_ops.argtypes = [u64, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32), sz]
     L.dtgpu_synth_ops.restype = sz
     L.dtgpu_synth_oplog.argtypes = [u64, ctypes.c_uint32, ctypes.POINTER(vp)]
+    L.dtgpu_oplog_export.argtypes = [vp, c, vp, sz]
+    L.dtgpu_oplog_export.restype = sz
+    L.dtgpu_decode_create.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz), sz,
+                                      ctypes.POINTER(BatchOpts), ctypes.POINTER(vp)]
+    L.dtgpu_decode_run.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
+    L.dtgpu_decode_size.argtypes = [vp]
+    L.dtgpu_decode_size.restype = sz
+    L.dtgpu_decode_status.argtypes = [vp, sz, pu64]
+    L.dtgpu_decode_export.argtypes = [vp, sz, c, vp, sz]
+    L.dtgpu_decode_export.restype = sz
+    L.dtgpu_decode_bytes.argtypes = [vp, c]
+    L.dtgpu_decode_bytes.restype = u64
+    L.dtgpu_decode_last_ms.argtypes = [vp]
+    L.dtgpu_decode_last_ms.restype = ctypes.c_float
+    L.dtgpu_decode_free.argtypes = [vp]
+    L.dtgpu_decode_profile.argtypes = [vp, sz, ctypes.POINTER(ctypes.c_uint32)]
     L.dtgpu_status_str.argtypes = [c]
     L.dtgpu_status_str.restype = ctypes.c_char_p
     _lib = L
@@ -246,6 +262,12 @@ class ListOpLog:
         lib().dtgpu_oplog_agent_runs(self._h, buf, n)
         return list(buf[:n])
 
+    def export(self, what):
+        """The decoded oplog's arrays (dtgpu_oplog_export): "ops", "agent_runs", "entries",
+        "parent_offsets", "parents", "content", "char_offsets", "version", "agent_names"."""
+        a = _export(lambda c, p, n: lib().dtgpu_oplog_export(self._h, c, p, n), what)
+        return _names(a) if what == "agent_names" else a
+
     def checkout_tip_bytes(self) -> bytes:
         n = ctypes.c_size_t()
         _check(lib().dtgpu_checkout_tip(self._h, None, 0, ctypes.byref(n)))
@@ -255,6 +277,35 @@ class ListOpLog:
 
     def checkout_tip(self) -> ListBranch:
         return ListBranch(self.checkout_tip_bytes(), self.local_frontier())
+
+
+# dtgpu_export codes (include/dtgpu.h): name -> (code, numpy dtype, fields per record)
+EXPORTS = {
+    "ops": (0, "<u4", 4), "agent_runs": (1, "<u4", 4), "entries": (2, "<u4", 2),
+    "parent_offsets": (3, "<u4", 1), "parents": (4, "<u4", 1), "content": (5, "u1", 1),
+    "char_offsets": (6, "<u4", 1), "version": (7, "<u4", 1), "agent_names": (8, "u1", 1),
+}
+DECODE_DEFER = 80
+
+
+def _export(fn, what):
+    import numpy as np
+    code, dt, per = EXPORTS[what]
+    n = fn(code, None, 0)
+    arr = np.zeros(max(n, 1) * per, dtype=dt)
+    fn(code, arr.ctypes.data_as(ctypes.c_void_p), n)
+    arr = arr[:n * per]
+    return arr.reshape(n, per) if per > 1 else arr
+
+
+def _names(blob):
+    out, i = [], 0
+    blob = bytes(blob)
+    while i < len(blob):
+        k = blob[i]
+        out.append(blob[i + 1:i + 1 + k])
+        i += 1 + k
+    return out
 
 
 def oplog_from_trace(txns, agent_name="jeremy") -> ListOpLog:
@@ -366,6 +417,59 @@ class Batch:
     @property
     def total_lv(self):
         return lib().dtgpu_batch_total_lv(self._h)
+
+
+class DecodeBatch:
+    """Batched `ListOpLog::load_from` on the GPU (dtgpu_decode_*): one wavefront per document."""
+
+    def __init__(self, docs, ignore_crc=False, device=0):
+        L = lib()
+        n = len(docs)
+        self._keep = [bytes(d) for d in docs]
+        arr = (ctypes.c_char_p * max(n, 1))(*self._keep)
+        lens = (ctypes.c_size_t * max(n, 1))(*[len(d) for d in self._keep])
+        opts = BatchOpts(1 if ignore_crc else 0, 0, device)
+        h = ctypes.c_void_p()
+        _check(L.dtgpu_decode_create(arr, lens, n, ctypes.byref(opts), ctypes.byref(h)))
+        self._h = h
+        self.n = n
+
+    def __len__(self):
+        return self.n
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            lib().dtgpu_decode_free(h)
+            self._h = None
+
+    def run(self) -> float:
+        """Full device decode of every document; returns the kernel time in ms."""
+        ms = ctypes.c_float()
+        _check(lib().dtgpu_decode_run(self._h, ctypes.byref(ms)))
+        return ms.value
+
+    def status(self, i):
+        out = (ctypes.c_uint64 * 12)()
+        _check(lib().dtgpu_decode_status(self._h, i, out))
+        keys = ("status", "n_lv", "n_ops", "n_aruns", "n_entries", "n_parents", "n_content", "n_version",
+                "n_agents", "content_complete", "ascii", "n_file_agents")
+        return dict(zip(keys, list(out)))
+
+    def export(self, i, what):
+        a = _export(lambda c, p, n: lib().dtgpu_decode_export(self._h, i, c, p, n), what)
+        return _names(a) if what == "agent_names" else a
+
+    def profile(self, i):
+        out = (ctypes.c_uint32 * 8)()
+        _check(lib().dtgpu_decode_profile(self._h, i, out))
+        return list(out)[:7]
+
+    def bytes_in(self) -> int:
+        return lib().dtgpu_decode_bytes(self._h, 0)
+
+    def bytes_out(self) -> int:
+        return lib().dtgpu_decode_bytes(self._h, 1)
 
 
 def batch_checkout(docs, **kw):

@@ -203,6 +203,48 @@ dtgpu_status dtgpu_synth_oplog(uint64_t doc, uint32_t target_ops, dtgpu_oplog **
 int dtgpu_device_count(void);
 const char *dtgpu_status_str(dtgpu_status status);
 
+
+/* ---- batched `.dt` decode on the GPU ---------------------------
+ * ListOpLog::load_from (src/list/encoding/decode_oplog.rs:447-960) for many documents at once:
+ * one wavefront per document (dt_decode.hip).  dtgpu_decode_create uploads the documents and
+ * runs a sizing pass; dtgpu_decode_run is the full decode (device only) and returns its kernel
+ * time.  Per document the status is a dtgpu_status, or DTGPU_DECODE_DEFER when the document
+ * uses something the device decoder hands to the host decoder (more than 2048 agents, 64
+ * parents on one entry, a frontier wider than 64, overlapping seq ranges of one agent, LVs or
+ * positions >= 2^31). */
+typedef struct dtgpu_decoded dtgpu_decoded;
+#define DTGPU_DECODE_DEFER 80
+dtgpu_status dtgpu_decode_create(const uint8_t *const *docs, const size_t *lens, size_t n,
+                                 const dtgpu_batch_opts *opts, dtgpu_decoded **out);
+dtgpu_status dtgpu_decode_run(dtgpu_decoded *dec, float *ms);
+size_t dtgpu_decode_size(const dtgpu_decoded *dec);
+/* out: status, n_lv, op runs, agent runs, graph entries, parents, content bytes, frontier size,
+ * agents, content_complete, ascii, file agents */
+dtgpu_status dtgpu_decode_status(const dtgpu_decoded *dec, size_t i, uint64_t out[12]);
+float dtgpu_decode_last_ms(const dtgpu_decoded *dec);
+/* core-clock cycles of document i's last decode by phase: LZ4, chunk directory, op/agent runs,
+ * seq lookup lists, parents, checks + CRC, content copy + entry split */
+dtgpu_status dtgpu_decode_profile(const dtgpu_decoded *dec, size_t i, uint32_t out[8]);
+/* which = 0: encoded bytes read; 1: SoA bytes written by the last run */
+uint64_t dtgpu_decode_bytes(const dtgpu_decoded *dec, int which);
+void dtgpu_decode_free(dtgpu_decoded *dec);
+
+/* Decoded-oplog arrays, the same layouts from the device decoder and from a host oplog.
+ * Returns the element count (bytes for CONTENT / AGENT_NAMES) and copies min(cap, count). */
+typedef enum dtgpu_export {
+    DTGPU_EXPORT_OPS = 0,            /* u32 x4: lv, len, pos, kind | fwd << 1 (split at entries) */
+    DTGPU_EXPORT_AGENT_RUNS = 1,     /* u32 x4: lv, len, agent, seq */
+    DTGPU_EXPORT_ENTRIES = 2,        /* u32 x2: start, end */
+    DTGPU_EXPORT_PARENT_OFFSETS = 3, /* u32: CSR offsets into PARENTS (entries + 1) */
+    DTGPU_EXPORT_PARENTS = 4,        /* u32: parent LVs, sorted per entry */
+    DTGPU_EXPORT_CONTENT = 5,        /* bytes: inserted UTF-8 in LV order */
+    DTGPU_EXPORT_CHAR_OFFSETS = 6,   /* u32 per LV: byte offset of an inserted char, else ~0 */
+    DTGPU_EXPORT_VERSION = 7,        /* u32: the frontier */
+    DTGPU_EXPORT_AGENT_NAMES = 8,    /* per agent id: u8 length + name bytes */
+} dtgpu_export;
+size_t dtgpu_decode_export(const dtgpu_decoded *dec, size_t i, int what, void *out, size_t cap);
+size_t dtgpu_oplog_export(const dtgpu_oplog *oplog, int what, void *out, size_t cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,136 @@
+"""GPU `.dt` decode (dt_decode.hip) vs the host decoder and the C oracle.
+
+The device decoder must reproduce `ListOpLog::load_from` (src/list/encoding/decode_oplog.rs:447-960)
+exactly: every decoded array equal to the host decoder's (which test_host_cpu.py pins to the
+oracle), and on corrupted input the same `ParseError` code as the oracle.  A document may be
+handed back to the host (DECODE_DEFER) only for the documented limits; no fixture here is.
+"""
+import numpy as np
+import pytest
+
+import golden_data as G
+from oracle.oracle import OpLog as OracleOpLog, OracleError
+
+pytestmark = pytest.mark.gpu
+
+import dt_amd  # noqa: E402
+
+WHAT = ["ops", "agent_runs", "entries", "parent_offsets", "parents", "content", "char_offsets", "version",
+        "agent_names"]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if dt_amd.device_count() < 1:
+        pytest.fail("no HIP device visible: the engine has no CPU fallback")
+
+
+def _host_code(data, ignore_crc=False):
+    try:
+        dt_amd.ListOpLog.load_from(data, ignore_crc=ignore_crc)
+        return 0
+    except dt_amd.ParseError as e:
+        return e.code
+
+
+def _oracle_code(data):
+    try:
+        OracleOpLog.load_from(data)
+        return 0
+    except OracleError as e:
+        return e.code
+
+
+def _same_arrays(dec, i, data, ignore_crc=False):
+    host = dt_amd.ListOpLog.load_from(data, ignore_crc=ignore_crc)
+    for w in WHAT:
+        a, b = dec.export(i, w), host.export(w)
+        if w == "agent_names":
+            assert a == b, w
+        else:
+            assert np.array_equal(a, b), (w, a[:8], b[:8])
+    st = dec.status(i)
+    assert st["n_lv"] == len(host)
+
+
+@pytest.mark.parametrize("name", G.DT_FILES)
+def test_benchmark_files_decode_identically(name):
+    data = G.dt_bytes(name)
+    dec = dt_amd.DecodeBatch([data])
+    dec.run()
+    assert dec.status(0)["status"] == 0
+    _same_arrays(dec, 0, data)
+
+
+def test_compat_vectors_decode_identically():
+    docs = [G.COMPAT_SIMPLE_1, G.COMPAT_SIMPLE_2, G.COMPAT_SIMPLE_LZ4, G.COMPAT_EMPTY_1, G.COMPAT_EMPTY_2]
+    dec = dt_amd.DecodeBatch(docs)
+    dec.run()
+    for i, d in enumerate(docs):
+        assert dec.status(i)["status"] == 0, i
+        _same_arrays(dec, i, d)
+
+
+def test_mixed_batch_and_repeat_runs():
+    docs = [G.dt_bytes(n) for n in G.DT_FILES] * 3 + [G.COMPAT_SIMPLE_LZ4, b"", b"DMNDTYPS"]
+    dec = dt_amd.DecodeBatch(docs)
+    for _ in range(2):
+        dec.run()
+        for i, d in enumerate(docs):
+            want = _host_code(d)
+            assert dec.status(i)["status"] == want, i
+            if want == 0:
+                _same_arrays(dec, i, d)
+
+
+@pytest.mark.parametrize("vec", ["COMPAT_SIMPLE_LZ4", "COMPAT_SIMPLE_1"])
+def test_parse_error_codes_on_every_corruption(vec):
+    """Every single-byte corruption and every truncation: device status == oracle ParseError."""
+    base = bytearray(getattr(G, vec))
+    docs = []
+    for i in range(len(base)):
+        for flip in (0xFF, 0x01, 0x80, 0x7F):
+            b = bytearray(base)
+            b[i] ^= flip
+            docs.append(bytes(b))
+    docs += [bytes(base[:cut]) for cut in range(len(base))]
+    dec = dt_amd.DecodeBatch(docs)
+    dec.run()
+    deferred = 0
+    for i, d in enumerate(docs):
+        got = dec.status(i)["status"]
+        if got == dt_amd.DECODE_DEFER:
+            deferred += 1
+            continue
+        assert got == _oracle_code(d) == _host_code(d), (i, d.hex())
+        if got == 0:
+            _same_arrays(dec, i, d)
+    assert deferred <= len(docs) // 20
+
+
+def test_corrupted_benchmark_file():
+    data = bytearray(G.dt_bytes("friendsforever"))
+    rng = np.random.default_rng(7)
+    docs = []
+    for _ in range(48):
+        b = bytearray(data)
+        b[int(rng.integers(0, len(b)))] ^= int(rng.integers(1, 256))
+        docs.append(bytes(b))
+    for cut in (9, 20, 100, 1000, len(data) // 2, len(data) - 5):
+        docs.append(bytes(data[:cut]))
+    dec = dt_amd.DecodeBatch(docs)
+    dec.run()
+    for i, d in enumerate(docs):
+        got = dec.status(i)["status"]
+        if got == dt_amd.DECODE_DEFER:
+            continue
+        assert got == _host_code(d), i
+    # the same bytes with the CRC check disabled decode like the host decoder does
+    dec2 = dt_amd.DecodeBatch(docs[:16], ignore_crc=True)
+    dec2.run()
+    for i, d in enumerate(docs[:16]):
+        got = dec2.status(i)["status"]
+        if got != dt_amd.DECODE_DEFER:
+            assert got == _host_code(d, ignore_crc=True), i
+            if got == 0:
+                _same_arrays(dec2, i, d, ignore_crc=True)

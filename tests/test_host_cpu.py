@@ -61,7 +61,7 @@ def _code(fn, data):
 def test_parse_error_codes_match_oracle_on_corruption():
     base = bytearray(G.COMPAT_SIMPLE_LZ4)
     for i in range(len(base)):
-        for flip in (0xFF, 0x01, 0x80):
+        for flip in (0xFF, 0x01, 0x80, 0x7F, 0x40, 0x02):
             b = bytearray(base)
             b[i] ^= flip
             d = bytes(b)
