@@ -39,6 +39,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     p.add_argument("--cpu-cores", type=int, default=16)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-decode", action="store_true", help="skip the GPU .dt decode measurement")
     return p.parse_args()
 
 
@@ -72,6 +73,25 @@ def cpu_baseline(data, budget_s, cores):
     return {"value": docs * n_lv / wall, "unit": "merged ops/s", "cores": cores, "kind": "port",
             "sample": f"{docs} x friendsforever.dt checkout_tip (decoded oplog, C oracle) on {cores} host threads, "
                       f"{wall:.2f} s"}
+
+
+def decode_leg(docs, device, steps):
+    """Device `.dt` decode (dt_decode.hip) of the same documents: kernel time from HIP events,
+    throughput over the encoded bytes (the E2E roofline basis of SURVEY.md 8d), parity-checked
+    against the host decoder on document 0."""
+    dec = dt_amd.DecodeBatch(docs, device=device)
+    dec.run()
+    ms = min(dec.run() for _ in range(max(1, min(steps, 5))))
+    bad = sum(1 for i in range(len(docs)) if dec.status(i)["status"] != 0)
+    assert bad == 0, f"{bad} documents failed the device decode"
+    host = dt_amd.ListOpLog.load_from(docs[0])
+    for w in ("ops", "agent_runs", "parents", "char_offsets"):
+        assert (dec.export(0, w) == host.export(w)).all(), w
+    bi, bo = dec.bytes_in(), dec.bytes_out()
+    gbs = bi / (ms / 1000.0) / 1e9
+    return {"kernel": "decode_kernel", "ms": ms, "docs": len(docs), "encoded_GBps": gbs,
+            "soa_written_GBps": bo / (ms / 1000.0) / 1e9, "frac_hbm": (bi + bo) / (ms / 1000.0) / 1e9 / HBM_PEAK_GBS,
+            "bytes_in": bi, "bytes_out": bo}
 
 
 def main():
@@ -177,6 +197,8 @@ def main():
                      "algorithmic_formula": "per doc: 16*op_runs + (8+4*parents)*graph_entries + 12*agent_runs "
                                             "+ inserted_bytes + text_out_bytes (SURVEY.md 8d merge-only)"},
     }
+    if not args.no_decode:   # batched .dt decode on the GPU, same documents
+        out["decode"] = decode_leg([bytes(data) for _ in mine], local_rank if world > 1 else 0, args.steps)
     if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(data, args.cpu_seconds, args.cpu_cores)
     if rank == 0:
