@@ -79,6 +79,7 @@ def decode_leg(docs, device, steps):
     """Device `.dt` decode (dt_decode.hip) of the same documents: kernel time from HIP events,
     throughput over the encoded bytes (the E2E roofline basis of SURVEY.md 8d), parity-checked
     against the host decoder on document 0."""
+    import dt_amd
     dec = dt_amd.DecodeBatch(docs, device=device)
     dec.run()
     ms = min(dec.run() for _ in range(max(1, min(steps, 5))))
