@@ -76,27 +76,16 @@ __device__ __forceinline__ uint32_t wbyte(Win &W, uint32_t off) {
     return (rdl(W.w, d >> 2) >> ((d & 3u) << 3)) & 0xFFu;
 }
 
-// A reader over one byte stream: source s selects the register window (the streams that the
-// main loop interleaves each keep their own): 0 document (chunk headers), 1 LZ4 buffer,
-// 2 OpVersions, 3 OpTypeAndPosition, 4 / 5 ContentIsKnown of inserts / deletes, 6 OpParents.
+// A reader over one byte stream: source s selects the register window, 0 document (chunk
+// headers), 1 LZ4 buffer.  The varint-only streams the main loop interleaves use queues (VQ).
 struct Rd { uint32_t s, p, n; };
-enum : uint32_t { SRC_DOC = 0, SRC_LZ = 1, SRC_AV = 2, SRC_TP = 3, SRC_RUNS_INS = 4, SRC_RUNS_DEL = 5, SRC_HIST = 6 };
+enum : uint32_t { SRC_DOC = 0, SRC_LZ = 1 };
 
 struct Ctx {
-    Win w0, w1, w2, w3, w4, w5, w6;
+    Win w0, w1;
     const uint8_t *in;   // the document
     uint8_t *lz;         // its decompressed LZ4 buffer
-    __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t off) {
-        switch (s) {
-            case SRC_LZ: return wbyte(w1, off);
-            case SRC_AV: return wbyte(w2, off);
-            case SRC_TP: return wbyte(w3, off);
-            case SRC_RUNS_INS: return wbyte(w4, off);
-            case SRC_RUNS_DEL: return wbyte(w5, off);
-            case SRC_HIST: return wbyte(w6, off);
-            default: return wbyte(w0, off);
-        }
-    }
+    __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t off) { return s ? wbyte(w1, off) : wbyte(w0, off); }
     __device__ __forceinline__ const uint8_t *ptr(uint32_t s) const { return s == SRC_LZ ? lz : in; }
 
     // unsigned LEB128 (leb.rs:113-178)
@@ -169,6 +158,85 @@ struct Ctx {
         return t == want ? S_OK : MissingChunk;
     }
 };
+
+// ---------------------------------------------------------------------------------------------
+// varint queues
+// ---------------------------------------------------------------------------------------------
+// A varint-only stream (OpVersions, OpTypeAndPosition, ContentIsKnown, OpParents) is decoded 64
+// bytes at a time: lane i holds byte i, a ballot finds the terminator bytes, each terminator lane
+// assembles its varint from up to 10 preceding bytes with lane shuffles, and the values are
+// compacted into lanes in stream order.  The parser pops them with readlane.  Error entries
+// carry the status the byte-serial reader (leb.rs:113-178) would return at that varint.
+struct VQ {
+    const uint8_t *base;   // stream start
+    uint32_t len;          // stream bytes
+    uint32_t at;           // bytes consumed by popped varints
+    uint32_t wpos;         // end of the last queued varint
+    uint32_t head, cnt;    // queue cursor / size (uniform)
+    uint32_t lo, hi, end;  // lane k: varint k (end = ~0: error entry, lo = its status)
+    __device__ __forceinline__ uint32_t left() const { return len - at; }
+};
+
+__device__ __forceinline__ VQ vq_make(const uint8_t *doc, const Rd &r) {
+    VQ q;
+    q.base = doc + r.p; q.len = r.n; q.at = 0; q.wpos = 0; q.head = 0; q.cnt = 0;
+    q.lo = q.hi = q.end = 0;
+    return q;
+}
+
+__device__ __forceinline__ void vq_refill(VQ &q, uint32_t *scratch) {
+    const uint32_t i = lane();
+    const uint32_t rem = q.len - q.wpos;
+    const uint32_t b = i < rem ? q.base[q.wpos + i] : 0x80u;
+    const uint64_t T = ballot(i < rem && b < 0x80u);
+    q.head = 0;
+    if (!T) {   // no varint ends within the window (or the stream): the reader's verdict
+        q.cnt = 1;
+        q.lo = rem >= 10 ? uint32_t(InvalidVarInt) : uint32_t(UnexpectedEOF);
+        q.end = 0xFFFFFFFFu;
+        return;
+    }
+    const bool term = (T >> i) & 1;
+    const uint64_t below = T & lt_mask();
+    const uint32_t start = below ? uint32_t(64 - __clzll((long long)below)) : 0u;
+    const uint32_t L = i - start + 1;
+    uint64_t v = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 10; j++) {
+        const uint32_t bj = uint32_t(__shfl(int(b), int(i >= j ? i - j : 0)));
+        if (j < L) v |= uint64_t(bj & 0x7fu) << (7 * (L - 1 - j));
+    }
+    const bool err = L > 10 || (L == 10 && (b & 0x7fu) > 1u);
+    if (term) {
+        const uint32_t k = popc(below);
+        scratch[3 * k] = err ? uint32_t(InvalidVarInt) : uint32_t(v);
+        scratch[3 * k + 1] = uint32_t(v >> 32);
+        scratch[3 * k + 2] = err ? 0xFFFFFFFFu : q.wpos + i + 1;
+    }
+    __syncthreads();
+    q.cnt = popc(T);
+    if (i < q.cnt) { q.lo = scratch[3 * i]; q.hi = scratch[3 * i + 1]; q.end = scratch[3 * i + 2]; }
+    __syncthreads();
+    q.wpos += uint32_t(64 - __clzll((long long)T));
+}
+
+// Reader::u64v on a queue
+__device__ __forceinline__ int vq_pop(VQ &q, uint64_t &v, uint32_t *scratch) {
+    if (q.at >= q.len) return UnexpectedEOF;
+    if (q.head == q.cnt) vq_refill(q, scratch);
+    const uint32_t e = rdl(q.end, q.head);
+    if (e == 0xFFFFFFFFu) return int(rdl(q.lo, q.head));
+    v = uint64_t(rdl(q.lo, q.head)) | (uint64_t(rdl(q.hi, q.head)) << 32);
+    q.at = e;
+    q.head++;
+    return S_OK;
+}
+__device__ __forceinline__ int vq_zigzag(VQ &q, int64_t &v, uint32_t *scratch) {
+    uint64_t u;
+    TRY(vq_pop(q, u, scratch));
+    v = int64_t(u >> 1) * ((u & 1) ? -1 : 1);
+    return S_OK;
+}
 
 // ---------------------------------------------------------------------------------------------
 // lane-parallel helpers
@@ -377,11 +445,13 @@ struct Lds {                 // per-wave tables, F = max file agents of the batc
     uint32_t *amono;         // agent id -> 1 if its runs' seq ranges increase in LV order
     uint32_t *crc;           // CRC-32C table (256)
     uint32_t *fr;            // frontier compaction scratch (64)
+    uint32_t *vq;            // varint queue compaction scratch (192)
 };
 
 struct CRuns {               // ContentIsKnown run iterator (ReadPatchContentIter)
     uint32_t present, ascii;
-    Rd runs, text;
+    VQ runs;
+    Rd text;
     uint32_t t0;                 // where the text started
     uint32_t pb, pb_known;
     uint64_t pb_len;
@@ -414,17 +484,18 @@ __device__ __forceinline__ int content_str(Ctx &C, Rd &chunks, Rd &comp, bool ha
     return S_OK;
 }
 
-__device__ __forceinline__ int cruns_next(Ctx &C, CRuns &R, bool &has, uint64_t &len, bool &known, Rd &s) {
+__device__ __forceinline__ int cruns_next(Ctx &C, CRuns &R, bool &has, uint64_t &len, bool &known, Rd &s,
+                                          uint32_t *scratch) {
     if (R.pb) {
         R.pb = 0; has = true; len = R.pb_len; known = R.pb_known; s = R.pb_s;
         return S_OK;
     }
-    if (!R.runs.n) {
+    if (!R.runs.left()) {
         if (!R.text.n) { has = false; return S_OK; }
         return UnexpectedEOF;
     }
     uint64_t x;
-    TRY(C.u64v(R.runs, x));
+    TRY(vq_pop(R.runs, x, scratch));
     len = x >> 1;
     known = x & 1;
     s = Rd{R.text.s, R.text.p, 0};
@@ -551,7 +622,6 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
     C.lz = P.lz + D.lz_off;
     C.w0 = Win{C.in, 0x80000000u, 0};
     C.w1 = Win{C.lz, 0x80000000u, 0};
-    C.w2 = C.w3 = C.w4 = C.w5 = C.w6 = C.w0;
     const uint32_t len = D.in_len;
     Out O;
     O.aruns = reinterpret_cast<uint4 *>(P.aruns) + D.arun_off;
@@ -692,19 +762,19 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
         CRuns it{};
         it.present = 1;
         TRY(content_str<SIZE>(C, ch, comp, has_comp, it.text, it.ascii));
-        TRY(C.expect_chunk(ch, 25, it.runs));
-        it.runs.s = tag == 0 ? SRC_RUNS_INS : SRC_RUNS_DEL;
+        Rd runs;
+        TRY(C.expect_chunk(ch, 25, runs));
+        it.runs = vq_make(C.in, runs);
         it.t0 = it.text.p;
-        cik_bytes += it.runs.n;
+        cik_bytes += runs.n;
         if (tag == 0) ins = it; else del = it;
     }
     Rd av, tp, hist;
     TRY(C.expect_chunk(pc, 21, av));
     TRY(C.expect_chunk(pc, 22, tp));
     TRY(C.expect_chunk(pc, 23, hist));
-    av.s = SRC_AV;
-    tp.s = SRC_TP;
-    hist.s = SRC_HIST;
+    VQ qav = vq_make(C.in, av), qtp = vq_make(C.in, tp), qhist = vq_make(C.in, hist);
+    uint32_t *vs = L.vq;
     prof_mark(1);
 
     if (SIZE) {   // OpVersions: LV count and agent runs
@@ -713,13 +783,13 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
         R.tp_bytes = tp.n;
         R.cik_bytes = cik_bytes;
         R.hist_bytes = hist.n;
-        while (av.n) {
+        while (qav.left()) {
             uint64_t n, alen;
             int64_t jump = 0;
-            TRY(C.u64v(av, n));
+            TRY(vq_pop(qav, n, vs));
             const bool hj = n & 1;
-            TRY(C.u64v(av, alen));
-            if (hj) TRY(C.zigzag(av, jump));
+            TRY(vq_pop(qav, alen, vs));
+            if (hj) TRY(vq_zigzag(qav, jump, vs));
             lv += alen;
             runs++;
             R.raw_aruns = runs;   // partial counts size a pass that fails later
@@ -760,14 +830,14 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
         for (uint64_t i = lane(); i < k; i += 64) O.cbyte[lv0 + i] = v;
     };
 
-    while (av.n) {
+    while (qav.left()) {
         uint64_t n, alen;
         int64_t jump = 0;
-        TRY(C.u64v(av, n));
+        TRY(vq_pop(qav, n, vs));
         const bool has_jump = n & 1;
         n >>= 1;
-        TRY(C.u64v(av, alen));
-        if (has_jump) TRY(C.zigzag(av, jump));
+        TRY(vq_pop(qav, alen, vs));
+        if (has_jump) TRY(vq_zigzag(qav, jump, vs));
         if (n == 0 || n - 1 >= n_file) return InvalidLength;
         const uint32_t fa = uint32_t(n - 1);
         const int64_t sstart = int64_t(L.fseq[fa]) + jump;
@@ -788,9 +858,9 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
         uint64_t want = alen;
         while (want) {
             if (!have_op) {
-                if (!tp.n) return InvalidLength;
+                if (!qtp.left()) return InvalidLength;
                 uint64_t x;
-                TRY(C.u64v(tp, x));
+                TRY(vq_pop(qtp, x, vs));
                 const bool has_length = x & 1; x >>= 1;
                 const bool diff_nz = x & 1; x >>= 1;
                 const bool is_del = x & 1; x >>= 1;
@@ -799,7 +869,7 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
                 uint64_t l;
                 if (has_length) {
                     if (is_del) { fwd = x & 1; x >>= 1; }
-                    if (diff_nz) TRY(C.zigzag(tp, diff));
+                    if (diff_nz) TRY(vq_zigzag(qtp, diff, vs));
                     l = x;
                 } else {
                     l = 1;
@@ -820,7 +890,7 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
             Rd cs{0, 0, 0};
             if (ci.present) {
                 bool has, cknown; uint64_t clen;
-                TRY(cruns_next(C, ci, has, clen, cknown, cs));
+                TRY(cruns_next(C, ci, has, clen, cknown, cs, vs));
                 if (!has) return InvalidLength;
                 if (clen < take) take = clen;
                 if (clen > take) {   // push the remainder back
@@ -916,14 +986,14 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
     uint32_t pe_valid = 0, pe_start = 0, pe_end = 0, pe_poff = 0;   // pending graph entry
     uint32_t n_ent = 0, n_par = 0;
     uint32_t fr = 0, fn = 0;   // frontier: lane k holds element k (sorted)
-    while (hist.n) {
+    while (qhist.left()) {
         uint64_t hl;
-        TRY(C.u64v(hist, hl));
+        TRY(vq_pop(qhist, hl, vs));
         uint32_t parv = 0, np = 0;
         bool par_bad = false;   // next_time - n underflowed (fails the range check below)
         for (;;) {
             uint64_t n;
-            TRY(C.u64v(hist, n));
+            TRY(vq_pop(qhist, n, vs));
             const bool foreign = n & 1; n >>= 1;
             const bool more = n & 1; n >>= 1;
             uint64_t p;
@@ -931,7 +1001,7 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
                 if (n == 0) break;
                 if (n - 1 >= n_file) return InvalidLength;
                 uint64_t seq;
-                TRY(C.u64v(hist, seq));
+                TRY(vq_pop(qhist, seq, vs));
                 const int64_t lv = lookup_lv(O, L, L.fmap[n - 1], seq);
                 if (lv < 0) return InvalidLength;
                 p = uint64_t(lv);
@@ -992,12 +1062,12 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
     if (pc.n) return InvalidLength;
     if (ins.present) {   // the content iterators must be exhausted
         bool has, kn; uint64_t l; Rd s;
-        const int e = cruns_next(C, ins, has, l, kn, s);
+        const int e = cruns_next(C, ins, has, l, kn, s, vs);
         if (e || has) return InvalidContent;
     }
     if (del.present) {
         bool has, kn; uint64_t l; Rd s;
-        const int e = cruns_next(C, del, has, l, kn, s);
+        const int e = cruns_next(C, del, has, l, kn, s, vs);
         if (e || has) return InvalidContent;
     }
     {   // CRC (decode_oplog.rs:940-955)
@@ -1102,7 +1172,8 @@ __global__ __launch_bounds__(64) void decode_kernel(DecodeParams P) {
     const uint32_t F = P.max_file_agents;
     L.crc = lds;
     L.fr = lds + 256;
-    L.fmap = lds + 320;
+    L.vq = lds + 320;
+    L.fmap = lds + 512;
     L.fseq = L.fmap + F;
     L.noff = L.fseq + F;
     L.nlen = L.noff + F;
@@ -1130,7 +1201,7 @@ __global__ __launch_bounds__(64) void decode_kernel(DecodeParams P) {
 
 int launch_decode(const DecodeParams &p, void *stream) {
     if (!p.n_docs) return 0;
-    const size_t lds = (320 + 8 * size_t(p.max_file_agents)) * 4;
+    const size_t lds = (512 + 8 * size_t(p.max_file_agents)) * 4;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (p.size_only)
         hipLaunchKernelGGL(ddec::decode_kernel<true>, dim3(p.n_docs), dim3(64), lds, s, p);

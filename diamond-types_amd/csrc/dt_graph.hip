@@ -1,0 +1,397 @@
+// dt_graph.hip -- batched causal-graph queries on MI355X.
+//
+// One 64-lane wavefront answers one query against one graph held in HBM (entries as
+// (start, end, shadow, parents offset) quads plus a parents array, the layout of
+// graph/mod.rs:25-53).  The three queries walk the graph from the newest versions down with a
+// max-priority queue, as the reference does, because the conflict-span fixtures pin the walk
+// order (spans come out newest-first, merged when contiguous):
+//   DIFF      Graph::diff_rev / diff_slow_internal        src/causalgraph/graph/tools.rs:176-292
+//   CONFLICT  Graph::find_conflicting(_slow)              tools.rs:296-484 (TimePoint heap)
+//   CONTAINS  Graph::frontier_contains_version            tools.rs:88-146 (shadow shortcut)
+// The queues live in LDS (per wave); the walk is wave-uniform scalar code and the batch gives
+// the parallelism: every query of the batch runs concurrently, one per wavefront.  (The
+// checkout path itself diffs versions with per-chain version vectors in dt_plan.hip; these
+// kernels serve merge(from != ROOT) callers and the graph fixtures.)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dt_graph.hpp"
+
+namespace dtgpu {
+namespace gdev {
+
+constexpr int KEY_CAP = 256;     // diff / contains queue (entries)
+constexpr int TP_CAP = 64;       // find_conflicting queue (time points)
+constexpr int TP_WORDS = 4 + GQ_MAX_FRONTIER;
+enum : uint32_t { F_A = 0, F_B = 1, F_S = 2 };
+
+struct Ent { int32_t start, end, shadow; uint32_t poff; };
+
+struct G {
+    const Ent *e;          // n + 1 quads (the last one carries the parents end offset)
+    const uint32_t *par;
+    uint32_t n;
+    __device__ __forceinline__ uint32_t find(int32_t lv) const {   // entry holding lv, or n
+        uint32_t lo = 0, hi = n;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (lv >= e[mid].end) lo = mid + 1; else hi = mid;
+        }
+        return lo < n && lv >= e[lo].start ? lo : n;
+    }
+};
+
+// ---- max-heap of (lv << 2 | flag) keys in LDS (BinaryHeap<(LV, DiffFlag)>) ------------------
+struct KHeap {
+    uint32_t *v;
+    uint32_t n;
+    __device__ __forceinline__ bool push(uint32_t k) {
+        if (n >= uint32_t(KEY_CAP)) return false;
+        uint32_t i = n++;
+        while (i > 0) {
+            const uint32_t p = (i - 1) >> 1;
+            const uint32_t vp = v[p];
+            if (vp >= k) break;
+            v[i] = vp;
+            i = p;
+        }
+        v[i] = k;
+        return true;
+    }
+    __device__ __forceinline__ uint32_t top() const { return v[0]; }
+    __device__ __forceinline__ uint32_t pop() {
+        const uint32_t t = v[0];
+        const uint32_t x = v[--n];
+        uint32_t i = 0;
+        for (;;) {
+            const uint32_t l = 2 * i + 1, r = l + 1;
+            uint32_t m = i, vm = x;
+            if (l < n && v[l] > vm) { m = l; vm = v[l]; }
+            if (r < n && v[r] > vm) { m = r; vm = v[r]; }
+            if (m == i) break;
+            v[i] = vm;
+            i = m;
+        }
+        if (n) v[i] = x;
+        return t;
+    }
+};
+__device__ __forceinline__ int32_t k_lv(uint32_t k) { return int32_t(k >> 2); }
+__device__ __forceinline__ uint32_t k_fl(uint32_t k) { return k & 3u; }
+__device__ __forceinline__ uint32_t mkkey(int32_t lv, uint32_t f) { return (uint32_t(lv) << 2) | f; }
+
+// Span lists written newest-first, merging a span that ends where the previous one starts
+// (push_reversed_rle / the harness's push_rev_rle).
+struct Spans {
+    uint32_t *out;
+    uint32_t cap, n, words;   // words per span: 2 (diff) or 3 (with flag)
+    int32_t ls, le;
+    uint32_t lf;
+    bool have, overflow;
+    __device__ __forceinline__ void init(uint32_t *o, uint32_t c, uint32_t w) {
+        out = o; cap = c; n = 0; words = w; have = false; overflow = false; ls = le = 0; lf = 0;
+    }
+    __device__ __forceinline__ void flush() {
+        if (!have) return;
+        if (n >= cap) { overflow = true; have = false; return; }
+        if (__lane_id() == 0) {
+            out[words * n] = uint32_t(ls);
+            out[words * n + 1] = uint32_t(le);
+            if (words == 3) out[words * n + 2] = lf;
+        }
+        n++;
+        have = false;
+    }
+    __device__ __forceinline__ void push(int32_t s, int32_t e, uint32_t f) {
+        if (have && lf == f && ls == e) { ls = s; return; }
+        flush();
+        have = true; ls = s; le = e; lf = f;
+    }
+};
+
+// ---- diff_rev (tools.rs:176-292) --------------------------------------------------------------
+__device__ __forceinline__ uint32_t q_diff(const G &g, const GraphQuery &q, uint32_t *heap, Spans &sa, Spans &sb) {
+    const int32_t *a = q.a, *b = q.b;
+    bool same = q.na == q.nb;
+    for (uint32_t i = 0; same && i < q.na; i++) same = a[i] == b[i];
+    if (same) return GQ_OK;
+    if (q.na == 1 && q.nb == 1) {   // is_direct_descendant_coarse
+        const int32_t x = a[0], y = b[0];
+        const uint32_t ex = g.find(x), ey = g.find(y);
+        if (ex == g.n || ey == g.n) return GQ_BAD_INPUT;
+        if (x > y && y >= g.e[ex].start) { sa.push(y + 1, x + 1, 0); return GQ_OK; }
+        if (y > x && x >= g.e[ey].start) { sb.push(x + 1, y + 1, 0); return GQ_OK; }
+    }
+    KHeap h{heap, 0};
+    for (uint32_t i = 0; i < q.na; i++) if (!h.push(mkkey(a[i], F_A))) return GQ_OVERFLOW;
+    for (uint32_t i = 0; i < q.nb; i++) if (!h.push(mkkey(b[i], F_B))) return GQ_OVERFLOW;
+    int32_t shared = 0;
+    while (h.n) {
+        const uint32_t it = h.pop();
+        int32_t ord = k_lv(it);
+        uint32_t flag = k_fl(it);
+        if (flag == F_S) shared--;
+        while (h.n && k_lv(h.top()) == ord) {
+            const uint32_t pk = h.top();
+            if (k_fl(pk) != flag) flag = F_S;
+            if (k_fl(pk) == F_S) shared--;
+            h.pop();
+        }
+        const uint32_t ei = g.find(ord);
+        if (ei == g.n) return GQ_BAD_INPUT;
+        const Ent e = g.e[ei];
+        while (h.n && k_lv(h.top()) >= e.start) {
+            const uint32_t pk = h.top();
+            if (k_fl(pk) != flag) {
+                if (flag == F_A) sa.push(k_lv(pk) + 1, ord + 1, 0);
+                else if (flag == F_B) sb.push(k_lv(pk) + 1, ord + 1, 0);
+                ord = k_lv(pk);
+                flag = F_S;
+            }
+            if (k_fl(pk) == F_S) shared--;
+            h.pop();
+        }
+        if (flag == F_A) sa.push(e.start, ord + 1, 0);
+        else if (flag == F_B) sb.push(e.start, ord + 1, 0);
+        const uint32_t p1 = g.e[ei + 1].poff;
+        for (uint32_t k = e.poff; k < p1; k++) {
+            if (!h.push(mkkey(int32_t(g.par[k]), flag))) return GQ_OVERFLOW;
+            if (flag == F_S) shared++;
+        }
+        if (int32_t(h.n) == shared) break;
+    }
+    return GQ_OK;
+}
+
+// ---- frontier_contains_version (tools.rs:88-146) ----------------------------------------------
+__device__ __forceinline__ uint32_t q_contains(const G &g, const GraphQuery &q, uint32_t *heap, uint32_t &found) {
+    const int32_t t = q.target;
+    found = 0;
+    if (t < 0) { found = 1; return GQ_OK; }   // ROOT is in every version
+    for (uint32_t i = 0; i < q.na; i++) if (q.a[i] == t) { found = 1; return GQ_OK; }
+    if (!q.na) return GQ_OK;
+    for (uint32_t i = 0; i < q.na; i++) {
+        if (q.a[i] > t) {
+            const uint32_t ei = g.find(q.a[i]);
+            if (ei == g.n) return GQ_BAD_INPUT;
+            if (t >= g.e[ei].shadow) { found = 1; return GQ_OK; }
+        }
+    }
+    KHeap h{heap, 0};
+    for (uint32_t i = 0; i < q.na; i++) if (q.a[i] > t && !h.push(mkkey(q.a[i], 0))) return GQ_OVERFLOW;
+    while (h.n) {
+        const int32_t ord = k_lv(h.pop());
+        const uint32_t ei = g.find(ord);
+        if (ei == g.n) return GQ_BAD_INPUT;
+        const Ent e = g.e[ei];
+        if (t >= e.shadow) { found = 1; return GQ_OK; }
+        while (h.n && k_lv(h.top()) >= e.start) h.pop();
+        const uint32_t p1 = g.e[ei + 1].poff;
+        for (uint32_t k = e.poff; k < p1; k++) {
+            const int32_t p = int32_t(g.par[k]);
+            if (p == t) { found = 1; return GQ_OK; }
+            if (p > t && !h.push(mkkey(p, 0))) return GQ_OVERFLOW;
+        }
+    }
+    return GQ_OK;
+}
+
+// ---- find_conflicting (tools.rs:296-484) ------------------------------------------------------
+// TimePoint = (last, merged_with), compared by last + 1 (ROOT first), then fewer merged_with is
+// greater, then the flag (the Ord of (TimePoint, DiffFlag)).  LDS layout per time point:
+// [last, nm, flag, pad, merged_with...].
+struct TPHeap {
+    uint32_t *v;   // TP_CAP * TP_WORDS
+    uint32_t n;
+    __device__ __forceinline__ uint32_t *at(uint32_t i) const { return v + i * TP_WORDS; }
+    __device__ __forceinline__ static int cmp(const uint32_t *x, const uint32_t *y) {
+        const uint32_t lx = x[0] + 1u, ly = y[0] + 1u;   // ROOT (-1) -> 0
+        if (lx != ly) return lx < ly ? -1 : 1;
+        if (x[1] != y[1]) return x[1] > y[1] ? -1 : 1;
+        if (x[2] != y[2]) return x[2] < y[2] ? -1 : 1;
+        return 0;
+    }
+    __device__ __forceinline__ static void copy(uint32_t *d, const uint32_t *s) {
+        for (int w = 0; w < TP_WORDS; w++) d[w] = s[w];
+    }
+    __device__ __forceinline__ static void swap(uint32_t *x, uint32_t *y) {
+        for (int w = 0; w < TP_WORDS; w++) { const uint32_t t = x[w]; x[w] = y[w]; y[w] = t; }
+    }
+    __device__ __forceinline__ bool push(const uint32_t *tp) {
+        if (n >= uint32_t(TP_CAP)) return false;
+        uint32_t i = n++;
+        copy(at(i), tp);
+        while (i > 0) {
+            const uint32_t p = (i - 1) >> 1;
+            if (cmp(at(i), at(p)) <= 0) break;
+            swap(at(i), at(p));
+            i = p;
+        }
+        return true;
+    }
+    __device__ __forceinline__ void pop(uint32_t *out) {
+        copy(out, at(0));
+        n--;
+        if (n) copy(at(0), at(n));
+        uint32_t i = 0;
+        for (;;) {
+            const uint32_t l = 2 * i + 1, r = l + 1;
+            uint32_t m = i;
+            if (l < n && cmp(at(l), at(m)) > 0) m = l;
+            if (r < n && cmp(at(r), at(m)) > 0) m = r;
+            if (m == i) break;
+            swap(at(i), at(m));
+            i = m;
+        }
+    }
+    __device__ __forceinline__ static bool eq_time(const uint32_t *x, const uint32_t *y) {
+        if (x[0] != y[0] || x[1] != y[1]) return false;
+        for (uint32_t k = 0; k < x[1]; k++) if (x[4 + k] != y[4 + k]) return false;
+        return true;
+    }
+};
+// TimePoint from a sorted frontier (last = newest, merged_with = the rest)
+__device__ __forceinline__ void tp_make(uint32_t *t, const int32_t *f, uint32_t n, uint32_t flag) {
+    t[0] = n ? uint32_t(f[n - 1]) : 0xFFFFFFFFu;
+    t[1] = n > 1 ? n - 1 : 0;
+    t[2] = flag;
+    t[3] = 0;
+    for (uint32_t k = 0; k + 1 < n; k++) t[4 + k] = uint32_t(f[k]);
+}
+__device__ __forceinline__ void tp_one(uint32_t *t, uint32_t lv, uint32_t flag) {
+    t[0] = lv; t[1] = 0; t[2] = flag; t[3] = 0;
+}
+
+__device__ __forceinline__ uint32_t q_conflict(const G &g, const GraphQuery &q, uint32_t *tpv, uint32_t *scratch,
+                                               Spans &sp, int32_t *common, uint32_t &nc) {
+    nc = 0;
+    bool same = q.na == q.nb;
+    for (uint32_t i = 0; same && i < q.na; i++) same = q.a[i] == q.b[i];
+    if (same) {
+        for (uint32_t i = 0; i < q.na; i++) common[nc++] = q.a[i];
+        return GQ_OK;
+    }
+    if (q.na == 1 && q.nb == 1) {
+        const int32_t x = q.a[0], y = q.b[0];
+        const uint32_t ex = g.find(x), ey = g.find(y);
+        if (ex == g.n || ey == g.n) return GQ_BAD_INPUT;
+        if (x > y && y >= g.e[ex].start) { sp.push(y + 1, x + 1, F_A); common[nc++] = y; return GQ_OK; }
+        if (y > x && x >= g.e[ey].start) { sp.push(x + 1, y + 1, F_B); common[nc++] = x; return GQ_OK; }
+    }
+    TPHeap h{tpv, 0};
+    uint32_t *tm = scratch, *tmp = scratch + TP_WORDS, *pk = scratch + 2 * TP_WORDS;
+    tp_make(tmp, q.a, q.na, F_A);
+    if (!h.push(tmp)) return GQ_OVERFLOW;
+    tp_make(tmp, q.b, q.nb, F_B);
+    if (!h.push(tmp)) return GQ_OVERFLOW;
+    for (;;) {
+        h.pop(tm);
+        uint32_t flag = tm[2];
+        const int32_t t = int32_t(tm[0]);
+        if (t < 0) return GQ_OK;   // ROOT: nothing in common
+        while (h.n && TPHeap::eq_time(h.at(0), tm)) {
+            if (h.at(0)[2] != flag) flag = F_S;
+            h.pop(tmp);
+        }
+        if (!h.n) {
+            for (uint32_t k = 0; k < tm[1]; k++) common[nc++] = int32_t(tm[4 + k]);
+            common[nc++] = t;
+            return GQ_OK;
+        }
+        for (uint32_t k = 0; k < tm[1]; k++) {   // shatter a merge point
+            tp_one(tmp, tm[4 + k], flag);
+            if (!h.push(tmp)) return GQ_OVERFLOW;
+        }
+        const uint32_t ei = g.find(t);
+        if (ei == g.n) return GQ_BAD_INPUT;
+        const Ent e = g.e[ei];
+        int32_t rs = e.start, re = t + 1;
+        for (;;) {
+            if (!h.n) {
+                common[nc++] = re - 1;
+                return GQ_OK;
+            }
+            const int32_t pl = int32_t(h.at(0)[0]);
+            if (pl >= 0 && pl >= e.start) {   // the next point lies inside this entry: consume it
+                h.pop(pk);
+                const uint32_t next_flag = pk[2];
+                if (int32_t(pk[0]) + 1 < re) {
+                    const int32_t cut = rs + (int32_t(pk[0]) + 1 - e.start);   // range.truncate
+                    sp.push(cut, re, flag);
+                    re = cut;
+                }
+                for (uint32_t k = 0; k < pk[1]; k++) {
+                    tp_one(tmp, pk[4 + k], next_flag);
+                    if (!h.push(tmp)) return GQ_OVERFLOW;
+                }
+                if (next_flag != flag) flag = F_S;
+            } else {   // emit the rest of the entry and continue from its parents
+                sp.push(rs, re, flag);
+                const uint32_t p0 = e.poff, p1 = g.e[ei + 1].poff;
+                const uint32_t np = p1 - p0;
+                if (np > GQ_MAX_FRONTIER) return GQ_OVERFLOW;
+                tmp[0] = np ? g.par[p1 - 1] : 0xFFFFFFFFu;
+                tmp[1] = np > 1 ? np - 1 : 0;
+                tmp[2] = flag;
+                tmp[3] = 0;
+                for (uint32_t k = 0; k + 1 < np; k++) tmp[4 + k] = g.par[p0 + k];
+                if (!h.push(tmp)) return GQ_OVERFLOW;
+                break;
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(64) void graph_query_kernel(GraphParams P) {
+    __shared__ uint32_t heap[KEY_CAP];
+    __shared__ uint32_t tpv[TP_CAP * TP_WORDS];
+    __shared__ uint32_t scratch[3 * TP_WORDS];
+    const uint32_t qi = blockIdx.x;
+    if (qi >= P.n_queries) return;
+    const GraphQuery q = P.queries[qi];
+    G g{reinterpret_cast<const Ent *>(P.ents) + q.ent_off, P.par, q.n_ent};
+    GraphResult r{};
+    uint32_t *out = P.out + size_t(q.out_off);
+    uint32_t st = GQ_OK;
+    if (q.na > GQ_MAX_FRONTIER || q.nb > GQ_MAX_FRONTIER) {
+        st = GQ_BAD_INPUT;
+    } else if (q.kind == GQ_DIFF) {
+        Spans sa, sb;
+        sa.init(out, q.out_cap / 4, 2);
+        sb.init(out + 2 * (q.out_cap / 4), q.out_cap / 4, 2);
+        st = q_diff(g, q, heap, sa, sb);
+        sa.flush();
+        sb.flush();
+        if (st == GQ_OK && (sa.overflow || sb.overflow)) st = GQ_OVERFLOW;
+        r.n0 = sa.n;
+        r.n1 = sb.n;
+    } else if (q.kind == GQ_CONFLICT) {
+        Spans sp;
+        sp.init(out, q.out_cap / 3, 3);
+        uint32_t nc = 0;
+        st = q_conflict(g, q, tpv, scratch, sp, r.common, nc);
+        sp.flush();
+        if (st == GQ_OK && sp.overflow) st = GQ_OVERFLOW;
+        r.n0 = sp.n;
+        r.n_common = nc;
+    } else if (q.kind == GQ_CONTAINS) {
+        uint32_t f = 0;
+        st = q_contains(g, q, heap, f);
+        r.n0 = f;
+    } else {
+        st = GQ_BAD_INPUT;
+    }
+    r.status = st;
+    if (__lane_id() == 0) P.results[qi] = r;
+}
+
+}  // namespace gdev
+
+int launch_graph_queries(const GraphParams &p, void *stream) {
+    if (!p.n_queries) return 0;
+    hipLaunchKernelGGL(gdev::graph_query_kernel, dim3(p.n_queries), dim3(64), 0,
+                       reinterpret_cast<hipStream_t>(stream), p);
+    return hipGetLastError() == hipSuccess ? 0 : 66;
+}
+
+}  // namespace dtgpu

@@ -1,0 +1,35 @@
+// dt_graph.hpp -- host/device layout of the batched causal-graph queries (dt_graph.hip).
+#pragma once
+#include <stdint.h>
+
+namespace dtgpu {
+
+constexpr uint32_t GQ_MAX_FRONTIER = 16;
+enum : uint32_t { GQ_DIFF = 0, GQ_CONFLICT = 1, GQ_CONTAINS = 2 };
+enum : uint32_t { GQ_OK = 0, GQ_OVERFLOW = 1, GQ_BAD_INPUT = 2 };
+
+// Graph arena: per graph, n_ent + 1 quads (start, end, shadow, parents offset); the extra quad
+// carries the parents end offset.  Parents are absolute offsets into one parents array.
+struct GraphQuery {
+    uint32_t kind, ent_off, n_ent, na, nb, out_off, out_cap;
+    int32_t target;                      // CONTAINS (-1 = ROOT)
+    int32_t a[GQ_MAX_FRONTIER], b[GQ_MAX_FRONTIER];
+};
+
+struct GraphResult {
+    uint32_t status, n0, n1, n_common;   // DIFF: spans only-a / only-b; CONFLICT: spans; CONTAINS: n0 = 0/1
+    int32_t common[GQ_MAX_FRONTIER];
+};
+
+struct GraphParams {
+    const uint32_t *ents;
+    const uint32_t *par;
+    uint32_t *out;                       // DIFF: pairs, a then b (out_cap / 4 each); CONFLICT: triples
+    const GraphQuery *queries;
+    GraphResult *results;
+    uint32_t n_queries;
+};
+
+int launch_graph_queries(const GraphParams &p, void *stream);
+
+}  // namespace dtgpu

@@ -1,0 +1,140 @@
+// dtgpu_graph.cpp -- C ABI of the batched causal-graph queries (include/dtgpu.h,
+// dtgpu_graph_queries).  Graphs arrive as the reference's GraphEntrySimple lists and are built
+// with Graph::push (entry merging and shadows as graph/mod.rs:85-128 computes them), then every
+// query of the batch runs on the device, one wavefront each (dt_graph.hip).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "../../include/dtgpu.h"
+#include "dt_devbuf.hpp"
+#include "dt_graph.hpp"
+#include "dt_host.hpp"
+
+using namespace dtgpu;
+
+extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *hist_off, size_t n_graphs,
+                                            const dtgpu_graph_query *queries, size_t nq, int64_t *spans,
+                                            size_t span_cap, dtgpu_graph_answer *answers, float *ms) {
+    if ((n_graphs && (!hist || !hist_off)) || (nq && (!queries || !answers)) || (nq && span_cap && !spans))
+        return DTGPU_ERR_ARG;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return DTGPU_ERR_NO_DEVICE;
+    // graphs -> entry quads + parents
+    std::vector<uint32_t> ents, par;
+    std::vector<uint32_t> goff(n_graphs), gn(n_graphs);
+    for (size_t g = 0; g < n_graphs; g++) {
+        Graph G;
+        for (size_t i = hist_off[g]; i < hist_off[g + 1];) {
+            if (i + 3 > hist_off[g + 1]) return DTGPU_ERR_ARG;
+            const int64_t s = hist[i], e = hist[i + 1], np = hist[i + 2];
+            if (s < 0 || e <= s || e >= (int64_t(1) << 30) || np < 0 || i + 3 + size_t(np) > hist_off[g + 1])
+                return DTGPU_ERR_ARG;
+            std::vector<uint64_t> p(static_cast<size_t>(np));
+            for (int64_t k = 0; k < np; k++) {
+                if (hist[i + 3 + k] < 0 || hist[i + 3 + k] >= s) return DTGPU_ERR_ARG;
+                p[size_t(k)] = uint64_t(hist[i + 3 + k]);
+            }
+            G.push(p, uint64_t(s), uint64_t(e));
+            i += 3 + size_t(np);
+        }
+        goff[g] = uint32_t(ents.size() / 4);
+        gn[g] = uint32_t(G.entries.size());
+        for (const GraphEntry &e : G.entries) {
+            ents.push_back(uint32_t(e.start));
+            ents.push_back(uint32_t(e.end));
+            ents.push_back(uint32_t(e.shadow));
+            ents.push_back(uint32_t(par.size()));
+            for (uint64_t p : e.parents) par.push_back(uint32_t(p));
+        }
+        ents.insert(ents.end(), {0u, 0u, 0u, uint32_t(par.size())});
+    }
+    std::vector<GraphQuery> q(nq);
+    const uint32_t out_cap = uint32_t(4 * std::max<size_t>(span_cap, 1));
+    for (size_t i = 0; i < nq; i++) {
+        const dtgpu_graph_query &s = queries[i];
+        GraphQuery &d = q[i];
+        std::memset(&d, 0, sizeof d);
+        if (s.graph >= n_graphs || s.na > GQ_MAX_FRONTIER || s.nb > GQ_MAX_FRONTIER || s.kind > 2) return DTGPU_ERR_ARG;
+        d.kind = s.kind;
+        d.ent_off = goff[s.graph];
+        d.n_ent = gn[s.graph];
+        d.na = s.na;
+        d.nb = s.nb;
+        for (uint32_t k = 0; k < s.na; k++) d.a[k] = int32_t(s.a[k]);
+        for (uint32_t k = 0; k < s.nb; k++) d.b[k] = int32_t(s.b[k]);
+        d.target = int32_t(std::max<int64_t>(s.target, -1));
+        d.out_off = uint32_t(i) * out_cap;
+        d.out_cap = out_cap;
+    }
+    hipStream_t st = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    DevBuf<uint32_t> d_ents, d_par, d_out;
+    DevBuf<GraphQuery> d_q;
+    DevBuf<GraphResult> d_r;
+    dtgpu_status rc = DTGPU_OK;
+    std::vector<GraphResult> res(nq);
+    std::vector<uint32_t> out(size_t(nq) * out_cap);
+    do {
+#define CK(x) do { if ((x) != hipSuccess) { rc = DTGPU_ERR_HIP; goto done; } } while (0)
+        CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        CK(hipEventCreate(&e0));
+        CK(hipEventCreate(&e1));
+        CK(d_ents.upload(ents, st));
+        CK(d_par.upload(par, st));
+        CK(d_q.upload(q, st));
+        CK(d_r.alloc(nq));
+        CK(d_out.alloc(out.size()));
+        {
+            GraphParams P{d_ents.p, d_par.p, d_out.p, d_q.p, d_r.p, uint32_t(nq)};
+            CK(hipEventRecord(e0, st));
+            if (launch_graph_queries(P, st)) { rc = DTGPU_ERR_HIP; goto done; }
+            CK(hipEventRecord(e1, st));
+        }
+        if (nq) {
+            CK(hipMemcpyAsync(res.data(), d_r.p, nq * sizeof(GraphResult), hipMemcpyDeviceToHost, st));
+            CK(hipMemcpyAsync(out.data(), d_out.p, out.size() * 4, hipMemcpyDeviceToHost, st));
+        }
+        CK(hipStreamSynchronize(st));
+        if (ms) {
+            float t = 0;
+            CK(hipEventElapsedTime(&t, e0, e1));
+            *ms = t;
+        }
+#undef CK
+    } while (false);
+    for (size_t i = 0; i < nq && rc == DTGPU_OK; i++) {
+        const GraphResult &r = res[i];
+        dtgpu_graph_answer &a = answers[i];
+        std::memset(&a, 0, sizeof a);
+        a.status = r.status;
+        const uint32_t *o = out.data() + size_t(i) * out_cap;
+        int64_t *sp = spans ? spans + i * span_cap * 3 : nullptr;
+        if (q[i].kind == GQ_DIFF) {
+            if (r.n0 + r.n1 > span_cap) { a.status = GQ_OVERFLOW; continue; }
+            for (uint32_t k = 0; k < r.n0; k++) { sp[3 * k] = int32_t(o[2 * k]); sp[3 * k + 1] = int32_t(o[2 * k + 1]); sp[3 * k + 2] = 0; }
+            const uint32_t *ob = o + 2 * (out_cap / 4);
+            for (uint32_t k = 0; k < r.n1; k++) {
+                int64_t *t = sp + 3 * (r.n0 + k);
+                t[0] = int32_t(ob[2 * k]); t[1] = int32_t(ob[2 * k + 1]); t[2] = 1;
+            }
+            a.n_a = r.n0;
+            a.n_b = r.n1;
+        } else if (q[i].kind == GQ_CONFLICT) {
+            if (r.n0 > span_cap) { a.status = GQ_OVERFLOW; continue; }
+            for (uint32_t k = 0; k < 3 * r.n0; k++) sp[k] = int32_t(o[k]);
+            a.n_a = r.n0;
+            a.n_common = r.n_common;
+            for (uint32_t k = 0; k < r.n_common && k < GQ_MAX_FRONTIER; k++) a.common[k] = r.common[k];
+        } else {
+            a.n_a = r.n0;
+        }
+    }
+done:
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (st) (void)hipStreamDestroy(st);
+    return rc;
+}

@@ -45,6 +45,17 @@ class BatchOpts(ctypes.Structure):
     _fields_ = [("ignore_crc", ctypes.c_int), ("host_threads", ctypes.c_int), ("device", ctypes.c_int)]
 
 
+class GraphQuery(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_uint32), ("graph", ctypes.c_uint32), ("na", ctypes.c_uint32),
+                ("nb", ctypes.c_uint32), ("a", ctypes.c_int64 * 16), ("b", ctypes.c_int64 * 16),
+                ("target", ctypes.c_int64)]
+
+
+class GraphAnswer(ctypes.Structure):
+    _fields_ = [("status", ctypes.c_uint32), ("n_a", ctypes.c_uint32), ("n_b", ctypes.c_uint32),
+                ("n_common", ctypes.c_uint32), ("common", ctypes.c_int64 * 16)]
+
+
 _lib = None
 
 
@@ -133,6 +144,9 @@ def lib():
     L.dtgpu_decode_last_ms.restype = ctypes.c_float
     L.dtgpu_decode_free.argtypes = [vp]
     L.dtgpu_decode_profile.argtypes = [vp, sz, ctypes.POINTER(ctypes.c_uint32)]
+    L.dtgpu_graph_queries.argtypes = [ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(sz), sz,
+                                      ctypes.POINTER(GraphQuery), sz, ctypes.POINTER(ctypes.c_int64), sz,
+                                      ctypes.POINTER(GraphAnswer), ctypes.POINTER(ctypes.c_float)]
     L.dtgpu_status_str.argtypes = [c]
     L.dtgpu_status_str.restype = ctypes.c_char_p
     _lib = L
@@ -470,6 +484,59 @@ class DecodeBatch:
 
     def bytes_out(self) -> int:
         return lib().dtgpu_decode_bytes(self._h, 1)
+
+
+GQ_KINDS = {"diff": 0, "conflict": 1, "contains": 2}
+DIFF_FLAGS = ["OnlyA", "OnlyB", "Shared"]
+
+
+def graph_queries(graphs, queries, span_cap=512, timing=False):
+    """Batched causal-graph queries on the GPU (dtgpu_graph_queries, one wavefront per query).
+
+    graphs: GraphEntrySimple lists ([{"span": [start, end], "parents": [...]}, ...]).
+    queries: ("diff", g, a, b) -> (only_a, only_b) span lists, newest first (Graph::diff_rev);
+             ("conflict", g, a, b) -> ([(start, end, flag)], common) (Graph::find_conflicting);
+             ("contains", g, frontier, target) -> bool (frontier_contains_version; -1 = ROOT).
+    A query the device could not answer yields ("error", status)."""
+    hist, off = [], [0]
+    for g in graphs:
+        for e in g:
+            hist += [e["span"][0], e["span"][1], len(e["parents"])] + list(e["parents"])
+        off.append(len(hist))
+    H = (ctypes.c_int64 * max(1, len(hist)))(*hist)
+    O = (ctypes.c_size_t * len(off))(*off)
+    nq = len(queries)
+    Q = (GraphQuery * max(1, nq))()
+    for i, (kind, g, a, b) in enumerate(queries):
+        q = Q[i]
+        q.kind, q.graph, q.na = GQ_KINDS[kind], g, len(a)
+        for k, v in enumerate(a):
+            q.a[k] = v
+        if kind == "contains":
+            q.target = b
+        else:
+            q.nb = len(b)
+            for k, v in enumerate(b):
+                q.b[k] = v
+    spans = (ctypes.c_int64 * (max(1, nq) * span_cap * 3))()
+    ans = (GraphAnswer * max(1, nq))()
+    ms = ctypes.c_float()
+    _check(lib().dtgpu_graph_queries(H, O, len(graphs), Q, nq, spans, span_cap, ans, ctypes.byref(ms)))
+    out = []
+    for i, (kind, _g, _a, _b) in enumerate(queries):
+        r = ans[i]
+        if r.status:
+            out.append(("error", r.status))
+            continue
+        base = 3 * span_cap * i
+        tri = [(spans[base + 3 * k], spans[base + 3 * k + 1], spans[base + 3 * k + 2]) for k in range(r.n_a + r.n_b)]
+        if kind == "diff":
+            out.append(([(s, e) for s, e, _ in tri[:r.n_a]], [(s, e) for s, e, _ in tri[r.n_a:]]))
+        elif kind == "conflict":
+            out.append(([(s, e, DIFF_FLAGS[f]) for s, e, f in tri[:r.n_a]], list(r.common[:r.n_common])))
+        else:
+            out.append(bool(r.n_a))
+    return (out, ms.value) if timing else out
 
 
 def batch_checkout(docs, **kw):

@@ -245,6 +245,34 @@ typedef enum dtgpu_export {
 size_t dtgpu_decode_export(const dtgpu_decoded *dec, size_t i, int what, void *out, size_t cap);
 size_t dtgpu_oplog_export(const dtgpu_oplog *oplog, int what, void *out, size_t cap);
 
+
+/* ---- batched causal-graph queries ------------------------------
+ * One wavefront per query (dt_graph.hip).  Graphs are GraphEntrySimple lists flattened as
+ * (start, end, n_parents, parents...) int64 runs; graph g spans hist[hist_off[g], hist_off[g+1]).
+ *   DTGPU_GQ_DIFF      Graph::diff (tools.rs:158-292): spans only in a, then only in b, newest
+ *                      first (flag 0 = a, 1 = b)
+ *   DTGPU_GQ_CONFLICT  Graph::find_conflicting (tools.rs:296-484): visited spans newest first with
+ *                      flag 0 OnlyA / 1 OnlyB / 2 Shared, and the common frontier
+ *   DTGPU_GQ_CONTAINS  Graph::frontier_contains_version (tools.rs:88-146): n_a = 1 if a contains
+ *                      target (-1 = ROOT)
+ * spans: span_cap (start, end, flag) triples per query.  answer.status: 0 ok, 1 capacity
+ * (queue or span_cap), 2 bad input (a version outside the graph). */
+#define DTGPU_GQ_DIFF 0
+#define DTGPU_GQ_CONFLICT 1
+#define DTGPU_GQ_CONTAINS 2
+typedef struct dtgpu_graph_query {
+    uint32_t kind, graph, na, nb;   /* frontier sizes <= 16 */
+    int64_t a[16], b[16];
+    int64_t target;
+} dtgpu_graph_query;
+typedef struct dtgpu_graph_answer {
+    uint32_t status, n_a, n_b, n_common;
+    int64_t common[16];
+} dtgpu_graph_answer;
+dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *hist_off, size_t n_graphs,
+                                 const dtgpu_graph_query *queries, size_t n_queries, int64_t *spans,
+                                 size_t span_cap, dtgpu_graph_answer *answers, float *ms);
+
 #ifdef __cplusplus
 }
 #endif

@@ -192,8 +192,9 @@ class Graph:
     def diff(self, a, b):
         A, na = _arr(a)
         B, nb = _arr(b)
-        oa = (ctypes.c_int64 * 512)()
-        ob = (ctypes.c_int64 * 512)()
+        cap = 4 * lib().dto_graph_num_entries(self.h) + 64   # ranges <= 2 per entry
+        oa = (ctypes.c_int64 * cap)()
+        ob = (ctypes.c_int64 * cap)()
         ca, cb = ctypes.c_int(), ctypes.c_int()
         lib().dto_graph_diff(self.h, A, na, B, nb, oa, ctypes.byref(ca), ob, ctypes.byref(cb))
         return ([(oa[2 * i], oa[2 * i + 1]) for i in range(ca.value)],
@@ -206,7 +207,7 @@ class Graph:
     def find_conflicting(self, a, b):
         A, na = _arr(a)
         B, nb = _arr(b)
-        spans = (ctypes.c_int64 * 768)()
+        spans = (ctypes.c_int64 * (6 * lib().dto_graph_num_entries(self.h) + 96))()
         common = (ctypes.c_int64 * 64)()
         nc = ctypes.c_int()
         n = lib().dto_graph_find_conflicting(self.h, A, na, B, nb, spans, common, ctypes.byref(nc))

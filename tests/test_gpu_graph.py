@@ -1,0 +1,87 @@
+"""GPU causal-graph queries (dt_graph.hip) vs the reference's fixtures and the C oracle.
+
+diff / find_conflicting / version_contains over every test_data/causal_graph fixture in one
+batch (tools.rs:779-901 semantics), then random queries over the benchmark files' graphs
+against the oracle's restatement (oracle/dt_oracle.c, pinned by the same fixtures).
+"""
+import random
+
+import pytest
+
+import golden_data as G
+from oracle.oracle import Graph as OracleGraph
+
+pytestmark = pytest.mark.gpu
+
+import dt_amd  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if dt_amd.device_count() < 1:
+        pytest.fail("no HIP device visible: the engine has no CPU fallback")
+
+
+def _ranges(rs):
+    return [tuple(r) for r in rs]
+
+
+def test_fixtures_one_batch():
+    graphs, queries, checks = [], [], []
+    for case in G.cg_fixture("diff"):
+        graphs.append(case["hist"])
+        queries.append(("diff", len(graphs) - 1, case["a"], case["b"]))
+        checks.append(case)
+    for case in G.cg_fixture("conflicting"):
+        graphs.append(case["hist"])
+        queries.append(("conflict", len(graphs) - 1, case["a"], case["b"]))
+        checks.append(case)
+    for case in G.cg_fixture("version_contains"):
+        graphs.append(case["hist"])
+        queries.append(("contains", len(graphs) - 1, case["frontier"], case["target"]))
+        checks.append(case)
+    got = dt_amd.graph_queries(graphs, queries)
+    for (kind, _g, _a, _b), case, ans in zip(queries, checks, got):
+        if kind == "diff":
+            assert ans == (_ranges(case["expect_a"]), _ranges(case["expect_b"])), case
+        elif kind == "conflict":
+            want = [(s["start"], s["end"], f) for s, f in reversed(case["expect_spans"])]
+            assert ans == (want, case["expect_common"]), case
+        else:
+            assert ans == case["expected"], case
+
+
+def _hist_of(name):
+    o = dt_amd.ListOpLog.load_from(G.dt_bytes(name))
+    ent, po, par = o.export("entries"), o.export("parent_offsets"), o.export("parents")
+    return [{"span": [int(s), int(e)], "parents": [int(p) for p in par[po[k]:po[k + 1]]]}
+            for k, (s, e) in enumerate(ent)], len(o)
+
+
+@pytest.mark.parametrize("name", G.DT_FILES)
+def test_random_queries_vs_oracle(name):
+    hist, n = _hist_of(name)
+    og = OracleGraph(hist)
+    rng = random.Random(1234)
+    queries = []
+    for _ in range(300):
+        a = sorted(rng.sample(range(n), rng.choice([1, 1, 2])))
+        b = sorted(rng.sample(range(n), rng.choice([1, 1, 2])))
+        queries.append(("diff", 0, a, b))
+        queries.append(("conflict", 0, a, b))
+        queries.append(("contains", 0, a, rng.randrange(-1, n)))
+    got = dt_amd.graph_queries([hist], queries, span_cap=4096)
+    checked = 0
+    for (kind, _g, a, b), ans in zip(queries, got):
+        if isinstance(ans, tuple) and ans and ans[0] == "error":
+            assert ans[1] == 1, (kind, a, b, ans)   # only queue / span capacity may stop a query
+            continue
+        if kind == "diff":
+            oa, ob = og.diff(a, b)
+            assert ans == (list(reversed(oa)), list(reversed(ob))), (a, b)
+        elif kind == "conflict":
+            assert ans == og.find_conflicting(a, b), (a, b)
+        else:
+            assert ans == og.contains(a, b), (a, b)
+        checked += 1
+    assert checked >= 0.95 * len(queries)
