@@ -6,8 +6,10 @@ friendsforever.dt workload (BASELINE.json configs[1]) replicated to --docs copie
 (weak scaling: every rank owns its own copies).  The timed pass runs the walk planner
 (dt_plan.hip: spanning-tree walk + retreat/advance sets) and the replay + materialisation
 (dt_replay.hip) -- everything the reference's `checkout_tip()` does on a decoded oplog
-(crates/bench `complex/merge`).  The `.dt` decode happens once when the batch is staged
-(the reference benches it separately as `complex/decode`; reported here as `host_stage_s`).
+(crates/bench `complex/merge`).  The batch is staged on the device: the `.dt` bytes go to HBM and
+are decoded (dt_decode.hip) and turned into planner inputs (dt_prep.hip) by kernels; the reference
+benches decode separately (`complex/decode`), so staging is outside the timed pass (`stage_s`) and
+the whole chain -- decode + prep + plan + replay from the encoded bytes -- is reported as `e2e`.
 
 Contract: `python bench.py --gpus N --steps K --warmup W` prints ONE JSON line on rank 0.
 For N > 1 it is launched by torch.distributed.run, one process per GPU; per-rank times are
@@ -39,7 +41,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     p.add_argument("--cpu-cores", type=int, default=16)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--no-decode", action="store_true", help="skip the GPU .dt decode measurement")
+    p.add_argument("--no-decode", action="store_true", help="skip the end-to-end (.dt bytes -> text) measurement")
+    p.add_argument("--host-staging", action="store_true", help="decode and prepare planner inputs on host threads")
     return p.parse_args()
 
 
@@ -75,24 +78,29 @@ def cpu_baseline(data, budget_s, cores):
                       f"{wall:.2f} s"}
 
 
-def decode_leg(docs, device, steps):
-    """Device `.dt` decode (dt_decode.hip) of the same documents: kernel time from HIP events,
-    throughput over the encoded bytes (the E2E roofline basis of SURVEY.md 8d), parity-checked
-    against the host decoder on document 0."""
+def e2e_leg(batch, docs, steps, text_len, total_lv):
+    """`.dt` bytes in HBM -> text: device decode (dt_decode.hip) + planner inputs (dt_prep.hip) +
+    walk plan + replay, re-run `steps` times on the device-staged batch (HIP events per kernel).
+    Roofline basis = SURVEY.md 8d E2E: encoded bytes + text bytes per document.  The decoder's
+    arrays are parity-checked against the host decoder on document 0."""
     import dt_amd
-    dec = dt_amd.DecodeBatch(docs, device=device)
+    split = [batch.run_e2e_timed() for _ in range(max(1, steps))]
+    res = batch.results()
+    assert all(r["status"] == 0 and r["text_len"] == text_len for r in res), "end-to-end results differ"
+    dec = dt_amd.DecodeBatch(docs[:1])
     dec.run()
-    ms = min(dec.run() for _ in range(max(1, min(steps, 5))))
-    bad = sum(1 for i in range(len(docs)) if dec.status(i)["status"] != 0)
-    assert bad == 0, f"{bad} documents failed the device decode"
     host = dt_amd.ListOpLog.load_from(docs[0])
-    for w in ("ops", "agent_runs", "parents", "char_offsets"):
+    for w in ("ops", "agent_runs", "entries", "parents", "char_offsets", "content"):
         assert (dec.export(0, w) == host.export(w)).all(), w
-    bi, bo = dec.bytes_in(), dec.bytes_out()
-    gbs = bi / (ms / 1000.0) / 1e9
-    return {"kernel": "decode_kernel", "ms": ms, "docs": len(docs), "encoded_GBps": gbs,
-            "soa_written_GBps": bo / (ms / 1000.0) / 1e9, "frac_hbm": (bi + bo) / (ms / 1000.0) / 1e9 / HBM_PEAK_GBS,
-            "bytes_in": bi, "bytes_out": bo}
+    mean = [statistics.mean(x[k] for x in split) for k in range(4)]
+    total = sum(mean)
+    enc = sum(len(d) for d in docs)
+    basis = enc + text_len * len(docs)
+    return {"decode_ms": mean[0], "prep_ms": mean[1], "plan_ms": mean[2], "replay_ms": mean[3], "total_ms": total,
+            "merged_ops_per_s": total_lv / (total / 1000.0), "docs_per_s": len(docs) / (total / 1000.0),
+            "encoded_bytes": enc, "roofline_bytes": basis,
+            "achieved_GBps": basis / (total / 1000.0) / 1e9, "frac_hbm": basis / (total / 1000.0) / 1e9 / HBM_PEAK_GBS,
+            "basis": "SURVEY.md 8d E2E: |.dt bytes| + |text out| per document; kernel time of decode + prep + plan + replay"}
 
 
 def main():
@@ -116,7 +124,8 @@ def main():
     dev = f"cuda:{local_rank}" if dist is not None else None
 
     t0 = time.perf_counter()
-    batch = dt_amd.Batch(docs=[bytes(data) for _ in mine], device=local_rank if world > 1 else 0)
+    staging = "host" if args.host_staging else "device"
+    batch = dt_amd.Batch(docs=[bytes(data) for _ in mine], device=local_rank if world > 1 else 0, staging=staging)
     host_stage_s = time.perf_counter() - t0
 
     for _ in range(args.warmup):
@@ -189,7 +198,8 @@ def main():
                             "(decoded oplogs resident in HBM)",
                    "parallelism": f"dp{world} (documents sharded, no data-path collective)"},
         "docs_per_sec": n_total * args.steps / elapsed,
-        "host_stage_s": host_stage_s,
+        "stage_s": host_stage_s,
+        "staging": staging,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "plan_kernel + replay_kernel (one checkout pass)",
@@ -198,8 +208,8 @@ def main():
                      "algorithmic_formula": "per doc: 16*op_runs + (8+4*parents)*graph_entries + 12*agent_runs "
                                             "+ inserted_bytes + text_out_bytes (SURVEY.md 8d merge-only)"},
     }
-    if not args.no_decode:   # batched .dt decode on the GPU, same documents
-        out["decode"] = decode_leg([bytes(data) for _ in mine], local_rank if world > 1 else 0, args.steps)
+    if not args.no_decode and staging == "device":   # .dt bytes -> text, all on the GPU
+        out["e2e"] = e2e_leg(batch, [bytes(data) for _ in mine], min(args.steps, 5), len(want), lv_per_doc * len(mine))
     if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(data, args.cpu_seconds, args.cpu_cores)
     if rank == 0:

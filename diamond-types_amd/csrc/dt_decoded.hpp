@@ -1,0 +1,36 @@
+// dt_decoded.hpp -- the decoder handle (dtgpu_decoded): device arenas of a decoded batch,
+// shared by the decode API (dtgpu_decode.cpp) and the device-staged checkout batches
+// (dtgpu_api.cpp), which read the decoded oplogs in place.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "dt_decode.hpp"
+#include "dt_devbuf.hpp"
+
+using dtgpu::DecodeDesc;
+using dtgpu::DecodeParams;
+using dtgpu::DecodeResult;
+using dtgpu::DevBuf;
+
+struct dtgpu_decoded {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    size_t n = 0;
+    uint64_t in_bytes = 0;
+    float last_ms = 0;
+    std::vector<DecodeDesc> desc;
+    std::vector<DecodeResult> res;
+    DevBuf<uint8_t> in, lz, content;
+    DevBuf<uint32_t> aruns, alist, pre, ops, ent, poff, par, cbyte, agents, ver;
+    DevBuf<DecodeDesc> d_desc;
+    DevBuf<DecodeResult> d_res;
+    DecodeParams P{};
+    ~dtgpu_decoded() {
+        if (ev0) (void)hipEventDestroy(ev0);
+        if (ev1) (void)hipEventDestroy(ev1);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};

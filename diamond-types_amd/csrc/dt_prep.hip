@@ -1,0 +1,328 @@
+// dt_prep.hip -- planner inputs from the device-decoded oplog (the device half of
+// dt_host.cpp build_plan_input), one 64-lane wavefront per document.
+//
+//   parents -> entry index (Graph::find_packed, graph/mod.rs), children CSR in child-index order
+//   op runs -> apply commands and each entry's first op run (ops never cross entries)
+//   agent runs -> (lv, name rank, seq, agent) quads; ranks order agent names byte-wise, the
+//                 YjsMod tie-break of listmerge/merge.rs:199-218
+//   causal-chain decomposition (see dt_host.cpp build_plan_input): an entry joins a chain whose
+//                 every op is in its history (its parent vector over chains equals the chain's
+//                 length), preferring its first parent's chain, else opens a chain.  Sequential
+//                 over entries; the parent vector is one VGPR (lane = chain), vectors of earlier
+//                 entries come back from HBM (or from registers for the previous entry, the usual
+//                 parent), so a linear stretch of history costs no memory round trip.
+//   entry records, per-chain dense seq -> (LV | is_del) tables, tips with their entries.
+// Everything but the decomposition is lane-parallel.  Documents with more than 64 chains are
+// reported PREP_WIDE and prepared on the host.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dt_prep.hpp"
+
+namespace dtgpu {
+namespace prep {
+
+__device__ __forceinline__ uint32_t lane() { return __lane_id(); }
+__device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t l) {
+    return uint32_t(__builtin_amdgcn_readlane(int(v), int(l)));
+}
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ uint64_t lt_mask() { return (1ull << lane()) - 1ull; }
+__device__ __forceinline__ uint32_t popc(uint64_t m) { return uint32_t(__popcll(m)); }
+__device__ __forceinline__ uint32_t ctz(uint64_t m) { return uint32_t(__ffsll((unsigned long long)m) - 1); }
+__device__ __forceinline__ void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+__device__ __forceinline__ uint32_t scan_incl(uint32_t v) {   // inclusive prefix sum over the wave
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = uint32_t(__shfl_up(int(v), d));
+        if (lane() >= uint32_t(d)) v += o;
+    }
+    return v;
+}
+
+// 64 consecutive words / pairs cached in one VGPR, addressed by a uniform index
+struct Chunk {
+    uint32_t blk, v;
+    __device__ __forceinline__ void init() { blk = 0xFFFFFFFFu; v = 0; }
+    template <typename F>
+    __device__ __forceinline__ uint32_t get(uint32_t i, uint32_t n, F load) {
+        if ((i & ~63u) != blk) {
+            blk = i & ~63u;
+            const uint32_t k = blk + lane();
+            v = k < n ? load(k) : 0xFFFFFFFFu;
+        }
+        return rdl(v, i & 63u);
+    }
+};
+
+// entry of `lv` among entries [0, hi) (sorted, contiguous): the previous entry first
+__device__ __forceinline__ uint32_t entry_of(const uint2 *ent, uint32_t hi, uint32_t lv) {
+    if (hi && lv >= ent[hi - 1].x && lv < ent[hi - 1].y) return hi - 1;
+    uint32_t lo = 0, h = hi;
+    while (lo < h) {
+        const uint32_t mid = (lo + h) >> 1;
+        if (lv >= ent[mid].y) lo = mid + 1; else h = mid;
+    }
+    return lo < hi && lv >= ent[lo].x ? lo : 0xFFFFFFFFu;
+}
+
+__global__ __launch_bounds__(64) void prep_kernel(PrepParams P) {
+    extern __shared__ uint32_t lfill[];   // per entry: child count, then next child slot
+    const uint32_t doc = blockIdx.x;
+    if (doc >= P.n_docs) return;
+    const PrepDesc D = P.docs[doc];
+    PrepResult R{};
+    if (D.skip) {
+        if (lane() == 0) { R.status = PREP_SKIP; P.results[doc] = R; }
+        return;
+    }
+    const uint32_t l = lane();
+    const uint32_t ne = D.ne, npar = D.n_par, nops = D.n_ops;
+    const uint2 *ent = reinterpret_cast<const uint2 *>(P.d_ent) + D.d_ent;
+    const uint32_t *poff = P.d_poff + D.d_poff;
+    const uint32_t *par_in = P.d_par + D.d_par;
+    const uint4 *ops = reinterpret_cast<const uint4 *>(P.d_ops) + D.d_op;
+    const uint4 *ar = reinterpret_cast<const uint4 *>(P.d_aruns) + D.d_arun;
+    uint32_t *par = P.par + D.o_par, *pent = P.pent + D.o_par, *pch = P.pch + D.o_par, *pcnt = P.pcnt + D.o_par;
+    uint32_t *child = P.child + D.o_child;
+    uint32_t *erec = P.erec + D.o_erec;
+    uint32_t *doff = P.doff + D.o_doff;
+    uint32_t *dense = P.dense + D.o_dense;
+    uint32_t *rows = P.rows + D.o_rows;
+    uint32_t *owner = P.scr + D.o_scr;
+    uint32_t *chain = owner + npar, *seq0 = chain + ne, *coff = seq0 + ne, *eop = coff + ne + 1;
+    Cmd *opc = P.opc + D.o_op;
+    if (ne > P.max_entries || D.n_lv >= (1u << 30)) {
+        if (l == 0) { R.status = PREP_BAD; P.results[doc] = R; }
+        return;
+    }
+
+    // ---- 1. parents: entry of each parent, child counts ------------------------------------------
+    for (uint32_t i = l; i < ne; i += 64) lfill[i] = 0;
+    __syncthreads();
+    bool bad = false;
+    for (uint32_t i0 = 0; i0 < ne; i0 += 64) {
+        const uint32_t i = i0 + l;
+        if (i < ne) {
+            const uint32_t k1 = poff[i + 1];
+            for (uint32_t k = poff[i]; k < k1; k++) {
+                const uint32_t p = par_in[k];
+                const uint32_t pe = entry_of(ent, i, p);
+                if (pe == 0xFFFFFFFFu) { bad = true; break; }
+                owner[k] = i;
+                par[k] = p;
+                pent[k] = pe;
+                atomicAdd(&lfill[pe], 1u);
+            }
+        }
+    }
+    if (ballot(bad)) {
+        if (l == 0) { R.status = PREP_BAD; P.results[doc] = R; }
+        return;
+    }
+    __syncthreads();
+    // children CSR offsets (exclusive scan); lfill becomes each entry's next free child slot
+    {
+        uint32_t carry = 0;
+        for (uint32_t i0 = 0; i0 < ne; i0 += 64) {
+            const uint32_t i = i0 + l;
+            const uint32_t c = i < ne ? lfill[i] : 0;
+            const uint32_t inc = scan_incl(c);
+            if (i < ne) { coff[i] = carry + inc - c; lfill[i] = carry + inc - c; }
+            carry += rdl(inc, 63);
+        }
+        if (l == 0) coff[ne] = carry;
+    }
+    __syncthreads();
+    wave_fence();
+    // children in child-index order (slots are in (child, parent) order): a stable scatter,
+    // one parent entry per round
+    for (uint32_t k0 = 0; k0 < npar; k0 += 64) {
+        const uint32_t k = k0 + l;
+        const uint32_t key = k < npar ? pent[k] : 0xFFFFFFFFu;
+        const uint32_t own = k < npar ? owner[k] : 0;
+        bool todo = k < npar;
+        for (uint64_t m = ballot(todo); m; m = ballot(todo)) {
+            const uint32_t lead = rdl(key, ctz(m));
+            const uint64_t mm = ballot(todo && key == lead);
+            const uint32_t base = lfill[lead];
+            if (todo && key == lead) {
+                child[base + popc(mm & lt_mask())] = own;
+                todo = false;
+            }
+            __syncthreads();
+            if (l == 0) lfill[lead] = base + popc(mm);
+            __syncthreads();
+        }
+    }
+
+    // ---- 2. each entry's first op run (ops are split at entry boundaries) ------------------------
+    {
+        Chunk ce, co, ob;
+        ce.init(); co.init(); ob.init();
+        uint32_t j = 0, buf = 0;
+        for (uint32_t i = 0; i < ne; i++) {
+            const uint32_t s = ce.get(i, ne, [&](uint32_t k) { return ent[k].x; });
+            while (j < nops && co.get(j, nops, [&](uint32_t k) { return ops[k].x; }) < s) j++;
+            buf = (i & 63u) == l ? j : buf;
+            if ((i & 63u) == 63u || i + 1 == ne) {
+                const uint32_t at = i & ~63u;
+                if (at + l <= i) eop[at + l] = buf;
+            }
+        }
+        if (l == 0) eop[ne] = nops;
+    }
+    wave_fence();
+
+    // ---- 3. causal-chain decomposition (sequential over entries) ---------------------------------
+    uint32_t clen = 0, nch = 0;      // lane c: ops in chain c so far
+    uint32_t prev_row = 0;           // parent vector of entry i - 1
+    uint32_t prev_chain = 0, prev_seq0 = 0, prev_start = 0;
+    {
+        Chunk cp, cx, cy, cpar, cpe;
+        cp.init(); cx.init(); cy.init(); cpar.init(); cpe.init();
+        uint32_t bch = 0, bsq = 0;   // chain / seq0 of the current 64 entries, flushed per 64
+        for (uint32_t i = 0; i < ne; i++) {
+            const uint32_t k0 = cp.get(i, ne + 1, [&](uint32_t k) { return poff[k]; });
+            const uint32_t k1 = cp.get(i + 1, ne + 1, [&](uint32_t k) { return poff[k]; });
+            uint32_t row = 0;
+            uint32_t first_chain = 0xFFFFFFFFu;
+            for (uint32_t k = k0; k < k1; k++) {
+                const uint32_t p = cpar.get(k, npar, [&](uint32_t x) { return par_in[x]; });
+                const uint32_t pe = cpe.get(k, npar, [&](uint32_t x) { return pent[x]; });
+                uint32_t prow, pc, ps0, pst;
+                if (pe + 1 == i) {
+                    prow = prev_row; pc = prev_chain; ps0 = prev_seq0; pst = prev_start;
+                } else {
+                    prow = rows[size_t(pe) * PREP_MAX_CHAINS + l];
+                    if (pe >= (i & ~63u)) {   // not flushed yet: from the registers
+                        pc = rdl(bch, pe & 63u); ps0 = rdl(bsq, pe & 63u);
+                    } else {
+                        pc = chain[pe]; ps0 = seq0[pe];
+                    }
+                    pst = ent[pe].x;
+                }
+                row = max(row, prow);
+                if (l == pc) row = max(row, ps0 + (p - pst) + 1);
+                if (k == k0) first_chain = pc;
+            }
+            rows[size_t(i) * PREP_MAX_CHAINS + l] = row;
+            uint32_t c = 0xFFFFFFFFu;
+            if (first_chain != 0xFFFFFFFFu && rdl(row, first_chain) == rdl(clen, first_chain)) c = first_chain;
+            if (c == 0xFFFFFFFFu) {
+                const uint64_t m = ballot(l < nch && row == clen);
+                if (m) c = ctz(m);
+            }
+            if (c == 0xFFFFFFFFu) {
+                if (nch == PREP_MAX_CHAINS) {
+                    if (l == 0) { R.status = PREP_WIDE; R.n_chains = nch + 1; P.results[doc] = R; }
+                    return;
+                }
+                c = nch++;
+            }
+            const uint32_t s = cx.get(i, ne, [&](uint32_t k) { return ent[k].x; });
+            const uint32_t e = cy.get(i, ne, [&](uint32_t k) { return ent[k].y; });
+            const uint32_t s0 = rdl(clen, c);
+            if (l == c) clen += e - s;
+            bch = (i & 63u) == l ? c : bch;
+            bsq = (i & 63u) == l ? s0 : bsq;
+            if ((i & 63u) == 63u || i + 1 == ne) {
+                const uint32_t at = i & ~63u;
+                if (at + l <= i) { chain[at + l] = bch; seq0[at + l] = bsq; }
+            }
+            prev_row = row; prev_chain = c; prev_seq0 = s0; prev_start = s;
+        }
+    }
+    wave_fence();
+    // per chain: offset of its dense table
+    {
+        const uint32_t c = l < nch ? clen : 0;
+        const uint32_t inc = scan_incl(c);
+        if (l < nch) doff[l] = inc - c;
+        if (l == 0) doff[nch] = rdl(inc, 63);
+    }
+
+    // ---- 4. lane-parallel outputs -----------------------------------------------------------------
+    for (uint32_t k = l; k < npar; k += 64) {   // parent slots: chain and ops of that chain up to it
+        const uint32_t pe = pent[k];
+        pch[k] = chain[pe];
+        pcnt[k] = seq0[pe] + (par[k] - ent[pe].x) + 1;
+    }
+    wave_fence();
+    for (uint32_t i = l; i < ne; i += 64) {    // entry records (dt_host.hpp PlanInput::erec)
+        uint32_t *r = erec + size_t(i) * EREC_WORDS;
+        const uint2 e = ent[i];
+        const uint32_t p0 = poff[i], np = poff[i + 1] - p0;
+        const uint32_t c0 = coff[i], nc = coff[i + 1] - c0;
+        r[0] = e.x; r[1] = e.y; r[2] = p0; r[3] = np;
+        r[4] = eop[i]; r[5] = eop[i + 1] - eop[i];
+        r[6] = chain[i]; r[7] = seq0[i];
+        r[8] = c0; r[9] = nc;
+        r[10] = np ? par[p0] : 0xFFFFFFFFu;
+        for (uint32_t j = 0; j < 2; j++) {
+            const bool has = np > j;
+            r[11 + 3 * j] = has ? pent[p0 + j] : 0xFFFFFFFFu;
+            r[12 + 3 * j] = has ? pch[p0 + j] : 0u;
+            r[13 + 3 * j] = has ? pcnt[p0 + j] : 0u;
+        }
+        r[17] = nc ? child[c0 + nc - 1] : 0xFFFFFFFFu;
+        r[18] = 0; r[19] = 0;
+    }
+    // op runs: apply commands and the dense chain tables (LV | is_del per chain seq)
+    uint32_t n_ins = 0;
+    for (uint32_t i = l; i < ne; i += 64) {
+        const uint32_t e0 = ent[i].x, j1 = eop[i + 1];
+        const uint32_t d0 = doff[chain[i]] + seq0[i];
+        for (uint32_t j = eop[i]; j < j1; j++) {
+            const uint4 o = ops[j];   // lv, len, pos, kind | fwd << 1
+            const bool del = o.w & 1u;
+            opc[j] = Cmd{del ? (CMD_DEL | ((o.w & 2u) ? 16u : 0u)) : uint32_t(CMD_INS), o.x, o.y, o.z};
+            if (!del) n_ins += o.y;
+            for (uint32_t v = 0; v < o.y; v++) dense[d0 + (o.x - e0) + v] = (o.x + v) | (del ? TL_DEL : 0u);
+        }
+    }
+    for (uint32_t t = l; t < D.n_ver; t += 64) {   // tips and their entries
+        const uint32_t v = P.d_ver[D.d_ver + t];
+        P.tip[2 * (D.o_tip + t)] = v;
+        P.tip[2 * (D.o_tip + t) + 1] = entry_of(ent, ne, v);
+    }
+    // agent runs with name ranks (byte-wise name order; names are distinct)
+    {
+        const uint2 *names = reinterpret_cast<const uint2 *>(P.d_agents) + D.d_agent;
+        const uint8_t *in = P.in + D.d_in;
+        for (uint32_t k = l; k < D.n_aruns; k += 64) {
+            const uint4 a = ar[k];   // lv, len, agent, seq
+            const uint2 me = names[a.z];
+            uint32_t rank = 0;
+            for (uint32_t b = 0; b < D.n_agents; b++) {
+                const uint2 o = names[b];
+                const uint32_t n = min(o.y, me.y);
+                int cmp = 0;
+                for (uint32_t x = 0; x < n && !cmp; x++) {
+                    const uint32_t cb = in[o.x + x], cm = in[me.x + x];
+                    cmp = cb < cm ? -1 : cb > cm ? 1 : 0;
+                }
+                if (!cmp) cmp = o.y < me.y ? -1 : o.y > me.y ? 1 : 0;
+                rank += cmp < 0 ? 1u : 0u;
+            }
+            uint32_t *q = P.aruns + 4 * (D.o_arun + k);
+            q[0] = a.x; q[1] = rank; q[2] = a.w; q[3] = a.z;
+        }
+    }
+    for (int d = 32; d >= 1; d >>= 1) n_ins += uint32_t(__shfl_xor(int(n_ins), d));
+    R.status = PREP_OK;
+    R.n_chains = nch;
+    R.n_ins = n_ins;
+    if (l == 0) P.results[doc] = R;
+}
+
+}  // namespace prep
+
+int launch_prep(const PrepParams &p, void *stream) {
+    if (!p.n_docs) return 0;
+    hipLaunchKernelGGL(prep::prep_kernel, dim3(p.n_docs), dim3(64), size_t(p.max_entries) * 4,
+                       reinterpret_cast<hipStream_t>(stream), p);
+    return hipGetLastError() == hipSuccess ? 0 : 66;
+}
+
+}  // namespace dtgpu

@@ -1,0 +1,48 @@
+// dt_prep.hpp -- host/device layout of the planner-input builder (dt_prep.hip): the decoded
+// oplog arenas of dt_decode.hip in, the PlanInput arrays of dt_host.hpp (build_plan_input) out.
+#pragma once
+#include <stdint.h>
+
+#include "dt_host.hpp"
+
+namespace dtgpu {
+
+constexpr uint32_t PREP_MAX_CHAINS = 64;   // wider histories are prepared on the host
+enum : uint32_t { PREP_OK = 0, PREP_WIDE = 1, PREP_BAD = 2, PREP_SKIP = 3 };
+
+struct PrepDesc {
+    // decoder arenas (offsets in the decoder's units: quads / pairs / words / bytes)
+    uint64_t d_op, d_arun, d_ent, d_poff, d_par, d_ver, d_agent, d_in;
+    uint32_t n_ops, n_aruns, ne, n_par, n_ver, n_agents, n_lv, skip;
+    // planner arenas (offsets in PlanDesc units)
+    uint64_t o_par;     // par / pent / pch / pcnt slots
+    uint64_t o_child;   // child slots
+    uint64_t o_op;      // Cmd units
+    uint64_t o_arun;    // quads
+    uint64_t o_tip;     // pairs
+    uint64_t o_erec;    // words (EREC_WORDS per entry)
+    uint64_t o_doff;    // words (PREP_MAX_CHAINS + 1)
+    uint64_t o_dense;   // words (n_lv)
+    uint64_t o_rows;    // words (PREP_MAX_CHAINS per entry): parent vectors of the decomposition
+    uint64_t o_scr;     // words: owner (n_par), chain, seq0 (ne each), coff, eop (ne + 1 each)
+};
+
+struct PrepResult {
+    uint32_t status, n_chains, n_ins, pad;
+};
+
+struct PrepParams {
+    const uint8_t *in;
+    const uint32_t *d_ops, *d_aruns, *d_ent, *d_poff, *d_par, *d_ver, *d_agents;
+    uint32_t *par, *pent, *pch, *pcnt, *child, *aruns, *tip, *erec, *doff, *dense, *rows, *scr;
+    Cmd *opc;
+    const PrepDesc *docs;
+    PrepResult *results;
+    uint32_t n_docs, max_entries;
+};
+
+inline uint64_t prep_scratch_words(uint32_t n_par, uint32_t ne) { return uint64_t(n_par) + 4ull * ne + 2; }
+
+int launch_prep(const PrepParams &p, void *stream);
+
+}  // namespace dtgpu

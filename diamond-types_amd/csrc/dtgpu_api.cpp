@@ -13,9 +13,11 @@
 #include <vector>
 
 #include "../../include/dtgpu.h"
+#include "dt_decoded.hpp"
 #include "dt_devbuf.hpp"
 #include "dt_device.hpp"
 #include "dt_host.hpp"
+#include "dt_prep.hpp"
 
 using namespace dtgpu;
 
@@ -63,7 +65,20 @@ struct dtgpu_batch {
     DevBuf<DocResult> d_results;
     BatchParams small{}, large{};
 
+    // device-staged batches (dtgpu_batch_create_device): the decoded oplogs stay in the
+    // decoder's arenas (content and per-LV offsets are read there by the replay) and the
+    // planner inputs are built by the prep kernel
+    std::unique_ptr<dtgpu_decoded> dec;
+    DevBuf<uint32_t> pr_rows, pr_scr;
+    DevBuf<PrepDesc> pr_docs;
+    DevBuf<PrepResult> pr_res;
+    PrepParams prep{};
+    hipEvent_t ev_dec = nullptr, ev_prep = nullptr;
+    float last_decode_ms = 0, last_prep_ms = 0;
+
     ~dtgpu_batch() {
+        if (ev_dec) (void)hipEventDestroy(ev_dec);
+        if (ev_prep) (void)hipEventDestroy(ev_prep);
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev_mid) (void)hipEventDestroy(ev_mid);
         if (ev1) (void)hipEventDestroy(ev1);
@@ -377,6 +392,233 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     return DTGPU_OK;
 }
 
+// Device-staged batch: `.dt` bytes -> device decode -> device prep -> planner sizing pass ->
+// replay layout.  The host only reads back per-document counts to size the arenas.  Documents
+// the device path hands back (decoder or prep limits) get status DTGPU_DECODE_DEFER.
+dtgpu_status stage_device(const uint8_t *const *docs, const size_t *lens, size_t n, const dtgpu_batch_opts *opts,
+                          dtgpu_batch **out) {
+    auto B = std::make_unique<dtgpu_batch>();
+    B->device = opts ? opts->device : 0;
+    {
+        dtgpu_decoded *dh = nullptr;
+        dtgpu_status st = dtgpu_decode_create(docs, lens, n, opts, &dh);
+        if (st != DTGPU_OK) return st;
+        B->dec.reset(dh);
+    }
+    dtgpu_decoded &Dd = *B->dec;
+    if (hipSetDevice(B->device) != hipSuccess) return DTGPU_ERR_HIP;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, B->device) == hipSuccess && prop.multiProcessorCount > 0)
+        B->n_cu = prop.multiProcessorCount;
+    B->stream = Dd.stream;   // one stream for decode, prep, plan and replay
+    Dd.stream = nullptr;     // owned by the batch from here on
+#define CK(x) do { if ((x) != hipSuccess) return DTGPU_ERR_HIP; } while (0)
+    CK(hipEventCreate(&B->ev0)); CK(hipEventCreate(&B->ev_mid)); CK(hipEventCreate(&B->ev1));
+    CK(hipEventCreate(&B->ev_dec)); CK(hipEventCreate(&B->ev_prep));
+    hipStream_t s = B->stream;
+    if (launch_decode(Dd.P, s)) return DTGPU_ERR_HIP;
+    CK(hipMemcpyAsync(Dd.res.data(), Dd.d_res.p, n * sizeof(DecodeResult), hipMemcpyDeviceToHost, s));
+    CK(hipStreamSynchronize(s));
+    B->n = n;
+    B->host_status.assign(n, OK);
+    B->n_lv.assign(n, 0);
+    B->docs.assign(n, DocDesc{});
+    B->host_planned.assign(n, 0);
+
+    // ---- prep layout ----------------------------------------------------------------------------
+    std::vector<PrepDesc> pd(n);
+    uint64_t o_par = 0, o_op = 0, o_arun = 0, o_tip = 0, o_erec = 0, o_doff = 0, o_dense = 0, o_rows = 0, o_scr = 0;
+    uint32_t max_e = 1;
+    for (size_t i = 0; i < n; i++) {
+        const DecodeResult &r = Dd.res[i];
+        const DecodeDesc &d = Dd.desc[i];
+        PrepDesc &q = pd[i];
+        std::memset(&q, 0, sizeof q);
+        q.skip = 1;
+        uint32_t st = r.status;
+        if (st == OK && !r.content_complete) st = ErrCheckout;   // content.unwrap() in apply_to
+        if (st == OK && (r.n_lv >= MAX_PLAN_LV || r.n_entries > PLAN_MAX_LDS_ENTRIES)) st = DECODE_DEFER;
+        B->host_status[i] = st;
+        B->n_lv[i] = r.n_lv;
+        if (st != OK) continue;
+        q.skip = 0;
+        q.d_op = d.op_off; q.d_arun = d.arun_off; q.d_ent = d.ent_off; q.d_poff = d.poff_off; q.d_par = d.par_off;
+        q.d_ver = d.ver_off; q.d_agent = d.agent_off; q.d_in = d.in_off;
+        q.n_ops = r.n_ops; q.n_aruns = r.n_aruns; q.ne = r.n_entries; q.n_par = r.n_parents; q.n_ver = r.n_version;
+        q.n_agents = r.n_agents; q.n_lv = uint32_t(r.n_lv);
+        q.o_par = o_par; o_par += r.n_parents;
+        q.o_child = q.o_par;
+        q.o_op = o_op; o_op += r.n_ops;
+        q.o_arun = o_arun; o_arun += r.n_aruns;
+        q.o_tip = o_tip; o_tip += r.n_version;
+        q.o_erec = o_erec; o_erec += uint64_t(EREC_WORDS) * r.n_entries;
+        q.o_doff = o_doff; o_doff += PREP_MAX_CHAINS + 1;
+        q.o_dense = o_dense; o_dense += r.n_lv;
+        q.o_rows = o_rows; o_rows += uint64_t(PREP_MAX_CHAINS) * r.n_entries;
+        q.o_scr = o_scr; o_scr += prep_scratch_words(r.n_parents, r.n_entries);
+        max_e = std::max<uint32_t>(max_e, r.n_entries);
+    }
+    CK(B->p_par.alloc(o_par)); CK(B->p_pent.alloc(o_par)); CK(B->p_pch.alloc(o_par)); CK(B->p_pcnt.alloc(o_par));
+    CK(B->p_child.alloc(o_par)); CK(B->p_opc.alloc(o_op)); CK(B->d_aruns.alloc(4 * o_arun));
+    CK(B->p_tip.alloc(2 * o_tip)); CK(B->p_erec.alloc(o_erec)); CK(B->p_doff.alloc(o_doff));
+    CK(B->p_dense.alloc(o_dense)); CK(B->pr_rows.alloc(o_rows)); CK(B->pr_scr.alloc(o_scr));
+    CK(B->pr_docs.upload(pd, s)); CK(B->pr_res.alloc(n));
+    PrepParams &pp = B->prep;
+    pp.in = Dd.in.p;
+    pp.d_ops = Dd.ops.p; pp.d_aruns = Dd.aruns.p; pp.d_ent = Dd.ent.p; pp.d_poff = Dd.poff.p; pp.d_par = Dd.par.p;
+    pp.d_ver = Dd.ver.p; pp.d_agents = Dd.agents.p;
+    pp.par = B->p_par.p; pp.pent = B->p_pent.p; pp.pch = B->p_pch.p; pp.pcnt = B->p_pcnt.p; pp.child = B->p_child.p;
+    pp.aruns = B->d_aruns.p; pp.tip = B->p_tip.p; pp.erec = B->p_erec.p; pp.doff = B->p_doff.p; pp.dense = B->p_dense.p;
+    pp.rows = B->pr_rows.p; pp.scr = B->pr_scr.p; pp.opc = B->p_opc.p;
+    pp.docs = B->pr_docs.p; pp.results = B->pr_res.p; pp.n_docs = uint32_t(n); pp.max_entries = max_e;
+    if (launch_prep(pp, s)) return DTGPU_ERR_HIP;
+    std::vector<PrepResult> prr(n);
+    CK(hipMemcpyAsync(prr.data(), B->pr_res.p, n * sizeof(PrepResult), hipMemcpyDeviceToHost, s));
+    CK(hipStreamSynchronize(s));
+
+    // ---- planner sizing pass ----------------------------------------------------------------------
+    std::vector<PlanDesc> pdesc(n);
+    uint64_t base_total = 0;
+    uint32_t lds_entries = 0, max_agents = 0;
+    for (size_t i = 0; i < n; i++) {
+        PlanDesc &q = pdesc[i];
+        std::memset(&q, 0, sizeof q);
+        q.skip = 1;
+        if (B->host_status[i] != OK) continue;
+        if (prr[i].status != PREP_OK) { B->host_status[i] = prr[i].status == PREP_WIDE ? DECODE_DEFER : ErrCheckout; continue; }
+        const PrepDesc &r = pd[i];
+        q.skip = 0;
+        q.par_off = r.o_par; q.child_off = r.o_child; q.op_off = r.o_op; q.arun_off = r.o_arun; q.tip_off = r.o_tip;
+        q.erec_off = r.o_erec; q.doff_off = r.o_doff; q.dense_off = r.o_dense;
+        q.base_off = base_total;
+        q.ne = r.ne; q.n_agents = prr[i].n_chains; q.n_aruns = r.n_aruns; q.ntip = r.n_ver; q.n_lv = r.n_lv;
+        base_total += uint64_t(r.ne) * std::max<uint32_t>(prr[i].n_chains, 1);
+        lds_entries = std::max<uint32_t>(lds_entries, r.ne);
+        max_agents = std::max<uint32_t>(max_agents, prr[i].n_chains);
+    }
+    CK(B->p_base.alloc(base_total));
+    CK(B->p_docs.upload(pdesc, s));
+    CK(B->p_results.alloc(n));
+    CK(hipMemsetAsync(B->p_results.p, 0, std::max<size_t>(n, 1) * sizeof(PlanResult), s));
+    PlanParams &q = B->plan;
+    q.par = B->p_par.p; q.pent = B->p_pent.p; q.pch = B->p_pch.p; q.pcnt = B->p_pcnt.p; q.child = B->p_child.p;
+    q.opc = B->p_opc.p; q.aruns = B->d_aruns.p; q.tip = B->p_tip.p; q.erec = B->p_erec.p; q.doff = B->p_doff.p;
+    q.dense = B->p_dense.p; q.base = B->p_base.p;
+    q.lds_entries = (lds_entries + 7) & ~7u;
+    q.max_agents = max_agents;
+    q.prof = getenv("DTGPU_PLAN_PROF") ? 1u : 0u;
+    q.docs = B->p_docs.p; q.results = B->p_results.p; q.n_docs = uint32_t(n);
+    q.count_only = 1;
+    if (launch_plan(q, s) != OK) return DTGPU_ERR_HIP;
+    q.count_only = 0;
+    std::vector<PlanResult> pres(n);
+    CK(hipMemcpyAsync(pres.data(), B->p_results.p, std::max<size_t>(n, 1) * sizeof(PlanResult), hipMemcpyDeviceToHost, s));
+    CK(hipStreamSynchronize(s));
+
+    // ---- replay layout ---------------------------------------------------------------------------
+    uint64_t cmd_total = 0, tlist_total = 0, blk_total = 0, out_total = 0, gidx_total = 0;
+    uint64_t lds_fill = 40;
+    if (const char *e = getenv("DTGPU_LDS_FILL")) lds_fill = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
+    for (size_t i = 0; i < n; i++) {
+        DocDesc &d = B->docs[i];
+        std::memset(&d, 0, sizeof d);
+        if (B->host_status[i] != OK) { pdesc[i].skip = 1; continue; }
+        if (pres[i].status != PLAN_OK) { B->host_status[i] = DECODE_DEFER; pdesc[i].skip = 1; continue; }
+        const DecodeResult &r = Dd.res[i];
+        const DecodeDesc &dd = Dd.desc[i];
+        const uint64_t n_ins = prr[i].n_ins;
+        if (n_ins / 32 + 2 > std::min<uint64_t>(LOC_MAX_BLOCKS, MAX_DOC_BLOCKS)) { B->host_status[i] = ErrCapacity; pdesc[i].skip = 1; continue; }
+        d.cmd_off = cmd_total; d.tlist_off = tlist_total;
+        d.ncmd = pres[i].ncmd;
+        pdesc[i].cmd_off = cmd_total; pdesc[i].tlist_off = tlist_total;
+        pdesc[i].ccap = pres[i].ncmd; pdesc[i].tcap = pres[i].ntlist;
+        cmd_total += pres[i].ncmd;
+        tlist_total += pres[i].ntlist;
+        B->n_gpu_planned++;
+        d.ascii = r.n_content == n_ins ? 1u : 0u;
+        d.lv_off = dd.lv_off;                 // per-LV arenas share the decoder's LV numbering
+        d.n_lv = uint32_t(r.n_lv);
+        d.content_off = dd.content_off;       // inserted text read in place
+        d.content_len = r.n_content;
+        d.arun_off = pd[i].o_arun * 4;
+        d.n_aruns = r.n_aruns;
+        d.max_blocks = uint32_t(n_ins / 32 + 2);
+        d.blk_off = blk_total;
+        d.out_off = out_total;
+        d.out_cap = r.n_content;
+        blk_total += d.max_blocks;
+        out_total += d.out_cap;
+        B->total_lv += r.n_lv;
+        B->alg_in_bytes += 16ull * r.n_ops + 8ull * r.n_entries + 4ull * r.n_parents + 12ull * r.n_aruns + r.n_content;
+        d.gidx_off = gidx_total;
+        gidx_total += index_bytes(d.max_blocks);
+        const uint32_t est = uint32_t(std::min<uint64_t>(d.max_blocks, n_ins / lds_fill + 8));
+        if (index_bytes(est) <= kLdsIndexBudget) {
+            B->small_list.push_back(uint32_t(i));
+            B->lds_blocks = std::max(B->lds_blocks, est);
+        } else {
+            B->large_list.push_back(uint32_t(i));
+        }
+    }
+    const uint64_t lv_total = Dd.cbyte.n;
+    CK(B->d_cmds.alloc(cmd_total));
+    CK(B->d_tlist.alloc(tlist_total));
+    CK(B->p_docs.upload(pdesc, s));
+    B->plan.docs = B->p_docs.p;
+    B->plan.cmds = B->d_cmds.p;
+    B->plan.tlist = B->d_tlist.p;
+    CK(B->d_docs.upload(B->docs, s));
+    std::vector<uint32_t> lists(B->small_list);
+    lists.insert(lists.end(), B->large_list.begin(), B->large_list.end());
+    CK(B->d_lists.upload(lists, s));
+    CK(B->d_pos.alloc(lv_total));
+    CK(B->d_cv.alloc(lv_total));
+    CK(B->d_ao.alloc(lv_total));
+    CK(B->d_items.alloc(blk_total * 64));
+    CK(B->d_m2.alloc(2 * blk_total));
+    CK(B->d_out.alloc(out_total));
+    CK(B->d_gidx.alloc(gidx_total));
+    CK(B->d_fb.alloc(B->small_list.size() + 1));
+    CK(B->d_counter.alloc(2));
+    CK(B->d_results.alloc(n));
+    CK(hipMemsetAsync(B->d_results.p, 0, std::max<size_t>(n, 1) * sizeof(DocResult), s));
+    CK(hipStreamSynchronize(s));
+#undef CK
+    BatchParams base{};
+    if (const char *dbg = getenv("DTGPU_DEBUG")) base.debug = uint32_t(atoi(dbg) ? atoi(dbg) : 1);
+    base.cmds = B->d_cmds.p;
+    base.tlist = B->d_tlist.p;
+    base.cbyte = Dd.cbyte.p;
+    base.content = Dd.content.p;
+    base.aruns = B->d_aruns.p;
+    base.pos = B->d_pos.p;
+    base.cv = B->d_cv.p;
+    base.ao = B->d_ao.p;
+    base.items = B->d_items.p;
+    base.m2 = B->d_m2.p;
+    base.out = B->d_out.p;
+    base.gidx = B->d_gidx.p;
+    base.docs = B->d_docs.p;
+    base.results = B->d_results.p;
+    B->small = base;
+    B->small.doc_list = B->d_lists.p;
+    B->small.n_list = uint32_t(B->small_list.size());
+    B->small.lds_blocks = B->lds_blocks;
+    B->small.counter = B->d_counter.p;
+    B->large = base;
+    B->large.doc_list = B->d_lists.p + B->small_list.size();
+    B->large.n_list = uint32_t(B->large_list.size());
+    B->large.counter = B->d_counter.p + 1;
+    if (!B->small_list.empty() && !getenv("DTGPU_NO_FALLBACK")) {
+        B->small.fb_count = B->d_fb.p;
+        B->small.fb_list = B->d_fb.p + 1;
+        B->large.fb_count = B->d_fb.p;
+        B->large.fb_list = B->d_fb.p + 1;
+    }
+    *out = B.release();
+    return DTGPU_OK;
+}
+
 // Plan (device) then replay, on stream s.
 int launch_all(dtgpu_batch *B, hipStream_t s) {
     if (B->n_gpu_planned) {
@@ -580,6 +822,35 @@ dtgpu_status dtgpu_batch_create_from_oplogs(const dtgpu_oplog *const *oplogs, si
         prepare_input(prep[i]);
     });
     return stage(prep, opts, out);
+}
+dtgpu_status dtgpu_batch_create_device(const uint8_t *const *docs, const size_t *lens, size_t n,
+                                       const dtgpu_batch_opts *opts, dtgpu_batch **out) {
+    if (!out || (n && (!docs || !lens))) return DTGPU_ERR_ARG;
+    return stage_device(docs, lens, n, opts, out);
+}
+dtgpu_status dtgpu_batch_run_e2e_timed(dtgpu_batch *B, float ms[4]) {
+    if (!B || !B->dec) return DTGPU_ERR_ARG;
+    if (hipSetDevice(B->device) != hipSuccess) return DTGPU_ERR_HIP;
+    hipStream_t s = B->stream;
+    // decode + prep + plan + replay from the `.dt` bytes in HBM
+    if (hipEventRecord(B->ev_dec, s) != hipSuccess) return DTGPU_ERR_HIP;
+    if (launch_decode(B->dec->P, s)) return DTGPU_ERR_HIP;
+    if (hipEventRecord(B->ev_prep, s) != hipSuccess) return DTGPU_ERR_HIP;
+    if (launch_prep(B->prep, s)) return DTGPU_ERR_HIP;
+    if (hipEventRecord(B->ev0, s) != hipSuccess) return DTGPU_ERR_HIP;
+    if (B->n_gpu_planned && launch_plan(B->plan, s) != OK) return DTGPU_ERR_HIP;
+    if (hipEventRecord(B->ev_mid, s) != hipSuccess) return DTGPU_ERR_HIP;
+    int st = launch_replay(B->small, B->large, s, B->n_cu);
+    if (st) return dtgpu_status(st);
+    if (hipEventRecord(B->ev1, s) != hipSuccess) return DTGPU_ERR_HIP;
+    if (hipEventSynchronize(B->ev1) != hipSuccess) return DTGPU_ERR_HIP;
+    float td = 0, tp = 0, tl = 0, tr = 0;
+    if (hipEventElapsedTime(&td, B->ev_dec, B->ev_prep) != hipSuccess || hipEventElapsedTime(&tp, B->ev_prep, B->ev0) != hipSuccess ||
+        hipEventElapsedTime(&tl, B->ev0, B->ev_mid) != hipSuccess || hipEventElapsedTime(&tr, B->ev_mid, B->ev1) != hipSuccess)
+        return DTGPU_ERR_HIP;
+    B->last_decode_ms = td; B->last_prep_ms = tp; B->last_plan_ms = tl; B->last_replay_ms = tr;
+    if (ms) { ms[0] = td; ms[1] = tp; ms[2] = tl; ms[3] = tr; }
+    return DTGPU_OK;
 }
 dtgpu_status dtgpu_batch_run(dtgpu_batch *B, void *stream) {
     if (!B) return DTGPU_ERR_ARG;

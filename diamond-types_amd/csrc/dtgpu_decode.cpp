@@ -12,32 +12,10 @@
 #include <vector>
 
 #include "../../include/dtgpu.h"
-#include "dt_decode.hpp"
-#include "dt_devbuf.hpp"
+#include "dt_decoded.hpp"
 #include "dt_host.hpp"
 
 using namespace dtgpu;
-
-struct dtgpu_decoded {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    size_t n = 0;
-    uint64_t in_bytes = 0;
-    float last_ms = 0;
-    std::vector<DecodeDesc> desc;
-    std::vector<DecodeResult> res;
-    DevBuf<uint8_t> in, lz, content;
-    DevBuf<uint32_t> aruns, alist, pre, ops, ent, poff, par, cbyte, agents, ver;
-    DevBuf<DecodeDesc> d_desc;
-    DevBuf<DecodeResult> d_res;
-    DecodeParams P{};
-    ~dtgpu_decoded() {
-        if (ev0) (void)hipEventDestroy(ev0);
-        if (ev1) (void)hipEventDestroy(ev1);
-        if (stream) (void)hipStreamDestroy(stream);
-    }
-};
 
 namespace {
 

@@ -120,6 +120,9 @@ def lib():
     L.dtgpu_batch_total_lv.argtypes = [vp]
     L.dtgpu_batch_total_lv.restype = u64
     L.dtgpu_batch_free.argtypes = [vp]
+    L.dtgpu_batch_create_device.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz), sz,
+                                            ctypes.POINTER(BatchOpts), ctypes.POINTER(vp)]
+    L.dtgpu_batch_run_e2e_timed.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
     L.dtgpu_batch_checkout.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz), sz,
                                        ctypes.POINTER(BatchOpts), ctypes.POINTER(DocResult)]
     L.dtgpu_text_hash.argtypes = [ctypes.c_char_p, sz]
@@ -336,10 +339,12 @@ def oplog_from_trace(txns, agent_name="jeremy") -> ListOpLog:
 
 
 class Batch:
-    """A batch staged in HBM: decode on host threads; walk planning (dt_plan.hip), replay and
-    materialisation (dt_replay.hip) on the GPU."""
+    """A batch staged in HBM.  staging="host": decode and planner inputs on host threads;
+    staging="device": `.dt` bytes to HBM, then decode (dt_decode.hip) and planner inputs
+    (dt_prep.hip) on the GPU as well.  Walk planning (dt_plan.hip), replay and materialisation
+    (dt_replay.hip) always run on the GPU."""
 
-    def __init__(self, docs=None, oplogs=None, ignore_crc=False, host_threads=0, device=0):
+    def __init__(self, docs=None, oplogs=None, ignore_crc=False, host_threads=0, device=0, staging="host"):
         L = lib()
         opts = BatchOpts(int(ignore_crc), int(host_threads), int(device))
         out = ctypes.c_void_p()
@@ -352,7 +357,8 @@ class Batch:
             self._keep = list(docs)
             ptrs = (ctypes.c_char_p * max(1, len(self._keep)))(*self._keep)
             lens = (ctypes.c_size_t * max(1, len(self._keep)))(*[len(d) for d in self._keep])
-            _check(L.dtgpu_batch_create(ptrs, lens, len(self._keep), ctypes.byref(opts), ctypes.byref(out)))
+            create = L.dtgpu_batch_create_device if staging == "device" else L.dtgpu_batch_create
+            _check(create(ptrs, lens, len(self._keep), ctypes.byref(opts), ctypes.byref(out)))
             self.n = len(self._keep)
         self._h = out.value
 
@@ -372,6 +378,12 @@ class Batch:
         ms = ctypes.c_float()
         _check(lib().dtgpu_batch_run_timed(self._h, ctypes.byref(ms)))
         return ms.value
+
+    def run_e2e_timed(self):
+        """Device-staged batches: decode + prep + plan + replay again; kernel ms of each."""
+        ms = (ctypes.c_float * 4)()
+        _check(lib().dtgpu_batch_run_e2e_timed(self._h, ms))
+        return list(ms)
 
     def sync(self):
         _check(lib().dtgpu_batch_sync(self._h))

@@ -204,6 +204,17 @@ int dtgpu_device_count(void);
 const char *dtgpu_status_str(dtgpu_status status);
 
 
+/* Device-staged batch: the `.dt` bytes go to HBM and everything after runs on the device --
+ * decode (dt_decode.hip), planner inputs (dt_prep.hip: parents, children, causal chains, entry
+ * records), walk planning and replay; the host only sizes arenas from per-document counts.
+ * Documents outside the device path's limits (see dtgpu_decode_*, and histories wider than 64
+ * causal chains) report status DTGPU_DECODE_DEFER: check them out with dtgpu_batch_create.
+ * dtgpu_batch_run / run_timed then re-run plan + replay; run_e2e_timed re-runs decode + prep +
+ * plan + replay and returns the four kernel times (ms). */
+dtgpu_status dtgpu_batch_create_device(const uint8_t *const *docs, const size_t *lens, size_t n,
+                                       const dtgpu_batch_opts *opts, dtgpu_batch **out);
+dtgpu_status dtgpu_batch_run_e2e_timed(dtgpu_batch *batch, float ms[4]);
+
 /* ---- batched `.dt` decode on the GPU ---------------------------
  * ListOpLog::load_from (src/list/encoding/decode_oplog.rs:447-960) for many documents at once:
  * one wavefront per document (dt_decode.hip).  dtgpu_decode_create uploads the documents and
