@@ -76,8 +76,9 @@ constexpr uint32_t PLAN_MAX_AGENTS = 512;
 constexpr uint32_t PLAN_MAX_LDS_ENTRIES = 16384;   // u16 todo + u16 pending per entry in LDS
 enum PlanStatus : uint32_t {
     PLAN_OK = 0, PLAN_NOT_CHAIN = 1, PLAN_TLIST_FULL = 2, PLAN_CMDS_FULL = 3, PLAN_TOO_MANY_AGENTS = 4,
-    PLAN_ERR_INTERNAL = 5,
+    PLAN_ERR_INTERNAL = 5, PLAN_TODO_FULL = 6, PLAN_WIDE_MERGE = 7,
 };
+constexpr uint32_t PLAN_TODO_CAP = 512;   // ready-entry stack slots per wave (LDS, u16 each)
 struct PlanDesc {       // per document; offsets index the concatenated PlanInput arrays
     uint64_t e_off;     // entries
     uint64_t par_off;   // par / pent

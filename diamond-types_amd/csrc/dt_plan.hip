@@ -55,7 +55,8 @@ struct P {
     uint32_t ne, A, ntip, n_lv;
     // scratch: vv rows in HBM; todo stack and pending parent counts in LDS (u16)
     uint32_t *base;
-    uint16_t *todo, *pending;
+    uint16_t *todo;      // ready entries (PLAN_TODO_CAP slots)
+    uint8_t *pending;    // per entry: unvisited parents | merge flag
     // outputs
     Cmd *cmds;
     uint32_t *tlist;
@@ -205,7 +206,7 @@ DEV void push_cmd(P &p, uint32_t op, uint32_t a, uint32_t n, uint32_t pos) {
     p.nc++;
 }
 
-constexpr uint16_t MERGE_BIT = 0x8000;   // pending word: parent count | merge flag
+constexpr uint8_t MERGE_BIT = 0x80;   // pending byte: parent count (<= 127) | merge flag
 
 // Next entry to consume: the todo top, unless it is a merge and a non-merge is ready
 // (txn_trace.rs:249-266).  Pops it.
@@ -244,11 +245,13 @@ DEV void plan_doc(P &p, PlanResult *res) {
     }
     // pending parent counts (+ merge flag); the todo stack holds the roots, first root on top
     uint32_t top = 0;
+    bool bad_np = false;
     for (uint32_t c = 0; c < p.ne; c += 64) {
         const uint32_t e = c + l;
         if (e < p.ne) {
             const uint32_t np = p.erec[size_t(e) * EREC_WORDS + R_NP];
-            p.pending[e] = uint16_t(min(np, 0x7FFFu) | (np >= 2 ? MERGE_BIT : 0));
+            if (np > 0x7Fu) bad_np = true;
+            p.pending[e] = uint8_t(min(np, 0x7Fu) | (np >= 2 ? MERGE_BIT : 0));
         }
     }
     for (int c = int((p.ne + 63) / 64) - 1; c >= 0; c--) {
@@ -257,9 +260,11 @@ DEV void plan_doc(P &p, PlanResult *res) {
         const bool root = e < p.ne && p.erec[size_t(e) * EREC_WORDS + R_NP] == 0;
         const u64 m = __ballot(root);
         const uint32_t rank = uint32_t(__popcll(m & ((1ull << l) - 1ull)));
+        if (top + uint32_t(__popcll(m)) > PLAN_TODO_CAP) { fail(p, PLAN_TODO_FULL); break; }
         if (root) p.todo[top + rank] = uint16_t(e);
         top += uint32_t(__popcll(m));
     }
+    if (__ballot(bad_np)) fail(p, PLAN_WIDE_MERGE);
     wave_fence();
     uint64_t t_last = tk(p);
     PT(5);
@@ -336,12 +341,13 @@ DEV void plan_doc(P &p, PlanResult *res) {
             const uint32_t chv = c == 0 ? ch : (c + l < nch ? p.child[ch0 + c + l] : 0);
             bool ready = false;
             if (c + l < nch) {
-                const uint16_t pd = uint16_t(p.pending[chv] - 1);
+                const uint8_t pd = uint8_t(p.pending[chv] - 1);
                 p.pending[chv] = pd;
-                ready = (pd & 0x7FFF) == 0;
+                ready = (pd & 0x7F) == 0;
             }
             const u64 m = __ballot(ready);
             const uint32_t rank = uint32_t(__popcll(m & ((1ull << l) - 1ull)));
+            if (top + uint32_t(__popcll(m)) > PLAN_TODO_CAP) { fail(p, PLAN_TODO_FULL); break; }
             if (ready) p.todo[top + rank] = uint16_t(chv);
             top += uint32_t(__popcll(m));
         }
@@ -428,7 +434,7 @@ __global__ __launch_bounds__(64) void plan_kernel(PlanParams Q) {
     p.ntip = U(pd.ntip);
     p.n_lv = U(pd.n_lv);
     p.todo = lds16;
-    p.pending = lds16 + Q.lds_entries;
+    p.pending = reinterpret_cast<uint8_t *>(lds16 + PLAN_TODO_CAP);
     p.base = Q.base + pd.base_off;
     p.cmds = Q.cmds + pd.cmd_off;
     p.tlist = Q.tlist + pd.tlist_off;
@@ -454,7 +460,7 @@ __global__ __launch_bounds__(64) void plan_kernel(PlanParams Q) {
 int launch_plan(const PlanParams &q, void *stream) {
     if (!q.n_docs) return OK;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    const size_t lds = size_t(q.lds_entries) * 4;   // u16 todo + u16 pending per entry
+    const size_t lds = 2 * size_t(PLAN_TODO_CAP) + ((size_t(q.lds_entries) + 15) & ~size_t(15));   // todo + pending
     hipLaunchKernelGGL(pdev::plan_kernel<1>, dim3(q.n_docs), dim3(64), lds, s, q);
     if (hipGetLastError() != hipSuccess) return ErrHip;
     if (q.max_agents > 64) {

@@ -25,7 +25,7 @@ def main():
         if distinct:
             b = dt_amd.Batch(oplogs=[pool[i % distinct] for i in range(n)])
         else:
-            b = dt_amd.Batch(docs=[data] * n)
+            b = dt_amd.Batch(docs=[data] * n, staging="device")
         stage = time.time() - t
         b.run(); b.sync()
         ms, split = [], []
