@@ -38,6 +38,8 @@
 // Document order is the lexicographic order of (top position, index in superblock, slot):
 // YjsMod compares those keys directly (merge.rs:154-278) instead of counting items.
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 #include <stdint.h>
 
 #include "dt_device.hpp"
@@ -970,7 +972,8 @@ int launch_replay(const BatchParams &small, const BatchParams &large, void *stre
     const bool prof = (small.debug | large.debug) & 2u;
     if (small.n_list) {
         if (small.fb_count && hipMemsetAsync(small.fb_count, 0, sizeof(uint32_t), s) != hipSuccess) return ErrHip;
-        const size_t lds = size_t(index_bytes(small.lds_blocks));
+        size_t lds = size_t(index_bytes(small.lds_blocks));
+        if (const char *pad = getenv("DTGPU_LDS_PAD")) lds += size_t(strtoul(pad, nullptr, 10));   // occupancy experiments
         if (prof) hipLaunchKernelGGL((dev::replay_kernel<true, true>), dim3(small.n_list), dim3(64), lds, s, small);
         else hipLaunchKernelGGL((dev::replay_kernel<true, false>), dim3(small.n_list), dim3(64), lds, s, small);
         if (hipGetLastError() != hipSuccess) return ErrHip;
