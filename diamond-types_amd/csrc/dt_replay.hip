@@ -163,6 +163,11 @@ struct Doc {
     uint64_t prof[P_N];
     uint32_t doc;
     uint32_t *fb_list, *fb_count;   // LDS tier: capacity-overflow queue for the HBM tier
+    // the block the last insert / delete left behind, in registers (items lane by lane, masks):
+    // typing keeps hitting it, so the next command skips its load.  Memory always holds the
+    // same state (every change is stored); a toggle touching the block drops it.
+    uint32_t cb, cit;
+    u64 cmv, cml;
 };
 
 DEV void fail(Doc &D, uint32_t code, uint32_t site) {
@@ -377,6 +382,7 @@ template <bool L> DEV uint32_t cut_point(uint32_t s) { return L ? min(max(s, 16u
 template <bool L, bool PROF>
 DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml, uint32_t lv, uint32_t k,
                     uint32_t ol, uint32_t orr) {
+    D.cb = NONE;
     const uint32_t l = lane_id();
     const uint32_t lv0 = lv, k0 = k;
     while (k > 0) {
@@ -431,6 +437,7 @@ DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml,
         k -= m;
         s += m;
     }
+    D.cb = b; D.cit = it; D.cmv = mv; D.cml = ml;   // block state after the run
     const uint64_t t3 = tick<PROF>();
     for (uint32_t j = l; j < k0; j += 64) {
         const uint32_t nit = lv0 + j;
@@ -561,7 +568,8 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
     const uint32_t bc = c_items(U(ix<L>(D.cnt + b)));
     uint32_t it;
     u64 mv, ml;
-    load_block<L>(D, b, bc, it, mv, ml);
+    if (b == D.cb) { it = D.cit; mv = D.cmv; ml = D.cml; }
+    else load_block<L>(D, b, bc, it, mv, ml);
     uint32_t s = 0, ol = ROOT_ID;
     if (pos) {
         const uint32_t s0 = select_bit(mv, kk);
@@ -603,7 +611,10 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
         const uint32_t b0 = b;
         yjs_scan<L>(D, b, s, rb, rs, my_l, my_r, orr, lv);
         if (D.err) return;
-        if (b != b0) load_block<L>(D, b, c_items(U(ix<L>(D.cnt + b))), it, mv, ml);
+        if (b != b0) {
+            if (b == D.cb) { it = D.cit; mv = D.cmv; ml = D.cml; }
+            else load_block<L>(D, b, c_items(U(ix<L>(D.cnt + b))), it, mv, ml);
+        }
         if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_YJS] += t - tp; tp = t; D.prof[P_N_YJS]++; }
     }
     const uint64_t sp0 = PROF ? D.prof[P_SPLIT] : 0;
@@ -626,7 +637,8 @@ DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
         const uint32_t c = U(ix<L>(D.cnt + b));
         uint32_t it;
         u64 mv, ml;
-        load_block<L>(D, b, c_items(c), it, mv, ml);
+        if (b == D.cb) { it = D.cit; mv = D.cmv; ml = D.cml; }
+        else load_block<L>(D, b, c_items(c), it, mv, ml);
         const uint32_t avail = c_vis(c) - kk;
         const uint32_t take = min(avail, n - j0);
         const uint32_t r = uint32_t(__popcll(mv & lanes_below(l)));
@@ -645,6 +657,7 @@ DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
             D.top[f.tp] = ix<L>(D.top + f.tp) - take;
         }
         wave_fence();
+        D.cb = b; D.cit = it; D.cmv = mv & ~selm; D.cml = ml;
         j0 += take;
     }
 }
@@ -657,7 +670,7 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
     const uint32_t l = lane_id();
     for (uint32_t j = 0; j < n; j += 64) {
         if (!charge(D)) return;
-        bool bad = false;
+        bool bad = false, hit_cached = false;
         if (j + l < n) {
             const uint32_t e = (j == 0 && have_pre) ? pre : D.tlist[off + j + l];
             const uint32_t lv = e & 0x3FFFFFFFu;
@@ -671,6 +684,7 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
                 const uint32_t oc = cv_add(D.cv + item, adv ? 1u : 0xFFFFFFFFu);
                 const uint32_t nc = adv ? oc + 1 : oc - 1;
                 const uint32_t b = pos_blk(w);
+                hit_cached = b == D.cb;
                 if ((!adv && oc == 0) || (adv && oc >= 0x7FFFFFFFu) || b >= D.nb) {
                     bad = true;
                 } else {
@@ -696,6 +710,7 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
                 }
             }
         }
+        if (__ballot(hit_cached)) D.cb = NONE;
         if (__ballot(bad)) { fail(D, ErrCheckout, 16); return; }
     }
     wave_fence();
@@ -831,6 +846,9 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
     D.step_limit = 64ull * (uint64_t(D.ncmd) + D.n_lv) + 4096;
     D.site = 0;
     D.ci = 0;
+    D.cb = NONE;
+    D.cit = 0;
+    D.cmv = D.cml = 0;
     if (PROF) for (int i = 0; i < P_N; i++) D.prof[i] = 0;
     const uint64_t t_start = tick<PROF>();
     // commands are fetched 64 at a time (one per lane) and broadcast with readlane; the first
