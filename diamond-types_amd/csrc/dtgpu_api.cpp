@@ -753,12 +753,17 @@ size_t dtgpu_oplog_export(const dtgpu_oplog *h, int what, void *out, size_t cap)
     std::vector<uint8_t> b;
     bool bytes = false;
     switch (what) {
-        case DTGPU_EXPORT_OPS:
-            for (const OpRun &r : o.ops) {
+        case DTGPU_EXPORT_OPS: {   // split at graph entries, as the decoders produce them
+            HostOpLog f;
+            f.ops = o.ops;
+            f.graph = o.graph;
+            f.finish();
+            for (const OpRun &r : f.ops) {
                 w.push_back(uint32_t(r.lv)); w.push_back(uint32_t(r.len)); w.push_back(uint32_t(r.pos));
                 w.push_back(uint32_t(r.kind) | (uint32_t(r.fwd) << 1));
             }
             break;
+        }
         case DTGPU_EXPORT_AGENT_RUNS:
             for (const AgentRun &r : o.agent_runs) {
                 w.push_back(uint32_t(r.lv)); w.push_back(uint32_t(r.len)); w.push_back(r.agent); w.push_back(uint32_t(r.seq));
