@@ -36,8 +36,11 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--docs", type=int, default=10000, help="friendsforever copies per GPU")
-    p.add_argument("--workload", default="friendsforever")
+    p.add_argument("--docs", type=int, default=10000, help="documents per GPU")
+    p.add_argument("--workload", default="friendsforever",
+                   help="friendsforever | git-makefile | node_nodecc (benchmark_data copies) or synth "
+                        "(BASELINE configs[3]: synthetic concurrent documents, dt_synth.cpp, written as .dt)")
+    p.add_argument("--distinct", type=int, default=256, help="synth: distinct documents, replicated to --docs")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     p.add_argument("--cpu-cores", type=int, default=16)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -46,24 +49,26 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(data, budget_s, cores):
+def cpu_baseline(pool, budget_s, cores):
     """The CPU oracle (C restatement of the reference algorithm, one document per thread)
     timed on a bounded sample of the same workload: checkout_tip() on an already-decoded
-    oplog, as the reference's `complex/merge` bench times it."""
+    oplog, as the reference's `complex/merge` bench times it.  `pool`: the distinct documents."""
     from oracle.oracle import OpLog as OracleOpLog
-    o = OracleOpLog.load_from(data)
+    o = OracleOpLog.load_from(pool[0])
     t0 = time.perf_counter()
     o.checkout_tip_bytes()
     one = time.perf_counter() - t0
     per_core = max(1, int(budget_s / max(one, 1e-4) / cores))
-    n_lv = len(o)
     done = [0] * cores
-    logs = [OracleOpLog.load_from(data) for _ in range(cores)]
+    lvs = [0] * cores
+    logs = [[OracleOpLog.load_from(pool[(k + j) % len(pool)]) for j in range(min(len(pool), 4))] for k in range(cores)]
 
     def work(k):
-        for _ in range(per_core):
-            logs[k].checkout_tip_bytes()
+        for i in range(per_core):
+            lg = logs[k][i % len(logs[k])]
+            lg.checkout_tip_bytes()
             done[k] += 1
+            lvs[k] += len(lg)
 
     th = [threading.Thread(target=work, args=(k,)) for k in range(cores)]
     t0 = time.perf_counter()
@@ -73,12 +78,12 @@ def cpu_baseline(data, budget_s, cores):
         t.join()
     wall = time.perf_counter() - t0
     docs = sum(done)
-    return {"value": docs * n_lv / wall, "unit": "merged ops/s", "cores": cores, "kind": "port",
+    return {"value": sum(lvs) / wall, "unit": "merged ops/s", "cores": cores, "kind": "port",
             "sample": f"{docs} x friendsforever.dt checkout_tip (decoded oplog, C oracle) on {cores} host threads, "
                       f"{wall:.2f} s"}
 
 
-def e2e_leg(batch, docs, steps, text_len, total_lv):
+def e2e_leg(batch, docs, steps, expect, total_lv):
     """`.dt` bytes in HBM -> text: device decode (dt_decode.hip) + planner inputs (dt_prep.hip) +
     walk plan + replay, re-run `steps` times on the device-staged batch (HIP events per kernel).
     Roofline basis = SURVEY.md 8d E2E: encoded bytes + text bytes per document.  The decoder's
@@ -86,7 +91,8 @@ def e2e_leg(batch, docs, steps, text_len, total_lv):
     import dt_amd
     split = [batch.run_e2e_timed() for _ in range(max(1, steps))]
     res = batch.results()
-    assert all(r["status"] == 0 and r["text_len"] == text_len for r in res), "end-to-end results differ"
+    assert all(r["status"] == 0 and (r["text_len"], r["text_hash"]) == e for r, e in zip(res, expect)), \
+        "end-to-end results differ"
     dec = dt_amd.DecodeBatch(docs[:1])
     dec.run()
     host = dt_amd.ListOpLog.load_from(docs[0])
@@ -95,12 +101,45 @@ def e2e_leg(batch, docs, steps, text_len, total_lv):
     mean = [statistics.mean(x[k] for x in split) for k in range(4)]
     total = sum(mean)
     enc = sum(len(d) for d in docs)
-    basis = enc + text_len * len(docs)
+    basis = enc + sum(e[0] for e in expect)
     return {"decode_ms": mean[0], "prep_ms": mean[1], "plan_ms": mean[2], "replay_ms": mean[3], "total_ms": total,
             "merged_ops_per_s": total_lv / (total / 1000.0), "docs_per_s": len(docs) / (total / 1000.0),
             "encoded_bytes": enc, "roofline_bytes": basis,
             "achieved_GBps": basis / (total / 1000.0) / 1e9, "frac_hbm": basis / (total / 1000.0) / 1e9 / HBM_PEAK_GBS,
             "basis": "SURVEY.md 8d E2E: |.dt bytes| + |text out| per document; kernel time of decode + prep + plan + replay"}
+
+
+def workload_pool(args):
+    """The distinct documents of the workload (raw `.dt` bytes) and the `data` description."""
+    if args.workload == "synth":
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import dt_amd
+        from dt_encode import encode_dt
+        pool = []
+        for d in range(args.distinct):
+            na, ops = dt_amd.synth_ops(d, 5000)
+            pool.append(encode_dt([f"a{i}" for i in range(na)], ops))
+        return pool, (f"synthetic concurrent documents (dt_synth.cpp: seed 0xD1A00000 + doc, 4-16 agents, "
+                      f"~5k ops), {args.distinct} distinct written as .dt and replicated")
+    path = os.path.join(ROOT, "tests", "golden", "benchmark_data", args.workload + ".dt")
+    return [open(path, "rb").read()], f"benchmark_data/{args.workload}.dt replicated (byte-identical copies in distinct buffers)"
+
+
+def expected_texts(args, pool):
+    """(len, hash) of the reference's checkout per distinct document: friendsforever's golden
+    endContent; otherwise the C oracle (a bounded number of distinct documents)."""
+    import dt_amd
+    if args.workload == "friendsforever":
+        import gzip
+        gold = json.load(gzip.open(os.path.join(ROOT, "tests", "golden", "benchmark_data",
+                                                "friendsforever_flat.json.gz")))["endContent"].encode()
+        return [(len(gold), dt_amd.text_hash(gold))]
+    from oracle.oracle import OpLog as OracleOpLog
+    out = []
+    for d in pool:
+        t = OracleOpLog.load_from(d).checkout_tip_bytes()
+        out.append((len(t), dt_amd.text_hash(t)))
+    return out
 
 
 def main():
@@ -117,15 +156,17 @@ def main():
 
     import dt_amd
     from dt_amd.shard import doc_cost, gather_results, lpt_assign, max_over_ranks
-    data = open(os.path.join(ROOT, "tests", "golden", "benchmark_data", args.workload + ".dt"), "rb").read()
+    pool, data_desc = workload_pool(args)
     n_total = args.docs * world
-    # weak scaling: the global batch is docs x world copies; LPT gives every rank its shard
-    mine = lpt_assign([doc_cost(data)] * n_total, world)[rank]
+    # weak scaling: the global batch is docs x world documents (document g is pool[g % distinct]);
+    # LPT gives every rank its shard
+    mine = lpt_assign([doc_cost(pool[g % len(pool)]) for g in range(n_total)], world)[rank]
+    docs = [bytes(pool[g % len(pool)]) for g in mine]
     dev = f"cuda:{local_rank}" if dist is not None else None
 
     t0 = time.perf_counter()
     staging = "host" if args.host_staging else "device"
-    batch = dt_amd.Batch(docs=[bytes(data) for _ in mine], device=local_rank if world > 1 else 0, staging=staging)
+    batch = dt_amd.Batch(docs=docs, device=local_rank if world > 1 else 0, staging=staging)
     host_stage_s = time.perf_counter() - t0
 
     for _ in range(args.warmup):
@@ -150,23 +191,23 @@ def main():
     # correctness gate (outside the timed region, on the last timed pass's output, so that a
     # --warmup 0 profiling run checks real results): every document's text equals the golden
     res = batch.results()
-    want = batch.text(0)
-    if args.workload == "friendsforever":
-        import gzip
-        gold = json.load(gzip.open(os.path.join(ROOT, "tests", "golden", "benchmark_data",
-                                                "friendsforever_flat.json.gz")))["endContent"].encode()
-        assert want == gold, "device checkout differs from the golden endContent"
-    h = dt_amd.text_hash(want)
-    bad = sum(1 for r in res if r["status"] != 0 or r["text_hash"] != h or r["text_len"] != len(want))
-    assert bad == 0, f"{bad} documents differ"
+    gold = expected_texts(args, pool)   # golden endContent / oracle checkout per distinct document
+    want = [gold[g % len(pool)] for g in mine]
+    bad = sum(1 for r, w in zip(res, want) if r["status"] != 0 or (r["text_len"], r["text_hash"]) != w)
+    assert bad == 0, f"{bad} documents differ from the golden / oracle text"
+    total_lv_mine = sum(r["n_lv"] for r in res)
+    total_lv = total_lv_mine
     if dist is not None:   # RCCL all-gather of per-document (len, hash) records
         table = gather_results([(g, r["status"], r["text_len"], r["text_hash"]) for g, r in zip(mine, res)],
                                n_total, dist, device=dev)
-        assert all(row is not None and row[1] == 0 and row[2] == len(want) for row in table), "gather mismatch"
+        assert all(row is not None and row[1] == 0 and row[2] == gold[row[0] % len(pool)][0] for row in table), \
+            "gather mismatch"
+        import torch
+        t = torch.tensor([float(total_lv_mine)], dtype=torch.float64, device=dev)
+        dist.all_reduce(t)   # whole-job merged ops
+        total_lv = int(t.item())
         dist.barrier()
-
-    lv_per_doc = res[0]["n_lv"]
-    total_lv = lv_per_doc * n_total
+    lv_per_doc = total_lv_mine / max(1, len(mine))
     ms_per_step = elapsed * 1000.0 / args.steps
     value = total_lv * args.steps / elapsed
     avg_kernel_ms = statistics.mean(kernel_ms)
@@ -191,8 +232,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u32/u8 integer",
-        "data": "benchmark_data/friendsforever.dt replicated (byte-identical copies in distinct buffers)",
-        "config": {"workload": f"{args.workload}.dt x {args.docs} docs per GPU (checkout_tip)",
+        "data": data_desc,
+        "config": {"workload": f"{args.workload} x {args.docs} docs per GPU (checkout_tip)",
                    "docs_per_gpu": args.docs, "merged_ops_per_doc": lv_per_doc,
                    "timed": "device walk planning + replay + materialisation of the whole batch "
                             "(decoded oplogs resident in HBM)",
@@ -209,9 +250,9 @@ def main():
                                             "+ inserted_bytes + text_out_bytes (SURVEY.md 8d merge-only)"},
     }
     if not args.no_decode and staging == "device":   # .dt bytes -> text, all on the GPU
-        out["e2e"] = e2e_leg(batch, [bytes(data) for _ in mine], min(args.steps, 5), len(want), lv_per_doc * len(mine))
+        out["e2e"] = e2e_leg(batch, docs, min(args.steps, 5), want, total_lv_mine)
     if rank == 0 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(data, args.cpu_seconds, args.cpu_cores)
+        out["cpu_baseline"] = cpu_baseline(pool, args.cpu_seconds, args.cpu_cores)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -30,12 +30,24 @@ def chunk(t, body):
     return leb(t) + leb(len(body)) + bytes(body)
 
 
-def crc32c(data):
-    c = 0xFFFFFFFF
-    for b in data:
-        c ^= b
+def _crc_table():
+    t = []
+    for i in range(256):
+        c = i
         for _ in range(8):
             c = (c >> 1) ^ 0x82F63B78 if c & 1 else c >> 1
+        t.append(c)
+    return t
+
+
+_CRC = _crc_table()
+
+
+def crc32c(data):   # CRC-32/ISCSI (src/encoding/tools.rs:111-115)
+    c = 0xFFFFFFFF
+    t = _CRC
+    for b in data:
+        c = t[(c ^ b) & 0xFF] ^ (c >> 8)
     return c ^ 0xFFFFFFFF
 
 
