@@ -38,8 +38,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--docs", type=int, default=10000, help="documents per GPU")
     p.add_argument("--workload", default="friendsforever",
-                   help="friendsforever | git-makefile | node_nodecc (benchmark_data copies) or synth "
-                        "(BASELINE configs[3]: synthetic concurrent documents, dt_synth.cpp, written as .dt)")
+                   help="friendsforever | git-makefile | node_nodecc (benchmark_data copies), synth "
+                        "(BASELINE configs[3]: synthetic concurrent documents, dt_synth.cpp, written as .dt) or "
+                        "mixed (configs[4]: all 8 benchmark_data traces)")
     p.add_argument("--distinct", type=int, default=256, help="synth: distinct documents, replicated to --docs")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     p.add_argument("--cpu-cores", type=int, default=16)
@@ -121,8 +122,32 @@ def workload_pool(args):
             pool.append(encode_dt([f"a{i}" for i in range(na)], ops))
         return pool, (f"synthetic concurrent documents (dt_synth.cpp: seed 0xD1A00000 + doc, 4-16 agents, "
                       f"~5k ops), {args.distinct} distinct written as .dt and replicated")
+    if args.workload == "mixed":   # BASELINE configs[4]: all benchmark_data traces, skewed sizes
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import golden_data as G
+        from dt_encode import encode_dt
+        pool = [open(os.path.join(ROOT, "tests", "golden", "benchmark_data", n + ".dt"), "rb").read()
+                for n in G.DT_FILES]
+        for name in G.JSON_TRACES:
+            pool.append(encode_dt(["jeremy"], trace_ops(G.trace(name)["txns"])))
+        return pool, ("all 8 benchmark_data traces (3 .dt files + 5 JSON traces written as .dt the way "
+                      "crates/bench/src/utils.rs:25-44 builds their oplogs), replicated round-robin")
     path = os.path.join(ROOT, "tests", "golden", "benchmark_data", args.workload + ".dt")
     return [open(path, "rb").read()], f"benchmark_data/{args.workload}.dt replicated (byte-identical copies in distinct buffers)"
+
+
+def trace_ops(txns):
+    """JSON trace -> op list (agent 0, delete then insert per patch, linear history)."""
+    ops, lv = [], 0
+    for txn in txns:
+        for pos, dl, ins in txn["patches"]:
+            if dl > 0:
+                ops.append((0, 1, pos, dl, "", [lv - 1] if lv else []))
+                lv += dl
+            if ins:
+                ops.append((0, 0, pos, len(ins), ins, [lv - 1] if lv else []))
+                lv += len(ins)
+    return ops
 
 
 def expected_texts(args, pool):
