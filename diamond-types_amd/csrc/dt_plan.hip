@@ -200,6 +200,71 @@ DEV void emit_diff(P &p, const VV<K> &from, const VV<K> &to, const VV<K> &dlo, c
     }
 }
 
+// emit_diff for <= 64 chains split in two: emit_issue (as soon as both vectors are known)
+// computes the per-chain ranges and issues the gather of the first 64 dense-table words;
+// emit_store (after the children bookkeeping has hidden that latency) writes them and any
+// further chunks.  Same output as emit_diff<1>.
+struct Emit {
+    bool any;
+    u64 am;
+    uint32_t off, n, src, fl;    // per chain lane: output offset, count, dense source, advance flag
+    uint32_t total, n_adv;
+    uint32_t dv, dfl;            // lane u < 64: dense word and flag of output u
+};
+DEV void emit_issue(P &p, const VV<1> &from, const VV<1> &to, const VV<1> &dlo, const VV<1> &dhi,
+                    bool allow_retreat, Emit &E) {
+    const uint32_t l = lane_id();
+    const bool act = l < p.A && from.v[0] != to.v[0];
+    E.am = __ballot(act);
+    E.any = E.am != 0;
+    E.total = E.n_adv = 0;
+    E.dv = 0; E.dfl = 0;
+    if (!E.any) return;
+    if (__ballot(act && to.v[0] < from.v[0] && !allow_retreat)) { fail(p, PLAN_ERR_INTERNAL); E.any = false; return; }
+    const bool adv = to.v[0] > from.v[0];
+    const uint32_t s0 = adv ? from.v[0] : to.v[0];
+    const uint32_t n = act ? (adv ? to.v[0] - from.v[0] : from.v[0] - to.v[0]) : 0;
+    if (__ballot(act && dlo.v[0] + s0 + n > dhi.v[0])) { fail(p, PLAN_ERR_INTERNAL); E.any = false; return; }
+    const uint32_t inc = wave_scan(n);
+    E.total = bcast(inc, 63);
+    E.n_adv = bcast(wave_scan(adv ? n : 0), 63);
+    E.off = inc - n; E.n = n; E.src = dlo.v[0] + s0; E.fl = adv ? TL_ADV : 0u;
+    if (p.count_only) return;
+    uint32_t from_idx = 0, flag = 0;
+    for (u64 m = E.am; m; m &= m - 1) {   // the chain whose output slice holds lane l
+        const uint32_t j = first_lane(m);
+        const uint32_t o = U(bcast(E.off, j)), nn = U(bcast(E.n, j));
+        if (l >= o && l < o + nn) { from_idx = U(bcast(E.src, j)) + (l - o); flag = U(bcast(E.fl, j)); }
+    }
+    if (l < E.total) { E.dv = p.dense[from_idx]; E.dfl = flag; }
+}
+DEV void emit_store(P &p, const Emit &E) {
+    const uint32_t l = lane_id();
+    if (uint64_t(p.nt) + E.total > p.tcap) { fail(p, PLAN_TLIST_FULL); return; }
+    if (!p.count_only) {
+        bool bad = l < E.total && E.dv == 0xFFFFFFFFu;
+        if (l < E.total) p.tlist[p.nt + l] = E.dv | E.dfl;
+        for (uint32_t c = 64; c < E.total; c += 64) {
+            const uint32_t u = c + l;
+            uint32_t from_idx = 0, flag = 0;
+            for (u64 m = E.am; m; m &= m - 1) {
+                const uint32_t j = first_lane(m);
+                const uint32_t o = U(bcast(E.off, j)), nn = U(bcast(E.n, j));
+                if (u >= o && u < o + nn) { from_idx = U(bcast(E.src, j)) + (u - o); flag = U(bcast(E.fl, j)); }
+            }
+            if (u < E.total) {
+                const uint32_t v = p.dense[from_idx];
+                if (v == 0xFFFFFFFFu) bad = true;
+                p.tlist[p.nt + u] = v | flag;
+            }
+        }
+        if (__ballot(bad)) { fail(p, PLAN_ERR_INTERNAL); return; }
+    }
+    p.nt += E.total;
+    p.n_adv += E.n_adv;
+    p.n_ret += E.total - E.n_adv;
+}
+
 DEV void push_cmd(P &p, uint32_t op, uint32_t a, uint32_t n, uint32_t pos) {
     if (uint64_t(p.nc) >= p.ccap) { fail(p, PLAN_CMDS_FULL); return; }
     if (lane_id() == 0 && !p.count_only) p.cmds[p.nc] = Cmd{op, a, n, pos};
@@ -335,6 +400,13 @@ DEV void plan_doc(P &p, PlanResult *res) {
         vf = vp;
         fold_entry<K>(p, e_start, e_end, e_end - 1, chain, seq0, vf, true);
         if (p.err) break;
+        // K = 1: the retreat / advance gather is issued now and stored after the children work
+        Emit em;
+        em.any = false;
+        if constexpr (K == 1) {
+            if (vv_differ(v_old, vp)) emit_issue(p, v_old, vp, dlo, dhi, true, em);
+            if (p.err) break;
+        }
         // children whose last parent this was become ready (pushed in child index order); the
         // next entry is picked and its record requested before this entry's output is written
         for (uint32_t c = 0; c < nch; c += 64) {
@@ -359,7 +431,14 @@ DEV void plan_doc(P &p, PlanResult *res) {
         }
         PT(2);
         // retreat / advance to the parents, then apply the entry's op runs
-        if (vv_differ(v_old, vp)) {
+        if constexpr (K == 1) {
+            if (em.any) {
+                const uint32_t t0 = p.nt;
+                emit_store(p, em);
+                if (p.err) break;
+                if (p.nt > t0) push_cmd(p, CMD_TOG, t0, p.nt - t0, 0);
+            }
+        } else if (vv_differ(v_old, vp)) {
             const uint32_t t0 = p.nt;
             emit_diff<K>(p, v_old, vp, dlo, dhi, true);
             if (p.err) break;

@@ -16,7 +16,7 @@ def main():
     for a in args:
         name, _, copies = a.partition("x")
         copies = int(copies or 1)
-        b = dt_amd.Batch(docs=[G.dt_bytes(name)] * copies)
+        b = dt_amd.Batch(docs=[G.dt_bytes(name)] * copies, staging="device")
         ms = b.run_timed()
         idx = range(0, copies, max(1, copies // 16))
         sts = [b.doc_stats(i) for i in idx]
@@ -40,7 +40,7 @@ def plan_profile(names):
     for a in names:
         name, _, copies = a.partition("x")
         copies = int(copies or 1)
-        b = dt_amd.Batch(docs=[G.dt_bytes(name)] * copies)
+        b = dt_amd.Batch(docs=[G.dt_bytes(name)] * copies, staging="device")
         b.run_timed()
         ms = b.last_times()
         pr = [b.plan_profile(i) for i in range(0, copies, max(1, copies // 16))]
