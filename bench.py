@@ -176,8 +176,11 @@ def main():
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        # rehearsal of the N-rank path on a 1-GPU box: every rank on GPU 0, collectives over gloo
+        shared = os.environ.get("DTGPU_BENCH_SHARED_GPU") == "1"
+        gpu = 0 if shared else local_rank
+        torch.cuda.set_device(gpu)
+        dist.init_process_group("gloo" if shared else "nccl")
 
     import dt_amd
     from dt_amd.shard import doc_cost, gather_results, lpt_assign, max_over_ranks
@@ -187,11 +190,12 @@ def main():
     # LPT gives every rank its shard
     mine = lpt_assign([doc_cost(pool[g % len(pool)]) for g in range(n_total)], world)[rank]
     docs = [bytes(pool[g % len(pool)]) for g in mine]
-    dev = f"cuda:{local_rank}" if dist is not None else None
+    gpu = 0 if (dist is None or os.environ.get("DTGPU_BENCH_SHARED_GPU") == "1") else local_rank
+    dev = (None if os.environ.get("DTGPU_BENCH_SHARED_GPU") == "1" else f"cuda:{local_rank}") if dist is not None else None
 
     t0 = time.perf_counter()
     staging = "host" if args.host_staging else "device"
-    batch = dt_amd.Batch(docs=docs, device=local_rank if world > 1 else 0, staging=staging)
+    batch = dt_amd.Batch(docs=docs, device=gpu, staging=staging)
     host_stage_s = time.perf_counter() - t0
 
     for _ in range(args.warmup):
