@@ -690,6 +690,31 @@ size_t dtgpu_oplog_local_frontier(const dtgpu_oplog *h, uint64_t *out, size_t ca
     return h->o.version.size();
 }
 
+// Graph::find_dominators_2 (src/causalgraph/graph/tools.rs:545-578): the frontier of the union
+// of two versions -- the members not in the history of another member, ascending.
+int64_t dtgpu_oplog_dominators(const dtgpu_oplog *h, const uint64_t *a, size_t na, const uint64_t *b, size_t nb,
+                               uint64_t *out, size_t cap) {
+    if (!h || (na && !a) || (nb && !b)) return -1;
+    std::vector<uint64_t> u(a, a + na);
+    u.insert(u.end(), b, b + nb);
+    for (uint64_t v : u) if (v >= h->o.n_lv) return -1;
+    std::sort(u.begin(), u.end());
+    u.erase(std::unique(u.begin(), u.end()), u.end());
+    std::vector<uint64_t> dom;
+    std::vector<std::pair<uint64_t, uint64_t>> only_a, only_b;
+    for (uint64_t v : u) {
+        bool dominated = false;
+        for (uint64_t w : u) {
+            if (w <= v) continue;   // a version is only in the history of later LVs
+            h->o.graph.diff_rev({v}, {w}, only_a, only_b);
+            if (only_a.empty()) { dominated = true; break; }
+        }
+        if (!dominated) dom.push_back(v);
+    }
+    for (size_t i = 0; i < dom.size() && i < cap; i++) out[i] = dom[i];
+    return int64_t(dom.size());
+}
+
 dtgpu_status dtgpu_oplog_plan_stats(const dtgpu_oplog *h, uint64_t out[4]) {
     if (!h || !out) return DTGPU_ERR_ARG;
     Prepared p;
@@ -1012,6 +1037,109 @@ dtgpu_status dtgpu_batch_checkout(const uint8_t *const *docs, const size_t *lens
     if (!s) s = dtgpu_batch_results(B, results);
     dtgpu_batch_free(B);
     return s;
+}
+
+// ListOpLog::checkout(&[LV]) (src/list/oplog.rs:32-36) is a merge from ROOT over the history of
+// `version`.  That history is closed under parents, so it is an oplog of its own: its LVs are
+// compacted in order (agents, seqs and op positions unchanged -- every op's position is relative
+// to its parents' version, which lies inside the history) and its tip checkout is the checkout
+// at `version`.  The sub-oplog is built here and checked out by the same device path.
+static Status history_oplog(const HostOpLog &o, const std::vector<uint64_t> &version, HostOpLog &s) {
+    for (uint64_t v : version) if (v >= o.n_lv) return ErrCheckout;
+    std::vector<std::pair<uint64_t, uint64_t>> hist, none;
+    o.graph.diff_rev(version, {}, hist, none);   // Hist(version), newest first
+    std::reverse(hist.begin(), hist.end());
+    std::vector<uint64_t> base(hist.size());      // new LV of each range's start
+    uint64_t nn = 0;
+    for (size_t i = 0; i < hist.size(); i++) { base[i] = nn; nn += hist[i].second - hist[i].first; }
+    auto map = [&](uint64_t lv) -> uint64_t {      // old LV (inside the history) -> new LV
+        size_t i = size_t(std::upper_bound(hist.begin(), hist.end(), lv,
+                                           [](uint64_t v, const std::pair<uint64_t, uint64_t> &r) { return v < r.second; }) -
+                          hist.begin());
+        return base[i] + (lv - hist[i].first);
+    };
+    s = HostOpLog();
+    s.agent_names = o.agent_names;
+    s.agent_seqs.assign(o.agent_names.size(), {});
+    size_t oi = 0, ai = 0, ei = 0;
+    for (const auto &r : hist) {
+        // agent assignment
+        while (ai < o.agent_runs.size() && o.agent_runs[ai].lv + o.agent_runs[ai].len <= r.first) ai++;
+        for (size_t k = ai; k < o.agent_runs.size() && o.agent_runs[k].lv < r.second; k++) {
+            const AgentRun &a = o.agent_runs[k];
+            const uint64_t x = std::max(a.lv, r.first), y = std::min(a.lv + a.len, r.second);
+            if (x < y) s.assign(a.agent, a.seq + (x - a.lv), map(x), y - x);
+        }
+        // op runs, clipped (rev delete runs delete right to left: op_metrics.rs:184-202)
+        while (oi < o.ops.size() && o.ops[oi].lv + o.ops[oi].len <= r.first) oi++;
+        for (size_t k = oi; k < o.ops.size() && o.ops[k].lv < r.second; k++) {
+            const OpRun &op = o.ops[k];
+            const uint64_t x = std::max(op.lv, r.first), y = std::min(op.lv + op.len, r.second);
+            if (x >= y) continue;
+            if (op.kind == 0) {
+                for (uint64_t u = x; u < y;) {   // pieces of uniform ContentIsKnown
+                    const bool known = o.ins_cbyte[u] != ~0u;
+                    uint64_t w = u + 1;
+                    while (w < y && (o.ins_cbyte[w] != ~0u) == known) w++;
+                    size_t b0 = 0, b1 = 0;
+                    if (known) {
+                        b0 = o.ins_cbyte[u];
+                        b1 = o.ins_cbyte[w - 1] + utf8_len(o.ins_content[o.ins_cbyte[w - 1]]);
+                    }
+                    s.push_ins(op.pos + (u - op.lv), known ? o.ins_content.data() + b0 : nullptr, b1 - b0, w - u, known);
+                    u = w;
+                }
+            } else if (op.fwd) {
+                s.push_del(op.pos, y - x, true);
+            } else {
+                s.push_del(op.pos + (op.lv + op.len - y), y - x, false);
+            }
+        }
+        // graph entries, clipped: a piece that starts inside an entry continues its previous LV
+        while (ei < o.graph.entries.size() && o.graph.entries[ei].end <= r.first) ei++;
+        for (size_t k = ei; k < o.graph.entries.size() && o.graph.entries[k].start < r.second; k++) {
+            const GraphEntry &e = o.graph.entries[k];
+            const uint64_t x = std::max(e.start, r.first), y = std::min(e.end, r.second);
+            if (x >= y) continue;
+            std::vector<uint64_t> par;
+            if (x == e.start) for (uint64_t p : e.parents) par.push_back(map(p));
+            else par.push_back(map(x - 1));
+            std::sort(par.begin(), par.end());
+            s.graph.push(par, map(x), map(y - 1) + 1);
+        }
+    }
+    for (uint64_t v : version) s.version.push_back(map(v));
+    std::sort(s.version.begin(), s.version.end());
+    s.version.erase(std::unique(s.version.begin(), s.version.end()), s.version.end());
+    if (s.n_lv != nn) return ErrCheckout;
+    s.finish();
+    return OK;
+}
+
+dtgpu_status dtgpu_oplog_history(const dtgpu_oplog *h, const uint64_t *version, size_t n_version, dtgpu_oplog **out) {
+    if (!h || !out || (n_version && !version)) return DTGPU_ERR_ARG;
+    *out = nullptr;
+    std::vector<uint64_t> v(n_version + 1);
+    const int64_t nv = dtgpu_oplog_dominators(h, version, n_version, nullptr, 0, v.data(), v.size());
+    if (nv < 0) return DTGPU_ERR_ARG;
+    v.resize(size_t(nv));
+    auto *sub = new dtgpu_oplog;
+    const Status st = history_oplog(h->o, v, sub->o);
+    if (st != OK) { delete sub; return dtgpu_status(st); }
+    *out = sub;
+    return DTGPU_OK;
+}
+dtgpu_status dtgpu_checkout(const dtgpu_oplog *h, const uint64_t *version, size_t n_version, uint8_t *out, size_t cap,
+                            size_t *out_len) {
+    if (!h || (n_version && !version)) return DTGPU_ERR_ARG;
+    std::vector<uint64_t> v(n_version + 1);   // reduce to a frontier (Frontier::from_unsorted)
+    const int64_t nv = dtgpu_oplog_dominators(h, version, n_version, nullptr, 0, v.data(), v.size());
+    if (nv < 0) return DTGPU_ERR_CHECKOUT;
+    v.resize(size_t(nv));
+    dtgpu_oplog sub;
+    const Status st = history_oplog(h->o, v, sub.o);
+    if (st != OK) return dtgpu_status(st);
+    return dtgpu_checkout_tip(&sub, out, cap, out_len);
 }
 
 dtgpu_status dtgpu_checkout_tip(const dtgpu_oplog *h, uint8_t *out, size_t cap, size_t *out_len) {

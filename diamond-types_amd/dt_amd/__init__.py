@@ -103,6 +103,10 @@ def lib():
     L.dtgpu_oplog_agent_runs.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32), sz]
     L.dtgpu_oplog_agent_runs.restype = sz
     L.dtgpu_checkout_tip.argtypes = [vp, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
+    L.dtgpu_checkout.argtypes = [vp, pu64, sz, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
+    L.dtgpu_oplog_dominators.argtypes = [vp, pu64, sz, pu64, sz, pu64, sz]
+    L.dtgpu_oplog_dominators.restype = ctypes.c_int64
+    L.dtgpu_oplog_history.argtypes = [vp, pu64, sz, ctypes.POINTER(vp)]
     L.dtgpu_batch_create.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz), sz,
                                      ctypes.POINTER(BatchOpts), ctypes.POINTER(vp)]
     L.dtgpu_batch_create_from_oplogs.argtypes = [ctypes.POINTER(vp), sz, ctypes.POINTER(BatchOpts), ctypes.POINTER(vp)]
@@ -172,9 +176,37 @@ def text_hash(data: bytes) -> int:
 class ListBranch:
     """Result of a checkout: `ListBranch` (src/list/mod.rs:65-76) content + version."""
 
-    def __init__(self, content: bytes, version):
+    def __init__(self, content: bytes = b"", version=()):
         self._content = content
         self.version = list(version)
+
+    @classmethod
+    def new(cls) -> "ListBranch":
+        """ListBranch::new() (src/list/branch.rs:12-20): empty content at ROOT."""
+        return cls()
+
+    @classmethod
+    def new_at_local_version(cls, oplog: "ListOpLog", version) -> "ListBranch":
+        """ListBranch::new_at_local_version (src/list/branch.rs:22-26) = oplog.checkout(version)."""
+        return oplog.checkout(version)
+
+    @classmethod
+    def new_at_tip(cls, oplog: "ListOpLog") -> "ListBranch":
+        """ListBranch::new_at_tip (src/list/branch.rs:30-32)."""
+        return oplog.checkout_tip()
+
+    def merge(self, oplog: "ListOpLog", merge_frontier) -> None:
+        """ListBranch::merge(&mut self, oplog, merge_frontier) (src/list/merge.rs:63-95).
+
+        The branch ends at find_dominators_2(self.version, merge_frontier) with the text of that
+        version.  A branch's content always equals the oplog's checkout at its version (every
+        edit goes through the oplog), so the merged text is the device checkout at the new
+        version (dtgpu_checkout) rather than the reference's incremental transformed-op replay;
+        the result is the same text and frontier."""
+        v = oplog.dominators(self.version, merge_frontier)
+        if v != self.version:
+            self._content = oplog.checkout_bytes(v)
+            self.version = v
 
     def content(self) -> str:
         return self._content.decode("utf-8")
@@ -294,6 +326,37 @@ class ListOpLog:
 
     def checkout_tip(self) -> ListBranch:
         return ListBranch(self.checkout_tip_bytes(), self.local_frontier())
+
+    def dominators(self, a, b=()):
+        """Graph::find_dominators_2 (src/causalgraph/graph/tools.rs:545-578) over this oplog."""
+        pa, na = _u64s(a)
+        pb, nb = _u64s(b)
+        cap = na + nb + 1
+        out = (ctypes.c_uint64 * cap)()
+        n = lib().dtgpu_oplog_dominators(self._h, pa, na, pb, nb, out, cap)
+        if n < 0:
+            raise ValueError("version names an LV outside the oplog")
+        return list(out[:n])
+
+    def checkout_bytes(self, version) -> bytes:
+        p, nv = _u64s(version)
+        n = ctypes.c_size_t()
+        _check(lib().dtgpu_checkout(self._h, p, nv, None, 0, ctypes.byref(n)))
+        buf = ctypes.create_string_buffer(max(1, n.value))
+        _check(lib().dtgpu_checkout(self._h, p, nv, buf, n.value, ctypes.byref(n)))
+        return buf.raw[:n.value]
+
+    def history(self, version) -> "ListOpLog":
+        """The history of `version` as its own oplog (dtgpu_oplog_history)."""
+        p, nv = _u64s(version)
+        out = ctypes.c_void_p()
+        _check(lib().dtgpu_oplog_history(self._h, p, nv, ctypes.byref(out)))
+        return ListOpLog(out.value)
+
+    def checkout(self, version) -> ListBranch:
+        """ListOpLog::checkout(&[LV]) (src/list/oplog.rs:32-36): the branch at `version`."""
+        v = self.dominators(version)
+        return ListBranch(self.checkout_bytes(v), v)
 
 
 # dtgpu_export codes (include/dtgpu.h): name -> (code, numpy dtype, fields per record)

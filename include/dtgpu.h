@@ -84,6 +84,13 @@ size_t dtgpu_oplog_len(const dtgpu_oplog *oplog);
  * writes min(len, cap) LVs. */
 size_t dtgpu_oplog_local_frontier(const dtgpu_oplog *oplog, uint64_t *out, size_t cap);
 
+/* Graph::find_dominators_2 (src/causalgraph/graph/tools.rs:545-578): the frontier of the union
+ * of versions a and b (ascending LVs), the version ListBranch::merge ends at
+ * (src/list/merge.rs:63-95, iter.into_frontier()).  Returns its length (writes min(len, cap)),
+ * or -1 on an LV outside the oplog. */
+int64_t dtgpu_oplog_dominators(const dtgpu_oplog *oplog, const uint64_t *a, size_t na, const uint64_t *b,
+                               size_t nb, uint64_t *out, size_t cap);
+
 /* Host-side walk plan of checkout_tip for this oplog (SpanningTreeWalker over all LVs,
  * src/listmerge/txn_trace.rs:114-333): out[0] walk steps, out[1] retreated LVs, out[2]
  * advanced LVs, out[3] device commands.  Pure host code; usable without a GPU. */
@@ -110,7 +117,17 @@ size_t dtgpu_oplog_agent_runs(const dtgpu_oplog *oplog, uint32_t *out, size_t ca
  * (src/list/oplog.rs:38-42, src/list/merge.rs:63-95, src/list/branch.rs:38-63).
  * Runs on the GPU.  out == NULL (or cap too small) returns the required length in *out_len
  * (with DTGPU_ERR_ARG when a non-NULL buffer was too small). */
+/* ListOpLog::checkout(&[LV]) (src/list/oplog.rs:32-36): the text at `version` (any frontier of
+ * the oplog; an empty version is ROOT).  Same buffer protocol as dtgpu_checkout_tip. */
+dtgpu_status dtgpu_checkout(const dtgpu_oplog *oplog, const uint64_t *version, size_t n_version, uint8_t *out,
+                            size_t cap, size_t *out_len);
 dtgpu_status dtgpu_checkout_tip(const dtgpu_oplog *oplog, uint8_t *out, size_t cap, size_t *out_len);
+/* The history of `version` as an oplog of its own (what ListOpLog::checkout(&[LV]) replays:
+ * diff_rev(version, ROOT), src/causalgraph/graph/tools.rs:176-292), LVs compacted in order,
+ * agents / seqs / positions unchanged; its tip checkout is the checkout at `version`. */
+dtgpu_status dtgpu_oplog_history(const dtgpu_oplog *oplog, const uint64_t *version, size_t n_version,
+                                 dtgpu_oplog **out);
+
 
 /* ---- batch checkout (SURVEY.md §8b "batch entry") ------------------------------------------ */
 

@@ -54,6 +54,8 @@ def lib():
         L.dto_ins_content_len.restype = i64
         L.dto_checkout_tip.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
                                        ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(Stats)]
+        L.dto_checkout.argtypes = [ctypes.c_void_p, P64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
+                                   ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(Stats)]
         L.dto_free_buf.argtypes = [ctypes.c_void_p]
         L.dto_crc32c.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
         L.dto_crc32c.restype = ctypes.c_uint32
@@ -141,6 +143,19 @@ class OpLog:
         lib().dto_free_buf(out)
         if with_stats:
             return data, {k: getattr(st, k) for k, _ in Stats._fields_}
+        return data
+
+    def checkout_bytes(self, version, order=0) -> bytes:
+        """ListOpLog::checkout(&[LV]) (src/list/oplog.rs:32-36) restated: walk Hist(version)."""
+        v = (ctypes.c_int64 * max(1, len(version)))(*version)
+        out = ctypes.c_void_p()
+        ln = ctypes.c_size_t()
+        st = Stats()
+        e = lib().dto_checkout(self.h, v, len(version), order, ctypes.byref(out), ctypes.byref(ln), ctypes.byref(st))
+        if e:
+            raise OracleError(e)
+        data = ctypes.string_at(out.value, ln.value) if ln.value else b""
+        lib().dto_free_buf(out)
         return data
 
     def checkout_tip(self, order=0) -> str:
