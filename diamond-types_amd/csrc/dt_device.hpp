@@ -57,6 +57,11 @@ struct BatchParams {
     uint32_t *fb_count;
     uint32_t debug;         // DTGPU_DEBUG: bit 0 invariant checks, bit 1 cycle profile
     DocResult *results;
+    // transformed-ops mode only (launch_replay_xf): never-deleted masks per block, never-deleted
+    // totals per top position (blk_off + 2 * doc), transformed position per LV
+    unsigned long long *mup;
+    uint32_t *tup;
+    uint32_t *xf;
 };
 
 // Superblock capacity for an index of `mb` blocks: every superblock but the first holds >= 32
@@ -110,5 +115,7 @@ int launch_plan(const PlanParams &q, void *stream);
 
 // Launch both tiers on `stream` (hipStream_t).  small/large lists index docs[].
 int launch_replay(const BatchParams &small, const BatchParams &large, void *stream, int n_cu);
+// Transformed-ops replay of large's documents (HBM index tier): BaseMoved positions per LV.
+int launch_replay_xf(const BatchParams &large, void *stream);
 
 }  // namespace dtgpu

@@ -697,7 +697,15 @@ Status decode_dt(const uint8_t *data, size_t len, bool ignore_crc, HostOpLog &o)
 // ------------------------------------------------------------------------------------------
 // walk plan (src/listmerge/txn_trace.rs:114-333 + merge.rs:564-581)
 // ------------------------------------------------------------------------------------------
-Status build_plan(const HostOpLog &o, Plan &plan) {
+Status build_plan(const HostOpLog &o, Plan &plan) { return build_plan_from(o, plan, false); }
+Status build_xf_plan(const HostOpLog &o, Plan &plan) { return build_plan_from(o, plan, true); }
+
+// xf == false: SpanningTreeWalker over every graph entry from ROOT.  xf == true: the order
+// TransformedOpsIter applies ops in (src/listmerge/merge.rs:788-940) -- fast-forward through the
+// leading entries whose parents are the current frontier, then a SpanningTreeWalker over the
+// remaining entries starting at that frontier (parents outside the input are ignored,
+// txn_trace.rs:140-148).
+Status build_plan_from(const HostOpLog &o, Plan &plan, bool xf) {
     plan.cmds.clear();
     plan.tlist.clear();
     plan.agent_runs.clear();
@@ -721,13 +729,21 @@ Status build_plan(const HostOpLog &o, Plan &plan) {
     // VisitEntry table: parent / child indexes inside the (whole-graph) input
     std::vector<std::vector<uint32_t>> pidx(ne), cidx(ne);
     std::vector<uint32_t> todo;
-    for (size_t i = 0; i < ne; i++) {
-        for (uint64_t p : E[i].parents) pidx[i].push_back(uint32_t(o.graph.find_idx(p)));
+    std::vector<uint64_t> frontier;
+    size_t first = 0;   // entries before `first` were fast-forwarded
+    if (xf)
+        while (first < ne && E[first].parents == frontier) frontier.assign(1, E[first++].end - 1);
+    for (size_t i = first; i < ne; i++) {
+        for (uint64_t p : E[i].parents) {
+            const int64_t pe = o.graph.find_idx(p);
+            if (pe >= int64_t(first)) pidx[i].push_back(uint32_t(pe));
+        }
         if (pidx[i].empty()) todo.push_back(uint32_t(i));
     }
     for (size_t i = 0; i < ne; i++) for (uint32_t p : pidx[i]) cidx[p].push_back(uint32_t(i));
     std::reverse(todo.begin(), todo.end());
     std::vector<uint8_t> visited(ne, 0);
+    for (size_t i = 0; i < first; i++) visited[i] = 1;
 
     // op-run lookup
     const auto &ops = o.ops;
@@ -766,7 +782,7 @@ Status build_plan(const HostOpLog &o, Plan &plan) {
         }
     };
 
-    std::vector<uint64_t> frontier;
+    for (size_t i = 0; i < first; i++) emit_apply(E[i].start, E[i].end);
     std::vector<std::pair<uint64_t, uint64_t>> only_a, only_b;
     while (!todo.empty()) {
         uint32_t idx = todo.back();

@@ -96,6 +96,10 @@ struct Plan {
 // SpanningTreeWalker over the whole graph from ROOT (src/listmerge/txn_trace.rs:114-333) turned
 // into the device command stream (retreat / advance / apply, src/listmerge/merge.rs:564-581).
 Status build_plan(const HostOpLog &o, Plan &plan);
+// The order TransformedOpsIter applies ops in for iter_xf_operations (src/list/merge.rs:24-48;
+// src/listmerge/merge.rs:788-940): the fast-forward prefix, then the walker from its frontier.
+Status build_xf_plan(const HostOpLog &o, Plan &plan);
+Status build_plan_from(const HostOpLog &o, Plan &plan, bool xf);
 
 // The decoded oplog as flat arrays for the device planner (dt_plan.hip): the same information
 // the reference's ListOpLog holds (Graph entries with parents and child indexes, the agent

@@ -104,9 +104,11 @@ constexpr uint32_t END_ID = 0xFFFFFFFEu;
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 // packed per-block counts
 constexpr uint32_t C_VIS = 1u, C_LIVE = 1u << 8, C_ITEMS = 1u << 16;
+constexpr uint32_t C_UP = 1u << 24;   // transformed-ops mode: items never deleted
 DEV uint32_t c_vis(uint32_t c) { return c & 0xFFu; }
 DEV uint32_t c_live(uint32_t c) { return (c >> 8) & 0xFFu; }
 DEV uint32_t c_items(uint32_t c) { return (c >> 16) & 0xFFu; }
+DEV uint32_t c_up(uint32_t c) { return c >> 24; }
 
 DEV uint32_t pos_blk(uint32_t w) { return w >> 6; }
 DEV uint32_t pos_slot(uint32_t w) { return w & 63u; }
@@ -168,6 +170,11 @@ struct Doc {
     // same state (every change is stored); a toggle touching the block drops it.
     uint32_t cb, cit;
     u64 cmv, cml;
+    // transformed-ops mode (iter_xf_operations): per block the never-deleted mask, per top
+    // position the never-deleted total, per LV the transformed position written out
+    u64 *mup;
+    uint32_t *tup;
+    uint32_t *xf;
 };
 
 DEV void fail(Doc &D, uint32_t code, uint32_t site) {
@@ -286,17 +293,18 @@ DEV uint32_t next_live_block(Doc &D, uint32_t b) {
 
 // Split the full superblock S (64 blocks): its upper half becomes a new superblock right after
 // it in the top order.
-template <bool L>
+template <bool L, bool XF>
 DEV void split_sb(Doc &D, uint32_t S) {
     const uint32_t l = lane_id();
     if (D.nsb >= D.max_sb) { fail(D, ErrCapacity, 21); return; }
     const uint32_t S2 = D.nsb;
-    uint32_t vis = 0, live = 0;
+    uint32_t vis = 0, live = 0, up = 0;
     {
         const uint32_t b = ix16<L>(D.sbl + size_t(S) * SBC + l);
         const uint32_t c = ix<L>(D.cnt + b);
         vis = c_vis(c);
         live = c_live(c);
+        up = c_up(c);
         wave_fence();
         if (l >= SBC / 2) {
             D.sbl[size_t(S2) * SBC + (l - SBC / 2)] = uint16_t(b);
@@ -305,14 +313,18 @@ DEV void split_sb(Doc &D, uint32_t S) {
     }
     const uint32_t vh = wave_sum(l >= 32 ? vis : 0), lh = wave_sum(l >= 32 ? live : 0);
     const uint32_t vl = wave_sum(l < 32 ? vis : 0), ll = wave_sum(l < 32 ? live : 0);
+    const uint32_t uh = XF ? wave_sum(l >= 32 ? up : 0) : 0, ul = XF ? wave_sum(l < 32 ? up : 0) : 0;
     const uint32_t p = U(ix<L>(D.sbpos + S)) + 1;
     // shift top[p .. nsb) / tlive right by one, highest chunk first
     for (int c = int(D.nsb) - 1; c >= int(p); c -= 64) {
         const int i = c - int(l);
-        uint32_t w = 0, lv = 0;
-        if (i >= int(p)) { w = ix<L>(D.top + i); lv = ix<L>(D.tlive + i); }
+        uint32_t w = 0, lv = 0, uv = 0;
+        if (i >= int(p)) { w = ix<L>(D.top + i); lv = ix<L>(D.tlive + i); if (XF) uv = ix<L>(D.tup + i); }
         wave_fence();
-        if (i >= int(p)) { D.top[i + 1] = w; D.tlive[i + 1] = lv; D.sbpos[w >> 16] = uint32_t(i + 1); }
+        if (i >= int(p)) {
+            D.top[i + 1] = w; D.tlive[i + 1] = lv; D.sbpos[w >> 16] = uint32_t(i + 1);
+            if (XF) D.tup[i + 1] = uv;
+        }
         wave_fence();
     }
     if (l == 0) {
@@ -321,6 +333,7 @@ DEV void split_sb(Doc &D, uint32_t S) {
         D.top[p - 1] = (S << 16) | vl; D.tlive[p - 1] = ll;
         D.top[p] = (S2 << 16) | vh; D.tlive[p] = lh;
         D.sbpos[S2] = p;
+        if (XF) { D.tup[p - 1] = ul; D.tup[p] = uh; }
     }
     wave_fence();
     D.nsb++;
@@ -328,11 +341,17 @@ DEV void split_sb(Doc &D, uint32_t S) {
 
 // Split the full block b (items in `it` lane by lane, masks mv / ml) at slot c: items [c, 64)
 // move to a new block b2 placed right after b in its superblock.
-template <bool L>
+template <bool L, bool XF>
 DEV uint32_t split_block(Doc &D, uint32_t b, uint32_t c, uint32_t it, u64 mv, u64 ml) {
     const uint32_t l = lane_id();
     if (D.nb >= D.max_blocks) { fail(D, ErrCapacity, 12); return 0; }
     const uint32_t b2 = D.nb;
+    u64 mu = 0, mu_lo = 0, mu_hi = 0;
+    if (XF) {
+        mu = U64(ld_sc(D.mup + b));
+        mu_lo = mu & lanes_below(c);
+        mu_hi = c >= 64 ? 0ull : mu >> c;
+    }
     if (l >= c) {
         D.items[size_t(b2) * BLK + (l - c)] = it;
         D.pos[it] = pos_of(b2, l - c);
@@ -356,15 +375,18 @@ DEV uint32_t split_block(Doc &D, uint32_t b, uint32_t c, uint32_t it, u64 mv, u6
         }
     }
     if (l == 0) {
-        D.cnt[b2] = uint32_t(__popcll(mv_hi)) * C_VIS + uint32_t(__popcll(ml_hi)) * C_LIVE + (BLK - c) * C_ITEMS;
-        D.cnt[b] = uint32_t(__popcll(mv & lo)) * C_VIS + uint32_t(__popcll(ml & lo)) * C_LIVE + c * C_ITEMS;
+        D.cnt[b2] = uint32_t(__popcll(mv_hi)) * C_VIS + uint32_t(__popcll(ml_hi)) * C_LIVE + (BLK - c) * C_ITEMS +
+                    uint32_t(__popcll(mu_hi)) * C_UP;
+        D.cnt[b] = uint32_t(__popcll(mv & lo)) * C_VIS + uint32_t(__popcll(ml & lo)) * C_LIVE + c * C_ITEMS +
+                   uint32_t(__popcll(mu_lo)) * C_UP;
+        if (XF) { st_sc(D.mup + b, mu_lo); st_sc(D.mup + b2, mu_hi); }
         D.sbl[size_t(S) * SBC + i + 1] = uint16_t(b2);
         D.opos[b2] = (S << 6) | (i + 1);
         D.sbn[S] = n + 1;
     }
     wave_fence();
     D.nb++;
-    if (n + 1 == SBC) split_sb<L>(D, S);
+    if (n + 1 == SBC) split_sb<L, XF>(D, S);
     return b2;
 }
 
@@ -377,14 +399,34 @@ DEV uint32_t split_block(Doc &D, uint32_t b, uint32_t c, uint32_t it, u64 mv, u6
 // n_ins / 32 + 2 blocks suffice.
 template <bool L> DEV uint32_t cut_point(uint32_t s) { return L ? min(max(s, 16u), 48u) : BLK / 2; }
 
+// Transformed-ops mode: the upstream position of slot s of block b -- the never-deleted items
+// before it in document order (MarkerMetrics upstream_len, metrics.rs:18-66; the position
+// integrate() / apply() report as BaseMoved, merge.rs:154-278, 457-556).
+template <bool L>
+DEV uint32_t up_rank(Doc &D, uint32_t b, uint32_t s) {
+    const uint32_t l = lane_id();
+    const uint32_t o = U(ix<L>(D.opos + b));
+    const uint32_t S = o >> 6, i = o & 63u, tp = U(ix<L>(D.sbpos + S));
+    uint32_t r = 0;
+    for (uint32_t c = 0; c < tp; c += 64) r += wave_sum(c + l < tp ? ix<L>(D.tup + c + l) : 0u);
+    const uint32_t bl = l < i ? ix16<L>(D.sbl + size_t(S) * SBC + l) : 0;
+    r += wave_sum(l < i ? c_up(ix<L>(D.cnt + bl)) : 0u);
+    r += uint32_t(__popcll(U64(ld_sc(D.mup + b)) & lanes_below(s)));
+    return U(r);
+}
+
 // Insert the run [lv, lv+k) before slot s of block b (all new items visible).  `it` holds the
 // block's items lane by lane (lanes >= the block count are don't-care); mv / ml its masks.
-template <bool L, bool PROF>
+template <bool L, bool PROF, bool XF>
 DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml, uint32_t lv, uint32_t k,
                     uint32_t ol, uint32_t orr) {
     D.cb = NONE;
     const uint32_t l = lane_id();
     const uint32_t lv0 = lv, k0 = k;
+    if (XF) {   // the run's items land at consecutive upstream positions
+        const uint32_t r0 = up_rank<L>(D, b, s);
+        for (uint32_t j = l; j < k0; j += 64) D.xf[lv0 + j] = r0 + j;
+    }
     while (k > 0) {
         if (!charge(D)) return;
         const uint32_t c = U(ix<L>(D.cnt + b));
@@ -392,7 +434,7 @@ DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml,
         if (bc == BLK) {
             const uint64_t t0 = tick<PROF>();
             const uint32_t cut = cut_point<L>(s);
-            const uint32_t b2 = split_block<L>(D, b, cut, it, mv, ml);
+            const uint32_t b2 = split_block<L, XF>(D, b, cut, it, mv, ml);
             if (D.err) return;
             if (s > cut || cut == BLK) {
                 b = b2;
@@ -425,11 +467,17 @@ DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml,
         mv = m == 64 ? ins : ((mv & low) | ((mv & ~low) << m) | ins);
         ml = m == 64 ? ins : ((ml & low) | ((ml & ~low) << m) | ins);
         if (l < 2) st_sc(D.m2 + 2 * size_t(b) + l, l == 0 ? mv : ml);
+        if (XF) {
+            u64 mu = U64(ld_sc(D.mup + b));
+            mu = m == 64 ? ins : ((mu & low) | ((mu & ~low) << m) | ins);
+            if (l == 0) st_sc(D.mup + b, mu);
+        }
         if (l == 0) {
-            D.cnt[b] = c + m * (C_VIS + C_LIVE + C_ITEMS);
+            D.cnt[b] = c + m * (C_VIS + C_LIVE + C_ITEMS + (XF ? C_UP : 0u));
             const uint32_t tp = ix<L>(D.sbpos + (ix<L>(D.opos + b) >> 6));
             D.top[tp] = ix<L>(D.top + tp) + m;
             D.tlive[tp] = ix<L>(D.tlive + tp) + m;
+            if (XF) D.tup[tp] = ix<L>(D.tup + tp) + m;
         }
         wave_fence();
         if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_R2] += t - tr; tr = t; }
@@ -552,7 +600,7 @@ DEV void load_block(const Doc &D, uint32_t b, uint32_t bc, uint32_t &it, u64 &mv
 
 // Apply an insert run at visible position pos (M2Tracker::apply Ins + integrate,
 // merge.rs:154-278, 383-455).
-template <bool L, bool PROF>
+template <bool L, bool PROF, bool XF>
 DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
     uint64_t tp = tick<PROF>();
     uint32_t b, kk = 0;
@@ -618,17 +666,18 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
         if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_YJS] += t - tp; tp = t; D.prof[P_N_YJS]++; }
     }
     const uint64_t sp0 = PROF ? D.prof[P_SPLIT] : 0;
-    insert_run<L, PROF>(D, b, s, it, mv, ml, lv, k, ol, orr);
+    insert_run<L, PROF, XF>(D, b, s, it, mv, ml, lv, k, ol, orr);
     if (PROF) D.prof[P_RUN] += tick<PROF>() - tp - (D.prof[P_SPLIT] - sp0);
     D.n_items += k;
 }
 
 // Apply a delete run: n visible items from position pos (merge.rs:457-556).  LV lv+j targets
 // the j-th item (fwd) or the (n-1-j)-th item (reversed / backspace runs, op_metrics.rs:184-202).
-template <bool L>
+template <bool L, bool XF>
 DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
     const uint32_t l = lane_id();
     uint32_t j0 = 0;
+    uint32_t up_done = 0;   // XF: never-deleted items this run deleted in earlier (left) blocks
     while (j0 < n) {
         if (!charge(D)) return;
         Found f;
@@ -645,16 +694,37 @@ DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
         const bool sel = ((mv >> l) & 1ull) && r >= kk && r < kk + take;
         const u64 selm = __ballot(sel);
         if (uint32_t(__popcll(selm)) != take || take == 0) { fail(D, ErrCheckout, 15); return; }
+        u64 mu = 0;
+        uint32_t base = 0;
+        if (XF) {
+            mu = U64(ld_sc(D.mup + b));
+            base = up_rank<L>(D, b, 0);
+        }
         if (sel) {
             const uint32_t j = j0 + (r - kk);
             const uint32_t dlv = fwd ? lv + j : lv + n - 1 - j;
             st_sc(D.cv + it, 2u);   // visible (count 1) -> deleted once
             *reinterpret_cast<uint32_t *>(D.ao + dlv) = it;
+            if (XF) {
+                // LV order applies a forward run left to right (the run's items to the left are
+                // already gone) and a backspace run right to left (the ones to the left, in
+                // this block and in earlier blocks, are still there)
+                const u64 below = lanes_below(l);
+                const uint32_t x = fwd ? base + uint32_t(__popcll(mu & ~selm & below))
+                                       : base + uint32_t(__popcll(mu & below)) + up_done;
+                D.xf[dlv] = ((mu >> l) & 1ull) ? x : NONE;   // NONE: DeleteAlreadyHappened
+            }
         }
+        const uint32_t gone = XF ? uint32_t(__popcll(mu & selm)) : 0u;   // never-deleted items deleted now
+        up_done += gone;
         if (l == 0) {
             st_sc(D.m2 + 2 * size_t(b), mv & ~selm);
-            D.cnt[b] = c - take * C_VIS;
+            D.cnt[b] = c - take * C_VIS - gone * C_UP;
             D.top[f.tp] = ix<L>(D.top + f.tp) - take;
+            if (XF) {
+                st_sc(D.mup + b, mu & ~selm);
+                D.tup[f.tp] = ix<L>(D.tup + f.tp) - gone;
+            }
         }
         wave_fence();
         D.cb = b; D.cit = it; D.cmv = mv & ~selm; D.cml = ml;
@@ -777,7 +847,7 @@ DEV void materialise(Doc &D, uint8_t *out, uint32_t cap, uint32_t &len_out, u64 
 }
 
 // Debug-mode consistency check of the whole structure (DTGPU_DEBUG=1): returns 0 or a code.
-template <bool L>
+template <bool L, bool XF>
 DEV uint32_t check_invariants(Doc &D, DocResult *res) {
     const uint32_t l = lane_id();
     uint32_t blocks = 0;
@@ -786,7 +856,7 @@ DEV uint32_t check_invariants(Doc &D, DocResult *res) {
         if (U(ix<L>(D.sbpos + S)) != p) return 205;
         const uint32_t n = U(ix<L>(D.sbn + S));
         if (n == 0 || n >= SBC) return 206;
-        uint32_t tv = 0, tl = 0;
+        uint32_t tv = 0, tl = 0, tu = 0;
         for (uint32_t i = 0; i < n; i++) {
             const uint32_t b = U(ix16<L>(D.sbl + size_t(S) * SBC + i));
             if (U(ix<L>(D.opos + b)) != ((S << 6) | i)) return 201;
@@ -794,6 +864,8 @@ DEV uint32_t check_invariants(Doc &D, DocResult *res) {
             const uint32_t cnt = c_items(c);
             const u64 mv = U64(ld_sc(D.m2 + 2 * size_t(b))), ml = U64(ld_sc(D.m2 + 2 * size_t(b) + 1));
             if (uint32_t(__popcll(mv)) != c_vis(c) || uint32_t(__popcll(ml)) != c_live(c)) return 207;
+            if (XF && uint32_t(__popcll(U64(ld_sc(D.mup + b)))) != c_up(c)) return 209;
+            if (XF) tu += c_up(c);
             tv += c_vis(c);
             tl += c_live(c);
             bool bad = false;
@@ -822,12 +894,13 @@ DEV uint32_t check_invariants(Doc &D, DocResult *res) {
         }
         if (tv != (U(ix<L>(D.top + p)) & 0xFFFFu)) return 203;
         if (tl != U(ix<L>(D.tlive + p))) return 204;
+        if (XF && tu != U(ix<L>(D.tup + p))) return 210;
     }
     if (blocks != D.nb) return 208;
     return 0;
 }
 
-template <bool L, bool PROF>
+template <bool L, bool PROF, bool XF>
 DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
     const uint32_t l = lane_id();
     // fresh tracker: one empty block in one superblock (per-LV words are written when their
@@ -835,6 +908,7 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
     if (l == 0) {
         D.cnt[0] = 0; D.opos[0] = 0;
         D.sbl[0] = 0; D.sbn[0] = 1; D.sbpos[0] = 0; D.top[0] = 0; D.tlive[0] = 0;
+        if (XF) { D.tup[0] = 0; st_sc(D.mup, 0ull); }
     }
     if (l < 2) st_sc(D.m2 + l, 0ull);
     wave_fence();
@@ -875,12 +949,12 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
             switch (op & 15u) {
                 case CMD_INS:
                     if (n == 0 || a >= D.n_lv || n > D.n_lv - a) { fail(D, ErrCheckout, 17); break; }
-                    do_insert<L, PROF>(D, a, n, pos);
+                    do_insert<L, PROF, XF>(D, a, n, pos);
                     if (PROF) D.prof[P_INS] += tick<PROF>() - t0;
                     break;
                 case CMD_DEL:
                     if (n == 0 || a >= D.n_lv || n > D.n_lv - a) { fail(D, ErrCheckout, 17); break; }
-                    do_delete<L>(D, a, n, pos, (op & 16u) != 0);
+                    do_delete<L, XF>(D, a, n, pos, (op & 16u) != 0);
                     if (PROF) D.prof[P_DEL] += tick<PROF>() - t0;
                     break;
                 case CMD_TOG:
@@ -890,7 +964,7 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
                 default: fail(D, ErrCheckout, 18); break;
             }
             if (D.debug && !D.err) {
-                const uint32_t code = check_invariants<L>(D, res);
+                const uint32_t code = check_invariants<L, XF>(D, res);
                 if (code) fail(D, ErrCheckout, code);
             }
             pf = nx_pf;
@@ -938,7 +1012,7 @@ DEV void bind_index(Doc &D, uint8_t *base, uint32_t mb, uint32_t ms) {
 
 // One 64-lane workgroup per document of the list (the hardware dispatcher is the work queue;
 // LDS per workgroup bounds how many documents share a CU).
-template <bool LDS_INDEX, bool PROF>
+template <bool LDS_INDEX, bool PROF, bool XF>
 __global__ __launch_bounds__(64) void replay_kernel(BatchParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t di = U(blockIdx.x);
@@ -980,7 +1054,12 @@ __global__ __launch_bounds__(64) void replay_kernel(BatchParams P) {
     } else {
         bind_index(D, P.gidx + dd.gidx_off, D.max_blocks, D.max_sb);
     }
-    run_doc<LDS_INDEX, PROF>(D, P.out + dd.out_off, U(dd.out_cap), &P.results[d]);
+    if (XF) {
+        D.mup = P.mup + dd.blk_off;
+        D.tup = P.tup + dd.blk_off + 2ull * d;   // sb_capacity(mb) <= mb + 2 slots per document
+        D.xf = P.xf + dd.lv_off;
+    }
+    run_doc<LDS_INDEX, PROF, XF>(D, P.out + dd.out_off, U(dd.out_cap), &P.results[d]);
 }
 
 }  // namespace dev
@@ -992,18 +1071,28 @@ int launch_replay(const BatchParams &small, const BatchParams &large, void *stre
         if (small.fb_count && hipMemsetAsync(small.fb_count, 0, sizeof(uint32_t), s) != hipSuccess) return ErrHip;
         size_t lds = size_t(index_bytes(small.lds_blocks));
         if (const char *pad = getenv("DTGPU_LDS_PAD")) lds += size_t(strtoul(pad, nullptr, 10));   // occupancy experiments
-        if (prof) hipLaunchKernelGGL((dev::replay_kernel<true, true>), dim3(small.n_list), dim3(64), lds, s, small);
-        else hipLaunchKernelGGL((dev::replay_kernel<true, false>), dim3(small.n_list), dim3(64), lds, s, small);
+        if (prof) hipLaunchKernelGGL((dev::replay_kernel<true, true, false>), dim3(small.n_list), dim3(64), lds, s, small);
+        else hipLaunchKernelGGL((dev::replay_kernel<true, false, false>), dim3(small.n_list), dim3(64), lds, s, small);
         if (hipGetLastError() != hipSuccess) return ErrHip;
     }
     // HBM tier: its own list plus a slot per LDS-tier document that may be handed back
     const uint32_t grid = large.n_list + (small.fb_list ? small.n_list : 0);
     if (grid) {
-        if (prof) hipLaunchKernelGGL((dev::replay_kernel<false, true>), dim3(grid), dim3(64), 0, s, large);
-        else hipLaunchKernelGGL((dev::replay_kernel<false, false>), dim3(grid), dim3(64), 0, s, large);
+        if (prof) hipLaunchKernelGGL((dev::replay_kernel<false, true, false>), dim3(grid), dim3(64), 0, s, large);
+        else hipLaunchKernelGGL((dev::replay_kernel<false, false, false>), dim3(grid), dim3(64), 0, s, large);
         if (hipGetLastError() != hipSuccess) return ErrHip;
     }
     return OK;
+}
+
+// Transformed-ops replay (iter_xf_operations): HBM-tier index, one workgroup per document of
+// `large`, per-LV transformed positions into large.xf.
+int launch_replay_xf(const BatchParams &large, void *stream) {
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (!large.n_list) return OK;
+    if (!large.xf || !large.mup || !large.tup) return ErrArg;
+    hipLaunchKernelGGL((dev::replay_kernel<false, false, true>), dim3(large.n_list), dim3(64), 0, s, large);
+    return hipGetLastError() == hipSuccess ? OK : ErrHip;
 }
 
 }  // namespace dtgpu

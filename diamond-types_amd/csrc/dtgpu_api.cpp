@@ -58,7 +58,8 @@ struct dtgpu_batch {
 
     DevBuf<Cmd> d_cmds;
     DevBuf<uint32_t> d_tlist, d_cbyte, d_aruns, d_pos, d_cv, d_items, d_lists, d_counter;
-    DevBuf<unsigned long long> d_ao, d_m2;
+    DevBuf<unsigned long long> d_ao, d_m2, d_mup;
+    DevBuf<uint32_t> d_tup, d_xf;   // transformed-ops batches only
     DevBuf<uint8_t> d_content, d_out, d_gidx;
     DevBuf<uint32_t> d_fb;   // [0] = count, then the handed-back documents
     DevBuf<DocDesc> d_docs;
@@ -125,7 +126,10 @@ void parallel_for(size_t n, int threads, F f) {
 template <typename T>
 void append(std::vector<T> &dst, const std::vector<T> &src) { dst.insert(dst.end(), src.begin(), src.end()); }
 
-dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dtgpu_batch **out) {
+// xf: a transformed-ops batch (iter_xf_operations): host plans in TransformedOpsIter order
+// (build_xf_plan), every document on the HBM-index tier, never-deleted masks / totals and the
+// per-LV transformed-position arena allocated.
+dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dtgpu_batch **out, bool xf = false) {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return DTGPU_ERR_NO_DEVICE;
     auto B = std::make_unique<dtgpu_batch>();
@@ -147,7 +151,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     B->n_lv.resize(n);
     B->docs.resize(n);
     B->host_planned.assign(n, 0);
-    const bool force_host = getenv("DTGPU_HOST_PLAN") != nullptr;
+    const bool force_host = xf || getenv("DTGPU_HOST_PLAN") != nullptr;
 
     // ---- 1. device planner inputs; a sizing pass of the planner gives exact stream sizes ----
     std::vector<PlanDesc> pdesc(n);
@@ -226,7 +230,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     }
     parallel_for(n, threads, [&](size_t i) {
         Prepared &p = prep[i];
-        if (p.status == OK && p.host_plan) p.status = build_plan(p.log, p.plan);
+        if (p.status == OK && p.host_plan) p.status = xf ? build_xf_plan(p.log, p.plan) : build_plan(p.log, p.plan);
     });
 
     // ---- 2. per-document layout ---------------------------------------------------------------
@@ -301,7 +305,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         d.gidx_off = gidx_total;
         gidx_total += index_bytes(d.max_blocks);
         const uint32_t est = uint32_t(std::min<uint64_t>(d.max_blocks, n_ins / lds_fill + 8));
-        if (index_bytes(est) <= kLdsIndexBudget) {
+        if (!xf && index_bytes(est) <= kLdsIndexBudget) {
             B->small_list.push_back(uint32_t(i));
             B->lds_blocks = std::max(B->lds_blocks, est);
         } else {
@@ -355,9 +359,17 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     CK(B->d_counter.alloc(2));
     CK(B->d_results.alloc(n));
     CK(hipMemsetAsync(B->d_results.p, 0, std::max<size_t>(n, 1) * sizeof(DocResult), s));
+    if (xf) {
+        CK(B->d_mup.alloc(blk_total));
+        CK(B->d_tup.alloc(blk_total + 2 * n));
+        CK(B->d_xf.alloc(lv_total));
+    }
     CK(hipStreamSynchronize(s));
 #undef CK
     BatchParams base{};
+    base.mup = B->d_mup.p;
+    base.tup = B->d_tup.p;
+    base.xf = B->d_xf.p;
     if (const char *dbg = getenv("DTGPU_DEBUG")) base.debug = uint32_t(atoi(dbg) ? atoi(dbg) : 1);
     base.cmds = B->d_cmds.p;
     base.tlist = B->d_tlist.p;
@@ -739,6 +751,20 @@ size_t dtgpu_oplog_plan_commands(const dtgpu_oplog *h, uint32_t *cmds, size_t ca
         cmds[4 * i + 3] = p.plan.cmds[i].pos;
     }
     return p.plan.cmds.size();
+}
+
+size_t dtgpu_oplog_xf_order(const dtgpu_oplog *h, uint32_t *out, size_t cap) {
+    if (!h) return 0;
+    HostOpLog log = h->o;
+    log.finish();
+    Plan plan;
+    if (build_xf_plan(log, plan) != OK) return 0;
+    size_t k = 0;
+    for (const Cmd &c : plan.cmds) {
+        if ((c.op & 15u) == CMD_TOG) continue;
+        for (uint32_t j = 0; j < c.len; j++, k++) if (k < cap) out[k] = c.lv + j;
+    }
+    return k;
 }
 
 size_t dtgpu_oplog_plan_tlist(const dtgpu_oplog *h, uint32_t *out, size_t cap) {
@@ -1140,6 +1166,44 @@ dtgpu_status dtgpu_checkout(const dtgpu_oplog *h, const uint64_t *version, size_
     const Status st = history_oplog(h->o, v, sub.o);
     if (st != OK) return dtgpu_status(st);
     return dtgpu_checkout_tip(&sub, out, cap, out_len);
+}
+
+dtgpu_status dtgpu_xf_operations(const dtgpu_oplog *h, uint32_t *out, size_t cap, size_t *n_out) {
+    if (!h) return DTGPU_ERR_ARG;
+    const uint64_t n_lv = h->o.n_lv;
+    if (n_out) *n_out = size_t(n_lv);
+    if (!out) return DTGPU_OK;
+    if (cap < n_lv) return DTGPU_ERR_ARG;
+    if (n_lv == 0) return DTGPU_OK;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return DTGPU_ERR_NO_DEVICE;
+    std::vector<Prepared> prep(1);
+    prep[0].log = h->o;
+    prep[0].log.finish();
+    prepare_input(prep[0]);
+    dtgpu_batch *B = nullptr;
+    dtgpu_status st = stage(prep, nullptr, &B, true);
+    if (st) return st;
+    std::unique_ptr<dtgpu_batch> hold(B);
+    if (B->host_status[0] != OK) return dtgpu_status(B->host_status[0]);
+    if (launch_replay_xf(B->large, B->stream) != OK) return DTGPU_ERR_HIP;
+    DocResult r;
+    std::vector<uint32_t> xfv(n_lv);
+    if (hipMemcpyAsync(&r, B->d_results.p, sizeof r, hipMemcpyDeviceToHost, B->stream) != hipSuccess ||
+        hipMemcpyAsync(xfv.data(), B->d_xf.p, n_lv * 4, hipMemcpyDeviceToHost, B->stream) != hipSuccess ||
+        hipStreamSynchronize(B->stream) != hipSuccess)
+        return DTGPU_ERR_HIP;
+    if (r.status != OK) return dtgpu_status(r.status);
+    // application order = the plan's INS / DEL commands in order
+    size_t k = 0;
+    for (const Cmd &c : prep[0].plan.cmds) {
+        if ((c.op & 15u) == CMD_TOG) continue;
+        for (uint32_t j = 0; j < c.len && k < n_lv; j++, k++) {
+            out[2 * k] = c.lv + j;
+            out[2 * k + 1] = xfv[c.lv + j];
+        }
+    }
+    return k == n_lv ? DTGPU_OK : DTGPU_ERR_CHECKOUT;
 }
 
 dtgpu_status dtgpu_checkout_tip(const dtgpu_oplog *h, uint8_t *out, size_t cap, size_t *out_len) {

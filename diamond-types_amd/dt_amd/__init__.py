@@ -107,6 +107,9 @@ def lib():
     L.dtgpu_oplog_dominators.argtypes = [vp, pu64, sz, pu64, sz, pu64, sz]
     L.dtgpu_oplog_dominators.restype = ctypes.c_int64
     L.dtgpu_oplog_history.argtypes = [vp, pu64, sz, ctypes.POINTER(vp)]
+    L.dtgpu_xf_operations.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32), sz, ctypes.POINTER(sz)]
+    L.dtgpu_oplog_xf_order.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32), sz]
+    L.dtgpu_oplog_xf_order.restype = sz
     L.dtgpu_batch_create.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz), sz,
                                      ctypes.POINTER(BatchOpts), ctypes.POINTER(vp)]
     L.dtgpu_batch_create_from_oplogs.argtypes = [ctypes.POINTER(vp), sz, ctypes.POINTER(BatchOpts), ctypes.POINTER(vp)]
@@ -326,6 +329,73 @@ class ListOpLog:
 
     def checkout_tip(self) -> ListBranch:
         return ListBranch(self.checkout_tip_bytes(), self.local_frontier())
+
+    def xf_order(self):
+        """LV order of iter_xf_operations (host plan: fast-forward prefix, then the walker)."""
+        n = len(self)
+        buf = (ctypes.c_uint32 * max(1, n))()
+        k = lib().dtgpu_oplog_xf_order(self._h, buf, n)
+        return list(buf[:k])
+
+    def xf_operations_lv(self):
+        """Per-LV transformed positions in application order, computed on the GPU
+        (dtgpu_xf_operations): [(lv, pos or None)], None = DeleteAlreadyHappened."""
+        n = len(self)
+        buf = (ctypes.c_uint32 * max(2, 2 * n))()
+        k = ctypes.c_size_t()
+        _check(lib().dtgpu_xf_operations(self._h, buf, n, ctypes.byref(k)))
+        return [(buf[2 * i], None if buf[2 * i + 1] == 0xFFFFFFFF else buf[2 * i + 1]) for i in range(k.value)]
+
+    def iter_xf_operations(self):
+        """ListOpLog::iter_xf_operations() (src/list/merge.rs:24-48): yields (range(lv, lv+len),
+        op) with op = ("ins", pos, text) / ("del", pos, len) / None (DeleteAlreadyHappened).
+        Consecutive LVs of one op run are merged when they form one reference-style op: an
+        insert at consecutive positions, a forward delete at one position, a backspace run at
+        descending positions (reported at its lowest position, like BaseMoved)."""
+        ops = self.export("ops").reshape(-1, 4)
+        content = self.ins_content()
+        coff = self.char_offsets()
+        run_of = {}
+        for r, (lv, ln, _pos, kf) in enumerate(ops):
+            for k in range(int(ln)):
+                run_of[int(lv) + k] = (r, int(kf) & 1)
+
+        def char(v):
+            b = coff[v]
+            n = 1 if content[b] < 0x80 else 2 if content[b] < 0xE0 else 3 if content[b] < 0xF0 else 4
+            return content[b:b + n].decode("utf-8")
+
+        cur = None   # [start_lv, end_lv, run, kind, first_pos, last_pos, text, step]
+        for lv, x in self.xf_operations_lv():
+            r, kind = run_of[lv]
+            if cur is not None and lv == cur[1] and r == cur[2]:
+                if x is None and cur[3] is None:
+                    cur[1] += 1
+                    continue
+                if x is not None and cur[3] == kind:
+                    step = x - cur[5]
+                    want = {0: (1,), 1: (0, -1)}[kind] if cur[7] is None else (cur[7],)
+                    if step in want and (kind == 0 or cur[1] - cur[0] == 1 or step == cur[7]):
+                        cur[1] += 1
+                        cur[5] = x
+                        cur[7] = step
+                        if kind == 0:
+                            cur[6] += char(lv)
+                        continue
+            if cur is not None:
+                yield self._xf_item(cur)
+            cur = [lv, lv + 1, r, None if x is None else kind, x, x, char(lv) if (x is not None and kind == 0) else "", None]
+        if cur is not None:
+            yield self._xf_item(cur)
+
+    @staticmethod
+    def _xf_item(cur):
+        rng = range(cur[0], cur[1])
+        if cur[3] is None:
+            return rng, None
+        if cur[3] == 0:
+            return rng, ("ins", cur[4], cur[6])
+        return rng, ("del", min(cur[4], cur[5]), cur[1] - cur[0])
 
     def dominators(self, a, b=()):
         """Graph::find_dominators_2 (src/causalgraph/graph/tools.rs:545-578) over this oplog."""

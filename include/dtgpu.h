@@ -122,6 +122,18 @@ size_t dtgpu_oplog_agent_runs(const dtgpu_oplog *oplog, uint32_t *out, size_t ca
 dtgpu_status dtgpu_checkout(const dtgpu_oplog *oplog, const uint64_t *version, size_t n_version, uint8_t *out,
                             size_t cap, size_t *out_len);
 dtgpu_status dtgpu_checkout_tip(const dtgpu_oplog *oplog, uint8_t *out, size_t cap, size_t *out_len);
+
+/* ListOpLog::iter_xf_operations() (src/list/merge.rs:24-48): the transformed operations that
+ * bring an empty document to the tip, in the order TransformedOpsIter yields them
+ * (src/listmerge/merge.rs:788-940: fast-forward prefix, then a SpanningTreeWalker from its
+ * frontier).  Runs on the GPU.  Writes n_lv records of two u32 {lv, pos} in application order:
+ * pos = the BaseMoved position of that LV applied on its own (an insert lands at pos; a delete
+ * removes the char at pos), 0xFFFFFFFF = DeleteAlreadyHappened.  out == NULL returns the record
+ * count in *n_out; cap counts records. */
+dtgpu_status dtgpu_xf_operations(const dtgpu_oplog *oplog, uint32_t *out, size_t cap, size_t *n_out);
+/* The LV order dtgpu_xf_operations applies ops in (host plan only; usable without a GPU).
+ * Returns the LV count; writes at most cap LVs. */
+size_t dtgpu_oplog_xf_order(const dtgpu_oplog *oplog, uint32_t *out, size_t cap);
 /* The history of `version` as an oplog of its own (what ListOpLog::checkout(&[LV]) replays:
  * diff_rev(version, ROOT), src/causalgraph/graph/tools.rs:176-292), LVs compacted in order,
  * agents / seqs / positions unchanged; its tip checkout is the checkout at `version`. */

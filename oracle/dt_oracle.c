@@ -875,7 +875,7 @@ static int walker_next(Walker *w, WalkStep *st) {
 /* ------------------------------------------------------------------------------------------ */
 /* per-item tracker on an implicit treap                                                      */
 /* ------------------------------------------------------------------------------------------ */
-typedef struct { int l, r, p; u32 prio; int cnt, vis; } TNode;
+typedef struct { int l, r, p; u32 prio; int cnt, vis, up; } TNode;   /* up: items never deleted */
 typedef struct {
     const dto_oplog *o;
     TNode *t; int root;
@@ -884,6 +884,7 @@ typedef struct {
     i64 *ol, *orr;       /* origin_left / origin_right per insert LV (ROOT=-1, END=-2) */
     i64 *del_target;     /* per delete LV */
     i64 n_items;
+    i64 xf;              /* transformed position of the last applied LV (-1: DeleteAlreadyHappened) */
     u64 rng;
     int err;
     /* stats */
@@ -894,10 +895,12 @@ typedef struct {
 static inline int tcnt(Tracker *T, int x) { return x < 0 ? 0 : T->t[x].cnt; }
 static inline int tvis(Tracker *T, int x) { return x < 0 ? 0 : T->t[x].vis; }
 static inline int isvis(Tracker *T, int x) { return T->state[x] == 1; }
+static inline int tup(Tracker *T, int x) { return x < 0 ? 0 : T->t[x].up; }
 static void tupd(Tracker *T, int x) {
     TNode *n = &T->t[x];
     n->cnt = 1 + tcnt(T, n->l) + tcnt(T, n->r);
     n->vis = isvis(T, x) + tvis(T, n->l) + tvis(T, n->r);
+    n->up = !T->ever_deleted[x] + tup(T, n->l) + tup(T, n->r);
     if (n->l >= 0) T->t[n->l].p = x;
     if (n->r >= 0) T->t[n->r].p = x;
 }
@@ -915,6 +918,13 @@ static void tsplit(Tracker *T, int x, int k, int *L, int *R) {   /* first k item
 static int trank(Tracker *T, int x) {   /* index of x in document order */
     int r = tcnt(T, T->t[x].l);
     while (T->t[x].p >= 0) { int p = T->t[x].p; if (T->t[p].r == x) r += tcnt(T, T->t[p].l) + 1; x = p; }
+    return r;
+}
+/* upstream position of x: never-deleted items before it (MarkerMetrics upstream_len,
+ * metrics.rs:18-66; upstream_cursor_pos) */
+static int tuprank(Tracker *T, int x) {
+    int r = tup(T, T->t[x].l);
+    while (T->t[x].p >= 0) { int p = T->t[x].p; if (T->t[p].r == x) r += tup(T, T->t[p].l) + !T->ever_deleted[p]; x = p; }
     return r;
 }
 static int tfind_vis(Tracker *T, i64 p) {   /* the item holding visible index p */
@@ -988,16 +998,18 @@ static void apply_ins(Tracker *T, i64 lv, i64 pos) {
         ins_at = scanning ? scan_start : c;
     }
     T->state[lv] = 1; T->ol[lv] = origin_left; T->orr[lv] = origin_right;
-    TNode *n = &T->t[lv]; n->l = n->r = n->p = -1; n->prio = xrand(T); n->cnt = 1; n->vis = 1;
+    TNode *n = &T->t[lv]; n->l = n->r = n->p = -1; n->prio = xrand(T); n->cnt = 1; n->vis = 1; n->up = 1;
     int L, R; tsplit(T, T->root, ins_at, &L, &R);
     T->root = tmerge(T, tmerge(T, L, (int)lv), R);
     T->t[T->root].p = -1;
     T->n_items++;
+    T->xf = tuprank(T, (int)lv);   /* integrate's ins_pos (merge.rs:154-278) */
 }
 /* M2Tracker::apply for one delete LV (merge.rs:457-556) */
 static void apply_del(Tracker *T, i64 lv, i64 pos) {
     int x = tfind_vis(T, pos);
     if (x < 0 || T->state[x] != 1) { T->err = E_CheckoutPanic; return; }
+    T->xf = T->ever_deleted[x] ? -1 : tuprank(T, x);   /* BaseMoved(del_start_xf) / DeleteAlreadyHappened */
     T->state[x] = 2; T->ever_deleted[x] = 1; T->del_target[lv] = x;
     tfix_up(T, x);
 }
@@ -1094,6 +1106,62 @@ EXPORT int dto_checkout_tip(const dto_oplog *o, int order, u8 **out, size_t *out
     return dto_checkout(o, o->version.v, (int)o->version.n, order, out, out_len, stats);
 }
 EXPORT void dto_free_buf(u8 *p) { free(p); }
+/* ListOpLog::iter_xf_operations() (src/list/merge.rs:24-48) restated per LV: the
+ * TransformedOpsIter order (src/listmerge/merge.rs:618-940) -- fast-forward through the leading
+ * graph entries whose parents are the current frontier, then a SpanningTreeWalker over the rest
+ * starting at that frontier -- and each LV's transformed position (the upstream position of the
+ * inserted item / of the deleted item, or -1 when the delete already happened).  out receives
+ * (lv, xf) pairs in application order; returns 0 or an error. */
+EXPORT int dto_xf_operations(const dto_oplog *o, i64 *out) {
+    i64 n = o->kind.n;
+    Tracker T; memset(&T, 0, sizeof T);
+    T.o = o; T.root = -1; T.rng = 0x9E3779B97F4A7C15ull;
+    T.t = malloc(sizeof(TNode) * (size_t)(n + 1));
+    T.state = calloc((size_t)n + 1, sizeof(u32));
+    T.ever_deleted = calloc((size_t)n + 1, 1);
+    T.ol = malloc(sizeof(i64) * (size_t)(n + 1)); T.orr = malloc(sizeof(i64) * (size_t)(n + 1));
+    T.del_target = malloc(sizeof(i64) * (size_t)(n + 1));
+    for (i64 v = 0; v < n; v++) if (o->kind.v[v] == 0 && o->cbyte.v[v] < 0) T.err = E_CheckoutPanic;
+    i64 k = 0, ff_end = 0;
+    VecI64 front = {0};
+    /* fast-forward (merge.rs:792-835): consume whole entries while parents == next_frontier */
+    for (i64 ei = 0; ei < o->g.e.n && !T.err; ei++) {
+        const GEntry *e = &o->g.e.v[ei];
+        if (e->np != front.n) break;
+        int same = 1; for (int q = 0; q < e->np; q++) if (e->parents[q] != front.v[q]) same = 0;
+        if (!same) break;
+        for (i64 v = e->start; v < e->end && !T.err; v++) {
+            if (o->kind.v[v] == 0) apply_ins(&T, v, o->pos.v[v]); else apply_del(&T, v, o->pos.v[v]);
+            out[2 * k] = v; out[2 * k + 1] = T.xf; k++;
+        }
+        front.n = 0; VPUSH(front, e->end - 1);
+        ff_end = e->end;
+    }
+    if (ff_end < n && !T.err) {
+        Range rest = { ff_end, n };
+        Walker w; WalkStep st; memset(&st, 0, sizeof st);
+        walker_init(&w, &o->g, &rest, 1);
+        for (i64 q = 0; q < front.n; q++) VPUSH(w.frontier, front.v[q]);   /* SpanningTreeWalker::new(.., frontier) */
+        while (!T.err && walker_next(&w, &st)) {
+            for (i64 i = 0; i < st.retreat.n && !T.err; i++)
+                for (i64 v = st.retreat.v[i].end - 1; v >= st.retreat.v[i].start && !T.err; v--) retreat_lv(&T, v);
+            for (i64 i = st.advance_rev.n - 1; i >= 0 && !T.err; i--)
+                for (i64 v = st.advance_rev.v[i].start; v < st.advance_rev.v[i].end && !T.err; v++) advance_lv(&T, v);
+            for (i64 v = st.consume.start; v < st.consume.end && !T.err; v++) {
+                if (o->kind.v[v] == 0) apply_ins(&T, v, o->pos.v[v]); else apply_del(&T, v, o->pos.v[v]);
+                out[2 * k] = v; out[2 * k + 1] = T.xf; k++;
+            }
+        }
+        walker_free(&w);
+        VFREE(st.retreat); VFREE(st.advance_rev);
+    }
+    int err = T.err;
+    if (!err && k != n) err = E_CheckoutPanic;
+    VFREE(front);
+    free(T.t); free(T.state); free(T.ever_deleted); free(T.ol); free(T.orr); free(T.del_target);
+    return err;
+}
+
 
 /* ------------------------------------------------------------------------------------------ */
 /* graph-tool entry points for the causal_graph fixtures                                      */

@@ -57,6 +57,7 @@ def lib():
         L.dto_checkout.argtypes = [ctypes.c_void_p, P64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
                                    ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(Stats)]
         L.dto_free_buf.argtypes = [ctypes.c_void_p]
+        L.dto_xf_operations.argtypes = [ctypes.c_void_p, P64]
         L.dto_crc32c.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
         L.dto_crc32c.restype = ctypes.c_uint32
         L.dto_lz4_decompress.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]
@@ -157,6 +158,15 @@ class OpLog:
         data = ctypes.string_at(out.value, ln.value) if ln.value else b""
         lib().dto_free_buf(out)
         return data
+
+    def xf_operations(self):
+        """(lv, xf) per LV in TransformedOpsIter order (xf -1: DeleteAlreadyHappened)."""
+        n = len(self)
+        buf = (ctypes.c_int64 * max(2, 2 * n))()
+        e = lib().dto_xf_operations(self.h, buf)
+        if e:
+            raise OracleError(e)
+        return [(buf[2 * i], buf[2 * i + 1]) for i in range(n)]
 
     def checkout_tip(self, order=0) -> str:
         return self.checkout_tip_bytes(order).decode("utf-8")
