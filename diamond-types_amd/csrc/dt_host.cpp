@@ -697,22 +697,10 @@ Status decode_dt(const uint8_t *data, size_t len, bool ignore_crc, HostOpLog &o)
 // ------------------------------------------------------------------------------------------
 // walk plan (src/listmerge/txn_trace.rs:114-333 + merge.rs:564-581)
 // ------------------------------------------------------------------------------------------
-Status build_plan(const HostOpLog &o, Plan &plan) { return build_plan_from(o, plan, false); }
-Status build_xf_plan(const HostOpLog &o, Plan &plan) { return build_plan_from(o, plan, true); }
-
-// xf == false: SpanningTreeWalker over every graph entry from ROOT.  xf == true: the order
-// TransformedOpsIter applies ops in (src/listmerge/merge.rs:788-940) -- fast-forward through the
-// leading entries whose parents are the current frontier, then a SpanningTreeWalker over the
-// remaining entries starting at that frontier (parents outside the input are ignored,
-// txn_trace.rs:140-148).
-Status build_plan_from(const HostOpLog &o, Plan &plan, bool xf) {
-    plan.cmds.clear();
-    plan.tlist.clear();
+// Agent-name ranks for the YjsMod tie-break (byte-wise name order, merge.rs:199-218) as the
+// device's (first LV, rank, first seq, agent) quads.
+static void plan_agent_runs(const HostOpLog &o, Plan &plan) {
     plan.agent_runs.clear();
-    if (o.n_lv >= MAX_PLAN_LV) return ErrCapacity;
-    if (!o.content_complete) return ErrCheckout;   // content.unwrap() in apply_to (merge.rs:329)
-
-    // agent name ranks for the YjsMod tie-break (byte-wise name order, merge.rs:199-218)
     std::vector<uint32_t> order(o.agent_names.size()), rank(o.agent_names.size());
     for (uint32_t i = 0; i < order.size(); i++) order[i] = i;
     std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return o.agent_names[a] < o.agent_names[b]; });
@@ -723,27 +711,30 @@ Status build_plan_from(const HostOpLog &o, Plan &plan, bool xf) {
         plan.agent_runs.push_back(uint32_t(r.seq));
         plan.agent_runs.push_back(r.agent);
     }
+}
+
+// SpanningTreeWalker over every graph entry from ROOT.
+Status build_plan(const HostOpLog &o, Plan &plan) {
+    plan.cmds.clear();
+    plan.tlist.clear();
+    plan.agent_runs.clear();
+    if (o.n_lv >= MAX_PLAN_LV) return ErrCapacity;
+    if (!o.content_complete) return ErrCheckout;   // content.unwrap() in apply_to (merge.rs:329)
+
+    plan_agent_runs(o, plan);
 
     const auto &E = o.graph.entries;
     const size_t ne = E.size();
     // VisitEntry table: parent / child indexes inside the (whole-graph) input
     std::vector<std::vector<uint32_t>> pidx(ne), cidx(ne);
     std::vector<uint32_t> todo;
-    std::vector<uint64_t> frontier;
-    size_t first = 0;   // entries before `first` were fast-forwarded
-    if (xf)
-        while (first < ne && E[first].parents == frontier) frontier.assign(1, E[first++].end - 1);
-    for (size_t i = first; i < ne; i++) {
-        for (uint64_t p : E[i].parents) {
-            const int64_t pe = o.graph.find_idx(p);
-            if (pe >= int64_t(first)) pidx[i].push_back(uint32_t(pe));
-        }
+    for (size_t i = 0; i < ne; i++) {
+        for (uint64_t p : E[i].parents) pidx[i].push_back(uint32_t(o.graph.find_idx(p)));
         if (pidx[i].empty()) todo.push_back(uint32_t(i));
     }
     for (size_t i = 0; i < ne; i++) for (uint32_t p : pidx[i]) cidx[p].push_back(uint32_t(i));
     std::reverse(todo.begin(), todo.end());
     std::vector<uint8_t> visited(ne, 0);
-    for (size_t i = 0; i < first; i++) visited[i] = 1;
 
     // op-run lookup
     const auto &ops = o.ops;
@@ -782,7 +773,7 @@ Status build_plan_from(const HostOpLog &o, Plan &plan, bool xf) {
         }
     };
 
-    for (size_t i = 0; i < first; i++) emit_apply(E[i].start, E[i].end);
+    std::vector<uint64_t> frontier;
     std::vector<std::pair<uint64_t, uint64_t>> only_a, only_b;
     while (!todo.empty()) {
         uint32_t idx = todo.back();
@@ -818,6 +809,157 @@ Status build_plan_from(const HostOpLog &o, Plan &plan, bool xf) {
     flush_step(t0);
     if (plan.tlist.size() >= 0xFFFFFFFFull) return ErrCapacity;
     return OK;
+}
+
+// ---- transformed-ops plans ----------------------------------------------------------------
+namespace {
+struct XfPlanner {
+    const HostOpLog &o;
+    Plan &plan;
+    size_t run_of(uint64_t lv) const {
+        auto it = std::upper_bound(o.ops.begin(), o.ops.end(), lv, [](uint64_t v, const OpRun &r) { return v < r.lv + r.len; });
+        return size_t(it - o.ops.begin());
+    }
+    void state(uint64_t s, uint64_t e, bool retreat) {   // retreat / advance entries, tagged Ins/Del
+        for (size_t ri = run_of(s); s < e; ri++) {
+            const OpRun &r = o.ops[ri];
+            const uint64_t hi = std::min(e, r.lv + r.len);
+            const uint32_t tag = (r.kind ? TL_DEL : 0u) | (retreat ? 0u : TL_ADV);
+            for (uint64_t v = s; v < hi; v++) plan.tlist.push_back(uint32_t(v) | tag);
+            s = hi;
+        }
+    }
+    // retreat / advance from `cur` to `to` as one TOG command (Graph::diff_rev)
+    void move(const std::vector<uint64_t> &cur, const std::vector<uint64_t> &to) {
+        std::vector<std::pair<uint64_t, uint64_t>> a, b;
+        o.graph.diff_rev(cur, to, a, b);
+        const size_t t0 = plan.tlist.size();
+        for (auto &rg : a) { state(rg.first, rg.second, true); plan.n_retreat += rg.second - rg.first; }
+        for (auto &rg : b) { state(rg.first, rg.second, false); plan.n_advance += rg.second - rg.first; }
+        if (plan.tlist.size() > t0) plan.cmds.push_back(Cmd{CMD_TOG, uint32_t(t0), uint32_t(plan.tlist.size() - t0), 0});
+    }
+    void apply(uint64_t s, uint64_t e) {   // op runs clipped to [s, e) (truncate_tagged_span)
+        for (size_t ri = run_of(s); s < e; ri++) {
+            const OpRun &r = o.ops[ri];
+            const uint64_t hi = std::min(e, r.lv + r.len);
+            const uint64_t k = s - r.lv, m = hi - s;
+            if (r.kind == 0) plan.cmds.push_back(Cmd{CMD_INS, uint32_t(s), uint32_t(m), uint32_t(r.pos + k)});
+            else if (r.fwd) plan.cmds.push_back(Cmd{CMD_DEL | 16u, uint32_t(s), uint32_t(m), uint32_t(r.pos)});
+            else plan.cmds.push_back(Cmd{CMD_DEL, uint32_t(s), uint32_t(m), uint32_t(r.pos + r.len - k - m)});
+            s = hi;
+        }
+    }
+    std::vector<uint64_t> parents_at(uint64_t lv) const {   // clone_parents_at_version
+        const GraphEntry &e = o.graph.entries[size_t(o.graph.find_idx(lv))];
+        return lv > e.start ? std::vector<uint64_t>{lv - 1} : e.parents;
+    }
+    // SpanningTreeWalker::new(graph, spans, frontier) + its iteration (txn_trace.rs:114-333):
+    // ascending spans split per graph entry; parents outside the input are ignored.
+    void walk(const std::vector<std::pair<uint64_t, uint64_t>> &spans, std::vector<uint64_t> &frontier) {
+        struct In { uint64_t start, end; std::vector<uint64_t> parents; std::vector<uint32_t> pidx, cidx; };
+        std::vector<In> in;
+        for (auto sp : spans) {
+            for (uint64_t s = sp.first; s < sp.second;) {
+                const GraphEntry &e = o.graph.entries[size_t(o.graph.find_idx(s))];
+                const uint64_t t = std::min(e.end, sp.second);
+                in.push_back(In{s, t, parents_at(s), {}, {}});
+                s = t;
+            }
+        }
+        auto find_in = [&](uint64_t lv) -> int64_t {
+            auto it = std::upper_bound(in.begin(), in.end(), lv, [](uint64_t v, const In &x) { return v < x.end; });
+            return it != in.end() && it->start <= lv ? int64_t(it - in.begin()) : -1;
+        };
+        std::vector<uint32_t> todo;
+        for (size_t i = 0; i < in.size(); i++) {
+            for (uint64_t p : in[i].parents) { const int64_t j = find_in(p); if (j >= 0) in[i].pidx.push_back(uint32_t(j)); }
+            if (in[i].pidx.empty()) todo.push_back(uint32_t(i));
+        }
+        for (size_t i = 0; i < in.size(); i++) for (uint32_t p : in[i].pidx) in[p].cidx.push_back(uint32_t(i));
+        std::reverse(todo.begin(), todo.end());
+        std::vector<uint8_t> visited(in.size(), 0);
+        while (!todo.empty()) {
+            uint32_t idx = todo.back();
+            if (in[idx].parents.size() >= 2) {   // prefer non-merge entries (txn_trace.rs:243-265)
+                int64_t found = -1;
+                for (int64_t ii = int64_t(todo.size()) - 1; ii >= 0; ii--)
+                    if (in[todo[size_t(ii)]].parents.size() < 2) { found = ii; break; }
+                if (found >= 0) { idx = todo[size_t(found)]; todo[size_t(found)] = todo.back(); todo.pop_back(); }
+                else todo.pop_back();
+            } else todo.pop_back();
+            visited[idx] = 1;
+            move(frontier, in[idx].parents);
+            apply(in[idx].start, in[idx].end);
+            frontier.assign(1, in[idx].end - 1);
+            plan.n_steps++;
+            for (uint32_t c : in[idx].cidx) {
+                if (visited[c]) continue;
+                bool ok = true;
+                for (uint32_t p : in[c].pidx) if (!visited[p]) { ok = false; break; }
+                if (ok) todo.push_back(c);
+            }
+        }
+    }
+};
+std::vector<std::pair<uint64_t, uint64_t>> ascending(std::vector<std::pair<uint64_t, uint64_t>> v) {
+    std::reverse(v.begin(), v.end());
+    return v;
+}
+}  // namespace
+
+Status build_xf_plan_from(const HostOpLog &o, const std::vector<uint64_t> &from, const std::vector<uint64_t> &merge,
+                          Plan &plan, size_t &first_emitted) {
+    plan = Plan();
+    first_emitted = 0;
+    if (o.n_lv >= MAX_PLAN_LV) return ErrCapacity;
+    if (!o.content_complete) return ErrCheckout;
+    for (uint64_t v : from) if (v >= o.n_lv) return ErrArg;
+    for (uint64_t v : merge) if (v >= o.n_lv) return ErrArg;
+    plan_agent_runs(o, plan);
+    XfPlanner P{o, plan};
+    std::vector<std::pair<uint64_t, uint64_t>> hist, newr, none;
+    o.graph.diff_rev(from, {}, hist, none);      // Hist(from): the branch's content
+    o.graph.diff_rev(merge, from, newr, none);   // new ops: Hist(merge) - Hist(from)
+    hist = ascending(hist);
+    newr = ascending(newr);
+    std::vector<uint64_t> frontier;
+    if (!hist.empty()) P.walk(hist, frontier);
+    P.move(frontier, from);
+    frontier = from;
+    first_emitted = plan.cmds.size();
+    // fast-forward (merge.rs:792-835): up to the entry's end while its parents are the frontier
+    size_t si = 0;
+    while (si < newr.size()) {
+        const uint64_t s0 = newr[si].first;
+        if (P.parents_at(s0) != frontier) break;
+        const GraphEntry &e = o.graph.entries[size_t(o.graph.find_idx(s0))];
+        const uint64_t s1 = std::min(e.end, newr[si].second);
+        P.apply(s0, s1);
+        frontier.assign(1, s1 - 1);
+        newr[si].first = s1;
+        if (s1 == newr[si].second) si++;
+    }
+    newr.erase(newr.begin(), newr.begin() + ptrdiff_t(si));
+    if (!newr.empty()) P.walk(newr, frontier);
+    // end at the merged version (ListBranch::merge's frontier, find_dominators_2)
+    std::vector<uint64_t> u(from);
+    u.insert(u.end(), merge.begin(), merge.end());
+    std::sort(u.begin(), u.end());
+    u.erase(std::unique(u.begin(), u.end()), u.end());
+    std::vector<uint64_t> fin;
+    std::vector<std::pair<uint64_t, uint64_t>> a, b;
+    for (uint64_t v : u) {
+        bool dom = false;
+        for (uint64_t w : u) if (w > v) { o.graph.diff_rev({v}, {w}, a, b); if (a.empty()) { dom = true; break; } }
+        if (!dom) fin.push_back(v);
+    }
+    P.move(frontier, fin);
+    if (plan.tlist.size() >= 0xFFFFFFFFull) return ErrCapacity;
+    return OK;
+}
+Status build_xf_plan(const HostOpLog &o, Plan &plan) {
+    size_t first = 0;
+    return build_xf_plan_from(o, {}, o.version, plan, first);
 }
 
 Status build_plan_input(const HostOpLog &o, PlanInput &pi) {

@@ -99,7 +99,12 @@ Status build_plan(const HostOpLog &o, Plan &plan);
 // The order TransformedOpsIter applies ops in for iter_xf_operations (src/list/merge.rs:24-48;
 // src/listmerge/merge.rs:788-940): the fast-forward prefix, then the walker from its frontier.
 Status build_xf_plan(const HostOpLog &o, Plan &plan);
-Status build_plan_from(const HostOpLog &o, Plan &plan, bool xf);
+// iter_xf_operations_from(from, merge) (src/list/merge.rs:24-38): the walk that rebuilds the
+// branch at `from` (not reported), then the new ops Hist(merge) - Hist(from) in
+// TransformedOpsIter order; ends at the merged version.  first_emitted = index of the first
+// command whose ops are reported.
+Status build_xf_plan_from(const HostOpLog &o, const std::vector<uint64_t> &from, const std::vector<uint64_t> &merge,
+                          Plan &plan, size_t &first_emitted);
 
 // The decoded oplog as flat arrays for the device planner (dt_plan.hip): the same information
 // the reference's ListOpLog holds (Graph entries with parents and child indexes, the agent

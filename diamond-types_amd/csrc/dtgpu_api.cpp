@@ -10,6 +10,7 @@
 #include <cstring>
 #include <memory>
 #include <thread>
+#include <tuple>
 #include <vector>
 
 #include "../../include/dtgpu.h"
@@ -95,6 +96,8 @@ struct Prepared {
     PlanInput pi;
     Plan plan;             // host plan: only for documents the device planner declines
     bool host_plan = false;
+    std::vector<uint64_t> xf_from, xf_merge;   // transformed-ops batches: the merge to report
+    size_t xf_first = 0;                       // first reported command of the plan
 };
 
 void prepare_from_oplog(const HostOpLog &src, Prepared &p) {
@@ -230,7 +233,8 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     }
     parallel_for(n, threads, [&](size_t i) {
         Prepared &p = prep[i];
-        if (p.status == OK && p.host_plan) p.status = xf ? build_xf_plan(p.log, p.plan) : build_plan(p.log, p.plan);
+        if (p.status == OK && p.host_plan)
+            p.status = xf ? build_xf_plan_from(p.log, p.xf_from, p.xf_merge, p.plan, p.xf_first) : build_plan(p.log, p.plan);
     });
 
     // ---- 2. per-document layout ---------------------------------------------------------------
@@ -753,14 +757,23 @@ size_t dtgpu_oplog_plan_commands(const dtgpu_oplog *h, uint32_t *cmds, size_t ca
     return p.plan.cmds.size();
 }
 
-size_t dtgpu_oplog_xf_order(const dtgpu_oplog *h, uint32_t *out, size_t cap) {
-    if (!h) return 0;
+size_t dtgpu_oplog_xf_order(const dtgpu_oplog *h, const uint64_t *from, size_t n_from, const uint64_t *merge,
+                            size_t n_merge, uint32_t *out, size_t cap) {
+    if (!h || (n_from && !from) || (n_merge && !merge)) return 0;
     HostOpLog log = h->o;
     log.finish();
+    std::vector<uint64_t> f(n_from + 1), m(n_merge + 1);
+    const int64_t nf = dtgpu_oplog_dominators(h, from, n_from, nullptr, 0, f.data(), f.size());
+    const int64_t nm = dtgpu_oplog_dominators(h, merge, n_merge, nullptr, 0, m.data(), m.size());
+    if (nf < 0 || nm < 0) return 0;
+    f.resize(size_t(nf));
+    m.resize(size_t(nm));
     Plan plan;
-    if (build_xf_plan(log, plan) != OK) return 0;
+    size_t first = 0;
+    if (build_xf_plan_from(log, f, m, plan, first) != OK) return 0;
     size_t k = 0;
-    for (const Cmd &c : plan.cmds) {
+    for (size_t i = first; i < plan.cmds.size(); i++) {
+        const Cmd &c = plan.cmds[i];
         if ((c.op & 15u) == CMD_TOG) continue;
         for (uint32_t j = 0; j < c.len; j++, k++) if (k < cap) out[k] = c.lv + j;
     }
@@ -1168,19 +1181,34 @@ dtgpu_status dtgpu_checkout(const dtgpu_oplog *h, const uint64_t *version, size_
     return dtgpu_checkout_tip(&sub, out, cap, out_len);
 }
 
-dtgpu_status dtgpu_xf_operations(const dtgpu_oplog *h, uint32_t *out, size_t cap, size_t *n_out) {
-    if (!h) return DTGPU_ERR_ARG;
-    const uint64_t n_lv = h->o.n_lv;
-    if (n_out) *n_out = size_t(n_lv);
-    if (!out) return DTGPU_OK;
-    if (cap < n_lv) return DTGPU_ERR_ARG;
-    if (n_lv == 0) return DTGPU_OK;
+dtgpu_status dtgpu_xf_operations_from(const dtgpu_oplog *h, const uint64_t *from, size_t n_from, const uint64_t *merge,
+                                      size_t n_merge, uint32_t *out, size_t cap, size_t *n_out) {
+    if (!h || (n_from && !from) || (n_merge && !merge)) return DTGPU_ERR_ARG;
+    std::vector<Prepared> prep(1);
+    Prepared &p = prep[0];
+    p.log = h->o;
+    p.log.finish();
+    for (auto [v, n, dst] : {std::make_tuple(from, n_from, &p.xf_from), std::make_tuple(merge, n_merge, &p.xf_merge)}) {
+        dst->resize(n + 1);   // reduce to frontiers (Frontier::from_unsorted)
+        const int64_t k = dtgpu_oplog_dominators(h, v, n, nullptr, 0, dst->data(), dst->size());
+        if (k < 0) return DTGPU_ERR_ARG;
+        dst->resize(size_t(k));
+    }
+    {   // the reported LV count comes from the host plan (no GPU needed for a size query)
+        Plan plan;
+        size_t first = 0;
+        const Status st = build_xf_plan_from(p.log, p.xf_from, p.xf_merge, plan, first);
+        if (st != OK) return dtgpu_status(st);
+        size_t k = 0;
+        for (size_t i = first; i < plan.cmds.size(); i++) if ((plan.cmds[i].op & 15u) != CMD_TOG) k += plan.cmds[i].len;
+        if (n_out) *n_out = k;
+        if (!out) return DTGPU_OK;
+        if (cap < k) return DTGPU_ERR_ARG;
+        if (k == 0) return DTGPU_OK;
+    }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return DTGPU_ERR_NO_DEVICE;
-    std::vector<Prepared> prep(1);
-    prep[0].log = h->o;
-    prep[0].log.finish();
-    prepare_input(prep[0]);
+    prepare_input(p);
     dtgpu_batch *B = nullptr;
     dtgpu_status st = stage(prep, nullptr, &B, true);
     if (st) return st;
@@ -1188,22 +1216,27 @@ dtgpu_status dtgpu_xf_operations(const dtgpu_oplog *h, uint32_t *out, size_t cap
     if (B->host_status[0] != OK) return dtgpu_status(B->host_status[0]);
     if (launch_replay_xf(B->large, B->stream) != OK) return DTGPU_ERR_HIP;
     DocResult r;
-    std::vector<uint32_t> xfv(n_lv);
+    std::vector<uint32_t> xfv(p.log.n_lv);
     if (hipMemcpyAsync(&r, B->d_results.p, sizeof r, hipMemcpyDeviceToHost, B->stream) != hipSuccess ||
-        hipMemcpyAsync(xfv.data(), B->d_xf.p, n_lv * 4, hipMemcpyDeviceToHost, B->stream) != hipSuccess ||
+        hipMemcpyAsync(xfv.data(), B->d_xf.p, xfv.size() * 4, hipMemcpyDeviceToHost, B->stream) != hipSuccess ||
         hipStreamSynchronize(B->stream) != hipSuccess)
         return DTGPU_ERR_HIP;
     if (r.status != OK) return dtgpu_status(r.status);
-    // application order = the plan's INS / DEL commands in order
+    // application order = the plan's reported INS / DEL commands in order
     size_t k = 0;
-    for (const Cmd &c : prep[0].plan.cmds) {
+    for (size_t i = p.xf_first; i < p.plan.cmds.size(); i++) {
+        const Cmd &c = p.plan.cmds[i];
         if ((c.op & 15u) == CMD_TOG) continue;
-        for (uint32_t j = 0; j < c.len && k < n_lv; j++, k++) {
+        for (uint32_t j = 0; j < c.len && k < cap; j++, k++) {
             out[2 * k] = c.lv + j;
             out[2 * k + 1] = xfv[c.lv + j];
         }
     }
-    return k == n_lv ? DTGPU_OK : DTGPU_ERR_CHECKOUT;
+    return DTGPU_OK;
+}
+dtgpu_status dtgpu_xf_operations(const dtgpu_oplog *h, uint32_t *out, size_t cap, size_t *n_out) {
+    if (!h) return DTGPU_ERR_ARG;
+    return dtgpu_xf_operations_from(h, nullptr, 0, h->o.version.data(), h->o.version.size(), out, cap, n_out);
 }
 
 dtgpu_status dtgpu_checkout_tip(const dtgpu_oplog *h, uint8_t *out, size_t cap, size_t *out_len) {

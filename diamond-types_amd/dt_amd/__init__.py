@@ -108,8 +108,10 @@ def lib():
     L.dtgpu_oplog_dominators.restype = ctypes.c_int64
     L.dtgpu_oplog_history.argtypes = [vp, pu64, sz, ctypes.POINTER(vp)]
     L.dtgpu_xf_operations.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32), sz, ctypes.POINTER(sz)]
-    L.dtgpu_oplog_xf_order.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32), sz]
+    L.dtgpu_oplog_xf_order.argtypes = [vp, pu64, sz, pu64, sz, ctypes.POINTER(ctypes.c_uint32), sz]
     L.dtgpu_oplog_xf_order.restype = sz
+    L.dtgpu_xf_operations_from.argtypes = [vp, pu64, sz, pu64, sz, ctypes.POINTER(ctypes.c_uint32), sz,
+                                           ctypes.POINTER(sz)]
     L.dtgpu_batch_create.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz), sz,
                                      ctypes.POINTER(BatchOpts), ctypes.POINTER(vp)]
     L.dtgpu_batch_create_from_oplogs.argtypes = [ctypes.POINTER(vp), sz, ctypes.POINTER(BatchOpts), ctypes.POINTER(vp)]
@@ -199,17 +201,23 @@ class ListBranch:
         return oplog.checkout_tip()
 
     def merge(self, oplog: "ListOpLog", merge_frontier) -> None:
-        """ListBranch::merge(&mut self, oplog, merge_frontier) (src/list/merge.rs:63-95).
-
-        The branch ends at find_dominators_2(self.version, merge_frontier) with the text of that
-        version.  A branch's content always equals the oplog's checkout at its version (every
-        edit goes through the oplog), so the merged text is the device checkout at the new
-        version (dtgpu_checkout) rather than the reference's incremental transformed-op replay;
-        the result is the same text and frontier."""
+        """ListBranch::merge(&mut self, oplog, merge_frontier) (src/list/merge.rs:63-95): apply
+        the transformed operations iter_xf_operations_from(self.version, merge_frontier)
+        (computed on the GPU) to this branch's content, then move to
+        find_dominators_2(self.version, merge_frontier)."""
         v = oplog.dominators(self.version, merge_frontier)
-        if v != self.version:
-            self._content = oplog.checkout_bytes(v)
-            self.version = v
+        if v == self.version:
+            return
+        text = list(self.content())
+        for _rng, op in oplog.iter_xf_operations(self.version, merge_frontier):
+            if op is None:
+                continue
+            if op[0] == "ins":
+                text[op[1]:op[1]] = list(op[2])
+            else:
+                del text[op[1]:op[1] + op[2]]
+        self._content = "".join(text).encode()
+        self.version = v
 
     def content(self) -> str:
         return self._content.decode("utf-8")
@@ -330,24 +338,39 @@ class ListOpLog:
     def checkout_tip(self) -> ListBranch:
         return ListBranch(self.checkout_tip_bytes(), self.local_frontier())
 
-    def xf_order(self):
-        """LV order of iter_xf_operations (host plan: fast-forward prefix, then the walker)."""
+    def xf_order(self, frm=None, merging=None):
+        """LV order of iter_xf_operations(_from) (host plan: fast-forward prefix, then the
+        walker); default ROOT to the tip."""
+        if frm is None and merging is None:
+            frm, merging = [], self.local_frontier()
+        pa, na = _u64s(frm or [])
+        pb, nb = _u64s(merging or [])
         n = len(self)
         buf = (ctypes.c_uint32 * max(1, n))()
-        k = lib().dtgpu_oplog_xf_order(self._h, buf, n)
+        k = lib().dtgpu_oplog_xf_order(self._h, pa, na, pb, nb, buf, n)
         return list(buf[:k])
 
-    def xf_operations_lv(self):
+    def xf_operations_lv(self, frm=None, merging=None):
         """Per-LV transformed positions in application order, computed on the GPU
-        (dtgpu_xf_operations): [(lv, pos or None)], None = DeleteAlreadyHappened."""
-        n = len(self)
-        buf = (ctypes.c_uint32 * max(2, 2 * n))()
+        (dtgpu_xf_operations_from; default: ROOT to the tip): [(lv, pos or None)], None =
+        DeleteAlreadyHappened."""
+        if frm is None and merging is None:
+            frm, merging = [], self.local_frontier()
+        pa, na = _u64s(frm or [])
+        pb, nb = _u64s(merging or [])
         k = ctypes.c_size_t()
-        _check(lib().dtgpu_xf_operations(self._h, buf, n, ctypes.byref(k)))
+        _check(lib().dtgpu_xf_operations_from(self._h, pa, na, pb, nb, None, 0, ctypes.byref(k)))
+        n = k.value
+        buf = (ctypes.c_uint32 * max(2, 2 * n))()
+        _check(lib().dtgpu_xf_operations_from(self._h, pa, na, pb, nb, buf, n, ctypes.byref(k)))
         return [(buf[2 * i], None if buf[2 * i + 1] == 0xFFFFFFFF else buf[2 * i + 1]) for i in range(k.value)]
 
-    def iter_xf_operations(self):
-        """ListOpLog::iter_xf_operations() (src/list/merge.rs:24-48): yields (range(lv, lv+len),
+    def iter_xf_operations_from(self, frm, merging):
+        """ListOpLog::iter_xf_operations_from (src/list/merge.rs:24-38); see iter_xf_operations."""
+        return self.iter_xf_operations(frm, merging)
+
+    def iter_xf_operations(self, frm=None, merging=None):
+        """ListOpLog::iter_xf_operations() (src/list/merge.rs:40-48): yields (range(lv, lv+len),
         op) with op = ("ins", pos, text) / ("del", pos, len) / None (DeleteAlreadyHappened).
         Consecutive LVs of one op run are merged when they form one reference-style op: an
         insert at consecutive positions, a forward delete at one position, a backspace run at
@@ -366,7 +389,7 @@ class ListOpLog:
             return content[b:b + n].decode("utf-8")
 
         cur = None   # [start_lv, end_lv, run, kind, first_pos, last_pos, text, step]
-        for lv, x in self.xf_operations_lv():
+        for lv, x in self.xf_operations_lv(frm, merging):
             r, kind = run_of[lv]
             if cur is not None and lv == cur[1] and r == cur[2]:
                 if x is None and cur[3] is None:

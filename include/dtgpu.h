@@ -131,9 +131,17 @@ dtgpu_status dtgpu_checkout_tip(const dtgpu_oplog *oplog, uint8_t *out, size_t c
  * removes the char at pos), 0xFFFFFFFF = DeleteAlreadyHappened.  out == NULL returns the record
  * count in *n_out; cap counts records. */
 dtgpu_status dtgpu_xf_operations(const dtgpu_oplog *oplog, uint32_t *out, size_t cap, size_t *n_out);
-/* The LV order dtgpu_xf_operations applies ops in (host plan only; usable without a GPU).
- * Returns the LV count; writes at most cap LVs. */
-size_t dtgpu_oplog_xf_order(const dtgpu_oplog *oplog, uint32_t *out, size_t cap);
+/* ListOpLog::iter_xf_operations_from(from, merging) (src/list/merge.rs:24-38): the transformed
+ * operations that take a branch at version `from` to find_dominators_2(from, merging) -- exactly
+ * what ListBranch::merge applies to its content (src/list/merge.rs:63-95).  Same record format;
+ * only the new ops Hist(merging) - Hist(from) are reported. */
+dtgpu_status dtgpu_xf_operations_from(const dtgpu_oplog *oplog, const uint64_t *from, size_t n_from,
+                                      const uint64_t *merging, size_t n_merging, uint32_t *out, size_t cap,
+                                      size_t *n_out);
+/* The LV order dtgpu_xf_operations_from reports (host plan only; usable without a GPU).
+ * Returns the LV count (0 on an invalid version); writes at most cap LVs. */
+size_t dtgpu_oplog_xf_order(const dtgpu_oplog *oplog, const uint64_t *from, size_t n_from, const uint64_t *merging,
+                            size_t n_merging, uint32_t *out, size_t cap);
 /* The history of `version` as an oplog of its own (what ListOpLog::checkout(&[LV]) replays:
  * diff_rev(version, ROOT), src/causalgraph/graph/tools.rs:176-292), LVs compacted in order,
  * agents / seqs / positions unchanged; its tip checkout is the checkout at `version`. */

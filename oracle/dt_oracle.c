@@ -1106,14 +1106,43 @@ EXPORT int dto_checkout_tip(const dto_oplog *o, int order, u8 **out, size_t *out
     return dto_checkout(o, o->version.v, (int)o->version.n, order, out, out_len, stats);
 }
 EXPORT void dto_free_buf(u8 *p) { free(p); }
-/* ListOpLog::iter_xf_operations() (src/list/merge.rs:24-48) restated per LV: the
- * TransformedOpsIter order (src/listmerge/merge.rs:618-940) -- fast-forward through the leading
- * graph entries whose parents are the current frontier, then a SpanningTreeWalker over the rest
- * starting at that frontier -- and each LV's transformed position (the upstream position of the
- * inserted item / of the deleted item, or -1 when the delete already happened).  out receives
- * (lv, xf) pairs in application order; returns 0 or an error. */
-EXPORT int dto_xf_operations(const dto_oplog *o, i64 *out) {
+/* ListOpLog::iter_xf_operations_from(from, merging) (src/list/merge.rs:24-38) restated per LV,
+ * in the TransformedOpsIter order (src/listmerge/merge.rs:618-940): the new ops are
+ * Hist(merging) - Hist(from); fast-forward through them while the next op's parents are the
+ * current frontier (whole graph entries, :792-835), then a SpanningTreeWalker over the rest
+ * starting at that frontier.  The tracker first replays Hist(from) (not emitted), so every item
+ * the branch at `from` holds is in it; a transformed position is the upstream position of the
+ * inserted item / of the deleted item (-1: the delete already happened).  out receives
+ * (lv, xf) pairs in application order; *n_out their count. */
+static void walk_apply(Tracker *T, const Graph *g, const Range *spans, i64 nspans, VecI64 *front, i64 *out, i64 *k) {
+    Walker w; WalkStep st; memset(&st, 0, sizeof st);
+    walker_init(&w, g, spans, nspans);
+    for (i64 q = 0; q < front->n; q++) VPUSH(w.frontier, front->v[q]);   /* SpanningTreeWalker::new(.., start_at) */
+    while (!T->err && walker_next(&w, &st)) {
+        for (i64 i = 0; i < st.retreat.n && !T->err; i++)
+            for (i64 v = st.retreat.v[i].end - 1; v >= st.retreat.v[i].start && !T->err; v--) retreat_lv(T, v);
+        for (i64 i = st.advance_rev.n - 1; i >= 0 && !T->err; i--)
+            for (i64 v = st.advance_rev.v[i].start; v < st.advance_rev.v[i].end && !T->err; v++) advance_lv(T, v);
+        for (i64 v = st.consume.start; v < st.consume.end && !T->err; v++) {
+            if (T->o->kind.v[v] == 0) apply_ins(T, v, T->o->pos.v[v]); else apply_del(T, v, T->o->pos.v[v]);
+            if (out) { out[2 * *k] = v; out[2 * *k + 1] = T->xf; }
+            (*k)++;
+        }
+    }
+    front->n = 0;
+    for (i64 q = 0; q < w.frontier.n; q++) VPUSH(*front, w.frontier.v[q]);
+    walker_free(&w);
+    VFREE(st.retreat); VFREE(st.advance_rev);
+}
+static void ascending(VecRange *r) {
+    for (i64 i = 0, j = r->n - 1; i < j; i++, j--) { Range t = r->v[i]; r->v[i] = r->v[j]; r->v[j] = t; }
+}
+EXPORT int dto_xf_operations_from(const dto_oplog *o, const i64 *from, int nf, const i64 *merge, int nm,
+                                  i64 *out, i64 *n_out) {
     i64 n = o->kind.n;
+    *n_out = 0;
+    for (int i = 0; i < nf; i++) if (from[i] < 0 || from[i] >= n) return E_CheckoutPanic;
+    for (int i = 0; i < nm; i++) if (merge[i] < 0 || merge[i] >= n) return E_CheckoutPanic;
     Tracker T; memset(&T, 0, sizeof T);
     T.o = o; T.root = -1; T.rng = 0x9E3779B97F4A7C15ull;
     T.t = malloc(sizeof(TNode) * (size_t)(n + 1));
@@ -1121,47 +1150,61 @@ EXPORT int dto_xf_operations(const dto_oplog *o, i64 *out) {
     T.ever_deleted = calloc((size_t)n + 1, 1);
     T.ol = malloc(sizeof(i64) * (size_t)(n + 1)); T.orr = malloc(sizeof(i64) * (size_t)(n + 1));
     T.del_target = malloc(sizeof(i64) * (size_t)(n + 1));
-    for (i64 v = 0; v < n; v++) if (o->kind.v[v] == 0 && o->cbyte.v[v] < 0) T.err = E_CheckoutPanic;
-    i64 k = 0, ff_end = 0;
+    VecRange hist = {0}, newr = {0}, none = {0}, ra = {0}, rb = {0};
     VecI64 front = {0};
-    /* fast-forward (merge.rs:792-835): consume whole entries while parents == next_frontier */
-    for (i64 ei = 0; ei < o->g.e.n && !T.err; ei++) {
-        const GEntry *e = &o->g.e.v[ei];
-        if (e->np != front.n) break;
-        int same = 1; for (int q = 0; q < e->np; q++) if (e->parents[q] != front.v[q]) same = 0;
+    i64 k = 0, warm = 0;
+    graph_diff_rev(&o->g, from, nf, NULL, 0, &hist, &none);       /* Hist(from) */
+    graph_diff_rev(&o->g, merge, nm, from, nf, &newr, &none);     /* new ops: Hist(merge) - Hist(from) */
+    ascending(&hist); ascending(&newr);
+    for (i64 i = 0; i < hist.n; i++) for (i64 v = hist.v[i].start; v < hist.v[i].end; v++)
+        if (o->kind.v[v] == 0 && o->cbyte.v[v] < 0) T.err = E_CheckoutPanic;
+    for (i64 i = 0; i < newr.n; i++) for (i64 v = newr.v[i].start; v < newr.v[i].end; v++)
+        if (o->kind.v[v] == 0 && o->cbyte.v[v] < 0) T.err = E_CheckoutPanic;
+    /* the branch at `from`: replay its history, then sit exactly at `from` */
+    if (!T.err && hist.n) walk_apply(&T, &o->g, hist.v, hist.n, &front, NULL, &warm);
+    if (!T.err) {
+        graph_diff_rev(&o->g, front.v, (int)front.n, from, nf, &ra, &rb);
+        for (i64 i = 0; i < ra.n && !T.err; i++)
+            for (i64 v = ra.v[i].end - 1; v >= ra.v[i].start && !T.err; v--) retreat_lv(&T, v);
+        for (i64 i = rb.n - 1; i >= 0 && !T.err; i--)
+            for (i64 v = rb.v[i].start; v < rb.v[i].end && !T.err; v++) advance_lv(&T, v);
+        front.n = 0;
+        for (int i = 0; i < nf; i++) VPUSH(front, from[i]);
+    }
+    /* fast-forward: consume up to the end of the entry while its parents are the frontier */
+    i64 si = 0;
+    while (!T.err && si < newr.n) {
+        i64 s0 = newr.v[si].start;
+        i64 gi = graph_find_idx(&o->g, s0);
+        const GEntry *e = &o->g.e.v[gi];
+        i64 p1 = s0 - 1; const i64 *par = &p1; int np = 1;    /* clone_parents_at_version */
+        if (s0 == e->start) { par = e->parents; np = e->np; }
+        if (np != front.n) break;
+        int same = 1; for (int q = 0; q < np; q++) if (par[q] != front.v[q]) same = 0;
         if (!same) break;
-        for (i64 v = e->start; v < e->end && !T.err; v++) {
+        i64 s1 = e->end < newr.v[si].end ? e->end : newr.v[si].end;
+        for (i64 v = s0; v < s1 && !T.err; v++) {
             if (o->kind.v[v] == 0) apply_ins(&T, v, o->pos.v[v]); else apply_del(&T, v, o->pos.v[v]);
             out[2 * k] = v; out[2 * k + 1] = T.xf; k++;
         }
-        front.n = 0; VPUSH(front, e->end - 1);
-        ff_end = e->end;
+        front.n = 0; VPUSH(front, s1 - 1);
+        newr.v[si].start = s1;
+        if (s1 == newr.v[si].end) si++;
     }
-    if (ff_end < n && !T.err) {
-        Range rest = { ff_end, n };
-        Walker w; WalkStep st; memset(&st, 0, sizeof st);
-        walker_init(&w, &o->g, &rest, 1);
-        for (i64 q = 0; q < front.n; q++) VPUSH(w.frontier, front.v[q]);   /* SpanningTreeWalker::new(.., frontier) */
-        while (!T.err && walker_next(&w, &st)) {
-            for (i64 i = 0; i < st.retreat.n && !T.err; i++)
-                for (i64 v = st.retreat.v[i].end - 1; v >= st.retreat.v[i].start && !T.err; v--) retreat_lv(&T, v);
-            for (i64 i = st.advance_rev.n - 1; i >= 0 && !T.err; i--)
-                for (i64 v = st.advance_rev.v[i].start; v < st.advance_rev.v[i].end && !T.err; v++) advance_lv(&T, v);
-            for (i64 v = st.consume.start; v < st.consume.end && !T.err; v++) {
-                if (o->kind.v[v] == 0) apply_ins(&T, v, o->pos.v[v]); else apply_del(&T, v, o->pos.v[v]);
-                out[2 * k] = v; out[2 * k + 1] = T.xf; k++;
-            }
-        }
-        walker_free(&w);
-        VFREE(st.retreat); VFREE(st.advance_rev);
-    }
+    if (!T.err && si < newr.n) walk_apply(&T, &o->g, newr.v + si, newr.n - si, &front, out, &k);
     int err = T.err;
-    if (!err && k != n) err = E_CheckoutPanic;
-    VFREE(front);
+    *n_out = k;
+    VFREE(front); VFREE(hist); VFREE(newr); VFREE(none); VFREE(ra); VFREE(rb);
     free(T.t); free(T.state); free(T.ever_deleted); free(T.ol); free(T.orr); free(T.del_target);
     return err;
 }
-
+/* ListOpLog::iter_xf_operations() (src/list/merge.rs:40-48): from ROOT to the tip. */
+EXPORT int dto_xf_operations(const dto_oplog *o, i64 *out) {
+    i64 k = 0;
+    int err = dto_xf_operations_from(o, NULL, 0, o->version.v, (int)o->version.n, out, &k);
+    if (!err && k != o->kind.n) err = E_CheckoutPanic;
+    return err;
+}
 
 /* ------------------------------------------------------------------------------------------ */
 /* graph-tool entry points for the causal_graph fixtures                                      */

@@ -58,6 +58,7 @@ def lib():
                                    ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(Stats)]
         L.dto_free_buf.argtypes = [ctypes.c_void_p]
         L.dto_xf_operations.argtypes = [ctypes.c_void_p, P64]
+        L.dto_xf_operations_from.argtypes = [ctypes.c_void_p, P64, ctypes.c_int, P64, ctypes.c_int, P64, P64]
         L.dto_crc32c.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
         L.dto_crc32c.restype = ctypes.c_uint32
         L.dto_lz4_decompress.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]
@@ -167,6 +168,18 @@ class OpLog:
         if e:
             raise OracleError(e)
         return [(buf[2 * i], buf[2 * i + 1]) for i in range(n)]
+
+    def xf_operations_from(self, frm, merge):
+        """(lv, xf) of iter_xf_operations_from(frm, merge) in TransformedOpsIter order."""
+        n = len(self)
+        buf = (ctypes.c_int64 * max(2, 2 * n))()
+        a = (ctypes.c_int64 * max(1, len(frm)))(*frm)
+        b = (ctypes.c_int64 * max(1, len(merge)))(*merge)
+        k = ctypes.c_int64()
+        e = lib().dto_xf_operations_from(self.h, a, len(frm), b, len(merge), buf, ctypes.byref(k))
+        if e:
+            raise OracleError(e)
+        return [(buf[2 * i], buf[2 * i + 1]) for i in range(k.value)]
 
     def checkout_tip(self, order=0) -> str:
         return self.checkout_tip_bytes(order).decode("utf-8")

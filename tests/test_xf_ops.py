@@ -94,11 +94,9 @@ def test_host_xf_order_matches_oracle(name):
 def test_host_xf_order_synthetic():
     for doc in range(4):
         o = dt_amd.synth_oplog(doc, 2000)
-        ops = o.export("ops").reshape(-1, 4)
         ora = _oracle_copy(o)
         assert o.xf_order() == [lv for lv, _ in ora.xf_operations()], doc
         assert sorted(o.xf_order()) == list(range(len(o)))
-        del ops
 
 
 def _oracle_copy(o):
@@ -174,3 +172,79 @@ def test_gpu_iter_xf_operations_rebuild_the_text(name):
             del s[op[1]:op[1] + op[2]]
     assert n == len(o)
     assert "".join(s) == o.checkout_tip().content()
+
+
+# ---- incremental merges: iter_xf_operations_from / ListBranch::merge ------------------------
+
+def _pairs(o, rng, k):
+    n = len(o)
+    out = []
+    for _ in range(k):
+        a = o.dominators(sorted(rng.sample(range(n), rng.choice([1, 1, 2]))))
+        b = o.dominators(sorted(rng.sample(range(n), rng.choice([1, 1, 2]))))
+        out.append((a, b))
+    out.append(([], o.local_frontier()))
+    out.append((o.local_frontier(), o.local_frontier()))
+    return out
+
+
+def _apply(text, ops):
+    s = text
+    for op in ops:
+        s = s[:op[1]] + s[op[1] + 1:] if op[0] == "D" else s[:op[1]] + op[2] + s[op[1]:]
+    return s
+
+
+@pytest.mark.parametrize("name", ["friendsforever", "git-makefile"])
+def test_oracle_xf_from_rebuilds_the_merged_checkout(name):
+    """The oracle's incremental stream, applied to the checkout at `from`, gives the checkout at
+    find_dominators_2(from, merging) -- the invariant ListBranch::merge relies on."""
+    data = G.dt_bytes(name)
+    ora = OracleOpLog.load_from(data)
+    eng = dt_amd.ListOpLog.load_from(data)
+    ex = _exports(eng)
+    for a, b in _pairs(eng, random.Random(21), 8 if name == "friendsforever" else 1):
+        got = _apply(ora.checkout_bytes(a).decode(), _per_char(ex, ora.xf_operations_from(a, b)))
+        assert got == ora.checkout_bytes(eng.dominators(a, b)).decode(), (a, b)
+
+
+@pytest.mark.parametrize("name", ["friendsforever", "git-makefile", "node_nodecc"])
+def test_host_xf_from_order_matches_oracle(name):
+    data = G.dt_bytes(name)
+    ora = OracleOpLog.load_from(data)
+    eng = dt_amd.ListOpLog.load_from(data)
+    for a, b in _pairs(eng, random.Random(5), 6 if name == "friendsforever" else 1):
+        assert eng.xf_order(a, b) == [lv for lv, _ in ora.xf_operations_from(a, b)], (a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["friendsforever", "git-makefile"])
+def test_gpu_xf_from_matches_oracle(name):
+    data = G.dt_bytes(name)
+    ora = OracleOpLog.load_from(data)
+    eng = dt_amd.ListOpLog.load_from(data)
+    for a, b in _pairs(eng, random.Random(17), 6 if name == "friendsforever" else 2):
+        want = [(lv, None if x < 0 else x) for lv, x in ora.xf_operations_from(a, b)]
+        assert eng.xf_operations_lv(a, b) == want, (a, b)
+
+
+@pytest.mark.gpu
+def test_gpu_branch_merge_applies_transformed_ops():
+    """ListBranch::merge chains (src/list/merge.rs:63-95): every step's content equals the
+    oracle's checkout at the branch's new version; the last merge reaches the golden text."""
+    data = G.dt_bytes("friendsforever")
+    ora = OracleOpLog.load_from(data)
+    o = dt_amd.ListOpLog.load_from(data)
+    rng = random.Random(29)
+    br = dt_amd.ListBranch.new()
+    for _ in range(5):
+        br.merge(o, [rng.randrange(len(o))])
+        assert br.content_bytes() == ora.checkout_bytes(br.local_frontier())
+    br.merge(o, o.local_frontier())
+    assert br.content() == G.trace("friendsforever_flat")["endContent"]
+    for doc in range(2):
+        s = dt_amd.synth_oplog(doc, 2000)
+        sora = _oracle_copy(s)
+        br = dt_amd.ListBranch.new_at_local_version(s, [len(s) // 3])
+        br.merge(s, [2 * len(s) // 3])
+        assert br.content_bytes() == sora.checkout_bytes(br.local_frontier())
