@@ -61,6 +61,7 @@ struct dtgpu_batch {
     DevBuf<uint32_t> d_tlist, d_cbyte, d_aruns, d_pos, d_cv, d_items, d_lists, d_counter;
     DevBuf<unsigned long long> d_ao, d_m2, d_mup;
     DevBuf<uint32_t> d_tup, d_xf;   // transformed-ops batches only
+    bool xf_mode = false;
     DevBuf<uint8_t> d_content, d_out, d_gidx;
     DevBuf<uint32_t> d_fb;   // [0] = count, then the handed-back documents
     DevBuf<DocDesc> d_docs;
@@ -371,6 +372,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     CK(hipStreamSynchronize(s));
 #undef CK
     BatchParams base{};
+    B->xf_mode = xf;
     base.mup = B->d_mup.p;
     base.tup = B->d_tup.p;
     base.xf = B->d_xf.p;
@@ -637,6 +639,7 @@ dtgpu_status stage_device(const uint8_t *const *docs, const size_t *lens, size_t
 
 // Plan (device) then replay, on stream s.
 int launch_all(dtgpu_batch *B, hipStream_t s) {
+    if (B->xf_mode) return launch_replay_xf(B->large, s);
     if (B->n_gpu_planned) {
         int e = launch_plan(B->plan, s);
         if (e) return e;
@@ -892,6 +895,34 @@ dtgpu_status dtgpu_batch_create_from_oplogs(const dtgpu_oplog *const *oplogs, si
     });
     return stage(prep, opts, out);
 }
+dtgpu_status dtgpu_batch_create_xf(const dtgpu_oplog *const *oplogs, size_t n, const dtgpu_batch_opts *opts,
+                                   dtgpu_batch **out) {
+    if (!out || (n && !oplogs)) return DTGPU_ERR_ARG;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return DTGPU_ERR_NO_DEVICE;
+    std::vector<Prepared> prep(n);
+    parallel_for(n, threads_for(opts, n), [&](size_t i) {
+        prep[i].log = oplogs[i]->o;
+        prep[i].log.finish();
+        prep[i].xf_merge = prep[i].log.version;
+        prepare_input(prep[i]);
+    });
+    return stage(prep, opts, out, true);
+}
+dtgpu_status dtgpu_batch_xf_positions(dtgpu_batch *B, size_t i, uint32_t *out, size_t cap, size_t *n_out) {
+    if (!B || i >= B->n || !B->xf_mode) return DTGPU_ERR_ARG;
+    if (B->host_status[i] != OK) return dtgpu_status(B->host_status[i]);
+    const size_t n = size_t(B->n_lv[i]);
+    if (n_out) *n_out = n;
+    if (!out) return DTGPU_OK;
+    if (cap < n) return DTGPU_ERR_ARG;
+    DocResult r;
+    if (hipMemcpyAsync(&r, B->d_results.p + i, sizeof r, hipMemcpyDeviceToHost, B->stream) != hipSuccess ||
+        (n && hipMemcpyAsync(out, B->d_xf.p + B->docs[i].lv_off, n * 4, hipMemcpyDeviceToHost, B->stream) != hipSuccess) ||
+        hipStreamSynchronize(B->stream) != hipSuccess)
+        return DTGPU_ERR_HIP;
+    return r.status == OK ? DTGPU_OK : dtgpu_status(r.status);
+}
 dtgpu_status dtgpu_batch_create_device(const uint8_t *const *docs, const size_t *lens, size_t n,
                                        const dtgpu_batch_opts *opts, dtgpu_batch **out) {
     if (!out || (n && (!docs || !lens))) return DTGPU_ERR_ARG;
@@ -941,7 +972,7 @@ dtgpu_status dtgpu_batch_run_timed(dtgpu_batch *B, float *ms) {
     if (hipEventRecord(B->ev0, B->stream) != hipSuccess) return DTGPU_ERR_HIP;
     if (B->n_gpu_planned && launch_plan(B->plan, B->stream) != OK) return DTGPU_ERR_HIP;
     if (hipEventRecord(B->ev_mid, B->stream) != hipSuccess) return DTGPU_ERR_HIP;
-    int s = launch_replay(B->small, B->large, B->stream, B->n_cu);
+    int s = B->xf_mode ? launch_replay_xf(B->large, B->stream) : launch_replay(B->small, B->large, B->stream, B->n_cu);
     if (s) return dtgpu_status(s);
     if (hipEventRecord(B->ev1, B->stream) != hipSuccess) return DTGPU_ERR_HIP;
     if (hipEventSynchronize(B->ev1) != hipSuccess) return DTGPU_ERR_HIP;

@@ -115,6 +115,8 @@ def lib():
     L.dtgpu_batch_create.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz), sz,
                                      ctypes.POINTER(BatchOpts), ctypes.POINTER(vp)]
     L.dtgpu_batch_create_from_oplogs.argtypes = [ctypes.POINTER(vp), sz, ctypes.POINTER(BatchOpts), ctypes.POINTER(vp)]
+    L.dtgpu_batch_create_xf.argtypes = [ctypes.POINTER(vp), sz, ctypes.POINTER(BatchOpts), ctypes.POINTER(vp)]
+    L.dtgpu_batch_xf_positions.argtypes = [vp, sz, ctypes.POINTER(ctypes.c_uint32), sz, ctypes.POINTER(sz)]
     L.dtgpu_batch_run.argtypes = [vp, vp]
     L.dtgpu_batch_run_timed.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
     L.dtgpu_batch_sync.argtypes = [vp]
@@ -500,14 +502,18 @@ class Batch:
     (dt_prep.hip) on the GPU as well.  Walk planning (dt_plan.hip), replay and materialisation
     (dt_replay.hip) always run on the GPU."""
 
-    def __init__(self, docs=None, oplogs=None, ignore_crc=False, host_threads=0, device=0, staging="host"):
+    def __init__(self, docs=None, oplogs=None, ignore_crc=False, host_threads=0, device=0, staging="host",
+                 xf=False):
+        """xf=True (with oplogs): a transformed-ops batch, every document's iter_xf_operations()
+        computed by the replay (dtgpu_batch_create_xf); read it with xf_positions(i)."""
         L = lib()
         opts = BatchOpts(int(ignore_crc), int(host_threads), int(device))
         out = ctypes.c_void_p()
         if oplogs is not None:
             arr = (ctypes.c_void_p * max(1, len(oplogs)))(*[o._h for o in oplogs])
             self._keep = oplogs
-            _check(L.dtgpu_batch_create_from_oplogs(arr, len(oplogs), ctypes.byref(opts), ctypes.byref(out)))
+            create = L.dtgpu_batch_create_xf if xf else L.dtgpu_batch_create_from_oplogs
+            _check(create(arr, len(oplogs), ctypes.byref(opts), ctypes.byref(out)))
             self.n = len(oplogs)
         else:
             self._keep = list(docs)
@@ -520,6 +526,14 @@ class Batch:
 
     def __len__(self):
         return self.n
+
+    def xf_positions(self, i):
+        """Per-LV BaseMoved positions of document i (xf batches; None = DeleteAlreadyHappened)."""
+        k = ctypes.c_size_t()
+        _check(lib().dtgpu_batch_xf_positions(self._h, i, None, 0, ctypes.byref(k)))
+        buf = (ctypes.c_uint32 * max(1, k.value))()
+        _check(lib().dtgpu_batch_xf_positions(self._h, i, buf, k.value, ctypes.byref(k)))
+        return [None if x == 0xFFFFFFFF else x for x in buf[:k.value]]
 
     def __del__(self):
         h = getattr(self, "_h", None)

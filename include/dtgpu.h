@@ -226,6 +226,14 @@ dtgpu_status dtgpu_batch_checkout(const uint8_t *const *docs, const size_t *lens
  * wrapping.  Computed on device for the RCCL length/hash gather; exported for checking. */
 uint64_t dtgpu_text_hash(const uint8_t *text, size_t len);
 
+/* Transformed-ops batch: every document's iter_xf_operations() (src/list/merge.rs:40-48) on the
+ * GPU, host-planned in TransformedOpsIter order.  dtgpu_batch_run / run_timed replay it (the
+ * merged text is materialised too: dtgpu_batch_text works); dtgpu_batch_xf_positions copies one
+ * document's per-LV BaseMoved positions (indexed by LV, 0xFFFFFFFF = DeleteAlreadyHappened). */
+dtgpu_status dtgpu_batch_create_xf(const dtgpu_oplog *const *oplogs, size_t n_docs, const dtgpu_batch_opts *opts,
+                                   dtgpu_batch **out);
+dtgpu_status dtgpu_batch_xf_positions(dtgpu_batch *batch, size_t doc, uint32_t *out, size_t cap, size_t *n_out);
+
 /* ---- synthetic concurrent documents (BASELINE.json configs[3]) ---------------------------- */
 
 /* Deterministic synthetic document `doc` (seed 0xD1A00000 + doc, 4..16 agents, epochs of
