@@ -3,6 +3,7 @@
 #include "dt_host.hpp"
 
 #include <algorithm>
+#include <functional>
 #include <cstring>
 #include <queue>
 
@@ -812,6 +813,58 @@ Status build_plan(const HostOpLog &o, Plan &plan) {
 }
 
 // ---- transformed-ops plans ----------------------------------------------------------------
+std::vector<uint64_t> parents_at(const HostOpLog &o, uint64_t lv) {   // clone_parents_at_version
+    const GraphEntry &e = o.graph.entries[size_t(o.graph.find_idx(lv))];
+    return lv > e.start ? std::vector<uint64_t>{lv - 1} : e.parents;
+}
+
+// SpanningTreeWalker::new(graph, spans, frontier) + its iteration (txn_trace.rs:114-333):
+// ascending spans split per graph entry; parents outside the input are ignored.  visit(start,
+// end, parents) is called per consumed span in walk order.
+void spanning_walk(const HostOpLog &o, const std::vector<std::pair<uint64_t, uint64_t>> &spans,
+                   const std::function<void(uint64_t, uint64_t, const std::vector<uint64_t> &)> &visit) {
+    struct In { uint64_t start, end; std::vector<uint64_t> parents; std::vector<uint32_t> pidx, cidx; };
+    std::vector<In> in;
+    for (auto sp : spans) {
+        for (uint64_t s = sp.first; s < sp.second;) {
+            const GraphEntry &e = o.graph.entries[size_t(o.graph.find_idx(s))];
+            const uint64_t t = std::min(e.end, sp.second);
+            in.push_back(In{s, t, parents_at(o, s), {}, {}});
+            s = t;
+        }
+    }
+    auto find_in = [&](uint64_t lv) -> int64_t {
+        auto it = std::upper_bound(in.begin(), in.end(), lv, [](uint64_t v, const In &x) { return v < x.end; });
+        return it != in.end() && it->start <= lv ? int64_t(it - in.begin()) : -1;
+    };
+    std::vector<uint32_t> todo;
+    for (size_t i = 0; i < in.size(); i++) {
+        for (uint64_t p : in[i].parents) { const int64_t j = find_in(p); if (j >= 0) in[i].pidx.push_back(uint32_t(j)); }
+        if (in[i].pidx.empty()) todo.push_back(uint32_t(i));
+    }
+    for (size_t i = 0; i < in.size(); i++) for (uint32_t p : in[i].pidx) in[p].cidx.push_back(uint32_t(i));
+    std::reverse(todo.begin(), todo.end());
+    std::vector<uint8_t> visited(in.size(), 0);
+    while (!todo.empty()) {
+        uint32_t idx = todo.back();
+        if (in[idx].parents.size() >= 2) {   // prefer non-merge entries (txn_trace.rs:243-265)
+            int64_t found = -1;
+            for (int64_t ii = int64_t(todo.size()) - 1; ii >= 0; ii--)
+                if (in[todo[size_t(ii)]].parents.size() < 2) { found = ii; break; }
+            if (found >= 0) { idx = todo[size_t(found)]; todo[size_t(found)] = todo.back(); todo.pop_back(); }
+            else todo.pop_back();
+        } else todo.pop_back();
+        visited[idx] = 1;
+        visit(in[idx].start, in[idx].end, in[idx].parents);
+        for (uint32_t c : in[idx].cidx) {
+            if (visited[c]) continue;
+            bool ok = true;
+            for (uint32_t p : in[c].pidx) if (!visited[p]) { ok = false; break; }
+            if (ok) todo.push_back(c);
+        }
+    }
+}
+
 namespace {
 struct XfPlanner {
     const HostOpLog &o;
@@ -849,56 +902,13 @@ struct XfPlanner {
             s = hi;
         }
     }
-    std::vector<uint64_t> parents_at(uint64_t lv) const {   // clone_parents_at_version
-        const GraphEntry &e = o.graph.entries[size_t(o.graph.find_idx(lv))];
-        return lv > e.start ? std::vector<uint64_t>{lv - 1} : e.parents;
-    }
-    // SpanningTreeWalker::new(graph, spans, frontier) + its iteration (txn_trace.rs:114-333):
-    // ascending spans split per graph entry; parents outside the input are ignored.
     void walk(const std::vector<std::pair<uint64_t, uint64_t>> &spans, std::vector<uint64_t> &frontier) {
-        struct In { uint64_t start, end; std::vector<uint64_t> parents; std::vector<uint32_t> pidx, cidx; };
-        std::vector<In> in;
-        for (auto sp : spans) {
-            for (uint64_t s = sp.first; s < sp.second;) {
-                const GraphEntry &e = o.graph.entries[size_t(o.graph.find_idx(s))];
-                const uint64_t t = std::min(e.end, sp.second);
-                in.push_back(In{s, t, parents_at(s), {}, {}});
-                s = t;
-            }
-        }
-        auto find_in = [&](uint64_t lv) -> int64_t {
-            auto it = std::upper_bound(in.begin(), in.end(), lv, [](uint64_t v, const In &x) { return v < x.end; });
-            return it != in.end() && it->start <= lv ? int64_t(it - in.begin()) : -1;
-        };
-        std::vector<uint32_t> todo;
-        for (size_t i = 0; i < in.size(); i++) {
-            for (uint64_t p : in[i].parents) { const int64_t j = find_in(p); if (j >= 0) in[i].pidx.push_back(uint32_t(j)); }
-            if (in[i].pidx.empty()) todo.push_back(uint32_t(i));
-        }
-        for (size_t i = 0; i < in.size(); i++) for (uint32_t p : in[i].pidx) in[p].cidx.push_back(uint32_t(i));
-        std::reverse(todo.begin(), todo.end());
-        std::vector<uint8_t> visited(in.size(), 0);
-        while (!todo.empty()) {
-            uint32_t idx = todo.back();
-            if (in[idx].parents.size() >= 2) {   // prefer non-merge entries (txn_trace.rs:243-265)
-                int64_t found = -1;
-                for (int64_t ii = int64_t(todo.size()) - 1; ii >= 0; ii--)
-                    if (in[todo[size_t(ii)]].parents.size() < 2) { found = ii; break; }
-                if (found >= 0) { idx = todo[size_t(found)]; todo[size_t(found)] = todo.back(); todo.pop_back(); }
-                else todo.pop_back();
-            } else todo.pop_back();
-            visited[idx] = 1;
-            move(frontier, in[idx].parents);
-            apply(in[idx].start, in[idx].end);
-            frontier.assign(1, in[idx].end - 1);
+        spanning_walk(o, spans, [&](uint64_t s, uint64_t e, const std::vector<uint64_t> &parents) {
+            move(frontier, parents);
+            apply(s, e);
+            frontier.assign(1, e - 1);
             plan.n_steps++;
-            for (uint32_t c : in[idx].cidx) {
-                if (visited[c]) continue;
-                bool ok = true;
-                for (uint32_t p : in[c].pidx) if (!visited[p]) { ok = false; break; }
-                if (ok) todo.push_back(c);
-            }
-        }
+        });
     }
 };
 std::vector<std::pair<uint64_t, uint64_t>> ascending(std::vector<std::pair<uint64_t, uint64_t>> v) {
@@ -931,7 +941,7 @@ Status build_xf_plan_from(const HostOpLog &o, const std::vector<uint64_t> &from,
     size_t si = 0;
     while (si < newr.size()) {
         const uint64_t s0 = newr[si].first;
-        if (P.parents_at(s0) != frontier) break;
+        if (parents_at(o, s0) != frontier) break;
         const GraphEntry &e = o.graph.entries[size_t(o.graph.find_idx(s0))];
         const uint64_t s1 = std::min(e.end, newr[si].second);
         P.apply(s0, s1);

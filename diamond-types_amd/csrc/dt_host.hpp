@@ -8,6 +8,7 @@
 //   GraphEntry<- GraphEntryInternal   (src/causalgraph/graph/mod.rs:25-53)
 #pragma once
 #include <cstdint>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -72,6 +73,9 @@ struct HostOpLog {
 // ListOpLog::load_from (src/list/encoding/decode_oplog.rs:447-960)
 Status decode_dt(const uint8_t *data, size_t len, bool ignore_crc, HostOpLog &out);
 uint32_t crc32c(const uint8_t *d, size_t n);
+// ListOpLog::encode_from (src/list/encoding/encode_oplog.rs:404-747), content uncompressed.
+Status encode_dt(const HostOpLog &o, const std::vector<uint64_t> &from, bool store_inserted_content,
+                 bool store_start_branch_content, std::vector<uint8_t> &result);
 bool lz4_block_decompress(const uint8_t *src, size_t n, uint8_t *dst, size_t out_len);
 bool utf8_valid(const uint8_t *s, size_t n);
 inline uint32_t utf8_len(uint8_t c) { return c < 0x80 ? 1 : (c & 0xE0) == 0xC0 ? 2 : (c & 0xF0) == 0xE0 ? 3 : 4; }
@@ -98,6 +102,11 @@ struct Plan {
 Status build_plan(const HostOpLog &o, Plan &plan);
 // The order TransformedOpsIter applies ops in for iter_xf_operations (src/list/merge.rs:24-48;
 // src/listmerge/merge.rs:788-940): the fast-forward prefix, then the walker from its frontier.
+// SpanningTreeWalker over ascending spans (txn_trace.rs:114-333): visit(start, end, parents) per
+// consumed span in walk order (Graph::optimized_txns_between when spans = diff from a version).
+void spanning_walk(const HostOpLog &o, const std::vector<std::pair<uint64_t, uint64_t>> &spans,
+                   const std::function<void(uint64_t, uint64_t, const std::vector<uint64_t> &)> &visit);
+std::vector<uint64_t> parents_at(const HostOpLog &o, uint64_t lv);
 Status build_xf_plan(const HostOpLog &o, Plan &plan);
 // iter_xf_operations_from(from, merge) (src/list/merge.rs:24-38): the walk that rebuilds the
 // branch at `from` (not reported), then the new ops Hist(merge) - Hist(from) in

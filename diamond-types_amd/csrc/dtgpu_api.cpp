@@ -760,6 +760,24 @@ size_t dtgpu_oplog_plan_commands(const dtgpu_oplog *h, uint32_t *cmds, size_t ca
     return p.plan.cmds.size();
 }
 
+dtgpu_status dtgpu_oplog_encode(const dtgpu_oplog *h, const uint64_t *from, size_t n_from, uint32_t flags, uint8_t *out,
+                                size_t cap, size_t *out_len) {
+    if (!h || (n_from && !from)) return DTGPU_ERR_ARG;
+    if (flags & ~uint32_t(DTGPU_ENCODE_STORE_INSERTED_CONTENT)) return DTGPU_ERR_ARG;   // see dtgpu.h
+    std::vector<uint64_t> f(n_from + 1);
+    const int64_t nf = dtgpu_oplog_dominators(h, from, n_from, nullptr, 0, f.data(), f.size());
+    if (nf < 0) return DTGPU_ERR_ARG;
+    f.resize(size_t(nf));
+    std::vector<uint8_t> bytes;
+    const Status st = encode_dt(h->o, f, (flags & DTGPU_ENCODE_STORE_INSERTED_CONTENT) != 0, false, bytes);
+    if (st != OK) return dtgpu_status(st);
+    if (out_len) *out_len = bytes.size();
+    if (!out) return DTGPU_OK;
+    if (cap < bytes.size()) return DTGPU_ERR_ARG;
+    std::memcpy(out, bytes.data(), bytes.size());
+    return DTGPU_OK;
+}
+
 size_t dtgpu_oplog_xf_order(const dtgpu_oplog *h, const uint64_t *from, size_t n_from, const uint64_t *merge,
                             size_t n_merge, uint32_t *out, size_t cap) {
     if (!h || (n_from && !from) || (n_merge && !merge)) return 0;

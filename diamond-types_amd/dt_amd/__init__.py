@@ -107,6 +107,7 @@ def lib():
     L.dtgpu_oplog_dominators.argtypes = [vp, pu64, sz, pu64, sz, pu64, sz]
     L.dtgpu_oplog_dominators.restype = ctypes.c_int64
     L.dtgpu_oplog_history.argtypes = [vp, pu64, sz, ctypes.POINTER(vp)]
+    L.dtgpu_oplog_encode.argtypes = [vp, pu64, sz, ctypes.c_uint32, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
     L.dtgpu_xf_operations.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32), sz, ctypes.POINTER(sz)]
     L.dtgpu_oplog_xf_order.argtypes = [vp, pu64, sz, pu64, sz, ctypes.POINTER(ctypes.c_uint32), sz]
     L.dtgpu_oplog_xf_order.restype = sz
@@ -421,6 +422,20 @@ class ListOpLog:
         if cur[3] == 0:
             return rng, ("ins", cur[4], cur[6])
         return rng, ("del", min(cur[4], cur[5]), cur[1] - cur[0])
+
+    def encode(self, store_inserted_content=True) -> bytes:
+        """ListOpLog::encode (src/list/encoding/encode_oplog.rs:745-747), content uncompressed."""
+        return self.encode_from([], store_inserted_content)
+
+    def encode_from(self, frm, store_inserted_content=True) -> bytes:
+        """ListOpLog::encode_from (encode_oplog.rs:404-743): the ops after version `frm`."""
+        p, nf = _u64s(frm)
+        flags = 1 if store_inserted_content else 0
+        n = ctypes.c_size_t()
+        _check(lib().dtgpu_oplog_encode(self._h, p, nf, flags, None, 0, ctypes.byref(n)))
+        buf = ctypes.create_string_buffer(max(1, n.value))
+        _check(lib().dtgpu_oplog_encode(self._h, p, nf, flags, buf, n.value, ctypes.byref(n)))
+        return buf.raw[:n.value]
 
     def dominators(self, a, b=()):
         """Graph::find_dominators_2 (src/causalgraph/graph/tools.rs:545-578) over this oplog."""

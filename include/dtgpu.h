@@ -78,6 +78,17 @@ int64_t dtgpu_oplog_add_delete_at(dtgpu_oplog *oplog, int32_t agent, const uint6
 int64_t dtgpu_oplog_add_insert(dtgpu_oplog *oplog, int32_t agent, uint64_t pos, const char *utf8, size_t n_bytes);
 int64_t dtgpu_oplog_add_delete_without_content(dtgpu_oplog *oplog, int32_t agent, uint64_t del_start, uint64_t del_end);
 
+/* ListOpLog::encode(opts) / encode_from(opts, from) (src/list/encoding/encode_oplog.rs:404-747):
+ * the `.dt` bytes of the ops after `from` (an empty `from` is ROOT: the whole oplog).  Written in
+ * the reference's order (Graph::optimized_txns_between) through the reference's run mergers, so
+ * the bytes equal the reference encoder's when its content is not LZ4-compressed.  Content is
+ * written uncompressed (lz4_flex's compressor is not reproduced; every reader accepts it).
+ * flags: DTGPU_ENCODE_STORE_INSERTED_CONTENT (EncodeOptions::store_inserted_content, set in
+ * ENCODE_FULL / ENCODE_PATCH).  out == NULL returns the size in *out_len. */
+#define DTGPU_ENCODE_STORE_INSERTED_CONTENT 1u
+dtgpu_status dtgpu_oplog_encode(const dtgpu_oplog *oplog, const uint64_t *from, size_t n_from, uint32_t flags,
+                                uint8_t *out, size_t cap, size_t *out_len);
+
 /* ListOpLog::len() (src/list/oplog.rs:89-91) */
 size_t dtgpu_oplog_len(const dtgpu_oplog *oplog);
 /* ListOpLog::local_frontier() (src/list/oplog.rs:329-331).  Returns the frontier length;
