@@ -275,6 +275,12 @@ Status encode_dt(const HostOpLog &o, const std::vector<uint64_t> &from, bool sto
     }
     // ---- file info ----
     std::vector<uint8_t> fileinfo;
+    if (o.has_doc_id) {   // write_chunk_str (encode_oplog.rs:311-318, 639-641)
+        std::vector<uint8_t> d;
+        leb(d, PLAIN_TEXT);
+        d.insert(d.end(), o.doc_id.begin(), o.doc_id.end());
+        chunk(fileinfo, C_DocId, d);
+    }
     chunk(fileinfo, C_AgentNames, am.names);
     // ---- patches ----
     std::vector<uint8_t> patches;

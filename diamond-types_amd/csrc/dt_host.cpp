@@ -434,9 +434,58 @@ void HostOpLog::finish() {
 }
 
 // ------------------------------------------------------------------------------------------
-// .dt decode (src/list/encoding/decode_oplog.rs:590-960)
+// .dt decode (src/list/encoding/decode_oplog.rs:476-960)
 // ------------------------------------------------------------------------------------------
-Status decode_dt(const uint8_t *data, size_t len, bool ignore_crc, HostOpLog &o) {
+namespace {
+
+constexpr uint64_t UNDERWATER = ~uint64_t(0) / 4;   // UNDERWATER_START (src/dtrange.rs:197)
+
+// Frontier::advance_by_known_run (src/frontier.rs:251-279); false where the reference asserts.
+bool advance_known_run(std::vector<uint64_t> &ver, const std::vector<uint64_t> &par, uint64_t start, uint64_t end) {
+    const uint64_t last = end - 1;
+    if (par.size() == 1 && ver.size() == 1 && par[0] == ver[0]) { ver[0] = last; return true; }
+    if (ver == par) { ver.assign(1, last); return true; }
+    if (std::find(ver.begin(), ver.end(), start) != ver.end()) return false;
+    std::vector<uint64_t> nv;
+    for (uint64_t v : ver) if (std::find(par.begin(), par.end(), v) == par.end()) nv.push_back(v);
+    nv.insert(std::upper_bound(nv.begin(), nv.end(), last), last);
+    ver.swap(nv);
+    return true;
+}
+
+// version_map of decode_internal (decode_oplog.rs:717-727): file time -> local LV, RLE
+struct VMap { uint64_t file, local, len; };
+void vmap_push(std::vector<VMap> &vm, uint64_t file, uint64_t local, uint64_t len) {
+    if (!vm.empty()) {
+        VMap &l = vm.back();
+        if (l.file + l.len == file && l.local + l.len == local) { l.len += len; return; }
+    }
+    vm.push_back(VMap{file, local, len});
+}
+const VMap *vmap_find(const std::vector<VMap> &vm, uint64_t file) {   // find_packed_with_offset
+    auto it = std::upper_bound(vm.begin(), vm.end(), file, [](uint64_t f, const VMap &m) { return f < m.file; });
+    if (it == vm.begin()) return nullptr;
+    --it;
+    return file < it->file + it->len ? &*it : nullptr;
+}
+
+// ClientData::item_times.find_sparse (decode_oplog.rs:811-819): the known run holding `seq`
+// (its LV), or the end of the unknown gap starting at `seq`.
+bool seq_find_sparse(const HostOpLog &o, uint32_t agent, uint64_t seq, uint64_t &lv, uint64_t &run_end) {
+    uint64_t gap_end = ~uint64_t(0);
+    for (const SeqRun &r : o.agent_seqs[agent]) {
+        if (seq >= r.seq && seq < r.seq + r.len) { lv = r.lv + (seq - r.seq); run_end = r.seq + r.len; return true; }
+        if (r.seq > seq) gap_end = std::min(gap_end, r.seq);
+    }
+    run_end = gap_end;
+    return false;
+}
+
+// decode_internal (decode_oplog.rs:590-960) into `o`, which may already hold operations: the
+// overlap filter (:706-850) drops what `o` already has; `file_frontier` gets the file's version.
+// On error `o` is left partially modified: decode_and_add unwinds it.
+Status decode_into(const uint8_t *data, size_t len, bool ignore_crc, HostOpLog &o,
+                   std::vector<uint64_t> &file_frontier) {
     Reader r{data, len};
     if (r.n < 8) return UnexpectedEOF;
     if (std::memcmp(r.p, "DMNDTYPS", 8) != 0) return InvalidMagic;
@@ -465,17 +514,18 @@ Status decode_dt(const uint8_t *data, size_t len, bool ignore_crc, HostOpLog &o)
 
     struct AMap { uint32_t agent; uint64_t seq; };
     std::vector<AMap> amap;
-    {   // FileInfo (decode_oplog.rs:197-227)
-        Reader fi, an, tmp;
+    {   // FileInfo (decode_oplog.rs:197-227, 638-649)
+        Reader fi, an, tmp, did;
         bool found;
         if (Status s = expect_chunk(r, C_FileInfo, fi)) return s;
-        if (Status s = chunk_if(fi, C_DocId, found, tmp)) return s;
-        if (found) {
+        if (Status s = chunk_if(fi, C_DocId, found, did)) return s;
+        if (found) {   // into_content_str (decode_tools.rs:133-144)
             uint64_t dt;
-            if (Status s = tmp.u32v(dt)) return s;
+            if (Status s = did.u32v(dt)) return s;
             if (dt != 4) return UnknownChunk;
-            if (!utf8_valid(tmp.p, tmp.n)) return InvalidUTF8;
+            if (!utf8_valid(did.p, did.n)) return InvalidUTF8;
         }
+        const bool has_did = found;
         if (Status s = expect_chunk(fi, C_AgentNames, an)) return s;
         if (Status s = chunk_if(fi, C_UserData, found, tmp)) return s;
         while (!an.empty()) {
@@ -489,23 +539,33 @@ Status decode_dt(const uint8_t *data, size_t len, bool ignore_crc, HostOpLog &o)
             if (id < 0) return ErrCheckout;
             amap.push_back(AMap{uint32_t(id), 0});
         }
+        if (has_did) {   // a doc id must match a non-empty oplog's
+            std::string id(reinterpret_cast<const char *>(did.p), did.n);
+            if (o.has_doc_id && id != o.doc_id && o.n_lv != 0) return DocIdMismatch;
+            o.doc_id.swap(id);
+            o.has_doc_id = true;
+        }
     }
-    {   // StartBranch (decode_oplog.rs:652-664)
+    std::vector<uint64_t> start_version;
+    {   // StartBranch (decode_oplog.rs:652-664), read_version (:70-93)
         Reader sb, ver;
         bool found;
         if (Status s = expect_chunk(r, C_StartBranch, sb)) return s;
         if (Status s = chunk_if(sb, C_Version, found, ver)) return s;
-        if (found) {   // read_version: any named version is unknown to a fresh oplog
+        if (found) {
             for (;;) {
                 uint64_t n, seq;
                 if (Status s = ver.u64v(n)) return s;
                 if (Status s = ver.u64v(seq)) return s;
                 if ((n >> 1) == 0) break;
                 if ((n >> 1) - 1 >= amap.size()) return InvalidLength;
-                if (o.seq_to_lv(amap[size_t((n >> 1) - 1)].agent, seq) < 0) return BaseVersionUnknown;
+                const int64_t lv = o.seq_to_lv(amap[size_t((n >> 1) - 1)].agent, seq);
+                if (lv < 0) return BaseVersionUnknown;
+                start_version.push_back(uint64_t(lv));
                 if (!(n & 1)) break;
             }
             if (!ver.empty()) return InvalidLength;
+            std::sort(start_version.begin(), start_version.end());
         }
         if (!sb.empty()) {
             const uint8_t *s; size_t sn;
@@ -539,9 +599,15 @@ Status decode_dt(const uint8_t *data, size_t len, bool ignore_crc, HostOpLog &o)
     uint64_t op_len = 0;
     int64_t op_start = 0;
     bool op_del = false, op_fwd = true;
-    uint64_t next_assign = 0;
+    // The file continues this oplog's version, or its operations must be filtered against what
+    // the oplog already has (patches_overlap, decode_oplog.rs:670; file times go underwater).
+    const bool overlap = start_version != o.version;
+    const uint64_t first_new = o.n_lv;
+    const uint64_t new_op_start = overlap ? UNDERWATER : first_new;
+    uint64_t next_assign = first_new, next_file = new_op_start;
+    std::vector<VMap> vm;
 
-    while (!av.empty()) {   // read_next_agent_assignment (decode_oplog.rs:29-68)
+    while (!av.empty()) {   // read_next_agent_assignment (decode_oplog.rs:29-68, 780-850)
         uint64_t n, alen;
         int64_t jump = 0;
         if (Status s = av.u64v(n)) return s;
@@ -551,12 +617,24 @@ Status decode_dt(const uint8_t *data, size_t len, bool ignore_crc, HostOpLog &o)
         if (has_jump) { if (Status s = av.zigzag(jump)) return s; }
         if (n == 0 || n - 1 >= amap.size()) return InvalidLength;
         AMap &m = amap[size_t(n - 1)];
-        const uint64_t sstart = uint64_t(int64_t(m.seq) + jump);
-        m.seq = sstart + alen;
-        o.assign(m.agent, sstart, next_assign, alen);
-        next_assign += alen;
+        uint64_t sstart = uint64_t(int64_t(m.seq) + jump);
+        const uint64_t send = sstart + alen;
+        m.seq = send;
+      while (sstart < send) {
+        uint64_t known_lv = 0, run_end = send;
+        const bool keep = !overlap || !seq_find_sparse(o, m.agent, sstart, known_lv, run_end);
+        const uint64_t l = std::min(send, run_end) - sstart;
+        if (keep) {
+            o.assign(m.agent, sstart, next_assign, l);
+            vmap_push(vm, next_file, next_assign, l);
+            next_assign += l;
+        } else {   // already here: map the file's items onto the local ones
+            vmap_push(vm, next_file, known_lv, l);
+        }
+        next_file += l;
+        sstart += l;
 
-        uint64_t want = alen;   // parse_next_patches (decode_oplog.rs:731-778)
+        uint64_t want = l;   // parse_next_patches (decode_oplog.rs:731-778)
         while (want) {
             if (!have_op) {
                 if (tp.empty()) return InvalidLength;
@@ -607,8 +685,9 @@ Status decode_dt(const uint8_t *data, size_t len, bool ignore_crc, HostOpLog &o)
             }
             if (!take) return ErrCheckout;
             if (!op_del) {
-                o.push_ins(uint64_t(op_start), cs, csn, take, known);
+                if (keep) o.push_ins(uint64_t(op_start), cs, csn, take, known);
                 op_start += int64_t(take);
+            } else if (!keep) {
             } else if (op_fwd) {
                 o.push_del(uint64_t(op_start), take, true);
             } else {
@@ -618,12 +697,16 @@ Status decode_dt(const uint8_t *data, size_t len, bool ignore_crc, HostOpLog &o)
             if (!op_len) have_op = false;
             want -= take;
         }
+      }
     }
     if (o.n_lv != next_assign) return InvalidLength;
+    const uint64_t file_end = next_file;
 
-    // OpParents (decode_oplog.rs:95-148, 856-913): fresh load => identity version map
-    uint64_t next_file = 0;
-    std::vector<uint64_t> par;
+    // OpParents (decode_oplog.rs:95-148, 856-913)
+    next_file = new_op_start;
+    uint64_t next_hist = first_new;
+    file_frontier = start_version;
+    std::vector<uint64_t> par, mp;
     while (!hist.empty()) {
         uint64_t hl;
         if (Status s = hist.u64v(hl)) return s;
@@ -643,32 +726,50 @@ Status decode_dt(const uint8_t *data, size_t len, bool ignore_crc, HostOpLog &o)
                 if (lv < 0) return InvalidLength;
                 p = uint64_t(lv);
             } else {   // next_time - n: an out-of-range value fails the range check below
+                if (overlap && n > next_file - new_op_start) return InvalidLength;   // would surface from underwater
                 p = next_file - n;
             }
             par.push_back(p);
             if (!more) break;
         }
         std::sort(par.begin(), par.end());
-        if (hl == 0 || next_file + hl > next_assign) return InvalidLength;
+        if (hl == 0 || next_file + hl > file_end) return InvalidLength;
         for (uint64_t p : par) if (p >= next_file) return InvalidLength;
-        // graph.push + cg.version.advance_by_known_run, without the agent assignment
-        o.graph.push(par, next_file, next_file + hl);
-        {
-            const uint64_t last = next_file + hl - 1;
-            auto &ver = o.version;
-            if (par.size() == 1 && ver.size() == 1 && par[0] == ver[0]) ver[0] = last;
-            else if (ver == par) ver.assign(1, last);
-            else {
-                std::vector<uint64_t> nv;
-                for (uint64_t v : ver) if (std::find(par.begin(), par.end(), v) == par.end()) nv.push_back(v);
-                nv.push_back(last);
-                std::sort(nv.begin(), nv.end());
-                ver.swap(nv);
+        // history_entry_map_and_truncate (decode_oplog.rs:241-269), one mapped piece at a time
+        uint64_t es = next_file;
+        const uint64_t ee = next_file + hl;
+        next_file = ee;
+        for (;;) {
+            const VMap *m = vmap_find(vm, es);
+            if (!m) return InvalidLength;
+            const uint64_t take = std::min(ee - es, m->len - (es - m->file));
+            uint64_t ms = m->local + (es - m->file);
+            const uint64_t me = ms + take;
+            mp.clear();
+            for (uint64_t p : par) {
+                if (p >= UNDERWATER) {
+                    const VMap *pm = vmap_find(vm, p);
+                    if (!pm) return InvalidLength;
+                    p = pm->local + (p - pm->file);
+                }
+                mp.push_back(p);
             }
+            std::sort(mp.begin(), mp.end());
+            if (!advance_known_run(file_frontier, mp, ms, me)) return InvalidLength;
+            if (me > next_hist) {   // new here: graph.push + cg.version.advance_by_known_run
+                if (ms > next_hist) return InvalidLength;   // assert!(mapped.span.start <= next_history_time)
+                if (ms < next_hist) { mp.assign(1, next_hist - 1); ms = next_hist; }   // truncate_keeping_right
+                for (uint64_t p : mp) if (p >= ms) return InvalidLength;
+                o.graph.push(mp, ms, me);
+                if (!advance_known_run(o.version, mp, ms, me)) return InvalidLength;
+                next_hist = me;
+            }
+            es += take;
+            if (es == ee) break;
+            par.assign(1, es - 1);   // GraphEntrySimple::trim: the remainder's parent, unmapped
         }
-        next_file += hl;
     }
-    if (next_file != next_assign) return InvalidLength;
+    if (next_file != file_end || next_hist != next_assign) return InvalidLength;
     if (!pc.empty()) return InvalidLength;
     if (ins.present) {
         bool has; uint64_t l; bool k; const uint8_t *s; size_t sn;
@@ -693,6 +794,24 @@ Status decode_dt(const uint8_t *data, size_t len, bool ignore_crc, HostOpLog &o)
     }
     o.finish();
     return OK;
+}
+
+}  // namespace
+
+Status decode_dt(const uint8_t *data, size_t len, bool ignore_crc, HostOpLog &o) {
+    std::vector<uint64_t> frontier;
+    return decode_into(data, len, ignore_crc, o, frontier);
+}
+
+// ListOpLog::decode_and_add_opts (decode_oplog.rs:476-583): on error the oplog is unwound to
+// what it was before the call (the reference truncates each structure back to its old length;
+// here the prior state is restored wholesale, with the same result).
+Status decode_and_add(const uint8_t *data, size_t len, bool ignore_crc, HostOpLog &o,
+                      std::vector<uint64_t> &file_frontier) {
+    HostOpLog before = o;
+    const Status s = decode_into(data, len, ignore_crc, o, file_frontier);
+    if (s != OK) { o = std::move(before); file_frontier.clear(); }
+    return s;
 }
 
 // ------------------------------------------------------------------------------------------

@@ -59,6 +59,8 @@ struct HostOpLog {
     Graph graph;
     std::vector<uint64_t> version;                 // cg.version (frontier)
     uint64_t n_lv = 0;
+    std::string doc_id;                            // ListOpLog::doc_id (src/list/mod.rs:109)
+    bool has_doc_id = false;
 
     int32_t agent_id(const char *name, size_t len);          // get_or_create_agent_id
     uint64_t next_seq(uint32_t agent) const;
@@ -72,6 +74,11 @@ struct HostOpLog {
 
 // ListOpLog::load_from (src/list/encoding/decode_oplog.rs:447-960)
 Status decode_dt(const uint8_t *data, size_t len, bool ignore_crc, HostOpLog &out);
+// ListOpLog::decode_and_add_opts (decode_oplog.rs:476-583): merge a `.dt` patch into `o`, skipping
+// the operations it already has; `file_frontier` = the version of the loaded data.  On error `o`
+// is unchanged.
+Status decode_and_add(const uint8_t *data, size_t len, bool ignore_crc, HostOpLog &o,
+                      std::vector<uint64_t> &file_frontier);
 uint32_t crc32c(const uint8_t *d, size_t n);
 // ListOpLog::encode_from (src/list/encoding/encode_oplog.rs:404-747), content uncompressed.
 Status encode_dt(const HostOpLog &o, const std::vector<uint64_t> &from, bool store_inserted_content,

@@ -662,6 +662,29 @@ dtgpu_status dtgpu_oplog_load(const uint8_t *bytes, size_t len, int ignore_crc, 
 }
 dtgpu_oplog *dtgpu_oplog_new(void) { return new dtgpu_oplog(); }
 void dtgpu_oplog_free(dtgpu_oplog *o) { delete o; }
+dtgpu_status dtgpu_oplog_decode_and_add(dtgpu_oplog *h, const uint8_t *bytes, size_t len, int ignore_crc,
+                                        uint64_t *frontier, size_t cap, size_t *n_frontier) {
+    if (!h || (!bytes && len) || (!frontier && cap)) return DTGPU_ERR_ARG;
+    std::vector<uint64_t> f;
+    const Status s = decode_and_add(bytes, len, ignore_crc != 0, h->o, f);
+    if (s != OK) return dtgpu_status(s);
+    for (size_t i = 0; i < f.size() && i < cap; i++) frontier[i] = f[i];
+    if (n_frontier) *n_frontier = f.size();
+    return DTGPU_OK;
+}
+int64_t dtgpu_oplog_doc_id(const dtgpu_oplog *h, char *out, size_t cap) {
+    if (!h || !h->o.has_doc_id) return -1;
+    if (out) std::memcpy(out, h->o.doc_id.data(), std::min(cap, h->o.doc_id.size()));
+    return int64_t(h->o.doc_id.size());
+}
+dtgpu_status dtgpu_oplog_set_doc_id(dtgpu_oplog *h, const char *id, size_t len) {
+    if (!h) return DTGPU_ERR_ARG;
+    if (!id) { h->o.doc_id.clear(); h->o.has_doc_id = false; return DTGPU_OK; }
+    if (!utf8_valid(reinterpret_cast<const uint8_t *>(id), len)) return DTGPU_ERR_ARG;
+    h->o.doc_id.assign(id, len);
+    h->o.has_doc_id = true;
+    return DTGPU_OK;
+}
 int32_t dtgpu_oplog_get_or_create_agent_id(dtgpu_oplog *o, const char *name, size_t len) {
     if (!o || (!name && len)) return -1;
     return o->o.agent_id(name, len);

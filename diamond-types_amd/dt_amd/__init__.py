@@ -108,6 +108,10 @@ def lib():
     L.dtgpu_oplog_dominators.restype = ctypes.c_int64
     L.dtgpu_oplog_history.argtypes = [vp, pu64, sz, ctypes.POINTER(vp)]
     L.dtgpu_oplog_encode.argtypes = [vp, pu64, sz, ctypes.c_uint32, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
+    L.dtgpu_oplog_decode_and_add.argtypes = [vp, ctypes.c_char_p, sz, c, pu64, sz, ctypes.POINTER(sz)]
+    L.dtgpu_oplog_doc_id.argtypes = [vp, ctypes.c_char_p, sz]
+    L.dtgpu_oplog_doc_id.restype = ctypes.c_int64
+    L.dtgpu_oplog_set_doc_id.argtypes = [vp, ctypes.c_char_p, sz]
     L.dtgpu_xf_operations.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32), sz, ctypes.POINTER(sz)]
     L.dtgpu_oplog_xf_order.argtypes = [vp, pu64, sz, pu64, sz, ctypes.POINTER(ctypes.c_uint32), sz]
     L.dtgpu_oplog_xf_order.restype = sz
@@ -255,6 +259,40 @@ class ListOpLog:
         out = ctypes.c_void_p()
         _check(lib().dtgpu_oplog_load(data, len(data), int(ignore_crc), ctypes.byref(out)))
         return cls(out.value)
+
+    def decode_and_add(self, data: bytes, ignore_crc: bool = False):
+        """ListOpLog::decode_and_add(_opts) (src/list/encoding/decode_oplog.rs:465-583): merge a
+        `.dt` file or patch, skipping operations already here; returns the file's version.  On a
+        ParseError the oplog is left as it was."""
+        cap = 64
+        while True:
+            buf = (ctypes.c_uint64 * cap)()
+            n = ctypes.c_size_t()
+            _check(lib().dtgpu_oplog_decode_and_add(self._h, data, len(data), int(ignore_crc), buf, cap,
+                                                    ctypes.byref(n)))
+            if n.value <= cap:
+                return list(buf[:n.value])
+            # a wider version than the buffer: merging the same data again adds nothing and
+            # reports the version in full
+            cap = n.value
+
+    @property
+    def doc_id(self):
+        """ListOpLog::doc_id (src/list/mod.rs:109): None or the document id string."""
+        n = lib().dtgpu_oplog_doc_id(self._h, None, 0)
+        if n < 0:
+            return None
+        buf = ctypes.create_string_buffer(max(1, n))
+        lib().dtgpu_oplog_doc_id(self._h, buf, n)
+        return buf.raw[:n].decode()
+
+    @doc_id.setter
+    def doc_id(self, value):
+        if value is None:
+            _check(lib().dtgpu_oplog_set_doc_id(self._h, None, 0))
+        else:
+            b = value.encode()
+            _check(lib().dtgpu_oplog_set_doc_id(self._h, b, len(b)))
 
     def __len__(self):
         return lib().dtgpu_oplog_len(self._h)

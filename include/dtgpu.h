@@ -64,6 +64,19 @@ dtgpu_status dtgpu_oplog_load(const uint8_t *bytes, size_t len, int ignore_crc, 
 dtgpu_oplog *dtgpu_oplog_new(void);
 void dtgpu_oplog_free(dtgpu_oplog *oplog);
 
+/* ListOpLog::decode_and_add_opts(&[u8], DecodeOptions) -> Result<Frontier, ParseError>
+ * (src/list/encoding/decode_oplog.rs:476-583): merge a `.dt` file or patch into the oplog,
+ * skipping the operations it already has (the overlap filter, :780-850).  On success writes the
+ * file's version (min(len, cap) LVs, ascending) and its length in *n_frontier.  On error the
+ * oplog is unchanged (the reference unwinds the partial merge) and the ParseError is returned.
+ * Not safe to call while another thread reads the same oplog. */
+dtgpu_status dtgpu_oplog_decode_and_add(dtgpu_oplog *oplog, const uint8_t *bytes, size_t len, int ignore_crc,
+                                        uint64_t *frontier, size_t cap, size_t *n_frontier);
+/* ListOpLog::doc_id (src/list/mod.rs:109): returns the id's byte length (copying min(len, cap)
+ * bytes), or -1 when the oplog has none.  set_doc_id with id == NULL clears it. */
+int64_t dtgpu_oplog_doc_id(const dtgpu_oplog *oplog, char *out, size_t cap);
+dtgpu_status dtgpu_oplog_set_doc_id(dtgpu_oplog *oplog, const char *id, size_t len);
+
 /* ListOpLog::get_or_create_agent_id (src/list/oplog.rs:44-46).  Returns -1 on a reserved or
  * over-long name (the reference panics: agent_assignment/mod.rs:88-91). */
 int32_t dtgpu_oplog_get_or_create_agent_id(dtgpu_oplog *oplog, const char *name, size_t name_len);
