@@ -1227,6 +1227,132 @@ static Status history_oplog(const HostOpLog &o, const std::vector<uint64_t> &ver
     return OK;
 }
 
+// TextInfo::merge_into's subgraph (src/listmerge/merge.rs:954-1054 via Graph::subgraph_raw and
+// project_onto_subgraph_raw, src/causalgraph/graph/subgraph.rs:39-250): the ops of one text CRDT
+// are the LV spans `T` of a shared causal graph; the text is checked out over the graph
+// projected onto T, where a version's projection is the frontier of Hist(version) n T.  The
+// sub-oplog is compacted like history_oplog (agents, seqs and positions kept: a text op's
+// position is relative to that text alone), so the same device path checks it out.
+static Status project_oplog(const HostOpLog &o, std::vector<std::pair<uint64_t, uint64_t>> spans, HostOpLog &s) {
+    std::sort(spans.begin(), spans.end());
+    std::vector<std::pair<uint64_t, uint64_t>> t;   // merged, non-empty
+    for (auto r : spans) {
+        if (r.first > r.second || r.second > o.n_lv) return ErrArg;
+        if (r.first == r.second) continue;
+        if (!t.empty() && r.first <= t.back().second) t.back().second = std::max(t.back().second, r.second);
+        else t.push_back(r);
+    }
+    std::vector<uint64_t> base(t.size());
+    uint64_t nn = 0;
+    for (size_t i = 0; i < t.size(); i++) { base[i] = nn; nn += t[i].second - t[i].first; }
+    auto span_of = [&](uint64_t lv) -> int64_t {   // last span starting at or before lv
+        return int64_t(std::upper_bound(t.begin(), t.end(), lv, [](uint64_t v, const std::pair<uint64_t, uint64_t> &r) {
+                           return v < r.first; }) - t.begin()) - 1;
+    };
+    auto map = [&](uint64_t lv) -> uint64_t { const int64_t i = span_of(lv); return base[size_t(i)] + (lv - t[size_t(i)].first); };
+    // Projection of a version: walk back from each member; inside an entry the LVs form a chain,
+    // so the latest member of T at or below the walked LV (and not below the entry start) is a
+    // candidate, otherwise the walk continues at the entry's parents.  The frontier is the
+    // candidates not in the history of another candidate.
+    auto project = [&](const std::vector<uint64_t> &ver) -> std::vector<uint64_t> {
+        std::vector<uint64_t> stack(ver), cand;
+        std::vector<uint8_t> seen(o.graph.entries.size(), 0);
+        while (!stack.empty()) {
+            const uint64_t v = stack.back();
+            stack.pop_back();
+            const int64_t ei = o.graph.find_idx(v);
+            if (ei < 0) continue;
+            const GraphEntry &e = o.graph.entries[size_t(ei)];
+            const int64_t si = span_of(v);
+            if (si >= 0 && t[size_t(si)].second > e.start) {
+                const uint64_t c = std::min(v, t[size_t(si)].second - 1);
+                if (c >= e.start) { cand.push_back(c); continue; }
+            }
+            if (seen[size_t(ei)]) continue;   // the entry's parents were walked already
+            seen[size_t(ei)] = 1;
+            for (uint64_t p : e.parents) stack.push_back(p);
+        }
+        std::sort(cand.begin(), cand.end());
+        cand.erase(std::unique(cand.begin(), cand.end()), cand.end());
+        std::vector<uint64_t> dom;
+        std::vector<std::pair<uint64_t, uint64_t>> only_a, only_b;
+        for (uint64_t c : cand) {
+            bool dominated = false;
+            for (uint64_t d : cand) {
+                if (d <= c) continue;
+                o.graph.diff_rev({c}, {d}, only_a, only_b);
+                if (only_a.empty()) { dominated = true; break; }
+            }
+            if (!dominated) dom.push_back(map(c));
+        }
+        return dom;
+    };
+    s = HostOpLog();
+    s.agent_names = o.agent_names;
+    s.agent_seqs.assign(o.agent_names.size(), {});
+    size_t oi = 0, ai = 0, ei = 0;
+    for (const auto &r : t) {
+        while (ai < o.agent_runs.size() && o.agent_runs[ai].lv + o.agent_runs[ai].len <= r.first) ai++;
+        for (size_t k = ai; k < o.agent_runs.size() && o.agent_runs[k].lv < r.second; k++) {
+            const AgentRun &a = o.agent_runs[k];
+            const uint64_t x = std::max(a.lv, r.first), y = std::min(a.lv + a.len, r.second);
+            if (x < y) s.assign(a.agent, a.seq + (x - a.lv), map(x), y - x);
+        }
+        while (oi < o.ops.size() && o.ops[oi].lv + o.ops[oi].len <= r.first) oi++;
+        for (size_t k = oi; k < o.ops.size() && o.ops[k].lv < r.second; k++) {
+            const OpRun &op = o.ops[k];
+            const uint64_t x = std::max(op.lv, r.first), y = std::min(op.lv + op.len, r.second);
+            if (x >= y) continue;
+            if (op.kind == 0) {
+                for (uint64_t u = x; u < y;) {
+                    const bool known = o.ins_cbyte[u] != ~0u;
+                    uint64_t w = u + 1;
+                    while (w < y && (o.ins_cbyte[w] != ~0u) == known) w++;
+                    size_t b0 = 0, b1 = 0;
+                    if (known) {
+                        b0 = o.ins_cbyte[u];
+                        b1 = o.ins_cbyte[w - 1] + utf8_len(o.ins_content[o.ins_cbyte[w - 1]]);
+                    }
+                    s.push_ins(op.pos + (u - op.lv), known ? o.ins_content.data() + b0 : nullptr, b1 - b0, w - u, known);
+                    u = w;
+                }
+            } else if (op.fwd) {
+                s.push_del(op.pos, y - x, true);
+            } else {
+                s.push_del(op.pos + (op.lv + op.len - y), y - x, false);
+            }
+        }
+        while (ei < o.graph.entries.size() && o.graph.entries[ei].end <= r.first) ei++;
+        for (size_t k = ei; k < o.graph.entries.size() && o.graph.entries[k].start < r.second; k++) {
+            const GraphEntry &e = o.graph.entries[k];
+            const uint64_t x = std::max(e.start, r.first), y = std::min(e.end, r.second);
+            if (x >= y) continue;
+            std::vector<uint64_t> par = x == e.start ? project(e.parents) : project({x - 1});
+            std::sort(par.begin(), par.end());
+            s.graph.push(par, map(x), map(y - 1) + 1);
+        }
+    }
+    s.version = project(o.version);
+    std::sort(s.version.begin(), s.version.end());
+    if (s.n_lv != nn) return ErrCheckout;
+    s.finish();
+    return OK;
+}
+
+dtgpu_status dtgpu_oplog_project(const dtgpu_oplog *h, const uint64_t *spans, size_t n_spans, dtgpu_oplog **out) {
+    if (!h || !out || (n_spans && !spans)) return DTGPU_ERR_ARG;
+    *out = nullptr;
+    std::vector<std::pair<uint64_t, uint64_t>> t(n_spans);
+    for (size_t i = 0; i < n_spans; i++) t[i] = {spans[2 * i], spans[2 * i + 1]};
+    HostOpLog log = h->o;
+    log.finish();   // op runs split at graph entries
+    auto *sub = new dtgpu_oplog;
+    const Status st = project_oplog(log, t, sub->o);
+    if (st != OK) { delete sub; return dtgpu_status(st); }
+    *out = sub;
+    return DTGPU_OK;
+}
+
 dtgpu_status dtgpu_oplog_history(const dtgpu_oplog *h, const uint64_t *version, size_t n_version, dtgpu_oplog **out) {
     if (!h || !out || (n_version && !version)) return DTGPU_ERR_ARG;
     *out = nullptr;

@@ -107,6 +107,7 @@ def lib():
     L.dtgpu_oplog_dominators.argtypes = [vp, pu64, sz, pu64, sz, pu64, sz]
     L.dtgpu_oplog_dominators.restype = ctypes.c_int64
     L.dtgpu_oplog_history.argtypes = [vp, pu64, sz, ctypes.POINTER(vp)]
+    L.dtgpu_oplog_project.argtypes = [vp, pu64, sz, ctypes.POINTER(vp)]
     L.dtgpu_oplog_encode.argtypes = [vp, pu64, sz, ctypes.c_uint32, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
     L.dtgpu_oplog_decode_and_add.argtypes = [vp, ctypes.c_char_p, sz, c, pu64, sz, ctypes.POINTER(sz)]
     L.dtgpu_oplog_doc_id.argtypes = [vp, ctypes.c_char_p, sz]
@@ -500,6 +501,20 @@ class ListOpLog:
         out = ctypes.c_void_p()
         _check(lib().dtgpu_oplog_history(self._h, p, nv, ctypes.byref(out)))
         return ListOpLog(out.value)
+
+    def project(self, spans) -> "ListOpLog":
+        """The ops in the LV spans [(start, end), ...] with the causal graph projected onto them
+        (Graph::subgraph_raw, src/causalgraph/graph/subgraph.rs:39-250; dtgpu_oplog_project)."""
+        flat = [int(x) for s in spans for x in s]
+        p = (ctypes.c_uint64 * max(1, len(flat)))(*flat)
+        out = ctypes.c_void_p()
+        _check(lib().dtgpu_oplog_project(self._h, p, len(flat) // 2, ctypes.byref(out)))
+        return ListOpLog(out.value)
+
+    def checkout_text_bytes(self, spans) -> bytes:
+        """OpLog::checkout_text (src/oplog.rs:388-394) for the text whose ops are `spans`: the
+        projected sub-oplog checked out on the device."""
+        return self.project(spans).checkout_tip_bytes()
 
     def checkout(self, version) -> ListBranch:
         """ListOpLog::checkout(&[LV]) (src/list/oplog.rs:32-36): the branch at `version`."""

@@ -166,6 +166,13 @@ dtgpu_status dtgpu_xf_operations_from(const dtgpu_oplog *oplog, const uint64_t *
  * Returns the LV count (0 on an invalid version); writes at most cap LVs. */
 size_t dtgpu_oplog_xf_order(const dtgpu_oplog *oplog, const uint64_t *from, size_t n_from, const uint64_t *merging,
                             size_t n_merging, uint32_t *out, size_t cap);
+/* One text CRDT of a shared causal graph (OpLog::checkout_text, src/oplog.rs:388-394, via
+ * TextInfo::merge_into, src/listmerge/merge.rs:954-1054): the ops in the LV spans
+ * [spans[2i], spans[2i+1]) with the causal graph projected onto them (Graph::subgraph_raw /
+ * project_onto_subgraph_raw, src/causalgraph/graph/subgraph.rs:39-250: a version's projection is
+ * the frontier of its history restricted to the spans), LVs compacted in order, agents / seqs /
+ * positions unchanged.  Its tip checkout (dtgpu_checkout_tip, on the device) is the text. */
+dtgpu_status dtgpu_oplog_project(const dtgpu_oplog *oplog, const uint64_t *spans, size_t n_spans, dtgpu_oplog **out);
 /* The history of `version` as an oplog of its own (what ListOpLog::checkout(&[LV]) replays:
  * diff_rev(version, ROOT), src/causalgraph/graph/tools.rs:176-292), LVs compacted in order,
  * agents / seqs / positions unchanged; its tip checkout is the checkout at `version`. */
