@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <queue>
 #include <thread>
 #include <tuple>
 #include <vector>
@@ -1249,44 +1250,8 @@ static Status project_oplog(const HostOpLog &o, std::vector<std::pair<uint64_t, 
         return int64_t(std::upper_bound(t.begin(), t.end(), lv, [](uint64_t v, const std::pair<uint64_t, uint64_t> &r) {
                            return v < r.first; }) - t.begin()) - 1;
     };
+    auto in_t = [&](uint64_t lv) { const int64_t i = span_of(lv); return i >= 0 && lv < t[size_t(i)].second; };
     auto map = [&](uint64_t lv) -> uint64_t { const int64_t i = span_of(lv); return base[size_t(i)] + (lv - t[size_t(i)].first); };
-    // Projection of a version: walk back from each member; inside an entry the LVs form a chain,
-    // so the latest member of T at or below the walked LV (and not below the entry start) is a
-    // candidate, otherwise the walk continues at the entry's parents.  The frontier is the
-    // candidates not in the history of another candidate.
-    auto project = [&](const std::vector<uint64_t> &ver) -> std::vector<uint64_t> {
-        std::vector<uint64_t> stack(ver), cand;
-        std::vector<uint8_t> seen(o.graph.entries.size(), 0);
-        while (!stack.empty()) {
-            const uint64_t v = stack.back();
-            stack.pop_back();
-            const int64_t ei = o.graph.find_idx(v);
-            if (ei < 0) continue;
-            const GraphEntry &e = o.graph.entries[size_t(ei)];
-            const int64_t si = span_of(v);
-            if (si >= 0 && t[size_t(si)].second > e.start) {
-                const uint64_t c = std::min(v, t[size_t(si)].second - 1);
-                if (c >= e.start) { cand.push_back(c); continue; }
-            }
-            if (seen[size_t(ei)]) continue;   // the entry's parents were walked already
-            seen[size_t(ei)] = 1;
-            for (uint64_t p : e.parents) stack.push_back(p);
-        }
-        std::sort(cand.begin(), cand.end());
-        cand.erase(std::unique(cand.begin(), cand.end()), cand.end());
-        std::vector<uint64_t> dom;
-        std::vector<std::pair<uint64_t, uint64_t>> only_a, only_b;
-        for (uint64_t c : cand) {
-            bool dominated = false;
-            for (uint64_t d : cand) {
-                if (d <= c) continue;
-                o.graph.diff_rev({c}, {d}, only_a, only_b);
-                if (only_a.empty()) { dominated = true; break; }
-            }
-            if (!dominated) dom.push_back(map(c));
-        }
-        return dom;
-    };
     s = HostOpLog();
     s.agent_names = o.agent_names;
     s.agent_seqs.assign(o.agent_names.size(), {});
@@ -1322,18 +1287,91 @@ static Status project_oplog(const HostOpLog &o, std::vector<std::pair<uint64_t, 
                 s.push_del(op.pos + (op.lv + op.len - y), y - x, false);
             }
         }
-        while (ei < o.graph.entries.size() && o.graph.entries[ei].end <= r.first) ei++;
-        for (size_t k = ei; k < o.graph.entries.size() && o.graph.entries[k].start < r.second; k++) {
-            const GraphEntry &e = o.graph.entries[k];
-            const uint64_t x = std::max(e.start, r.first), y = std::min(e.end, r.second);
-            if (x >= y) continue;
-            std::vector<uint64_t> par = x == e.start ? project(e.parents) : project({x - 1});
-            std::sort(par.begin(), par.end());
-            s.graph.push(par, map(x), map(y - 1) + 1);
+    }
+    (void)ei;
+    // The graph, in one pass over the entries cut into runs inside / outside T.  A run outside T
+    // gets its projected version P (constant along the run: the chain below it); a run inside T
+    // is an entry of the projected graph whose parents are the projection of its own parents.  A
+    // projection is the union of the parents' P (a T member projects to itself), reduced to its
+    // frontier in the projected graph built so far (it holds every earlier T member).
+    // Projected versions can be wide antichains (a text whose ops hang off another's), so runs
+    // share them and a union is reduced by one walk down the projected graph, newest entry first,
+    // that stops below the union's lowest member (the reference's find_dominators heap walk,
+    // src/causalgraph/graph/tools.rs:545-578).
+    using Set = std::shared_ptr<const std::vector<uint64_t>>;
+    struct Piece { uint64_t start, end; Set proj; };
+    std::vector<Piece> outside;   // ascending
+    std::vector<uint64_t> seen_to(1, 0);   // per projected entry: 1 + highest LV walked
+    auto frontier_of = [&](std::vector<uint64_t> u) -> std::vector<uint64_t> {
+        std::sort(u.begin(), u.end());
+        u.erase(std::unique(u.begin(), u.end()), u.end());
+        if (u.size() < 2) return u;
+        const uint64_t lo = u.front();
+        std::vector<uint8_t> dominated(u.size(), 0);
+        std::priority_queue<uint64_t> heap;
+        std::vector<size_t> touched;
+        seen_to.resize(s.graph.entries.size(), 0);
+        auto push_parents = [&](uint64_t x) {   // parents of LV x in the projected graph
+            const int64_t ei = s.graph.find_idx(x);
+            const GraphEntry &e = s.graph.entries[size_t(ei)];
+            if (x > e.start) heap.push(x - 1);
+            else for (uint64_t p : e.parents) heap.push(p);
+        };
+        for (uint64_t c : u) push_parents(c);
+        while (!heap.empty()) {
+            const uint64_t v = heap.top();
+            heap.pop();
+            if (v < lo) break;
+            const size_t ei = size_t(s.graph.find_idx(v));
+            if (seen_to[ei] > v) continue;
+            const GraphEntry &e = s.graph.entries[ei];
+            const uint64_t from = std::max(e.start, seen_to[ei]);   // [from, v] is new history
+            if (!seen_to[ei]) touched.push_back(ei);
+            seen_to[ei] = v + 1;
+            for (auto it = std::lower_bound(u.begin(), u.end(), from); it != u.end() && *it <= v; ++it)
+                dominated[size_t(it - u.begin())] = 1;
+            if (from == e.start) for (uint64_t p : e.parents) heap.push(p);
+        }
+        for (size_t ei : touched) seen_to[ei] = 0;
+        std::vector<uint64_t> dom;
+        for (size_t i = 0; i < u.size(); i++) if (!dominated[i]) dom.push_back(u[i]);
+        return dom;
+    };
+    auto project_set = [&](const std::vector<uint64_t> &ver) -> Set {
+        std::vector<uint64_t> u;
+        Set only;
+        size_t sources = 0;
+        for (uint64_t p : ver) {
+            sources++;
+            if (in_t(p)) { u.push_back(map(p)); continue; }
+            auto it = std::upper_bound(outside.begin(), outside.end(), p,
+                                       [](uint64_t v, const Piece &q) { return v < q.start; });
+            if (it == outside.begin() || p >= (--it)->end) continue;   // cannot happen: parents precede
+            only = it->proj;
+            u.insert(u.end(), it->proj->begin(), it->proj->end());
+        }
+        if (sources == 1 && only) return only;   // one parent outside T: its run's projection
+        return std::make_shared<const std::vector<uint64_t>>(frontier_of(std::move(u)));
+    };
+    auto project = [&](const std::vector<uint64_t> &ver) -> std::vector<uint64_t> { return *project_set(ver); };
+    for (const GraphEntry &e : o.graph.entries) {
+        for (uint64_t x = e.start; x < e.end;) {
+            const bool inside = in_t(x);
+            uint64_t y = x + 1;
+            if (inside) {
+                y = std::min(e.end, t[size_t(span_of(x))].second);
+            } else {
+                const int64_t i = span_of(x);   // next T span starts after x
+                const size_t nx = size_t(i + 1);
+                y = nx < t.size() ? std::min(e.end, t[nx].first) : e.end;
+            }
+            Set par = project_set(x == e.start ? e.parents : std::vector<uint64_t>{x - 1});
+            if (inside) s.graph.push(*par, map(x), map(y - 1) + 1);
+            else outside.push_back(Piece{x, y, std::move(par)});
+            x = y;
         }
     }
     s.version = project(o.version);
-    std::sort(s.version.begin(), s.version.end());
     if (s.n_lv != nn) return ErrCheckout;
     s.finish();
     return OK;

@@ -118,11 +118,13 @@ def test_projection_gives_back_the_text_order(seed):
 
 
 def test_projection_of_the_relay_text():
-    a = dt_amd.synth_oplog(2, 1500)
-    c, _a_spans, b_spans, n_b = _interleave(a, 3)
-    sub = c.project(b_spans)
-    assert len(sub) == n_b
-    assert _oracle_rebuild(sub).checkout_tip_bytes() == b"x" * n_b
+    """B's ops hang off A's, so B's projected versions are wide antichains (thousands wide on
+    friendsforever); every B op inserts "x" at 0, so its text is n_B x's."""
+    for a in (dt_amd.synth_oplog(2, 1500), dt_amd.ListOpLog.load_from(G.dt_bytes("friendsforever"))):
+        c, _a_spans, b_spans, n_b = _interleave(a, 3)
+        sub = c.project(b_spans)
+        assert len(sub) == n_b
+        assert _oracle_rebuild(sub).checkout_tip_bytes() == b"x" * n_b
 
 
 def test_projection_onto_everything_and_onto_a_history():
