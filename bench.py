@@ -42,6 +42,7 @@ def parse():
                         "(BASELINE configs[3]: synthetic concurrent documents, dt_synth.cpp, written as .dt) or "
                         "mixed (configs[4]: all 8 benchmark_data traces)")
     p.add_argument("--distinct", type=int, default=256, help="synth: distinct documents, replicated to --docs")
+    p.add_argument("--gen-threads", type=int, default=16, help="host threads generating / checking distinct documents")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     p.add_argument("--cpu-cores", type=int, default=16)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -50,7 +51,7 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(pool, budget_s, cores):
+def cpu_baseline(pool, budget_s, cores, workload="friendsforever"):
     """The CPU oracle (C restatement of the reference algorithm, one document per thread)
     timed on a bounded sample of the same workload: checkout_tip() on an already-decoded
     oplog, as the reference's `complex/merge` bench times it.  `pool`: the distinct documents."""
@@ -80,7 +81,7 @@ def cpu_baseline(pool, budget_s, cores):
     wall = time.perf_counter() - t0
     docs = sum(done)
     return {"value": sum(lvs) / wall, "unit": "merged ops/s", "cores": cores, "kind": "port",
-            "sample": f"{docs} x friendsforever.dt checkout_tip (decoded oplog, C oracle) on {cores} host threads, "
+            "sample": f"{docs} x {workload} checkout_tip (decoded oplog, C oracle) on {cores} host threads, "
                       f"{wall:.2f} s"}
 
 
@@ -113,15 +114,19 @@ def e2e_leg(batch, docs, steps, expect, total_lv):
 def workload_pool(args):
     """The distinct documents of the workload (raw `.dt` bytes) and the `data` description."""
     if args.workload == "synth":
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
         import dt_amd
-        from dt_encode import encode_dt
+        from concurrent.futures import ThreadPoolExecutor
+
+        def gen(d):   # generator and encoder are native (ctypes releases the GIL)
+            return dt_amd.synth_oplog(d, 5000).encode()
         pool = []
-        for d in range(args.distinct):
-            na, ops = dt_amd.synth_ops(d, 5000)
-            pool.append(encode_dt([f"a{i}" for i in range(na)], ops))
+        with ThreadPoolExecutor(max(1, args.gen_threads)) as ex:
+            for c in range(0, args.distinct, 4096):   # progress on stderr for long pools
+                pool += list(ex.map(gen, range(c, min(args.distinct, c + 4096))))
+                if args.distinct > 4096:
+                    print(f"[bench] generated {len(pool)}/{args.distinct} distinct documents", file=sys.stderr, flush=True)
         return pool, (f"synthetic concurrent documents (dt_synth.cpp: seed 0xD1A00000 + doc, 4-16 agents, "
-                      f"~5k ops), {args.distinct} distinct written as .dt and replicated")
+                      f"~5k ops), {args.distinct} distinct encoded as .dt (dtgpu_oplog_encode) and replicated")
     if args.workload == "mixed":   # BASELINE configs[4]: all benchmark_data traces, skewed sizes
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import golden_data as G
@@ -160,11 +165,13 @@ def expected_texts(args, pool):
                                                 "friendsforever_flat.json.gz")))["endContent"].encode()
         return [(len(gold), dt_amd.text_hash(gold))]
     from oracle.oracle import OpLog as OracleOpLog
-    out = []
-    for d in pool:
+    from concurrent.futures import ThreadPoolExecutor
+
+    def one(d):
         t = OracleOpLog.load_from(d).checkout_tip_bytes()
-        out.append((len(t), dt_amd.text_hash(t)))
-    return out
+        return (len(t), dt_amd.text_hash(t))
+    with ThreadPoolExecutor(max(1, args.gen_threads)) as ex:
+        return list(ex.map(one, pool))
 
 
 def main():
@@ -281,7 +288,7 @@ def main():
     if not args.no_decode and staging == "device":   # .dt bytes -> text, all on the GPU
         out["e2e"] = e2e_leg(batch, docs, min(args.steps, 5), want, total_lv_mine)
     if rank == 0 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(pool, args.cpu_seconds, args.cpu_cores)
+        out["cpu_baseline"] = cpu_baseline(pool, args.cpu_seconds, args.cpu_cores, args.workload)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
