@@ -42,6 +42,8 @@ def parse():
                         "(BASELINE configs[3]: synthetic concurrent documents, dt_synth.cpp, written as .dt) or "
                         "mixed (configs[4]: all 8 benchmark_data traces)")
     p.add_argument("--distinct", type=int, default=256, help="synth: distinct documents, replicated to --docs")
+    p.add_argument("--rebalance", action="store_true",
+                   help="N>1: move documents from busy to idle ranks by measured cost before timing")
     p.add_argument("--gen-threads", type=int, default=16, help="host threads generating / checking distinct documents")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     p.add_argument("--cpu-cores", type=int, default=16)
@@ -209,6 +211,28 @@ def main():
         batch.run()
     batch.sync()
 
+    rebalance = None
+    if dist is not None and args.rebalance:
+        # measured-cost rebalancing: all-gather each rank's busy time for one
+        # pass, plan the moves identically on every rank, send the moved documents' .dt bytes
+        # point to point and re-stage (all outside the timed region)
+        from dt_amd.shard import all_gather_floats, exchange_documents, plan_moves
+        costs = [doc_cost(pool[g % len(pool)]) for g in range(n_total)]
+        assign = lpt_assign(costs, world)
+        busy = all_gather_floats(batch.run_timed(), dist, device=dev)
+        new_assign, moves = plan_moves(assign, costs, busy)
+        local = exchange_documents(moves, rank, dict(zip(mine, docs)), dist)
+        mine = new_assign[rank]
+        docs = [local[g] for g in mine]
+        if moves:
+            del batch
+            batch = dt_amd.Batch(docs=docs, device=gpu, staging=staging)
+            for _ in range(max(1, args.warmup)):
+                batch.run()
+            batch.sync()
+        after = all_gather_floats(batch.run_timed(), dist, device=dev)
+        rebalance = {"moves": len(moves), "busy_ms_before": busy, "busy_ms_after": after}
+
     # timed region: K device passes over the resident batch
     kernel_ms, split = [], []
     batch.sync()
@@ -285,6 +309,8 @@ def main():
                      "algorithmic_formula": "per doc: 16*op_runs + (8+4*parents)*graph_entries + 12*agent_runs "
                                             "+ inserted_bytes + text_out_bytes (SURVEY.md 8d merge-only)"},
     }
+    if rebalance is not None:
+        out["rebalance"] = rebalance
     if not args.no_decode and staging == "device":   # .dt bytes -> text, all on the GPU
         out["e2e"] = e2e_leg(batch, docs, min(args.steps, 5), want, total_lv_mine)
     if rank == 0 and not args.no_cpu_baseline:

@@ -55,3 +55,95 @@ def max_over_ranks(value: float, dist, device=None) -> float:
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def plan_moves(assign, costs, busy_ms, max_moves=None, tol=0.02):
+    """Measured-cost rebalancing of a skewed batch: every rank reports the busy
+    time of the same pass; a document's measured cost is its cost estimate times its rank's
+    measured ms per estimate unit.  Documents then move, one at a time, from the busiest to the
+    idlest rank -- each time the largest one that still narrows the gap -- until the spread is
+    within `tol` of the mean or no move helps.  Deterministic: every rank computes the same moves
+    from the all-gathered busy times.  Returns (new assignment, [(doc, src, dst), ...])."""
+    world = len(assign)
+    rate = [busy_ms[r] / max(1e-9, sum(costs[i] for i in assign[r])) for r in range(world)]
+    est = {}
+    for r in range(world):
+        for i in assign[r]:
+            est[i] = costs[i] * rate[r]
+    load = [float(busy_ms[r]) for r in range(world)]
+    parts = [sorted(a, key=lambda i: (est[i], i)) for a in assign]   # ascending measured cost
+    moves = []
+    limit = max_moves if max_moves is not None else sum(len(a) for a in assign)
+    mean = sum(load) / max(1, world)
+    while len(moves) < limit:
+        src = max(range(world), key=lambda r: (load[r], -r))
+        dst = min(range(world), key=lambda r: (load[r], r))
+        gap = load[src] - load[dst]
+        if gap <= tol * mean or not parts[src]:
+            break
+        # the documents either side of half the gap; take the one leaving the lower maximum of
+        # the pair, if that is below the busiest rank's load
+        lo, hi = 0, len(parts[src])
+        while lo < hi:
+            mid = (lo + hi) // 2
+            if est[parts[src][mid]] <= gap / 2:
+                lo = mid + 1
+            else:
+                hi = mid
+
+        def at_dst(i):   # at the destination the document runs at the destination's rate
+            return costs[i] * rate[dst] if rate[dst] > 0 else est[i]
+        best = None
+        for k in (lo - 1, lo):
+            if 0 <= k < len(parts[src]):
+                i = parts[src][k]
+                peak = max(load[src] - est[i], load[dst] + at_dst(i))
+                if peak < load[src] - 1e-12 and (best is None or peak < best[0]):
+                    best = (peak, k)
+        if best is None:
+            break
+        i = parts[src].pop(best[1])
+        c_dst = at_dst(i)
+        load[src] -= est[i]
+        load[dst] += c_dst
+        est[i] = c_dst
+        k = 0
+        while k < len(parts[dst]) and (est[parts[dst][k]], parts[dst][k]) < (c_dst, i):
+            k += 1
+        parts[dst].insert(k, i)
+        moves.append((i, src, dst))
+    return [sorted(p) for p in parts], moves
+
+
+def exchange_documents(moves, rank, local, dist):
+    """Carry out `moves` point to point: the source rank sends each moved document's encoded
+    `.dt` bytes (length, then bytes), the destination receives them; `local` maps document index
+    -> bytes on this rank and is updated in place.  Every rank walks the same move list, so the
+    send/recv pairs match (RCCL over xGMI on MI355X, gloo on CPU)."""
+    import torch
+    dev = None
+    if dist.get_backend() == "nccl":
+        dev = torch.device("cuda", torch.cuda.current_device())
+    for i, src, dst in moves:
+        if rank == src:
+            data = local.pop(i)
+            n = torch.tensor([len(data)], dtype=torch.int64, device=dev)
+            dist.send(n, dst)
+            buf = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+            dist.send(buf.to(dev) if dev is not None else buf, dst)
+        elif rank == dst:
+            n = torch.zeros(1, dtype=torch.int64, device=dev)
+            dist.recv(n, src)
+            buf = torch.empty(int(n.item()), dtype=torch.uint8, device=dev)
+            dist.recv(buf, src)
+            local[i] = bytes(buf.cpu().numpy().tobytes())
+    return local
+
+
+def all_gather_floats(value, dist, device=None):
+    """Every rank's float (e.g. its busy time), in rank order."""
+    import torch
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [float(x.item()) for x in out]
