@@ -220,7 +220,7 @@ def main():
         costs = [doc_cost(pool[g % len(pool)]) for g in range(n_total)]
         assign = lpt_assign(costs, world)
         busy = all_gather_floats(batch.run_timed(), dist, device=dev)
-        new_assign, moves = plan_moves(assign, costs, busy)
+        new_assign, moves = plan_moves(assign, costs, busy, tol=0.10)   # spreads under 10 % are noise
         local = exchange_documents(moves, rank, dict(zip(mine, docs)), dist)
         mine = new_assign[rank]
         docs = [local[g] for g in mine]
