@@ -68,11 +68,13 @@ struct BatchParams {
 // blocks (they split 64 -> 32 + 32).
 __host__ __device__ inline uint32_t sb_capacity(uint32_t mb) { return mb / 32 + 2; }
 // Bytes of a block index for `mb` blocks (dt_replay.hip bind_index): per block the packed
-// counts and the (superblock, index) position (u32 each); per superblock visible / live totals,
-// list length, top position, top order (u32 each) and a 64-entry u16 block list.
-__host__ __device__ inline uint64_t index_bytes(uint64_t mb) {
+// counts (u32) and the (superblock, index) position (u32; u16 when `narrow`, the LDS tier); per
+// superblock visible / live totals, list length, top position (u32 each)
+// and a 64-entry u16 block list.
+__host__ __device__ inline uint64_t index_bytes(uint64_t mb, bool narrow = false) {
     const uint64_t ms = sb_capacity(uint32_t(mb));
-    return ((8 * mb + 20 * ms + 128 * ms) + 15) & ~uint64_t(15);
+    const uint64_t per_block = narrow ? 4 * mb + 4 * ((mb + 1) / 2) : 8 * mb;
+    return ((per_block + 16 * ms + 128 * ms) + 15) & ~uint64_t(15);
 }
 constexpr uint32_t MAX_DOC_BLOCKS = 65535;   // block ids are u16 in the superblock lists
 

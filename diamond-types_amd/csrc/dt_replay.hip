@@ -150,7 +150,8 @@ struct Doc {
     u64 *m2;         // per block: visible mask, live mask (adjacent: one wave load / store)
     uint32_t max_blocks, max_sb;
     // index (LDS or HBM)
-    uint32_t *cnt, *opos;                                // per block
+    uint32_t *cnt, *opos;                                // per block (opos: HBM tier)
+    uint16_t *opos16;                                    // per block (opos: LDS tier)
     uint32_t *sbn, *sbpos;                               // per superblock
     uint32_t *top, *tlive;                               // by top position
     uint16_t *sbl;                                       // per superblock: SBC block ids
@@ -188,6 +189,17 @@ DEV bool charge(Doc &D) {
 }
 template <bool PROF> DEV uint64_t tick() { return PROF ? __builtin_amdgcn_s_memtime() : 0; }
 
+// Block -> (superblock << 6 | index in its list).  The LDS tier keeps it in 16 bits (its
+// superblock ids stay below 1024), which lets six documents share a SIMD instead of five.
+template <bool L> DEV uint32_t opos_of(const Doc &D, uint32_t b) {
+    if (L) return D.opos16[b];
+    return ix<L>(D.opos + b);
+}
+template <bool L> DEV void set_opos(Doc &D, uint32_t b, uint32_t v) {
+    if (L) D.opos16[b] = uint16_t(v);
+    else D.opos[b] = v;
+}
+
 // ---- navigation ------------------------------------------------------------------------------
 
 template <bool L> DEV uint32_t first_block(const Doc &D) {
@@ -195,7 +207,7 @@ template <bool L> DEV uint32_t first_block(const Doc &D) {
 }
 // Next block in document order, or NONE.
 template <bool L> DEV uint32_t next_block(const Doc &D, uint32_t b) {
-    const uint32_t o = U(ix<L>(D.opos + b));
+    const uint32_t o = U(opos_of<L>(D, b));
     const uint32_t S = o >> 6, i = o & 63u;
     if (i + 1 < U(ix<L>(D.sbn + S))) return U(ix16<L>(D.sbl + size_t(S) * SBC + i + 1));
     const uint32_t p = U(ix<L>(D.sbpos + S)) + 1;
@@ -204,7 +216,7 @@ template <bool L> DEV uint32_t next_block(const Doc &D, uint32_t b) {
 }
 // Document-order key of (block, slot).
 template <bool L> DEV uint32_t key_at(const Doc &D, uint32_t b, uint32_t s) {
-    const uint32_t o = ix<L>(D.opos + b);
+    const uint32_t o = opos_of<L>(D, b);
     return (ix<L>(D.sbpos + (o >> 6)) << 12) | ((o & 63u) << 6) | s;
 }
 template <bool L> DEV uint32_t key_of(const Doc &D, uint32_t item) {
@@ -265,7 +277,7 @@ DEV uint32_t select_bit(u64 m, uint32_t k) {
 template <bool L>
 DEV uint32_t next_live_block(Doc &D, uint32_t b) {
     const uint32_t l = lane_id();
-    const uint32_t o = U(ix<L>(D.opos + b));
+    const uint32_t o = U(opos_of<L>(D, b));
     uint32_t S = o >> 6;
     {   // rest of b's superblock
         const uint32_t n = U(ix<L>(D.sbn + S)), i0 = (o & 63u) + 1;
@@ -308,7 +320,7 @@ DEV void split_sb(Doc &D, uint32_t S) {
         wave_fence();
         if (l >= SBC / 2) {
             D.sbl[size_t(S2) * SBC + (l - SBC / 2)] = uint16_t(b);
-            D.opos[b] = (S2 << 6) | (l - SBC / 2);
+            set_opos<L>(D, b, (S2 << 6) | (l - SBC / 2));
         }
     }
     const uint32_t vh = wave_sum(l >= 32 ? vis : 0), lh = wave_sum(l >= 32 ? live : 0);
@@ -362,7 +374,7 @@ DEV uint32_t split_block(Doc &D, uint32_t b, uint32_t c, uint32_t it, u64 mv, u6
         const u64 v = l == 0 ? (mv & lo) : l == 1 ? (ml & lo) : l == 2 ? mv_hi : ml_hi;
         st_sc(D.m2 + 2 * size_t(l < 2 ? b : b2) + (l & 1), v);
     }
-    const uint32_t o = U(ix<L>(D.opos + b));
+    const uint32_t o = U(opos_of<L>(D, b));
     const uint32_t S = o >> 6, i = o & 63u, n = U(ix<L>(D.sbn + S));
     {   // shift S's list after i right by one
         uint32_t v = 0;
@@ -371,7 +383,7 @@ DEV uint32_t split_block(Doc &D, uint32_t b, uint32_t c, uint32_t it, u64 mv, u6
         wave_fence();
         if (mv_lane) {
             D.sbl[size_t(S) * SBC + l + 1] = uint16_t(v);
-            D.opos[v] = (S << 6) | (l + 1);
+            set_opos<L>(D, v, (S << 6) | (l + 1));
         }
     }
     if (l == 0) {
@@ -381,7 +393,7 @@ DEV uint32_t split_block(Doc &D, uint32_t b, uint32_t c, uint32_t it, u64 mv, u6
                    uint32_t(__popcll(mu_lo)) * C_UP;
         if (XF) { st_sc(D.mup + b, mu_lo); st_sc(D.mup + b2, mu_hi); }
         D.sbl[size_t(S) * SBC + i + 1] = uint16_t(b2);
-        D.opos[b2] = (S << 6) | (i + 1);
+        set_opos<L>(D, b2, (S << 6) | (i + 1));
         D.sbn[S] = n + 1;
     }
     wave_fence();
@@ -405,7 +417,7 @@ template <bool L> DEV uint32_t cut_point(uint32_t s) { return L ? min(max(s, 16u
 template <bool L>
 DEV uint32_t up_rank(Doc &D, uint32_t b, uint32_t s) {
     const uint32_t l = lane_id();
-    const uint32_t o = U(ix<L>(D.opos + b));
+    const uint32_t o = U(opos_of<L>(D, b));
     const uint32_t S = o >> 6, i = o & 63u, tp = U(ix<L>(D.sbpos + S));
     uint32_t r = 0;
     for (uint32_t c = 0; c < tp; c += 64) r += wave_sum(c + l < tp ? ix<L>(D.tup + c + l) : 0u);
@@ -474,7 +486,7 @@ DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml,
         }
         if (l == 0) {
             D.cnt[b] = c + m * (C_VIS + C_LIVE + C_ITEMS + (XF ? C_UP : 0u));
-            const uint32_t tp = ix<L>(D.sbpos + (ix<L>(D.opos + b) >> 6));
+            const uint32_t tp = ix<L>(D.sbpos + (opos_of<L>(D, b) >> 6));
             D.top[tp] = ix<L>(D.top + tp) + m;
             D.tlive[tp] = ix<L>(D.tlive + tp) + m;
             if (XF) D.tup[tp] = ix<L>(D.tup + tp) + m;
@@ -761,7 +773,7 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
                     const u64 bit = 1ull << pos_slot(w);
                     const bool fv = (oc == 1) != (nc == 1), fl = (oc != 0) != (nc != 0);
                     if (fv || fl) {
-                        const uint32_t tp = ix<L>(D.sbpos + (ix<L>(D.opos + b) >> 6));
+                        const uint32_t tp = ix<L>(D.sbpos + (opos_of<L>(D, b) >> 6));
                         uint32_t dc = 0;
                         if (fv) {
                             at_xor(D.m2 + 2 * size_t(b), bit);
@@ -859,7 +871,7 @@ DEV uint32_t check_invariants(Doc &D, DocResult *res) {
         uint32_t tv = 0, tl = 0, tu = 0;
         for (uint32_t i = 0; i < n; i++) {
             const uint32_t b = U(ix16<L>(D.sbl + size_t(S) * SBC + i));
-            if (U(ix<L>(D.opos + b)) != ((S << 6) | i)) return 201;
+            if (U(opos_of<L>(D, b)) != ((S << 6) | i)) return 201;
             const uint32_t c = U(ix<L>(D.cnt + b));
             const uint32_t cnt = c_items(c);
             const u64 mv = U64(ld_sc(D.m2 + 2 * size_t(b))), ml = U64(ld_sc(D.m2 + 2 * size_t(b) + 1));
@@ -906,7 +918,7 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
     // fresh tracker: one empty block in one superblock (per-LV words are written when their
     // item is inserted)
     if (l == 0) {
-        D.cnt[0] = 0; D.opos[0] = 0;
+        D.cnt[0] = 0; set_opos<L>(D, 0, 0);
         D.sbl[0] = 0; D.sbn[0] = 1; D.sbpos[0] = 0; D.top[0] = 0; D.tlive[0] = 0;
         if (XF) { D.tup[0] = 0; st_sc(D.mup, 0ull); }
     }
@@ -999,10 +1011,11 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
 
 // Carve an index for `mb` blocks / `ms` superblocks out of `base` (LDS or HBM); layout must
 // match index_bytes().
-DEV void bind_index(Doc &D, uint8_t *base, uint32_t mb, uint32_t ms) {
+DEV void bind_index(Doc &D, uint8_t *base, uint32_t mb, uint32_t ms, bool narrow) {
     uint32_t *w = reinterpret_cast<uint32_t *>(base);
     D.cnt = w; w += mb;
-    D.opos = w; w += mb;
+    if (narrow) { D.opos16 = reinterpret_cast<uint16_t *>(w); D.opos = nullptr; w += (mb + 1) / 2; }
+    else { D.opos = w; D.opos16 = nullptr; w += mb; }
     D.top = w; w += ms;
     D.tlive = w; w += ms;
     D.sbn = w; w += ms;
@@ -1050,9 +1063,9 @@ __global__ __launch_bounds__(64) void replay_kernel(BatchParams P) {
     if (LDS_INDEX) {
         if (D.max_blocks > P.lds_blocks) D.max_blocks = P.lds_blocks;
         D.max_sb = sb_capacity(P.lds_blocks);
-        bind_index(D, smem, P.lds_blocks, D.max_sb);
+        bind_index(D, smem, P.lds_blocks, D.max_sb, true);
     } else {
-        bind_index(D, P.gidx + dd.gidx_off, D.max_blocks, D.max_sb);
+        bind_index(D, P.gidx + dd.gidx_off, D.max_blocks, D.max_sb, false);
     }
     if (XF) {
         D.mup = P.mup + dd.blk_off;
@@ -1069,7 +1082,7 @@ int launch_replay(const BatchParams &small, const BatchParams &large, void *stre
     const bool prof = (small.debug | large.debug) & 2u;
     if (small.n_list) {
         if (small.fb_count && hipMemsetAsync(small.fb_count, 0, sizeof(uint32_t), s) != hipSuccess) return ErrHip;
-        size_t lds = size_t(index_bytes(small.lds_blocks));
+        size_t lds = size_t(index_bytes(small.lds_blocks, true));
         if (const char *pad = getenv("DTGPU_LDS_PAD")) lds += size_t(strtoul(pad, nullptr, 10));   // occupancy experiments
         if (prof) hipLaunchKernelGGL((dev::replay_kernel<true, true, false>), dim3(small.n_list), dim3(64), lds, s, small);
         else hipLaunchKernelGGL((dev::replay_kernel<true, false, false>), dim3(small.n_list), dim3(64), lds, s, small);

@@ -311,7 +311,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         d.gidx_off = gidx_total;
         gidx_total += index_bytes(d.max_blocks);
         const uint32_t est = uint32_t(std::min<uint64_t>(d.max_blocks, n_ins / lds_fill + 8));
-        if (!xf && index_bytes(est) <= kLdsIndexBudget) {
+        if (!xf && index_bytes(est, true) <= kLdsIndexBudget) {
             B->small_list.push_back(uint32_t(i));
             B->lds_blocks = std::max(B->lds_blocks, est);
         } else {
@@ -572,7 +572,7 @@ dtgpu_status stage_device(const uint8_t *const *docs, const size_t *lens, size_t
         d.gidx_off = gidx_total;
         gidx_total += index_bytes(d.max_blocks);
         const uint32_t est = uint32_t(std::min<uint64_t>(d.max_blocks, n_ins / lds_fill + 8));
-        if (index_bytes(est) <= kLdsIndexBudget) {
+        if (index_bytes(est, true) <= kLdsIndexBudget) {
             B->small_list.push_back(uint32_t(i));
             B->lds_blocks = std::max(B->lds_blocks, est);
         } else {
