@@ -87,6 +87,27 @@ def cpu_baseline(pool, budget_s, cores, workload="friendsforever"):
                       f"{wall:.2f} s"}
 
 
+def single_doc_latency(data, gpu, staging):
+    """One document alone (single-doc latency on one core, median of 5 after a
+    warmup): the GPU checkout pass of a one-document batch next to the C oracle's checkout_tip()
+    on one host thread.  A single document is one sequential replay chain, so the GPU is not
+    expected to win here; the batch is what it is for."""
+    import dt_amd
+    from oracle.oracle import OpLog as OracleOpLog
+    b = dt_amd.Batch(docs=[data], device=gpu, staging=staging)
+    b.run()
+    b.sync()
+    g = sorted(b.run_timed() for _ in range(5))[2]
+    o = OracleOpLog.load_from(data)
+    o.checkout_tip_bytes()
+    ts = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        o.checkout_tip_bytes()
+        ts.append((time.perf_counter() - t0) * 1000.0)
+    return {"gpu_ms": g, "cpu_ms": sorted(ts)[2], "cpu_cores": 1, "doc": "first document of the workload"}
+
+
 def e2e_leg(batch, docs, steps, expect, total_lv):
     """`.dt` bytes in HBM -> text: device decode (dt_decode.hip) + planner inputs (dt_prep.hip) +
     walk plan + replay, re-run `steps` times on the device-staged batch (HIP events per kernel).
@@ -315,6 +336,7 @@ def main():
         out["e2e"] = e2e_leg(batch, docs, min(args.steps, 5), want, total_lv_mine)
     if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(pool, args.cpu_seconds, args.cpu_cores, args.workload)
+        out["single_doc_latency"] = single_doc_latency(pool[0], gpu, staging)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
