@@ -1336,7 +1336,10 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
 }
 
 template <bool SIZE>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void decode_kernel(DecodeParams P) {
+#ifndef DTGPU_DECODE_WAVES
+#define DTGPU_DECODE_WAVES 6   // occupancy target (tuning knob; the register budget follows from it)
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_DECODE_WAVES))) void decode_kernel(DecodeParams P) {
     extern __shared__ uint32_t lds[];
     const uint32_t doc = blockIdx.x;
     if (doc >= P.n_docs) return;
