@@ -488,7 +488,7 @@ DEV void plan_doc(P &p, PlanResult *res) {
 // K = agent chunks per lane.  Documents with <= 64 agents run in the K = 1 instantiation, the
 // others (<= PLAN_MAX_AGENTS) in the wide one; each kernel skips the other's documents.
 template <int K>
-__global__ __launch_bounds__(64) void plan_kernel(PlanParams Q) {
+DEV void plan_entry(const PlanParams &Q) {
     extern __shared__ __attribute__((aligned(16))) uint16_t lds16[];
     const uint32_t d = U(blockIdx.x);
     if (d >= Q.n_docs) return;
@@ -534,16 +534,24 @@ __global__ __launch_bounds__(64) void plan_kernel(PlanParams Q) {
     plan_doc<K>(p, res);
 }
 
+#ifndef DTGPU_PLAN_WAVES
+#define DTGPU_PLAN_WAVES 6   // occupancy target of the <= 64-chain planner (tuning knob)
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PLAN_WAVES))) void plan_kernel_1(PlanParams Q) {
+    plan_entry<1>(Q);
+}
+__global__ __launch_bounds__(64) void plan_kernel_wide(PlanParams Q) { plan_entry<PLAN_MAX_AGENTS / 64>(Q); }
+
 }  // namespace pdev
 
 int launch_plan(const PlanParams &q, void *stream) {
     if (!q.n_docs) return OK;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const size_t lds = 2 * size_t(PLAN_TODO_CAP) + ((size_t(q.lds_entries) + 15) & ~size_t(15));   // todo + pending
-    hipLaunchKernelGGL(pdev::plan_kernel<1>, dim3(q.n_docs), dim3(64), lds, s, q);
+    hipLaunchKernelGGL(pdev::plan_kernel_1, dim3(q.n_docs), dim3(64), lds, s, q);
     if (hipGetLastError() != hipSuccess) return ErrHip;
     if (q.max_agents > 64) {
-        hipLaunchKernelGGL(pdev::plan_kernel<PLAN_MAX_AGENTS / 64>, dim3(q.n_docs), dim3(64), lds, s, q);
+        hipLaunchKernelGGL(pdev::plan_kernel_wide, dim3(q.n_docs), dim3(64), lds, s, q);
         if (hipGetLastError() != hipSuccess) return ErrHip;
     }
     return OK;
