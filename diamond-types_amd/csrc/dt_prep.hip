@@ -67,7 +67,10 @@ __device__ __forceinline__ uint32_t entry_of(const uint2 *ent, uint32_t hi, uint
 }
 
 __global__ __launch_bounds__(64) void prep_kernel(PrepParams P) {
-    extern __shared__ uint32_t lfill[];   // per entry: child count, then next child slot
+    // per entry (u16, two per LDS word): child count, then the next free slot of its children
+    // list relative to coff -- half the LDS of absolute u32 slots, so more documents share a CU
+    extern __shared__ uint32_t lfw[];
+    uint16_t *lfill = reinterpret_cast<uint16_t *>(lfw);
     const uint32_t doc = blockIdx.x;
     if (doc >= P.n_docs) return;
     const PrepDesc D = P.docs[doc];
@@ -96,9 +99,13 @@ __global__ __launch_bounds__(64) void prep_kernel(PrepParams P) {
         if (l == 0) { R.status = PREP_BAD; P.results[doc] = R; }
         return;
     }
+    if (npar >= 0xFFFFu) {   // a child count could overflow its u16: prepared on the host
+        if (l == 0) { R.status = PREP_WIDE; P.results[doc] = R; }
+        return;
+    }
 
     // ---- 1. parents: entry of each parent, child counts ------------------------------------------
-    for (uint32_t i = l; i < ne; i += 64) lfill[i] = 0;
+    for (uint32_t i = l; i < (ne + 1) / 2; i += 64) lfw[i] = 0;
     __syncthreads();
     bool bad = false;
     for (uint32_t i0 = 0; i0 < ne; i0 += 64) {
@@ -112,7 +119,7 @@ __global__ __launch_bounds__(64) void prep_kernel(PrepParams P) {
                 owner[k] = i;
                 par[k] = p;
                 pent[k] = pe;
-                atomicAdd(&lfill[pe], 1u);
+                atomicAdd(&lfw[pe >> 1], 1u << (16 * (pe & 1u)));
             }
         }
     }
@@ -122,13 +129,14 @@ __global__ __launch_bounds__(64) void prep_kernel(PrepParams P) {
     }
     __syncthreads();
     // children CSR offsets (exclusive scan); lfill becomes each entry's next free child slot
+    // (relative to its offset)
     {
         uint32_t carry = 0;
         for (uint32_t i0 = 0; i0 < ne; i0 += 64) {
             const uint32_t i = i0 + l;
             const uint32_t c = i < ne ? lfill[i] : 0;
             const uint32_t inc = scan_incl(c);
-            if (i < ne) { coff[i] = carry + inc - c; lfill[i] = carry + inc - c; }
+            if (i < ne) { coff[i] = carry + inc - c; lfill[i] = 0; }
             carry += rdl(inc, 63);
         }
         if (l == 0) coff[ne] = carry;
@@ -145,13 +153,14 @@ __global__ __launch_bounds__(64) void prep_kernel(PrepParams P) {
         for (uint64_t m = ballot(todo); m; m = ballot(todo)) {
             const uint32_t lead = rdl(key, ctz(m));
             const uint64_t mm = ballot(todo && key == lead);
-            const uint32_t base = lfill[lead];
+            const uint32_t rel = lfill[lead];
+            const uint32_t base = coff[lead] + rel;
             if (todo && key == lead) {
                 child[base + popc(mm & lt_mask())] = own;
                 todo = false;
             }
             __syncthreads();
-            if (l == 0) lfill[lead] = base + popc(mm);
+            if (l == 0) lfill[lead] = uint16_t(rel + popc(mm));
             __syncthreads();
         }
     }
@@ -320,7 +329,7 @@ __global__ __launch_bounds__(64) void prep_kernel(PrepParams P) {
 
 int launch_prep(const PrepParams &p, void *stream) {
     if (!p.n_docs) return 0;
-    hipLaunchKernelGGL(prep::prep_kernel, dim3(p.n_docs), dim3(64), size_t(p.max_entries) * 4,
+    hipLaunchKernelGGL(prep::prep_kernel, dim3(p.n_docs), dim3(64), ((size_t(p.max_entries) + 1) / 2) * 4,
                        reinterpret_cast<hipStream_t>(stream), p);
     return hipGetLastError() == hipSuccess ? 0 : 66;
 }
