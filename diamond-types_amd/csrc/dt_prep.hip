@@ -144,25 +144,33 @@ __global__ __launch_bounds__(64) void prep_kernel(PrepParams P) {
     __syncthreads();
     wave_fence();
     // children in child-index order (slots are in (child, parent) order): a stable scatter,
-    // one parent entry per round
+    // 64 slots at a time: each lane gathers its key's CSR offset and fill once, register-only
+    // rounds (one key each) rank the lanes sharing a key, then one parallel store places them and
+    // the last lane of each key advances its fill
     for (uint32_t k0 = 0; k0 < npar; k0 += 64) {
         const uint32_t k = k0 + l;
-        const uint32_t key = k < npar ? pent[k] : 0xFFFFFFFFu;
-        const uint32_t own = k < npar ? owner[k] : 0;
-        bool todo = k < npar;
+        const bool live = k < npar;
+        const uint32_t key = live ? pent[k] : 0xFFFFFFFFu;
+        const uint32_t own = live ? owner[k] : 0;
+        const uint32_t kco = live ? coff[key] : 0;
+        const uint32_t krel = live ? uint32_t(lfill[key]) : 0;
+        uint32_t rank = 0, cnt = 0;
+        bool todo = live;
         for (uint64_t m = ballot(todo); m; m = ballot(todo)) {
             const uint32_t lead = rdl(key, ctz(m));
-            const uint64_t mm = ballot(todo && key == lead);
-            const uint32_t rel = lfill[lead];
-            const uint32_t base = coff[lead] + rel;
-            if (todo && key == lead) {
-                child[base + popc(mm & lt_mask())] = own;
+            const bool mine = todo && key == lead;
+            const uint64_t mm = ballot(mine);
+            if (mine) {
+                rank = popc(mm & lt_mask());
+                cnt = popc(mm);
                 todo = false;
             }
-            __syncthreads();
-            if (l == 0) lfill[lead] = uint16_t(rel + popc(mm));
-            __syncthreads();
         }
+        if (live) {
+            child[kco + krel + rank] = own;
+            if (rank + 1 == cnt) lfill[key] = uint16_t(krel + cnt);
+        }
+        __syncthreads();
     }
 
     // ---- 2. each entry's first op run (ops are split at entry boundaries) ------------------------
