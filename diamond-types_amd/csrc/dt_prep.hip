@@ -104,6 +104,9 @@ __global__ __launch_bounds__(64) void prep_kernel(PrepParams P) {
         return;
     }
 
+#ifdef DTGPU_PREP_PROF
+    const uint64_t T0 = wall_clock64();
+#endif
     // ---- 1. parents: entry of each parent, child counts ------------------------------------------
     for (uint32_t i = l; i < (ne + 1) / 2; i += 64) lfw[i] = 0;
     __syncthreads();
@@ -144,6 +147,9 @@ __global__ __launch_bounds__(64) void prep_kernel(PrepParams P) {
     __syncthreads();
     wave_fence();
     // children in child-index order (slots are in (child, parent) order): a stable scatter,
+#ifdef DTGPU_PREP_PROF
+    const uint64_t T1 = wall_clock64();
+#endif
     // 64 slots at a time: each lane gathers its key's CSR offset and fill once, register-only
     // rounds (one key each) rank the lanes sharing a key, then one parallel store places them and
     // the last lane of each key advances its fill
@@ -173,6 +179,9 @@ __global__ __launch_bounds__(64) void prep_kernel(PrepParams P) {
         __syncthreads();
     }
 
+#ifdef DTGPU_PREP_PROF
+    const uint64_t T2 = wall_clock64();
+#endif
     // ---- 2. each entry's first op run (ops are split at entry boundaries) ------------------------
     {
         Chunk ce, co, ob;
@@ -191,6 +200,9 @@ __global__ __launch_bounds__(64) void prep_kernel(PrepParams P) {
     }
     wave_fence();
 
+#ifdef DTGPU_PREP_PROF
+    const uint64_t T3 = wall_clock64();
+#endif
     // ---- 3. causal-chain decomposition (sequential over entries) ---------------------------------
     uint32_t clen = 0, nch = 0;      // lane c: ops in chain c so far
     uint32_t prev_row = 0;           // parent vector of entry i - 1
@@ -251,6 +263,9 @@ __global__ __launch_bounds__(64) void prep_kernel(PrepParams P) {
         }
     }
     wave_fence();
+#ifdef DTGPU_PREP_PROF
+    const uint64_t T4 = wall_clock64();
+#endif
     // per chain: offset of its dense table
     {
         const uint32_t c = l < nch ? clen : 0;
@@ -298,6 +313,9 @@ __global__ __launch_bounds__(64) void prep_kernel(PrepParams P) {
             for (uint32_t v = 0; v < o.y; v++) dense[d0 + (o.x - e0) + v] = (o.x + v) | (del ? TL_DEL : 0u);
         }
     }
+#ifdef DTGPU_PREP_PROF
+    const uint64_t T5 = wall_clock64();
+#endif
     for (uint32_t t = l; t < D.n_ver; t += 64) {   // tips and their entries
         const uint32_t v = P.d_ver[D.d_ver + t];
         P.tip[2 * (D.o_tip + t)] = v;
@@ -331,6 +349,13 @@ __global__ __launch_bounds__(64) void prep_kernel(PrepParams P) {
     R.n_chains = nch;
     R.n_ins = n_ins;
     if (l == 0) P.results[doc] = R;
+#ifdef DTGPU_PREP_PROF   // phase split (100 MHz wall clock) of two documents: profiles/r1_v19
+    const uint64_t T6 = wall_clock64();
+    if (l == 0 && (doc == 0 || doc == P.n_docs / 2))
+        printf("PREPPROF doc %u ne %u npar %u parents %llu scatter %llu firstop %llu chains %llu outputs %llu tail %llu\n", doc, ne, npar,
+               (unsigned long long)(T1 - T0), (unsigned long long)(T2 - T1), (unsigned long long)(T3 - T2),
+               (unsigned long long)(T4 - T3), (unsigned long long)(T5 - T4), (unsigned long long)(T6 - T5));
+#endif
 }
 
 }  // namespace prep
