@@ -93,7 +93,10 @@ __global__ __launch_bounds__(64) void prep_kernel(PrepParams P) {
     uint32_t *dense = P.dense + D.o_dense;
     uint32_t *rows = P.rows + D.o_rows;
     uint32_t *owner = P.scr + D.o_scr;
-    uint32_t *chain = owner + npar, *seq0 = chain + ne, *coff = seq0 + ne, *eop = coff + ne + 1;
+    // per entry {chain, seq0 - start (mod 2^32)}: one 8-byte load gives a parent's chain and the
+    // offset that turns its parent LV into a chain length (dt_prep.hpp prep_scratch_words)
+    uint2 *cs = reinterpret_cast<uint2 *>(owner + ((npar + 1) & ~1u));
+    uint32_t *coff = reinterpret_cast<uint32_t *>(cs + ne), *eop = coff + ne + 1;
     Cmd *opc = P.opc + D.o_op;
     if (ne > P.max_entries || D.n_lv >= (1u << 30)) {
         if (l == 0) { R.status = PREP_BAD; P.results[doc] = R; }
@@ -206,11 +209,11 @@ __global__ __launch_bounds__(64) void prep_kernel(PrepParams P) {
     // ---- 3. causal-chain decomposition (sequential over entries) ---------------------------------
     uint32_t clen = 0, nch = 0;      // lane c: ops in chain c so far
     uint32_t prev_row = 0;           // parent vector of entry i - 1
-    uint32_t prev_chain = 0, prev_seq0 = 0, prev_start = 0;
+    uint32_t prev_chain = 0, prev_sd = 0;   // chain, seq0 - start of entry i - 1
     {
         Chunk cp, cx, cy, cpar, cpe;
         cp.init(); cx.init(); cy.init(); cpar.init(); cpe.init();
-        uint32_t bch = 0, bsq = 0;   // chain / seq0 of the current 64 entries, flushed per 64
+        uint32_t bch = 0, bsd = 0;   // chain / seq0 - start of the current 64 entries, flushed per 64
         for (uint32_t i = 0; i < ne; i++) {
             const uint32_t k0 = cp.get(i, ne + 1, [&](uint32_t k) { return poff[k]; });
             const uint32_t k1 = cp.get(i + 1, ne + 1, [&](uint32_t k) { return poff[k]; });
@@ -219,20 +222,20 @@ __global__ __launch_bounds__(64) void prep_kernel(PrepParams P) {
             for (uint32_t k = k0; k < k1; k++) {
                 const uint32_t p = cpar.get(k, npar, [&](uint32_t x) { return par_in[x]; });
                 const uint32_t pe = cpe.get(k, npar, [&](uint32_t x) { return pent[x]; });
-                uint32_t prow, pc, ps0, pst;
+                uint32_t prow, pc, psd;
                 if (pe + 1 == i) {
-                    prow = prev_row; pc = prev_chain; ps0 = prev_seq0; pst = prev_start;
+                    prow = prev_row; pc = prev_chain; psd = prev_sd;
                 } else {
                     prow = rows[size_t(pe) * PREP_MAX_CHAINS + l];
                     if (pe >= (i & ~63u)) {   // not flushed yet: from the registers
-                        pc = rdl(bch, pe & 63u); ps0 = rdl(bsq, pe & 63u);
+                        pc = rdl(bch, pe & 63u); psd = rdl(bsd, pe & 63u);
                     } else {
-                        pc = chain[pe]; ps0 = seq0[pe];
+                        const uint2 q = cs[pe];
+                        pc = q.x; psd = q.y;
                     }
-                    pst = ent[pe].x;
                 }
                 row = max(row, prow);
-                if (l == pc) row = max(row, ps0 + (p - pst) + 1);
+                if (l == pc) row = max(row, psd + p + 1);   // seq0 + (p - start) + 1
                 if (k == k0) first_chain = pc;
             }
             rows[size_t(i) * PREP_MAX_CHAINS + l] = row;
@@ -254,12 +257,12 @@ __global__ __launch_bounds__(64) void prep_kernel(PrepParams P) {
             const uint32_t s0 = rdl(clen, c);
             if (l == c) clen += e - s;
             bch = (i & 63u) == l ? c : bch;
-            bsq = (i & 63u) == l ? s0 : bsq;
+            bsd = (i & 63u) == l ? s0 - s : bsd;
             if ((i & 63u) == 63u || i + 1 == ne) {
                 const uint32_t at = i & ~63u;
-                if (at + l <= i) { chain[at + l] = bch; seq0[at + l] = bsq; }
+                if (at + l <= i) cs[at + l] = make_uint2(bch, bsd);
             }
-            prev_row = row; prev_chain = c; prev_seq0 = s0; prev_start = s;
+            prev_row = row; prev_chain = c; prev_sd = s0 - s;
         }
     }
     wave_fence();
@@ -277,8 +280,9 @@ __global__ __launch_bounds__(64) void prep_kernel(PrepParams P) {
     // ---- 4. lane-parallel outputs -----------------------------------------------------------------
     for (uint32_t k = l; k < npar; k += 64) {   // parent slots: chain and ops of that chain up to it
         const uint32_t pe = pent[k];
-        pch[k] = chain[pe];
-        pcnt[k] = seq0[pe] + (par[k] - ent[pe].x) + 1;
+        const uint2 q = cs[pe];
+        pch[k] = q.x;
+        pcnt[k] = q.y + par[k] + 1;
     }
     wave_fence();
     for (uint32_t i = l; i < ne; i += 64) {    // entry records (dt_host.hpp PlanInput::erec)
@@ -288,7 +292,8 @@ __global__ __launch_bounds__(64) void prep_kernel(PrepParams P) {
         const uint32_t c0 = coff[i], nc = coff[i + 1] - c0;
         r[0] = e.x; r[1] = e.y; r[2] = p0; r[3] = np;
         r[4] = eop[i]; r[5] = eop[i + 1] - eop[i];
-        r[6] = chain[i]; r[7] = seq0[i];
+        const uint2 q = cs[i];
+        r[6] = q.x; r[7] = q.y + e.x;
         r[8] = c0; r[9] = nc;
         r[10] = np ? par[p0] : 0xFFFFFFFFu;
         for (uint32_t j = 0; j < 2; j++) {
@@ -304,7 +309,8 @@ __global__ __launch_bounds__(64) void prep_kernel(PrepParams P) {
     uint32_t n_ins = 0;
     for (uint32_t i = l; i < ne; i += 64) {
         const uint32_t e0 = ent[i].x, j1 = eop[i + 1];
-        const uint32_t d0 = doff[chain[i]] + seq0[i];
+        const uint2 q = cs[i];
+        const uint32_t d0 = doff[q.x] + q.y + e0;   // seq0 + chain offset
         for (uint32_t j = eop[i]; j < j1; j++) {
             const uint4 o = ops[j];   // lv, len, pos, kind | fwd << 1
             const bool del = o.w & 1u;

@@ -24,7 +24,7 @@ struct PrepDesc {
     uint64_t o_doff;    // words (PREP_MAX_CHAINS + 1)
     uint64_t o_dense;   // words (n_lv)
     uint64_t o_rows;    // words (PREP_MAX_CHAINS per entry): parent vectors of the decomposition
-    uint64_t o_scr;     // words: owner (n_par), chain, seq0 (ne each), coff, eop (ne + 1 each)
+    uint64_t o_scr;     // words (even): owner (n_par, padded), {chain, seq0 - start} (2 ne), coff, eop (ne + 1 each)
 };
 
 struct PrepResult {
@@ -41,7 +41,9 @@ struct PrepParams {
     uint32_t n_docs, max_entries;
 };
 
-inline uint64_t prep_scratch_words(uint32_t n_par, uint32_t ne) { return uint64_t(n_par) + 4ull * ne + 2; }
+// owner (n_par, padded to even), {chain, seq0 - start} pairs (2 ne), coff, eop (ne + 1 each): even,
+// so every document's pair array is 8-byte aligned
+inline uint64_t prep_scratch_words(uint32_t n_par, uint32_t ne) { return (uint64_t(n_par) + 1) / 2 * 2 + 4ull * ne + 2; }
 
 int launch_prep(const PrepParams &p, void *stream);
 
