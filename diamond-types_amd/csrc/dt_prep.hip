@@ -66,7 +66,10 @@ __device__ __forceinline__ uint32_t entry_of(const uint2 *ent, uint32_t hi, uint
     return lo < hi && lv >= ent[lo].x ? lo : 0xFFFFFFFFu;
 }
 
-__global__ __launch_bounds__(64) void prep_kernel(PrepParams P) {
+#ifndef DTGPU_PREP_WAVES
+#define DTGPU_PREP_WAVES 8   // occupancy target (tuning knob; the register budget follows from it)
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_WAVES))) void prep_kernel(PrepParams P) {
     // per entry (u16, two per LDS word): child count, then the next free slot of its children
     // list relative to coff -- half the LDS of absolute u32 slots, so more documents share a CU
     extern __shared__ uint32_t lfw[];
