@@ -289,24 +289,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
     }
     wave_fence();
     for (uint32_t i = l; i < ne; i += 64) {    // entry records (dt_host.hpp PlanInput::erec)
-        uint32_t *r = erec + size_t(i) * EREC_WORDS;
+        // five 16-byte stores (records are 80 bytes, so 16-byte aligned): words 0-3 start, end,
+        // parents offset / count; 4-7 first op run, op runs, chain, seq0; 8-10 children offset /
+        // count, first parent LV; 11-13 and 14-16 the first two parents' entry, chain, count;
+        // 17 last child
+        static_assert(EREC_WORDS == 20, "erec layout");
+        uint4 *r = reinterpret_cast<uint4 *>(erec + size_t(i) * EREC_WORDS);
         const uint2 e = ent[i];
         const uint32_t p0 = poff[i], np = poff[i + 1] - p0;
         const uint32_t c0 = coff[i], nc = coff[i + 1] - c0;
-        r[0] = e.x; r[1] = e.y; r[2] = p0; r[3] = np;
-        r[4] = eop[i]; r[5] = eop[i + 1] - eop[i];
+        const uint32_t o0 = eop[i], o1 = eop[i + 1];
         const uint2 q = cs[i];
-        r[6] = q.x; r[7] = q.y + e.x;
-        r[8] = c0; r[9] = nc;
-        r[10] = np ? par[p0] : 0xFFFFFFFFu;
-        for (uint32_t j = 0; j < 2; j++) {
-            const bool has = np > j;
-            r[11 + 3 * j] = has ? pent[p0 + j] : 0xFFFFFFFFu;
-            r[12 + 3 * j] = has ? pch[p0 + j] : 0u;
-            r[13 + 3 * j] = has ? pcnt[p0 + j] : 0u;
-        }
-        r[17] = nc ? child[c0 + nc - 1] : 0xFFFFFFFFu;
-        r[18] = 0; r[19] = 0;
+        const bool h0 = np > 0, h1 = np > 1;
+        r[0] = make_uint4(e.x, e.y, p0, np);
+        r[1] = make_uint4(o0, o1 - o0, q.x, q.y + e.x);
+        r[2] = make_uint4(c0, nc, h0 ? par[p0] : 0xFFFFFFFFu, h0 ? pent[p0] : 0xFFFFFFFFu);
+        r[3] = make_uint4(h0 ? pch[p0] : 0u, h0 ? pcnt[p0] : 0u, h1 ? pent[p0 + 1] : 0xFFFFFFFFu,
+                          h1 ? pch[p0 + 1] : 0u);
+        r[4] = make_uint4(h1 ? pcnt[p0 + 1] : 0u, nc ? child[c0 + nc - 1] : 0xFFFFFFFFu, 0u, 0u);
     }
     // op runs: apply commands and the dense chain tables (LV | is_del per chain seq)
     uint32_t n_ins = 0;
