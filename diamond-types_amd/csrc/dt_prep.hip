@@ -217,7 +217,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
         Chunk cp, cx, cy, cpar, cpe;
         cp.init(); cx.init(); cy.init(); cpar.init(); cpe.init();
         uint32_t bch = 0, bsd = 0;   // chain / seq0 - start of the current 64 entries, flushed per 64
+        uint64_t keep = 0;   // entries of the current 64 whose row a later, non-adjacent child reads
         for (uint32_t i = 0; i < ne; i++) {
+            if ((i & 63u) == 0) {   // an entry whose only child is the next one needs no stored row
+                const uint32_t j = i + l;
+                bool need = false;
+                if (j < ne) {
+                    const uint32_t c0 = coff[j], nc = coff[j + 1] - c0;
+                    need = nc > 1 || (nc == 1 && child[c0] != j + 1);
+                }
+                keep = ballot(need);
+            }
             const uint32_t k0 = cp.get(i, ne + 1, [&](uint32_t k) { return poff[k]; });
             const uint32_t k1 = cp.get(i + 1, ne + 1, [&](uint32_t k) { return poff[k]; });
             uint32_t row = 0;
@@ -241,7 +251,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
                 if (l == pc) row = max(row, psd + p + 1);   // seq0 + (p - start) + 1
                 if (k == k0) first_chain = pc;
             }
-            rows[size_t(i) * PREP_MAX_CHAINS + l] = row;
+            if ((keep >> (i & 63u)) & 1u) rows[size_t(i) * PREP_MAX_CHAINS + l] = row;
             uint32_t c = 0xFFFFFFFFu;
             if (first_chain != 0xFFFFFFFFu && rdl(row, first_chain) == rdl(clen, first_chain)) c = first_chain;
             if (c == 0xFFFFFFFFu) {
