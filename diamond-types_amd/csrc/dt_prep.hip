@@ -189,18 +189,30 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
     const uint64_t T2 = wall_clock64();
 #endif
     // ---- 2. each entry's first op run (ops are split at entry boundaries) ------------------------
+    // eop[i] = lower bound of the entry's first LV among the op runs' first LVs (strictly
+    // increasing): 64 entries at a time, each lane binary-searches 64-op windows by lane permute;
+    // a batch starts at the previous batch's last bound
     {
-        Chunk ce, co, ob;
-        ce.init(); co.init(); ob.init();
-        uint32_t j = 0, buf = 0;
-        for (uint32_t i = 0; i < ne; i++) {
-            const uint32_t s = ce.get(i, ne, [&](uint32_t k) { return ent[k].x; });
-            while (j < nops && co.get(j, nops, [&](uint32_t k) { return ops[k].x; }) < s) j++;
-            buf = (i & 63u) == l ? j : buf;
-            if ((i & 63u) == 63u || i + 1 == ne) {
-                const uint32_t at = i & ~63u;
-                if (at + l <= i) eop[at + l] = buf;
+        const uint32_t *opx = reinterpret_cast<const uint32_t *>(ops);   // ops[k].x = opx[4 k]
+        uint32_t j0 = 0;
+        for (uint32_t i0 = 0; i0 < ne; i0 += 64) {
+            const uint32_t i = i0 + l;
+            const bool live = i < ne;
+            const uint32_t s = live ? ent[i].x : 0u;
+            uint32_t res = 0xFFFFFFFFu;
+            for (uint32_t jb = j0;; jb += 64) {
+                const uint32_t k = jb + l;
+                const uint32_t ox = k < nops ? opx[4 * size_t(k)] : 0xFFFFFFFFu;
+                uint32_t c = 0;   // ops of this window below s
+#pragma unroll
+                for (uint32_t step = 32; step >= 1; step >>= 1)
+                    if (uint32_t(__shfl(int(ox), int(c + step - 1))) < s) c += step;
+                if (c == 63 && rdl(ox, 63) < s) c = 64;   // (a permute here would run divergent)
+                if (res == 0xFFFFFFFFu && c < 64) res = jb + c;
+                if (!ballot(live && res == 0xFFFFFFFFu) || jb >= nops) break;
             }
+            if (live) eop[i] = res;
+            j0 = rdl(res, min(ne - 1 - i0, 63u));
         }
         if (l == 0) eop[ne] = nops;
     }
