@@ -58,7 +58,13 @@ struct Chunk {
 // entry of `lv` among entries [0, hi) (sorted, contiguous): the previous entry first
 __device__ __forceinline__ uint32_t entry_of(const uint2 *ent, uint32_t hi, uint32_t lv) {
     if (hi && lv >= ent[hi - 1].x && lv < ent[hi - 1].y) return hi - 1;
+    // gallop back from hi (a merge's other parent is usually a few entries back), then bisect
     uint32_t lo = 0, h = hi;
+    for (uint32_t step = 1; step < h; step <<= 1) {
+        const uint32_t m = h - step;
+        if (ent[m].x <= lv) { lo = m; break; }
+        h = m;
+    }
     while (lo < h) {
         const uint32_t mid = (lo + h) >> 1;
         if (lv >= ent[mid].y) lo = mid + 1; else h = mid;
