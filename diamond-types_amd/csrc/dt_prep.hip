@@ -347,7 +347,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
             const bool del = o.w & 1u;
             opc[j] = Cmd{del ? (CMD_DEL | ((o.w & 2u) ? 16u : 0u)) : uint32_t(CMD_INS), o.x, o.y, o.z};
             if (!del) n_ins += o.y;
-            for (uint32_t v = 0; v < o.y; v++) dense[d0 + (o.x - e0) + v] = (o.x + v) | (del ? TL_DEL : 0u);
+            // the run's dense slots: 16-byte stores between a scalar head and tail
+            const uint32_t flag = del ? TL_DEL : 0u;
+            uint32_t *dp = dense + uint32_t(d0 + (o.x - e0));
+            uint32_t v = 0;
+            for (; v < o.y && (reinterpret_cast<uintptr_t>(dp + v) & 15u); v++) dp[v] = (o.x + v) | flag;
+            for (; v + 4 <= o.y; v += 4) {
+                const uint32_t b = o.x + v;
+                *reinterpret_cast<uint4 *>(dp + v) = make_uint4(b | flag, (b + 1) | flag, (b + 2) | flag, (b + 3) | flag);
+            }
+            for (; v < o.y; v++) dp[v] = (o.x + v) | flag;
         }
     }
 #ifdef DTGPU_PREP_PROF
