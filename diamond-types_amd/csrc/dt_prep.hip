@@ -55,6 +55,22 @@ struct Chunk {
     }
 };
 
+// two such words per index, refilled by one load issue (one round trip, not two)
+struct Chunk2 {
+    uint32_t blk, a, b;
+    __device__ __forceinline__ void init() { blk = 0xFFFFFFFFu; a = b = 0; }
+    template <typename F>
+    __device__ __forceinline__ uint2 get(uint32_t i, uint32_t n, F load) {
+        if ((i & ~63u) != blk) {
+            blk = i & ~63u;
+            const uint32_t k = blk + lane();
+            const uint2 v = k < n ? load(k) : make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+            a = v.x; b = v.y;
+        }
+        return make_uint2(rdl(a, i & 63u), rdl(b, i & 63u));
+    }
+};
+
 // entry of `lv` among entries [0, hi) (sorted, contiguous): the previous entry first
 __device__ __forceinline__ uint32_t entry_of(const uint2 *ent, uint32_t hi, uint32_t lv) {
     if (hi && lv >= ent[hi - 1].x && lv < ent[hi - 1].y) return hi - 1;
@@ -232,8 +248,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
     uint32_t prev_row = 0;           // parent vector of entry i - 1
     uint32_t prev_chain = 0, prev_sd = 0;   // chain, seq0 - start of entry i - 1
     {
-        Chunk cp, cx, cy, cpar, cpe;
-        cp.init(); cx.init(); cy.init(); cpar.init(); cpe.init();
+        Chunk cp;
+        Chunk2 cxy, cpp;   // entry (start, end); parent slot (LV, entry)
+        cp.init(); cxy.init(); cpp.init();
         uint32_t bch = 0, bsd = 0;   // chain / seq0 - start of the current 64 entries, flushed per 64
         uint64_t keep = 0;   // entries of the current 64 whose row a later, non-adjacent child reads
         for (uint32_t i = 0; i < ne; i++) {
@@ -251,8 +268,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
             uint32_t row = 0;
             uint32_t first_chain = 0xFFFFFFFFu;
             for (uint32_t k = k0; k < k1; k++) {
-                const uint32_t p = cpar.get(k, npar, [&](uint32_t x) { return par_in[x]; });
-                const uint32_t pe = cpe.get(k, npar, [&](uint32_t x) { return pent[x]; });
+                const uint2 pp = cpp.get(k, npar, [&](uint32_t x) { return make_uint2(par_in[x], pent[x]); });
+                const uint32_t p = pp.x, pe = pp.y;
                 uint32_t prow, pc, psd;
                 if (pe + 1 == i) {
                     prow = prev_row; pc = prev_chain; psd = prev_sd;
@@ -283,8 +300,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
                 }
                 c = nch++;
             }
-            const uint32_t s = cx.get(i, ne, [&](uint32_t k) { return ent[k].x; });
-            const uint32_t e = cy.get(i, ne, [&](uint32_t k) { return ent[k].y; });
+            const uint2 se = cxy.get(i, ne, [&](uint32_t k) { return ent[k]; });
+            const uint32_t s = se.x, e = se.y;
             const uint32_t s0 = rdl(clen, c);
             if (l == c) clen += e - s;
             bch = (i & 63u) == l ? c : bch;
