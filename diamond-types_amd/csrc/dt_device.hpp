@@ -41,8 +41,7 @@ struct BatchParams {
     const uint32_t *cbyte;
     const uint8_t *content;
     const uint32_t *aruns;
-    uint32_t *pos;
-    uint32_t *cv;
+    uint32_t *pos;   // per LV: block | count << 16 (dt_replay.hip pc[])
     unsigned long long *ao;
     uint32_t *items;
     unsigned long long *m2;   // per block: visible, live slot masks

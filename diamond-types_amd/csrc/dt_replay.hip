@@ -15,22 +15,32 @@
 //   block -> (superblock, index) opos; the superblock lists and totals) lives in LDS for
 //   documents whose index fits the LDS budget and in HBM otherwise (same code).  A full block
 //   splits 64 -> 32 + 32 and a full superblock 64 -> 32 + 32, so a split costs O(64) work.
-//   pos[lv]      inserted LV: block << 6 | slot.  Written with plain stores (an insert
-//                rewrites the positions of the items it shifts; no read-modify-write).
-//   cv[lv]       inserted LV: count (0 NIY, 1 inserted, k >= 2 deleted k-1 times); the only
-//                per-item word that needs an atomic (a retreat/advance pass may touch one item
-//                from two lanes).
+//   pc[lv]       inserted LV: its block (low 16 bits) | its count << 16 (count 0 = NIY, 1 =
+//                inserted, k >= 2 deleted k-1 times).  One word, so a retreat/advance lane and a
+//                block rebuild read one array.  The block is written when the item is inserted
+//                and when a split moves it to a new block -- never for the items an insert shifts
+//                inside a block (content-tree notifies its marker index only when an entry
+//                changes leaf, crates/content-tree/src/mutations.rs:76-110,196;
+//                src/listmerge/markers.rs).  The slot, where needed (YjsMod's document-order
+//                keys), is found in the row.
+//   Block masks (visible / live) are a cache of the counts: a retreat/advance pass changes
+//   counts only and marks the blocks whose masks it invalidated (DIRTY bit of the packed
+//   count); the next command that loads such a block rebuilds its masks from pc[].
 //   ao[lv]       Ins: origin_left | origin_right << 32; Del: the item it deleted.
-//   Every per-document structure is touched by its own wave only, so all atomics are
-//   workgroup-scope and stay in the CU's L2 path.
+//   Every per-document structure is touched by its own wave only, so no global atomics are
+//   needed: on gfx950 every global atomic, whatever its scope, leaves L2 as a memory-side
+//   request (profiles/r2_calib: 32 B of WRITE_SIZE per atomic even on an L2-resident line),
+//   while plain stores are absorbed by the write-back L2.  Lanes of one pass that touch the
+//   same item are merged in registers; the index counts live in LDS (LDS tier) or take one
+//   atomic per distinct block (HBM tier).
 //
 // Commands: INS / DEL apply one op run; TOG applies one walk step's whole retreat + advance
 // set in one lane-parallel pass.  Counters make that legal: a retreat subtracts one, an advance
-// adds one, visibility (count == 1) and liveness (count >= 1) flip by XOR whenever the returned
-// old count crosses the boundary, and XOR / add commute, so the pass ends in the state the
-// reference reaches by retreating in descending LV order and then advancing
-// (advance_retreat.rs:58-153).  Intermediate counts never go negative: the retreat set is
-// contained in the current version.
+// adds one, and an item's final count is its old count plus the sum of its deltas whatever the
+// order, so the pass ends in the state the reference reaches by retreating in descending LV
+// order and then advancing (advance_retreat.rs:58-153).  Visibility (count == 1) and liveness
+// (count >= 1) follow from the old and new counts.  The retreat set is contained in the
+// current version, so old count + the retreats never goes negative (checked).
 //
 // The plan ends with a TOG that advances to the tip, so the final visible set is the checkout:
 // materialisation stream-compacts visible items in document order (list/merge.rs:63-95).
@@ -104,15 +114,16 @@ constexpr uint32_t END_ID = 0xFFFFFFFEu;
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 // packed per-block counts
 constexpr uint32_t C_VIS = 1u, C_LIVE = 1u << 8, C_ITEMS = 1u << 16;
-constexpr uint32_t C_UP = 1u << 24;   // transformed-ops mode: items never deleted
+constexpr uint32_t C_UP = 1u << 24;   // transformed-ops mode: items never deleted (<= 64: 7 bits)
+constexpr uint32_t C_DIRTY = 1u << 31;   // the block's masks are stale (a toggle changed counts)
 DEV uint32_t c_vis(uint32_t c) { return c & 0xFFu; }
 DEV uint32_t c_live(uint32_t c) { return (c >> 8) & 0xFFu; }
 DEV uint32_t c_items(uint32_t c) { return (c >> 16) & 0xFFu; }
-DEV uint32_t c_up(uint32_t c) { return c >> 24; }
-
-DEV uint32_t pos_blk(uint32_t w) { return w >> 6; }
-DEV uint32_t pos_slot(uint32_t w) { return w & 63u; }
-DEV uint32_t pos_of(uint32_t b, uint32_t s) { return (b << 6) | s; }
+DEV uint32_t c_up(uint32_t c) { return (c >> 24) & 0x7Fu; }
+// pc[] word: block | count << 16 (MAX_DOC_BLOCKS = 65535; a count past 65535 is ErrCheckout)
+DEV uint32_t pc_blk(uint32_t w) { return w & 0xFFFFu; }
+DEV uint32_t pc_cnt(uint32_t w) { return w >> 16; }
+DEV uint32_t pc_of(uint32_t b, uint32_t k) { return b | (k << 16); }
 
 // L2-coherent accesses (returning atomics and loads must never meet a stale L1 line).
 template <typename T> DEV T ld_sc(const T *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
@@ -120,6 +131,7 @@ template <typename T> DEV void st_sc(T *p, T v) { __hip_atomic_store(p, v, __ATO
 DEV uint32_t cv_add(uint32_t *p, uint32_t d) { return __hip_atomic_fetch_add(p, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 template <typename T> DEV void at_xor(T *p, T v) { __hip_atomic_fetch_xor(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 template <typename T> DEV void at_add(T *p, T v) { __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+template <typename T> DEV void at_or(T *p, T v) { __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 
 // Index accessors.  LDS tier: plain LDS (one wave owns the workgroup).  HBM tier: words that
 // atomics touch are read L2-coherently.
@@ -142,8 +154,7 @@ struct Doc {
     uint32_t n_aruns;
     uint32_t ascii;
     // per-LV state (HBM)
-    uint32_t *pos;   // inserted LV: block << 6 | slot (plain stores only)
-    uint32_t *cv;    // inserted LV: count (0 NIY, 1 inserted, k >= 2 deleted k-1 times)
+    uint32_t *pc;    // inserted LV: block | count << 16 (plain loads / stores)
     u64 *ao;         // Ins: origin_left | origin_right << 32; Del: the item it deleted (low word)
     // blocks (HBM)
     uint32_t *items;
@@ -219,9 +230,37 @@ template <bool L> DEV uint32_t key_at(const Doc &D, uint32_t b, uint32_t s) {
     const uint32_t o = opos_of<L>(D, b);
     return (ix<L>(D.sbpos + (o >> 6)) << 12) | ((o & 63u) << 6) | s;
 }
+// Slot of `item` in block b, per lane (divergent lanes allowed): the first match in the row.
+// Rows are never cleared above their count, so a stale copy of an item can sit there -- but
+// only above the live part, and the live copy comes first.
+DEV uint32_t find_slot(const Doc &D, uint32_t b, uint32_t item) {
+    const uint4 *row = reinterpret_cast<const uint4 *>(D.items + size_t(b) * BLK);
+    uint32_t s = BLK;
+    for (uint32_t q = 0; q < BLK / 4 && s == BLK; q += 2) {   // 32 bytes per round: few VGPRs
+        uint4 v[2];
+#pragma unroll
+        for (uint32_t j = 0; j < 2; j++) v[j] = row[q + j];
+#pragma unroll
+        for (int j = 1; j >= 0; j--) {
+            const uint32_t o = 4 * (q + uint32_t(j));
+            if (v[j].w == item) s = o + 3;
+            if (v[j].z == item) s = o + 2;
+            if (v[j].y == item) s = o + 1;
+            if (v[j].x == item) s = o;
+        }
+    }
+    return s;
+}
+// Document-order key of an inserted item, per lane.
 template <bool L> DEV uint32_t key_of(const Doc &D, uint32_t item) {
-    const uint32_t w = D.pos[item];
-    return key_at<L>(D, pos_blk(w), pos_slot(w));
+    const uint32_t b = pc_blk(ld_sc(D.pc + item));
+    return key_at<L>(D, b, find_slot(D, b, item));
+}
+// Same for a wave-uniform item: one row load and a ballot.
+template <bool L> DEV uint32_t ukey_of(const Doc &D, uint32_t item) {
+    const uint32_t b = U(pc_blk(ld_sc(D.pc + item)));
+    const u64 m = __ballot(D.items[size_t(b) * BLK + lane_id()] == item);
+    return U(key_at<L>(D, b, first_lane(m)));
 }
 
 // Block holding visible index p and the rank k of that item among the block's visible items
@@ -364,9 +403,9 @@ DEV uint32_t split_block(Doc &D, uint32_t b, uint32_t c, uint32_t it, u64 mv, u6
         mu_lo = mu & lanes_below(c);
         mu_hi = c >= 64 ? 0ull : mu >> c;
     }
-    if (l >= c) {
+    if (l >= c) {   // the moved items change block (content-tree's notify on a leaf split)
         D.items[size_t(b2) * BLK + (l - c)] = it;
-        D.pos[it] = pos_of(b2, l - c);
+        st_sc(D.pc + it, (ld_sc(D.pc + it) & 0xFFFF0000u) | b2);
     }
     const u64 lo = lanes_below(c);
     const u64 mv_hi = c >= 64 ? 0ull : mv >> c, ml_hi = c >= 64 ? 0ull : ml >> c;
@@ -464,15 +503,12 @@ DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml,
         uint64_t tr = tick<PROF>();
         const uint32_t m = min(k, BLK - bc);
         uint32_t *items = D.items + size_t(b) * BLK;
-        // the block after the insert, lane = slot: shifted items and the new ones are written
-        // with one store each for items and positions
+        // the block after the insert, lane = slot: the row from the insert point on is written
+        // with one store; only the new items get a block in pos[] (shifted ones stay put)
         const uint32_t shifted = shfl(it, l >= m ? l - m : l);
         it = l < s ? it : (l < s + m ? lv + (l - s) : shifted);
-        if (l >= s && l < bc + m) {
-            items[l] = it;
-            D.pos[it] = pos_of(b, l);
-        }
-        if (l >= s && l < s + m) st_sc(D.cv + it, 1u);   // cv: atomics elsewhere, so scoped stores
+        if (l >= s && l < bc + m) items[l] = it;
+        if (l >= s && l < s + m) st_sc(D.pc + it, pc_of(b, 1u));
         if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_R1] += t - tr; tr = t; }
         const u64 low = lanes_below(s);
         const u64 ins = lanes_below(m) << s;
@@ -599,15 +635,27 @@ DEV void yjs_scan(Doc &D, uint32_t &b, uint32_t &s, uint32_t rb, uint32_t rs, ui
     s = U(s);
 }
 
-// Items and masks of block b into registers (items lane by lane, masks wave-uniform).
+// Items and masks of block b (packed count c) into registers: items lane by lane, masks
+// wave-uniform.  A block whose masks a retreat/advance pass invalidated (DIRTY) gets them
+// rebuilt from the items' counts and stored back clean.
 template <bool L>
-DEV void load_block(const Doc &D, uint32_t b, uint32_t bc, uint32_t &it, u64 &mv, u64 &ml) {
+DEV void load_block(Doc &D, uint32_t b, uint32_t c, uint32_t &it, u64 &mv, u64 &ml) {
     const uint32_t l = lane_id();
+    const uint32_t bc = c_items(c);
     it = l < bc ? D.items[size_t(b) * BLK + l] : 0;
-    u64 x = 0;
-    if (l < 2) x = ld_sc(D.m2 + 2 * size_t(b) + l);
-    mv = bcast64(x, 0);
-    ml = bcast64(x, 1);
+    if (c & C_DIRTY) {
+        const uint32_t k = l < bc ? pc_cnt(ld_sc(D.pc + it)) : 0u;
+        mv = __ballot(l < bc && k == 1u);
+        ml = __ballot(l < bc && k != 0u);
+        if (l < 2) st_sc(D.m2 + 2 * size_t(b) + l, l == 0 ? mv : ml);
+        if (l == 0) D.cnt[b] = c & ~C_DIRTY;
+        wave_fence();
+    } else {
+        u64 x = 0;
+        if (l < 2) x = ld_sc(D.m2 + 2 * size_t(b) + l);
+        mv = bcast64(x, 0);
+        ml = bcast64(x, 1);
+    }
 }
 
 // Apply an insert run at visible position pos (M2Tracker::apply Ins + integrate,
@@ -625,11 +673,12 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
         kk = f.k;
     }
     if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_FIND] += t - tp; tp = t; }
-    const uint32_t bc = c_items(U(ix<L>(D.cnt + b)));
+    const uint32_t c0 = U(ix<L>(D.cnt + b));
+    const uint32_t bc = c_items(c0);
     uint32_t it;
     u64 mv, ml;
     if (b == D.cb) { it = D.cit; mv = D.cmv; ml = D.cml; }
-    else load_block<L>(D, b, bc, it, mv, ml);
+    else load_block<L>(D, b, c0, it, mv, ml);
     uint32_t s = 0, ol = ROOT_ID;
     if (pos) {
         const uint32_t s0 = select_bit(mv, kk);
@@ -651,8 +700,11 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
         rb = next_live_block<L>(D, b);
         if (D.err) return;
         if (rb != NONE) {
-            rs = first_lane(U64(ld_sc(D.m2 + 2 * size_t(rb) + 1)));
-            orr = U(D.items[size_t(rb) * BLK + rs]);
+            uint32_t rit;
+            u64 rmv, rml;
+            load_block<L>(D, rb, U(ix<L>(D.cnt + rb)), rit, rmv, rml);
+            rs = first_lane(rml);
+            orr = U(bcast(rit, rs));
         } else {
             rs = 0;
             orr = END_ID;
@@ -666,14 +718,14 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
     }
     if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_ORR] += t - tp; tp = t; }
     if (!direct) {
-        const uint32_t my_l = ol == ROOT_ID ? 0u : U(key_of<L>(D, ol)) + 1u;
-        const uint32_t my_r = orr == END_ID ? 0xFFFFFFFFu : U(key_of<L>(D, orr));
+        const uint32_t my_l = ol == ROOT_ID ? 0u : ukey_of<L>(D, ol) + 1u;
+        const uint32_t my_r = orr == END_ID ? 0xFFFFFFFFu : ukey_of<L>(D, orr);
         const uint32_t b0 = b;
         yjs_scan<L>(D, b, s, rb, rs, my_l, my_r, orr, lv);
         if (D.err) return;
         if (b != b0) {
             if (b == D.cb) { it = D.cit; mv = D.cmv; ml = D.cml; }
-            else load_block<L>(D, b, c_items(U(ix<L>(D.cnt + b))), it, mv, ml);
+            else load_block<L>(D, b, U(ix<L>(D.cnt + b)), it, mv, ml);
         }
         if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_YJS] += t - tp; tp = t; D.prof[P_N_YJS]++; }
     }
@@ -695,11 +747,12 @@ DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
         Found f;
         if (!find_vis<L>(D, pos, f)) { fail(D, ErrCheckout, 14); return; }
         const uint32_t b = f.b, kk = f.k;
-        const uint32_t c = U(ix<L>(D.cnt + b));
+        const uint32_t c0 = U(ix<L>(D.cnt + b));
         uint32_t it;
         u64 mv, ml;
         if (b == D.cb) { it = D.cit; mv = D.cmv; ml = D.cml; }
-        else load_block<L>(D, b, c_items(c), it, mv, ml);
+        else load_block<L>(D, b, c0, it, mv, ml);
+        const uint32_t c = c0 & ~C_DIRTY;   // load_block left the block clean
         const uint32_t avail = c_vis(c) - kk;
         const uint32_t take = min(avail, n - j0);
         const uint32_t r = uint32_t(__popcll(mv & lanes_below(l)));
@@ -715,7 +768,7 @@ DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
         if (sel) {
             const uint32_t j = j0 + (r - kk);
             const uint32_t dlv = fwd ? lv + j : lv + n - 1 - j;
-            st_sc(D.cv + it, 2u);   // visible (count 1) -> deleted once
+            st_sc(D.pc + it, pc_of(b, 2u));   // visible (count 1) -> deleted once
             *reinterpret_cast<uint32_t *>(D.ao + dlv) = it;
             if (XF) {
                 // LV order applies a forward run left to right (the run's items to the left are
@@ -747,59 +800,102 @@ DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
 // One walk step's retreat + advance set (advance_retreat.rs:58-153), lane-parallel.
 // Entry: LV | is_del << 30 | advance << 31.
 // `pre` is the first 64-entry chunk when the caller prefetched it (have_pre).
+// Counts change with plain loads and stores (the wave owns the document): lanes that touch the
+// same item -- only a deleted item can be touched twice (two deletes of it, or a delete and its
+// own insert) -- are merged first.  Blocks whose visibility / liveness changed are marked
+// DIRTY; their masks are rebuilt when a command next loads them.
 template <bool L>
 DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_pre) {
     const uint32_t l = lane_id();
     for (uint32_t j = 0; j < n; j += 64) {
         if (!charge(D)) return;
-        bool bad = false, hit_cached = false;
+        bool bad = false, act = false, del = false;
+        uint32_t item = 0;
+        int32_t d = 0, dneg = 0;   // net delta; sum of the retreats (applied first)
         if (j + l < n) {
             const uint32_t e = (j == 0 && have_pre) ? pre : D.tlist[off + j + l];
             const uint32_t lv = e & 0x3FFFFFFFu;
-            const bool is_del = (e >> 30) & 1u, adv = (e >> 31) != 0;
-            uint32_t item = lv;
+            del = (e >> 30) & 1u;
+            const bool adv = (e >> 31) != 0;
+            item = lv;
             if (lv >= D.n_lv) bad = true;
-            else if (is_del) item = *reinterpret_cast<const uint32_t *>(D.ao + lv);
+            else if (del) item = *reinterpret_cast<const uint32_t *>(D.ao + lv);
             if (!bad && item >= D.n_lv) bad = true;
-            if (!bad) {
-                const uint32_t w = D.pos[item];
-                const uint32_t oc = cv_add(D.cv + item, adv ? 1u : 0xFFFFFFFFu);
-                const uint32_t nc = adv ? oc + 1 : oc - 1;
-                const uint32_t b = pos_blk(w);
-                hit_cached = b == D.cb;
-                if ((!adv && oc == 0) || (adv && oc >= 0x7FFFFFFFu) || b >= D.nb) {
-                    bad = true;
-                } else {
-                    const u64 bit = 1ull << pos_slot(w);
-                    const bool fv = (oc == 1) != (nc == 1), fl = (oc != 0) != (nc != 0);
-                    if (fv || fl) {
-                        const uint32_t tp = ix<L>(D.sbpos + (opos_of<L>(D, b) >> 6));
-                        uint32_t dc = 0;
-                        if (fv) {
-                            at_xor(D.m2 + 2 * size_t(b), bit);
-                            const uint32_t d = nc == 1 ? 1u : 0xFFFFFFFFu;
-                            at_add(D.top + tp, d);
-                            dc += d * C_VIS;
-                        }
-                        if (fl) {
-                            at_xor(D.m2 + 2 * size_t(b) + 1, bit);
-                            const uint32_t d = nc != 0 ? 1u : 0xFFFFFFFFu;
-                            at_add(D.tlive + tp, d);
-                            dc += d * C_LIVE;
-                        }
-                        at_add(D.cnt + b, dc);
-                    }
+            act = !bad;
+            d = adv ? 1 : -1;
+            dneg = adv ? 0 : -1;
+        }
+        if (__ballot(bad)) { fail(D, ErrCheckout, 16); return; }
+        for (u64 dm = __ballot(act && del); dm;) {
+            if (!charge(D)) return;
+            const uint32_t t = bcast(item, first_lane(dm));
+            const u64 same = __ballot(act && item == t);
+            if (same & (same - 1)) {
+                const bool mine = (same >> l) & 1ull;
+                const int32_t sum = int32_t(wave_sum(mine ? uint32_t(d) : 0u));
+                const int32_t neg = int32_t(wave_sum(mine ? uint32_t(dneg) : 0u));
+                if (mine) {
+                    if (l == first_lane(same)) { d = sum; dneg = neg; }
+                    else act = false;
                 }
             }
+            dm &= ~same;
         }
-        if (__ballot(hit_cached)) D.cb = NONE;
+        bool fv = false, fl = false;
+        uint32_t b = 0;
+        int32_t dv = 0, dl = 0;
+        if (act) {
+            const uint32_t w = ld_sc(D.pc + item);
+            b = pc_blk(w);
+            const uint32_t oc = pc_cnt(w);
+            const uint32_t nc = oc + uint32_t(d);
+            if (int32_t(oc) + dneg < 0 || int32_t(oc) + d > 0xFFFF || b >= D.nb) {
+                bad = true;
+            } else {
+                st_sc(D.pc + item, pc_of(b, nc));
+                fv = (oc == 1) != (nc == 1);
+                fl = (oc != 0) != (nc != 0);
+                dv = fv ? (nc == 1 ? 1 : -1) : 0;
+                dl = fl ? (nc != 0 ? 1 : -1) : 0;
+            }
+        }
         if (__ballot(bad)) { fail(D, ErrCheckout, 16); return; }
+        const bool flip = fv || fl;
+        if (__ballot(flip && b == D.cb)) D.cb = NONE;
+        if (L) {   // LDS index: per-lane LDS atomics
+            if (flip) {
+                const uint32_t tp = ix<L>(D.sbpos + (opos_of<L>(D, b) >> 6));
+                if (fv) at_add(D.top + tp, uint32_t(dv));
+                if (fl) at_add(D.tlive + tp, uint32_t(dl));
+                at_add(D.cnt + b, uint32_t(dv) * C_VIS + uint32_t(dl) * C_LIVE);
+                at_or(D.cnt + b, C_DIRTY);
+            }
+        } else {   // HBM index: one atomic per distinct block (a global atomic is a memory-side request)
+            for (u64 pend = __ballot(flip); pend;) {
+                if (!charge(D)) return;
+                const uint32_t f = first_lane(pend);
+                const uint32_t bb = bcast(b, f);
+                const u64 same = __ballot(flip && b == bb);
+                const bool mine = (same >> l) & 1ull;
+                const uint32_t sv = wave_sum(mine ? uint32_t(dv) : 0u), sl = wave_sum(mine ? uint32_t(dl) : 0u);
+                if (l == f) {
+                    const uint32_t tp = ix<L>(D.sbpos + (opos_of<L>(D, bb) >> 6));
+                    if (sv) at_add(D.top + tp, sv);
+                    if (sl) at_add(D.tlive + tp, sl);
+                    at_add(D.cnt + bb, sv * C_VIS + sl * C_LIVE);
+                    at_or(D.cnt + bb, C_DIRTY);
+                }
+                pend &= ~same;
+            }
+        }
     }
     wave_fence();
 }
 
 // Stream-compact the visible items (the tip's content) in document order into out[]
 // (list/merge.rs:63-95).  G blocks per round keep that many dependent gathers in flight.
+// Visibility comes from the counts (the final advance to the tip leaves masks stale): the
+// count and the byte offset of every item are gathered together, so this adds no round trip.
 template <bool L>
 DEV void materialise(Doc &D, uint8_t *out, uint32_t cap, uint32_t &len_out, u64 &hash_out) {
     constexpr uint32_t G = 8;
@@ -810,19 +906,24 @@ DEV void materialise(Doc &D, uint8_t *out, uint32_t cap, uint32_t &len_out, u64 
         const uint32_t S = U(ix<L>(D.top + p)) >> 16;
         const uint32_t n = U(ix<L>(D.sbn + S));
         for (uint32_t i = 0; i < n; i += G) {
-            // lane g < G fetches block g's visible mask
+            // lane g < G fetches block g's id and item count
             const uint32_t bl = l < G && i + l < n ? ix16<L>(D.sbl + size_t(S) * SBC + i + l) : 0;
-            const u64 mvl = l < G && i + l < n ? ld_sc(D.m2 + 2 * size_t(bl)) : 0ull;
-            uint32_t it[G], cb[G];
+            const uint32_t nl = l < G && i + l < n ? c_items(ix<L>(D.cnt + bl)) : 0;
+            uint32_t it[G], cb[G], k[G];
             bool vis[G];
 #pragma unroll
             for (uint32_t g = 0; g < G; g++) {
                 const uint32_t b = bcast(bl, g);
-                vis[g] = (bcast64(mvl, g) >> l) & 1ull;
+                vis[g] = l < bcast(nl, g);
                 it[g] = vis[g] ? D.items[size_t(b) * BLK + l] : 0;
             }
 #pragma unroll
-            for (uint32_t g = 0; g < G; g++) cb[g] = vis[g] ? D.cbyte[it[g]] : 0;
+            for (uint32_t g = 0; g < G; g++) {
+                k[g] = vis[g] ? pc_cnt(ld_sc(D.pc + it[g])) : 0;
+                cb[g] = vis[g] ? D.cbyte[it[g]] : 0;
+            }
+#pragma unroll
+            for (uint32_t g = 0; g < G; g++) vis[g] = vis[g] && k[g] == 1u;
             if (D.ascii) {
                 uint8_t by[G];
 #pragma unroll
@@ -859,6 +960,8 @@ DEV void materialise(Doc &D, uint8_t *out, uint32_t cap, uint32_t &len_out, u64 
 }
 
 // Debug-mode consistency check of the whole structure (DTGPU_DEBUG=1): returns 0 or a code.
+// Checks every block's counts against its masks (clean blocks) or against cv[] (DIRTY blocks),
+// and that pos[] names each item's block.
 template <bool L, bool XF>
 DEV uint32_t check_invariants(Doc &D, DocResult *res) {
     const uint32_t l = lane_id();
@@ -874,7 +977,14 @@ DEV uint32_t check_invariants(Doc &D, DocResult *res) {
             if (U(opos_of<L>(D, b)) != ((S << 6) | i)) return 201;
             const uint32_t c = U(ix<L>(D.cnt + b));
             const uint32_t cnt = c_items(c);
-            const u64 mv = U64(ld_sc(D.m2 + 2 * size_t(b))), ml = U64(ld_sc(D.m2 + 2 * size_t(b) + 1));
+            const bool dirty = (c & C_DIRTY) != 0;
+            u64 mv = U64(ld_sc(D.m2 + 2 * size_t(b))), ml = U64(ld_sc(D.m2 + 2 * size_t(b) + 1));
+            if (dirty) {   // stale masks: check the counts against cv[] instead
+                const uint32_t i2 = l < cnt ? D.items[size_t(b) * BLK + l] : 0;
+                const uint32_t k = l < cnt && i2 < D.n_lv ? pc_cnt(ld_sc(D.pc + i2)) : 0u;
+                mv = __ballot(l < cnt && k == 1u);
+                ml = __ballot(l < cnt && k != 0u);
+            }
             if (uint32_t(__popcll(mv)) != c_vis(c) || uint32_t(__popcll(ml)) != c_live(c)) return 207;
             if (XF && uint32_t(__popcll(U64(ld_sc(D.mup + b)))) != c_up(c)) return 209;
             if (XF) tu += c_up(c);
@@ -886,11 +996,11 @@ DEV uint32_t check_invariants(Doc &D, DocResult *res) {
                 it = D.items[size_t(b) * BLK + l];
                 if (it >= D.n_lv) bad = true;
                 else {
-                    w = D.pos[it];
-                    const uint32_t k = ld_sc(D.cv + it);
+                    w = pc_blk(ld_sc(D.pc + it));
+                    const uint32_t k = pc_cnt(ld_sc(D.pc + it));
                     if (((mv >> l) & 1) != (k == 1 ? 1u : 0u)) bad = true;
                     if (((ml >> l) & 1) != (k != 0 ? 1u : 0u)) bad = true;
-                    if (pos_blk(w) != b || pos_slot(w) != l) bad = true;
+                    if (w != b || find_slot(D, b, it) != l) bad = true;
                 }
             } else if (((mv | ml) >> l) & 1) bad = true;
             const u64 bm = __ballot(bad);
@@ -1053,8 +1163,7 @@ __global__ __launch_bounds__(64) void replay_kernel(BatchParams P) {
     D.aruns = P.aruns + dd.arun_off;
     D.n_aruns = U(dd.n_aruns);
     D.ascii = U(dd.ascii);
-    D.pos = P.pos + dd.lv_off;
-    D.cv = P.cv + dd.lv_off;
+    D.pc = P.pos + dd.lv_off;
     D.ao = P.ao + dd.lv_off;
     D.items = P.items + dd.blk_off * BLK;
     D.m2 = P.m2 + 2 * dd.blk_off;

@@ -59,7 +59,7 @@ struct dtgpu_batch {
     uint32_t n_gpu_planned = 0;
 
     DevBuf<Cmd> d_cmds;
-    DevBuf<uint32_t> d_tlist, d_cbyte, d_aruns, d_pos, d_cv, d_items, d_lists, d_counter;
+    DevBuf<uint32_t> d_tlist, d_cbyte, d_aruns, d_pos, d_items, d_lists, d_counter;
     DevBuf<unsigned long long> d_ao, d_m2, d_mup;
     DevBuf<uint32_t> d_tup, d_xf;   // transformed-ops batches only
     bool xf_mode = false;
@@ -355,7 +355,6 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     lists.insert(lists.end(), B->large_list.begin(), B->large_list.end());
     CK(B->d_lists.upload(lists, s));
     CK(B->d_pos.alloc(lv_total));
-    CK(B->d_cv.alloc(lv_total));
     CK(B->d_ao.alloc(lv_total));
     CK(B->d_items.alloc(blk_total * 64));
     CK(B->d_m2.alloc(2 * blk_total));
@@ -384,7 +383,6 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     base.content = B->d_content.p;
     base.aruns = B->d_aruns.p;
     base.pos = B->d_pos.p;
-    base.cv = B->d_cv.p;
     base.ao = B->d_ao.p;
     base.items = B->d_items.p;
     base.m2 = B->d_m2.p;
@@ -591,7 +589,6 @@ dtgpu_status stage_device(const uint8_t *const *docs, const size_t *lens, size_t
     lists.insert(lists.end(), B->large_list.begin(), B->large_list.end());
     CK(B->d_lists.upload(lists, s));
     CK(B->d_pos.alloc(lv_total));
-    CK(B->d_cv.alloc(lv_total));
     CK(B->d_ao.alloc(lv_total));
     CK(B->d_items.alloc(blk_total * 64));
     CK(B->d_m2.alloc(2 * blk_total));
@@ -611,7 +608,6 @@ dtgpu_status stage_device(const uint8_t *const *docs, const size_t *lens, size_t
     base.content = Dd.content.p;
     base.aruns = B->d_aruns.p;
     base.pos = B->d_pos.p;
-    base.cv = B->d_cv.p;
     base.ao = B->d_ao.p;
     base.items = B->d_items.p;
     base.m2 = B->d_m2.p;
@@ -638,9 +634,10 @@ dtgpu_status stage_device(const uint8_t *const *docs, const size_t *lens, size_t
     return DTGPU_OK;
 }
 
-// Plan (device) then replay, on stream s.
+// One checkout pass on stream s: prep (device-staged batches), plan (device), replay.
 int launch_all(dtgpu_batch *B, hipStream_t s) {
     if (B->xf_mode) return launch_replay_xf(B->large, s);
+    if (B->dec && launch_prep(B->prep, s)) return ErrHip;   // device-staged: walker inputs first
     if (B->n_gpu_planned) {
         int e = launch_plan(B->plan, s);
         if (e) return e;
@@ -1010,19 +1007,28 @@ dtgpu_status dtgpu_batch_run(dtgpu_batch *B, void *stream) {
 dtgpu_status dtgpu_batch_run_timed(dtgpu_batch *B, float *ms) {
     if (!B) return DTGPU_ERR_ARG;
     if (hipSetDevice(B->device) != hipSuccess) return DTGPU_ERR_HIP;
-    // plan (device walk planner) + replay + materialisation, all on the batch's stream
-    if (hipEventRecord(B->ev0, B->stream) != hipSuccess) return DTGPU_ERR_HIP;
-    if (B->n_gpu_planned && launch_plan(B->plan, B->stream) != OK) return DTGPU_ERR_HIP;
-    if (hipEventRecord(B->ev_mid, B->stream) != hipSuccess) return DTGPU_ERR_HIP;
-    int s = B->xf_mode ? launch_replay_xf(B->large, B->stream) : launch_replay(B->small, B->large, B->stream, B->n_cu);
-    if (s) return dtgpu_status(s);
-    if (hipEventRecord(B->ev1, B->stream) != hipSuccess) return DTGPU_ERR_HIP;
+    // one checkout pass of the whole batch on its stream: for device-staged batches the walker
+    // inputs (prep_kernel: parent entries, children CSR, chain decomposition -- what
+    // SpanningTreeWalker::new builds inside checkout_tip, txn_trace.rs:114-188), then the walk
+    // planner, then replay + materialisation
+    hipStream_t s = B->stream;
+    const bool prep = B->dec && !B->xf_mode;
+    if (hipEventRecord(B->ev_prep, s) != hipSuccess) return DTGPU_ERR_HIP;
+    if (prep && launch_prep(B->prep, s)) return DTGPU_ERR_HIP;
+    if (hipEventRecord(B->ev0, s) != hipSuccess) return DTGPU_ERR_HIP;
+    if (B->n_gpu_planned && launch_plan(B->plan, s) != OK) return DTGPU_ERR_HIP;
+    if (hipEventRecord(B->ev_mid, s) != hipSuccess) return DTGPU_ERR_HIP;
+    int st = B->xf_mode ? launch_replay_xf(B->large, s) : launch_replay(B->small, B->large, s, B->n_cu);
+    if (st) return dtgpu_status(st);
+    if (hipEventRecord(B->ev1, s) != hipSuccess) return DTGPU_ERR_HIP;
     if (hipEventSynchronize(B->ev1) != hipSuccess) return DTGPU_ERR_HIP;
-    float t = 0, tp = 0;
-    if (hipEventElapsedTime(&t, B->ev0, B->ev1) != hipSuccess) return DTGPU_ERR_HIP;
+    float t = 0, tp = 0, tq = 0;
+    if (hipEventElapsedTime(&t, B->ev_prep, B->ev1) != hipSuccess) return DTGPU_ERR_HIP;
+    if (hipEventElapsedTime(&tq, B->ev_prep, B->ev0) != hipSuccess) return DTGPU_ERR_HIP;
     if (hipEventElapsedTime(&tp, B->ev0, B->ev_mid) != hipSuccess) return DTGPU_ERR_HIP;
+    B->last_prep_ms = prep ? tq : 0.0f;
     B->last_plan_ms = tp;
-    B->last_replay_ms = t - tp;
+    B->last_replay_ms = t - tp - tq;
     if (ms) *ms = t;
     return DTGPU_OK;
 }
@@ -1031,10 +1037,11 @@ dtgpu_status dtgpu_batch_sync(dtgpu_batch *B) {
     return hipStreamSynchronize(B->stream) == hipSuccess ? DTGPU_OK : DTGPU_ERR_HIP;
 }
 size_t dtgpu_batch_size(const dtgpu_batch *B) { return B ? B->n : 0; }
-dtgpu_status dtgpu_batch_last_times(const dtgpu_batch *B, float out[2]) {
+dtgpu_status dtgpu_batch_last_times(const dtgpu_batch *B, float out[3]) {
     if (!B || !out) return DTGPU_ERR_ARG;
     out[0] = B->last_plan_ms;
     out[1] = B->last_replay_ms;
+    out[2] = B->last_prep_ms;
     return DTGPU_OK;
 }
 size_t dtgpu_batch_host_planned(const dtgpu_batch *B, uint8_t *flags, size_t cap) {

@@ -639,10 +639,10 @@ class Batch:
         return buf.raw[:n.value]
 
     def last_times(self):
-        """(plan_ms, replay_ms) of the last run_timed()."""
-        out = (ctypes.c_float * 2)()
+        """(plan_ms, replay_ms, prep_ms) of the last run_timed() (prep_ms 0 when host-staged)."""
+        out = (ctypes.c_float * 3)()
         _check(lib().dtgpu_batch_last_times(self._h, out))
-        return out[0], out[1]
+        return out[0], out[1], out[2]
 
     def host_planned(self):
         n = len(self)

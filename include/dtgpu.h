@@ -207,14 +207,17 @@ dtgpu_status dtgpu_batch_create_from_oplogs(const dtgpu_oplog *const *oplogs, si
 /* Enqueue the device checkout of the whole batch on `stream` (hipStream_t, NULL = the batch's
  * own stream).  Asynchronous; inputs are already resident in HBM. */
 dtgpu_status dtgpu_batch_run(dtgpu_batch *batch, void *stream);
-/* Run once, synchronously, and report device time of the planner + replay kernels (hipEvents
- * on the launch stream) in *kernel_ms. */
+/* Run once, synchronously, and report the device time of one whole checkout pass (hipEvents on
+ * the launch stream) in *kernel_ms: for device-staged batches the walker-input kernel
+ * (dt_prep.hip: parent entries, children CSR, chain decomposition -- SpanningTreeWalker::new,
+ * src/listmerge/txn_trace.rs:114-188), then the walk planner and the replay. */
 dtgpu_status dtgpu_batch_run_timed(dtgpu_batch *batch, float *kernel_ms);
 dtgpu_status dtgpu_batch_sync(dtgpu_batch *batch);
 size_t dtgpu_batch_size(const dtgpu_batch *batch);
-/* Device time of the last dtgpu_batch_run_timed split into out[0] = walk planning (dt_plan.hip)
- * and out[1] = replay + materialisation (dt_replay.hip), milliseconds. */
-dtgpu_status dtgpu_batch_last_times(const dtgpu_batch *batch, float out[2]);
+/* Device time of the last dtgpu_batch_run_timed split into out[0] = walk planning (dt_plan.hip),
+ * out[1] = replay + materialisation (dt_replay.hip) and out[2] = walker inputs (dt_prep.hip; 0 for
+ * host-staged batches), milliseconds. */
+dtgpu_status dtgpu_batch_last_times(const dtgpu_batch *batch, float out[3]);
 /* Documents planned on the host because the device planner declined them: returns their count
  * and, when flags is not NULL, one code per document: 0 device-planned, 1 DTGPU_HOST_PLAN set,
  * 2 outside the planner's limits (> 512 agents, > 16384 graph entries, sparse agent seq
