@@ -3,13 +3,14 @@
 
 One step = one device pass of `checkout_tip()` over the whole batch resident in HBM: the
 friendsforever.dt workload (BASELINE.json configs[1]) replicated to --docs copies per GPU
-(weak scaling: every rank owns its own copies).  The timed pass runs the walk planner
-(dt_plan.hip: spanning-tree walk + retreat/advance sets) and the replay + materialisation
-(dt_replay.hip) -- everything the reference's `checkout_tip()` does on a decoded oplog
-(crates/bench `complex/merge`).  The batch is staged on the device: the `.dt` bytes go to HBM and
-are decoded (dt_decode.hip) and turned into planner inputs (dt_prep.hip) by kernels; the reference
-benches decode separately (`complex/decode`), so staging is outside the timed pass (`stage_s`) and
-the whole chain -- decode + prep + plan + replay from the encoded bytes -- is reported as `e2e`.
+(weak scaling: every rank owns its own copies).  The timed pass runs the walker inputs
+(dt_prep.hip: parent entries, children CSR, chain decomposition -- what SpanningTreeWalker::new
+builds inside checkout_tip, src/listmerge/txn_trace.rs:114-188), the walk planner (dt_plan.hip:
+spanning-tree walk + retreat/advance sets) and the replay + materialisation (dt_replay.hip) --
+everything the reference's `checkout_tip()` does on a decoded oplog (crates/bench
+`complex/merge`).  The `.dt` bytes are decoded on the device too (dt_decode.hip); the reference
+benches decode separately (`complex/decode`), so decode is outside the timed pass and the whole
+chain -- decode + prep + plan + replay from the encoded bytes -- is reported as `e2e`.
 
 Contract: `python bench.py --gpus N --steps K --warmup W` prints ONE JSON line on rank 0.
 For N > 1 it is launched by torch.distributed.run, one process per GPU; per-rank times are
@@ -46,18 +47,56 @@ def parse():
                    help="N>1: move documents from busy to idle ranks by measured cost before timing")
     p.add_argument("--gen-threads", type=int, default=16, help="host threads generating / checking distinct documents")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
-    p.add_argument("--cpu-cores", type=int, default=16)
+    p.add_argument("--cpu-cores", type=int, default=0,
+                   help="host threads of the CPU baseline (0: the host CPUs this process may use, "
+                        "capped by the job's CPU share -- cgroup quota / OMP_NUM_THREADS)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-decode", action="store_true", help="skip the end-to-end (.dt bytes -> text) measurement")
     p.add_argument("--host-staging", action="store_true", help="decode and prepare planner inputs on host threads")
     return p.parse_args()
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def host_threads():
+    """Threads for the CPU baseline: the CPUs this process may run on (hardware_concurrency as
+    the affinity mask sees it), capped by the job's CPU share -- the cgroup cpu.max quota and
+    OMP_NUM_THREADS, which the GPU box sets to its per-GPU share.  Returns (threads, why)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    why = [f"affinity {n}"]
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(per))))
+            why.append(f"cgroup quota {int(q) / int(per):g}")
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+        why.append(f"OMP_NUM_THREADS {omp}")
+    return max(1, n), ", ".join(why)
+
+
 def cpu_baseline(pool, budget_s, cores, workload="friendsforever"):
     """The CPU oracle (C restatement of the reference algorithm, one document per thread)
     timed on a bounded sample of the same workload: checkout_tip() on an already-decoded
-    oplog, as the reference's `complex/merge` bench times it.  `pool`: the distinct documents."""
+    oplog, as the reference's `complex/merge` bench times it.  `pool`: the distinct documents.
+    The oracle replays every LV through a per-item tracker; the reference fast-forwards linear
+    prefixes (src/listmerge/merge.rs:811-840) and uses RLE spans, so on concurrent histories
+    the real Rust path is likely faster than this restatement."""
     from oracle.oracle import OpLog as OracleOpLog
+    why = "--cpu-cores"
+    if cores <= 0:
+        cores, why = host_threads()
     o = OracleOpLog.load_from(pool[0])
     t0 = time.perf_counter()
     o.checkout_tip_bytes()
@@ -83,8 +122,43 @@ def cpu_baseline(pool, budget_s, cores, workload="friendsforever"):
     wall = time.perf_counter() - t0
     docs = sum(done)
     return {"value": sum(lvs) / wall, "unit": "merged ops/s", "cores": cores, "kind": "port",
-            "sample": f"{docs} x {workload} checkout_tip (decoded oplog, C oracle) on {cores} host threads, "
-                      f"{wall:.2f} s"}
+            "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(), "threads_from": why,
+            "sample": f"{docs} x {workload} checkout_tip (decoded oplog) on {cores} host threads, {wall:.2f} s: "
+                      f"C per-item restatement of the reference algorithm (oracle/dt_oracle.c), no fast-forward "
+                      f"path (the reference fast-forwards linear prefixes, merge.rs:811-840)"}
+
+
+def cpu_config0():
+    """BASELINE configs[0]: automerge-paper.json.gz -> ListOpLog (untimed, the
+    apply_edits_push_merge construction of crates/bench/src/utils.rs:25-44) -> checkout_tip on
+    one host core, median of 5 after one warmup (criterion-style; bench.sh:5-7 pins one core).
+    The history is linear, so the reference's checkout is all fast-forward (merge.rs:811-840):
+    the oracle's FF path (dto_checkout_tip_ff) is the baseline; its per-item tracker is timed
+    beside it."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import golden_data as G
+    from oracle.oracle import oplog_from_trace
+    t = G.trace("automerge-paper")
+    o = oplog_from_trace(t["txns"])
+    want = t["endContent"].encode()
+
+    def med(fn):
+        fn()
+        ts = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            out = fn()
+            ts.append(time.perf_counter() - t0)
+        return sorted(ts)[2], out
+    ff_s, (text, ff) = med(o.checkout_tip_ff_bytes)
+    assert ff and text == want, "automerge-paper FF checkout differs from endContent"
+    tr_s, text2 = med(o.checkout_tip_bytes)
+    assert text2 == want, "automerge-paper tracker checkout differs from endContent"
+    return {"workload": "automerge-paper.json.gz -> checkout_tip (BASELINE configs[0])", "merged_ops": len(o),
+            "ff_ms": ff_s * 1e3, "ff_merged_ops_per_s": len(o) / ff_s,
+            "tracker_ms": tr_s * 1e3, "tracker_merged_ops_per_s": len(o) / tr_s,
+            "cores": 1, "cpu_model": cpu_model(), "stat": "median of 5 after 1 warmup",
+            "text_bytes": len(want), "checked": "endContent"}
 
 
 def single_doc_latency(data, gpu, staging):
@@ -254,7 +328,7 @@ def main():
         after = all_gather_floats(batch.run_timed(), dist, device=dev)
         rebalance = {"moves": len(moves), "busy_ms_before": busy, "busy_ms_after": after}
 
-    # timed region: K device passes over the resident batch
+    # timed region: K device checkout passes (prep + plan + replay) over the resident batch
     kernel_ms, split = [], []
     batch.sync()
     if dist is not None:
@@ -294,12 +368,19 @@ def main():
     avg_kernel_ms = statistics.mean(kernel_ms)
     plan_ms = statistics.mean(x[0] for x in split)
     replay_ms = statistics.mean(x[1] for x in split)
+    prep_ms = statistics.mean(x[2] for x in split)
     alg_bytes = batch.algorithmic_bytes
-    achieved = alg_bytes / (avg_kernel_ms / 1000.0) / 1e9
-    traffic = None
+    # roofline of the dominant kernel (replay_kernel): the pass's algorithmic bytes over the
+    # replay launch's own HIP-event time on the batch's stream
+    achieved = alg_bytes / (replay_ms / 1000.0) / 1e9
+    traffic = pass_traffic = None
     tpath = os.path.join(ROOT, "profiles", f"traffic_{args.workload}_{args.docs}.json")
-    if os.path.exists(tpath):   # HBM bytes per pass from a rocprofv3 PMC run of this command
-        traffic = json.load(open(tpath)).get("hbm_bytes_per_pass")
+    if os.path.exists(tpath):   # HBM bytes per launch from rocprofv3 PMC runs of this command
+        tj = json.load(open(tpath))
+        pass_traffic = tj.get("hbm_bytes_per_pass")
+        rk = [v for k, v in tj.get("per_kernel", {}).items() if "replay_kernel<true" in k]
+        if rk:
+            traffic = (2 * rk[0]["fetch_kib"] + rk[0]["write_kib"]) * 1024
 
     out = {
         "metric": "merged ops/sec (whole node) for batched checkout",
@@ -316,16 +397,20 @@ def main():
         "data": data_desc,
         "config": {"workload": f"{args.workload} x {args.docs} docs per GPU (checkout_tip)",
                    "docs_per_gpu": args.docs, "merged_ops_per_doc": lv_per_doc,
-                   "timed": "device walk planning + replay + materialisation of the whole batch "
-                            "(decoded oplogs resident in HBM)",
+                   "timed": "device walker inputs (prep) + walk planning + replay + materialisation of the "
+                            "whole batch (decoded oplogs resident in HBM)",
                    "parallelism": f"dp{world} (documents sharded, no data-path collective)"},
         "docs_per_sec": n_total * args.steps / elapsed,
         "stage_s": host_stage_s,
         "staging": staging,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "plan_kernel + replay_kernel (one checkout pass)",
-                     "kernel_ms": avg_kernel_ms, "plan_ms": plan_ms, "replay_ms": replay_ms,
+                     "kernel": "replay_kernel (dominant kernel of the pass)", "kernel_ms": replay_ms,
+                     "pass": {"kernels": "prep_kernel + plan_kernel + replay_kernel", "ms": avg_kernel_ms,
+                              "prep_ms": prep_ms, "plan_ms": plan_ms, "replay_ms": replay_ms,
+                              "achieved": alg_bytes / (avg_kernel_ms / 1000.0) / 1e9,
+                              "frac": alg_bytes / (avg_kernel_ms / 1000.0) / 1e9 / HBM_PEAK_GBS,
+                              "traffic": pass_traffic},
                      "algorithmic_bytes_per_launch": alg_bytes,
                      "algorithmic_formula": "per doc: 16*op_runs + (8+4*parents)*graph_entries + 12*agent_runs "
                                             "+ inserted_bytes + text_out_bytes (SURVEY.md 8d merge-only)"},
@@ -337,6 +422,7 @@ def main():
     if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(pool, args.cpu_seconds, args.cpu_cores, args.workload)
         out["single_doc_latency"] = single_doc_latency(pool[0], gpu, staging)
+        out["cpu_config0"] = cpu_config0()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

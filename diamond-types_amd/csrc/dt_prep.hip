@@ -309,6 +309,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
             if ((i & 63u) == 63u || i + 1 == ne) {
                 const uint32_t at = i & ~63u;
                 if (at + l <= i) cs[at + l] = make_uint2(bch, bsd);
+                wave_fence();   // later entries read these pairs back from other lanes
             }
             prev_row = row; prev_chain = c; prev_sd = s0 - s;
         }
@@ -379,10 +380,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
 #ifdef DTGPU_PREP_PROF
     const uint64_t T5 = wall_clock64();
 #endif
+    bool tip_miss = false;
     for (uint32_t t = l; t < D.n_ver; t += 64) {   // tips and their entries
         const uint32_t v = P.d_ver[D.d_ver + t];
+        const uint32_t e = entry_of(ent, ne, v);
+        if (e >= ne || v < ent[e].x || v >= ent[e].y) tip_miss = true;   // host path: ErrCheckout
         P.tip[2 * (D.o_tip + t)] = v;
-        P.tip[2 * (D.o_tip + t) + 1] = entry_of(ent, ne, v);
+        P.tip[2 * (D.o_tip + t) + 1] = e;
+    }
+    if (ballot(tip_miss)) {
+        if (l == 0) { R.status = PREP_BAD; P.results[doc] = R; }
+        return;
     }
     // agent runs with name ranks (byte-wise name order; names are distinct)
     {

@@ -288,7 +288,7 @@ const char *dtgpu_status_str(dtgpu_status status);
  * records), walk planning and replay; the host only sizes arenas from per-document counts.
  * Documents outside the device path's limits (see dtgpu_decode_*, and histories wider than 64
  * causal chains) report status DTGPU_DECODE_DEFER: check them out with dtgpu_batch_create.
- * dtgpu_batch_run / run_timed then re-run plan + replay; run_e2e_timed re-runs decode + prep +
+ * dtgpu_batch_run / run_timed then re-run prep + plan + replay; run_e2e_timed re-runs decode + prep +
  * plan + replay and returns the four kernel times (ms). */
 dtgpu_status dtgpu_batch_create_device(const uint8_t *const *docs, const size_t *lens, size_t n,
                                        const dtgpu_batch_opts *opts, dtgpu_batch **out);

@@ -1106,6 +1106,58 @@ EXPORT int dto_checkout_tip(const dto_oplog *o, int order, u8 **out, size_t *out
     return dto_checkout(o, o->version.v, (int)o->version.n, order, out, out_len, stats);
 }
 EXPORT void dto_free_buf(u8 *p) { free(p); }
+/* The reference's fast-forward path for a linear history (TransformedOpsIter::next while
+ * `can_ff`, src/listmerge/merge.rs:811-840; ListBranch::merge applies each op at its original
+ * position to the rope, src/list/merge.rs:68-89): when every graph entry's parents are the LV
+ * just before it, checkout_tip needs no tracker -- the ops are applied in LV order to a gap
+ * buffer of code points.  Any other history takes the per-item tracker (dto_checkout_tip).
+ * Used as the CPU baseline for linear traces (BASELINE configs[0], automerge-paper); parity
+ * against dto_checkout_tip is tested on every linear fixture.  *ff = 1 when the FF path ran. */
+static u32 utf8_decode(const u8 *s) {
+    if (s[0] < 0x80) return s[0];
+    if ((s[0] & 0xE0) == 0xC0) return ((u32)(s[0] & 0x1F) << 6) | (s[1] & 0x3F);
+    if ((s[0] & 0xF0) == 0xE0) return ((u32)(s[0] & 0x0F) << 12) | ((u32)(s[1] & 0x3F) << 6) | (s[2] & 0x3F);
+    return ((u32)(s[0] & 0x07) << 18) | ((u32)(s[1] & 0x3F) << 12) | ((u32)(s[2] & 0x3F) << 6) | (s[3] & 0x3F);
+}
+static size_t utf8_encode(u32 c, u8 *o) {
+    if (c < 0x80) { o[0] = (u8)c; return 1; }
+    if (c < 0x800) { o[0] = (u8)(0xC0 | (c >> 6)); o[1] = (u8)(0x80 | (c & 0x3F)); return 2; }
+    if (c < 0x10000) { o[0] = (u8)(0xE0 | (c >> 12)); o[1] = (u8)(0x80 | ((c >> 6) & 0x3F)); o[2] = (u8)(0x80 | (c & 0x3F)); return 3; }
+    o[0] = (u8)(0xF0 | (c >> 18)); o[1] = (u8)(0x80 | ((c >> 12) & 0x3F)); o[2] = (u8)(0x80 | ((c >> 6) & 0x3F)); o[3] = (u8)(0x80 | (c & 0x3F));
+    return 4;
+}
+EXPORT int dto_checkout_tip_ff(const dto_oplog *o, u8 **out, size_t *out_len, int *ff) {
+    const i64 n = o->kind.n;
+    int linear = o->version.n == (n ? 1 : 0) && (n == 0 || o->version.v[0] == n - 1);
+    for (i64 i = 0; i < o->g.e.n && linear; i++) {
+        const GEntry *e = &o->g.e.v[i];
+        if (e->start == 0 ? e->np != 0 : (e->np != 1 || e->parents[0] != e->start - 1)) linear = 0;
+    }
+    for (i64 v = 0; v < n && linear; v++) if (o->kind.v[v] == 0 && o->cbyte.v[v] < 0) linear = 0;
+    *ff = linear;
+    if (!linear) return dto_checkout_tip(o, 0, out, out_len, NULL);
+    /* gap buffer: [0, gs) text before the gap, [ge, cap) text after it */
+    i64 cap = 16;
+    for (i64 v = 0; v < n; v++) cap += o->kind.v[v] == 0;
+    u32 *buf = malloc(sizeof(u32) * (size_t)cap);
+    i64 gs = 0, ge = cap;
+    for (i64 v = 0; v < n; v++) {
+        const i64 p = o->pos.v[v], len = gs + (cap - ge);
+        if (p < 0 || p > len || (o->kind.v[v] == 1 && p >= len)) { free(buf); return E_CheckoutPanic; }
+        if (p < gs) { memmove(buf + ge - (gs - p), buf + p, sizeof(u32) * (size_t)(gs - p)); ge -= gs - p; gs = p; }
+        else if (p > gs) { memmove(buf + gs, buf + ge, sizeof(u32) * (size_t)(p - gs)); ge += p - gs; gs = p; }
+        if (o->kind.v[v] == 0) buf[gs++] = utf8_decode(&o->ins_content.v[o->cbyte.v[v]]);
+        else ge++;
+    }
+    u8 *t = malloc((size_t)(4 * (gs + cap - ge) + 1));
+    size_t k = 0;
+    for (i64 i = 0; i < gs; i++) k += utf8_encode(buf[i], t + k);
+    for (i64 i = ge; i < cap; i++) k += utf8_encode(buf[i], t + k);
+    free(buf);
+    *out = t; *out_len = k;
+    return E_OK;
+}
+
 /* ListOpLog::iter_xf_operations_from(from, merging) (src/list/merge.rs:24-38) restated per LV,
  * in the TransformedOpsIter order (src/listmerge/merge.rs:618-940): the new ops are
  * Hist(merging) - Hist(from); fast-forward through them while the next op's parents are the

@@ -57,6 +57,8 @@ def lib():
         L.dto_checkout.argtypes = [ctypes.c_void_p, P64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
                                    ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(Stats)]
         L.dto_free_buf.argtypes = [ctypes.c_void_p]
+        L.dto_checkout_tip_ff.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
+                                          ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_int)]
         L.dto_xf_operations.argtypes = [ctypes.c_void_p, P64]
         L.dto_xf_operations_from.argtypes = [ctypes.c_void_p, P64, ctypes.c_int, P64, ctypes.c_int, P64, P64]
         L.dto_crc32c.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
@@ -146,6 +148,19 @@ class OpLog:
         if with_stats:
             return data, {k: getattr(st, k) for k, _ in Stats._fields_}
         return data
+
+    def checkout_tip_ff_bytes(self):
+        """checkout_tip with the reference's fast-forward path for linear histories
+        (merge.rs:811-840); (text, ff) with ff True when no tracker was needed."""
+        out = ctypes.c_void_p()
+        ln = ctypes.c_size_t()
+        ff = ctypes.c_int()
+        e = lib().dto_checkout_tip_ff(self.h, ctypes.byref(out), ctypes.byref(ln), ctypes.byref(ff))
+        if e:
+            raise OracleError(e)
+        data = ctypes.string_at(out.value, ln.value) if ln.value else b""
+        lib().dto_free_buf(out)
+        return data, bool(ff.value)
 
     def checkout_bytes(self, version, order=0) -> bytes:
         """ListOpLog::checkout(&[LV]) (src/list/oplog.rs:32-36) restated: walk Hist(version)."""

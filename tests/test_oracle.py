@@ -28,6 +28,22 @@ def test_json_trace_endcontent(name):
     assert o.checkout_tip() == t["endContent"]
 
 
+@pytest.mark.parametrize("name", G.JSON_TRACES)
+def test_json_trace_fast_forward_path(name):
+    # the reference's FF path for linear histories (merge.rs:811-840), the CPU baseline of
+    # BASELINE configs[0]: same text as the tracker and as endContent
+    t = G.trace(name)
+    o = oplog_from_trace(t["txns"])
+    text, ff = o.checkout_tip_ff_bytes()
+    assert ff and text == t["endContent"].encode()
+
+
+def test_fast_forward_declines_concurrent_history():
+    o = OpLog.load_from(G.dt_bytes("friendsforever"))
+    text, ff = o.checkout_tip_ff_bytes()
+    assert not ff and text == o.checkout_tip_bytes()
+
+
 # ---- 3/4. compat byte vectors ------------------------------------------------------------
 @pytest.mark.parametrize("vec", [G.COMPAT_SIMPLE_1, G.COMPAT_SIMPLE_2, G.COMPAT_SIMPLE_LZ4])
 def test_compat_simple_doc(vec):
@@ -176,6 +192,8 @@ def test_unicode_content():
     o.add_delete(s, 1, 2)
     o.add_insert(s, 6, "✓")
     assert o.checkout_tip() == "hllo 𝄞✓ wörld"
+    text, ff = o.checkout_tip_ff_bytes()
+    assert ff and text == "hllo 𝄞✓ wörld".encode()
 
 
 # ---- 7. unpinned large docs: oracle-pinned by two-order convergence --------------------------

@@ -15,3 +15,4 @@ timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run -f csv -- 
 echo "fetch rc=$?"
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run -f csv -- python -u bench.py "${ARGS[@]}" --no-cpu-baseline --steps 1 --warmup 0 > "$OUT/write.log" 2>&1
 echo "write rc=$?"
+python tools/traffic.py "$OUT/fetch" "$OUT/write" "$OUT/traffic.json" > /dev/null && echo "traffic ok"

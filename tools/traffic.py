@@ -9,7 +9,7 @@ import json
 import os
 import sys
 
-KERNELS = ("plan_kernel", "replay_kernel")
+KERNELS = ("prep_kernel", "plan_kernel", "replay_kernel")
 
 
 def last_per_kernel(d, counter):

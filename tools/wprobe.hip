@@ -8,6 +8,8 @@
 //   atom_nr_x2   workgroup-scope non-returning 8-byte atomic xor (mask toggles), random lines
 //   atom_ret_l2  returning atomic add confined to a 1 MiB window (L2-resident)
 //   store_l2     4-byte scattered stores confined to a 1 MiB window, repeated
+//   gather4      one 4-byte load per lane, every lane in a different random 128-B line
+//   rowload256   64 lanes x 4 B contiguous loads of random 256-B rows
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
@@ -32,6 +34,24 @@ __global__ void row256(uint32_t *buf, uint32_t mask_rows, int iters) {
         const uint32_t row = hsh(w * 131u + uint32_t(i) * 0x9E3779B9u) & mask_rows;
         buf[row * 64u + l] = w + uint32_t(i);
     }
+}
+__global__ void gather4(const uint32_t *buf, uint32_t mask_lines, int iters, uint32_t *sink) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t acc = 0;
+    for (int i = 0; i < iters; i++) {
+        const uint32_t line = hsh(g * 977u + uint32_t(i) * 0x9E3779B9u) & mask_lines;
+        acc += buf[line * 32u];
+    }
+    if (acc == 0xFFFFFFFFu) sink[0] = acc;
+}
+__global__ void rowload256(const uint32_t *buf, uint32_t mask_rows, int iters, uint32_t *sink) {
+    const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, l = threadIdx.x & 63u;
+    uint32_t acc = 0;
+    for (int i = 0; i < iters; i++) {
+        const uint32_t row = hsh(w * 131u + uint32_t(i) * 0x9E3779B9u) & mask_rows;
+        acc += buf[row * 64u + l];
+    }
+    if (acc == 0xFFFFFFFFu) sink[0] = acc;
 }
 __global__ void atom_ret(uint32_t *buf, uint32_t mask_lines, int iters, uint32_t *sink) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -80,6 +100,8 @@ int main() {
     run("atom_ret", lanes * 4, [&] { hipLaunchKernelGGL(atom_ret, dim3(grid), dim3(block), 0, 0, buf, lines_all, iters, sink); });
     run("atom_nr_x2", lanes * 8, [&] { hipLaunchKernelGGL(atom_nr_x2, dim3(grid), dim3(block), 0, 0, (unsigned long long *)buf, lines_all, iters); });
     run("atom_ret_l2", lanes * 4, [&] { hipLaunchKernelGGL(atom_ret, dim3(grid), dim3(block), 0, 0, buf, lines_l2, iters, sink); });
+    run("gather4", lanes * 4, [&] { hipLaunchKernelGGL(gather4, dim3(grid), dim3(block), 0, 0, buf, lines_all, iters, sink); });
+    run("rowload256", lanes * 4, [&] { hipLaunchKernelGGL(rowload256, dim3(grid), dim3(block), 0, 0, buf, uint32_t(bytes / 256) - 1, iters, sink); });
     run("store_l2", lanes * 4, [&] { hipLaunchKernelGGL(scatter4, dim3(grid), dim3(block), 0, 0, buf, lines_l2, iters); });
     return 0;
 }
