@@ -43,6 +43,8 @@ def parse():
                         "(BASELINE configs[3]: synthetic concurrent documents, dt_synth.cpp, written as .dt) or "
                         "mixed (configs[4]: all 8 benchmark_data traces)")
     p.add_argument("--distinct", type=int, default=256, help="synth: distinct documents, replicated to --docs")
+    p.add_argument("--synth-family", default="merge", choices=["merge", "epoch"],
+                   help="synth: SURVEY 8(d)4 pairwise-merge generator (default) or the epoch generator")
     p.add_argument("--rebalance", action="store_true",
                    help="N>1: move documents from busy to idle ranks by measured cost before timing")
     p.add_argument("--gen-threads", type=int, default=16, help="host threads generating / checking distinct documents")
@@ -215,15 +217,20 @@ def workload_pool(args):
         from concurrent.futures import ThreadPoolExecutor
 
         def gen(d):   # generator and encoder are native (ctypes releases the GIL)
-            return dt_amd.synth_oplog(d, 5000).encode()
+            if args.synth_family == "epoch":
+                return dt_amd.synth_oplog(d, 5000).encode()
+            return dt_amd.synth_merge_oplog(d, 5000).encode()
         pool = []
         with ThreadPoolExecutor(max(1, args.gen_threads)) as ex:
             for c in range(0, args.distinct, 4096):   # progress on stderr for long pools
                 pool += list(ex.map(gen, range(c, min(args.distinct, c + 4096))))
                 if args.distinct > 4096:
                     print(f"[bench] generated {len(pool)}/{args.distinct} distinct documents", file=sys.stderr, flush=True)
+        fam = ("epoch merges (dtgpu_synth_oplog)" if args.synth_family == "epoch" else
+               "SURVEY 8(d)4: per-step pairwise merges p=0.1 via find_dominators_2 (dtgpu_synth_merge_oplog)")
         return pool, (f"synthetic concurrent documents (dt_synth.cpp: seed 0xD1A00000 + doc, 4-16 agents, "
-                      f"~5k ops), {args.distinct} distinct encoded as .dt (dtgpu_oplog_encode) and replicated")
+                      f"~5k ops, {fam}), {args.distinct} distinct encoded as .dt (dtgpu_oplog_encode) "
+                      f"and replicated")
     if args.workload == "mixed":   # BASELINE configs[4]: all benchmark_data traces, skewed sizes
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import golden_data as G
@@ -292,7 +299,10 @@ def main():
     n_total = args.docs * world
     # weak scaling: the global batch is docs x world documents (document g is pool[g % distinct]);
     # LPT gives every rank its shard
-    mine = lpt_assign([doc_cost(pool[g % len(pool)]) for g in range(n_total)], world)[rank]
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max(1, args.gen_threads)) as ex:   # per distinct document, native (GIL released)
+        pool_cost = list(ex.map(doc_cost, pool))
+    mine = lpt_assign([pool_cost[g % len(pool)] for g in range(n_total)], world)[rank]
     docs = [bytes(pool[g % len(pool)]) for g in mine]
     gpu = 0 if (dist is None or os.environ.get("DTGPU_BENCH_SHARED_GPU") == "1") else local_rank
     dev = (None if os.environ.get("DTGPU_BENCH_SHARED_GPU") == "1" else f"cuda:{local_rank}") if dist is not None else None
@@ -312,7 +322,7 @@ def main():
         # pass, plan the moves identically on every rank, send the moved documents' .dt bytes
         # point to point and re-stage (all outside the timed region)
         from dt_amd.shard import all_gather_floats, exchange_documents, plan_moves
-        costs = [doc_cost(pool[g % len(pool)]) for g in range(n_total)]
+        costs = [pool_cost[g % len(pool)] for g in range(n_total)]
         assign = lpt_assign(costs, world)
         busy = all_gather_floats(batch.run_timed(), dist, device=dev)
         new_assign, moves = plan_moves(assign, costs, busy, tol=0.10)   # spreads under 10 % are noise
@@ -397,6 +407,7 @@ def main():
         "data": data_desc,
         "config": {"workload": f"{args.workload} x {args.docs} docs per GPU (checkout_tip)",
                    "docs_per_gpu": args.docs, "merged_ops_per_doc": lv_per_doc,
+                   "distinct_docs": len(pool),
                    "timed": "device walker inputs (prep) + walk planning + replay + materialisation of the "
                             "whole batch (decoded oplogs resident in HBM)",
                    "parallelism": f"dp{world} (documents sharded, no data-path collective)"},

@@ -148,6 +148,7 @@ def lib():
     L.dtgpu_synth_ops.argtypes = [u64, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32), sz]
     L.dtgpu_synth_ops.restype = sz
     L.dtgpu_synth_oplog.argtypes = [u64, ctypes.c_uint32, ctypes.POINTER(vp)]
+    L.dtgpu_synth_merge_oplog.argtypes = [u64, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(vp)]
     L.dtgpu_oplog_export.argtypes = [vp, c, vp, sz]
     L.dtgpu_oplog_export.restype = sz
     L.dtgpu_decode_create.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz), sz,
@@ -823,4 +824,13 @@ def synth_oplog(doc, target_ops=5000):
     """Synthetic document `doc` built as a ListOpLog."""
     h = ctypes.c_void_p()
     _check(lib().dtgpu_synth_oplog(doc, target_ops, ctypes.byref(h)))
+    return ListOpLog(h.value)
+
+
+def synth_merge_oplog(doc, target_ops=5000, n_agents=0):
+    """SURVEY.md 8(d)4 synthetic document `doc` (dt_synth.cpp MergeGen: per-step pairwise merges
+    with p = 0.1 via find_dominators_2, make_random_change edits), built as a ListOpLog.
+    n_agents = 0 draws U{4..16}; a larger count gives a wide history (many causal chains)."""
+    h = ctypes.c_void_p()
+    _check(lib().dtgpu_synth_merge_oplog(doc, target_ops, n_agents, ctypes.byref(h)))
     return ListOpLog(h.value)

@@ -22,9 +22,26 @@ def lpt_assign(costs, world):
     return [sorted(x) for x in out]
 
 
-def doc_cost(data: bytes) -> int:
-    """Cost proxy before decoding: encoded size (LVs and op runs scale with it)."""
-    return len(data)
+COST_ALPHA = 1.0    # per op run x log2(op runs): positional lookups in the content index
+COST_BETA = 0.25    # per retreated / advanced LV of the walk plan: lane-parallel toggle passes
+
+
+def doc_cost(data: bytes) -> float:
+    """SURVEY.md 8(e) cost estimate of one document's checkout, from its host decode and host
+    walk plan (native, no GPU): c = LVs + alpha * runs * log2(runs) + beta * walk, with runs =
+    op runs and walk = LVs retreated + advanced by the SpanningTreeWalker plan.  alpha = 1 and
+    beta = 0.25 fit the single-document replay times of the three benchmark .dt files (kprof,
+    profiles/r2_calib: git-makefile / friendsforever 9.5-10x, node_nodecc / friendsforever
+    ~22x; the model gives 9.2x and 22x).  A document that does not decode costs its size."""
+    import math
+    import dt_amd
+    try:
+        o = dt_amd.ListOpLog.load_from(data)
+    except Exception:
+        return float(len(data))
+    runs = max(1, len(o.export("ops")))
+    ps = o.plan_stats()
+    return len(o) + COST_ALPHA * runs * math.log2(runs + 1) + COST_BETA * (ps["retreat"] + ps["advance"])
 
 
 def gather_results(records, n_total, dist, device=None):

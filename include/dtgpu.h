@@ -277,6 +277,11 @@ dtgpu_status dtgpu_batch_xf_positions(dtgpu_batch *batch, size_t doc, uint32_t *
 size_t dtgpu_synth_ops(uint64_t doc, uint32_t target_ops, uint32_t *n_agents, uint32_t *out, size_t cap);
 /* The same document built as an oplog (agents "a0".."a15"). */
 dtgpu_status dtgpu_synth_oplog(uint64_t doc, uint32_t target_ops, dtgpu_oplog **out);
+/* The SURVEY.md 8(d)4 generator (BASELINE configs[3]): every step one agent, with p = 0.1 a
+ * pairwise merge of another agent's frontier (find_dominators_2), then one make_random_change
+ * edit at a position of its own branch text.  n_agents = 0: U{4..16}; otherwise that many (the
+ * wide variant: more concurrent causal chains than the device prep handles). */
+dtgpu_status dtgpu_synth_merge_oplog(uint64_t doc, uint32_t target_ops, uint32_t n_agents, dtgpu_oplog **out);
 
 /* Number of HIP devices visible (0 when there is no GPU). */
 int dtgpu_device_count(void);

@@ -1258,6 +1258,48 @@ EXPORT int dto_xf_operations(const dto_oplog *o, i64 *out) {
     return err;
 }
 
+/* Decoded arrays, for the element-by-element check of the product's decoders against this
+ * independent restatement (tests/test_decode_parity.py).  Each returns the element count and
+ * copies min(count, cap) elements.
+ *   dto_export_lv:      3 x i64 per LV: kind (0 ins, 1 del), position, content byte offset (-1)
+ *   dto_export_aruns:   4 x i64 per agent run: lv_start, len, agent, seq_start
+ *   dto_export_entries: 3 x i64 per graph entry: start, end, parent count; parents in *par
+ *   dto_export_version: the frontier
+ *   dto_agent_name:     bytes of agent i's name */
+EXPORT i64 dto_export_lv(const dto_oplog *o, i64 *out, i64 cap) {
+    for (i64 v = 0; v < o->kind.n && v < cap; v++) {
+        out[3 * v] = o->kind.v[v]; out[3 * v + 1] = o->pos.v[v]; out[3 * v + 2] = o->cbyte.v[v];
+    }
+    return o->kind.n;
+}
+EXPORT i64 dto_export_aruns(const dto_oplog *o, i64 *out, i64 cap) {
+    for (i64 i = 0; i < o->aruns.n && i < cap; i++) {
+        const AgentRun *r = &o->aruns.v[i];
+        out[4 * i] = r->lv_start; out[4 * i + 1] = r->len; out[4 * i + 2] = r->agent; out[4 * i + 3] = r->seq_start;
+    }
+    return o->aruns.n;
+}
+EXPORT i64 dto_export_entries(const dto_oplog *o, i64 *out, i64 cap, i64 *par, i64 par_cap) {
+    i64 k = 0;
+    for (i64 i = 0; i < o->g.e.n; i++) {
+        const GEntry *e = &o->g.e.v[i];
+        if (i < cap) { out[3 * i] = e->start; out[3 * i + 1] = e->end; out[3 * i + 2] = e->np; }
+        for (int j = 0; j < e->np; j++, k++) if (k < par_cap) par[k] = e->parents[j];
+    }
+    return o->g.e.n;
+}
+EXPORT i64 dto_export_version(const dto_oplog *o, i64 *out, i64 cap) {
+    for (i64 i = 0; i < o->version.n && i < cap; i++) out[i] = o->version.v[i];
+    return o->version.n;
+}
+EXPORT int dto_agent_name(const dto_oplog *o, int i, char *out, int cap) {
+    if (i < 0 || i >= o->agents.n) return -1;
+    const Agent *a = &o->agents.v[i];
+    memcpy(out, a->name, (size_t)(a->name_len < cap ? a->name_len : cap));
+    return a->name_len;
+}
+EXPORT const u8 *dto_ins_content(const dto_oplog *o) { return o->ins_content.v; }
+
 /* ------------------------------------------------------------------------------------------ */
 /* graph-tool entry points for the causal_graph fixtures                                      */
 /* ------------------------------------------------------------------------------------------ */

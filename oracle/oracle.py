@@ -57,6 +57,15 @@ def lib():
         L.dto_checkout.argtypes = [ctypes.c_void_p, P64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
                                    ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(Stats)]
         L.dto_free_buf.argtypes = [ctypes.c_void_p]
+        for f in ("dto_export_lv", "dto_export_aruns", "dto_export_version"):
+            getattr(L, f).argtypes = [ctypes.c_void_p, P64, i64]
+            getattr(L, f).restype = i64
+        L.dto_export_entries.argtypes = [ctypes.c_void_p, P64, i64, P64, i64]
+        L.dto_export_entries.restype = i64
+        L.dto_agent_name.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+        L.dto_agent_name.restype = ctypes.c_int
+        L.dto_ins_content.argtypes = [ctypes.c_void_p]
+        L.dto_ins_content.restype = ctypes.c_void_p
         L.dto_checkout_tip_ff.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
                                           ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_int)]
         L.dto_xf_operations.argtypes = [ctypes.c_void_p, P64]
@@ -148,6 +157,44 @@ class OpLog:
         if with_stats:
             return data, {k: getattr(st, k) for k, _ in Stats._fields_}
         return data
+
+    def decoded(self):
+        """The oracle's decoded arrays (independent restatement of decode_internal): per-LV
+        (kind, pos, cbyte) triples, agent runs, graph entries (start, end, parents), version,
+        agent names and inserted content."""
+        L = lib()
+
+        def grab(fn, per, *extra):
+            n = fn(self.h, None, 0, *extra)
+            buf = (ctypes.c_int64 * max(1, per * n))()
+            fn(self.h, buf, n, *extra)
+            return [tuple(buf[per * i:per * i + per]) for i in range(n)]
+        lvs = grab(L.dto_export_lv, 3)
+        aruns = grab(L.dto_export_aruns, 4)
+        ne = L.dto_export_entries(self.h, None, 0, None, 0)
+        eb = (ctypes.c_int64 * max(1, 3 * ne))()
+        L.dto_export_entries(self.h, eb, ne, None, 0)
+        npar = sum(eb[3 * i + 2] for i in range(ne))
+        pb = (ctypes.c_int64 * max(1, npar))()
+        L.dto_export_entries(self.h, eb, ne, pb, npar)
+        entries, k = [], 0
+        for i in range(ne):
+            np_ = eb[3 * i + 2]
+            entries.append((eb[3 * i], eb[3 * i + 1], tuple(pb[k:k + np_])))
+            k += np_
+        nv = L.dto_export_version(self.h, None, 0)
+        vb = (ctypes.c_int64 * max(1, nv))()
+        L.dto_export_version(self.h, vb, nv)
+        names = []
+        for i in range(L.dto_num_agents(self.h)):
+            n = L.dto_agent_name(self.h, i, None, 0)
+            nb = ctypes.create_string_buffer(max(1, n))
+            L.dto_agent_name(self.h, i, nb, n)
+            names.append(nb.raw[:n].decode())
+        clen = L.dto_ins_content_len(self.h)
+        content = ctypes.string_at(L.dto_ins_content(self.h), clen) if clen else b""
+        return {"lv": lvs, "agent_runs": aruns, "entries": entries, "version": list(vb[:nv]),
+                "agent_names": names, "content": content}
 
     def checkout_tip_ff_bytes(self):
         """checkout_tip with the reference's fast-forward path for linear histories

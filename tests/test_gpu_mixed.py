@@ -1,0 +1,68 @@
+"""BASELINE configs[4]: one device-staged, skewed batch of all 8 benchmark_data traces (3 .dt
+files + the 5 JSON traces written as .dt the way crates/bench/src/utils.rs:25-44 builds their
+oplogs), ~36x apart in LVs, every document checked against its golden endContent (the JSON
+traces, friendsforever) or the oracle (git-makefile, node_nodecc: oracle-pinned)."""
+import gzip
+import json
+import os
+import sys
+
+import pytest
+
+import golden_data as G
+from oracle.oracle import OpLog as OracleOpLog
+
+pytestmark = pytest.mark.gpu
+
+import dt_amd  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def mixed():
+    sys.path.insert(0, ROOT)
+    from bench import trace_ops
+    from dt_encode import encode_dt
+    if dt_amd.device_count() < 1:
+        pytest.fail("no HIP device visible: the engine has no CPU fallback")
+    docs, want = [], []
+    for n in G.DT_FILES:
+        d = G.dt_bytes(n)
+        docs.append(d)
+        if n == "friendsforever":
+            want.append(json.load(gzip.open(os.path.join(ROOT, "tests", "golden", "benchmark_data",
+                                                          "friendsforever_flat.json.gz")))["endContent"].encode())
+        else:
+            want.append(OracleOpLog.load_from(d).checkout_tip_bytes())
+    for n in G.JSON_TRACES:
+        t = G.trace(n)
+        docs.append(encode_dt(["jeremy"], trace_ops(t["txns"])))
+        want.append(t["endContent"].encode())
+    # skew: the small traces many times, the big ones twice (configs[4] replicates the set)
+    reps = [4, 2, 2, 2, 2, 3, 4, 6]
+    batch_docs, batch_want = [], []
+    for d, w, r in zip(docs, want, reps):
+        batch_docs += [d] * r
+        batch_want += [w] * r
+    order = sorted(range(len(batch_docs)), key=lambda i: (i * 7919) % len(batch_docs))   # interleaved
+    return [batch_docs[i] for i in order], [batch_want[i] for i in order]
+
+
+def test_mixed_skewed_batch_device_staged(mixed):
+    docs, want = mixed
+    b = dt_amd.Batch(docs=docs, staging="device")
+    b.run()
+    b.sync()
+    res = b.results()
+    lvs = sorted(r["n_lv"] for r in res)
+    assert lvs[-1] / lvs[0] > 30                      # skewed
+    for i, (r, w) in enumerate(zip(res, want)):
+        assert r["status"] == 0, (i, r)
+        assert (r["text_len"], r["text_hash"]) == (len(w), dt_amd.text_hash(w)), i
+        assert b.text(i) == w, i
+    # timed pass over the same resident batch: prep + plan + replay, results unchanged
+    ms = b.run_timed()
+    assert ms > 0
+    assert [(r["status"], r["text_len"], r["text_hash"]) for r in b.results()] == \
+           [(0, len(w), dt_amd.text_hash(w)) for w in want]

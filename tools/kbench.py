@@ -17,7 +17,7 @@ def main():
     distinct = None
     if name.startswith("synth"):   # synth[:distinct] -- synthetic concurrent docs (dt_synth.cpp)
         distinct = int(name.split(":")[1]) if ":" in name else 256
-        pool = [dt_amd.synth_oplog(i, 5000) for i in range(distinct)]
+        pool = [dt_amd.synth_merge_oplog(i, 5000) for i in range(distinct)]
     else:
         data = G.dt_bytes(name)
     for n in counts:
