@@ -234,29 +234,16 @@ def workload_pool(args):
     if args.workload == "mixed":   # BASELINE configs[4]: all benchmark_data traces, skewed sizes
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import golden_data as G
-        from dt_encode import encode_dt
+        import dt_amd
         pool = [open(os.path.join(ROOT, "tests", "golden", "benchmark_data", n + ".dt"), "rb").read()
                 for n in G.DT_FILES]
-        for name in G.JSON_TRACES:
-            pool.append(encode_dt(["jeremy"], trace_ops(G.trace(name)["txns"])))
-        return pool, ("all 8 benchmark_data traces (3 .dt files + 5 JSON traces written as .dt the way "
-                      "crates/bench/src/utils.rs:25-44 builds their oplogs), replicated round-robin")
+        for name in G.JSON_TRACES:   # oplog as crates/bench builds it, encoded by the native encoder
+            pool.append(dt_amd.apply_edits_push_merge(G.trace(name)["txns"]).encode())
+        return pool, ("all 8 benchmark_data traces (3 .dt files + 5 JSON traces built the way "
+                      "crates/bench/src/utils.rs:25-44 builds their oplogs and written as .dt by "
+                      "dtgpu_oplog_encode), replicated round-robin")
     path = os.path.join(ROOT, "tests", "golden", "benchmark_data", args.workload + ".dt")
     return [open(path, "rb").read()], f"benchmark_data/{args.workload}.dt replicated (byte-identical copies in distinct buffers)"
-
-
-def trace_ops(txns):
-    """JSON trace -> op list (agent 0, delete then insert per patch, linear history)."""
-    ops, lv = [], 0
-    for txn in txns:
-        for pos, dl, ins in txn["patches"]:
-            if dl > 0:
-                ops.append((0, 1, pos, dl, "", [lv - 1] if lv else []))
-                lv += dl
-            if ins:
-                ops.append((0, 0, pos, len(ins), ins, [lv - 1] if lv else []))
-                lv += len(ins)
-    return ops
 
 
 def expected_texts(args, pool):

@@ -26,6 +26,7 @@ struct DocResult {
     uint64_t hash;
     uint32_t n_items, n_blocks;
     uint32_t fail_cmd, fail_site;   // diagnostics: command index and code site of the first error
+    uint32_t n_sb, lds;             // superblocks at the end; 1 when the index was in LDS
     uint32_t dbg[16];               // DTGPU_DEBUG invariant-failure detail / cycle profile
 };
 
@@ -50,10 +51,11 @@ struct BatchParams {
     const DocDesc *docs;
     const uint32_t *doc_list;
     uint32_t n_list;
-    uint32_t lds_blocks;    // block-index capacity held in LDS (small tier)
-    uint32_t *counter;      // work-queue head, zeroed before each launch
+    uint32_t lds_blocks;    // block-index capacity held in LDS (LDS tiers)
+    uint32_t lds_sb;        // superblock capacity held in LDS (LDS tiers)
     uint32_t *fb_list;      // LDS-tier documents handed to the HBM tier (capacity overflow)
     uint32_t *fb_count;
+    uint32_t fb_slots;      // HBM tier: grid slots for handed-back documents (all LDS-tier docs)
     uint32_t debug;         // DTGPU_DEBUG: bit 0 invariant checks, bit 1 cycle profile
     DocResult *results;
     // transformed-ops mode only (launch_replay_xf): never-deleted masks per block, never-deleted
@@ -70,10 +72,21 @@ __host__ __device__ inline uint32_t sb_capacity(uint32_t mb) { return mb / 32 + 
 // counts (u32) and the (superblock, index) position (u32; u16 when `narrow`, the LDS tier); per
 // superblock visible / live totals, list length, top position (u32 each)
 // and a 64-entry u16 block list.
-__host__ __device__ inline uint64_t index_bytes(uint64_t mb, bool narrow = false) {
-    const uint64_t ms = sb_capacity(uint32_t(mb));
+__host__ __device__ inline uint64_t index_bytes_ms(uint64_t mb, uint64_t ms, bool narrow) {
     const uint64_t per_block = narrow ? 4 * mb + 4 * ((mb + 1) / 2) : 8 * mb;
     return ((per_block + 16 * ms + 128 * ms) + 15) & ~uint64_t(15);
+}
+__host__ __device__ inline uint64_t index_bytes(uint64_t mb, bool narrow = false) {
+    return index_bytes_ms(mb, sb_capacity(uint32_t(mb)), narrow);
+}
+// LDS tiers size the superblock pool for the expected fill (superblocks hold 32..64 blocks,
+// ~44 on the benchmark traces) rather than the worst case: LDS is what bounds how many
+// documents share a CU, and a document that outgrows the pool is handed to the HBM tier like
+// one that outgrows its blocks (split_sb, ErrCapacity site 21).
+constexpr uint32_t LDS_SB_FILL = 40;
+__host__ __device__ inline uint32_t lds_sb_capacity(uint32_t mb, uint32_t fill = LDS_SB_FILL) {
+    const uint32_t opt = mb / fill + 3;
+    return opt < sb_capacity(mb) ? opt : sb_capacity(mb);
 }
 constexpr uint32_t MAX_DOC_BLOCKS = 65535;   // block ids are u16 in the superblock lists
 
@@ -114,8 +127,19 @@ struct PlanParams {
 };
 int launch_plan(const PlanParams &q, void *stream);
 
-// Launch both tiers on `stream` (hipStream_t).  small/large lists index docs[].
-int launch_replay(const BatchParams &small, const BatchParams &large, void *stream, int n_cu);
+// One replay pass: the LDS tiers (index in LDS, sized per tier) and then the HBM-index tier,
+// which also replays the LDS-tier documents that outgrew their LDS capacity.  The two biggest
+// LDS tiers (few, long documents) run on `side`, forked from and joined back into `stream`,
+// beside the small ones; every list indexes docs[].
+constexpr int kMaxLdsTiers = 4;
+struct ReplayLaunch {
+    const BatchParams *lds;   // n_lds LDS tiers, smallest index first
+    int n_lds;
+    const BatchParams *large;
+    void *stream, *side;      // hipStream_t
+    void *ev_fork, *ev_join;  // hipEvent_t
+};
+int launch_replay(const ReplayLaunch &r);
 // Transformed-ops replay of large's documents (HBM index tier): BaseMoved positions per LV.
 int launch_replay_xf(const BatchParams &large, void *stream);
 

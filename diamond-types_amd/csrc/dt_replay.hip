@@ -1109,6 +1109,8 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
         res->hash = h;
         res->n_items = D.n_items;
         res->n_blocks = D.nb;
+        res->n_sb = D.nsb;
+        res->lds = L ? 1u : 0u;
         res->fail_cmd = D.err ? D.ci : 0;
         res->fail_site = D.err ? D.site : 0;
         if (PROF) {
@@ -1171,7 +1173,7 @@ __global__ __launch_bounds__(64) void replay_kernel(BatchParams P) {
     D.max_sb = sb_capacity(D.max_blocks);
     if (LDS_INDEX) {
         if (D.max_blocks > P.lds_blocks) D.max_blocks = P.lds_blocks;
-        D.max_sb = sb_capacity(P.lds_blocks);
+        D.max_sb = P.lds_sb;
         bind_index(D, smem, P.lds_blocks, D.max_sb, true);
     } else {
         bind_index(D, P.gidx + dd.gidx_off, D.max_blocks, D.max_sb, false);
@@ -1186,19 +1188,60 @@ __global__ __launch_bounds__(64) void replay_kernel(BatchParams P) {
 
 }  // namespace dev
 
-int launch_replay(const BatchParams &small, const BatchParams &large, void *stream, int n_cu) {
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    const bool prof = (small.debug | large.debug) & 2u;
-    if (small.n_list) {
-        if (small.fb_count && hipMemsetAsync(small.fb_count, 0, sizeof(uint32_t), s) != hipSuccess) return ErrHip;
-        size_t lds = size_t(index_bytes(small.lds_blocks, true));
-        if (const char *pad = getenv("DTGPU_LDS_PAD")) lds += size_t(strtoul(pad, nullptr, 10));   // occupancy experiments
-        if (prof) hipLaunchKernelGGL((dev::replay_kernel<true, true, false>), dim3(small.n_list), dim3(64), lds, s, small);
-        else hipLaunchKernelGGL((dev::replay_kernel<true, false, false>), dim3(small.n_list), dim3(64), lds, s, small);
-        if (hipGetLastError() != hipSuccess) return ErrHip;
+static int launch_lds_tier(const BatchParams &q, hipStream_t s, bool prof) {
+    if (!q.n_list) return OK;
+    size_t lds = size_t(index_bytes_ms(q.lds_blocks, q.lds_sb, true));
+    if (const char *pad = getenv("DTGPU_LDS_PAD")) lds += size_t(strtoul(pad, nullptr, 10));   // occupancy experiments
+    if (lds > 160 * 1024) return ErrArg;   // a tier cap above the CU's LDS
+    static bool attr = false;   // allow dynamic LDS up to the CU's 160 KiB
+    if (!attr) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&dev::replay_kernel<true, false, false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess ||
+            hipFuncSetAttribute(reinterpret_cast<const void *>(&dev::replay_kernel<true, true, false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+            return ErrHip;
+        attr = true;
+    }
+    if (prof) hipLaunchKernelGGL((dev::replay_kernel<true, true, false>), dim3(q.n_list), dim3(64), lds, s, q);
+    else hipLaunchKernelGGL((dev::replay_kernel<true, false, false>), dim3(q.n_list), dim3(64), lds, s, q);
+    return hipGetLastError() == hipSuccess ? OK : ErrHip;
+}
+
+int launch_replay(const ReplayLaunch &r) {
+    hipStream_t s = reinterpret_cast<hipStream_t>(r.stream);
+    hipStream_t side = reinterpret_cast<hipStream_t>(r.side);
+    const BatchParams &large = *r.large;
+    bool prof = large.debug & 2u;
+    uint32_t n_lds = 0;
+    const uint32_t *fb_count = nullptr;
+    for (int t = 0; t < r.n_lds; t++) {
+        prof |= (r.lds[t].debug & 2u) != 0;
+        n_lds += r.lds[t].n_list;
+        if (r.lds[t].fb_count) fb_count = r.lds[t].fb_count;
+    }
+    if (n_lds) {
+        if (fb_count && hipMemsetAsync(const_cast<uint32_t *>(fb_count), 0, sizeof(uint32_t), s) != hipSuccess) return ErrHip;
+        // fork: the two biggest tiers (few documents, long replays) start first, on the side
+        // stream; the small tiers fill the rest of the chip on the main stream
+        const int split = r.n_lds > 2 ? r.n_lds - 2 : r.n_lds;
+        const bool fork = side && r.ev_fork && r.ev_join && split < r.n_lds;
+        if (fork) {
+            if (hipEventRecord(reinterpret_cast<hipEvent_t>(r.ev_fork), s) != hipSuccess ||
+                hipStreamWaitEvent(side, reinterpret_cast<hipEvent_t>(r.ev_fork), 0) != hipSuccess)
+                return ErrHip;
+        }
+        for (int t = r.n_lds - 1; t >= 0; t--) {
+            const int e = launch_lds_tier(r.lds[t], (fork && t >= split) ? side : s, prof);
+            if (e) return e;
+        }
+        if (fork) {
+            if (hipEventRecord(reinterpret_cast<hipEvent_t>(r.ev_join), side) != hipSuccess ||
+                hipStreamWaitEvent(s, reinterpret_cast<hipEvent_t>(r.ev_join), 0) != hipSuccess)
+                return ErrHip;
+        }
     }
     // HBM tier: its own list plus a slot per LDS-tier document that may be handed back
-    const uint32_t grid = large.n_list + (small.fb_list ? small.n_list : 0);
+    const uint32_t grid = large.n_list + (large.fb_list ? large.fb_slots : 0);
     if (grid) {
         if (prof) hipLaunchKernelGGL((dev::replay_kernel<false, true, false>), dim3(grid), dim3(64), 0, s, large);
         else hipLaunchKernelGGL((dev::replay_kernel<false, false, false>), dim3(grid), dim3(64), 0, s, large);

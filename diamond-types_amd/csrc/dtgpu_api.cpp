@@ -29,8 +29,21 @@ struct dtgpu_oplog {
 
 namespace {
 
-// Number of documents whose block index fits the LDS tier: up to 64 KiB of index per wave.
-constexpr uint64_t kLdsIndexBudget = 64 * 1024;
+// LDS tiers by block-index size: a document whose (optimistically sized) index fits a tier's
+// cap replays with its index in LDS; each tier is its own launch with the LDS its largest
+// document needs, so friendsforever-sized documents keep ~24 per CU while a node_nodecc-sized
+// one (~129 KiB of index) takes a CU's LDS alone instead of the HBM-index tier.  Bigger
+// documents and LDS overflows replay on the HBM-index tier.
+constexpr int kLdsTiers = kMaxLdsTiers;
+constexpr uint64_t kTierCap[kLdsTiers] = {12 * 1024, 32 * 1024, 64 * 1024, 160 * 1024};
+uint32_t sb_fill() {   // DTGPU_LDS_SB_FILL: superblock-pool sizing experiments
+    const char *e = getenv("DTGPU_LDS_SB_FILL");
+    return e ? std::max<uint32_t>(32, uint32_t(strtoul(e, nullptr, 10))) : LDS_SB_FILL;
+}
+int lds_tier(uint64_t bytes) {
+    for (int t = 0; t < kLdsTiers; t++) if (bytes <= kTierCap[t]) return t;
+    return -1;
+}
 
 }  // namespace
 
@@ -43,9 +56,12 @@ struct dtgpu_batch {
     std::vector<uint32_t> host_status;   // decode / plan status per doc
     std::vector<uint64_t> n_lv;
     std::vector<DocDesc> docs;
-    std::vector<uint32_t> small_list, large_list;
+    std::vector<uint32_t> tier_list[kLdsTiers], large_list;   // LDS tiers (index bytes), HBM tier
     std::vector<uint8_t> host_planned;   // 0: device-planned; else why the host planned it
-    uint32_t lds_blocks = 0;
+    uint32_t tier_blocks[kLdsTiers] = {};
+    uint32_t debug = 0;
+    hipStream_t side = nullptr;          // big LDS tiers run beside the small ones
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     uint64_t alg_in_bytes = 0, total_lv = 0;
     float last_plan_ms = 0, last_replay_ms = 0;
 
@@ -67,7 +83,7 @@ struct dtgpu_batch {
     DevBuf<uint32_t> d_fb;   // [0] = count, then the handed-back documents
     DevBuf<DocDesc> d_docs;
     DevBuf<DocResult> d_results;
-    BatchParams small{}, large{};
+    BatchParams tier[kLdsTiers]{}, large{};
 
     // device-staged batches (dtgpu_batch_create_device): the decoded oplogs stay in the
     // decoder's arenas (content and per-LV offsets are read there by the replay) and the
@@ -86,6 +102,9 @@ struct dtgpu_batch {
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev_mid) (void)hipEventDestroy(ev_mid);
         if (ev1) (void)hipEventDestroy(ev1);
+        if (ev_fork) (void)hipEventDestroy(ev_fork);
+        if (ev_join) (void)hipEventDestroy(ev_join);
+        if (side) (void)hipStreamDestroy(side);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -131,6 +150,63 @@ void parallel_for(size_t n, int threads, F f) {
 template <typename T>
 void append(std::vector<T> &dst, const std::vector<T> &src) { dst.insert(dst.end(), src.begin(), src.end()); }
 
+size_t n_lds_docs(const dtgpu_batch &B) {
+    size_t k = 0;
+    for (int t = 0; t < kLdsTiers; t++) k += B.tier_list[t].size();
+    return k;
+}
+// Launch order of the documents: the LDS tiers, then the HBM tier; inside a list the documents
+// go by descending LVs, so the hardware dispatcher starts the longest replays first (LPT inside
+// the GPU: the short ones fill in behind them).
+std::vector<uint32_t> tier_lists(dtgpu_batch &B) {
+    std::vector<uint32_t> all;
+    auto by_cost = [&](std::vector<uint32_t> &v) {
+        std::stable_sort(v.begin(), v.end(), [&](uint32_t a, uint32_t b) { return B.n_lv[a] > B.n_lv[b]; });
+        append(all, v);
+    };
+    for (int t = 0; t < kLdsTiers; t++) by_cost(B.tier_list[t]);
+    by_cost(B.large_list);
+    return all;
+}
+dtgpu_status set_tier_params(dtgpu_batch &B, const BatchParams &base) {
+    const bool fb = n_lds_docs(B) && !getenv("DTGPU_NO_FALLBACK");
+    size_t off = 0;
+    for (int t = 0; t < kLdsTiers; t++) {
+        BatchParams &q = B.tier[t];
+        q = base;
+        q.doc_list = B.d_lists.p + off;
+        q.n_list = uint32_t(B.tier_list[t].size());
+        q.lds_blocks = B.tier_blocks[t];
+        q.lds_sb = lds_sb_capacity(q.lds_blocks, sb_fill());
+        off += B.tier_list[t].size();
+        if (fb) { q.fb_count = B.d_fb.p; q.fb_list = B.d_fb.p + 1; }
+    }
+    B.large = base;
+    B.large.doc_list = B.d_lists.p + off;
+    B.large.n_list = uint32_t(B.large_list.size());
+    if (fb) {
+        B.large.fb_count = B.d_fb.p;
+        B.large.fb_list = B.d_fb.p + 1;
+        B.large.fb_slots = uint32_t(off);   // every LDS-tier document may be handed back
+    }
+    B.debug = base.debug;
+    if (!B.side && hipStreamCreateWithFlags(&B.side, hipStreamNonBlocking) != hipSuccess) return DTGPU_ERR_HIP;
+    if (!B.ev_fork && hipEventCreateWithFlags(&B.ev_fork, hipEventDisableTiming) != hipSuccess) return DTGPU_ERR_HIP;
+    if (!B.ev_join && hipEventCreateWithFlags(&B.ev_join, hipEventDisableTiming) != hipSuccess) return DTGPU_ERR_HIP;
+    return DTGPU_OK;
+}
+int replay_all(dtgpu_batch *B, hipStream_t s) {
+    ReplayLaunch r{};
+    r.lds = B->tier;
+    r.n_lds = kLdsTiers;
+    r.large = &B->large;
+    r.stream = s;
+    r.side = B->side;
+    r.ev_fork = B->ev_fork;
+    r.ev_join = B->ev_join;
+    return launch_replay(r);
+}
+
 // xf: a transformed-ops batch (iter_xf_operations): host plans in TransformedOpsIter order
 // (build_xf_plan), every document on the HBM-index tier, never-deleted masks / totals and the
 // per-LV transformed-position arena allocated.
@@ -145,7 +221,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         B->n_cu = prop.multiProcessorCount;
     if (hipStreamCreateWithFlags(&B->stream, hipStreamNonBlocking) != hipSuccess) return DTGPU_ERR_HIP;
     if (hipEventCreate(&B->ev0) != hipSuccess || hipEventCreate(&B->ev_mid) != hipSuccess ||
-        hipEventCreate(&B->ev1) != hipSuccess)
+        hipEventCreate(&B->ev1) != hipSuccess || hipEventCreate(&B->ev_prep) != hipSuccess)
         return DTGPU_ERR_HIP;
     hipStream_t s = B->stream;
 #define CK(x) do { if ((x) != hipSuccess) return DTGPU_ERR_HIP; } while (0)
@@ -311,9 +387,10 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         d.gidx_off = gidx_total;
         gidx_total += index_bytes(d.max_blocks);
         const uint32_t est = uint32_t(std::min<uint64_t>(d.max_blocks, n_ins / lds_fill + 8));
-        if (!xf && index_bytes(est, true) <= kLdsIndexBudget) {
-            B->small_list.push_back(uint32_t(i));
-            B->lds_blocks = std::max(B->lds_blocks, est);
+        const int t = xf ? -1 : lds_tier(index_bytes_ms(est, lds_sb_capacity(est, sb_fill()), true));
+        if (t >= 0) {
+            B->tier_list[t].push_back(uint32_t(i));
+            B->tier_blocks[t] = std::max(B->tier_blocks[t], est);
         } else {
             B->large_list.push_back(uint32_t(i));
         }
@@ -351,16 +428,14 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     CK(B->d_cbyte.upload(cbyte, s));
     CK(B->d_content.upload(content, s));
     CK(B->d_docs.upload(B->docs, s));
-    std::vector<uint32_t> lists(B->small_list);
-    lists.insert(lists.end(), B->large_list.begin(), B->large_list.end());
-    CK(B->d_lists.upload(lists, s));
+    CK(B->d_lists.upload(tier_lists(*B), s));
     CK(B->d_pos.alloc(lv_total));
     CK(B->d_ao.alloc(lv_total));
     CK(B->d_items.alloc(blk_total * 64));
     CK(B->d_m2.alloc(2 * blk_total));
     CK(B->d_out.alloc(out_total));
     CK(B->d_gidx.alloc(gidx_total));
-    CK(B->d_fb.alloc(B->small_list.size() + 1));
+    CK(B->d_fb.alloc(n_lds_docs(*B) + 1));
     CK(B->d_counter.alloc(2));
     CK(B->d_results.alloc(n));
     CK(hipMemsetAsync(B->d_results.p, 0, std::max<size_t>(n, 1) * sizeof(DocResult), s));
@@ -390,21 +465,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     base.gidx = B->d_gidx.p;
     base.docs = B->d_docs.p;
     base.results = B->d_results.p;
-    B->small = base;
-    B->small.doc_list = B->d_lists.p;
-    B->small.n_list = uint32_t(B->small_list.size());
-    B->small.lds_blocks = B->lds_blocks;
-    B->small.counter = B->d_counter.p;
-    B->large = base;
-    B->large.doc_list = B->d_lists.p + B->small_list.size();
-    B->large.n_list = uint32_t(B->large_list.size());
-    B->large.counter = B->d_counter.p + 1;
-    if (!B->small_list.empty() && !getenv("DTGPU_NO_FALLBACK")) {
-        B->small.fb_count = B->d_fb.p;
-        B->small.fb_list = B->d_fb.p + 1;
-        B->large.fb_count = B->d_fb.p;
-        B->large.fb_list = B->d_fb.p + 1;
-    }
+    if (set_tier_params(*B, base) != DTGPU_OK) return DTGPU_ERR_HIP;
     *out = B.release();
     return DTGPU_OK;
 }
@@ -570,9 +631,10 @@ dtgpu_status stage_device(const uint8_t *const *docs, const size_t *lens, size_t
         d.gidx_off = gidx_total;
         gidx_total += index_bytes(d.max_blocks);
         const uint32_t est = uint32_t(std::min<uint64_t>(d.max_blocks, n_ins / lds_fill + 8));
-        if (index_bytes(est, true) <= kLdsIndexBudget) {
-            B->small_list.push_back(uint32_t(i));
-            B->lds_blocks = std::max(B->lds_blocks, est);
+        const int t = lds_tier(index_bytes_ms(est, lds_sb_capacity(est, sb_fill()), true));
+        if (t >= 0) {
+            B->tier_list[t].push_back(uint32_t(i));
+            B->tier_blocks[t] = std::max(B->tier_blocks[t], est);
         } else {
             B->large_list.push_back(uint32_t(i));
         }
@@ -585,16 +647,14 @@ dtgpu_status stage_device(const uint8_t *const *docs, const size_t *lens, size_t
     B->plan.cmds = B->d_cmds.p;
     B->plan.tlist = B->d_tlist.p;
     CK(B->d_docs.upload(B->docs, s));
-    std::vector<uint32_t> lists(B->small_list);
-    lists.insert(lists.end(), B->large_list.begin(), B->large_list.end());
-    CK(B->d_lists.upload(lists, s));
+    CK(B->d_lists.upload(tier_lists(*B), s));
     CK(B->d_pos.alloc(lv_total));
     CK(B->d_ao.alloc(lv_total));
     CK(B->d_items.alloc(blk_total * 64));
     CK(B->d_m2.alloc(2 * blk_total));
     CK(B->d_out.alloc(out_total));
     CK(B->d_gidx.alloc(gidx_total));
-    CK(B->d_fb.alloc(B->small_list.size() + 1));
+    CK(B->d_fb.alloc(n_lds_docs(*B) + 1));
     CK(B->d_counter.alloc(2));
     CK(B->d_results.alloc(n));
     CK(hipMemsetAsync(B->d_results.p, 0, std::max<size_t>(n, 1) * sizeof(DocResult), s));
@@ -615,21 +675,7 @@ dtgpu_status stage_device(const uint8_t *const *docs, const size_t *lens, size_t
     base.gidx = B->d_gidx.p;
     base.docs = B->d_docs.p;
     base.results = B->d_results.p;
-    B->small = base;
-    B->small.doc_list = B->d_lists.p;
-    B->small.n_list = uint32_t(B->small_list.size());
-    B->small.lds_blocks = B->lds_blocks;
-    B->small.counter = B->d_counter.p;
-    B->large = base;
-    B->large.doc_list = B->d_lists.p + B->small_list.size();
-    B->large.n_list = uint32_t(B->large_list.size());
-    B->large.counter = B->d_counter.p + 1;
-    if (!B->small_list.empty() && !getenv("DTGPU_NO_FALLBACK")) {
-        B->small.fb_count = B->d_fb.p;
-        B->small.fb_list = B->d_fb.p + 1;
-        B->large.fb_count = B->d_fb.p;
-        B->large.fb_list = B->d_fb.p + 1;
-    }
+    if (set_tier_params(*B, base) != DTGPU_OK) return DTGPU_ERR_HIP;
     *out = B.release();
     return DTGPU_OK;
 }
@@ -642,7 +688,7 @@ int launch_all(dtgpu_batch *B, hipStream_t s) {
         int e = launch_plan(B->plan, s);
         if (e) return e;
     }
-    return launch_replay(B->small, B->large, s, B->n_cu);
+    return replay_all(B, s);
 }
 
 }  // namespace
@@ -979,7 +1025,7 @@ dtgpu_status dtgpu_batch_run_e2e_timed(dtgpu_batch *B, float ms[4]) {
     if (hipEventRecord(B->ev0, s) != hipSuccess) return DTGPU_ERR_HIP;
     if (B->n_gpu_planned && launch_plan(B->plan, s) != OK) return DTGPU_ERR_HIP;
     if (hipEventRecord(B->ev_mid, s) != hipSuccess) return DTGPU_ERR_HIP;
-    int st = launch_replay(B->small, B->large, s, B->n_cu);
+    int st = replay_all(B, s);
     if (st) return dtgpu_status(st);
     if (hipEventRecord(B->ev1, s) != hipSuccess) return DTGPU_ERR_HIP;
     if (hipEventSynchronize(B->ev1) != hipSuccess) return DTGPU_ERR_HIP;
@@ -995,9 +1041,12 @@ dtgpu_status dtgpu_batch_run(dtgpu_batch *B, void *stream) {
     if (!B) return DTGPU_ERR_ARG;
     if (hipSetDevice(B->device) != hipSuccess) return DTGPU_ERR_HIP;
     void *s = stream ? stream : reinterpret_cast<void *>(B->stream);
-    if (B->small.debug) fprintf(stderr, "[dtgpu] launch small=%u large=%u lds_blocks=%u\n", B->small.n_list, B->large.n_list, B->lds_blocks);
+    if (B->debug)
+        fprintf(stderr, "[dtgpu] launch lds tiers %u/%u/%u/%u (blocks %u/%u/%u/%u) hbm %u\n", B->tier[0].n_list,
+                B->tier[1].n_list, B->tier[2].n_list, B->tier[3].n_list, B->tier[0].lds_blocks, B->tier[1].lds_blocks,
+                B->tier[2].lds_blocks, B->tier[3].lds_blocks, B->large.n_list);
     dtgpu_status st = dtgpu_status(launch_all(B, reinterpret_cast<hipStream_t>(s)));
-    if (B->small.debug) {
+    if (B->debug) {
         fprintf(stderr, "[dtgpu] launched status %d\n", int(st));
         hipError_t e = hipStreamSynchronize(reinterpret_cast<hipStream_t>(s));
         fprintf(stderr, "[dtgpu] synced %d\n", int(e));
@@ -1018,7 +1067,7 @@ dtgpu_status dtgpu_batch_run_timed(dtgpu_batch *B, float *ms) {
     if (hipEventRecord(B->ev0, s) != hipSuccess) return DTGPU_ERR_HIP;
     if (B->n_gpu_planned && launch_plan(B->plan, s) != OK) return DTGPU_ERR_HIP;
     if (hipEventRecord(B->ev_mid, s) != hipSuccess) return DTGPU_ERR_HIP;
-    int st = B->xf_mode ? launch_replay_xf(B->large, s) : launch_replay(B->small, B->large, s, B->n_cu);
+    int st = B->xf_mode ? launch_replay_xf(B->large, s) : replay_all(B, s);
     if (st) return dtgpu_status(st);
     if (hipEventRecord(B->ev1, s) != hipSuccess) return DTGPU_ERR_HIP;
     if (hipEventSynchronize(B->ev1) != hipSuccess) return DTGPU_ERR_HIP;
@@ -1095,7 +1144,7 @@ dtgpu_status dtgpu_batch_plan_profile(dtgpu_batch *B, size_t i, uint64_t out[8])
     out[7] = r.ntlist;
     return DTGPU_OK;
 }
-dtgpu_status dtgpu_batch_doc_stats(dtgpu_batch *B, size_t i, uint32_t out[22]) {
+dtgpu_status dtgpu_batch_doc_stats(dtgpu_batch *B, size_t i, uint32_t out[24]) {
     if (!B || i >= B->n || !out) return DTGPU_ERR_ARG;
     DocResult r;
     if (hipMemcpyAsync(&r, B->d_results.p + i, sizeof r, hipMemcpyDeviceToHost, B->stream) != hipSuccess ||
@@ -1104,6 +1153,8 @@ dtgpu_status dtgpu_batch_doc_stats(dtgpu_batch *B, size_t i, uint32_t out[22]) {
     out[0] = r.n_items; out[1] = r.n_blocks; out[2] = r.fail_cmd; out[3] = r.fail_site;
     out[4] = B->docs[i].ncmd; out[5] = B->docs[i].max_blocks;
     for (int k = 0; k < 16; k++) out[6 + k] = r.dbg[k];
+    out[22] = r.n_sb;
+    out[23] = r.lds;
     return DTGPU_OK;
 }
 uint64_t dtgpu_batch_total_lv(const dtgpu_batch *B) { return B ? B->total_lv : 0; }
@@ -1131,7 +1182,7 @@ dtgpu_status dtgpu_batch_text(dtgpu_batch *B, size_t i, uint8_t *out, size_t cap
         hipStreamSynchronize(B->stream) != hipSuccess)
         return DTGPU_ERR_HIP;
     if (r.status != OK) {
-        if (B->small.debug)
+        if (B->debug)
             fprintf(stderr, "[dtgpu] doc %zu status %u fail_cmd %u fail_site %u items %u blocks %u dbg %u %u %u %u %u %u %u %x %x %x\n", i, r.status,
                     r.fail_cmd, r.fail_site, r.n_items, r.n_blocks, r.dbg[0], r.dbg[1], r.dbg[2], r.dbg[3], r.dbg[4],
                     r.dbg[5], r.dbg[6], r.dbg[7], r.dbg[8], r.dbg[9]);

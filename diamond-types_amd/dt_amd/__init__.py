@@ -668,11 +668,12 @@ class Batch:
 
     def doc_stats(self, i):
         """Diagnostics of document i after a run (see dtgpu_batch_doc_stats)."""
-        out = (ctypes.c_uint32 * 22)()
+        out = (ctypes.c_uint32 * 24)()
         _check(lib().dtgpu_batch_doc_stats(self._h, i, out))
         keys = ["n_items", "n_blocks", "fail_cmd", "fail_site", "n_cmds", "max_blocks",
                 "cyc_ins", "cyc_del", "cyc_tog", "cyc_mat", "cyc_yjs", "cyc_split", "cyc_find", "cyc_bload",
-                "cyc_orr", "cyc_run", "cyc_r1", "cyc_r2", "cyc_r3", "n_yjs", "n_split", "cyc_total"]
+                "cyc_orr", "cyc_run", "cyc_r1", "cyc_r2", "cyc_r3", "n_yjs", "n_split", "cyc_total",
+                "n_sb", "lds_index"]
         return dict(zip(keys, list(out)))
 
     @property
@@ -834,3 +835,18 @@ def synth_merge_oplog(doc, target_ops=5000, n_agents=0):
     h = ctypes.c_void_p()
     _check(lib().dtgpu_synth_merge_oplog(doc, target_ops, n_agents, ctypes.byref(h)))
     return ListOpLog(h.value)
+
+
+def apply_edits_push_merge(txns, agent_name="jeremy"):
+    """crates/bench/src/utils.rs:25-44 (apply_edits_push_merge): a JSON trace's patches
+    (pos, del, ins) pushed into a new ListOpLog by one agent at the current version, delete
+    before insert.  The oplog the reference's benches and checkout_tip run on."""
+    o = ListOpLog()
+    a = o.get_or_create_agent_id(agent_name)
+    for txn in txns:
+        for pos, dl, ins in txn["patches"]:
+            if dl:
+                o.add_delete_without_content(a, pos, pos + dl)
+            if ins:
+                o.add_insert(a, pos, ins)
+    return o

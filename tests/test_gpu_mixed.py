@@ -1,11 +1,10 @@
 """BASELINE configs[4]: one device-staged, skewed batch of all 8 benchmark_data traces (3 .dt
 files + the 5 JSON traces written as .dt the way crates/bench/src/utils.rs:25-44 builds their
-oplogs), ~36x apart in LVs, every document checked against its golden endContent (the JSON
+oplogs, written by the native encoder), ~36x apart in LVs, every document checked against its golden endContent (the JSON
 traces, friendsforever) or the oracle (git-makefile, node_nodecc: oracle-pinned)."""
 import gzip
 import json
 import os
-import sys
 
 import pytest
 
@@ -21,9 +20,6 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 @pytest.fixture(scope="module")
 def mixed():
-    sys.path.insert(0, ROOT)
-    from bench import trace_ops
-    from dt_encode import encode_dt
     if dt_amd.device_count() < 1:
         pytest.fail("no HIP device visible: the engine has no CPU fallback")
     docs, want = [], []
@@ -37,7 +33,7 @@ def mixed():
             want.append(OracleOpLog.load_from(d).checkout_tip_bytes())
     for n in G.JSON_TRACES:
         t = G.trace(n)
-        docs.append(encode_dt(["jeremy"], trace_ops(t["txns"])))
+        docs.append(dt_amd.apply_edits_push_merge(t["txns"]).encode())
         want.append(t["endContent"].encode())
     # skew: the small traces many times, the big ones twice (configs[4] replicates the set)
     reps = [4, 2, 2, 2, 2, 3, 4, 6]
@@ -66,3 +62,14 @@ def test_mixed_skewed_batch_device_staged(mixed):
     assert ms > 0
     assert [(r["status"], r["text_len"], r["text_hash"]) for r in b.results()] == \
            [(0, len(w), dt_amd.text_hash(w)) for w in want]
+
+
+def test_run_timed_on_host_and_device_staged_batches():
+    d = G.dt_bytes("friendsforever")
+    for staging in ("host", "device"):
+        b = dt_amd.Batch(docs=[d, d, d], staging=staging)
+        ms = b.run_timed()
+        plan, replay, prep = b.last_times()
+        assert ms > 0 and plan > 0 and replay > 0
+        assert (prep > 0) == (staging == "device")   # walker inputs are a kernel only when device-staged
+        assert all(r["status"] == 0 for r in b.results())
