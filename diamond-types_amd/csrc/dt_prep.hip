@@ -253,6 +253,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
         cp.init(); cxy.init(); cpp.init();
         uint32_t bch = 0, bsd = 0;   // chain / seq0 - start of the current 64 entries, flushed per 64
         uint64_t keep = 0;   // entries of the current 64 whose row a later, non-adjacent child reads
+        // the last RING entries' parent vectors (one VGPR each) with their chain and seq offset:
+        // a merge's other parent is almost always a few entries back (friendsforever: all within
+        // 7, git-makefile 63 % within 8), so its row comes from registers, not an HBM round trip
+        constexpr uint32_t RING = 8;
+        uint32_t ring_id[RING], ring_row[RING], ring_ch[RING], ring_sd[RING];
+#pragma unroll
+        for (uint32_t j = 0; j < RING; j++) { ring_id[j] = 0xFFFFFFFFu; ring_row[j] = ring_ch[j] = ring_sd[j] = 0; }
         for (uint32_t i = 0; i < ne; i++) {
             if ((i & 63u) == 0) {   // an entry whose only child is the next one needs no stored row
                 const uint32_t j = i + l;
@@ -274,12 +281,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
                 if (pe + 1 == i) {
                     prow = prev_row; pc = prev_chain; psd = prev_sd;
                 } else {
-                    prow = rows[size_t(pe) * PREP_MAX_CHAINS + l];
-                    if (pe >= (i & ~63u)) {   // not flushed yet: from the registers
-                        pc = rdl(bch, pe & 63u); psd = rdl(bsd, pe & 63u);
-                    } else {
-                        const uint2 q = cs[pe];
-                        pc = q.x; psd = q.y;
+                    bool hit = false;
+                    prow = pc = psd = 0;
+#pragma unroll
+                    for (uint32_t j = 0; j < RING; j++)
+                        if (ring_id[j] == pe) { prow = ring_row[j]; pc = ring_ch[j]; psd = ring_sd[j]; hit = true; }
+                    if (!hit) {
+                        prow = rows[size_t(pe) * PREP_MAX_CHAINS + l];
+                        if (pe >= (i & ~63u)) {   // not flushed yet: from the registers
+                            pc = rdl(bch, pe & 63u); psd = rdl(bsd, pe & 63u);
+                        } else {
+                            const uint2 q = cs[pe];
+                            pc = q.x; psd = q.y;
+                        }
                     }
                 }
                 row = max(row, prow);
@@ -312,6 +326,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
                 wave_fence();   // later entries read these pairs back from other lanes
             }
             prev_row = row; prev_chain = c; prev_sd = s0 - s;
+#pragma unroll
+            for (uint32_t j = 0; j < RING; j++)
+                if (j == (i & (RING - 1))) { ring_id[j] = i; ring_row[j] = row; ring_ch[j] = c; ring_sd[j] = s0 - s; }
         }
     }
     wave_fence();

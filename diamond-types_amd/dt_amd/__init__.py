@@ -15,7 +15,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libdtgpu.so")
+# DTGPU_LIB_DIR: an alternative in-tree build (A/B experiments, e.g. lib_exp/); default lib/
+LIB_PATH = os.path.join(os.path.dirname(_HERE), os.environ.get("DTGPU_LIB_DIR", "lib"), "libdtgpu.so")
 
 STATUS_NAMES = {
     0: "OK", 1: "InvalidMagic", 2: "UnsupportedProtocolVersion", 3: "DocIdMismatch", 4: "BaseVersionUnknown",
