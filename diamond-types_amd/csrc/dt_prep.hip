@@ -252,21 +252,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
         Chunk2 cxy, cpp;   // entry (start, end); parent slot (LV, entry)
         cp.init(); cxy.init(); cpp.init();
         uint32_t bch = 0, bsd = 0;   // chain / seq0 - start of the current 64 entries, flushed per 64
-        uint64_t keep = 0;   // entries of the current 64 whose row a later, non-adjacent child reads
+        constexpr uint32_t RING = 8;
+        uint64_t keep = 0;   // entries of the current 64 whose row a child beyond the ring reads
         // the last RING entries' parent vectors (one VGPR each) with their chain and seq offset:
         // a merge's other parent is almost always a few entries back (friendsforever: all within
         // 7, git-makefile 63 % within 8), so its row comes from registers, not an HBM round trip
-        constexpr uint32_t RING = 8;
         uint32_t ring_id[RING], ring_row[RING], ring_ch[RING], ring_sd[RING];
 #pragma unroll
         for (uint32_t j = 0; j < RING; j++) { ring_id[j] = 0xFFFFFFFFu; ring_row[j] = ring_ch[j] = ring_sd[j] = 0; }
         for (uint32_t i = 0; i < ne; i++) {
-            if ((i & 63u) == 0) {   // an entry whose only child is the next one needs no stored row
+            if ((i & 63u) == 0) {   // a row is stored only for a child more than RING entries on
+                // (children are in index order: the last is the farthest; nearer ones read the
+                // row from the ring or, for the next entry, from prev_row)
                 const uint32_t j = i + l;
                 bool need = false;
                 if (j < ne) {
                     const uint32_t c0 = coff[j], nc = coff[j + 1] - c0;
-                    need = nc > 1 || (nc == 1 && child[c0] != j + 1);
+                    need = nc > 0 && child[c0 + nc - 1] > j + RING;
                 }
                 keep = ballot(need);
             }

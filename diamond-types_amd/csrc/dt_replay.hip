@@ -141,7 +141,8 @@ template <bool L> DEV uint32_t ix(const uint32_t *p) {
 }
 template <bool L> DEV uint32_t ix16(const uint16_t *p) { return *p; }
 
-enum ProfSlot { P_INS = 0, P_DEL, P_TOG, P_MAT, P_YJS, P_SPLIT, P_FIND, P_BLOAD, P_ORR, P_RUN, P_R1, P_R2, P_R3, P_N_YJS, P_N_SPLIT, P_N };
+enum ProfSlot { P_INS = 0, P_DEL, P_TOG, P_MAT, P_YJS, P_SPLIT, P_FIND, P_BLOAD, P_ORR, P_RUN, P_R1, P_R2, P_R3, P_N_YJS, P_N_SPLIT,
+                P_T1, P_T2, P_T3, P_N };   // P_T*: retreat/advance pass split (entries + merge, counts, index)
 
 struct Doc {
     // inputs
@@ -804,29 +805,70 @@ DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
 // same item -- only a deleted item can be touched twice (two deletes of it, or a delete and its
 // own insert) -- are merged first.  Blocks whose visibility / liveness changed are marked
 // DIRTY; their masks are rebuilt when a command next loads them.
-template <bool L>
+template <bool L, bool PROF>
 DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_pre) {
     const uint32_t l = lane_id();
-    for (uint32_t j = 0; j < n; j += 64) {
-        if (!charge(D)) return;
-        bool bad = false, act = false, del = false;
-        uint32_t item = 0;
-        int32_t d = 0, dneg = 0;   // net delta; sum of the retreats (applied first)
+    uint64_t tq = tick<PROF>();
+    // Software pipeline over the 64-entry chunks: the entry list and the delete targets are
+    // read-only here, so chunk j + 1's entries and targets are fetched while chunk j's counts
+    // are read and written; the counts themselves are read only after the previous chunk's
+    // stores (same-address order within the wave), so a later chunk sees earlier updates.
+    auto resolve = [&](uint32_t j, uint32_t e, uint32_t &item, bool &del, bool &bad) {
+        item = 0; del = false; bad = false;
         if (j + l < n) {
-            const uint32_t e = (j == 0 && have_pre) ? pre : D.tlist[off + j + l];
             const uint32_t lv = e & 0x3FFFFFFFu;
             del = (e >> 30) & 1u;
-            const bool adv = (e >> 31) != 0;
             item = lv;
             if (lv >= D.n_lv) bad = true;
             else if (del) item = *reinterpret_cast<const uint32_t *>(D.ao + lv);
+        }
+    };
+    uint32_t e_cur = have_pre ? pre : (l < n ? D.tlist[off + l] : 0u);
+    uint32_t e_nx = 64 + l < n ? D.tlist[off + 64 + l] : 0u;
+    uint32_t it_cur;
+    bool del_cur, bad_cur;
+    resolve(0, e_cur, it_cur, del_cur, bad_cur);
+    for (uint32_t j = 0; j < n; j += 64) {
+        if (!charge(D)) return;
+        bool bad = bad_cur, act = false;
+        const bool del = del_cur;
+        const uint32_t item = it_cur;
+        int32_t d = 0, dneg = 0;   // net delta; sum of the retreats (applied first)
+        if (j + l < n) {
+            const bool adv = (e_cur >> 31) != 0;
             if (!bad && item >= D.n_lv) bad = true;
             act = !bad;
             d = adv ? 1 : -1;
             dneg = adv ? 0 : -1;
         }
+        // the next chunk's targets and the one after's entries, in flight behind this chunk
+        if (j + 64 < n) {
+            e_cur = e_nx;
+            resolve(j + 64, e_cur, it_cur, del_cur, bad_cur);
+            e_nx = j + 128 + l < n ? D.tlist[off + j + 128 + l] : 0u;
+        }
         if (__ballot(bad)) { fail(D, ErrCheckout, 16); return; }
-        for (u64 dm = __ballot(act && del); dm;) {
+        if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_T1] += t - tq; tq = t; }
+        // lanes whose item another lane also touches: every lane's item against every other
+        // lane's (63 lane rotations, four independent chains); only those go through the merge
+        // (a few delete lanes: the merge loop over them is cheaper than the rotations)
+        const u64 dmask = __ballot(act && del);
+        bool dup = del;
+        if (__popcll(dmask) > 4) {
+            dup = false;
+            const uint32_t x = act ? item : (0x80000000u | l);   // inactive lanes never match
+            uint32_t r0 = x, r1 = shfl(x, (l + 16) & 63u), r2 = shfl(x, (l + 32) & 63u), r3 = shfl(x, (l + 48) & 63u);
+            dup = (r1 == x) | (r2 == x) | (r3 == x);
+#pragma unroll
+            for (int k = 1; k < 16; k++) {
+                r0 = uint32_t(__builtin_amdgcn_mov_dpp(int(r0), 0x13C, 0xF, 0xF, false));   // wave_ror:1
+                r1 = uint32_t(__builtin_amdgcn_mov_dpp(int(r1), 0x13C, 0xF, 0xF, false));
+                r2 = uint32_t(__builtin_amdgcn_mov_dpp(int(r2), 0x13C, 0xF, 0xF, false));
+                r3 = uint32_t(__builtin_amdgcn_mov_dpp(int(r3), 0x13C, 0xF, 0xF, false));
+                dup |= (r0 == x) | (r1 == x) | (r2 == x) | (r3 == x);
+            }
+        }
+        for (u64 dm = __ballot(act && dup); dm;) {
             if (!charge(D)) return;
             const uint32_t t = bcast(item, first_lane(dm));
             const u64 same = __ballot(act && item == t);
@@ -862,6 +904,7 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
         if (__ballot(bad)) { fail(D, ErrCheckout, 16); return; }
         const bool flip = fv || fl;
         if (__ballot(flip && b == D.cb)) D.cb = NONE;
+        if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_T2] += t - tq; tq = t; }
         if (L) {   // LDS index: per-lane LDS atomics
             if (flip) {
                 const uint32_t tp = ix<L>(D.sbpos + (opos_of<L>(D, b) >> 6));
@@ -888,6 +931,7 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
                 pend &= ~same;
             }
         }
+        if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_T3] += t - tq; tq = t; }
     }
     wave_fence();
 }
@@ -1080,7 +1124,7 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
                     if (PROF) D.prof[P_DEL] += tick<PROF>() - t0;
                     break;
                 case CMD_TOG:
-                    toggle_pass<L>(D, a, n, pf, pf_ok);
+                    toggle_pass<L, PROF>(D, a, n, pf, pf_ok);
                     if (PROF) D.prof[P_TOG] += tick<PROF>() - t0;
                     break;
                 default: fail(D, ErrCheckout, 18); break;
@@ -1115,8 +1159,9 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
         res->fail_site = D.err ? D.site : 0;
         if (PROF) {
             D.prof[P_MAT] = tick<PROF>() - t_mat;
-            for (int i = 0; i < P_N; i++) res->dbg[i] = uint32_t(D.prof[i] >> (i < P_N_YJS ? 4 : 0));
+            for (int i = 0; i < P_T1; i++) res->dbg[i] = uint32_t(D.prof[i] >> (i < P_N_YJS ? 4 : 0));
             res->dbg[15] = uint32_t((tick<PROF>() - t_start) >> 4);
+            for (int i = P_T1; i < P_N; i++) res->dbg[16 + (i - P_T1)] = uint32_t(D.prof[i] >> 4);
         }
     }
 }

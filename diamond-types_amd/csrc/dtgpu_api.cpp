@@ -1144,7 +1144,7 @@ dtgpu_status dtgpu_batch_plan_profile(dtgpu_batch *B, size_t i, uint64_t out[8])
     out[7] = r.ntlist;
     return DTGPU_OK;
 }
-dtgpu_status dtgpu_batch_doc_stats(dtgpu_batch *B, size_t i, uint32_t out[24]) {
+dtgpu_status dtgpu_batch_doc_stats(dtgpu_batch *B, size_t i, uint32_t out[27]) {
     if (!B || i >= B->n || !out) return DTGPU_ERR_ARG;
     DocResult r;
     if (hipMemcpyAsync(&r, B->d_results.p + i, sizeof r, hipMemcpyDeviceToHost, B->stream) != hipSuccess ||
@@ -1155,6 +1155,7 @@ dtgpu_status dtgpu_batch_doc_stats(dtgpu_batch *B, size_t i, uint32_t out[24]) {
     for (int k = 0; k < 16; k++) out[6 + k] = r.dbg[k];
     out[22] = r.n_sb;
     out[23] = r.lds;
+    for (int k = 0; k < 3; k++) out[24 + k] = r.dbg[16 + k];
     return DTGPU_OK;
 }
 uint64_t dtgpu_batch_total_lv(const dtgpu_batch *B) { return B ? B->total_lv : 0; }

@@ -242,7 +242,7 @@ uint64_t dtgpu_batch_algorithmic_bytes(dtgpu_batch *batch);
  * (DTGPU_DEBUG=2: cycles/16 in insert, delete, retreat+advance, materialise, YjsMod scans,
  * splits, and the insert phases find / block load / origin_right / run; scan and split
  * counts; total cycles/16). */
-dtgpu_status dtgpu_batch_doc_stats(dtgpu_batch *batch, size_t doc, uint32_t out[24]);
+dtgpu_status dtgpu_batch_doc_stats(dtgpu_batch *batch, size_t doc, uint32_t out[27]);
 /* Device planner cycle profile of one document (DTGPU_PLAN_PROF set at batch creation):
  * out[0..5] cycles waiting for entry records, computing parent vectors, children + next pick,
  * emitting retreat/advance entries, copying op runs, initialising; out[6] commands, out[7]
