@@ -125,7 +125,12 @@ DEV uint32_t pc_blk(uint32_t w) { return w & 0xFFFFu; }
 DEV uint32_t pc_cnt(uint32_t w) { return w >> 16; }
 DEV uint32_t pc_of(uint32_t b, uint32_t k) { return b | (k << 16); }
 
-// L2-coherent accesses (returning atomics and loads must never meet a stale L1 line).
+// Per-document state (pc, masks) is only ever read and written by its own wave with plain
+// accesses, which the CU keeps coherent for that wave: plain loads may hit L1.  The HBM-index
+// words that the HBM tier updates with memory-side atomics are read L2-coherently (ld_sc).
+template <typename T> DEV T ld(const T *p) { return *p; }
+template <typename T> DEV void st(T *p, T v) { *p = v; }
+// L2-coherent accesses (a load must never meet a stale L1 line of a word an atomic changed).
 template <typename T> DEV T ld_sc(const T *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 template <typename T> DEV void st_sc(T *p, T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 DEV uint32_t cv_add(uint32_t *p, uint32_t d) { return __hip_atomic_fetch_add(p, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
@@ -173,7 +178,7 @@ struct Doc {
     uint32_t n_items;
     uint32_t debug;
     uint32_t site, ci;
-    uint64_t steps, step_limit;   // watchdog: every loop iteration is charged; a bound
+    uint32_t steps, step_limit;   // watchdog: every loop iteration is charged; a bound
                                   // violation ends the document with ErrCapacity
     uint64_t prof[P_N];
     uint32_t doc;
@@ -254,12 +259,12 @@ DEV uint32_t find_slot(const Doc &D, uint32_t b, uint32_t item) {
 }
 // Document-order key of an inserted item, per lane.
 template <bool L> DEV uint32_t key_of(const Doc &D, uint32_t item) {
-    const uint32_t b = pc_blk(ld_sc(D.pc + item));
+    const uint32_t b = pc_blk(ld(D.pc + item));
     return key_at<L>(D, b, find_slot(D, b, item));
 }
 // Same for a wave-uniform item: one row load and a ballot.
 template <bool L> DEV uint32_t ukey_of(const Doc &D, uint32_t item) {
-    const uint32_t b = U(pc_blk(ld_sc(D.pc + item)));
+    const uint32_t b = U(pc_blk(ld(D.pc + item)));
     const u64 m = __ballot(D.items[size_t(b) * BLK + lane_id()] == item);
     return U(key_at<L>(D, b, first_lane(m)));
 }
@@ -400,19 +405,19 @@ DEV uint32_t split_block(Doc &D, uint32_t b, uint32_t c, uint32_t it, u64 mv, u6
     const uint32_t b2 = D.nb;
     u64 mu = 0, mu_lo = 0, mu_hi = 0;
     if (XF) {
-        mu = U64(ld_sc(D.mup + b));
+        mu = U64(ld(D.mup + b));
         mu_lo = mu & lanes_below(c);
         mu_hi = c >= 64 ? 0ull : mu >> c;
     }
     if (l >= c) {   // the moved items change block (content-tree's notify on a leaf split)
         D.items[size_t(b2) * BLK + (l - c)] = it;
-        st_sc(D.pc + it, (ld_sc(D.pc + it) & 0xFFFF0000u) | b2);
+        st(D.pc + it, (ld(D.pc + it) & 0xFFFF0000u) | b2);
     }
     const u64 lo = lanes_below(c);
     const u64 mv_hi = c >= 64 ? 0ull : mv >> c, ml_hi = c >= 64 ? 0ull : ml >> c;
     if (l < 4) {   // both blocks' mask pairs in one store
         const u64 v = l == 0 ? (mv & lo) : l == 1 ? (ml & lo) : l == 2 ? mv_hi : ml_hi;
-        st_sc(D.m2 + 2 * size_t(l < 2 ? b : b2) + (l & 1), v);
+        st(D.m2 + 2 * size_t(l < 2 ? b : b2) + (l & 1), v);
     }
     const uint32_t o = U(opos_of<L>(D, b));
     const uint32_t S = o >> 6, i = o & 63u, n = U(ix<L>(D.sbn + S));
@@ -431,7 +436,7 @@ DEV uint32_t split_block(Doc &D, uint32_t b, uint32_t c, uint32_t it, u64 mv, u6
                     uint32_t(__popcll(mu_hi)) * C_UP;
         D.cnt[b] = uint32_t(__popcll(mv & lo)) * C_VIS + uint32_t(__popcll(ml & lo)) * C_LIVE + c * C_ITEMS +
                    uint32_t(__popcll(mu_lo)) * C_UP;
-        if (XF) { st_sc(D.mup + b, mu_lo); st_sc(D.mup + b2, mu_hi); }
+        if (XF) { st(D.mup + b, mu_lo); st(D.mup + b2, mu_hi); }
         D.sbl[size_t(S) * SBC + i + 1] = uint16_t(b2);
         set_opos<L>(D, b2, (S << 6) | (i + 1));
         D.sbn[S] = n + 1;
@@ -463,7 +468,7 @@ DEV uint32_t up_rank(Doc &D, uint32_t b, uint32_t s) {
     for (uint32_t c = 0; c < tp; c += 64) r += wave_sum(c + l < tp ? ix<L>(D.tup + c + l) : 0u);
     const uint32_t bl = l < i ? ix16<L>(D.sbl + size_t(S) * SBC + l) : 0;
     r += wave_sum(l < i ? c_up(ix<L>(D.cnt + bl)) : 0u);
-    r += uint32_t(__popcll(U64(ld_sc(D.mup + b)) & lanes_below(s)));
+    r += uint32_t(__popcll(U64(ld(D.mup + b)) & lanes_below(s)));
     return U(r);
 }
 
@@ -471,7 +476,7 @@ DEV uint32_t up_rank(Doc &D, uint32_t b, uint32_t s) {
 // block's items lane by lane (lanes >= the block count are don't-care); mv / ml its masks.
 template <bool L, bool PROF, bool XF>
 DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml, uint32_t lv, uint32_t k,
-                    uint32_t ol, uint32_t orr) {
+                    uint32_t ol, uint32_t orr, uint32_t tph) {
     D.cb = NONE;
     const uint32_t l = lane_id();
     const uint32_t lv0 = lv, k0 = k;
@@ -488,6 +493,7 @@ DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml,
             const uint32_t cut = cut_point<L>(s);
             const uint32_t b2 = split_block<L, XF>(D, b, cut, it, mv, ml);
             if (D.err) return;
+            tph = NONE;   // a split may move superblocks in the top order
             if (s > cut || cut == BLK) {
                 b = b2;
                 s -= cut;
@@ -509,24 +515,24 @@ DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml,
         const uint32_t shifted = shfl(it, l >= m ? l - m : l);
         it = l < s ? it : (l < s + m ? lv + (l - s) : shifted);
         if (l >= s && l < bc + m) items[l] = it;
-        if (l >= s && l < s + m) st_sc(D.pc + it, pc_of(b, 1u));
+        if (l >= s && l < s + m) st(D.pc + it, pc_of(b, 1u));
         if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_R1] += t - tr; tr = t; }
         const u64 low = lanes_below(s);
         const u64 ins = lanes_below(m) << s;
         mv = m == 64 ? ins : ((mv & low) | ((mv & ~low) << m) | ins);
         ml = m == 64 ? ins : ((ml & low) | ((ml & ~low) << m) | ins);
-        if (l < 2) st_sc(D.m2 + 2 * size_t(b) + l, l == 0 ? mv : ml);
+        if (l < 2) st(D.m2 + 2 * size_t(b) + l, l == 0 ? mv : ml);
         if (XF) {
-            u64 mu = U64(ld_sc(D.mup + b));
+            u64 mu = U64(ld(D.mup + b));
             mu = m == 64 ? ins : ((mu & low) | ((mu & ~low) << m) | ins);
-            if (l == 0) st_sc(D.mup + b, mu);
+            if (l == 0) st(D.mup + b, mu);
         }
-        if (l == 0) {
+        if (l == 0) {   // the superblock's totals by atomic add: no dependent read
             D.cnt[b] = c + m * (C_VIS + C_LIVE + C_ITEMS + (XF ? C_UP : 0u));
-            const uint32_t tp = ix<L>(D.sbpos + (opos_of<L>(D, b) >> 6));
-            D.top[tp] = ix<L>(D.top + tp) + m;
-            D.tlive[tp] = ix<L>(D.tlive + tp) + m;
-            if (XF) D.tup[tp] = ix<L>(D.tup + tp) + m;
+            const uint32_t tp = tph != NONE ? tph : ix<L>(D.sbpos + (opos_of<L>(D, b) >> 6));
+            at_add(D.top + tp, m);
+            at_add(D.tlive + tp, m);
+            if (XF) at_add(D.tup + tp, m);
         }
         wave_fence();
         if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_R2] += t - tr; tr = t; }
@@ -645,15 +651,15 @@ DEV void load_block(Doc &D, uint32_t b, uint32_t c, uint32_t &it, u64 &mv, u64 &
     const uint32_t bc = c_items(c);
     it = l < bc ? D.items[size_t(b) * BLK + l] : 0;
     if (c & C_DIRTY) {
-        const uint32_t k = l < bc ? pc_cnt(ld_sc(D.pc + it)) : 0u;
+        const uint32_t k = l < bc ? pc_cnt(ld(D.pc + it)) : 0u;
         mv = __ballot(l < bc && k == 1u);
         ml = __ballot(l < bc && k != 0u);
-        if (l < 2) st_sc(D.m2 + 2 * size_t(b) + l, l == 0 ? mv : ml);
+        if (l < 2) st(D.m2 + 2 * size_t(b) + l, l == 0 ? mv : ml);
         if (l == 0) D.cnt[b] = c & ~C_DIRTY;
         wave_fence();
     } else {
         u64 x = 0;
-        if (l < 2) x = ld_sc(D.m2 + 2 * size_t(b) + l);
+        if (l < 2) x = ld(D.m2 + 2 * size_t(b) + l);
         mv = bcast64(x, 0);
         ml = bcast64(x, 1);
     }
@@ -664,7 +670,7 @@ DEV void load_block(Doc &D, uint32_t b, uint32_t c, uint32_t &it, u64 &mv, u64 &
 template <bool L, bool PROF, bool XF>
 DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
     uint64_t tp = tick<PROF>();
-    uint32_t b, kk = 0;
+    uint32_t b, kk = 0, tph = 0;   // tph: top position of b's superblock (first block: 0)
     if (pos == 0) {
         b = first_block<L>(D);
     } else {
@@ -672,6 +678,7 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
         if (!find_vis<L>(D, pos - 1, f)) { fail(D, ErrCheckout, 13); return; }
         b = f.b;
         kk = f.k;
+        tph = f.tp;
     }
     if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_FIND] += t - tp; tp = t; }
     const uint32_t c0 = U(ix<L>(D.cnt + b));
@@ -727,11 +734,12 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
         if (b != b0) {
             if (b == D.cb) { it = D.cit; mv = D.cmv; ml = D.cml; }
             else load_block<L>(D, b, U(ix<L>(D.cnt + b)), it, mv, ml);
+            tph = NONE;
         }
         if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_YJS] += t - tp; tp = t; D.prof[P_N_YJS]++; }
     }
     const uint64_t sp0 = PROF ? D.prof[P_SPLIT] : 0;
-    insert_run<L, PROF, XF>(D, b, s, it, mv, ml, lv, k, ol, orr);
+    insert_run<L, PROF, XF>(D, b, s, it, mv, ml, lv, k, ol, orr, tph);
     if (PROF) D.prof[P_RUN] += tick<PROF>() - tp - (D.prof[P_SPLIT] - sp0);
     D.n_items += k;
 }
@@ -763,13 +771,13 @@ DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
         u64 mu = 0;
         uint32_t base = 0;
         if (XF) {
-            mu = U64(ld_sc(D.mup + b));
+            mu = U64(ld(D.mup + b));
             base = up_rank<L>(D, b, 0);
         }
         if (sel) {
             const uint32_t j = j0 + (r - kk);
             const uint32_t dlv = fwd ? lv + j : lv + n - 1 - j;
-            st_sc(D.pc + it, pc_of(b, 2u));   // visible (count 1) -> deleted once
+            st(D.pc + it, pc_of(b, 2u));   // visible (count 1) -> deleted once
             *reinterpret_cast<uint32_t *>(D.ao + dlv) = it;
             if (XF) {
                 // LV order applies a forward run left to right (the run's items to the left are
@@ -784,11 +792,11 @@ DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
         const uint32_t gone = XF ? uint32_t(__popcll(mu & selm)) : 0u;   // never-deleted items deleted now
         up_done += gone;
         if (l == 0) {
-            st_sc(D.m2 + 2 * size_t(b), mv & ~selm);
+            st(D.m2 + 2 * size_t(b), mv & ~selm);
             D.cnt[b] = c - take * C_VIS - gone * C_UP;
-            D.top[f.tp] = ix<L>(D.top + f.tp) - take;
+            at_add(D.top + f.tp, 0u - take);
             if (XF) {
-                st_sc(D.mup + b, mu & ~selm);
+                st(D.mup + b, mu & ~selm);
                 D.tup[f.tp] = ix<L>(D.tup + f.tp) - gone;
             }
         }
@@ -887,14 +895,14 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
         uint32_t b = 0;
         int32_t dv = 0, dl = 0;
         if (act) {
-            const uint32_t w = ld_sc(D.pc + item);
+            const uint32_t w = ld(D.pc + item);
             b = pc_blk(w);
             const uint32_t oc = pc_cnt(w);
             const uint32_t nc = oc + uint32_t(d);
             if (int32_t(oc) + dneg < 0 || int32_t(oc) + d > 0xFFFF || b >= D.nb) {
                 bad = true;
             } else {
-                st_sc(D.pc + item, pc_of(b, nc));
+                st(D.pc + item, pc_of(b, nc));
                 fv = (oc == 1) != (nc == 1);
                 fl = (oc != 0) != (nc != 0);
                 dv = fv ? (nc == 1 ? 1 : -1) : 0;
@@ -963,7 +971,7 @@ DEV void materialise(Doc &D, uint8_t *out, uint32_t cap, uint32_t &len_out, u64 
             }
 #pragma unroll
             for (uint32_t g = 0; g < G; g++) {
-                k[g] = vis[g] ? pc_cnt(ld_sc(D.pc + it[g])) : 0;
+                k[g] = vis[g] ? pc_cnt(ld(D.pc + it[g])) : 0;
                 cb[g] = vis[g] ? D.cbyte[it[g]] : 0;
             }
 #pragma unroll
@@ -1022,15 +1030,15 @@ DEV uint32_t check_invariants(Doc &D, DocResult *res) {
             const uint32_t c = U(ix<L>(D.cnt + b));
             const uint32_t cnt = c_items(c);
             const bool dirty = (c & C_DIRTY) != 0;
-            u64 mv = U64(ld_sc(D.m2 + 2 * size_t(b))), ml = U64(ld_sc(D.m2 + 2 * size_t(b) + 1));
+            u64 mv = U64(ld(D.m2 + 2 * size_t(b))), ml = U64(ld(D.m2 + 2 * size_t(b) + 1));
             if (dirty) {   // stale masks: check the counts against cv[] instead
                 const uint32_t i2 = l < cnt ? D.items[size_t(b) * BLK + l] : 0;
-                const uint32_t k = l < cnt && i2 < D.n_lv ? pc_cnt(ld_sc(D.pc + i2)) : 0u;
+                const uint32_t k = l < cnt && i2 < D.n_lv ? pc_cnt(ld(D.pc + i2)) : 0u;
                 mv = __ballot(l < cnt && k == 1u);
                 ml = __ballot(l < cnt && k != 0u);
             }
             if (uint32_t(__popcll(mv)) != c_vis(c) || uint32_t(__popcll(ml)) != c_live(c)) return 207;
-            if (XF && uint32_t(__popcll(U64(ld_sc(D.mup + b)))) != c_up(c)) return 209;
+            if (XF && uint32_t(__popcll(U64(ld(D.mup + b)))) != c_up(c)) return 209;
             if (XF) tu += c_up(c);
             tv += c_vis(c);
             tl += c_live(c);
@@ -1040,8 +1048,8 @@ DEV uint32_t check_invariants(Doc &D, DocResult *res) {
                 it = D.items[size_t(b) * BLK + l];
                 if (it >= D.n_lv) bad = true;
                 else {
-                    w = pc_blk(ld_sc(D.pc + it));
-                    const uint32_t k = pc_cnt(ld_sc(D.pc + it));
+                    w = pc_blk(ld(D.pc + it));
+                    const uint32_t k = pc_cnt(ld(D.pc + it));
                     if (((mv >> l) & 1) != (k == 1 ? 1u : 0u)) bad = true;
                     if (((ml >> l) & 1) != (k != 0 ? 1u : 0u)) bad = true;
                     if (w != b || find_slot(D, b, it) != l) bad = true;
@@ -1074,16 +1082,16 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
     if (l == 0) {
         D.cnt[0] = 0; set_opos<L>(D, 0, 0);
         D.sbl[0] = 0; D.sbn[0] = 1; D.sbpos[0] = 0; D.top[0] = 0; D.tlive[0] = 0;
-        if (XF) { D.tup[0] = 0; st_sc(D.mup, 0ull); }
+        if (XF) { D.tup[0] = 0; st(D.mup, 0ull); }
     }
-    if (l < 2) st_sc(D.m2 + l, 0ull);
+    if (l < 2) st(D.m2 + l, 0ull);
     wave_fence();
     D.nb = 1;
     D.nsb = 1;
     D.err = 0;
     D.n_items = 0;
     D.steps = 0;
-    D.step_limit = 64ull * (uint64_t(D.ncmd) + D.n_lv) + 4096;
+    D.step_limit = uint32_t(min<uint64_t>(64ull * (uint64_t(D.ncmd) + D.n_lv) + 4096, 0xFFFFFFF0ull));
     D.site = 0;
     D.ci = 0;
     D.cb = NONE;
