@@ -198,8 +198,10 @@ struct Doc {
 DEV void fail(Doc &D, uint32_t code, uint32_t site) {
     if (!D.err) { D.err = code; D.site = site; }
 }
-// Charge one loop iteration; returns false (and flags the document) past the budget, so every
-// loop in the replay provably terminates whatever the input.
+// Charge one loop iteration; returns false (and flags the document) past the budget.  Charged:
+// the command loop and the loops that walk the index (YjsMod scan, next live block, agent
+// search), whose termination rests on the index being consistent; every other loop retires at
+// least one item, lane or block per round.
 DEV bool charge(Doc &D) {
     if (++D.steps > D.step_limit) { fail(D, ErrCapacity, 1); return false; }
     return true;
@@ -484,8 +486,7 @@ DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml,
         const uint32_t r0 = up_rank<L>(D, b, s);
         for (uint32_t j = l; j < k0; j += 64) D.xf[lv0 + j] = r0 + j;
     }
-    while (k > 0) {
-        if (!charge(D)) return;
+    while (k > 0) {   // each round inserts >= 1 item or splits (bounded by max_blocks)
         const uint32_t c = U(ix<L>(D.cnt + b));
         const uint32_t bc = c_items(c);
         if (bc == BLK) {
@@ -514,7 +515,7 @@ DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml,
         // with one store; only the new items get a block in pos[] (shifted ones stay put)
         const uint32_t shifted = shfl(it, l >= m ? l - m : l);
         it = l < s ? it : (l < s + m ? lv + (l - s) : shifted);
-        if (l >= s && l < bc + m) items[l] = it;
+        items[l] = it;   // the whole row: slots past the count are don't-care
         if (l >= s && l < s + m) st(D.pc + it, pc_of(b, 1u));
         if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_R1] += t - tr; tr = t; }
         const u64 low = lanes_below(s);
@@ -751,8 +752,7 @@ DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
     const uint32_t l = lane_id();
     uint32_t j0 = 0;
     uint32_t up_done = 0;   // XF: never-deleted items this run deleted in earlier (left) blocks
-    while (j0 < n) {
-        if (!charge(D)) return;
+    while (j0 < n) {   // each round deletes >= 1 item or fails
         Found f;
         if (!find_vis<L>(D, pos, f)) { fail(D, ErrCheckout, 14); return; }
         const uint32_t b = f.b, kk = f.k;
@@ -837,7 +837,6 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
     bool del_cur, bad_cur;
     resolve(0, e_cur, it_cur, del_cur, bad_cur);
     for (uint32_t j = 0; j < n; j += 64) {
-        if (!charge(D)) return;
         bool bad = bad_cur, act = false;
         const bool del = del_cur;
         const uint32_t item = it_cur;
@@ -876,8 +875,7 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
                 dup |= (r0 == x) | (r1 == x) | (r2 == x) | (r3 == x);
             }
         }
-        for (u64 dm = __ballot(act && dup); dm;) {
-            if (!charge(D)) return;
+        for (u64 dm = __ballot(act && dup); dm;) {   // each round retires >= 1 lane
             const uint32_t t = bcast(item, first_lane(dm));
             const u64 same = __ballot(act && item == t);
             if (same & (same - 1)) {
@@ -922,8 +920,7 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
                 at_or(D.cnt + b, C_DIRTY);
             }
         } else {   // HBM index: one atomic per distinct block (a global atomic is a memory-side request)
-            for (u64 pend = __ballot(flip); pend;) {
-                if (!charge(D)) return;
+            for (u64 pend = __ballot(flip); pend;) {   // each round retires >= 1 lane
                 const uint32_t f = first_lane(pend);
                 const uint32_t bb = bcast(b, f);
                 const u64 same = __ballot(flip && b == bb);
@@ -1120,6 +1117,26 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
                 nx_ok = true;
             }
             const uint64_t t0 = tick<PROF>();
+#ifdef DTGPU_SALU_PAD   // experiment: extra independent scalar adds per command (SALU issue-bound?)
+            {
+                uint32_t x0 = D.ci, x1 = x0 + 1, x2 = x0 + 2, x3 = x0 + 3;
+#pragma unroll
+                for (int q = 0; q < DTGPU_SALU_PAD; q++)
+                    asm volatile("s_add_u32 %0, %0, 1\n\ts_add_u32 %1, %1, 1\n\ts_add_u32 %2, %2, 1\n\ts_add_u32 %3, %3, 1"
+                                 : "+s"(x0), "+s"(x1), "+s"(x2), "+s"(x3));
+                D.site += (x0 + x1 + x2 + x3 == 0x12345u) ? 1u : 0u;
+            }
+#endif
+#ifdef DTGPU_VALU_PAD   // experiment: extra independent vector adds per command (VALU issue-bound?)
+            {
+                uint32_t x0 = l, x1 = l + 1, x2 = l + 2, x3 = l + 3;
+#pragma unroll
+                for (int q = 0; q < DTGPU_VALU_PAD; q++)
+                    asm volatile("v_add_u32 %0, %0, 1\n\tv_add_u32 %1, %1, 1\n\tv_add_u32 %2, %2, 1\n\tv_add_u32 %3, %3, 1"
+                                 : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
+                if (__ballot(x0 + x1 + x2 + x3 == 0x12345u)) D.site++;
+            }
+#endif
             switch (op & 15u) {
                 case CMD_INS:
                     if (n == 0 || a >= D.n_lv || n > D.n_lv - a) { fail(D, ErrCheckout, 17); break; }
