@@ -804,13 +804,62 @@ Status decode_dt(const uint8_t *data, size_t len, bool ignore_crc, HostOpLog &o)
 }
 
 // ListOpLog::decode_and_add_opts (decode_oplog.rs:476-583): on error the oplog is unwound to
-// what it was before the call (the reference truncates each structure back to its old length;
-// here the prior state is restored wholesale, with the same result).
+// what it was before the call.  Like the reference, each structure is truncated back to its old
+// length; the RLE appends may have extended the last run of a structure in place, so that run is
+// recorded and restored too.  O(agents + version) to record, no copy of the oplog.
+namespace {
+struct OpLogMark {
+    size_t n_agents, n_agent_runs, n_ops, n_content, n_cbyte, n_entries;
+    std::vector<std::pair<size_t, uint64_t>> seqs;   // per agent: runs, len of the last run
+    AgentRun last_agent_run{};
+    OpRun last_op{};
+    uint64_t last_entry_end = 0;
+    std::vector<uint64_t> version;
+    uint64_t n_lv;
+    bool content_complete, has_doc_id;
+    std::string doc_id;
+
+    explicit OpLogMark(const HostOpLog &o)
+        : n_agents(o.agent_names.size()), n_agent_runs(o.agent_runs.size()), n_ops(o.ops.size()),
+          n_content(o.ins_content.size()), n_cbyte(o.ins_cbyte.size()), n_entries(o.graph.entries.size()),
+          version(o.version), n_lv(o.n_lv), content_complete(o.content_complete),
+          has_doc_id(o.has_doc_id), doc_id(o.doc_id) {
+        seqs.reserve(o.agent_seqs.size());
+        for (const auto &v : o.agent_seqs) seqs.emplace_back(v.size(), v.empty() ? 0 : v.back().len);
+        if (n_agent_runs) last_agent_run = o.agent_runs.back();
+        if (n_ops) last_op = o.ops.back();
+        if (n_entries) last_entry_end = o.graph.entries.back().end;
+    }
+    void unwind(HostOpLog &o) const {
+        o.agent_names.resize(n_agents);
+        o.agent_seqs.resize(seqs.size());
+        for (size_t a = 0; a < seqs.size(); a++) {
+            auto &v = o.agent_seqs[a];
+            v.resize(seqs[a].first);
+            if (!v.empty()) v.back().len = seqs[a].second;
+        }
+        o.agent_runs.resize(n_agent_runs);
+        if (n_agent_runs) o.agent_runs.back() = last_agent_run;
+        o.ops.resize(n_ops);
+        if (n_ops) o.ops.back() = last_op;
+        o.ins_content.resize(n_content);
+        o.ins_cbyte.resize(n_cbyte);
+        o.graph.entries.resize(n_entries);
+        if (n_entries) o.graph.entries.back().end = last_entry_end;
+        o.version = version;
+        o.n_lv = n_lv;
+        o.content_complete = content_complete;
+        o.has_doc_id = has_doc_id;
+        o.doc_id = doc_id;
+    }
+};
+}  // namespace
+
 Status decode_and_add(const uint8_t *data, size_t len, bool ignore_crc, HostOpLog &o,
                       std::vector<uint64_t> &file_frontier) {
-    HostOpLog before = o;
+    const OpLogMark mark(o);
     const Status s = decode_into(data, len, ignore_crc, o, file_frontier);
-    if (s != OK) { o = std::move(before); file_frontier.clear(); }
+    if (s != OK) { mark.unwind(o); file_frontier.clear(); }
     return s;
 }
 

@@ -184,6 +184,26 @@ def test_error_unrolling_into_non_empty_oplog():
     assert _check_unroll_works(prefix, src) > 0
 
 
+@pytest.mark.parametrize("name", ["friendsforever", "git-makefile"])
+def test_failed_merge_unwinds_runs_extended_in_place(name):
+    """A whole benchmark file with a bad checksum merged on top of a prefix of itself: the decode
+    appends every operation (extending the prefix's last op / agent / graph runs in place) before
+    the checksum fails, and the truncating unwind restores the prefix exactly; the good file then
+    merges as if the failed call never happened (the per-agent seq maps were unwound too)."""
+    data = G.dt_bytes(name)
+    full = dt_amd.ListOpLog.load_from(data)
+    want = _keyed(full)
+    v = full.dominators([len(full) // 3])
+    d = dt_amd.ListOpLog.load_from(full.history(v).encode())
+    before = _exact(d)
+    bad = bytearray(data)
+    bad[-1] ^= 0xFF
+    assert _err(lambda: d.decode_and_add(bytes(bad))) == ChecksumFailed
+    assert _exact(d) == before
+    assert d.decode_and_add(data) == d.local_frontier()
+    assert _keyed(d) == want
+
+
 def test_save_load_save_load():   # :237-268 (content not stored)
     o2 = dt_amd.ListOpLog.load_from(_simple_doc().encode(store_inserted_content=False))
     o3 = dt_amd.ListOpLog.load_from(o2.encode(store_inserted_content=False))
