@@ -8,6 +8,7 @@
 //   DIFF      Graph::diff_rev / diff_slow_internal        src/causalgraph/graph/tools.rs:176-292
 //   CONFLICT  Graph::find_conflicting(_slow)              tools.rs:296-484 (TimePoint heap)
 //   CONTAINS  Graph::frontier_contains_version            tools.rs:88-146 (shadow shortcut)
+//   DOMINATORS Graph::find_dominators_2                   tools.rs:545-647 (tagged-LV heap)
 // The queues live in LDS (per wave); the walk is wave-uniform scalar code and the batch gives
 // the parallelism: every query of the batch runs concurrently, one per wavefront.  (The
 // checkout path itself diffs versions with per-chain version vectors in dt_plan.hip; these
@@ -164,21 +165,21 @@ __device__ __forceinline__ uint32_t q_diff(const G &g, const GraphQuery &q, uint
 }
 
 // ---- frontier_contains_version (tools.rs:88-146) ----------------------------------------------
-__device__ __forceinline__ uint32_t q_contains(const G &g, const GraphQuery &q, uint32_t *heap, uint32_t &found) {
-    const int32_t t = q.target;
+__device__ __forceinline__ uint32_t contains_version(const G &g, const int32_t *a, uint32_t na, int32_t t, uint32_t *heap,
+                                                     uint32_t &found) {
     found = 0;
     if (t < 0) { found = 1; return GQ_OK; }   // ROOT is in every version
-    for (uint32_t i = 0; i < q.na; i++) if (q.a[i] == t) { found = 1; return GQ_OK; }
-    if (!q.na) return GQ_OK;
-    for (uint32_t i = 0; i < q.na; i++) {
-        if (q.a[i] > t) {
-            const uint32_t ei = g.find(q.a[i]);
+    for (uint32_t i = 0; i < na; i++) if (a[i] == t) { found = 1; return GQ_OK; }
+    if (!na) return GQ_OK;
+    for (uint32_t i = 0; i < na; i++) {
+        if (a[i] > t) {
+            const uint32_t ei = g.find(a[i]);
             if (ei == g.n) return GQ_BAD_INPUT;
             if (t >= g.e[ei].shadow) { found = 1; return GQ_OK; }
         }
     }
     KHeap h{heap, 0};
-    for (uint32_t i = 0; i < q.na; i++) if (q.a[i] > t && !h.push(mkkey(q.a[i], 0))) return GQ_OVERFLOW;
+    for (uint32_t i = 0; i < na; i++) if (a[i] > t && !h.push(mkkey(a[i], 0))) return GQ_OVERFLOW;
     while (h.n) {
         const int32_t ord = k_lv(h.pop());
         const uint32_t ei = g.find(ord);
@@ -193,6 +194,74 @@ __device__ __forceinline__ uint32_t q_contains(const G &g, const GraphQuery &q, 
             if (p > t && !h.push(mkkey(p, 0))) return GQ_OVERFLOW;
         }
     }
+    return GQ_OK;
+}
+__device__ __forceinline__ uint32_t q_contains(const G &g, const GraphQuery &q, uint32_t *heap, uint32_t &found) {
+    return contains_version(g, q.a, q.na, q.target, heap, found);
+}
+
+// ---- find_dominators_2 (tools.rs:545-578) over find_dominators_full_internal (:588-647) ----------
+// The union's members in no other member's history, ascending.  a and b are sorted frontiers
+// (dominator sets, as the reference assumes).  The heap holds LV << 1, low bit 0 for an input
+// and 1 for a parent reached by the walk, so a walked LV pops before an input equal to it; the
+// walk stops once every input has popped or an entry's shadow covers the smallest input.
+__device__ __forceinline__ uint32_t q_dominators(const G &g, const GraphQuery &q, uint32_t *heap, int32_t *out,
+                                                 uint32_t &n_out) {
+    n_out = 0;
+    const int32_t *a = q.a, *b = q.b;
+    if (!q.na || !q.nb) {
+        const int32_t *s = q.na ? a : b;
+        const uint32_t n = q.na ? q.na : q.nb;
+        for (uint32_t i = 0; i < n; i++) out[n_out++] = s[i];
+        return GQ_OK;
+    }
+    for (uint32_t i = 0; i < q.na; i++) if (g.find(a[i]) == g.n) return GQ_BAD_INPUT;
+    for (uint32_t i = 0; i < q.nb; i++) if (g.find(b[i]) == g.n) return GQ_BAD_INPUT;
+    if (q.na == 1 && q.nb == 1) {   // version_cmp (tools.rs:67-85)
+        const int32_t x = a[0], y = b[0];
+        if (x == y) { out[n_out++] = y; return GQ_OK; }
+        const int32_t hi = x > y ? x : y, lo = x > y ? y : x;
+        uint32_t f = 0;
+        const uint32_t st = contains_version(g, &hi, 1, lo, heap, f);
+        if (st != GQ_OK) return st;
+        if (!f) out[n_out++] = lo;
+        out[n_out++] = hi;
+        return GQ_OK;
+    }
+    const int32_t first_v = a[0] < b[0] ? a[0] : b[0];
+    KHeap h{heap, 0};
+    for (uint32_t i = 0; i < q.na; i++) if (!h.push(uint32_t(a[i]) << 1)) return GQ_OVERFLOW;
+    for (uint32_t i = 0; i < q.nb; i++) if (!h.push(uint32_t(b[i]) << 1)) return GQ_OVERFLOW;
+    uint32_t remaining = q.na + q.nb;
+    int32_t last = -1;
+    int32_t rev[2 * GQ_MAX_FRONTIER];
+    uint32_t nr = 0;
+    while (h.n) {
+        const uint32_t ve = h.pop();
+        const int32_t v = int32_t(ve >> 1);
+        if (!(ve & 1u)) {   // an input: a dominator (nothing walked covers it)
+            rev[nr++] = v;
+            last = v;
+            remaining--;
+        }
+        const uint32_t ei = g.find(v);
+        if (ei == g.n) return GQ_BAD_INPUT;
+        const Ent e = g.e[ei];
+        if (e.shadow <= first_v) break;   // every input left lies in this entry's shadow
+        while (h.n && int32_t(h.top() >> 1) >= e.start) {   // inside this entry: covered
+            const uint32_t ve2 = h.pop();
+            if (!(ve2 & 1u)) {
+                if (last != int32_t(ve2 >> 1)) last = int32_t(ve2 >> 1);   // dominated (visit(v, false))
+                remaining--;
+            }
+        }
+        if (!remaining) break;
+        const uint32_t p1 = g.e[ei + 1].poff;
+        for (uint32_t k = e.poff; k < p1; k++)
+            if (!h.push((g.par[k] << 1) | 1u)) return GQ_OVERFLOW;
+    }
+    if (nr > GQ_MAX_FRONTIER) return GQ_OVERFLOW;
+    for (uint32_t i = 0; i < nr; i++) out[n_out++] = rev[nr - 1 - i];
     return GQ_OK;
 }
 
@@ -378,6 +447,10 @@ __global__ __launch_bounds__(64) void graph_query_kernel(GraphParams P) {
         uint32_t f = 0;
         st = q_contains(g, q, heap, f);
         r.n0 = f;
+    } else if (q.kind == GQ_DOMINATORS) {
+        uint32_t nd = 0;
+        st = q_dominators(g, q, heap, r.common, nd);
+        r.n_common = nd;
     } else {
         st = GQ_BAD_INPUT;
     }

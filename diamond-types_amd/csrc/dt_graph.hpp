@@ -5,7 +5,7 @@
 namespace dtgpu {
 
 constexpr uint32_t GQ_MAX_FRONTIER = 16;
-enum : uint32_t { GQ_DIFF = 0, GQ_CONFLICT = 1, GQ_CONTAINS = 2 };
+enum : uint32_t { GQ_DIFF = 0, GQ_CONFLICT = 1, GQ_CONTAINS = 2, GQ_DOMINATORS = 3 };
 enum : uint32_t { GQ_OK = 0, GQ_OVERFLOW = 1, GQ_BAD_INPUT = 2 };
 
 // Graph arena: per graph, n_ent + 1 quads (start, end, shadow, parents offset); the extra quad
@@ -18,7 +18,7 @@ struct GraphQuery {
 
 struct GraphResult {
     uint32_t status, n0, n1, n_common;   // DIFF: spans only-a / only-b; CONFLICT: spans; CONTAINS: n0 = 0/1
-    int32_t common[GQ_MAX_FRONTIER];
+    int32_t common[GQ_MAX_FRONTIER];     // CONFLICT: the common frontier; DOMINATORS: the result
 };
 
 struct GraphParams {

@@ -515,7 +515,11 @@ DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml,
         // with one store; only the new items get a block in pos[] (shifted ones stay put)
         const uint32_t shifted = shfl(it, l >= m ? l - m : l);
         it = l < s ? it : (l < s + m ? lv + (l - s) : shifted);
+#ifdef DTGPU_ROW_MASKED   // experiment: store only the slots the insert changed
+        if (l >= s && l < bc + m) items[l] = it;
+#else
         items[l] = it;   // the whole row: slots past the count are don't-care
+#endif
         if (l >= s && l < s + m) st(D.pc + it, pc_of(b, 1u));
         if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_R1] += t - tr; tr = t; }
         const u64 low = lanes_below(s);

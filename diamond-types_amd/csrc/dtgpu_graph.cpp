@@ -57,7 +57,7 @@ extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *h
         const dtgpu_graph_query &s = queries[i];
         GraphQuery &d = q[i];
         std::memset(&d, 0, sizeof d);
-        if (s.graph >= n_graphs || s.na > GQ_MAX_FRONTIER || s.nb > GQ_MAX_FRONTIER || s.kind > 2) return DTGPU_ERR_ARG;
+        if (s.graph >= n_graphs || s.na > GQ_MAX_FRONTIER || s.nb > GQ_MAX_FRONTIER || s.kind > 3) return DTGPU_ERR_ARG;
         d.kind = s.kind;
         d.ent_off = goff[s.graph];
         d.n_ent = gn[s.graph];
@@ -126,6 +126,9 @@ extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *h
             if (r.n0 > span_cap) { a.status = GQ_OVERFLOW; continue; }
             for (uint32_t k = 0; k < 3 * r.n0; k++) sp[k] = int32_t(o[k]);
             a.n_a = r.n0;
+            a.n_common = r.n_common;
+            for (uint32_t k = 0; k < r.n_common && k < GQ_MAX_FRONTIER; k++) a.common[k] = r.common[k];
+        } else if (q[i].kind == GQ_DOMINATORS) {
             a.n_common = r.n_common;
             for (uint32_t k = 0; k < r.n_common && k < GQ_MAX_FRONTIER; k++) a.common[k] = r.common[k];
         } else {

@@ -739,7 +739,7 @@ class DecodeBatch:
         return lib().dtgpu_decode_bytes(self._h, 1)
 
 
-GQ_KINDS = {"diff": 0, "conflict": 1, "contains": 2}
+GQ_KINDS = {"diff": 0, "conflict": 1, "contains": 2, "dominators": 3}
 DIFF_FLAGS = ["OnlyA", "OnlyB", "Shared"]
 
 
@@ -749,7 +749,8 @@ def graph_queries(graphs, queries, span_cap=512, timing=False):
     graphs: GraphEntrySimple lists ([{"span": [start, end], "parents": [...]}, ...]).
     queries: ("diff", g, a, b) -> (only_a, only_b) span lists, newest first (Graph::diff_rev);
              ("conflict", g, a, b) -> ([(start, end, flag)], common) (Graph::find_conflicting);
-             ("contains", g, frontier, target) -> bool (frontier_contains_version; -1 = ROOT).
+             ("contains", g, frontier, target) -> bool (frontier_contains_version; -1 = ROOT);
+             ("dominators", g, a, b) -> sorted list (find_dominators_2 of two dominator sets).
     A query the device could not answer yields ("error", status)."""
     hist, off = [], [0]
     for g in graphs:
@@ -787,6 +788,8 @@ def graph_queries(graphs, queries, span_cap=512, timing=False):
             out.append(([(s, e) for s, e, _ in tri[:r.n_a]], [(s, e) for s, e, _ in tri[r.n_a:]]))
         elif kind == "conflict":
             out.append(([(s, e, DIFF_FLAGS[f]) for s, e, f in tri[:r.n_a]], list(r.common[:r.n_common])))
+        elif kind == "dominators":
+            out.append(list(r.common[:r.n_common]))
         else:
             out.append(bool(r.n_a))
     return (out, ms.value) if timing else out

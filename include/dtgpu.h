@@ -350,11 +350,15 @@ size_t dtgpu_oplog_export(const dtgpu_oplog *oplog, int what, void *out, size_t 
  *                      flag 0 OnlyA / 1 OnlyB / 2 Shared, and the common frontier
  *   DTGPU_GQ_CONTAINS  Graph::frontier_contains_version (tools.rs:88-146): n_a = 1 if a contains
  *                      target (-1 = ROOT)
+ *   DTGPU_GQ_DOMINATORS Graph::find_dominators_2 (tools.rs:545-578; a, b sorted dominator sets):
+ *                      common[0, n_common) = the union's dominators, ascending (ListBranch::merge's
+ *                      end version); more than 16 is status 1
  * spans: span_cap (start, end, flag) triples per query.  answer.status: 0 ok, 1 capacity
  * (queue or span_cap), 2 bad input (a version outside the graph). */
 #define DTGPU_GQ_DIFF 0
 #define DTGPU_GQ_CONFLICT 1
 #define DTGPU_GQ_CONTAINS 2
+#define DTGPU_GQ_DOMINATORS 3
 typedef struct dtgpu_graph_query {
     uint32_t kind, graph, na, nb;   /* frontier sizes <= 16 */
     int64_t a[16], b[16];

@@ -1327,6 +1327,25 @@ EXPORT int dto_graph_contains(const Graph *g, const i64 *f, int n, i64 target) {
     if (target == ROOT_LV) return 1;   /* version_contains_time: ROOT is in every version */
     return frontier_contains_version(g, f, n, target);
 }
+/* Graph::find_dominators_2 / find_dominators (tools.rs:505-578) restated by its definition, not
+ * its heap walk: the members of a u b that are in the history of no other member, ascending.
+ * Returns the count; out holds them. */
+EXPORT int dto_graph_dominators(const Graph *g, const i64 *a, int na, const i64 *b, int nb, i64 *out) {
+    i64 u[128];
+    int n = 0;
+    for (int i = 0; i < na && n < 128; i++) u[n++] = a[i];
+    for (int i = 0; i < nb && n < 128; i++) u[n++] = b[i];
+    sort_frontier(u, n);
+    int m = 0;
+    for (int i = 0; i < n; i++) if (!m || u[m - 1] != u[i]) u[m++] = u[i];
+    int k = 0;
+    for (int i = 0; i < m; i++) {
+        int dominated = 0;
+        for (int j = i + 1; j < m && !dominated; j++) dominated = frontier_contains_version(g, &u[j], 1, u[i]);
+        if (!dominated) out[k++] = u[i];
+    }
+    return k;
+}
 typedef struct { i64 *spans; int n; } ConfCtx;
 static void conf_visit(void *ctx, i64 s, i64 e, int flag) {
     ConfCtx *c = ctx;   /* push_rev_rle of the test harness (tools.rs:745-752) */

@@ -81,6 +81,7 @@ def lib():
         L.dto_graph_diff.argtypes = [ctypes.c_void_p, P64, ctypes.c_int, P64, ctypes.c_int,
                                      P64, ctypes.POINTER(ctypes.c_int), P64, ctypes.POINTER(ctypes.c_int)]
         L.dto_graph_contains.argtypes = [ctypes.c_void_p, P64, ctypes.c_int, i64]
+        L.dto_graph_dominators.argtypes = [ctypes.c_void_p, P64, ctypes.c_int, P64, ctypes.c_int, P64]
         L.dto_graph_find_conflicting.argtypes = [ctypes.c_void_p, P64, ctypes.c_int, P64, ctypes.c_int,
                                                  P64, P64, ctypes.POINTER(ctypes.c_int)]
         _lib = L
@@ -303,6 +304,15 @@ class Graph:
     def contains(self, frontier, target):
         A, n = _arr(frontier)
         return bool(lib().dto_graph_contains(self.h, A, n, target))
+
+    def dominators(self, a, b=()):
+        """find_dominators_2(a, b) / find_dominators(a): the union's members not in another
+        member's history, ascending (dto_graph_dominators)."""
+        A, na = _arr(a)
+        B, nb = _arr(b)
+        out = (ctypes.c_int64 * max(1, na + nb))()
+        n = lib().dto_graph_dominators(self.h, A, na, B, nb, out)
+        return list(out[:n])
 
     def find_conflicting(self, a, b):
         A, na = _arr(a)

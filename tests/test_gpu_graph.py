@@ -85,3 +85,44 @@ def test_random_queries_vs_oracle(name):
             assert ans == og.contains(a, b), (a, b)
         checked += 1
     assert checked >= 0.95 * len(queries)
+
+
+FANCY = [{"span": [0, 3], "parents": []}, {"span": [3, 6], "parents": []},
+         {"span": [6, 9], "parents": [1, 4]}, {"span": [9, 11], "parents": [2, 8]}]
+# dominator_smoke_test (tools.rs:1030-1051)
+DOMINATOR_KATS = [([0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10], [5, 10]), ([10], [10]), ([5, 6], [5, 6]), ([5, 9], [5, 9]),
+                  ([4, 9], [9]), ([1, 2], [2]), ([0, 2], [2]), ([0, 10], [10]), ([], []), ([2], [2]),
+                  ([1, 4], [1, 4]), ([9, 10], [10]), ([2, 8, 9], [9]), ([2, 7, 9], [9]), ([6, 7], [7]), ([0], [0])]
+
+
+def test_dominator_kats_one_batch():
+    """find_dominators_2 on the device for every split of every dominator_smoke_test input into
+    two dominator sets, both orders (check_dominators, tools.rs:993-1028)."""
+    og = OracleGraph(FANCY)
+    queries, want = [], []
+    for inp, exp in DOMINATOR_KATS:
+        for k in range(len(inp) + 1):
+            a, b = og.dominators(inp[:k]), og.dominators(inp[k:])
+            queries += [("dominators", 0, a, b), ("dominators", 0, b, a)]
+            want += [exp, exp]
+    assert dt_amd.graph_queries([FANCY], queries) == want
+
+
+@pytest.mark.parametrize("name", G.DT_FILES)
+def test_random_dominators_vs_oracle_and_host(name):
+    """Device find_dominators_2 of random dominator-set pairs over the benchmark graphs against
+    the oracle's definition (no member in another's history) and the host engine's."""
+    hist, n = _hist_of(name)
+    og = OracleGraph(hist)
+    o = dt_amd.ListOpLog.load_from(G.dt_bytes(name))
+    rng = random.Random(77)
+    queries = []
+    for _ in range(400):
+        a = og.dominators(sorted(rng.sample(range(n), rng.choice([1, 1, 2, 3]))))
+        b = og.dominators(sorted(rng.sample(range(n), rng.choice([1, 1, 2, 3]))))
+        queries.append(("dominators", 0, a, b))
+    got = dt_amd.graph_queries([hist], queries)
+    for (_k, _g, a, b), ans in zip(queries, got):
+        want = og.dominators(a, b)
+        assert ans == want, (a, b)
+        assert o.dominators(a, b) == want, (a, b)

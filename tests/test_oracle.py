@@ -124,6 +124,26 @@ def test_fancy_graph_shadows():
     assert [e[2] for e in g.entries()] == [0, 3, 6, 6]
 
 
+
+FANCY = [{"span": [0, 3], "parents": []}, {"span": [3, 6], "parents": []},
+         {"span": [6, 9], "parents": [1, 4]}, {"span": [9, 11], "parents": [2, 8]}]
+# dominator_smoke_test (tools.rs:1030-1051): (input, expected dominators)
+DOMINATOR_KATS = [([0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10], [5, 10]), ([10], [10]), ([5, 6], [5, 6]), ([5, 9], [5, 9]),
+                  ([4, 9], [9]), ([1, 2], [2]), ([0, 2], [2]), ([0, 10], [10]), ([], []), ([2], [2]),
+                  ([1, 4], [1, 4]), ([9, 10], [10]), ([2, 8, 9], [9]), ([2, 7, 9], [9]), ([6, 7], [7]), ([0], [0])]
+
+
+@pytest.mark.parametrize("inp,want", DOMINATOR_KATS)
+def test_dominator_kats(inp, want):
+    """find_dominators of the input, and find_dominators_2 of every split of it into two
+    dominator sets, both orders (check_dominators, tools.rs:993-1028)."""
+    g = Graph(FANCY)
+    assert g.dominators(inp) == want
+    for k in range(len(inp) + 1):
+        a, b = g.dominators(inp[:k]), g.dominators(inp[k:])
+        assert g.dominators(a, b) == want and g.dominators(b, a) == want
+    assert g.dominators([1, 1, 1]) == [1]   # dominator_duplicates (tools.rs:1053-1064)
+
 # ---- 6. merge KATs (src/listmerge/merge.rs:1109-1325, src/list/branch.rs:166-193) ----------
 def test_ff_merge_kat():
     o = OpLog()
