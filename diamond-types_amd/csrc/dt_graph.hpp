@@ -5,7 +5,7 @@
 namespace dtgpu {
 
 constexpr uint32_t GQ_MAX_FRONTIER = 16;
-enum : uint32_t { GQ_DIFF = 0, GQ_CONFLICT = 1, GQ_CONTAINS = 2, GQ_DOMINATORS = 3 };
+enum : uint32_t { GQ_DIFF = 0, GQ_CONFLICT = 1, GQ_CONTAINS = 2, GQ_DOMINATORS = 3, GQ_DIFF_LEVEL = 4 };
 enum : uint32_t { GQ_OK = 0, GQ_OVERFLOW = 1, GQ_BAD_INPUT = 2 };
 
 // Graph arena: per graph, n_ent + 1 quads (start, end, shadow, parents offset); the extra quad
@@ -31,5 +31,22 @@ struct GraphParams {
 };
 
 int launch_graph_queries(const GraphParams &p, void *stream);
+
+// Level-synchronous kernels (dt_level.hip).  Per-entry arrays are indexed like the entry quads
+// (graph g's entry e at ent_off + e; every graph owns n_ent + 1 slots), per-slot arrays like
+// the parents array.
+constexpr uint32_t LVL_MAX_ENTRIES = 8192;   // per-entry state of one graph lives in LDS
+struct LevelGraph { uint32_t ent_off, n_ent; };
+struct LevelParams {
+    const uint32_t *ents, *par;   // the GraphParams arena
+    uint32_t *pent, *child;       // per parent slot: its parent's entry; children CSR (by parent entry)
+    uint32_t *level, *order;      // per entry: its level; the entries in level order
+    uint32_t *lvl_off;            // per graph: level L's entries are order[lvl_off[L], lvl_off[L + 1])
+    uint32_t *meta;               // per graph at 2 * ent_off: number of levels, status
+    const LevelGraph *graphs;
+    uint32_t n_graphs;
+};
+int launch_levels(const LevelParams &p, void *stream);
+int launch_level_diff(const LevelParams &p, const GraphParams &q, void *stream);
 
 }  // namespace dtgpu

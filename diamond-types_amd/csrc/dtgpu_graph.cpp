@@ -57,7 +57,7 @@ extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *h
         const dtgpu_graph_query &s = queries[i];
         GraphQuery &d = q[i];
         std::memset(&d, 0, sizeof d);
-        if (s.graph >= n_graphs || s.na > GQ_MAX_FRONTIER || s.nb > GQ_MAX_FRONTIER || s.kind > 3) return DTGPU_ERR_ARG;
+        if (s.graph >= n_graphs || s.na > GQ_MAX_FRONTIER || s.nb > GQ_MAX_FRONTIER || s.kind > 4) return DTGPU_ERR_ARG;
         d.kind = s.kind;
         d.ent_off = goff[s.graph];
         d.n_ent = gn[s.graph];
@@ -69,11 +69,20 @@ extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *h
         d.out_off = uint32_t(i) * out_cap;
         d.out_cap = out_cap;
     }
+    // graphs that level-synchronous diffs run on
+    std::vector<LevelGraph> lg;
+    {
+        std::vector<uint8_t> want(n_graphs, 0);
+        for (size_t i = 0; i < nq; i++) if (queries[i].kind == GQ_DIFF_LEVEL) want[queries[i].graph] = 1;
+        for (size_t g = 0; g < n_graphs; g++) if (want[g]) lg.push_back(LevelGraph{goff[g], gn[g]});
+    }
     hipStream_t st = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     DevBuf<uint32_t> d_ents, d_par, d_out;
     DevBuf<GraphQuery> d_q;
     DevBuf<GraphResult> d_r;
+    DevBuf<uint32_t> d_pent, d_child, d_level, d_order, d_loff, d_meta;
+    DevBuf<LevelGraph> d_lg;
     dtgpu_status rc = DTGPU_OK;
     std::vector<GraphResult> res(nq);
     std::vector<uint32_t> out(size_t(nq) * out_cap);
@@ -89,8 +98,22 @@ extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *h
         CK(d_out.alloc(out.size()));
         {
             GraphParams P{d_ents.p, d_par.p, d_out.p, d_q.p, d_r.p, uint32_t(nq)};
+            LevelParams LP{};
+            if (!lg.empty()) {
+                const size_t nquad = ents.size() / 4;
+                CK(d_pent.alloc(par.size()));
+                CK(d_child.alloc(par.size()));
+                CK(d_level.alloc(nquad));
+                CK(d_order.alloc(nquad));
+                CK(d_loff.alloc(nquad));
+                CK(d_meta.alloc(2 * nquad));
+                CK(d_lg.upload(lg, st));
+                LP = LevelParams{d_ents.p, d_par.p, d_pent.p, d_child.p, d_level.p, d_order.p, d_loff.p, d_meta.p,
+                                 d_lg.p, uint32_t(lg.size())};
+            }
             CK(hipEventRecord(e0, st));
             if (launch_graph_queries(P, st)) { rc = DTGPU_ERR_HIP; goto done; }
+            if (!lg.empty() && (launch_levels(LP, st) || launch_level_diff(LP, P, st))) { rc = DTGPU_ERR_HIP; goto done; }
             CK(hipEventRecord(e1, st));
         }
         if (nq) {
@@ -112,7 +135,7 @@ extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *h
         a.status = r.status;
         const uint32_t *o = out.data() + size_t(i) * out_cap;
         int64_t *sp = spans ? spans + i * span_cap * 3 : nullptr;
-        if (q[i].kind == GQ_DIFF) {
+        if (q[i].kind == GQ_DIFF || q[i].kind == GQ_DIFF_LEVEL) {
             if (r.n0 + r.n1 > span_cap) { a.status = GQ_OVERFLOW; continue; }
             for (uint32_t k = 0; k < r.n0; k++) { sp[3 * k] = int32_t(o[2 * k]); sp[3 * k + 1] = int32_t(o[2 * k + 1]); sp[3 * k + 2] = 0; }
             const uint32_t *ob = o + 2 * (out_cap / 4);

@@ -739,7 +739,7 @@ class DecodeBatch:
         return lib().dtgpu_decode_bytes(self._h, 1)
 
 
-GQ_KINDS = {"diff": 0, "conflict": 1, "contains": 2, "dominators": 3}
+GQ_KINDS = {"diff": 0, "conflict": 1, "contains": 2, "dominators": 3, "diff_level": 4}
 DIFF_FLAGS = ["OnlyA", "OnlyB", "Shared"]
 
 
@@ -750,7 +750,8 @@ def graph_queries(graphs, queries, span_cap=512, timing=False):
     queries: ("diff", g, a, b) -> (only_a, only_b) span lists, newest first (Graph::diff_rev);
              ("conflict", g, a, b) -> ([(start, end, flag)], common) (Graph::find_conflicting);
              ("contains", g, frontier, target) -> bool (frontier_contains_version; -1 = ROOT);
-             ("dominators", g, a, b) -> sorted list (find_dominators_2 of two dominator sets).
+             ("dominators", g, a, b) -> sorted list (find_dominators_2 of two dominator sets);
+             ("diff_level", g, a, b) -> as "diff", by level-synchronous propagation (dt_level.hip).
     A query the device could not answer yields ("error", status)."""
     hist, off = [], [0]
     for g in graphs:
@@ -784,7 +785,7 @@ def graph_queries(graphs, queries, span_cap=512, timing=False):
             continue
         base = 3 * span_cap * i
         tri = [(spans[base + 3 * k], spans[base + 3 * k + 1], spans[base + 3 * k + 2]) for k in range(r.n_a + r.n_b)]
-        if kind == "diff":
+        if kind in ("diff", "diff_level"):
             out.append(([(s, e) for s, e, _ in tri[:r.n_a]], [(s, e) for s, e, _ in tri[r.n_a:]]))
         elif kind == "conflict":
             out.append(([(s, e, DIFF_FLAGS[f]) for s, e, f in tri[:r.n_a]], list(r.common[:r.n_common])))

@@ -353,12 +353,17 @@ size_t dtgpu_oplog_export(const dtgpu_oplog *oplog, int what, void *out, size_t 
  *   DTGPU_GQ_DOMINATORS Graph::find_dominators_2 (tools.rs:545-578; a, b sorted dominator sets):
  *                      common[0, n_common) = the union's dominators, ascending (ListBranch::merge's
  *                      end version); more than 16 is status 1
+ *   DTGPU_GQ_DIFF_LEVEL Graph::diff as DTGPU_GQ_DIFF, computed level-synchronously: the graph's
+ *                      entries are levelled (Kahn, one level per round) and the two versions'
+ *                      marks propagate down the levels over the CSR parent arrays (dt_level.hip);
+ *                      graphs up to 8192 entries
  * spans: span_cap (start, end, flag) triples per query.  answer.status: 0 ok, 1 capacity
  * (queue or span_cap), 2 bad input (a version outside the graph). */
 #define DTGPU_GQ_DIFF 0
 #define DTGPU_GQ_CONFLICT 1
 #define DTGPU_GQ_CONTAINS 2
 #define DTGPU_GQ_DOMINATORS 3
+#define DTGPU_GQ_DIFF_LEVEL 4
 typedef struct dtgpu_graph_query {
     uint32_t kind, graph, na, nb;   /* frontier sizes <= 16 */
     int64_t a[16], b[16];

@@ -126,3 +126,36 @@ def test_random_dominators_vs_oracle_and_host(name):
         want = og.dominators(a, b)
         assert ans == want, (a, b)
         assert o.dominators(a, b) == want, (a, b)
+
+
+def test_level_synchronous_diff_fixtures():
+    """Graph::diff by level-synchronous propagation (dt_level.hip) on every diff.json fixture."""
+    graphs, queries, cases = [], [], []
+    for case in G.cg_fixture("diff"):
+        graphs.append(case["hist"])
+        queries.append(("diff_level", len(graphs) - 1, case["a"], case["b"]))
+        cases.append(case)
+    for case, ans in zip(cases, dt_amd.graph_queries(graphs, queries)):
+        assert ans == (_ranges(case["expect_a"]), _ranges(case["expect_b"])), case
+
+
+@pytest.mark.parametrize("name", G.DT_FILES)
+def test_level_synchronous_diff_vs_heap_walk_and_oracle(name):
+    """The level sweep and the heap walk give the same span lists on random version pairs of the
+    benchmark graphs (one batch holding both kinds), and both equal the oracle's diff."""
+    hist, n = _hist_of(name)
+    og = OracleGraph(hist)
+    rng = random.Random(4321)
+    pairs = []
+    for _ in range(150):
+        a = og.dominators(sorted(rng.sample(range(n), rng.choice([1, 1, 2]))))
+        b = og.dominators(sorted(rng.sample(range(n), rng.choice([1, 1, 2]))))
+        pairs.append((a, b))
+    queries = [("diff_level", 0, a, b) for a, b in pairs] + [("diff", 0, a, b) for a, b in pairs]
+    got = dt_amd.graph_queries([hist], queries, span_cap=4096)
+    lev, heap = got[:len(pairs)], got[len(pairs):]
+    for (a, b), x, y in zip(pairs, lev, heap):
+        oa, ob = og.diff(a, b)
+        assert x == (list(reversed(oa)), list(reversed(ob))), (a, b)
+        if not (isinstance(y, tuple) and y and y[0] == "error"):
+            assert x == y, (a, b)
