@@ -284,7 +284,8 @@ DEV bool find_vis(Doc &D, uint32_t p, Found &f) {
     uint32_t base = 0, S = NONE;
     for (uint32_t c = 0; c < D.nsb; c += 64) {
         const uint32_t i = c + l;
-        const uint32_t w = i < D.nsb ? ix<L>(D.top + i) : 0;
+        const uint32_t w0 = ix<L>(D.top + min(i, D.nsb - 1));   // clamped, then masked: no exec branch
+        const uint32_t w = i < D.nsb ? w0 : 0;
         const uint32_t v = w & 0xFFFFu;
         const uint32_t inc = wave_scan(v);
         const u64 m = __ballot(base + inc > p);
@@ -300,8 +301,10 @@ DEV bool find_vis(Doc &D, uint32_t p, Found &f) {
     if (S == NONE) return false;
     f.S = S;
     const uint32_t n = U(ix<L>(D.sbn + S));
-    const uint32_t b = l < n ? ix16<L>(D.sbl + size_t(S) * SBC + l) : 0;
-    const uint32_t v = l < n ? c_vis(ix<L>(D.cnt + b)) : 0;
+    const uint32_t b0 = ix16<L>(D.sbl + size_t(S) * SBC + l);   // a list row holds SBC slots
+    const uint32_t b = l < n ? b0 : 0;
+    const uint32_t v0 = c_vis(ix<L>(D.cnt + b));
+    const uint32_t v = l < n ? v0 : 0;
     const uint32_t inc = wave_scan(v);
     const u64 m = __ballot(base + inc > p);
     if (!m) return false;
@@ -328,19 +331,24 @@ DEV uint32_t next_live_block(Doc &D, uint32_t b) {
     uint32_t S = o >> 6;
     {   // rest of b's superblock
         const uint32_t n = U(ix<L>(D.sbn + S)), i0 = (o & 63u) + 1;
-        const uint32_t bl = l < n ? ix16<L>(D.sbl + size_t(S) * SBC + l) : 0;
-        const u64 m = __ballot(l >= i0 && l < n && c_live(ix<L>(D.cnt + bl)) != 0);
+        const uint32_t b0 = ix16<L>(D.sbl + size_t(S) * SBC + l);
+        const uint32_t bl = l < n ? b0 : 0;
+        const uint32_t cl = c_live(ix<L>(D.cnt + bl));
+        const u64 m = __ballot(l >= i0 && l < n && cl != 0);
         if (m) return U(bcast(bl, first_lane(m)));
     }
     for (uint32_t p = U(ix<L>(D.sbpos + S)) + 1; p < D.nsb; p += 64) {
         if (!charge(D)) return NONE;
         const uint32_t i = p + l;
-        const u64 m = __ballot(i < D.nsb && ix<L>(D.tlive + i) != 0);
+        const uint32_t tl = ix<L>(D.tlive + min(i, D.nsb - 1));
+        const u64 m = __ballot(i < D.nsb && tl != 0);
         if (m) {
             S = U(ix<L>(D.top + p + first_lane(m)) >> 16);
             const uint32_t n = U(ix<L>(D.sbn + S));
-            const uint32_t bl = l < n ? ix16<L>(D.sbl + size_t(S) * SBC + l) : 0;
-            const u64 m2 = __ballot(l < n && c_live(ix<L>(D.cnt + bl)) != 0);
+            const uint32_t b0 = ix16<L>(D.sbl + size_t(S) * SBC + l);
+            const uint32_t bl = l < n ? b0 : 0;
+            const uint32_t cl = c_live(ix<L>(D.cnt + bl));
+            const u64 m2 = __ballot(l < n && cl != 0);
             if (!m2) { fail(D, ErrCheckout, 19); return NONE; }
             return U(bcast(bl, first_lane(m2)));
         }
@@ -526,7 +534,7 @@ DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml,
         const u64 ins = lanes_below(m) << s;
         mv = m == 64 ? ins : ((mv & low) | ((mv & ~low) << m) | ins);
         ml = m == 64 ? ins : ((ml & low) | ((ml & ~low) << m) | ins);
-        if (l < 2) st(D.m2 + 2 * size_t(b) + l, l == 0 ? mv : ml);
+        st(D.m2 + 2 * size_t(b) + (l & 1u), (l & 1u) ? ml : mv);   // every lane: no exec branch
         if (XF) {
             u64 mu = U64(ld(D.mup + b));
             mu = m == 64 ? ins : ((mu & low) | ((mu & ~low) << m) | ins);
@@ -547,9 +555,9 @@ DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml,
     }
     D.cb = b; D.cit = it; D.cmv = mv; D.cml = ml;   // block state after the run
     const uint64_t t3 = tick<PROF>();
-    for (uint32_t j = l; j < k0; j += 64) {
-        const uint32_t nit = lv0 + j;
-        D.ao[nit] = u64(j == 0 ? ol : nit - 1) | (u64(orr) << 32);
+    for (uint32_t j0 = 0; j0 < k0; j0 += 64) {   // wave-uniform loop, masked store
+        const uint32_t j = j0 + l, nit = lv0 + j;
+        if (j < k0) D.ao[nit] = u64(j == 0 ? ol : nit - 1) | (u64(orr) << 32);
     }
     if (PROF) D.prof[P_R3] += tick<PROF>() - t3;
 }
@@ -654,17 +662,17 @@ template <bool L>
 DEV void load_block(Doc &D, uint32_t b, uint32_t c, uint32_t &it, u64 &mv, u64 &ml) {
     const uint32_t l = lane_id();
     const uint32_t bc = c_items(c);
-    it = l < bc ? D.items[size_t(b) * BLK + l] : 0;
+    const uint32_t it0 = D.items[size_t(b) * BLK + l];   // the row holds BLK slots
+    it = l < bc ? it0 : 0;
     if (c & C_DIRTY) {
-        const uint32_t k = l < bc ? pc_cnt(ld(D.pc + it)) : 0u;
+        const uint32_t k = pc_cnt(ld(D.pc + it));   // lanes past the count read item 0's word
         mv = __ballot(l < bc && k == 1u);
         ml = __ballot(l < bc && k != 0u);
-        if (l < 2) st(D.m2 + 2 * size_t(b) + l, l == 0 ? mv : ml);
+        st(D.m2 + 2 * size_t(b) + (l & 1u), (l & 1u) ? ml : mv);
         if (l == 0) D.cnt[b] = c & ~C_DIRTY;
         wave_fence();
     } else {
-        u64 x = 0;
-        if (l < 2) x = ld(D.m2 + 2 * size_t(b) + l);
+        const u64 x = ld(D.m2 + 2 * size_t(b) + (l & 1u));
         mv = bcast64(x, 0);
         ml = bcast64(x, 1);
     }
@@ -825,18 +833,20 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
     // read-only here, so chunk j + 1's entries and targets are fetched while chunk j's counts
     // are read and written; the counts themselves are read only after the previous chunk's
     // stores (same-address order within the wave), so a later chunk sees earlier updates.
+    // (loads are issued by every lane at clamped addresses and masked after: no exec branches;
+    // a lane with no delete target reads ao[0], one line for the whole wave)
     auto resolve = [&](uint32_t j, uint32_t e, uint32_t &item, bool &del, bool &bad) {
-        item = 0; del = false; bad = false;
-        if (j + l < n) {
-            const uint32_t lv = e & 0x3FFFFFFFu;
-            del = (e >> 30) & 1u;
-            item = lv;
-            if (lv >= D.n_lv) bad = true;
-            else if (del) item = *reinterpret_cast<const uint32_t *>(D.ao + lv);
-        }
+        const bool valid = j + l < n;
+        const uint32_t lv = e & 0x3FFFFFFFu;
+        bad = valid && lv >= D.n_lv;
+        del = valid && !bad && ((e >> 30) & 1u);
+        const uint32_t tgt = *reinterpret_cast<const uint32_t *>(D.ao + (del ? lv : 0u));
+        item = valid ? (del ? tgt : lv) : 0u;
     };
-    uint32_t e_cur = have_pre ? pre : (l < n ? D.tlist[off + l] : 0u);
-    uint32_t e_nx = 64 + l < n ? D.tlist[off + 64 + l] : 0u;
+    if (n == 0) return;
+    const uint32_t last = off + n - 1;
+    uint32_t e_cur = have_pre ? pre : D.tlist[min(off + l, last)];
+    uint32_t e_nx = D.tlist[min(off + 64 + l, last)];
     uint32_t it_cur;
     bool del_cur, bad_cur;
     resolve(0, e_cur, it_cur, del_cur, bad_cur);
@@ -856,7 +866,7 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
         if (j + 64 < n) {
             e_cur = e_nx;
             resolve(j + 64, e_cur, it_cur, del_cur, bad_cur);
-            e_nx = j + 128 + l < n ? D.tlist[off + j + 128 + l] : 0u;
+            e_nx = D.tlist[min(off + j + 128 + l, last)];
         }
         if (__ballot(bad)) { fail(D, ErrCheckout, 16); return; }
         if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_T1] += t - tq; tq = t; }
@@ -896,20 +906,18 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
         bool fv = false, fl = false;
         uint32_t b = 0;
         int32_t dv = 0, dl = 0;
-        if (act) {
-            const uint32_t w = ld(D.pc + item);
-            b = pc_blk(w);
-            const uint32_t oc = pc_cnt(w);
-            const uint32_t nc = oc + uint32_t(d);
-            if (int32_t(oc) + dneg < 0 || int32_t(oc) + d > 0xFFFF || b >= D.nb) {
-                bad = true;
-            } else {
-                st(D.pc + item, pc_of(b, nc));
-                fv = (oc == 1) != (nc == 1);
-                fl = (oc != 0) != (nc != 0);
-                dv = fv ? (nc == 1 ? 1 : -1) : 0;
-                dl = fl ? (nc != 0 ? 1 : -1) : 0;
-            }
+        {   // every lane loads (inactive ones item 0's word); only the store is masked
+            const uint32_t w = ld(D.pc + (act ? item : 0u));
+            const uint32_t bw = pc_blk(w), oc = pc_cnt(w), nc = oc + uint32_t(d);
+            const bool badc = act && (int32_t(oc) + dneg < 0 || int32_t(oc) + d > 0xFFFF || bw >= D.nb);
+            const bool ok = act && !badc;
+            bad = bad || badc;
+            if (ok) st(D.pc + item, pc_of(bw, nc));
+            b = ok ? bw : 0u;
+            fv = ok && ((oc == 1) != (nc == 1));
+            fl = ok && ((oc != 0) != (nc != 0));
+            dv = fv ? (nc == 1 ? 1 : -1) : 0;
+            dl = fl ? (nc != 0 ? 1 : -1) : 0;
         }
         if (__ballot(bad)) { fail(D, ErrCheckout, 16); return; }
         const bool flip = fv || fl;
@@ -960,20 +968,25 @@ DEV void materialise(Doc &D, uint8_t *out, uint32_t cap, uint32_t &len_out, u64 
         const uint32_t n = U(ix<L>(D.sbn + S));
         for (uint32_t i = 0; i < n; i += G) {
             // lane g < G fetches block g's id and item count
-            const uint32_t bl = l < G && i + l < n ? ix16<L>(D.sbl + size_t(S) * SBC + i + l) : 0;
-            const uint32_t nl = l < G && i + l < n ? c_items(ix<L>(D.cnt + bl)) : 0;
+            const bool gl = l < G && i + l < n;
+            const uint32_t b0 = ix16<L>(D.sbl + size_t(S) * SBC + min(i + (l & (G - 1)), SBC - 1));
+            const uint32_t bl = gl ? b0 : 0;
+            const uint32_t n0 = c_items(ix<L>(D.cnt + bl));
+            const uint32_t nl = gl ? n0 : 0;
             uint32_t it[G], cb[G], k[G];
             bool vis[G];
 #pragma unroll
             for (uint32_t g = 0; g < G; g++) {
                 const uint32_t b = bcast(bl, g);
                 vis[g] = l < bcast(nl, g);
-                it[g] = vis[g] ? D.items[size_t(b) * BLK + l] : 0;
+                const uint32_t i0 = D.items[size_t(b) * BLK + l];   // the row holds BLK slots
+                it[g] = vis[g] ? i0 : 0;
             }
 #pragma unroll
             for (uint32_t g = 0; g < G; g++) {
-                k[g] = vis[g] ? pc_cnt(ld(D.pc + it[g])) : 0;
-                cb[g] = vis[g] ? D.cbyte[it[g]] : 0;
+                const uint32_t w = ld(D.pc + it[g]), c = D.cbyte[it[g]];   // it = 0 past the count
+                k[g] = vis[g] ? pc_cnt(w) : 0;
+                cb[g] = vis[g] ? c : 0;
             }
 #pragma unroll
             for (uint32_t g = 0; g < G; g++) vis[g] = vis[g] && k[g] == 1u;
@@ -1107,7 +1120,7 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
     for (uint32_t base = 0; base < D.ncmd && !D.err; base += 64) {
         const uint32_t n_here = min(64u, D.ncmd - base);
         Cmd pre = {0, 0, 0, 0};
-        if (l < n_here) pre = D.cmds[base + l];
+        pre = D.cmds[min(base + l, D.ncmd - 1)];   // lanes past n_here are never read
         for (uint32_t j = 0; j < n_here && !D.err; j++) {
             D.ci = base + j;
             const uint32_t op = U(bcast(pre.op, j)), a = U(bcast(pre.lv, j)), n = U(bcast(pre.len, j)),
@@ -1117,7 +1130,7 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
             bool nx_ok = false;
             if (j + 1 < n_here && (U(bcast(pre.op, j + 1)) & 15u) == CMD_TOG) {
                 const uint32_t o2 = U(bcast(pre.lv, j + 1)), n2 = U(bcast(pre.len, j + 1));
-                if (l < n2) nx_pf = D.tlist[o2 + l];
+                if (n2) nx_pf = D.tlist[o2 + min(l, n2 - 1)];
                 nx_ok = true;
             }
             const uint64_t t0 = tick<PROF>();
