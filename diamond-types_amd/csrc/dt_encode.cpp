@@ -4,17 +4,18 @@
 // The history is written in the reference's order, Graph::optimized_txns_between(from, tip)
 // (a SpanningTreeWalker over the new spans, txn_trace.rs:356-360), through the same run mergers
 // the reference uses, so the output is byte-identical to the reference encoder's whenever the
-// content is not LZ4-compressed (content shorter than 20 bytes, or compression off):
+// same options are set (EncodeOptions, encode_oplog.rs:88-130):
 //   agent assignment  AgentAssignmentRun (agent, seq jump, len), merged on same agent + no jump
 //                     (encode_oplog.rs:142-189)
 //   ops               ListOpMetrics runs merged by can_append_ops / append_ops
 //                     (op_metrics.rs:235-293), written by write_op (encode_oplog.rs:20-92)
 //   parents           GraphEntrySimple runs (graph/mod.rs:239-254): local parents as output-order
 //                     deltas, foreign parents as (mapped agent, seq) (encode_oplog.rs:476-541)
-//   content           PatchContent: Content + ContentIsKnown bit runs (encode_oplog.rs:347-399)
+//   content           PatchContent: Content + ContentIsKnown bit runs (encode_oplog.rs:347-399);
+//                     with compress_content, every content field of >= 20 bytes goes into one
+//                     LZ4 block written first as CompressedFieldsLZ4 (encode_oplog.rs:270-343,
+//                     661-677), start-branch content before inserted content (:606-660)
 //   CRC-32C           over everything before the CRC chunk (encode_oplog.rs:731-734)
-// LZ4 compression (lz4_flex) is not reproduced: the encoder writes content uncompressed, which
-// every reader accepts (decode_oplog.rs reads Content and ContentCompressed alike).
 #include "dt_host.hpp"
 
 #include <algorithm>
@@ -36,7 +37,8 @@ void chunk(std::vector<uint8_t> &o, uint32_t type, const std::vector<uint8_t> &d
     o.insert(o.end(), data.begin(), data.end());
 }
 enum : uint32_t {
-    C_FileInfo = 1, C_DocId = 2, C_AgentNames = 3, C_StartBranch = 10, C_Version = 12, C_Content = 13,
+    C_FileInfo = 1, C_DocId = 2, C_AgentNames = 3, C_CompressedFieldsLZ4 = 5, C_StartBranch = 10, C_Version = 12,
+    C_Content = 13, C_ContentCompressed = 14,
     C_Patches = 20, C_OpVersions = 21, C_OpTypeAndPosition = 22, C_OpParents = 23, C_PatchContent = 24,
     C_ContentIsKnown = 25, C_Crc = 100,
 };
@@ -128,8 +130,75 @@ void write_version(std::vector<uint8_t> &dest, const std::vector<uint64_t> &v, A
 
 }  // namespace
 
+// lz4_flex 0.10 block compressor (`lz4_flex::compress_into`, called at encode_oplog.rs:326).
+// lz4_flex is a third-party crate absent from the reference tree; this restates its published
+// greedy parse, and the parameters below are pinned by the reference's own files: the LZ4 blocks
+// inside friendsforever.dt (U16 table), git-makefile.dt and node_nodecc.dt (U32 table) are
+// reproduced byte for byte from their decompressed content (tests/test_encoder.py).
+//   * inputs < 65,535 B: 8,192-entry table of u16 positions, hash = (u32 LE * 2654435761) >> 19;
+//     larger inputs: 4,096-entry table, hash = ((u64 LE << 24) * 889523592379) >> 52;
+//   * position 0 is hashed first and the search starts at 1; positions past len - 12 (MFLIMIT)
+//     are never searched; a search run of k misses steps by 1 + (k >> 5) bytes;
+//   * a candidate is taken when its first four bytes equal the current ones and it lies within
+//     65,535 bytes; the match is extended backwards over the pending literals, forwards up to
+//     len - 6, and position (match end - 2) is hashed;
+//   * sequences are token (literal length, match length - 4), 255-run length extensions, the
+//     literals, the 16-bit LE offset; the tail is one literal-only sequence.
+void lz4_block_compress(const uint8_t *in, size_t n, std::vector<uint8_t> &out) {
+    auto u32at = [&](size_t p) { uint32_t v; std::memcpy(&v, in + p, 4); return v; };
+    auto ext = [&](size_t v) {
+        while (v >= 255) { out.push_back(255); v -= 255; }
+        out.push_back(uint8_t(v));
+    };
+    auto emit = [&](size_t l0, size_t l1, size_t off, size_t mlen) {
+        const size_t ll = l1 - l0;
+        out.push_back(uint8_t((std::min<size_t>(ll, 15) << 4) | (off ? std::min<size_t>(mlen - 4, 15) : 0)));
+        if (ll >= 15) ext(ll - 15);
+        out.insert(out.end(), in + l0, in + l1);
+        if (!off) return;
+        out.push_back(uint8_t(off));
+        out.push_back(uint8_t(off >> 8));
+        if (mlen - 4 >= 15) ext(mlen - 4 - 15);
+    };
+    if (n < 13) { emit(0, n, 0, 0); return; }
+    const bool small = n < 65535;
+    std::vector<uint32_t> table(small ? 8192 : 4096, 0);
+    auto hash = [&](size_t p) -> size_t {
+        if (small) return size_t((u32at(p) * 2654435761u) >> 19);
+        uint64_t v;
+        std::memcpy(&v, in + p, 8);
+        return size_t(((v << 24) * 889523592379ull) >> 52);
+    };
+    const size_t end_check = n - 12, match_lim = n - 6;
+    size_t lit = 0, cur = 1;
+    table[hash(0)] = 0;
+    for (;;) {
+        size_t cand, nmc = 32, next = cur;
+        for (;;) {
+            const size_t step = nmc >> 5;
+            nmc++;
+            cur = next;
+            next += step;
+            if (cur > end_check) { emit(lit, n, 0, 0); return; }
+            const size_t h = hash(cur);
+            cand = table[h];
+            table[h] = uint32_t(cur);
+            if (cur - cand > 65535) continue;
+            if (u32at(cand) == u32at(cur)) break;
+        }
+        while (cur > lit && cand > 0 && in[cur - 1] == in[cand - 1]) { cur--; cand--; }
+        const size_t m0 = cur, off = cur - cand;
+        cur += 4;
+        cand += 4;
+        while (cur < match_lim && in[cur] == in[cand]) { cur++; cand++; }
+        table[hash(cur - 2)] = uint32_t(cur - 2);
+        emit(lit, m0, off, cur - m0);
+        lit = cur;
+    }
+}
+
 Status encode_dt(const HostOpLog &o, const std::vector<uint64_t> &from, bool store_inserted_content,
-                 bool store_start_branch_content, std::vector<uint8_t> &result) {
+                 bool compress_content, const std::vector<uint8_t> *start_content, std::vector<uint8_t> &result) {
     result.clear();
     for (uint64_t v : from) if (v >= o.n_lv) return ErrArg;
     AgentMap am(o);
@@ -267,11 +336,27 @@ Status encode_dt(const HostOpLog &o, const std::vector<uint64_t> &from, bool sto
     if (tx_have) tx_write();
     if (kr_have) leb(known_out, mix(kr_len, kr_val));
 
-    // ---- start branch (encode_oplog.rs:606-618) ----
+    // ---- content fields: write_content (encode_oplog.rs:270-305).  A field of >= 20 bytes goes
+    // into the shared LZ4 buffer when compressing (ContentCompressed holds its length in situ).
+    std::vector<uint8_t> lz;
+    auto write_content = [&](std::vector<uint8_t> &dest, const uint8_t *b, size_t n) {
+        std::vector<uint8_t> buf;
+        leb(buf, PLAIN_TEXT);
+        if (compress_content && n >= 20) {
+            leb(buf, n);
+            lz.insert(lz.end(), b, b + n);
+            chunk(dest, C_ContentCompressed, buf);
+        } else {
+            buf.insert(buf.end(), b, b + n);
+            chunk(dest, C_Content, buf);
+        }
+    };
+    // ---- start branch (encode_oplog.rs:606-618): the version, then the checkout at `from`
+    // (the caller runs it on the device) when store_start_branch_content ----
     std::vector<uint8_t> start_branch;
     if (!from.empty()) {
         write_version(start_branch, from, am, o);
-        if (store_start_branch_content) return ErrArg;   // needs the checkout at `from` (GPU); not offered here
+        if (start_content) write_content(start_branch, start_content->data(), start_content->size());
     }
     // ---- file info ----
     std::vector<uint8_t> fileinfo;
@@ -284,12 +369,10 @@ Status encode_dt(const HostOpLog &o, const std::vector<uint64_t> &from, bool sto
     chunk(fileinfo, C_AgentNames, am.names);
     // ---- patches ----
     std::vector<uint8_t> patches;
-    if (store_inserted_content && !ins_text.empty()) {
-        std::vector<uint8_t> pc, content;
+    if (store_inserted_content && !ins_text.empty()) {   // ContentChunk::flush (encode_oplog.rs:381-398)
+        std::vector<uint8_t> pc;
         leb(pc, 0);   // Ins
-        leb(content, PLAIN_TEXT);
-        content.insert(content.end(), ins_text.begin(), ins_text.end());
-        chunk(pc, C_Content, content);
+        write_content(pc, ins_text.data(), ins_text.size());
         chunk(pc, C_ContentIsKnown, known_out);
         chunk(patches, C_PatchContent, pc);
     }
@@ -299,6 +382,12 @@ Status encode_dt(const HostOpLog &o, const std::vector<uint64_t> &from, bool sto
     static const uint8_t magic[8] = {'D', 'M', 'N', 'D', 'T', 'Y', 'P', 'S'};
     result.assign(magic, magic + 8);
     leb(result, 0);   // PROTOCOL_VERSION
+    if (!lz.empty()) {   // write_compressed_chunk (encode_oplog.rs:320-343), the first chunk
+        std::vector<uint8_t> c;
+        leb(c, lz.size());
+        lz4_block_compress(lz.data(), lz.size(), c);
+        chunk(result, C_CompressedFieldsLZ4, c);
+    }
     chunk(result, C_FileInfo, fileinfo);
     chunk(result, C_StartBranch, start_branch);
     chunk(result, C_Patches, patches);

@@ -80,9 +80,13 @@ Status decode_dt(const uint8_t *data, size_t len, bool ignore_crc, HostOpLog &ou
 Status decode_and_add(const uint8_t *data, size_t len, bool ignore_crc, HostOpLog &o,
                       std::vector<uint64_t> &file_frontier);
 uint32_t crc32c(const uint8_t *d, size_t n);
-// ListOpLog::encode_from (src/list/encoding/encode_oplog.rs:404-747), content uncompressed.
+// ListOpLog::encode_from (src/list/encoding/encode_oplog.rs:404-747).  compress_content: LZ4 for
+// content fields of >= 20 bytes; start_content: the StartBranch content (the checkout at `from`,
+// store_start_branch_content) or null.
 Status encode_dt(const HostOpLog &o, const std::vector<uint64_t> &from, bool store_inserted_content,
-                 bool store_start_branch_content, std::vector<uint8_t> &result);
+                 bool compress_content, const std::vector<uint8_t> *start_content, std::vector<uint8_t> &result);
+// lz4_flex::compress_into (lz4_flex 0.10 block format, no length prefix)
+void lz4_block_compress(const uint8_t *in, size_t n, std::vector<uint8_t> &out);
 bool lz4_block_decompress(const uint8_t *src, size_t n, uint8_t *dst, size_t out_len);
 bool utf8_valid(const uint8_t *s, size_t n);
 inline uint32_t utf8_len(uint8_t c) { return c < 0x80 ? 1 : (c & 0xE0) == 0xC0 ? 2 : (c & 0xF0) == 0xE0 ? 3 : 4; }

@@ -830,18 +830,38 @@ size_t dtgpu_oplog_plan_commands(const dtgpu_oplog *h, uint32_t *cmds, size_t ca
 dtgpu_status dtgpu_oplog_encode(const dtgpu_oplog *h, const uint64_t *from, size_t n_from, uint32_t flags, uint8_t *out,
                                 size_t cap, size_t *out_len) {
     if (!h || (n_from && !from)) return DTGPU_ERR_ARG;
-    if (flags & ~uint32_t(DTGPU_ENCODE_STORE_INSERTED_CONTENT)) return DTGPU_ERR_ARG;   // see dtgpu.h
+    if (flags & ~uint32_t(DTGPU_ENCODE_FULL)) return DTGPU_ERR_ARG;   // see dtgpu.h
     std::vector<uint64_t> f(n_from + 1);
     const int64_t nf = dtgpu_oplog_dominators(h, from, n_from, nullptr, 0, f.data(), f.size());
     if (nf < 0) return DTGPU_ERR_ARG;
     f.resize(size_t(nf));
-    std::vector<uint8_t> bytes;
-    const Status st = encode_dt(h->o, f, (flags & DTGPU_ENCODE_STORE_INSERTED_CONTENT) != 0, false, bytes);
+    std::vector<uint8_t> start, bytes;
+    const bool with_start = (flags & DTGPU_ENCODE_STORE_START_BRANCH_CONTENT) && !f.empty();
+    if (with_start) {   // ListBranch::new_at_local_version(self, from) (encode_oplog.rs:612-615), on the GPU
+        size_t n = 0;   // the text is at most every inserted byte
+        start.resize(h->o.ins_content.size() + 1);
+        const dtgpu_status cs = dtgpu_checkout(h, f.data(), f.size(), start.data(), start.size(), &n);
+        if (cs != DTGPU_OK) return cs;
+        start.resize(n);
+    }
+    const Status st = encode_dt(h->o, f, (flags & DTGPU_ENCODE_STORE_INSERTED_CONTENT) != 0,
+                                (flags & DTGPU_ENCODE_COMPRESS_CONTENT) != 0, with_start ? &start : nullptr, bytes);
     if (st != OK) return dtgpu_status(st);
     if (out_len) *out_len = bytes.size();
     if (!out) return DTGPU_OK;
     if (cap < bytes.size()) return DTGPU_ERR_ARG;
     std::memcpy(out, bytes.data(), bytes.size());
+    return DTGPU_OK;
+}
+
+dtgpu_status dtgpu_lz4_compress(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_t *out_len) {
+    if (!in && n) return DTGPU_ERR_ARG;
+    std::vector<uint8_t> c;
+    lz4_block_compress(in, n, c);
+    if (out_len) *out_len = c.size();
+    if (!out) return DTGPU_OK;
+    if (cap < c.size()) return DTGPU_ERR_ARG;
+    std::memcpy(out, c.data(), c.size());
     return DTGPU_OK;
 }
 

@@ -11,6 +11,7 @@ Mirrors (reference paths under jarrodhroberson/diamond-types):
 There is no CPU fallback: every checkout runs the HIP kernels, and a missing library or a
 missing GPU raises immediately.
 """
+import collections
 import ctypes
 import os
 
@@ -110,6 +111,7 @@ def lib():
     L.dtgpu_oplog_history.argtypes = [vp, pu64, sz, ctypes.POINTER(vp)]
     L.dtgpu_oplog_project.argtypes = [vp, pu64, sz, ctypes.POINTER(vp)]
     L.dtgpu_oplog_encode.argtypes = [vp, pu64, sz, ctypes.c_uint32, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
+    L.dtgpu_lz4_compress.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
     L.dtgpu_oplog_decode_and_add.argtypes = [vp, ctypes.c_char_p, sz, c, pu64, sz, ctypes.POINTER(sz)]
     L.dtgpu_oplog_doc_id.argtypes = [vp, ctypes.c_char_p, sz]
     L.dtgpu_oplog_doc_id.restype = ctypes.c_int64
@@ -243,6 +245,29 @@ class ListBranch:
 
     def local_frontier(self):
         return list(self.version)
+
+
+class EncodeOptions(collections.namedtuple(
+        "EncodeOptions", "store_inserted_content compress_content store_start_branch_content")):
+    """EncodeOptions (src/list/encoding/encode_oplog.rs:88-110): the fields libdtgpu honours
+    (user_data, store_deleted_content and the experimental end branch are not offered)."""
+    def flags(self):
+        return ((1 if self.store_inserted_content else 0) | (2 if self.compress_content else 0)
+                | (4 if self.store_start_branch_content else 0))
+
+
+ENCODE_FULL = EncodeOptions(True, True, True)     # encode_oplog.rs:122-130
+ENCODE_PATCH = EncodeOptions(True, True, False)   # encode_oplog.rs:112-120
+
+
+def lz4_compress(data: bytes) -> bytes:
+    """lz4_flex::compress_into as the encoder calls it (encode_oplog.rs:320-343): one raw LZ4
+    block, no length prefix."""
+    n = ctypes.c_size_t()
+    _check(lib().dtgpu_lz4_compress(data, len(data), None, 0, ctypes.byref(n)))
+    buf = ctypes.create_string_buffer(max(1, n.value))
+    _check(lib().dtgpu_lz4_compress(data, len(data), buf, n.value, ctypes.byref(n)))
+    return buf.raw[:n.value]
 
 
 class ListOpLog:
@@ -464,14 +489,17 @@ class ListOpLog:
             return rng, ("ins", cur[4], cur[6])
         return rng, ("del", min(cur[4], cur[5]), cur[1] - cur[0])
 
-    def encode(self, store_inserted_content=True) -> bytes:
-        """ListOpLog::encode (src/list/encoding/encode_oplog.rs:745-747), content uncompressed."""
-        return self.encode_from([], store_inserted_content)
+    def encode(self, opts=None) -> bytes:
+        """ListOpLog::encode(opts) (src/list/encoding/encode_oplog.rs:745-747); opts defaults to
+        ENCODE_FULL (EncodeOptions::default, :133-137)."""
+        return self.encode_from([], opts)
 
-    def encode_from(self, frm, store_inserted_content=True) -> bytes:
-        """ListOpLog::encode_from (encode_oplog.rs:404-743): the ops after version `frm`."""
+    def encode_from(self, frm, opts=None) -> bytes:
+        """ListOpLog::encode_from(opts, from) (encode_oplog.rs:404-743): the ops after version
+        `frm`.  With opts.store_start_branch_content and a non-ROOT `frm`, the StartBranch holds
+        the checkout at `frm`, run on the GPU."""
         p, nf = _u64s(frm)
-        flags = 1 if store_inserted_content else 0
+        flags = (opts or ENCODE_FULL).flags()
         n = ctypes.c_size_t()
         _check(lib().dtgpu_oplog_encode(self._h, p, nf, flags, None, 0, ctypes.byref(n)))
         buf = ctypes.create_string_buffer(max(1, n.value))

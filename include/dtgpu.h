@@ -93,12 +93,22 @@ int64_t dtgpu_oplog_add_delete_without_content(dtgpu_oplog *oplog, int32_t agent
 
 /* ListOpLog::encode(opts) / encode_from(opts, from) (src/list/encoding/encode_oplog.rs:404-747):
  * the `.dt` bytes of the ops after `from` (an empty `from` is ROOT: the whole oplog).  Written in
- * the reference's order (Graph::optimized_txns_between) through the reference's run mergers, so
- * the bytes equal the reference encoder's when its content is not LZ4-compressed.  Content is
- * written uncompressed (lz4_flex's compressor is not reproduced; every reader accepts it).
- * flags: DTGPU_ENCODE_STORE_INSERTED_CONTENT (EncodeOptions::store_inserted_content, set in
- * ENCODE_FULL / ENCODE_PATCH).  out == NULL returns the size in *out_len. */
+ * the reference's order (Graph::optimized_txns_between) through the reference's run mergers, with
+ * content fields of >= 20 bytes LZ4-compressed by a restatement of lz4_flex 0.10's block
+ * compressor (encode_oplog.rs:270-343), so the bytes equal the reference encoder's for the same
+ * options.  flags mirror EncodeOptions (encode_oplog.rs:88-130):
+ *   DTGPU_ENCODE_STORE_INSERTED_CONTENT      store_inserted_content
+ *   DTGPU_ENCODE_COMPRESS_CONTENT            compress_content
+ *   DTGPU_ENCODE_STORE_START_BRANCH_CONTENT  store_start_branch_content: with a non-ROOT `from`
+ *                                            the StartBranch holds the checkout at `from`, which
+ *                                            runs on the GPU (DTGPU_ERR_NO_DEVICE without one)
+ * DTGPU_ENCODE_FULL / DTGPU_ENCODE_PATCH are the reference's ENCODE_FULL / ENCODE_PATCH.
+ * out == NULL returns the size in *out_len. */
 #define DTGPU_ENCODE_STORE_INSERTED_CONTENT 1u
+#define DTGPU_ENCODE_COMPRESS_CONTENT 2u
+#define DTGPU_ENCODE_STORE_START_BRANCH_CONTENT 4u
+#define DTGPU_ENCODE_FULL 7u
+#define DTGPU_ENCODE_PATCH 3u
 dtgpu_status dtgpu_oplog_encode(const dtgpu_oplog *oplog, const uint64_t *from, size_t n_from, uint32_t flags,
                                 uint8_t *out, size_t cap, size_t *out_len);
 
@@ -146,6 +156,9 @@ size_t dtgpu_oplog_agent_runs(const dtgpu_oplog *oplog, uint32_t *out, size_t ca
 dtgpu_status dtgpu_checkout(const dtgpu_oplog *oplog, const uint64_t *version, size_t n_version, uint8_t *out,
                             size_t cap, size_t *out_len);
 dtgpu_status dtgpu_checkout_tip(const dtgpu_oplog *oplog, uint8_t *out, size_t cap, size_t *out_len);
+/* lz4_flex::compress_into (the raw block the encoder writes, encode_oplog.rs:320-343; no length
+ * prefix).  out == NULL returns the size in *out_len. */
+dtgpu_status dtgpu_lz4_compress(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_t *out_len);
 
 /* ListOpLog::iter_xf_operations() (src/list/merge.rs:24-48): the transformed operations that
  * bring an empty document to the tip, in the order TransformedOpsIter yields them

@@ -91,7 +91,7 @@ def test_decode_in_parts():   # :49-74
     doc.add_delete_without_content(1, 3, 7)
     doc.add_insert(0, 3, "m")
     f2 = doc.local_frontier()
-    data_2 = doc.encode_from(f1)
+    data_2 = doc.encode_from(f1, dt_amd.ENCODE_PATCH)
 
     d2 = dt_amd.ListOpLog()
     assert d2.decode_and_add(data_1) == f1
@@ -115,7 +115,7 @@ def test_merge_parts():   # :76-90
 def test_merge_future_patch_errors():   # :92-101
     oplog = _simple_doc()
     v = oplog.local_frontier()[0]
-    data = oplog.encode_from([v - 1])
+    data = oplog.encode_from([v - 1], dt_amd.ENCODE_PATCH)
     assert _err(lambda: dt_amd.ListOpLog.load_from(data)) == BaseVersionUnknown
 
 
@@ -126,7 +126,7 @@ def test_merge_parts_2():   # :103-130 (#[ignore] in the reference: b before a n
     t1 = oplog_a.add_insert(0, 0, "aa")
     data_a = oplog_a.encode()
     oplog_a.add_insert_at(1, [], 0, "bbb")
-    data_b = oplog_a.encode_from([t1])
+    data_b = oplog_a.encode_from([t1], dt_amd.ENCODE_PATCH)
 
     a_then_b = dt_amd.ListOpLog()
     a_then_b.decode_and_add(data_a)
@@ -205,8 +205,8 @@ def test_failed_merge_unwinds_runs_extended_in_place(name):
 
 
 def test_save_load_save_load():   # :237-268 (content not stored)
-    o2 = dt_amd.ListOpLog.load_from(_simple_doc().encode(store_inserted_content=False))
-    o3 = dt_amd.ListOpLog.load_from(o2.encode(store_inserted_content=False))
+    o2 = dt_amd.ListOpLog.load_from(_simple_doc().encode(dt_amd.EncodeOptions(False, True, True)))
+    o3 = dt_amd.ListOpLog.load_from(o2.encode(dt_amd.EncodeOptions(False, True, True)))
     assert _state(o2) == _state(o3)
 
 
@@ -254,7 +254,7 @@ def test_merge_patch_returns_correct_version():   # :333-348
     v = oplog.local_frontier()
     o2 = _clone(oplog)
     oplog.add_insert(0, 0, "x")
-    assert o2.decode_and_add(oplog.encode_from(v)) == o2.local_frontier()
+    assert o2.decode_and_add(oplog.encode_from(v, dt_amd.ENCODE_PATCH)) == o2.local_frontier()
     assert _state(o2) == _state(oplog)
 
 
@@ -291,7 +291,7 @@ def test_catch_up_and_overlap_merges_rebuild_the_file(name):
         part = full.history(v).encode()
         # catch-up: the patch starts at the part's version (no filtering)
         d = dt_amd.ListOpLog.load_from(part)
-        assert d.decode_and_add(full.encode_from(v)) == d.local_frontier()
+        assert d.decode_and_add(full.encode_from(v, dt_amd.ENCODE_PATCH)) == d.local_frontier()
         assert _keyed(d) == want, v
         # overlap: the whole file on top of the part (the part's operations are filtered out)
         d = dt_amd.ListOpLog.load_from(part)

@@ -1,6 +1,11 @@
 """`.dt` encoder: `ListOpLog::encode` / `encode_from` (src/list/encoding/encode_oplog.rs:404-747),
 libdtgpu's dtgpu_oplog_encode (host code, csrc/dt_encode.cpp).
 
+LZ4 (lz4_flex 0.10's block compressor, encode_oplog.rs:320-343): the LZ4 blocks the reference
+wrote into friendsforever.dt, git-makefile.dt and node_nodecc.dt are reproduced byte for byte from
+their decompressed content (decompressed by the oracle), covering both hash tables (inputs below
+and above 64 KiB), and compat_simple_doc's LZ4 vector (tests.rs:404-415) too.
+
 Byte-exact against the reference encoder's own outputs held in its tests
 (src/list/encoding/tests.rs): `compat_simple_doc` bytes2 (:418) and `compat_empty_doc` bytes2
 (:383) exactly; `regression_1` doc_data (:362) exactly up to the older StartBranch-at-ROOT form
@@ -8,6 +13,7 @@ that file carries (tests.rs:379-383 documents that change).  Semantically on the
 and the other vectors: the re-decoded oplog holds the same ops, keyed by (agent, seq), with the
 same parents, and checks out to the same text.
 """
+import ctypes
 import json
 import os
 import struct
@@ -18,6 +24,35 @@ import golden_data as G
 from dt_encode import crc32c
 from oracle.oracle import OpLog as OracleOpLog
 import dt_amd
+from oracle import oracle as O
+
+
+def _leb(b, i):
+    v = s = 0
+    while True:
+        x = b[i]
+        i += 1
+        v |= (x & 0x7F) << s
+        s += 7
+        if x < 0x80:
+            return v, i
+
+
+def _lz4_chunk(data):
+    """The leading CompressedFieldsLZ4 chunk of a `.dt` file: (uncompressed length, raw block)."""
+    assert data[:8] == b"DMNDTYPS"
+    _, i = _leb(data, 8)
+    t, i = _leb(data, i)
+    n, i = _leb(data, i)
+    assert t == 5
+    ul, j = _leb(data[i:i + n], 0)
+    return ul, data[i + j:i + n]
+
+
+def _oracle_lz4_decompress(block, ul):
+    out = ctypes.create_string_buffer(max(1, ul))
+    assert O.lib().dto_lz4_decompress(block, len(block), out, ul) == 0
+    return out.raw[:ul]
 
 VECTORS = json.load(open(os.path.join(G.HERE, "golden", "decode_vectors.json")))
 OLD_START_BRANCH = bytes([10, 7, 12, 2, 0, 0, 13, 1, 4])   # StartBranch{Version[ROOT], Content ""}
@@ -111,7 +146,57 @@ def test_synthetic_round_trip():
 def test_encode_from_version_holds_only_the_new_ops():
     o = dt_amd.ListOpLog.load_from(G.dt_bytes("friendsforever"))
     v = [12000]
-    patch = o.encode_from(v)
+    patch = o.encode_from(v, dt_amd.ENCODE_PATCH)
     assert len(patch) < len(o.encode())
     with pytest.raises(Exception):
         dt_amd.ListOpLog.load_from(patch)   # foreign parents: BaseVersionUnknown on an empty oplog
+
+
+@pytest.mark.parametrize("name", G.DT_FILES)
+def test_lz4_compressor_reproduces_the_reference_blocks(name):
+    ul, block = _lz4_chunk(G.dt_bytes(name))
+    raw = _oracle_lz4_decompress(block, ul)
+    assert dt_amd.lz4_compress(raw) == block
+
+
+def test_lz4_compat_vector_and_short_inputs():
+    ul, block = _lz4_chunk(bytes(G.COMPAT_SIMPLE_LZ4))
+    assert dt_amd.lz4_compress(_oracle_lz4_decompress(block, ul)) == block
+    for n in (0, 1, 12, 13, 20, 100):   # literal-only below 13 bytes; every block decodes back
+        data = bytes((i * 7) % 5 + 97 for i in range(n))
+        c = dt_amd.lz4_compress(data)
+        assert _oracle_lz4_decompress(c, n) == data
+        if n < 13:
+            assert c[0] >> 4 == min(n, 15) and len(c) == 1 + n + (n >= 15)
+
+
+def test_encode_full_compresses_content_of_20_bytes_or_more():
+    """write_content (encode_oplog.rs:270-305): content >= 20 bytes goes into the leading LZ4
+    chunk as ContentCompressed; shorter content stays inline; ENCODE_PATCH compresses too and
+    compress_content = false writes Content."""
+    o = dt_amd.ListOpLog()
+    a = o.get_or_create_agent_id("seph")
+    o.add_insert(a, 0, "the quick brown fox jumps over the lazy dog " * 4)
+    full = o.encode()
+    assert full[9] == 5 and o.encode(dt_amd.ENCODE_PATCH) == full
+    plain = o.encode(dt_amd.EncodeOptions(True, False, True))
+    assert plain[9] != 5 and len(plain) > len(full)
+    for data in (full, plain):
+        assert OracleOpLog.load_from(data).checkout_tip_bytes() == b"the quick brown fox jumps over the lazy dog " * 4
+        assert _keyed(dt_amd.ListOpLog.load_from(data)) == _keyed(o)
+    short = dt_amd.ListOpLog()
+    short.add_insert(short.get_or_create_agent_id("seph"), 0, "nineteen characters")
+    assert short.encode()[9] != 5
+
+
+@pytest.mark.parametrize("name", G.DT_FILES)
+def test_benchmark_files_encode_full_compressed(name):
+    """ENCODE_FULL of a benchmark file: one LZ4 chunk holding the inserted text in the encoder's
+    walk order, which the oracle decompresses and decodes to the same history."""
+    o = dt_amd.ListOpLog.load_from(G.dt_bytes(name))
+    e = o.encode()
+    ul, block = _lz4_chunk(e)
+    raw = _oracle_lz4_decompress(block, ul)
+    assert ul == len(bytes(o.export("content"))) and sorted(raw) == sorted(bytes(o.export("content")))
+    assert dt_amd.lz4_compress(raw) == block
+    assert len(OracleOpLog.load_from(e)) == len(o)
