@@ -836,10 +836,13 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
         bool found;
         TRY(C.expect_chunk(r, 1, fi));
         TRY(C.chunk_if(fi, 2, found, tmp));
+        R.doc_id_len = 0xFFFFFFFFu;
         if (found) {
             uint64_t dt;
             TRY(C.u32v(tmp, dt));
             if (dt != 4) return UnknownChunk;
+            R.doc_id_off = tmp.p;
+            R.doc_id_len = tmp.n;
             bool asc;
             if (!SIZE && !utf8_ok(C.in + tmp.p, tmp.n, asc)) return InvalidUTF8;
         }

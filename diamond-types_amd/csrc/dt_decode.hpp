@@ -37,6 +37,7 @@ struct DecodeResult {
     // sizing pass (size_only): what the full pass needs
     uint32_t lz_len, tp_bytes, cik_bytes, hist_bytes, raw_aruns, pad;
     uint32_t prof[8];       // core-clock cycles per decode phase (full pass)
+    uint32_t doc_id_off, doc_id_len;   // the DocId bytes in the document (len ~0: none)
 };
 
 constexpr uint32_t DECODE_DEFER = 80;           // a case the device decoder hands to the host

@@ -1,0 +1,803 @@
+// dt_encoder.hip -- batched `.dt` encoder: ListOpLog::encode(ENCODE_FULL / ENCODE_PATCH) from ROOT
+// (src/list/encoding/encode_oplog.rs:404-747), one 64-lane wavefront per document.
+//
+// Inputs stay where the device-staged batch left them: the decoded oplog in the decoder's arenas
+// (agent runs, entries + parents, content + per-LV byte offsets, agent names in the document
+// bytes) and the walk -- Graph::optimized_txns_between(ROOT, tip), the SpanningTreeWalker order the
+// planner already produced for the checkout: its INS / DEL commands are the op runs of each entry
+// in walk order.  Output bytes equal dt_encode.cpp's (the host encoder) for the same options.
+//
+//   A  walk       lane-parallel: each command's entry (bisection), entry starts in walk order,
+//                 every entry's output position (prefix sums)
+//   B  records    the reference's run mergers, which are sequential state machines: agent
+//                 assignment (encode_oplog.rs:142-189), ops (op_metrics.rs:235-293) and txns
+//                 (graph/mod.rs:239-254) -- the gathers are lane-parallel per 64 items, the merge
+//                 decisions a wave-uniform loop over registers (readlane), one record store per run
+//   C  sizes      lane-parallel: each record's varint bytes, prefix sums -> every chunk's length
+//   D  text       the inserted content in walk order (one lane per op run)
+//   E  LZ4        lz4_flex 0.10's greedy parse (see dt_encode.cpp lz4_block_compress) with 64
+//                 probe positions per step: a probe's candidate is the last earlier probe of the
+//                 same hash in the step, else the table (LDS); the first matching probe ends the
+//                 step and only probes up to it enter the table; backtrack / extend 64 bytes at a time
+//   F  write      chunk headers (one lane), records serialised lane-parallel at final offsets
+//   G  CRC-32C    64 lane segments combined (as in dt_decode.hip)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dt_encoder.hpp"
+
+namespace dtgpu {
+namespace enc {
+
+#define DEV __device__ __forceinline__
+
+DEV uint32_t lane() { return __lane_id(); }
+DEV uint32_t rdl(uint32_t v, uint32_t l) { return uint32_t(__builtin_amdgcn_readlane(int(v), int(l))); }
+DEV uint64_t ballot(bool p) { return __ballot(p); }
+DEV uint64_t lt_mask() { return (1ull << lane()) - 1ull; }
+DEV uint32_t popc(uint64_t m) { return uint32_t(__popcll(m)); }
+DEV uint32_t ctz(uint64_t m) { return uint32_t(__ffsll((unsigned long long)m) - 1); }
+DEV void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+DEV uint32_t scan_incl(uint32_t v) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = uint32_t(__shfl_up(int(v), d));
+        if (lane() >= uint32_t(d)) v += o;
+    }
+    return v;
+}
+DEV uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += uint32_t(__shfl_xor(int(v), d));
+    return v;
+}
+
+// ---- varints (leb.rs) ---------------------------------------------------------------------------
+DEV uint32_t leb_len(uint64_t v) {
+    uint32_t n = 1;
+    while (v >= 0x80) { v >>= 7; n++; }
+    return n;
+}
+DEV uint32_t put_leb(uint8_t *d, uint64_t v) {
+    uint32_t n = 0;
+    while (v >= 0x80) { d[n++] = uint8_t(v | 0x80); v >>= 7; }
+    d[n++] = uint8_t(v);
+    return n;
+}
+DEV uint64_t zz_old(int64_t v) { return (uint64_t(v < 0 ? -v : v) << 1) | (v < 0 ? 1u : 0u); }
+DEV uint32_t utf8_len(uint8_t c) { return c < 0x80 ? 1 : (c & 0xE0) == 0xC0 ? 2 : (c & 0xF0) == 0xE0 ? 3 : 4; }
+
+constexpr uint32_t CRC_POLY = 0x82F63B78u;
+constexpr uint32_t ST_OK = 0, ST_CHECKOUT = 64, ST_CAPACITY = 65;
+constexpr uint32_t C_LZ4 = 5, C_FILEINFO = 1, C_DOCID = 2, C_AGENTNAMES = 3, C_STARTBRANCH = 10, C_CONTENT = 13,
+                   C_CONTENTCOMP = 14, C_PATCHES = 20, C_OPVERSIONS = 21, C_OPTYPEPOS = 22, C_OPPARENTS = 23,
+                   C_PATCHCONTENT = 24, C_CONTENTKNOWN = 25, C_CRC = 100;
+
+DEV uint32_t entry_of(const uint2 *ent, uint32_t ne, uint32_t lv) {   // Graph::find_packed
+    uint32_t lo = 0, hi = ne;
+    while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (ent[m].y <= lv) lo = m + 1; else hi = m;
+    }
+    return lo;
+}
+DEV uint32_t arun_of(const uint4 *ar, uint32_t n, uint32_t lv) {   // last run with ar.lv <= lv
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (ar[m].x <= lv) lo = m + 1; else hi = m;
+    }
+    return lo ? lo - 1 : 0;
+}
+
+// ---- CRC-32C (zlib's crc32_combine scheme over the reflected polynomial) ------------------------
+DEV uint32_t multmodp(uint32_t a, uint32_t b) {
+    if (!a) return 0;
+    uint32_t m = 1u << 31, p = 0;
+    for (;;) {
+        if (a & m) {
+            p ^= b;
+            if ((a & (m - 1)) == 0) break;
+        }
+        m >>= 1;
+        b = (b & 1u) ? (b >> 1) ^ CRC_POLY : b >> 1;
+    }
+    return p;
+}
+DEV uint32_t x2nmodp(const uint32_t *x2n, uint64_t n, uint32_t k) {
+    uint32_t p = 1u << 31;
+    while (n) {
+        if (n & 1) p = multmodp(x2n[k & 31], p);
+        n >>= 1;
+        k++;
+    }
+    return p;
+}
+DEV uint32_t crc32c_par(const uint8_t *s, uint32_t n, const uint32_t *T, const uint32_t *x2n) {
+    const uint32_t S = (n + 63) / 64;
+    const uint32_t b0 = lane() * S;
+    const uint32_t e0 = b0 < n ? min(b0 + S, n) : b0;
+    uint32_t c = ~0u;
+    for (uint32_t i = b0; i < e0; i++) c = T[(c ^ s[i]) & 0xFFu] ^ (c >> 8);
+    c = ~c;
+    if (e0 <= b0) c = 0;
+    const uint32_t op_full = x2nmodp(x2n, S, 3);
+    uint32_t crc = rdl(c, 0);
+    for (uint32_t l = 1; l < 64; l++) {
+        const uint32_t sb = l * S;
+        if (sb >= n) break;
+        const uint32_t len = sb + S <= n ? S : n - sb;
+        crc = multmodp(len == S ? op_full : x2nmodp(x2n, len, 3), crc) ^ rdl(c, l);
+    }
+    return crc;
+}
+
+// ---- LZ4 (lz4_flex 0.10 compress_into, restated in dt_encode.cpp) -----------------------------
+DEV uint32_t ld32(const uint8_t *p) {
+    return uint32_t(p[0]) | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) | (uint32_t(p[3]) << 24);
+}
+DEV uint64_t ld64(const uint8_t *p) { return uint64_t(ld32(p)) | (uint64_t(ld32(p + 4)) << 32); }
+
+struct Lz {
+    const uint8_t *in;
+    uint8_t *out;
+    uint32_t n, o;
+    bool small;
+    uint32_t *tab;   // LDS: 8,192 u16 (small) or 4,096 u32
+    DEV uint32_t hash(uint32_t p) const {
+        if (small) return (ld32(in + p) * 2654435761u) >> 19;
+        return uint32_t(((ld64(in + p) << 24) * 889523592379ull) >> 52);
+    }
+    DEV uint32_t get(uint32_t h) const {
+        return small ? uint32_t(reinterpret_cast<const uint16_t *>(tab)[h]) : tab[h];
+    }
+    DEV void put(uint32_t h, uint32_t v) {
+        if (small) reinterpret_cast<uint16_t *>(tab)[h] = uint16_t(v);
+        else tab[h] = v;
+    }
+    DEV void ext(uint32_t v) {   // 255-run length extension
+        const uint32_t nb = v / 255 + 1;
+        for (uint32_t i = lane(); i < nb; i += 64) out[o + i] = i + 1 < nb ? 255 : uint8_t(v - 255 * (nb - 1));
+        o += nb;
+    }
+    DEV void emit(uint32_t l0, uint32_t l1, uint32_t off, uint32_t mlen) {
+        const uint32_t ll = l1 - l0;
+        if (lane() == 0) out[o] = uint8_t((min(ll, 15u) << 4) | (off ? min(mlen - 4, 15u) : 0u));
+        o++;
+        if (ll >= 15) ext(ll - 15);
+        for (uint32_t i = lane(); i < ll; i += 64) out[o + i] = in[l0 + i];
+        o += ll;
+        if (!off) return;
+        if (lane() == 0) { out[o] = uint8_t(off); out[o + 1] = uint8_t(off >> 8); }
+        o += 2;
+        if (mlen - 4 >= 15) ext(mlen - 19);
+    }
+    DEV uint32_t run() {
+        o = 0;
+        small = n < 65535;
+        for (uint32_t i = lane(); i < 4096; i += 64) tab[i] = 0;
+        if (n < 13) { emit(0, n, 0, 0); return o; }
+        const uint32_t end_check = n - 12, match_lim = n - 6;
+        uint32_t lit = 0, cur = 1;   // position 0 is hashed first: its entry is the table's zero
+        const uint32_t l = lane();
+        for (;;) {
+            uint32_t nmc = 32, pos = cur, cand = 0;
+            bool found = false;
+            for (;;) {   // 64 probes of the miss loop
+                const uint32_t step = (nmc + l) >> 5;
+                const uint32_t p = pos + scan_incl(step) - step;
+                const bool valid = p <= end_check;
+                const uint32_t nv = popc(ballot(valid));   // valid probes form a prefix
+                const uint32_t h = valid ? hash(p) : 0xFFFFFFFFu;
+                int prevj = -1;
+                uint32_t nextj = 64;
+                for (uint32_t j = 0; j < nv; j++) {
+                    const uint32_t hj = rdl(h, j);
+                    if (hj == h) {
+                        if (j < l) prevj = int(j);
+                        else if (j > l && nextj == 64) nextj = j;
+                    }
+                }
+                const uint32_t pp = uint32_t(__shfl(int(p), prevj < 0 ? int(l) : prevj));
+                const uint32_t c = prevj >= 0 ? pp : (valid ? get(h) : 0u);
+                const bool ok = valid && p - c <= 65535u && ld32(in + c) == ld32(in + p);
+                const uint64_t m = ballot(ok);
+                const uint32_t lim = m ? ctz(m) + 1 : nv;
+                if (l < lim && nextj >= lim) put(h, p);   // the last probe of each hash wins
+                if (m) {
+                    cur = rdl(p, lim - 1);
+                    cand = rdl(c, lim - 1);
+                    found = true;
+                    break;
+                }
+                if (nv < 64) break;
+                pos = rdl(p, 63) + rdl(step, 63);
+                nmc += 64;
+            }
+            if (!found) { emit(lit, n, 0, 0); return o; }
+            for (;;) {   // extend backwards over the pending literals
+                const uint32_t mb = min(cur - lit, cand);
+                const bool eq = l < mb && in[cur - 1 - l] == in[cand - 1 - l];
+                const uint64_t x = ballot(!eq);
+                const uint32_t b = x ? ctz(x) : 64;
+                cur -= b;
+                cand -= b;
+                if (b < 64) break;
+            }
+            const uint32_t m0 = cur, off = cur - cand;
+            cur += 4;
+            cand += 4;
+            for (;;) {   // extend forwards up to len - 6
+                const bool eq = cur + l < match_lim && in[cur + l] == in[cand + l];
+                const uint64_t x = ballot(!eq);
+                const uint32_t b = x ? ctz(x) : 64;
+                cur += b;
+                cand += b;
+                if (b < 64) break;
+            }
+            const uint32_t h2 = hash(cur - 2);
+            if (l == 0) put(h2, cur - 2);
+            emit(lit, m0, off, cur - m0);
+            lit = cur;
+        }
+    }
+};
+
+// ---- op runs: ListOpMetrics merge (op_metrics.rs:235-293) and write_op (encode_oplog.rs:20-92)
+struct Op {
+    uint32_t start, end, c0, c1;
+    bool fwd, del, content;
+    DEV uint32_t len() const { return end - start; }
+};
+DEV bool can_append(const Op &a, const Op &b) {
+    if (a.del != b.del || a.content != b.content) return false;
+    if (a.content && a.c1 != b.c0) return false;
+    const bool af = a.len() == 1 || a.fwd, bf = b.len() == 1 || b.fwd;
+    if (af && bf && ((!a.del && b.start == a.end) || (a.del && b.start == a.start))) return true;
+    const bool ar = a.len() == 1 || !a.fwd, br = b.len() == 1 || !b.fwd;
+    return a.del && ar && br && b.end == a.start;
+}
+DEV void append(Op &a, const Op &b) {
+    a.fwd = b.start >= a.start && (b.start != a.start || a.del);
+    if (a.del && !a.fwd) a.start = b.start;
+    else a.end += b.len();
+    if (a.content) a.c1 = b.c1;
+}
+// the varint head of a written op run and its optional diff; op_end is the next cursor
+DEV void op_code(uint4 r, uint32_t cursor, uint64_t &n, int64_t &diff, bool &has_diff, uint32_t &op_end) {
+    const uint32_t start = r.x, end = r.y, len = end - start;
+    const bool del = r.z & 1u, fwd = (r.z & 2u) || len == 1;
+    const uint32_t op_start = (del && !fwd) ? end : start;
+    op_end = (!del && fwd) ? end : start;
+    diff = int64_t(op_start) - int64_t(cursor);
+    uint64_t v;
+    if (len != 1) v = del ? (uint64_t(len) * 2 + (fwd ? 1 : 0)) : len;
+    else v = diff != 0 ? zz_old(diff) : 0;
+    v = v * 2 + (del ? 1 : 0);
+    v = v * 2 + (diff != 0 ? 1 : 0);
+    v = v * 2 + (len != 1 ? 1 : 0);
+    n = v;
+    has_diff = len != 1 && diff != 0;
+}
+
+struct Layout {   // byte offsets of the streams in the output
+    uint32_t aa, ops, tx, names, text, known, lz, total;
+};
+
+__global__ __launch_bounds__(64) void encode_kernel(EncParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const uint32_t doc = blockIdx.x;
+    if (doc >= P.n_docs) return;
+    const EncDesc D = P.docs[doc];
+    EncResult R{};
+    if (D.skip) return;
+    const uint32_t l = lane();
+    uint64_t t_prev = P.prof ? clock64() : 0;
+    auto mark = [&](int i) {
+        if (P.prof) { const uint64_t t = clock64(); R.prof[i] = t - t_prev; t_prev = t; }
+    };
+    uint32_t *T = lds;                       // CRC table (256)
+    uint32_t *tab = lds + 256;               // LZ4 hash table (4,096 words)
+    uint32_t *amap = lds + 256 + 4096;       // agent -> mapped id (0: not yet), max_agents
+    uint32_t *alast = amap + P.max_agents;   // agent -> end of its last seq range written
+    for (uint32_t i = l; i < 256; i += 64) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ CRC_POLY : c >> 1;
+        T[i] = c;
+    }
+    for (uint32_t i = l; i < D.n_agents; i += 64) { amap[i] = 0; alast[i] = 0; }
+
+    const uint8_t *in = P.in + D.in_off;
+    const uint4 *ar = reinterpret_cast<const uint4 *>(P.aruns) + D.arun_off;
+    const uint2 *ent = reinterpret_cast<const uint2 *>(P.ent) + D.ent_off;
+    const uint32_t *poff = P.poff + D.poff_off, *par = P.par + D.par_off;
+    const uint8_t *content = P.content + D.content_off;
+    const uint32_t *cbyte = P.cbyte + D.lv_off;
+    const uint2 *names = reinterpret_cast<const uint2 *>(P.agents) + D.agent_off;
+    const Cmd *cmds = P.cmds + D.cmd_off;
+    const uint32_t ne = D.ne, ncmd = D.ncmd;
+    uint32_t *worder = P.w + D.w_off, *outpos = worder + ne;
+    uint32_t *oprec = outpos + ne;                          // 8 words per op run
+    uint32_t *aarec = oprec + 8ull * ncmd;                  // 4 words per agent run
+    uint32_t *heads = aarec + 4ull * (D.n_aruns + ne);      // walk index of each txn head
+    uint32_t *ainv = heads + ne;                            // mapped id - 1 -> agent
+    uint8_t *text = P.b + D.b_off, *lzb = text + D.n_content;
+    uint8_t *out = P.out + D.out_off;
+    const bool store_text = P.flags & 1u, compress = P.flags & 2u;
+
+    // ---- A: the walk ---------------------------------------------------------------------------
+    uint32_t nw = 0, opos = 0;
+    for (uint32_t c0 = 0; c0 < ncmd; c0 += 64) {
+        const uint32_t c = c0 + l;
+        uint32_t e = 0, len = 0;
+        bool starts = false;
+        if (c < ncmd) {
+            const Cmd cm = cmds[c];
+            if ((cm.op & 15u) != CMD_TOG) {
+                e = entry_of(ent, ne, cm.lv);
+                if (e < ne) {
+                    const uint2 se = ent[e];
+                    starts = se.x == cm.lv;
+                    len = se.y - se.x;
+                }
+            }
+        }
+        const uint64_t m = ballot(starts);
+        if (!starts) len = 0;
+        const uint32_t incl = scan_incl(len);
+        if (starts && nw + popc(m & lt_mask()) < ne) {
+            worder[nw + popc(m & lt_mask())] = e;
+            outpos[e] = opos + incl - len;
+        }
+        nw += popc(m);
+        opos += rdl(incl, 63);
+    }
+    if (nw != ne || opos != D.n_lv) {
+        if (l == 0) { R.status = ST_CHECKOUT; P.results[doc] = R; }
+        return;
+    }
+    wave_fence();
+    mark(0);
+
+    // ---- B: records ------------------------------------------------------------------------------
+    // txn heads: an entry continues the previous txn when it follows it directly with that txn's
+    // last LV as its only parent (tx_push; GraphEntrySimple::can_append)
+    uint32_t ntx = 0, carry_end = 0xFFFFFFFFu;
+    for (uint32_t k0 = 0; k0 < ne; k0 += 64) {
+        const uint32_t k = k0 + l;
+        uint2 se = make_uint2(0, 0);
+        uint32_t np = 0, p0v = 0;
+        if (k < ne) {
+            const uint32_t e = worder[k];
+            se = ent[e];
+            const uint32_t p0 = poff[e];
+            np = poff[e + 1] - p0;
+            if (np == 1) p0v = par[p0];
+        }
+        const uint32_t prev_end_l = uint32_t(__shfl_up(int(se.y), 1));
+        const uint32_t prev_end = l == 0 ? carry_end : prev_end_l;
+        const bool merge = k > 0 && se.x == prev_end && np == 1 && p0v + 1 == se.x;
+        const bool head = k < ne && !merge;
+        const uint64_t m = ballot(head);
+        if (head) heads[ntx + popc(m & lt_mask())] = k;
+        ntx += popc(m);
+        carry_end = rdl(se.y, 63);
+    }
+    // agent assignment runs (encode_oplog.rs:142-189, AgentMapping :191-240)
+    uint32_t n_mapped = 0, naa = 0;
+    bool aa_have = false;
+    uint32_t aa_agent = 0, aa_len = 0;
+    int32_t aa_delta = 0;
+    uint32_t cur_agent = 0xFFFFFFFFu, cur_mapped = 0, cur_last = 0;
+    for (uint32_t k0 = 0; k0 < ne; k0 += 64) {
+        const uint32_t k = k0 + l;
+        uint32_t s = 0, e_end = 0, ai = 0;
+        uint4 q = make_uint4(0, 0, 0, 0);
+        if (k < ne) {
+            const uint2 se = ent[worder[k]];
+            s = se.x; e_end = se.y;
+            ai = arun_of(ar, D.n_aruns, s);
+            q = ar[ai];
+        }
+        const uint32_t nk = min(64u, ne - k0);
+        for (uint32_t j = 0; j < nk; j++) {
+            const uint32_t js = rdl(s, j), je = rdl(e_end, j);
+            uint32_t i = rdl(ai, j);
+            uint4 r = make_uint4(rdl(q.x, j), rdl(q.y, j), rdl(q.z, j), rdl(q.w, j));
+            for (;;) {
+                const uint32_t x = max(r.x, js), y = min(r.x + r.y, je);
+                if (x < y) {
+                    const uint32_t agent = r.z;
+                    if (agent != cur_agent) {
+                        if (cur_agent != 0xFFFFFFFFu && l == 0) alast[cur_agent] = cur_last;
+                        cur_agent = agent;
+                        cur_mapped = amap[agent];
+                        cur_last = alast[agent];
+                        if (!cur_mapped) {
+                            cur_mapped = ++n_mapped;
+                            if (l == 0) { amap[agent] = cur_mapped; ainv[cur_mapped - 1] = agent; }
+                        }
+                    }
+                    const uint32_t s0 = r.w + (x - r.x);
+                    const int32_t d = int32_t(s0 - cur_last);
+                    cur_last = s0 + (y - x);
+                    if (aa_have && aa_agent == cur_mapped && d == 0) {
+                        aa_len += y - x;
+                    } else {
+                        if (aa_have && l == 0) {
+                            uint32_t *w = aarec + 4 * naa;
+                            w[0] = aa_agent; w[1] = uint32_t(aa_delta); w[2] = aa_len;
+                        }
+                        naa += aa_have ? 1 : 0;
+                        aa_have = true; aa_agent = cur_mapped; aa_delta = d; aa_len = y - x;
+                    }
+                }
+                if (r.x + r.y >= je || ++i >= D.n_aruns) break;
+                r = ar[i];
+            }
+        }
+    }
+    if (aa_have) {
+        if (l == 0) { uint32_t *w = aarec + 4 * naa; w[0] = aa_agent; w[1] = uint32_t(aa_delta); w[2] = aa_len; }
+        naa++;
+    }
+    // op runs in walk order (the INS / DEL commands), merged
+    uint32_t nop = 0, n_ins = 0;
+    bool op_have = false;
+    Op a{};
+    auto op_store = [&](const Op &o) {
+        if (l == 0) {
+            uint32_t *w = oprec + 8ull * nop;
+            w[0] = o.start; w[1] = o.end; w[2] = (o.del ? 1u : 0u) | (o.fwd ? 2u : 0u) | (o.content ? 4u : 0u);
+            w[3] = o.c0; w[4] = o.c1;
+        }
+        nop++;
+    };
+    for (uint32_t c0 = 0; c0 < ncmd; c0 += 64) {
+        const uint32_t c = c0 + l;
+        Cmd cm{CMD_TOG, 0, 0, 0};
+        uint32_t cb0 = 0, cb1 = 0;
+        if (c < ncmd) {
+            cm = cmds[c];
+            if ((cm.op & 15u) == CMD_INS) {
+                cb0 = cbyte[cm.lv];
+                const uint32_t lb = cbyte[cm.lv + cm.len - 1];
+                cb1 = lb != 0xFFFFFFFFu ? lb + utf8_len(content[lb]) : 0xFFFFFFFFu;
+            }
+        }
+        const uint32_t nk = min(64u, ncmd - c0);
+        for (uint32_t j = 0; j < nk; j++) {
+            const uint32_t op = rdl(cm.op, j);
+            if ((op & 15u) == CMD_TOG) continue;
+            Op b;
+            b.start = rdl(cm.pos, j);
+            b.end = b.start + rdl(cm.len, j);
+            b.del = (op & 15u) == CMD_DEL;
+            b.fwd = !b.del || (op & 16u);
+            b.content = !b.del && rdl(cb0, j) != 0xFFFFFFFFu;
+            b.c0 = rdl(cb0, j);
+            b.c1 = rdl(cb1, j);
+            if (!b.del) n_ins += b.len();
+            if (op_have && can_append(a, b)) { append(a, b); continue; }
+            if (op_have) op_store(a);
+            op_have = true;
+            a = b;
+        }
+    }
+    if (op_have) op_store(a);
+    wave_fence();
+    mark(1);
+
+    // ---- C: sizes ----------------------------------------------------------------------------------
+    uint32_t aa_bytes = 0, op_bytes = 0, tx_bytes = 0, nm_bytes = 0, text_len = 0;
+    for (uint32_t i0 = 0; i0 < naa; i0 += 64) {
+        const uint32_t i = i0 + l;
+        if (i < naa) {
+            const uint32_t *w = aarec + 4 * i;
+            const int32_t d = int32_t(w[1]);
+            aa_bytes += leb_len(uint64_t(w[0]) * 2 + (d != 0 ? 1 : 0)) + leb_len(w[2]) + (d != 0 ? leb_len(zz_old(d)) : 0);
+        }
+    }
+    aa_bytes = wave_sum(aa_bytes);
+    for (uint32_t i0 = 0; i0 < nop; i0 += 64) {
+        const uint32_t i = i0 + l;
+        if (i < nop) {
+            const uint32_t *w = oprec + 8ull * i;
+            uint32_t cursor = 0;
+            if (i > 0) {
+                const uint32_t *pw = w - 8;
+                uint64_t n2; int64_t d2; bool h2; op_code(make_uint4(pw[0], pw[1], pw[2], 0), 0, n2, d2, h2, cursor);
+            }
+            uint64_t n; int64_t d; bool hd; uint32_t oe;
+            op_code(make_uint4(w[0], w[1], w[2], 0), cursor, n, d, hd, oe);
+            op_bytes += leb_len(n) + (hd ? leb_len(zz_old(d)) : 0);
+            if (!(w[2] & 1u) && (w[2] & 4u)) text_len += w[4] - w[3];
+        }
+    }
+    op_bytes = wave_sum(op_bytes);
+    text_len = store_text ? wave_sum(text_len) : 0;
+    // txns: len, then parents as output-order distances (all local from ROOT)
+    auto tx_record = [&](uint32_t t, uint8_t *dst) -> uint32_t {
+        const uint32_t e = worder[heads[t]];
+        const uint32_t out0 = outpos[e];
+        const uint32_t nxt = t + 1 < ntx ? outpos[worder[heads[t + 1]]] : D.n_lv;
+        uint32_t nb = dst ? put_leb(dst, nxt - out0) : leb_len(nxt - out0);
+        const uint32_t p0 = poff[e], np = poff[e + 1] - p0;
+        if (np == 0) {
+            if (dst) dst[nb] = 1;
+            return nb + 1;
+        }
+        for (uint32_t j = 0; j < np; j++) {
+            const uint32_t p = par[p0 + j];
+            const uint32_t pe = min(entry_of(ent, ne, p), ne - 1);
+            const uint32_t mp = outpos[pe] + (p - ent[pe].x);
+            const uint64_t v = (uint64_t(out0 - mp) * 2 + (j + 1 < np ? 1 : 0)) * 2;
+            nb += dst ? put_leb(dst + nb, v) : leb_len(v);
+        }
+        return nb;
+    };
+    for (uint32_t t0 = 0; t0 < ntx; t0 += 64)
+        if (t0 + l < ntx) tx_bytes += tx_record(t0 + l, nullptr);
+    tx_bytes = wave_sum(tx_bytes);
+    for (uint32_t i = l; i < n_mapped; i += 64) {
+        const uint32_t nl = names[ainv[i]].y;
+        nm_bytes += leb_len(nl) + nl;
+    }
+    nm_bytes = wave_sum(nm_bytes);
+    mark(2);
+
+    // ---- D + E: walk-order text, LZ4 ---------------------------------------------------------------
+    if (text_len > D.n_content) {
+        if (l == 0) { R.status = ST_CHECKOUT; P.results[doc] = R; }
+        return;
+    }
+    if (text_len) {
+        uint32_t tpos = 0;
+        for (uint32_t i0 = 0; i0 < nop; i0 += 64) {
+            const uint32_t i = i0 + l;
+            uint32_t tl = 0, c0b = 0;
+            if (i < nop) {
+                const uint32_t *w = oprec + 8ull * i;
+                if (!(w[2] & 1u) && (w[2] & 4u)) { c0b = w[3]; tl = w[4] - w[3]; }
+            }
+            const uint32_t incl = scan_incl(tl);
+            uint8_t *d = text + tpos + incl - tl;
+            for (uint32_t x = 0; x < tl; x++) d[x] = content[c0b + x];
+            tpos += rdl(incl, 63);
+        }
+        if (tpos != text_len) {
+            if (l == 0) { R.status = ST_CHECKOUT; P.results[doc] = R; }
+            return;
+        }
+    }
+    const bool use_lz = compress && text_len >= 20;
+    uint32_t lz_len = 0;
+    if (use_lz) {
+        wave_fence();
+        Lz z;
+        z.in = text;
+        z.out = lzb;
+        z.n = text_len;
+        z.tab = tab;
+        lz_len = z.run();
+    }
+    wave_fence();
+    R.lz_len = lz_len;
+    mark(3);
+
+    // ---- F: layout and write -----------------------------------------------------------------------
+    const bool has_doc_id = D.doc_id_len != 0xFFFFFFFFu;
+    const uint32_t lz_body = use_lz ? leb_len(text_len) + lz_len : 0;
+    const uint32_t lz_chunk = use_lz ? 1 + leb_len(lz_body) + lz_body : 0;
+    const uint32_t docid_body = has_doc_id ? 1 + D.doc_id_len : 0;
+    const uint32_t fi_body = (has_doc_id ? 1 + leb_len(docid_body) + docid_body : 0) + 1 + leb_len(nm_bytes) + nm_bytes;
+    const uint32_t content_body = use_lz ? 1 + leb_len(text_len) : 1 + text_len;
+    const uint64_t known_v = uint64_t(n_ins) * 2 + 1;
+    const uint32_t known_body = leb_len(known_v);
+    const uint32_t pc_body = 1 + (1 + leb_len(content_body) + content_body) + (1 + leb_len(known_body) + known_body);
+    const uint32_t pc_chunk = text_len ? 1 + leb_len(pc_body) + pc_body : 0;
+    const uint32_t patches_body = pc_chunk + (1 + leb_len(aa_bytes) + aa_bytes) + (1 + leb_len(op_bytes) + op_bytes) +
+                                  (1 + leb_len(tx_bytes) + tx_bytes);
+    const uint32_t total = 9 + lz_chunk + (1 + leb_len(fi_body) + fi_body) + 2 + (1 + leb_len(patches_body) + patches_body) + 6;
+    if (total > D.out_cap) {
+        if (l == 0) { R.status = ST_CAPACITY; P.results[doc] = R; }
+        return;
+    }
+    Layout L;
+    uint32_t at = 0;
+    if (l == 0) {
+        const uint8_t magic[8] = {'D', 'M', 'N', 'D', 'T', 'Y', 'P', 'S'};
+        for (int i = 0; i < 8; i++) out[i] = magic[i];
+        out[8] = 0;
+        at = 9;
+        if (use_lz) {
+            out[at++] = C_LZ4;
+            at += put_leb(out + at, lz_body);
+            at += put_leb(out + at, text_len);
+        }
+    }
+    at = 9 + (use_lz ? 1 + leb_len(lz_body) + leb_len(text_len) : 0);
+    L.lz = at;
+    at += lz_len;
+    if (l == 0) {
+        uint32_t p = at;
+        out[p++] = C_FILEINFO;
+        p += put_leb(out + p, fi_body);
+        if (has_doc_id) {
+            out[p++] = C_DOCID;
+            p += put_leb(out + p, docid_body);
+            out[p++] = 4;   // DataType::PlainText
+        }
+    }
+    at += 1 + leb_len(fi_body) + (has_doc_id ? 1 + leb_len(docid_body) + 1 : 0);
+    const uint32_t docid_at = at;
+    at += has_doc_id ? D.doc_id_len : 0;
+    if (l == 0) {
+        out[at] = C_AGENTNAMES;
+        put_leb(out + at + 1, nm_bytes);
+    }
+    at += 1 + leb_len(nm_bytes);
+    L.names = at;
+    at += nm_bytes;
+    if (l == 0) {
+        uint32_t p = at;
+        out[p++] = C_STARTBRANCH;
+        out[p++] = 0;
+        out[p++] = C_PATCHES;
+        p += put_leb(out + p, patches_body);
+        if (text_len) {
+            out[p++] = C_PATCHCONTENT;
+            p += put_leb(out + p, pc_body);
+            out[p++] = 0;   // Ins
+            out[p++] = use_lz ? C_CONTENTCOMP : C_CONTENT;
+            p += put_leb(out + p, content_body);
+            out[p++] = 4;
+            if (use_lz) p += put_leb(out + p, text_len);
+        }
+    }
+    at += 2 + 1 + leb_len(patches_body);
+    if (text_len) at += 1 + leb_len(pc_body) + 1 + 1 + leb_len(content_body) + 1 + (use_lz ? leb_len(text_len) : 0);
+    L.text = at;
+    if (text_len && !use_lz) at += text_len;
+    if (text_len) {
+        if (l == 0) {
+            out[at] = C_CONTENTKNOWN;
+            put_leb(out + at + 1, known_body);
+            put_leb(out + at + 2, known_v);   // known_body < 128
+        }
+        at += 2 + known_body;
+    }
+    if (l == 0) { out[at] = C_OPVERSIONS; put_leb(out + at + 1, aa_bytes); }
+    at += 1 + leb_len(aa_bytes);
+    L.aa = at;
+    at += aa_bytes;
+    if (l == 0) { out[at] = C_OPTYPEPOS; put_leb(out + at + 1, op_bytes); }
+    at += 1 + leb_len(op_bytes);
+    L.ops = at;
+    at += op_bytes;
+    if (l == 0) { out[at] = C_OPPARENTS; put_leb(out + at + 1, tx_bytes); }
+    at += 1 + leb_len(tx_bytes);
+    L.tx = at;
+    at += tx_bytes;
+    L.total = at + 6;
+    if (L.total != total) {
+        if (l == 0) { R.status = ST_CAPACITY; P.results[doc] = R; }
+        return;
+    }
+    // doc id, LZ4 block or text
+    if (has_doc_id)
+        for (uint32_t i = l; i < D.doc_id_len; i += 64) out[docid_at + i] = in[D.doc_id_off + i];
+    if (use_lz)
+        for (uint32_t i = l; i < lz_len; i += 64) out[L.lz + i] = lzb[i];
+    else if (text_len)
+        for (uint32_t i = l; i < text_len; i += 64) out[L.text + i] = text[i];
+    // names
+    {
+        uint32_t base = L.names;
+        for (uint32_t i0 = 0; i0 < n_mapped; i0 += 64) {
+            const uint32_t i = i0 + l;
+            uint32_t nb = 0;
+            uint2 nmv = make_uint2(0, 0);
+            if (i < n_mapped) { nmv = names[ainv[i]]; nb = leb_len(nmv.y) + nmv.y; }
+            const uint32_t incl = scan_incl(nb);
+            if (i < n_mapped) {
+                uint8_t *d = out + base + incl - nb;
+                const uint32_t h = put_leb(d, nmv.y);
+                for (uint32_t x = 0; x < nmv.y; x++) d[h + x] = in[nmv.x + x];
+            }
+            base += rdl(incl, 63);
+        }
+    }
+    // agent assignment runs
+    {
+        uint32_t base = L.aa;
+        for (uint32_t i0 = 0; i0 < naa; i0 += 64) {
+            const uint32_t i = i0 + l;
+            uint32_t nb = 0, ag = 0, ln = 0;
+            int32_t d = 0;
+            if (i < naa) {
+                const uint32_t *w = aarec + 4 * i;
+                ag = w[0]; d = int32_t(w[1]); ln = w[2];
+                nb = leb_len(uint64_t(ag) * 2 + (d != 0 ? 1 : 0)) + leb_len(ln) + (d != 0 ? leb_len(zz_old(d)) : 0);
+            }
+            const uint32_t incl = scan_incl(nb);
+            if (i < naa) {
+                uint8_t *p = out + base + incl - nb;
+                uint32_t k = put_leb(p, uint64_t(ag) * 2 + (d != 0 ? 1 : 0));
+                k += put_leb(p + k, ln);
+                if (d != 0) put_leb(p + k, zz_old(d));
+            }
+            base += rdl(incl, 63);
+        }
+    }
+    // op runs
+    {
+        uint32_t base = L.ops;
+        for (uint32_t i0 = 0; i0 < nop; i0 += 64) {
+            const uint32_t i = i0 + l;
+            uint32_t nb = 0;
+            uint64_t n = 0;
+            int64_t d = 0;
+            bool hd = false;
+            if (i < nop) {
+                const uint32_t *w = oprec + 8ull * i;
+                uint32_t cursor = 0, oe;
+                if (i > 0) {
+                    const uint32_t *pw = w - 8;
+                    uint64_t n2; int64_t d2; bool h2; op_code(make_uint4(pw[0], pw[1], pw[2], 0), 0, n2, d2, h2, cursor);
+                }
+                op_code(make_uint4(w[0], w[1], w[2], 0), cursor, n, d, hd, oe);
+                nb = leb_len(n) + (hd ? leb_len(zz_old(d)) : 0);
+            }
+            const uint32_t incl = scan_incl(nb);
+            if (i < nop) {
+                uint8_t *p = out + base + incl - nb;
+                const uint32_t k = put_leb(p, n);
+                if (hd) put_leb(p + k, zz_old(d));
+            }
+            base += rdl(incl, 63);
+        }
+    }
+    // txns
+    {
+        uint32_t base = L.tx;
+        for (uint32_t t0 = 0; t0 < ntx; t0 += 64) {
+            const uint32_t t = t0 + l;
+            const uint32_t nb = t < ntx ? tx_record(t, nullptr) : 0;
+            const uint32_t incl = scan_incl(nb);
+            if (t < ntx) tx_record(t, out + base + incl - nb);
+            base += rdl(incl, 63);
+        }
+    }
+    wave_fence();
+    mark(4);
+
+    // ---- G: CRC chunk --------------------------------------------------------------------------------
+    const uint32_t crc = crc32c_par(out, L.total - 6, T, P.x2n);
+    if (l == 0) {
+        uint8_t *p = out + L.total - 6;
+        p[0] = C_CRC; p[1] = 4;
+        p[2] = uint8_t(crc); p[3] = uint8_t(crc >> 8); p[4] = uint8_t(crc >> 16); p[5] = uint8_t(crc >> 24);
+    }
+    mark(5);
+    if (l == 0) {
+        R.status = ST_OK;
+        R.len = L.total;
+        R.n_op_runs = nop;
+        R.n_agent_runs = naa;
+        R.n_txns = ntx;
+        R.text_len = text_len;
+        P.results[doc] = R;
+    }
+}
+
+}  // namespace enc
+
+int launch_encode(const EncParams &p, void *stream) {
+    if (!p.n_docs) return OK;
+    const size_t lds = (256 + 4096 + 2 * size_t(p.max_agents)) * 4;
+    hipLaunchKernelGGL(enc::encode_kernel, dim3(p.n_docs), dim3(64), lds, reinterpret_cast<hipStream_t>(stream), p);
+    return hipGetLastError() == hipSuccess ? OK : ErrHip;
+}
+
+}  // namespace dtgpu

@@ -20,6 +20,7 @@
 #include "dt_device.hpp"
 #include "dt_host.hpp"
 #include "dt_prep.hpp"
+#include "dt_encoder.hpp"
 
 using namespace dtgpu;
 
@@ -95,6 +96,15 @@ struct dtgpu_batch {
     PrepParams prep{};
     hipEvent_t ev_dec = nullptr, ev_prep = nullptr;
     float last_decode_ms = 0, last_prep_ms = 0;
+
+    // batched encoder (dtgpu_batch_encode): per-document descriptors, scratch, output
+    std::vector<EncDesc> e_desc;
+    std::vector<EncResult> e_res;
+    DevBuf<EncDesc> e_docs;
+    DevBuf<EncResult> e_dres;
+    DevBuf<uint32_t> e_w;
+    DevBuf<uint8_t> e_b, e_out;
+    EncParams enc{};
 
     ~dtgpu_batch() {
         if (ev_dec) (void)hipEventDestroy(ev_dec);
@@ -1057,6 +1067,102 @@ dtgpu_status dtgpu_batch_run_e2e_timed(dtgpu_batch *B, float ms[4]) {
     if (ms) { ms[0] = td; ms[1] = tp; ms[2] = tl; ms[3] = tr; }
     return DTGPU_OK;
 }
+dtgpu_status dtgpu_batch_encode(dtgpu_batch *B, uint32_t flags, float *kernel_ms) {
+    if (!B || !B->dec || B->xf_mode) return DTGPU_ERR_ARG;
+    if (flags & ~uint32_t(DTGPU_ENCODE_FULL)) return DTGPU_ERR_ARG;
+    if (hipSetDevice(B->device) != hipSuccess) return DTGPU_ERR_HIP;
+    hipStream_t s = B->stream;
+#define CK(x) do { if ((x) != hipSuccess) return DTGPU_ERR_HIP; } while (0)
+    if (B->e_desc.empty() && B->n) {   // layout once per batch
+        const dtgpu_decoded &Dd = *B->dec;
+        B->e_desc.assign(B->n, EncDesc{});
+        uint64_t w = 0, b = 0, o = 0;
+        uint32_t max_agents = 1;
+        for (size_t i = 0; i < B->n; i++) {
+            EncDesc &e = B->e_desc[i];
+            e.skip = 1;
+            if (B->host_status[i] != OK) continue;
+            const DecodeResult &r = Dd.res[i];
+            const DecodeDesc &d = Dd.desc[i];
+            const DocDesc &dd = B->docs[i];
+            e.skip = 0;
+            e.in_off = d.in_off; e.arun_off = d.arun_off; e.ent_off = d.ent_off; e.poff_off = d.poff_off;
+            e.par_off = d.par_off; e.content_off = d.content_off; e.lv_off = d.lv_off; e.agent_off = d.agent_off;
+            e.cmd_off = dd.cmd_off;
+            e.ncmd = dd.ncmd; e.n_aruns = r.n_aruns; e.ne = r.n_entries; e.n_agents = r.n_agents;
+            e.n_lv = uint32_t(r.n_lv); e.n_content = r.n_content;
+            e.doc_id_off = r.doc_id_off; e.doc_id_len = r.doc_id_len;
+            e.w_off = w; w += enc_words(e.ne, e.ncmd, e.n_aruns, e.n_agents);
+            e.b_off = b; b += r.n_content + lz4_bound(r.n_content);
+            // output bound: header + names + doc id + every stream at its widest varints
+            const uint64_t cap = 128 + 11ull * r.n_agents + 64 + (r.doc_id_len != 0xFFFFFFFFu ? r.doc_id_len : 0) +
+                                 30ull * (uint64_t(r.n_aruns) + r.n_entries) + 20ull * e.ncmd + 10ull * r.n_entries +
+                                 10ull * r.n_parents + lz4_bound(r.n_content) + d.in_len;   // names are in the input
+            e.out_off = o; e.out_cap = uint32_t(std::min<uint64_t>(cap, 0xFFFFFFFFull)); o += e.out_cap;
+            max_agents = std::max(max_agents, r.n_agents);
+        }
+        CK(B->e_docs.upload(B->e_desc, s));
+        CK(B->e_dres.alloc(B->n));
+        CK(B->e_w.alloc(std::max<uint64_t>(w, 1)));
+        CK(B->e_b.alloc(std::max<uint64_t>(b, 1)));
+        CK(B->e_out.alloc(std::max<uint64_t>(o, 1)));
+        EncParams &q = B->enc;
+        q.in = Dd.in.p; q.content = Dd.content.p;
+        q.aruns = Dd.aruns.p; q.ent = Dd.ent.p; q.poff = Dd.poff.p; q.par = Dd.par.p; q.cbyte = Dd.cbyte.p;
+        q.agents = Dd.agents.p;
+        q.cmds = B->d_cmds.p;
+        q.w = B->e_w.p; q.b = B->e_b.p; q.out = B->e_out.p;
+        q.docs = B->e_docs.p; q.results = B->e_dres.p;
+        q.n_docs = uint32_t(B->n);
+        q.max_agents = max_agents;
+        q.prof = getenv("DTGPU_ENC_PROF") ? 1u : 0u;
+        for (int k = 0; k < 32; k++) q.x2n[k] = Dd.P.x2n[k];
+    }
+    // the walk order: the planner's commands (prep + plan, as a checkout pass runs them)
+    if (launch_prep(B->prep, s)) return DTGPU_ERR_HIP;
+    if (B->n_gpu_planned && launch_plan(B->plan, s) != OK) return DTGPU_ERR_HIP;
+    B->enc.flags = flags;
+    CK(hipMemsetAsync(B->e_dres.p, 0, std::max<size_t>(B->n, 1) * sizeof(EncResult), s));
+    CK(hipEventRecord(B->ev0, s));
+    if (launch_encode(B->enc, s)) return DTGPU_ERR_HIP;
+    CK(hipEventRecord(B->ev1, s));
+    B->e_res.resize(B->n);
+    CK(hipMemcpyAsync(B->e_res.data(), B->e_dres.p, B->n * sizeof(EncResult), hipMemcpyDeviceToHost, s));
+    CK(hipStreamSynchronize(s));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, B->ev0, B->ev1));
+#undef CK
+    if (kernel_ms) *kernel_ms = ms;
+    return DTGPU_OK;
+}
+
+dtgpu_status dtgpu_batch_encoded(const dtgpu_batch *B, size_t i, uint8_t *out, size_t cap, size_t *out_len,
+                                 uint64_t prof[6]) {
+    if (!B || i >= B->n || B->e_res.size() != B->n) return DTGPU_ERR_ARG;
+    if (B->host_status[i] != OK) return dtgpu_status(B->host_status[i]);
+    const EncResult &r = B->e_res[i];
+    if (r.status != OK) return dtgpu_status(r.status);
+    if (prof) for (int k = 0; k < 6; k++) prof[k] = r.prof[k];
+    if (out_len) *out_len = r.len;
+    if (!out) return DTGPU_OK;
+    if (cap < r.len) return DTGPU_ERR_ARG;
+    if (hipSetDevice(B->device) != hipSuccess) return DTGPU_ERR_HIP;
+    if (hipMemcpy(out, B->e_out.p + B->e_desc[i].out_off, r.len, hipMemcpyDeviceToHost) != hipSuccess) return DTGPU_ERR_HIP;
+    return DTGPU_OK;
+}
+
+uint64_t dtgpu_batch_encoded_bytes(const dtgpu_batch *B, int which) {
+    if (!B || B->e_res.size() != B->n) return 0;
+    uint64_t t = 0;
+    for (size_t i = 0; i < B->n; i++) {
+        if (B->host_status[i] != OK || B->e_res[i].status != OK) continue;
+        const DecodeResult &r = B->dec->res[i];
+        if (which == 0) t += B->e_res[i].len;
+        else t += 16ull * r.n_ops + 8ull * r.n_entries + 4ull * r.n_parents + 16ull * r.n_aruns + r.n_content;
+    }
+    return t;
+}
+
 dtgpu_status dtgpu_batch_run(dtgpu_batch *B, void *stream) {
     if (!B) return DTGPU_ERR_ARG;
     if (hipSetDevice(B->device) != hipSuccess) return DTGPU_ERR_HIP;

@@ -143,6 +143,10 @@ def lib():
     L.dtgpu_batch_create_device.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz), sz,
                                             ctypes.POINTER(BatchOpts), ctypes.POINTER(vp)]
     L.dtgpu_batch_run_e2e_timed.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
+    L.dtgpu_batch_encode.argtypes = [vp, ctypes.c_uint32, ctypes.POINTER(ctypes.c_float)]
+    L.dtgpu_batch_encoded.argtypes = [vp, sz, ctypes.c_char_p, sz, ctypes.POINTER(sz), ctypes.POINTER(ctypes.c_uint64)]
+    L.dtgpu_batch_encoded_bytes.argtypes = [vp, ctypes.c_int]
+    L.dtgpu_batch_encoded_bytes.restype = ctypes.c_uint64
     L.dtgpu_batch_checkout.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz), sz,
                                        ctypes.POINTER(BatchOpts), ctypes.POINTER(DocResult)]
     L.dtgpu_text_hash.argtypes = [ctypes.c_char_p, sz]
@@ -652,6 +656,33 @@ class Batch:
         ms = (ctypes.c_float * 4)()
         _check(lib().dtgpu_batch_run_e2e_timed(self._h, ms))
         return list(ms)
+
+    def encode(self, opts=None) -> float:
+        """Device-staged batches: ListOpLog::encode(opts) from ROOT for every document on the GPU
+        (dtgpu_batch_encode); returns the encode kernel's ms.  Read the bytes with encoded(i)."""
+        ms = ctypes.c_float()
+        _check(lib().dtgpu_batch_encode(self._h, (opts or ENCODE_FULL).flags(), ctypes.byref(ms)))
+        return ms.value
+
+    def encoded(self, i) -> bytes:
+        n = ctypes.c_size_t()
+        _check(lib().dtgpu_batch_encoded(self._h, i, None, 0, ctypes.byref(n), None))
+        buf = ctypes.create_string_buffer(max(1, n.value))
+        _check(lib().dtgpu_batch_encoded(self._h, i, buf, n.value, ctypes.byref(n), None))
+        return buf.raw[:n.value]
+
+    def encoded_status(self, i) -> int:
+        n = ctypes.c_size_t()
+        return lib().dtgpu_batch_encoded(self._h, i, None, 0, ctypes.byref(n), None)
+
+    def encode_profile(self, i):
+        n = ctypes.c_size_t()
+        out = (ctypes.c_uint64 * 6)()
+        _check(lib().dtgpu_batch_encoded(self._h, i, None, 0, ctypes.byref(n), out))
+        return dict(zip(["walk", "records", "sizes", "text_lz4", "write", "crc"], list(out)))
+
+    def encoded_bytes(self, which=0) -> int:
+        return lib().dtgpu_batch_encoded_bytes(self._h, which)
 
     def sync(self):
         _check(lib().dtgpu_batch_sync(self._h))

@@ -311,6 +311,20 @@ const char *dtgpu_status_str(dtgpu_status status);
 dtgpu_status dtgpu_batch_create_device(const uint8_t *const *docs, const size_t *lens, size_t n,
                                        const dtgpu_batch_opts *opts, dtgpu_batch **out);
 dtgpu_status dtgpu_batch_run_e2e_timed(dtgpu_batch *batch, float ms[4]);
+/* Batched ListOpLog::encode(opts) from ROOT (src/list/encoding/encode_oplog.rs:404-747) for every
+ * document of a device-staged batch, on the GPU (dt_encoder.hip): the decoded oplogs and the
+ * planner's walk order (Graph::optimized_txns_between) are read in place, the `.dt` bytes --
+ * LZ4-compressed content, CRC-32C -- are written per document in HBM.  flags: DTGPU_ENCODE_FULL /
+ * DTGPU_ENCODE_PATCH / their bits (the StartBranch is ROOT, so the two presets agree).
+ * *kernel_ms = the encode kernel's time (HIP events).  The bytes equal dtgpu_oplog_encode's. */
+dtgpu_status dtgpu_batch_encode(dtgpu_batch *batch, uint32_t flags, float *kernel_ms);
+/* Document `doc`'s encoded bytes (out == NULL: size in *out_len); the document's status when the
+ * batch did not stage it on the device (e.g. DTGPU_DECODE_DEFER).  prof (may be NULL): per-phase
+ * cycles when DTGPU_ENC_PROF is set. */
+dtgpu_status dtgpu_batch_encoded(const dtgpu_batch *batch, size_t doc, uint8_t *out, size_t cap, size_t *out_len,
+                                 uint64_t prof[6]);
+/* which = 0: encoded bytes written by the last dtgpu_batch_encode; 1: decoded SoA bytes it read */
+uint64_t dtgpu_batch_encoded_bytes(const dtgpu_batch *batch, int which);
 
 /* ---- batched `.dt` decode on the GPU ---------------------------
  * ListOpLog::load_from (src/list/encoding/decode_oplog.rs:447-960) for many documents at once:

@@ -40,3 +40,83 @@ def test_encode_from_full_stores_the_start_branch_checkout(name, frac):
         d = dt_amd.ListOpLog.load_from(o.history(v).encode())
         assert d.decode_and_add(p) == o.local_frontier()
         assert d.checkout_tip_bytes() == o.checkout_tip_bytes()
+
+
+# ---- the batched device encoder (dt_encoder.hip, dtgpu_batch_encode) ------------------------------
+def _unicode_doc(seed):
+    o = dt_amd.ListOpLog()
+    a, b = o.get_or_create_agent_id("ünï"), o.get_or_create_agent_id("agent-β")
+    t1 = o.add_insert(a, 0, "héllo wörld, 日本語のテキスト " * 3)
+    o.add_insert_at(b, [t1], 5, "αβγ" * (seed + 1))
+    o.add_delete_at(a, [t1], 2, 9)
+    o.add_insert(a, 0, "∑ " * 12)
+    o.add_delete_without_content(b, 4, 6)
+    return o
+
+
+@pytest.fixture(scope="module")
+def corpus():
+    docs = [G.dt_bytes(n) for n in G.DT_FILES]
+    docs += [dt_amd.apply_edits_push_merge(G.trace(n)["txns"]).encode() for n in ("sveltecomponent", "friendsforever_flat")]
+    docs += [dt_amd.synth_merge_oplog(d, 3000).encode() for d in range(12)]
+    docs += [dt_amd.synth_oplog(d, 1500).encode(dt_amd.EncodeOptions(True, False, True)) for d in range(4)]
+    docs += [_unicode_doc(s).encode() for s in range(3)]
+    with_id = dt_amd.synth_merge_oplog(99, 800)
+    with_id.doc_id = "doc-ïd-42"
+    docs.append(with_id.encode())
+    empty = dt_amd.ListOpLog()
+    empty.get_or_create_agent_id("nobody")
+    docs.append(empty.encode())
+    tiny = dt_amd.ListOpLog()
+    tiny.add_insert(tiny.get_or_create_agent_id("seph"), 0, "hi")   # content below the 20-byte LZ4 cut
+    docs.append(tiny.encode())
+    return docs
+
+
+@pytest.mark.parametrize("opts", [dt_amd.ENCODE_FULL, dt_amd.EncodeOptions(True, False, True),
+                                  dt_amd.EncodeOptions(False, True, True)], ids=["full", "uncompressed", "no_content"])
+def test_device_encoder_bytes_equal_host_encoder(corpus, opts):
+    b = dt_amd.Batch(docs=corpus, staging="device")
+    ms = b.encode(opts)
+    assert ms > 0
+    for i, d in enumerate(corpus):
+        host = dt_amd.ListOpLog.load_from(d).encode(opts)
+        assert b.encoded(i) == host, i
+
+
+def test_device_encoded_files_check_out_to_the_goldens(corpus):
+    """Re-encoded on the device, decoded by the oracle: same text as the original (friendsforever
+    and the JSON traces: their golden endContent); the LZ4 block decompresses to the walk-order
+    text, a permutation of the inserted content."""
+    b = dt_amd.Batch(docs=corpus[:5], staging="device")
+    b.encode()
+    gold = [json_end("friendsforever_flat")] + [None, None] + [json_end("sveltecomponent"), json_end("friendsforever_flat")]
+    for i, d in enumerate(corpus[:5]):
+        e = b.encoded(i)
+        assert e[9] == 5   # CompressedFieldsLZ4 first
+        ul, block = _lz4_chunk(e)
+        raw = _oracle_lz4_decompress(block, ul)
+        assert sorted(raw) == sorted(bytes(dt_amd.ListOpLog.load_from(d).export("content")))
+        want = gold[i] if gold[i] is not None else OracleOpLog.load_from(d).checkout_tip_bytes()
+        if i != 2:   # node_nodecc: oracle-pinned through the original; the device checks out both
+            assert OracleOpLog.load_from(e).checkout_tip_bytes() == want, i
+        assert dt_amd.ListOpLog.load_from(e).checkout_tip_bytes() == want, i
+
+
+def json_end(name):
+    return G.trace(name)["endContent"].encode()
+
+
+def test_device_encoder_reports_deferred_documents():
+    """A document the batch hands back to the host (DECODE_DEFER: wider than 64 causal chains)
+    gets that status from dtgpu_batch_encoded, not bytes."""
+    wide = dt_amd.synth_merge_oplog(7, 3000, n_agents=80).encode()
+    ok = G.dt_bytes("friendsforever")
+    b = dt_amd.Batch(docs=[ok, wide], staging="device")
+    b.encode()
+    assert b.encoded(0) == dt_amd.ListOpLog.load_from(ok).encode()
+    st = b.encoded_status(1)
+    if st == 0:   # staged on the device after all: then its bytes must be exact too
+        assert b.encoded(1) == dt_amd.ListOpLog.load_from(wide).encode()
+    else:
+        assert st == 80
