@@ -54,6 +54,7 @@ def parse():
                         "capped by the job's CPU share -- cgroup quota / OMP_NUM_THREADS)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-decode", action="store_true", help="skip the end-to-end (.dt bytes -> text) measurement")
+    p.add_argument("--no-encode", action="store_true", help="skip the batched encoder (oplogs -> .dt) measurement")
     p.add_argument("--host-staging", action="store_true", help="decode and prepare planner inputs on host threads")
     return p.parse_args()
 
@@ -208,6 +209,50 @@ def e2e_leg(batch, docs, steps, expect, total_lv):
             "encoded_bytes": enc, "roofline_bytes": basis,
             "achieved_GBps": basis / (total / 1000.0) / 1e9, "frac_hbm": basis / (total / 1000.0) / 1e9 / HBM_PEAK_GBS,
             "basis": "SURVEY.md 8d E2E: |.dt bytes| + |text out| per document; kernel time of decode + prep + plan + replay"}
+
+
+def encode_leg(batch, docs, steps, cpu_budget_s, cores):
+    """SURVEY.md 8(f)2, the `.dt` encoder: ListOpLog::encode(ENCODE_FULL) from ROOT for every
+    document of the resident batch on the GPU (dt_encoder.hip: records kernel + LZ4/write
+    kernel, HIP events), bytes checked against the host encoder on the first and last document.
+    Roofline basis: decoded SoA bytes read + `.dt` bytes written.  CPU baseline: the host encoder
+    (C++ restatement of encode_oplog.rs + lz4_flex's compressor) on a bounded sample, one
+    document per host thread."""
+    import dt_amd
+    ms = [batch.encode() for _ in range(max(1, steps))]
+    n_docs = len(docs)
+    for i in (0, n_docs - 1):
+        assert batch.encoded(i) == dt_amd.ListOpLog.load_from(docs[i]).encode(), "device encoder bytes differ from the host encoder's"
+
+    out_b, in_b = batch.encoded_bytes(0), batch.encoded_bytes(1)
+    t = statistics.mean(ms)
+    logs = [dt_amd.ListOpLog.load_from(d) for d in docs[:8]]
+    t0 = time.perf_counter()
+    logs[0].encode()
+    one = time.perf_counter() - t0
+    if cores <= 0:
+        cores, _ = host_threads()
+    per = max(1, int(cpu_budget_s / max(one, 1e-4) / cores))
+    done = [0] * cores
+
+    def work(k):
+        for i in range(per):
+            logs[(k + i) % len(logs)].encode()
+            done[k] += 1
+    th = [threading.Thread(target=work, args=(k,)) for k in range(cores)]
+    t0 = time.perf_counter()
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    wall = time.perf_counter() - t0
+    return {"kernel_ms": t, "docs_per_s": n_docs / (t / 1000.0), "encoded_bytes": out_b, "soa_bytes_read": in_b,
+            "achieved_GBps": (out_b + in_b) / (t / 1000.0) / 1e9,
+            "frac_hbm": (out_b + in_b) / (t / 1000.0) / 1e9 / HBM_PEAK_GBS,
+            "checked": "bytes of documents 0 and n-1 equal dtgpu_oplog_encode (host)",
+            "cpu_baseline": {"docs_per_s": sum(done) / wall, "cores": cores, "kind": "port",
+                             "sample": f"{sum(done)} host encodes (dtgpu_oplog_encode, ENCODE_FULL) on {cores} threads, "
+                                       f"{wall:.2f} s"}}
 
 
 def workload_pool(args):
@@ -417,6 +462,8 @@ def main():
         out["rebalance"] = rebalance
     if not args.no_decode and staging == "device":   # .dt bytes -> text, all on the GPU
         out["e2e"] = e2e_leg(batch, docs, min(args.steps, 5), want, total_lv_mine)
+    if not args.no_encode and staging == "device" and rank == 0:   # oplogs -> .dt bytes on the GPU
+        out["encode"] = encode_leg(batch, docs, min(args.steps, 5), 3.0, args.cpu_cores)
     if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(pool, args.cpu_seconds, args.cpu_cores, args.workload)
         out["single_doc_latency"] = single_doc_latency(pool[0], gpu, staging)

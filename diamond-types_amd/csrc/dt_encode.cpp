@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <map>
 
 namespace dtgpu {
 
@@ -241,20 +242,24 @@ Status encode_dt(const HostOpLog &o, const std::vector<uint64_t> &from, bool sto
         kr_have = true; kr_val = val; kr_len = len;
     };
     // ---- parents ----
-    struct TxnMap { uint64_t start, end, out; };
-    std::vector<TxnMap> txn_map;   // LV range -> output range start (ascending LV after sort)
+    struct TxnMap { uint64_t end, out; };
+    std::map<uint64_t, TxnMap> txn_map;   // written txns: LV start -> (end, output start)
     std::vector<uint8_t> txns_chunk;
     uint64_t next_out = 0;
     bool tx_have = false;
     uint64_t tx_s = 0, tx_e = 0;
     std::vector<uint64_t> tx_par;
     auto find_local = [&](uint64_t p, uint64_t &mapped) -> bool {
-        for (const TxnMap &m : txn_map) if (p >= m.start && p < m.end) { mapped = m.out + (p - m.start); return true; }
-        return false;
+        auto it = txn_map.upper_bound(p);
+        if (it == txn_map.begin()) return false;
+        --it;
+        if (p >= it->second.end) return false;
+        mapped = it->second.out + (p - it->first);
+        return true;
     };
     auto tx_write = [&]() {
         const uint64_t len = tx_e - tx_s, out0 = next_out;
-        txn_map.push_back(TxnMap{tx_s, tx_e, out0});
+        txn_map.emplace(tx_s, TxnMap{tx_e, out0});
         next_out += len;
         leb(txns_chunk, len);
         if (tx_par.empty()) { leb(txns_chunk, 1); return; }   // ROOT: foreign agent 0

@@ -138,83 +138,153 @@ DEV uint32_t ld32(const uint8_t *p) {
 }
 DEV uint64_t ld64(const uint8_t *p) { return uint64_t(ld32(p)) | (uint64_t(ld32(p + 4)) << 32); }
 
+// sum_{i < x} (i >> 5): the miss loop's probe offsets in closed form (step = nmc >> 5, nmc += 1)
+DEV uint64_t probe_sum(uint64_t x) {
+    const uint64_t q = x >> 5, r = x & 31;
+    return 16 * q * (q - (q ? 1 : 0)) + r * q;
+}
+
+typedef __attribute__((address_space(3))) uint16_t LDS16;
+typedef __attribute__((address_space(3))) uint32_t LDS32;
+
+constexpr uint32_t LZ_RING = 512;   // LDS staging of the compressed bytes (flushed to HBM)
+
 struct Lz {
-    const uint8_t *in;
-    uint8_t *out;
-    uint32_t n, o;
-    bool small;
+    const uint8_t *in;   // the text: LDS or HBM (one address space per instantiation site)
+    uint8_t *out;        // HBM
+    uint8_t *ring;       // LDS, LZ_RING bytes
+    uint32_t n, o, f;    // text length, bytes emitted, bytes flushed
+    bool small, prof;
+    uint32_t st[4];      // profile: probe steps, steps with shared hashes, sequences, -
+    uint64_t cyc[3];     // profile: cycles in probing, extending, emitting
     uint32_t *tab;   // LDS: 8,192 u16 (small) or 4,096 u32
     DEV uint32_t hash(uint32_t p) const {
         if (small) return (ld32(in + p) * 2654435761u) >> 19;
         return uint32_t(((ld64(in + p) << 24) * 889523592379ull) >> 52);
     }
-    DEV uint32_t get(uint32_t h) const {
-        return small ? uint32_t(reinterpret_cast<const uint16_t *>(tab)[h]) : tab[h];
+    // volatile LDS (address space 3) accesses: ds ops that are never forwarded or merged
+    DEV uint32_t vget(uint32_t h) const {
+        return small ? uint32_t(((volatile LDS16 *)tab)[h]) : ((volatile LDS32 *)tab)[h];
     }
-    DEV void put(uint32_t h, uint32_t v) {
-        if (small) reinterpret_cast<uint16_t *>(tab)[h] = uint16_t(v);
-        else tab[h] = v;
+    DEV void vput(uint32_t h, uint32_t v) {
+        if (small) ((volatile LDS16 *)tab)[h] = uint16_t(v);
+        else ((volatile LDS32 *)tab)[h] = v;
+    }
+    // the output goes through the LDS ring, so the parse never waits on HBM stores (vmcnt)
+    DEV void flush() {
+        for (uint32_t i = f + lane(); i < o; i += 64) out[i] = ring[i & (LZ_RING - 1)];
+        f = o;
+    }
+    DEV void reserve(uint32_t k) {   // k <= 128
+        if (o + k - f > LZ_RING) flush();
+    }
+    DEV void put1(uint8_t v) {
+        reserve(1);
+        if (lane() == 0) ring[o & (LZ_RING - 1)] = v;
+        o++;
     }
     DEV void ext(uint32_t v) {   // 255-run length extension
         const uint32_t nb = v / 255 + 1;
-        for (uint32_t i = lane(); i < nb; i += 64) out[o + i] = i + 1 < nb ? 255 : uint8_t(v - 255 * (nb - 1));
-        o += nb;
+        for (uint32_t x = 0; x < nb; x += 64) {
+            const uint32_t k = min(64u, nb - x);
+            reserve(k);
+            if (lane() < k) ring[(o + lane()) & (LZ_RING - 1)] = x + lane() + 1 < nb ? 255 : uint8_t(v - 255 * (nb - 1));
+            o += k;
+        }
     }
     DEV void emit(uint32_t l0, uint32_t l1, uint32_t off, uint32_t mlen) {
         const uint32_t ll = l1 - l0;
-        if (lane() == 0) out[o] = uint8_t((min(ll, 15u) << 4) | (off ? min(mlen - 4, 15u) : 0u));
-        o++;
+        put1(uint8_t((min(ll, 15u) << 4) | (off ? min(mlen - 4, 15u) : 0u)));
         if (ll >= 15) ext(ll - 15);
-        for (uint32_t i = lane(); i < ll; i += 64) out[o + i] = in[l0 + i];
-        o += ll;
+        for (uint32_t x = 0; x < ll; x += 64) {
+            const uint32_t k = min(64u, ll - x);
+            reserve(k);
+            if (lane() < k) ring[(o + lane()) & (LZ_RING - 1)] = in[l0 + x + lane()];
+            o += k;
+        }
         if (!off) return;
-        if (lane() == 0) { out[o] = uint8_t(off); out[o + 1] = uint8_t(off >> 8); }
-        o += 2;
+        put1(uint8_t(off));
+        put1(uint8_t(off >> 8));
         if (mlen - 4 >= 15) ext(mlen - 19);
     }
     DEV uint32_t run() {
-        o = 0;
+        o = f = 0;
         small = n < 65535;
+        st[0] = st[1] = st[2] = st[3] = 0;
+        cyc[0] = cyc[1] = cyc[2] = 0;
+        uint64_t tc = prof ? clock64() : 0;
+        auto tick = [&](int k) {
+            if (prof) { const uint64_t t = clock64(); cyc[k] += t - tc; tc = t; }
+        };
         for (uint32_t i = lane(); i < 4096; i += 64) tab[i] = 0;
-        if (n < 13) { emit(0, n, 0, 0); return o; }
+        if (n < 13) { emit(0, n, 0, 0); flush(); return o; }
         const uint32_t end_check = n - 12, match_lim = n - 6;
         uint32_t lit = 0, cur = 1;   // position 0 is hashed first: its entry is the table's zero
         const uint32_t l = lane();
         for (;;) {
             uint32_t nmc = 32, pos = cur, cand = 0;
             bool found = false;
-            for (;;) {   // 64 probes of the miss loop
-                const uint32_t step = (nmc + l) >> 5;
-                const uint32_t p = pos + scan_incl(step) - step;
-                const bool valid = p <= end_check;
+            // probes of the miss loop: 16 in the first step (a match is usually a few bytes
+            // away: fewer shared hashes to resolve), 64 in later ones
+            for (uint32_t width = 16;; width = 64) {
+                const uint64_t base = probe_sum(nmc);
+                const uint32_t p = pos + uint32_t(probe_sum(nmc + l) - base);
+                const bool valid = l < width && p <= end_check;
                 const uint32_t nv = popc(ballot(valid));   // valid probes form a prefix
                 const uint32_t h = valid ? hash(p) : 0xFFFFFFFFu;
-                int prevj = -1;
-                uint32_t nextj = 64;
-                for (uint32_t j = 0; j < nv; j++) {
-                    const uint32_t hj = rdl(h, j);
-                    if (hj == h) {
-                        if (j < l) prevj = int(j);
-                        else if (j > l && nextj == 64) nextj = j;
+                // every probe writes its position into its slot and reads the slot back: when
+                // each probe won its own slot, no two probes share a hash and the table held
+                // every candidate (volatile: the read-back must see the other lanes' writes)
+                const uint32_t old = valid ? vget(h) : 0u;
+                if (valid) vput(h, p);
+                const bool won = !valid || vget(h) == p;
+                uint32_t c, lim;
+                uint64_t m;
+                st[0]++;
+                if (!ballot(!won)) {
+                    c = old;
+                    const bool ok = valid && p - c <= 65535u && ld32(in + c) == ld32(in + p);
+                    m = ballot(ok);
+                    lim = m ? ctz(m) + 1 : nv;
+                    if (valid && l >= lim) vput(h, old);   // probes past the match never ran
+                } else {   // shared hashes: a probe's candidate is the last earlier probe of its hash
+                    st[1]++;
+                    if (valid) vput(h, old);
+                    // one ballot per contested hash: each group lost at least one slot write
+                    uint64_t lost = ballot(!won);
+                    int prevj = -1;
+                    uint32_t nextj = 64;
+                    while (lost) {
+                        const uint32_t hj = rdl(h, ctz(lost));
+                        const bool mine = valid && h == hj;
+                        const uint64_t g = ballot(mine);
+                        if (mine) {
+                            const uint64_t below = g & lt_mask(), above = g & ~lt_mask() & ~(1ull << l);
+                            prevj = below ? int(63 - __clzll((long long)below)) : -1;
+                            nextj = above ? ctz(above) : 64;
+                        }
+                        lost &= ~g;
                     }
+                    const uint32_t pp = uint32_t(__shfl(int(p), prevj < 0 ? int(l) : prevj));
+                    c = prevj >= 0 ? pp : old;
+                    const bool ok = valid && p - c <= 65535u && ld32(in + c) == ld32(in + p);
+                    m = ballot(ok);
+                    lim = m ? ctz(m) + 1 : nv;
+                    if (l < lim && nextj >= lim) vput(h, p);   // the last probe of each hash wins
                 }
-                const uint32_t pp = uint32_t(__shfl(int(p), prevj < 0 ? int(l) : prevj));
-                const uint32_t c = prevj >= 0 ? pp : (valid ? get(h) : 0u);
-                const bool ok = valid && p - c <= 65535u && ld32(in + c) == ld32(in + p);
-                const uint64_t m = ballot(ok);
-                const uint32_t lim = m ? ctz(m) + 1 : nv;
-                if (l < lim && nextj >= lim) put(h, p);   // the last probe of each hash wins
                 if (m) {
                     cur = rdl(p, lim - 1);
                     cand = rdl(c, lim - 1);
                     found = true;
                     break;
                 }
-                if (nv < 64) break;
-                pos = rdl(p, 63) + rdl(step, 63);
-                nmc += 64;
+                if (nv < width) break;   // past len - 12: the tail is literals
+                pos += uint32_t(probe_sum(nmc + width) - base);
+                nmc += width;
             }
-            if (!found) { emit(lit, n, 0, 0); return o; }
+            tick(0);
+            if (!found) { emit(lit, n, 0, 0); flush(); return o; }
+            st[2]++;
             for (;;) {   // extend backwards over the pending literals
                 const uint32_t mb = min(cur - lit, cand);
                 const bool eq = l < mb && in[cur - 1 - l] == in[cand - 1 - l];
@@ -236,9 +306,11 @@ struct Lz {
                 if (b < 64) break;
             }
             const uint32_t h2 = hash(cur - 2);
-            if (l == 0) put(h2, cur - 2);
+            if (l == 0) vput(h2, cur - 2);
+            tick(1);
             emit(lit, m0, off, cur - m0);
             lit = cur;
+            tick(2);
         }
     }
 };
@@ -284,7 +356,32 @@ struct Layout {   // byte offsets of the streams in the output
     uint32_t aa, ops, tx, names, text, known, lz, total;
 };
 
-__global__ __launch_bounds__(64) void encode_kernel(EncParams P) {
+// tx_record(t, dst): txn t's bytes (len, then parents as output-order distances, all local from
+// ROOT); dst == nullptr counts them
+#define ENC_TX_RECORD \
+    auto tx_record = [&](uint32_t t, uint32_t ntx_, uint8_t *dst) -> uint32_t { \
+        const uint32_t e = worder[heads[t]]; \
+        const uint32_t out0 = outpos[e]; \
+        const uint32_t nxt = t + 1 < ntx_ ? outpos[worder[heads[t + 1]]] : D.n_lv; \
+        uint32_t nb = dst ? put_leb(dst, nxt - out0) : leb_len(nxt - out0); \
+        const uint32_t p0 = poff[e], np = poff[e + 1] - p0; \
+        if (np == 0) { \
+            if (dst) dst[nb] = 1; \
+            return nb + 1; \
+        } \
+        for (uint32_t j = 0; j < np; j++) { \
+            const uint32_t p = par[p0 + j]; \
+            const uint32_t pe = min(entry_of(ent, ne, p), ne - 1); \
+            const uint32_t mp = outpos[pe] + (p - ent[pe].x); \
+            const uint64_t v = (uint64_t(out0 - mp) * 2 + (j + 1 < np ? 1 : 0)) * 2; \
+            nb += dst ? put_leb(dst + nb, v) : leb_len(v); \
+        } \
+        return nb; \
+    }; \
+    do {} while (0);
+
+// Kernel 1: A walk, B records, C sizes, D text -- small LDS (the agent map), high occupancy.
+__global__ __launch_bounds__(64) void encode_records_kernel(EncParams P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t doc = blockIdx.x;
     if (doc >= P.n_docs) return;
@@ -296,17 +393,10 @@ __global__ __launch_bounds__(64) void encode_kernel(EncParams P) {
     auto mark = [&](int i) {
         if (P.prof) { const uint64_t t = clock64(); R.prof[i] = t - t_prev; t_prev = t; }
     };
-    uint32_t *T = lds;                       // CRC table (256)
-    uint32_t *tab = lds + 256;               // LZ4 hash table (4,096 words)
-    uint32_t *amap = lds + 256 + 4096;       // agent -> mapped id (0: not yet), max_agents
+    uint32_t *amap = lds;                    // agent -> mapped id (0: not yet), max_agents
     uint32_t *alast = amap + P.max_agents;   // agent -> end of its last seq range written
-    for (uint32_t i = l; i < 256; i += 64) {
-        uint32_t c = i;
-        for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ CRC_POLY : c >> 1;
-        T[i] = c;
-    }
     for (uint32_t i = l; i < D.n_agents; i += 64) { amap[i] = 0; alast[i] = 0; }
-
+#define ENC_UNUSED (void)in; (void)lzb; (void)out; (void)compress; (void)store_text;
     const uint8_t *in = P.in + D.in_off;
     const uint4 *ar = reinterpret_cast<const uint4 *>(P.aruns) + D.arun_off;
     const uint2 *ent = reinterpret_cast<const uint2 *>(P.ent) + D.ent_off;
@@ -324,7 +414,8 @@ __global__ __launch_bounds__(64) void encode_kernel(EncParams P) {
     uint8_t *text = P.b + D.b_off, *lzb = text + D.n_content;
     uint8_t *out = P.out + D.out_off;
     const bool store_text = P.flags & 1u, compress = P.flags & 2u;
-
+    ENC_TX_RECORD
+    ENC_UNUSED
     // ---- A: the walk ---------------------------------------------------------------------------
     uint32_t nw = 0, opos = 0;
     for (uint32_t c0 = 0; c0 < ncmd; c0 += 64) {
@@ -516,28 +607,8 @@ __global__ __launch_bounds__(64) void encode_kernel(EncParams P) {
     }
     op_bytes = wave_sum(op_bytes);
     text_len = store_text ? wave_sum(text_len) : 0;
-    // txns: len, then parents as output-order distances (all local from ROOT)
-    auto tx_record = [&](uint32_t t, uint8_t *dst) -> uint32_t {
-        const uint32_t e = worder[heads[t]];
-        const uint32_t out0 = outpos[e];
-        const uint32_t nxt = t + 1 < ntx ? outpos[worder[heads[t + 1]]] : D.n_lv;
-        uint32_t nb = dst ? put_leb(dst, nxt - out0) : leb_len(nxt - out0);
-        const uint32_t p0 = poff[e], np = poff[e + 1] - p0;
-        if (np == 0) {
-            if (dst) dst[nb] = 1;
-            return nb + 1;
-        }
-        for (uint32_t j = 0; j < np; j++) {
-            const uint32_t p = par[p0 + j];
-            const uint32_t pe = min(entry_of(ent, ne, p), ne - 1);
-            const uint32_t mp = outpos[pe] + (p - ent[pe].x);
-            const uint64_t v = (uint64_t(out0 - mp) * 2 + (j + 1 < np ? 1 : 0)) * 2;
-            nb += dst ? put_leb(dst + nb, v) : leb_len(v);
-        }
-        return nb;
-    };
     for (uint32_t t0 = 0; t0 < ntx; t0 += 64)
-        if (t0 + l < ntx) tx_bytes += tx_record(t0 + l, nullptr);
+        if (t0 + l < ntx) tx_bytes += tx_record(t0 + l, ntx, nullptr);
     tx_bytes = wave_sum(tx_bytes);
     for (uint32_t i = l; i < n_mapped; i += 64) {
         const uint32_t nl = names[ainv[i]].y;
@@ -570,16 +641,85 @@ __global__ __launch_bounds__(64) void encode_kernel(EncParams P) {
             return;
         }
     }
+    R.status = ST_OK;
+    R.n_op_runs = nop;
+    R.n_agent_runs = naa;
+    R.n_txns = ntx;
+    R.text_len = text_len;
+    R.n_mapped = n_mapped;
+    R.aa_bytes = aa_bytes;
+    R.op_bytes = op_bytes;
+    R.tx_bytes = tx_bytes;
+    R.nm_bytes = nm_bytes;
+    R.n_ins = n_ins;
+    R.stage = 1;
+    if (l == 0) P.results[doc] = R;
+}
+
+// Kernel 2: E LZ4 (the text staged in LDS when it fits), F write, G CRC.
+__global__ __launch_bounds__(64) void encode_write_kernel(EncParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const uint32_t doc = blockIdx.x;
+    if (doc >= P.n_docs) return;
+    const EncDesc D = P.docs[doc];
+    if (D.skip) return;
+    EncResult R = P.results[doc];
+    if (R.status != ST_OK || R.stage != 1) return;
+    const uint32_t l = lane();
+    uint64_t t_prev = P.prof ? clock64() : 0;
+    auto mark = [&](int i) {
+        if (P.prof) { const uint64_t t = clock64(); R.prof[i] = t - t_prev; t_prev = t; }
+    };
+    uint32_t *tab = lds;                     // LZ4 hash table (4,096 words), then the CRC table
+    uint8_t *lring = reinterpret_cast<uint8_t *>(lds + 4096);                 // LZ4 output staging
+    uint8_t *ltext = reinterpret_cast<uint8_t *>(lds + 4096 + LZ_RING / 4);   // the text, when it fits
+    const uint8_t *in = P.in + D.in_off;
+    const uint4 *ar = reinterpret_cast<const uint4 *>(P.aruns) + D.arun_off;
+    const uint2 *ent = reinterpret_cast<const uint2 *>(P.ent) + D.ent_off;
+    const uint32_t *poff = P.poff + D.poff_off, *par = P.par + D.par_off;
+    const uint8_t *content = P.content + D.content_off;
+    const uint32_t *cbyte = P.cbyte + D.lv_off;
+    const uint2 *names = reinterpret_cast<const uint2 *>(P.agents) + D.agent_off;
+    const Cmd *cmds = P.cmds + D.cmd_off;
+    const uint32_t ne = D.ne, ncmd = D.ncmd;
+    uint32_t *worder = P.w + D.w_off, *outpos = worder + ne;
+    uint32_t *oprec = outpos + ne;                          // 8 words per op run
+    uint32_t *aarec = oprec + 8ull * ncmd;                  // 4 words per agent run
+    uint32_t *heads = aarec + 4ull * (D.n_aruns + ne);      // walk index of each txn head
+    uint32_t *ainv = heads + ne;                            // mapped id - 1 -> agent
+    uint8_t *text = P.b + D.b_off, *lzb = text + D.n_content;
+    uint8_t *out = P.out + D.out_off;
+    const bool store_text = P.flags & 1u, compress = P.flags & 2u;
+    ENC_TX_RECORD
+    const uint32_t nop = R.n_op_runs, naa = R.n_agent_runs, ntx = R.n_txns, text_len = R.text_len;
+    const uint32_t n_mapped = R.n_mapped, aa_bytes = R.aa_bytes, op_bytes = R.op_bytes, tx_bytes = R.tx_bytes;
+    const uint32_t nm_bytes = R.nm_bytes, n_ins = R.n_ins;
+    (void)cmds; (void)cbyte; (void)content; (void)ar;
+    ENC_UNUSED
     const bool use_lz = compress && text_len >= 20;
     uint32_t lz_len = 0;
     if (use_lz) {
         wave_fence();
         Lz z;
-        z.in = text;
+        z.prof = P.prof;
         z.out = lzb;
+        z.ring = lring;
         z.n = text_len;
         z.tab = tab;
-        lz_len = z.run();
+        if (text_len <= P.lds_text) {   // stage the text in LDS (16-byte copies); ds reads from here on
+            const uint4 *g = reinterpret_cast<const uint4 *>(text);
+            uint4 *d = reinterpret_cast<uint4 *>(ltext);
+            for (uint32_t i = l; i < (text_len + 15) / 16; i += 64) d[i] = g[i];
+            z.in = ltext;
+            lz_len = z.run();
+        } else {
+            z.in = text;
+            lz_len = z.run();
+        }
+        if (P.prof) {
+            for (int k = 0; k < 3; k++) R.lzcyc[k] = z.cyc[k];
+            for (int k = 0; k < 3; k++) R.lzst[k] = z.st[k];
+        }
     }
     wave_fence();
     R.lz_len = lz_len;
@@ -763,9 +903,9 @@ __global__ __launch_bounds__(64) void encode_kernel(EncParams P) {
         uint32_t base = L.tx;
         for (uint32_t t0 = 0; t0 < ntx; t0 += 64) {
             const uint32_t t = t0 + l;
-            const uint32_t nb = t < ntx ? tx_record(t, nullptr) : 0;
+            const uint32_t nb = t < ntx ? tx_record(t, ntx, nullptr) : 0;
             const uint32_t incl = scan_incl(nb);
-            if (t < ntx) tx_record(t, out + base + incl - nb);
+            if (t < ntx) tx_record(t, ntx, out + base + incl - nb);
             base += rdl(incl, 63);
         }
     }
@@ -773,6 +913,12 @@ __global__ __launch_bounds__(64) void encode_kernel(EncParams P) {
     mark(4);
 
     // ---- G: CRC chunk --------------------------------------------------------------------------------
+    uint32_t *T = tab;
+    for (uint32_t i = l; i < 256; i += 64) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ CRC_POLY : c >> 1;
+        T[i] = c;
+    }
     const uint32_t crc = crc32c_par(out, L.total - 6, T, P.x2n);
     if (l == 0) {
         uint8_t *p = out + L.total - 6;
@@ -795,8 +941,10 @@ __global__ __launch_bounds__(64) void encode_kernel(EncParams P) {
 
 int launch_encode(const EncParams &p, void *stream) {
     if (!p.n_docs) return OK;
-    const size_t lds = (256 + 4096 + 2 * size_t(p.max_agents)) * 4;
-    hipLaunchKernelGGL(enc::encode_kernel, dim3(p.n_docs), dim3(64), lds, reinterpret_cast<hipStream_t>(stream), p);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(enc::encode_records_kernel, dim3(p.n_docs), dim3(64), 2 * size_t(p.max_agents) * 4, s, p);
+    if (hipGetLastError() != hipSuccess) return ErrHip;
+    hipLaunchKernelGGL(enc::encode_write_kernel, dim3(p.n_docs), dim3(64), 4096 * 4 + enc::LZ_RING + size_t(p.lds_text + 15) / 16 * 16, s, p);
     return hipGetLastError() == hipSuccess ? OK : ErrHip;
 }
 

@@ -32,8 +32,11 @@ struct EncDesc {
 
 struct EncResult {
     uint32_t status, len;
-    uint32_t n_op_runs, n_agent_runs, n_txns, text_len, lz_len, pad;
+    uint32_t n_op_runs, n_agent_runs, n_txns, text_len, lz_len, stage;
+    uint32_t n_mapped, aa_bytes, op_bytes, tx_bytes, nm_bytes, n_ins;   // kernel 1 -> kernel 2
     uint64_t prof[6];       // cycles: walk, records, sizes, text + LZ4, write, CRC
+    uint64_t lzcyc[3];      // LZ4 cycles: probing, extending, emitting
+    uint32_t lzst[4];       // LZ4 counts: probe steps, steps with shared hashes, sequences, -
 };
 
 struct EncParams {
@@ -45,6 +48,7 @@ struct EncParams {
     const EncDesc *docs;
     EncResult *results;
     uint32_t n_docs, flags, max_agents, prof;
+    uint32_t lds_text, pad;   // text bytes kernel 2 stages in LDS (LZ4 input)
     uint32_t x2n[32];       // x^(2^k) mod the CRC-32C polynomial
 };
 

@@ -1077,7 +1077,7 @@ dtgpu_status dtgpu_batch_encode(dtgpu_batch *B, uint32_t flags, float *kernel_ms
         const dtgpu_decoded &Dd = *B->dec;
         B->e_desc.assign(B->n, EncDesc{});
         uint64_t w = 0, b = 0, o = 0;
-        uint32_t max_agents = 1;
+        uint32_t max_agents = 1, max_text = 0;
         for (size_t i = 0; i < B->n; i++) {
             EncDesc &e = B->e_desc[i];
             e.skip = 1;
@@ -1093,13 +1093,14 @@ dtgpu_status dtgpu_batch_encode(dtgpu_batch *B, uint32_t flags, float *kernel_ms
             e.n_lv = uint32_t(r.n_lv); e.n_content = r.n_content;
             e.doc_id_off = r.doc_id_off; e.doc_id_len = r.doc_id_len;
             e.w_off = w; w += enc_words(e.ne, e.ncmd, e.n_aruns, e.n_agents);
-            e.b_off = b; b += r.n_content + lz4_bound(r.n_content);
+            e.b_off = b; b += (r.n_content + lz4_bound(r.n_content) + 15) / 16 * 16;   // 16-B aligned text
             // output bound: header + names + doc id + every stream at its widest varints
             const uint64_t cap = 128 + 11ull * r.n_agents + 64 + (r.doc_id_len != 0xFFFFFFFFu ? r.doc_id_len : 0) +
                                  30ull * (uint64_t(r.n_aruns) + r.n_entries) + 20ull * e.ncmd + 10ull * r.n_entries +
                                  10ull * r.n_parents + lz4_bound(r.n_content) + d.in_len;   // names are in the input
             e.out_off = o; e.out_cap = uint32_t(std::min<uint64_t>(cap, 0xFFFFFFFFull)); o += e.out_cap;
             max_agents = std::max(max_agents, r.n_agents);
+            max_text = std::max(max_text, r.n_content);
         }
         CK(B->e_docs.upload(B->e_desc, s));
         CK(B->e_dres.alloc(B->n));
@@ -1115,6 +1116,13 @@ dtgpu_status dtgpu_batch_encode(dtgpu_batch *B, uint32_t flags, float *kernel_ms
         q.docs = B->e_docs.p; q.results = B->e_dres.p;
         q.n_docs = uint32_t(B->n);
         q.max_agents = max_agents;
+        // kernel 2 stages a document's text in LDS for the LZ4 pass when it fits: 16 KiB of hash
+        // table + 512 B of output ring + <= 23.5 KiB of text keeps 4 waves per CU
+        // measured (10k friendsforever): 60 ms with the text in LDS (4 waves per CU), 44 ms with
+        // it read from HBM at 9 waves per CU -- occupancy wins in a batch, so staging is opt-in
+        q.lds_text = 0;
+        (void)max_text;
+        if (const char *e = getenv("DTGPU_ENC_LDS_TEXT")) q.lds_text = std::min<uint32_t>(uint32_t(strtoul(e, nullptr, 10)), 24064);
         q.prof = getenv("DTGPU_ENC_PROF") ? 1u : 0u;
         for (int k = 0; k < 32; k++) q.x2n[k] = Dd.P.x2n[k];
     }
@@ -1137,12 +1145,16 @@ dtgpu_status dtgpu_batch_encode(dtgpu_batch *B, uint32_t flags, float *kernel_ms
 }
 
 dtgpu_status dtgpu_batch_encoded(const dtgpu_batch *B, size_t i, uint8_t *out, size_t cap, size_t *out_len,
-                                 uint64_t prof[6]) {
+                                 uint64_t prof[12]) {
     if (!B || i >= B->n || B->e_res.size() != B->n) return DTGPU_ERR_ARG;
     if (B->host_status[i] != OK) return dtgpu_status(B->host_status[i]);
     const EncResult &r = B->e_res[i];
     if (r.status != OK) return dtgpu_status(r.status);
-    if (prof) for (int k = 0; k < 6; k++) prof[k] = r.prof[k];
+    if (prof) {
+        for (int k = 0; k < 6; k++) prof[k] = r.prof[k];
+        for (int k = 0; k < 3; k++) prof[6 + k] = r.lzcyc[k];
+        for (int k = 0; k < 3; k++) prof[9 + k] = r.lzst[k];
+    }
     if (out_len) *out_len = r.len;
     if (!out) return DTGPU_OK;
     if (cap < r.len) return DTGPU_ERR_ARG;

@@ -319,10 +319,12 @@ dtgpu_status dtgpu_batch_run_e2e_timed(dtgpu_batch *batch, float ms[4]);
  * *kernel_ms = the encode kernel's time (HIP events).  The bytes equal dtgpu_oplog_encode's. */
 dtgpu_status dtgpu_batch_encode(dtgpu_batch *batch, uint32_t flags, float *kernel_ms);
 /* Document `doc`'s encoded bytes (out == NULL: size in *out_len); the document's status when the
- * batch did not stage it on the device (e.g. DTGPU_DECODE_DEFER).  prof (may be NULL): per-phase
- * cycles when DTGPU_ENC_PROF is set. */
+ * batch did not stage it on the device (e.g. DTGPU_DECODE_DEFER).  prof (may be NULL), when
+ * DTGPU_ENC_PROF is set: cycles per phase (walk, records, sizes, text + LZ4, write, CRC), LZ4
+ * cycles (probing, extending, emitting) and counts (probe steps, steps with shared hashes,
+ * sequences). */
 dtgpu_status dtgpu_batch_encoded(const dtgpu_batch *batch, size_t doc, uint8_t *out, size_t cap, size_t *out_len,
-                                 uint64_t prof[6]);
+                                 uint64_t prof[12]);
 /* which = 0: encoded bytes written by the last dtgpu_batch_encode; 1: decoded SoA bytes it read */
 uint64_t dtgpu_batch_encoded_bytes(const dtgpu_batch *batch, int which);
 
