@@ -11,7 +11,8 @@ of B ops whose first member has the A parents) and other B ops hang off A ops.  
 onto A must then give back A's own causal order: the same ops keyed by (agent, seq) with the same
 parents, so the oracle's checkout of the rebuilt projection equals its checkout of A.  Parity is
 anchored on the oracle's checkout of A (itself pinned on the reference's golden vectors); the
-multi-CRDT container itself is "parity unpinned" (no reference fixture holds one).
+multi-CRDT container itself is "parity unpinned" (no reference fixture holds one).  The projection
+is pinned by the reference's own subgraph KATs (subgraph.rs:353-380 over fancy_graph, below).
 """
 import random
 
@@ -177,3 +178,68 @@ def test_gpu_checkout_text(seed):
         c, a_spans, b_spans, n_b = _interleave(a, seed)
         assert c.checkout_text_bytes(a_spans) == want, name
         assert c.checkout_text_bytes(b_spans) == b"x" * n_b, name
+
+
+# ---- Graph::subgraph KATs (src/causalgraph/graph/subgraph.rs:353-380, test_subgraph) -------------
+# fancy_graph (graph/tools.rs:903-919): 0..3 and 3..6 from ROOT, 6..9 after [1, 4], 9..11 after
+# [2, 8].  check_subgraph(filter, frontier, parents of each subgraph entry, projected frontier);
+# the reference keeps LV numbering, libdtgpu compacts it (history at `frontier`, then the
+# projection), so the expectations are mapped through both compactions.
+FANCY = [(0, 3, []), (3, 6, []), (6, 9, [1, 4]), (9, 11, [2, 8])]
+SUBGRAPH_KATS = [
+    ([(0, 11)], [5, 10], [[], [], [1, 4], [2, 8]], [5, 10]),
+    ([(1, 11)], [5, 10], [[], [], [1, 4], [2, 8]], [5, 10]),
+    ([(5, 6)], [5, 10], [[]], [5]),
+    ([(0, 1), (10, 11)], [5, 10], [[], [0]], [10]),
+    ([(0, 11)], [10], [[], [], [1, 4], [2, 8]], [10]),
+    ([(0, 11)], [5], [[]], [5]),
+    ([(0, 3), (9, 11)], [10], [[], [2]], [10]),
+    ([(9, 11)], [3], [], []),
+    ([(5, 6)], [9], [], []),
+    ([(0, 1), (2, 3)], [2], [[], [0]], [2]),
+    ([(0, 1), (2, 3)], [9], [[], [0]], [2]),
+]
+
+
+def _fancy_oplog():
+    o = dt_amd.ListOpLog()
+    for i, (s, e, par) in enumerate(FANCY):
+        a = o.get_or_create_agent_id("abcd"[i])
+        assert o.add_insert_at(a, par, 0, "xyz"[:e - s]) == e - 1
+    return o
+
+
+def _hist(frontier):
+    ents = {v: (s, par) for s, e, par in FANCY for v in range(s, e)}
+    seen, todo = set(), list(frontier)
+    while todo:
+        v = todo.pop()
+        if v in seen:
+            continue
+        seen.add(v)
+        s, par = ents[v]
+        todo += par if v == s else [v - 1]
+    return sorted(seen)
+
+
+@pytest.mark.parametrize("kat", range(len(SUBGRAPH_KATS)))
+def test_projection_matches_reference_subgraph_kats(kat):
+    filt, frontier, expect_parents, expect_frontier = SUBGRAPH_KATS[kat]
+    hist = _hist(frontier)
+    h_of = {v: i for i, v in enumerate(hist)}                       # original -> history LV
+    inside = [v for v in hist if any(a <= v < b for a, b in filt)]
+    t_of = {v: i for i, v in enumerate(inside)}                     # original -> projected LV
+    h = _fancy_oplog().history(frontier)
+    sub = h.project(_spans(h_of[v] for v in inside))
+    assert len(sub) == len(inside)
+    ents = sub.export("entries").reshape(-1, 2)
+    off = sub.export("parent_offsets")
+    par = sub.export("parents")
+    got = [sorted(int(x) for x in par[off[i]:off[i + 1]]) for i in range(len(ents))]
+    # the subgraph's entries cover diff(frontier) n filter; each entry's parents as the KAT says
+    assert [int(x) for x in ents.reshape(-1)][:1] == ([0] if inside else [])
+    want = [sorted(t_of[p] for p in ps) for ps in expect_parents]
+    for g, w in zip(got, want):
+        assert g == w, (kat, got, want)
+    assert len(got) == len(want)
+    assert sorted(int(x) for x in sub.local_frontier()) == sorted(t_of[v] for v in expect_frontier)
