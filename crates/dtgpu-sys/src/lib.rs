@@ -31,6 +31,12 @@ pub struct dtgpu_batch_opts {
 }
 pub type dtgpu_status = c_int;
 pub const DTGPU_OK: dtgpu_status = 0;
+// EncodeOptions (src/list/encoding/encode_oplog.rs:88-130) as dtgpu_oplog_encode flags
+pub const DTGPU_ENCODE_STORE_INSERTED_CONTENT: u32 = 1;
+pub const DTGPU_ENCODE_COMPRESS_CONTENT: u32 = 2;
+pub const DTGPU_ENCODE_STORE_START_BRANCH_CONTENT: u32 = 4;
+pub const DTGPU_ENCODE_FULL: u32 = 7;
+pub const DTGPU_ENCODE_PATCH: u32 = 3;
 
 extern "C" {
     // ListOpLog (src/list/oplog.rs, src/list/encoding/decode_oplog.rs:447)
@@ -48,6 +54,7 @@ extern "C" {
     pub fn dtgpu_oplog_add_delete_without_content(oplog: *mut dtgpu_oplog, agent: i32, del_start: u64, del_end: u64) -> i64;
     pub fn dtgpu_oplog_encode(oplog: *const dtgpu_oplog, from: *const u64, n_from: usize, flags: u32, out: *mut u8,
                               cap: usize, out_len: *mut usize) -> dtgpu_status;
+    pub fn dtgpu_lz4_compress(input: *const u8, n: usize, out: *mut u8, cap: usize, out_len: *mut usize) -> dtgpu_status;
     pub fn dtgpu_oplog_len(oplog: *const dtgpu_oplog) -> usize;
     pub fn dtgpu_oplog_local_frontier(oplog: *const dtgpu_oplog, out: *mut u64, cap: usize) -> usize;
     pub fn dtgpu_oplog_dominators(oplog: *const dtgpu_oplog, a: *const u64, na: usize, b: *const u64, nb: usize,
@@ -70,6 +77,10 @@ extern "C" {
     pub fn dtgpu_batch_results(batch: *mut dtgpu_batch, results: *mut dtgpu_doc_result) -> dtgpu_status;
     pub fn dtgpu_batch_text(batch: *mut dtgpu_batch, doc: usize, out: *mut u8, cap: usize, out_len: *mut usize) -> dtgpu_status;
     pub fn dtgpu_batch_free(batch: *mut dtgpu_batch);
+    // many ListOpLog::encode(opts) at once on the GPU (device-staged batches)
+    pub fn dtgpu_batch_encode(batch: *mut dtgpu_batch, flags: u32, kernel_ms: *mut f32) -> dtgpu_status;
+    pub fn dtgpu_batch_encoded(batch: *const dtgpu_batch, doc: usize, out: *mut u8, cap: usize, out_len: *mut usize,
+                               prof: *mut u64) -> dtgpu_status;
     pub fn dtgpu_batch_checkout(docs: *const *const u8, lens: *const usize, n_docs: usize, opts: *const dtgpu_batch_opts,
                                 results: *mut dtgpu_doc_result) -> dtgpu_status;
     pub fn dtgpu_text_hash(text: *const u8, len: usize) -> u64;
