@@ -474,6 +474,7 @@ __global__ __launch_bounds__(64) void encode_records_kernel(EncParams P) {
         ntx += popc(m);
         carry_end = rdl(se.y, 63);
     }
+    mark(6);
     // agent assignment runs (encode_oplog.rs:142-189, AgentMapping :191-240)
     uint32_t n_mapped = 0, naa = 0;
     bool aa_have = false;
@@ -482,20 +483,26 @@ __global__ __launch_bounds__(64) void encode_records_kernel(EncParams P) {
     uint32_t cur_agent = 0xFFFFFFFFu, cur_mapped = 0, cur_last = 0;
     for (uint32_t k0 = 0; k0 < ne; k0 += 64) {
         const uint32_t k = k0 + l;
+        // each lane gathers its entry's first AGQ agent runs (an entry of a linear stretch often
+        // spans several), so the uniform loop below rarely waits on a load behind its stores
         uint32_t s = 0, e_end = 0, ai = 0;
-        uint4 q = make_uint4(0, 0, 0, 0);
+        uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0, q2 = q0, q3 = q0;
         if (k < ne) {
             const uint2 se = ent[worder[k]];
             s = se.x; e_end = se.y;
             ai = arun_of(ar, D.n_aruns, s);
-            q = ar[ai];
+            const uint32_t na = D.n_aruns;
+            q0 = ar[ai];
+            if (ai + 1 < na) q1 = ar[ai + 1];
+            if (ai + 2 < na) q2 = ar[ai + 2];
+            if (ai + 3 < na) q3 = ar[ai + 3];
         }
         const uint32_t nk = min(64u, ne - k0);
         for (uint32_t j = 0; j < nk; j++) {
             const uint32_t js = rdl(s, j), je = rdl(e_end, j);
             uint32_t i = rdl(ai, j);
-            uint4 r = make_uint4(rdl(q.x, j), rdl(q.y, j), rdl(q.z, j), rdl(q.w, j));
-            for (;;) {
+            uint4 r = make_uint4(rdl(q0.x, j), rdl(q0.y, j), rdl(q0.z, j), rdl(q0.w, j));
+            for (uint32_t u = 1;; u++) {
                 const uint32_t x = max(r.x, js), y = min(r.x + r.y, je);
                 if (x < y) {
                     const uint32_t agent = r.z;
@@ -524,7 +531,12 @@ __global__ __launch_bounds__(64) void encode_records_kernel(EncParams P) {
                     }
                 }
                 if (r.x + r.y >= je || ++i >= D.n_aruns) break;
-                r = ar[i];
+                if (u < 4) {
+                    const uint4 v = u == 1 ? q1 : u == 2 ? q2 : q3;
+                    r = make_uint4(rdl(v.x, j), rdl(v.y, j), rdl(v.z, j), rdl(v.w, j));
+                } else {
+                    r = ar[i];
+                }
             }
         }
     }
@@ -532,6 +544,7 @@ __global__ __launch_bounds__(64) void encode_records_kernel(EncParams P) {
         if (l == 0) { uint32_t *w = aarec + 4 * naa; w[0] = aa_agent; w[1] = uint32_t(aa_delta); w[2] = aa_len; }
         naa++;
     }
+    mark(7);
     // op runs in walk order (the INS / DEL commands), merged
     uint32_t nop = 0, n_ins = 0;
     bool op_have = false;

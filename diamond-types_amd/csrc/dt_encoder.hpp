@@ -34,7 +34,7 @@ struct EncResult {
     uint32_t status, len;
     uint32_t n_op_runs, n_agent_runs, n_txns, text_len, lz_len, stage;
     uint32_t n_mapped, aa_bytes, op_bytes, tx_bytes, nm_bytes, n_ins;   // kernel 1 -> kernel 2
-    uint64_t prof[6];       // cycles: walk, records, sizes, text + LZ4, write, CRC
+    uint64_t prof[8];       // cycles: walk, records (ops), sizes, text + LZ4, write, CRC, txn heads, agent runs
     uint64_t lzcyc[3];      // LZ4 cycles: probing, extending, emitting
     uint32_t lzst[4];       // LZ4 counts: probe steps, steps with shared hashes, sequences, -
 };

@@ -1145,7 +1145,7 @@ dtgpu_status dtgpu_batch_encode(dtgpu_batch *B, uint32_t flags, float *kernel_ms
 }
 
 dtgpu_status dtgpu_batch_encoded(const dtgpu_batch *B, size_t i, uint8_t *out, size_t cap, size_t *out_len,
-                                 uint64_t prof[12]) {
+                                 uint64_t prof[14]) {
     if (!B || i >= B->n || B->e_res.size() != B->n) return DTGPU_ERR_ARG;
     if (B->host_status[i] != OK) return dtgpu_status(B->host_status[i]);
     const EncResult &r = B->e_res[i];
@@ -1154,6 +1154,8 @@ dtgpu_status dtgpu_batch_encoded(const dtgpu_batch *B, size_t i, uint8_t *out, s
         for (int k = 0; k < 6; k++) prof[k] = r.prof[k];
         for (int k = 0; k < 3; k++) prof[6 + k] = r.lzcyc[k];
         for (int k = 0; k < 3; k++) prof[9 + k] = r.lzst[k];
+        prof[12] = r.prof[6];
+        prof[13] = r.prof[7];
     }
     if (out_len) *out_len = r.len;
     if (!out) return DTGPU_OK;

@@ -677,10 +677,10 @@ class Batch:
 
     def encode_profile(self, i):
         n = ctypes.c_size_t()
-        out = (ctypes.c_uint64 * 12)()
+        out = (ctypes.c_uint64 * 14)()
         _check(lib().dtgpu_batch_encoded(self._h, i, None, 0, ctypes.byref(n), out))
-        return dict(zip(["walk", "records", "sizes", "text_lz4", "write", "crc", "lz_probe", "lz_extend",
-                         "lz_emit", "lz_steps", "lz_shared_steps", "lz_sequences"], list(out)))
+        return dict(zip(["walk", "op_runs", "sizes", "text_lz4", "write", "crc", "lz_probe", "lz_extend",
+                         "lz_emit", "lz_steps", "lz_shared_steps", "lz_sequences", "txn_heads", "agent_runs"], list(out)))
 
     def encoded_bytes(self, which=0) -> int:
         return lib().dtgpu_batch_encoded_bytes(self._h, which)

@@ -321,10 +321,10 @@ dtgpu_status dtgpu_batch_encode(dtgpu_batch *batch, uint32_t flags, float *kerne
 /* Document `doc`'s encoded bytes (out == NULL: size in *out_len); the document's status when the
  * batch did not stage it on the device (e.g. DTGPU_DECODE_DEFER).  prof (may be NULL), when
  * DTGPU_ENC_PROF is set: cycles per phase (walk, records, sizes, text + LZ4, write, CRC), LZ4
- * cycles (probing, extending, emitting) and counts (probe steps, steps with shared hashes,
- * sequences). */
+ * cycles (probing, extending, emitting), counts (probe steps, steps with shared hashes,
+ * sequences), cycles of the txn-head and agent-run passes (the records figure is the op runs). */
 dtgpu_status dtgpu_batch_encoded(const dtgpu_batch *batch, size_t doc, uint8_t *out, size_t cap, size_t *out_len,
-                                 uint64_t prof[12]);
+                                 uint64_t prof[14]);
 /* which = 0: encoded bytes written by the last dtgpu_batch_encode; 1: decoded SoA bytes it read */
 uint64_t dtgpu_batch_encoded_bytes(const dtgpu_batch *batch, int which);
 
