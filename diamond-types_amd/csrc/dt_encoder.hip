@@ -113,12 +113,37 @@ DEV uint32_t x2nmodp(const uint32_t *x2n, uint64_t n, uint32_t k) {
     }
     return p;
 }
+// s must be 16-byte aligned: each lane's segment is a multiple of 16 bytes, read as uint4 words
+// with the next word in flight while the current one goes through the table
+DEV uint32_t crc_word(uint32_t c, uint32_t w, const uint32_t *T) {
+    c ^= w;
+    c = T[c & 0xFFu] ^ (c >> 8);
+    c = T[c & 0xFFu] ^ (c >> 8);
+    c = T[c & 0xFFu] ^ (c >> 8);
+    return T[c & 0xFFu] ^ (c >> 8);
+}
 DEV uint32_t crc32c_par(const uint8_t *s, uint32_t n, const uint32_t *T, const uint32_t *x2n) {
-    const uint32_t S = (n + 63) / 64;
+    const uint32_t S = ((n + 63) / 64 + 15) & ~15u;
     const uint32_t b0 = lane() * S;
     const uint32_t e0 = b0 < n ? min(b0 + S, n) : b0;
     uint32_t c = ~0u;
-    for (uint32_t i = b0; i < e0; i++) c = T[(c ^ s[i]) & 0xFFu] ^ (c >> 8);
+    uint32_t i = b0;
+    if (i + 16 <= e0) {
+        const uint4 *w = reinterpret_cast<const uint4 *>(s + i);
+        uint4 cur = w[0];
+        for (uint32_t k = 1;; k++) {
+            const bool more = i + 32 <= e0;
+            const uint4 nxt = more ? w[k] : cur;
+            c = crc_word(c, cur.x, T);
+            c = crc_word(c, cur.y, T);
+            c = crc_word(c, cur.z, T);
+            c = crc_word(c, cur.w, T);
+            i += 16;
+            if (!more) break;
+            cur = nxt;
+        }
+    }
+    for (; i < e0; i++) c = T[(c ^ s[i]) & 0xFFu] ^ (c >> 8);
     c = ~c;
     if (e0 <= b0) c = 0;
     const uint32_t op_full = x2nmodp(x2n, S, 3);
@@ -191,6 +216,18 @@ struct Lz {
             if (lane() < k) ring[(o + lane()) & (LZ_RING - 1)] = x + lane() + 1 < nb ? 255 : uint8_t(v - 255 * (nb - 1));
             o += k;
         }
+    }
+    // emit() with the (<= 64) literals already in registers: lane j holds in[l0 + j]
+    DEV void emit_lits(uint32_t l0, uint32_t l1, uint32_t lb, uint32_t off, uint32_t mlen) {
+        const uint32_t ll = l1 - l0;
+        put1(uint8_t((min(ll, 15u) << 4) | min(mlen - 4, 15u)));
+        if (ll >= 15) ext(ll - 15);
+        reserve(ll);
+        if (lane() < ll) ring[(o + lane()) & (LZ_RING - 1)] = uint8_t(lb);
+        o += ll;
+        put1(uint8_t(off));
+        put1(uint8_t(off >> 8));
+        if (mlen - 4 >= 15) ext(mlen - 19);
     }
     DEV void emit(uint32_t l0, uint32_t l1, uint32_t off, uint32_t mlen) {
         const uint32_t ll = l1 - l0;
@@ -285,56 +322,56 @@ struct Lz {
             tick(0);
             if (!found) { emit(lit, n, 0, 0); flush(); return o; }
             st[2]++;
-            for (;;) {   // extend backwards over the pending literals
-                const uint32_t mb = min(cur - lit, cand);
-                const bool eq = l < mb && in[cur - 1 - l] == in[cand - 1 - l];
-                const uint64_t x = ballot(!eq);
-                const uint32_t b = x ? ctz(x) : 64;
+            // one round of loads serves the usual sequence: 64 bytes before the match (backwards
+            // extension), 64 after its first four (forwards extension: independent of how far
+            // the backwards one goes, since the backtracked bytes match) and the pending literals
+            const uint32_t cur0 = cur, cand0 = cand;
+            const uint32_t mb0 = min(cur - lit, cand);
+            const bool bok = l < mb0, fok = cur + 4 + l < match_lim, lok = lit + l < cur;
+            const uint32_t bx = bok ? in[cur - 1 - l] : 0u, by = bok ? in[cand - 1 - l] : 1u;
+            const uint32_t fx = fok ? in[cur + 4 + l] : 0u, fy = fok ? in[cand + 4 + l] : 1u;
+            const uint32_t lb = lok ? in[lit + l] : 0u;
+            {
+                const uint64_t x = ballot(bx != by);
+                uint32_t b = x ? ctz(x) : 64;
                 cur -= b;
                 cand -= b;
-                if (b < 64) break;
+                while (b == 64) {   // extend backwards over the pending literals
+                    const uint32_t mb = min(cur - lit, cand);
+                    const bool eq = l < mb && in[cur - 1 - l] == in[cand - 1 - l];
+                    const uint64_t y = ballot(!eq);
+                    b = y ? ctz(y) : 64;
+                    cur -= b;
+                    cand -= b;
+                }
             }
             const uint32_t m0 = cur, off = cur - cand;
-            cur += 4;
-            cand += 4;
-            for (;;) {   // extend forwards up to len - 6
-                const bool eq = cur + l < match_lim && in[cur + l] == in[cand + l];
-                const uint64_t x = ballot(!eq);
-                const uint32_t b = x ? ctz(x) : 64;
-                cur += b;
-                cand += b;
-                if (b < 64) break;
+            {
+                const uint64_t x = ballot(fx != fy);
+                uint32_t b = x ? ctz(x) : 64;
+                cur = cur0 + 4 + b;
+                cand = cand0 + 4 + b;
+                while (b == 64) {   // extend forwards up to len - 6
+                    const bool eq = cur + l < match_lim && in[cur + l] == in[cand + l];
+                    const uint64_t y = ballot(!eq);
+                    b = y ? ctz(y) : 64;
+                    cur += b;
+                    cand += b;
+                }
             }
             const uint32_t h2 = hash(cur - 2);
             if (l == 0) vput(h2, cur - 2);
             tick(1);
-            emit(lit, m0, off, cur - m0);
+            if (m0 - lit <= 64) emit_lits(lit, m0, lb, off, cur - m0);
+            else emit(lit, m0, off, cur - m0);
             lit = cur;
             tick(2);
         }
     }
 };
 
-// ---- op runs: ListOpMetrics merge (op_metrics.rs:235-293) and write_op (encode_oplog.rs:20-92)
-struct Op {
-    uint32_t start, end, c0, c1;
-    bool fwd, del, content;
-    DEV uint32_t len() const { return end - start; }
-};
-DEV bool can_append(const Op &a, const Op &b) {
-    if (a.del != b.del || a.content != b.content) return false;
-    if (a.content && a.c1 != b.c0) return false;
-    const bool af = a.len() == 1 || a.fwd, bf = b.len() == 1 || b.fwd;
-    if (af && bf && ((!a.del && b.start == a.end) || (a.del && b.start == a.start))) return true;
-    const bool ar = a.len() == 1 || !a.fwd, br = b.len() == 1 || !b.fwd;
-    return a.del && ar && br && b.end == a.start;
-}
-DEV void append(Op &a, const Op &b) {
-    a.fwd = b.start >= a.start && (b.start != a.start || a.del);
-    if (a.del && !a.fwd) a.start = b.start;
-    else a.end += b.len();
-    if (a.content) a.c1 = b.c1;
-}
+// ---- op runs: write_op (encode_oplog.rs:20-92); the ListOpMetrics merge (op_metrics.rs:235-293)
+// is in encode_records_kernel
 // the varint head of a written op run and its optional diff; op_end is the next cursor
 DEV void op_code(uint4 r, uint32_t cursor, uint64_t &n, int64_t &diff, bool &has_diff, uint32_t &op_end) {
     const uint32_t start = r.x, end = r.y, len = end - start;
@@ -545,50 +582,135 @@ __global__ __launch_bounds__(64) void encode_records_kernel(EncParams P) {
         naa++;
     }
     mark(7);
-    // op runs in walk order (the INS / DEL commands), merged
+    // op runs in walk order (the INS / DEL commands), merged lane-parallel.  can_append /
+    // append (op_metrics.rs:235-293) depend on the run so far only through three facts about its
+    // last piece P: whether P started the run, P's own (start, end, fwd), and -- when P was
+    // appended -- the direction the append gave the run (P.start >= the piece before P's start,
+    // for deletes; always forwards for inserts).  So "piece i is appended" is a boolean function of
+    // "piece i-1 was appended", one of {0, 1, id, not}: the flags are a prefix composition of those
+    // functions (six shuffles per 64 commands), and each run's record is built at its last piece.
     uint32_t nop = 0, n_ins = 0;
-    bool op_have = false;
-    Op a{};
-    auto op_store = [&](const Op &o) {
+    bool cy = false, cM = false;                          // the last piece so far: exists, appended
+    uint32_t cS = 0, cE = 0, cF = 0, cD = 0, cC = 0, cC1 = 0, cPS = 0;
+    bool oy = false;                                      // the open run (continues into the next chunk)
+    uint32_t oS = 0, oD = 0, oC = 0, oC0 = 0, oLen = 0, oIdx = 0;
+    auto close_open = [&]() {   // record of the open run, whose last piece is the carried one
+        uint32_t st, en, dl, fw, cc = oC;
+        if (!cM) { st = cS; en = cE; dl = cD; fw = cF; cc = cC; }
+        else if (!oD) { st = oS; en = oS + oLen; dl = 0; fw = 1; }
+        else if (cS >= cPS) { st = oS; en = oS + oLen; dl = 1; fw = 1; }
+        else { st = cS; en = cS + oLen; dl = 1; fw = 0; }
         if (l == 0) {
-            uint32_t *w = oprec + 8ull * nop;
-            w[0] = o.start; w[1] = o.end; w[2] = (o.del ? 1u : 0u) | (o.fwd ? 2u : 0u) | (o.content ? 4u : 0u);
-            w[3] = o.c0; w[4] = o.c1;
+            uint32_t *w = oprec + 8ull * oIdx;
+            w[0] = st; w[1] = en; w[2] = dl | (fw << 1) | (cc << 2); w[3] = oC0; w[4] = cC1;
         }
-        nop++;
+        oy = false;
     };
     for (uint32_t c0 = 0; c0 < ncmd; c0 += 64) {
         const uint32_t c = c0 + l;
-        Cmd cm{CMD_TOG, 0, 0, 0};
-        uint32_t cb0 = 0, cb1 = 0;
+        bool valid = false;
+        uint32_t S = 0, E = 0, D = 0, F = 0, C = 0, C0 = 0, C1 = 0;
         if (c < ncmd) {
-            cm = cmds[c];
-            if ((cm.op & 15u) == CMD_INS) {
-                cb0 = cbyte[cm.lv];
-                const uint32_t lb = cbyte[cm.lv + cm.len - 1];
-                cb1 = lb != 0xFFFFFFFFu ? lb + utf8_len(content[lb]) : 0xFFFFFFFFu;
+            const Cmd cm = cmds[c];
+            const uint32_t opc = cm.op & 15u;
+            if (opc != CMD_TOG) {
+                valid = true;
+                S = cm.pos; E = cm.pos + cm.len;
+                D = opc == CMD_DEL ? 1u : 0u;
+                F = (!D || (cm.op & 16u)) ? 1u : 0u;
+                if (!D) {
+                    C0 = cbyte[cm.lv];
+                    const uint32_t lb = cbyte[cm.lv + cm.len - 1];
+                    C1 = lb != 0xFFFFFFFFu ? lb + utf8_len(content[lb]) : 0xFFFFFFFFu;
+                    C = C0 != 0xFFFFFFFFu ? 1u : 0u;
+                }
             }
         }
-        const uint32_t nk = min(64u, ncmd - c0);
-        for (uint32_t j = 0; j < nk; j++) {
-            const uint32_t op = rdl(cm.op, j);
-            if ((op & 15u) == CMD_TOG) continue;
-            Op b;
-            b.start = rdl(cm.pos, j);
-            b.end = b.start + rdl(cm.len, j);
-            b.del = (op & 15u) == CMD_DEL;
-            b.fwd = !b.del || (op & 16u);
-            b.content = !b.del && rdl(cb0, j) != 0xFFFFFFFFu;
-            b.c0 = rdl(cb0, j);
-            b.c1 = rdl(cb1, j);
-            if (!b.del) n_ins += b.len();
-            if (op_have && can_append(a, b)) { append(a, b); continue; }
-            if (op_have) op_store(a);
-            op_have = true;
-            a = b;
+        const uint32_t L = E - S;
+        if (valid && !D) n_ins += L;
+        const uint64_t vm = ballot(valid);
+        const uint64_t below = vm & lt_mask();
+        const int pi = below ? int(63 - __clzll((long long)below)) : -1;
+        const int psrc = pi >= 0 ? pi : int(l);
+        uint32_t PS = uint32_t(__shfl(int(S), psrc)), PE = uint32_t(__shfl(int(E), psrc));
+        uint32_t PD = uint32_t(__shfl(int(D), psrc)), PF = uint32_t(__shfl(int(F), psrc));
+        uint32_t PC = uint32_t(__shfl(int(C), psrc)), PC1 = uint32_t(__shfl(int(C1), psrc));
+        const int ppi = __shfl(pi, psrc);
+        uint32_t PPS = uint32_t(__shfl(int(S), ppi >= 0 ? ppi : int(l)));
+        bool pex = true;
+        if (pi < 0) {
+            pex = cy;
+            PS = cS; PE = cE; PD = cD; PF = cF; PC = cC; PC1 = cC1; PPS = cPS;
+        } else if (ppi < 0) {
+            PPS = cS;
         }
+        const uint32_t PL = PE - PS;
+        bool g0 = false, g1 = true;   // identity for TOG lanes
+        if (valid) {
+            const bool base = pex && PD == D && PC == C && (!C || PC1 == C0);
+            if (!D) {
+                g0 = g1 = base && S == PE;
+            } else {
+                const bool bf = L == 1 || F, br = L == 1 || !F;
+                const bool af0 = PL == 1 || PF, ar0 = PL == 1 || !PF, fw1 = PS >= PPS;
+                g0 = base && ((af0 && bf && S == PS) || (ar0 && br && E == PS));
+                g1 = base && ((fw1 && bf && S == PS) || (!fw1 && br && E == PS));
+            }
+        }
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {   // prefix composition: f_i o ... o f_0
+            const bool b0 = __shfl_up(int(g0), d) != 0, b1 = __shfl_up(int(g1), d) != 0;
+            if (l >= uint32_t(d)) {
+                const bool n0 = b0 ? g1 : g0, n1 = b1 ? g1 : g0;
+                g0 = n0; g1 = n1;
+            }
+        }
+        const bool merged = valid && (cy && cM ? g1 : g0);
+        const bool head = valid && !merged;
+        const uint64_t hm = ballot(head);
+        if (vm && oy && ((hm >> ctz(vm)) & 1)) close_open();
+        const uint32_t myidx = nop + popc(hm & lt_mask());
+        const uint32_t pref = scan_incl(valid ? L : 0u);
+        const uint64_t hle = hm & (lt_mask() | (1ull << l));
+        const int h = hle ? int(63 - __clzll((long long)hle)) : -1;
+        const int hsrc = h >= 0 ? h : int(l);
+        const uint32_t HS = uint32_t(__shfl(int(S), hsrc)), HD = uint32_t(__shfl(int(D), hsrc));
+        const uint32_t HC = uint32_t(__shfl(int(C), hsrc)), HC0 = uint32_t(__shfl(int(C0), hsrc));
+        const uint32_t Hpre = uint32_t(__shfl(int(pref - L), hsrc)), Hidx = uint32_t(__shfl(int(myidx), hsrc));
+        const uint64_t above = vm & ~(lt_mask() | (1ull << l));
+        const bool last = valid && above && ((hm >> ctz(above)) & 1);
+        if (last) {   // this piece ends a run whose next piece heads a new one
+            const bool hin = h >= 0;
+            const uint32_t total = hin ? pref - Hpre : oLen + pref;
+            const uint32_t rS = hin ? HS : oS, rD = hin ? HD : oD, rC = hin ? HC : oC, rC0 = hin ? HC0 : oC0;
+            const uint32_t idx = hin ? Hidx : oIdx;
+            uint32_t st, en, dl, fw, cc = rC;
+            if (!merged) { st = S; en = E; dl = D; fw = F; cc = C; }
+            else if (!rD) { st = rS; en = rS + total; dl = 0; fw = 1; }
+            else if (S >= PS) { st = rS; en = rS + total; dl = 1; fw = 1; }
+            else { st = S; en = S + total; dl = 1; fw = 0; }
+            uint32_t *w = oprec + 8ull * idx;
+            w[0] = st; w[1] = en; w[2] = dl | (fw << 1) | (cc << 2); w[3] = rC0; w[4] = C1;
+        }
+        if (vm) {   // carry the chunk's last piece and its open run
+            const uint32_t t = 63 - uint32_t(__clzll((long long)vm));
+            const int ht = __shfl(h, int(t));
+            if (ht >= 0) {
+                oy = true;
+                oS = rdl(HS, t); oD = rdl(HD, t); oC = rdl(HC, t); oC0 = rdl(HC0, t);
+                oLen = rdl(pref - Hpre, t); oIdx = rdl(Hidx, t);
+            } else {
+                oLen += rdl(pref, t);
+            }
+            cy = true;
+            cS = rdl(S, t); cE = rdl(E, t); cF = rdl(F, t); cD = rdl(D, t); cC = rdl(C, t); cC1 = rdl(C1, t);
+            cPS = rdl(PS, t);
+            cM = rdl(merged ? 1u : 0u, t) != 0;
+        }
+        nop += popc(hm);
     }
-    if (op_have) op_store(a);
+    if (oy) close_open();
+    n_ins = wave_sum(n_ins);
     wave_fence();
     mark(1);
 

@@ -1098,7 +1098,7 @@ dtgpu_status dtgpu_batch_encode(dtgpu_batch *B, uint32_t flags, float *kernel_ms
             const uint64_t cap = 128 + 11ull * r.n_agents + 64 + (r.doc_id_len != 0xFFFFFFFFu ? r.doc_id_len : 0) +
                                  30ull * (uint64_t(r.n_aruns) + r.n_entries) + 20ull * e.ncmd + 10ull * r.n_entries +
                                  10ull * r.n_parents + lz4_bound(r.n_content) + d.in_len;   // names are in the input
-            e.out_off = o; e.out_cap = uint32_t(std::min<uint64_t>(cap, 0xFFFFFFFFull)); o += e.out_cap;
+            e.out_off = o; e.out_cap = uint32_t(std::min<uint64_t>(cap, 0xFFFFFFF0ull)); o += (e.out_cap + 15) / 16 * 16;   // 16-B aligned (CRC reads)
             max_agents = std::max(max_agents, r.n_agents);
             max_text = std::max(max_text, r.n_content);
         }
