@@ -269,6 +269,7 @@ struct Lz {
                 const bool valid = l < width && p <= end_check;
                 const uint32_t nv = popc(ballot(valid));   // valid probes form a prefix
                 const uint32_t h = valid ? hash(p) : 0xFFFFFFFFu;
+                const uint32_t w32 = valid ? ld32(in + p) : 0u;
                 // every probe writes its position into its slot and reads the slot back: when
                 // each probe won its own slot, no two probes share a hash and the table held
                 // every candidate (volatile: the read-back must see the other lanes' writes)
@@ -280,7 +281,7 @@ struct Lz {
                 st[0]++;
                 if (!ballot(!won)) {
                     c = old;
-                    const bool ok = valid && p - c <= 65535u && ld32(in + c) == ld32(in + p);
+                    const bool ok = valid && p - c <= 65535u && ld32(in + c) == w32;
                     m = ballot(ok);
                     lim = m ? ctz(m) + 1 : nv;
                     if (valid && l >= lim) vput(h, old);   // probes past the match never ran
@@ -304,7 +305,7 @@ struct Lz {
                     }
                     const uint32_t pp = uint32_t(__shfl(int(p), prevj < 0 ? int(l) : prevj));
                     c = prevj >= 0 ? pp : old;
-                    const bool ok = valid && p - c <= 65535u && ld32(in + c) == ld32(in + p);
+                    const bool ok = valid && p - c <= 65535u && ld32(in + c) == w32;
                     m = ballot(ok);
                     lim = m ? ctz(m) + 1 : nv;
                     if (l < lim && nextj >= lim) vput(h, p);   // the last probe of each hash wins
@@ -512,75 +513,157 @@ __global__ __launch_bounds__(64) void encode_records_kernel(EncParams P) {
         carry_end = rdl(se.y, 63);
     }
     mark(6);
-    // agent assignment runs (encode_oplog.rs:142-189, AgentMapping :191-240)
-    uint32_t n_mapped = 0, naa = 0;
-    bool aa_have = false;
-    uint32_t aa_agent = 0, aa_len = 0;
-    int32_t aa_delta = 0;
-    uint32_t cur_agent = 0xFFFFFFFFu, cur_mapped = 0, cur_last = 0;
+    // agent assignment runs (encode_oplog.rs:142-189, AgentMapping :191-240).  A piece is an agent
+    // run clipped to a walk entry; it continues the previous piece's run when it has the same
+    // (file) agent and no seq jump -- a pairwise test once each piece knows its agent's mapped id
+    // and the end of that agent's previous piece.  Those come from one ballot per distinct agent
+    // among 64 pieces (first use assigns the next id, as AgentMapping::map does).  An entry
+    // spanning more than four agent runs sends its 64 entries down the sequential path.
+    uint32_t n_mapped = 0, naa = 0;    // naa: runs started so far (the open run is naa - 1)
+    bool ay = false;                   // an open run: agent, seq jump, length
+    uint32_t aA = 0, aL = 0;
+    int32_t aJ = 0;
+    auto aa_store = [&](uint32_t idx, uint32_t a, int32_t d, uint32_t len) {
+        uint32_t *w = aarec + 4 * idx;
+        w[0] = a; w[1] = uint32_t(d); w[2] = len;
+    };
+    uint32_t *pb = alast + P.max_agents;   // LDS: up to 256 pieces (agent, seq, len) of 64 entries
     for (uint32_t k0 = 0; k0 < ne; k0 += 64) {
         const uint32_t k = k0 + l;
-        // each lane gathers its entry's first AGQ agent runs (an entry of a linear stretch often
-        // spans several), so the uniform loop below rarely waits on a load behind its stores
+        // each lane gathers its entry's first four agent runs
         uint32_t s = 0, e_end = 0, ai = 0;
         uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0, q2 = q0, q3 = q0;
+        const uint32_t na = D.n_aruns;
+        uint32_t npk = 0;
+        bool over = false;
         if (k < ne) {
             const uint2 se = ent[worder[k]];
             s = se.x; e_end = se.y;
-            ai = arun_of(ar, D.n_aruns, s);
-            const uint32_t na = D.n_aruns;
+            ai = arun_of(ar, na, s);
             q0 = ar[ai];
             if (ai + 1 < na) q1 = ar[ai + 1];
             if (ai + 2 < na) q2 = ar[ai + 2];
             if (ai + 3 < na) q3 = ar[ai + 3];
+            npk = 1;
+            if (q0.x + q0.y < e_end && ai + 1 < na) npk = 2;
+            if (npk == 2 && q1.x + q1.y < e_end && ai + 2 < na) npk = 3;
+            if (npk == 3 && q2.x + q2.y < e_end && ai + 3 < na) npk = 4;
+            over = npk == 4 && q3.x + q3.y < e_end && ai + 4 < na;
         }
-        const uint32_t nk = min(64u, ne - k0);
-        for (uint32_t j = 0; j < nk; j++) {
-            const uint32_t js = rdl(s, j), je = rdl(e_end, j);
-            uint32_t i = rdl(ai, j);
-            uint4 r = make_uint4(rdl(q0.x, j), rdl(q0.y, j), rdl(q0.z, j), rdl(q0.w, j));
-            for (uint32_t u = 1;; u++) {
-                const uint32_t x = max(r.x, js), y = min(r.x + r.y, je);
-                if (x < y) {
-                    const uint32_t agent = r.z;
-                    if (agent != cur_agent) {
-                        if (cur_agent != 0xFFFFFFFFu && l == 0) alast[cur_agent] = cur_last;
-                        cur_agent = agent;
-                        cur_mapped = amap[agent];
-                        cur_last = alast[agent];
-                        if (!cur_mapped) {
-                            cur_mapped = ++n_mapped;
-                            if (l == 0) { amap[agent] = cur_mapped; ainv[cur_mapped - 1] = agent; }
+        if (ballot(over)) {   // the sequential path for these 64 entries
+            uint32_t cur_agent = 0xFFFFFFFFu, cur_mapped = 0, cur_last = 0;
+            const uint32_t nk = min(64u, ne - k0);
+            for (uint32_t j = 0; j < nk; j++) {
+                const uint32_t js = rdl(s, j), je = rdl(e_end, j);
+                uint32_t i = rdl(ai, j);
+                uint4 r = make_uint4(rdl(q0.x, j), rdl(q0.y, j), rdl(q0.z, j), rdl(q0.w, j));
+                for (uint32_t u = 1;; u++) {
+                    const uint32_t x = max(r.x, js), y = min(r.x + r.y, je);
+                    if (x < y) {
+                        const uint32_t agent = r.z;
+                        if (agent != cur_agent) {
+                            if (cur_agent != 0xFFFFFFFFu && l == 0) alast[cur_agent] = cur_last;
+                            cur_agent = agent;
+                            cur_mapped = amap[agent];
+                            cur_last = alast[agent];
+                            if (!cur_mapped) {
+                                cur_mapped = ++n_mapped;
+                                if (l == 0) { amap[agent] = cur_mapped; ainv[cur_mapped - 1] = agent; }
+                            }
+                        }
+                        const uint32_t s0 = r.w + (x - r.x);
+                        const int32_t d = int32_t(s0 - cur_last);
+                        cur_last = s0 + (y - x);
+                        if (ay && aA == cur_mapped && d == 0) {
+                            aL += y - x;
+                        } else {
+                            if (ay && l == 0) aa_store(naa - 1, aA, aJ, aL);
+                            naa++;
+                            ay = true; aA = cur_mapped; aJ = d; aL = y - x;
                         }
                     }
-                    const uint32_t s0 = r.w + (x - r.x);
-                    const int32_t d = int32_t(s0 - cur_last);
-                    cur_last = s0 + (y - x);
-                    if (aa_have && aa_agent == cur_mapped && d == 0) {
-                        aa_len += y - x;
+                    if (r.x + r.y >= je || ++i >= na) break;
+                    if (u < 4) {
+                        const uint4 v = u == 1 ? q1 : u == 2 ? q2 : q3;
+                        r = make_uint4(rdl(v.x, j), rdl(v.y, j), rdl(v.z, j), rdl(v.w, j));
                     } else {
-                        if (aa_have && l == 0) {
-                            uint32_t *w = aarec + 4 * naa;
-                            w[0] = aa_agent; w[1] = uint32_t(aa_delta); w[2] = aa_len;
-                        }
-                        naa += aa_have ? 1 : 0;
-                        aa_have = true; aa_agent = cur_mapped; aa_delta = d; aa_len = y - x;
+                        r = ar[i];
                     }
-                }
-                if (r.x + r.y >= je || ++i >= D.n_aruns) break;
-                if (u < 4) {
-                    const uint4 v = u == 1 ? q1 : u == 2 ? q2 : q3;
-                    r = make_uint4(rdl(v.x, j), rdl(v.y, j), rdl(v.z, j), rdl(v.w, j));
-                } else {
-                    r = ar[i];
                 }
             }
+            if (cur_agent != 0xFFFFFFFFu && l == 0) alast[cur_agent] = cur_last;
+            continue;
+        }
+        // pieces in walk order into LDS
+        const uint32_t pincl = scan_incl(npk);
+        const uint32_t np = rdl(pincl, 63);
+        {
+            uint32_t at = pincl - npk;
+            for (uint32_t u = 0; u < npk; u++, at++) {
+                const uint4 r = u == 0 ? q0 : u == 1 ? q1 : u == 2 ? q2 : q3;
+                const uint32_t x = max(r.x, s), y = min(r.x + r.y, e_end);
+                pb[3 * at] = r.z; pb[3 * at + 1] = r.w + (x - r.x); pb[3 * at + 2] = y - x;
+            }
+        }
+        wave_fence();
+        for (uint32_t j0 = 0; j0 < np; j0 += 64) {
+            const uint32_t j = j0 + l;
+            const bool valid = j < np;
+            const uint32_t A = valid ? pb[3 * j] : 0xFFFFFFFFu, S0 = valid ? pb[3 * j + 1] : 0;
+            const uint32_t LN = valid ? pb[3 * j + 2] : 0, endv = S0 + LN;
+            uint32_t MA = 0, PE = 0;
+            for (uint64_t todo = ballot(valid); todo;) {   // one round per distinct agent
+                const uint32_t lead = rdl(A, ctz(todo));
+                const bool mine = valid && A == lead;
+                const uint64_t g = ballot(mine);
+                uint32_t m = amap[lead];
+                const uint32_t last = alast[lead];
+                if (!m) {
+                    m = ++n_mapped;
+                    if (l == 0) { amap[lead] = m; ainv[m - 1] = lead; }
+                }
+                const uint64_t gb = g & lt_mask();
+                const int pe = gb ? int(63 - __clzll((long long)gb)) : int(l);
+                const uint32_t pv = uint32_t(__shfl(int(endv), pe));
+                if (mine) { MA = m; PE = gb ? pv : last; }
+                const uint32_t newlast = rdl(endv, 63 - uint32_t(__clzll((long long)g)));
+                if (l == 0) alast[lead] = newlast;
+                todo &= ~g;
+            }
+            const int32_t d = int32_t(S0 - PE);
+            const uint32_t prevA = uint32_t(__shfl_up(int(MA), 1));
+            const bool pexist = l > 0 ? true : ay;
+            const uint32_t pA = l > 0 ? prevA : aA;
+            const bool head = valid && !(pexist && pA == MA && d == 0);
+            const uint64_t hm = ballot(head);
+            const uint64_t vm = ballot(valid);
+            if ((hm & 1ull) && ay && l == 0) aa_store(naa - 1, aA, aJ, aL);   // the open run ends here
+            // run of each piece: index, head fields, length so far
+            const uint32_t lincl = scan_incl(valid ? LN : 0u);
+            const uint64_t hle = hm & (lt_mask() | (1ull << l));
+            const int h = hle ? int(63 - __clzll((long long)hle)) : -1;
+            const int hsrc = h >= 0 ? h : int(l);
+            const uint32_t HA = uint32_t(__shfl(int(MA), hsrc)), Hpre = uint32_t(__shfl(int(lincl - LN), hsrc));
+            const int32_t HJ = __shfl(d, hsrc);
+            const uint32_t Hidx = naa + uint32_t(__shfl(int(popc(hm & lt_mask())), hsrc));
+            const bool last_in_run = valid && (l == 63 ? false : ((vm >> (l + 1)) & 1) && ((hm >> (l + 1)) & 1));
+            if (last_in_run) {
+                if (h >= 0) aa_store(Hidx, HA, HJ, lincl - Hpre);
+                else aa_store(naa - 1, aA, aJ, aL + lincl);
+            }
+            // carry the open run: the last piece's run
+            const uint32_t t = 63 - uint32_t(__clzll((long long)vm));
+            const int ht = __shfl(h, int(t));
+            if (ht >= 0) {
+                aA = rdl(HA, t); aJ = int32_t(rdl(uint32_t(HJ), t)); aL = rdl(lincl - Hpre, t);
+            } else {
+                aL += rdl(lincl, t);
+            }
+            ay = true;
+            naa += popc(hm);
         }
     }
-    if (aa_have) {
-        if (l == 0) { uint32_t *w = aarec + 4 * naa; w[0] = aa_agent; w[1] = uint32_t(aa_delta); w[2] = aa_len; }
-        naa++;
-    }
+    if (ay && l == 0) aa_store(naa - 1, aA, aJ, aL);
     mark(7);
     // op runs in walk order (the INS / DEL commands), merged lane-parallel.  can_append /
     // append (op_metrics.rs:235-293) depend on the run so far only through three facts about its
@@ -1077,7 +1160,7 @@ __global__ __launch_bounds__(64) void encode_write_kernel(EncParams P) {
 int launch_encode(const EncParams &p, void *stream) {
     if (!p.n_docs) return OK;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(enc::encode_records_kernel, dim3(p.n_docs), dim3(64), 2 * size_t(p.max_agents) * 4, s, p);
+    hipLaunchKernelGGL(enc::encode_records_kernel, dim3(p.n_docs), dim3(64), (2 * size_t(p.max_agents) + 3 * 256) * 4, s, p);
     if (hipGetLastError() != hipSuccess) return ErrHip;
     hipLaunchKernelGGL(enc::encode_write_kernel, dim3(p.n_docs), dim3(64), 4096 * 4 + enc::LZ_RING + size_t(p.lds_text + 15) / 16 * 16, s, p);
     return hipGetLastError() == hipSuccess ? OK : ErrHip;
