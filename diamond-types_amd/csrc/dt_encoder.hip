@@ -274,6 +274,7 @@ struct Lz {
                 // each probe won its own slot, no two probes share a hash and the table held
                 // every candidate (volatile: the read-back must see the other lanes' writes)
                 const uint32_t old = valid ? vget(h) : 0u;
+                const uint32_t cw = valid ? ld32(in + old) : 0u;   // in flight across the slot check
                 if (valid) vput(h, p);
                 const bool won = !valid || vget(h) == p;
                 uint32_t c, lim;
@@ -281,7 +282,7 @@ struct Lz {
                 st[0]++;
                 if (!ballot(!won)) {
                     c = old;
-                    const bool ok = valid && p - c <= 65535u && ld32(in + c) == w32;
+                    const bool ok = valid && p - c <= 65535u && cw == w32;
                     m = ballot(ok);
                     lim = m ? ctz(m) + 1 : nv;
                     if (valid && l >= lim) vput(h, old);   // probes past the match never ran
@@ -305,7 +306,7 @@ struct Lz {
                     }
                     const uint32_t pp = uint32_t(__shfl(int(p), prevj < 0 ? int(l) : prevj));
                     c = prevj >= 0 ? pp : old;
-                    const bool ok = valid && p - c <= 65535u && ld32(in + c) == w32;
+                    const bool ok = valid && p - c <= 65535u && (prevj >= 0 ? ld32(in + c) : cw) == w32;
                     m = ballot(ok);
                     lim = m ? ctz(m) + 1 : nv;
                     if (l < lim && nextj >= lim) vput(h, p);   // the last probe of each hash wins
