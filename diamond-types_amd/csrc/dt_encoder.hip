@@ -52,6 +52,19 @@ DEV uint32_t wave_sum(uint32_t v) {
     return v;
 }
 
+// wave-wide byte copy, eight loads in flight per lane before their stores
+DEV void copy_bytes(uint8_t *dst, const uint8_t *src, uint32_t n) {
+    uint32_t i = lane();
+    for (; i + 7 * 64 < n; i += 8 * 64) {
+        uint8_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[k] = src[i + 64 * k];
+#pragma unroll
+        for (int k = 0; k < 8; k++) dst[i + 64 * k] = v[k];
+    }
+    for (; i < n; i += 64) dst[i] = src[i];
+}
+
 // ---- varints (leb.rs) ---------------------------------------------------------------------------
 DEV uint32_t leb_len(uint64_t v) {
     uint32_t n = 1;
@@ -1047,9 +1060,9 @@ __global__ __launch_bounds__(64) void encode_write_kernel(EncParams P) {
     if (has_doc_id)
         for (uint32_t i = l; i < D.doc_id_len; i += 64) out[docid_at + i] = in[D.doc_id_off + i];
     if (use_lz)
-        for (uint32_t i = l; i < lz_len; i += 64) out[L.lz + i] = lzb[i];
+        copy_bytes(out + L.lz, lzb, lz_len);
     else if (text_len)
-        for (uint32_t i = l; i < text_len; i += 64) out[L.text + i] = text[i];
+        copy_bytes(out + L.text, text, text_len);
     // names
     {
         uint32_t base = L.names;
