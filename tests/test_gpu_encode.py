@@ -144,3 +144,29 @@ def test_device_encoder_random_documents():
         if i % 8 == 0:
             assert OracleOpLog.load_from(e).checkout_tip_bytes() == OracleOpLog.load_from(d).checkout_tip_bytes(), i
     assert n_dev >= 48
+
+
+def _round_robin(n_agents, turns, width):
+    """A linear history typed by n_agents in turn: one graph entry spanning n_agents * turns agent
+    runs (the encoder's sequential agent-run path when that exceeds four)."""
+    o = dt_amd.ListOpLog()
+    ids = [o.get_or_create_agent_id(f"rr{i}") for i in range(n_agents)]
+    pos = 0
+    for t in range(turns):
+        for a in ids:
+            o.add_insert(a, pos, "abcdefgh"[:width])
+            pos += width
+            if t % 3 == 2:
+                o.add_delete_without_content(a, pos - 2, pos - 1)
+                pos -= 1
+    return o
+
+
+@pytest.mark.parametrize("n_agents,turns", [(2, 2), (4, 1), (5, 1), (3, 30), (9, 12)])
+def test_device_encoder_entries_spanning_many_agent_runs(n_agents, turns):
+    docs = [_round_robin(n_agents, turns, w).encode() for w in (1, 3)]
+    docs.append(G.dt_bytes("friendsforever"))   # beside a regular document in the same batch
+    b = dt_amd.Batch(docs=docs, staging="device")
+    b.encode()
+    for i, d in enumerate(docs):
+        assert b.encoded(i) == dt_amd.ListOpLog.load_from(d).encode(), i
