@@ -623,13 +623,216 @@ __device__ __forceinline__ int64_t lookup_lv(const Out &O, const Lds &L, uint32_
 // per-LV offsets.
 // Anything unusual -- including any error -- returns status 1 and decode_doc re-decodes along the
 // exact piecewise path, which yields the reference's status.
-struct FastOut { uint32_t status, n_aruns, n_pre, n_lv, ins_size; };
+
+__device__ __forceinline__ uint32_t scan_incl(uint32_t v) {   // inclusive prefix sum over the wave
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = uint32_t(__shfl_up(int(v), d));
+        if (lane() >= uint32_t(d)) v += o;
+    }
+    return v;
+}
+
+// Up to 64 OpTypeAndPosition records at once (the fast path's common case): the queued varints'
+// roles (record head or a head's diff) by a prefix composition, each record's cursor and LV by
+// prefix sums, its agent run by a lane-permute search of 64 boundaries, the RLE merge of the op
+// runs (op_metrics.rs:235-293) as in the encoder -- "record i extends the run" is a boolean
+// function of "record i-1 extended it" -- and each run written at its last record.  Returns
+// false without consuming anything when the batch is not the plain case (an error entry, a
+// record crossing an agent-run boundary or the end of the assigned LVs, an incomplete record
+// at the queue's end, a position out of range): the caller then takes one record the exact way.
+__device__ __forceinline__ bool batch_records(VQ &q, const uint32_t *bnd, uint32_t nb, uint32_t &bi, uint32_t &lv,
+                                              uint32_t total, uint32_t &ins_size, int64_t &last_cursor,
+                                              uint32_t &cr_valid, uint32_t &cr_lv, uint32_t &cr_len, uint32_t &cr_pos,
+                                              uint32_t &cr_kind, uint32_t &cr_fwd, Quads &qp, uint4 *pre_out,
+                                              uint32_t pre_cap, uint32_t *cbyte) {
+    const uint32_t l = lane();
+    const uint32_t h0 = q.head, cnt = q.cnt;
+    const bool inq = l >= h0 && l < cnt;
+    if (ballot(inq && q.end == 0xFFFFFFFFu)) return false;
+    const uint64_t x = uint64_t(q.lo) | (uint64_t(q.hi) << 32);
+    // roles: a head with has_length and diff_nz is followed by its diff varint
+    const bool needs = (x & 1) && ((x >> 1) & 1);
+    bool g0 = inq ? needs : false, g1 = false;      // successor's role given mine (head 0 / diff 1)
+    if (!inq) { g0 = false; g1 = true; }            // identity outside the queue
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const bool b0 = __shfl_up(int(g0), d) != 0, b1 = __shfl_up(int(g1), d) != 0;
+        if (l >= uint32_t(d)) {
+            const bool n0 = b0 ? g1 : g0, n1 = b1 ? g1 : g0;
+            g0 = n0; g1 = n1;
+        }
+    }
+    const bool role_after = g0;                      // role of lane l + 1 (the head lane starts as a head)
+    const bool role_here = __shfl_up(int(role_after), 1) != 0;   // (every lane runs the permute)
+    const bool is_diff = l > h0 && role_here;
+    const bool head = inq && !is_diff;
+    const uint64_t x2 = uint64_t(uint32_t(__shfl(int(q.lo), int(min(l + 1, 63u))))) |
+                        (uint64_t(uint32_t(__shfl(int(q.hi), int(min(l + 1, 63u))))) << 32);
+    bool complete = head && (!needs || l + 1 < cnt);
+    const uint64_t hm_all = ballot(head);
+    const uint64_t inc = ballot(head && !complete);   // at most the last head
+    uint64_t hm = hm_all & ~inc;
+    if (!hm) return false;
+    // record fields (head lanes)
+    const bool has_length = x & 1, is_del = (x >> 2) & 1;
+    uint64_t rest = x >> 3;
+    bool fwd = true;
+    uint64_t len;
+    int64_t diff = 0;
+    if (has_length) {
+        if (is_del) { fwd = rest & 1; rest >>= 1; }
+        len = rest;
+        if (needs) diff = int64_t(x2 >> 1) * ((x2 & 1) ? -1 : 1);
+    } else {
+        len = 1;
+        diff = int64_t(rest >> 1) * ((rest & 1) ? -1 : 1);
+    }
+    const bool rec = (hm >> l) & 1;
+    bool bad = rec && (len == 0 || len >= LIM31);
+    const uint32_t L = rec && !bad ? uint32_t(len) : 0u;
+    // LVs and cursors (64-bit cursor prefix over the records)
+    const uint32_t lincl = scan_incl(L);
+    const uint32_t lv_r = lv + lincl - L;
+    const int64_t adj = !is_del ? int64_t(len) : (fwd ? 0 : -int64_t(len));
+    int64_t step = rec ? diff + adj : 0;
+    int64_t cincl = step;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int64_t o = __shfl_up(cincl, d);
+        if (l >= uint32_t(d)) cincl += o;
+    }
+    const int64_t raw = last_cursor + (cincl - step) + diff;
+    const int64_t st = (is_del && !fwd) ? raw - int64_t(len) : raw;
+    bad = bad || (rec && (raw < 0 || st < 0 || uint64_t(st) + len >= LIM31 || uint64_t(raw) >= LIM31));
+    bad = bad || (rec && uint64_t(lv_r) + len > total);
+    // the agent run of each record: boundaries bnd[bi ..] (ascending ends of agent runs)
+    const uint32_t bw = bi + l < nb ? bnd[bi + l] : 0xFFFFFFFFu;
+    uint32_t c = 0;
+#pragma unroll
+    for (uint32_t sstep = 32; sstep >= 1; sstep >>= 1)
+        if (uint32_t(__shfl(int(bw), int(c + sstep - 1))) <= lv_r) c += sstep;
+    if (c == 63 && rdl(bw, 63) <= lv_r) c = 64;
+    const uint32_t be = uint32_t(__shfl(int(bw), int(min(c, 63u))));
+    bad = bad || (rec && (c >= 64 || uint64_t(lv_r) + len > be));
+    if (ballot(bad)) return false;
+    // content offsets per LV
+    const uint32_t ilen = rec && !is_del ? L : 0u;
+    const uint32_t iincl = scan_incl(ilen);
+    if (rec) {
+        if (!is_del) {
+            const uint32_t b0 = ins_size + iincl - ilen;
+            for (uint32_t i = 0; i < L; i++) cbyte[lv_r + i] = b0 + i;
+        } else {
+            for (uint32_t i = 0; i < L; i++) cbyte[lv_r + i] = 0xFFFFFFFFu;
+        }
+    }
+    // RLE merge of the records into op runs
+    const uint32_t pos = uint32_t(st), kind = is_del ? 1u : 0u, ofw = (!is_del || fwd) ? 1u : 0u;
+    const uint64_t below = hm & lt_mask();
+    const int pi = below ? int(63 - __clzll((long long)below)) : -1;
+    const int psrc = pi >= 0 ? pi : int(l);
+    uint32_t Pk = uint32_t(__shfl(int(kind), psrc)), Ppos = uint32_t(__shfl(int(pos), psrc));
+    uint32_t PL = uint32_t(__shfl(int(L), psrc)), Plv = uint32_t(__shfl(int(lv_r), psrc));
+    uint32_t Pf = uint32_t(__shfl(int(ofw), psrc));
+    const int ppi = __shfl(pi, psrc);
+    uint32_t PPpos = uint32_t(__shfl(int(pos), ppi >= 0 ? ppi : int(l)));
+    bool pex = true, first = false;
+    if (pi < 0) {   // the previous record is the open run's last one (the carry)
+        first = true;
+        pex = cr_valid != 0;
+    } else if (ppi < 0) {
+        PPpos = cr_pos;
+    }
+    bool g_0 = false, g_1 = true;   // identity on non-record lanes
+    if (rec) {
+        if (first) {   // the run state is known exactly: (cr_len == 1, cr_fwd)
+            bool m = false;
+            if (pex && cr_kind == kind && cr_lv + cr_len == lv_r) {
+                if (!is_del) m = cr_pos + cr_len == pos;
+                else m = ((cr_len == 1 || cr_fwd) && (L == 1 || fwd) && pos == cr_pos) ||
+                         ((cr_len == 1 || !cr_fwd) && (L == 1 || !fwd) && pos + L == cr_pos);
+            }
+            g_0 = g_1 = m;
+        } else {
+            const bool base = Pk == kind && Plv + PL == lv_r;
+            if (!is_del) {
+                g_0 = g_1 = base && Ppos + PL == pos;
+            } else {
+                const bool f1 = Ppos == PPpos;   // P was appended: forwards iff it kept the run's position
+                g_0 = base && (((PL == 1 || Pf) && (L == 1 || fwd) && pos == Ppos) ||
+                               ((PL == 1 || !Pf) && (L == 1 || !fwd) && pos + L == Ppos));
+                g_1 = base && ((f1 && (L == 1 || fwd) && pos == Ppos) || (!f1 && (L == 1 || !fwd) && pos + L == Ppos));
+            }
+        }
+    }
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const bool b0 = __shfl_up(int(g_0), d) != 0, b1 = __shfl_up(int(g_1), d) != 0;
+        if (l >= uint32_t(d)) {
+            const bool n0 = b0 ? g_1 : g_0, n1 = b1 ? g_1 : g_0;
+            g_0 = n0; g_1 = n1;
+        }
+    }
+    const bool merged = rec && g_0;   // the first record's function is constant: any start works
+    const bool rhead = rec && !merged;
+    const uint64_t rh = ballot(rhead);
+    // runs that close in this batch: the open one (at slot qp.at) as soon as any record heads a
+    // new run, and every run headed here except the last (it stays open, in cr_*)
+    qp.flush(pre_out);
+    const uint32_t n_heads = popc(rh);
+    const uint32_t n_close = (n_heads && cr_valid ? 1u : 0u) + (n_heads ? n_heads - 1 : 0u);
+    if (qp.at + n_close > pre_cap) return false;
+    const uint64_t base_at = qp.at + (cr_valid ? 1u : 0u);   // slot of the first run headed here
+    // run fields at each record: its head's, the length so far, the current pos / direction
+    const uint64_t hle = rh & (lt_mask() | (1ull << l));
+    const int hh = hle ? int(63 - __clzll((long long)hle)) : -1;
+    const int hs = hh >= 0 ? hh : int(l);
+    const uint32_t Hlv = uint32_t(__shfl(int(lv_r), hs)), Hpos = uint32_t(__shfl(int(pos), hs));
+    const uint32_t Hk = uint32_t(__shfl(int(kind), hs));
+    const uint32_t Hpre = uint32_t(__shfl(int(lincl - L), hs));
+    const uint32_t rank = uint32_t(__shfl(int(popc(rh & lt_mask())), hs));
+    uint32_t rlv, rlen, rpos, rk, rf;
+    if (hh >= 0) {
+        rlv = Hlv; rlen = lincl - Hpre; rk = Hk;
+        if (!merged) { rpos = pos; rf = ofw; }
+        else if (!Hk) { rpos = Hpos; rf = 1; }
+        else { rf = pos == Ppos ? 1u : 0u; rpos = rf ? Hpos : pos; }
+    } else {   // still the open run
+        rlv = cr_lv; rlen = cr_len + lincl; rk = cr_kind;
+        if (!cr_kind) { rpos = cr_pos; rf = 1; }
+        else { rf = (first ? pos == cr_pos : pos == Ppos) ? 1u : 0u; rpos = rf ? cr_pos : pos; }
+    }
+    // the open run closes where the first run head appears: written from the carry when that
+    // head is the batch's first record, else by the record before that head
+    const uint32_t f0 = ctz(hm);
+    if (cr_valid && ((rh >> f0) & 1) && l == 0) pre_out[qp.at] = make_uint4(cr_lv, cr_len, cr_pos, cr_kind | (cr_fwd << 1));
+    const uint64_t above = hm & ~(lt_mask() | (1ull << l));
+    const bool last = rec && above && ((rh >> ctz(above)) & 1);
+    if (last) pre_out[hh >= 0 ? base_at + rank : qp.at] = make_uint4(rlv, rlen, rpos, rk | (rf << 1));
+    qp.at += n_close;
+    // the batch's last record carries the open run
+    const uint32_t t = 63 - uint32_t(__clzll((long long)hm));
+    cr_valid = 1;
+    cr_lv = rdl(rlv, t); cr_len = rdl(rlen, t); cr_pos = rdl(rpos, t); cr_kind = rdl(rk, t); cr_fwd = rdl(rf, t);
+    // consume the records' varints
+    const uint32_t vlast = t + rdl(needs ? 1u : 0u, t);
+    q.at = rdl(q.end, vlast);
+    q.head = vlast + 1;
+    lv += rdl(lincl, t);
+    ins_size += rdl(iincl, t);
+    last_cursor += int64_t(uint64_t(rdl(uint32_t(uint64_t(cincl)), t)) | (uint64_t(rdl(uint32_t(uint64_t(cincl) >> 32), t)) << 32));
+    bi += rdl(c, t);
+    return true;
+}
+
+struct FastOut { uint32_t status, n_aruns, n_pre, n_lv, ins_size; uint64_t t_mid; };
 
 __device__ __forceinline__ FastOut fast_runs(VQ qav, VQ qtp, VQ runs, uint32_t text_n, uint32_t n_file, uint32_t *fseq,
                                           const uint32_t *fmap, uint32_t *vs, uint4 *aruns_out, uint4 *pre_out,
                                           uint32_t *cbyte, uint32_t *bnd, uint32_t arun_cap, uint32_t pre_cap,
                                           uint32_t lv_cap) {
-    FastOut fo{1, 0, 0, 0, 0};
+    FastOut fo{1, 0, 0, 0, 0, 0};
     uint64_t ins_total = 0;
     while (runs.left()) {
         uint64_t x;
@@ -677,6 +880,7 @@ __device__ __forceinline__ FastOut fast_runs(VQ qav, VQ qtp, VQ runs, uint32_t t
     }
     if ((nb & 63u) && lane() < (nb & 63u)) bnd[(nb & ~63u) + lane()] = bbuf;
     wave_fence();
+    fo.t_mid = __builtin_amdgcn_s_memtime();
     uint32_t bblk = 0xFFFFFFFFu, bcache = 0, bi = 0;
     const uint32_t total = uint32_t(next_assign);
     if (total > lv_cap) return fo;
@@ -684,6 +888,12 @@ __device__ __forceinline__ FastOut fast_runs(VQ qav, VQ qtp, VQ runs, uint32_t t
     int64_t last_cursor = 0;
     while (lv < total) {
         if (!qtp.left()) return fo;
+        if (qtp.head == qtp.cnt) vq_refill(qtp, vs);
+        if (qtp.cnt - qtp.head >= 8 && batch_records(qtp, bnd, nb, bi, lv, total, ins_size, last_cursor, cr_valid, cr_lv,
+                                                     cr_len, cr_pos, cr_kind, cr_fwd, qp, pre_out, pre_cap, cbyte)) {
+            bblk = 0xFFFFFFFFu;   // bi moved: the cached boundary window is stale
+            continue;
+        }
         uint64_t x;
         if (vq_pop(qtp, x, vs)) return fo;
         const bool has_length = x & 1; x >>= 1;
@@ -988,9 +1198,11 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
     };
 
     if (ins.present && ins.ascii && !del.present) {
+        const uint64_t t_runs = __builtin_amdgcn_s_memtime();
         const FastOut fo = fast_runs(qav, qtp, ins.runs, ins.text.n, n_file, L.fseq, L.fmap, vs, O.aruns, O.pre,
                                      O.cbyte, O.alist, D.arun_cap, D.pre_cap, D.lv_cap);
         if (fo.status == 0) {
+            R.prof[7] += uint32_t(fo.t_mid - t_runs);   // the agent-assignment half of the fast path
             qa.at = fo.n_aruns;
             qp.at = fo.n_pre;
             n_lv = next_assign = fo.n_lv;

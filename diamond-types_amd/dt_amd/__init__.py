@@ -790,7 +790,7 @@ class DecodeBatch:
     def profile(self, i):
         out = (ctypes.c_uint32 * 8)()
         _check(lib().dtgpu_decode_profile(self._h, i, out))
-        return list(out)[:7]
+        return list(out)
 
     def bytes_in(self) -> int:
         return lib().dtgpu_decode_bytes(self._h, 0)
