@@ -1492,46 +1492,47 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
     }
 
     // ---- split op runs at graph-entry boundaries (HostOpLog::finish) --------------------------
+    // one run per lane: its first entry by bisection, its pieces (one per entry it touches) at a
+    // prefix-sum offset; a run rarely spans entries, so the per-lane loops are short
+    wave_fence();   // the entries were written by lane 0 above
     {
-        Quads qo;
-        qo.init();
-        uint32_t gi = 0;
-        uint32_t gend = 0xFFFFFFFFu;   // end of entry gi (uniform)
-        uint32_t eblk = 0xFFFFFFFFu, ew = 0;   // 64 entry ends cached in lanes
-        auto entry_end = [&](uint32_t g) -> uint32_t {
-            if (g >= n_ent) return 0xFFFFFFFFu;
-            if ((g & ~63u) != eblk) {
-                eblk = g & ~63u;
-                const uint32_t k = eblk + lane();
-                ew = k < n_ent ? O.ent[k].y : 0xFFFFFFFFu;
-            }
-            return rdl(ew, g & 63u);
-        };
-        gend = entry_end(0);
+        uint32_t nout = 0;
         for (uint32_t b0 = 0; b0 < n_pre; b0 += 64) {
-            uint4 q = make_uint4(0, 0, 0, 0);
-            if (b0 + lane() < n_pre) q = O.pre[b0 + lane()];
-            const uint32_t m = n_pre - b0 < 64 ? n_pre - b0 : 64;
-            for (uint32_t k = 0; k < m; k++) {
-                uint32_t rlv = rdl(q.x, k), rlen = rdl(q.y, k), rpos = rdl(q.z, k);
-                const uint32_t kf = rdl(q.w, k);
-                const uint32_t kind = kf & 1u, fwd = kf >> 1;
+            const uint32_t i = b0 + lane();
+            const bool live = i < n_pre;
+            const uint4 q = live ? O.pre[i] : make_uint4(0, 0, 0, 0);
+            uint32_t lo = 0, hi = live ? n_ent : 0;
+            while (lo < hi) {
+                const uint32_t m = (lo + hi) >> 1;
+                if (O.ent[m].y <= q.x) lo = m + 1; else hi = m;
+            }
+            uint32_t npc = 0;
+            if (live) {
+                npc = 1;
+                const uint32_t end = q.x + q.y;
+                for (uint32_t e = lo; e < n_ent && O.ent[e].y < end; e++) npc++;
+            }
+            const uint32_t incl = scan_incl(npc);
+            const uint32_t tot = rdl(incl, 63);
+            if (uint64_t(nout) + tot > D.op_cap) return ErrCapacity;
+            if (live) {
+                uint32_t rlv = q.x, rlen = q.y, rpos = q.z, e = lo, k = nout + incl - npc;
+                const uint32_t kf = q.w, kind = kf & 1u, fwd = kf >> 1;
                 while (rlen) {
-                    while (gi < n_ent && gend <= rlv) gend = entry_end(++gi);
-                    const uint32_t cut = gi < n_ent ? gend : rlv + rlen;
+                    const uint32_t cut = e < n_ent ? O.ent[e].y : rlv + rlen;
                     const uint32_t mm = rlen < cut - rlv ? rlen : cut - rlv;
                     uint32_t apos = rpos;
                     if (kind == 0) rpos += mm;
                     else if (!fwd) apos = rpos + rlen - mm;
-                    if (qo.count() >= D.op_cap) return ErrCapacity;
-                    qo.push(rlv, mm, apos, kf, O.ops);
+                    O.ops[k++] = make_uint4(rlv, mm, apos, kf);
                     rlv += mm;
                     rlen -= mm;
+                    if (rlv >= cut) e++;
                 }
             }
+            nout += tot;
         }
-        qo.flush(O.ops);
-        R.n_ops = uint32_t(qo.at);
+        R.n_ops = nout;
     }
     prof_mark(6);
     if (lane() < fn) O.ver[lane()] = fr;
