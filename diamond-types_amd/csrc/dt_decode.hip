@@ -1429,14 +1429,15 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
         for (uint32_t j = 0; j < np; j++) in_par |= rdl(parv, j) == fr;
         const bool keep = lane() < fn && !in_par;
         const uint64_t km = ballot(keep);
-        if (keep) L.fr[popc(km & lt_mask())] = fr;
-        __syncthreads();
-        fn = popc(km);
+        // compaction by a lane permute: kept lanes to the front in order, the others behind them
+        const uint32_t nk = popc(km);
+        const uint32_t to = keep ? popc(km & lt_mask()) : nk + popc(~km & lt_mask());
+        const uint32_t moved = uint32_t(__builtin_amdgcn_ds_permute(int(to << 2), int(fr)));
+        fn = nk;
         if (fn >= DECODE_MAX_FRONTIER) return Defer;
-        fr = lane() < fn ? L.fr[lane()] : 0u;
+        fr = lane() < fn ? moved : 0u;
         fr = lane() == fn ? end - 1 : fr;
         fn++;
-        __syncthreads();
         next_file += hl;
     }
     if (next_file != next_assign) return InvalidLength;
