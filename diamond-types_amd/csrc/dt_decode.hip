@@ -826,6 +826,137 @@ __device__ __forceinline__ bool batch_records(VQ &q, const uint32_t *bnd, uint32
     return true;
 }
 
+// Up to 64 queued OpParents varints at once (decode_oplog.rs:856-913): each record is its span
+// length and a parent list; the varints' roles (span length or parent) come from a prefix
+// composition (a parent continues the list iff it is local with "more" set), span starts from a
+// prefix sum, Graph::push's extension test (one parent, the span just before) is pairwise, and
+// the entries closed here, their parent offsets and sorted parents are written by rank.  The
+// frontier after the batch is (frontier before + every span's last LV) minus every parent named
+// in it: a parent is always below its record's start, so it names an element present at that
+// point, and elements are never re-added.  Returns false without consuming anything when the
+// batch is not the plain case (a foreign parent other than ROOT, more than 8 parents, an error
+// entry, an out-of-range length or parent, capacity, a frontier that could reach 64): the caller
+// then takes one record the exact way, which yields the reference's status.
+__device__ __forceinline__ bool batch_parents(VQ &q, uint32_t &next_file, uint32_t next_assign, uint32_t &pe_valid,
+                                              uint32_t &pe_start, uint32_t &pe_end, uint32_t &pe_poff, uint32_t &n_ent,
+                                              uint32_t &n_par, uint32_t &fr, uint32_t &fn, const DecodeDesc &D,
+                                              const Out &O) {
+    const uint32_t l = lane();
+    const uint32_t h0 = q.head, cnt = q.cnt;
+    const bool inq = l >= h0 && l < cnt;
+    if (ballot(inq && q.end == 0xFFFFFFFFu)) return false;
+    const uint32_t x = q.lo;
+    const bool foreign = x & 1u, more = (x >> 1) & 1u;
+    const uint64_t nn64 = (uint64_t(q.lo) | (uint64_t(q.hi) << 32)) >> 2;
+    // roles: state 1 = a parent varint; a span length is always followed by a parent
+    bool g0 = inq, g1 = inq ? (!foreign && more) : true;   // successor's state given mine (0 / 1)
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const bool b0 = __shfl_up(int(g0), d) != 0, b1 = __shfl_up(int(g1), d) != 0;
+        if (l >= uint32_t(d)) {
+            const bool n0 = b0 ? g1 : g0, n1 = b1 ? g1 : g0;
+            g0 = n0; g1 = n1;
+        }
+    }
+    const bool role_here = __shfl_up(int(g0), 1) != 0;   // (every lane runs the permute)
+    const bool isP = inq && l > h0 && role_here;
+    const bool isH = inq && !isP;
+    const uint64_t fb = ballot(isP && foreign && nn64 != 0);
+    const uint32_t first_bad = fb ? ctz(fb) : 64u;
+    const uint64_t tm = ballot(isP && (foreign || !more));   // list terminators
+    const uint64_t after = tm & ~(lt_mask() | (1ull << l));
+    const uint32_t e = after ? ctz(after) : 64u;              // this span's terminator
+    const bool root_e = __shfl(int(foreign), int(min(e, 63u))) != 0;
+    const uint32_t np = e - l - (root_e ? 1u : 0u);
+    const bool ok = e < cnt && e < first_bad && np <= 8u;
+    const uint64_t nk_ = ballot(isH && !ok);
+    const uint32_t first_notok = nk_ ? ctz(nk_) : 64u;
+    const bool rec = isH && l < first_notok;
+    const uint64_t hm = ballot(rec);
+    if (!hm) return false;
+    const uint32_t nrec = popc(hm);
+    if (fn + nrec > DECODE_MAX_FRONTIER) return false;
+    // spans
+    bool bad = rec && (q.hi != 0 || x == 0 || x >= (1u << 25));
+    const uint32_t L = rec && !bad ? x : 0u;
+    const uint32_t incl = scan_incl(L);
+    const uint32_t start = next_file + incl - L;
+    bad = bad || (rec && uint64_t(start) + L > next_assign);
+    // parents: a parent varint reads its span's start from the nearest span lane below it
+    const uint64_t hall = ballot(isH) & (lt_mask() | (1ull << l));
+    const int hsrc = hall ? int(63 - __clzll((long long)hall)) : int(l);
+    const uint32_t pstart = uint32_t(__shfl(int(start), hsrc));
+    const bool prec = __shfl(int(rec), hsrc) != 0;
+    const bool pl = isP && prec && !foreign;
+    const uint32_t nn = uint32_t(nn64);
+    bad = bad || (pl && (nn64 == 0 || nn64 > pstart));
+    if (ballot(bad)) return false;
+    const uint32_t pv = pstart - nn;
+    const uint32_t p0 = uint32_t(__shfl(int(pv), int(min(l + 1, 63u))));
+    // Graph::push: one parent, the span just before (the pending entry always ends at `start`)
+    const bool ext = rec && np == 1u && p0 + 1u == start && (l != h0 || pe_valid);
+    const bool eh = rec && !ext;
+    const uint64_t em = ballot(eh);
+    const uint32_t npe = eh ? np : 0u;
+    const uint32_t pincl = scan_incl(npe);
+    const uint32_t poff = n_par + pincl - npe;
+    const uint32_t t = 63 - uint32_t(__clzll((long long)hm));
+    const uint32_t n_close = em ? popc(em) - 1u + pe_valid : 0u;
+    if (n_ent + n_close > D.ent_cap || n_par + rdl(pincl, t) > D.par_cap) return false;
+    // entries closed here: each entry head closes the one before it
+    const uint32_t k = popc(em & lt_mask());
+    const uint64_t pem = em & lt_mask();
+    const int psrc = pem ? int(63 - __clzll((long long)pem)) : int(l);
+    const uint32_t prev_start = uint32_t(__shfl(int(start), psrc)), prev_poff = uint32_t(__shfl(int(poff), psrc));
+    if (eh && (k || pe_valid)) {
+        const uint32_t idx = n_ent + pe_valid + k - 1u;
+        O.ent[idx] = make_uint2(k ? prev_start : pe_start, start);
+        O.poff[idx] = k ? prev_poff : pe_poff;
+    }
+    // each parent at its rank in its list: smaller values, then equal values at lower lanes
+    const int gk = pl ? hsrc : -1;
+    uint32_t prank = 0;
+    for (int d = 1; d < 8; d++) {
+        if (!ballot(rec && np > uint32_t(d))) break;   // lists no longer than d are ranked
+        const uint32_t pd = uint32_t(__shfl_up(int(pv), d)), pu = uint32_t(__shfl_down(int(pv), d));
+        const int gd = __shfl_up(gk, d), gu = __shfl_down(gk, d);
+        prank += (l >= uint32_t(d) && gd == gk && pd <= pv) ? 1u : 0u;
+        prank += (l + d < 64u && gu == gk && pu < pv) ? 1u : 0u;
+    }
+    const bool peh = __shfl(int(eh), hsrc) != 0;
+    const uint32_t ppoff = uint32_t(__shfl(int(poff), hsrc));
+    if (pl && peh) O.par[ppoff + prank] = pv;
+    // frontier: the old elements, then each span's last LV, minus every parent named here
+    const uint32_t ridx = popc(hm & lt_mask());
+    const uint32_t dst = rec ? fn + ridx : (fn + nrec + popc(~hm & lt_mask())) & 63u;
+    const uint32_t ev = uint32_t(__builtin_amdgcn_ds_permute(int(dst << 2), int(start + L - 1u)));
+    const uint32_t cand = l < fn ? fr : ev;
+    bool rm = false;
+    for (uint64_t pm = ballot(pl); pm; pm &= pm - 1) rm |= cand == rdl(pv, ctz(pm));
+    const bool keep = l < fn + nrec && !rm;
+    const uint64_t km = ballot(keep);
+    const uint32_t nk = popc(km);
+    const uint32_t to = keep ? popc(km & lt_mask()) : nk + popc(~km & lt_mask());
+    const uint32_t moved = uint32_t(__builtin_amdgcn_ds_permute(int(to << 2), int(cand)));
+    fn = nk;
+    fr = l < fn ? moved : 0u;
+    // state after the batch
+    const uint32_t last_e = rdl(e, t);
+    q.at = rdl(q.end, last_e);
+    q.head = last_e + 1;
+    next_file += rdl(incl, t);
+    pe_end = rdl(start + L, t);
+    if (em) {
+        const uint32_t le = 63 - uint32_t(__clzll((long long)em));
+        pe_start = rdl(start, le);
+        pe_poff = rdl(poff, le);
+    }
+    pe_valid = 1;
+    n_ent += n_close;
+    n_par += rdl(pincl, t);
+    return true;
+}
+
 struct FastOut { uint32_t status, n_aruns, n_pre, n_lv, ins_size; uint64_t t_mid; };
 
 __device__ __forceinline__ FastOut fast_runs(VQ qav, VQ qtp, VQ runs, uint32_t text_n, uint32_t n_file, uint32_t *fseq,
@@ -1375,6 +1506,15 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
     uint32_t n_ent = 0, n_par = 0;
     uint32_t fr = 0, fn = 0;   // frontier: lane k holds element k (sorted)
     while (qhist.left()) {
+        if (qhist.head == qhist.cnt) vq_refill(qhist, vs);
+        if (qhist.cnt - qhist.head >= 4) {   // next_assign < 2^31 (checked with the agent runs)
+            uint32_t nf = uint32_t(next_file);
+            if (batch_parents(qhist, nf, uint32_t(next_assign), pe_valid, pe_start, pe_end, pe_poff, n_ent, n_par,
+                              fr, fn, D, O)) {
+                next_file = nf;
+                continue;
+            }
+        }
         uint64_t hl;
         TRY(vq_pop(qhist, hl, vs));
         uint32_t parv = 0, np = 0;

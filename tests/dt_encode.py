@@ -7,6 +7,7 @@ order :404-747), decode side decode_oplog.rs:590-960.  Ops are (agent, kind, pos
 parents) in LV order, as dt_amd.synth_ops returns them; every op is its own agent run and its
 own graph entry (the decoder merges them back exactly like the builder API does).
 """
+import random
 import struct
 
 
@@ -74,10 +75,14 @@ def write_op(kind, start, length, fwd, cursor):
     return out, op_end
 
 
-def encode_dt(agent_names, ops, del_content_unknown=False, ins_runs_per_op=False, unknown_every=0):
+def encode_dt(agent_names, ops, del_content_unknown=False, ins_runs_per_op=False, unknown_every=0,
+              sort_parents=True, foreign_every=0):
     """.dt bytes for `ops`.  del_content_unknown adds a delete PatchContent whose runs are all
     unknown; ins_runs_per_op writes one ContentIsKnown run per insert (else one run);
-    unknown_every > 0 marks every n-th insert's content unknown (and leaves its text out)."""
+    unknown_every > 0 marks every n-th insert's content unknown (and leaves its text out);
+    sort_parents=False keeps each parent list in the given order (the decoder sorts it);
+    foreign_every > 0 writes every n-th parent as a foreign (agent, seq) reference
+    (decode_oplog.rs:880-890) instead of a local distance."""
     out = bytearray(b"DMNDTYPS") + leb(0)
     names = b"".join(leb(len(n.encode())) + n.encode() for n in agent_names)
     out += chunk(1, chunk(3, names))
@@ -89,7 +94,10 @@ def encode_dt(agent_names, ops, del_content_unknown=False, ins_runs_per_op=False
     cursor = 0
     lv = 0
     n_ins = 0
+    n_par = 0
+    spans = []   # (lv, agent, seq) per op: a parent's (agent, seq) for foreign references
     for agent, kind, pos, length, text, parents in ops:
+        spans.append((lv, agent, seq[agent]))
         versions += leb(((agent + 1) << 1) | 0) + leb(length)
         seq[agent] += length
         if kind == 0:
@@ -109,9 +117,14 @@ def encode_dt(agent_names, ops, del_content_unknown=False, ins_runs_per_op=False
         if not parents:
             hist += leb(1)   # foreign, n = 0: ROOT
         else:
-            for k, p in enumerate(sorted(parents)):
+            for k, p in enumerate(sorted(parents) if sort_parents else parents):
                 more = 1 if k + 1 < len(parents) else 0
-                hist += leb(((lv - p) << 2) | (more << 1))
+                n_par += 1
+                if foreign_every and n_par % foreign_every == 0:
+                    j = max(i for i, sp in enumerate(spans) if sp[0] <= p)
+                    hist += leb(((spans[j][1] + 1) << 2) | (more << 1) | 1) + leb(spans[j][2] + p - spans[j][0])
+                else:
+                    hist += leb(((lv - p) << 2) | (more << 1))
         lv += length
     if not (ins_runs_per_op or unknown_every):
         runs = bytearray(leb((ins_total << 1) | 1)) if ins_total else bytearray()
@@ -124,3 +137,37 @@ def encode_dt(agent_names, ops, del_content_unknown=False, ins_runs_per_op=False
     crc = crc32c(bytes(out))
     out += chunk(100, struct.pack("<I", crc))
     return bytes(out)
+
+
+def graph_docs():
+    """Documents whose histories stress the OpParents decode: merges of up to 12 parents in
+    arbitrary order (duplicates included), foreign (agent, seq) parents, runs of single-parent
+    spans (Graph::push extensions), ROOT parents, a frontier that grows past 64 (the device hands
+    that document back: DECODE_DEFER) and one that grows to just under it."""
+    out = []
+    for doc in range(10):
+        rng = random.Random(1000 + doc)
+        na = 1 + doc % 5
+        ops, lv, fr = [], 0, []
+        wide = 70 if doc == 8 else (56 if doc == 9 else 0)
+        for i in range(400):
+            length = rng.choice([1, 1, 2, 5])
+            if i < wide or not fr or rng.random() < 0.02:
+                parents = []
+            elif rng.random() < 0.35:
+                parents = [lv - 1]
+            elif rng.random() < 0.25:   # a fork from an interior version: a new frontier element
+                parents = [rng.randrange(lv)]
+            else:   # a merge of frontier elements, sometimes an interior version and a duplicate too
+                parents = rng.sample(fr, min(rng.choice([1, 2, 2, 3, 4, 7, 12]), len(fr)))
+                if rng.random() < 0.3:
+                    parents.append(rng.randrange(lv))
+                if rng.random() < 0.1:
+                    parents.append(parents[0])
+            ops.append((rng.randrange(na), 0, 0, length, "x" * length, parents))
+            fr = [x for x in fr if x not in parents] + [lv + length - 1]
+            lv += length
+        out.append(encode_dt([f"g{i}" for i in range(na)], ops, sort_parents=(doc % 2 == 0),
+                             foreign_every=(7 if doc % 3 == 1 else 0)))
+    return out
+

@@ -50,3 +50,16 @@ def test_unknown_and_deleted_content_decode():
     o2 = dt_amd.ListOpLog.load_from(data2)
     with pytest.raises(dt_amd.ParseError):
         o2.checkout_tip()
+
+
+def test_graph_shape_docs_host_matches_oracle():
+    """The OpParents stress documents (dt_encode.graph_docs): the host decoder and the oracle
+    read the same history; parent lists come back sorted whatever order they were written in."""
+    from dt_encode import graph_docs
+    for d in graph_docs():
+        host = dt_amd.ListOpLog.load_from(d)
+        orc = OracleOpLog.load_from(d)
+        assert len(host) == len(orc)
+        poff, par = host.export("parent_offsets"), host.export("parents")
+        for a, b in zip(poff[:-1], poff[1:]):
+            assert list(par[a:b]) == sorted(par[a:b])

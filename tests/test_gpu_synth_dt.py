@@ -4,7 +4,7 @@ unknown content) and the device-staged checkout, against the host decoder and th
 import numpy as np
 import pytest
 
-from dt_encode import encode_dt
+from dt_encode import encode_dt, graph_docs
 from oracle.oracle import OpLog as OracleOpLog
 from test_dt_encode import WHAT, _unicode
 
@@ -57,3 +57,19 @@ def test_device_staged_checkout_matches_oracle_on_synthetic_dt():
             continue
         assert res[i]["status"] == 0, (i, res[i])
         assert b.text(i) == OracleOpLog.load_from(d).checkout_tip_bytes(), i
+
+
+def test_device_decode_matches_host_on_graph_shapes():
+    docs = graph_docs()
+    dec = dt_amd.DecodeBatch(docs)
+    dec.run()
+    for i, d in enumerate(docs):
+        st = dec.status(i)["status"]
+        if i == 8:   # the frontier passes 64 elements
+            assert st == dt_amd.DECODE_DEFER, i
+            continue
+        assert st == 0, (i, st)
+        host = dt_amd.ListOpLog.load_from(d)
+        for w in WHAT:
+            a, b = dec.export(i, w), host.export(w)
+            assert (a == b) if w == "agent_names" else np.array_equal(a, b), (i, w)
