@@ -719,12 +719,19 @@ __device__ __forceinline__ bool batch_records(VQ &q, const uint32_t *bnd, uint32
     // content offsets per LV
     const uint32_t ilen = rec && !is_del ? L : 0u;
     const uint32_t iincl = scan_incl(ilen);
-    if (rec) {
-        if (!is_del) {
-            const uint32_t b0 = ins_size + iincl - ilen;
-            for (uint32_t i = 0; i < L; i++) cbyte[lv_r + i] = b0 + i;
-        } else {
-            for (uint32_t i = 0; i < L; i++) cbyte[lv_r + i] = 0xFFFFFFFFu;
+    {   // every LV of the batch, wave-strided: its record is the first lane whose lincl exceeds it
+        const uint32_t tot = rdl(lincl, 63);
+        const uint32_t vk = ins_size + iincl - ilen - (lincl - L);   // content byte = vk + LV offset
+        const bool dk = rec && is_del;
+        for (uint32_t b = 0; b < tot; b += 64) {   // uniform: every lane runs the shuffles
+            const uint32_t j = b + l;
+            uint32_t r = 0;
+#pragma unroll
+            for (uint32_t s = 32; s >= 1; s >>= 1)
+                if (uint32_t(__shfl(int(lincl), int(r + s - 1))) <= j) r += s;
+            const uint32_t v = uint32_t(__shfl(int(vk), int(r)));
+            const bool d = __shfl(int(dk), int(r)) != 0;
+            if (j < tot) cbyte[lv + j] = d ? 0xFFFFFFFFu : v + j;
         }
     }
     // RLE merge of the records into op runs
@@ -957,6 +964,141 @@ __device__ __forceinline__ bool batch_parents(VQ &q, uint32_t &next_file, uint32
     return true;
 }
 
+// Up to 64 queued OpVersions varints at once (decode_oplog.rs:764-800): each record is (file agent
+// + jump flag, length[, jump]); the roles come from a prefix composition of 4-state functions
+// (agent / length, no jump follows / length, a jump follows / jump), each record's seq start
+// from its file agent's cursor plus a prefix sum over the records of that agent, the RLE merge
+// of agent runs (same agent, seq contiguous) is pairwise, and the runs closed here are written
+// by rank, as are the run-end boundaries the op records are split at.  Returns false without
+// consuming anything when the batch is not the plain case (an error entry, an unknown agent, a
+// seq or LV out of range, capacity): the caller then takes one record the exact way.
+__device__ __forceinline__ uint32_t compose4(uint32_t g, uint32_t f) {   // (g after f)[s] = g[f[s]]
+    uint32_t r = 0;
+#pragma unroll
+    for (uint32_t s = 0; s < 4; s++) r |= ((g >> (2u * ((f >> (2u * s)) & 3u))) & 3u) << (2u * s);
+    return r;
+}
+
+__device__ __forceinline__ bool batch_agents(VQ &q, uint32_t n_file, uint32_t *fseq, const uint32_t *fmap,
+                                             uint64_t &next_assign, uint32_t &ca_valid, uint32_t &ca_lv,
+                                             uint32_t &ca_len, uint32_t &ca_agent, uint32_t &ca_seq, Quads &qa,
+                                             uint4 *aruns_out, uint32_t arun_cap, uint32_t &nb, uint32_t &bbuf,
+                                             uint32_t *bnd) {
+    const uint32_t l = lane();
+    const uint32_t h0 = q.head, cnt = q.cnt;
+    const bool inq = l >= h0 && l < cnt;
+    if (ballot(inq && q.end == 0xFFFFFFFFu)) return false;
+    const uint32_t x = q.lo;
+    // successor's state given mine: agent -> length (kind by my jump flag); length -> agent or
+    // jump; jump -> agent.  Identity (0xE4) outside the queue.
+    uint32_t f = inq ? (((x & 1u) ? 2u : 1u) | (3u << 4)) : 0xE4u;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = uint32_t(__shfl_up(int(f), d));
+        if (l >= uint32_t(d)) f = compose4(f, o);
+    }
+    const uint32_t fb = uint32_t(__shfl_up(int(f), 1));   // every lane runs the permute (no inactive sources)
+    const uint32_t st = l > h0 ? (fb & 3u) : 0u;
+    const bool head = inq && st == 0u;
+    const bool hj = x & 1u;
+    const uint32_t x1 = uint32_t(__shfl(int(q.lo), int(min(l + 1, 63u))));
+    const uint32_t x1h = uint32_t(__shfl(int(q.hi), int(min(l + 1, 63u))));
+    const uint32_t x2 = uint32_t(__shfl(int(q.lo), int(min(l + 2, 63u))));
+    const uint32_t x2h = uint32_t(__shfl(int(q.hi), int(min(l + 2, 63u))));
+    const bool ok = l + 1u + (hj ? 1u : 0u) < cnt;
+    const uint64_t nk_ = ballot(head && !ok);
+    const uint32_t first_nk = nk_ ? ctz(nk_) : 64u;
+    const bool rec = head && l < first_nk;
+    const uint64_t hm = ballot(rec);
+    if (!hm) return false;
+    const uint32_t fa1 = x >> 1;
+    bool bad = rec && (q.hi != 0 || fa1 == 0 || fa1 - 1u >= n_file || x1h != 0 || x1 >= (1u << 25));
+    const uint32_t fa = rec && !bad ? fa1 - 1u : 0u;
+    const uint32_t alen = rec && !bad ? x1 : 0u;
+    const uint64_t jz = uint64_t(x2) | (uint64_t(x2h) << 32);
+    const int64_t jump = (rec && hj) ? int64_t(jz >> 1) * ((jz & 1) ? -1 : 1) : 0;
+    const int64_t delta = jump + int64_t(alen);
+    const uint32_t base = rec ? fseq[fa] : 0u;
+    // each record's cursor: its file agent's cursor plus the deltas of that agent's earlier records
+    int64_t cb = 0;
+    bool last_of_agent = false;
+    for (uint64_t rem = hm; rem;) {
+        const uint32_t f0 = rdl(fa, ctz(rem));
+        const uint64_t same = ballot(rec && fa == f0);
+        const bool me = (same >> l) & 1;
+        const int64_t v = me ? delta : 0;
+        int64_t inc = v;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int64_t o = __shfl_up(inc, d);
+            if (l >= uint32_t(d)) inc += o;
+        }
+        if (me) { cb = inc - v; last_of_agent = l == 63u - uint32_t(__clzll((long long)same)); }
+        rem &= ~same;
+    }
+    const int64_t sstart = int64_t(base) + cb + jump;
+    bad = bad || (rec && (sstart < 0 || uint64_t(sstart) + alen >= LIM31));
+    const uint32_t lincl = scan_incl(alen);
+    bad = bad || (rec && next_assign + lincl >= LIM31);
+    const uint32_t t = 63 - uint32_t(__clzll((long long)hm));
+    const uint32_t total = rdl(lincl, t);
+    if (ballot(bad)) return false;
+    const uint32_t s32 = uint32_t(sstart), lv_r = uint32_t(next_assign) + lincl - alen;
+    const uint32_t agent = rec ? fmap[fa] : 0u;
+    // agent runs (AgentAssignment RLE): same agent and seq contiguous with the previous record
+    const uint64_t below = hm & lt_mask();
+    const int psrc = below ? int(63 - __clzll((long long)below)) : int(l);
+    const uint32_t Pa = uint32_t(__shfl(int(agent), psrc)), Pe = uint32_t(__shfl(int(s32 + alen), psrc));
+    const bool merged = rec && (below ? (Pa == agent && Pe == s32)
+                                      : (ca_valid && ca_agent == agent && ca_seq + ca_len == s32));
+    const uint64_t rh = ballot(rec && !merged);
+    const uint32_t n_heads = popc(rh);
+    const uint32_t n_close = (n_heads && ca_valid ? 1u : 0u) + (n_heads ? n_heads - 1u : 0u);
+    const uint64_t nzm = ballot(rec && alen != 0);
+    const uint32_t nzc = popc(nzm);
+    if (qa.count() + n_close > arun_cap || nb + nzc > 4 * arun_cap) return false;
+    // file agent cursors
+    __syncthreads();
+    if (rec && last_of_agent) fseq[fa] = s32 + alen;
+    __syncthreads();
+    // runs closed here: the open one (if a record heads a new run), every head but the last
+    qa.flush(aruns_out);
+    const uint32_t lv_f0 = uint32_t(__shfl(int(lv_r), int(rh ? ctz(rh) : 0u)));
+    if (rh && ca_valid && l == 0)
+        aruns_out[qa.at] = make_uint4(ca_lv, ca_len + (lv_f0 - uint32_t(next_assign)), ca_agent, ca_seq);
+    const uint64_t hab = rh & ~(lt_mask() | (1ull << l));
+    const uint32_t lvn = uint32_t(__shfl(int(lv_r), int(hab ? ctz(hab) : l)));
+    const bool hd = (rh >> l) & 1;
+    if (hd && hab) aruns_out[qa.at + (ca_valid ? 1u : 0u) + popc(rh & lt_mask())] = make_uint4(lv_r, lvn - lv_r, agent, s32);
+    qa.at += n_close;
+    if (rh) {
+        const uint32_t th = 63 - uint32_t(__clzll((long long)rh));
+        ca_lv = rdl(lv_r, th); ca_agent = rdl(agent, th); ca_seq = rdl(s32, th);
+        ca_len = uint32_t(next_assign) + total - ca_lv;
+    } else {
+        ca_len += total;
+    }
+    ca_valid = 1;
+    // run-end boundaries of the non-empty records; the partial block stays in bbuf
+    const bool nz = (nzm >> l) & 1;
+    const uint32_t rk = popc(nzm & lt_mask());
+    const uint32_t endv = lv_r + alen;
+    if (nz) bnd[nb + rk] = endv;
+    if (l < (nb & 63u)) bnd[(nb & ~63u) + l] = bbuf;
+    const uint32_t dst = nz ? rk : nzc + popc(~nzm & lt_mask());
+    const uint32_t cmp = uint32_t(__builtin_amdgcn_ds_permute(int(dst << 2), int(endv)));
+    const uint32_t nb2 = nb + nzc;
+    const uint32_t idx = (nb2 & ~63u) + l;
+    const uint32_t pulled = uint32_t(__builtin_amdgcn_ds_bpermute(int(((idx - nb) & 63u) << 2), int(cmp)));
+    bbuf = idx < nb ? bbuf : pulled;
+    nb = nb2;
+    next_assign += total;
+    const uint32_t vlast = t + 1u + rdl(hj ? 1u : 0u, t);
+    q.at = rdl(q.end, vlast);
+    q.head = vlast + 1;
+    return true;
+}
+
 struct FastOut { uint32_t status, n_aruns, n_pre, n_lv, ins_size; uint64_t t_mid; };
 
 __device__ __forceinline__ FastOut fast_runs(VQ qav, VQ qtp, VQ runs, uint32_t text_n, uint32_t n_file, uint32_t *fseq,
@@ -978,6 +1120,10 @@ __device__ __forceinline__ FastOut fast_runs(VQ qav, VQ qtp, VQ runs, uint32_t t
     uint64_t next_assign = 0;
     uint32_t nb = 0, bbuf = 0;
     while (qav.left()) {
+        if (qav.head == qav.cnt) vq_refill(qav, vs);
+        if (qav.cnt - qav.head >= 6 && batch_agents(qav, n_file, fseq, fmap, next_assign, ca_valid, ca_lv, ca_len, ca_agent,
+                                                    ca_seq, qa, aruns_out, arun_cap, nb, bbuf, bnd))
+            continue;
         uint64_t n, alen;
         int64_t jump = 0;
         if (vq_pop(qav, n, vs)) return fo;

@@ -134,3 +134,16 @@ def test_corrupted_benchmark_file():
             assert got == _host_code(d, ignore_crc=True), i
             if got == 0:
                 _same_arrays(dec2, i, d, ignore_crc=True)
+
+
+@pytest.mark.parametrize("name", G.DT_FILES)
+def test_fast_path_taken_on_benchmark_files(name):
+    """The benchmark files are the plain case (ASCII inserts in known runs, no delete content):
+    the lane-parallel fast path must decode them itself.  Its agent-assignment half leaves a
+    nonzero cycle count in profile slot 7; when it bails the exact path still yields the same
+    arrays, so only this check notices a fast path that silently stopped working."""
+    data = G.dt_bytes(name)
+    dec = dt_amd.DecodeBatch([data])
+    dec.run()
+    assert dec.status(0)["status"] == 0
+    assert dec.profile(0)[7] > 0
