@@ -380,56 +380,95 @@ __device__ __forceinline__ uint32_t crc32c_par(const uint8_t *s, uint32_t n, con
     return crc;
 }
 
-// LZ4 raw block (lz4_flex::decompress; decode_oplog.rs:621-633) from the document into dst.
+// LZ4 raw block (lz4_flex::decompress; decode_oplog.rs:621-633) from the document into dst, up to
+// 64 sequences at a time.  The sequence headers are parsed serially from the register window
+// into lanes (sequence j: output start, literal length and source, match offset and length),
+// with the reader's checks.  Then every output byte of the batch is resolved to where its value
+// already lies -- an input literal byte, or an output byte written before the batch -- by
+// following match offsets back through the batch's sequences (an overlapping match is periodic:
+// its byte k repeats byte k mod offset, so one hop leaves the match; every hop lands in an
+// earlier sequence, so at most 64 hops), and the bytes are copied wave-wide, one gather load and
+// one store per lane per 64 bytes, instead of a dependent load round trip per sequence.
 __device__ __forceinline__ bool lz4_block(Ctx &C, const Rd &src, uint8_t *dst, uint32_t out_len) {
     const uint8_t *sp = C.in + src.p;
-    const uint64_t n = src.n;
-    uint64_t ip = 0, op = 0, fenced = 0;
-    while (ip < n) {
-        const uint32_t tok = C.byte(0, src.p + uint32_t(ip++));
-        uint64_t lit = tok >> 4;
-        if (lit == 15) {
-            uint32_t b;
-            do {
-                if (ip >= n) return false;
-                b = C.byte(0, src.p + uint32_t(ip++));
-                lit += b;
-            } while (b == 255);
+    const uint32_t n = src.n;
+    uint32_t ip = 0, op = 0;
+    bool end = n == 0;
+    while (!end) {
+        // ---- parse up to 64 sequences (uniform) ----
+        uint32_t so = 0xFFFFFFFFu, slit = 0, ssrc = 0, soff = 0, sml = 0;   // lane j: sequence j
+        const uint32_t bs = op;
+        uint32_t ns = 0;
+        while (ns < 64 && !end) {
+            const uint32_t tok = C.byte(0, src.p + ip++);
+            uint32_t lit = tok >> 4;
+            if (lit == 15) {
+                uint32_t b;
+                do {
+                    if (ip >= n) return false;
+                    b = C.byte(0, src.p + ip++);
+                    lit += b;
+                } while (b == 255 && lit < 0x80000000u);
+            }
+            if (uint64_t(ip) + lit > n || uint64_t(op) + lit > out_len) return false;
+            const uint32_t lsrc = ip, o0 = op;
+            ip += lit;
+            op += lit;
+            uint32_t off = 0, ml = 0;
+            if (ip >= n) {
+                end = true;
+            } else {
+                if (ip + 2 > n) return false;
+                off = C.byte(0, src.p + ip) | (C.byte(0, src.p + ip + 1) << 8);
+                ip += 2;
+                if (off == 0 || off > op) return false;
+                ml = tok & 15u;
+                if (ml == 15) {
+                    uint32_t b;
+                    do {
+                        if (ip >= n) return false;
+                        b = C.byte(0, src.p + ip++);
+                        ml += b;
+                    } while (b == 255 && ml < 0x80000000u);
+                }
+                ml += 4;
+                if (uint64_t(op) + ml > out_len) return false;
+                op += ml;
+                end = ip >= n;
+            }
+            const bool me = lane() == ns;
+            so = me ? o0 : so; slit = me ? lit : slit; ssrc = me ? lsrc : ssrc;
+            soff = me ? off : soff; sml = me ? ml : sml;
+            ns++;
         }
-        if (ip + lit > n || op + lit > out_len) return false;
-        for (uint64_t k = lane(); k < lit; k += 64) dst[op + k] = sp[ip + k];
-        ip += lit;
-        op += lit;
-        if (ip >= n) break;
-        if (ip + 2 > n) return false;
-        const uint64_t off = C.byte(0, src.p + uint32_t(ip)) | (C.byte(0, src.p + uint32_t(ip + 1)) << 8);
-        ip += 2;
-        if (off == 0 || off > op) return false;
-        uint64_t ml = tok & 15u;
-        if (ml == 15) {
-            uint32_t b;
-            do {
-                if (ip >= n) return false;
-                b = C.byte(0, src.p + uint32_t(ip++));
-                ml += b;
-            } while (b == 255);
+        // ---- resolve and copy the batch's output bytes [bs, op) ----
+        for (uint32_t g = bs; g < op; g += 64) {   // uniform
+            const uint32_t p = g + lane();
+            uint32_t cur = p, from = 0;
+            bool inp = false, done = p >= op;
+            while (ballot(!done)) {
+                uint32_t r = 0;
+#pragma unroll
+                for (uint32_t st = 32; st >= 1; st >>= 1)
+                    if (uint32_t(__shfl(int(so), int(r + st))) <= cur) r += st;
+                const uint32_t o0 = uint32_t(__shfl(int(so), int(r))), lit = uint32_t(__shfl(int(slit), int(r)));
+                const uint32_t ls = uint32_t(__shfl(int(ssrc), int(r))), off = uint32_t(__shfl(int(soff), int(r)));
+                const uint32_t ml = uint32_t(__shfl(int(sml), int(r)));
+                if (!done) {
+                    const uint32_t k = cur - o0;
+                    if (k < lit) {
+                        from = ls + k; inp = true; done = true;
+                    } else {
+                        const uint32_t m = k - lit;
+                        const uint32_t q = o0 + lit - off + (off < ml ? m % off : m);
+                        if (q < bs) { from = q; done = true; } else cur = q;
+                    }
+                }
+            }
+            if (p < op) dst[p] = inp ? sp[from] : dst[from];
         }
-        ml += 4;
-        if (op + ml > out_len) return false;
-        // the match reads [op - off, op - off + min(off, ml)): make earlier stores visible
-        if (op - off + (off < ml ? off : ml) > fenced) {
-            wave_fence();
-            fenced = op;
-        }
-        if (off >= ml) {
-            for (uint64_t k = lane(); k < ml; k += 64) dst[op + k] = dst[op - off + k];
-        } else {   // overlapping match: the output repeats with period `off`
-            const uint32_t o32 = uint32_t(off);
-            for (uint32_t k = lane(); k < ml; k += 64) dst[op + k] = dst[op - off + (k % o32)];
-        }
-        op += ml;
+        wave_fence();   // the next batch reads these bytes
     }
-    wave_fence();
     return op == out_len;
 }
 
