@@ -400,6 +400,33 @@ __device__ __forceinline__ bool lz4_block(Ctx &C, const Rd &src, uint8_t *dst, u
         const uint32_t bs = op;
         uint32_t ns = 0;
         while (ns < 64 && !end) {
+            {   // the common sequence: no length bytes, a match follows the literals (one-byte
+                // length extensions measured slower: more issue per sequence than they save)
+                const uint32_t pos = src.p + ip;
+                Win &W = C.w0;
+                if (pos - W.wpos + 20u > 256u) {   // one window covers the token, literals and offset
+                    W.wpos = pos & ~3u;
+                    W.w = *reinterpret_cast<const uint32_t *>(W.base + W.wpos + 4u * lane());
+                }
+                const uint32_t d = pos - W.wpos;
+                const uint32_t tok = (rdl(W.w, d >> 2) >> ((d & 3u) << 3)) & 0xFFu;
+                const uint32_t lit = tok >> 4, ml = (tok & 15u) + 4u;
+                const uint32_t e = d + 1u + lit;   // the offset's two bytes (e + 2 <= d + 18 <= 254)
+                const uint64_t pr = uint64_t(rdl(W.w, e >> 2)) | (uint64_t(rdl(W.w, min((e >> 2) + 1u, 63u))) << 32);
+                const uint32_t off = uint32_t(pr >> ((e & 3u) << 3)) & 0xFFFFu;
+                const uint32_t ms = op + lit;   // the match's output start
+                if (lit < 15u && ml < 19u && ip + 3u + lit <= n && off != 0 && off <= ms &&
+                    uint64_t(ms) + ml <= out_len) {
+                    const bool me = lane() == ns;
+                    so = me ? op : so; slit = me ? lit : slit; ssrc = me ? ip + 1u : ssrc;
+                    soff = me ? off : soff; sml = me ? ml : sml;
+                    ns++;
+                    ip += 3u + lit;
+                    op = ms + ml;
+                    end = ip >= n;
+                    continue;
+                }
+            }
             const uint32_t tok = C.byte(0, src.p + ip++);
             uint32_t lit = tok >> 4;
             if (lit == 15) {
