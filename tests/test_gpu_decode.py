@@ -147,3 +147,42 @@ def test_fast_path_taken_on_benchmark_files(name):
     dec.run()
     assert dec.status(0)["status"] == 0
     assert dec.profile(0)[7] > 0
+
+
+def _lz4_shape_docs():
+    """Documents whose LZ4-compressed insert content covers the decompressor's cases: runs with
+    match offsets 1-3 (overlapping, periodic copies) and length-extension chains past 255, long
+    literal runs (extension bytes, 255 chains), matches reaching back more than one 64-sequence
+    batch and more than one 256-byte window, and short texts that stay uncompressed."""
+    import random
+    rng = random.Random(7)
+    vocab = ["".join(rng.choice("abcdefghij ") for _ in range(rng.randint(2, 9))) for _ in range(40)]
+    texts = [
+        "a" * 1000,
+        "ab" * 300 + "xyz" * 200,
+        "".join(chr(33 + rng.randrange(90)) for _ in range(300)),
+        "".join(chr(33 + rng.randrange(90)) for _ in range(5000)),
+        " ".join(rng.choice(vocab) for _ in range(20000)),
+        "q" * 20 + "".join(chr(33 + rng.randrange(90)) for _ in range(17)) + "q" * 300,
+        "short",
+    ]
+    docs = []
+    for t in texts:
+        o = dt_amd.ListOpLog()
+        a = o.get_or_create_agent_id("lz")
+        pos = 0
+        for i in range(0, len(t), 997):   # several insert runs
+            piece = t[i:i + 997]
+            o.add_insert(a, pos, piece)
+            pos += len(piece)
+        docs.append(o.encode(dt_amd.ENCODE_FULL))
+    return docs
+
+
+def test_lz4_shapes_decode_identically():
+    docs = _lz4_shape_docs()
+    dec = dt_amd.DecodeBatch(docs)
+    dec.run()
+    for i, d in enumerate(docs):
+        assert dec.status(i)["status"] == 0, i
+        _same_arrays(dec, i, d)
