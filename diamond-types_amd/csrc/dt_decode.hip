@@ -1849,12 +1849,20 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
     // prefix-sum offset; a run rarely spans entries, so the per-lane loops are short
     wave_fence();   // the entries were written by lane 0 above
     {
-        uint32_t nout = 0;
+        uint32_t nout = 0, ebase = 0;   // ebase: the entry of the previous chunk's last run
         for (uint32_t b0 = 0; b0 < n_pre; b0 += 64) {
             const uint32_t i = b0 + lane();
             const bool live = i < n_pre;
             const uint4 q = live ? O.pre[i] : make_uint4(0, 0, 0, 0);
-            uint32_t lo = 0, hi = live ? n_ent : 0;
+            // runs and entries are both in LV order, so a run's first entry is at or after ebase:
+            // search the 64 entries from there in registers, HBM only past that window
+            const uint32_t we = ebase + lane() < n_ent ? O.ent[ebase + lane()].y : 0xFFFFFFFFu;
+            uint32_t c = 0;
+#pragma unroll
+            for (uint32_t st = 32; st >= 1; st >>= 1)
+                if (uint32_t(__shfl(int(we), int(c + st - 1))) <= q.x) c += st;
+            if (c == 63 && rdl(we, 63) <= q.x) c = 64;
+            uint32_t lo = ebase + c, hi = live && c == 64 ? n_ent : lo;
             while (lo < hi) {
                 const uint32_t m = (lo + hi) >> 1;
                 if (O.ent[m].y <= q.x) lo = m + 1; else hi = m;
@@ -1884,6 +1892,7 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
                 }
             }
             nout += tot;
+            ebase = rdl(lo, min(n_pre - 1 - b0, 63u));
         }
         R.n_ops = nout;
     }
