@@ -30,19 +30,14 @@ struct dtgpu_oplog {
 
 namespace {
 
-// LDS tiers by block-index size: a document whose (optimistically sized) index fits a tier's
-// cap replays with its index in LDS; each tier is its own launch with the LDS its largest
-// document needs, so friendsforever-sized documents keep ~24 per CU while a node_nodecc-sized
-// one (~129 KiB of index) takes a CU's LDS alone instead of the HBM-index tier.  Bigger
-// documents and LDS overflows replay on the HBM-index tier.
+// LDS tiers of the span replay by expected block count (kSpanTierBlocks: 320 / 1,280 / 4,096 /
+// 11,000 blocks, ~5 / 18 / 57 / 152 KiB of index): a document whose expected index fits a tier
+// replays with its index in LDS, friendsforever-sized documents many per CU, a node_nodecc-sized
+// one alone on a CU.  Bigger documents and LDS overflows replay on the HBM-index tier.
 constexpr int kLdsTiers = kMaxLdsTiers;
-constexpr uint64_t kTierCap[kLdsTiers] = {12 * 1024, 32 * 1024, 64 * 1024, 160 * 1024};
-uint32_t sb_fill() {   // DTGPU_LDS_SB_FILL: superblock-pool sizing experiments
-    const char *e = getenv("DTGPU_LDS_SB_FILL");
-    return e ? std::max<uint32_t>(32, uint32_t(strtoul(e, nullptr, 10))) : LDS_SB_FILL;
-}
-int lds_tier(uint64_t bytes) {
-    for (int t = 0; t < kLdsTiers; t++) if (bytes <= kTierCap[t]) return t;
+static_assert(kSpanTiers == kLdsTiers, "one launch slot per span tier");
+int span_tier(uint32_t est_blocks) {
+    for (int t = 0; t < kLdsTiers; t++) if (est_blocks <= kSpanTierBlocks[t]) return t;
     return -1;
 }
 
@@ -77,7 +72,7 @@ struct dtgpu_batch {
 
     DevBuf<Cmd> d_cmds;
     DevBuf<uint32_t> d_tlist, d_cbyte, d_aruns, d_pos, d_items, d_lists, d_counter;
-    DevBuf<unsigned long long> d_ao, d_m2, d_mup;
+    DevBuf<unsigned long long> d_ao, d_m2, d_mup, d_rows;
     DevBuf<uint32_t> d_tup, d_xf;   // transformed-ops batches only
     bool xf_mode = false;
     DevBuf<uint8_t> d_content, d_out, d_gidx;
@@ -187,7 +182,7 @@ dtgpu_status set_tier_params(dtgpu_batch &B, const BatchParams &base) {
         q.doc_list = B.d_lists.p + off;
         q.n_list = uint32_t(B.tier_list[t].size());
         q.lds_blocks = B.tier_blocks[t];
-        q.lds_sb = lds_sb_capacity(q.lds_blocks, sb_fill());
+        q.lds_sb = span_lds_sb(q.lds_blocks);
         off += B.tier_list[t].size();
         if (fb) { q.fb_count = B.d_fb.p; q.fb_list = B.d_fb.p + 1; }
     }
@@ -214,7 +209,7 @@ int replay_all(dtgpu_batch *B, hipStream_t s) {
     r.side = B->side;
     r.ev_fork = B->ev_fork;
     r.ev_join = B->ev_join;
-    return launch_replay(r);
+    return launch_span_replay(r);
 }
 
 // xf: a transformed-ops batch (iter_xf_operations): host plans in TransformedOpsIter order
@@ -331,9 +326,9 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     std::vector<uint8_t> content;
     uint64_t cmd_total = 0, tlist_total = 0;
     uint64_t lv_total = 0, blk_total = 0, out_total = 0, gidx_total = 0;
-    // expected items per block in the LDS tier (insert-point splits keep typing runs in full
-    // blocks); DTGPU_LDS_FILL overrides it for experiments
-    uint64_t lds_fill = 40;
+    // expected inserted chars per block of spans in the LDS tier; DTGPU_LDS_FILL overrides it
+    // for experiments (a document that outgrows its LDS index replays on the HBM tier)
+    uint64_t lds_fill = SPAN_LDS_FILL;
     if (const char *e = getenv("DTGPU_LDS_FILL")) lds_fill = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
     for (size_t i = 0; i < n; i++) {
         Prepared &p = prep[i];
@@ -347,7 +342,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         if (p.status != OK) { pdesc[i].skip = 1; continue; }
         uint64_t n_ins = 0;
         for (const OpRun &r : p.log.ops) if (r.kind == 0) n_ins += r.len;
-        if (n_ins / 32 + 2 > std::min<uint64_t>(LOC_MAX_BLOCKS, MAX_DOC_BLOCKS)) { B->host_status[i] = ErrCapacity; pdesc[i].skip = 1; continue; }
+        if (xf && n_ins / 32 + 2 > std::min<uint64_t>(LOC_MAX_BLOCKS, MAX_DOC_BLOCKS)) { B->host_status[i] = ErrCapacity; pdesc[i].skip = 1; continue; }
         d.cmd_off = cmd_total;
         d.tlist_off = tlist_total;
         if (p.host_plan) {
@@ -376,7 +371,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         d.content_off = content.size();
         d.content_len = uint32_t(p.log.ins_content.size());
         d.n_aruns = uint32_t(aq);
-        d.max_blocks = uint32_t(n_ins / 32 + 2);
+        d.max_blocks = uint32_t(xf ? n_ins / 32 + 2 : span_max_blocks(n_ins));
         d.blk_off = blk_total;
         d.out_off = out_total;
         d.out_cap = uint32_t(p.log.ins_content.size());
@@ -395,12 +390,11 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         // every document gets an HBM index (the LDS tier hands back documents that outgrow
         // their optimistic LDS capacity); the LDS tier is sized from the expected block fill
         d.gidx_off = gidx_total;
-        gidx_total += index_bytes(d.max_blocks);
-        const uint32_t est = uint32_t(std::min<uint64_t>(d.max_blocks, n_ins / lds_fill + 8));
-        const int t = xf ? -1 : lds_tier(index_bytes_ms(est, lds_sb_capacity(est, sb_fill()), true));
+        gidx_total += xf ? index_bytes(d.max_blocks) : span_index_bytes(d.max_blocks, span_sb_capacity(d.max_blocks), false);
+        const int t = xf ? -1 : span_tier(span_lds_blocks(n_ins, lds_fill));
         if (t >= 0) {
             B->tier_list[t].push_back(uint32_t(i));
-            B->tier_blocks[t] = std::max(B->tier_blocks[t], est);
+            B->tier_blocks[t] = kSpanTierBlocks[t];
         } else {
             B->large_list.push_back(uint32_t(i));
         }
@@ -441,8 +435,12 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     CK(B->d_lists.upload(tier_lists(*B), s));
     CK(B->d_pos.alloc(lv_total));
     CK(B->d_ao.alloc(lv_total));
-    CK(B->d_items.alloc(blk_total * 64));
-    CK(B->d_m2.alloc(2 * blk_total));
+    if (xf) {   // the per-item transformed-ops tracker (dt_replay.hip)
+        CK(B->d_items.alloc(blk_total * 64));
+        CK(B->d_m2.alloc(2 * blk_total));
+    } else {
+        CK(B->d_rows.alloc(blk_total * SPAN_NS));
+    }
     CK(B->d_out.alloc(out_total));
     CK(B->d_gidx.alloc(gidx_total));
     CK(B->d_fb.alloc(n_lds_docs(*B) + 1));
@@ -471,6 +469,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     base.ao = B->d_ao.p;
     base.items = B->d_items.p;
     base.m2 = B->d_m2.p;
+    base.rows = B->d_rows.p;
     base.out = B->d_out.p;
     base.gidx = B->d_gidx.p;
     base.docs = B->d_docs.p;
@@ -605,7 +604,7 @@ dtgpu_status stage_device(const uint8_t *const *docs, const size_t *lens, size_t
 
     // ---- replay layout ---------------------------------------------------------------------------
     uint64_t cmd_total = 0, tlist_total = 0, blk_total = 0, out_total = 0, gidx_total = 0;
-    uint64_t lds_fill = 40;
+    uint64_t lds_fill = SPAN_LDS_FILL;
     if (const char *e = getenv("DTGPU_LDS_FILL")) lds_fill = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
     for (size_t i = 0; i < n; i++) {
         DocDesc &d = B->docs[i];
@@ -615,7 +614,6 @@ dtgpu_status stage_device(const uint8_t *const *docs, const size_t *lens, size_t
         const DecodeResult &r = Dd.res[i];
         const DecodeDesc &dd = Dd.desc[i];
         const uint64_t n_ins = prr[i].n_ins;
-        if (n_ins / 32 + 2 > std::min<uint64_t>(LOC_MAX_BLOCKS, MAX_DOC_BLOCKS)) { B->host_status[i] = ErrCapacity; pdesc[i].skip = 1; continue; }
         d.cmd_off = cmd_total; d.tlist_off = tlist_total;
         d.ncmd = pres[i].ncmd;
         pdesc[i].cmd_off = cmd_total; pdesc[i].tlist_off = tlist_total;
@@ -630,7 +628,7 @@ dtgpu_status stage_device(const uint8_t *const *docs, const size_t *lens, size_t
         d.content_len = r.n_content;
         d.arun_off = pd[i].o_arun * 4;
         d.n_aruns = r.n_aruns;
-        d.max_blocks = uint32_t(n_ins / 32 + 2);
+        d.max_blocks = uint32_t(span_max_blocks(n_ins));
         d.blk_off = blk_total;
         d.out_off = out_total;
         d.out_cap = r.n_content;
@@ -639,12 +637,11 @@ dtgpu_status stage_device(const uint8_t *const *docs, const size_t *lens, size_t
         B->total_lv += r.n_lv;
         B->alg_in_bytes += 16ull * r.n_ops + 8ull * r.n_entries + 4ull * r.n_parents + 12ull * r.n_aruns + r.n_content;
         d.gidx_off = gidx_total;
-        gidx_total += index_bytes(d.max_blocks);
-        const uint32_t est = uint32_t(std::min<uint64_t>(d.max_blocks, n_ins / lds_fill + 8));
-        const int t = lds_tier(index_bytes_ms(est, lds_sb_capacity(est, sb_fill()), true));
+        gidx_total += span_index_bytes(d.max_blocks, span_sb_capacity(d.max_blocks), false);
+        const int t = span_tier(span_lds_blocks(n_ins, lds_fill));
         if (t >= 0) {
             B->tier_list[t].push_back(uint32_t(i));
-            B->tier_blocks[t] = std::max(B->tier_blocks[t], est);
+            B->tier_blocks[t] = kSpanTierBlocks[t];
         } else {
             B->large_list.push_back(uint32_t(i));
         }
@@ -660,8 +657,7 @@ dtgpu_status stage_device(const uint8_t *const *docs, const size_t *lens, size_t
     CK(B->d_lists.upload(tier_lists(*B), s));
     CK(B->d_pos.alloc(lv_total));
     CK(B->d_ao.alloc(lv_total));
-    CK(B->d_items.alloc(blk_total * 64));
-    CK(B->d_m2.alloc(2 * blk_total));
+    CK(B->d_rows.alloc(blk_total * SPAN_NS));
     CK(B->d_out.alloc(out_total));
     CK(B->d_gidx.alloc(gidx_total));
     CK(B->d_fb.alloc(n_lds_docs(*B) + 1));
@@ -679,8 +675,7 @@ dtgpu_status stage_device(const uint8_t *const *docs, const size_t *lens, size_t
     base.aruns = B->d_aruns.p;
     base.pos = B->d_pos.p;
     base.ao = B->d_ao.p;
-    base.items = B->d_items.p;
-    base.m2 = B->d_m2.p;
+    base.rows = B->d_rows.p;
     base.out = B->d_out.p;
     base.gidx = B->d_gidx.p;
     base.docs = B->d_docs.p;
