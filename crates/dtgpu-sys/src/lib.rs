@@ -57,6 +57,7 @@ extern "C" {
     pub fn dtgpu_lz4_compress(input: *const u8, n: usize, out: *mut u8, cap: usize, out_len: *mut usize) -> dtgpu_status;
     pub fn dtgpu_oplog_len(oplog: *const dtgpu_oplog) -> usize;
     pub fn dtgpu_oplog_local_frontier(oplog: *const dtgpu_oplog, out: *mut u64, cap: usize) -> usize;
+    pub fn dtgpu_oplog_last_added_frontier(oplog: *const dtgpu_oplog, out: *mut u64, cap: usize) -> usize;
     pub fn dtgpu_oplog_dominators(oplog: *const dtgpu_oplog, a: *const u64, na: usize, b: *const u64, nb: usize,
                                   out: *mut u64, cap: usize) -> i64;
     // checkout (src/list/oplog.rs:32-42) and transformed ops (src/list/merge.rs:24-48)
@@ -145,10 +146,9 @@ impl ListOpLog {
             let mut n = 0usize;
             let s = dtgpu_oplog_decode_and_add(self.h, data.as_ptr(), data.len(), 0, f.as_mut_ptr(), f.len(), &mut n);
             if s != DTGPU_OK { return Err(s); }
-            if n > f.len() {   // adding the same data again is a no-op that reports the whole version
+            if n > f.len() {   // the buffer was short: read the whole reported frontier back
                 f.resize(n, 0);
-                let s = dtgpu_oplog_decode_and_add(self.h, data.as_ptr(), data.len(), 0, f.as_mut_ptr(), n, &mut n);
-                if s != DTGPU_OK { return Err(s); }
+                n = dtgpu_oplog_last_added_frontier(self.h, f.as_mut_ptr(), n);
             }
             f.truncate(n);
             Ok(f)

@@ -1280,15 +1280,13 @@ static int launch_lds_tier(const BatchParams &q, hipStream_t s, bool prof) {
     size_t lds = size_t(index_bytes_ms(q.lds_blocks, q.lds_sb, true));
     if (const char *pad = getenv("DTGPU_LDS_PAD")) lds += size_t(strtoul(pad, nullptr, 10));   // occupancy experiments
     if (lds > 160 * 1024) return ErrArg;   // a tier cap above the CU's LDS
-    static bool attr = false;   // allow dynamic LDS up to the CU's 160 KiB
-    if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(&dev::replay_kernel<true, false, false>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess ||
-            hipFuncSetAttribute(reinterpret_cast<const void *>(&dev::replay_kernel<true, true, false>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
-            return ErrHip;
-        attr = true;
-    }
+    // allow dynamic LDS up to the CU's 160 KiB: a per-function, per-device attribute, set on
+    // every launch (cheap) so it holds on whatever device the batch runs
+    if (lds > 64 * 1024 &&
+        hipFuncSetAttribute(reinterpret_cast<const void *>(prof ? &dev::replay_kernel<true, true, false>
+                                                                : &dev::replay_kernel<true, false, false>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+        return ErrHip;
     if (prof) hipLaunchKernelGGL((dev::replay_kernel<true, true, false>), dim3(q.n_list), dim3(64), lds, s, q);
     else hipLaunchKernelGGL((dev::replay_kernel<true, false, false>), dim3(q.n_list), dim3(64), lds, s, q);
     return hipGetLastError() == hipSuccess ? OK : ErrHip;

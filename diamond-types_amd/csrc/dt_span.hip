@@ -188,6 +188,13 @@ template <uint32_t MB> DEV void set_sbl(Doc &D, size_t i, uint32_t v) {
     if (MB) reinterpret_cast<uint16_t *>(EXT<MB>(D))[mb_of<MB>(D) + i] = uint16_t(v);
     else EXT<MB>(D)[mb_of<MB>(D) + i] = v;
 }
+// Index counter update from one lane.  LDS tiers: a returnless LDS atomic (fire and forget: no
+// read-back round trip on the command's critical path).  HBM tier: plain read-modify-write (the
+// wave owns the document; a global atomic would leave L2 as a memory-side request).
+template <uint32_t MB> DEV void ix_add(uint32_t *p, uint32_t v) {
+    if (MB) __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    else *p += v;
+}
 template <uint32_t MB> DEV uint32_t top_of(const Doc &D, uint32_t b) { return U(SBPOS<MB>(D)[U(opos_of<MB>(D, b)) >> 6]); }
 
 // ---- rows ------------------------------------------------------------------------------------
@@ -639,15 +646,15 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
             }
         }
         if (l == 0) {
-            CNT<MB>(D)[b] += kk;
-            META<MB>(D)[b] += grow * (1u + M_LIVE);
-            if (known) TV<MB>(D)[tp] += kk, TL<MB>(D)[tp] += grow;
+            ix_add<MB>(&CNT<MB>(D)[b], kk);
+            ix_add<MB>(&META<MB>(D)[b], grow * (1u + M_LIVE));
+            if (known) { ix_add<MB>(&TV<MB>(D)[tp], kk); ix_add<MB>(&TL<MB>(D)[tp], grow); }
         }
         if (!known) {   // after a YjsMod scan moved the insertion point: its top position
             if (l == 0) {
                 const uint32_t t2 = SBPOS<MB>(D)[opos_of<MB>(D, b) >> 6];
-                TV<MB>(D)[t2] += kk;
-                TL<MB>(D)[t2] += grow;
+                ix_add<MB>(&TV<MB>(D)[t2], kk);
+                ix_add<MB>(&TL<MB>(D)[t2], grow);
             }
         }
         wave_fence();
@@ -658,7 +665,6 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
         left -= kk;
     }
     if (D.err) return;
-    g_cold.n_items += k;
     if (known) {
         D.cb = b; D.cn = n; D.ccnt = wave_sum(s_vis(rw)); D.ctp = tp; D.cbase = base;
         D.crl = rl; D.crw = rw;
@@ -730,10 +736,10 @@ DEV void do_delete(Doc &D, uint32_t lv, uint32_t n_del, uint32_t pos, bool fwd) 
         const uint32_t from = first_lane(cm);
         store_row(D, b, rl, rw, from, n + grow);
         if (l == 0) {
-            CNT<MB>(D)[b] -= take;
-            META<MB>(D)[b] += grow * (1u + M_LIVE);   // every piece of a visible span is live
-            TV<MB>(D)[tp] -= take;
-            TL<MB>(D)[tp] += grow;
+            ix_add<MB>(&CNT<MB>(D)[b], 0u - (take));
+            ix_add<MB>(&META<MB>(D)[b], grow * (1u + M_LIVE));   // every piece of a visible span is live
+            ix_add<MB>(&TV<MB>(D)[tp], 0u - (take));
+            ix_add<MB>(&TL<MB>(D)[tp], grow);
         }
         wave_fence();
         D.cb = b; D.cn = n + grow; D.ccnt = bvis - take; D.ctp = tp; D.cbase = base;
@@ -795,10 +801,10 @@ DEV void apply_run(Doc &D, uint32_t b, uint32_t lo, uint32_t hi, uint32_t kd, ui
         const uint32_t o = U(opos_of<MB>(D, b));
         const uint32_t tp = U(SBPOS<MB>(D)[o >> 6]);
         if (l == 0) {
-            CNT<MB>(D)[b] += dv;
-            META<MB>(D)[b] += grow + (dl << 8);
-            TV<MB>(D)[tp] += dv;
-            TL<MB>(D)[tp] += dl;
+            ix_add<MB>(&CNT<MB>(D)[b], dv);
+            ix_add<MB>(&META<MB>(D)[b], grow + (dl << 8));
+            ix_add<MB>(&TV<MB>(D)[tp], dv);
+            ix_add<MB>(&TL<MB>(D)[tp], dl);
         }
         wave_fence();
         if (b == D.cb) {
@@ -856,6 +862,7 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
         };
         u64 heads = heads_of(blk);
         u64 pend = vm;
+        uint32_t nB = NONE, nrl = 0, nrw = 0, nn = 0;   // the next distinct block's row, in flight
         u64 bound = heads | ~vm;   // run boundaries: run starts and lanes outside the runs
         auto tail_of = [&](uint32_t hl) -> uint32_t {
             const u64 after = bound & ~lanes_below(hl + 1);
@@ -868,7 +875,25 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
             const u64 hb = heads & inB;
             // one pass over B's row: per span, the runs overlapping it
             uint32_t rl, rw, nsp;
-            get_row<MB>(D, B, rl, rw, nsp);
+            if (B == nB) {
+                rl = nrl; rw = l < nn ? nrw : 0u; nsp = nn;
+            } else {
+                get_row<MB>(D, B, rl, rw, nsp);
+            }
+            nB = NONE;
+            {   // issue the next distinct block's row load before working on this one
+                const u64 rest = pend & ~inB;
+                if (rest) {
+                    const uint32_t B2 = U(bcast(blk, first_lane(rest)));
+                    if (B2 != D.cb) {
+                        const u64 v = D.rows[size_t(B2) * NS + l];
+                        nrl = uint32_t(v);
+                        nrw = uint32_t(v >> 32);
+                        nn = U(m_n(META<MB>(D)[B2]));
+                        nB = B2;
+                    }
+                }
+            }
             const uint32_t len = s_len(rw), st = s_st(rw);
             uint32_t nov = 0, dd = 0, kk = 0;
             bool part = false;
@@ -930,10 +955,10 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
                 const uint32_t o = U(opos_of<MB>(D, B));
                 const uint32_t tp = U(SBPOS<MB>(D)[o >> 6]);
                 if (l == 0) {
-                    CNT<MB>(D)[B] += dv;
-                    META<MB>(D)[B] += dl << 8;
-                    TV<MB>(D)[tp] += dv;
-                    TL<MB>(D)[tp] += dl;
+                    ix_add<MB>(&CNT<MB>(D)[B], dv);
+                    ix_add<MB>(&META<MB>(D)[B], dl << 8);
+                    ix_add<MB>(&TV<MB>(D)[tp], dv);
+                    ix_add<MB>(&TL<MB>(D)[tp], dl);
                 }
                 wave_fence();
                 if (B == D.cb) {
@@ -945,6 +970,7 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
             }
             pend &= ~inB;
             if (relinked) {   // a block split moved LVs: the pending lanes' blocks are stale
+                nB = NONE;
                 blk = isdel ? D.lk[item] : D.lk[xs];
                 heads = (heads_of(blk) | (pend & ~(pend << 1))) & pend;
                 bound = heads | ~pend;
@@ -959,7 +985,7 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
 // order into out[] (list/merge.rs:63-95), with the order-dependent hash the host checks.
 template <uint32_t MB> DEV void materialise(Doc &D, uint8_t *out, uint32_t cap, uint32_t &len_out, u64 &hash_out) {
     const uint32_t l = lane_id();
-    uint32_t total = 0;
+    uint32_t total = 0, items = 0;
     u64 h = 0;
     for (uint32_t p = 0; p < D.nsb; p++) {
         const uint32_t S = U(TS<MB>(D)[p]), nbk = U(TN<MB>(D)[p]);
@@ -969,6 +995,7 @@ template <uint32_t MB> DEV void materialise(Doc &D, uint8_t *out, uint32_t cap, 
             if (n == 0) continue;   // the empty first block of an empty document
             uint32_t rl, rw;
             load_row(D, b, n, rl, rw);
+            items += wave_sum(s_len(rw));
             const uint32_t len = s_vis(rw);
             const uint32_t c0 = g_cold.cbyte[len ? rl : 0u];
             uint32_t nb = len;
@@ -994,6 +1021,7 @@ template <uint32_t MB> DEV void materialise(Doc &D, uint8_t *out, uint32_t cap, 
     }
     len_out = total;
     hash_out = wave_sum64(h);
+    g_cold.n_items = items;
 }
 
 // Debug-mode consistency check of the whole structure (DTGPU_DEBUG=1): 0 or a code.  Every block

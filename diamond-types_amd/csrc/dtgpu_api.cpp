@@ -26,6 +26,7 @@ using namespace dtgpu;
 
 struct dtgpu_oplog {
     HostOpLog o;
+    std::vector<uint64_t> last_added;   // the frontier the last decode_and_add reported
 };
 
 namespace {
@@ -39,6 +40,33 @@ static_assert(kSpanTiers == kLdsTiers, "one launch slot per span tier");
 int span_tier(uint32_t est_blocks) {
     for (int t = 0; t < kLdsTiers; t++) if (est_blocks <= kSpanTierBlocks[t]) return t;
     return -1;
+}
+// DTGPU_ITEM_REPLAY=1: replay checkouts on the round-2 per-item tracker (dt_replay.hip) instead,
+// for A/B measurements on the same box.  Its LDS tiers go by index bytes.
+bool item_replay() { return getenv("DTGPU_ITEM_REPLAY") != nullptr; }
+constexpr uint64_t kItemTierCap[kLdsTiers] = {12 * 1024, 32 * 1024, 64 * 1024, 160 * 1024};
+int item_tier(uint32_t est) {
+    const uint64_t bytes = index_bytes_ms(est, lds_sb_capacity(est), true);
+    for (int t = 0; t < kLdsTiers; t++) if (bytes <= kItemTierCap[t]) return t;
+    return -1;
+}
+// Per-document replay layout of either tracker: block capacity, HBM index bytes, LDS tier.
+struct Layout { uint32_t max_blocks; uint64_t gidx; int tier; uint32_t tier_blocks; };
+Layout replay_layout(uint64_t n_ins, uint64_t lds_fill, bool item, bool hbm_only) {
+    Layout L{};
+    if (item) {
+        L.max_blocks = uint32_t(n_ins / 32 + 2);
+        L.gidx = index_bytes(L.max_blocks);
+        const uint32_t est = uint32_t(std::min<uint64_t>(L.max_blocks, n_ins / 40 + 8));
+        L.tier = hbm_only ? -1 : item_tier(est);
+        L.tier_blocks = est;
+    } else {
+        L.max_blocks = uint32_t(span_max_blocks(n_ins));
+        L.gidx = span_index_bytes(L.max_blocks, span_sb_capacity(L.max_blocks), false);
+        L.tier = hbm_only ? -1 : span_tier(span_lds_blocks(n_ins, lds_fill));
+        L.tier_blocks = L.tier >= 0 ? kSpanTierBlocks[L.tier] : 0;
+    }
+    return L;
 }
 
 }  // namespace
@@ -75,6 +103,7 @@ struct dtgpu_batch {
     DevBuf<unsigned long long> d_ao, d_m2, d_mup, d_rows;
     DevBuf<uint32_t> d_tup, d_xf;   // transformed-ops batches only
     bool xf_mode = false;
+    bool item_mode = false;   // DTGPU_ITEM_REPLAY: the per-item tracker replays checkouts
     DevBuf<uint8_t> d_content, d_out, d_gidx;
     DevBuf<uint32_t> d_fb;   // [0] = count, then the handed-back documents
     DevBuf<DocDesc> d_docs;
@@ -182,7 +211,7 @@ dtgpu_status set_tier_params(dtgpu_batch &B, const BatchParams &base) {
         q.doc_list = B.d_lists.p + off;
         q.n_list = uint32_t(B.tier_list[t].size());
         q.lds_blocks = B.tier_blocks[t];
-        q.lds_sb = span_lds_sb(q.lds_blocks);
+        q.lds_sb = B.item_mode ? lds_sb_capacity(q.lds_blocks) : span_lds_sb(q.lds_blocks);
         off += B.tier_list[t].size();
         if (fb) { q.fb_count = B.d_fb.p; q.fb_list = B.d_fb.p + 1; }
     }
@@ -209,7 +238,7 @@ int replay_all(dtgpu_batch *B, hipStream_t s) {
     r.side = B->side;
     r.ev_fork = B->ev_fork;
     r.ev_join = B->ev_join;
-    return launch_span_replay(r);
+    return B->item_mode ? launch_replay(r) : launch_span_replay(r);
 }
 
 // xf: a transformed-ops batch (iter_xf_operations): host plans in TransformedOpsIter order
@@ -237,6 +266,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     B->n_lv.resize(n);
     B->docs.resize(n);
     B->host_planned.assign(n, 0);
+    B->item_mode = !xf && item_replay();
     const bool force_host = xf || getenv("DTGPU_HOST_PLAN") != nullptr;
 
     // ---- 1. device planner inputs; a sizing pass of the planner gives exact stream sizes ----
@@ -342,7 +372,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         if (p.status != OK) { pdesc[i].skip = 1; continue; }
         uint64_t n_ins = 0;
         for (const OpRun &r : p.log.ops) if (r.kind == 0) n_ins += r.len;
-        if (xf && n_ins / 32 + 2 > std::min<uint64_t>(LOC_MAX_BLOCKS, MAX_DOC_BLOCKS)) { B->host_status[i] = ErrCapacity; pdesc[i].skip = 1; continue; }
+        if ((xf || B->item_mode) && n_ins / 32 + 2 > std::min<uint64_t>(LOC_MAX_BLOCKS, MAX_DOC_BLOCKS)) { B->host_status[i] = ErrCapacity; pdesc[i].skip = 1; continue; }
         d.cmd_off = cmd_total;
         d.tlist_off = tlist_total;
         if (p.host_plan) {
@@ -371,7 +401,8 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         d.content_off = content.size();
         d.content_len = uint32_t(p.log.ins_content.size());
         d.n_aruns = uint32_t(aq);
-        d.max_blocks = uint32_t(xf ? n_ins / 32 + 2 : span_max_blocks(n_ins));
+        const Layout lay = replay_layout(n_ins, lds_fill, xf || B->item_mode, xf);
+        d.max_blocks = lay.max_blocks;
         d.blk_off = blk_total;
         d.out_off = out_total;
         d.out_cap = uint32_t(p.log.ins_content.size());
@@ -390,11 +421,11 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         // every document gets an HBM index (the LDS tier hands back documents that outgrow
         // their optimistic LDS capacity); the LDS tier is sized from the expected block fill
         d.gidx_off = gidx_total;
-        gidx_total += xf ? index_bytes(d.max_blocks) : span_index_bytes(d.max_blocks, span_sb_capacity(d.max_blocks), false);
-        const int t = xf ? -1 : span_tier(span_lds_blocks(n_ins, lds_fill));
+        gidx_total += lay.gidx;
+        const int t = lay.tier;
         if (t >= 0) {
             B->tier_list[t].push_back(uint32_t(i));
-            B->tier_blocks[t] = kSpanTierBlocks[t];
+            B->tier_blocks[t] = std::max(B->tier_blocks[t], lay.tier_blocks);
         } else {
             B->large_list.push_back(uint32_t(i));
         }
@@ -435,7 +466,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     CK(B->d_lists.upload(tier_lists(*B), s));
     CK(B->d_pos.alloc(lv_total));
     CK(B->d_ao.alloc(lv_total));
-    if (xf) {   // the per-item transformed-ops tracker (dt_replay.hip)
+    if (xf || B->item_mode) {   // the per-item tracker (dt_replay.hip): transformed ops, A/B runs
         CK(B->d_items.alloc(blk_total * 64));
         CK(B->d_m2.alloc(2 * blk_total));
     } else {
@@ -511,6 +542,7 @@ dtgpu_status stage_device(const uint8_t *const *docs, const size_t *lens, size_t
     B->n_lv.assign(n, 0);
     B->docs.assign(n, DocDesc{});
     B->host_planned.assign(n, 0);
+    B->item_mode = item_replay();
 
     // ---- prep layout ----------------------------------------------------------------------------
     std::vector<PrepDesc> pd(n);
@@ -628,7 +660,9 @@ dtgpu_status stage_device(const uint8_t *const *docs, const size_t *lens, size_t
         d.content_len = r.n_content;
         d.arun_off = pd[i].o_arun * 4;
         d.n_aruns = r.n_aruns;
-        d.max_blocks = uint32_t(span_max_blocks(n_ins));
+        if (B->item_mode && n_ins / 32 + 2 > std::min<uint64_t>(LOC_MAX_BLOCKS, MAX_DOC_BLOCKS)) { B->host_status[i] = ErrCapacity; pdesc[i].skip = 1; continue; }
+        const Layout lay = replay_layout(n_ins, lds_fill, B->item_mode, false);
+        d.max_blocks = lay.max_blocks;
         d.blk_off = blk_total;
         d.out_off = out_total;
         d.out_cap = r.n_content;
@@ -637,11 +671,11 @@ dtgpu_status stage_device(const uint8_t *const *docs, const size_t *lens, size_t
         B->total_lv += r.n_lv;
         B->alg_in_bytes += 16ull * r.n_ops + 8ull * r.n_entries + 4ull * r.n_parents + 12ull * r.n_aruns + r.n_content;
         d.gidx_off = gidx_total;
-        gidx_total += span_index_bytes(d.max_blocks, span_sb_capacity(d.max_blocks), false);
-        const int t = span_tier(span_lds_blocks(n_ins, lds_fill));
+        gidx_total += lay.gidx;
+        const int t = lay.tier;
         if (t >= 0) {
             B->tier_list[t].push_back(uint32_t(i));
-            B->tier_blocks[t] = kSpanTierBlocks[t];
+            B->tier_blocks[t] = std::max(B->tier_blocks[t], lay.tier_blocks);
         } else {
             B->large_list.push_back(uint32_t(i));
         }
@@ -657,7 +691,12 @@ dtgpu_status stage_device(const uint8_t *const *docs, const size_t *lens, size_t
     CK(B->d_lists.upload(tier_lists(*B), s));
     CK(B->d_pos.alloc(lv_total));
     CK(B->d_ao.alloc(lv_total));
-    CK(B->d_rows.alloc(blk_total * SPAN_NS));
+    if (B->item_mode) {
+        CK(B->d_items.alloc(blk_total * 64));
+        CK(B->d_m2.alloc(2 * blk_total));
+    } else {
+        CK(B->d_rows.alloc(blk_total * SPAN_NS));
+    }
     CK(B->d_out.alloc(out_total));
     CK(B->d_gidx.alloc(gidx_total));
     CK(B->d_fb.alloc(n_lds_docs(*B) + 1));
@@ -675,6 +714,8 @@ dtgpu_status stage_device(const uint8_t *const *docs, const size_t *lens, size_t
     base.aruns = B->d_aruns.p;
     base.pos = B->d_pos.p;
     base.ao = B->d_ao.p;
+    base.items = B->d_items.p;
+    base.m2 = B->d_m2.p;
     base.rows = B->d_rows.p;
     base.out = B->d_out.p;
     base.gidx = B->d_gidx.p;
@@ -719,7 +760,13 @@ dtgpu_status dtgpu_oplog_decode_and_add(dtgpu_oplog *h, const uint8_t *bytes, si
     if (s != OK) return dtgpu_status(s);
     for (size_t i = 0; i < f.size() && i < cap; i++) frontier[i] = f[i];
     if (n_frontier) *n_frontier = f.size();
+    h->last_added = std::move(f);
     return DTGPU_OK;
+}
+size_t dtgpu_oplog_last_added_frontier(const dtgpu_oplog *h, uint64_t *out, size_t cap) {
+    if (!h) return 0;
+    for (size_t i = 0; i < h->last_added.size() && i < cap; i++) out[i] = h->last_added[i];
+    return h->last_added.size();
 }
 int64_t dtgpu_oplog_doc_id(const dtgpu_oplog *h, char *out, size_t cap) {
     if (!h || !h->o.has_doc_id) return -1;

@@ -113,6 +113,8 @@ def lib():
     L.dtgpu_oplog_encode.argtypes = [vp, pu64, sz, ctypes.c_uint32, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
     L.dtgpu_lz4_compress.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
     L.dtgpu_oplog_decode_and_add.argtypes = [vp, ctypes.c_char_p, sz, c, pu64, sz, ctypes.POINTER(sz)]
+    L.dtgpu_oplog_last_added_frontier.argtypes = [vp, pu64, sz]
+    L.dtgpu_oplog_last_added_frontier.restype = sz
     L.dtgpu_oplog_doc_id.argtypes = [vp, ctypes.c_char_p, sz]
     L.dtgpu_oplog_doc_id.restype = ctypes.c_int64
     L.dtgpu_oplog_set_doc_id.argtypes = [vp, ctypes.c_char_p, sz]
@@ -297,16 +299,15 @@ class ListOpLog:
         `.dt` file or patch, skipping operations already here; returns the file's version.  On a
         ParseError the oplog is left as it was."""
         cap = 64
-        while True:
-            buf = (ctypes.c_uint64 * cap)()
-            n = ctypes.c_size_t()
-            _check(lib().dtgpu_oplog_decode_and_add(self._h, data, len(data), int(ignore_crc), buf, cap,
-                                                    ctypes.byref(n)))
-            if n.value <= cap:
-                return list(buf[:n.value])
-            # a wider version than the buffer: merging the same data again adds nothing and
-            # reports the version in full
-            cap = n.value
+        buf = (ctypes.c_uint64 * cap)()
+        n = ctypes.c_size_t()
+        _check(lib().dtgpu_oplog_decode_and_add(self._h, data, len(data), int(ignore_crc), buf, cap, ctypes.byref(n)))
+        if n.value <= cap:
+            return list(buf[:n.value])
+        # a wider version than the buffer: read the reported frontier back (adds nothing)
+        full = (ctypes.c_uint64 * n.value)()
+        lib().dtgpu_oplog_last_added_frontier(self._h, full, n.value)
+        return list(full)
 
     @property
     def doc_id(self):

@@ -37,7 +37,7 @@ def doc_cost(data: bytes) -> float:
     import dt_amd
     try:
         o = dt_amd.ListOpLog.load_from(data)
-    except Exception:
+    except dt_amd.ParseError:   # only an undecodable document; any other error is a bug and raises
         return float(len(data))
     runs = max(1, len(o.export("ops")))
     ps = o.plan_stats()

@@ -72,6 +72,9 @@ void dtgpu_oplog_free(dtgpu_oplog *oplog);
  * Not safe to call while another thread reads the same oplog. */
 dtgpu_status dtgpu_oplog_decode_and_add(dtgpu_oplog *oplog, const uint8_t *bytes, size_t len, int ignore_crc,
                                         uint64_t *frontier, size_t cap, size_t *n_frontier);
+/* The whole frontier the last successful dtgpu_oplog_decode_and_add reported (for a caller whose
+ * buffer was too small): copies min(len, cap) LVs, returns len.  Reads only; adds nothing. */
+size_t dtgpu_oplog_last_added_frontier(const dtgpu_oplog *oplog, uint64_t *out, size_t cap);
 /* ListOpLog::doc_id (src/list/mod.rs:109): returns the id's byte length (copying min(len, cap)
  * bytes), or -1 when the oplog has none.  set_doc_id with id == NULL clears it. */
 int64_t dtgpu_oplog_doc_id(const dtgpu_oplog *oplog, char *out, size_t cap);
@@ -95,8 +98,11 @@ int64_t dtgpu_oplog_add_delete_without_content(dtgpu_oplog *oplog, int32_t agent
  * the `.dt` bytes of the ops after `from` (an empty `from` is ROOT: the whole oplog).  Written in
  * the reference's order (Graph::optimized_txns_between) through the reference's run mergers, with
  * content fields of >= 20 bytes LZ4-compressed by a restatement of lz4_flex 0.10's block
- * compressor (encode_oplog.rs:270-343), so the bytes equal the reference encoder's for the same
- * options.  flags mirror EncodeOptions (encode_oplog.rs:88-130):
+ * compressor (encode_oplog.rs:270-343).  Byte parity with the reference encoder is pinned on the
+ * reference's own vectors (compat_simple_doc, compat_empty_doc, the LZ4 blocks of the three
+ * benchmark files); for concurrent (multi-agent) histories it is unpinned: no reference-produced
+ * encoding of one exists, so those are checked by round trip only.  flags mirror EncodeOptions
+ * (encode_oplog.rs:88-130):
  *   DTGPU_ENCODE_STORE_INSERTED_CONTENT      store_inserted_content
  *   DTGPU_ENCODE_COMPRESS_CONTENT            compress_content
  *   DTGPU_ENCODE_STORE_START_BRANCH_CONTENT  store_start_branch_content: with a non-ROOT `from`
