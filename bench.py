@@ -445,6 +445,7 @@ def main():
                             "whole batch (decoded oplogs resident in HBM)",
                    "parallelism": f"dp{world} (documents sharded, no data-path collective)"},
         "docs_per_sec": n_total * args.steps / elapsed,
+        "total_merged_ops": total_lv,
         "stage_s": host_stage_s,
         "staging": staging,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

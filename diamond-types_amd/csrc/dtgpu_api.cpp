@@ -41,9 +41,14 @@ int span_tier(uint32_t est_blocks) {
     for (int t = 0; t < kLdsTiers; t++) if (est_blocks <= kSpanTierBlocks[t]) return t;
     return -1;
 }
-// DTGPU_ITEM_REPLAY=1: replay checkouts on the round-2 per-item tracker (dt_replay.hip) instead,
-// for A/B measurements on the same box.  Its LDS tiers go by index bytes.
-bool item_replay() { return getenv("DTGPU_ITEM_REPLAY") != nullptr; }
+// Checkouts replay on the per-item tracker (dt_replay.hip) -- measured faster than the span
+// tracker on every benchmark document (profiles/r3_ab) -- unless DTGPU_REPLAY=span selects the
+// run-length span tracker (dt_span.hip).  Read per batch, so one process can A/B both.  The
+// per-item tracker's LDS tiers go by index bytes.
+bool item_replay() {
+    const char *m = getenv("DTGPU_REPLAY");
+    return !(m && std::strcmp(m, "span") == 0);
+}
 constexpr uint64_t kItemTierCap[kLdsTiers] = {12 * 1024, 32 * 1024, 64 * 1024, 160 * 1024};
 int item_tier(uint32_t est) {
     const uint64_t bytes = index_bytes_ms(est, lds_sb_capacity(est), true);
@@ -103,7 +108,7 @@ struct dtgpu_batch {
     DevBuf<unsigned long long> d_ao, d_m2, d_mup, d_rows;
     DevBuf<uint32_t> d_tup, d_xf;   // transformed-ops batches only
     bool xf_mode = false;
-    bool item_mode = false;   // DTGPU_ITEM_REPLAY: the per-item tracker replays checkouts
+    bool item_mode = true;    // the per-item tracker replays checkouts (DTGPU_REPLAY=span: spans)
     DevBuf<uint8_t> d_content, d_out, d_gidx;
     DevBuf<uint32_t> d_fb;   // [0] = count, then the handed-back documents
     DevBuf<DocDesc> d_docs;

@@ -27,7 +27,17 @@ def _texts(b):
     return res, [b.text(i) if r["status"] == 0 else None for i, r in enumerate(res)]
 
 
-def test_friendsforever_device_staged():
+@pytest.fixture(params=["item", "span"])
+def replay_mode(request, monkeypatch):
+    """Both trackers: the per-item default and the run-length span tracker (DTGPU_REPLAY=span)."""
+    if request.param == "span":
+        monkeypatch.setenv("DTGPU_REPLAY", "span")
+    else:
+        monkeypatch.delenv("DTGPU_REPLAY", raising=False)
+    return request.param
+
+
+def test_friendsforever_device_staged(replay_mode):
     want = G.trace("friendsforever_flat")["endContent"].encode()
     b = dt_amd.Batch(docs=[G.dt_bytes("friendsforever")] * 64, staging="device")
     res, texts = _texts(b)
@@ -37,13 +47,14 @@ def test_friendsforever_device_staged():
 
 
 @pytest.mark.parametrize("name", ["git-makefile", "node_nodecc"])
-def test_large_docs_device_staged(name):
+def test_large_docs_device_staged(name, replay_mode):
     data = G.dt_bytes(name)
     b = dt_amd.Batch(docs=[data], staging="device")
     res, texts = _texts(b)
-    if res[0]["status"] == dt_amd.DECODE_DEFER:
-        pytest.skip("history wider than the device prep limit")
+    # the benchmark files must take the all-device path: a deferral is a regression, not a skip
+    assert res[0]["status"] != dt_amd.DECODE_DEFER, "benchmark file deferred to the host"
     assert res[0]["status"] == 0
+    assert b.host_planned() == [0]
     want = OracleOpLog.load_from(data).checkout_tip_bytes()
     assert hashlib.sha256(texts[0]).hexdigest() == hashlib.sha256(want).hexdigest()
 
@@ -53,9 +64,10 @@ def test_device_plan_equals_host_plan():
     dev = dt_amd.Batch(docs=docs, staging="device")
     host = dt_amd.Batch(docs=docs)
     dev.run(); dev.sync(); host.run(); host.sync()
+    assert [r["status"] for r in dev.results()] == [0] * len(docs)
+    assert [r["status"] for r in host.results()] == [0] * len(docs)
+    assert dev.host_planned() == [0] * len(docs)
     for i in range(len(docs)):
-        if dev.results()[i]["status"] != 0:
-            continue
         (dc, dt), (hc, ht) = dev.plan(i), host.plan(i)
         assert np.array_equal(dc, hc), G.DT_FILES[i]
         assert np.array_equal(dt, ht), G.DT_FILES[i]
@@ -77,3 +89,27 @@ def test_mixed_errors_and_e2e_rerun():
     r3, t3 = [b.results(), [b.text(i) if r["status"] == 0 else None for i, r in enumerate(b.results())]]
     assert t3 == t1
 
+
+
+def test_document_past_the_block_limit(replay_mode):
+    """A document of 2.2 M inserted chars: more than the per-item tracker's 65,535 blocks
+    (n_ins / 32 + 2, MAX_DOC_BLOCKS: block ids are 16 bits in pc[] and the superblock lists).
+    Either tracker must report a status or the exact text, never a wrong text."""
+    o = dt_amd.ListOpLog()
+    a = o.get_or_create_agent_id("big")
+    text = ""
+    for k in range(22):
+        chunk = chr(ord("a") + k % 26) * 100_000
+        pos = (k * 7919) % (len(text) + 1)
+        o.add_insert(a, pos, chunk)
+        text = text[:pos] + chunk + text[pos:]
+    o.add_delete_without_content(a, 1000, 250_000)
+    text = text[:1000] + text[250_000:]
+    b = dt_amd.Batch(oplogs=[o])
+    res, texts = _texts(b)
+    st = res[0]["status"]
+    if replay_mode == "item":
+        assert st == 65   # DTGPU_ERR_CAPACITY
+    assert st in (0, 65)
+    if st == 0:
+        assert texts[0] == text.encode()

@@ -103,6 +103,25 @@ def test_device_encoded_files_check_out_to_the_goldens(corpus):
         assert dt_amd.ListOpLog.load_from(e).checkout_tip_bytes() == want, i
 
 
+def test_device_encoder_reproduces_reference_bytes():
+    """The reference-held encoder outputs, byte for byte from the device encoder (not only via the
+    host encoder): compat_simple_doc / compat_empty_doc bytes2 (src/list/encoding/tests.rs:374-424)
+    from their three older encodings each, and from compat_simple_doc's construction (:396-400)."""
+    built = dt_amd.ListOpLog()
+    a = built.get_or_create_agent_id("seph")
+    built.add_insert(a, 0, "hi there")
+    built.add_delete_without_content(a, 3, 7)
+    built.add_insert(a, 3, "m")
+    srcs = [G.COMPAT_SIMPLE_2, G.COMPAT_SIMPLE_1, G.COMPAT_SIMPLE_LZ4, built.encode(),
+            G.COMPAT_EMPTY_2, G.COMPAT_EMPTY_1, dt_amd.ListOpLog().encode()]
+    want = [bytes(G.COMPAT_SIMPLE_2)] * 4 + [bytes(G.COMPAT_EMPTY_2)] * 3
+    b = dt_amd.Batch(docs=[bytes(x) for x in srcs], staging="device")
+    b.encode(dt_amd.ENCODE_FULL)
+    for i, w in enumerate(want):
+        assert b.encoded_status(i) == 0, i
+        assert b.encoded(i) == w, i
+
+
 def json_end(name):
     return G.trace(name)["endContent"].encode()
 
