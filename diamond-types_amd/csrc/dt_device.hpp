@@ -138,7 +138,9 @@ struct PlanDesc {       // per document; offsets index the concatenated PlanInpu
     uint64_t base_off;  // vv rows scratch (n_entries * n_agents)
     uint64_t erec_off, doff_off, dense_off;
     uint64_t cmd_off, tlist_off;
+    uint64_t prow_off;    // parent version vectors (per entry, row_stride words, chains < n_agents)
     uint32_t ne, n_agents, n_aruns, ntip, n_lv, ccap, tcap, skip;
+    uint32_t row_stride, pad;
 };
 struct PlanResult {
     uint32_t status, ncmd, ntlist, n_tip;
@@ -149,6 +151,7 @@ struct PlanParams {
     const uint32_t *par, *pent, *pch, *pcnt, *child, *aruns, *tip, *erec, *doff, *dense;
     const Cmd *opc;
     uint32_t *base;
+    const uint32_t *prow;   // per-entry parent version vectors (prep / build_plan_input), <= 64 chains
     uint32_t lds_entries;   // per-wave LDS capacity (entries) of the todo stack / pending counts
     uint32_t max_agents;    // largest agent count among device-planned documents
     uint32_t prof;          // cycle profile into PlanResult.prof

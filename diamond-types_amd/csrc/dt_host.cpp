@@ -1265,6 +1265,13 @@ Status build_plan_input(const HostOpLog &o, PlanInput &pi) {
         clen[c] += E[i].end - E[i].start;
     }
     pi.n_chains = uint32_t(clen.size());
+    // the parent vectors, n_chains words per entry (chains opened later are 0): the device
+    // planner reads each consumed entry's vector instead of rebuilding it from its parents'
+    if (pi.n_chains <= 64) {
+        pi.prow.assign(ne * pi.n_chains, 0);
+        for (size_t i = 0; i < ne; i++)
+            for (size_t c = 0; c < prow[i].size(); c++) pi.prow[i * pi.n_chains + c] = prow[i][c];
+    }
     pi.pch.resize(pi.par.size());
     pi.pcnt.resize(pi.par.size());
     for (size_t k = 0; k < pi.par.size(); k++) {
@@ -1295,6 +1302,7 @@ Status build_plan_input(const HostOpLog &o, PlanInput &pi) {
             r[13 + 3 * j] = has ? pi.pcnt[k] : 0;
         }
         r[17] = r[9] ? pi.child[pi.coff[i + 1] - 1] : 0xFFFFFFFFu;
+        r[18] = r[9] ? pi.child[pi.coff[i]] : 0xFFFFFFFFu;
     }
     // dense chain seq -> LV | is_del tables (the planner copies retreat/advance ranges out)
     pi.doff.assign(pi.n_chains + 1, 0);

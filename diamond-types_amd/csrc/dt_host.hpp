@@ -147,10 +147,12 @@ struct PlanInput {
     std::vector<uint32_t> tip;      // pairs (LV, entry) of cg.version
     // per entry, EREC_WORDS words: start, end, parents offset, parent count, first op run, op
     // runs, chain, first seq in the chain, children offset, child count, first parent LV, then
-    // for the first two parents (entry, chain, ops of that chain up to the parent), last child
+    // for the first two parents (entry, chain, ops of that chain up to the parent), last child,
+    // first child
     std::vector<uint32_t> erec;
     std::vector<uint32_t> pch, pcnt;  // per parent slot: its chain and that chain's ops up to it
     uint32_t n_chains = 0;          // causal chains the entries are partitioned into
+    std::vector<uint32_t> prow;     // per entry: parent version vector over chains (n_chains words)
     std::vector<uint32_t> doff;     // per chain: offset of its dense seq table (n_chains + 1)
     std::vector<uint32_t> dense;    // per chain, by seq: LV | is_del << 30
     bool device_ok = true;

@@ -55,6 +55,8 @@ struct P {
     uint32_t ne, A, ntip, n_lv;
     // scratch: vv rows in HBM; todo stack and pending parent counts in LDS (u16)
     uint32_t *base;
+    const uint32_t *prow;  // K = 1: each entry's parent version vector (row_stride words)
+    uint32_t row_stride;
     uint16_t *todo;      // ready entries (PLAN_TODO_CAP slots)
     uint8_t *pending;    // per entry: unvisited parents | merge flag
     // outputs
@@ -64,13 +66,17 @@ struct P {
     uint32_t count_only;   // sizing pass: count commands and entries, write nothing
     // wave-uniform state
     uint32_t nc, nt, err;
-    uint64_t steps, limit;
-    uint64_t n_ret, n_adv;
+    uint32_t steps, limit;
+    uint32_t n_ret, n_adv;
     uint32_t prof;
-    uint64_t pc[6];
 };
-DEV uint64_t tk(const P &p) { return p.prof ? __builtin_amdgcn_s_memtime() : 0; }
-#define PT(slot) do { if (p.prof) { const uint64_t t_ = __builtin_amdgcn_s_memtime(); p.pc[slot] += t_ - t_last; t_last = t_; } } while (0)
+// DTGPU_PLAN_PROF cycle counters: in LDS, so that the (usually off) profile holds no SGPRs
+__shared__ uint64_t g_pc[7];   // six phases, then the last timestamp
+DEV void tk(const P &p) {
+    if (p.prof && lane_id() == 0) { for (int i = 0; i < 6; i++) g_pc[i] = 0; g_pc[6] = __builtin_amdgcn_s_memtime(); }
+}
+#define PT(slot) do { if (p.prof) { const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+    if (lane_id() == 0) { g_pc[slot] += t_ - g_pc[6]; g_pc[6] = t_; } } } while (0)
 
 DEV void fail(P &p, uint32_t code) {
     if (!p.err) p.err = code;
@@ -83,7 +89,7 @@ DEV bool charge(P &p) {
 // Entry record (EREC_WORDS words) lane by lane; R(rw, k) reads word k.
 enum {
     R_START = 0, R_END, R_POFF, R_NP, R_OP0, R_NOP, R_CHAIN, R_SEQ0, R_CH0, R_NCH, R_PAR0,
-    R_PENT0, R_PCH0, R_PCNT0, R_PENT1, R_PCH1, R_PCNT1, R_LASTCH
+    R_PENT0, R_PCH0, R_PCNT0, R_PENT1, R_PCH1, R_PCNT1, R_LASTCH, R_FIRSTCH
 };
 DEV uint32_t load_rec(const P &p, uint32_t e) {
     const uint32_t l = lane_id();
@@ -231,9 +237,10 @@ DEV void emit_issue(P &p, const VV<1> &from, const VV<1> &to, const VV<1> &dlo, 
     E.off = inc - n; E.n = n; E.src = dlo.v[0] + s0; E.fl = adv ? TL_ADV : 0u;
     if (p.count_only) return;
     uint32_t from_idx = 0, flag = 0;
-    for (u64 m = E.am; m; m &= m - 1) {   // the chain whose output slice holds lane l
+    for (u64 m = E.am; m; m &= m - 1) {   // the chain whose output slice holds lane l (few chains move)
         const uint32_t j = first_lane(m);
         const uint32_t o = U(bcast(E.off, j)), nn = U(bcast(E.n, j));
+        if (o >= 64) break;
         if (l >= o && l < o + nn) { from_idx = U(bcast(E.src, j)) + (l - o); flag = U(bcast(E.fl, j)); }
     }
     if (l < E.total) { E.dv = p.dense[from_idx]; E.dfl = flag; }
@@ -244,18 +251,22 @@ DEV void emit_store(P &p, const Emit &E) {
     if (!p.count_only) {
         bool bad = l < E.total && E.dv == 0xFFFFFFFFu;
         if (l < E.total) p.tlist[p.nt + l] = E.dv | E.dfl;
-        for (uint32_t c = 64; c < E.total; c += 64) {
-            const uint32_t u = c + l;
-            uint32_t from_idx = 0, flag = 0;
+        // outputs past the first 64: each moving chain's slice is one contiguous copy out of its
+        // dense table
+        if (E.total > 64) {
             for (u64 m = E.am; m; m &= m - 1) {
                 const uint32_t j = first_lane(m);
                 const uint32_t o = U(bcast(E.off, j)), nn = U(bcast(E.n, j));
-                if (u >= o && u < o + nn) { from_idx = U(bcast(E.src, j)) + (u - o); flag = U(bcast(E.fl, j)); }
-            }
-            if (u < E.total) {
-                const uint32_t v = p.dense[from_idx];
-                if (v == 0xFFFFFFFFu) bad = true;
-                p.tlist[p.nt + u] = v | flag;
+                const uint32_t src = U(bcast(E.src, j)), fl = U(bcast(E.fl, j));
+                const uint32_t a = max(o, 64u), b = o + nn;
+                for (uint32_t u0 = a; u0 < b; u0 += 64) {
+                    const uint32_t u = u0 + l;
+                    if (u < b) {
+                        const uint32_t v = p.dense[src + (u - o)];
+                        if (v == 0xFFFFFFFFu) bad = true;
+                        p.tlist[p.nt + u] = v | fl;
+                    }
+                }
             }
         }
         if (__ballot(bad)) { fail(p, PLAN_ERR_INTERNAL); return; }
@@ -331,7 +342,7 @@ DEV void plan_doc(P &p, PlanResult *res) {
     }
     if (__ballot(bad_np)) fail(p, PLAN_WIDE_MERGE);
     wave_fence();
-    uint64_t t_last = tk(p);
+    tk(p);
     PT(5);
     uint32_t f = 0xFFFFFFFFu;   // current frontier: ROOT or one LV
     bool have = top > 0;
@@ -468,7 +479,7 @@ DEV void plan_doc(P &p, PlanResult *res) {
         }
         if (!p.err && vv_differ(vf, vt)) {
             const uint32_t t0 = p.nt;
-            const uint64_t adv0 = p.n_adv;
+            const uint32_t adv0 = p.n_adv;
             emit_diff<K>(p, vf, vt, dlo, dhi, false);
             if (!p.err && p.nt > t0) push_cmd(p, CMD_TOG, t0, p.nt - t0, 0);
             res->n_tip = uint32_t(p.n_adv - adv0);
@@ -476,7 +487,263 @@ DEV void plan_doc(P &p, PlanResult *res) {
         }
     }
     if (l == 0) {
-        for (int i = 0; i < 6; i++) res->prof[i] = p.pc[i];
+        for (int i = 0; i < 6; i++) res->prof[i] = p.prof ? g_pc[i] : 0;
+        res->status = p.err;
+        res->ncmd = p.nc;
+        res->ntlist = p.nt;
+        res->n_retreat = p.n_ret;
+        res->n_advance = p.n_adv;
+    }
+}
+
+// ---- <= 64 chains: the software-pipelined walk ------------------------------------------------
+//
+// Same walk, same output as plan_doc<1>, reordered so that one entry's memory round trips hide
+// behind another's work:
+//   * the ready stack lives in registers (Stk below): a push or pick is a few lane operations,
+//     not a chain of dependent LDS reads;
+//   * the next entry is picked right after the current entry's children are counted (a child
+//     list of <= 2 comes from the record: its first and last child), and its record and its
+//     parent version vector are requested before this entry's diff work;
+//   * the parent version vector of every entry is precomputed (the prep kernel's chain
+//     decomposition / build_plan_input compute it anyway), so a merge costs no parent-row
+//     round trips;
+//   * this entry's retreat / advance gather is issued, and written out (with its op-run
+//     commands) one iteration later, behind the next entry's children / pick.
+// The record sits in one VGPR (lane k: word k), fields broadcast on demand.  (Through the
+// scalar cache it would share lgkmcnt with the walk's LDS traffic: every LDS read after the
+// s_load would wait for it -- measured slower.)
+struct Rec { uint32_t w, row; };   // the record and the entry's parent version vector (lane = chain)
+DEV Rec srec(const P &p, uint32_t e) {
+    const uint32_t l = lane_id();
+    return Rec{load_rec(p, e), l < p.A ? p.prow[size_t(e) * p.row_stride + l] : 0u};
+}
+DEV uint32_t F(const Rec &r, int k) { return R(r.w, k); }
+
+// The ready stack with its top 64 entries in registers: lane i holds position nl + i (the
+// nl bottom entries sit in LDS todo[0, nl)), bit i of mm says whether lane i's entry is a merge.
+// Pushes, pops and the merge-skipping pick (txn_trace.rs:249-266, same positions as pick()) are
+// register operations; LDS is touched only when the stack outgrows 64 or drains into its
+// bottom part.
+struct Stk {
+    uint32_t v;      // lane i: entry at position nl + i (i < n)
+    u64 mm;          // merge flags of the register part
+    uint32_t n, nl;  // entries in registers / in LDS
+};
+// Push the lanes of `ready` (child index order = lane order), entry in chv, merge flag in mg.
+DEV bool stk_push(P &p, Stk &S, u64 ready, uint32_t chv, bool mg) {
+    const uint32_t l = lane_id();
+    const uint32_t cnt = uint32_t(__popcll(ready));
+    if (!cnt) return true;
+    if (S.nl + S.n + cnt > PLAN_TODO_CAP) { fail(p, PLAN_TODO_FULL); return false; }
+    if (S.n + cnt > 64) {   // spill the register part to LDS (merge flags stay in pending[])
+        if (l < S.n) p.todo[S.nl + l] = uint16_t(S.v);
+        S.nl += S.n;
+        S.n = 0;
+        S.mm = 0;
+        wave_fence();
+    }
+    // ready lanes in lane order onto positions n, n + 1, ... (usually one or two)
+    const u64 mgm = __ballot(mg);
+    uint32_t at = S.n;
+    for (u64 r = ready; r; r &= r - 1, at++) {
+        const uint32_t j = first_lane(r);
+        const uint32_t e = bcast(chv, j);
+        S.v = l == at ? e : S.v;
+        if ((mgm >> j) & 1ull) S.mm |= 1ull << at;
+    }
+    S.n += cnt;
+    return true;
+}
+// Pop the next entry (as pick()); has_any: S.n + S.nl > 0.
+DEV uint32_t stk_pick(P &p, Stk &S) {
+    const uint32_t l = lane_id();
+    if (S.n == 0) {   // refill from LDS: its top 32 (or fewer) positions
+        const uint32_t k = min(S.nl, 32u);
+        const uint32_t base = S.nl - k;
+        const uint32_t e = l < k ? uint32_t(p.todo[base + l]) : 0u;
+        const bool mg = l < k && (p.pending[e] & MERGE_BIT);
+        S.v = e;
+        S.mm = __ballot(mg);
+        S.n = k;
+        S.nl = base;
+    }
+    const uint32_t t = S.n - 1;
+    uint32_t idx = bcast(S.v, t);
+    if ((S.mm >> t) & 1ull) {
+        const u64 nm = ~S.mm & ((1ull << t) - 1ull);
+        if (nm) {   // the highest non-merge below the top takes its place
+            const uint32_t pos = 63u - uint32_t(__clzll((long long)nm));
+            const uint32_t x = bcast(S.v, pos);
+            S.v = l == pos ? idx : S.v;
+            S.mm |= 1ull << pos;
+            idx = x;
+        } else if (S.nl) {   // scan the LDS part, top down
+            int found = -1;
+            for (int hi = int(S.nl) - 1; hi >= 0 && found < 0; hi -= 64) {
+                const int i = hi - int(l);
+                const bool ok = i >= 0 && !(p.pending[p.todo[i]] & MERGE_BIT);
+                const u64 m = __ballot(ok);
+                if (m) found = hi - int(first_lane(m));
+            }
+            if (found >= 0) {
+                const uint32_t x = U(p.todo[found]);
+                if (l == 0) p.todo[found] = uint16_t(idx);
+                wave_fence();
+                idx = x;
+            }
+        }
+    }
+    S.mm &= ~(1ull << t);
+    S.n--;
+    return U(idx);
+}
+
+DEV void plan_doc1(P &p, PlanResult *res) {
+    const uint32_t l = lane_id();
+    const uint32_t dlo = l < p.A ? p.doff[l] : 0, dhi = l < p.A ? p.doff[l + 1] : 0;
+    VV<1> dl, dh;
+    dl.v[0] = dlo; dh.v[0] = dhi;
+    uint32_t top = 0;
+    bool bad_np = false;
+    for (uint32_t c = 0; c < p.ne; c += 64) {
+        const uint32_t e = c + l;
+        if (e < p.ne) {
+            const uint32_t np = p.erec[size_t(e) * EREC_WORDS + R_NP];
+            if (np > 0x7Fu) bad_np = true;
+            p.pending[e] = uint8_t(min(np, 0x7Fu) | (np >= 2 ? MERGE_BIT : 0));
+        }
+    }
+    for (int c = int((p.ne + 63) / 64) - 1; c >= 0; c--) {
+        if (!charge(p)) break;
+        const uint32_t e = uint32_t(c) * 64 + (63 - l);
+        const bool root = e < p.ne && p.erec[size_t(e) * EREC_WORDS + R_NP] == 0;
+        const u64 m = __ballot(root);
+        const uint32_t rank = uint32_t(__popcll(m & ((1ull << l) - 1ull)));
+        if (top + uint32_t(__popcll(m)) > PLAN_TODO_CAP) { fail(p, PLAN_TODO_FULL); break; }
+        if (root) p.todo[top + rank] = uint16_t(e);
+        top += uint32_t(__popcll(m));
+    }
+    if (__ballot(bad_np)) fail(p, PLAN_WIDE_MERGE);
+    wave_fence();
+    Stk S;
+    S.v = 0; S.mm = 0; S.n = 0; S.nl = top;
+    tk(p);
+    PT(5);
+    VV<1> vf;
+    vf.v[0] = 0;
+    uint32_t f = 0xFFFFFFFFu;
+    // the previous entry's deferred output: its diff (gather in flight) and its op runs
+    Emit pe_em;
+    pe_em.any = false;
+    uint32_t pe_nop = 0, pe_op0 = 0;
+    uint4 pe_oc = make_uint4(0, 0, 0, 0);
+    bool pe_have = false;
+    const uint4 *opw4 = reinterpret_cast<const uint4 *>(p.opc);
+    auto flush = [&]() {   // the previous entry's TOG, tlist slice and op-run commands
+        if (!pe_have) return;
+        if (pe_em.any) {
+            const uint32_t t0 = p.nt;
+            emit_store(p, pe_em);
+            if (p.err) return;
+            if (p.nt > t0) push_cmd(p, CMD_TOG, t0, p.nt - t0, 0);
+        }
+        if (uint64_t(p.nc) + pe_nop > p.ccap) { fail(p, PLAN_CMDS_FULL); return; }
+        if (!p.count_only) {
+            uint4 *cw = reinterpret_cast<uint4 *>(p.cmds) + p.nc;
+            if (l < pe_nop) cw[l] = pe_oc;
+            for (uint32_t j = 64 + l; j < pe_nop; j += 64) cw[j] = opw4[pe_op0 + j];
+        }
+        p.nc += pe_nop;
+        pe_have = false;
+    };
+    bool have = S.nl > 0;
+    uint32_t idx = have ? stk_pick(p, S) : 0;
+    Rec rc;
+    if (have) rc = srec(p, idx);
+    while (have && !p.err) {
+        if (!charge(p)) break;
+        const uint32_t nch = F(rc, R_NCH), ch0 = F(rc, R_CH0), lastch = F(rc, R_LASTCH), firstch = F(rc, R_FIRSTCH);
+        PT(0);
+        // children whose last parent this is become ready (pushed in child index order); the
+        // next entry is picked and its record requested before this entry's own work
+        uint32_t ch = l == 0 ? firstch : lastch;
+        if (nch > 2) ch = l < nch ? p.child[ch0 + l] : 0;
+        for (uint32_t c = 0; c < nch; c += 64) {
+            const uint32_t chv = c == 0 ? ch : (c + l < nch ? p.child[ch0 + c + l] : 0);
+            bool ready = false, mg = false;
+            if (c + l < nch) {
+                const uint8_t pd = uint8_t(p.pending[chv] - 1);
+                p.pending[chv] = pd;
+                ready = (pd & 0x7F) == 0;
+                mg = (pd & MERGE_BIT) != 0;
+            }
+            if (!stk_push(p, S, __ballot(ready), chv, mg)) break;
+        }
+        if (p.err) break;
+        have = S.n + S.nl > 0;
+        uint32_t nidx = 0;
+        Rec nrc;
+        if (have) {
+            nidx = stk_pick(p, S);
+            nrc = srec(p, nidx);
+        }
+        PT(2);
+        // this entry's op runs (written out with its diff one iteration later)
+        const uint32_t op0 = F(rc, R_OP0), nop = F(rc, R_NOP);
+        uint4 oc = make_uint4(0, 0, 0, 0);
+        if (l < nop && !p.count_only) oc = opw4[op0 + l];
+        // the previous entry's output (its gather has been in flight since the end of its
+        // iteration)
+        flush();
+        if (p.err) break;
+        PT(4);
+        const uint32_t e_start = F(rc, R_START), e_end = F(rc, R_END), po = F(rc, R_POFF), np = F(rc, R_NP);
+        const uint32_t chain = F(rc, R_CHAIN), seq0 = F(rc, R_SEQ0), par0 = F(rc, R_PAR0);
+        // version vector of the parents: the entry's precomputed row
+        VV<1> vp;
+        vp.v[0] = rc.row;
+        (void)po; (void)np; (void)par0;
+        PT(1);
+        const VV<1> v_old = vf;
+        vf = vp;
+        fold_entry<1>(p, e_start, e_end, e_end - 1, chain, seq0, vf, true);
+        if (p.err) break;
+        pe_em.any = false;
+        if (vv_differ(v_old, vp)) emit_issue(p, v_old, vp, dl, dh, true, pe_em);
+        if (p.err) break;
+        pe_have = true;
+        pe_nop = nop; pe_op0 = op0;
+        pe_oc = oc;
+        f = e_end - 1;
+        idx = nidx;
+        rc = nrc;
+        PT(3);
+    }
+    if (!p.err) flush();
+    // advance to the tip (cg.version): the replay then holds the checkout
+    if (!p.err) {
+        VV<1> vt;
+        vv_zero(vt);
+        for (uint32_t j = 0; j < p.ntip; j++) {
+            const uint32_t tlv = U(p.tip[2 * j]), te = U(p.tip[2 * j + 1]);
+            const Rec tr = srec(p, te);
+            VV<1> t;
+            t.v[0] = tr.row;
+            fold_entry<1>(p, F(tr, R_START), F(tr, R_END), tlv, F(tr, R_CHAIN), F(tr, R_SEQ0), t, false);
+            vv_max(vt, t);
+        }
+        if (!p.err && vv_differ(vf, vt)) {
+            const uint32_t t0 = p.nt;
+            const uint32_t adv0 = p.n_adv;
+            emit_diff<1>(p, vf, vt, dl, dh, false);
+            if (!p.err && p.nt > t0) push_cmd(p, CMD_TOG, t0, p.nt - t0, 0);
+            res->n_tip = uint32_t(p.n_adv - adv0);
+            p.n_adv = adv0;
+        }
+    }
+    if (l == 0) {
+        for (int i = 0; i < 6; i++) res->prof[i] = p.prof ? g_pc[i] : 0;
         res->status = p.err;
         res->ncmd = p.nc;
         res->ntlist = p.nt;
@@ -515,6 +782,8 @@ DEV void plan_entry(const PlanParams &Q) {
     p.todo = lds16;
     p.pending = reinterpret_cast<uint8_t *>(lds16 + PLAN_TODO_CAP);
     p.base = Q.base + pd.base_off;
+    p.prow = Q.prow + pd.prow_off;
+    p.row_stride = pd.row_stride;
     p.cmds = Q.cmds + pd.cmd_off;
     p.tlist = Q.tlist + pd.tlist_off;
     p.count_only = Q.count_only;
@@ -522,16 +791,20 @@ DEV void plan_entry(const PlanParams &Q) {
     p.tcap = Q.count_only ? 0xFFFFFFFFu : U(pd.tcap);
     p.nc = p.nt = p.err = 0;
     p.steps = 0;
-    p.limit = 1024ull * (uint64_t(p.ne) + 16) + 4ull * pd.n_lv + (1u << 20);
+    p.limit = uint32_t(min<uint64_t>(1024ull * (uint64_t(p.ne) + 16) + 4ull * pd.n_lv + (1u << 20), 0xFFFFFFF0ull));
     p.n_ret = p.n_adv = 0;
     p.prof = Q.prof;
-    for (int i = 0; i < 6; i++) p.pc[i] = 0;
     res->n_tip = 0;
     if (p.ne > Q.lds_entries) {
         if (lane_id() == 0) res->status = PLAN_ERR_INTERNAL;
         return;
     }
+#ifndef DTGPU_PLAN_OLD
+    if constexpr (K == 1) plan_doc1(p, res);
+    else plan_doc<K>(p, res);
+#else
     plan_doc<K>(p, res);
+#endif
 }
 
 #ifndef DTGPU_PLAN_WAVES

@@ -302,7 +302,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
                 if (l == pc) row = max(row, psd + p + 1);   // seq0 + (p - start) + 1
                 if (k == k0) first_chain = pc;
             }
-            if ((keep >> (i & 63u)) & 1u) rows[size_t(i) * PREP_MAX_CHAINS + l] = row;
+            // every entry's parent vector (the planner reads it); the ring serves this loop
+            if (l < nch || ((keep >> (i & 63u)) & 1u)) rows[size_t(i) * PREP_MAX_CHAINS + l] = row;
             uint32_t c = 0xFFFFFFFFu;
             if (first_chain != 0xFFFFFFFFu && rdl(row, first_chain) == rdl(clen, first_chain)) c = first_chain;
             if (c == 0xFFFFFFFFu) {
@@ -357,7 +358,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
         // five 16-byte stores (records are 80 bytes, so 16-byte aligned): words 0-3 start, end,
         // parents offset / count; 4-7 first op run, op runs, chain, seq0; 8-10 children offset /
         // count, first parent LV; 11-13 and 14-16 the first two parents' entry, chain, count;
-        // 17 last child
+        // 17 last child, 18 first child
         static_assert(EREC_WORDS == 20, "erec layout");
         uint4 *r = reinterpret_cast<uint4 *>(erec + size_t(i) * EREC_WORDS);
         const uint2 e = ent[i];
@@ -371,7 +372,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
         r[2] = make_uint4(c0, nc, h0 ? par[p0] : 0xFFFFFFFFu, h0 ? pent[p0] : 0xFFFFFFFFu);
         r[3] = make_uint4(h0 ? pch[p0] : 0u, h0 ? pcnt[p0] : 0u, h1 ? pent[p0 + 1] : 0xFFFFFFFFu,
                           h1 ? pch[p0 + 1] : 0u);
-        r[4] = make_uint4(h1 ? pcnt[p0 + 1] : 0u, nc ? child[c0 + nc - 1] : 0xFFFFFFFFu, 0u, 0u);
+        r[4] = make_uint4(h1 ? pcnt[p0 + 1] : 0u, nc ? child[c0 + nc - 1] : 0xFFFFFFFFu, nc ? child[c0] : 0xFFFFFFFFu, 0u);
     }
     // op runs: apply commands and the dense chain tables (LV | is_del per chain seq)
     uint32_t n_ins = 0;

@@ -277,7 +277,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     // ---- 1. device planner inputs; a sizing pass of the planner gives exact stream sizes ----
     std::vector<PlanDesc> pdesc(n);
     {
-        std::vector<uint32_t> par, pent, pch, pcnt, child, tip, aruns, erec, doff, dense;
+        std::vector<uint32_t> par, pent, pch, pcnt, child, tip, aruns, erec, doff, dense, base_rows;
         std::vector<Cmd> opc;
         uint64_t base_total = 0, n_entries = 0;
         uint32_t lds_entries = 0, max_agents = 0;
@@ -303,6 +303,8 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
             q.doff_off = doff.size();
             q.dense_off = dense.size();
             q.base_off = base_total;
+            q.prow_off = base_total;   // host-staged: the base rows arrive filled (build_plan_input)
+            q.row_stride = pi.n_chains;
             q.ne = uint32_t(ne);
             q.n_agents = pi.n_chains;
             q.n_aruns = uint32_t(pi.aruns.size() / 4);
@@ -313,6 +315,8 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
             append(par, pi.par); append(pent, pi.pent); append(pch, pi.pch); append(pcnt, pi.pcnt);
             append(child, pi.child); append(opc, pi.opc);
             append(tip, pi.tip); append(erec, pi.erec); append(doff, pi.doff); append(dense, pi.dense);
+            if (pi.prow.size() == ne * pi.n_chains) append(base_rows, pi.prow);
+            else base_rows.resize(base_rows.size() + ne * pi.n_chains, 0);
             base_total += ne * pi.n_chains;
             n_entries += ne;
             lds_entries = std::max<uint32_t>(lds_entries, uint32_t(ne));
@@ -322,7 +326,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         CK(B->p_pch.upload(pch, s)); CK(B->p_pcnt.upload(pcnt, s));
         CK(B->p_opc.upload(opc, s)); CK(B->d_aruns.upload(aruns, s)); CK(B->p_tip.upload(tip, s));
         CK(B->p_erec.upload(erec, s)); CK(B->p_doff.upload(doff, s)); CK(B->p_dense.upload(dense, s));
-        CK(B->p_base.alloc(base_total));
+        CK(B->p_base.upload(base_rows, s));
         CK(B->p_docs.upload(pdesc, s));
         CK(B->p_results.alloc(n));
         CK(hipMemsetAsync(B->p_results.p, 0, std::max<size_t>(n, 1) * sizeof(PlanResult), s));
@@ -330,7 +334,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         q.par = B->p_par.p; q.pent = B->p_pent.p; q.pch = B->p_pch.p; q.pcnt = B->p_pcnt.p;
         q.child = B->p_child.p; q.opc = B->p_opc.p;
         q.aruns = B->d_aruns.p; q.tip = B->p_tip.p; q.erec = B->p_erec.p; q.doff = B->p_doff.p;
-        q.dense = B->p_dense.p; q.base = B->p_base.p;
+        q.dense = B->p_dense.p; q.base = B->p_base.p; q.prow = B->p_base.p;
         q.lds_entries = (lds_entries + 7) & ~7u;
         q.max_agents = max_agents;
         q.prof = getenv("DTGPU_PLAN_PROF") ? 1u : 0u;
@@ -586,6 +590,9 @@ dtgpu_status stage_device(const uint8_t *const *docs, const size_t *lens, size_t
     CK(B->p_child.alloc(o_par)); CK(B->p_opc.alloc(o_op)); CK(B->d_aruns.alloc(4 * o_arun));
     CK(B->p_tip.alloc(2 * o_tip)); CK(B->p_erec.alloc(o_erec)); CK(B->p_doff.alloc(o_doff));
     CK(B->p_dense.alloc(o_dense)); CK(B->pr_rows.alloc(o_rows)); CK(B->pr_scr.alloc(o_scr));
+    // prep stores each entry's parent vector at the chains that exist by then; the words past
+    // them stay zero from here on (every pass writes the same words)
+    CK(hipMemsetAsync(B->pr_rows.p, 0, std::max<uint64_t>(o_rows, 1) * sizeof(uint32_t), s));
     CK(B->pr_docs.upload(pd, s)); CK(B->pr_res.alloc(n));
     PrepParams &pp = B->prep;
     pp.in = Dd.in.p;
@@ -615,6 +622,8 @@ dtgpu_status stage_device(const uint8_t *const *docs, const size_t *lens, size_t
         q.par_off = r.o_par; q.child_off = r.o_child; q.op_off = r.o_op; q.arun_off = r.o_arun; q.tip_off = r.o_tip;
         q.erec_off = r.o_erec; q.doff_off = r.o_doff; q.dense_off = r.o_dense;
         q.base_off = base_total;
+        q.prow_off = r.o_rows;   // device-staged: the prep kernel's parent vectors
+        q.row_stride = PREP_MAX_CHAINS;
         q.ne = r.ne; q.n_agents = prr[i].n_chains; q.n_aruns = r.n_aruns; q.ntip = r.n_ver; q.n_lv = r.n_lv;
         base_total += uint64_t(r.ne) * std::max<uint32_t>(prr[i].n_chains, 1);
         lds_entries = std::max<uint32_t>(lds_entries, r.ne);
@@ -627,7 +636,7 @@ dtgpu_status stage_device(const uint8_t *const *docs, const size_t *lens, size_t
     PlanParams &q = B->plan;
     q.par = B->p_par.p; q.pent = B->p_pent.p; q.pch = B->p_pch.p; q.pcnt = B->p_pcnt.p; q.child = B->p_child.p;
     q.opc = B->p_opc.p; q.aruns = B->d_aruns.p; q.tip = B->p_tip.p; q.erec = B->p_erec.p; q.doff = B->p_doff.p;
-    q.dense = B->p_dense.p; q.base = B->p_base.p;
+    q.dense = B->p_dense.p; q.base = B->p_base.p; q.prow = B->pr_rows.p;
     q.lds_entries = (lds_entries + 7) & ~7u;
     q.max_agents = max_agents;
     q.prof = getenv("DTGPU_PLAN_PROF") ? 1u : 0u;
