@@ -244,7 +244,7 @@ template <bool L> DEV uint32_t key_at(const Doc &D, uint32_t b, uint32_t s) {
 DEV uint32_t find_slot(const Doc &D, uint32_t b, uint32_t item) {
     const uint4 *row = reinterpret_cast<const uint4 *>(D.items + size_t(b) * BLK);
     uint32_t s = BLK;
-    for (uint32_t q = 0; q < BLK / 4 && s == BLK; q += 2) {   // 32 bytes per round: few VGPRs
+    for (uint32_t q = 0; q < BLK / 4 && s == BLK; q += 2) {
         uint4 v[2];
 #pragma unroll
         for (uint32_t j = 0; j < 2; j++) v[j] = row[q + j];
@@ -591,7 +591,7 @@ DEV void agent_of(Doc &D, uint32_t lv, uint32_t &rank, uint32_t &seq) {
 // last event lane before it.  Returns the insertion point in (b, s).
 template <bool L>
 DEV void yjs_scan(Doc &D, uint32_t &b, uint32_t &s, uint32_t rb, uint32_t rs, uint32_t my_l, uint32_t my_r,
-                  uint32_t orr_new, uint32_t lv) {
+                  uint32_t ol_new, uint32_t orr_new, uint32_t lv) {
     const uint32_t l = lane_id();
     uint32_t new_rank, new_seq;
     agent_of(D, lv, new_rank, new_seq);
@@ -618,8 +618,23 @@ DEV void yjs_scan(Doc &D, uint32_t &b, uint32_t &s, uint32_t rb, uint32_t rs, ui
             ol_o = uint32_t(x);
             orr_o = uint32_t(x >> 32);
         }
-        const uint32_t kl = ol_o == ROOT_ID ? 0u : key_of<L>(D, ol_o) + 1u;
-        const uint32_t kr = orr_o == END_ID ? 0xFFFFFFFFu : key_of<L>(D, orr_o);
+        // kl = key(origin_left) + 1 against my_l.  Without a key lookup when the candidate's
+        // origin_left is mine (equal), ROOT (0), or the candidate just before it in the scanned
+        // range (after the cursor, so after my origin_left: greater) -- concurrent typing
+        // (merge.rs:199-243 compares cursor positions; the same order).
+        const uint32_t prev = shfl(o, (l - 1) & 63u);
+        const bool l_eq = ol_o == ol_new, l_root = ol_o == ROOT_ID;
+        const bool l_gt = !l_eq && !l_root && l > cs && ol_o == prev;
+        uint32_t kl = l_eq ? my_l : (l_root ? 0u : (l_gt ? my_l + 1u : 0u));
+        if (__ballot(inr && !l_eq && !l_root && !l_gt)) {
+            if (inr && !l_eq && !l_root && !l_gt) kl = key_of<L>(D, ol_o) + 1u;
+        }
+        // kr = key(origin_right): only where the scan state machine reads it
+        uint32_t kr = 0xFFFFFFFFu;
+        const bool need_r = inr && kl == my_l && orr_o != orr_new && orr_o != END_ID;
+        if (__ballot(need_r)) {
+            if (need_r) kr = key_of<L>(D, orr_o);
+        }
         const bool tie = inr && kl == my_l && orr_o == orr_new;
         bool new_lt = false;
         for (u64 mt = __ballot(tie); mt; mt &= mt - 1) {
@@ -742,7 +757,7 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
         const uint32_t my_l = ol == ROOT_ID ? 0u : ukey_of<L>(D, ol) + 1u;
         const uint32_t my_r = orr == END_ID ? 0xFFFFFFFFu : ukey_of<L>(D, orr);
         const uint32_t b0 = b;
-        yjs_scan<L>(D, b, s, rb, rs, my_l, my_r, orr, lv);
+        yjs_scan<L>(D, b, s, rb, rs, my_l, my_r, ol, orr, lv);
         if (D.err) return;
         if (b != b0) {
             if (b == D.cb) { it = D.cit; mv = D.cmv; ml = D.cml; }

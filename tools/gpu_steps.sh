@@ -19,7 +19,8 @@ ok() { echo "== $1 rc=$2"; [[ $2 == 0 ]] || exit "$2"; }
 kb() {   # kbench over the three benchmark files
   timeout -k 10 200 python -u tools/kbench.py friendsforever 1,10000 3 && \
   timeout -k 10 200 python -u tools/kbench.py git-makefile 1 3 && \
-  timeout -k 10 200 python -u tools/kbench.py node_nodecc 1 3
+  timeout -k 10 200 python -u tools/kbench.py node_nodecc 1 3 && \
+  if [[ -n $KB_SYNTH ]]; then timeout -k 10 300 python -u tools/kbench.py synth:$KB_SYNTH 1,20000 3; fi
 }
 for s in ${STEPS//,/ }; do
   case $s in
@@ -37,7 +38,7 @@ for s in ${STEPS//,/ }; do
     kbench)
       kb > "$OUT/kbench.log" 2>&1; rc=$?; cat "$OUT/kbench.log"; ok kbench $rc ;;
     kprof)
-      timeout -k 10 300 python -u tools/kprof.py friendsforever friendsforeverx4096 git-makefile node_nodecc \
+      timeout -k 10 300 python -u tools/kprof.py ${KPROF_DOCS:-friendsforever friendsforeverx4096 git-makefile node_nodecc} \
         > "$OUT/kprof.log" 2>&1
       rc=$?; cut -c1-400 "$OUT/kprof.log"; ok kprof $rc ;;
     ab)

@@ -16,7 +16,12 @@ def main():
     for a in args:
         name, _, copies = a.partition("x")
         copies = int(copies or 1)
-        b = dt_amd.Batch(docs=[G.dt_bytes(name)] * copies, staging="device")
+        if name.startswith("synth"):   # synth[:distinct]x<copies>: pairwise-merge synthetic docs
+            distinct = int(name.split(":")[1]) if ":" in name else 64
+            pool = [dt_amd.synth_merge_oplog(i, 5000).encode() for i in range(distinct)]
+            b = dt_amd.Batch(docs=[pool[i % distinct] for i in range(copies)], staging="device")
+        else:
+            b = dt_amd.Batch(docs=[G.dt_bytes(name)] * copies, staging="device")
         ms = b.run_timed()
         idx = range(0, copies, max(1, copies // 16))
         sts = [b.doc_stats(i) for i in idx]
