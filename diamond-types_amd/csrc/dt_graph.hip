@@ -418,7 +418,7 @@ __global__ __launch_bounds__(64) void graph_query_kernel(GraphParams P) {
     const uint32_t qi = blockIdx.x;
     if (qi >= P.n_queries) return;
     const GraphQuery q = P.queries[qi];
-    if (q.kind == GQ_DIFF_LEVEL) return;   // dt_level.hip answers these
+    if (q.kind == GQ_DIFF_LEVEL || q.kind == GQ_CONFLICT_LEVEL) return;   // dt_level.hip answers these
     G g{reinterpret_cast<const Ent *>(P.ents) + q.ent_off, P.par, q.n_ent};
     GraphResult r{};
     uint32_t *out = P.out + size_t(q.out_off);

@@ -1,23 +1,35 @@
-// dt_level.hip -- level-synchronous causal-graph kernels (north_star "Causal graph": diff and
-// topological levelling as level-synchronous propagation over CSR parent arrays in HBM).
+// dt_level.hip -- level-synchronous causal-graph kernels (north_star "Causal graph": conflict-span
+// detection, diff and topological levelling as level-synchronous propagation over CSR parent
+// arrays in HBM).  Every per-entry array lives in HBM, so graphs of any size are levelled.
 //
 // level_kernel (one 256-thread workgroup per graph) levels the graph's entries: level(e) =
 // 1 + max level of its parent entries (roots 0), so every child sits on a higher level than
 // its parents.  Built in place from the entry quads and parent LVs of dt_graph.hip's arena:
 //   1. parent slot -> parent entry (one binary search per slot, all slots in parallel) and a
-//      children CSR (counting sort of the slots by parent entry, LDS atomics);
+//      children CSR (counting sort of the slots by parent entry, atomics on the graph's
+//      counter words);
 //   2. Kahn's algorithm one level per round: the round's frontier releases the children whose
 //      last pending parent it held; the rounds' frontiers, concatenated, are the entries in
 //      level order (order[], level offsets lvl_off[]).
-// level_diff_kernel (one workgroup per query) answers Graph::diff (tools.rs:158-292) by
-// propagating two marks down the levels: mA[e] / mB[e] = the highest LV of entry e in the
-// history of a / b (the history holds a prefix of every entry it touches); a level's entries
-// push their marks to their parents' entries with LDS atomicMax, all in parallel, and a barrier
-// separates the levels.  only-a of entry e is (mB[e], mA[e]], and the spans come out newest
-// first, merged when contiguous -- the same lists as the heap walk (dt_graph.hip q_diff).
+// Marks (both query kernels): mA[e] / mB[e] = the highest LV of entry e in the history of a / b
+// (a history holds a prefix of every entry it touches).  Seeded with the two versions, they are
+// pushed level by level from the highest level down: a level's entries push their marks to
+// their parents' entries with atomicMax, all in parallel, and a barrier separates the levels.
 //
-// The heap walk stops as soon as the two walks meet; the level sweep visits every level from
-// the inputs' highest down to the roots.  tools/level_bench.py times both on the same queries.
+// level_diff_kernel answers Graph::diff (tools.rs:158-292) from the marks: only-a of entry e is
+// (mB[e], mA[e]], the spans newest first, merged when contiguous -- the same lists as the heap
+// walk (dt_graph.hip q_diff).
+//
+// level_conflict_kernel answers Graph::find_conflicting (tools.rs:296-484).  The marks decide
+// each span's flag: an LV x of entry e is in the history of a iff x <= mA[e] (of b iff x <=
+// mB[e]), so a span is OnlyA, OnlyB or Shared by membership.  What the marks do not give is
+// where the reference's walk cuts its spans and where it stops (the single common point): the
+// walk pops time points (a version, or an entry's parents) highest first, consumes every point
+// inside the entry it enters (a span boundary at each), then pushes the entry's parents, and
+// stops when one point is left.  Because a point is always pushed below the entry that creates
+// it, the walk is a sweep over the entries in descending order with each entry's pending points
+// in a bucket: no heap.  One thread runs that sweep over the entries the marks touch; the
+// buckets, the point pool and the marks are HBM scratch of the query.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -40,9 +52,6 @@ __device__ __forceinline__ uint32_t find(const Ent *e, uint32_t n, int32_t lv) {
 constexpr uint32_t NT = 256;
 
 __global__ __launch_bounds__(256) void level_kernel(LevelParams P) {
-    __shared__ uint32_t s_cur[LVL_MAX_ENTRIES + 1];    // child counts, then fill cursors
-    __shared__ uint32_t s_cofs[LVL_MAX_ENTRIES + 1];   // children CSR offsets
-    __shared__ uint32_t s_pend[LVL_MAX_ENTRIES];       // parents not yet levelled
     __shared__ uint32_t s_sum[NT];
     __shared__ uint32_t s_tail, s_bad;
     const uint32_t g = blockIdx.x, t = threadIdx.x;
@@ -50,23 +59,22 @@ __global__ __launch_bounds__(256) void level_kernel(LevelParams P) {
     const LevelGraph G = P.graphs[g];
     const uint32_t n = G.n_ent, base = G.ent_off;
     uint32_t *meta = P.meta + 2 * size_t(base);   // [0] = levels, [1] = status
-    if (n > LVL_MAX_ENTRIES) {
-        if (t == 0) { meta[0] = 0; meta[1] = GQ_OVERFLOW; }
-        return;
-    }
+    uint32_t *cur = P.gscr + 3 * size_t(base);    // child counts, then fill cursors (n + 1)
+    uint32_t *cofs = cur + (n + 1);               // children CSR offsets (n + 1)
+    uint32_t *pend = cofs + (n + 1);              // parents not yet levelled (n)
     const Ent *E = reinterpret_cast<const Ent *>(P.ents) + base;
     const uint32_t plo = E[0].poff, phi = E[n].poff;
     if (t == 0) { s_bad = 0; s_tail = 0; }
     for (uint32_t e = t; e < n; e += NT) {
-        s_cur[e] = 0;
-        s_pend[e] = E[e + 1].poff - E[e].poff;
+        cur[e] = 0;
+        pend[e] = E[e + 1].poff - E[e].poff;
     }
     __syncthreads();
     for (uint32_t k = plo + t; k < phi; k += NT) {
         const uint32_t pe = find(E, n, int32_t(P.par[k]));
         if (pe == n) { s_bad = 1; continue; }
         P.pent[k] = pe;
-        atomicAdd(&s_cur[pe], 1u);
+        atomicAdd(&cur[pe], 1u);
     }
     __syncthreads();
     if (s_bad) {
@@ -76,29 +84,29 @@ __global__ __launch_bounds__(256) void level_kernel(LevelParams P) {
     // exclusive scan of the child counts: per-thread chunks, then the 256 chunk totals
     const uint32_t per = (n + NT - 1) / NT, c0 = min(n, t * per), c1 = min(n, c0 + per);
     uint32_t sum = 0;
-    for (uint32_t e = c0; e < c1; e++) sum += s_cur[e];
+    for (uint32_t e = c0; e < c1; e++) sum += cur[e];
     s_sum[t] = sum;
     __syncthreads();
     if (t == 0) {
         uint32_t run = 0;
         for (uint32_t i = 0; i < NT; i++) { const uint32_t x = s_sum[i]; s_sum[i] = run; run += x; }
-        s_cofs[n] = run;
+        cofs[n] = run;
     }
     __syncthreads();
     {
         uint32_t run = s_sum[t];
         for (uint32_t e = c0; e < c1; e++) {
-            const uint32_t c = s_cur[e];
-            s_cofs[e] = run;
-            s_cur[e] = run;
+            const uint32_t c = cur[e];
+            cofs[e] = run;
+            cur[e] = run;
             run += c;
         }
     }
     __syncthreads();
     for (uint32_t e = t; e < n; e += NT)
-        for (uint32_t k = E[e].poff; k < E[e + 1].poff; k++) P.child[plo + atomicAdd(&s_cur[P.pent[k]], 1u)] = e;
+        for (uint32_t k = E[e].poff; k < E[e + 1].poff; k++) P.child[plo + atomicAdd(&cur[P.pent[k]], 1u)] = e;
     for (uint32_t e = t; e < n; e += NT)
-        if (s_pend[e] == 0) P.order[base + atomicAdd(&s_tail, 1u)] = e;   // roots: level 0
+        if (pend[e] == 0) P.order[base + atomicAdd(&s_tail, 1u)] = e;   // roots: level 0
     __syncthreads();
     // one level per round; a round's frontier is order[head, tail)
     uint32_t head = 0, tail = s_tail, L = 0;
@@ -107,9 +115,9 @@ __global__ __launch_bounds__(256) void level_kernel(LevelParams P) {
         for (uint32_t i = head + t; i < tail; i += NT) {
             const uint32_t e = P.order[base + i];
             P.level[base + e] = L;
-            for (uint32_t j = s_cofs[e]; j < s_cofs[e + 1]; j++) {
+            for (uint32_t j = cofs[e]; j < cofs[e + 1]; j++) {
                 const uint32_t c = P.child[plo + j];
-                if (atomicSub(&s_pend[c], 1u) == 1u) P.order[base + atomicAdd(&s_tail, 1u)] = c;
+                if (atomicSub(&pend[c], 1u) == 1u) P.order[base + atomicAdd(&s_tail, 1u)] = c;
             }
         }
         __syncthreads();
@@ -125,29 +133,71 @@ __global__ __launch_bounds__(256) void level_kernel(LevelParams P) {
     }
 }
 
-// Spans newest first, contiguous ones merged (push_reversed_rle), as dt_graph.hip writes them.
+// The marks of a query (see the header), level by level.  Every thread returns the same status.
+__device__ uint32_t push_marks(const LevelParams &P, const GraphQuery &q, const Ent *E, int32_t *mA, int32_t *mB,
+                               uint32_t *s_top, uint32_t *s_st) {
+    const uint32_t t = threadIdx.x, n = q.n_ent, base = q.ent_off;
+    for (uint32_t e = t; e < n; e += NT) { mA[e] = -1; mB[e] = -1; }
+    __syncthreads();
+    if (t == 0) {   // seed the marks with the two versions
+        uint32_t top = 0, st = GQ_OK;
+        for (uint32_t i = 0; i < q.na + q.nb && st == GQ_OK; i++) {
+            const int32_t v = i < q.na ? q.a[i] : q.b[i - q.na];
+            const uint32_t e = find(E, n, v);
+            if (e == n) { st = GQ_BAD_INPUT; break; }
+            int32_t *m = i < q.na ? mA : mB;
+            m[e] = max(m[e], v);
+            top = max(top, P.level[base + e]);
+        }
+        *s_top = top;
+        *s_st = st;
+    }
+    __syncthreads();
+    if (*s_st != GQ_OK) return *s_st;
+    // highest level first: a level's marks are final once every higher level has pushed
+    for (int32_t L = int32_t(*s_top); L >= 0; L--) {
+        const uint32_t i0 = P.lvl_off[base + L], i1 = P.lvl_off[base + L + 1];
+        for (uint32_t i = i0 + t; i < i1; i += NT) {
+            const uint32_t e = P.order[base + i];
+            const int32_t xa = mA[e], xb = mB[e];
+            if (xa < 0 && xb < 0) continue;
+            for (uint32_t k = E[e].poff; k < E[e + 1].poff; k++) {
+                const uint32_t pe = P.pent[k];
+                const int32_t p = int32_t(P.par[k]);
+                if (xa >= 0) atomicMax(&mA[pe], p);
+                if (xb >= 0) atomicMax(&mB[pe], p);
+            }
+        }
+        __syncthreads();
+    }
+    return GQ_OK;
+}
+
+// Spans newest first, contiguous ones merged (push_reversed_rle); 2 words per span (diff) or 3
+// (with the flag, conflict), as dt_graph.hip writes them.
 struct RevSpans {
     uint32_t *out;
-    uint32_t cap, n;
+    uint32_t cap, n, words;
     int32_t ls, le;
+    uint32_t lf;
     bool have, overflow;
-    __device__ void push(int32_t s, int32_t e) {
-        if (have && ls == e) { ls = s; return; }
+    __device__ void push(int32_t s, int32_t e, uint32_t f = 0) {
+        if (have && ls == e && lf == f) { ls = s; return; }
         flush();
-        have = true; ls = s; le = e;
+        have = true; ls = s; le = e; lf = f;
     }
     __device__ void flush() {
         if (!have) return;
         if (n >= cap) { overflow = true; have = false; return; }
-        out[2 * n] = uint32_t(ls);
-        out[2 * n + 1] = uint32_t(le);
+        out[words * n] = uint32_t(ls);
+        out[words * n + 1] = uint32_t(le);
+        if (words == 3) out[words * n + 2] = lf;
         n++;
         have = false;
     }
 };
 
 __global__ __launch_bounds__(256) void level_diff_kernel(LevelParams P, GraphParams Q) {
-    __shared__ int32_t mA[LVL_MAX_ENTRIES], mB[LVL_MAX_ENTRIES];
     __shared__ uint32_t s_top, s_st;
     const uint32_t qi = blockIdx.x, t = threadIdx.x;
     if (qi >= Q.n_queries) return;
@@ -161,46 +211,16 @@ __global__ __launch_bounds__(256) void level_diff_kernel(LevelParams P, GraphPar
         return;
     }
     const Ent *E = reinterpret_cast<const Ent *>(P.ents) + base;
-    for (uint32_t e = t; e < n; e += NT) { mA[e] = -1; mB[e] = -1; }
-    __syncthreads();
-    if (t == 0) {   // seed the marks with the two versions
-        uint32_t top = 0, st = GQ_OK;
-        for (uint32_t i = 0; i < q.na + q.nb && st == GQ_OK; i++) {
-            const int32_t v = i < q.na ? q.a[i] : q.b[i - q.na];
-            const uint32_t e = find(E, n, v);
-            if (e == n) { st = GQ_BAD_INPUT; break; }
-            int32_t *m = i < q.na ? mA : mB;
-            m[e] = max(m[e], v);
-            top = max(top, P.level[base + e]);
-        }
-        s_top = top;
-        s_st = st;
-    }
-    __syncthreads();
-    if (s_st != GQ_OK) {
-        if (t == 0) { res->status = s_st; res->n0 = res->n1 = res->n_common = 0; }
+    int32_t *mA = reinterpret_cast<int32_t *>(P.qscr + q.scr_off), *mB = mA + n;
+    const uint32_t st = push_marks(P, q, E, mA, mB, &s_top, &s_st);
+    if (st != GQ_OK) {
+        if (t == 0) { res->status = st; res->n0 = res->n1 = res->n_common = 0; }
         return;
-    }
-    // highest level first: a level's marks are final once every higher level has pushed
-    for (int32_t L = int32_t(s_top); L >= 0; L--) {
-        const uint32_t i0 = P.lvl_off[base + L], i1 = P.lvl_off[base + L + 1];
-        for (uint32_t i = i0 + t; i < i1; i += NT) {
-            const uint32_t e = P.order[base + i];
-            const int32_t xa = mA[e], xb = mB[e];
-            if (xa < 0 && xb < 0) continue;
-            for (uint32_t k = E[e].poff; k < E[e + 1].poff; k++) {
-                const uint32_t pe = P.pent[k];
-                const int32_t p = int32_t(Q.par[k]);
-                if (xa >= 0) atomicMax(&mA[pe], p);
-                if (xb >= 0) atomicMax(&mB[pe], p);
-            }
-        }
-        __syncthreads();
     }
     if (t == 0) {
         uint32_t *out = Q.out + size_t(q.out_off);
-        RevSpans sa{out, q.out_cap / 4, 0, 0, 0, false, false};
-        RevSpans sb{out + 2 * (q.out_cap / 4), q.out_cap / 4, 0, 0, 0, false, false};
+        RevSpans sa{out, q.out_cap / 4, 0, 2, 0, 0, 0, false, false};
+        RevSpans sb{out + 2 * (q.out_cap / 4), q.out_cap / 4, 0, 2, 0, 0, 0, false, false};
         for (int32_t e = int32_t(n) - 1; e >= 0; e--) {
             const int32_t xa = mA[e], xb = mB[e], s = E[e].start;
             if (xa > xb) sa.push(xb >= s ? xb + 1 : s, xa + 1);
@@ -215,6 +235,197 @@ __global__ __launch_bounds__(256) void level_diff_kernel(LevelParams P, GraphPar
     }
 }
 
+// ---- find_conflicting: marks + a bucketed sweep ------------------------------------------------
+enum : uint32_t { F_A = 0, F_B = 1, F_S = 2 };
+enum : uint32_t { TP_ONE = 0, TP_PARENTS = 1, TP_QA = 2, TP_QB = 3 };
+constexpr int32_t ROOT_LV = -1;
+constexpr uint32_t BUCKET_CAP = 64;   // time points that enter one entry (else GQ_OVERFLOW)
+
+// A time point (the reference's TimePoint + DiffFlag) in the query's pool: 4 words
+// {next in its bucket, flag | kind << 2, frontier size, reference}: a single LV (TP_ONE: ref =
+// the LV), an entry's parents (TP_PARENTS: ref = the entry), or one of the two versions.
+struct Sweep {
+    const Ent *E;
+    const uint32_t *par;
+    const GraphQuery *q;
+    int32_t *head;
+    uint32_t *pool;
+    uint32_t n, cap, used, npend;
+    bool overflow;
+
+    __device__ int32_t elem(uint32_t tp, uint32_t k) const {
+        const uint32_t *w = pool + 4 * size_t(tp);
+        switch (w[1] >> 2) {
+            case TP_ONE: return int32_t(w[3]);
+            case TP_PARENTS: return int32_t(par[E[w[3]].poff + k]);
+            case TP_QA: return q->a[k];
+            default: return q->b[k];
+        }
+    }
+    __device__ uint32_t size(uint32_t tp) const { return pool[4 * size_t(tp) + 2]; }
+    __device__ uint32_t flag(uint32_t tp) const { return pool[4 * size_t(tp) + 1] & 3u; }
+    __device__ int32_t last(uint32_t tp) const { const uint32_t s = size(tp); return s ? elem(tp, s - 1) : ROOT_LV; }
+    __device__ bool same(uint32_t x, uint32_t y) const {   // TimePoint equality: the whole frontier
+        const uint32_t s = size(x);
+        if (s != size(y)) return false;
+        for (uint32_t k = 0; k < s; k++) if (elem(x, k) != elem(y, k)) return false;
+        return true;
+    }
+    // heap order of (TimePoint, DiffFlag) (tools.rs:309-318): higher last first, fewer merged
+    // members first, then the higher flag
+    __device__ bool before(uint32_t x, uint32_t y) const {
+        const int32_t lx = last(x), ly = last(y);
+        if (lx != ly) return lx > ly;
+        if (size(x) != size(y)) return size(x) < size(y);
+        return flag(x) > flag(y);
+    }
+    __device__ void push(uint32_t kind, uint32_t ref, uint32_t sz, uint32_t f) {
+        if (used >= cap) { overflow = true; return; }
+        const uint32_t tp = used++;
+        uint32_t *w = pool + 4 * size_t(tp);
+        w[1] = f | (kind << 2);
+        w[2] = sz;
+        w[3] = ref;
+        npend++;
+        const int32_t l = last(tp);
+        if (l == ROOT_LV) { w[0] = 0xFFFFFFFFu; return; }   // ROOT: popped only when nothing else is left
+        const uint32_t e = find(E, n, l);
+        if (e == n) { overflow = true; return; }
+        w[0] = uint32_t(head[e]);
+        head[e] = int32_t(tp);
+    }
+};
+
+__global__ __launch_bounds__(256) void level_conflict_kernel(LevelParams P, GraphParams Q) {
+    __shared__ uint32_t s_top, s_st;
+    const uint32_t qi = blockIdx.x, t = threadIdx.x;
+    if (qi >= Q.n_queries) return;
+    const GraphQuery &q = Q.queries[qi];
+    if (q.kind != GQ_CONFLICT_LEVEL) return;
+    const uint32_t n = q.n_ent, base = q.ent_off;
+    const uint32_t *meta = P.meta + 2 * size_t(base);
+    GraphResult *res = Q.results + qi;
+    const Ent *E = reinterpret_cast<const Ent *>(P.ents) + base;
+    uint32_t *out = Q.out + size_t(q.out_off);
+    if (meta[1] != GQ_OK || q.na > GQ_MAX_FRONTIER || q.nb > GQ_MAX_FRONTIER) {
+        if (t == 0) { res->status = meta[1] != GQ_OK ? meta[1] : GQ_BAD_INPUT; res->n0 = res->n_common = 0; }
+        return;
+    }
+    // the reference's short circuits (tools.rs:445-480), decided by thread 0 for the group
+    if (t == 0) {
+        uint32_t st = 0xFFFFFFFFu;   // 0xFFFFFFFF: no short circuit
+        bool same = q.na == q.nb;
+        for (uint32_t i = 0; same && i < q.na; i++) same = q.a[i] == q.b[i];
+        RevSpans sp{out, q.out_cap / 3, 0, 3, 0, 0, 0, false, false};
+        uint32_t nc = 0;
+        if (same) {
+            for (uint32_t i = 0; i < q.na; i++) res->common[nc++] = q.a[i];
+            st = GQ_OK;
+        } else if (q.na == 1 && q.nb == 1) {
+            const int32_t x = q.a[0], y = q.b[0];
+            const uint32_t ex = find(E, n, x), ey = find(E, n, y);
+            if (ex == n || ey == n) st = GQ_BAD_INPUT;
+            else if (x > y && y >= E[ex].start) { sp.push(y + 1, x + 1, F_A); res->common[nc++] = y; st = GQ_OK; }
+            else if (y > x && x >= E[ey].start) { sp.push(x + 1, y + 1, F_B); res->common[nc++] = x; st = GQ_OK; }
+        }
+        if (st != 0xFFFFFFFFu) {
+            sp.flush();
+            res->status = st;
+            res->n0 = sp.n;
+            res->n_common = nc;
+        }
+        s_st = st;
+    }
+    __syncthreads();
+    if (s_st != 0xFFFFFFFFu) return;
+    __syncthreads();   // every thread read s_st before push_marks reuses it
+    int32_t *mA = reinterpret_cast<int32_t *>(P.qscr + q.scr_off), *mB = mA + n, *head = mB + n;
+    uint32_t *pool = reinterpret_cast<uint32_t *>(head + n);
+    for (uint32_t e = t; e < n; e += NT) head[e] = -1;
+    const uint32_t mst = push_marks(P, q, E, mA, mB, &s_top, &s_st);
+    if (mst != GQ_OK) {
+        if (t == 0) { res->status = mst; res->n0 = res->n_common = 0; }
+        return;
+    }
+    if (t != 0) return;
+    // ---- the sweep (one thread) ----
+    Sweep S{E, P.par, &q, head, pool, n, q.scr_tp, 0, 0, false};
+    RevSpans sp{out, q.out_cap / 3, 0, 3, 0, 0, 0, false, false};
+    // a span's flag is its membership: x in H(a) iff x <= mA[e], in H(b) iff x <= mB[e]
+    auto mflag = [&](uint32_t e, int32_t x) -> uint32_t {
+        const bool ia = x <= mA[e], ib = x <= mB[e];
+        return ia && ib ? F_S : (ia ? F_A : F_B);
+    };
+    S.push(TP_QA, 0, q.na, F_A);
+    S.push(TP_QB, 0, q.nb, F_B);
+    uint32_t st = GQ_OK, nc = 0;
+    uint32_t bk[BUCKET_CAP];
+    int32_t e = int32_t(n) - 1;
+    for (;;) {
+        // the next entry holding a pending point: only entries the marks touch can
+        while (e >= 0 && (head[e] < 0 || (mA[e] < E[e].start && mB[e] < E[e].start))) e--;
+        if (S.overflow) { st = GQ_OVERFLOW; break; }
+        if (e < 0) break;   // only ROOT points left: nothing in common
+        // the bucket in heap order (insertion sort; buckets are small)
+        uint32_t m = 0;
+        for (int32_t x = head[e]; x >= 0; x = int32_t(pool[4 * size_t(x)])) {
+            if (m == BUCKET_CAP) { st = GQ_OVERFLOW; break; }
+            uint32_t j = m++;
+            while (j > 0 && S.before(uint32_t(x), bk[j - 1])) { bk[j] = bk[j - 1]; j--; }
+            bk[j] = uint32_t(x);
+        }
+        if (st != GQ_OK) break;
+        head[e] = -1;
+        // pop the top point and its duplicates
+        const uint32_t T = bk[0];
+        uint32_t flag = S.flag(T);
+        S.npend--;
+        uint32_t i = 1;
+        while (i < m && S.same(bk[i], T)) {
+            if (S.flag(bk[i]) != flag) flag = F_S;
+            S.npend--;
+            i++;
+        }
+        if (S.npend == 0) {   // collapsed to one point: the common version
+            const uint32_t sz = S.size(T);
+            if (sz > GQ_MAX_FRONTIER) { st = GQ_OVERFLOW; break; }
+            for (uint32_t k = 0; k < sz; k++) res->common[nc++] = S.elem(T, k);
+            break;
+        }
+        for (uint32_t k = 0; k + 1 < S.size(T); k++) S.push(TP_ONE, uint32_t(S.elem(T, k)), 1, flag);   // shatter
+        const int32_t es = E[e].start;
+        int32_t re = S.last(T) + 1;
+        bool stopped = false;
+        for (; i < m; i++) {   // the other points inside this entry, highest first
+            const uint32_t u = bk[i];
+            const int32_t ul = S.last(u);
+            S.npend--;
+            if (ul + 1 < re) {
+                sp.push(ul + 1, re, mflag(uint32_t(e), re - 1));
+                re = ul + 1;
+            }
+            for (uint32_t k = 0; k + 1 < S.size(u); k++) S.push(TP_ONE, uint32_t(S.elem(u, k)), 1, S.flag(u));
+            if (S.flag(u) != flag) flag = F_S;
+            if (S.npend == 0) {   // nothing left but this point: it is the common version
+                res->common[nc++] = re - 1;
+                stopped = true;
+                break;
+            }
+        }
+        if (stopped) break;
+        sp.push(es, re, mflag(uint32_t(e), re - 1));
+        const uint32_t np = E[e + 1].poff - E[e].poff;
+        S.push(TP_PARENTS, uint32_t(e), np, flag);
+        e--;
+    }
+    if (st == GQ_OK && S.overflow) st = GQ_OVERFLOW;
+    sp.flush();
+    if (st == GQ_OK && sp.overflow) st = GQ_OVERFLOW;
+    res->status = st;
+    res->n0 = sp.n;
+    res->n_common = nc;
+}
+
 }  // namespace ldev
 
 int launch_levels(const LevelParams &p, void *stream) {
@@ -226,6 +437,13 @@ int launch_levels(const LevelParams &p, void *stream) {
 int launch_level_diff(const LevelParams &p, const GraphParams &q, void *stream) {
     if (!q.n_queries) return 0;
     hipLaunchKernelGGL(ldev::level_diff_kernel, dim3(q.n_queries), dim3(ldev::NT), 0, reinterpret_cast<hipStream_t>(stream), p, q);
+    return hipGetLastError() == hipSuccess ? 0 : 66;
+}
+
+int launch_level_conflict(const LevelParams &p, const GraphParams &q, void *stream) {
+    if (!q.n_queries) return 0;
+    hipLaunchKernelGGL(ldev::level_conflict_kernel, dim3(q.n_queries), dim3(ldev::NT), 0,
+                       reinterpret_cast<hipStream_t>(stream), p, q);
     return hipGetLastError() == hipSuccess ? 0 : 66;
 }
 

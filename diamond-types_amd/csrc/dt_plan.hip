@@ -632,7 +632,6 @@ DEV void plan_doc1(P &p, PlanResult *res) {
     PT(5);
     VV<1> vf;
     vf.v[0] = 0;
-    uint32_t f = 0xFFFFFFFFu;
     // the previous entry's deferred output: its diff (gather in flight) and its op runs
     Emit pe_em;
     pe_em.any = false;
@@ -715,7 +714,6 @@ DEV void plan_doc1(P &p, PlanResult *res) {
         pe_have = true;
         pe_nop = nop; pe_op0 = op0;
         pe_oc = oc;
-        f = e_end - 1;
         idx = nidx;
         rc = nrc;
         PT(3);

@@ -57,7 +57,7 @@ extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *h
         const dtgpu_graph_query &s = queries[i];
         GraphQuery &d = q[i];
         std::memset(&d, 0, sizeof d);
-        if (s.graph >= n_graphs || s.na > GQ_MAX_FRONTIER || s.nb > GQ_MAX_FRONTIER || s.kind > 4) return DTGPU_ERR_ARG;
+        if (s.graph >= n_graphs || s.na > GQ_MAX_FRONTIER || s.nb > GQ_MAX_FRONTIER || s.kind > GQ_CONFLICT_LEVEL) return DTGPU_ERR_ARG;
         d.kind = s.kind;
         d.ent_off = goff[s.graph];
         d.n_ent = gn[s.graph];
@@ -69,11 +69,26 @@ extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *h
         d.out_off = uint32_t(i) * out_cap;
         d.out_cap = out_cap;
     }
+    // HBM scratch of the level-synchronous queries: marks (diff), marks + buckets + time points
+    // (conflict spans), sized by the query's graph
+    uint64_t qscr_words = 0;
+    for (size_t i = 0; i < nq; i++) {
+        GraphQuery &d = q[i];
+        if (d.kind != GQ_DIFF_LEVEL && d.kind != GQ_CONFLICT_LEVEL) continue;
+        const uint64_t npar = ents[4 * (size_t(d.ent_off) + d.n_ent) + 3] - ents[4 * size_t(d.ent_off) + 3];
+        d.scr_off = qscr_words;
+        if (d.kind == GQ_DIFF_LEVEL) qscr_words += 2ull * d.n_ent;
+        else {
+            d.scr_tp = conflict_level_tps(d.n_ent, npar);
+            qscr_words += conflict_level_words(d.n_ent, npar);
+        }
+    }
     // graphs that level-synchronous diffs run on
     std::vector<LevelGraph> lg;
     {
         std::vector<uint8_t> want(n_graphs, 0);
-        for (size_t i = 0; i < nq; i++) if (queries[i].kind == GQ_DIFF_LEVEL) want[queries[i].graph] = 1;
+        for (size_t i = 0; i < nq; i++)
+            if (queries[i].kind == GQ_DIFF_LEVEL || queries[i].kind == GQ_CONFLICT_LEVEL) want[queries[i].graph] = 1;
         for (size_t g = 0; g < n_graphs; g++) if (want[g]) lg.push_back(LevelGraph{goff[g], gn[g]});
     }
     hipStream_t st = nullptr;
@@ -81,7 +96,7 @@ extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *h
     DevBuf<uint32_t> d_ents, d_par, d_out;
     DevBuf<GraphQuery> d_q;
     DevBuf<GraphResult> d_r;
-    DevBuf<uint32_t> d_pent, d_child, d_level, d_order, d_loff, d_meta;
+    DevBuf<uint32_t> d_pent, d_child, d_level, d_order, d_loff, d_meta, d_gscr, d_qscr;
     DevBuf<LevelGraph> d_lg;
     dtgpu_status rc = DTGPU_OK;
     std::vector<GraphResult> res(nq);
@@ -107,13 +122,18 @@ extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *h
                 CK(d_order.alloc(nquad));
                 CK(d_loff.alloc(nquad));
                 CK(d_meta.alloc(2 * nquad));
+                CK(d_gscr.alloc(3 * nquad));
+                CK(d_qscr.alloc(std::max<uint64_t>(qscr_words, 1)));
                 CK(d_lg.upload(lg, st));
                 LP = LevelParams{d_ents.p, d_par.p, d_pent.p, d_child.p, d_level.p, d_order.p, d_loff.p, d_meta.p,
-                                 d_lg.p, uint32_t(lg.size())};
+                                 d_gscr.p, d_qscr.p, d_lg.p, uint32_t(lg.size())};
             }
             CK(hipEventRecord(e0, st));
             if (launch_graph_queries(P, st)) { rc = DTGPU_ERR_HIP; goto done; }
-            if (!lg.empty() && (launch_levels(LP, st) || launch_level_diff(LP, P, st))) { rc = DTGPU_ERR_HIP; goto done; }
+            if (!lg.empty() && (launch_levels(LP, st) || launch_level_diff(LP, P, st) || launch_level_conflict(LP, P, st))) {
+                rc = DTGPU_ERR_HIP;
+                goto done;
+            }
             CK(hipEventRecord(e1, st));
         }
         if (nq) {
@@ -145,7 +165,7 @@ extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *h
             }
             a.n_a = r.n0;
             a.n_b = r.n1;
-        } else if (q[i].kind == GQ_CONFLICT) {
+        } else if (q[i].kind == GQ_CONFLICT || q[i].kind == GQ_CONFLICT_LEVEL) {
             if (r.n0 > span_cap) { a.status = GQ_OVERFLOW; continue; }
             for (uint32_t k = 0; k < 3 * r.n0; k++) sp[k] = int32_t(o[k]);
             a.n_a = r.n0;

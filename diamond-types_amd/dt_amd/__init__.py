@@ -800,7 +800,7 @@ class DecodeBatch:
         return lib().dtgpu_decode_bytes(self._h, 1)
 
 
-GQ_KINDS = {"diff": 0, "conflict": 1, "contains": 2, "dominators": 3, "diff_level": 4}
+GQ_KINDS = {"diff": 0, "conflict": 1, "contains": 2, "dominators": 3, "diff_level": 4, "conflict_level": 5}
 DIFF_FLAGS = ["OnlyA", "OnlyB", "Shared"]
 
 
@@ -812,7 +812,8 @@ def graph_queries(graphs, queries, span_cap=512, timing=False):
              ("conflict", g, a, b) -> ([(start, end, flag)], common) (Graph::find_conflicting);
              ("contains", g, frontier, target) -> bool (frontier_contains_version; -1 = ROOT);
              ("dominators", g, a, b) -> sorted list (find_dominators_2 of two dominator sets);
-             ("diff_level", g, a, b) -> as "diff", by level-synchronous propagation (dt_level.hip).
+             ("diff_level", g, a, b) -> as "diff", by level-synchronous propagation (dt_level.hip);
+             ("conflict_level", g, a, b) -> as "conflict": level-synchronous marks + a bucketed sweep.
     A query the device could not answer yields ("error", status)."""
     hist, off = [], [0]
     for g in graphs:
@@ -848,7 +849,7 @@ def graph_queries(graphs, queries, span_cap=512, timing=False):
         tri = [(spans[base + 3 * k], spans[base + 3 * k + 1], spans[base + 3 * k + 2]) for k in range(r.n_a + r.n_b)]
         if kind in ("diff", "diff_level"):
             out.append(([(s, e) for s, e, _ in tri[:r.n_a]], [(s, e) for s, e, _ in tri[r.n_a:]]))
-        elif kind == "conflict":
+        elif kind in ("conflict", "conflict_level"):
             out.append(([(s, e, DIFF_FLAGS[f]) for s, e, f in tri[:r.n_a]], list(r.common[:r.n_common])))
         elif kind == "dominators":
             out.append(list(r.common[:r.n_common]))

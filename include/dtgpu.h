@@ -391,7 +391,12 @@ size_t dtgpu_oplog_export(const dtgpu_oplog *oplog, int what, void *out, size_t 
  *   DTGPU_GQ_DIFF_LEVEL Graph::diff as DTGPU_GQ_DIFF, computed level-synchronously: the graph's
  *                      entries are levelled (Kahn, one level per round) and the two versions'
  *                      marks propagate down the levels over the CSR parent arrays (dt_level.hip);
- *                      graphs up to 8192 entries
+ *                      every per-entry array in HBM (graphs of any size)
+ *   DTGPU_GQ_CONFLICT_LEVEL Graph::find_conflicting as DTGPU_GQ_CONFLICT: the level-synchronous
+ *                      marks give each span's OnlyA / OnlyB / Shared flag (membership); the span
+ *                      cuts and the common frontier come from a sweep over the entries in
+ *                      descending order with each entry's pending time points in a bucket (the
+ *                      reference's heap walk without the heap, dt_level.hip)
  * spans: span_cap (start, end, flag) triples per query.  answer.status: 0 ok, 1 capacity
  * (queue or span_cap), 2 bad input (a version outside the graph). */
 #define DTGPU_GQ_DIFF 0
@@ -399,6 +404,7 @@ size_t dtgpu_oplog_export(const dtgpu_oplog *oplog, int what, void *out, size_t 
 #define DTGPU_GQ_CONTAINS 2
 #define DTGPU_GQ_DOMINATORS 3
 #define DTGPU_GQ_DIFF_LEVEL 4
+#define DTGPU_GQ_CONFLICT_LEVEL 5
 typedef struct dtgpu_graph_query {
     uint32_t kind, graph, na, nb;   /* frontier sizes <= 16 */
     int64_t a[16], b[16];

@@ -159,3 +159,72 @@ def test_level_synchronous_diff_vs_heap_walk_and_oracle(name):
         assert x == (list(reversed(oa)), list(reversed(ob))), (a, b)
         if not (isinstance(y, tuple) and y and y[0] == "error"):
             assert x == y, (a, b)
+
+
+def test_level_synchronous_conflict_fixtures():
+    """Graph::find_conflicting by level-synchronous marks + the bucketed sweep (dt_level.hip) on
+    every conflicting.json fixture (tools.rs:779-901 semantics)."""
+    graphs, queries, cases = [], [], []
+    for case in G.cg_fixture("conflicting"):
+        graphs.append(case["hist"])
+        queries.append(("conflict_level", len(graphs) - 1, case["a"], case["b"]))
+        cases.append(case)
+    for case, ans in zip(cases, dt_amd.graph_queries(graphs, queries)):
+        want = [(s["start"], s["end"], f) for s, f in reversed(case["expect_spans"])]
+        assert ans == (want, case["expect_common"]), case
+
+
+@pytest.mark.parametrize("name", G.DT_FILES)
+def test_level_conflict_random_vs_oracle_and_heap_walk(name):
+    hist, n = _hist_of(name)
+    og = OracleGraph(hist)
+    rng = random.Random(4321)
+    pairs = []
+    for _ in range(300):
+        a = og.dominators(sorted(rng.sample(range(n), rng.choice([1, 1, 2, 3]))))
+        b = og.dominators(sorted(rng.sample(range(n), rng.choice([1, 1, 2, 3]))))
+        pairs.append((a, b))
+    queries = [("conflict_level", 0, a, b) for a, b in pairs] + [("conflict", 0, a, b) for a, b in pairs]
+    got = dt_amd.graph_queries([hist], queries, span_cap=8192)
+    lvl, heap = got[:len(pairs)], got[len(pairs):]
+    for (a, b), x, y in zip(pairs, lvl, heap):
+        assert x == og.find_conflicting(a, b), (a, b)
+        if not (isinstance(y, tuple) and y and y[0] == "error"):   # the heap walk's LDS queue may overflow
+            assert x == y, (a, b)
+
+
+def _wide_history(n_entries, seed):
+    """Two agents taking turns, each entry a 2-LV run whose parents are the dominators of the
+    agent's own last LV and a random recent LV of the other's (oracle Graph::find_dominators)."""
+    rng = random.Random(seed)
+    og = OracleGraph()
+    hist, last = [], [None, None]
+    for i in range(n_entries):
+        who = i % 2
+        cand = [x for x in (last[who],) if x is not None]
+        if last[1 - who] is not None and rng.random() < 0.7:
+            cand.append(max(0, last[1 - who] - 2 * rng.randrange(3)))
+        parents = og.dominators(sorted(set(cand))) if cand else []
+        og.push(parents, 2 * i, 2 * i + 2)
+        hist.append({"span": [2 * i, 2 * i + 2], "parents": parents})
+        last[who] = 2 * i + 1
+    return hist, og
+
+
+def test_level_kernels_past_the_old_lds_cap():
+    """12,000 entries (the round-2 level kernels held per-entry state in LDS, capped at 8,192):
+    level-synchronous diff and conflict spans against the oracle."""
+    hist, og = _wide_history(12000, 7)
+    n = 24000
+    rng = random.Random(9)
+    pairs = []
+    for _ in range(40):
+        a = og.dominators(sorted(rng.sample(range(n), rng.choice([1, 2]))))
+        b = og.dominators(sorted(rng.sample(range(n // 2), rng.choice([1, 2]))))
+        pairs.append((a, b))
+    queries = [("diff_level", 0, a, b) for a, b in pairs] + [("conflict_level", 0, a, b) for a, b in pairs]
+    got = dt_amd.graph_queries([hist], queries, span_cap=32768)
+    for (a, b), d, c in zip(pairs, got[:len(pairs)], got[len(pairs):]):
+        oa, ob = og.diff(a, b)
+        assert d == (list(reversed(oa)), list(reversed(ob))), (a, b)
+        assert c == og.find_conflicting(a, b), (a, b)

@@ -1,5 +1,5 @@
-"""Heap-walk diff (dt_graph.hip, one wavefront per query) vs level-synchronous diff
-(dt_level.hip: levelling + one workgroup per query) on the same random version pairs of the
+"""Heap-walk diff / find_conflicting (dt_graph.hip, one wavefront per query) vs the
+level-synchronous forms (dt_level.hip: levelling + one workgroup per query) on the same random version pairs of the
 configs[2] graphs (node_nodecc, git-makefile) and friendsforever.  Device time of one batch,
 levelling included in the level-synchronous figure; a one-query batch gives the levelling cost."""
 import os
@@ -25,7 +25,7 @@ def main():
         pairs = [(o.dominators(sorted(rng.sample(range(n), rng.choice([1, 2])))),
                   o.dominators(sorted(rng.sample(range(n), rng.choice([1, 2]))))) for _ in range(nq)]
         res = {}
-        for kind in ("diff", "diff_level"):
+        for kind in ("diff", "diff_level", "conflict", "conflict_level"):
             best = None
             for _ in range(3):
                 out, ms = dt_amd.graph_queries([hist], [(kind, 0, a, b) for a, b in pairs], span_cap=4096, timing=True)
@@ -33,8 +33,11 @@ def main():
             res[kind] = (best, out)
         one = min(dt_amd.graph_queries([hist], [("diff_level", 0, *pairs[0])], timing=True)[1] for _ in range(3))
         same = sum(1 for x, y in zip(res["diff"][1], res["diff_level"][1]) if x == y)
-        print(f"{name}: entries={len(hist)} queries={nq} heap_walk_ms={res['diff'][0]:.3f} "
-              f"level_sync_ms={res['diff_level'][0]:.3f} (levelling+1 query {one:.3f} ms) agree={same}/{nq}", flush=True)
+        csame = sum(1 for x, y in zip(res["conflict"][1], res["conflict_level"][1]) if x == y)
+        print(f"{name}: entries={len(hist)} queries={nq} diff: heap_walk_ms={res['diff'][0]:.3f} "
+              f"level_sync_ms={res['diff_level'][0]:.3f} (levelling+1 query {one:.3f} ms) agree={same}/{nq}; "
+              f"conflict: heap_walk_ms={res['conflict'][0]:.3f} level_sync_ms={res['conflict_level'][0]:.3f} "
+              f"agree={csame}/{nq}", flush=True)
 
 
 if __name__ == "__main__":
