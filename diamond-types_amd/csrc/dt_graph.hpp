@@ -40,7 +40,7 @@ int launch_graph_queries(const GraphParams &p, void *stream);
 // the parents array.  All per-entry state is in HBM (no size cap): the levelling's counters
 // (3 words per entry slot, at 3 * ent_off), each level query's marks (and, for conflict spans,
 // bucket heads and a time-point pool) at its scr_off.
-inline uint64_t conflict_level_words(uint64_t n_ent, uint64_t n_par) { return 3 * n_ent + 4 * (34 + n_ent + n_par); }
+inline uint64_t conflict_level_words(uint64_t n_ent, uint64_t n_par) { return 4 * n_ent + 4 * (34 + n_ent + n_par); }
 inline uint32_t conflict_level_tps(uint64_t n_ent, uint64_t n_par) { return uint32_t(34 + n_ent + n_par); }
 struct LevelGraph { uint32_t ent_off, n_ent; };
 struct LevelParams {

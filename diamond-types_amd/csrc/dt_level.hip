@@ -28,8 +28,10 @@
 // inside the entry it enters (a span boundary at each), then pushes the entry's parents, and
 // stops when one point is left.  Because a point is always pushed below the entry that creates
 // it, the walk is a sweep over the entries in descending order with each entry's pending points
-// in a bucket: no heap.  One thread runs that sweep over the entries the marks touch; the
-// buckets, the point pool and the marks are HBM scratch of the query.
+// in a bucket: no heap.  The workgroup lists the entries the marks touch, highest first (a
+// prefix-sum compaction), and one thread runs the sweep over that list, sorting each entry's
+// points in an LDS buffer; the marks, the list, the bucket heads and the point pool are HBM
+// scratch of the query.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -297,7 +299,9 @@ struct Sweep {
 };
 
 __global__ __launch_bounds__(256) void level_conflict_kernel(LevelParams P, GraphParams Q) {
-    __shared__ uint32_t s_top, s_st;
+    __shared__ uint32_t s_top, s_st, s_ncand;
+    __shared__ uint32_t s_sum[NT];
+    __shared__ uint32_t bk[BUCKET_CAP];
     const uint32_t qi = blockIdx.x, t = threadIdx.x;
     if (qi >= Q.n_queries) return;
     const GraphQuery &q = Q.queries[qi];
@@ -340,12 +344,37 @@ __global__ __launch_bounds__(256) void level_conflict_kernel(LevelParams P, Grap
     if (s_st != 0xFFFFFFFFu) return;
     __syncthreads();   // every thread read s_st before push_marks reuses it
     int32_t *mA = reinterpret_cast<int32_t *>(P.qscr + q.scr_off), *mB = mA + n, *head = mB + n;
-    uint32_t *pool = reinterpret_cast<uint32_t *>(head + n);
+    uint32_t *cand = reinterpret_cast<uint32_t *>(head + n);
+    uint32_t *pool = cand + n;
     for (uint32_t e = t; e < n; e += NT) head[e] = -1;
     const uint32_t mst = push_marks(P, q, E, mA, mB, &s_top, &s_st);
     if (mst != GQ_OK) {
         if (t == 0) { res->status = mst; res->n0 = res->n_common = 0; }
         return;
+    }
+    // the entries the marks touch, highest first (a workgroup prefix sum over per-thread chunks):
+    // the only ones the sweep can visit
+    {
+        const uint32_t per = (n + NT - 1) / NT, c0 = min(n, t * per), c1 = min(n, c0 + per);
+        uint32_t cnt = 0;
+        for (uint32_t i = c0; i < c1; i++) {
+            const uint32_t e = n - 1 - i;
+            cnt += (mA[e] >= E[e].start || mB[e] >= E[e].start) ? 1u : 0u;
+        }
+        s_sum[t] = cnt;
+        __syncthreads();
+        if (t == 0) {
+            uint32_t run = 0;
+            for (uint32_t i = 0; i < NT; i++) { const uint32_t x = s_sum[i]; s_sum[i] = run; run += x; }
+            s_ncand = run;
+        }
+        __syncthreads();
+        uint32_t at = s_sum[t];
+        for (uint32_t i = c0; i < c1; i++) {
+            const uint32_t e = n - 1 - i;
+            if (mA[e] >= E[e].start || mB[e] >= E[e].start) cand[at++] = e;
+        }
+        __syncthreads();
     }
     if (t != 0) return;
     // ---- the sweep (one thread) ----
@@ -359,11 +388,16 @@ __global__ __launch_bounds__(256) void level_conflict_kernel(LevelParams P, Grap
     S.push(TP_QA, 0, q.na, F_A);
     S.push(TP_QB, 0, q.nb, F_B);
     uint32_t st = GQ_OK, nc = 0;
-    uint32_t bk[BUCKET_CAP];
-    int32_t e = int32_t(n) - 1;
+    const uint32_t ncand = s_ncand;
+    uint32_t ci = 0;
+    int32_t e = -1;
     for (;;) {
         // the next entry holding a pending point: only entries the marks touch can
-        while (e >= 0 && (head[e] < 0 || (mA[e] < E[e].start && mB[e] < E[e].start))) e--;
+        e = -1;
+        while (ci < ncand) {
+            const uint32_t x = cand[ci++];
+            if (head[x] >= 0) { e = int32_t(x); break; }
+        }
         if (S.overflow) { st = GQ_OVERFLOW; break; }
         if (e < 0) break;   // only ROOT points left: nothing in common
         // the bucket in heap order (insertion sort; buckets are small)
@@ -416,7 +450,6 @@ __global__ __launch_bounds__(256) void level_conflict_kernel(LevelParams P, Grap
         sp.push(es, re, mflag(uint32_t(e), re - 1));
         const uint32_t np = E[e + 1].poff - E[e].poff;
         S.push(TP_PARENTS, uint32_t(e), np, flag);
-        e--;
     }
     if (st == GQ_OK && S.overflow) st = GQ_OVERFLOW;
     sp.flush();
