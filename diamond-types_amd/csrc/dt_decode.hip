@@ -36,7 +36,7 @@ namespace dtgpu {
 namespace ddec {
 
 enum : int {
-    S_OK = 0, InvalidMagic = 1, UnsupportedProtocolVersion = 2, BaseVersionUnknown = 4, UnknownChunk = 5,
+    S_OK = 0, InvalidMagic = 1, UnsupportedProtocolVersion = 2, DocIdMismatch = 3, BaseVersionUnknown = 4, UnknownChunk = 5,
     LZ4DecompressionError = 7, CompressedDataMissing = 8, MissingChunk = 10, InvalidLength = 11,
     UnexpectedEOF = 12, InvalidUTF8 = 13, InvalidVarInt = 15, InvalidContent = 16, ChecksumFailed = 18,
     ErrCheckout = 64, ErrCapacity = 65, Defer = int(DECODE_DEFER),
@@ -1449,7 +1449,8 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
                 TRY(C.u64v(ver, seq));
                 if ((n >> 1) == 0) break;
                 if ((n >> 1) - 1 >= n_file) return InvalidLength;
-                return BaseVersionUnknown;
+                if (!(SIZE && D.patch)) return BaseVersionUnknown;   // sizing a patch: resolved later
+                if (!(n & 1)) break;
             }
             if (ver.n) return InvalidLength;
         }
@@ -1951,6 +1952,747 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_DECODE
     if (lane() == 0) P.results[doc] = R;
 }
 
+
+// =============================================================================================
+// decode_and_add (ListOpLog::decode_and_add_opts, decode_oplog.rs:476-583; decode_internal's
+// overlap filter :670-913).  One wavefront per (resident oplog, patch) pair; the parse is the
+// decoder's exact path (wave-uniform, varint queues), each step restating dt_host.cpp decode_into
+// so the error order is the host's.  The resident arrays are copied to the merged arenas first
+// (lane-parallel); agent runs, op runs, entries and the frontier then grow with the reference's
+// RLE rules, so the merged arrays equal the host decode_and_add's element for element.
+// =============================================================================================
+constexpr uint64_t UNDERWATER = ~uint64_t(0) / 4;   // UNDERWATER_START (src/dtrange.rs:197)
+
+struct Merged {              // this document's merged arenas
+    uint8_t *in, *content;
+    uint4 *aruns, *ops, *pre, *vm;
+    uint2 *ent, *agents;
+    uint32_t *poff, *par, *cbyte, *ver, *ffr;
+};
+
+// Frontier::advance_by_known_run (frontier.rs:251-279) on a lane-array frontier (lane k = element
+// k, sorted): false where the reference asserts.
+__device__ __forceinline__ int advance_known(uint32_t &fv, uint32_t &fn, uint32_t par, uint32_t np, uint32_t start,
+                                             uint32_t end, uint32_t *scratch) {
+    const uint32_t last = end - 1;
+    if (np == 1 && fn == 1 && rdl(par, 0) == rdl(fv, 0)) { fv = lane() == 0 ? last : 0u; return S_OK; }
+    if (np == fn && !ballot(lane() < fn && fv != par)) { fv = lane() == 0 ? last : 0u; fn = 1; return S_OK; }
+    if (ballot(lane() < fn && fv == start)) return InvalidLength;
+    bool in_par = false;
+    for (uint32_t j = 0; j < np; j++) in_par |= rdl(par, j) == fv;
+    const bool keep = lane() < fn && !in_par;
+    const uint64_t km = ballot(keep);
+    const uint32_t nk = popc(km);
+    if (nk + 1 > DECODE_MAX_FRONTIER) return Defer;
+    // kept elements in order, `last` at its upper bound
+    const uint32_t below = popc(ballot(keep && fv <= last));
+    const uint32_t to = keep ? popc(km & lt_mask()) + (fv <= last ? 0u : 1u) : 64u;
+    if (keep) scratch[to] = fv;
+    if (lane() == 0) scratch[below] = last;
+    __syncthreads();
+    fn = nk + 1;
+    fv = lane() < fn ? scratch[lane()] : 0u;
+    __syncthreads();
+    return S_OK;
+}
+
+// ascending sort of lanes [0, n) of a lane array (rank = smaller values + equal values at lower lanes)
+__device__ __forceinline__ uint32_t lane_sort(uint32_t v, uint32_t n, uint32_t *scratch) {
+    uint32_t rank = 0;
+    for (uint32_t j = 0; j < n; j++) {
+        const uint32_t pj = rdl(v, j);
+        rank += (pj < v || (pj == v && j < lane())) ? 1u : 0u;
+    }
+    if (lane() < n) scratch[rank] = v;
+    __syncthreads();
+    const uint32_t out = lane() < n ? scratch[lane()] : 0u;
+    __syncthreads();
+    return out;
+}
+
+__device__ __forceinline__ int add_doc(const AddParams &P, const AddDesc &D, DecodeResult &R, const Lds &L,
+                                       const Merged &M) {
+    Ctx C;
+    C.in = M.in + D.p_rel;
+    C.lz = P.lz + D.lz_off;
+    C.w0 = Win{C.in, 0x80000000u, 0};
+    C.w1 = Win{C.lz, 0x80000000u, 0};
+    const uint32_t len = D.p_len;
+    uint32_t *vs = L.vq;
+
+    // ---- merged state (uniform), starting as the resident oplog -----------------------------
+    uint32_t n_agents = D.b_n_agents, n_aruns = D.b_n_aruns, n_ent = D.b_n_ent, n_par = D.b_n_par;
+    uint32_t n_content = D.b_n_content, complete = D.b_complete, all_ascii = D.b_ascii;
+    uint64_t n_lv = D.b_n_lv;
+    uint32_t vf = lane() < D.b_n_ver ? M.ver[lane()] : 0u, vn = D.b_n_ver;   // cg.version
+    uint32_t la_lv = 0, la_len = 0, la_agent = 0xFFFFFFFFu, la_seq = 0;    // last agent run
+    if (n_aruns) { const uint4 a = M.aruns[n_aruns - 1]; la_lv = a.x; la_len = a.y; la_agent = a.z; la_seq = a.w; }
+    uint32_t last_end = n_ent ? M.ent[n_ent - 1].y : 0u;                 // last graph entry's end
+    uint32_t cr_valid = 0, cr_lv = 0, cr_len = 0, cr_pos = 0, cr_kind = 0, cr_fwd = 0;   // pending op run
+    if (D.b_n_ops) {
+        const uint4 o = M.ops[D.b_n_ops - 1];
+        cr_valid = 1; cr_lv = o.x; cr_len = o.y; cr_pos = o.z; cr_kind = o.w & 1u; cr_fwd = (o.w >> 1) & 1u;
+    }
+    uint32_t n_pre = 0, n_vm = 0;
+    uint32_t vm_file = 0, vm_local = 0, vm_len = 0;   // last version-map run (file offset from new_op_start)
+    bool dirty = false;   // lane-0 stores the next lane-parallel scan must see (fenced lazily)
+
+    // AgentAssignment::local_to_agent_version's inverse over the merged agent runs (LV order =
+    // each agent's insertion order): the first run holding seq; gap = the next run start above it
+    auto seq_find = [&](uint32_t a, uint64_t seq, uint64_t &lv, uint64_t &gap) -> bool {
+        if (dirty) { wave_fence(); dirty = false; }
+        gap = ~uint64_t(0);
+        for (uint32_t k0 = 0; k0 < n_aruns; k0 += 64) {
+            const uint32_t k = k0 + lane();
+            const uint4 r = k < n_aruns ? M.aruns[k] : make_uint4(0, 0, 0xFFFFFFFFu, 0);
+            const bool mine = r.z == a && r.y != 0;
+            const uint64_t hm = ballot(mine && seq >= r.w && seq < uint64_t(r.w) + r.y);
+            if (hm) {
+                const uint32_t l = ctz(hm);
+                lv = uint64_t(rdl(r.x, l)) + (seq - rdl(r.w, l));
+                gap = uint64_t(rdl(r.w, l)) + rdl(r.y, l);   // the run's end (seq)
+                return true;
+            }
+            uint64_t g = mine && r.w > seq ? uint64_t(r.w) : ~uint64_t(0);
+            for (int d = 32; d >= 1; d >>= 1) {
+                const uint64_t o = uint64_t(uint32_t(__shfl_xor(int(uint32_t(g)), d))) |
+                                   (uint64_t(uint32_t(__shfl_xor(int(uint32_t(g >> 32)), d))) << 32);
+                g = o < g ? o : g;
+            }
+            gap = g < gap ? g : gap;
+        }
+        return false;
+    };
+    auto seq_to_lv = [&](uint32_t a, uint64_t seq) -> int64_t {
+        uint64_t lv, gap;
+        return seq_find(a, seq, lv, gap) ? int64_t(lv) : -1;
+    };
+    // cg.assign (agent_runs RLE, agent_assignment/mod.rs)
+    auto assign = [&](uint32_t agent, uint32_t seq, uint32_t lv, uint32_t ln) -> int {
+        if (n_aruns && la_agent == agent && la_lv + la_len == lv && la_seq + la_len == seq) {
+            la_len += ln;
+            if (lane() == 0) M.aruns[n_aruns - 1].y = la_len;
+        } else {
+            if (n_aruns >= D.c_arun) return int(ErrCapacity);
+            if (lane() == 0) M.aruns[n_aruns] = make_uint4(lv, ln, agent, seq);
+            n_aruns++;
+            la_lv = lv; la_len = ln; la_agent = agent; la_seq = seq;
+        }
+        dirty = true;
+        return S_OK;
+    };
+    auto vmap_push = [&](uint32_t file, uint32_t local, uint32_t ln) -> int {
+        if (n_vm && vm_file + vm_len == file && vm_local + vm_len == local) {
+            vm_len += ln;
+            if (lane() == 0) M.vm[n_vm - 1].z = vm_len;
+        } else {
+            if (n_vm >= D.c_vm) return int(ErrCapacity);
+            if (lane() == 0) M.vm[n_vm] = make_uint4(file, local, ln, 0);
+            n_vm++;
+            vm_file = file; vm_local = local; vm_len = ln;
+        }
+        dirty = true;
+        return S_OK;
+    };
+    // find_packed_with_offset: the version-map run holding file offset f (per lane)
+    auto vmap_find = [&](uint32_t f, uint32_t &local, uint32_t &rem) -> bool {
+        uint32_t lo = 0, hi = n_vm;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (M.vm[mid].x <= f) lo = mid + 1; else hi = mid;
+        }
+        if (!lo) return false;
+        const uint4 m = M.vm[lo - 1];
+        if (f >= m.x + m.z) return false;
+        local = m.y + (f - m.x);
+        rem = m.z - (f - m.x);
+        return true;
+    };
+    auto flush_op = [&]() -> int {
+        if (!cr_valid) return S_OK;
+        if (n_pre >= D.c_pre) return int(ErrCapacity);
+        if (lane() == 0) M.pre[n_pre] = make_uint4(cr_lv, cr_len, cr_pos, cr_kind | (cr_fwd << 1));
+        n_pre++;
+        cr_valid = 0;
+        return S_OK;
+    };
+
+    // ---- header, LZ4 --------------------------------------------------------------------------
+    if (len < 8) return UnexpectedEOF;
+    {
+        const char *magic = "DMNDTYPS";
+        for (uint32_t i = 0; i < 8; i++)
+            if (C.byte(0, i) != uint32_t(uint8_t(magic[i]))) return InvalidMagic;
+    }
+    Rd r{0, 8, len - 8};
+    uint64_t pv;
+    TRY(C.u64v(r, pv));
+    if (pv != 0) return UnsupportedProtocolVersion;
+    Rd comp{SRC_LZ, 0, 0};
+    bool has_comp = false;
+    {
+        bool found; Rd c;
+        TRY(C.chunk_if(r, 5, found, c));
+        if (found) {
+            uint64_t ulen;
+            TRY(C.u64v(c, ulen));
+            if (ulen > (uint64_t(1) << 34)) return LZ4DecompressionError;
+            if (ulen > 255ull * c.n + 64) return LZ4DecompressionError;
+            if (ulen > D.lz_cap) return ErrCapacity;
+            if (!lz4_block(C, c, C.lz, uint32_t(ulen))) return LZ4DecompressionError;
+            comp.n = uint32_t(ulen);
+            has_comp = true;
+        }
+    }
+
+    // ---- FileInfo: doc id, agent names (get_or_create_agent_id on the merged agents) ----------
+    uint32_t n_file = 0;
+    uint32_t did_off = D.b_doc_id_off, did_len = D.b_doc_id_len;
+    {
+        Rd fi, an, tmp, did;
+        bool found;
+        TRY(C.expect_chunk(r, 1, fi));
+        TRY(C.chunk_if(fi, 2, found, did));
+        if (found) {
+            uint64_t dt;
+            TRY(C.u32v(did, dt));
+            if (dt != 4) return UnknownChunk;
+            bool asc;
+            if (!utf8_ok(C.in + did.p, did.n, asc)) return InvalidUTF8;
+        }
+        const bool has_did = found;
+        TRY(C.expect_chunk(fi, 3, an));
+        TRY(C.chunk_if(fi, 4, found, tmp));
+        while (an.n) {
+            uint64_t nl;
+            TRY(C.u64v(an, nl));
+            if (nl > an.n) return InvalidLength;
+            const uint32_t noff = an.p, nlen = uint32_t(nl);
+            an.p += nlen; an.n -= nlen;
+            bool asc;
+            if (!utf8_ok(C.in + noff, nlen, asc)) return InvalidUTF8;
+            if (n_file >= P.max_file_agents) return Defer;
+            uint32_t id = 0xFFFFFFFFu;
+            for (uint32_t j0 = 0; j0 < n_agents && id == 0xFFFFFFFFu; j0 += 64) {
+                const uint32_t j = j0 + lane();
+                bool eq = false;
+                if (j < n_agents) {
+                    const uint2 a = M.agents[j];
+                    eq = a.y == nlen;
+                    for (uint32_t k = 0; k < nlen && eq; k++) eq = M.in[a.x + k] == C.in[noff + k];
+                }
+                const uint64_t m = ballot(eq);
+                if (m) id = j0 + ctz(m);
+            }
+            if (id == 0xFFFFFFFFu) {
+                const bool root = nlen == 4 && C.byte(0, noff) == 'R' && C.byte(0, noff + 1) == 'O' &&
+                                  C.byte(0, noff + 2) == 'O' && C.byte(0, noff + 3) == 'T';
+                if (root || nlen >= 50) return ErrCheckout;   // mod.rs:88-91
+                if (n_agents >= D.c_agent) return ErrCapacity;
+                id = n_agents++;
+                if (lane() == 0) M.agents[id] = make_uint2(D.p_rel + noff, nlen);
+                wave_fence();
+            }
+            if (lane() == 0) { L.fmap[n_file] = id; L.fseq[n_file] = 0; }
+            n_file++;
+            __syncthreads();
+        }
+        if (has_did) {   // a doc id must match a non-empty oplog's (decode_oplog.rs:520-530)
+            if (D.b_doc_id_len != 0xFFFFFFFFu && D.b_n_lv != 0) {
+                bool same = D.b_doc_id_len == did.n;
+                for (uint32_t i = lane(); same && i < did.n; i += 64)
+                    same = M.in[D.b_doc_id_off + i] == C.in[did.p + i];
+                if (ballot(D.b_doc_id_len == did.n && !same) || D.b_doc_id_len != did.n) return DocIdMismatch;
+            }
+            did_off = D.p_rel + did.p;
+            did_len = did.n;
+        }
+    }
+    R.doc_id_off = did_off;
+    R.doc_id_len = did_len;
+
+    // ---- StartBranch: the version the patch starts from, in merged LVs -------------------------
+    uint32_t sv = 0, svn = 0;   // lane k: element k
+    {
+        Rd sb, ver;
+        bool found;
+        TRY(C.expect_chunk(r, 10, sb));
+        TRY(C.chunk_if(sb, 12, found, ver));
+        if (found) {
+            for (;;) {
+                uint64_t n, seq;
+                TRY(C.u64v(ver, n));
+                TRY(C.u64v(ver, seq));
+                if ((n >> 1) == 0) break;
+                if ((n >> 1) - 1 >= n_file) return InvalidLength;
+                const int64_t lv = seq_to_lv(L.fmap[(n >> 1) - 1], seq);
+                if (lv < 0) return BaseVersionUnknown;
+                if (svn == DECODE_MAX_FRONTIER) return Defer;
+                sv = lane() == svn ? uint32_t(lv) : sv;
+                svn++;
+                if (!(n & 1)) break;
+            }
+            if (ver.n) return InvalidLength;
+            sv = lane_sort(sv, svn, L.fr);
+        }
+        if (sb.n) {
+            Rd s; uint32_t asc;
+            TRY(content_str<false>(C, sb, comp, has_comp, s, asc));
+        }
+    }
+    Rd pc;
+    TRY(C.expect_chunk(r, 20, pc));
+    CRuns ins{}, del{};
+    for (;;) {
+        bool found; Rd ch;
+        TRY(C.chunk_if(pc, 24, found, ch));
+        if (!found) break;
+        uint64_t tag;
+        TRY(C.u32v(ch, tag));
+        if (tag > 1) return InvalidContent;
+        CRuns it{};
+        it.present = 1;
+        TRY(content_str<false>(C, ch, comp, has_comp, it.text, it.ascii));
+        Rd runs;
+        TRY(C.expect_chunk(ch, 25, runs));
+        it.runs = vq_make(C.in, runs);
+        it.t0 = it.text.p;
+        if (tag == 0) ins = it; else del = it;
+    }
+    Rd av, tp, hist;
+    TRY(C.expect_chunk(pc, 21, av));
+    TRY(C.expect_chunk(pc, 22, tp));
+    TRY(C.expect_chunk(pc, 23, hist));
+    VQ qav = vq_make(C.in, av), qtp = vq_make(C.in, tp), qhist = vq_make(C.in, hist);
+
+    // The file continues the resident version, or its operations are filtered against what the
+    // oplog already has (patches_overlap, decode_oplog.rs:670; file times go underwater).
+    const bool overlap = svn != vn || ballot(lane() < vn && sv != vf);
+    const uint64_t first_new = n_lv;
+    const uint64_t new_op_start = overlap ? UNDERWATER : first_new;
+    uint64_t next_assign = first_new, next_file = new_op_start;
+
+    // ---- OpVersions + OpTypeAndPosition + content runs (decode_oplog.rs:29-68, 731-850) -------
+    int64_t last_cursor = 0;
+    bool have_op = false;
+    uint64_t op_len = 0;
+    int64_t op_start = 0;
+    bool op_del = false, op_fwd = true;
+    while (qav.left()) {
+        uint64_t n, alen;
+        int64_t jump = 0;
+        TRY(vq_pop(qav, n, vs));
+        const bool has_jump = n & 1;
+        n >>= 1;
+        TRY(vq_pop(qav, alen, vs));
+        if (has_jump) TRY(vq_zigzag(qav, jump, vs));
+        if (n == 0 || n - 1 >= n_file) return InvalidLength;
+        const uint32_t fa = uint32_t(n - 1);
+        const uint32_t agent = L.fmap[fa];
+        int64_t sstart = int64_t(L.fseq[fa]) + jump;
+        const int64_t send = sstart + int64_t(alen);
+        if (sstart < 0 || uint64_t(send) >= LIM31 || next_assign + alen >= LIM31) return Defer;
+        __syncthreads();
+        if (lane() == 0) L.fseq[fa] = uint32_t(send);
+        __syncthreads();
+        while (sstart < send) {
+            uint64_t known_lv = 0, run_end = uint64_t(send);
+            bool keep = true;
+            if (overlap) {
+                uint64_t gap;
+                keep = !seq_find(agent, uint64_t(sstart), known_lv, gap);
+                run_end = gap;
+            }
+            const uint64_t l = (uint64_t(send) < run_end ? uint64_t(send) : run_end) - uint64_t(sstart);
+            const uint32_t frel = uint32_t(next_file - new_op_start);
+            if (keep) {
+                TRY(assign(agent, uint32_t(sstart), uint32_t(next_assign), uint32_t(l)));
+                TRY(vmap_push(frel, uint32_t(next_assign), uint32_t(l)));
+                next_assign += l;
+            } else {   // already here: map the file's items onto the local ones
+                TRY(vmap_push(frel, uint32_t(known_lv), uint32_t(l)));
+            }
+            next_file += l;
+            sstart += int64_t(l);
+
+            uint64_t want = l;   // parse_next_patches (decode_oplog.rs:731-778)
+            while (want) {
+                if (!have_op) {
+                    if (!qtp.left()) return InvalidLength;
+                    uint64_t x;
+                    TRY(vq_pop(qtp, x, vs));
+                    const bool has_length = x & 1; x >>= 1;
+                    const bool diff_nz = x & 1; x >>= 1;
+                    const bool is_del = x & 1; x >>= 1;
+                    int64_t diff = 0;
+                    bool fwd = true;
+                    uint64_t ol;
+                    if (has_length) {
+                        if (is_del) { fwd = x & 1; x >>= 1; }
+                        if (diff_nz) TRY(vq_zigzag(qtp, diff, vs));
+                        ol = x;
+                    } else {
+                        ol = 1;
+                        diff = int64_t(x >> 1) * ((x & 1) ? -1 : 1);
+                    }
+                    const int64_t raw = int64_t(uint64_t(last_cursor) + uint64_t(diff));
+                    int64_t st, raw_end;
+                    if (!is_del) { st = raw; raw_end = raw + int64_t(ol); }
+                    else if (fwd) { st = raw; raw_end = raw; }
+                    else { st = raw - int64_t(ol); raw_end = raw - int64_t(ol); }
+                    last_cursor = raw_end;
+                    if (ol == 0) return ErrCheckout;   // assert!(max_len > 0)
+                    op_len = ol; op_start = st; op_del = is_del; op_fwd = fwd; have_op = true;
+                }
+                uint64_t take = want < op_len ? want : op_len;
+                CRuns ci = op_del ? del : ins;
+                bool known = false;
+                Rd cs{0, 0, 0};
+                if (ci.present) {
+                    bool has, cknown; uint64_t clen;
+                    TRY(cruns_next(C, ci, has, clen, cknown, cs, vs));
+                    if (!has) return InvalidLength;
+                    if (clen < take) take = clen;
+                    if (clen > take) {   // push the remainder back (SplitableSpan truncate)
+                        uint32_t b = 0;
+                        if (cknown) {
+                            uint64_t c2;
+                            walk_chars(C.ptr(cs.s) + cs.p, cs.n, take, ci.ascii, b, c2);
+                        }
+                        ci.pb = 1;
+                        ci.pb_len = clen - take; ci.pb_known = cknown;
+                        ci.pb_s = cknown ? Rd{cs.s, cs.p + b, cs.n - b} : Rd{cs.s, cs.p, 0};
+                        cs.n = b;
+                    }
+                    known = cknown;
+                }
+                if (op_del) del = ci; else ins = ci;
+                if (!take) return ErrCheckout;
+                if (keep) {
+                    int64_t ppos;
+                    bool pfwd = true;
+                    if (!op_del) ppos = op_start;
+                    else if (op_fwd) ppos = op_start;
+                    else { ppos = op_start + int64_t(op_len) - int64_t(take); pfwd = false; }
+                    if (ppos < 0 || uint64_t(ppos) >= LIM31) return Defer;
+                    const uint32_t lv = uint32_t(n_lv);
+                    if (n_lv + take > D.c_lv) return ErrCapacity;
+                    if (!op_del) {   // push_ins
+                        if (known) {
+                            if (n_content + cs.n > D.c_content) return ErrCapacity;
+                            const uint8_t *src = C.ptr(cs.s) + cs.p;
+                            // a catch-up patch keeps every piece: the known pieces tile the insert
+                            // text in order, copied whole at the end
+                            if (overlap)
+                                for (uint32_t i = lane(); i < cs.n; i += 64) M.content[n_content + i] = src[i];
+                            if (ci.ascii) {
+                                for (uint64_t i = lane(); i < take; i += 64) M.cbyte[lv + i] = n_content + uint32_t(i);
+                            } else {
+                                all_ascii = 0;
+                                uint32_t cnt = 0;
+                                for (uint32_t i = 0; i < cs.n; i += 64) {
+                                    const uint32_t j = i + lane();
+                                    const bool s0 = j < cs.n && (src[j] & 0xC0u) != 0x80u;
+                                    const uint64_t m = ballot(s0);
+                                    if (s0) M.cbyte[lv + cnt + popc(m & lt_mask())] = n_content + j;
+                                    cnt += popc(m);
+                                }
+                            }
+                            n_content += cs.n;
+                        } else {
+                            for (uint64_t i = lane(); i < take; i += 64) M.cbyte[lv + i] = 0xFFFFFFFFu;
+                            complete = 0;
+                        }
+                        n_lv += take;
+                        if (cr_valid && cr_kind == 0 && cr_lv + cr_len == lv && uint64_t(cr_pos) + cr_len == uint64_t(ppos)) {
+                            cr_len += uint32_t(take);
+                        } else {
+                            TRY(flush_op());
+                            cr_valid = 1; cr_lv = lv; cr_len = uint32_t(take); cr_pos = uint32_t(ppos); cr_kind = 0; cr_fwd = 1;
+                        }
+                    } else {         // push_del
+                        for (uint64_t i = lane(); i < take; i += 64) M.cbyte[lv + i] = 0xFFFFFFFFu;
+                        n_lv += take;
+                        const uint32_t pos = uint32_t(ppos), ln = uint32_t(take);
+                        bool merged = false;
+                        if (cr_valid && cr_kind == 1 && cr_lv + cr_len == lv) {
+                            if ((cr_len == 1 || cr_fwd) && (ln == 1 || pfwd) && pos == cr_pos) {
+                                cr_len += ln; cr_fwd = 1; merged = true;
+                            } else if ((cr_len == 1 || !cr_fwd) && (ln == 1 || !pfwd) && uint64_t(pos) + ln == cr_pos) {
+                                cr_pos = pos; cr_len += ln; cr_fwd = 0; merged = true;
+                            }
+                        }
+                        if (!merged) {
+                            TRY(flush_op());
+                            cr_valid = 1; cr_lv = lv; cr_len = ln; cr_pos = pos; cr_kind = 1; cr_fwd = pfwd ? 1 : 0;
+                        }
+                    }
+                }
+                if (!op_del) op_start += int64_t(take);
+                op_len -= take;
+                if (!op_len) have_op = false;
+                want -= take;
+            }
+        }
+    }
+    if (n_lv != next_assign) return InvalidLength;
+    TRY(flush_op());
+    const uint64_t file_end = next_file;
+    if (!overlap && n_content > D.b_n_content) {
+        const uint8_t *src = C.ptr(ins.text.s) + ins.t0;
+        for (uint32_t i = lane(); i < n_content - D.b_n_content; i += 64) M.content[D.b_n_content + i] = src[i];
+    }
+    wave_fence();   // the agent runs and the version map, read lane-parallel from here on
+    dirty = false;
+
+    // ---- OpParents (decode_oplog.rs:95-148, 856-913) -----------------------------------------
+    next_file = new_op_start;
+    uint64_t next_hist = first_new;
+    uint32_t ff = sv, ffn = svn;   // the file's version, advanced run by run
+    while (qhist.left()) {
+        uint64_t hl;
+        TRY(vq_pop(qhist, hl, vs));
+        uint64_t pv64 = 0;   // lane k: parent k (a merged LV, or a file time >= UNDERWATER)
+        uint32_t np = 0;
+        bool under = false;  // next_time - n below zero (fails the range check)
+        for (;;) {
+            uint64_t n;
+            TRY(vq_pop(qhist, n, vs));
+            const bool foreign = n & 1; n >>= 1;
+            const bool more = n & 1; n >>= 1;
+            uint64_t p;
+            if (foreign) {
+                if (n == 0) break;
+                if (n - 1 >= n_file) return InvalidLength;
+                uint64_t seq;
+                TRY(vq_pop(qhist, seq, vs));
+                const int64_t lv = seq_to_lv(L.fmap[n - 1], seq);
+                if (lv < 0) return InvalidLength;
+                p = uint64_t(lv);
+            } else {
+                if (overlap && n > next_file - new_op_start) return InvalidLength;   // would surface from underwater
+                under |= n > next_file;
+                p = next_file - n;
+            }
+            if (np == DECODE_MAX_PARENTS) return Defer;
+            pv64 = lane() == np ? p : pv64;
+            np++;
+            if (!more) break;
+        }
+        if (hl == 0 || next_file + hl > file_end) return InvalidLength;
+        if (under || ballot(lane() < np && pv64 >= next_file)) return InvalidLength;
+        // history_entry_map_and_truncate (decode_oplog.rs:241-269), one mapped piece at a time
+        uint64_t es = next_file;
+        const uint64_t ee = next_file + hl;
+        next_file = ee;
+        for (;;) {
+            uint32_t ms, mrem;
+            if (!vmap_find(uint32_t(es - new_op_start), ms, mrem)) return InvalidLength;
+            const uint32_t take = uint32_t(ee - es < uint64_t(mrem) ? ee - es : uint64_t(mrem));
+            uint32_t me = ms + take;
+            uint32_t mp = 0;
+            bool bad = false;
+            if (lane() < np) {
+                if (pv64 >= UNDERWATER) {
+                    uint32_t loc, rem;
+                    if (vmap_find(uint32_t(pv64 - new_op_start), loc, rem)) mp = loc; else bad = true;
+                } else {
+                    mp = uint32_t(pv64);
+                }
+            }
+            if (ballot(bad)) return InvalidLength;
+            mp = lane_sort(mp, np, L.fr);
+            TRY(advance_known(ff, ffn, mp, np, ms, me, L.fr));
+            if (me > next_hist) {   // new here: graph.push + cg.version.advance_by_known_run
+                uint32_t mpn = np;
+                if (ms > next_hist) return InvalidLength;   // assert!(mapped.span.start <= next_history_time)
+                if (ms < next_hist) { mp = lane() == 0 ? uint32_t(next_hist - 1) : 0u; mpn = 1; ms = uint32_t(next_hist); }
+                if (ballot(lane() < mpn && mp >= ms)) return InvalidLength;
+                if (mpn == 1 && n_ent && rdl(mp, 0) == last_end - 1 && last_end == ms) {   // Graph::push extends
+                    last_end = me;
+                    if (lane() == 0) M.ent[n_ent - 1].y = me;
+                } else {
+                    if (n_ent >= D.c_ent || n_par + mpn > D.c_par) return ErrCapacity;
+                    if (lane() == 0) { M.ent[n_ent] = make_uint2(ms, me); M.poff[n_ent] = n_par; }
+                    if (lane() < mpn) M.par[n_par + lane()] = mp;
+                    n_ent++;
+                    n_par += mpn;
+                    last_end = me;
+                }
+                TRY(advance_known(vf, vn, mp, mpn, ms, me, L.fr));
+                next_hist = me;
+            }
+            es += take;
+            if (es == ee) break;
+            pv64 = lane() == 0 ? es - 1 : 0;   // GraphEntrySimple::trim: the remainder's parent, unmapped
+            np = 1;
+        }
+    }
+    if (next_file != file_end || next_hist != next_assign) return InvalidLength;
+    if (pc.n) return InvalidLength;
+    if (ins.present) {
+        bool has, kn; uint64_t l; Rd s;
+        const int e = cruns_next(C, ins, has, l, kn, s, vs);
+        if (e || has) return InvalidContent;
+    }
+    if (del.present) {
+        bool has, kn; uint64_t l; Rd s;
+        const int e = cruns_next(C, del, has, l, kn, s, vs);
+        if (e || has) return InvalidContent;
+    }
+    {   // CRC (decode_oplog.rs:940-955)
+        const uint32_t reader_len = r.n;
+        bool found; Rd c;
+        TRY(C.chunk_if(r, 100, found, c));
+        if (found && !D.ignore_crc) {
+            if (c.n < 4) return UnexpectedEOF;
+            const uint32_t want = C.byte(0, c.p) | (C.byte(0, c.p + 1) << 8) | (C.byte(0, c.p + 2) << 16) |
+                                  (C.byte(0, c.p + 3) << 24);
+            if (crc32c_par(C.in, len - reader_len, L.crc, P.x2n) != want) return ChecksumFailed;
+        }
+    }
+    wave_fence();
+
+    // ---- HostOpLog::finish: the new op runs (and the resident's last) split at entry ends ------
+    {
+        const uint32_t o0 = D.b_n_ops ? D.b_n_ops - 1 : 0;
+        uint32_t nout = o0;
+        for (uint32_t b0 = 0; b0 < n_pre; b0 += 64) {
+            const uint32_t i = b0 + lane();
+            const bool live = i < n_pre;
+            const uint4 q = live ? M.pre[i] : make_uint4(0, 0, 0, 0);
+            uint32_t lo = 0, hi = live ? n_ent : 0;   // first entry ending above the run's first LV
+            while (lo < hi) {
+                const uint32_t m = (lo + hi) >> 1;
+                if (M.ent[m].y <= q.x) lo = m + 1; else hi = m;
+            }
+            uint32_t npc = 0;
+            if (live) {
+                npc = 1;
+                const uint32_t end = q.x + q.y;
+                for (uint32_t e = lo; e < n_ent && M.ent[e].y < end; e++) npc++;
+            }
+            const uint32_t incl = scan_incl(npc);
+            const uint32_t tot = rdl(incl, 63);
+            if (uint64_t(nout) + tot > D.c_op) return ErrCapacity;
+            if (live) {
+                uint32_t rlv = q.x, rlen = q.y, rpos = q.z, e = lo, k = nout + incl - npc;
+                const uint32_t kf = q.w, kind = kf & 1u, fwd = kf >> 1;
+                while (rlen) {
+                    const uint32_t cut = e < n_ent ? M.ent[e].y : rlv + rlen;
+                    const uint32_t mm = rlen < cut - rlv ? rlen : cut - rlv;
+                    uint32_t apos = rpos;
+                    if (kind == 0) rpos += mm;
+                    else if (!fwd) apos = rpos + rlen - mm;
+                    M.ops[k++] = make_uint4(rlv, mm, apos, kf);
+                    rlv += mm;
+                    rlen -= mm;
+                    if (rlv >= cut) e++;
+                }
+            }
+            nout += tot;
+        }
+        R.n_ops = n_pre ? nout : D.b_n_ops;
+    }
+    if (lane() == 0) M.poff[n_ent] = n_par;
+    if (lane() < vn) M.ver[lane()] = vf;
+    if (lane() < ffn) M.ffr[lane()] = ff;
+    R.n_agents = n_agents;
+    R.n_aruns = n_aruns;
+    R.n_entries = n_ent;
+    R.n_parents = n_par;
+    R.n_content = n_content;
+    R.n_version = vn;
+    R.n_file_frontier = ffn;
+    R.content_complete = complete;
+    R.ascii = all_ascii;
+    R.n_lv = n_lv;
+    R.n_file_agents = n_file;
+    return S_OK;
+}
+
+// copies of the resident arrays (lane-parallel), and their restoration after an error
+__device__ __forceinline__ void add_copy_base(const AddParams &P, const AddDesc &D, const Merged &M) {
+    {   // the resident's bytes (agent names, doc id), then the patch after them
+        const uint4 *s = reinterpret_cast<const uint4 *>(P.b_in + D.b_in);
+        uint4 *d = reinterpret_cast<uint4 *>(M.in);
+        for (uint32_t i = lane(); i < (D.b_in_len + 15) / 16; i += 64) d[i] = s[i];
+        const uint4 *ps = reinterpret_cast<const uint4 *>(P.p_in + D.p_off);
+        uint4 *pd = reinterpret_cast<uint4 *>(M.in + D.p_rel);
+        for (uint32_t i = lane(); i < (D.p_len + 15) / 16; i += 64) pd[i] = ps[i];
+    }
+    const uint4 *ba = reinterpret_cast<const uint4 *>(P.b_aruns) + D.b_arun;
+    for (uint32_t i = lane(); i < D.b_n_aruns; i += 64) M.aruns[i] = ba[i];
+    const uint4 *bo = reinterpret_cast<const uint4 *>(P.b_ops) + D.b_op;
+    for (uint32_t i = lane(); i < D.b_n_ops; i += 64) M.ops[i] = bo[i];
+    const uint2 *be = reinterpret_cast<const uint2 *>(P.b_ent) + D.b_ent;
+    for (uint32_t i = lane(); i < D.b_n_ent; i += 64) M.ent[i] = be[i];
+    for (uint32_t i = lane(); i <= D.b_n_ent; i += 64) M.poff[i] = P.b_poff[D.b_poff + i];
+    for (uint32_t i = lane(); i < D.b_n_par; i += 64) M.par[i] = P.b_par[D.b_par + i];
+    for (uint32_t i = lane(); i < D.b_n_content; i += 64) M.content[i] = P.b_content[D.b_content + i];
+    for (uint32_t i = lane(); i < D.b_n_lv; i += 64) M.cbyte[i] = P.b_cbyte[D.b_lv + i];
+    const uint2 *bg = reinterpret_cast<const uint2 *>(P.b_agents) + D.b_agent;
+    for (uint32_t i = lane(); i < D.b_n_agents; i += 64) M.agents[i] = bg[i];
+    if (lane() < D.b_n_ver) M.ver[lane()] = P.b_ver[D.b_ver + lane()];
+    wave_fence();
+}
+
+#ifndef DTGPU_ADD_WAVES
+#define DTGPU_ADD_WAVES 2   // 231 VGPRs, no VGPR spills (4: 218 spilled, 3.6x slower)
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_ADD_WAVES))) void decode_add_kernel(AddParams P) {
+    extern __shared__ uint32_t lds[];
+    const uint32_t doc = blockIdx.x;
+    if (doc >= P.n_docs) return;
+    const AddDesc D = P.docs[doc];
+    Lds L{};
+    const uint32_t F = P.max_file_agents;
+    L.crc = lds;
+    L.fr = lds + 256;
+    L.vq = lds + 320;
+    L.fmap = lds + 512;
+    L.fseq = L.fmap + F;
+    for (uint32_t i = lane(); i < 256; i += 64) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ CRC_POLY : c >> 1;
+        L.crc[i] = c;
+    }
+    __syncthreads();
+    Merged M;
+    M.in = P.m_in + D.m_in;
+    M.content = P.m_content + D.m_content;
+    M.aruns = reinterpret_cast<uint4 *>(P.m_aruns) + D.m_arun;
+    M.ops = reinterpret_cast<uint4 *>(P.m_ops) + D.m_op;
+    M.pre = reinterpret_cast<uint4 *>(P.scr) + D.m_scr;
+    M.vm = M.pre + D.c_pre;
+    M.ent = reinterpret_cast<uint2 *>(P.m_ent) + D.m_ent;
+    M.agents = reinterpret_cast<uint2 *>(P.m_agents) + D.m_agent;
+    M.poff = P.m_poff + D.m_poff;
+    M.par = P.m_par + D.m_par;
+    M.cbyte = P.m_cbyte + D.m_lv;
+    M.ver = P.m_ver + D.m_ver;
+    M.ffr = P.m_ffr + D.m_ver;
+    DecodeResult R{};
+    int st = Defer;
+    add_copy_base(P, D, M);   // (a resident document that failed its own decode has no arrays)
+    if (!D.skip) st = add_doc(P, D, R, L, M);
+    if (st != S_OK) {   // the unwind: the merged document is the resident one
+        const uint4 *ba = reinterpret_cast<const uint4 *>(P.b_aruns) + D.b_arun;
+        const uint2 *be = reinterpret_cast<const uint2 *>(P.b_ent) + D.b_ent;
+        if (lane() == 0 && D.b_n_aruns) M.aruns[D.b_n_aruns - 1] = ba[D.b_n_aruns - 1];
+        if (lane() == 0 && D.b_n_ent) M.ent[D.b_n_ent - 1] = be[D.b_n_ent - 1];
+        if (lane() == 0) M.poff[D.b_n_ent] = D.b_n_par;
+        if (lane() < D.b_n_ver) M.ver[lane()] = P.b_ver[D.b_ver + lane()];
+        R = DecodeResult{};
+        R.n_agents = D.b_n_agents; R.n_aruns = D.b_n_aruns; R.n_ops = D.b_n_ops; R.n_entries = D.b_n_ent;
+        R.n_parents = D.b_n_par; R.n_content = D.b_n_content; R.n_version = D.b_n_ver; R.n_lv = D.b_n_lv;
+        R.content_complete = D.b_complete; R.ascii = D.b_ascii;
+        R.doc_id_off = D.b_doc_id_off; R.doc_id_len = D.b_doc_id_len;
+    }
+    R.status = uint32_t(st);
+    if (lane() == 0) P.results[doc] = R;
+}
+
 }  // namespace ddec
 
 int launch_decode(const DecodeParams &p, void *stream) {
@@ -1961,6 +2703,13 @@ int launch_decode(const DecodeParams &p, void *stream) {
         hipLaunchKernelGGL(ddec::decode_kernel<true>, dim3(p.n_docs), dim3(64), lds, s, p);
     else
         hipLaunchKernelGGL(ddec::decode_kernel<false>, dim3(p.n_docs), dim3(64), lds, s, p);
+    return hipGetLastError() == hipSuccess ? 0 : 66;
+}
+
+int launch_decode_add(const AddParams &p, void *stream) {
+    if (!p.n_docs) return 0;
+    const size_t lds = (512 + 2 * size_t(p.max_file_agents)) * 4;
+    hipLaunchKernelGGL(ddec::decode_add_kernel, dim3(p.n_docs), dim3(64), lds, reinterpret_cast<hipStream_t>(stream), p);
     return hipGetLastError() == hipSuccess ? 0 : 66;
 }
 

@@ -27,6 +27,7 @@ struct DecodeDesc {
     uint64_t ver_off;       // words: the frontier (cg.version), <= 64 LVs
     uint32_t in_len, lz_cap, arun_cap, pre_cap, op_cap, ent_cap, par_cap, content_cap, lv_cap, agent_cap;
     uint32_t ignore_crc, skip;
+    uint32_t patch, pad;    // sizing a patch for decode_and_add: a StartBranch version is not an error
 };
 
 struct DecodeResult {
@@ -35,7 +36,8 @@ struct DecodeResult {
     uint32_t n_content, n_version, content_complete, ascii;
     uint64_t n_lv;
     // sizing pass (size_only): what the full pass needs
-    uint32_t lz_len, tp_bytes, cik_bytes, hist_bytes, raw_aruns, pad;
+    uint32_t lz_len, tp_bytes, cik_bytes, hist_bytes, raw_aruns;
+    uint32_t n_file_frontier;   // decode_and_add: the patch's version (decode_and_add's return value)
     uint32_t prof[8];       // core-clock cycles per decode phase (full pass)
     uint32_t doc_id_off, doc_id_len;   // the DocId bytes in the document (len ~0: none)
 };
@@ -57,5 +59,37 @@ struct DecodeParams {
 };
 
 int launch_decode(const DecodeParams &p, void *stream);
+
+// decode_and_add (ListOpLog::decode_and_add_opts, decode_oplog.rs:476-583 and the overlap filter of
+// decode_internal :670-913) on the device: one wavefront per (resident oplog, patch) pair.  The
+// merged oplog goes to a new set of arenas: the resident arrays are copied, then the patch's new
+// operations appended with the reference's RLE rules (agent runs, op runs, Graph::push); on an
+// error the merged document is the resident one again (the reference's unwind).
+struct AddDesc {
+    // the resident oplog (a decoded handle's document)
+    uint64_t b_in, b_arun, b_op, b_ent, b_poff, b_par, b_content, b_lv, b_agent, b_ver;
+    uint32_t b_in_len, b_n_aruns, b_n_ops, b_n_ent, b_n_par, b_n_content, b_n_agents, b_n_ver, b_n_lv;
+    uint32_t b_complete, b_ascii, b_doc_id_off, b_doc_id_len;
+    // the patch: its bytes in the merged `in` region at p_rel, its LZ4 buffer
+    uint32_t p_rel, p_len, lz_cap, pad0;
+    uint64_t p_off, lz_off;   // the patch in the patch arena (copied to m_in + p_rel first)
+    // merged arenas (offsets in elements) and capacities; scr: op-run pieces, then the version map
+    uint64_t m_in, m_arun, m_op, m_ent, m_poff, m_par, m_content, m_lv, m_agent, m_ver, m_scr;
+    uint32_t c_arun, c_op, c_ent, c_par, c_content, c_lv, c_agent, c_pre, c_vm;
+    uint32_t ignore_crc, skip, pad1;
+};
+
+struct AddParams {
+    const uint8_t *b_in, *b_content, *p_in;
+    const uint32_t *b_aruns, *b_ops, *b_ent, *b_poff, *b_par, *b_cbyte, *b_agents, *b_ver;
+    uint8_t *m_in, *lz, *m_content;
+    uint32_t *m_aruns, *m_ops, *m_ent, *m_poff, *m_par, *m_cbyte, *m_agents, *m_ver, *m_ffr, *scr;
+    const AddDesc *docs;
+    DecodeResult *results;
+    uint32_t n_docs, max_file_agents;
+    uint32_t x2n[32];
+};
+
+int launch_decode_add(const AddParams &p, void *stream);
 
 }  // namespace dtgpu

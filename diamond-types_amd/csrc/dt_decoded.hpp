@@ -25,6 +25,11 @@ struct dtgpu_decoded {
     std::vector<DecodeResult> res;
     DevBuf<uint8_t> in, lz, content;
     DevBuf<uint32_t> aruns, alist, pre, ops, ent, poff, par, cbyte, agents, ver;
+    // dtgpu_decode_add results: the merged oplogs (not re-decodable), each merge's status and the
+    // patch's version
+    bool merged = false;
+    std::vector<uint32_t> add_status;
+    DevBuf<uint32_t> ffr;
     DevBuf<DecodeDesc> d_desc;
     DevBuf<DecodeResult> d_res;
     DecodeParams P{};

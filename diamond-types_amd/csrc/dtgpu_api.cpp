@@ -522,17 +522,13 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
 // Device-staged batch: `.dt` bytes -> device decode -> device prep -> planner sizing pass ->
 // replay layout.  The host only reads back per-document counts to size the arenas.  Documents
 // the device path hands back (decoder or prep limits) get status DTGPU_DECODE_DEFER.
-dtgpu_status stage_device(const uint8_t *const *docs, const size_t *lens, size_t n, const dtgpu_batch_opts *opts,
-                          dtgpu_batch **out) {
+// `dec` is a decoded handle (dtgpu_decode_create: decoded here; dtgpu_decode_add: already merged).
+dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     auto B = std::make_unique<dtgpu_batch>();
-    B->device = opts ? opts->device : 0;
-    {
-        dtgpu_decoded *dh = nullptr;
-        dtgpu_status st = dtgpu_decode_create(docs, lens, n, opts, &dh);
-        if (st != DTGPU_OK) return st;
-        B->dec.reset(dh);
-    }
+    B->device = dec->device;
+    B->dec.reset(dec);
     dtgpu_decoded &Dd = *B->dec;
+    const size_t n = Dd.n;
     if (hipSetDevice(B->device) != hipSuccess) return DTGPU_ERR_HIP;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, B->device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -543,9 +539,11 @@ dtgpu_status stage_device(const uint8_t *const *docs, const size_t *lens, size_t
     CK(hipEventCreate(&B->ev0)); CK(hipEventCreate(&B->ev_mid)); CK(hipEventCreate(&B->ev1));
     CK(hipEventCreate(&B->ev_dec)); CK(hipEventCreate(&B->ev_prep));
     hipStream_t s = B->stream;
-    if (launch_decode(Dd.P, s)) return DTGPU_ERR_HIP;
-    CK(hipMemcpyAsync(Dd.res.data(), Dd.d_res.p, n * sizeof(DecodeResult), hipMemcpyDeviceToHost, s));
-    CK(hipStreamSynchronize(s));
+    if (!Dd.merged) {
+        if (launch_decode(Dd.P, s)) return DTGPU_ERR_HIP;
+        CK(hipMemcpyAsync(Dd.res.data(), Dd.d_res.p, n * sizeof(DecodeResult), hipMemcpyDeviceToHost, s));
+        CK(hipStreamSynchronize(s));
+    }
     B->n = n;
     B->host_status.assign(n, OK);
     B->n_lv.assign(n, 0);
@@ -1026,6 +1024,11 @@ size_t dtgpu_oplog_export(const dtgpu_oplog *h, int what, void *out, size_t cap)
             for (const std::string &nm : o.agent_names) { b.push_back(uint8_t(nm.size())); b.insert(b.end(), nm.begin(), nm.end()); }
             bytes = true;
             break;
+        case DTGPU_EXPORT_DOC_ID:
+            b.push_back(o.has_doc_id ? 1 : 0);
+            if (o.has_doc_id) b.insert(b.end(), o.doc_id.begin(), o.doc_id.end());
+            bytes = true;
+            break;
         default: return 0;
     }
     const size_t per = what == DTGPU_EXPORT_OPS || what == DTGPU_EXPORT_AGENT_RUNS ? 4 : what == DTGPU_EXPORT_ENTRIES ? 2 : 1;
@@ -1097,10 +1100,19 @@ dtgpu_status dtgpu_batch_xf_positions(dtgpu_batch *B, size_t i, uint32_t *out, s
 dtgpu_status dtgpu_batch_create_device(const uint8_t *const *docs, const size_t *lens, size_t n,
                                        const dtgpu_batch_opts *opts, dtgpu_batch **out) {
     if (!out || (n && (!docs || !lens))) return DTGPU_ERR_ARG;
-    return stage_device(docs, lens, n, opts, out);
+    dtgpu_decoded *dh = nullptr;
+    const dtgpu_status st = dtgpu_decode_create(docs, lens, n, opts, &dh);
+    if (st != DTGPU_OK) return st;
+    return stage_device(dh, out);
+}
+
+dtgpu_status dtgpu_batch_create_decoded(dtgpu_decoded *dec, dtgpu_batch **out) {
+    if (!dec || !out) return DTGPU_ERR_ARG;
+    if (!dec->stream && hipStreamCreateWithFlags(&dec->stream, hipStreamNonBlocking) != hipSuccess) return DTGPU_ERR_HIP;
+    return stage_device(dec, out);
 }
 dtgpu_status dtgpu_batch_run_e2e_timed(dtgpu_batch *B, float ms[4]) {
-    if (!B || !B->dec) return DTGPU_ERR_ARG;
+    if (!B || !B->dec || B->dec->merged) return DTGPU_ERR_ARG;
     if (hipSetDevice(B->device) != hipSuccess) return DTGPU_ERR_HIP;
     hipStream_t s = B->stream;
     // decode + prep + plan + replay from the `.dt` bytes in HBM

@@ -154,7 +154,7 @@ dtgpu_status dtgpu_decode_create(const uint8_t *const *docs, const size_t *lens,
 }
 
 dtgpu_status dtgpu_decode_run(dtgpu_decoded *D, float *ms) {
-    if (!D) return DTGPU_ERR_ARG;
+    if (!D || D->merged) return DTGPU_ERR_ARG;
     if (hipSetDevice(D->device) != hipSuccess) return DTGPU_ERR_HIP;
     if (hipEventRecord(D->ev0, D->stream) != hipSuccess) return DTGPU_ERR_HIP;
     if (launch_decode(D->P, D->stream)) return DTGPU_ERR_HIP;
@@ -168,6 +168,170 @@ dtgpu_status dtgpu_decode_run(dtgpu_decoded *D, float *ms) {
     D->last_ms = t;
     if (ms) *ms = t;
     return DTGPU_OK;
+}
+
+// ListOpLog::decode_and_add_opts for a batch (decode_oplog.rs:476-583): patch i merged into
+// document i of `base` on the device (dt_decode.hip decode_add_kernel).  Staging: the patches go to
+// HBM, the decoder's sizing pass reads their chunk directories (a StartBranch version is not an
+// error there), and the merged arenas are sized from the resident counts plus the patch counts.
+dtgpu_status dtgpu_decode_add(const dtgpu_decoded *B, const uint8_t *const *patches, const size_t *lens, size_t n,
+                              int ignore_crc, float *ms, dtgpu_decoded **out) {
+    if (!B || !out || n != B->n || (n && (!patches || !lens))) return DTGPU_ERR_ARG;
+    auto M = new dtgpu_decoded();
+    std::unique_ptr<dtgpu_decoded> guard(M);
+    M->device = B->device;
+    M->merged = true;
+#define CK(x) do { if ((x) != hipSuccess) return DTGPU_ERR_HIP; } while (0)
+    CK(hipSetDevice(M->device));
+    CK(hipStreamCreateWithFlags(&M->stream, hipStreamNonBlocking));
+    CK(hipEventCreate(&M->ev0));
+    CK(hipEventCreate(&M->ev1));
+    hipStream_t s = M->stream;
+    M->n = n;
+    // the patches, packed like dtgpu_decode_create's documents
+    std::vector<DecodeDesc> pd(n, DecodeDesc{});
+    uint64_t ptotal = 0;
+    for (size_t i = 0; i < n; i++) {
+        if (lens[i] >= (1ull << 31)) return DTGPU_ERR_ARG;
+        pd[i].in_off = ptotal;
+        pd[i].in_len = uint32_t(lens[i]);
+        pd[i].patch = 1;
+        ptotal = align256(ptotal + lens[i] + 256);
+        M->in_bytes += lens[i];
+    }
+    DevBuf<uint8_t> pin;
+    {
+        std::vector<uint8_t> host(ptotal, 0);
+        for (size_t i = 0; i < n; i++)
+            if (lens[i]) std::memcpy(host.data() + pd[i].in_off, patches[i], lens[i]);
+        CK(pin.upload(host, s));
+    }
+    DevBuf<DecodeDesc> d_pd;
+    DevBuf<DecodeResult> d_pr;
+    CK(d_pd.upload(pd, s));
+    CK(d_pr.alloc(n));
+    std::vector<DecodeResult> pr(n);
+    {   // sizing pass over the patches
+        DecodeParams P{};
+        P.in = pin.p;
+        P.docs = d_pd.p;
+        P.results = d_pr.p;
+        P.n_docs = uint32_t(n);
+        P.size_only = 1;
+        if (launch_decode(P, s)) return DTGPU_ERR_HIP;
+        CK(hipMemcpyAsync(pr.data(), d_pr.p, n * sizeof(DecodeResult), hipMemcpyDeviceToHost, s));
+        CK(hipStreamSynchronize(s));
+    }
+    // merged arenas
+    std::vector<AddDesc> ad(n, AddDesc{});
+    M->desc.assign(n, DecodeDesc{});
+    uint64_t in = 0, lz = 0, ar = 0, ops = 0, ent = 0, poff = 0, par = 0, content = 0, lv = 0, ag = 0, ver = 0, scr = 0;
+    uint32_t max_f = 1;
+    for (size_t i = 0; i < n; i++) {
+        const DecodeDesc &bd = B->desc[i];
+        const DecodeResult &br = B->res[i];
+        const DecodeResult &r = pr[i];
+        AddDesc &a = ad[i];
+        DecodeDesc &md = M->desc[i];
+        a.skip = br.status != 0 || r.status == DECODE_DEFER || r.n_file_agents > DECODE_MAX_FILE_AGENTS;
+        a.ignore_crc = ignore_crc ? 1u : 0u;
+        a.b_in = bd.in_off; a.b_arun = bd.arun_off; a.b_op = bd.op_off; a.b_ent = bd.ent_off; a.b_poff = bd.poff_off;
+        a.b_par = bd.par_off; a.b_content = bd.content_off; a.b_lv = bd.lv_off; a.b_agent = bd.agent_off; a.b_ver = bd.ver_off;
+        a.b_in_len = bd.in_len;
+        const bool bok = br.status == 0;
+        a.b_n_aruns = bok ? br.n_aruns : 0; a.b_n_ops = bok ? br.n_ops : 0; a.b_n_ent = bok ? br.n_entries : 0;
+        a.b_n_par = bok ? br.n_parents : 0; a.b_n_content = bok ? br.n_content : 0; a.b_n_agents = bok ? br.n_agents : 0;
+        a.b_n_ver = bok ? br.n_version : 0; a.b_n_lv = bok ? uint32_t(br.n_lv) : 0;
+        a.b_complete = bok ? br.content_complete : 1; a.b_ascii = bok ? br.ascii : 1;
+        a.b_doc_id_off = br.doc_id_off; a.b_doc_id_len = bok ? br.doc_id_len : 0xFFFFFFFFu;
+        a.p_off = pd[i].in_off;
+        a.p_len = uint32_t(lens[i]);
+        a.p_rel = uint32_t(align256(uint64_t(bd.in_len) + 256));
+        a.m_in = in;
+        in = align256(in + a.p_rel + a.p_len + 256);
+        a.lz_off = lz; a.lz_cap = r.lz_len;
+        lz = align256(lz + r.lz_len + 256);
+        // pieces: records split at the resident's run boundaries
+        const uint64_t pieces = uint64_t(r.raw_aruns) + 2ull * a.b_n_aruns + 1;
+        a.c_vm = uint32_t(pieces);
+        a.c_pre = uint32_t(1 + r.tp_bytes + r.cik_bytes + pieces);
+        a.c_arun = uint32_t(a.b_n_aruns + pieces);
+        a.c_ent = uint32_t(a.b_n_ent + r.hist_bytes / 2 + 1 + pieces);
+        a.c_par = uint32_t(a.b_n_par + r.hist_bytes + pieces);
+        a.c_op = uint32_t(a.b_n_ops + a.c_pre + a.c_ent);
+        a.c_content = uint32_t(std::min<uint64_t>(uint64_t(a.b_n_content) + a.p_len + r.lz_len, 0xFFFFFFFFull));
+        a.c_lv = uint32_t(std::min<uint64_t>(uint64_t(a.b_n_lv) + r.n_lv, 0xFFFFFFFFull));
+        a.c_agent = a.b_n_agents + r.n_file_agents;
+        a.m_arun = ar; ar += a.c_arun;
+        a.m_op = ops; ops += a.c_op;
+        a.m_ent = ent; ent += a.c_ent;
+        a.m_poff = poff; poff += a.c_ent + 1;
+        a.m_par = par; par += a.c_par;
+        a.m_content = content; content += a.c_content;
+        a.m_lv = lv; lv += a.c_lv;
+        a.m_agent = ag; ag += a.c_agent;
+        a.m_ver = ver; ver += DECODE_MAX_FRONTIER;
+        a.m_scr = scr; scr += uint64_t(a.c_pre) + a.c_vm;
+        if (!a.skip) max_f = std::max(max_f, r.n_file_agents);
+        md.in_off = a.m_in; md.in_len = a.p_rel + a.p_len;
+        md.arun_off = a.m_arun; md.op_off = a.m_op; md.ent_off = a.m_ent; md.poff_off = a.m_poff; md.par_off = a.m_par;
+        md.content_off = a.m_content; md.lv_off = a.m_lv; md.agent_off = a.m_agent; md.ver_off = a.m_ver;
+        md.arun_cap = a.c_arun; md.op_cap = a.c_op; md.ent_cap = a.c_ent; md.par_cap = a.c_par;
+        md.content_cap = a.c_content; md.lv_cap = a.c_lv; md.agent_cap = a.c_agent;
+    }
+    CK(M->in.alloc(in)); CK(M->lz.alloc(lz)); CK(M->aruns.alloc(4 * ar)); CK(M->ops.alloc(4 * ops));
+    CK(M->ent.alloc(2 * ent)); CK(M->poff.alloc(poff)); CK(M->par.alloc(par)); CK(M->content.alloc(content));
+    CK(M->cbyte.alloc(lv)); CK(M->agents.alloc(2 * ag)); CK(M->ver.alloc(ver)); CK(M->ffr.alloc(ver));
+    DevBuf<uint32_t> d_scr;
+    CK(d_scr.alloc(4 * scr));
+    DevBuf<AddDesc> d_ad;
+    CK(d_ad.upload(ad, s));
+    CK(M->d_res.alloc(n));
+    AddParams A{};
+    A.b_in = B->in.p; A.b_content = B->content.p; A.p_in = pin.p;
+    A.b_aruns = B->aruns.p; A.b_ops = B->ops.p; A.b_ent = B->ent.p; A.b_poff = B->poff.p; A.b_par = B->par.p;
+    A.b_cbyte = B->cbyte.p; A.b_agents = B->agents.p; A.b_ver = B->ver.p;
+    A.m_in = M->in.p; A.lz = M->lz.p; A.m_content = M->content.p;
+    A.m_aruns = M->aruns.p; A.m_ops = M->ops.p; A.m_ent = M->ent.p; A.m_poff = M->poff.p; A.m_par = M->par.p;
+    A.m_cbyte = M->cbyte.p; A.m_agents = M->agents.p; A.m_ver = M->ver.p; A.m_ffr = M->ffr.p; A.scr = d_scr.p;
+    A.docs = d_ad.p; A.results = M->d_res.p; A.n_docs = uint32_t(n); A.max_file_agents = max_f;
+    A.x2n[0] = 1u << 30;
+    for (int k = 1; k < 32; k++) A.x2n[k] = multmodp_host(A.x2n[k - 1], A.x2n[k - 1]);
+    CK(hipEventRecord(M->ev0, s));
+    if (launch_decode_add(A, s)) return DTGPU_ERR_HIP;
+    CK(hipEventRecord(M->ev1, s));
+    M->res.assign(n, DecodeResult{});
+    CK(hipMemcpyAsync(M->res.data(), M->d_res.p, n * sizeof(DecodeResult), hipMemcpyDeviceToHost, s));
+    CK(hipStreamSynchronize(s));
+    float t = 0;
+    CK(hipEventElapsedTime(&t, M->ev0, M->ev1));
+    M->last_ms = t;
+    if (ms) *ms = t;
+#undef CK
+    // each merged document is valid (the resident one again after a failed merge); the merge's
+    // own status is kept apart
+    M->add_status.assign(n, 0);
+    for (size_t i = 0; i < n; i++) {
+        M->add_status[i] = M->res[i].status;
+        M->res[i].status = B->res[i].status;
+    }
+    *out = guard.release();
+    return DTGPU_OK;
+}
+
+dtgpu_status dtgpu_decode_add_result(const dtgpu_decoded *M, size_t i, uint64_t *frontier, size_t cap,
+                                     size_t *n_frontier) {
+    if (!M || !M->merged || i >= M->n || (!frontier && cap)) return DTGPU_ERR_ARG;
+    const uint32_t st = M->add_status[i];
+    const size_t k = st == 0 ? M->res[i].n_file_frontier : 0;
+    if (n_frontier) *n_frontier = k;
+    if (k && cap) {
+        std::vector<uint32_t> f(k);
+        if (hipMemcpy(f.data(), M->ffr.p + M->desc[i].ver_off, k * 4, hipMemcpyDeviceToHost) != hipSuccess)
+            return DTGPU_ERR_HIP;
+        for (size_t j = 0; j < k && j < cap; j++) frontier[j] = f[j];
+    }
+    return dtgpu_status(st);
 }
 
 size_t dtgpu_decode_size(const dtgpu_decoded *D) { return D ? D->n : 0; }
@@ -209,6 +373,18 @@ size_t dtgpu_decode_export(const dtgpu_decoded *D, size_t i, int what, void *out
             for (uint32_t a = 0; a < r.n_agents; a++) {
                 blob.push_back(uint8_t(pairs[2 * a + 1]));
                 blob.insert(blob.end(), doc.begin() + pairs[2 * a], doc.begin() + pairs[2 * a] + pairs[2 * a + 1]);
+            }
+            if (out) std::memcpy(out, blob.data(), std::min(cap, blob.size()));
+            return blob.size();
+        }
+        case DTGPU_EXPORT_DOC_ID: {
+            std::vector<uint8_t> blob(1, 0);
+            if (r.doc_id_len != 0xFFFFFFFFu) {
+                blob[0] = 1;
+                blob.resize(1 + r.doc_id_len);
+                if (r.doc_id_len &&
+                    hipMemcpy(blob.data() + 1, D->in.p + d.in_off + r.doc_id_off, r.doc_id_len, hipMemcpyDeviceToHost) != hipSuccess)
+                    return 0;
             }
             if (out) std::memcpy(out, blob.data(), std::min(cap, blob.size()));
             return blob.size();

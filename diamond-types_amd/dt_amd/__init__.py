@@ -174,6 +174,10 @@ def lib():
     L.dtgpu_decode_last_ms.restype = ctypes.c_float
     L.dtgpu_decode_free.argtypes = [vp]
     L.dtgpu_decode_profile.argtypes = [vp, sz, ctypes.POINTER(ctypes.c_uint32)]
+    L.dtgpu_decode_add.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz), sz, c,
+                                   ctypes.POINTER(ctypes.c_float), ctypes.POINTER(vp)]
+    L.dtgpu_decode_add_result.argtypes = [vp, sz, pu64, sz, ctypes.POINTER(sz)]
+    L.dtgpu_batch_create_decoded.argtypes = [vp, ctypes.POINTER(vp)]
     L.dtgpu_graph_queries.argtypes = [ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(sz), sz,
                                       ctypes.POINTER(GraphQuery), sz, ctypes.POINTER(ctypes.c_int64), sz,
                                       ctypes.POINTER(GraphAnswer), ctypes.POINTER(ctypes.c_float)]
@@ -562,6 +566,7 @@ EXPORTS = {
     "ops": (0, "<u4", 4), "agent_runs": (1, "<u4", 4), "entries": (2, "<u4", 2),
     "parent_offsets": (3, "<u4", 1), "parents": (4, "<u4", 1), "content": (5, "u1", 1),
     "char_offsets": (6, "<u4", 1), "version": (7, "<u4", 1), "agent_names": (8, "u1", 1),
+    "doc_id": (9, "u1", 1),
 }
 DECODE_DEFER = 80
 
@@ -787,6 +792,42 @@ class DecodeBatch:
     def export(self, i, what):
         a = _export(lambda c, p, n: lib().dtgpu_decode_export(self._h, i, c, p, n), what)
         return _names(a) if what == "agent_names" else a
+
+    def doc_id(self, i):
+        a = bytes(self.export(i, "doc_id"))
+        return a[1:].decode() if a and a[0] else None
+
+    def add(self, patches, ignore_crc=False):
+        """ListOpLog::decode_and_add of patches[i] into document i, on the GPU (dtgpu_decode_add):
+        a new DecodeBatch of the merged oplogs (this one is unchanged).  Per-document outcome:
+        add_result(i)."""
+        n = len(patches)
+        keep = [bytes(p) for p in patches]
+        arr = (ctypes.c_char_p * max(n, 1))(*keep)
+        lens = (ctypes.c_size_t * max(n, 1))(*[len(p) for p in keep])
+        ms = ctypes.c_float()
+        h = ctypes.c_void_p()
+        _check(lib().dtgpu_decode_add(self._h, arr, lens, n, int(ignore_crc), ctypes.byref(ms), ctypes.byref(h)))
+        m = DecodeBatch.__new__(DecodeBatch)
+        m._h, m.n, m._keep, m.last_ms = h, n, keep, ms.value
+        return m
+
+    def add_result(self, i):
+        """(status, the patch's version): decode_and_add's Result for document i of a merged batch."""
+        k = ctypes.c_size_t()
+        buf = (ctypes.c_uint64 * 64)()
+        st = lib().dtgpu_decode_add_result(self._h, i, buf, 64, ctypes.byref(k))
+        return st, list(buf[:k.value])
+
+    def checkout_batch(self):
+        """A device-staged checkout Batch over these decoded (or merged) oplogs; consumes this
+        handle (dtgpu_batch_create_decoded)."""
+        h, self._h = self._h, None
+        b = Batch.__new__(Batch)
+        out = ctypes.c_void_p()
+        _check(lib().dtgpu_batch_create_decoded(h, ctypes.byref(out)))
+        b._h, b.n, b._keep = out.value, self.n, None
+        return b
 
     def profile(self, i):
         out = (ctypes.c_uint32 * 8)()

@@ -359,6 +359,25 @@ dtgpu_status dtgpu_decode_profile(const dtgpu_decoded *dec, size_t i, uint32_t o
 uint64_t dtgpu_decode_bytes(const dtgpu_decoded *dec, int which);
 void dtgpu_decode_free(dtgpu_decoded *dec);
 
+/* ListOpLog::decode_and_add_opts (src/list/encoding/decode_oplog.rs:476-583, with decode_internal's
+ * overlap filter :670-913) for a batch on the GPU: patch i (any `.dt` file or encode_from patch) is
+ * merged into decoded document i of `base` (after dtgpu_decode_run, or a previous dtgpu_decode_add)
+ * by one wavefront per document (dt_decode.hip decode_add_kernel).  The merged oplogs form a new
+ * handle (base is unchanged): its arrays equal what dtgpu_oplog_decode_and_add leaves in a host
+ * oplog, element for element; a document whose merge fails is the resident document again (the
+ * reference's unwind).  *ms = the merge kernel's time.  Per-document outcome and the patch's
+ * version (decode_and_add's return value): dtgpu_decode_add_result, which returns the document's
+ * status (DTGPU_DECODE_DEFER: a case for the host's dtgpu_oplog_decode_and_add, as in
+ * dtgpu_decode_create).  A merged handle checks out on the device with dtgpu_batch_create_decoded;
+ * it cannot be re-decoded (dtgpu_decode_run returns DTGPU_ERR_ARG). */
+dtgpu_status dtgpu_decode_add(const dtgpu_decoded *base, const uint8_t *const *patches, const size_t *lens,
+                              size_t n, int ignore_crc, float *ms, dtgpu_decoded **out);
+dtgpu_status dtgpu_decode_add_result(const dtgpu_decoded *merged, size_t i, uint64_t *frontier, size_t cap,
+                                     size_t *n_frontier);
+/* A device-staged checkout batch over a decoded handle (consumed, also on failure): decoded here
+ * unless it already holds merged oplogs; then as dtgpu_batch_create_device. */
+dtgpu_status dtgpu_batch_create_decoded(dtgpu_decoded *dec, dtgpu_batch **out);
+
 /* Decoded-oplog arrays, the same layouts from the device decoder and from a host oplog.
  * Returns the element count (bytes for CONTENT / AGENT_NAMES) and copies min(cap, count). */
 typedef enum dtgpu_export {
@@ -371,6 +390,7 @@ typedef enum dtgpu_export {
     DTGPU_EXPORT_CHAR_OFFSETS = 6,   /* u32 per LV: byte offset of an inserted char, else ~0 */
     DTGPU_EXPORT_VERSION = 7,        /* u32: the frontier */
     DTGPU_EXPORT_AGENT_NAMES = 8,    /* per agent id: u8 length + name bytes */
+    DTGPU_EXPORT_DOC_ID = 9,         /* bytes: 1 + the doc id, or 0 when there is none */
 } dtgpu_export;
 size_t dtgpu_decode_export(const dtgpu_decoded *dec, size_t i, int what, void *out, size_t cap);
 size_t dtgpu_oplog_export(const dtgpu_oplog *oplog, int what, void *out, size_t cap);
