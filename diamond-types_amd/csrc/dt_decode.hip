@@ -2638,7 +2638,7 @@ __device__ __forceinline__ void add_copy_base(const AddParams &P, const AddDesc 
 }
 
 #ifndef DTGPU_ADD_WAVES
-#define DTGPU_ADD_WAVES 2   // 231 VGPRs, no VGPR spills (4: 218 spilled, 3.6x slower)
+#define DTGPU_ADD_WAVES 2   // 231 VGPRs, no VGPR spills (4: 218 spilled, 1.5x slower)
 #endif
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_ADD_WAVES))) void decode_add_kernel(AddParams P) {
     extern __shared__ uint32_t lds[];

@@ -164,16 +164,20 @@ struct PlanParams {
 int launch_plan(const PlanParams &q, void *stream);
 
 // One replay pass: the LDS tiers (index in LDS, sized per tier) and then the HBM-index tier,
-// which also replays the LDS-tier documents that outgrew their LDS capacity.  The two biggest
-// LDS tiers (few, long documents) run on `side`, forked from and joined back into `stream`,
-// beside the small ones; every list indexes docs[].
+// which also replays the LDS-tier documents that outgrew their LDS capacity.  A tier kernel
+// lasts as long as its longest replay, so tiers queued on one stream add up: the biggest tiers
+// (few, long documents) each run on a side stream of their own, forked from and joined back
+// into `stream`, beside the smallest tier; every list indexes docs[].
 constexpr int kMaxLdsTiers = 4;
+constexpr int kSideStreams = kMaxLdsTiers - 1;
 struct ReplayLaunch {
     const BatchParams *lds;   // n_lds LDS tiers, smallest index first
     int n_lds;
     const BatchParams *large;
-    void *stream, *side;      // hipStream_t
-    void *ev_fork, *ev_join;  // hipEvent_t
+    void *stream;                   // hipStream_t
+    void *side[kSideStreams];       // hipStream_t: tier n_lds - 1 - k on side[k]
+    void *ev_fork;                  // hipEvent_t
+    void *ev_join[kSideStreams];    // hipEvent_t
 };
 int launch_replay(const ReplayLaunch &r);
 // The same pass on the span tracker (dt_span.hip): BatchParams.rows holds the span blocks,

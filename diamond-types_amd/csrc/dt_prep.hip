@@ -374,27 +374,49 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
                           h1 ? pch[p0 + 1] : 0u);
         r[4] = make_uint4(h1 ? pcnt[p0 + 1] : 0u, nc ? child[c0 + nc - 1] : 0xFFFFFFFFu, nc ? child[c0] : 0xFFFFFFFFu, 0u);
     }
-    // op runs: apply commands and the dense chain tables (LV | is_del per chain seq)
+    // op runs: apply commands and the dense chain tables (LV | is_del per chain seq), one op run
+    // per lane -- per entry, a history of few long entries (node_nodecc: 91 entries, 53k runs)
+    // would leave most lanes idle behind one entry's runs.  A run's entry is the last entry whose
+    // first run is at or below it: searched among the 64 entries from the previous chunk's last
+    // run's entry in registers, by bisection past that window.
     uint32_t n_ins = 0;
-    for (uint32_t i = l; i < ne; i += 64) {
-        const uint32_t e0 = ent[i].x, j1 = eop[i + 1];
-        const uint2 q = cs[i];
-        const uint32_t d0 = doff[q.x] + q.y + e0;   // seq0 + chain offset
-        for (uint32_t j = eop[i]; j < j1; j++) {
-            const uint4 o = ops[j];   // lv, len, pos, kind | fwd << 1
-            const bool del = o.w & 1u;
-            opc[j] = Cmd{del ? (CMD_DEL | ((o.w & 2u) ? 16u : 0u)) : uint32_t(CMD_INS), o.x, o.y, o.z};
-            if (!del) n_ins += o.y;
-            // the run's dense slots: 16-byte stores between a scalar head and tail
-            const uint32_t flag = del ? TL_DEL : 0u;
-            uint32_t *dp = dense + uint32_t(d0 + (o.x - e0));
-            uint32_t v = 0;
-            for (; v < o.y && (reinterpret_cast<uintptr_t>(dp + v) & 15u); v++) dp[v] = (o.x + v) | flag;
-            for (; v + 4 <= o.y; v += 4) {
-                const uint32_t b = o.x + v;
-                *reinterpret_cast<uint4 *>(dp + v) = make_uint4(b | flag, (b + 1) | flag, (b + 2) | flag, (b + 3) | flag);
+    {
+        uint32_t ebase = 0;
+        for (uint32_t j0 = 0; j0 < nops; j0 += 64) {
+            const uint32_t j = j0 + l;
+            const bool live = j < nops;
+            const uint32_t we = ebase + l < ne ? eop[ebase + l + 1] : 0xFFFFFFFFu;   // end of entry ebase + l
+            uint32_t c = 0;
+#pragma unroll
+            for (uint32_t st = 32; st >= 1; st >>= 1)
+                if (uint32_t(__shfl(int(we), int(c + st - 1))) <= j) c += st;
+            if (c == 63 && rdl(we, 63) <= j) c = 64;
+            uint32_t lo = ebase + c, hi = live && c == 64 ? ne : lo;
+            while (lo < hi) {   // past the window: first entry whose end is above j
+                const uint32_t mid = (lo + hi) >> 1;
+                if (eop[mid + 1] <= j) lo = mid + 1; else hi = mid;
             }
-            for (; v < o.y; v++) dp[v] = (o.x + v) | flag;
+            const uint32_t i = lo;
+            if (live) {
+                const uint32_t e0 = ent[i].x;
+                const uint2 q = cs[i];
+                const uint32_t d0 = doff[q.x] + q.y + e0;   // seq0 + chain offset
+                const uint4 o = ops[j];   // lv, len, pos, kind | fwd << 1
+                const bool del = o.w & 1u;
+                opc[j] = Cmd{del ? (CMD_DEL | ((o.w & 2u) ? 16u : 0u)) : uint32_t(CMD_INS), o.x, o.y, o.z};
+                if (!del) n_ins += o.y;
+                // the run's dense slots: 16-byte stores between a scalar head and tail
+                const uint32_t flag = del ? TL_DEL : 0u;
+                uint32_t *dp = dense + uint32_t(d0 + (o.x - e0));
+                uint32_t v = 0;
+                for (; v < o.y && (reinterpret_cast<uintptr_t>(dp + v) & 15u); v++) dp[v] = (o.x + v) | flag;
+                for (; v + 4 <= o.y; v += 4) {
+                    const uint32_t b = o.x + v;
+                    *reinterpret_cast<uint4 *>(dp + v) = make_uint4(b | flag, (b + 1) | flag, (b + 2) | flag, (b + 3) | flag);
+                }
+                for (; v < o.y; v++) dp[v] = (o.x + v) | flag;
+            }
+            ebase = rdl(i, min(nops - 1 - j0, 63u));
         }
     }
 #ifdef DTGPU_PREP_PROF

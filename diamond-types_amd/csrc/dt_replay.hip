@@ -1309,7 +1309,6 @@ static int launch_lds_tier(const BatchParams &q, hipStream_t s, bool prof) {
 
 int launch_replay(const ReplayLaunch &r) {
     hipStream_t s = reinterpret_cast<hipStream_t>(r.stream);
-    hipStream_t side = reinterpret_cast<hipStream_t>(r.side);
     const BatchParams &large = *r.large;
     bool prof = large.debug & 2u;
     uint32_t n_lds = 0;
@@ -1321,23 +1320,28 @@ int launch_replay(const ReplayLaunch &r) {
     }
     if (n_lds) {
         if (fb_count && hipMemsetAsync(const_cast<uint32_t *>(fb_count), 0, sizeof(uint32_t), s) != hipSuccess) return ErrHip;
-        // fork: the two biggest tiers (few documents, long replays) start first, on the side
-        // stream; the small tiers fill the rest of the chip on the main stream
-        const int split = r.n_lds > 2 ? r.n_lds - 2 : r.n_lds;
-        const bool fork = side && r.ev_fork && r.ev_join && split < r.n_lds;
+        // fork: the biggest tiers start first, each on its own side stream; the smallest tier
+        // runs on the main stream
+        int n_side = 0;
+        while (n_side < kSideStreams && n_side < r.n_lds - 1 && r.side[n_side] && r.ev_join[n_side]) n_side++;
+        const bool fork = n_side > 0 && r.ev_fork;
         if (fork) {
-            if (hipEventRecord(reinterpret_cast<hipEvent_t>(r.ev_fork), s) != hipSuccess ||
-                hipStreamWaitEvent(side, reinterpret_cast<hipEvent_t>(r.ev_fork), 0) != hipSuccess)
-                return ErrHip;
+            if (hipEventRecord(reinterpret_cast<hipEvent_t>(r.ev_fork), s) != hipSuccess) return ErrHip;
+            for (int k = 0; k < n_side; k++)
+                if (hipStreamWaitEvent(reinterpret_cast<hipStream_t>(r.side[k]), reinterpret_cast<hipEvent_t>(r.ev_fork), 0) !=
+                    hipSuccess)
+                    return ErrHip;
         }
         for (int t = r.n_lds - 1; t >= 0; t--) {
-            const int e = launch_lds_tier(r.lds[t], (fork && t >= split) ? side : s, prof);
+            const int k = r.n_lds - 1 - t;
+            const int e = launch_lds_tier(r.lds[t], (fork && k < n_side) ? reinterpret_cast<hipStream_t>(r.side[k]) : s, prof);
             if (e) return e;
         }
         if (fork) {
-            if (hipEventRecord(reinterpret_cast<hipEvent_t>(r.ev_join), side) != hipSuccess ||
-                hipStreamWaitEvent(s, reinterpret_cast<hipEvent_t>(r.ev_join), 0) != hipSuccess)
-                return ErrHip;
+            for (int k = 0; k < n_side; k++)
+                if (hipEventRecord(reinterpret_cast<hipEvent_t>(r.ev_join[k]), reinterpret_cast<hipStream_t>(r.side[k])) != hipSuccess ||
+                    hipStreamWaitEvent(s, reinterpret_cast<hipEvent_t>(r.ev_join[k]), 0) != hipSuccess)
+                    return ErrHip;
         }
     }
     // HBM tier: its own list plus a slot per LDS-tier document that may be handed back

@@ -89,8 +89,8 @@ struct dtgpu_batch {
     std::vector<uint8_t> host_planned;   // 0: device-planned; else why the host planned it
     uint32_t tier_blocks[kLdsTiers] = {};
     uint32_t debug = 0;
-    hipStream_t side = nullptr;          // big LDS tiers run beside the small ones
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipStream_t side[kSideStreams] = {};   // big LDS tiers run beside the small ones, one stream each
+    hipEvent_t ev_fork = nullptr, ev_join[kSideStreams] = {};
     uint64_t alg_in_bytes = 0, total_lv = 0;
     float last_plan_ms = 0, last_replay_ms = 0;
 
@@ -142,8 +142,10 @@ struct dtgpu_batch {
         if (ev_mid) (void)hipEventDestroy(ev_mid);
         if (ev1) (void)hipEventDestroy(ev1);
         if (ev_fork) (void)hipEventDestroy(ev_fork);
-        if (ev_join) (void)hipEventDestroy(ev_join);
-        if (side) (void)hipStreamDestroy(side);
+        for (int k = 0; k < kSideStreams; k++) {
+            if (ev_join[k]) (void)hipEventDestroy(ev_join[k]);
+            if (side[k]) (void)hipStreamDestroy(side[k]);
+        }
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -229,9 +231,11 @@ dtgpu_status set_tier_params(dtgpu_batch &B, const BatchParams &base) {
         B.large.fb_slots = uint32_t(off);   // every LDS-tier document may be handed back
     }
     B.debug = base.debug;
-    if (!B.side && hipStreamCreateWithFlags(&B.side, hipStreamNonBlocking) != hipSuccess) return DTGPU_ERR_HIP;
     if (!B.ev_fork && hipEventCreateWithFlags(&B.ev_fork, hipEventDisableTiming) != hipSuccess) return DTGPU_ERR_HIP;
-    if (!B.ev_join && hipEventCreateWithFlags(&B.ev_join, hipEventDisableTiming) != hipSuccess) return DTGPU_ERR_HIP;
+    for (int k = 0; k < kSideStreams; k++) {
+        if (!B.side[k] && hipStreamCreateWithFlags(&B.side[k], hipStreamNonBlocking) != hipSuccess) return DTGPU_ERR_HIP;
+        if (!B.ev_join[k] && hipEventCreateWithFlags(&B.ev_join[k], hipEventDisableTiming) != hipSuccess) return DTGPU_ERR_HIP;
+    }
     return DTGPU_OK;
 }
 int replay_all(dtgpu_batch *B, hipStream_t s) {
@@ -240,9 +244,8 @@ int replay_all(dtgpu_batch *B, hipStream_t s) {
     r.n_lds = kLdsTiers;
     r.large = &B->large;
     r.stream = s;
-    r.side = B->side;
+    for (int k = 0; k < kSideStreams; k++) { r.side[k] = B->side[k]; r.ev_join[k] = B->ev_join[k]; }
     r.ev_fork = B->ev_fork;
-    r.ev_join = B->ev_join;
     return B->item_mode ? launch_replay(r) : launch_span_replay(r);
 }
 
