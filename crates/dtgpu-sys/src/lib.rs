@@ -14,6 +14,10 @@ pub struct dtgpu_batch {
     _p: [u8; 0],
 }
 #[repr(C)]
+pub struct dtgpu_decoded {
+    _p: [u8; 0],
+}
+#[repr(C)]
 #[derive(Default, Clone, Copy, Debug)]
 pub struct dtgpu_doc_result {
     pub status: u32,
@@ -85,6 +89,16 @@ extern "C" {
     pub fn dtgpu_batch_checkout(docs: *const *const u8, lens: *const usize, n_docs: usize, opts: *const dtgpu_batch_opts,
                                 results: *mut dtgpu_doc_result) -> dtgpu_status;
     pub fn dtgpu_text_hash(text: *const u8, len: usize) -> u64;
+    // batched load_from / decode_and_add on the GPU (decode_oplog.rs:447-960, 476-583)
+    pub fn dtgpu_decode_create(docs: *const *const u8, lens: *const usize, n: usize, opts: *const dtgpu_batch_opts,
+                               out: *mut *mut dtgpu_decoded) -> dtgpu_status;
+    pub fn dtgpu_decode_run(dec: *mut dtgpu_decoded, ms: *mut f32) -> dtgpu_status;
+    pub fn dtgpu_decode_free(dec: *mut dtgpu_decoded);
+    pub fn dtgpu_decode_add(base: *const dtgpu_decoded, patches: *const *const u8, lens: *const usize, n: usize,
+                            ignore_crc: c_int, ms: *mut f32, out: *mut *mut dtgpu_decoded) -> dtgpu_status;
+    pub fn dtgpu_decode_add_result(merged: *const dtgpu_decoded, i: usize, frontier: *mut u64, cap: usize,
+                                   n_frontier: *mut usize) -> dtgpu_status;
+    pub fn dtgpu_batch_create_decoded(dec: *mut dtgpu_decoded, out: *mut *mut dtgpu_batch) -> dtgpu_status;
     pub fn dtgpu_device_count() -> c_int;
 }
 
@@ -185,4 +199,65 @@ pub fn batch_checkout(docs: &[&[u8]], device: i32) -> Result<Vec<dtgpu_doc_resul
     let mut res = vec![dtgpu_doc_result::default(); docs.len()];
     let s = unsafe { dtgpu_batch_checkout(ptrs.as_ptr(), lens.as_ptr(), docs.len(), &opts, res.as_mut_ptr()) };
     if s != DTGPU_OK { Err(s) } else { Ok(res) }
+}
+
+/// Many `ListOpLog::load_from(doc)` at once, decoded into HBM (dtgpu_decode_*); `add` merges one
+/// patch per document on the GPU (`decode_and_add`), `checkout` checks the oplogs out in place.
+pub struct DecodedBatch {
+    h: *mut dtgpu_decoded,
+    n: usize,
+}
+
+impl DecodedBatch {
+    pub fn load(docs: &[&[u8]], device: i32) -> Result<DecodedBatch, i32> {
+        let ptrs: Vec<*const u8> = docs.iter().map(|d| d.as_ptr()).collect();
+        let lens: Vec<usize> = docs.iter().map(|d| d.len()).collect();
+        let opts = dtgpu_batch_opts { ignore_crc: 0, host_threads: 0, device };
+        let mut h = std::ptr::null_mut();
+        let s = unsafe { dtgpu_decode_create(ptrs.as_ptr(), lens.as_ptr(), docs.len(), &opts, &mut h) };
+        if s != DTGPU_OK { return Err(s); }
+        let b = DecodedBatch { h, n: docs.len() };
+        let s = unsafe { dtgpu_decode_run(b.h, std::ptr::null_mut()) };
+        if s != DTGPU_OK { Err(s) } else { Ok(b) }
+    }
+    /// `decode_and_add(patches[i])` into document i; per document `Result<Frontier, ParseError>`.
+    pub fn add(&self, patches: &[&[u8]]) -> Result<(DecodedBatch, Vec<Result<Vec<u64>, i32>>), i32> {
+        let ptrs: Vec<*const u8> = patches.iter().map(|d| d.as_ptr()).collect();
+        let lens: Vec<usize> = patches.iter().map(|d| d.len()).collect();
+        let mut h = std::ptr::null_mut();
+        let s = unsafe { dtgpu_decode_add(self.h, ptrs.as_ptr(), lens.as_ptr(), patches.len(), 0, std::ptr::null_mut(), &mut h) };
+        if s != DTGPU_OK { return Err(s); }
+        let m = DecodedBatch { h, n: self.n };
+        let mut out = Vec::with_capacity(m.n);
+        for i in 0..m.n {
+            let mut f = vec![0u64; 64];
+            let mut k = 0usize;
+            let s = unsafe { dtgpu_decode_add_result(m.h, i, f.as_mut_ptr(), f.len(), &mut k) };
+            f.truncate(k);
+            out.push(if s == DTGPU_OK { Ok(f) } else { Err(s) });
+        }
+        Ok((m, out))
+    }
+    /// checkout_tip of every document on the GPU (consumes the decoded oplogs).
+    pub fn checkout(mut self) -> Result<Vec<dtgpu_doc_result>, i32> {
+        let mut b = std::ptr::null_mut();
+        let s = unsafe { dtgpu_batch_create_decoded(self.h, &mut b) };
+        self.h = std::ptr::null_mut();
+        if s != DTGPU_OK { return Err(s); }
+        let mut res = vec![dtgpu_doc_result::default(); self.n];
+        let s = unsafe {
+            let s = dtgpu_batch_run(b, std::ptr::null_mut());
+            let s = if s == DTGPU_OK { dtgpu_batch_sync(b) } else { s };
+            let s = if s == DTGPU_OK { dtgpu_batch_results(b, res.as_mut_ptr()) } else { s };
+            dtgpu_batch_free(b);
+            s
+        };
+        if s != DTGPU_OK { Err(s) } else { Ok(res) }
+    }
+}
+
+impl Drop for DecodedBatch {
+    fn drop(&mut self) {
+        if !self.h.is_null() { unsafe { dtgpu_decode_free(self.h) } }
+    }
 }
