@@ -1239,8 +1239,11 @@ DEV void bind_index(Doc &D, uint8_t *base, uint32_t mb, uint32_t ms, bool narrow
 
 // One 64-lane workgroup per document of the list (the hardware dispatcher is the work queue;
 // LDS per workgroup bounds how many documents share a CU).
+#ifndef DTGPU_REPLAY_WAVES
+#define DTGPU_REPLAY_WAVES 1   // occupancy floor for the compiler's register budget (tuning knob)
+#endif
 template <bool LDS_INDEX, bool PROF, bool XF>
-__global__ __launch_bounds__(64) void replay_kernel(BatchParams P) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_REPLAY_WAVES))) void replay_kernel(BatchParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t di = U(blockIdx.x);
     uint32_t d;
