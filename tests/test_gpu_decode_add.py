@@ -213,3 +213,51 @@ def test_merged_benchmark_files_check_out():
     b.run()
     for i, t in enumerate(want):
         assert b.text(i) == t, i
+
+
+def test_chained_merges_rebuild_the_history():
+    """A history delivered as a chain of patches (encode_from at increasing versions), each merged
+    into the previous merge's output on the device -- the merged handle is the next base --
+    for several random version chains at once: every link equals the host's oplog after the same
+    sequence of decode_and_add calls, and the last one checks out to the oracle's text."""
+    data = G.dt_bytes("friendsforever")
+    full = dt_amd.ListOpLog.load_from(data)
+    ora = OracleOpLog.load_from(data)
+    rng = random.Random(13)
+    chains = []
+    for _ in range(4):
+        vs = [full.dominators([x]) for x in sorted(rng.sample(range(1, len(full) - 1), 4))] + [full.local_frontier()]
+        parts = [full.history(vs[0]).encode()]
+        parts += [full.history(b).encode_from(a, dt_amd.ENCODE_PATCH) for a, b in zip(vs, vs[1:])]
+        chains.append((vs, parts))
+    hosts = [dt_amd.ListOpLog.load_from(parts[0]) for _, parts in chains]
+    d = dt_amd.DecodeBatch([parts[0] for _, parts in chains])
+    d.run()
+    cur = d
+    for k in range(1, 5):
+        m = cur.add([parts[k] for _, parts in chains])
+        for i, (vs, parts) in enumerate(chains):
+            st, f = m.add_result(i)
+            hf = hosts[i].decode_and_add(parts[k])
+            assert st == 0 and sorted(f) == sorted(hf), (i, k)
+            assert _dev_exact(m, i) == _host_exact(hosts[i]), (i, k)
+        cur = m
+    b = cur.checkout_batch()
+    b.run()
+    want = ora.checkout_tip_bytes()
+    for i in range(len(chains)):
+        assert b.text(i) == want, i
+
+
+def test_random_split_merges_in_random_order():
+    """Hist(v) parts of a git-makefile history at random versions merged into each other in
+    random order (overlap filter everywhere): statuses and arrays equal the host's."""
+    data = G.dt_bytes("git-makefile")
+    full = dt_amd.ListOpLog.load_from(data)
+    rng = random.Random(17)
+    pairs = []
+    for _ in range(8):
+        a, b = (full.dominators([x]) for x in rng.sample(range(1, len(full) - 1), 2))
+        pairs.append((full.history(a).encode(), full.history(b).encode()))
+    _, sts = _check_batch(pairs)
+    assert all(s == 0 for s in sts), sts
