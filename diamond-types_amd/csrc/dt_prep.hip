@@ -254,12 +254,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
         uint32_t bch = 0, bsd = 0;   // chain / seq0 - start of the current 64 entries, flushed per 64
         constexpr uint32_t RING = 8;
         uint64_t keep = 0;   // entries of the current 64 whose row a child beyond the ring reads
-        // the last RING entries' parent vectors (one VGPR each) with their chain and seq offset:
-        // a merge's other parent is almost always a few entries back (friendsforever: all within
-        // 7, git-makefile 63 % within 8), so its row comes from registers, not an HBM round trip
-        uint32_t ring_id[RING], ring_row[RING], ring_ch[RING], ring_sd[RING];
-#pragma unroll
-        for (uint32_t j = 0; j < RING; j++) { ring_id[j] = 0xFFFFFFFFu; ring_row[j] = ring_ch[j] = ring_sd[j] = 0; }
+        // the last RING entries' parent vectors with their chain and seq offset, in LDS (the
+        // child-count table's space, free after the scatter), slot = entry mod RING: a merge's
+        // other parent is almost always a few entries back (friendsforever: all within 7,
+        // git-makefile 63 % within 8), so its row is one LDS read, not an HBM round trip (a
+        // register ring costs a compare-and-select chain over every slot per entry)
+        uint32_t *ring_row = lfw;                  // RING x 64 words
+        uint32_t *ring_meta = lfw + RING * 64;     // RING x {entry, chain, seq0 - start}
+        if (l < RING) ring_meta[3 * l] = 0xFFFFFFFFu;
+        __syncthreads();
         for (uint32_t i = 0; i < ne; i++) {
             if ((i & 63u) == 0) {   // a row is stored only for a child more than RING entries on
                 // (children are in index order: the last is the farthest; nearer ones read the
@@ -283,11 +286,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
                 if (pe + 1 == i) {
                     prow = prev_row; pc = prev_chain; psd = prev_sd;
                 } else {
-                    bool hit = false;
+                    const uint32_t slot = pe & (RING - 1);
+                    const bool hit = ring_meta[3 * slot] == pe;
                     prow = pc = psd = 0;
-#pragma unroll
-                    for (uint32_t j = 0; j < RING; j++)
-                        if (ring_id[j] == pe) { prow = ring_row[j]; pc = ring_ch[j]; psd = ring_sd[j]; hit = true; }
+                    if (hit) { prow = ring_row[slot * 64 + l]; pc = ring_meta[3 * slot + 1]; psd = ring_meta[3 * slot + 2]; }
                     if (!hit) {
                         prow = rows[size_t(pe) * PREP_MAX_CHAINS + l];
                         if (pe >= (i & ~63u)) {   // not flushed yet: from the registers
@@ -329,9 +331,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
                 wave_fence();   // later entries read these pairs back from other lanes
             }
             prev_row = row; prev_chain = c; prev_sd = s0 - s;
-#pragma unroll
-            for (uint32_t j = 0; j < RING; j++)
-                if (j == (i & (RING - 1))) { ring_id[j] = i; ring_row[j] = row; ring_ch[j] = c; ring_sd[j] = s0 - s; }
+            {
+                const uint32_t slot = i & (RING - 1);
+                ring_row[slot * 64 + l] = row;
+                if (l == 0) { ring_meta[3 * slot] = i; ring_meta[3 * slot + 1] = c; ring_meta[3 * slot + 2] = s0 - s; }
+            }
         }
     }
     wave_fence();
@@ -475,7 +479,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
 
 int launch_prep(const PrepParams &p, void *stream) {
     if (!p.n_docs) return 0;
-    hipLaunchKernelGGL(prep::prep_kernel, dim3(p.n_docs), dim3(64), ((size_t(p.max_entries) + 1) / 2) * 4,
+    // LDS: the child counts (u16 per entry), later the chain decomposition's ring (8 rows + meta)
+    const size_t cw = (size_t(p.max_entries) + 1) / 2, rw = 8 * 64 + 24;
+    const size_t lds = (cw > rw ? cw : rw) * 4;
+    hipLaunchKernelGGL(prep::prep_kernel, dim3(p.n_docs), dim3(64), lds,
                        reinterpret_cast<hipStream_t>(stream), p);
     return hipGetLastError() == hipSuccess ? 0 : 66;
 }
