@@ -2039,9 +2039,29 @@ __device__ __forceinline__ int add_doc(const AddParams &P, const AddDesc &D, Dec
 
     // AgentAssignment::local_to_agent_version's inverse over the merged agent runs (LV order =
     // each agent's insertion order): the first run holding seq; gap = the next run start above it
+    // Per merged agent (LDS): the end of its seq ranges so far, whether its runs' seq ranges
+    // increase along LV order (then a run holding seq is the only one), and its last hit.  An
+    // agent whose runs increase answers a seq at or past its end without a scan (the overlap
+    // filter's new pieces), and a known one usually from the 64 runs around its last hit.
+    uint32_t *A_end = L.acnt, *A_mono = L.amono, *A_cur = L.acur;
     auto seq_find = [&](uint32_t a, uint64_t seq, uint64_t &lv, uint64_t &gap) -> bool {
         if (dirty) { wave_fence(); dirty = false; }
         gap = ~uint64_t(0);
+        const bool mono = A_mono[a] != 0;
+        if (mono) {
+            if (seq >= A_end[a]) return false;
+            const uint32_t c = A_cur[a], w0 = c >= 16 ? c - 16 : 0;
+            const uint32_t k = w0 + lane();
+            const uint4 r = k < n_aruns ? M.aruns[k] : make_uint4(0, 0, 0xFFFFFFFFu, 0);
+            const uint64_t hm = ballot(r.z == a && r.y != 0 && seq >= r.w && seq < uint64_t(r.w) + r.y);
+            if (hm) {
+                const uint32_t l = ctz(hm);
+                lv = uint64_t(rdl(r.x, l)) + (seq - rdl(r.w, l));
+                gap = uint64_t(rdl(r.w, l)) + rdl(r.y, l);
+                if (lane() == 0) A_cur[a] = w0 + l;
+                return true;
+            }
+        }
         for (uint32_t k0 = 0; k0 < n_aruns; k0 += 64) {
             const uint32_t k = k0 + lane();
             const uint4 r = k < n_aruns ? M.aruns[k] : make_uint4(0, 0, 0xFFFFFFFFu, 0);
@@ -2051,6 +2071,7 @@ __device__ __forceinline__ int add_doc(const AddParams &P, const AddDesc &D, Dec
                 const uint32_t l = ctz(hm);
                 lv = uint64_t(rdl(r.x, l)) + (seq - rdl(r.w, l));
                 gap = uint64_t(rdl(r.w, l)) + rdl(r.y, l);   // the run's end (seq)
+                if (mono && lane() == 0) A_cur[a] = k0 + l;
                 return true;
             }
             uint64_t g = mine && r.w > seq ? uint64_t(r.w) : ~uint64_t(0);
@@ -2069,6 +2090,11 @@ __device__ __forceinline__ int add_doc(const AddParams &P, const AddDesc &D, Dec
     };
     // cg.assign (agent_runs RLE, agent_assignment/mod.rs)
     auto assign = [&](uint32_t agent, uint32_t seq, uint32_t lv, uint32_t ln) -> int {
+        if (lane() == 0) {
+            const uint32_t e = A_end[agent];
+            if (seq < e) A_mono[agent] = 0;
+            A_end[agent] = max(e, seq + ln);
+        }
         if (n_aruns && la_agent == agent && la_lv + la_len == lv && la_seq + la_len == seq) {
             la_len += ln;
             if (lane() == 0) M.aruns[n_aruns - 1].y = la_len;
@@ -2116,6 +2142,38 @@ __device__ __forceinline__ int add_doc(const AddParams &P, const AddDesc &D, Dec
         cr_valid = 0;
         return S_OK;
     };
+
+    // the per-agent tables from the resident's runs: agents one round at a time per 64 runs
+    // (runs of one agent in LV order), each run checked against the end of the agent's previous
+    for (uint32_t a = lane(); a < D.c_agent; a += 64) { A_end[a] = 0; A_mono[a] = 1; A_cur[a] = 0; }
+    __syncthreads();
+    for (uint32_t k0 = 0; k0 < n_aruns; k0 += 64) {
+        const uint32_t k = k0 + lane();
+        const uint4 r = k < n_aruns ? M.aruns[k] : make_uint4(0, 0, 0xFFFFFFFFu, 0);
+        const uint32_t end = r.w + r.y;
+        bool todo = k < n_aruns && r.y != 0;
+        while (ballot(todo)) {
+            const uint32_t lead = rdl(todo ? r.z : 0xFFFFFFFFu, ctz(ballot(todo)));
+            const bool mine = todo && r.z == lead;
+            const uint64_t m = ballot(mine);
+            const uint64_t below = m & lt_mask();
+            const uint32_t src = below ? 63u - uint32_t(__clzll((long long)below)) : lane();
+            const uint32_t prev_end = uint32_t(__shfl(int(end), int(src)));
+            const uint32_t first_end = A_end[lead];
+            const bool bad = mine && r.w < (below ? prev_end : first_end);
+            const uint32_t last = 63u - uint32_t(__clzll((long long)m));
+            const uint32_t last_end = rdl(end, last);
+            const uint64_t anybad = ballot(bad);
+            __syncthreads();
+            if (lane() == 0) {
+                if (anybad) A_mono[lead] = 0;
+                A_end[lead] = max(first_end, last_end);   // increasing runs: the last ends highest
+            }
+            __syncthreads();
+            if (mine) todo = false;
+        }
+    }
+    __syncthreads();
 
     // ---- header, LZ4 --------------------------------------------------------------------------
     if (len < 8) return UnexpectedEOF;
@@ -2652,6 +2710,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_ADD_WA
     L.vq = lds + 320;
     L.fmap = lds + 512;
     L.fseq = L.fmap + F;
+    L.acnt = L.fseq + F;            // per merged agent: seq end,
+    L.amono = L.acnt + P.max_agents;   // runs increase,
+    L.acur = L.amono + P.max_agents;   // last hit
     for (uint32_t i = lane(); i < 256; i += 64) {
         uint32_t c = i;
         for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ CRC_POLY : c >> 1;
@@ -2708,7 +2769,12 @@ int launch_decode(const DecodeParams &p, void *stream) {
 
 int launch_decode_add(const AddParams &p, void *stream) {
     if (!p.n_docs) return 0;
-    const size_t lds = (512 + 2 * size_t(p.max_file_agents)) * 4;
+    const size_t lds = (512 + 2 * size_t(p.max_file_agents) + 3 * size_t(p.max_agents)) * 4;
+    if (lds > 160 * 1024) return 65;   // ErrCapacity: more agents than the LDS tables hold
+    if (lds > 64 * 1024 &&
+        hipFuncSetAttribute(reinterpret_cast<const void *>(&ddec::decode_add_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+        return 66;
     hipLaunchKernelGGL(ddec::decode_add_kernel, dim3(p.n_docs), dim3(64), lds, reinterpret_cast<hipStream_t>(stream), p);
     return hipGetLastError() == hipSuccess ? 0 : 66;
 }

@@ -86,7 +86,7 @@ struct AddParams {
     uint32_t *m_aruns, *m_ops, *m_ent, *m_poff, *m_par, *m_cbyte, *m_agents, *m_ver, *m_ffr, *scr;
     const AddDesc *docs;
     DecodeResult *results;
-    uint32_t n_docs, max_file_agents;
+    uint32_t n_docs, max_file_agents, max_agents, pad;   // max_agents: merged agents of any document
     uint32_t x2n[32];
 };
 

@@ -226,7 +226,7 @@ dtgpu_status dtgpu_decode_add(const dtgpu_decoded *B, const uint8_t *const *patc
     std::vector<AddDesc> ad(n, AddDesc{});
     M->desc.assign(n, DecodeDesc{});
     uint64_t in = 0, lz = 0, ar = 0, ops = 0, ent = 0, poff = 0, par = 0, content = 0, lv = 0, ag = 0, ver = 0, scr = 0;
-    uint32_t max_f = 1;
+    uint32_t max_f = 1, max_a = 1;
     for (size_t i = 0; i < n; i++) {
         const DecodeDesc &bd = B->desc[i];
         const DecodeResult &br = B->res[i];
@@ -272,7 +272,7 @@ dtgpu_status dtgpu_decode_add(const dtgpu_decoded *B, const uint8_t *const *patc
         a.m_agent = ag; ag += a.c_agent;
         a.m_ver = ver; ver += DECODE_MAX_FRONTIER;
         a.m_scr = scr; scr += uint64_t(a.c_pre) + a.c_vm;
-        if (!a.skip) max_f = std::max(max_f, r.n_file_agents);
+        if (!a.skip) { max_f = std::max(max_f, r.n_file_agents); max_a = std::max(max_a, a.c_agent); }
         md.in_off = a.m_in; md.in_len = a.p_rel + a.p_len;
         md.arun_off = a.m_arun; md.op_off = a.m_op; md.ent_off = a.m_ent; md.poff_off = a.m_poff; md.par_off = a.m_par;
         md.content_off = a.m_content; md.lv_off = a.m_lv; md.agent_off = a.m_agent; md.ver_off = a.m_ver;
@@ -294,7 +294,7 @@ dtgpu_status dtgpu_decode_add(const dtgpu_decoded *B, const uint8_t *const *patc
     A.m_in = M->in.p; A.lz = M->lz.p; A.m_content = M->content.p;
     A.m_aruns = M->aruns.p; A.m_ops = M->ops.p; A.m_ent = M->ent.p; A.m_poff = M->poff.p; A.m_par = M->par.p;
     A.m_cbyte = M->cbyte.p; A.m_agents = M->agents.p; A.m_ver = M->ver.p; A.m_ffr = M->ffr.p; A.scr = d_scr.p;
-    A.docs = d_ad.p; A.results = M->d_res.p; A.n_docs = uint32_t(n); A.max_file_agents = max_f;
+    A.docs = d_ad.p; A.results = M->d_res.p; A.n_docs = uint32_t(n); A.max_file_agents = max_f; A.max_agents = max_a;
     A.x2n[0] = 1u << 30;
     for (int k = 1; k < 32; k++) A.x2n[k] = multmodp_host(A.x2n[k - 1], A.x2n[k - 1]);
     CK(hipEventRecord(M->ev0, s));
