@@ -43,6 +43,11 @@ int launch_graph_queries(const GraphParams &p, void *stream);
 inline uint64_t conflict_level_words(uint64_t n_ent, uint64_t n_par) { return 4 * n_ent + 4 * (34 + n_ent + n_par); }
 inline uint32_t conflict_level_tps(uint64_t n_ent, uint64_t n_par) { return uint32_t(34 + n_ent + n_par); }
 struct LevelGraph { uint32_t ent_off, n_ent; };
+// The query kernels keep the marks (2 words per entry) in LDS when every levelled graph of the
+// launch has at most this many entries (48 KiB; sized to the largest graph, so small graphs keep
+// many queries per CU); larger graphs keep them in HBM scratch.  (The conflict sweep's bucket
+// heads and candidates in LDS as well measured slower: half the queries per CU.)
+constexpr uint32_t kLevelLdsEntries = 6144;
 struct LevelParams {
     const uint32_t *ents, *par;   // the GraphParams arena
     uint32_t *pent, *child;       // per parent slot: its parent's entry; children CSR (by parent entry)
@@ -53,6 +58,7 @@ struct LevelParams {
     uint32_t *qscr;               // per level query at its scr_off
     const LevelGraph *graphs;
     uint32_t n_graphs;
+    uint32_t lds_ent;             // query kernels: the marks of graphs up to this many entries in LDS
 };
 int launch_levels(const LevelParams &p, void *stream);
 int launch_level_diff(const LevelParams &p, const GraphParams &q, void *stream);

@@ -1,6 +1,7 @@
 // dt_level.hip -- level-synchronous causal-graph kernels (north_star "Causal graph": conflict-span
 // detection, diff and topological levelling as level-synchronous propagation over CSR parent
-// arrays in HBM).  Every per-entry array lives in HBM, so graphs of any size are levelled.
+// arrays in HBM).  Every per-entry array can live in HBM, so graphs of any size are levelled
+// (the query kernels' marks sit in LDS for graphs up to kLevelLdsEntries entries).
 //
 // level_kernel (one 256-thread workgroup per graph) levels the graph's entries: level(e) =
 // 1 + max level of its parent entries (roots 0), so every child sits on a higher level than
@@ -30,8 +31,9 @@
 // it, the walk is a sweep over the entries in descending order with each entry's pending points
 // in a bucket: no heap.  The workgroup lists the entries the marks touch, highest first (a
 // prefix-sum compaction), and one thread runs the sweep over that list, sorting each entry's
-// points in an LDS buffer; the marks, the list, the bucket heads and the point pool are HBM
-// scratch of the query.
+// points in an LDS buffer; the list, the bucket heads and the point pool are HBM scratch of the
+// query.  The marks of both query kernels sit in LDS for graphs up to kLevelLdsEntries entries
+// (their per-level atomicMax traffic), in HBM scratch beyond.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -213,7 +215,8 @@ __global__ __launch_bounds__(256) void level_diff_kernel(LevelParams P, GraphPar
         return;
     }
     const Ent *E = reinterpret_cast<const Ent *>(P.ents) + base;
-    int32_t *mA = reinterpret_cast<int32_t *>(P.qscr + q.scr_off), *mB = mA + n;
+    extern __shared__ int32_t lmarks[];   // P.lds_ent > 0: the marks live in LDS
+    int32_t *mA = P.lds_ent ? lmarks : reinterpret_cast<int32_t *>(P.qscr + q.scr_off), *mB = mA + n;
     const uint32_t st = push_marks(P, q, E, mA, mB, &s_top, &s_st);
     if (st != GQ_OK) {
         if (t == 0) { res->status = st; res->n0 = res->n1 = res->n_common = 0; }
@@ -343,7 +346,9 @@ __global__ __launch_bounds__(256) void level_conflict_kernel(LevelParams P, Grap
     __syncthreads();
     if (s_st != 0xFFFFFFFFu) return;
     __syncthreads();   // every thread read s_st before push_marks reuses it
-    int32_t *mA = reinterpret_cast<int32_t *>(P.qscr + q.scr_off), *mB = mA + n, *head = mB + n;
+    int32_t *hbm = reinterpret_cast<int32_t *>(P.qscr + q.scr_off);
+    extern __shared__ int32_t lmarks[];   // P.lds_ent > 0: the marks live in LDS
+    int32_t *mA = P.lds_ent ? lmarks : hbm, *mB = mA + n, *head = hbm + 2 * n;
     uint32_t *cand = reinterpret_cast<uint32_t *>(head + n);
     uint32_t *pool = cand + n;
     for (uint32_t e = t; e < n; e += NT) head[e] = -1;
@@ -469,13 +474,14 @@ int launch_levels(const LevelParams &p, void *stream) {
 
 int launch_level_diff(const LevelParams &p, const GraphParams &q, void *stream) {
     if (!q.n_queries) return 0;
-    hipLaunchKernelGGL(ldev::level_diff_kernel, dim3(q.n_queries), dim3(ldev::NT), 0, reinterpret_cast<hipStream_t>(stream), p, q);
+    hipLaunchKernelGGL(ldev::level_diff_kernel, dim3(q.n_queries), dim3(ldev::NT), 2 * size_t(p.lds_ent) * 4,
+                       reinterpret_cast<hipStream_t>(stream), p, q);
     return hipGetLastError() == hipSuccess ? 0 : 66;
 }
 
 int launch_level_conflict(const LevelParams &p, const GraphParams &q, void *stream) {
     if (!q.n_queries) return 0;
-    hipLaunchKernelGGL(ldev::level_conflict_kernel, dim3(q.n_queries), dim3(ldev::NT), 0,
+    hipLaunchKernelGGL(ldev::level_conflict_kernel, dim3(q.n_queries), dim3(ldev::NT), 2 * size_t(p.lds_ent) * 4,
                        reinterpret_cast<hipStream_t>(stream), p, q);
     return hipGetLastError() == hipSuccess ? 0 : 66;
 }

@@ -125,8 +125,11 @@ extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *h
                 CK(d_gscr.alloc(3 * nquad));
                 CK(d_qscr.alloc(std::max<uint64_t>(qscr_words, 1)));
                 CK(d_lg.upload(lg, st));
+                uint32_t max_ent = 0;
+                for (const LevelGraph &g : lg) max_ent = std::max(max_ent, g.n_ent);
                 LP = LevelParams{d_ents.p, d_par.p, d_pent.p, d_child.p, d_level.p, d_order.p, d_loff.p, d_meta.p,
-                                 d_gscr.p, d_qscr.p, d_lg.p, uint32_t(lg.size())};
+                                 d_gscr.p, d_qscr.p, d_lg.p, uint32_t(lg.size()),
+                                 max_ent <= kLevelLdsEntries ? max_ent : 0u};
             }
             CK(hipEventRecord(e0, st));
             if (launch_graph_queries(P, st)) { rc = DTGPU_ERR_HIP; goto done; }
