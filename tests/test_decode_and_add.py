@@ -372,3 +372,23 @@ def test_gpu_checkout_of_concurrent_merge():
         d.decode_and_add(full.history(v1).encode())
         assert d.checkout_tip_bytes() == ora.checkout_bytes(u)
         done += 1
+
+
+def test_doc_id_export_matches_the_oplog():
+    """DTGPU_EXPORT_DOC_ID (the array the device decode_and_add tests compare): a presence byte,
+    then the id's bytes."""
+    o = _simple_doc()
+    assert bytes(o.export("doc_id")) == b"\x00"
+    o.doc_id = "hi"
+    assert bytes(o.export("doc_id")) == b"\x01hi"
+    assert bytes(dt_amd.ListOpLog.load_from(o.encode()).export("doc_id")) == b"\x01hi"
+
+
+def test_device_decode_add_rejects_bad_arguments():
+    """dtgpu_decode_add / dtgpu_decode_add_result validate their handles before any device work."""
+    import ctypes
+    L = dt_amd.lib()
+    out = ctypes.c_void_p()
+    assert L.dtgpu_decode_add(None, None, None, 0, 0, None, ctypes.byref(out)) == 67   # DTGPU_ERR_ARG
+    assert L.dtgpu_decode_add_result(None, 0, None, 0, None) == 67
+    assert L.dtgpu_batch_create_decoded(None, ctypes.byref(out)) == 67
