@@ -159,7 +159,8 @@ struct PlanParams {
     uint32_t *tlist;
     const PlanDesc *docs;
     PlanResult *results;
-    uint32_t n_docs, count_only;
+    uint32_t n_docs, count_only;   // n_docs: the grid (the list's length when doc_list is set)
+    const uint32_t *doc_list;      // nullable: block i plans docs[doc_list[i]]
 };
 int launch_plan(const PlanParams &q, void *stream);
 
@@ -178,6 +179,7 @@ struct ReplayLaunch {
     void *side[kSideStreams];       // hipStream_t: tier n_lds - 1 - k on side[k]
     void *ev_fork;                  // hipEvent_t
     void *ev_join[kSideStreams];    // hipEvent_t
+    bool keep_fb = false;           // the fallback counter was reset by the caller (split passes)
 };
 int launch_replay(const ReplayLaunch &r);
 // The same pass on the span tracker (dt_span.hip): BatchParams.rows holds the span blocks,

@@ -755,8 +755,8 @@ DEV void plan_doc1(P &p, PlanResult *res) {
 template <int K>
 DEV void plan_entry(const PlanParams &Q) {
     extern __shared__ __attribute__((aligned(16))) uint16_t lds16[];
-    const uint32_t d = U(blockIdx.x);
-    if (d >= Q.n_docs) return;
+    if (blockIdx.x >= Q.n_docs) return;
+    const uint32_t d = U(Q.doc_list ? Q.doc_list[blockIdx.x] : blockIdx.x);
     const PlanDesc pd = Q.docs[d];
     PlanResult *res = Q.results + d;
     if (pd.skip) return;   // planned on the host

@@ -96,8 +96,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
     // list relative to coff -- half the LDS of absolute u32 slots, so more documents share a CU
     extern __shared__ uint32_t lfw[];
     uint16_t *lfill = reinterpret_cast<uint16_t *>(lfw);
-    const uint32_t doc = blockIdx.x;
-    if (doc >= P.n_docs) return;
+    if (blockIdx.x >= P.n_docs) return;
+    const uint32_t doc = P.doc_list ? P.doc_list[blockIdx.x] : blockIdx.x;
     const PrepDesc D = P.docs[doc];
     PrepResult R{};
     if (D.skip) {

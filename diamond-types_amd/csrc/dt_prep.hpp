@@ -38,7 +38,8 @@ struct PrepParams {
     Cmd *opc;
     const PrepDesc *docs;
     PrepResult *results;
-    uint32_t n_docs, max_entries;
+    uint32_t n_docs, max_entries;   // n_docs: the grid (the list's length when doc_list is set)
+    const uint32_t *doc_list;       // nullable: block i prepares docs[doc_list[i]]
 };
 
 // owner (n_par, padded to even), {chain, seq0 - start} pairs (2 ne), coff, eop (ne + 1 each): even,

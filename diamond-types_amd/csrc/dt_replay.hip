@@ -1322,7 +1322,8 @@ int launch_replay(const ReplayLaunch &r) {
         if (r.lds[t].fb_count) fb_count = r.lds[t].fb_count;
     }
     if (n_lds) {
-        if (fb_count && hipMemsetAsync(const_cast<uint32_t *>(fb_count), 0, sizeof(uint32_t), s) != hipSuccess) return ErrHip;
+        if (fb_count && !r.keep_fb && hipMemsetAsync(const_cast<uint32_t *>(fb_count), 0, sizeof(uint32_t), s) != hipSuccess)
+            return ErrHip;
         // fork: the biggest tiers start first, each on its own side stream; the smallest tier
         // runs on the main stream
         int n_side = 0;

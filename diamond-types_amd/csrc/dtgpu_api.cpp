@@ -91,6 +91,13 @@ struct dtgpu_batch {
     uint32_t debug = 0;
     hipStream_t side[kSideStreams] = {};   // big LDS tiers run beside the small ones, one stream each
     hipEvent_t ev_fork = nullptr, ev_join[kSideStreams] = {};
+    // device-staged split pass: the biggest LDS tier's documents run prep -> plan -> replay on
+    // that tier's side stream, beside the other documents' prep and plan (d_split: the big
+    // tier's documents, then the rest)
+    bool split = false;
+    int split_tier = -1;
+    uint32_t n_big = 0, n_rest = 0;
+    DevBuf<uint32_t> d_split;
     uint64_t alg_in_bytes = 0, total_lv = 0;
     float last_plan_ms = 0, last_replay_ms = 0;
 
@@ -238,9 +245,15 @@ dtgpu_status set_tier_params(dtgpu_batch &B, const BatchParams &base) {
     }
     return DTGPU_OK;
 }
-int replay_all(dtgpu_batch *B, hipStream_t s) {
+int replay_all(dtgpu_batch *B, hipStream_t s, int skip_tier = -1) {
     ReplayLaunch r{};
-    r.lds = B->tier;
+    BatchParams tiers[kLdsTiers];
+    for (int t = 0; t < kLdsTiers; t++) {
+        tiers[t] = B->tier[t];
+        if (t == skip_tier) tiers[t].n_list = 0;   // replayed by the split pipeline
+    }
+    r.lds = tiers;
+    r.keep_fb = skip_tier >= 0;
     r.n_lds = kLdsTiers;
     r.large = &B->large;
     r.stream = s;
@@ -737,13 +750,91 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     base.docs = B->d_docs.p;
     base.results = B->d_results.p;
     if (set_tier_params(*B, base) != DTGPU_OK) return DTGPU_ERR_HIP;
+    // split pass: when the biggest non-empty LDS tier rides a side stream and other documents
+    // exist, its documents' prep and plan do not wait for everyone else's (a skewed batch's
+    // longest replays start as soon as their own plans are done)
+    if (B->item_mode && !getenv("DTGPU_NO_SPLIT")) {
+        int tb = -1;
+        for (int t = kLdsTiers - 1; t >= 1; t--)
+            if (!B->tier_list[t].empty()) { tb = t; break; }
+        if (tb >= 1) {
+            std::vector<uint32_t> lst = B->tier_list[tb];
+            std::vector<uint8_t> big(n, 0);
+            for (uint32_t d : lst) big[d] = 1;
+            const size_t nb = lst.size();
+            for (size_t i = 0; i < n; i++)
+                if (!big[i]) lst.push_back(uint32_t(i));
+            if (lst.size() > nb) {
+                if (B->d_split.upload(lst, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) return DTGPU_ERR_HIP;
+                B->split = true;
+                B->split_tier = tb;
+                B->n_big = uint32_t(nb);
+                B->n_rest = uint32_t(lst.size() - nb);
+            }
+        }
+    }
     *out = B.release();
     return DTGPU_OK;
+}
+
+// The split pass's side pipeline (see stage_device): after a fork from s, the big tier's
+// prep, plan and replay on its side stream.  The fallback counter is reset first, on s, since
+// both pipelines' LDS tiers append to it; the main pipeline's replay_all(skip_tier) joins the
+// side stream (launch_replay's fork / join of that tier's stream) before the HBM tier.
+int launch_split_side(dtgpu_batch *B, hipStream_t s) {
+    const int tb = B->split_tier;
+    hipStream_t sb = B->side[kLdsTiers - 1 - tb];
+    const BatchParams &q = B->tier[tb];
+    if (q.fb_count && hipMemsetAsync(const_cast<uint32_t *>(q.fb_count), 0, sizeof(uint32_t), s) != hipSuccess) return ErrHip;
+    if (hipEventRecord(B->ev_fork, s) != hipSuccess || hipStreamWaitEvent(sb, B->ev_fork, 0) != hipSuccess) return ErrHip;
+    PrepParams pp = B->prep;
+    pp.doc_list = B->d_split.p;
+    pp.n_docs = B->n_big;
+    if (launch_prep(pp, sb)) return ErrHip;
+    PlanParams qq = B->plan;
+    qq.doc_list = B->d_split.p;
+    qq.n_docs = B->n_big;
+    if (B->n_gpu_planned && launch_plan(qq, sb) != OK) return ErrHip;
+    BatchParams tiers[kLdsTiers];
+    for (int t = 0; t < kLdsTiers; t++) {
+        tiers[t] = B->tier[t];
+        if (t != tb) tiers[t].n_list = 0;
+    }
+    BatchParams large = B->large;
+    large.n_list = 0;
+    large.fb_slots = 0;
+    ReplayLaunch r{};
+    r.lds = tiers;
+    r.n_lds = kLdsTiers;
+    r.large = &large;
+    r.stream = sb;
+    r.keep_fb = true;
+    return launch_replay(r);
+}
+// The main pipeline's prep and plan of a split pass (the documents outside the big tier).
+int launch_split_prep(dtgpu_batch *B, hipStream_t s) {
+    PrepParams pp = B->prep;
+    pp.doc_list = B->d_split.p + B->n_big;
+    pp.n_docs = B->n_rest;
+    return launch_prep(pp, s) ? ErrHip : OK;
+}
+int launch_split_plan(dtgpu_batch *B, hipStream_t s) {
+    if (!B->n_gpu_planned) return OK;
+    PlanParams qq = B->plan;
+    qq.doc_list = B->d_split.p + B->n_big;
+    qq.n_docs = B->n_rest;
+    return launch_plan(qq, s);
 }
 
 // One checkout pass on stream s: prep (device-staged batches), plan (device), replay.
 int launch_all(dtgpu_batch *B, hipStream_t s) {
     if (B->xf_mode) return launch_replay_xf(B->large, s);
+    if (B->split) {
+        int e = launch_split_side(B, s);
+        if (!e) e = launch_split_prep(B, s);
+        if (!e) e = launch_split_plan(B, s);
+        return e ? e : replay_all(B, s, B->split_tier);
+    }
     if (B->dec && launch_prep(B->prep, s)) return ErrHip;   // device-staged: walker inputs first
     if (B->n_gpu_planned) {
         int e = launch_plan(B->plan, s);
@@ -1273,12 +1364,14 @@ dtgpu_status dtgpu_batch_run_timed(dtgpu_batch *B, float *ms) {
     // planner, then replay + materialisation
     hipStream_t s = B->stream;
     const bool prep = B->dec && !B->xf_mode;
+    const bool split = prep && B->split;   // split pass: prep / plan times are the main pipeline's
     if (hipEventRecord(B->ev_prep, s) != hipSuccess) return DTGPU_ERR_HIP;
-    if (prep && launch_prep(B->prep, s)) return DTGPU_ERR_HIP;
+    if (split && launch_split_side(B, s)) return DTGPU_ERR_HIP;
+    if (split ? launch_split_prep(B, s) != OK : (prep && launch_prep(B->prep, s))) return DTGPU_ERR_HIP;
     if (hipEventRecord(B->ev0, s) != hipSuccess) return DTGPU_ERR_HIP;
-    if (B->n_gpu_planned && launch_plan(B->plan, s) != OK) return DTGPU_ERR_HIP;
+    if (split ? launch_split_plan(B, s) != OK : (B->n_gpu_planned && launch_plan(B->plan, s) != OK)) return DTGPU_ERR_HIP;
     if (hipEventRecord(B->ev_mid, s) != hipSuccess) return DTGPU_ERR_HIP;
-    int st = B->xf_mode ? launch_replay_xf(B->large, s) : replay_all(B, s);
+    int st = B->xf_mode ? launch_replay_xf(B->large, s) : replay_all(B, s, split ? B->split_tier : -1);
     if (st) return dtgpu_status(st);
     if (hipEventRecord(B->ev1, s) != hipSuccess) return DTGPU_ERR_HIP;
     if (hipEventSynchronize(B->ev1) != hipSuccess) return DTGPU_ERR_HIP;
