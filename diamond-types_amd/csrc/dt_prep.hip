@@ -342,11 +342,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
 #ifdef DTGPU_PREP_PROF
     const uint64_t T4 = wall_clock64();
 #endif
-    // per chain: offset of its dense table
+    // per chain: offset of its dense table (also kept in a register, lane = chain)
+    uint32_t doff_l;
     {
         const uint32_t c = l < nch ? clen : 0;
         const uint32_t inc = scan_incl(c);
-        if (l < nch) doff[l] = inc - c;
+        doff_l = inc - c;
+        if (l < nch) doff[l] = doff_l;
         if (l == 0) doff[nch] = rdl(inc, 63);
     }
 
@@ -382,14 +384,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
     // per lane -- per entry, a history of few long entries (node_nodecc: 91 entries, 53k runs)
     // would leave most lanes idle behind one entry's runs.  A run's entry is the last entry whose
     // first run is at or below it: searched among the 64 entries from the previous chunk's last
-    // run's entry in registers, by bisection past that window.
+    // run's entry in registers, by bisection past that window.  The window's chain pairs are
+    // loaded with it and the runs themselves, one round trip per 64 runs, and a chain's table
+    // offset comes from a register (lane = chain), not a dependent load.
     uint32_t n_ins = 0;
     {
         uint32_t ebase = 0;
         for (uint32_t j0 = 0; j0 < nops; j0 += 64) {
             const uint32_t j = j0 + l;
             const bool live = j < nops;
-            const uint32_t we = ebase + l < ne ? eop[ebase + l + 1] : 0xFFFFFFFFu;   // end of entry ebase + l
+            const uint32_t wi = ebase + l;
+            const bool wv = wi < ne;
+            const uint32_t we = wv ? eop[wi + 1] : 0xFFFFFFFFu;   // end of entry ebase + l
+            const uint2 wq = wv ? cs[wi] : make_uint2(0, 0);
+            const uint4 o = live ? ops[j] : make_uint4(0, 0, 0, 0);   // lv, len, pos, kind | fwd << 1
             uint32_t c = 0;
 #pragma unroll
             for (uint32_t st = 32; st >= 1; st >>= 1)
@@ -401,17 +409,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
                 if (eop[mid + 1] <= j) lo = mid + 1; else hi = mid;
             }
             const uint32_t i = lo;
-            if (live) {
-                const uint32_t e0 = ent[i].x;
+            const uint32_t src = min(i - ebase, 63u);
+            uint32_t qx = uint32_t(__shfl(int(wq.x), int(src))), qy = uint32_t(__shfl(int(wq.y), int(src)));
+            if (live && i - ebase >= 64) {   // past the window
                 const uint2 q = cs[i];
-                const uint32_t d0 = doff[q.x] + q.y + e0;   // seq0 + chain offset
-                const uint4 o = ops[j];   // lv, len, pos, kind | fwd << 1
+                qx = q.x; qy = q.y;
+            }
+            const uint32_t dch = uint32_t(__shfl(int(doff_l), int(qx & 63u)));
+            if (live) {
                 const bool del = o.w & 1u;
                 opc[j] = Cmd{del ? (CMD_DEL | ((o.w & 2u) ? 16u : 0u)) : uint32_t(CMD_INS), o.x, o.y, o.z};
                 if (!del) n_ins += o.y;
-                // the run's dense slots: 16-byte stores between a scalar head and tail
+                // the run's dense slots (chain offset + seq0 - start + LV): 16-byte stores between
+                // a scalar head and tail.  (Filling the chunk LV by LV across the lanes instead
+                // measured no faster.)
                 const uint32_t flag = del ? TL_DEL : 0u;
-                uint32_t *dp = dense + uint32_t(d0 + (o.x - e0));
+                uint32_t *dp = dense + uint32_t(dch + qy + o.x);
                 uint32_t v = 0;
                 for (; v < o.y && (reinterpret_cast<uintptr_t>(dp + v) & 15u); v++) dp[v] = (o.x + v) | flag;
                 for (; v + 4 <= o.y; v += 4) {
@@ -438,10 +451,35 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
         if (l == 0) { R.status = PREP_BAD; P.results[doc] = R; }
         return;
     }
-    // agent runs with name ranks (byte-wise name order; names are distinct)
-    {
-        const uint2 *names = reinterpret_cast<const uint2 *>(P.d_agents) + D.d_agent;
-        const uint8_t *in = P.in + D.d_in;
+    // agent runs with name ranks (byte-wise name order; names are distinct): each agent's rank
+    // once (lane per agent), into the scatter's owner scratch (free by now) when it fits, then
+    // one lookup per run; otherwise ranked per run
+    const uint2 *names = reinterpret_cast<const uint2 *>(P.d_agents) + D.d_agent;
+    const uint8_t *in = P.in + D.d_in;
+    if (D.n_agents <= ((npar + 1) & ~1u)) {
+        for (uint32_t a = l; a < D.n_agents; a += 64) {
+            const uint2 me = names[a];
+            uint32_t rank = 0;
+            for (uint32_t b = 0; b < D.n_agents; b++) {
+                const uint2 o = names[b];
+                const uint32_t n = min(o.y, me.y);
+                int cmp = 0;
+                for (uint32_t x = 0; x < n && !cmp; x++) {
+                    const uint32_t cb = in[o.x + x], cm = in[me.x + x];
+                    cmp = cb < cm ? -1 : cb > cm ? 1 : 0;
+                }
+                if (!cmp) cmp = o.y < me.y ? -1 : o.y > me.y ? 1 : 0;
+                rank += cmp < 0 ? 1u : 0u;
+            }
+            owner[a] = rank;
+        }
+        wave_fence();
+        for (uint32_t k = l; k < D.n_aruns; k += 64) {
+            const uint4 a = ar[k];   // lv, len, agent, seq
+            uint32_t *q = P.aruns + 4 * (D.o_arun + k);
+            q[0] = a.x; q[1] = owner[a.z]; q[2] = a.w; q[3] = a.z;
+        }
+    } else {
         for (uint32_t k = l; k < D.n_aruns; k += 64) {
             const uint4 a = ar[k];   // lv, len, agent, seq
             const uint2 me = names[a.z];
