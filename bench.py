@@ -317,7 +317,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    # a process group whenever the launcher started us (torch.distributed.run sets
+    # TORCHELASTIC_RUN_ID), also at one rank: the RCCL collectives then run on cuda:0
+    if world > 1 or "TORCHELASTIC_RUN_ID" in os.environ:
         import torch
         import torch.distributed as dist
         # rehearsal of the N-rank path on a 1-GPU box: every rank on GPU 0, collectives over gloo
@@ -395,6 +397,7 @@ def main():
     assert bad == 0, f"{bad} documents differ from the golden / oracle text"
     total_lv_mine = sum(r["n_lv"] for r in res)
     total_lv = total_lv_mine
+    collectives = None
     if dist is not None:   # RCCL all-gather of per-document (len, hash) records
         table = gather_results([(g, r["status"], r["text_len"], r["text_hash"]) for g, r in zip(mine, res)],
                                n_total, dist, device=dev)
@@ -405,6 +408,9 @@ def main():
         dist.all_reduce(t)   # whole-job merged ops
         total_lv = int(t.item())
         dist.barrier()
+        collectives = {"backend": dist.get_backend(), "device": str(dev) if dev is not None else "cpu",
+                       "world": world, "gathered_docs": len(table),
+                       "gathered_ok": sum(1 for row in table if row is not None and row[1] == 0)}
     lv_per_doc = total_lv_mine / max(1, len(mine))
     ms_per_step = elapsed * 1000.0 / args.steps
     value = total_lv * args.steps / elapsed
@@ -462,6 +468,8 @@ def main():
     }
     if rebalance is not None:
         out["rebalance"] = rebalance
+    if collectives is not None:
+        out["collectives"] = collectives
     if not args.no_decode and staging == "device":   # .dt bytes -> text, all on the GPU
         out["e2e"] = e2e_leg(batch, docs, min(args.steps, 5), want, total_lv_mine)
     if not args.no_encode and staging == "device" and rank == 0:   # oplogs -> .dt bytes on the GPU

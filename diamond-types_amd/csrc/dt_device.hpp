@@ -180,6 +180,8 @@ struct ReplayLaunch {
     void *ev_fork;                  // hipEvent_t
     void *ev_join[kSideStreams];    // hipEvent_t
     bool keep_fb = false;           // the fallback counter was reset by the caller (split passes)
+    int join_side = -1;             // split pass: side[join_side] carries the big tier's own
+                                    // prep / plan / replay; s joins it before the HBM tier always
 };
 int launch_replay(const ReplayLaunch &r);
 // The same pass on the span tracker (dt_span.hip): BatchParams.rows holds the span blocks,

@@ -1348,6 +1348,16 @@ int launch_replay(const ReplayLaunch &r) {
                     return ErrHip;
         }
     }
+    // split pass: the big tier's side pipeline must be done before the HBM tier reads the
+    // fallback queue and before anything synchronising on s sees the batch as finished -- also
+    // when no other LDS tier forked above (then nothing else joined that stream)
+    if (r.join_side >= 0) {
+        if (r.join_side >= kSideStreams || !r.side[r.join_side] || !r.ev_join[r.join_side]) return ErrArg;
+        if (hipEventRecord(reinterpret_cast<hipEvent_t>(r.ev_join[r.join_side]), reinterpret_cast<hipStream_t>(r.side[r.join_side])) !=
+                hipSuccess ||
+            hipStreamWaitEvent(s, reinterpret_cast<hipEvent_t>(r.ev_join[r.join_side]), 0) != hipSuccess)
+            return ErrHip;
+    }
     // HBM tier: its own list plus a slot per LDS-tier document that may be handed back
     const uint32_t grid = large.n_list + (large.fb_list ? large.fb_slots : 0);
     if (grid) {

@@ -55,6 +55,15 @@ int item_tier(uint32_t est) {
     for (int t = 0; t < kLdsTiers; t++) if (bytes <= kItemTierCap[t]) return t;
     return -1;
 }
+// Expected inserted chars per block when sizing a document's LDS index: the per-item tracker's
+// blocks end up ~43 items full on the benchmark traces (cut_point, dt_replay.hip), sized at 40;
+// the span tracker's at SPAN_LDS_FILL.  DTGPU_LDS_FILL overrides either (tests force the LDS
+// overflow -> HBM tier hand-back with it).
+uint64_t lds_fill_setting(bool item) {
+    uint64_t f = item ? 40 : SPAN_LDS_FILL;
+    if (const char *e = getenv("DTGPU_LDS_FILL")) f = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
+    return f;
+}
 // Per-document replay layout of either tracker: block capacity, HBM index bytes, LDS tier.
 struct Layout { uint32_t max_blocks; uint64_t gidx; int tier; uint32_t tier_blocks; };
 Layout replay_layout(uint64_t n_ins, uint64_t lds_fill, bool item, bool hbm_only) {
@@ -62,7 +71,7 @@ Layout replay_layout(uint64_t n_ins, uint64_t lds_fill, bool item, bool hbm_only
     if (item) {
         L.max_blocks = uint32_t(n_ins / 32 + 2);
         L.gidx = index_bytes(L.max_blocks);
-        const uint32_t est = uint32_t(std::min<uint64_t>(L.max_blocks, n_ins / 40 + 8));
+        const uint32_t est = uint32_t(std::min<uint64_t>(L.max_blocks, n_ins / lds_fill + 8));
         L.tier = hbm_only ? -1 : item_tier(est);
         L.tier_blocks = est;
     } else {
@@ -254,6 +263,7 @@ int replay_all(dtgpu_batch *B, hipStream_t s, int skip_tier = -1) {
     }
     r.lds = tiers;
     r.keep_fb = skip_tier >= 0;
+    r.join_side = skip_tier >= 0 ? kLdsTiers - 1 - skip_tier : -1;   // launch_split_side's stream
     r.n_lds = kLdsTiers;
     r.large = &B->large;
     r.stream = s;
@@ -381,10 +391,9 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     std::vector<uint8_t> content;
     uint64_t cmd_total = 0, tlist_total = 0;
     uint64_t lv_total = 0, blk_total = 0, out_total = 0, gidx_total = 0;
-    // expected inserted chars per block of spans in the LDS tier; DTGPU_LDS_FILL overrides it
+    // expected inserted chars per block in the LDS tier (per tracker); DTGPU_LDS_FILL overrides it
     // for experiments (a document that outgrows its LDS index replays on the HBM tier)
-    uint64_t lds_fill = SPAN_LDS_FILL;
-    if (const char *e = getenv("DTGPU_LDS_FILL")) lds_fill = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
+    const uint64_t lds_fill = lds_fill_setting(B->item_mode);
     for (size_t i = 0; i < n; i++) {
         Prepared &p = prep[i];
         B->host_status[i] = p.status;
@@ -664,8 +673,7 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
 
     // ---- replay layout ---------------------------------------------------------------------------
     uint64_t cmd_total = 0, tlist_total = 0, blk_total = 0, out_total = 0, gidx_total = 0;
-    uint64_t lds_fill = SPAN_LDS_FILL;
-    if (const char *e = getenv("DTGPU_LDS_FILL")) lds_fill = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
+    const uint64_t lds_fill = lds_fill_setting(B->item_mode);
     for (size_t i = 0; i < n; i++) {
         DocDesc &d = B->docs[i];
         std::memset(&d, 0, sizeof d);
@@ -1202,7 +1210,10 @@ dtgpu_status dtgpu_batch_create_device(const uint8_t *const *docs, const size_t 
 
 dtgpu_status dtgpu_batch_create_decoded(dtgpu_decoded *dec, dtgpu_batch **out) {
     if (!dec || !out) return DTGPU_ERR_ARG;
-    if (!dec->stream && hipStreamCreateWithFlags(&dec->stream, hipStreamNonBlocking) != hipSuccess) return DTGPU_ERR_HIP;
+    if (!dec->stream && hipStreamCreateWithFlags(&dec->stream, hipStreamNonBlocking) != hipSuccess) {
+        dtgpu_decode_free(dec);   // consumed on failure too (dtgpu.h)
+        return DTGPU_ERR_HIP;
+    }
     return stage_device(dec, out);
 }
 dtgpu_status dtgpu_batch_run_e2e_timed(dtgpu_batch *B, float ms[4]) {

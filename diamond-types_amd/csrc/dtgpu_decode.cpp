@@ -227,6 +227,7 @@ dtgpu_status dtgpu_decode_add(const dtgpu_decoded *B, const uint8_t *const *patc
     M->desc.assign(n, DecodeDesc{});
     uint64_t in = 0, lz = 0, ar = 0, ops = 0, ent = 0, poff = 0, par = 0, content = 0, lv = 0, ag = 0, ver = 0, scr = 0;
     uint32_t max_f = 1, max_a = 1;
+    constexpr uint32_t kAddMaxAgents = (160 * 1024 / 4 - 512 - 2 * DECODE_MAX_FILE_AGENTS) / 3;
     for (size_t i = 0; i < n; i++) {
         const DecodeDesc &bd = B->desc[i];
         const DecodeResult &br = B->res[i];
@@ -262,6 +263,11 @@ dtgpu_status dtgpu_decode_add(const dtgpu_decoded *B, const uint8_t *const *patc
         a.c_content = uint32_t(std::min<uint64_t>(uint64_t(a.b_n_content) + a.p_len + r.lz_len, 0xFFFFFFFFull));
         a.c_lv = uint32_t(std::min<uint64_t>(uint64_t(a.b_n_lv) + r.n_lv, 0xFFFFFFFFull));
         a.c_agent = a.b_n_agents + r.n_file_agents;
+        // the kernel's per-agent LDS tables (launch_decode_add: 512 + 2 max_file_agents + 3
+        // max_agents words) must fit the CU's 160 KiB for the batch's largest document: with
+        // n_file_agents <= DECODE_MAX_FILE_AGENTS that holds for every merged agent count up to
+        // kAddMaxAgents, and a document past it is deferred to the host alone (never failing the batch)
+        if (a.c_agent > kAddMaxAgents) a.skip = 1;
         a.m_arun = ar; ar += a.c_arun;
         a.m_op = ops; ops += a.c_op;
         a.m_ent = ent; ent += a.c_ent;

@@ -235,7 +235,10 @@ dtgpu_status dtgpu_batch_sync(dtgpu_batch *batch);
 size_t dtgpu_batch_size(const dtgpu_batch *batch);
 /* Device time of the last dtgpu_batch_run_timed split into out[0] = walk planning (dt_plan.hip),
  * out[1] = replay + materialisation (dt_replay.hip) and out[2] = walker inputs (dt_prep.hip; 0 for
- * host-staged batches), milliseconds. */
+ * host-staged batches), milliseconds.  In a split pass (a skewed device-staged batch whose
+ * biggest LDS tier runs its own prep -> plan -> replay on a side stream) out[2] and out[0] are
+ * the main pipeline's prep and plan; the big tier's prep and plan overlap them and are counted
+ * inside out[1]. */
 dtgpu_status dtgpu_batch_last_times(const dtgpu_batch *batch, float out[3]);
 /* Documents planned on the host because the device planner declined them: returns their count
  * and, when flags is not NULL, one code per document: 0 device-planned, 1 DTGPU_HOST_PLAN set,

@@ -24,11 +24,15 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run(extra):
-    env = dict(os.environ, DTGPU_BENCH_SHARED_GPU="1", MASTER_ADDR="127.0.0.1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+def _run(extra, nproc=2, shared=True):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    if shared:
+        env["DTGPU_BENCH_SHARED_GPU"] = "1"
+    else:
+        env.pop("DTGPU_BENCH_SHARED_GPU", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           os.path.join(ROOT, "bench.py"), "--gpus", str(nproc), "--steps", "2", "--warmup", "1",
            "--no-cpu-baseline", "--no-encode", "--gen-threads", "4"] + extra
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=420)
     assert p.returncode == 0, p.stderr[-3000:]
@@ -55,3 +59,21 @@ def test_bench_two_ranks_mixed_rebalance():
     rb = out["rebalance"]
     assert len(rb["busy_ms_before"]) == 2 and len(rb["busy_ms_after"]) == 2
     assert out["total_merged_ops"] > 0 and out["value"] > 0
+
+
+@pytest.mark.timeout(480)
+@pytest.mark.parametrize("extra", [["--docs", "200"], ["--workload", "mixed", "--docs", "24", "--rebalance"]])
+def test_bench_rccl_one_rank(extra):
+    """The RCCL code path, run once on the box: torch.distributed.run starts one rank (a fresh
+    process, before any GPU call), bench.py joins an `nccl` (RCCL) process group on cuda:0 and runs
+    max_over_ranks, gather_results (the per-document table, checked against the goldens / oracle
+    inside bench.py) and -- with --rebalance -- all_gather_floats on device tensors."""
+    out = _run(extra, nproc=1, shared=False)
+    c = out["collectives"]
+    assert c["backend"] == "nccl" and c["device"] == "cuda:0" and c["world"] == 1
+    assert c["gathered_docs"] == c["gathered_ok"] == int(extra[extra.index("--docs") + 1])
+    if "--rebalance" in extra:
+        assert len(out["rebalance"]["busy_ms_before"]) == 1 and out["rebalance"]["moves"] == 0
+        assert out["total_merged_ops"] > 0
+    else:
+        assert out["total_merged_ops"] == 200 * FF_LV

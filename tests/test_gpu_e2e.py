@@ -59,6 +59,48 @@ def test_large_docs_device_staged(name, replay_mode):
     assert hashlib.sha256(texts[0]).hexdigest() == hashlib.sha256(want).hexdigest()
 
 
+def _hbm_tier_doc():
+    """`.dt` bytes of a linear document with ~900k inserted chars: its LDS index estimate
+    exceeds the biggest LDS tier (160 KiB), so it replays on the HBM-index tier."""
+    o = dt_amd.ListOpLog()
+    a = o.get_or_create_agent_id("hbm")
+    n = 0
+    for k in range(9):
+        chunk = chr(ord("a") + k) * 100_000
+        o.add_insert(a, (k * 7919) % (n + 1), chunk)
+        n += len(chunk)
+    o.add_delete_without_content(a, 5000, 20_000)
+    return o.encode()
+
+
+@pytest.mark.parametrize("case", ["big_tier_with_error_doc", "big_tier_with_hbm_doc"])
+def test_split_pass_joins_big_tier(case):
+    """Split pass (a big LDS tier's prep -> plan -> replay on its side stream) with no other
+    LDS tier beside it: the main stream must still join the side stream before the HBM tier and
+    before the batch counts as done, so results and texts are read after the big tier's replay."""
+    if case == "big_tier_with_error_doc":
+        docs = [G.dt_bytes("node_nodecc"), b"nope"]
+    else:
+        docs = [G.dt_bytes("git-makefile"), _hbm_tier_doc()]
+    for timed in (False, True):
+        b = dt_amd.Batch(docs=docs, staging="device")
+        if timed:
+            b.run_timed()
+            res = b.results()
+            texts = [b.text(i) if r["status"] == 0 else None for i, r in enumerate(res)]
+        else:
+            res, texts = _texts(b)
+        assert res[0]["status"] == 0
+        want = OracleOpLog.load_from(docs[0]).checkout_tip_bytes()
+        assert hashlib.sha256(texts[0]).hexdigest() == hashlib.sha256(want).hexdigest()
+        if case == "big_tier_with_error_doc":
+            assert res[1]["status"] != 0
+        else:
+            assert res[1]["status"] == 0 and b.doc_stats(1)["lds_index"] == 0, res[1]
+            want1 = OracleOpLog.load_from(docs[1]).checkout_tip_bytes()
+            assert texts[1] == want1
+
+
 def test_device_plan_equals_host_plan():
     docs = [G.dt_bytes(n) for n in G.DT_FILES]
     dev = dt_amd.Batch(docs=docs, staging="device")
