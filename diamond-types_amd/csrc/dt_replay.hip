@@ -188,6 +188,12 @@ struct Doc {
     // same state (every change is stored); a toggle touching the block drops it.
     uint32_t cb, cit;
     u64 cmv, cml;
+    // cursor cache (content-tree cursor reuse): cvs = visible items before block cb in document
+    // order, valid while cvok (any visibility flip of a retreat/advance pass may move it); ctp =
+    // top position of cb's superblock or NONE (a superblock split shifts top positions).  An
+    // insert / delete whose position lands inside cb's visible range skips the index descent.
+    uint32_t cvs, ctp;
+    bool cvok;
     // transformed-ops mode (iter_xf_operations): per block the never-deleted mask, per top
     // position the never-deleted total, per LV the transformed position written out
     u64 *mup;
@@ -404,6 +410,7 @@ DEV void split_sb(Doc &D, uint32_t S) {
     }
     wave_fence();
     D.nsb++;
+    D.ctp = NONE;
 }
 
 // Split the full block b (items in `it` lane by lane, masks mv / ml) at slot c: items [c, 64)
@@ -486,7 +493,7 @@ DEV uint32_t up_rank(Doc &D, uint32_t b, uint32_t s) {
 // block's items lane by lane (lanes >= the block count are don't-care); mv / ml its masks.
 template <bool L, bool PROF, bool XF>
 DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml, uint32_t lv, uint32_t k,
-                    uint32_t ol, uint32_t orr, uint32_t tph) {
+                    uint32_t ol, uint32_t orr, uint32_t tph, uint32_t vs) {
     D.cb = NONE;
     const uint32_t l = lane_id();
     const uint32_t lv0 = lv, k0 = k;
@@ -504,6 +511,7 @@ DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml,
             if (D.err) return;
             tph = NONE;   // a split may move superblocks in the top order
             if (s > cut || cut == BLK) {
+                if (vs != NONE) vs += uint32_t(__popcll(mv & lanes_below(cut)));   // visible items left in b
                 b = b2;
                 s -= cut;
                 it = shfl(it, (l + cut) & 63u);
@@ -540,9 +548,10 @@ DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml,
             mu = m == 64 ? ins : ((mu & low) | ((mu & ~low) << m) | ins);
             if (l == 0) st(D.mup + b, mu);
         }
+        if (tph == NONE) tph = U(ix<L>(D.sbpos + (opos_of<L>(D, b) >> 6)));
         if (l == 0) {   // the superblock's totals by atomic add: no dependent read
             D.cnt[b] = c + m * (C_VIS + C_LIVE + C_ITEMS + (XF ? C_UP : 0u));
-            const uint32_t tp = tph != NONE ? tph : ix<L>(D.sbpos + (opos_of<L>(D, b) >> 6));
+            const uint32_t tp = tph;
             at_add(D.top + tp, m);
             at_add(D.tlive + tp, m);
             if (XF) at_add(D.tup + tp, m);
@@ -554,6 +563,7 @@ DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml,
         s += m;
     }
     D.cb = b; D.cit = it; D.cmv = mv; D.cml = ml;   // block state after the run
+    D.cvs = vs; D.cvok = vs != NONE; D.ctp = tph;
     const uint64_t t3 = tick<PROF>();
     for (uint32_t j0 = 0; j0 < k0; j0 += 64) {   // wave-uniform loop, masked store
         const uint32_t j = j0 + l, nit = lv0 + j;
@@ -698,15 +708,22 @@ DEV void load_block(Doc &D, uint32_t b, uint32_t c, uint32_t &it, u64 &mv, u64 &
 template <bool L, bool PROF, bool XF>
 DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
     uint64_t tp = tick<PROF>();
-    uint32_t b, kk = 0, tph = 0;   // tph: top position of b's superblock (first block: 0)
+    // tph: top position of b's superblock (first block: 0); vs: visible items before b
+    uint32_t b, kk = 0, tph = 0, vs = 0;
     if (pos == 0) {
         b = first_block<L>(D);
+    } else if (D.cb != NONE && D.cvok && pos - 1 >= D.cvs && pos - 1 - D.cvs < uint32_t(__popcll(D.cmv))) {
+        b = D.cb;   // the cursor's block holds visible index pos - 1
+        kk = pos - 1 - D.cvs;
+        tph = D.ctp;
+        vs = D.cvs;
     } else {
         Found f;
         if (!find_vis<L>(D, pos - 1, f)) { fail(D, ErrCheckout, 13); return; }
         b = f.b;
         kk = f.k;
         tph = f.tp;
+        vs = pos - 1 - f.k;
     }
     if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_FIND] += t - tp; tp = t; }
     const uint32_t c0 = U(ix<L>(D.cnt + b));
@@ -760,6 +777,9 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
         yjs_scan<L>(D, b, s, rb, rs, my_l, my_r, ol, orr, lv);
         if (D.err) return;
         if (b != b0) {
+            // the scan passed only not-yet-inserted items: b0's visible items all lie before
+            // the cursor and the blocks in between hold none
+            vs += uint32_t(__popcll(mv));
             if (b == D.cb) { it = D.cit; mv = D.cmv; ml = D.cml; }
             else load_block<L>(D, b, U(ix<L>(D.cnt + b)), it, mv, ml);
             tph = NONE;
@@ -767,7 +787,7 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
         if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_YJS] += t - tp; tp = t; D.prof[P_N_YJS]++; }
     }
     const uint64_t sp0 = PROF ? D.prof[P_SPLIT] : 0;
-    insert_run<L, PROF, XF>(D, b, s, it, mv, ml, lv, k, ol, orr, tph);
+    insert_run<L, PROF, XF>(D, b, s, it, mv, ml, lv, k, ol, orr, tph, vs);
     if (PROF) D.prof[P_RUN] += tick<PROF>() - tp - (D.prof[P_SPLIT] - sp0);
     D.n_items += k;
 }
@@ -780,9 +800,18 @@ DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
     uint32_t j0 = 0;
     uint32_t up_done = 0;   // XF: never-deleted items this run deleted in earlier (left) blocks
     while (j0 < n) {   // each round deletes >= 1 item or fails
-        Found f;
-        if (!find_vis<L>(D, pos, f)) { fail(D, ErrCheckout, 14); return; }
-        const uint32_t b = f.b, kk = f.k;
+        uint32_t b, kk, tpos;
+        if (D.cb != NONE && D.cvok && pos >= D.cvs && pos - D.cvs < uint32_t(__popcll(D.cmv))) {
+            b = D.cb;   // the cursor's block holds visible index pos
+            kk = pos - D.cvs;
+            tpos = D.ctp != NONE ? D.ctp : U(ix<L>(D.sbpos + (opos_of<L>(D, b) >> 6)));
+        } else {
+            Found f;
+            if (!find_vis<L>(D, pos, f)) { fail(D, ErrCheckout, 14); return; }
+            b = f.b;
+            kk = f.k;
+            tpos = f.tp;
+        }
         const uint32_t c0 = U(ix<L>(D.cnt + b));
         uint32_t it;
         u64 mv, ml;
@@ -821,14 +850,15 @@ DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
         if (l == 0) {
             st(D.m2 + 2 * size_t(b), mv & ~selm);
             D.cnt[b] = c - take * C_VIS - gone * C_UP;
-            at_add(D.top + f.tp, 0u - take);
+            at_add(D.top + tpos, 0u - take);
             if (XF) {
                 st(D.mup + b, mu & ~selm);
-                D.tup[f.tp] = ix<L>(D.tup + f.tp) - gone;
+                D.tup[tpos] = ix<L>(D.tup + tpos) - gone;
             }
         }
         wave_fence();
         D.cb = b; D.cit = it; D.cmv = mv & ~selm; D.cml = ml;
+        D.cvs = pos - kk; D.cvok = true; D.ctp = tpos;
         j0 += take;
     }
 }
@@ -937,6 +967,7 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
         if (__ballot(bad)) { fail(D, ErrCheckout, 16); return; }
         const bool flip = fv || fl;
         if (__ballot(flip && b == D.cb)) D.cb = NONE;
+        if (__ballot(fv)) D.cvok = false;   // visible items before the cursor's block may have moved
         if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_T2] += t - tq; tq = t; }
         if (L) {   // LDS index: per-lane LDS atomics
             if (flip) {
@@ -1124,6 +1155,9 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
     D.site = 0;
     D.ci = 0;
     D.cb = NONE;
+    D.cvs = 0;
+    D.ctp = NONE;
+    D.cvok = false;
     D.cit = 0;
     D.cmv = D.cml = 0;
     if (PROF) for (int i = 0; i < P_N; i++) D.prof[i] = 0;

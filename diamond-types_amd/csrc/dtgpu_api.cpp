@@ -1608,7 +1608,9 @@ static Status history_oplog(const HostOpLog &o, const std::vector<uint64_t> &ver
 // projected onto T, where a version's projection is the frontier of Hist(version) n T.  The
 // sub-oplog is compacted like history_oplog (agents, seqs and positions kept: a text op's
 // position is relative to that text alone), so the same device path checks it out.
-static Status project_oplog(const HostOpLog &o, std::vector<std::pair<uint64_t, uint64_t>> spans, HostOpLog &s) {
+static Status project_oplog(const HostOpLog &o, std::vector<std::pair<uint64_t, uint64_t>> spans, HostOpLog &s,
+                            const std::vector<std::vector<uint64_t>> *extra = nullptr,
+                            std::vector<std::vector<uint64_t>> *extra_out = nullptr) {
     std::sort(spans.begin(), spans.end());
     std::vector<std::pair<uint64_t, uint64_t>> t;   // merged, non-empty
     for (auto r : spans) {
@@ -1746,6 +1748,13 @@ static Status project_oplog(const HostOpLog &o, std::vector<std::pair<uint64_t, 
         }
     }
     s.version = project(o.version);
+    if (extra && extra_out) {   // further versions of the shared graph, projected the same way
+        extra_out->clear();
+        for (const auto &v : *extra) {
+            for (uint64_t x : v) if (x >= o.n_lv) return ErrArg;
+            extra_out->push_back(project(v));
+        }
+    }
     if (s.n_lv != nn) return ErrCheckout;
     s.finish();
     return OK;
@@ -1763,6 +1772,69 @@ dtgpu_status dtgpu_oplog_project(const dtgpu_oplog *h, const uint64_t *spans, si
     if (st != OK) { delete sub; return dtgpu_status(st); }
     *out = sub;
     return DTGPU_OK;
+}
+
+int64_t dtgpu_oplog_project_version(const dtgpu_oplog *h, const uint64_t *spans, size_t n_spans, const uint64_t *version,
+                                    size_t n_version, uint64_t *out, size_t cap) {
+    if (!h || (n_spans && !spans) || (n_version && !version) || (cap && !out)) return -1;
+    std::vector<std::pair<uint64_t, uint64_t>> t(n_spans);
+    for (size_t i = 0; i < n_spans; i++) t[i] = {spans[2 * i], spans[2 * i + 1]};
+    HostOpLog log = h->o;
+    log.finish();
+    HostOpLog sub;
+    const std::vector<std::vector<uint64_t>> vs{std::vector<uint64_t>(version, version + n_version)};
+    std::vector<std::vector<uint64_t>> pv;
+    if (project_oplog(log, t, sub, &vs, &pv) != OK || pv.size() != 1) return -1;
+    for (size_t i = 0; i < pv[0].size() && i < cap; i++) out[i] = pv[0][i];
+    return int64_t(pv[0].size());
+}
+
+// AgentAssignment::local_to_agent_version (src/causalgraph/agent_assignment/mod.rs): the agent
+// run holding lv, by binary search over the LV-ordered runs.
+dtgpu_status dtgpu_oplog_local_to_remote(const dtgpu_oplog *h, uint64_t lv, uint32_t *agent, uint64_t *seq) {
+    if (!h || !agent || !seq || lv >= h->o.n_lv) return DTGPU_ERR_ARG;
+    const auto &r = h->o.agent_runs;
+    auto it = std::upper_bound(r.begin(), r.end(), lv, [](uint64_t v, const AgentRun &a) { return v < a.lv; });
+    if (it == r.begin()) return DTGPU_ERR_ARG;
+    --it;
+    if (lv >= it->lv + it->len) return DTGPU_ERR_ARG;
+    *agent = it->agent;
+    *seq = it->seq + (lv - it->lv);
+    return DTGPU_OK;
+}
+
+// The local LV spans of the remote span (agent, seq .. seq + n), in seq order
+// (AgentAssignment::remote_to_local_version over a span): binary search over the agent's runs,
+// which are seq-ordered whenever the agent's ops arrived in seq order (a linear pass otherwise).
+// Returns the span count, or -1 when part of the span is not in the oplog.
+int64_t dtgpu_oplog_remote_to_local(const dtgpu_oplog *h, uint32_t agent, uint64_t seq, uint64_t n, uint64_t *spans,
+                                    size_t cap) {
+    if (!h || agent >= h->o.agent_seqs.size() || (cap && !spans)) return -1;
+    const auto &v = h->o.agent_seqs[agent];
+    const auto by_seq = [](const SeqRun &a, const SeqRun &b) { return a.seq < b.seq; };
+    std::vector<SeqRun> hit;
+    const uint64_t end = seq + n;
+    if (std::is_sorted(v.begin(), v.end(), by_seq)) {
+        auto it = std::upper_bound(v.begin(), v.end(), seq, [](uint64_t x, const SeqRun &r) { return x < r.seq; });
+        if (it != v.begin()) --it;
+        for (; it != v.end() && it->seq < end; ++it)
+            if (it->seq + it->len > seq) hit.push_back(*it);
+    } else {
+        for (const SeqRun &r : v)
+            if (r.seq < end && r.seq + r.len > seq) hit.push_back(r);
+        std::sort(hit.begin(), hit.end(), by_seq);
+    }
+    size_t k = 0;
+    uint64_t at = seq;
+    for (const SeqRun &r : hit) {
+        if (r.seq + r.len <= at) continue;
+        if (r.seq > at) return -1;   // a gap: that seq is not known here
+        const uint64_t hi = std::min(end, r.seq + r.len);
+        if (k < cap) { spans[2 * k] = r.lv + (at - r.seq); spans[2 * k + 1] = r.lv + (hi - r.seq); }
+        k++;
+        at = hi;
+    }
+    return at == end ? int64_t(k) : -1;
 }
 
 dtgpu_status dtgpu_oplog_history(const dtgpu_oplog *h, const uint64_t *version, size_t n_version, dtgpu_oplog **out) {

@@ -110,6 +110,11 @@ def lib():
     L.dtgpu_oplog_dominators.restype = ctypes.c_int64
     L.dtgpu_oplog_history.argtypes = [vp, pu64, sz, ctypes.POINTER(vp)]
     L.dtgpu_oplog_project.argtypes = [vp, pu64, sz, ctypes.POINTER(vp)]
+    L.dtgpu_oplog_project_version.argtypes = [vp, pu64, sz, pu64, sz, pu64, sz]
+    L.dtgpu_oplog_project_version.restype = i64
+    L.dtgpu_oplog_local_to_remote.argtypes = [vp, u64, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(u64)]
+    L.dtgpu_oplog_remote_to_local.argtypes = [vp, ctypes.c_uint32, u64, u64, pu64, sz]
+    L.dtgpu_oplog_remote_to_local.restype = i64
     L.dtgpu_oplog_encode.argtypes = [vp, pu64, sz, ctypes.c_uint32, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
     L.dtgpu_lz4_compress.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
     L.dtgpu_oplog_decode_and_add.argtypes = [vp, ctypes.c_char_p, sz, c, pu64, sz, ctypes.POINTER(sz)]
@@ -549,6 +554,42 @@ class ListOpLog:
         out = ctypes.c_void_p()
         _check(lib().dtgpu_oplog_project(self._h, p, len(flat) // 2, ctypes.byref(out)))
         return ListOpLog(out.value)
+
+    def project_version(self, spans, version):
+        """A version of this oplog projected onto the sub-oplog of `spans` (the numbering
+        `project(spans)` gives): the frontier of Hist(version) n spans
+        (Graph::project_onto_subgraph_raw; dtgpu_oplog_project_version)."""
+        flat = [int(x) for s in spans for x in s]
+        p = (ctypes.c_uint64 * max(1, len(flat)))(*flat)
+        pv, nv = _u64s(version)
+        cap = max(1, len(flat))
+        out = (ctypes.c_uint64 * cap)()
+        n = lib().dtgpu_oplog_project_version(self._h, p, len(flat) // 2, pv, nv, out, cap)
+        if n < 0:
+            raise ValueError("bad spans or version")
+        if n > cap:
+            out = (ctypes.c_uint64 * n)()
+            n = lib().dtgpu_oplog_project_version(self._h, p, len(flat) // 2, pv, nv, out, n)
+        return list(out[:n])
+
+    def local_to_remote(self, lv):
+        """AgentAssignment::local_to_agent_version: LV -> (agent id, seq)."""
+        a, q = ctypes.c_uint32(), ctypes.c_uint64()
+        _check(lib().dtgpu_oplog_local_to_remote(self._h, lv, ctypes.byref(a), ctypes.byref(q)))
+        return a.value, q.value
+
+    def remote_to_local(self, agent, seq, n=1):
+        """Local LV spans [(start, end)] of the remote span (agent id, seq .. seq + n), in seq
+        order; KeyError when part of it is unknown here."""
+        cap = 8
+        while True:
+            buf = (ctypes.c_uint64 * (2 * cap))()
+            k = lib().dtgpu_oplog_remote_to_local(self._h, agent, seq, n, buf, cap)
+            if k < 0:
+                raise KeyError((agent, seq, n))
+            if k <= cap:
+                return [(buf[2 * i], buf[2 * i + 1]) for i in range(k)]
+            cap = k
 
     def checkout_text_bytes(self, spans) -> bytes:
         """OpLog::checkout_text (src/oplog.rs:388-394) for the text whose ops are `spans`: the

@@ -18,7 +18,7 @@ graph's ops after a version (`encode_from`, merged with `decode_and_add`, which 
 receiver has) plus the map / text ownership of each op keyed by its remote id (agent name, seq),
 so two replicas converge whatever the merge order.
 """
-from . import ListOpLog
+from . import ListBranch, ListOpLog
 
 ROOT_CRDT_ID = (1 << 64) - 1   # usize::MAX (src/lib.rs:332)
 _PLACEHOLDER = "\x00"           # a map set's LV in the shared list
@@ -60,26 +60,28 @@ class OpLog:
     def _names(self):
         return self.log.export("agent_names")
 
+    def _agent_of_name(self, name):
+        names = self._names()
+        for a, n in enumerate(names):
+            if n == name:
+                return a
+        raise KeyError(name)
+
     def remote_id(self, lv):
-        """LV -> (agent name, seq) (AgentAssignment::local_to_agent_version)."""
+        """LV -> (agent name, seq) (AgentAssignment::local_to_agent_version; a binary search in
+        the native agent runs, dtgpu_oplog_local_to_remote)."""
         if lv == ROOT_CRDT_ID:
             return ("ROOT", 0)
-        runs = self.log.export("agent_runs").reshape(-1, 4)
-        for s, n, a, q in runs:
-            if s <= lv < s + n:
-                return (self._names()[a], int(q) + (lv - int(s)))
-        raise KeyError(lv)
+        if not 0 <= lv < len(self.log):
+            raise KeyError(lv)
+        a, q = self.log.local_to_remote(lv)
+        return (self._names()[a], q)
 
     def local_id(self, rid):
         if rid == ("ROOT", 0):
             return ROOT_CRDT_ID
         name, seq = rid
-        names = self._names()
-        runs = self.log.export("agent_runs").reshape(-1, 4)
-        for s, n, a, q in runs:
-            if names[a] == name and q <= seq < q + n:
-                return int(s) + (seq - int(q))
-        raise KeyError(rid)
+        return self.log.remote_to_local(self._agent_of_name(name), seq, 1)[0][0]
 
     # ---- maps ------------------------------------------------------------------------------------
     def _create(self, v, value):
@@ -160,20 +162,10 @@ class OpLog:
         self.owner[start] = ("text", crdt, end - start)
 
     def local_spans(self, rid, n):
-        """Local LV spans of the remote ids (name, seq .. seq + n), in seq order."""
+        """Local LV spans of the remote ids (name, seq .. seq + n), in seq order
+        (dtgpu_oplog_remote_to_local: a binary search in the agent's seq runs)."""
         name, seq = rid
-        names = self._names()
-        out = []
-        for s, ln, a, q in self.log.export("agent_runs").reshape(-1, 4):
-            s, ln, q = int(s), int(ln), int(q)
-            if names[a] != name:
-                continue
-            lo, hi = max(seq, q), min(seq + n, q + ln)
-            if lo < hi:
-                out.append((lo - q + s, hi - q + s, lo))
-        out.sort(key=lambda x: x[2])
-        assert sum(e - b for b, e, _ in out) == n, "remote run not fully present"
-        return [(b, e) for b, e, _ in out]
+        return [(int(b), int(e)) for b, e in self.log.remote_to_local(self._agent_of_name(name), seq, n)]
 
     def local_text_op(self, agent: int, crdt: int, op):
         """op: ("ins", pos, content) or ("del", start, end) (TextOperation::new_insert /
@@ -207,6 +199,25 @@ class OpLog:
 
     def checkout_text(self, crdt: int) -> str:
         return self.checkout_text_bytes(crdt).decode()
+
+    def merge_text_into(self, crdt: int, content: str, frm, merge_frontier=None) -> str:
+        """TextInfo::merge_into(into, cg, from, merge_frontier) (src/listmerge/merge.rs:1022-1054,
+        via with_xf_iter :954-985): the text's ops with the shared graph projected onto them
+        (dtgpu_oplog_project), `from` and `merge_frontier` projected the same way
+        (project_onto_subgraph_raw), and the transformed operations between the two -- replayed
+        on the device (dtgpu_xf_operations_from, f1) -- applied to `content`, the text as the
+        branch holds it at `from`."""
+        spans = self._text(crdt)
+        if merge_frontier is None:
+            merge_frontier = self.version()
+        if not spans:
+            return content
+        sub = self.log.project(spans)
+        pf = self.log.project_version(spans, list(frm))
+        pm = self.log.project_version(spans, list(merge_frontier))
+        b = ListBranch(content.encode(), pf)
+        b.merge(sub, pm)
+        return b.content()
 
     def checkout(self, crdt=ROOT_CRDT_ID):
         """OpLog::checkout / checkout_map (oplog.rs:396-426): registers resolved, child maps and
@@ -265,3 +276,28 @@ class OpLog:
                 else:
                     merged.append((b, e))
             self.texts[crdt] = merged
+
+
+class Branch:
+    """`Branch` (src/branch.rs): a checkout of every CRDT of an `OpLog` at `frontier`.  Texts are
+    kept as strings and moved forward with TextInfo::merge_into (branch.rs:180-232,
+    merge_changes_to_tip); registers and maps are resolved from the oplog at the branch's version
+    (only the tip is supported for them, as merge_changes_to_tip moves the branch there)."""
+
+    def __init__(self):
+        self.frontier = []
+        self.texts = {}
+
+    def merge_changes_to_tip(self, oplog: OpLog) -> None:
+        """Branch::merge_changes_to_tip (branch.rs:180-232): every text CRDT's new ops are merged
+        into this branch's copy of it, from the branch's frontier to the oplog's tip."""
+        tip = oplog.version()
+        for crdt, spans in oplog.texts.items():
+            if not spans:
+                self.texts.setdefault(crdt, "")
+                continue
+            self.texts[crdt] = oplog.merge_text_into(crdt, self.texts.get(crdt, ""), self.frontier, tip)
+        self.frontier = list(tip)
+
+    def text(self, crdt: int) -> str:
+        return self.texts.get(crdt, "")

@@ -192,6 +192,21 @@ size_t dtgpu_oplog_xf_order(const dtgpu_oplog *oplog, const uint64_t *from, size
  * the frontier of its history restricted to the spans), LVs compacted in order, agents / seqs /
  * positions unchanged.  Its tip checkout (dtgpu_checkout_tip, on the device) is the text. */
 dtgpu_status dtgpu_oplog_project(const dtgpu_oplog *oplog, const uint64_t *spans, size_t n_spans, dtgpu_oplog **out);
+/* The projection of a version of the shared graph onto the sub-oplog of `spans`
+ * (Graph::project_onto_subgraph_raw, src/causalgraph/graph/subgraph.rs; used by
+ * TextInfo::with_xf_iter, src/listmerge/merge.rs:954-985): the frontier of Hist(version) n spans
+ * in the sub-oplog's LVs (the numbering dtgpu_oplog_project gives).  Writes up to cap LVs and
+ * returns the frontier's size, or -1 on bad arguments. */
+int64_t dtgpu_oplog_project_version(const dtgpu_oplog *oplog, const uint64_t *spans, size_t n_spans,
+                                    const uint64_t *version, size_t n_version, uint64_t *out, size_t cap);
+/* AgentAssignment::local_to_agent_version (src/causalgraph/agent_assignment/mod.rs): the
+ * (agent, seq) of a local LV. */
+dtgpu_status dtgpu_oplog_local_to_remote(const dtgpu_oplog *oplog, uint64_t lv, uint32_t *agent, uint64_t *seq);
+/* The local LV spans [start, end) of the remote span (agent, seq .. seq + n), in seq order
+ * (AgentAssignment::remote_to_local_version, span form).  Writes up to cap pairs and returns
+ * their count, or -1 when part of the span is unknown to this oplog. */
+int64_t dtgpu_oplog_remote_to_local(const dtgpu_oplog *oplog, uint32_t agent, uint64_t seq, uint64_t n,
+                                    uint64_t *spans, size_t cap);
 /* The history of `version` as an oplog of its own (what ListOpLog::checkout(&[LV]) replays:
  * diff_rev(version, ROOT), src/causalgraph/graph/tools.rs:176-292), LVs compacted in order,
  * agents / seqs / positions unchanged; its tip checkout is the checkout at `version`. */

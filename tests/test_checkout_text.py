@@ -256,3 +256,22 @@ def test_projection_matches_reference_subgraph_kats(kat):
             want[t_of[v]] = sorted(t_of[p] for p in ps) if v == run[0] else [t_of[v] - 1]
     assert got == want, (kat, got, want)
     assert sorted(int(x) for x in sub.local_frontier()) == sorted(t_of[v] for v in expect_frontier)
+
+
+@pytest.mark.parametrize("kat", range(len(SUBGRAPH_KATS)))
+def test_project_version_matches_reference_subgraph_kats(kat):
+    """Graph::project_onto_subgraph_raw as the reference's KATs state it (subgraph.rs:353-380):
+    the projection of `frontier` onto the filter, over fancy_graph itself (dtgpu_oplog_project_version;
+    projected LVs are the filter's LVs in ascending order)."""
+    filt, frontier, _parents, expect_frontier = SUBGRAPH_KATS[kat]
+    members = [v for a, b in sorted(filt) for v in range(a, b)]
+    idx = {v: i for i, v in enumerate(members)}
+    assert _fancy_oplog().project_version(filt, frontier) == sorted(idx[v] for v in expect_frontier)
+
+
+def test_project_version_of_the_tip_is_the_sub_oplog_frontier():
+    a = dt_amd.ListOpLog.load_from(G.dt_bytes("friendsforever"))
+    c, a_spans, b_spans, _n = _interleave(a, 3)
+    for spans in (a_spans, b_spans):
+        assert c.project_version(spans, c.local_frontier()) == c.project(spans).local_frontier()
+        assert c.project_version(spans, []) == []
