@@ -63,7 +63,6 @@ struct BatchParams {
     unsigned long long *mup;
     uint32_t *tup;
     uint32_t *xf;
-    unsigned long long *rows;   // span replay: SPAN_NS spans per block (first LV | (len, ever_deleted, state) << 32)
 };
 
 // Superblock capacity for an index of `mb` blocks: every superblock but the first holds >= 32
@@ -90,38 +89,6 @@ __host__ __device__ inline uint32_t lds_sb_capacity(uint32_t mb, uint32_t fill =
     return opt < sb_capacity(mb) ? opt : sb_capacity(mb);
 }
 constexpr uint32_t MAX_DOC_BLOCKS = 65535;   // block ids are u16 in the superblock lists
-
-// ---- span replay (dt_span.hip) ----------------------------------------------------------------
-// A block holds up to SPAN_NS spans (8 B each: first LV, len | ever_deleted | state).  Every block
-// but the first keeps >= 31 spans (a block splits only when it cannot take 2 more), every span
-// holds >= 1 inserted char, so n_ins / 31 + 2 blocks always suffice.
-constexpr uint32_t SPAN_NS = 64;
-__host__ __device__ inline uint64_t span_max_blocks(uint64_t n_ins) { return n_ins / 31 + 2; }
-__host__ __device__ constexpr uint32_t span_sb_capacity(uint32_t mb) { return mb / 32 + 2; }
-// Bytes of a span index for mb blocks / ms superblocks (dt_span.hip bind_index).  u32 words: per
-// block visible items and span / live-span counts (+ never-deleted items in transformed-ops mode);
-// per superblock visible / live totals, id and block count by top position, block count and top
-// position by id (+ never-deleted total).  Then the per-block (superblock, index) position and the
-// 64-entry superblock block lists: u16 when `narrow` (LDS tiers), u32 otherwise.
-__host__ __device__ constexpr uint64_t span_index_bytes(uint64_t mb, uint64_t ms, bool narrow, bool xf = false) {
-    const uint64_t w = (xf ? 3 : 2) * mb + (xf ? 7 : 6) * ms;
-    const uint64_t e = mb + 64 * ms;
-    return (4 * w + (narrow ? 2 : 4) * e + 15) & ~uint64_t(15);
-}
-// LDS tiers size the index for the expected span count (DTGPU_LDS_FILL: inserted chars per
-// block); a document that outgrows it is handed to the HBM tier.
-constexpr uint32_t SPAN_LDS_FILL = 96;
-__host__ __device__ inline uint32_t span_lds_blocks(uint64_t n_ins, uint64_t fill) {
-    const uint64_t est = n_ins / fill + 16, mx = span_max_blocks(n_ins);
-    return uint32_t(est < mx ? est : mx);
-}
-__host__ __device__ constexpr uint32_t span_lds_sb(uint32_t mb) {
-    return mb / 40 + 3 < mb / 32 + 2 ? mb / 40 + 3 : mb / 32 + 2;
-}
-// LDS tiers of the span replay: compile-time block capacities (the index offsets become
-// immediates); a document goes to the smallest tier holding its expected block count.
-constexpr int kSpanTiers = 4;
-constexpr uint32_t kSpanTierBlocks[kSpanTiers] = {320, 1280, 4096, 11000};
 
 // ---- device planner (dt_plan.hip) -------------------------------------------------------------
 constexpr uint32_t PLAN_MAX_AGENTS = 512;
@@ -184,9 +151,6 @@ struct ReplayLaunch {
                                     // prep / plan / replay; s joins it before the HBM tier always
 };
 int launch_replay(const ReplayLaunch &r);
-// The same pass on the span tracker (dt_span.hip): BatchParams.rows holds the span blocks,
-// .pos the per-LV link word, .gidx the span indexes (span_index_bytes).
-int launch_span_replay(const ReplayLaunch &r);
 // Transformed-ops replay of large's documents (HBM index tier): BaseMoved positions per LV.
 int launch_replay_xf(const BatchParams &large, void *stream);
 

@@ -4,10 +4,16 @@
 
 namespace dtgpu {
 
-constexpr uint32_t GQ_MAX_FRONTIER = 16;
+// Frontiers have no size cap (the reference's are SmallVecs): a query's versions live in a
+// frontier arena, its common frontier / dominators in a common arena.  The heap walks run with
+// their queues in LDS (first pass); a query whose queue outgrows LDS -- or whose time points carry
+// more than GQ_LDS_MERGED merged versions -- is answered again in a second pass with its queues in
+// HBM scratch sized from its graph (no capacity limit).
+constexpr uint32_t GQ_LDS_MERGED = 16;
 enum : uint32_t { GQ_DIFF = 0, GQ_CONFLICT = 1, GQ_CONTAINS = 2, GQ_DOMINATORS = 3, GQ_DIFF_LEVEL = 4,
                   GQ_CONFLICT_LEVEL = 5 };
-enum : uint32_t { GQ_OK = 0, GQ_OVERFLOW = 1, GQ_BAD_INPUT = 2 };
+// statuses (0..2 public; GQ_QUEUE_FULL is internal: the query moves to the HBM pass)
+enum : uint32_t { GQ_OK = 0, GQ_OVERFLOW = 1, GQ_BAD_INPUT = 2, GQ_QUEUE_FULL = 3 };
 
 // Graph arena: per graph, n_ent + 1 quads (start, end, shadow, parents offset); the extra quad
 // carries the parents end offset.  Parents are absolute offsets into one parents array.
@@ -16,12 +22,15 @@ struct GraphQuery {
     int32_t target;                      // CONTAINS (-1 = ROOT)
     uint64_t scr_off;                    // level kinds: per-query HBM scratch (LevelParams.qscr)
     uint32_t scr_tp, pad;                // CONFLICT_LEVEL: time-point pool capacity
-    int32_t a[GQ_MAX_FRONTIER], b[GQ_MAX_FRONTIER];
+    uint32_t f_off;                      // a = front[f_off, +na), b = front[f_off + na, +nb)
+    uint32_t c_off, c_cap;               // common[c_off, +c_cap)
+    uint32_t max_par;                    // the most parents of any entry of the query's graph
+    uint64_t h_off;                      // HBM pass: heap scratch (GraphParams.hscr words)
+    uint32_t hk_cap, htp_cap;            // HBM pass: key heap / time-point heap capacities
 };
 
 struct GraphResult {
     uint32_t status, n0, n1, n_common;   // DIFF: spans only-a / only-b; CONFLICT: spans; CONTAINS: n0 = 0/1
-    int32_t common[GQ_MAX_FRONTIER];     // CONFLICT: the common frontier; DOMINATORS: the result
 };
 
 struct GraphParams {
@@ -31,17 +40,44 @@ struct GraphParams {
     const GraphQuery *queries;
     GraphResult *results;
     uint32_t n_queries;
+    const int32_t *front;                // frontier arena
+    int32_t *common;                     // CONFLICT: the common frontier; DOMINATORS: the result
+    uint32_t *hscr;                      // HBM pass heap scratch
 };
 
-int launch_graph_queries(const GraphParams &p, void *stream);
+// Heap scratch of a query in the HBM pass (words): a key heap of one entry per parent slot of the
+// graph and per version element, and a time-point heap whose points are (4 + widest version)
+// words each (see dt_graph.hip).
+__host__ __device__ inline uint32_t gq_key_cap(uint64_t n_par, uint32_t na, uint32_t nb) { return uint32_t(n_par + na + nb + 4); }
+__host__ __device__ inline uint32_t gq_tp_cap(uint64_t n_ent, uint64_t n_par, uint32_t na, uint32_t nb) {
+    return uint32_t(n_ent + n_par + na + nb + 8);
+}
+__host__ __device__ inline uint32_t gq_tp_words(uint32_t max_par, uint32_t na, uint32_t nb) {
+    uint32_t w = max_par;
+    if (na > w) w = na;
+    if (nb > w) w = nb;
+    return 4 + w;
+}
+
+// big = false: every heap-walk query, queues in LDS; big = true: only the queries the first launch
+// left at GQ_QUEUE_FULL, queues in HBM scratch (GraphQuery.h_off / hk_cap / htp_cap)
+int launch_graph_queries(const GraphParams &p, void *stream, bool big);
 
 // Level-synchronous kernels (dt_level.hip).  Per-entry arrays are indexed like the entry quads
 // (graph g's entry e at ent_off + e; every graph owns n_ent + 1 slots), per-slot arrays like
 // the parents array.  All per-entry state is in HBM (no size cap): the levelling's counters
 // (3 words per entry slot, at 3 * ent_off), each level query's marks (and, for conflict spans,
 // bucket heads and a time-point pool) at its scr_off.
-inline uint64_t conflict_level_words(uint64_t n_ent, uint64_t n_par) { return 4 * n_ent + 4 * (34 + n_ent + n_par); }
-inline uint32_t conflict_level_tps(uint64_t n_ent, uint64_t n_par) { return uint32_t(34 + n_ent + n_par); }
+// Time points of a level conflict query: the two versions, one per visited entry (its parents) and
+// one per version element or parent slot a merge point shatters into.
+inline uint32_t conflict_level_tps(uint64_t n_ent, uint64_t n_par, uint32_t na, uint32_t nb) {
+    return uint32_t(4 + n_ent + n_par + na + nb);
+}
+// marks (2 words per entry), bucket heads, candidates, the time-point pool (4 words each) and an
+// HBM bucket for entries that more than BUCKET_CAP points enter (one word per point)
+inline uint64_t conflict_level_words(uint64_t n_ent, uint64_t n_par, uint32_t na, uint32_t nb) {
+    return 4 * n_ent + 5ull * conflict_level_tps(n_ent, n_par, na, nb);
+}
 struct LevelGraph { uint32_t ent_off, n_ent; };
 // The query kernels keep the marks (2 words per entry) in LDS when every levelled graph of the
 // launch has at most this many entries (48 KiB; sized to the largest graph, so small graphs keep

@@ -138,15 +138,15 @@ __global__ __launch_bounds__(256) void level_kernel(LevelParams P) {
 }
 
 // The marks of a query (see the header), level by level.  Every thread returns the same status.
-__device__ uint32_t push_marks(const LevelParams &P, const GraphQuery &q, const Ent *E, int32_t *mA, int32_t *mB,
-                               uint32_t *s_top, uint32_t *s_st) {
+__device__ uint32_t push_marks(const LevelParams &P, const GraphQuery &q, const int32_t *qa, const Ent *E, int32_t *mA,
+                               int32_t *mB, uint32_t *s_top, uint32_t *s_st) {
     const uint32_t t = threadIdx.x, n = q.n_ent, base = q.ent_off;
     for (uint32_t e = t; e < n; e += NT) { mA[e] = -1; mB[e] = -1; }
     __syncthreads();
     if (t == 0) {   // seed the marks with the two versions
         uint32_t top = 0, st = GQ_OK;
         for (uint32_t i = 0; i < q.na + q.nb && st == GQ_OK; i++) {
-            const int32_t v = i < q.na ? q.a[i] : q.b[i - q.na];
+            const int32_t v = qa[i];   // a then b: one run in the frontier arena
             const uint32_t e = find(E, n, v);
             if (e == n) { st = GQ_BAD_INPUT; break; }
             int32_t *m = i < q.na ? mA : mB;
@@ -210,14 +210,14 @@ __global__ __launch_bounds__(256) void level_diff_kernel(LevelParams P, GraphPar
     const uint32_t n = q.n_ent, base = q.ent_off;
     const uint32_t *meta = P.meta + 2 * size_t(base);
     GraphResult *res = Q.results + qi;
-    if (meta[1] != GQ_OK || q.na > GQ_MAX_FRONTIER || q.nb > GQ_MAX_FRONTIER) {
-        if (t == 0) { res->status = meta[1] != GQ_OK ? meta[1] : GQ_BAD_INPUT; res->n0 = res->n1 = res->n_common = 0; }
+    if (meta[1] != GQ_OK) {
+        if (t == 0) { res->status = meta[1]; res->n0 = res->n1 = res->n_common = 0; }
         return;
     }
     const Ent *E = reinterpret_cast<const Ent *>(P.ents) + base;
     extern __shared__ int32_t lmarks[];   // P.lds_ent > 0: the marks live in LDS
     int32_t *mA = P.lds_ent ? lmarks : reinterpret_cast<int32_t *>(P.qscr + q.scr_off), *mB = mA + n;
-    const uint32_t st = push_marks(P, q, E, mA, mB, &s_top, &s_st);
+    const uint32_t st = push_marks(P, q, Q.front + q.f_off, E, mA, mB, &s_top, &s_st);
     if (st != GQ_OK) {
         if (t == 0) { res->status = st; res->n0 = res->n1 = res->n_common = 0; }
         return;
@@ -244,7 +244,7 @@ __global__ __launch_bounds__(256) void level_diff_kernel(LevelParams P, GraphPar
 enum : uint32_t { F_A = 0, F_B = 1, F_S = 2 };
 enum : uint32_t { TP_ONE = 0, TP_PARENTS = 1, TP_QA = 2, TP_QB = 3 };
 constexpr int32_t ROOT_LV = -1;
-constexpr uint32_t BUCKET_CAP = 64;   // time points that enter one entry (else GQ_OVERFLOW)
+constexpr uint32_t BUCKET_CAP = 64;   // time points that enter one entry sorted in LDS (more: in HBM)
 
 // A time point (the reference's TimePoint + DiffFlag) in the query's pool: 4 words
 // {next in its bucket, flag | kind << 2, frontier size, reference}: a single LV (TP_ONE: ref =
@@ -252,7 +252,7 @@ constexpr uint32_t BUCKET_CAP = 64;   // time points that enter one entry (else 
 struct Sweep {
     const Ent *E;
     const uint32_t *par;
-    const GraphQuery *q;
+    const int32_t *qa, *qb;   // the two versions (frontier arena)
     int32_t *head;
     uint32_t *pool;
     uint32_t n, cap, used, npend;
@@ -263,8 +263,8 @@ struct Sweep {
         switch (w[1] >> 2) {
             case TP_ONE: return int32_t(w[3]);
             case TP_PARENTS: return int32_t(par[E[w[3]].poff + k]);
-            case TP_QA: return q->a[k];
-            default: return q->b[k];
+            case TP_QA: return qa[k];
+            default: return qb[k];
         }
     }
     __device__ uint32_t size(uint32_t tp) const { return pool[4 * size_t(tp) + 2]; }
@@ -304,7 +304,7 @@ struct Sweep {
 __global__ __launch_bounds__(256) void level_conflict_kernel(LevelParams P, GraphParams Q) {
     __shared__ uint32_t s_top, s_st, s_ncand;
     __shared__ uint32_t s_sum[NT];
-    __shared__ uint32_t bk[BUCKET_CAP];
+    __shared__ uint32_t bkl[BUCKET_CAP];
     const uint32_t qi = blockIdx.x, t = threadIdx.x;
     if (qi >= Q.n_queries) return;
     const GraphQuery &q = Q.queries[qi];
@@ -314,26 +314,28 @@ __global__ __launch_bounds__(256) void level_conflict_kernel(LevelParams P, Grap
     GraphResult *res = Q.results + qi;
     const Ent *E = reinterpret_cast<const Ent *>(P.ents) + base;
     uint32_t *out = Q.out + size_t(q.out_off);
-    if (meta[1] != GQ_OK || q.na > GQ_MAX_FRONTIER || q.nb > GQ_MAX_FRONTIER) {
-        if (t == 0) { res->status = meta[1] != GQ_OK ? meta[1] : GQ_BAD_INPUT; res->n0 = res->n_common = 0; }
+    if (meta[1] != GQ_OK) {
+        if (t == 0) { res->status = meta[1]; res->n0 = res->n_common = 0; }
         return;
     }
+    const int32_t *qa = Q.front + q.f_off, *qb = qa + q.na;
+    int32_t *common = Q.common + q.c_off;   // written by thread 0 only
     // the reference's short circuits (tools.rs:445-480), decided by thread 0 for the group
     if (t == 0) {
         uint32_t st = 0xFFFFFFFFu;   // 0xFFFFFFFF: no short circuit
         bool same = q.na == q.nb;
-        for (uint32_t i = 0; same && i < q.na; i++) same = q.a[i] == q.b[i];
+        for (uint32_t i = 0; same && i < q.na; i++) same = qa[i] == qb[i];
         RevSpans sp{out, q.out_cap / 3, 0, 3, 0, 0, 0, false, false};
         uint32_t nc = 0;
         if (same) {
-            for (uint32_t i = 0; i < q.na; i++) res->common[nc++] = q.a[i];
-            st = GQ_OK;
-        } else if (q.na == 1 && q.nb == 1) {
-            const int32_t x = q.a[0], y = q.b[0];
+            st = q.na <= q.c_cap ? GQ_OK : GQ_OVERFLOW;
+            for (uint32_t i = 0; i < q.na && i < q.c_cap; i++) common[nc++] = qa[i];
+        } else if (q.na == 1 && q.nb == 1 && q.c_cap) {
+            const int32_t x = qa[0], y = qb[0];
             const uint32_t ex = find(E, n, x), ey = find(E, n, y);
             if (ex == n || ey == n) st = GQ_BAD_INPUT;
-            else if (x > y && y >= E[ex].start) { sp.push(y + 1, x + 1, F_A); res->common[nc++] = y; st = GQ_OK; }
-            else if (y > x && x >= E[ey].start) { sp.push(x + 1, y + 1, F_B); res->common[nc++] = x; st = GQ_OK; }
+            else if (x > y && y >= E[ex].start) { sp.push(y + 1, x + 1, F_A); common[nc++] = y; st = GQ_OK; }
+            else if (y > x && x >= E[ey].start) { sp.push(x + 1, y + 1, F_B); common[nc++] = x; st = GQ_OK; }
         }
         if (st != 0xFFFFFFFFu) {
             sp.flush();
@@ -352,7 +354,7 @@ __global__ __launch_bounds__(256) void level_conflict_kernel(LevelParams P, Grap
     uint32_t *cand = reinterpret_cast<uint32_t *>(head + n);
     uint32_t *pool = cand + n;
     for (uint32_t e = t; e < n; e += NT) head[e] = -1;
-    const uint32_t mst = push_marks(P, q, E, mA, mB, &s_top, &s_st);
+    const uint32_t mst = push_marks(P, q, qa, E, mA, mB, &s_top, &s_st);
     if (mst != GQ_OK) {
         if (t == 0) { res->status = mst; res->n0 = res->n_common = 0; }
         return;
@@ -383,7 +385,8 @@ __global__ __launch_bounds__(256) void level_conflict_kernel(LevelParams P, Grap
     }
     if (t != 0) return;
     // ---- the sweep (one thread) ----
-    Sweep S{E, P.par, &q, head, pool, n, q.scr_tp, 0, 0, false};
+    Sweep S{E, P.par, qa, qb, head, pool, n, q.scr_tp, 0, 0, false};
+    uint32_t *hbk = pool + 4 * size_t(q.scr_tp);   // an entry's bucket past BUCKET_CAP points
     RevSpans sp{out, q.out_cap / 3, 0, 3, 0, 0, 0, false, false};
     // a span's flag is its membership: x in H(a) iff x <= mA[e], in H(b) iff x <= mB[e]
     auto mflag = [&](uint32_t e, int32_t x) -> uint32_t {
@@ -405,15 +408,17 @@ __global__ __launch_bounds__(256) void level_conflict_kernel(LevelParams P, Grap
         }
         if (S.overflow) { st = GQ_OVERFLOW; break; }
         if (e < 0) break;   // only ROOT points left: nothing in common
-        // the bucket in heap order (insertion sort; buckets are small)
+        // the bucket in heap order (insertion sort; buckets are small -- in LDS up to BUCKET_CAP
+        // points, in the query's HBM scratch beyond)
         uint32_t m = 0;
+        for (int32_t x = head[e]; x >= 0; x = int32_t(pool[4 * size_t(x)])) m++;
+        uint32_t *bk = m <= BUCKET_CAP ? bkl : hbk;
+        m = 0;
         for (int32_t x = head[e]; x >= 0; x = int32_t(pool[4 * size_t(x)])) {
-            if (m == BUCKET_CAP) { st = GQ_OVERFLOW; break; }
             uint32_t j = m++;
             while (j > 0 && S.before(uint32_t(x), bk[j - 1])) { bk[j] = bk[j - 1]; j--; }
             bk[j] = uint32_t(x);
         }
-        if (st != GQ_OK) break;
         head[e] = -1;
         // pop the top point and its duplicates
         const uint32_t T = bk[0];
@@ -427,8 +432,8 @@ __global__ __launch_bounds__(256) void level_conflict_kernel(LevelParams P, Grap
         }
         if (S.npend == 0) {   // collapsed to one point: the common version
             const uint32_t sz = S.size(T);
-            if (sz > GQ_MAX_FRONTIER) { st = GQ_OVERFLOW; break; }
-            for (uint32_t k = 0; k < sz; k++) res->common[nc++] = S.elem(T, k);
+            if (sz > q.c_cap) { st = GQ_OVERFLOW; break; }
+            for (uint32_t k = 0; k < sz; k++) common[nc++] = S.elem(T, k);
             break;
         }
         for (uint32_t k = 0; k + 1 < S.size(T); k++) S.push(TP_ONE, uint32_t(S.elem(T, k)), 1, flag);   // shatter
@@ -446,7 +451,8 @@ __global__ __launch_bounds__(256) void level_conflict_kernel(LevelParams P, Grap
             for (uint32_t k = 0; k + 1 < S.size(u); k++) S.push(TP_ONE, uint32_t(S.elem(u, k)), 1, S.flag(u));
             if (S.flag(u) != flag) flag = F_S;
             if (S.npend == 0) {   // nothing left but this point: it is the common version
-                res->common[nc++] = re - 1;
+                if (!q.c_cap) { st = GQ_OVERFLOW; stopped = true; break; }
+                common[nc++] = re - 1;
                 stopped = true;
                 break;
             }

@@ -129,6 +129,13 @@ DEV uint32_t pc_of(uint32_t b, uint32_t k) { return b | (k << 16); }
 // accesses, which the CU keeps coherent for that wave: plain loads may hit L1.  The HBM-index
 // words that the HBM tier updates with memory-side atomics are read L2-coherently (ld_sc).
 template <typename T> DEV T ld(const T *p) { return *p; }
+// Cold state (kernel arguments and document descriptor fields used only at the end of a document
+// or on rare paths) is re-read where it is used: volatile, so the compiler neither keeps it in
+// SGPRs across the command loop nor spills it there (the hot loop is SGPR-bound).
+template <typename T> DEV T vld(const T *p) { return *reinterpret_cast<const volatile T *>(p); }
+DEV const BatchParams &KP() {
+    return *(const BatchParams *)(__builtin_amdgcn_kernarg_segment_ptr());
+}
 template <typename T> DEV void st(T *p, T v) { *p = v; }
 // L2-coherent accesses (a load must never meet a stale L1 line of a word an atomic changed).
 template <typename T> DEV T ld_sc(const T *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
@@ -154,11 +161,7 @@ struct Doc {
     const Cmd *cmds;
     uint32_t ncmd, n_lv;
     const uint32_t *tlist;
-    const uint32_t *cbyte;
-    const uint8_t *content;
-    const uint32_t *aruns;
-    uint32_t n_aruns;
-    uint32_t ascii;
+    const DocDesc *desc;   // cold fields (content, agent runs, output) are read from it when used
     // per-LV state (HBM)
     uint32_t *pc;    // inserted LV: block | count << 16 (plain loads / stores)
     u64 *ao;         // Ins: origin_left | origin_right << 32; Del: the item it deleted (low word)
@@ -175,25 +178,17 @@ struct Doc {
     // wave-uniform scalars
     uint32_t nb, nsb;
     uint32_t err;
-    uint32_t n_items;
     uint32_t debug;
-    uint32_t site, ci;
+    uint32_t site;
     uint32_t steps, step_limit;   // watchdog: every loop iteration is charged; a bound
                                   // violation ends the document with ErrCapacity
     uint64_t prof[P_N];
     uint32_t doc;
-    uint32_t *fb_list, *fb_count;   // LDS tier: capacity-overflow queue for the HBM tier
     // the block the last insert / delete left behind, in registers (items lane by lane, masks):
     // typing keeps hitting it, so the next command skips its load.  Memory always holds the
     // same state (every change is stored); a toggle touching the block drops it.
     uint32_t cb, cit;
     u64 cmv, cml;
-    // cursor cache (content-tree cursor reuse): cvs = visible items before block cb in document
-    // order, valid while cvok (any visibility flip of a retreat/advance pass may move it); ctp =
-    // top position of cb's superblock or NONE (a superblock split shifts top positions).  An
-    // insert / delete whose position lands inside cb's visible range skips the index descent.
-    uint32_t cvs, ctp;
-    bool cvok;
     // transformed-ops mode (iter_xf_operations): per block the never-deleted mask, per top
     // position the never-deleted total, per LV the transformed position written out
     u64 *mup;
@@ -213,6 +208,26 @@ DEV bool charge(Doc &D) {
     return true;
 }
 template <bool PROF> DEV uint64_t tick() { return PROF ? __builtin_amdgcn_s_memtime() : 0; }
+
+// Cursor (content-tree cursor reuse, crates/content-tree/src/root.rs:50-89 keeps the last cursor
+// for the same reason): the first two LDS words of every workgroup hold {block, visible items
+// before that block in document order}.  It names the block the last insert / delete left in
+// registers (D.cb); an insert / delete whose position lands inside that block's visible range
+// skips the index descent.  Kept in LDS, not registers: the command loop is SGPR-bound.  A
+// retreat / advance pass that flips any visibility clears it (items before the block may have
+// changed).
+constexpr uint32_t CURSOR_BYTES = 16;
+DEV uint32_t *cursor_words() { extern __shared__ uint32_t smem_words[]; return smem_words; }
+DEV void cursor_set(uint32_t b, uint32_t vstart) {
+    if (lane_id() == 0) { cursor_words()[0] = b; cursor_words()[1] = vstart; }
+}
+DEV void cursor_clear() { if (lane_id() == 0) cursor_words()[0] = 0xFFFFFFFFu; }
+// Returns true and the block's visible start when the cursor names block cb.
+DEV bool cursor_get(uint32_t cb, uint32_t &vstart) {
+    const uint2 c = *reinterpret_cast<const uint2 *>(cursor_words());
+    vstart = U(c.y);
+    return cb != 0xFFFFFFFFu && U(c.x) == cb;
+}
 
 // Block -> (superblock << 6 | index in its list).  The LDS tier keeps it in 16 bits (its
 // superblock ids stay below 1024), which lets six documents share a SIMD instead of five.
@@ -410,7 +425,6 @@ DEV void split_sb(Doc &D, uint32_t S) {
     }
     wave_fence();
     D.nsb++;
-    D.ctp = NONE;
 }
 
 // Split the full block b (items in `it` lane by lane, masks mv / ml) at slot c: items [c, 64)
@@ -563,7 +577,7 @@ DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml,
         s += m;
     }
     D.cb = b; D.cit = it; D.cmv = mv; D.cml = ml;   // block state after the run
-    D.cvs = vs; D.cvok = vs != NONE; D.ctp = tph;
+    if (vs != NONE) cursor_set(b, vs); else cursor_clear();
     const uint64_t t3 = tick<PROF>();
     for (uint32_t j0 = 0; j0 < k0; j0 += 64) {   // wave-uniform loop, masked store
         const uint32_t j = j0 + l, nit = lv0 + j;
@@ -576,22 +590,23 @@ DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml,
 // over the agent runs; `lv` is wave-uniform.
 DEV void agent_of(Doc &D, uint32_t lv, uint32_t &rank, uint32_t &seq) {
     const uint32_t l = lane_id();
-    uint32_t lo = 0, n = D.n_aruns;   // last run with start <= lv lies in [lo, lo+n)
+    const uint32_t *aruns = vld(&KP().aruns) + U(uint32_t(vld(&D.desc->arun_off)));
+    uint32_t lo = 0, n = U(vld(&D.desc->n_aruns));   // last run with start <= lv lies in [lo, lo+n)
     while (n > 64) {
         if (!charge(D)) { rank = seq = 0; return; }
         const uint32_t stride = (n + 63) / 64;
         const uint32_t idx = lo + l * stride;
-        const bool ok = l * stride < n && D.aruns[4 * idx] <= lv;
+        const bool ok = l * stride < n && aruns[4 * idx] <= lv;
         const uint32_t k = uint32_t(__popcll(__ballot(ok)));
         const uint32_t nlo = lo + (k ? k - 1 : 0) * stride;
         n = min(stride, lo + n - nlo);
         lo = nlo;
     }
-    const bool ok = l < n && D.aruns[4 * (lo + l)] <= lv;
+    const bool ok = l < n && aruns[4 * (lo + l)] <= lv;
     const uint32_t k = uint32_t(__popcll(__ballot(ok)));
     const uint32_t j = U(lo + (k ? k - 1 : 0));
-    rank = U(D.aruns[4 * j + 1]);
-    seq = U(D.aruns[4 * j + 2]) + (lv - U(D.aruns[4 * j]));
+    rank = U(aruns[4 * j + 1]);
+    seq = U(aruns[4 * j + 2]) + (lv - U(aruns[4 * j]));
 }
 
 // YjsMod integrate (merge.rs:154-278) over the not-inserted-yet items between the cursor
@@ -712,11 +727,10 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
     uint32_t b, kk = 0, tph = 0, vs = 0;
     if (pos == 0) {
         b = first_block<L>(D);
-    } else if (D.cb != NONE && D.cvok && pos - 1 >= D.cvs && pos - 1 - D.cvs < uint32_t(__popcll(D.cmv))) {
+    } else if (cursor_get(D.cb, vs) && pos - 1 >= vs && pos - 1 - vs < uint32_t(__popcll(D.cmv))) {
         b = D.cb;   // the cursor's block holds visible index pos - 1
-        kk = pos - 1 - D.cvs;
-        tph = D.ctp;
-        vs = D.cvs;
+        kk = pos - 1 - vs;
+        tph = NONE;
     } else {
         Found f;
         if (!find_vis<L>(D, pos - 1, f)) { fail(D, ErrCheckout, 13); return; }
@@ -789,7 +803,6 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
     const uint64_t sp0 = PROF ? D.prof[P_SPLIT] : 0;
     insert_run<L, PROF, XF>(D, b, s, it, mv, ml, lv, k, ol, orr, tph, vs);
     if (PROF) D.prof[P_RUN] += tick<PROF>() - tp - (D.prof[P_SPLIT] - sp0);
-    D.n_items += k;
 }
 
 // Apply a delete run: n visible items from position pos (merge.rs:457-556).  LV lv+j targets
@@ -801,10 +814,11 @@ DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
     uint32_t up_done = 0;   // XF: never-deleted items this run deleted in earlier (left) blocks
     while (j0 < n) {   // each round deletes >= 1 item or fails
         uint32_t b, kk, tpos;
-        if (D.cb != NONE && D.cvok && pos >= D.cvs && pos - D.cvs < uint32_t(__popcll(D.cmv))) {
+        uint32_t vs;
+        if (cursor_get(D.cb, vs) && pos >= vs && pos - vs < uint32_t(__popcll(D.cmv))) {
             b = D.cb;   // the cursor's block holds visible index pos
-            kk = pos - D.cvs;
-            tpos = D.ctp != NONE ? D.ctp : U(ix<L>(D.sbpos + (opos_of<L>(D, b) >> 6)));
+            kk = pos - vs;
+            tpos = U(ix<L>(D.sbpos + (opos_of<L>(D, b) >> 6)));
         } else {
             Found f;
             if (!find_vis<L>(D, pos, f)) { fail(D, ErrCheckout, 14); return; }
@@ -858,7 +872,7 @@ DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
         }
         wave_fence();
         D.cb = b; D.cit = it; D.cmv = mv & ~selm; D.cml = ml;
-        D.cvs = pos - kk; D.cvok = true; D.ctp = tpos;
+        cursor_set(b, pos - kk);
         j0 += take;
     }
 }
@@ -967,7 +981,7 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
         if (__ballot(bad)) { fail(D, ErrCheckout, 16); return; }
         const bool flip = fv || fl;
         if (__ballot(flip && b == D.cb)) D.cb = NONE;
-        if (__ballot(fv)) D.cvok = false;   // visible items before the cursor's block may have moved
+        if (__ballot(fv)) cursor_clear();   // visible items before the cursor's block may have moved
         if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_T2] += t - tq; tq = t; }
         if (L) {   // LDS index: per-lane LDS atomics
             if (flip) {
@@ -1004,10 +1018,13 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
 // Visibility comes from the counts (the final advance to the tip leaves masks stale): the
 // count and the byte offset of every item are gathered together, so this adds no round trip.
 template <bool L>
-DEV void materialise(Doc &D, uint8_t *out, uint32_t cap, uint32_t &len_out, u64 &hash_out) {
+DEV void materialise(Doc &D, uint8_t *out, uint32_t cap, uint32_t &len_out, u64 &hash_out, uint32_t &items_out) {
     constexpr uint32_t G = 8;
     const uint32_t l = lane_id();
-    uint32_t total = 0;
+    const uint32_t *cbyte = vld(&KP().cbyte) + vld(&D.desc->lv_off);
+    const uint8_t *content = vld(&KP().content) + vld(&D.desc->content_off);
+    const bool ascii = U(vld(&D.desc->ascii)) != 0;
+    uint32_t total = 0, items = 0;
     u64 h = 0;
     for (uint32_t p = 0; p < D.nsb; p++) {
         const uint32_t S = U(ix<L>(D.top + p)) >> 16;
@@ -1019,6 +1036,7 @@ DEV void materialise(Doc &D, uint8_t *out, uint32_t cap, uint32_t &len_out, u64 
             const uint32_t bl = gl ? b0 : 0;
             const uint32_t n0 = c_items(ix<L>(D.cnt + bl));
             const uint32_t nl = gl ? n0 : 0;
+            items += wave_sum(nl);
             uint32_t it[G], cb[G], k[G];
             bool vis[G];
 #pragma unroll
@@ -1030,16 +1048,16 @@ DEV void materialise(Doc &D, uint8_t *out, uint32_t cap, uint32_t &len_out, u64 
             }
 #pragma unroll
             for (uint32_t g = 0; g < G; g++) {
-                const uint32_t w = ld(D.pc + it[g]), c = D.cbyte[it[g]];   // it = 0 past the count
+                const uint32_t w = ld(D.pc + it[g]), c = cbyte[it[g]];   // it = 0 past the count
                 k[g] = vis[g] ? pc_cnt(w) : 0;
                 cb[g] = vis[g] ? c : 0;
             }
 #pragma unroll
             for (uint32_t g = 0; g < G; g++) vis[g] = vis[g] && k[g] == 1u;
-            if (D.ascii) {
+            if (ascii) {
                 uint8_t by[G];
 #pragma unroll
-                for (uint32_t g = 0; g < G; g++) by[g] = vis[g] ? D.content[cb[g]] : 0;
+                for (uint32_t g = 0; g < G; g++) by[g] = vis[g] ? content[cb[g]] : 0;
 #pragma unroll
                 for (uint32_t g = 0; g < G; g++) {
                     const uint32_t c = vis[g] ? 1u : 0u;
@@ -1054,11 +1072,11 @@ DEV void materialise(Doc &D, uint8_t *out, uint32_t cap, uint32_t &len_out, u64 
             } else {
 #pragma unroll
                 for (uint32_t g = 0; g < G; g++) {
-                    const uint32_t c = vis[g] ? utf8_len(D.content[cb[g]]) : 0u;
+                    const uint32_t c = vis[g] ? utf8_len(content[cb[g]]) : 0u;
                     const uint32_t inc = wave_scan(c);
                     const uint32_t at = total + inc - c;
                     for (uint32_t k = 0; k < c; k++) {
-                        const uint8_t byte = D.content[cb[g] + k];
+                        const uint8_t byte = content[cb[g] + k];
                         if (at + k < cap) out[at + k] = byte;
                         h += splitmix((u64(at + k) << 8) | byte);
                     }
@@ -1069,6 +1087,7 @@ DEV void materialise(Doc &D, uint8_t *out, uint32_t cap, uint32_t &len_out, u64 
     }
     len_out = total;
     hash_out = wave_sum64(h);
+    items_out = items;
 }
 
 // Debug-mode consistency check of the whole structure (DTGPU_DEBUG=1): returns 0 or a code.
@@ -1135,7 +1154,7 @@ DEV uint32_t check_invariants(Doc &D, DocResult *res) {
 }
 
 template <bool L, bool PROF, bool XF>
-DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
+DEV void run_doc(Doc &D) {
     const uint32_t l = lane_id();
     // fresh tracker: one empty block in one superblock (per-LV words are written when their
     // item is inserted)
@@ -1149,15 +1168,11 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
     D.nb = 1;
     D.nsb = 1;
     D.err = 0;
-    D.n_items = 0;
     D.steps = 0;
     D.step_limit = uint32_t(min<uint64_t>(64ull * (uint64_t(D.ncmd) + D.n_lv) + 4096, 0xFFFFFFF0ull));
     D.site = 0;
-    D.ci = 0;
     D.cb = NONE;
-    D.cvs = 0;
-    D.ctp = NONE;
-    D.cvok = false;
+    cursor_clear();
     D.cit = 0;
     D.cmv = D.cml = 0;
     if (PROF) for (int i = 0; i < P_N; i++) D.prof[i] = 0;
@@ -1166,12 +1181,13 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
     // tlist chunk of a TOG is fetched while the command before it runs (tlist is read-only)
     uint32_t pf = 0;
     bool pf_ok = false;
+    uint32_t ci = 0;   // the command being applied (the failing one when the loop ends on an error)
     for (uint32_t base = 0; base < D.ncmd && !D.err; base += 64) {
         const uint32_t n_here = min(64u, D.ncmd - base);
         Cmd pre = {0, 0, 0, 0};
         pre = D.cmds[min(base + l, D.ncmd - 1)];   // lanes past n_here are never read
         for (uint32_t j = 0; j < n_here && !D.err; j++) {
-            D.ci = base + j;
+            ci = base + j;
             const uint32_t op = U(bcast(pre.op, j)), a = U(bcast(pre.lv, j)), n = U(bcast(pre.len, j)),
                            pos = U(bcast(pre.pos, j));
             if (!charge(D)) break;
@@ -1185,7 +1201,7 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
             const uint64_t t0 = tick<PROF>();
 #ifdef DTGPU_SALU_PAD   // experiment: extra independent scalar adds per command (SALU issue-bound?)
             {
-                uint32_t x0 = D.ci, x1 = x0 + 1, x2 = x0 + 2, x3 = x0 + 3;
+                uint32_t x0 = ci, x1 = x0 + 1, x2 = x0 + 2, x3 = x0 + 3;
 #pragma unroll
                 for (int q = 0; q < DTGPU_SALU_PAD; q++)
                     asm volatile("s_add_u32 %0, %0, 1\n\ts_add_u32 %1, %1, 1\n\ts_add_u32 %2, %2, 1\n\ts_add_u32 %3, %3, 1"
@@ -1221,7 +1237,7 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
                 default: fail(D, ErrCheckout, 18); break;
             }
             if (D.debug && !D.err) {
-                const uint32_t code = check_invariants<L, XF>(D, res);
+                const uint32_t code = check_invariants<L, XF>(D, vld(&KP().results) + D.doc);
                 if (code) fail(D, ErrCheckout, code);
             }
             pf = nx_pf;
@@ -1230,23 +1246,30 @@ DEV void run_doc(Doc &D, uint8_t *out, uint32_t cap, DocResult *res) {
     }
     // an LDS-tier document that outgrew its optimistic block capacity is queued for the HBM
     // tier, which replays it again from scratch
-    if (L && D.err == ErrCapacity && (D.site == 12 || D.site == 21) && D.fb_list) {
-        if (l == 0) D.fb_list[atomicAdd(D.fb_count, 1u)] = D.doc;
-        return;
+    if (L && D.err == ErrCapacity && (D.site == 12 || D.site == 21)) {
+        uint32_t *fb_list = vld(&KP().fb_list);
+        if (fb_list) {
+            if (l == 0) fb_list[atomicAdd(vld(&KP().fb_count), 1u)] = D.doc;
+            return;
+        }
     }
-    uint32_t len = 0;
+    uint32_t len = 0, n_items = 0;
     u64 h = 0;
     const uint64_t t_mat = tick<PROF>();
-    if (!D.err) materialise<L>(D, out, cap, len, h);
+    if (!D.err) {
+        uint8_t *out = vld(&KP().out) + vld(&D.desc->out_off);
+        materialise<L>(D, out, U(vld(&D.desc->out_cap)), len, h, n_items);
+    }
+    DocResult *res = vld(&KP().results) + D.doc;
     if (l == 0) {
         res->status = D.err;
         res->out_len = len;
         res->hash = h;
-        res->n_items = D.n_items;
+        res->n_items = n_items;
         res->n_blocks = D.nb;
         res->n_sb = D.nsb;
         res->lds = L ? 1u : 0u;
-        res->fail_cmd = D.err ? D.ci : 0;
+        res->fail_cmd = D.err ? ci : 0;
         res->fail_site = D.err ? D.site : 0;
         if (PROF) {
             D.prof[P_MAT] = tick<PROF>() - t_mat;
@@ -1292,18 +1315,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_REPLAY
     const DocDesc dd = P.docs[d];
     Doc D;
     D.doc = d;
-    D.fb_list = LDS_INDEX ? P.fb_list : nullptr;
-    D.fb_count = P.fb_count;
+    D.desc = P.docs + d;
     D.debug = P.debug & 1u;
     D.cmds = P.cmds + dd.cmd_off;
     D.ncmd = U(dd.ncmd);
     D.n_lv = U(dd.n_lv);
     D.tlist = P.tlist + dd.tlist_off;
-    D.cbyte = P.cbyte + dd.lv_off;
-    D.content = P.content + dd.content_off;
-    D.aruns = P.aruns + dd.arun_off;
-    D.n_aruns = U(dd.n_aruns);
-    D.ascii = U(dd.ascii);
     D.pc = P.pos + dd.lv_off;
     D.ao = P.ao + dd.lv_off;
     D.items = P.items + dd.blk_off * BLK;
@@ -1313,7 +1330,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_REPLAY
     if (LDS_INDEX) {
         if (D.max_blocks > P.lds_blocks) D.max_blocks = P.lds_blocks;
         D.max_sb = P.lds_sb;
-        bind_index(D, smem, P.lds_blocks, D.max_sb, true);
+        bind_index(D, smem + CURSOR_BYTES, P.lds_blocks, D.max_sb, true);
     } else {
         bind_index(D, P.gidx + dd.gidx_off, D.max_blocks, D.max_sb, false);
     }
@@ -1322,14 +1339,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_REPLAY
         D.tup = P.tup + dd.blk_off + 2ull * d;   // sb_capacity(mb) <= mb + 2 slots per document
         D.xf = P.xf + dd.lv_off;
     }
-    run_doc<LDS_INDEX, PROF, XF>(D, P.out + dd.out_off, U(dd.out_cap), &P.results[d]);
+    run_doc<LDS_INDEX, PROF, XF>(D);
 }
 
 }  // namespace dev
 
 static int launch_lds_tier(const BatchParams &q, hipStream_t s, bool prof) {
     if (!q.n_list) return OK;
-    size_t lds = size_t(index_bytes_ms(q.lds_blocks, q.lds_sb, true));
+    size_t lds = size_t(index_bytes_ms(q.lds_blocks, q.lds_sb, true)) + dev::CURSOR_BYTES;
     if (const char *pad = getenv("DTGPU_LDS_PAD")) lds += size_t(strtoul(pad, nullptr, 10));   // occupancy experiments
     if (lds > 160 * 1024) return ErrArg;   // a tier cap above the CU's LDS
     // allow dynamic LDS up to the CU's 160 KiB: a per-function, per-device attribute, set on
@@ -1395,8 +1412,8 @@ int launch_replay(const ReplayLaunch &r) {
     // HBM tier: its own list plus a slot per LDS-tier document that may be handed back
     const uint32_t grid = large.n_list + (large.fb_list ? large.fb_slots : 0);
     if (grid) {
-        if (prof) hipLaunchKernelGGL((dev::replay_kernel<false, true, false>), dim3(grid), dim3(64), 0, s, large);
-        else hipLaunchKernelGGL((dev::replay_kernel<false, false, false>), dim3(grid), dim3(64), 0, s, large);
+        if (prof) hipLaunchKernelGGL((dev::replay_kernel<false, true, false>), dim3(grid), dim3(64), dev::CURSOR_BYTES, s, large);
+        else hipLaunchKernelGGL((dev::replay_kernel<false, false, false>), dim3(grid), dim3(64), dev::CURSOR_BYTES, s, large);
         if (hipGetLastError() != hipSuccess) return ErrHip;
     }
     return OK;
@@ -1408,7 +1425,7 @@ int launch_replay_xf(const BatchParams &large, void *stream) {
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (!large.n_list) return OK;
     if (!large.xf || !large.mup || !large.tup) return ErrArg;
-    hipLaunchKernelGGL((dev::replay_kernel<false, false, true>), dim3(large.n_list), dim3(64), 0, s, large);
+    hipLaunchKernelGGL((dev::replay_kernel<false, false, true>), dim3(large.n_list), dim3(64), dev::CURSOR_BYTES, s, large);
     return hipGetLastError() == hipSuccess ? OK : ErrHip;
 }
 

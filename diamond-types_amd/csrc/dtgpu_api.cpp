@@ -31,55 +31,35 @@ struct dtgpu_oplog {
 
 namespace {
 
-// LDS tiers of the span replay by expected block count (kSpanTierBlocks: 320 / 1,280 / 4,096 /
-// 11,000 blocks, ~5 / 18 / 57 / 152 KiB of index): a document whose expected index fits a tier
-// replays with its index in LDS, friendsforever-sized documents many per CU, a node_nodecc-sized
-// one alone on a CU.  Bigger documents and LDS overflows replay on the HBM-index tier.
+// Checkouts replay on the per-item tracker (dt_replay.hip); its LDS tiers go by index bytes: a
+// document whose expected index fits a tier replays with its index in LDS, friendsforever-sized
+// documents many per CU, a node_nodecc-sized one alone on a CU.  Bigger documents and LDS
+// overflows replay on the HBM-index tier.
 constexpr int kLdsTiers = kMaxLdsTiers;
-static_assert(kSpanTiers == kLdsTiers, "one launch slot per span tier");
-int span_tier(uint32_t est_blocks) {
-    for (int t = 0; t < kLdsTiers; t++) if (est_blocks <= kSpanTierBlocks[t]) return t;
-    return -1;
-}
-// Checkouts replay on the per-item tracker (dt_replay.hip) -- measured faster than the span
-// tracker on every benchmark document (profiles/r3_ab) -- unless DTGPU_REPLAY=span selects the
-// run-length span tracker (dt_span.hip).  Read per batch, so one process can A/B both.  The
-// per-item tracker's LDS tiers go by index bytes.
-bool item_replay() {
-    const char *m = getenv("DTGPU_REPLAY");
-    return !(m && std::strcmp(m, "span") == 0);
-}
-constexpr uint64_t kItemTierCap[kLdsTiers] = {12 * 1024, 32 * 1024, 64 * 1024, 160 * 1024};
+// index bytes per tier; the replay adds 16 bytes of cursor (dt_replay.hip CURSOR_BYTES)
+constexpr uint64_t kItemTierCap[kLdsTiers] = {12 * 1024 - 16, 32 * 1024 - 16, 64 * 1024 - 16, 160 * 1024 - 16};
 int item_tier(uint32_t est) {
     const uint64_t bytes = index_bytes_ms(est, lds_sb_capacity(est), true);
     for (int t = 0; t < kLdsTiers; t++) if (bytes <= kItemTierCap[t]) return t;
     return -1;
 }
-// Expected inserted chars per block when sizing a document's LDS index: the per-item tracker's
-// blocks end up ~43 items full on the benchmark traces (cut_point, dt_replay.hip), sized at 40;
-// the span tracker's at SPAN_LDS_FILL.  DTGPU_LDS_FILL overrides either (tests force the LDS
-// overflow -> HBM tier hand-back with it).
-uint64_t lds_fill_setting(bool item) {
-    uint64_t f = item ? 40 : SPAN_LDS_FILL;
+// Expected inserted chars per block when sizing a document's LDS index: blocks end up ~43 items
+// full on the benchmark traces (cut_point, dt_replay.hip), sized at 40.  DTGPU_LDS_FILL
+// overrides it (tests force the LDS overflow -> HBM tier hand-back with it).
+uint64_t lds_fill_setting() {
+    uint64_t f = 40;
     if (const char *e = getenv("DTGPU_LDS_FILL")) f = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
     return f;
 }
-// Per-document replay layout of either tracker: block capacity, HBM index bytes, LDS tier.
+// Per-document replay layout: block capacity, HBM index bytes, LDS tier.
 struct Layout { uint32_t max_blocks; uint64_t gidx; int tier; uint32_t tier_blocks; };
-Layout replay_layout(uint64_t n_ins, uint64_t lds_fill, bool item, bool hbm_only) {
+Layout replay_layout(uint64_t n_ins, uint64_t lds_fill, bool hbm_only) {
     Layout L{};
-    if (item) {
-        L.max_blocks = uint32_t(n_ins / 32 + 2);
-        L.gidx = index_bytes(L.max_blocks);
-        const uint32_t est = uint32_t(std::min<uint64_t>(L.max_blocks, n_ins / lds_fill + 8));
-        L.tier = hbm_only ? -1 : item_tier(est);
-        L.tier_blocks = est;
-    } else {
-        L.max_blocks = uint32_t(span_max_blocks(n_ins));
-        L.gidx = span_index_bytes(L.max_blocks, span_sb_capacity(L.max_blocks), false);
-        L.tier = hbm_only ? -1 : span_tier(span_lds_blocks(n_ins, lds_fill));
-        L.tier_blocks = L.tier >= 0 ? kSpanTierBlocks[L.tier] : 0;
-    }
+    L.max_blocks = uint32_t(n_ins / 32 + 2);
+    L.gidx = index_bytes(L.max_blocks);
+    const uint32_t est = uint32_t(std::min<uint64_t>(L.max_blocks, n_ins / lds_fill + 8));
+    L.tier = hbm_only ? -1 : item_tier(est);
+    L.tier_blocks = est;
     return L;
 }
 
@@ -121,10 +101,9 @@ struct dtgpu_batch {
 
     DevBuf<Cmd> d_cmds;
     DevBuf<uint32_t> d_tlist, d_cbyte, d_aruns, d_pos, d_items, d_lists, d_counter;
-    DevBuf<unsigned long long> d_ao, d_m2, d_mup, d_rows;
+    DevBuf<unsigned long long> d_ao, d_m2, d_mup;
     DevBuf<uint32_t> d_tup, d_xf;   // transformed-ops batches only
     bool xf_mode = false;
-    bool item_mode = true;    // the per-item tracker replays checkouts (DTGPU_REPLAY=span: spans)
     DevBuf<uint8_t> d_content, d_out, d_gidx;
     DevBuf<uint32_t> d_fb;   // [0] = count, then the handed-back documents
     DevBuf<DocDesc> d_docs;
@@ -234,7 +213,7 @@ dtgpu_status set_tier_params(dtgpu_batch &B, const BatchParams &base) {
         q.doc_list = B.d_lists.p + off;
         q.n_list = uint32_t(B.tier_list[t].size());
         q.lds_blocks = B.tier_blocks[t];
-        q.lds_sb = B.item_mode ? lds_sb_capacity(q.lds_blocks) : span_lds_sb(q.lds_blocks);
+        q.lds_sb = lds_sb_capacity(q.lds_blocks);
         off += B.tier_list[t].size();
         if (fb) { q.fb_count = B.d_fb.p; q.fb_list = B.d_fb.p + 1; }
     }
@@ -269,7 +248,7 @@ int replay_all(dtgpu_batch *B, hipStream_t s, int skip_tier = -1) {
     r.stream = s;
     for (int k = 0; k < kSideStreams; k++) { r.side[k] = B->side[k]; r.ev_join[k] = B->ev_join[k]; }
     r.ev_fork = B->ev_fork;
-    return B->item_mode ? launch_replay(r) : launch_span_replay(r);
+    return launch_replay(r);
 }
 
 // xf: a transformed-ops batch (iter_xf_operations): host plans in TransformedOpsIter order
@@ -297,7 +276,6 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     B->n_lv.resize(n);
     B->docs.resize(n);
     B->host_planned.assign(n, 0);
-    B->item_mode = !xf && item_replay();
     const bool force_host = xf || getenv("DTGPU_HOST_PLAN") != nullptr;
 
     // ---- 1. device planner inputs; a sizing pass of the planner gives exact stream sizes ----
@@ -393,7 +371,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     uint64_t lv_total = 0, blk_total = 0, out_total = 0, gidx_total = 0;
     // expected inserted chars per block in the LDS tier (per tracker); DTGPU_LDS_FILL overrides it
     // for experiments (a document that outgrows its LDS index replays on the HBM tier)
-    const uint64_t lds_fill = lds_fill_setting(B->item_mode);
+    const uint64_t lds_fill = lds_fill_setting();
     for (size_t i = 0; i < n; i++) {
         Prepared &p = prep[i];
         B->host_status[i] = p.status;
@@ -406,7 +384,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         if (p.status != OK) { pdesc[i].skip = 1; continue; }
         uint64_t n_ins = 0;
         for (const OpRun &r : p.log.ops) if (r.kind == 0) n_ins += r.len;
-        if ((xf || B->item_mode) && n_ins / 32 + 2 > std::min<uint64_t>(LOC_MAX_BLOCKS, MAX_DOC_BLOCKS)) { B->host_status[i] = ErrCapacity; pdesc[i].skip = 1; continue; }
+        if (n_ins / 32 + 2 > std::min<uint64_t>(LOC_MAX_BLOCKS, MAX_DOC_BLOCKS)) { B->host_status[i] = ErrCapacity; pdesc[i].skip = 1; continue; }
         d.cmd_off = cmd_total;
         d.tlist_off = tlist_total;
         if (p.host_plan) {
@@ -435,7 +413,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         d.content_off = content.size();
         d.content_len = uint32_t(p.log.ins_content.size());
         d.n_aruns = uint32_t(aq);
-        const Layout lay = replay_layout(n_ins, lds_fill, xf || B->item_mode, xf);
+        const Layout lay = replay_layout(n_ins, lds_fill, xf);
         d.max_blocks = lay.max_blocks;
         d.blk_off = blk_total;
         d.out_off = out_total;
@@ -500,12 +478,8 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     CK(B->d_lists.upload(tier_lists(*B), s));
     CK(B->d_pos.alloc(lv_total));
     CK(B->d_ao.alloc(lv_total));
-    if (xf || B->item_mode) {   // the per-item tracker (dt_replay.hip): transformed ops, A/B runs
-        CK(B->d_items.alloc(blk_total * 64));
-        CK(B->d_m2.alloc(2 * blk_total));
-    } else {
-        CK(B->d_rows.alloc(blk_total * SPAN_NS));
-    }
+    CK(B->d_items.alloc(blk_total * 64));
+    CK(B->d_m2.alloc(2 * blk_total));
     CK(B->d_out.alloc(out_total));
     CK(B->d_gidx.alloc(gidx_total));
     CK(B->d_fb.alloc(n_lds_docs(*B) + 1));
@@ -534,7 +508,6 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     base.ao = B->d_ao.p;
     base.items = B->d_items.p;
     base.m2 = B->d_m2.p;
-    base.rows = B->d_rows.p;
     base.out = B->d_out.p;
     base.gidx = B->d_gidx.p;
     base.docs = B->d_docs.p;
@@ -574,7 +547,6 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     B->n_lv.assign(n, 0);
     B->docs.assign(n, DocDesc{});
     B->host_planned.assign(n, 0);
-    B->item_mode = item_replay();
 
     // ---- prep layout ----------------------------------------------------------------------------
     std::vector<PrepDesc> pd(n);
@@ -673,7 +645,7 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
 
     // ---- replay layout ---------------------------------------------------------------------------
     uint64_t cmd_total = 0, tlist_total = 0, blk_total = 0, out_total = 0, gidx_total = 0;
-    const uint64_t lds_fill = lds_fill_setting(B->item_mode);
+    const uint64_t lds_fill = lds_fill_setting();
     for (size_t i = 0; i < n; i++) {
         DocDesc &d = B->docs[i];
         std::memset(&d, 0, sizeof d);
@@ -696,8 +668,8 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
         d.content_len = r.n_content;
         d.arun_off = pd[i].o_arun * 4;
         d.n_aruns = r.n_aruns;
-        if (B->item_mode && n_ins / 32 + 2 > std::min<uint64_t>(LOC_MAX_BLOCKS, MAX_DOC_BLOCKS)) { B->host_status[i] = ErrCapacity; pdesc[i].skip = 1; continue; }
-        const Layout lay = replay_layout(n_ins, lds_fill, B->item_mode, false);
+        if (n_ins / 32 + 2 > std::min<uint64_t>(LOC_MAX_BLOCKS, MAX_DOC_BLOCKS)) { B->host_status[i] = ErrCapacity; pdesc[i].skip = 1; continue; }
+        const Layout lay = replay_layout(n_ins, lds_fill, false);
         d.max_blocks = lay.max_blocks;
         d.blk_off = blk_total;
         d.out_off = out_total;
@@ -727,12 +699,8 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     CK(B->d_lists.upload(tier_lists(*B), s));
     CK(B->d_pos.alloc(lv_total));
     CK(B->d_ao.alloc(lv_total));
-    if (B->item_mode) {
-        CK(B->d_items.alloc(blk_total * 64));
-        CK(B->d_m2.alloc(2 * blk_total));
-    } else {
-        CK(B->d_rows.alloc(blk_total * SPAN_NS));
-    }
+    CK(B->d_items.alloc(blk_total * 64));
+    CK(B->d_m2.alloc(2 * blk_total));
     CK(B->d_out.alloc(out_total));
     CK(B->d_gidx.alloc(gidx_total));
     CK(B->d_fb.alloc(n_lds_docs(*B) + 1));
@@ -752,7 +720,6 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     base.ao = B->d_ao.p;
     base.items = B->d_items.p;
     base.m2 = B->d_m2.p;
-    base.rows = B->d_rows.p;
     base.out = B->d_out.p;
     base.gidx = B->d_gidx.p;
     base.docs = B->d_docs.p;
@@ -761,7 +728,7 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     // split pass: when the biggest non-empty LDS tier rides a side stream and other documents
     // exist, its documents' prep and plan do not wait for everyone else's (a skewed batch's
     // longest replays start as soon as their own plans are done)
-    if (B->item_mode && !getenv("DTGPU_NO_SPLIT")) {
+    if (!getenv("DTGPU_NO_SPLIT")) {
         int tb = -1;
         for (int t = kLdsTiers - 1; t >= 1; t--)
             if (!B->tier_list[t].empty()) { tb = t; break; }

@@ -17,14 +17,16 @@ using namespace dtgpu;
 
 extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *hist_off, size_t n_graphs,
                                             const dtgpu_graph_query *queries, size_t nq, int64_t *spans,
-                                            size_t span_cap, dtgpu_graph_answer *answers, float *ms) {
-    if ((n_graphs && (!hist || !hist_off)) || (nq && (!queries || !answers)) || (nq && span_cap && !spans))
+                                            size_t span_cap, int64_t *common, size_t common_cap,
+                                            dtgpu_graph_answer *answers, float *ms) {
+    if ((n_graphs && (!hist || !hist_off)) || (nq && (!queries || !answers)) || (nq && span_cap && !spans) ||
+        (nq && common_cap && !common))
         return DTGPU_ERR_ARG;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return DTGPU_ERR_NO_DEVICE;
     // graphs -> entry quads + parents
     std::vector<uint32_t> ents, par;
-    std::vector<uint32_t> goff(n_graphs), gn(n_graphs);
+    std::vector<uint32_t> goff(n_graphs), gn(n_graphs), gmaxp(n_graphs, 0);
     for (size_t g = 0; g < n_graphs; g++) {
         Graph G;
         for (size_t i = hist_off[g]; i < hist_off[g + 1];) {
@@ -43,6 +45,7 @@ extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *h
         goff[g] = uint32_t(ents.size() / 4);
         gn[g] = uint32_t(G.entries.size());
         for (const GraphEntry &e : G.entries) {
+            gmaxp[g] = std::max(gmaxp[g], uint32_t(e.parents.size()));
             ents.push_back(uint32_t(e.start));
             ents.push_back(uint32_t(e.end));
             ents.push_back(uint32_t(e.shadow));
@@ -52,22 +55,37 @@ extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *h
         ents.insert(ents.end(), {0u, 0u, 0u, uint32_t(par.size())});
     }
     std::vector<GraphQuery> q(nq);
+    std::vector<int32_t> front;   // every query's versions, a then b
     const uint32_t out_cap = uint32_t(4 * std::max<size_t>(span_cap, 1));
+    const uint32_t c_cap = uint32_t(std::min<size_t>(common_cap, 1u << 24));
+    auto npar_of = [&](uint32_t ent_off, uint32_t n_ent) -> uint64_t {
+        return ents[4 * (size_t(ent_off) + n_ent) + 3] - ents[4 * size_t(ent_off) + 3];
+    };
     for (size_t i = 0; i < nq; i++) {
         const dtgpu_graph_query &s = queries[i];
         GraphQuery &d = q[i];
         std::memset(&d, 0, sizeof d);
-        if (s.graph >= n_graphs || s.na > GQ_MAX_FRONTIER || s.nb > GQ_MAX_FRONTIER || s.kind > GQ_CONFLICT_LEVEL) return DTGPU_ERR_ARG;
+        const size_t nb = s.kind == GQ_CONTAINS ? 0 : s.nb;
+        if (s.graph >= n_graphs || s.kind > GQ_CONFLICT_LEVEL || (s.na && !s.a) || (nb && !s.b) ||
+            s.na + nb > (size_t(1) << 28))
+            return DTGPU_ERR_ARG;
         d.kind = s.kind;
         d.ent_off = goff[s.graph];
         d.n_ent = gn[s.graph];
-        d.na = s.na;
-        d.nb = s.nb;
-        for (uint32_t k = 0; k < s.na; k++) d.a[k] = int32_t(s.a[k]);
-        for (uint32_t k = 0; k < s.nb; k++) d.b[k] = int32_t(s.b[k]);
+        d.na = uint32_t(s.na);
+        d.nb = uint32_t(nb);
+        d.f_off = uint32_t(front.size());
+        for (size_t k = 0; k < s.na; k++) front.push_back(int32_t(std::max<int64_t>(std::min<int64_t>(s.a[k], INT32_MAX), -1)));
+        for (size_t k = 0; k < nb; k++) front.push_back(int32_t(std::max<int64_t>(std::min<int64_t>(s.b[k], INT32_MAX), -1)));
         d.target = int32_t(std::max<int64_t>(s.target, -1));
         d.out_off = uint32_t(i) * out_cap;
         d.out_cap = out_cap;
+        d.c_off = uint32_t(i) * c_cap;
+        d.c_cap = c_cap;
+        d.max_par = gmaxp[s.graph];
+        const uint64_t npar = npar_of(d.ent_off, d.n_ent);
+        d.hk_cap = gq_key_cap(npar, d.na, d.nb);
+        d.htp_cap = gq_tp_cap(d.n_ent, npar, d.na, d.nb);
     }
     // HBM scratch of the level-synchronous queries: marks (diff), marks + buckets + time points
     // (conflict spans), sized by the query's graph
@@ -75,12 +93,12 @@ extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *h
     for (size_t i = 0; i < nq; i++) {
         GraphQuery &d = q[i];
         if (d.kind != GQ_DIFF_LEVEL && d.kind != GQ_CONFLICT_LEVEL) continue;
-        const uint64_t npar = ents[4 * (size_t(d.ent_off) + d.n_ent) + 3] - ents[4 * size_t(d.ent_off) + 3];
+        const uint64_t npar = npar_of(d.ent_off, d.n_ent);
         d.scr_off = qscr_words;
         if (d.kind == GQ_DIFF_LEVEL) qscr_words += 2ull * d.n_ent;
         else {
-            d.scr_tp = conflict_level_tps(d.n_ent, npar);
-            qscr_words += conflict_level_words(d.n_ent, npar);
+            d.scr_tp = conflict_level_tps(d.n_ent, npar, d.na, d.nb);
+            qscr_words += conflict_level_words(d.n_ent, npar, d.na, d.nb);
         }
     }
     // graphs that level-synchronous diffs run on
@@ -93,7 +111,8 @@ extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *h
     }
     hipStream_t st = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    DevBuf<uint32_t> d_ents, d_par, d_out;
+    DevBuf<uint32_t> d_ents, d_par, d_out, d_hscr;
+    DevBuf<int32_t> d_front, d_common;
     DevBuf<GraphQuery> d_q;
     DevBuf<GraphResult> d_r;
     DevBuf<uint32_t> d_pent, d_child, d_level, d_order, d_loff, d_meta, d_gscr, d_qscr;
@@ -101,6 +120,7 @@ extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *h
     dtgpu_status rc = DTGPU_OK;
     std::vector<GraphResult> res(nq);
     std::vector<uint32_t> out(size_t(nq) * out_cap);
+    std::vector<int32_t> com(size_t(nq) * c_cap);
     do {
 #define CK(x) do { if ((x) != hipSuccess) { rc = DTGPU_ERR_HIP; goto done; } } while (0)
         CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -111,8 +131,10 @@ extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *h
         CK(d_q.upload(q, st));
         CK(d_r.alloc(nq));
         CK(d_out.alloc(out.size()));
+        CK(d_front.upload(front, st));
+        CK(d_common.alloc(std::max<size_t>(com.size(), 1)));
         {
-            GraphParams P{d_ents.p, d_par.p, d_out.p, d_q.p, d_r.p, uint32_t(nq)};
+            GraphParams P{d_ents.p, d_par.p, d_out.p, d_q.p, d_r.p, uint32_t(nq), d_front.p, d_common.p, nullptr};
             LevelParams LP{};
             if (!lg.empty()) {
                 const size_t nquad = ents.size() / 4;
@@ -132,7 +154,28 @@ extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *h
                                  max_ent <= kLevelLdsEntries ? max_ent : 0u};
             }
             CK(hipEventRecord(e0, st));
-            if (launch_graph_queries(P, st)) { rc = DTGPU_ERR_HIP; goto done; }
+            if (launch_graph_queries(P, st, false)) { rc = DTGPU_ERR_HIP; goto done; }
+            // the heap walks whose queues outgrew LDS, again with their queues in HBM scratch
+            bool any_heap = false;
+            for (size_t i = 0; i < nq; i++) any_heap |= q[i].kind != GQ_DIFF_LEVEL && q[i].kind != GQ_CONFLICT_LEVEL;
+            if (any_heap) {
+                std::vector<GraphResult> r1(nq);
+                CK(hipMemcpyAsync(r1.data(), d_r.p, nq * sizeof(GraphResult), hipMemcpyDeviceToHost, st));
+                CK(hipStreamSynchronize(st));
+                uint64_t hw = 0;
+                for (size_t i = 0; i < nq; i++) {
+                    if (r1[i].status != GQ_QUEUE_FULL) continue;
+                    GraphQuery &d = q[i];
+                    d.h_off = hw;
+                    hw += d.hk_cap + uint64_t(d.htp_cap + 3) * gq_tp_words(d.max_par, d.na, d.nb);
+                }
+                if (hw) {
+                    CK(d_hscr.alloc(hw));
+                    CK(d_q.upload(q, st));
+                    P.hscr = d_hscr.p;
+                    if (launch_graph_queries(P, st, true)) { rc = DTGPU_ERR_HIP; goto done; }
+                }
+            }
             if (!lg.empty() && (launch_levels(LP, st) || launch_level_diff(LP, P, st) || launch_level_conflict(LP, P, st))) {
                 rc = DTGPU_ERR_HIP;
                 goto done;
@@ -142,6 +185,7 @@ extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *h
         if (nq) {
             CK(hipMemcpyAsync(res.data(), d_r.p, nq * sizeof(GraphResult), hipMemcpyDeviceToHost, st));
             CK(hipMemcpyAsync(out.data(), d_out.p, out.size() * 4, hipMemcpyDeviceToHost, st));
+            if (!com.empty()) CK(hipMemcpyAsync(com.data(), d_common.p, com.size() * 4, hipMemcpyDeviceToHost, st));
         }
         CK(hipStreamSynchronize(st));
         if (ms) {
@@ -155,7 +199,7 @@ extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *h
         const GraphResult &r = res[i];
         dtgpu_graph_answer &a = answers[i];
         std::memset(&a, 0, sizeof a);
-        a.status = r.status;
+        a.status = r.status == GQ_QUEUE_FULL ? uint32_t(GQ_OVERFLOW) : r.status;
         const uint32_t *o = out.data() + size_t(i) * out_cap;
         int64_t *sp = spans ? spans + i * span_cap * 3 : nullptr;
         if (q[i].kind == GQ_DIFF || q[i].kind == GQ_DIFF_LEVEL) {
@@ -173,10 +217,10 @@ extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *h
             for (uint32_t k = 0; k < 3 * r.n0; k++) sp[k] = int32_t(o[k]);
             a.n_a = r.n0;
             a.n_common = r.n_common;
-            for (uint32_t k = 0; k < r.n_common && k < GQ_MAX_FRONTIER; k++) a.common[k] = r.common[k];
+            for (uint32_t k = 0; k < r.n_common && k < c_cap; k++) common[i * common_cap + k] = com[size_t(i) * c_cap + k];
         } else if (q[i].kind == GQ_DOMINATORS) {
             a.n_common = r.n_common;
-            for (uint32_t k = 0; k < r.n_common && k < GQ_MAX_FRONTIER; k++) a.common[k] = r.common[k];
+            for (uint32_t k = 0; k < r.n_common && k < c_cap; k++) common[i * common_cap + k] = com[size_t(i) * c_cap + k];
         } else {
             a.n_a = r.n0;
         }

@@ -48,14 +48,14 @@ class BatchOpts(ctypes.Structure):
 
 
 class GraphQuery(ctypes.Structure):
-    _fields_ = [("kind", ctypes.c_uint32), ("graph", ctypes.c_uint32), ("na", ctypes.c_uint32),
-                ("nb", ctypes.c_uint32), ("a", ctypes.c_int64 * 16), ("b", ctypes.c_int64 * 16),
+    _fields_ = [("kind", ctypes.c_uint32), ("graph", ctypes.c_uint32), ("na", ctypes.c_size_t),
+                ("nb", ctypes.c_size_t), ("a", ctypes.POINTER(ctypes.c_int64)), ("b", ctypes.POINTER(ctypes.c_int64)),
                 ("target", ctypes.c_int64)]
 
 
 class GraphAnswer(ctypes.Structure):
     _fields_ = [("status", ctypes.c_uint32), ("n_a", ctypes.c_uint32), ("n_b", ctypes.c_uint32),
-                ("n_common", ctypes.c_uint32), ("common", ctypes.c_int64 * 16)]
+                ("n_common", ctypes.c_uint32)]
 
 
 _lib = None
@@ -185,6 +185,7 @@ def lib():
     L.dtgpu_batch_create_decoded.argtypes = [vp, ctypes.POINTER(vp)]
     L.dtgpu_graph_queries.argtypes = [ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(sz), sz,
                                       ctypes.POINTER(GraphQuery), sz, ctypes.POINTER(ctypes.c_int64), sz,
+                                      ctypes.POINTER(ctypes.c_int64), sz,
                                       ctypes.POINTER(GraphAnswer), ctypes.POINTER(ctypes.c_float)]
     L.dtgpu_status_str.argtypes = [c]
     L.dtgpu_status_str.restype = ctypes.c_char_p
@@ -886,7 +887,7 @@ GQ_KINDS = {"diff": 0, "conflict": 1, "contains": 2, "dominators": 3, "diff_leve
 DIFF_FLAGS = ["OnlyA", "OnlyB", "Shared"]
 
 
-def graph_queries(graphs, queries, span_cap=512, timing=False):
+def graph_queries(graphs, queries, span_cap=512, timing=False, common_cap=None):
     """Batched causal-graph queries on the GPU (dtgpu_graph_queries, one wavefront per query).
 
     graphs: GraphEntrySimple lists ([{"span": [start, end], "parents": [...]}, ...]).
@@ -896,7 +897,7 @@ def graph_queries(graphs, queries, span_cap=512, timing=False):
              ("dominators", g, a, b) -> sorted list (find_dominators_2 of two dominator sets);
              ("diff_level", g, a, b) -> as "diff", by level-synchronous propagation (dt_level.hip);
              ("conflict_level", g, a, b) -> as "conflict": level-synchronous marks + a bucketed sweep.
-    A query the device could not answer yields ("error", status)."""
+    Frontiers may be of any width.  A query the device could not answer yields ("error", status)."""
     hist, off = [], [0]
     for g in graphs:
         for e in g:
@@ -906,21 +907,29 @@ def graph_queries(graphs, queries, span_cap=512, timing=False):
     O = (ctypes.c_size_t * len(off))(*off)
     nq = len(queries)
     Q = (GraphQuery * max(1, nq))()
+    keep = []   # the frontier arrays the query structs point at
     for i, (kind, g, a, b) in enumerate(queries):
         q = Q[i]
         q.kind, q.graph, q.na = GQ_KINDS[kind], g, len(a)
-        for k, v in enumerate(a):
-            q.a[k] = v
+        fa = (ctypes.c_int64 * max(1, len(a)))(*a)
+        keep.append(fa)
+        q.a = ctypes.cast(fa, ctypes.POINTER(ctypes.c_int64))
         if kind == "contains":
             q.target = b
         else:
             q.nb = len(b)
-            for k, v in enumerate(b):
-                q.b[k] = v
+            fb = (ctypes.c_int64 * max(1, len(b)))(*b)
+            keep.append(fb)
+            q.b = ctypes.cast(fb, ctypes.POINTER(ctypes.c_int64))
+    if common_cap is None:   # room for any answer: a common frontier / dominator set is never
+        common_cap = max([2] + [len(a) + (0 if k == "contains" else len(b)) + 1 for k, _g, a, b in queries]
+                         + [max([len(e["parents"]) for e in gr] or [0]) + 1 for gr in graphs])
     spans = (ctypes.c_int64 * (max(1, nq) * span_cap * 3))()
+    common = (ctypes.c_int64 * (max(1, nq) * common_cap))()
     ans = (GraphAnswer * max(1, nq))()
     ms = ctypes.c_float()
-    _check(lib().dtgpu_graph_queries(H, O, len(graphs), Q, nq, spans, span_cap, ans, ctypes.byref(ms)))
+    _check(lib().dtgpu_graph_queries(H, O, len(graphs), Q, nq, spans, span_cap, common, common_cap, ans,
+                                     ctypes.byref(ms)))
     out = []
     for i, (kind, _g, _a, _b) in enumerate(queries):
         r = ans[i]
@@ -932,9 +941,11 @@ def graph_queries(graphs, queries, span_cap=512, timing=False):
         if kind in ("diff", "diff_level"):
             out.append(([(s, e) for s, e, _ in tri[:r.n_a]], [(s, e) for s, e, _ in tri[r.n_a:]]))
         elif kind in ("conflict", "conflict_level"):
-            out.append(([(s, e, DIFF_FLAGS[f]) for s, e, f in tri[:r.n_a]], list(r.common[:r.n_common])))
+            cb = common_cap * i
+            out.append(([(s, e, DIFF_FLAGS[f]) for s, e, f in tri[:r.n_a]], list(common[cb:cb + r.n_common])))
         elif kind == "dominators":
-            out.append(list(r.common[:r.n_common]))
+            cb = common_cap * i
+            out.append(list(common[cb:cb + r.n_common]))
         else:
             out.append(bool(r.n_a))
     return (out, ms.value) if timing else out

@@ -425,7 +425,7 @@ size_t dtgpu_oplog_export(const dtgpu_oplog *oplog, int what, void *out, size_t 
  *                      target (-1 = ROOT)
  *   DTGPU_GQ_DOMINATORS Graph::find_dominators_2 (tools.rs:545-578; a, b sorted dominator sets):
  *                      common[0, n_common) = the union's dominators, ascending (ListBranch::merge's
- *                      end version); more than 16 is status 1
+ *                      end version)
  *   DTGPU_GQ_DIFF_LEVEL Graph::diff as DTGPU_GQ_DIFF, computed level-synchronously: the graph's
  *                      entries are levelled (Kahn, one level per round) and the two versions'
  *                      marks propagate down the levels over the CSR parent arrays (dt_level.hip);
@@ -435,8 +435,11 @@ size_t dtgpu_oplog_export(const dtgpu_oplog *oplog, int what, void *out, size_t 
  *                      cuts and the common frontier come from a sweep over the entries in
  *                      descending order with each entry's pending time points in a bucket (the
  *                      reference's heap walk without the heap, dt_level.hip)
- * spans: span_cap (start, end, flag) triples per query.  answer.status: 0 ok, 1 capacity
- * (queue or span_cap), 2 bad input (a version outside the graph). */
+ * spans: span_cap (start, end, flag) triples per query; common: common_cap LVs per query (the
+ * common frontier of CONFLICT, the dominators of DOMINATORS).  Frontiers and the walks' queues have
+ * no size limit: a heap walk whose queue outgrows LDS is answered again with its queue in HBM
+ * scratch sized from its graph.  answer.status: 0 ok, 1 capacity (span_cap or common_cap too
+ * small for the answer), 2 bad input (a version outside the graph). */
 #define DTGPU_GQ_DIFF 0
 #define DTGPU_GQ_CONFLICT 1
 #define DTGPU_GQ_CONTAINS 2
@@ -444,17 +447,18 @@ size_t dtgpu_oplog_export(const dtgpu_oplog *oplog, int what, void *out, size_t 
 #define DTGPU_GQ_DIFF_LEVEL 4
 #define DTGPU_GQ_CONFLICT_LEVEL 5
 typedef struct dtgpu_graph_query {
-    uint32_t kind, graph, na, nb;   /* frontier sizes <= 16 */
-    int64_t a[16], b[16];
+    uint32_t kind, graph;
+    size_t na, nb;                  /* frontier sizes: any (SmallVec frontiers in the reference) */
+    const int64_t *a, *b;           /* ascending LVs; b unused for CONTAINS */
     int64_t target;
 } dtgpu_graph_query;
 typedef struct dtgpu_graph_answer {
     uint32_t status, n_a, n_b, n_common;
-    int64_t common[16];
 } dtgpu_graph_answer;
 dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *hist_off, size_t n_graphs,
                                  const dtgpu_graph_query *queries, size_t n_queries, int64_t *spans,
-                                 size_t span_cap, dtgpu_graph_answer *answers, float *ms);
+                                 size_t span_cap, int64_t *common, size_t common_cap,
+                                 dtgpu_graph_answer *answers, float *ms);
 
 #ifdef __cplusplus
 }

@@ -328,7 +328,10 @@ static void graph_diff_rev(const Graph *g, const i64 *a, int na, const i64 *b, i
 }
 
 /* ---- find_conflicting (tools.rs:296-484) ---- */
-typedef struct { i64 last; int nm; i64 m[16]; int flag; } TP;   /* TimePoint + flag */
+/* TimePoint + flag; merged_with is a SmallVec in the reference: OR_TP_M bounds it here (a wider
+ * frontier or merge aborts the oracle rather than answer wrongly) */
+#define OR_TP_M 255
+typedef struct { i64 last; int nm; i64 m[OR_TP_M]; int flag; } TP;
 typedef VEC(TP) TPHeap;
 /* Ord for (TimePoint, DiffFlag): last.wrapping_add(1) asc, then fewer merged_with is greater,
  * then (Rust tuple / derived Ord) merged_with lexicographic is irrelevant once lens differ... */
@@ -361,6 +364,7 @@ static TP tph_pop(TPHeap *h) {
     return top;
 }
 static TP tp_from_frontier(const i64 *f, int n, int flag) {
+    if (n - 1 > OR_TP_M) abort();
     TP t; t.flag = flag; t.nm = 0;
     t.last = n ? f[n - 1] : ROOT_LV;
     if (n > 1) { t.nm = n - 1; for (int i = 0; i < n - 1; i++) t.m[i] = f[i]; }
@@ -368,7 +372,7 @@ static TP tp_from_frontier(const i64 *f, int n, int flag) {
 }
 typedef void (*visit_fn)(void *ctx, i64 s, i64 e, int flag);
 
-/* returns common-ancestor frontier size, writes into common[] (cap 64) */
+/* returns common-ancestor frontier size, writes into common[] (cap OR_TP_M + 1) */
 static int find_conflicting_slow(const Graph *g, const i64 *a, int na, const i64 *b, int nb, visit_fn visit, void *ctx, i64 *common) {
     TPHeap q = {0};
     tph_push(&q, tp_from_frontier(a, na, F_OnlyA));
@@ -1306,8 +1310,10 @@ EXPORT const u8 *dto_ins_content(const dto_oplog *o) { return o->ins_content.v; 
 EXPORT Graph *dto_graph_new(void) { return calloc(1, sizeof(Graph)); }
 EXPORT void dto_graph_free(Graph *g) { graph_free(g); free(g); }
 EXPORT void dto_graph_push(Graph *g, const i64 *parents, int np, i64 start, i64 end) {
-    i64 p[64]; memcpy(p, parents, sizeof(i64) * (size_t)np); sort_frontier(p, np);
+    i64 *p = malloc(sizeof(i64) * (size_t)(np ? np : 1));
+    memcpy(p, parents, sizeof(i64) * (size_t)np); sort_frontier(p, np);
     graph_push(g, p, np, start, end);
+    free(p);
 }
 EXPORT int dto_graph_num_entries(const Graph *g) { return (int)g->e.n; }
 EXPORT void dto_graph_entry(const Graph *g, int i, i64 *start, i64 *end, i64 *shadow) {

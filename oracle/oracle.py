@@ -318,7 +318,7 @@ class Graph:
         A, na = _arr(a)
         B, nb = _arr(b)
         spans = (ctypes.c_int64 * (6 * lib().dto_graph_num_entries(self.h) + 96))()
-        common = (ctypes.c_int64 * 64)()
+        common = (ctypes.c_int64 * 256)()   # OR_TP_M + 1 (dt_oracle.c)
         nc = ctypes.c_int()
         n = lib().dto_graph_find_conflicting(self.h, A, na, B, nb, spans, common, ctypes.byref(nc))
         flags = ["OnlyA", "OnlyB", "Shared"]

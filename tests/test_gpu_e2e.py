@@ -27,17 +27,7 @@ def _texts(b):
     return res, [b.text(i) if r["status"] == 0 else None for i, r in enumerate(res)]
 
 
-@pytest.fixture(params=["item", "span"])
-def replay_mode(request, monkeypatch):
-    """Both trackers: the per-item default and the run-length span tracker (DTGPU_REPLAY=span)."""
-    if request.param == "span":
-        monkeypatch.setenv("DTGPU_REPLAY", "span")
-    else:
-        monkeypatch.delenv("DTGPU_REPLAY", raising=False)
-    return request.param
-
-
-def test_friendsforever_device_staged(replay_mode):
+def test_friendsforever_device_staged():
     want = G.trace("friendsforever_flat")["endContent"].encode()
     b = dt_amd.Batch(docs=[G.dt_bytes("friendsforever")] * 64, staging="device")
     res, texts = _texts(b)
@@ -47,7 +37,7 @@ def test_friendsforever_device_staged(replay_mode):
 
 
 @pytest.mark.parametrize("name", ["git-makefile", "node_nodecc"])
-def test_large_docs_device_staged(name, replay_mode):
+def test_large_docs_device_staged(name):
     data = G.dt_bytes(name)
     b = dt_amd.Batch(docs=[data], staging="device")
     res, texts = _texts(b)
@@ -133,10 +123,10 @@ def test_mixed_errors_and_e2e_rerun():
 
 
 
-def test_document_past_the_block_limit(replay_mode):
-    """A document of 2.2 M inserted chars: more than the per-item tracker's 65,535 blocks
-    (n_ins / 32 + 2, MAX_DOC_BLOCKS: block ids are 16 bits in pc[] and the superblock lists).
-    Either tracker must report a status or the exact text, never a wrong text."""
+def test_document_past_the_block_limit():
+    """A document of 2.2 M inserted chars: more than the tracker's 65,535 blocks (n_ins / 32 + 2,
+    MAX_DOC_BLOCKS: block ids are 16 bits in pc[] and the superblock lists).  It must report a
+    status, never a wrong text."""
     o = dt_amd.ListOpLog()
     a = o.get_or_create_agent_id("big")
     text = ""
@@ -149,9 +139,4 @@ def test_document_past_the_block_limit(replay_mode):
     text = text[:1000] + text[250_000:]
     b = dt_amd.Batch(oplogs=[o])
     res, texts = _texts(b)
-    st = res[0]["status"]
-    if replay_mode == "item":
-        assert st == 65   # DTGPU_ERR_CAPACITY
-    assert st in (0, 65)
-    if st == 0:
-        assert texts[0] == text.encode()
+    assert res[0]["status"] == 65   # DTGPU_ERR_CAPACITY

@@ -6,7 +6,7 @@
 #   bench      bench.py line + rocprofv3 kernel stats + FETCH/WRITE passes   OUT/bp/ (tools/bench_profile.sh)
 #   kbench     friendsforever 1 / 10k, git-makefile, node_nodecc kernel ms  OUT/kbench.log
 #   kprof      per-document replay cycle profile (DTGPU_DEBUG=2)             OUT/kprof.log
-#   ab         kbench for every build in $LIBS (DTGPU_LIB_DIR) and every tracker in $MODES
+#   ab         kbench for every build in $LIBS (DTGPU_LIB_DIR, tools/variant.sh builds them)
 #   pmc        SQ / LDS / TCC counter passes on 10k friendsforever          OUT/pmc/ (tools/pmc.sh)
 #   mixed      bench.py --workload mixed (configs[4])                         OUT/mixed.json
 #   synth      bench.py --workload synth at $SYNTH_DOCS / $SYNTH_DISTINCT     OUT/synth.json
@@ -43,13 +43,9 @@ for s in ${STEPS//,/ }; do
       rc=$?; cut -c1-400 "$OUT/kprof.log"; ok kprof $rc ;;
     ab)
       for v in ${LIBS:-lib}; do
-        for m in ${MODES:-item}; do
-          if [[ $m == span ]]; then export DTGPU_REPLAY=span; else unset DTGPU_REPLAY; fi
-          DTGPU_LIB_DIR=$v kb > "$OUT/kbench_${v}_$m.log" 2>&1; rc=$?
-          echo "-- $v $m"; cut -c1-220 "$OUT/kbench_${v}_$m.log"; ok "ab $v $m" $rc
-        done
-      done
-      unset DTGPU_REPLAY ;;
+        DTGPU_LIB_DIR=$v kb > "$OUT/kbench_${v}.log" 2>&1; rc=$?
+        echo "-- $v"; cut -c1-220 "$OUT/kbench_${v}.log"; ok "ab $v" $rc
+      done ;;
     pmc)
       bash tools/pmc.sh "$OUT/pmc" python -u tools/kbench.py friendsforever 10000 1; ok pmc $? ;;
     mixed)
