@@ -91,6 +91,16 @@ __device__ __forceinline__ uint32_t entry_of(const uint2 *ent, uint32_t hi, uint
 #ifndef DTGPU_PREP_WAVES
 #define DTGPU_PREP_WAVES 8   // occupancy target (tuning knob; the register budget follows from it)
 #endif
+// CHECK (debug mode, DTGPU_DEBUG): every computed table index -- child slots, parent-vector rows,
+// chain pairs, chain offsets, dense chain slots, the parents and entries records read through
+// computed indexes -- is asserted inside the document's arena before it is used; a failure skips
+// the access and reports PREP_BOUNDS with the table (the host then fails the document), so a
+// layout bug shows up as a status instead of a stray store.  The release kernel is unchanged.
+#define PREP_ASSERT(cond, table)                                  \
+    do {                                                          \
+        if (CHECK && !(cond)) { oob = oob ? oob : (table); }      \
+    } while (0)
+template <bool CHECK>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_WAVES))) void prep_kernel(PrepParams P) {
     // per entry (u16, two per LDS word): child count, then the next free slot of its children
     // list relative to coff -- half the LDS of absolute u32 slots, so more documents share a CU
@@ -131,6 +141,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
         if (l == 0) { R.status = PREP_WIDE; P.results[doc] = R; }
         return;
     }
+    uint32_t oob = 0;   // CHECK: the first table whose bounds assert failed (per lane)
+    auto report_oob = [&]() -> bool {   // wave-uniform: true when a bounds assert failed anywhere
+        if (!CHECK) return false;
+        const uint64_t m = ballot(oob != 0);
+        if (!m) return false;
+        if (l == 0) { R.status = PREP_BOUNDS; R.pad = rdl(oob, ctz(m)); P.results[doc] = R; }
+        return true;
+    };
 
 #ifdef DTGPU_PREP_PROF
     const uint64_t T0 = wall_clock64();
@@ -147,6 +165,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
                 const uint32_t p = par_in[k];
                 const uint32_t pe = entry_of(ent, i, p);
                 if (pe == 0xFFFFFFFFu) { bad = true; break; }
+                PREP_ASSERT(pe < i, PREP_T_ENTRY);
                 owner[k] = i;
                 par[k] = p;
                 pent[k] = pe;
@@ -200,12 +219,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
                 todo = false;
             }
         }
-        if (live) {
+        PREP_ASSERT(!live || (key < ne && kco + krel + rank < npar), PREP_T_CHILD);
+        if (live && (!CHECK || !oob)) {
             child[kco + krel + rank] = own;
             if (rank + 1 == cnt) lfill[key] = uint16_t(krel + cnt);
         }
         __syncthreads();
     }
+    if (report_oob()) return;
 
 #ifdef DTGPU_PREP_PROF
     const uint64_t T2 = wall_clock64();
@@ -291,11 +312,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
                     prow = pc = psd = 0;
                     if (hit) { prow = ring_row[slot * 64 + l]; pc = ring_meta[3 * slot + 1]; psd = ring_meta[3 * slot + 2]; }
                     if (!hit) {
-                        prow = rows[size_t(pe) * PREP_MAX_CHAINS + l];
+                        PREP_ASSERT(pe < i, PREP_T_ROWS);
+                        prow = (!CHECK || pe < i) ? rows[size_t(pe) * PREP_MAX_CHAINS + l] : 0u;
                         if (pe >= (i & ~63u)) {   // not flushed yet: from the registers
                             pc = rdl(bch, pe & 63u); psd = rdl(bsd, pe & 63u);
                         } else {
-                            const uint2 q = cs[pe];
+                            PREP_ASSERT(pe < ne, PREP_T_PAIRS);
+                            const uint2 q = (!CHECK || pe < ne) ? cs[pe] : make_uint2(0, 0);
                             pc = q.x; psd = q.y;
                         }
                     }
@@ -339,6 +362,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
         }
     }
     wave_fence();
+    if (report_oob()) return;
 #ifdef DTGPU_PREP_PROF
     const uint64_t T4 = wall_clock64();
 #endif
@@ -348,6 +372,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
         const uint32_t c = l < nch ? clen : 0;
         const uint32_t inc = scan_incl(c);
         doff_l = inc - c;
+        PREP_ASSERT(rdl(inc, 63) == D.n_lv, PREP_T_DOFF);   // the chains partition the LVs
         if (l < nch) doff[l] = doff_l;
         if (l == 0) doff[nch] = rdl(inc, 63);
     }
@@ -355,7 +380,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
     // ---- 4. lane-parallel outputs -----------------------------------------------------------------
     for (uint32_t k = l; k < npar; k += 64) {   // parent slots: chain and ops of that chain up to it
         const uint32_t pe = pent[k];
-        const uint2 q = cs[pe];
+        PREP_ASSERT(pe < ne, PREP_T_PAIRS);
+        const uint2 q = (!CHECK || pe < ne) ? cs[pe] : make_uint2(0, 0);
         pch[k] = q.x;
         pcnt[k] = q.y + par[k] + 1;
     }
@@ -373,6 +399,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
         const uint32_t o0 = eop[i], o1 = eop[i + 1];
         const uint2 q = cs[i];
         const bool h0 = np > 0, h1 = np > 1;
+        PREP_ASSERT(p0 + np <= npar && c0 + nc <= npar && o0 <= o1 && o1 <= nops, PREP_T_ERECP);
+        if (CHECK && oob) continue;
         r[0] = make_uint4(e.x, e.y, p0, np);
         r[1] = make_uint4(o0, o1 - o0, q.x, q.y + e.x);
         r[2] = make_uint4(c0, nc, h0 ? par[p0] : 0xFFFFFFFFu, h0 ? pent[p0] : 0xFFFFFFFFu);
@@ -416,7 +444,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
                 qx = q.x; qy = q.y;
             }
             const uint32_t dch = uint32_t(__shfl(int(doff_l), int(qx & 63u)));
-            if (live) {
+            // the run's dense slots [dch + qy + lv, + len) lie inside the chain tables
+            PREP_ASSERT(!live || (qx < nch && uint64_t(uint32_t(dch + qy + o.x)) + o.y <= D.n_lv), PREP_T_DENSE);
+            if (live && (!CHECK || !oob)) {
                 const bool del = o.w & 1u;
                 opc[j] = Cmd{del ? (CMD_DEL | ((o.w & 2u) ? 16u : 0u)) : uint32_t(CMD_INS), o.x, o.y, o.z};
                 if (!del) n_ins += o.y;
@@ -436,6 +466,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
             ebase = rdl(i, min(nops - 1 - j0, 63u));
         }
     }
+    if (report_oob()) return;
 #ifdef DTGPU_PREP_PROF
     const uint64_t T5 = wall_clock64();
 #endif
@@ -520,8 +551,10 @@ int launch_prep(const PrepParams &p, void *stream) {
     // LDS: the child counts (u16 per entry), later the chain decomposition's ring (8 rows + meta)
     const size_t cw = (size_t(p.max_entries) + 1) / 2, rw = 8 * 64 + 24;
     const size_t lds = (cw > rw ? cw : rw) * 4;
-    hipLaunchKernelGGL(prep::prep_kernel, dim3(p.n_docs), dim3(64), lds,
-                       reinterpret_cast<hipStream_t>(stream), p);
+    if (p.check)
+        hipLaunchKernelGGL(prep::prep_kernel<true>, dim3(p.n_docs), dim3(64), lds, reinterpret_cast<hipStream_t>(stream), p);
+    else
+        hipLaunchKernelGGL(prep::prep_kernel<false>, dim3(p.n_docs), dim3(64), lds, reinterpret_cast<hipStream_t>(stream), p);
     return hipGetLastError() == hipSuccess ? 0 : 66;
 }
 

@@ -8,7 +8,11 @@
 namespace dtgpu {
 
 constexpr uint32_t PREP_MAX_CHAINS = 64;   // wider histories are prepared on the host
-enum : uint32_t { PREP_OK = 0, PREP_WIDE = 1, PREP_BAD = 2, PREP_SKIP = 3 };
+// PREP_BOUNDS: a debug-mode bounds assert failed (a table index outside the document's arena);
+// PrepResult.pad then names the table (PREP_T_*)
+enum : uint32_t { PREP_OK = 0, PREP_WIDE = 1, PREP_BAD = 2, PREP_SKIP = 3, PREP_BOUNDS = 4 };
+enum : uint32_t { PREP_T_CHILD = 1, PREP_T_ROWS = 2, PREP_T_PAIRS = 3, PREP_T_DOFF = 4, PREP_T_DENSE = 5, PREP_T_ERECP = 6,
+                  PREP_T_ENTRY = 7 };
 
 struct PrepDesc {
     // decoder arenas (offsets in the decoder's units: quads / pairs / words / bytes)
@@ -40,6 +44,7 @@ struct PrepParams {
     PrepResult *results;
     uint32_t n_docs, max_entries;   // n_docs: the grid (the list's length when doc_list is set)
     const uint32_t *doc_list;       // nullable: block i prepares docs[doc_list[i]]
+    uint32_t check;                 // debug mode (DTGPU_DEBUG): the bounds-checked kernel
 };
 
 // owner (n_par, padded to even), {chain, seq0 - start} pairs (2 ne), coff, eop (ne + 1 each): even,

@@ -136,6 +136,10 @@ template <typename T> DEV T vld(const T *p) { return *reinterpret_cast<const vol
 DEV const BatchParams &KP() {
     return *(const BatchParams *)(__builtin_amdgcn_kernarg_segment_ptr());
 }
+// A pointer re-read from the arguments is generic to the compiler: declare it global so its
+// accesses are global_load / global_store (vmcnt only), not flat.
+#define GLOBAL_AS __attribute__((address_space(1)))
+template <typename T> DEV GLOBAL_AS T *gp(T *p) { return (GLOBAL_AS T *)p; }
 template <typename T> DEV void st(T *p, T v) { *p = v; }
 // L2-coherent accesses (a load must never meet a stale L1 line of a word an atomic changed).
 template <typename T> DEV T ld_sc(const T *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
@@ -507,7 +511,7 @@ DEV uint32_t up_rank(Doc &D, uint32_t b, uint32_t s) {
 // block's items lane by lane (lanes >= the block count are don't-care); mv / ml its masks.
 template <bool L, bool PROF, bool XF>
 DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml, uint32_t lv, uint32_t k,
-                    uint32_t ol, uint32_t orr, uint32_t tph, uint32_t vs) {
+                    uint32_t ol, uint32_t orr, uint32_t tph, uint32_t vs, uint32_t c_in) {
     D.cb = NONE;
     const uint32_t l = lane_id();
     const uint32_t lv0 = lv, k0 = k;
@@ -516,7 +520,9 @@ DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml,
         for (uint32_t j = l; j < k0; j += 64) D.xf[lv0 + j] = r0 + j;
     }
     while (k > 0) {   // each round inserts >= 1 item or splits (bounded by max_blocks)
-        const uint32_t c = U(ix<L>(D.cnt + b));
+        // b's packed counts: the caller's clean copy on the first round, reloaded after a split
+        const uint32_t c = c_in != NONE ? c_in : U(ix<L>(D.cnt + b));
+        c_in = NONE;
         const uint32_t bc = c_items(c);
         if (bc == BLK) {
             const uint64_t t0 = tick<PROF>();
@@ -590,7 +596,7 @@ DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml,
 // over the agent runs; `lv` is wave-uniform.
 DEV void agent_of(Doc &D, uint32_t lv, uint32_t &rank, uint32_t &seq) {
     const uint32_t l = lane_id();
-    const uint32_t *aruns = vld(&KP().aruns) + U(uint32_t(vld(&D.desc->arun_off)));
+    const GLOBAL_AS uint32_t *aruns = gp(vld(&KP().aruns)) + U(uint32_t(vld(&D.desc->arun_off)));
     uint32_t lo = 0, n = U(vld(&D.desc->n_aruns));   // last run with start <= lv lies in [lo, lo+n)
     while (n > 64) {
         if (!charge(D)) { rank = seq = 0; return; }
@@ -742,6 +748,7 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
     if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_FIND] += t - tp; tp = t; }
     const uint32_t c0 = U(ix<L>(D.cnt + b));
     const uint32_t bc = c_items(c0);
+    uint32_t cb = c0 & ~C_DIRTY;   // b's packed counts once its masks are current
     uint32_t it;
     u64 mv, ml;
     if (b == D.cb) { it = D.cit; mv = D.cmv; ml = D.cml; }
@@ -794,14 +801,16 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
             // the scan passed only not-yet-inserted items: b0's visible items all lie before
             // the cursor and the blocks in between hold none
             vs += uint32_t(__popcll(mv));
+            cb = U(ix<L>(D.cnt + b));
             if (b == D.cb) { it = D.cit; mv = D.cmv; ml = D.cml; }
-            else load_block<L>(D, b, U(ix<L>(D.cnt + b)), it, mv, ml);
+            else load_block<L>(D, b, cb, it, mv, ml);
+            cb &= ~C_DIRTY;
             tph = NONE;
         }
         if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_YJS] += t - tp; tp = t; D.prof[P_N_YJS]++; }
     }
     const uint64_t sp0 = PROF ? D.prof[P_SPLIT] : 0;
-    insert_run<L, PROF, XF>(D, b, s, it, mv, ml, lv, k, ol, orr, tph, vs);
+    insert_run<L, PROF, XF>(D, b, s, it, mv, ml, lv, k, ol, orr, tph, vs, cb);
     if (PROF) D.prof[P_RUN] += tick<PROF>() - tp - (D.prof[P_SPLIT] - sp0);
 }
 
@@ -1018,11 +1027,11 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
 // Visibility comes from the counts (the final advance to the tip leaves masks stale): the
 // count and the byte offset of every item are gathered together, so this adds no round trip.
 template <bool L>
-DEV void materialise(Doc &D, uint8_t *out, uint32_t cap, uint32_t &len_out, u64 &hash_out, uint32_t &items_out) {
+DEV void materialise(Doc &D, GLOBAL_AS uint8_t *out, uint32_t cap, uint32_t &len_out, u64 &hash_out, uint32_t &items_out) {
     constexpr uint32_t G = 8;
     const uint32_t l = lane_id();
-    const uint32_t *cbyte = vld(&KP().cbyte) + vld(&D.desc->lv_off);
-    const uint8_t *content = vld(&KP().content) + vld(&D.desc->content_off);
+    const GLOBAL_AS uint32_t *cbyte = gp(vld(&KP().cbyte)) + vld(&D.desc->lv_off);
+    const GLOBAL_AS uint8_t *content = gp(vld(&KP().content)) + vld(&D.desc->content_off);
     const bool ascii = U(vld(&D.desc->ascii)) != 0;
     uint32_t total = 0, items = 0;
     u64 h = 0;
@@ -1249,7 +1258,7 @@ DEV void run_doc(Doc &D) {
     if (L && D.err == ErrCapacity && (D.site == 12 || D.site == 21)) {
         uint32_t *fb_list = vld(&KP().fb_list);
         if (fb_list) {
-            if (l == 0) fb_list[atomicAdd(vld(&KP().fb_count), 1u)] = D.doc;
+            if (l == 0) gp(fb_list)[atomicAdd(vld(&KP().fb_count), 1u)] = D.doc;
             return;
         }
     }
@@ -1257,10 +1266,10 @@ DEV void run_doc(Doc &D) {
     u64 h = 0;
     const uint64_t t_mat = tick<PROF>();
     if (!D.err) {
-        uint8_t *out = vld(&KP().out) + vld(&D.desc->out_off);
+        GLOBAL_AS uint8_t *out = gp(vld(&KP().out)) + vld(&D.desc->out_off);
         materialise<L>(D, out, U(vld(&D.desc->out_cap)), len, h, n_items);
     }
-    DocResult *res = vld(&KP().results) + D.doc;
+    GLOBAL_AS DocResult *res = gp(vld(&KP().results)) + D.doc;
     if (l == 0) {
         res->status = D.err;
         res->out_len = len;

@@ -597,6 +597,8 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     pp.aruns = B->d_aruns.p; pp.tip = B->p_tip.p; pp.erec = B->p_erec.p; pp.doff = B->p_doff.p; pp.dense = B->p_dense.p;
     pp.rows = B->pr_rows.p; pp.scr = B->pr_scr.p; pp.opc = B->p_opc.p;
     pp.docs = B->pr_docs.p; pp.results = B->pr_res.p; pp.n_docs = uint32_t(n); pp.max_entries = max_e;
+    // debug mode (DTGPU_DEBUG, or DTGPU_PREP_CHECK alone): the bounds-checked prep kernel
+    pp.check = (getenv("DTGPU_DEBUG") || getenv("DTGPU_PREP_CHECK")) ? 1u : 0u;
     if (launch_prep(pp, s)) return DTGPU_ERR_HIP;
     std::vector<PrepResult> prr(n);
     CK(hipMemcpyAsync(prr.data(), B->pr_res.p, n * sizeof(PrepResult), hipMemcpyDeviceToHost, s));

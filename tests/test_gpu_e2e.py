@@ -91,6 +91,21 @@ def test_split_pass_joins_big_tier(case):
             assert texts[1] == want1
 
 
+def test_prep_bounds_checked_kernel(monkeypatch):
+    """Debug mode (device-side bounds asserts): the prep kernel instantiated with an
+    assert on every computed table index (child slots, parent-vector rows, chain pairs and
+    offsets, dense chain slots, record fields) prepares the benchmark files and synthetic
+    concurrent documents with no assert firing, and the checkouts are exact."""
+    monkeypatch.setenv("DTGPU_PREP_CHECK", "1")
+    docs = [G.dt_bytes(n) for n in G.DT_FILES] + [dt_amd.synth_merge_oplog(i, 3000).encode() for i in range(6)]
+    b = dt_amd.Batch(docs=docs, staging="device")
+    res, texts = _texts(b)
+    assert [r["status"] for r in res] == [0] * len(docs)
+    assert b.host_planned() == [0] * len(docs)
+    for d, t in zip(docs, texts):
+        assert t == OracleOpLog.load_from(d).checkout_tip_bytes()
+
+
 def test_device_plan_equals_host_plan():
     docs = [G.dt_bytes(n) for n in G.DT_FILES]
     dev = dt_amd.Batch(docs=docs, staging="device")
