@@ -64,6 +64,15 @@ extern "C" {
     pub fn dtgpu_oplog_last_added_frontier(oplog: *const dtgpu_oplog, out: *mut u64, cap: usize) -> usize;
     pub fn dtgpu_oplog_dominators(oplog: *const dtgpu_oplog, a: *const u64, na: usize, b: *const u64, nb: usize,
                                   out: *mut u64, cap: usize) -> i64;
+    // multi-CRDT OpLog support (src/oplog.rs, src/branch.rs:180-232): a text's ops projected out of
+    // the shared graph, versions projected the same way, remote ids <-> LVs
+    pub fn dtgpu_oplog_project(oplog: *const dtgpu_oplog, spans: *const u64, n_spans: usize,
+                               out: *mut *mut dtgpu_oplog) -> dtgpu_status;
+    pub fn dtgpu_oplog_project_version(oplog: *const dtgpu_oplog, spans: *const u64, n_spans: usize,
+                                       version: *const u64, n_version: usize, out: *mut u64, cap: usize) -> i64;
+    pub fn dtgpu_oplog_local_to_remote(oplog: *const dtgpu_oplog, lv: u64, agent: *mut u32, seq: *mut u64) -> dtgpu_status;
+    pub fn dtgpu_oplog_remote_to_local(oplog: *const dtgpu_oplog, agent: u32, seq: u64, n: u64, spans: *mut u64,
+                                       cap: usize) -> i64;
     // checkout (src/list/oplog.rs:32-42) and transformed ops (src/list/merge.rs:24-48)
     pub fn dtgpu_checkout(oplog: *const dtgpu_oplog, version: *const u64, n_version: usize, out: *mut u8, cap: usize,
                           out_len: *mut usize) -> dtgpu_status;
