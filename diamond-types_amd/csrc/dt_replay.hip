@@ -213,29 +213,6 @@ DEV bool charge(Doc &D) {
 }
 template <bool PROF> DEV uint64_t tick() { return PROF ? __builtin_amdgcn_s_memtime() : 0; }
 
-// Cursor (content-tree cursor reuse, crates/content-tree/src/root.rs:50-89 keeps the last cursor
-// for the same reason): the first two LDS words of every workgroup hold {block, visible items
-// before that block in document order}.  It names the block the last insert / delete left in
-// registers (D.cb); an insert / delete whose position lands inside that block's visible range
-// skips the index descent.  Kept in LDS, not registers: the command loop is SGPR-bound.  A
-// retreat / advance pass that flips any visibility clears it (items before the block may have
-// changed).
-// LDS words 0-1: the cursor; 2-4: the prefetch helper's view of the main wave (HELP kernels):
-// the command it is applying, its superblock count, done.
-constexpr uint32_t CURSOR_BYTES = 32;
-enum : uint32_t { W_CUR_BLK = 0, W_CUR_VS = 1, W_HELP_CMD = 2, W_HELP_NSB = 3, W_HELP_DONE = 4 };
-DEV uint32_t *cursor_words() { extern __shared__ uint32_t smem_words[]; return smem_words; }
-DEV void cursor_set(uint32_t b, uint32_t vstart) {
-    if (lane_id() == 0) { cursor_words()[0] = b; cursor_words()[1] = vstart; }
-}
-DEV void cursor_clear() { if (lane_id() == 0) cursor_words()[0] = 0xFFFFFFFFu; }
-// Returns true and the block's visible start when the cursor names block cb.
-DEV bool cursor_get(uint32_t cb, uint32_t &vstart) {
-    const uint2 c = *reinterpret_cast<const uint2 *>(cursor_words());
-    vstart = U(c.y);
-    return cb != 0xFFFFFFFFu && U(c.x) == cb;
-}
-
 // Block -> (superblock << 6 | index in its list).  The LDS tier keeps it in 16 bits (its
 // superblock ids stay below 1024), which lets six documents share a SIMD instead of five.
 template <bool L> DEV uint32_t opos_of(const Doc &D, uint32_t b) {
@@ -514,7 +491,7 @@ DEV uint32_t up_rank(Doc &D, uint32_t b, uint32_t s) {
 // block's items lane by lane (lanes >= the block count are don't-care); mv / ml its masks.
 template <bool L, bool PROF, bool XF>
 DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml, uint32_t lv, uint32_t k,
-                    uint32_t ol, uint32_t orr, uint32_t tph, uint32_t vs, uint32_t c_in) {
+                    uint32_t ol, uint32_t orr, uint32_t tph, uint32_t c_in) {
     D.cb = NONE;
     const uint32_t l = lane_id();
     const uint32_t lv0 = lv, k0 = k;
@@ -534,7 +511,6 @@ DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml,
             if (D.err) return;
             tph = NONE;   // a split may move superblocks in the top order
             if (s > cut || cut == BLK) {
-                if (vs != NONE) vs += uint32_t(__popcll(mv & lanes_below(cut)));   // visible items left in b
                 b = b2;
                 s -= cut;
                 it = shfl(it, (l + cut) & 63u);
@@ -586,7 +562,6 @@ DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml,
         s += m;
     }
     D.cb = b; D.cit = it; D.cmv = mv; D.cml = ml;   // block state after the run
-    if (vs != NONE) cursor_set(b, vs); else cursor_clear();
     const uint64_t t3 = tick<PROF>();
     for (uint32_t j0 = 0; j0 < k0; j0 += 64) {   // wave-uniform loop, masked store
         const uint32_t j = j0 + l, nit = lv0 + j;
@@ -732,21 +707,15 @@ DEV void load_block(Doc &D, uint32_t b, uint32_t c, uint32_t &it, u64 &mv, u64 &
 template <bool L, bool PROF, bool XF>
 DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
     uint64_t tp = tick<PROF>();
-    // tph: top position of b's superblock (first block: 0); vs: visible items before b
-    uint32_t b, kk = 0, tph = 0, vs = 0;
+    uint32_t b, kk = 0, tph = 0;   // tph: top position of b's superblock (first block: 0)
     if (pos == 0) {
         b = first_block<L>(D);
-    } else if (cursor_get(D.cb, vs) && pos - 1 >= vs && pos - 1 - vs < uint32_t(__popcll(D.cmv))) {
-        b = D.cb;   // the cursor's block holds visible index pos - 1
-        kk = pos - 1 - vs;
-        tph = NONE;
     } else {
         Found f;
         if (!find_vis<L>(D, pos - 1, f)) { fail(D, ErrCheckout, 13); return; }
         b = f.b;
         kk = f.k;
         tph = f.tp;
-        vs = pos - 1 - f.k;
     }
     if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_FIND] += t - tp; tp = t; }
     const uint32_t c0 = U(ix<L>(D.cnt + b));
@@ -801,9 +770,6 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
         yjs_scan<L>(D, b, s, rb, rs, my_l, my_r, ol, orr, lv);
         if (D.err) return;
         if (b != b0) {
-            // the scan passed only not-yet-inserted items: b0's visible items all lie before
-            // the cursor and the blocks in between hold none
-            vs += uint32_t(__popcll(mv));
             cb = U(ix<L>(D.cnt + b));
             if (b == D.cb) { it = D.cit; mv = D.cmv; ml = D.cml; }
             else load_block<L>(D, b, cb, it, mv, ml);
@@ -813,7 +779,7 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
         if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_YJS] += t - tp; tp = t; D.prof[P_N_YJS]++; }
     }
     const uint64_t sp0 = PROF ? D.prof[P_SPLIT] : 0;
-    insert_run<L, PROF, XF>(D, b, s, it, mv, ml, lv, k, ol, orr, tph, vs, cb);
+    insert_run<L, PROF, XF>(D, b, s, it, mv, ml, lv, k, ol, orr, tph, cb);
     if (PROF) D.prof[P_RUN] += tick<PROF>() - tp - (D.prof[P_SPLIT] - sp0);
 }
 
@@ -825,19 +791,9 @@ DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
     uint32_t j0 = 0;
     uint32_t up_done = 0;   // XF: never-deleted items this run deleted in earlier (left) blocks
     while (j0 < n) {   // each round deletes >= 1 item or fails
-        uint32_t b, kk, tpos;
-        uint32_t vs;
-        if (cursor_get(D.cb, vs) && pos >= vs && pos - vs < uint32_t(__popcll(D.cmv))) {
-            b = D.cb;   // the cursor's block holds visible index pos
-            kk = pos - vs;
-            tpos = U(ix<L>(D.sbpos + (opos_of<L>(D, b) >> 6)));
-        } else {
-            Found f;
-            if (!find_vis<L>(D, pos, f)) { fail(D, ErrCheckout, 14); return; }
-            b = f.b;
-            kk = f.k;
-            tpos = f.tp;
-        }
+        Found f;
+        if (!find_vis<L>(D, pos, f)) { fail(D, ErrCheckout, 14); return; }
+        const uint32_t b = f.b, kk = f.k, tpos = f.tp;
         const uint32_t c0 = U(ix<L>(D.cnt + b));
         uint32_t it;
         u64 mv, ml;
@@ -884,7 +840,6 @@ DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
         }
         wave_fence();
         D.cb = b; D.cit = it; D.cmv = mv & ~selm; D.cml = ml;
-        cursor_set(b, pos - kk);
         j0 += take;
     }
 }
@@ -993,7 +948,6 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
         if (__ballot(bad)) { fail(D, ErrCheckout, 16); return; }
         const bool flip = fv || fl;
         if (__ballot(flip && b == D.cb)) D.cb = NONE;
-        if (__ballot(fv)) cursor_clear();   // visible items before the cursor's block may have moved
         if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_T2] += t - tq; tq = t; }
         if (L) {   // LDS index: per-lane LDS atomics
             if (flip) {
@@ -1165,7 +1119,7 @@ DEV uint32_t check_invariants(Doc &D, DocResult *res) {
     return 0;
 }
 
-template <bool L, bool PROF, bool XF, bool HELP>
+template <bool L, bool PROF, bool XF>
 DEV void run_doc(Doc &D) {
     const uint32_t l = lane_id();
     // fresh tracker: one empty block in one superblock (per-LV words are written when their
@@ -1184,7 +1138,6 @@ DEV void run_doc(Doc &D) {
     D.step_limit = uint32_t(min<uint64_t>(64ull * (uint64_t(D.ncmd) + D.n_lv) + 4096, 0xFFFFFFF0ull));
     D.site = 0;
     D.cb = NONE;
-    cursor_clear();
     D.cit = 0;
     D.cmv = D.cml = 0;
     if (PROF) for (int i = 0; i < P_N; i++) D.prof[i] = 0;
@@ -1200,7 +1153,6 @@ DEV void run_doc(Doc &D) {
         pre = D.cmds[min(base + l, D.ncmd - 1)];   // lanes past n_here are never read
         for (uint32_t j = 0; j < n_here && !D.err; j++) {
             ci = base + j;
-            if (HELP && l == 0) { cursor_words()[W_HELP_CMD] = ci; cursor_words()[W_HELP_NSB] = D.nsb; }
             const uint32_t op = U(bcast(pre.op, j)), a = U(bcast(pre.lv, j)), n = U(bcast(pre.len, j)),
                            pos = U(bcast(pre.pos, j));
             if (!charge(D)) break;
@@ -1293,81 +1245,6 @@ DEV void run_doc(Doc &D) {
     }
 }
 
-// ---- prefetch helper (HELP kernels: the biggest LDS tiers, a document alone or nearly alone on
-// its CU) ----------------------------------------------------------------------------------------
-// A second wave of the workgroup runs up to AHEAD commands in front of the replaying wave and
-// touches what they will load: for an insert / delete the block holding its position (found on
-// the LDS index, read while the replaying wave changes it: a torn read only picks a wrong block;
-// every index is clamped, so no access leaves the document's arenas), its item row and masks and,
-// when a retreat/advance pass left the block's masks stale, its items' counts; for a
-// retreat/advance pass its entries, the deleted items they name and those items' counts.  The
-// lines land in the CU's L1 and the XCD's L2 before the replaying wave asks for them (a
-// document of node_nodecc's size has ~15 MB of tracker state against a 4 MB L2).  The helper
-// writes nothing but one LDS word; it stops when the replaying wave sets W_HELP_DONE.
-constexpr uint32_t HELP_AHEAD = 2;
-template <bool L>
-DEV uint32_t help_block(const Doc &D, uint32_t p, uint32_t nsb) {
-    const uint32_t l = lane_id();
-    const uint32_t ms = D.max_sb, mb = D.max_blocks;
-    nsb = min(nsb, ms);
-    if (!nsb) return NONE;
-    uint32_t base = 0, S = NONE;
-    for (uint32_t c = 0; c < nsb; c += 64) {
-        const uint32_t i = c + l;
-        const uint32_t w = i < nsb ? ix<L>(D.top + i) : 0u;
-        const uint32_t v = w & 0xFFFFu;
-        const uint32_t inc = wave_scan(v);
-        const u64 m = __ballot(base + inc > p);
-        if (m) { S = U(bcast(w, first_lane(m)) >> 16); base += bcast(inc - v, first_lane(m)); break; }
-        base += bcast(inc, 63);
-    }
-    if (S >= ms) return NONE;
-    const uint32_t n = min(U(ix<L>(D.sbn + S)), SBC);
-    const uint32_t b0 = l < n ? ix16<L>(D.sbl + size_t(S) * SBC + l) : 0u;
-    const uint32_t b = b0 < mb ? b0 : 0u;
-    const uint32_t v = l < n ? c_vis(ix<L>(D.cnt + b)) : 0u;
-    const uint32_t inc = wave_scan(v);
-    const u64 m = __ballot(base + inc > p);
-    if (!m) return NONE;
-    return U(bcast(b, first_lane(m)));
-}
-template <bool L>
-DEV void help_doc(const Doc &D) {
-    const uint32_t l = lane_id();
-    volatile uint32_t *w = cursor_words();
-    uint32_t next = 0, acc = 0;
-    const uint32_t mb = D.max_blocks, nlv = D.n_lv;
-    for (uint64_t it = 0; it < 64ull * (uint64_t(D.ncmd) + 64); it++) {
-        if (w[W_HELP_DONE]) break;
-        const uint32_t cur = U(w[W_HELP_CMD]);
-        if (next <= cur) next = cur + 1;
-        if (next >= D.ncmd || next > cur + HELP_AHEAD) { __builtin_amdgcn_s_sleep(4); continue; }
-        const uint4 c = *reinterpret_cast<const uint4 *>(D.cmds + next);
-        const uint32_t op = U(c.x) & 15u, a = U(c.y), n = U(c.z), pos = U(c.w);
-        if (op == CMD_INS || op == CMD_DEL) {
-            const uint32_t p = op == CMD_INS ? (pos ? pos - 1 : 0) : pos;
-            const uint32_t b = help_block<L>(D, p, U(w[W_HELP_NSB]));
-            if (b < mb) {
-                const uint32_t item = D.items[size_t(b) * BLK + l];
-                const u64 mm = D.m2[2 * size_t(b) + (l & 1u)];
-                acc += item + uint32_t(mm);
-                if (ix<L>(D.cnt + b) & C_DIRTY) acc += D.pc[item < nlv ? item : 0u];
-            }
-        } else if (op == CMD_TOG && n) {
-            for (uint32_t k = 0; k < min(n, 128u); k += 64) {
-                const uint32_t e = D.tlist[a + min(k + l, n - 1)];
-                const uint32_t lv = min(e & 0x3FFFFFFFu, nlv - 1);
-                const bool del = (e >> 30) & 1u;
-                const uint32_t t = *reinterpret_cast<const uint32_t *>(D.ao + (del ? lv : 0u));
-                const uint32_t item = del ? t : lv;
-                acc += D.pc[item < nlv ? item : 0u];
-            }
-        }
-        next++;
-    }
-    if (acc == 0x9E3779B9u) w[5] = acc;   // keeps the touching loads; never true in practice
-}
-
 // Carve an index for `mb` blocks / `ms` superblocks out of `base` (LDS or HBM); layout must
 // match index_bytes().
 DEV void bind_index(Doc &D, uint8_t *base, uint32_t mb, uint32_t ms, bool narrow) {
@@ -1387,8 +1264,8 @@ DEV void bind_index(Doc &D, uint8_t *base, uint32_t mb, uint32_t ms, bool narrow
 #ifndef DTGPU_REPLAY_WAVES
 #define DTGPU_REPLAY_WAVES 1   // occupancy floor for the compiler's register budget (tuning knob)
 #endif
-template <bool LDS_INDEX, bool PROF, bool XF, bool HELP = false>
-__global__ __launch_bounds__(HELP ? 128 : 64) __attribute__((amdgpu_waves_per_eu(DTGPU_REPLAY_WAVES))) void replay_kernel(BatchParams P) {
+template <bool LDS_INDEX, bool PROF, bool XF>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_REPLAY_WAVES))) void replay_kernel(BatchParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t di = U(blockIdx.x);
     uint32_t d;
@@ -1418,7 +1295,7 @@ __global__ __launch_bounds__(HELP ? 128 : 64) __attribute__((amdgpu_waves_per_eu
     if (LDS_INDEX) {
         if (D.max_blocks > P.lds_blocks) D.max_blocks = P.lds_blocks;
         D.max_sb = P.lds_sb;
-        bind_index(D, smem + CURSOR_BYTES, P.lds_blocks, D.max_sb, true);
+        bind_index(D, smem, P.lds_blocks, D.max_sb, true);
     } else {
         bind_index(D, P.gidx + dd.gidx_off, D.max_blocks, D.max_sb, false);
     }
@@ -1427,37 +1304,24 @@ __global__ __launch_bounds__(HELP ? 128 : 64) __attribute__((amdgpu_waves_per_eu
         D.tup = P.tup + dd.blk_off + 2ull * d;   // sb_capacity(mb) <= mb + 2 slots per document
         D.xf = P.xf + dd.lv_off;
     }
-    if (HELP) {   // wave 1: the prefetch helper; wave 0 replays
-        if (threadIdx.x == 0) { cursor_words()[W_HELP_CMD] = 0; cursor_words()[W_HELP_NSB] = 1; cursor_words()[W_HELP_DONE] = 0; }
-        __syncthreads();
-        if (threadIdx.x >= 64) { help_doc<LDS_INDEX>(D); return; }
-    }
-    run_doc<LDS_INDEX, PROF, XF, HELP>(D);
-    if (HELP && lane_id() == 0) cursor_words()[W_HELP_DONE] = 1;
+    run_doc<LDS_INDEX, PROF, XF>(D);
 }
 
 }  // namespace dev
 
-static int launch_lds_tier(const BatchParams &q, hipStream_t s, bool prof, bool help) {
+static int launch_lds_tier(const BatchParams &q, hipStream_t s, bool prof) {
     if (!q.n_list) return OK;
-    size_t lds = size_t(index_bytes_ms(q.lds_blocks, q.lds_sb, true)) + dev::CURSOR_BYTES;
+    size_t lds = size_t(index_bytes_ms(q.lds_blocks, q.lds_sb, true));
     if (const char *pad = getenv("DTGPU_LDS_PAD")) lds += size_t(strtoul(pad, nullptr, 10));   // occupancy experiments
     if (lds > 160 * 1024) return ErrArg;   // a tier cap above the CU's LDS
     // allow dynamic LDS up to the CU's 160 KiB: a per-function, per-device attribute, set on
     // every launch (cheap) so it holds on whatever device the batch runs
-    const void *fn = help ? (prof ? reinterpret_cast<const void *>(&dev::replay_kernel<true, true, false, true>)
-                                  : reinterpret_cast<const void *>(&dev::replay_kernel<true, false, false, true>))
-                          : (prof ? reinterpret_cast<const void *>(&dev::replay_kernel<true, true, false>)
-                                  : reinterpret_cast<const void *>(&dev::replay_kernel<true, false, false>));
+    const void *fn = prof ? reinterpret_cast<const void *>(&dev::replay_kernel<true, true, false>)
+                          : reinterpret_cast<const void *>(&dev::replay_kernel<true, false, false>);
     if (lds > 64 * 1024 && hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
         return ErrHip;
-    if (help) {
-        if (prof) hipLaunchKernelGGL((dev::replay_kernel<true, true, false, true>), dim3(q.n_list), dim3(128), lds, s, q);
-        else hipLaunchKernelGGL((dev::replay_kernel<true, false, false, true>), dim3(q.n_list), dim3(128), lds, s, q);
-    } else {
-        if (prof) hipLaunchKernelGGL((dev::replay_kernel<true, true, false>), dim3(q.n_list), dim3(64), lds, s, q);
-        else hipLaunchKernelGGL((dev::replay_kernel<true, false, false>), dim3(q.n_list), dim3(64), lds, s, q);
-    }
+    if (prof) hipLaunchKernelGGL((dev::replay_kernel<true, true, false>), dim3(q.n_list), dim3(64), lds, s, q);
+    else hipLaunchKernelGGL((dev::replay_kernel<true, false, false>), dim3(q.n_list), dim3(64), lds, s, q);
     return hipGetLastError() == hipSuccess ? OK : ErrHip;
 }
 
@@ -1487,14 +1351,9 @@ int launch_replay(const ReplayLaunch &r) {
                     hipSuccess)
                     return ErrHip;
         }
-        // the prefetch helper wave rides with the tiers from DTGPU_HELP_TIER up (default 2: the
-        // two biggest, whose documents have a CU, or half of one, to themselves)
-        int help_tier = 2;
-        if (const char *h = getenv("DTGPU_HELP_TIER")) help_tier = atoi(h);
         for (int t = r.n_lds - 1; t >= 0; t--) {
             const int k = r.n_lds - 1 - t;
-            const int e = launch_lds_tier(r.lds[t], (fork && k < n_side) ? reinterpret_cast<hipStream_t>(r.side[k]) : s, prof,
-                                          t >= help_tier);
+            const int e = launch_lds_tier(r.lds[t], (fork && k < n_side) ? reinterpret_cast<hipStream_t>(r.side[k]) : s, prof);
             if (e) return e;
         }
         if (fork) {
@@ -1517,8 +1376,8 @@ int launch_replay(const ReplayLaunch &r) {
     // HBM tier: its own list plus a slot per LDS-tier document that may be handed back
     const uint32_t grid = large.n_list + (large.fb_list ? large.fb_slots : 0);
     if (grid) {
-        if (prof) hipLaunchKernelGGL((dev::replay_kernel<false, true, false>), dim3(grid), dim3(64), dev::CURSOR_BYTES, s, large);
-        else hipLaunchKernelGGL((dev::replay_kernel<false, false, false>), dim3(grid), dim3(64), dev::CURSOR_BYTES, s, large);
+        if (prof) hipLaunchKernelGGL((dev::replay_kernel<false, true, false>), dim3(grid), dim3(64), 0, s, large);
+        else hipLaunchKernelGGL((dev::replay_kernel<false, false, false>), dim3(grid), dim3(64), 0, s, large);
         if (hipGetLastError() != hipSuccess) return ErrHip;
     }
     return OK;
@@ -1530,7 +1389,7 @@ int launch_replay_xf(const BatchParams &large, void *stream) {
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (!large.n_list) return OK;
     if (!large.xf || !large.mup || !large.tup) return ErrArg;
-    hipLaunchKernelGGL((dev::replay_kernel<false, false, true>), dim3(large.n_list), dim3(64), dev::CURSOR_BYTES, s, large);
+    hipLaunchKernelGGL((dev::replay_kernel<false, false, true>), dim3(large.n_list), dim3(64), 0, s, large);
     return hipGetLastError() == hipSuccess ? OK : ErrHip;
 }
 

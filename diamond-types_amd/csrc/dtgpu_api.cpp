@@ -36,8 +36,7 @@ namespace {
 // documents many per CU, a node_nodecc-sized one alone on a CU.  Bigger documents and LDS
 // overflows replay on the HBM-index tier.
 constexpr int kLdsTiers = kMaxLdsTiers;
-// index bytes per tier; the replay adds 16 bytes of cursor (dt_replay.hip CURSOR_BYTES)
-constexpr uint64_t kItemTierCap[kLdsTiers] = {12 * 1024 - 16, 32 * 1024 - 16, 64 * 1024 - 16, 160 * 1024 - 16};
+constexpr uint64_t kItemTierCap[kLdsTiers] = {12 * 1024, 32 * 1024, 64 * 1024, 160 * 1024};
 int item_tier(uint32_t est) {
     const uint64_t bytes = index_bytes_ms(est, lds_sb_capacity(est), true);
     for (int t = 0; t < kLdsTiers; t++) if (bytes <= kItemTierCap[t]) return t;

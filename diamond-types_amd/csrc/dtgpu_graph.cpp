@@ -171,7 +171,8 @@ extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *h
                 }
                 if (hw) {
                     CK(d_hscr.alloc(hw));
-                    CK(d_q.upload(q, st));
+                    // the heap offsets into the same query buffer (P and the level kernels hold it)
+                    CK(hipMemcpyAsync(d_q.p, q.data(), nq * sizeof(GraphQuery), hipMemcpyHostToDevice, st));
                     P.hscr = d_hscr.p;
                     if (launch_graph_queries(P, st, true)) { rc = DTGPU_ERR_HIP; goto done; }
                 }
