@@ -27,7 +27,7 @@ struct DocResult {
     uint32_t n_items, n_blocks;
     uint32_t fail_cmd, fail_site;   // diagnostics: command index and code site of the first error
     uint32_t n_sb, lds;             // superblocks at the end; 1 when the index was in LDS
-    uint32_t dbg[20];               // DTGPU_DEBUG invariant-failure detail / cycle profile
+    uint32_t dbg[22];               // DTGPU_DEBUG invariant-failure detail / cycle profile
 };
 
 // Packed per-item location word (dt_replay.hip): count | block | slot.

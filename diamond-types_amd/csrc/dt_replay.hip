@@ -158,7 +158,7 @@ template <bool L> DEV uint32_t ix(const uint32_t *p) {
 template <bool L> DEV uint32_t ix16(const uint16_t *p) { return *p; }
 
 enum ProfSlot { P_INS = 0, P_DEL, P_TOG, P_MAT, P_YJS, P_SPLIT, P_FIND, P_BLOAD, P_ORR, P_RUN, P_R1, P_R2, P_R3, P_N_YJS, P_N_SPLIT,
-                P_T1, P_T2, P_T3, P_N };   // P_T*: retreat/advance pass split (entries + merge, counts, index)
+                P_T1, P_T2, P_T3, P_N_DIRTY, P_N_LOAD, P_N };   // P_T*: retreat/advance pass split (entries + merge, counts, index)
 
 struct Doc {
     // inputs
@@ -682,10 +682,11 @@ DEV void yjs_scan(Doc &D, uint32_t &b, uint32_t &s, uint32_t rb, uint32_t rs, ui
 // Items and masks of block b (packed count c) into registers: items lane by lane, masks
 // wave-uniform.  A block whose masks a retreat/advance pass invalidated (DIRTY) gets them
 // rebuilt from the items' counts and stored back clean.
-template <bool L>
+template <bool L, bool PROF = false>
 DEV void load_block(Doc &D, uint32_t b, uint32_t c, uint32_t &it, u64 &mv, u64 &ml) {
     const uint32_t l = lane_id();
     const uint32_t bc = c_items(c);
+    if (PROF) { D.prof[P_N_LOAD]++; if (c & C_DIRTY) D.prof[P_N_DIRTY]++; }
     const uint32_t it0 = D.items[size_t(b) * BLK + l];   // the row holds BLK slots
     it = l < bc ? it0 : 0;
     if (c & C_DIRTY) {
@@ -724,7 +725,7 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
     uint32_t it;
     u64 mv, ml;
     if (b == D.cb) { it = D.cit; mv = D.cmv; ml = D.cml; }
-    else load_block<L>(D, b, c0, it, mv, ml);
+    else load_block<L, PROF>(D, b, c0, it, mv, ml);
     uint32_t s = 0, ol = ROOT_ID;
     if (pos) {
         const uint32_t s0 = select_bit(mv, kk);
@@ -748,7 +749,7 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
         if (rb != NONE) {
             uint32_t rit;
             u64 rmv, rml;
-            load_block<L>(D, rb, U(ix<L>(D.cnt + rb)), rit, rmv, rml);
+            load_block<L, PROF>(D, rb, U(ix<L>(D.cnt + rb)), rit, rmv, rml);
             rs = first_lane(rml);
             orr = U(bcast(rit, rs));
         } else {
@@ -772,7 +773,7 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
         if (b != b0) {
             cb = U(ix<L>(D.cnt + b));
             if (b == D.cb) { it = D.cit; mv = D.cmv; ml = D.cml; }
-            else load_block<L>(D, b, cb, it, mv, ml);
+            else load_block<L, PROF>(D, b, cb, it, mv, ml);
             cb &= ~C_DIRTY;
             tph = NONE;
         }
@@ -785,7 +786,7 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
 
 // Apply a delete run: n visible items from position pos (merge.rs:457-556).  LV lv+j targets
 // the j-th item (fwd) or the (n-1-j)-th item (reversed / backspace runs, op_metrics.rs:184-202).
-template <bool L, bool XF>
+template <bool L, bool PROF, bool XF>
 DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
     const uint32_t l = lane_id();
     uint32_t j0 = 0;
@@ -798,7 +799,7 @@ DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
         uint32_t it;
         u64 mv, ml;
         if (b == D.cb) { it = D.cit; mv = D.cmv; ml = D.cml; }
-        else load_block<L>(D, b, c0, it, mv, ml);
+        else load_block<L, PROF>(D, b, c0, it, mv, ml);
         const uint32_t c = c0 & ~C_DIRTY;   // load_block left the block clean
         const uint32_t avail = c_vis(c) - kk;
         const uint32_t take = min(avail, n - j0);
@@ -1192,7 +1193,7 @@ DEV void run_doc(Doc &D) {
                     break;
                 case CMD_DEL:
                     if (n == 0 || a >= D.n_lv || n > D.n_lv - a) { fail(D, ErrCheckout, 17); break; }
-                    do_delete<L, XF>(D, a, n, pos, (op & 16u) != 0);
+                    do_delete<L, PROF, XF>(D, a, n, pos, (op & 16u) != 0);
                     if (PROF) D.prof[P_DEL] += tick<PROF>() - t0;
                     break;
                 case CMD_TOG:
@@ -1240,7 +1241,9 @@ DEV void run_doc(Doc &D) {
             D.prof[P_MAT] = tick<PROF>() - t_mat;
             for (int i = 0; i < P_T1; i++) res->dbg[i] = uint32_t(D.prof[i] >> (i < P_N_YJS ? 4 : 0));
             res->dbg[15] = uint32_t((tick<PROF>() - t_start) >> 4);
-            for (int i = P_T1; i < P_N; i++) res->dbg[16 + (i - P_T1)] = uint32_t(D.prof[i] >> 4);
+            for (int i = P_T1; i < P_N_DIRTY; i++) res->dbg[16 + (i - P_T1)] = uint32_t(D.prof[i] >> 4);
+            res->dbg[19] = uint32_t(D.prof[P_N_DIRTY]);
+            res->dbg[20] = uint32_t(D.prof[P_N_LOAD]);
         }
     }
 }

@@ -1427,7 +1427,7 @@ dtgpu_status dtgpu_batch_plan_profile(dtgpu_batch *B, size_t i, uint64_t out[8])
     out[7] = r.ntlist;
     return DTGPU_OK;
 }
-dtgpu_status dtgpu_batch_doc_stats(dtgpu_batch *B, size_t i, uint32_t out[27]) {
+dtgpu_status dtgpu_batch_doc_stats(dtgpu_batch *B, size_t i, uint32_t out[29]) {
     if (!B || i >= B->n || !out) return DTGPU_ERR_ARG;
     DocResult r;
     if (hipMemcpyAsync(&r, B->d_results.p + i, sizeof r, hipMemcpyDeviceToHost, B->stream) != hipSuccess ||
@@ -1439,6 +1439,8 @@ dtgpu_status dtgpu_batch_doc_stats(dtgpu_batch *B, size_t i, uint32_t out[27]) {
     out[22] = r.n_sb;
     out[23] = r.lds;
     for (int k = 0; k < 3; k++) out[24 + k] = r.dbg[16 + k];
+    out[27] = r.dbg[19];   // block loads that rebuilt stale masks
+    out[28] = r.dbg[20];   // block loads (not from the registers' cached block)
     return DTGPU_OK;
 }
 uint64_t dtgpu_batch_total_lv(const dtgpu_batch *B) { return B ? B->total_lv : 0; }

@@ -278,8 +278,9 @@ uint64_t dtgpu_batch_algorithmic_bytes(dtgpu_batch *batch);
  * command, [3] failing site, [4] commands, [5] block capacity, [6..21] profile / debug words
  * (DTGPU_DEBUG=2: cycles/16 in insert, delete, retreat+advance, materialise, YjsMod scans,
  * splits, and the insert phases find / block load / origin_right / run; scan and split
- * counts; total cycles/16). */
-dtgpu_status dtgpu_batch_doc_stats(dtgpu_batch *batch, size_t doc, uint32_t out[27]);
+ * counts; total cycles/16), [22] superblocks, [23] 1 if the index was in LDS, [24..26] the
+ * retreat/advance pass split, [27] block loads that rebuilt stale masks, [28] block loads. */
+dtgpu_status dtgpu_batch_doc_stats(dtgpu_batch *batch, size_t doc, uint32_t out[29]);
 /* Device planner cycle profile of one document (DTGPU_PLAN_PROF set at batch creation):
  * out[0..5] cycles waiting for entry records, computing parent vectors, children + next pick,
  * emitting retreat/advance entries, copying op runs, initialising; out[6] commands, out[7]

@@ -32,7 +32,7 @@ def main():
         parts = " ".join(f"{k[4:]}={v / 1e6:.2f}M({100 * v / tot:.0f}%)" for k, v in cyc.items())
         print(f"{name}x{copies}: status={res['status']} ms={ms:.2f} cmds={st['n_cmds']} items={st['n_items']} "
               f"blocks={st['n_blocks']}/{st['max_blocks']} sb={st['n_sb']} lds={st['lds_index']} yjs={st['n_yjs']} splits={st['n_split']} "
-              f"hits={st['n_hit']} runs={st['n_runs']} relinked={st['n_relink']} {parts}",
+              f"loads={st['n_load']} dirty={st['n_dirty']} {parts}",
               flush=True)
 
 
