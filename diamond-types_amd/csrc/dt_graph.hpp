@@ -73,10 +73,11 @@ int launch_graph_queries(const GraphParams &p, void *stream, bool big);
 inline uint32_t conflict_level_tps(uint64_t n_ent, uint64_t n_par, uint32_t na, uint32_t nb) {
     return uint32_t(4 + n_ent + n_par + na + nb);
 }
-// marks (2 words per entry), bucket heads, candidates, the time-point pool (4 words each) and an
-// HBM bucket for entries that more than BUCKET_CAP points enter (one word per point)
+// marks (2 words per entry), bucket heads, candidates, the time-point pool (kLevelPointWords
+// each) and an HBM bucket for entries that more than BUCKET_CAP points enter (one word per point)
+constexpr uint32_t kLevelPointWords = 5;
 inline uint64_t conflict_level_words(uint64_t n_ent, uint64_t n_par, uint32_t na, uint32_t nb) {
-    return 4 * n_ent + 5ull * conflict_level_tps(n_ent, n_par, na, nb);
+    return 4 * n_ent + (kLevelPointWords + 1ull) * conflict_level_tps(n_ent, n_par, na, nb);
 }
 struct LevelGraph { uint32_t ent_off, n_ent; };
 // The query kernels keep the marks (2 words per entry) in LDS when every levelled graph of the

@@ -244,14 +244,16 @@ __global__ __launch_bounds__(256) void level_diff_kernel(LevelParams P, GraphPar
 enum : uint32_t { F_A = 0, F_B = 1, F_S = 2 };
 enum : uint32_t { TP_ONE = 0, TP_PARENTS = 1, TP_QA = 2, TP_QB = 3 };
 constexpr int32_t ROOT_LV = -1;
+constexpr uint32_t PW = kLevelPointWords;
 constexpr uint32_t BUCKET_CAP = 64;   // time points that enter one entry sorted in LDS (more: in HBM)
 
-// A time point (the reference's TimePoint + DiffFlag) in the query's pool: 4 words
-// {next in its bucket, flag | kind << 2, frontier size, reference}: a single LV (TP_ONE: ref =
-// the LV), an entry's parents (TP_PARENTS: ref = the entry), or one of the two versions.
+// A time point (the reference's TimePoint + DiffFlag) in the query's pool: PW words
+// {next in its bucket, flag | kind << 2, frontier size, reference, last element}: a single LV
+// (TP_ONE: ref = the LV), an entry's parents (TP_PARENTS: ref = the entry), or one of the two
+// versions.
 struct Sweep {
     const Ent *E;
-    const uint32_t *par;
+    const uint32_t *par, *pent;   // parent LVs and their entries (per parent slot)
     const int32_t *qa, *qb;   // the two versions (frontier arena)
     int32_t *head;
     uint32_t *pool;
@@ -259,7 +261,7 @@ struct Sweep {
     bool overflow;
 
     __device__ int32_t elem(uint32_t tp, uint32_t k) const {
-        const uint32_t *w = pool + 4 * size_t(tp);
+        const uint32_t *w = pool + PW * size_t(tp);
         switch (w[1] >> 2) {
             case TP_ONE: return int32_t(w[3]);
             case TP_PARENTS: return int32_t(par[E[w[3]].poff + k]);
@@ -267,9 +269,9 @@ struct Sweep {
             default: return qb[k];
         }
     }
-    __device__ uint32_t size(uint32_t tp) const { return pool[4 * size_t(tp) + 2]; }
-    __device__ uint32_t flag(uint32_t tp) const { return pool[4 * size_t(tp) + 1] & 3u; }
-    __device__ int32_t last(uint32_t tp) const { const uint32_t s = size(tp); return s ? elem(tp, s - 1) : ROOT_LV; }
+    __device__ uint32_t size(uint32_t tp) const { return pool[PW * size_t(tp) + 2]; }
+    __device__ uint32_t flag(uint32_t tp) const { return pool[PW * size_t(tp) + 1] & 3u; }
+    __device__ int32_t last(uint32_t tp) const { return int32_t(pool[PW * size_t(tp) + 4]); }
     __device__ bool same(uint32_t x, uint32_t y) const {   // TimePoint equality: the whole frontier
         const uint32_t s = size(x);
         if (s != size(y)) return false;
@@ -284,20 +286,28 @@ struct Sweep {
         if (size(x) != size(y)) return size(x) < size(y);
         return flag(x) > flag(y);
     }
-    __device__ void push(uint32_t kind, uint32_t ref, uint32_t sz, uint32_t f) {
+    // `e`: the entry holding the point's last element when the caller knows it (the levelling's
+    // parent-slot entries), n when it must be searched (the versions)
+    __device__ void push(uint32_t kind, uint32_t ref, uint32_t sz, uint32_t f, int32_t l, uint32_t e) {
         if (used >= cap) { overflow = true; return; }
         const uint32_t tp = used++;
-        uint32_t *w = pool + 4 * size_t(tp);
+        uint32_t *w = pool + PW * size_t(tp);
         w[1] = f | (kind << 2);
         w[2] = sz;
         w[3] = ref;
+        w[4] = uint32_t(l);
         npend++;
-        const int32_t l = last(tp);
         if (l == ROOT_LV) { w[0] = 0xFFFFFFFFu; return; }   // ROOT: popped only when nothing else is left
-        const uint32_t e = find(E, n, l);
+        if (e == n) e = find(E, n, l);
         if (e == n) { overflow = true; return; }
         w[0] = uint32_t(head[e]);
         head[e] = int32_t(tp);
+    }
+    // element k of point tp as a TP_ONE point (a shattered frontier)
+    __device__ void push_elem(uint32_t tp, uint32_t k, uint32_t f) {
+        const uint32_t *w = pool + PW * size_t(tp);
+        const int32_t x = elem(tp, k);
+        push(TP_ONE, uint32_t(x), 1, f, x, (w[1] >> 2) == TP_PARENTS ? pent[E[w[3]].poff + k] : n);
     }
 };
 
@@ -385,16 +395,16 @@ __global__ __launch_bounds__(256) void level_conflict_kernel(LevelParams P, Grap
     }
     if (t != 0) return;
     // ---- the sweep (one thread) ----
-    Sweep S{E, P.par, qa, qb, head, pool, n, q.scr_tp, 0, 0, false};
-    uint32_t *hbk = pool + 4 * size_t(q.scr_tp);   // an entry's bucket past BUCKET_CAP points
+    Sweep S{E, P.par, P.pent, qa, qb, head, pool, n, q.scr_tp, 0, 0, false};
+    uint32_t *hbk = pool + PW * size_t(q.scr_tp);   // an entry's bucket past BUCKET_CAP points
     RevSpans sp{out, q.out_cap / 3, 0, 3, 0, 0, 0, false, false};
     // a span's flag is its membership: x in H(a) iff x <= mA[e], in H(b) iff x <= mB[e]
     auto mflag = [&](uint32_t e, int32_t x) -> uint32_t {
         const bool ia = x <= mA[e], ib = x <= mB[e];
         return ia && ib ? F_S : (ia ? F_A : F_B);
     };
-    S.push(TP_QA, 0, q.na, F_A);
-    S.push(TP_QB, 0, q.nb, F_B);
+    S.push(TP_QA, 0, q.na, F_A, q.na ? qa[q.na - 1] : ROOT_LV, n);
+    S.push(TP_QB, 0, q.nb, F_B, q.nb ? qb[q.nb - 1] : ROOT_LV, n);
     uint32_t st = GQ_OK, nc = 0;
     const uint32_t ncand = s_ncand;
     uint32_t ci = 0;
@@ -411,10 +421,10 @@ __global__ __launch_bounds__(256) void level_conflict_kernel(LevelParams P, Grap
         // the bucket in heap order (insertion sort; buckets are small -- in LDS up to BUCKET_CAP
         // points, in the query's HBM scratch beyond)
         uint32_t m = 0;
-        for (int32_t x = head[e]; x >= 0; x = int32_t(pool[4 * size_t(x)])) m++;
+        for (int32_t x = head[e]; x >= 0; x = int32_t(pool[PW * size_t(x)])) m++;
         uint32_t *bk = m <= BUCKET_CAP ? bkl : hbk;
         m = 0;
-        for (int32_t x = head[e]; x >= 0; x = int32_t(pool[4 * size_t(x)])) {
+        for (int32_t x = head[e]; x >= 0; x = int32_t(pool[PW * size_t(x)])) {
             uint32_t j = m++;
             while (j > 0 && S.before(uint32_t(x), bk[j - 1])) { bk[j] = bk[j - 1]; j--; }
             bk[j] = uint32_t(x);
@@ -436,7 +446,7 @@ __global__ __launch_bounds__(256) void level_conflict_kernel(LevelParams P, Grap
             for (uint32_t k = 0; k < sz; k++) common[nc++] = S.elem(T, k);
             break;
         }
-        for (uint32_t k = 0; k + 1 < S.size(T); k++) S.push(TP_ONE, uint32_t(S.elem(T, k)), 1, flag);   // shatter
+        for (uint32_t k = 0; k + 1 < S.size(T); k++) S.push_elem(T, k, flag);   // shatter
         const int32_t es = E[e].start;
         int32_t re = S.last(T) + 1;
         bool stopped = false;
@@ -448,7 +458,7 @@ __global__ __launch_bounds__(256) void level_conflict_kernel(LevelParams P, Grap
                 sp.push(ul + 1, re, mflag(uint32_t(e), re - 1));
                 re = ul + 1;
             }
-            for (uint32_t k = 0; k + 1 < S.size(u); k++) S.push(TP_ONE, uint32_t(S.elem(u, k)), 1, S.flag(u));
+            for (uint32_t k = 0; k + 1 < S.size(u); k++) S.push_elem(u, k, S.flag(u));
             if (S.flag(u) != flag) flag = F_S;
             if (S.npend == 0) {   // nothing left but this point: it is the common version
                 if (!q.c_cap) { st = GQ_OVERFLOW; stopped = true; break; }
@@ -459,8 +469,9 @@ __global__ __launch_bounds__(256) void level_conflict_kernel(LevelParams P, Grap
         }
         if (stopped) break;
         sp.push(es, re, mflag(uint32_t(e), re - 1));
-        const uint32_t np = E[e + 1].poff - E[e].poff;
-        S.push(TP_PARENTS, uint32_t(e), np, flag);
+        const uint32_t p0 = E[e].poff, np = E[e + 1].poff - p0;
+        if (np) S.push(TP_PARENTS, uint32_t(e), np, flag, int32_t(P.par[p0 + np - 1]), P.pent[p0 + np - 1]);
+        else S.push(TP_PARENTS, uint32_t(e), 0, flag, ROOT_LV, n);
     }
     if (st == GQ_OK && S.overflow) st = GQ_OVERFLOW;
     sp.flush();

@@ -11,6 +11,7 @@
 #   mixed      bench.py --workload mixed (configs[4])                         OUT/mixed.json
 #   synth      bench.py --workload synth at $SYNTH_DOCS / $SYNTH_DISTINCT     OUT/synth.json
 #   plan       planner cycle profile                                         OUT/plan.log
+#   level      heap walk vs level-synchronous graph queries                 OUT/level.log
 OUT=${1:?outdir}; STEPS=${2:?steps}; shift 2
 [[ $1 == -- ]] && shift
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
@@ -56,6 +57,9 @@ for s in ${STEPS//,/ }; do
       timeout -k 10 900 python -u bench.py --workload synth --distinct ${SYNTH_DISTINCT:-1024} \
         --docs ${SYNTH_DOCS:-20000} --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/synth.json" 2> "$OUT/synth.err"
       rc=$?; head -c 400 "$OUT/synth.json"; echo; tail -3 "$OUT/synth.err"; ok synth $rc ;;
+    level)
+      timeout -k 10 300 python -u tools/level_bench.py > "$OUT/level.log" 2>&1
+      rc=$?; cat "$OUT/level.log"; ok level $rc ;;
     plan)
       timeout -k 10 200 python -u tools/kprof.py --plan friendsforever friendsforeverx10000 git-makefile node_nodecc \
         > "$OUT/plan.log" 2>&1
