@@ -96,9 +96,20 @@ struct LevelParams {
     const LevelGraph *graphs;
     uint32_t n_graphs;
     uint32_t lds_ent;             // query kernels: the marks of graphs up to this many entries in LDS
+    uint32_t lvl_lds;             // level_kernel: its counters and frontier queue in LDS for graphs up
+                                  // to this many entries (0: in gscr / order in HBM)
+    uint32_t sweep_pts;           // conflict sweep, first pass: LDS capacity in live time points
+    uint32_t *prof;               // nullable (DTGPU_LVL_PROF): per conflict query 4 words -- cycles/16
+                                  // in marks, candidate list, sweep; entries the sweep visited
 };
+// level_kernel keeps child counts, CSR offsets, pending counts and the level-order queue (4 words
+// per entry) in LDS when every levelled graph has at most this many entries
+constexpr uint32_t kLevelLdsLevelling = 9000;
+inline size_t level_lds_bytes(uint32_t n) { return n ? 16 * (size_t(n) + 1) : 0; }
 int launch_levels(const LevelParams &p, void *stream);
 int launch_level_diff(const LevelParams &p, const GraphParams &q, void *stream);
-int launch_level_conflict(const LevelParams &p, const GraphParams &q, void *stream);
+// big = false: every level conflict query, time points in LDS; big = true: only the queries the
+// first launch left at GQ_QUEUE_FULL, time points in HBM scratch
+int launch_level_conflict(const LevelParams &p, const GraphParams &q, void *stream, bool big);
 
 }  // namespace dtgpu

@@ -55,6 +55,9 @@ __device__ __forceinline__ uint32_t find(const Ent *e, uint32_t n, int32_t lv) {
 
 constexpr uint32_t NT = 256;
 
+// LDS: every graph of the launch has at most P.lvl_lds entries (a template parameter, so every
+// access is an LDS or a global instruction, never a flat one)
+template <bool LDS>
 __global__ __launch_bounds__(256) void level_kernel(LevelParams P) {
     __shared__ uint32_t s_sum[NT];
     __shared__ uint32_t s_tail, s_bad;
@@ -63,9 +66,14 @@ __global__ __launch_bounds__(256) void level_kernel(LevelParams P) {
     const LevelGraph G = P.graphs[g];
     const uint32_t n = G.n_ent, base = G.ent_off;
     uint32_t *meta = P.meta + 2 * size_t(base);   // [0] = levels, [1] = status
-    uint32_t *cur = P.gscr + 3 * size_t(base);    // child counts, then fill cursors (n + 1)
-    uint32_t *cofs = cur + (n + 1);               // children CSR offsets (n + 1)
-    uint32_t *pend = cofs + (n + 1);              // parents not yet levelled (n)
+    // LDS (graphs up to P.lvl_lds entries): the round loop's dependent chain -- frontier entry,
+    // its children offsets, each child's pending count -- stays out of HBM and its memory-side
+    // atomics; the queue is copied to order[] at the end
+    extern __shared__ uint32_t lsh[];
+    uint32_t *cur = LDS ? lsh : P.gscr + 3 * size_t(base);   // child counts, then fill cursors (n + 1)
+    uint32_t *cofs = cur + (n + 1);                          // children CSR offsets (n + 1)
+    uint32_t *pend = cofs + (n + 1);                         // parents not yet levelled (n)
+    uint32_t *ord = LDS ? pend + n : P.order + base;         // entries in level order (n)
     const Ent *E = reinterpret_cast<const Ent *>(P.ents) + base;
     const uint32_t plo = E[0].poff, phi = E[n].poff;
     if (t == 0) { s_bad = 0; s_tail = 0; }
@@ -110,18 +118,18 @@ __global__ __launch_bounds__(256) void level_kernel(LevelParams P) {
     for (uint32_t e = t; e < n; e += NT)
         for (uint32_t k = E[e].poff; k < E[e + 1].poff; k++) P.child[plo + atomicAdd(&cur[P.pent[k]], 1u)] = e;
     for (uint32_t e = t; e < n; e += NT)
-        if (pend[e] == 0) P.order[base + atomicAdd(&s_tail, 1u)] = e;   // roots: level 0
+        if (pend[e] == 0) ord[atomicAdd(&s_tail, 1u)] = e;   // roots: level 0
     __syncthreads();
-    // one level per round; a round's frontier is order[head, tail)
+    // one level per round; a round's frontier is ord[head, tail)
     uint32_t head = 0, tail = s_tail, L = 0;
     while (head < tail) {
         if (t == 0) P.lvl_off[base + L] = head;
         for (uint32_t i = head + t; i < tail; i += NT) {
-            const uint32_t e = P.order[base + i];
+            const uint32_t e = ord[i];
             P.level[base + e] = L;
             for (uint32_t j = cofs[e]; j < cofs[e + 1]; j++) {
                 const uint32_t c = P.child[plo + j];
-                if (atomicSub(&pend[c], 1u) == 1u) P.order[base + atomicAdd(&s_tail, 1u)] = c;
+                if (atomicSub(&pend[c], 1u) == 1u) ord[atomicAdd(&s_tail, 1u)] = c;
             }
         }
         __syncthreads();
@@ -130,6 +138,8 @@ __global__ __launch_bounds__(256) void level_kernel(LevelParams P) {
         L++;
         __syncthreads();   // every thread has read s_tail before the next round adds to it
     }
+    if (LDS)
+        for (uint32_t i = t; i < head; i += NT) P.order[base + i] = ord[i];
     if (t == 0) {
         P.lvl_off[base + L] = head;
         meta[0] = L;
@@ -138,7 +148,7 @@ __global__ __launch_bounds__(256) void level_kernel(LevelParams P) {
 }
 
 // The marks of a query (see the header), level by level.  Every thread returns the same status.
-__device__ uint32_t push_marks(const LevelParams &P, const GraphQuery &q, const int32_t *qa, const Ent *E, int32_t *mA,
+__device__ __forceinline__ uint32_t push_marks(const LevelParams &P, const GraphQuery &q, const int32_t *qa, const Ent *E, int32_t *mA,
                                int32_t *mB, uint32_t *s_top, uint32_t *s_st) {
     const uint32_t t = threadIdx.x, n = q.n_ent, base = q.ent_off;
     for (uint32_t e = t; e < n; e += NT) { mA[e] = -1; mB[e] = -1; }
@@ -201,6 +211,7 @@ struct RevSpans {
     }
 };
 
+template <bool LM>   // the marks in LDS (every levelled graph has at most P.lds_ent entries)
 __global__ __launch_bounds__(256) void level_diff_kernel(LevelParams P, GraphParams Q) {
     __shared__ uint32_t s_top, s_st;
     const uint32_t qi = blockIdx.x, t = threadIdx.x;
@@ -215,8 +226,8 @@ __global__ __launch_bounds__(256) void level_diff_kernel(LevelParams P, GraphPar
         return;
     }
     const Ent *E = reinterpret_cast<const Ent *>(P.ents) + base;
-    extern __shared__ int32_t lmarks[];   // P.lds_ent > 0: the marks live in LDS
-    int32_t *mA = P.lds_ent ? lmarks : reinterpret_cast<int32_t *>(P.qscr + q.scr_off), *mB = mA + n;
+    extern __shared__ int32_t lmarks[];
+    int32_t *mA = LM ? lmarks : reinterpret_cast<int32_t *>(P.qscr + q.scr_off), *mB = mA + n;
     const uint32_t st = push_marks(P, q, Q.front + q.f_off, E, mA, mB, &s_top, &s_st);
     if (st != GQ_OK) {
         if (t == 0) { res->status = st; res->n0 = res->n1 = res->n_common = 0; }
@@ -250,18 +261,23 @@ constexpr uint32_t BUCKET_CAP = 64;   // time points that enter one entry sorted
 // A time point (the reference's TimePoint + DiffFlag) in the query's pool: PW words
 // {next in its bucket, flag | kind << 2, frontier size, reference, last element}: a single LV
 // (TP_ONE: ref = the LV), an entry's parents (TP_PARENTS: ref = the entry), or one of the two
-// versions.
+// versions.  LP: the pool is LDS (capacity P.sweep_pts; consumed points are recycled, so only
+// the live ones count), else the query's HBM scratch.
+template <bool LP>
 struct Sweep {
     const Ent *E;
     const uint32_t *par, *pent;   // parent LVs and their entries (per parent slot)
     const int32_t *qa, *qb;   // the two versions (frontier arena)
-    int32_t *head;
-    uint32_t *pool;
+    int32_t *head;            // per entry: its bucket (LDS or HBM)
+    uint32_t *lpool, *pool;
     uint32_t n, cap, used, npend;
     bool overflow;
+    uint32_t freed = 0xFFFFFFFFu;   // consumed points, linked through word 0: reused first, so the
+                                    // live points (a few per frontier element) stay in the LDS part
 
+    __device__ uint32_t *pt(uint32_t tp) const { return LP ? lpool + PW * tp : pool + PW * size_t(tp); }
     __device__ int32_t elem(uint32_t tp, uint32_t k) const {
-        const uint32_t *w = pool + PW * size_t(tp);
+        const uint32_t *w = pt(tp);
         switch (w[1] >> 2) {
             case TP_ONE: return int32_t(w[3]);
             case TP_PARENTS: return int32_t(par[E[w[3]].poff + k]);
@@ -269,9 +285,9 @@ struct Sweep {
             default: return qb[k];
         }
     }
-    __device__ uint32_t size(uint32_t tp) const { return pool[PW * size_t(tp) + 2]; }
-    __device__ uint32_t flag(uint32_t tp) const { return pool[PW * size_t(tp) + 1] & 3u; }
-    __device__ int32_t last(uint32_t tp) const { return int32_t(pool[PW * size_t(tp) + 4]); }
+    __device__ uint32_t size(uint32_t tp) const { return pt(tp)[2]; }
+    __device__ uint32_t flag(uint32_t tp) const { return pt(tp)[1] & 3u; }
+    __device__ int32_t last(uint32_t tp) const { return int32_t(pt(tp)[4]); }
     __device__ bool same(uint32_t x, uint32_t y) const {   // TimePoint equality: the whole frontier
         const uint32_t s = size(x);
         if (s != size(y)) return false;
@@ -289,9 +305,11 @@ struct Sweep {
     // `e`: the entry holding the point's last element when the caller knows it (the levelling's
     // parent-slot entries), n when it must be searched (the versions)
     __device__ void push(uint32_t kind, uint32_t ref, uint32_t sz, uint32_t f, int32_t l, uint32_t e) {
-        if (used >= cap) { overflow = true; return; }
-        const uint32_t tp = used++;
-        uint32_t *w = pool + PW * size_t(tp);
+        uint32_t tp;
+        if (freed != 0xFFFFFFFFu) { tp = freed; freed = pt(tp)[0]; }
+        else if (used >= cap) { overflow = true; return; }
+        else tp = used++;
+        uint32_t *w = pt(tp);
         w[1] = f | (kind << 2);
         w[2] = sz;
         w[3] = ref;
@@ -303,14 +321,21 @@ struct Sweep {
         w[0] = uint32_t(head[e]);
         head[e] = int32_t(tp);
     }
+    __device__ void release(uint32_t tp) { pt(tp)[0] = freed; freed = tp; }
     // element k of point tp as a TP_ONE point (a shattered frontier)
     __device__ void push_elem(uint32_t tp, uint32_t k, uint32_t f) {
-        const uint32_t *w = pool + PW * size_t(tp);
+        const uint32_t *w = pt(tp);
         const int32_t x = elem(tp, k);
         push(TP_ONE, uint32_t(x), 1, f, x, (w[1] >> 2) == TP_PARENTS ? pent[E[w[3]].poff + k] : n);
     }
 };
 
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t l) { return uint32_t(__builtin_amdgcn_readlane(int(v), int(l))); }
+
+// LM: marks and bucket heads in LDS.  LP (first pass): the time points and sorted buckets in LDS;
+// a query that outgrows them ends at GQ_QUEUE_FULL and is answered again by the !LP launch, which
+// handles only those queries, with its points in the query's HBM scratch.
+template <bool LM, bool LP>
 __global__ __launch_bounds__(256) void level_conflict_kernel(LevelParams P, GraphParams Q) {
     __shared__ uint32_t s_top, s_st, s_ncand;
     __shared__ uint32_t s_sum[NT];
@@ -322,6 +347,7 @@ __global__ __launch_bounds__(256) void level_conflict_kernel(LevelParams P, Grap
     const uint32_t n = q.n_ent, base = q.ent_off;
     const uint32_t *meta = P.meta + 2 * size_t(base);
     GraphResult *res = Q.results + qi;
+    if (!LP && res->status != GQ_QUEUE_FULL) return;   // the second pass: only the queries the first left
     const Ent *E = reinterpret_cast<const Ent *>(P.ents) + base;
     uint32_t *out = Q.out + size_t(q.out_off);
     if (meta[1] != GQ_OK) {
@@ -329,7 +355,7 @@ __global__ __launch_bounds__(256) void level_conflict_kernel(LevelParams P, Grap
         return;
     }
     const int32_t *qa = Q.front + q.f_off, *qb = qa + q.na;
-    int32_t *common = Q.common + q.c_off;   // written by thread 0 only
+    int32_t *common = Q.common + q.c_off;   // written by wave 0 only
     // the reference's short circuits (tools.rs:445-480), decided by thread 0 for the group
     if (t == 0) {
         uint32_t st = 0xFFFFFFFFu;   // 0xFFFFFFFF: no short circuit
@@ -359,12 +385,18 @@ __global__ __launch_bounds__(256) void level_conflict_kernel(LevelParams P, Grap
     if (s_st != 0xFFFFFFFFu) return;
     __syncthreads();   // every thread read s_st before push_marks reuses it
     int32_t *hbm = reinterpret_cast<int32_t *>(P.qscr + q.scr_off);
-    extern __shared__ int32_t lmarks[];   // P.lds_ent > 0: the marks live in LDS
-    int32_t *mA = P.lds_ent ? lmarks : hbm, *mB = mA + n, *head = hbm + 2 * n;
-    uint32_t *cand = reinterpret_cast<uint32_t *>(head + n);
+    // LDS: the marks and bucket heads (LM), then the time points (LP)
+    extern __shared__ int32_t lmarks[];
+    const uint32_t le = P.lds_ent;
+    int32_t *mA = LM ? lmarks : hbm, *mB = mA + n;
+    int32_t *head = LM ? lmarks + 2 * le : hbm + 2 * n;
+    uint32_t *lpool = reinterpret_cast<uint32_t *>(LM ? lmarks + 3 * le : lmarks);
+    uint32_t *cand = reinterpret_cast<uint32_t *>(hbm + 3 * n);
     uint32_t *pool = cand + n;
     for (uint32_t e = t; e < n; e += NT) head[e] = -1;
+    const uint64_t c0 = __builtin_amdgcn_s_memtime();
     const uint32_t mst = push_marks(P, q, qa, E, mA, mB, &s_top, &s_st);
+    const uint64_t c1 = __builtin_amdgcn_s_memtime();
     if (mst != GQ_OK) {
         if (t == 0) { res->status = mst; res->n0 = res->n_common = 0; }
         return;
@@ -393,9 +425,13 @@ __global__ __launch_bounds__(256) void level_conflict_kernel(LevelParams P, Grap
         }
         __syncthreads();
     }
-    if (t != 0) return;
-    // ---- the sweep (one thread) ----
-    Sweep S{E, P.par, P.pent, qa, qb, head, pool, n, q.scr_tp, 0, 0, false};
+    if (t >= 64) return;
+    const uint64_t c2 = __builtin_amdgcn_s_memtime();
+    uint32_t visited = 0;
+    // ---- the sweep: wave 0, every lane running the same sequential walk (so its state stays
+    // wave-uniform), the lanes fetching the next 64 candidates' entries and parents at once ----
+    const uint32_t lane = t;
+    Sweep<LP> S{E, P.par, P.pent, qa, qb, head, lpool, pool, n, LP ? P.sweep_pts : q.scr_tp, 0, 0, false};
     uint32_t *hbk = pool + PW * size_t(q.scr_tp);   // an entry's bucket past BUCKET_CAP points
     RevSpans sp{out, q.out_cap / 3, 0, 3, 0, 0, 0, false, false};
     // a span's flag is its membership: x in H(a) iff x <= mA[e], in H(b) iff x <= mB[e]
@@ -407,24 +443,50 @@ __global__ __launch_bounds__(256) void level_conflict_kernel(LevelParams P, Grap
     S.push(TP_QB, 0, q.nb, F_B, q.nb ? qb[q.nb - 1] : ROOT_LV, n);
     uint32_t st = GQ_OK, nc = 0;
     const uint32_t ncand = s_ncand;
-    uint32_t ci = 0;
-    int32_t e = -1;
+    // lane j of the batch: candidate cand[bbase - bhave + j], its start, parent count and last parent
+    uint32_t b_e = 0, b_np = 0, b_lpe = n;
+    int32_t b_s = 0, b_lp = ROOT_LV;
+    uint32_t bbase = 0, bhave = 0, bj = 0;
     for (;;) {
         // the next entry holding a pending point: only entries the marks touch can
-        e = -1;
-        while (ci < ncand) {
-            const uint32_t x = cand[ci++];
-            if (head[x] >= 0) { e = int32_t(x); break; }
+        int32_t e = -1;
+        uint32_t jj = 0;
+        for (;;) {
+            if (bj >= bhave) {
+                if (bbase >= ncand) break;
+                bhave = min(64u, ncand - bbase);
+                const uint32_t x = lane < bhave ? cand[bbase + lane] : 0u;
+                const uint32_t p0 = E[x].poff, p1 = E[x + 1].poff;
+                b_e = x;
+                b_s = E[x].start;
+                b_np = p1 - p0;
+                b_lp = ROOT_LV;
+                b_lpe = n;
+                if (p1 > p0) { b_lp = int32_t(P.par[p1 - 1]); b_lpe = P.pent[p1 - 1]; }
+                bbase += bhave;
+                bj = 0;
+            }
+            const int32_t hv = lane >= bj && lane < bhave ? head[b_e] : -1;
+            const uint64_t m = __ballot(hv >= 0);
+            if (m) {
+                jj = uint32_t(__ffsll((long long)m) - 1);
+                e = int32_t(rdlane(b_e, jj));
+                bj = jj + 1;
+                break;
+            }
+            bj = bhave;
         }
-        if (S.overflow) { st = GQ_OVERFLOW; break; }
+        if (S.overflow) { st = LP ? GQ_QUEUE_FULL : GQ_OVERFLOW; break; }
         if (e < 0) break;   // only ROOT points left: nothing in common
+        visited++;
         // the bucket in heap order (insertion sort; buckets are small -- in LDS up to BUCKET_CAP
         // points, in the query's HBM scratch beyond)
         uint32_t m = 0;
-        for (int32_t x = head[e]; x >= 0; x = int32_t(pool[PW * size_t(x)])) m++;
-        uint32_t *bk = m <= BUCKET_CAP ? bkl : hbk;
+        for (int32_t x = head[e]; x >= 0; x = int32_t(S.pt(uint32_t(x))[0])) m++;
+        if (LP && m > BUCKET_CAP) { st = GQ_QUEUE_FULL; break; }
+        uint32_t *bk = LP || m <= BUCKET_CAP ? bkl : hbk;
         m = 0;
-        for (int32_t x = head[e]; x >= 0; x = int32_t(pool[PW * size_t(x)])) {
+        for (int32_t x = head[e]; x >= 0; x = int32_t(S.pt(uint32_t(x))[0])) {
             uint32_t j = m++;
             while (j > 0 && S.before(uint32_t(x), bk[j - 1])) { bk[j] = bk[j - 1]; j--; }
             bk[j] = uint32_t(x);
@@ -447,7 +509,7 @@ __global__ __launch_bounds__(256) void level_conflict_kernel(LevelParams P, Grap
             break;
         }
         for (uint32_t k = 0; k + 1 < S.size(T); k++) S.push_elem(T, k, flag);   // shatter
-        const int32_t es = E[e].start;
+        const int32_t es = int32_t(rdlane(uint32_t(b_s), jj));
         int32_t re = S.last(T) + 1;
         bool stopped = false;
         for (; i < m; i++) {   // the other points inside this entry, highest first
@@ -469,37 +531,56 @@ __global__ __launch_bounds__(256) void level_conflict_kernel(LevelParams P, Grap
         }
         if (stopped) break;
         sp.push(es, re, mflag(uint32_t(e), re - 1));
-        const uint32_t p0 = E[e].poff, np = E[e + 1].poff - p0;
-        if (np) S.push(TP_PARENTS, uint32_t(e), np, flag, int32_t(P.par[p0 + np - 1]), P.pent[p0 + np - 1]);
-        else S.push(TP_PARENTS, uint32_t(e), 0, flag, ROOT_LV, n);
+        for (uint32_t k = 0; k < m; k++) S.release(bk[k]);   // every point of the bucket is consumed
+        S.push(TP_PARENTS, uint32_t(e), rdlane(b_np, jj), flag, int32_t(rdlane(uint32_t(b_lp), jj)), rdlane(b_lpe, jj));
     }
-    if (st == GQ_OK && S.overflow) st = GQ_OVERFLOW;
+    if (st == GQ_OK && S.overflow) st = LP ? GQ_QUEUE_FULL : GQ_OVERFLOW;
     sp.flush();
     if (st == GQ_OK && sp.overflow) st = GQ_OVERFLOW;
-    res->status = st;
-    res->n0 = sp.n;
-    res->n_common = nc;
+    if (lane == 0) {
+        res->status = st;
+        res->n0 = sp.n;
+        res->n_common = nc;
+        if (P.prof) {
+            const uint64_t c3 = __builtin_amdgcn_s_memtime();
+            uint32_t *w = P.prof + 4 * size_t(qi);
+            w[0] = uint32_t((c1 - c0) >> 4);
+            w[1] = uint32_t((c2 - c1) >> 4);
+            w[2] = uint32_t((c3 - c2) >> 4);
+            w[3] = visited;
+        }
+    }
 }
 
 }  // namespace ldev
 
 int launch_levels(const LevelParams &p, void *stream) {
     if (!p.n_graphs) return 0;
-    hipLaunchKernelGGL(ldev::level_kernel, dim3(p.n_graphs), dim3(ldev::NT), 0, reinterpret_cast<hipStream_t>(stream), p);
+    const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (p.lvl_lds) hipLaunchKernelGGL(ldev::level_kernel<true>, dim3(p.n_graphs), dim3(ldev::NT), level_lds_bytes(p.lvl_lds), st, p);
+    else hipLaunchKernelGGL(ldev::level_kernel<false>, dim3(p.n_graphs), dim3(ldev::NT), 0, st, p);
     return hipGetLastError() == hipSuccess ? 0 : 66;
 }
 
 int launch_level_diff(const LevelParams &p, const GraphParams &q, void *stream) {
     if (!q.n_queries) return 0;
-    hipLaunchKernelGGL(ldev::level_diff_kernel, dim3(q.n_queries), dim3(ldev::NT), 2 * size_t(p.lds_ent) * 4,
-                       reinterpret_cast<hipStream_t>(stream), p, q);
+    const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (p.lds_ent) hipLaunchKernelGGL(ldev::level_diff_kernel<true>, dim3(q.n_queries), dim3(ldev::NT), 8 * size_t(p.lds_ent), st, p, q);
+    else hipLaunchKernelGGL(ldev::level_diff_kernel<false>, dim3(q.n_queries), dim3(ldev::NT), 0, st, p, q);
     return hipGetLastError() == hipSuccess ? 0 : 66;
 }
 
-int launch_level_conflict(const LevelParams &p, const GraphParams &q, void *stream) {
+int launch_level_conflict(const LevelParams &p, const GraphParams &q, void *stream, bool big) {
     if (!q.n_queries) return 0;
-    hipLaunchKernelGGL(ldev::level_conflict_kernel, dim3(q.n_queries), dim3(ldev::NT), 2 * size_t(p.lds_ent) * 4,
-                       reinterpret_cast<hipStream_t>(stream), p, q);
+    const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const size_t lm = 12 * size_t(p.lds_ent), lp = big ? 0 : 4 * size_t(p.sweep_pts) * kLevelPointWords;
+    if (p.lds_ent) {
+        if (big) hipLaunchKernelGGL((ldev::level_conflict_kernel<true, false>), dim3(q.n_queries), dim3(ldev::NT), lm + lp, st, p, q);
+        else hipLaunchKernelGGL((ldev::level_conflict_kernel<true, true>), dim3(q.n_queries), dim3(ldev::NT), lm + lp, st, p, q);
+    } else {
+        if (big) hipLaunchKernelGGL((ldev::level_conflict_kernel<false, false>), dim3(q.n_queries), dim3(ldev::NT), lp, st, p, q);
+        else hipLaunchKernelGGL((ldev::level_conflict_kernel<false, true>), dim3(q.n_queries), dim3(ldev::NT), lp, st, p, q);
+    }
     return hipGetLastError() == hipSuccess ? 0 : 66;
 }
 

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -14,6 +16,12 @@
 #include "dt_host.hpp"
 
 using namespace dtgpu;
+
+// experiment switches for the level-synchronous conflict sweep (unset: the defaults)
+static uint32_t env_u32(const char *name, uint32_t dflt) {
+    const char *v = std::getenv(name);
+    return v && *v ? uint32_t(std::strtoul(v, nullptr, 10)) : dflt;
+}
 
 extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *hist_off, size_t n_graphs,
                                             const dtgpu_graph_query *queries, size_t nq, int64_t *spans,
@@ -115,7 +123,7 @@ extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *h
     DevBuf<int32_t> d_front, d_common;
     DevBuf<GraphQuery> d_q;
     DevBuf<GraphResult> d_r;
-    DevBuf<uint32_t> d_pent, d_child, d_level, d_order, d_loff, d_meta, d_gscr, d_qscr;
+    DevBuf<uint32_t> d_pent, d_child, d_level, d_order, d_loff, d_meta, d_gscr, d_qscr, d_prof;
     DevBuf<LevelGraph> d_lg;
     dtgpu_status rc = DTGPU_OK;
     std::vector<GraphResult> res(nq);
@@ -151,7 +159,14 @@ extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *h
                 for (const LevelGraph &g : lg) max_ent = std::max(max_ent, g.n_ent);
                 LP = LevelParams{d_ents.p, d_par.p, d_pent.p, d_child.p, d_level.p, d_order.p, d_loff.p, d_meta.p,
                                  d_gscr.p, d_qscr.p, d_lg.p, uint32_t(lg.size()),
-                                 max_ent <= kLevelLdsEntries ? max_ent : 0u};
+                                 max_ent <= kLevelLdsEntries ? max_ent : 0u,
+                                 max_ent <= kLevelLdsLevelling ? max_ent : 0u,
+                                 std::max<uint32_t>(8, env_u32("DTGPU_LVL_PTS_LDS", 64)), nullptr};
+                if (env_u32("DTGPU_LVL_PROF", 0)) {
+                    CK(d_prof.alloc(4 * nq));
+                    CK(hipMemsetAsync(d_prof.p, 0, 4 * nq * 4, st));
+                    LP.prof = d_prof.p;
+                }
             }
             CK(hipEventRecord(e0, st));
             if (launch_graph_queries(P, st, false)) { rc = DTGPU_ERR_HIP; goto done; }
@@ -177,9 +192,21 @@ extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *h
                     if (launch_graph_queries(P, st, true)) { rc = DTGPU_ERR_HIP; goto done; }
                 }
             }
-            if (!lg.empty() && (launch_levels(LP, st) || launch_level_diff(LP, P, st) || launch_level_conflict(LP, P, st))) {
+            if (!lg.empty() && (launch_levels(LP, st) || launch_level_diff(LP, P, st) || launch_level_conflict(LP, P, st, false))) {
                 rc = DTGPU_ERR_HIP;
                 goto done;
+            }
+            // the level conflict queries whose live time points or buckets outgrew LDS, again with
+            // their points in HBM scratch
+            bool any_lc = false;
+            for (size_t i = 0; i < nq; i++) any_lc |= q[i].kind == GQ_CONFLICT_LEVEL;
+            if (any_lc) {
+                std::vector<GraphResult> r1(nq);
+                CK(hipMemcpyAsync(r1.data(), d_r.p, nq * sizeof(GraphResult), hipMemcpyDeviceToHost, st));
+                CK(hipStreamSynchronize(st));
+                bool full = false;
+                for (size_t i = 0; i < nq; i++) full |= q[i].kind == GQ_CONFLICT_LEVEL && r1[i].status == GQ_QUEUE_FULL;
+                if (full && launch_level_conflict(LP, P, st, true)) { rc = DTGPU_ERR_HIP; goto done; }
             }
             CK(hipEventRecord(e1, st));
         }
@@ -189,6 +216,23 @@ extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *h
             if (!com.empty()) CK(hipMemcpyAsync(com.data(), d_common.p, com.size() * 4, hipMemcpyDeviceToHost, st));
         }
         CK(hipStreamSynchronize(st));
+        if (d_prof.p) {   // DTGPU_LVL_PROF: per-phase summary of the conflict sweeps (stderr)
+            std::vector<uint32_t> pr(4 * nq);
+            CK(hipMemcpy(pr.data(), d_prof.p, pr.size() * 4, hipMemcpyDeviceToHost));
+            double sum[4] = {0, 0, 0, 0};
+            uint32_t mx[4] = {0, 0, 0, 0}, nk = 0, worst = 0;
+            for (size_t i = 0; i < nq; i++) {
+                if (q[i].kind != GQ_CONFLICT_LEVEL) continue;
+                nk++;
+                for (int k = 0; k < 4; k++) { sum[k] += pr[4 * i + k]; mx[k] = std::max(mx[k], pr[4 * i + k]); }
+                if (pr[4 * i] + pr[4 * i + 1] + pr[4 * i + 2] > pr[4 * worst] + pr[4 * worst + 1] + pr[4 * worst + 2]) worst = uint32_t(i);
+            }
+            if (nk)
+                fprintf(stderr, "lvlprof queries=%u mean kcyc marks=%.1f cand=%.1f sweep=%.1f visited=%.1f | max %.1f %.1f %.1f %u"
+                        " | worst marks=%.1f cand=%.1f sweep=%.1f visited=%u\n", nk, sum[0] / nk * 0.016, sum[1] / nk * 0.016,
+                        sum[2] / nk * 0.016, sum[3] / nk, mx[0] * 0.016, mx[1] * 0.016, mx[2] * 0.016, mx[3],
+                        pr[4 * worst] * 0.016, pr[4 * worst + 1] * 0.016, pr[4 * worst + 2] * 0.016, pr[4 * worst + 3]);
+        }
         if (ms) {
             float t = 0;
             CK(hipEventElapsedTime(&t, e0, e1));
