@@ -122,6 +122,8 @@ struct PlanParams {
     uint32_t lds_entries;   // per-wave LDS capacity (entries) of the todo stack / pending counts
     uint32_t max_agents;    // largest agent count among device-planned documents
     uint32_t prof;          // cycle profile into PlanResult.prof
+    uint32_t split;         // <= 64 chains: the two-phase planner (order, then lane-parallel steps)
+    uint32_t *order;        // two-phase planner: walk orders, document d's at its entry offset
     Cmd *cmds;
     uint32_t *tlist;
     const PlanDesc *docs;

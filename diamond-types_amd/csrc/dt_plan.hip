@@ -55,6 +55,7 @@ struct P {
     uint32_t ne, A, ntip, n_lv;
     // scratch: vv rows in HBM; todo stack and pending parent counts in LDS (u16)
     uint32_t *base;
+    uint32_t *order;       // two-phase planner: the walk order (ne words)
     const uint32_t *prow;  // K = 1: each entry's parent version vector (row_stride words)
     uint32_t row_stride;
     uint16_t *todo;      // ready entries (PLAN_TODO_CAP slots)
@@ -750,9 +751,355 @@ DEV void plan_doc1(P &p, PlanResult *res) {
     }
 }
 
+// ---- <= 64 chains, two phases -----------------------------------------------------------------
+//
+// The walk order depends only on the graph (children, merge flags), and what a walk step emits
+// depends only on the step's entry and the one before it: the frontier before step i is the
+// previous entry's parent vector with that entry's own LVs folded in (fold_entry), the frontier it
+// moves to is entry i's parent vector.  So:
+//   phase A (sequential, wave-uniform): the spanning-tree order alone -- pick, children
+//     bookkeeping, one record load per step -- written to the document's scratch (p.base);
+//   phase B (lane-parallel, lane = walk step): each step's retreat / advance ranges and op runs
+//     sized, offsets by prefix sums, then every step's TOG command, tlist slice and op-run
+//     commands written by its own lane.
+// Same output as plan_doc1 (tested against the host walk).
+constexpr uint32_t kSplitLaneTl = 24, kSplitLaneOps = 8;   // per-lane step writes up to these sizes
+constexpr uint32_t kSplitRegChains = 4;   // up to this many chains: output-parallel chunk writes
+constexpr uint32_t kSplitSegChunk = 4096;
+constexpr uint32_t kSplitCopyDepth = 8;   // big steps: 8 x 64 dense-table loads per round trip   // ... for chunks writing up to this many entries / commands
+DEV void plan_doc_split(P &p, PlanResult *res) {
+    const uint32_t l = lane_id();
+    uint32_t top = 0;
+    bool bad_np = false;
+    for (uint32_t c = 0; c < p.ne; c += 64) {
+        const uint32_t e = c + l;
+        if (e < p.ne) {
+            const uint32_t np = p.erec[size_t(e) * EREC_WORDS + R_NP];
+            if (np > 0x7Fu) bad_np = true;
+            p.pending[e] = uint8_t(min(np, 0x7Fu) | (np >= 2 ? MERGE_BIT : 0));
+        }
+    }
+    for (int c = int((p.ne + 63) / 64) - 1; c >= 0; c--) {
+        if (!charge(p)) break;
+        const uint32_t e = uint32_t(c) * 64 + (63 - l);
+        const bool root = e < p.ne && p.erec[size_t(e) * EREC_WORDS + R_NP] == 0;
+        const u64 m = __ballot(root);
+        const uint32_t rank = uint32_t(__popcll(m & ((1ull << l) - 1ull)));
+        if (top + uint32_t(__popcll(m)) > PLAN_TODO_CAP) { fail(p, PLAN_TODO_FULL); break; }
+        if (root) p.todo[top + rank] = uint16_t(e);
+        top += uint32_t(__popcll(m));
+    }
+    if (__ballot(bad_np)) fail(p, PLAN_WIDE_MERGE);
+    wave_fence();
+    tk(p);
+    PT(5);
+    // ---- phase A: the order ----
+    uint32_t *order = p.order;   // ne words
+    Stk S;
+    S.v = 0; S.mm = 0; S.n = 0; S.nl = top;
+    bool have = S.nl > 0 && !p.err;
+    uint32_t idx = have ? stk_pick(p, S) : 0;
+    uint32_t rw = have ? load_rec(p, idx) : 0;
+    uint32_t ns = 0;
+    uint32_t ordv = 0;   // lane j: order[64 * (ns / 64) + j] until its 64 are stored together
+    while (have && !p.err) {
+        if (!charge(p)) break;
+        if (ns >= p.ne) { fail(p, PLAN_ERR_INTERNAL); break; }
+        ordv = l == (ns & 63u) ? idx : ordv;
+        if ((ns & 63u) == 63u) order[ns - 63 + l] = ordv;
+        ns++;
+        const uint32_t nch = R(rw, R_NCH), ch0 = R(rw, R_CH0), lastch = R(rw, R_LASTCH), firstch = R(rw, R_FIRSTCH);
+        uint32_t ch = l == 0 ? firstch : lastch;
+        if (nch > 2) ch = l < nch ? p.child[ch0 + l] : 0;
+        for (uint32_t c = 0; c < nch; c += 64) {
+            const uint32_t chv = c == 0 ? ch : (c + l < nch ? p.child[ch0 + c + l] : 0);
+            bool ready = false, mg = false;
+            if (c + l < nch) {
+                const uint8_t pd = uint8_t(p.pending[chv] - 1);
+                p.pending[chv] = pd;
+                ready = (pd & 0x7F) == 0;
+                mg = (pd & MERGE_BIT) != 0;
+            }
+            if (!stk_push(p, S, __ballot(ready), chv, mg)) break;
+        }
+        if (p.err) break;
+        have = S.n + S.nl > 0;
+        if (have) {
+            idx = stk_pick(p, S);
+            rw = load_rec(p, idx);
+        }
+    }
+    if ((ns & 63u) && l < (ns & 63u)) order[(ns & ~63u) + l] = ordv;
+    PT(0);
+    // every lane reads the order phase A wrote
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    // each chain's dense-table slice, in LDS (the todo stack's space: phase A is done)
+    uint32_t *sdoff = reinterpret_cast<uint32_t *>(p.todo);
+    if (l <= p.A) sdoff[l] = p.doff[l];
+    wave_fence();
+    // ---- phase B: per step, lane = step ----
+    const uint32_t A = p.A;
+    const uint32_t rs = p.row_stride;
+    uint32_t err_step = 0xFFFFFFFFu, err_code = 0;
+    uint32_t last_e = 0;
+    for (uint32_t c0 = 0; c0 < ns && !p.err; c0 += 64) {
+        const uint32_t i = c0 + l;
+        const bool valid = i < ns;
+        const uint32_t e = valid ? order[i] : 0;
+        const bool hp = valid && i > 0;
+        const uint32_t ep = hp ? order[i - 1] : 0;
+        const uint4 *r4 = reinterpret_cast<const uint4 *>(p.erec);
+        const uint4 a0 = r4[size_t(e) * (EREC_WORDS / 4)], a1 = r4[size_t(e) * (EREC_WORDS / 4) + 1];
+        uint4 b0 = make_uint4(0, 0, 0, 0), b1 = make_uint4(0, 0, 0, 0);
+        if (hp) { b0 = r4[size_t(ep) * (EREC_WORDS / 4)]; b1 = r4[size_t(ep) * (EREC_WORDS / 4) + 1]; }
+        const uint32_t e_start = a0.x, e_end = a0.y, op0 = a1.x, nop = a1.y, chain = a1.z, seq0 = a1.w;
+        const uint32_t p_start = b0.x, p_end = b0.y, p_chain = b1.z, p_seq0 = b1.w;
+        uint32_t code = 0;
+        if (valid && (chain >= A || e_end <= e_start)) code = PLAN_ERR_INTERNAL;
+        if (valid && p.prow[size_t(e) * rs + min(chain, rs - 1)] != seq0 && !code) code = PLAN_NOT_CHAIN;
+        // the frontier before the step (the previous entry folded) against the step's parents
+        uint32_t total = 0, nadv = 0;
+        uint32_t sn[kSplitRegChains], ss[kSplitRegChains], sadv = 0;   // A <= 4: the step's ranges
+#pragma unroll
+        for (uint32_t a = 0; a < kSplitRegChains; a++) sn[a] = ss[a] = 0;
+        for (uint32_t a = 0; a < A; a++) {
+            const uint32_t to = valid ? p.prow[size_t(e) * rs + a] : 0;
+            uint32_t from = hp ? p.prow[size_t(ep) * rs + a] : 0;
+            if (hp && a == p_chain) from = p_seq0 + (p_end - p_start);
+            const bool adv = to > from;
+            const uint32_t n = adv ? to - from : from - to;
+            const uint32_t s0 = adv ? from : to;
+            if (n && sdoff[a] + s0 + n > sdoff[a + 1] && !code) code = PLAN_ERR_INTERNAL;
+            total += n;
+            nadv += adv ? n : 0;
+#pragma unroll
+            for (uint32_t q = 0; q < kSplitRegChains; q++)
+                if (a == q) { sn[q] = n; ss[q] = sdoff[a] + s0; }
+            if (adv && a < kSplitRegChains) sadv |= 1u << a;
+        }
+        if (!valid) total = nadv = 0;
+        const uint32_t ncmd = valid ? (total ? 1u : 0u) + nop : 0u;
+        // offsets: prefix sums over the chunk's steps
+        const uint32_t ic = wave_scan(ncmd), it = wave_scan(total);
+        const uint32_t co = p.nc + ic - ncmd, to0 = p.nt + it - total;
+        const uint32_t sum_c = bcast(ic, 63), sum_t = bcast(it, 63);
+        const uint32_t sum_adv = bcast(wave_scan(nadv), 63);
+        PT(1);
+        if (code) { err_step = i; err_code = code; }
+        const u64 em = __ballot(code != 0);
+        if (em) {   // the first failing step ends the walk, as plan_doc1 stops there
+            fail(p, bcast(code, first_lane(em)));
+            break;
+        }
+        if (uint64_t(p.nc) + sum_c > p.ccap) { fail(p, PLAN_CMDS_FULL); break; }
+        if (uint64_t(p.nt) + sum_t > p.tcap) { fail(p, PLAN_TLIST_FULL); break; }
+        // small steps: each lane writes its own step; a step with a long diff or many op runs
+        // is written by the whole wave afterwards (a lane copying node_nodecc's thousands of
+        // entries alone would serialise the chunk)
+        // A <= 4: output-parallel chunk writes, unless the chunk's output is long (node_nodecc's
+        // steps retreat / advance thousands of entries each): then step by step, each step's
+        // ranges copied contiguously by the whole wave
+        const bool seg_chunk = sum_t > kSplitSegChunk || sum_c > kSplitSegChunk;
+        const bool outpar = A <= kSplitRegChains && !seg_chunk;
+        const bool big = valid && (A > kSplitRegChains ? (total > kSplitLaneTl || nop > kSplitLaneOps) : seg_chunk);
+        if (!p.count_only && outpar) {
+            // output-parallel: output u of the chunk belongs to the first step whose inclusive
+            // prefix exceeds it (a binary search over the lanes), inside it to the chain range
+            // that covers it; 4 x 64 outputs per round, their loads in flight together
+            const uint32_t T0 = p.nt, C0 = p.nc;
+            bool bad = false;
+            for (uint32_t r = 0; r < sum_t; r += 256) {
+                uint32_t val[4], fl[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const uint32_t u = r + 64 * uint32_t(q) + l;
+                    uint32_t j = 0;
+#pragma unroll
+                    for (uint32_t st = 32; st; st >>= 1)
+                        if (u >= uint32_t(__shfl(int(it), int(j + st - 1)))) j += st;
+                    j = min(j, 63u);
+                    const uint32_t w = u - (uint32_t(__shfl(int(it), int(j))) - uint32_t(__shfl(int(total), int(j))));
+                    const uint32_t av = uint32_t(__shfl(int(sadv), int(j)));
+                    uint32_t before = 0, src = 0, f = 0;
+                    bool found = false;
+#pragma unroll
+                    for (uint32_t a = 0; a < kSplitRegChains; a++) {
+                        const uint32_t na = uint32_t(__shfl(int(sn[a]), int(j)));
+                        const uint32_t sa = uint32_t(__shfl(int(ss[a]), int(j)));
+                        if (!found && w < before + na) { src = sa + (w - before); f = (av >> a) & 1u ? TL_ADV : 0u; found = true; }
+                        before += na;
+                    }
+                    val[q] = u < sum_t ? p.dense[src] : 0u;
+                    fl[q] = f;
+                }
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const uint32_t u = r + 64 * uint32_t(q) + l;
+                    if (u < sum_t) {
+                        bad |= val[q] == 0xFFFFFFFFu;
+                        p.tlist[T0 + u] = val[q] | fl[q];
+                    }
+                }
+            }
+            for (uint32_t r = 0; r < sum_c; r += 256) {   // 4 x 64 commands per round
+                Cmd cv[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const uint32_t u = r + 64 * uint32_t(q) + l;
+                    uint32_t j = 0;
+#pragma unroll
+                    for (uint32_t st = 32; st; st >>= 1)
+                        if (u >= uint32_t(__shfl(int(ic), int(j + st - 1)))) j += st;
+                    j = min(j, 63u);
+                    const uint32_t k = u - (uint32_t(__shfl(int(ic), int(j))) - uint32_t(__shfl(int(ncmd), int(j))));
+                    const uint32_t tj = uint32_t(__shfl(int(total), int(j))), t0j = uint32_t(__shfl(int(to0), int(j)));
+                    const uint32_t o0j = uint32_t(__shfl(int(op0), int(j)));
+                    cv[q] = Cmd{CMD_TOG, t0j, tj, 0};
+                    if (u < sum_c && !(tj && k == 0)) cv[q] = p.opc[o0j + k - (tj ? 1u : 0u)];
+                }
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const uint32_t u = r + 64 * uint32_t(q) + l;
+                    if (u < sum_c) p.cmds[C0 + u] = cv[q];
+                }
+            }
+            if (bad) { err_step = i; err_code = PLAN_ERR_INTERNAL; }
+        }
+        if (!p.count_only && valid && !big && A > kSplitRegChains) {
+            uint32_t cw = co;
+            bool bad = false;
+            if (total) {
+                p.cmds[cw++] = Cmd{CMD_TOG, to0, total, 0};
+                uint32_t u = to0;
+                for (uint32_t a = 0; a < A; a++) {
+                    const uint32_t to = p.prow[size_t(e) * rs + a];
+                    uint32_t from = hp ? p.prow[size_t(ep) * rs + a] : 0;
+                    if (hp && a == p_chain) from = p_seq0 + (p_end - p_start);
+                    if (to == from) continue;
+                    const bool adv = to > from;
+                    const uint32_t n = adv ? to - from : from - to;
+                    const uint32_t src = sdoff[a] + (adv ? from : to), fl = adv ? TL_ADV : 0u;
+                    uint32_t k = 0;
+                    for (; k + 4 <= n; k += 4) {   // four loads in flight per round
+                        uint32_t v[4];
+#pragma unroll
+                        for (int q = 0; q < 4; q++) v[q] = p.dense[src + k + q];
+#pragma unroll
+                        for (int q = 0; q < 4; q++) { bad |= v[q] == 0xFFFFFFFFu; p.tlist[u + q] = v[q] | fl; }
+                        u += 4;
+                    }
+                    for (; k < n; k++) {
+                        const uint32_t v = p.dense[src + k];
+                        bad |= v == 0xFFFFFFFFu;
+                        p.tlist[u++] = v | fl;
+                    }
+                }
+            }
+            for (uint32_t j = 0; j < nop; j++) p.cmds[cw + j] = p.opc[op0 + j];
+            if (bad) { err_step = i; err_code = PLAN_ERR_INTERNAL; }
+        }
+        PT(2);
+        if (!p.count_only) {
+            for (u64 bm = __ballot(big); bm; bm &= bm - 1) {   // the big steps, one at a time
+                const uint32_t j = first_lane(bm);
+                const uint32_t be = U(bcast(e, j)), bep = U(bcast(ep, j)), bhp = U(bcast(hp ? 1u : 0u, j));
+                const uint32_t bpc = U(bcast(p_chain, j)), bpv = U(bcast(p_seq0 + (p_end - p_start), j));
+                const uint32_t bto = U(bcast(to0, j)), bco = U(bcast(co, j)), btot = U(bcast(total, j));
+                const uint32_t bop0 = U(bcast(op0, j)), bnop = U(bcast(nop, j));
+                uint32_t cw = bco;
+                if (btot) {
+                    if (l == 0) p.cmds[cw] = Cmd{CMD_TOG, bto, btot, 0};
+                    cw++;
+                    // lane = chain: its range, its offset in the step's slice, then 64 outputs per round
+                    const uint32_t to = l < A ? p.prow[size_t(be) * rs + l] : 0u;
+                    uint32_t from = bhp && l < A ? p.prow[size_t(bep) * rs + l] : 0u;
+                    if (bhp && l == bpc) from = bpv;
+                    const bool adv = to > from;
+                    const uint32_t n = adv ? to - from : from - to;
+                    const uint32_t src = (l < A ? sdoff[l] : 0u) + (adv ? from : to), fl = adv ? TL_ADV : 0u;
+                    const uint32_t off = wave_scan(n) - n;
+                    bool bad = false;
+                    for (u64 am = __ballot(n != 0); am; am &= am - 1) {
+                        const uint32_t a = first_lane(am);
+                        const uint32_t o = U(bcast(off, a)), nn = U(bcast(n, a)), sa = U(bcast(src, a)), fa = U(bcast(fl, a));
+                        for (uint32_t u0 = 0; u0 < nn; u0 += 64 * kSplitCopyDepth) {   // loads in flight together
+                            uint32_t v[kSplitCopyDepth];
+#pragma unroll
+                            for (int q = 0; q < int(kSplitCopyDepth); q++) {
+                                const uint32_t u = u0 + 64 * uint32_t(q) + l;
+                                v[q] = u < nn ? p.dense[sa + u] : 0u;
+                            }
+#pragma unroll
+                            for (int q = 0; q < int(kSplitCopyDepth); q++) {
+                                const uint32_t u = u0 + 64 * uint32_t(q) + l;
+                                if (u < nn) {
+                                    bad |= v[q] == 0xFFFFFFFFu;
+                                    p.tlist[bto + o + u] = v[q] | fa;
+                                }
+                            }
+                        }
+                    }
+                    if (__ballot(bad)) err_code = PLAN_ERR_INTERNAL;
+                }
+                for (uint32_t k = l; k < bnop; k += 64) p.cmds[cw + k] = p.opc[bop0 + k];
+            }
+        }
+        PT(4);
+        if (__ballot(err_code != 0)) { fail(p, PLAN_ERR_INTERNAL); break; }
+        p.nc += sum_c;
+        p.nt += sum_t;
+        p.n_adv += sum_adv;
+        p.n_ret += sum_t - sum_adv;
+        last_e = U(bcast(e, min(63u, ns - 1 - c0)));
+    }
+    (void)err_step;
+    PT(3);
+    // advance to the tip (cg.version): from the last step's entry folded
+    if (!p.err) {
+        VV<1> vf;
+        vf.v[0] = 0;
+        if (ns) {
+            const uint32_t rl = load_rec(p, last_e);
+            vf.v[0] = l < A ? p.prow[size_t(last_e) * rs + l] : 0u;
+            fold_entry<1>(p, R(rl, R_START), R(rl, R_END), R(rl, R_END) - 1, R(rl, R_CHAIN), R(rl, R_SEQ0), vf, false);
+        }
+        VV<1> dl, dh;
+        dl.v[0] = l < A ? sdoff[l] : 0u;
+        dh.v[0] = l < A ? sdoff[l + 1] : 0u;
+        VV<1> vt;
+        vv_zero(vt);
+        for (uint32_t j = 0; j < p.ntip && !p.err; j++) {
+            const uint32_t tlv = U(p.tip[2 * j]), te = U(p.tip[2 * j + 1]);
+            const Rec tr = srec(p, te);
+            VV<1> t;
+            t.v[0] = tr.row;
+            fold_entry<1>(p, F(tr, R_START), F(tr, R_END), tlv, F(tr, R_CHAIN), F(tr, R_SEQ0), t, false);
+            vv_max(vt, t);
+        }
+        if (!p.err && vv_differ(vf, vt)) {
+            const uint32_t t0 = p.nt;
+            const uint32_t adv0 = p.n_adv;
+            emit_diff<1>(p, vf, vt, dl, dh, false);
+            if (!p.err && p.nt > t0) push_cmd(p, CMD_TOG, t0, p.nt - t0, 0);
+            res->n_tip = uint32_t(p.n_adv - adv0);
+            p.n_adv = adv0;
+        }
+    }
+    if (l == 0) {
+        for (int i = 0; i < 6; i++) res->prof[i] = p.prof ? g_pc[i] : 0;
+        res->status = p.err;
+        res->ncmd = p.nc;
+        res->ntlist = p.nt;
+        res->n_retreat = p.n_ret;
+        res->n_advance = p.n_adv;
+    }
+}
+
 // K = agent chunks per lane.  Documents with <= 64 agents run in the K = 1 instantiation, the
 // others (<= PLAN_MAX_AGENTS) in the wide one; each kernel skips the other's documents.
-template <int K>
+template <int K, bool SPLIT = false>
 DEV void plan_entry(const PlanParams &Q) {
     extern __shared__ __attribute__((aligned(16))) uint16_t lds16[];
     if (blockIdx.x >= Q.n_docs) return;
@@ -781,6 +1128,7 @@ DEV void plan_entry(const PlanParams &Q) {
     p.pending = reinterpret_cast<uint8_t *>(lds16 + PLAN_TODO_CAP);
     p.base = Q.base + pd.base_off;
     p.prow = Q.prow + pd.prow_off;
+    p.order = Q.order + pd.erec_off / EREC_WORDS;
     p.row_stride = pd.row_stride;
     p.cmds = Q.cmds + pd.cmd_off;
     p.tlist = Q.tlist + pd.tlist_off;
@@ -798,8 +1146,12 @@ DEV void plan_entry(const PlanParams &Q) {
         return;
     }
 #ifndef DTGPU_PLAN_OLD
-    if constexpr (K == 1) plan_doc1(p, res);
-    else plan_doc<K>(p, res);
+    if constexpr (K == 1) {
+        if constexpr (SPLIT) plan_doc_split(p, res);
+        else plan_doc1(p, res);
+    } else {
+        plan_doc<K>(p, res);
+    }
 #else
     plan_doc<K>(p, res);
 #endif
@@ -808,8 +1160,9 @@ DEV void plan_entry(const PlanParams &Q) {
 #ifndef DTGPU_PLAN_WAVES
 #define DTGPU_PLAN_WAVES 6   // occupancy target of the <= 64-chain planner (tuning knob)
 #endif
+template <bool SPLIT>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PLAN_WAVES))) void plan_kernel_1(PlanParams Q) {
-    plan_entry<1>(Q);
+    plan_entry<1, SPLIT>(Q);
 }
 __global__ __launch_bounds__(64) void plan_kernel_wide(PlanParams Q) { plan_entry<PLAN_MAX_AGENTS / 64>(Q); }
 
@@ -819,7 +1172,8 @@ int launch_plan(const PlanParams &q, void *stream) {
     if (!q.n_docs) return OK;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const size_t lds = 2 * size_t(PLAN_TODO_CAP) + ((size_t(q.lds_entries) + 15) & ~size_t(15));   // todo + pending
-    hipLaunchKernelGGL(pdev::plan_kernel_1, dim3(q.n_docs), dim3(64), lds, s, q);
+    if (q.split) hipLaunchKernelGGL(pdev::plan_kernel_1<true>, dim3(q.n_docs), dim3(64), lds, s, q);
+    else hipLaunchKernelGGL(pdev::plan_kernel_1<false>, dim3(q.n_docs), dim3(64), lds, s, q);
     if (hipGetLastError() != hipSuccess) return ErrHip;
     if (q.max_agents > 64) {
         hipLaunchKernelGGL(pdev::plan_kernel_wide, dim3(q.n_docs), dim3(64), lds, s, q);

@@ -50,6 +50,12 @@ uint64_t lds_fill_setting() {
     if (const char *e = getenv("DTGPU_LDS_FILL")) f = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
     return f;
 }
+// The <= 64-chain planner: two phases (walk order, then lane-parallel steps) unless
+// DTGPU_PLAN_SPLIT=0 selects the one-phase walk (A/B).
+uint32_t plan_split_setting() {
+    const char *e = getenv("DTGPU_PLAN_SPLIT");
+    return e && *e == '0' ? 0u : 1u;
+}
 // Per-document replay layout: block capacity, HBM index bytes, LDS tier.
 struct Layout { uint32_t max_blocks; uint64_t gidx; int tier; uint32_t tier_blocks; };
 Layout replay_layout(uint64_t n_ins, uint64_t lds_fill, bool hbm_only) {
@@ -93,6 +99,7 @@ struct dtgpu_batch {
     DevBuf<uint32_t> p_par, p_pent, p_pch, p_pcnt, p_child, p_tip, p_erec, p_doff, p_dense;
     DevBuf<Cmd> p_opc;
     DevBuf<uint32_t> p_base;
+    DevBuf<uint32_t> p_order;   // two-phase planner: each document's walk order (by entry arena offset)
     DevBuf<PlanDesc> p_docs;
     DevBuf<PlanResult> p_results;
     PlanParams plan{};
@@ -330,6 +337,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         CK(B->p_opc.upload(opc, s)); CK(B->d_aruns.upload(aruns, s)); CK(B->p_tip.upload(tip, s));
         CK(B->p_erec.upload(erec, s)); CK(B->p_doff.upload(doff, s)); CK(B->p_dense.upload(dense, s));
         CK(B->p_base.upload(base_rows, s));
+        CK(B->p_order.alloc(std::max<size_t>(erec.size() / EREC_WORDS, 1)));
         CK(B->p_docs.upload(pdesc, s));
         CK(B->p_results.alloc(n));
         CK(hipMemsetAsync(B->p_results.p, 0, std::max<size_t>(n, 1) * sizeof(PlanResult), s));
@@ -337,7 +345,8 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         q.par = B->p_par.p; q.pent = B->p_pent.p; q.pch = B->p_pch.p; q.pcnt = B->p_pcnt.p;
         q.child = B->p_child.p; q.opc = B->p_opc.p;
         q.aruns = B->d_aruns.p; q.tip = B->p_tip.p; q.erec = B->p_erec.p; q.doff = B->p_doff.p;
-        q.dense = B->p_dense.p; q.base = B->p_base.p; q.prow = B->p_base.p;
+        q.dense = B->p_dense.p; q.base = B->p_base.p; q.prow = B->p_base.p; q.order = B->p_order.p;
+        q.split = plan_split_setting();
         q.lds_entries = (lds_entries + 7) & ~7u;
         q.max_agents = max_agents;
         q.prof = getenv("DTGPU_PLAN_PROF") ? 1u : 0u;
@@ -626,13 +635,15 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
         max_agents = std::max<uint32_t>(max_agents, prr[i].n_chains);
     }
     CK(B->p_base.alloc(base_total));
+    CK(B->p_order.alloc(std::max<uint64_t>(o_erec / EREC_WORDS, 1)));
     CK(B->p_docs.upload(pdesc, s));
     CK(B->p_results.alloc(n));
     CK(hipMemsetAsync(B->p_results.p, 0, std::max<size_t>(n, 1) * sizeof(PlanResult), s));
     PlanParams &q = B->plan;
     q.par = B->p_par.p; q.pent = B->p_pent.p; q.pch = B->p_pch.p; q.pcnt = B->p_pcnt.p; q.child = B->p_child.p;
     q.opc = B->p_opc.p; q.aruns = B->d_aruns.p; q.tip = B->p_tip.p; q.erec = B->p_erec.p; q.doff = B->p_doff.p;
-    q.dense = B->p_dense.p; q.base = B->p_base.p; q.prow = B->pr_rows.p;
+    q.dense = B->p_dense.p; q.base = B->p_base.p; q.prow = B->pr_rows.p; q.order = B->p_order.p;
+    q.split = plan_split_setting();
     q.lds_entries = (lds_entries + 7) & ~7u;
     q.max_agents = max_agents;
     q.prof = getenv("DTGPU_PLAN_PROF") ? 1u : 0u;
