@@ -40,6 +40,12 @@ __device__ __forceinline__ uint32_t scan_incl(uint32_t v) {   // inclusive prefi
     return v;
 }
 
+// A refill waits for its load inside the refill branch: the compiler's counter analysis then
+// sees nothing pending where the paths meet, instead of a vmcnt(0) at every use -- which would
+// also wait for each entry's row store (vmcnt counts stores).  s_waitcnt vmcnt(0), the other
+// counters left alone.
+__device__ __forceinline__ void wait_vm() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 // 64 consecutive words / pairs cached in one VGPR, addressed by a uniform index
 struct Chunk {
     uint32_t blk, v;
@@ -50,6 +56,7 @@ struct Chunk {
             blk = i & ~63u;
             const uint32_t k = blk + lane();
             v = k < n ? load(k) : 0xFFFFFFFFu;
+            wait_vm();
         }
         return rdl(v, i & 63u);
     }
@@ -66,6 +73,7 @@ struct Chunk2 {
             const uint32_t k = blk + lane();
             const uint2 v = k < n ? load(k) : make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
             a = v.x; b = v.y;
+            wait_vm();
         }
         return make_uint2(rdl(a, i & 63u), rdl(b, i & 63u));
     }
@@ -327,8 +335,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
                 if (l == pc) row = max(row, psd + p + 1);   // seq0 + (p - start) + 1
                 if (k == k0) first_chain = pc;
             }
-            // every entry's parent vector (the planner reads it); the ring serves this loop
-            if (l < nch || ((keep >> (i & 63u)) & 1u)) rows[size_t(i) * PREP_MAX_CHAINS + l] = row;
+            // every entry's parent vector (the planner reads it) goes out with its ring: the
+            // rows of 8 entries stored together when the ring wraps, so the store's completion
+            // (vmcnt counts stores) is waited for once per 8 entries, not at every entry
             uint32_t c = 0xFFFFFFFFu;
             if (first_chain != 0xFFFFFFFFu && rdl(row, first_chain) == rdl(clen, first_chain)) c = first_chain;
             if (c == 0xFFFFFFFFu) {
@@ -358,6 +367,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
                 const uint32_t slot = i & (RING - 1);
                 ring_row[slot * 64 + l] = row;
                 if (l == 0) { ring_meta[3 * slot] = i; ring_meta[3 * slot + 1] = c; ring_meta[3 * slot + 2] = s0 - s; }
+                if (slot == RING - 1 || i + 1 == ne) {
+                    for (uint32_t r = i & ~(RING - 1); r <= i; r++) {
+                        // a row a child more than RING entries on reads back is stored whole
+                        // (chains opened later read as zero); the planner reads chains < nch
+                        if (l < nch || ((keep >> (r & 63u)) & 1u))
+                            rows[size_t(r) * PREP_MAX_CHAINS + l] = ring_row[(r & (RING - 1)) * 64 + l];
+                    }
+                }
             }
         }
     }
