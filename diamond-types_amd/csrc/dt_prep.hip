@@ -116,6 +116,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
     uint16_t *lfill = reinterpret_cast<uint16_t *>(lfw);
     if (blockIdx.x >= P.n_docs) return;
     const uint32_t doc = P.doc_list ? P.doc_list[blockIdx.x] : blockIdx.x;
+    uint32_t flag = 0;
+    if (P.mode == 1 && lane() == 0) P.chain_flag[doc] = 0;
+    if (P.mode == 2) {
+        flag = P.chain_flag[doc];
+        if (flag == 0) return;   // the first half ended the document (its status is written)
+    }
     const PrepDesc D = P.docs[doc];
     PrepResult R{};
     if (D.skip) {
@@ -161,6 +167,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
 #ifdef DTGPU_PREP_PROF
     const uint64_t T0 = wall_clock64();
 #endif
+    if (P.mode != 2) {
     // ---- 1. parents: entry of each parent, child counts ------------------------------------------
     for (uint32_t i = l; i < (ne + 1) / 2; i += 64) lfw[i] = 0;
     __syncthreads();
@@ -268,18 +275,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
         if (l == 0) eop[ne] = nops;
     }
     wave_fence();
+    }   // P.mode != 2
+    if (P.mode == 1) {   // first half done: chain_kernel (or the second half) goes on from HBM
+        if (l == 0) P.chain_flag[doc] = 1;
+        return;
+    }
 
 #ifdef DTGPU_PREP_PROF
     const uint64_t T3 = wall_clock64();
 #endif
     // ---- 3. causal-chain decomposition (sequential over entries) ---------------------------------
     uint32_t clen = 0, nch = 0;      // lane c: ops in chain c so far
+    if (flag == 2) nch = doff[PREP_MAX_CHAINS];   // chain_kernel decomposed it (<= CHAIN_GROUP chains)
     uint32_t prev_row = 0;           // parent vector of entry i - 1
     uint32_t prev_chain = 0, prev_sd = 0;   // chain, seq0 - start of entry i - 1
-    {
-        Chunk cp;
-        Chunk2 cxy, cpp;   // entry (start, end); parent slot (LV, entry)
-        cp.init(); cxy.init(); cpp.init();
+    if (flag != 2) {
+        Chunk2 cpp;   // parent slot (LV, entry)
+        cpp.init();
+        // the current 64 entries' parent-slot ranges and LV spans, lane = entry mod 64, loaded at
+        // each 64-entry boundary (no per-entry refill test)
+        uint32_t bk0 = 0, bk1 = 0, bs = 0, be = 0;
         uint32_t bch = 0, bsd = 0;   // chain / seq0 - start of the current 64 entries, flushed per 64
         constexpr uint32_t RING = 8;
         uint64_t keep = 0;   // entries of the current 64 whose row a child beyond the ring reads
@@ -292,7 +307,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
         uint32_t *ring_meta = lfw + RING * 64;     // RING x {entry, chain, seq0 - start}
         if (l < RING) ring_meta[3 * l] = 0xFFFFFFFFu;
         __syncthreads();
+#ifdef DTGPU_PREP_PROF
+        uint64_t pa = 0, pb = 0, pc_ = 0, pk = 0;
+#endif
         for (uint32_t i = 0; i < ne; i++) {
+#ifdef DTGPU_PREP_PROF
+            uint64_t tq = __builtin_amdgcn_s_memtime();
+#endif
+            if ((i & 63u) == 0) {
+                const uint32_t j = min(i + l, ne - 1);
+                bk0 = poff[j];
+                bk1 = poff[j + 1];
+                const uint2 se = ent[j];
+                bs = se.x;
+                be = se.y;
+                wait_vm();
+            }
             if ((i & 63u) == 0) {   // a row is stored only for a child more than RING entries on
                 // (children are in index order: the last is the farthest; nearer ones read the
                 // row from the ring or, for the next entry, from prev_row)
@@ -304,8 +334,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
                 }
                 keep = ballot(need);
             }
-            const uint32_t k0 = cp.get(i, ne + 1, [&](uint32_t k) { return poff[k]; });
-            const uint32_t k1 = cp.get(i + 1, ne + 1, [&](uint32_t k) { return poff[k]; });
+#ifdef DTGPU_PREP_PROF
+            { const uint64_t t = __builtin_amdgcn_s_memtime(); pk += t - tq; tq = t; }
+#endif
+            const uint32_t k0 = rdl(bk0, i & 63u), k1 = rdl(bk1, i & 63u);
             uint32_t row = 0;
             uint32_t first_chain = 0xFFFFFFFFu;
             for (uint32_t k = k0; k < k1; k++) {
@@ -338,6 +370,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
             // every entry's parent vector (the planner reads it) goes out with its ring: the
             // rows of 8 entries stored together when the ring wraps, so the store's completion
             // (vmcnt counts stores) is waited for once per 8 entries, not at every entry
+#ifdef DTGPU_PREP_PROF
+            { const uint64_t t = __builtin_amdgcn_s_memtime(); pa += t - tq; tq = t; }
+#endif
             uint32_t c = 0xFFFFFFFFu;
             if (first_chain != 0xFFFFFFFFu && rdl(row, first_chain) == rdl(clen, first_chain)) c = first_chain;
             if (c == 0xFFFFFFFFu) {
@@ -351,8 +386,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
                 }
                 c = nch++;
             }
-            const uint2 se = cxy.get(i, ne, [&](uint32_t k) { return ent[k]; });
-            const uint32_t s = se.x, e = se.y;
+#ifdef DTGPU_PREP_PROF
+            { const uint64_t t = __builtin_amdgcn_s_memtime(); pb += t - tq; tq = t; }
+#endif
+            const uint32_t s = rdl(bs, i & 63u), e = rdl(be, i & 63u);
             const uint32_t s0 = rdl(clen, c);
             if (l == c) clen += e - s;
             bch = (i & 63u) == l ? c : bch;
@@ -376,7 +413,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
                     }
                 }
             }
+#ifdef DTGPU_PREP_PROF
+            pc_ += __builtin_amdgcn_s_memtime() - tq;
+#endif
         }
+#ifdef DTGPU_PREP_PROF
+        if (l == 0 && (doc == 0 || doc == P.n_docs / 2))
+            printf("PREPCHAIN doc %u ne %u keep %llu parents %llu select %llu rest %llu (cycles)\n", doc, ne,
+                   (unsigned long long)pk, (unsigned long long)pa, (unsigned long long)pb, (unsigned long long)pc_);
+#endif
     }
     wave_fence();
     if (report_oob()) return;
@@ -385,7 +430,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
 #endif
     // per chain: offset of its dense table (also kept in a register, lane = chain)
     uint32_t doff_l;
-    {
+    if (flag == 2) {
+        doff_l = l < nch ? doff[l] : 0u;   // (doff[PREP_MAX_CHAINS] holds the chain count)
+    } else {
         const uint32_t c = l < nch ? clen : 0;
         const uint32_t inc = scan_incl(c);
         doff_l = inc - c;
@@ -561,6 +608,128 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
 #endif
 }
 
+
+// ---- chain_kernel: the causal-chain decomposition of CHAIN_DOCS documents per wave ---------------
+// Phase 3 of prep_kernel (see there) for documents of at most CHAIN_GROUP chains, each document on
+// its own 16-lane group (lane = chain): the decomposition is one sequential walk over the
+// entries, so a wave per document spent most of its issue slots on one document's scalar chain
+// of steps; four documents now share every instruction.  Group-uniform values live in VGPRs,
+// reads across a group's lanes are permutes within the group.  A document that opens a 17th
+// chain is left to the second half of prep_kernel (its flag stays 1).  Rows are stored whole
+// (CHAIN_GROUP words: the planner reads chains < its count), so no keep-list is needed.
+__device__ __forceinline__ uint32_t gsh(uint32_t v, uint32_t src) { return uint32_t(__shfl(int(v), int(src))); }
+
+__global__ __launch_bounds__(64) void chain_kernel(PrepParams P) {
+    constexpr uint32_t G = CHAIN_GROUP, RING = G;
+    extern __shared__ uint32_t csh[];   // per group: RING rows x G words, RING x {entry, chain, sd}
+    const uint32_t l = lane(), g = l / G, c = l % G, base = g * G;
+    uint32_t *rr = csh + g * (RING * G + 3 * RING), *rm = rr + RING * G;
+    const uint32_t li = blockIdx.x * CHAIN_DOCS + g;
+    bool live = li < P.n_docs;
+    const uint32_t doc = live ? (P.doc_list ? P.doc_list[li] : li) : 0u;
+    live = live && P.chain_flag[doc] == 1;
+    const PrepDesc D = P.docs[doc];
+    const uint32_t ne = live ? D.ne : 0u, npar = D.n_par;
+    const uint2 *ent = reinterpret_cast<const uint2 *>(P.d_ent) + D.d_ent;
+    const uint32_t *poff = P.d_poff + D.d_poff;
+    const uint32_t *par_in = P.d_par + D.d_par;
+    const uint32_t *pent = P.pent + D.o_par;
+    uint32_t *rows = P.rows + D.o_rows;
+    uint32_t *doff = P.doff + D.o_doff;
+    uint2 *cs = reinterpret_cast<uint2 *>(P.scr + D.o_scr + ((npar + 1) & ~1u));
+    if (c < RING) rm[3 * c] = 0xFFFFFFFFu;
+    __builtin_amdgcn_wave_barrier();
+    uint32_t maxne = ne;
+    for (int d = 32; d >= 1; d >>= 1) maxne = max(maxne, uint32_t(__shfl_xor(int(maxne), d)));
+    uint32_t clen = 0, nch = 0, prev_row = 0, prev_chain = 0, prev_sd = 0;
+    uint32_t bk0 = 0, bk1 = 0, bs = 0, be = 0, bch = 0, bsd = 0;   // lane c: entry (i & ~15) + c
+    uint32_t pblk = 0xFFFFFFFFu, ppa = 0, ppe = 0;                 // lane c: parent slot pblk + c
+    bool ok = live;
+    for (uint32_t i = 0; i < maxne; i++) {
+        const bool on = ok && i < ne;
+        const uint32_t ib = i & (G - 1);
+        if (ib == 0 && on) {
+            const uint32_t j = min(i + c, ne - 1);
+            bk0 = poff[j];
+            bk1 = poff[j + 1];
+            const uint2 se = ent[j];
+            bs = se.x;
+            be = se.y;
+            wait_vm();
+        }
+        if (on) {
+            const uint32_t k0 = gsh(bk0, base + ib), k1 = gsh(bk1, base + ib);
+            uint32_t row = 0, first_chain = 0xFFFFFFFFu;
+            for (uint32_t k = k0; k < k1; k++) {
+                if ((k & ~(G - 1)) != pblk) {
+                    pblk = k & ~(G - 1);
+                    const uint32_t x = min(pblk + c, npar - 1);
+                    ppa = par_in[x];
+                    ppe = pent[x];
+                    wait_vm();
+                }
+                const uint32_t p = gsh(ppa, base + (k & (G - 1))), pe = gsh(ppe, base + (k & (G - 1)));
+                uint32_t prow, pc, psd;
+                if (pe + 1 == i) {
+                    prow = prev_row; pc = prev_chain; psd = prev_sd;
+                } else {
+                    const uint32_t slot = pe & (RING - 1);
+                    if (rm[3 * slot] == pe) {
+                        prow = rr[slot * G + c]; pc = rm[3 * slot + 1]; psd = rm[3 * slot + 2];
+                    } else {
+                        prow = rows[size_t(pe) * PREP_MAX_CHAINS + c];
+                        if (pe >= (i & ~(G - 1))) { pc = gsh(bch, base + (pe & (G - 1))); psd = gsh(bsd, base + (pe & (G - 1))); }
+                        else { const uint2 q = cs[pe]; pc = q.x; psd = q.y; }
+                    }
+                }
+                row = max(row, prow);
+                if (c == pc) row = max(row, psd + p + 1);
+                if (k == k0) first_chain = pc;
+            }
+            uint32_t ch = 0xFFFFFFFFu;
+            if (first_chain != 0xFFFFFFFFu && gsh(row, base + first_chain) == gsh(clen, base + first_chain)) ch = first_chain;
+            if (ch == 0xFFFFFFFFu) {
+                const uint32_t m = uint32_t(ballot(c < nch && row == clen) >> base) & 0xFFFFu;
+                if (m) ch = uint32_t(__ffs(int(m)) - 1);
+            }
+            if (ch == 0xFFFFFFFFu) {
+                if (nch == G) ok = false;   // a 17th chain: prep_kernel's second half redoes it
+                else ch = nch++;
+            }
+            if (ok) {
+                const uint32_t s = gsh(bs, base + ib), e = gsh(be, base + ib);
+                const uint32_t s0 = gsh(clen, base + ch);
+                if (c == ch) clen += e - s;
+                bch = ib == c ? ch : bch;
+                bsd = ib == c ? s0 - s : bsd;
+                prev_row = row; prev_chain = ch; prev_sd = s0 - s;
+                const uint32_t slot = i & (RING - 1);
+                rr[slot * G + c] = row;
+                if (c == 0) { rm[3 * slot] = i; rm[3 * slot + 1] = ch; rm[3 * slot + 2] = s0 - s; }
+                // the block's rows and chain pairs go out together (one wait per 16 entries)
+                if (ib == G - 1 || i + 1 == ne) {
+                    const uint32_t at = i & ~(G - 1);
+                    for (uint32_t r = at; r <= i; r++) rows[size_t(r) * PREP_MAX_CHAINS + c] = rr[(r & (RING - 1)) * G + c];
+                    if (at + c <= i) cs[at + c] = make_uint2(bch, bsd);
+                    wave_fence();   // later entries read these back
+                }
+            }
+        }
+    }
+    if (ok) {   // the chain tables' offsets: exclusive prefix of the chain lengths
+        uint32_t v = c < nch ? clen : 0u;
+        for (uint32_t d = 1; d < G; d <<= 1) {
+            const uint32_t o = uint32_t(__shfl_up(int(v), d, int(G)));
+            if (c >= d) v += o;
+        }
+        const uint32_t ex = v - (c < nch ? clen : 0u);
+        if (c < nch) doff[c] = ex;
+        if (c == G - 1) doff[nch] = v;
+        if (c == 0) doff[PREP_MAX_CHAINS] = nch;
+        if (c == 0) P.chain_flag[doc] = 2;
+    }
+}
+
 }  // namespace prep
 
 int launch_prep(const PrepParams &p, void *stream) {
@@ -568,10 +737,21 @@ int launch_prep(const PrepParams &p, void *stream) {
     // LDS: the child counts (u16 per entry), later the chain decomposition's ring (8 rows + meta)
     const size_t cw = (size_t(p.max_entries) + 1) / 2, rw = 8 * 64 + 24;
     const size_t lds = (cw > rw ? cw : rw) * 4;
-    if (p.check)
-        hipLaunchKernelGGL(prep::prep_kernel<true>, dim3(p.n_docs), dim3(64), lds, reinterpret_cast<hipStream_t>(stream), p);
-    else
-        hipLaunchKernelGGL(prep::prep_kernel<false>, dim3(p.n_docs), dim3(64), lds, reinterpret_cast<hipStream_t>(stream), p);
+    const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    PrepParams q = p;
+    if (p.check || !p.chain_flag) {   // one launch (the debug kernel always)
+        q.mode = 0;
+        if (p.check) hipLaunchKernelGGL(prep::prep_kernel<true>, dim3(p.n_docs), dim3(64), lds, st, q);
+        else hipLaunchKernelGGL(prep::prep_kernel<false>, dim3(p.n_docs), dim3(64), lds, st, q);
+        return hipGetLastError() == hipSuccess ? 0 : 66;
+    }
+    // first half, the chain decomposition four documents per wave, second half
+    q.mode = 1;
+    hipLaunchKernelGGL(prep::prep_kernel<false>, dim3(p.n_docs), dim3(64), lds, st, q);
+    const size_t clds = size_t(CHAIN_DOCS) * (CHAIN_GROUP * CHAIN_GROUP + 3 * CHAIN_GROUP) * 4;
+    hipLaunchKernelGGL(prep::chain_kernel, dim3((p.n_docs + CHAIN_DOCS - 1) / CHAIN_DOCS), dim3(64), clds, st, q);
+    q.mode = 2;
+    hipLaunchKernelGGL(prep::prep_kernel<false>, dim3(p.n_docs), dim3(64), lds, st, q);
     return hipGetLastError() == hipSuccess ? 0 : 66;
 }
 

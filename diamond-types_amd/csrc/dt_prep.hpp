@@ -45,7 +45,14 @@ struct PrepParams {
     uint32_t n_docs, max_entries;   // n_docs: the grid (the list's length when doc_list is set)
     const uint32_t *doc_list;       // nullable: block i prepares docs[doc_list[i]]
     uint32_t check;                 // debug mode (DTGPU_DEBUG): the bounds-checked kernel
+    // nullable: per document (by index) the stage of a three-launch pass -- prep_kernel's first
+    // half (parents, children, first op runs) sets 1, chain_kernel sets 2 when it decomposed the
+    // document into chains, the second half decomposes the rest itself; null: one launch
+    uint32_t *chain_flag;
+    uint32_t mode;                  // set by launch_prep: 0 whole kernel, 1 first half, 2 second half
 };
+// chain_kernel: documents per wave, lanes (= chains) per document
+constexpr uint32_t CHAIN_GROUP = 16, CHAIN_DOCS = 64 / CHAIN_GROUP;
 
 // owner (n_par, padded to even), {chain, seq0 - start} pairs (2 ne), coff, eop (ne + 1 each): even,
 // so every document's pair array is 8-byte aligned

@@ -56,6 +56,12 @@ uint32_t plan_split_setting() {
     const char *e = getenv("DTGPU_PLAN_SPLIT");
     return e && *e == '0' ? 0u : 1u;
 }
+// Prep as three launches with the chain decomposition four documents per wave, unless
+// DTGPU_PREP_CHAINS=0 selects the single launch (A/B).
+uint32_t prep_chains_setting() {
+    const char *e = getenv("DTGPU_PREP_CHAINS");
+    return e && *e == '0' ? 0u : 1u;
+}
 // Per-document replay layout: block capacity, HBM index bytes, LDS tier.
 struct Layout { uint32_t max_blocks; uint64_t gidx; int tier; uint32_t tier_blocks; };
 Layout replay_layout(uint64_t n_ins, uint64_t lds_fill, bool hbm_only) {
@@ -99,7 +105,8 @@ struct dtgpu_batch {
     DevBuf<uint32_t> p_par, p_pent, p_pch, p_pcnt, p_child, p_tip, p_erec, p_doff, p_dense;
     DevBuf<Cmd> p_opc;
     DevBuf<uint32_t> p_base;
-    DevBuf<uint32_t> p_order;   // two-phase planner: each document's walk order (by entry arena offset)
+    DevBuf<uint32_t> p_order;
+    DevBuf<uint32_t> pr_chain;   // prep's three-launch pass: per document its stage (dt_prep.hpp)   // two-phase planner: each document's walk order (by entry arena offset)
     DevBuf<PlanDesc> p_docs;
     DevBuf<PlanResult> p_results;
     PlanParams plan{};
@@ -604,6 +611,10 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     pp.par = B->p_par.p; pp.pent = B->p_pent.p; pp.pch = B->p_pch.p; pp.pcnt = B->p_pcnt.p; pp.child = B->p_child.p;
     pp.aruns = B->d_aruns.p; pp.tip = B->p_tip.p; pp.erec = B->p_erec.p; pp.doff = B->p_doff.p; pp.dense = B->p_dense.p;
     pp.rows = B->pr_rows.p; pp.scr = B->pr_scr.p; pp.opc = B->p_opc.p;
+    if (prep_chains_setting()) {
+        CK(B->pr_chain.alloc(std::max<size_t>(n, 1)));
+        pp.chain_flag = B->pr_chain.p;
+    }
     pp.docs = B->pr_docs.p; pp.results = B->pr_res.p; pp.n_docs = uint32_t(n); pp.max_entries = max_e;
     // debug mode (DTGPU_DEBUG, or DTGPU_PREP_CHECK alone): the bounds-checked prep kernel
     pp.check = (getenv("DTGPU_DEBUG") || getenv("DTGPU_PREP_CHECK")) ? 1u : 0u;
