@@ -124,6 +124,8 @@ struct PlanParams {
     uint32_t prof;          // cycle profile into PlanResult.prof
     uint32_t split;         // <= 64 chains: the two-phase planner (order, then lane-parallel steps)
     uint32_t *order;        // two-phase planner: walk orders, document d's at its entry offset
+    uint32_t *walk;         // nullable: per document {status, steps} of walk_kernel (the orders
+                            // four documents per wave); null: the planner walks itself
     Cmd *cmds;
     uint32_t *tlist;
     const PlanDesc *docs;

@@ -63,6 +63,7 @@ struct P {
     // outputs
     Cmd *cmds;
     uint32_t *tlist;
+    const uint32_t *walk;  // walk_kernel's {status, steps} for this document, or null
     uint32_t ccap, tcap;
     uint32_t count_only;   // sizing pass: count commands and entries, write nothing
     // wave-uniform state
@@ -771,7 +772,7 @@ DEV void plan_doc_split(P &p, PlanResult *res) {
     const uint32_t l = lane_id();
     uint32_t top = 0;
     bool bad_np = false;
-    for (uint32_t c = 0; c < p.ne; c += 64) {
+    for (uint32_t c = 0; c < p.ne && !p.walk; c += 64) {
         const uint32_t e = c + l;
         if (e < p.ne) {
             const uint32_t np = p.erec[size_t(e) * EREC_WORDS + R_NP];
@@ -779,7 +780,7 @@ DEV void plan_doc_split(P &p, PlanResult *res) {
             p.pending[e] = uint8_t(min(np, 0x7Fu) | (np >= 2 ? MERGE_BIT : 0));
         }
     }
-    for (int c = int((p.ne + 63) / 64) - 1; c >= 0; c--) {
+    for (int c = p.walk ? -1 : int((p.ne + 63) / 64) - 1; c >= 0; c--) {
         if (!charge(p)) break;
         const uint32_t e = uint32_t(c) * 64 + (63 - l);
         const bool root = e < p.ne && p.erec[size_t(e) * EREC_WORDS + R_NP] == 0;
@@ -793,15 +794,20 @@ DEV void plan_doc_split(P &p, PlanResult *res) {
     wave_fence();
     tk(p);
     PT(5);
-    // ---- phase A: the order ----
+    // ---- phase A: the order (walk_kernel's, when it ran) ----
     uint32_t *order = p.order;   // ne words
     Stk S;
     S.v = 0; S.mm = 0; S.n = 0; S.nl = top;
-    bool have = S.nl > 0 && !p.err;
+    bool have = S.nl > 0 && !p.err && !p.walk;
     uint32_t idx = have ? stk_pick(p, S) : 0;
     uint32_t rw = have ? load_rec(p, idx) : 0;
     uint32_t ns = 0;
     uint32_t ordv = 0;   // lane j: order[64 * (ns / 64) + j] until its 64 are stored together
+    if (p.walk) {
+        const uint32_t wst = U(p.walk[0]);
+        ns = U(p.walk[1]);
+        if (wst) fail(p, wst);
+    }
     while (have && !p.err) {
         if (!charge(p)) break;
         if (ns >= p.ne) { fail(p, PLAN_ERR_INTERNAL); break; }
@@ -829,7 +835,7 @@ DEV void plan_doc_split(P &p, PlanResult *res) {
             rw = load_rec(p, idx);
         }
     }
-    if ((ns & 63u) && l < (ns & 63u)) order[(ns & ~63u) + l] = ordv;
+    if (!p.walk && (ns & 63u) && l < (ns & 63u)) order[(ns & ~63u) + l] = ordv;
     PT(0);
     // every lane reads the order phase A wrote
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -1129,6 +1135,7 @@ DEV void plan_entry(const PlanParams &Q) {
     p.base = Q.base + pd.base_off;
     p.prow = Q.prow + pd.prow_off;
     p.order = Q.order + pd.erec_off / EREC_WORDS;
+    p.walk = SPLIT && Q.walk ? Q.walk + 2 * size_t(d) : nullptr;
     p.row_stride = pd.row_stride;
     p.cmds = Q.cmds + pd.cmd_off;
     p.tlist = Q.tlist + pd.tlist_off;
@@ -1166,12 +1173,122 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PLAN_W
 }
 __global__ __launch_bounds__(64) void plan_kernel_wide(PlanParams Q) { plan_entry<PLAN_MAX_AGENTS / 64>(Q); }
 
+
+// ---- walk_kernel: the spanning-tree orders of CHAIN_WALK_DOCS documents per wave ----------------
+// plan_doc_split's phase A for <= 64-chain documents, each on a 16-lane group: the same stack
+// (a flat LDS stack here: push at the top, pick = the top unless it is a merge and a non-merge is
+// below, which then swaps places with it), the same pending counts, one record load per step.
+// A walk is a sequential chain of dependent steps whose work is a few lane operations, so one
+// document per wave left most issue slots to waiting; four share each instruction here.  The plan
+// kernel then runs phase B from the stored order (PlanParams.walk: status, steps).
+constexpr uint32_t WG = 16, WALK_DOCS = 64 / WG;
+DEV uint32_t wsh(uint32_t v, uint32_t src) { return uint32_t(__shfl(int(v), int(src))); }
+__global__ __launch_bounds__(64) void walk_kernel(PlanParams Q) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t wl16[];
+    const uint32_t l = lane_id(), g = l / WG, c = l % WG, base = g * WG;
+    const uint32_t stride = PLAN_TODO_CAP + (Q.lds_entries + 1) / 2;   // u16 per group: stack, pending bytes
+    uint16_t *todo = wl16 + g * stride;
+    uint8_t *pend = reinterpret_cast<uint8_t *>(todo + PLAN_TODO_CAP);
+    const uint32_t li = blockIdx.x * WALK_DOCS + g;
+    bool on = li < Q.n_docs;
+    const uint32_t d = on ? (Q.doc_list ? Q.doc_list[li] : li) : 0u;
+    const PlanDesc pd = Q.docs[d];
+    on = on && !pd.skip && pd.n_agents <= 64 && pd.ne <= Q.lds_entries;
+    const uint32_t ne = on ? pd.ne : 0u;
+    const uint32_t *erec = Q.erec + pd.erec_off;
+    const uint32_t *child = Q.child + pd.child_off;
+    uint32_t *order = Q.order + pd.erec_off / EREC_WORDS;
+    uint32_t err = 0, top = 0;
+    const uint32_t limit = uint32_t(min<uint64_t>(1024ull * (uint64_t(ne) + 16) + 4ull * pd.n_lv + (1u << 20), 0xFFFFFFF0ull));
+    uint32_t steps = 0;
+    const uint32_t below = (1u << c) - 1u;
+    bool bad_np = false;
+    for (uint32_t e = c; e < ne; e += WG) {
+        const uint32_t np = erec[size_t(e) * EREC_WORDS + R_NP];
+        if (np > 0x7Fu) bad_np = true;
+        pend[e] = uint8_t(min(np, 0x7Fu) | (np >= 2 ? MERGE_BIT : 0));
+    }
+    if ((uint32_t(__ballot(bad_np) >> base) & 0xFFFFu) && on) err = PLAN_WIDE_MERGE;
+    // roots, highest index first, so the lowest root ends on the top
+    for (int cb = int((ne + WG - 1) / WG) - 1; cb >= 0 && !err; cb--) {
+        const uint32_t e = uint32_t(cb) * WG + (WG - 1 - c);
+        const bool root = e < ne && erec[size_t(e) * EREC_WORDS + R_NP] == 0;
+        const uint32_t m = uint32_t(__ballot(root) >> base) & 0xFFFFu;
+        if (top + uint32_t(__popc(m)) > PLAN_TODO_CAP) { err = PLAN_TODO_FULL; break; }
+        if (root) todo[top + uint32_t(__popc(m & below))] = uint16_t(e);
+        top += uint32_t(__popc(m));
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    uint32_t ns = 0, ordv = 0;
+    bool act = on && !err && top > 0;
+    while (__ballot(act)) {
+        if (act) {
+            if (++steps > limit) { err = PLAN_ERR_INTERNAL; act = false; }
+        }
+        if (act) {
+            // pick: the top, unless it is a merge and a non-merge lies below (it takes its place)
+            const uint32_t t = top - 1;
+            uint32_t idx = todo[t];
+            if (pend[idx] & MERGE_BIT) {
+                int found = -1;
+                for (int hi = int(t) - 1; hi >= 0 && found < 0; hi -= int(WG)) {
+                    const int i = hi - int(c);
+                    const bool okk = i >= 0 && !(pend[todo[i]] & MERGE_BIT);
+                    const uint32_t m = uint32_t(__ballot(okk) >> base) & 0xFFFFu;
+                    if (m) found = hi - (__ffs(int(m)) - 1);
+                }
+                if (found >= 0) {
+                    const uint32_t x = todo[found];
+                    __builtin_amdgcn_wave_barrier();
+                    if (c == 0) todo[found] = uint16_t(idx);
+                    idx = x;
+                }
+            }
+            top = t;
+            ordv = c == (ns & (WG - 1)) ? idx : ordv;
+            if ((ns & (WG - 1)) == WG - 1) order[ns - (WG - 1) + c] = ordv;
+            ns++;
+            // the entry's children (first / last from the record; a longer list from the CSR)
+            const uint32_t wsel = c == 0 ? R_NCH : c == 1 ? R_CH0 : c == 2 ? R_FIRSTCH : R_LASTCH;
+            const uint32_t rv = erec[size_t(idx) * EREC_WORDS + wsel];
+            const uint32_t nch = wsh(rv, base), ch0 = wsh(rv, base + 1), firstch = wsh(rv, base + 2), lastch = wsh(rv, base + 3);
+            for (uint32_t cc = 0; cc < nch; cc += WG) {
+                const bool has = cc + c < nch;
+                uint32_t chv = 0;
+                if (has) chv = nch <= 2 ? (c == 0 ? firstch : lastch) : child[ch0 + cc + c];
+                bool ready = false;
+                if (has) {
+                    const uint8_t pdv = uint8_t(pend[chv] - 1);
+                    pend[chv] = pdv;
+                    ready = (pdv & 0x7F) == 0;
+                }
+                const uint32_t m = uint32_t(__ballot(ready) >> base) & 0xFFFFu;
+                if (top + uint32_t(__popc(m)) > PLAN_TODO_CAP) { err = PLAN_TODO_FULL; break; }
+                if (ready) todo[top + uint32_t(__popc(m & below))] = uint16_t(chv);
+                top += uint32_t(__popc(m));
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            act = !err && top > 0;
+        }
+    }
+    if (on && (ns & (WG - 1)) && c < (ns & (WG - 1))) order[(ns & ~(WG - 1)) + c] = ordv;
+    if (on && c == 0) {
+        Q.walk[2 * size_t(d)] = err;
+        Q.walk[2 * size_t(d) + 1] = ns;
+    }
+}
+
 }  // namespace pdev
 
 int launch_plan(const PlanParams &q, void *stream) {
     if (!q.n_docs) return OK;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const size_t lds = 2 * size_t(PLAN_TODO_CAP) + ((size_t(q.lds_entries) + 15) & ~size_t(15));   // todo + pending
+    if (q.split && q.walk) {
+        const size_t wlds = size_t(pdev::WALK_DOCS) * 2 * (PLAN_TODO_CAP + (q.lds_entries + 1) / 2);
+        hipLaunchKernelGGL(pdev::walk_kernel, dim3((q.n_docs + pdev::WALK_DOCS - 1) / pdev::WALK_DOCS), dim3(64), wlds, s, q);
+    }
     if (q.split) hipLaunchKernelGGL(pdev::plan_kernel_1<true>, dim3(q.n_docs), dim3(64), lds, s, q);
     else hipLaunchKernelGGL(pdev::plan_kernel_1<false>, dim3(q.n_docs), dim3(64), lds, s, q);
     if (hipGetLastError() != hipSuccess) return ErrHip;

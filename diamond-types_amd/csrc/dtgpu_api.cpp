@@ -56,6 +56,15 @@ uint32_t plan_split_setting() {
     const char *e = getenv("DTGPU_PLAN_SPLIT");
     return e && *e == '0' ? 0u : 1u;
 }
+// The walk orders four documents per wave (walk_kernel) before the plan kernel, unless
+// DTGPU_PLAN_WALK=0 lets the plan kernel walk each document itself (A/B).
+// Small batches (a walk kernel launch costs a single document more than it saves) walk in the
+// plan kernel.
+uint32_t walk_setting(size_t n_docs) {
+    const char *e = getenv("DTGPU_PLAN_WALK");
+    if (e && *e) return *e == '0' ? 0u : 1u;
+    return n_docs >= 256 ? 1u : 0u;
+}
 // Prep as three launches with the chain decomposition four documents per wave, unless
 // DTGPU_PREP_CHAINS=0 selects the single launch (A/B).
 uint32_t prep_chains_setting() {
@@ -106,6 +115,7 @@ struct dtgpu_batch {
     DevBuf<Cmd> p_opc;
     DevBuf<uint32_t> p_base;
     DevBuf<uint32_t> p_order;
+    DevBuf<uint32_t> p_walk;    // walk_kernel: per document {status, steps}
     DevBuf<uint32_t> pr_chain;   // prep's three-launch pass: per document its stage (dt_prep.hpp)   // two-phase planner: each document's walk order (by entry arena offset)
     DevBuf<PlanDesc> p_docs;
     DevBuf<PlanResult> p_results;
@@ -345,6 +355,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         CK(B->p_erec.upload(erec, s)); CK(B->p_doff.upload(doff, s)); CK(B->p_dense.upload(dense, s));
         CK(B->p_base.upload(base_rows, s));
         CK(B->p_order.alloc(std::max<size_t>(erec.size() / EREC_WORDS, 1)));
+        CK(B->p_walk.alloc(2 * std::max<size_t>(n, 1)));
         CK(B->p_docs.upload(pdesc, s));
         CK(B->p_results.alloc(n));
         CK(hipMemsetAsync(B->p_results.p, 0, std::max<size_t>(n, 1) * sizeof(PlanResult), s));
@@ -353,6 +364,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         q.child = B->p_child.p; q.opc = B->p_opc.p;
         q.aruns = B->d_aruns.p; q.tip = B->p_tip.p; q.erec = B->p_erec.p; q.doff = B->p_doff.p;
         q.dense = B->p_dense.p; q.base = B->p_base.p; q.prow = B->p_base.p; q.order = B->p_order.p;
+        q.walk = walk_setting(n) ? B->p_walk.p : nullptr;
         q.split = plan_split_setting();
         q.lds_entries = (lds_entries + 7) & ~7u;
         q.max_agents = max_agents;
@@ -647,6 +659,7 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     }
     CK(B->p_base.alloc(base_total));
     CK(B->p_order.alloc(std::max<uint64_t>(o_erec / EREC_WORDS, 1)));
+    CK(B->p_walk.alloc(2 * std::max<size_t>(n, 1)));
     CK(B->p_docs.upload(pdesc, s));
     CK(B->p_results.alloc(n));
     CK(hipMemsetAsync(B->p_results.p, 0, std::max<size_t>(n, 1) * sizeof(PlanResult), s));
@@ -654,6 +667,7 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     q.par = B->p_par.p; q.pent = B->p_pent.p; q.pch = B->p_pch.p; q.pcnt = B->p_pcnt.p; q.child = B->p_child.p;
     q.opc = B->p_opc.p; q.aruns = B->d_aruns.p; q.tip = B->p_tip.p; q.erec = B->p_erec.p; q.doff = B->p_doff.p;
     q.dense = B->p_dense.p; q.base = B->p_base.p; q.prow = B->pr_rows.p; q.order = B->p_order.p;
+    q.walk = walk_setting(n) ? B->p_walk.p : nullptr;
     q.split = plan_split_setting();
     q.lds_entries = (lds_entries + 7) & ~7u;
     q.max_agents = max_agents;
