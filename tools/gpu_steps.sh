@@ -26,9 +26,13 @@ kb() {   # kbench over the three benchmark files
 for s in ${STEPS//,/ }; do
   case $s in
     tests)
+      # a heartbeat line a minute: a slow test (the spawned multi-process ones on a cold box)
+      # prints nothing until it ends
+      ( while sleep 60; do echo "tests running: $(grep -c -E 'PASSED|FAILED' "$OUT/gpu_tests.log" 2>/dev/null) done"; done ) &
+      hb=$!
       timeout -k 10 900 python -u -m pytest ${@:-tests -m gpu} -x -v --timeout 480 --timeout-method thread \
         > "$OUT/gpu_tests.log" 2>&1
-      rc=$?; tail -3 "$OUT/gpu_tests.log"; [[ $rc != 0 ]] && grep -E "FAILED|Error" "$OUT/gpu_tests.log" | head -20
+      rc=$?; kill $hb 2>/dev/null; tail -3 "$OUT/gpu_tests.log"; [[ $rc != 0 ]] && grep -E "FAILED|Error" "$OUT/gpu_tests.log" | head -20
       ok tests $rc ;;
     smoke)
       timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
