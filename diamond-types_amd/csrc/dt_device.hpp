@@ -108,6 +108,7 @@ struct PlanDesc {       // per document; offsets index the concatenated PlanInpu
     uint64_t prow_off;    // parent version vectors (per entry, row_stride words, chains < n_agents)
     uint32_t ne, n_agents, n_aruns, ntip, n_lv, ccap, tcap, skip;
     uint32_t row_stride, pad;
+    uint64_t coff_off, poff_off;   // device staging: children CSR offsets (prep scratch), parent offsets (decoder)
 };
 struct PlanResult {
     uint32_t status, ncmd, ntlist, n_tip;
@@ -126,6 +127,7 @@ struct PlanParams {
     uint32_t *order;        // two-phase planner: walk orders, document d's at its entry offset
     uint32_t *walk;         // nullable: per document {status, steps} of walk_kernel (the orders
                             // four documents per wave); null: the planner walks itself
+    const uint32_t *coff, *poff;   // walk_kernel's CSR mode: children offsets, parent offsets
     Cmd *cmds;
     uint32_t *tlist;
     const PlanDesc *docs;
@@ -133,7 +135,10 @@ struct PlanParams {
     uint32_t n_docs, count_only;   // n_docs: the grid (the list's length when doc_list is set)
     const uint32_t *doc_list;      // nullable: block i plans docs[doc_list[i]]
 };
-int launch_plan(const PlanParams &q, void *stream);
+int launch_plan(const PlanParams &q, void *stream, bool walk = true);
+// walk_kernel alone; csr: children and parent counts from prep's CSR (ready after prep's first
+// half, so the walk can run beside the chain decomposition) instead of the entry records
+int launch_walk(const PlanParams &q, void *stream, bool csr);
 
 // One replay pass: the LDS tiers (index in LDS, sized per tier) and then the HBM-index tier,
 // which also replays the LDS-tier documents that outgrew their LDS capacity.  A tier kernel

@@ -1183,6 +1183,7 @@ __global__ __launch_bounds__(64) void plan_kernel_wide(PlanParams Q) { plan_entr
 // kernel then runs phase B from the stored order (PlanParams.walk: status, steps).
 constexpr uint32_t WG = 16, WALK_DOCS = 64 / WG;
 DEV uint32_t wsh(uint32_t v, uint32_t src) { return uint32_t(__shfl(int(v), int(src))); }
+template <bool CSR>
 __global__ __launch_bounds__(64) void walk_kernel(PlanParams Q) {
     extern __shared__ __attribute__((aligned(16))) uint16_t wl16[];
     const uint32_t l = lane_id(), g = l / WG, c = l % WG, base = g * WG;
@@ -1197,6 +1198,7 @@ __global__ __launch_bounds__(64) void walk_kernel(PlanParams Q) {
     const uint32_t ne = on ? pd.ne : 0u;
     const uint32_t *erec = Q.erec + pd.erec_off;
     const uint32_t *child = Q.child + pd.child_off;
+    const uint32_t *coff = CSR ? Q.coff + pd.coff_off : nullptr, *poff = CSR ? Q.poff + pd.poff_off : nullptr;
     uint32_t *order = Q.order + pd.erec_off / EREC_WORDS;
     uint32_t err = 0, top = 0;
     const uint32_t limit = uint32_t(min<uint64_t>(1024ull * (uint64_t(ne) + 16) + 4ull * pd.n_lv + (1u << 20), 0xFFFFFFF0ull));
@@ -1204,7 +1206,7 @@ __global__ __launch_bounds__(64) void walk_kernel(PlanParams Q) {
     const uint32_t below = (1u << c) - 1u;
     bool bad_np = false;
     for (uint32_t e = c; e < ne; e += WG) {
-        const uint32_t np = erec[size_t(e) * EREC_WORDS + R_NP];
+        const uint32_t np = CSR ? poff[e + 1] - poff[e] : erec[size_t(e) * EREC_WORDS + R_NP];
         if (np > 0x7Fu) bad_np = true;
         pend[e] = uint8_t(min(np, 0x7Fu) | (np >= 2 ? MERGE_BIT : 0));
     }
@@ -1212,7 +1214,7 @@ __global__ __launch_bounds__(64) void walk_kernel(PlanParams Q) {
     // roots, highest index first, so the lowest root ends on the top
     for (int cb = int((ne + WG - 1) / WG) - 1; cb >= 0 && !err; cb--) {
         const uint32_t e = uint32_t(cb) * WG + (WG - 1 - c);
-        const bool root = e < ne && erec[size_t(e) * EREC_WORDS + R_NP] == 0;
+        const bool root = e < ne && (CSR ? poff[e + 1] == poff[e] : erec[size_t(e) * EREC_WORDS + R_NP] == 0);
         const uint32_t m = uint32_t(__ballot(root) >> base) & 0xFFFFu;
         if (top + uint32_t(__popc(m)) > PLAN_TODO_CAP) { err = PLAN_TODO_FULL; break; }
         if (root) todo[top + uint32_t(__popc(m & below))] = uint16_t(e);
@@ -1250,13 +1252,20 @@ __global__ __launch_bounds__(64) void walk_kernel(PlanParams Q) {
             if ((ns & (WG - 1)) == WG - 1) order[ns - (WG - 1) + c] = ordv;
             ns++;
             // the entry's children (first / last from the record; a longer list from the CSR)
-            const uint32_t wsel = c == 0 ? R_NCH : c == 1 ? R_CH0 : c == 2 ? R_FIRSTCH : R_LASTCH;
-            const uint32_t rv = erec[size_t(idx) * EREC_WORDS + wsel];
-            const uint32_t nch = wsh(rv, base), ch0 = wsh(rv, base + 1), firstch = wsh(rv, base + 2), lastch = wsh(rv, base + 3);
+            uint32_t nch, ch0, firstch = 0, lastch = 0;
+            if (CSR) {   // the CSR offsets, then (below) the list itself
+                const uint32_t rv = coff[idx + (c & 1u)];
+                ch0 = wsh(rv, base);
+                nch = wsh(rv, base + 1) - ch0;
+            } else {
+                const uint32_t wsel = c == 0 ? R_NCH : c == 1 ? R_CH0 : c == 2 ? R_FIRSTCH : R_LASTCH;
+                const uint32_t rv = erec[size_t(idx) * EREC_WORDS + wsel];
+                nch = wsh(rv, base); ch0 = wsh(rv, base + 1); firstch = wsh(rv, base + 2); lastch = wsh(rv, base + 3);
+            }
             for (uint32_t cc = 0; cc < nch; cc += WG) {
                 const bool has = cc + c < nch;
                 uint32_t chv = 0;
-                if (has) chv = nch <= 2 ? (c == 0 ? firstch : lastch) : child[ch0 + cc + c];
+                if (has) chv = !CSR && nch <= 2 ? (c == 0 ? firstch : lastch) : child[ch0 + cc + c];
                 bool ready = false;
                 if (has) {
                     const uint8_t pdv = uint8_t(pend[chv] - 1);
@@ -1281,14 +1290,21 @@ __global__ __launch_bounds__(64) void walk_kernel(PlanParams Q) {
 
 }  // namespace pdev
 
-int launch_plan(const PlanParams &q, void *stream) {
+int launch_walk(const PlanParams &q, void *stream, bool csr) {
+    if (!q.n_docs || !q.split || !q.walk) return OK;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const size_t wlds = size_t(pdev::WALK_DOCS) * 2 * (PLAN_TODO_CAP + (q.lds_entries + 1) / 2);
+    const dim3 grid((q.n_docs + pdev::WALK_DOCS - 1) / pdev::WALK_DOCS);
+    if (csr) hipLaunchKernelGGL(pdev::walk_kernel<true>, grid, dim3(64), wlds, s, q);
+    else hipLaunchKernelGGL(pdev::walk_kernel<false>, grid, dim3(64), wlds, s, q);
+    return hipGetLastError() == hipSuccess ? OK : ErrHip;
+}
+
+int launch_plan(const PlanParams &q, void *stream, bool walk) {
     if (!q.n_docs) return OK;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const size_t lds = 2 * size_t(PLAN_TODO_CAP) + ((size_t(q.lds_entries) + 15) & ~size_t(15));   // todo + pending
-    if (q.split && q.walk) {
-        const size_t wlds = size_t(pdev::WALK_DOCS) * 2 * (PLAN_TODO_CAP + (q.lds_entries + 1) / 2);
-        hipLaunchKernelGGL(pdev::walk_kernel, dim3((q.n_docs + pdev::WALK_DOCS - 1) / pdev::WALK_DOCS), dim3(64), wlds, s, q);
-    }
+    if (walk && q.split && q.walk && launch_walk(q, stream, false)) return ErrHip;
     if (q.split) hipLaunchKernelGGL(pdev::plan_kernel_1<true>, dim3(q.n_docs), dim3(64), lds, s, q);
     else hipLaunchKernelGGL(pdev::plan_kernel_1<false>, dim3(q.n_docs), dim3(64), lds, s, q);
     if (hipGetLastError() != hipSuccess) return ErrHip;

@@ -732,6 +732,22 @@ __global__ __launch_bounds__(64) void chain_kernel(PrepParams P) {
 
 }  // namespace prep
 
+int launch_prep_stage(const PrepParams &p, void *stream, int stage) {
+    if (!p.n_docs) return 0;
+    const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const size_t cw = (size_t(p.max_entries) + 1) / 2, rw = 8 * 64 + 24;
+    const size_t lds = (cw > rw ? cw : rw) * 4;
+    PrepParams q = p;
+    if (stage == 2) {
+        const size_t clds = size_t(CHAIN_DOCS) * (CHAIN_GROUP * CHAIN_GROUP + 3 * CHAIN_GROUP) * 4;
+        hipLaunchKernelGGL(prep::chain_kernel, dim3((p.n_docs + CHAIN_DOCS - 1) / CHAIN_DOCS), dim3(64), clds, st, q);
+    } else {
+        q.mode = stage == 1 ? 1u : 2u;
+        hipLaunchKernelGGL(prep::prep_kernel<false>, dim3(p.n_docs), dim3(64), lds, st, q);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : 66;
+}
+
 int launch_prep(const PrepParams &p, void *stream) {
     if (!p.n_docs) return 0;
     // LDS: the child counts (u16 per entry), later the chain decomposition's ring (8 rows + meta)

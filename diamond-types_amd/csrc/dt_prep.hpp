@@ -59,5 +59,9 @@ constexpr uint32_t CHAIN_GROUP = 16, CHAIN_DOCS = 64 / CHAIN_GROUP;
 inline uint64_t prep_scratch_words(uint32_t n_par, uint32_t ne) { return (uint64_t(n_par) + 1) / 2 * 2 + 4ull * ne + 2; }
 
 int launch_prep(const PrepParams &p, void *stream);
+// The three-launch pass one stage at a time (1: first half, 2: chains, 3: second half), so a
+// caller can start work that needs only the first half (the planner's walk) beside the rest.
+// Requires p.chain_flag and !p.check.
+int launch_prep_stage(const PrepParams &p, void *stream, int stage);
 
 }  // namespace dtgpu

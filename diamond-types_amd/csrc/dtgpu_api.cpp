@@ -142,6 +142,8 @@ struct dtgpu_batch {
     DevBuf<PrepResult> pr_res;
     PrepParams prep{};
     hipEvent_t ev_dec = nullptr, ev_prep = nullptr;
+    hipStream_t wstream = nullptr;               // the planner's walk beside prep's second half
+    hipEvent_t ev_w0 = nullptr, ev_w1 = nullptr;
     float last_decode_ms = 0, last_prep_ms = 0;
 
     // batched encoder (dtgpu_batch_encode): per-document descriptors, scratch, output
@@ -154,6 +156,9 @@ struct dtgpu_batch {
     EncParams enc{};
 
     ~dtgpu_batch() {
+        if (ev_w0) (void)hipEventDestroy(ev_w0);
+        if (ev_w1) (void)hipEventDestroy(ev_w1);
+        if (wstream) (void)hipStreamDestroy(wstream);
         if (ev_dec) (void)hipEventDestroy(ev_dec);
         if (ev_prep) (void)hipEventDestroy(ev_prep);
         if (ev0) (void)hipEventDestroy(ev0);
@@ -563,6 +568,9 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
 #define CK(x) do { if ((x) != hipSuccess) return DTGPU_ERR_HIP; } while (0)
     CK(hipEventCreate(&B->ev0)); CK(hipEventCreate(&B->ev_mid)); CK(hipEventCreate(&B->ev1));
     CK(hipEventCreate(&B->ev_dec)); CK(hipEventCreate(&B->ev_prep));
+    CK(hipStreamCreateWithFlags(&B->wstream, hipStreamNonBlocking));
+    CK(hipEventCreateWithFlags(&B->ev_w0, hipEventDisableTiming));
+    CK(hipEventCreateWithFlags(&B->ev_w1, hipEventDisableTiming));
     hipStream_t s = B->stream;
     if (!Dd.merged) {
         if (launch_decode(Dd.P, s)) return DTGPU_ERR_HIP;
@@ -651,6 +659,8 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
         q.erec_off = r.o_erec; q.doff_off = r.o_doff; q.dense_off = r.o_dense;
         q.base_off = base_total;
         q.prow_off = r.o_rows;   // device-staged: the prep kernel's parent vectors
+        q.coff_off = r.o_scr + ((uint64_t(r.n_par) + 1) & ~1ull) + 2ull * r.ne;   // dt_prep.hpp scratch layout
+        q.poff_off = r.d_poff;
         q.row_stride = PREP_MAX_CHAINS;
         q.ne = r.ne; q.n_agents = prr[i].n_chains; q.n_aruns = r.n_aruns; q.ntip = r.n_ver; q.n_lv = r.n_lv;
         base_total += uint64_t(r.ne) * std::max<uint32_t>(prr[i].n_chains, 1);
@@ -668,6 +678,8 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     q.opc = B->p_opc.p; q.aruns = B->d_aruns.p; q.tip = B->p_tip.p; q.erec = B->p_erec.p; q.doff = B->p_doff.p;
     q.dense = B->p_dense.p; q.base = B->p_base.p; q.prow = B->pr_rows.p; q.order = B->p_order.p;
     q.walk = walk_setting(n) ? B->p_walk.p : nullptr;
+    q.coff = B->pr_scr.p;
+    q.poff = Dd.poff.p;
     q.split = plan_split_setting();
     q.lds_entries = (lds_entries + 7) & ~7u;
     q.max_agents = max_agents;
@@ -839,6 +851,29 @@ int launch_split_plan(dtgpu_batch *B, hipStream_t s) {
 }
 
 // One checkout pass on stream s: prep (device-staged batches), plan (device), replay.
+// Prep then plan for a device-staged batch.  With the three-launch prep and the walk kernel, the
+// walk (CSR mode: it needs only prep's first half) runs on B->wstream beside the chain
+// decomposition and prep's second half, and the plan kernel waits for it.  `mid` (nullable) is
+// recorded between the two on s.
+int prep_and_plan(dtgpu_batch *B, hipStream_t s, hipEvent_t mid) {
+    const bool prep = B->dec != nullptr;
+    const bool overlap = prep && B->n_gpu_planned && B->prep.chain_flag && !B->prep.check && B->plan.walk &&
+                         B->plan.coff && B->wstream && !getenv("DTGPU_NO_WALK_OVERLAP");
+    if (!overlap) {
+        if (prep && launch_prep(B->prep, s)) return ErrHip;
+        if (mid && hipEventRecord(mid, s) != hipSuccess) return ErrHip;
+        return B->n_gpu_planned ? launch_plan(B->plan, s) : OK;
+    }
+    if (launch_prep_stage(B->prep, s, 1)) return ErrHip;
+    if (hipEventRecord(B->ev_w0, s) != hipSuccess || hipStreamWaitEvent(B->wstream, B->ev_w0, 0) != hipSuccess) return ErrHip;
+    if (launch_walk(B->plan, B->wstream, true) != OK) return ErrHip;
+    if (hipEventRecord(B->ev_w1, B->wstream) != hipSuccess) return ErrHip;
+    if (launch_prep_stage(B->prep, s, 2) || launch_prep_stage(B->prep, s, 3)) return ErrHip;
+    if (mid && hipEventRecord(mid, s) != hipSuccess) return ErrHip;
+    if (hipStreamWaitEvent(s, B->ev_w1, 0) != hipSuccess) return ErrHip;
+    return launch_plan(B->plan, s, false);
+}
+
 int launch_all(dtgpu_batch *B, hipStream_t s) {
     if (B->xf_mode) return launch_replay_xf(B->large, s);
     if (B->split) {
@@ -847,12 +882,8 @@ int launch_all(dtgpu_batch *B, hipStream_t s) {
         if (!e) e = launch_split_plan(B, s);
         return e ? e : replay_all(B, s, B->split_tier);
     }
-    if (B->dec && launch_prep(B->prep, s)) return ErrHip;   // device-staged: walker inputs first
-    if (B->n_gpu_planned) {
-        int e = launch_plan(B->plan, s);
-        if (e) return e;
-    }
-    return replay_all(B, s);
+    const int e = prep_and_plan(B, s, nullptr);   // device-staged: walker inputs first
+    return e ? e : replay_all(B, s);
 }
 
 }  // namespace
@@ -1228,9 +1259,7 @@ dtgpu_status dtgpu_batch_run_e2e_timed(dtgpu_batch *B, float ms[4]) {
     if (hipEventRecord(B->ev_dec, s) != hipSuccess) return DTGPU_ERR_HIP;
     if (launch_decode(B->dec->P, s)) return DTGPU_ERR_HIP;
     if (hipEventRecord(B->ev_prep, s) != hipSuccess) return DTGPU_ERR_HIP;
-    if (launch_prep(B->prep, s)) return DTGPU_ERR_HIP;
-    if (hipEventRecord(B->ev0, s) != hipSuccess) return DTGPU_ERR_HIP;
-    if (B->n_gpu_planned && launch_plan(B->plan, s) != OK) return DTGPU_ERR_HIP;
+    if (prep_and_plan(B, s, B->ev0) != OK) return DTGPU_ERR_HIP;
     if (hipEventRecord(B->ev_mid, s) != hipSuccess) return DTGPU_ERR_HIP;
     int st = replay_all(B, s);
     if (st) return dtgpu_status(st);
@@ -1382,9 +1411,15 @@ dtgpu_status dtgpu_batch_run_timed(dtgpu_batch *B, float *ms) {
     const bool split = prep && B->split;   // split pass: prep / plan times are the main pipeline's
     if (hipEventRecord(B->ev_prep, s) != hipSuccess) return DTGPU_ERR_HIP;
     if (split && launch_split_side(B, s)) return DTGPU_ERR_HIP;
-    if (split ? launch_split_prep(B, s) != OK : (prep && launch_prep(B->prep, s))) return DTGPU_ERR_HIP;
-    if (hipEventRecord(B->ev0, s) != hipSuccess) return DTGPU_ERR_HIP;
-    if (split ? launch_split_plan(B, s) != OK : (B->n_gpu_planned && launch_plan(B->plan, s) != OK)) return DTGPU_ERR_HIP;
+    if (split) {
+        if (launch_split_prep(B, s) != OK || hipEventRecord(B->ev0, s) != hipSuccess || launch_split_plan(B, s) != OK)
+            return DTGPU_ERR_HIP;
+    } else if (B->xf_mode) {
+        if (hipEventRecord(B->ev0, s) != hipSuccess) return DTGPU_ERR_HIP;
+        if (B->n_gpu_planned && launch_plan(B->plan, s) != OK) return DTGPU_ERR_HIP;
+    } else if (prep_and_plan(B, s, B->ev0) != OK) {
+        return DTGPU_ERR_HIP;
+    }
     if (hipEventRecord(B->ev_mid, s) != hipSuccess) return DTGPU_ERR_HIP;
     int st = B->xf_mode ? launch_replay_xf(B->large, s) : replay_all(B, s, split ? B->split_tier : -1);
     if (st) return dtgpu_status(st);
