@@ -67,9 +67,12 @@ uint32_t walk_setting(size_t n_docs) {
 }
 // Prep as three launches with the chain decomposition four documents per wave, unless
 // DTGPU_PREP_CHAINS=0 selects the single launch (A/B).
-uint32_t prep_chains_setting() {
+// (Small batches keep the single launch: a document's chain walk on a 16-lane group is slower
+// than on a whole wave, and the launch saves nothing when the CU is not shared.)
+uint32_t prep_chains_setting(size_t n_docs) {
     const char *e = getenv("DTGPU_PREP_CHAINS");
-    return e && *e == '0' ? 0u : 1u;
+    if (e && *e) return *e == '0' ? 0u : 1u;
+    return n_docs >= 256 ? 1u : 0u;
 }
 // Per-document replay layout: block capacity, HBM index bytes, LDS tier.
 struct Layout { uint32_t max_blocks; uint64_t gidx; int tier; uint32_t tier_blocks; };
@@ -631,7 +634,7 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     pp.par = B->p_par.p; pp.pent = B->p_pent.p; pp.pch = B->p_pch.p; pp.pcnt = B->p_pcnt.p; pp.child = B->p_child.p;
     pp.aruns = B->d_aruns.p; pp.tip = B->p_tip.p; pp.erec = B->p_erec.p; pp.doff = B->p_doff.p; pp.dense = B->p_dense.p;
     pp.rows = B->pr_rows.p; pp.scr = B->pr_scr.p; pp.opc = B->p_opc.p;
-    if (prep_chains_setting()) {
+    if (prep_chains_setting(n)) {
         CK(B->pr_chain.alloc(std::max<size_t>(n, 1)));
         pp.chain_flag = B->pr_chain.p;
     }
