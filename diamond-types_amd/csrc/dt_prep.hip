@@ -450,27 +450,46 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
         pcnt[k] = q.y + par[k] + 1;
     }
     wave_fence();
-    for (uint32_t i = l; i < ne; i += 64) {    // entry records (dt_host.hpp PlanInput::erec)
-        // five 16-byte stores (records are 80 bytes, so 16-byte aligned): words 0-3 start, end,
-        // parents offset / count; 4-7 first op run, op runs, chain, seq0; 8-10 children offset /
-        // count, first parent LV; 11-13 and 14-16 the first two parents' entry, chain, count;
-        // 17 last child, 18 first child
+    // entry records (dt_host.hpp PlanInput::erec), 32 at a time: each lane builds its record in
+    // LDS (the ring's space), then the wave stores the 32 records (2,560 contiguous bytes) with
+    // 16-byte lanes side by side -- a lane storing its own 80-byte record leaves 16-byte pieces
+    // 80 bytes apart, each its own partial write request
+    for (uint32_t i0 = 0; i0 < ne; i0 += 32) {
+        // five 16-byte words per record: 0-3 start, end, parents offset / count; 4-7 first op
+        // run, op runs, chain, seq0; 8-10 children offset / count, first parent LV; 11-13 and
+        // 14-16 the first two parents' entry, chain, count; 17 last child, 18 first child
         static_assert(EREC_WORDS == 20, "erec layout");
-        uint4 *r = reinterpret_cast<uint4 *>(erec + size_t(i) * EREC_WORDS);
-        const uint2 e = ent[i];
-        const uint32_t p0 = poff[i], np = poff[i + 1] - p0;
-        const uint32_t c0 = coff[i], nc = coff[i + 1] - c0;
-        const uint32_t o0 = eop[i], o1 = eop[i + 1];
-        const uint2 q = cs[i];
-        const bool h0 = np > 0, h1 = np > 1;
-        PREP_ASSERT(p0 + np <= npar && c0 + nc <= npar && o0 <= o1 && o1 <= nops, PREP_T_ERECP);
-        if (CHECK && oob) continue;
-        r[0] = make_uint4(e.x, e.y, p0, np);
-        r[1] = make_uint4(o0, o1 - o0, q.x, q.y + e.x);
-        r[2] = make_uint4(c0, nc, h0 ? par[p0] : 0xFFFFFFFFu, h0 ? pent[p0] : 0xFFFFFFFFu);
-        r[3] = make_uint4(h0 ? pch[p0] : 0u, h0 ? pcnt[p0] : 0u, h1 ? pent[p0 + 1] : 0xFFFFFFFFu,
-                          h1 ? pch[p0 + 1] : 0u);
-        r[4] = make_uint4(h1 ? pcnt[p0 + 1] : 0u, nc ? child[c0 + nc - 1] : 0xFFFFFFFFu, nc ? child[c0] : 0xFFFFFFFFu, 0u);
+        uint4 *stage = reinterpret_cast<uint4 *>(lfw);
+        const uint32_t i = i0 + l;
+        if (l < 32 && i < ne) {
+            uint4 *r = stage + 5 * l;
+            const uint2 e = ent[i];
+            const uint32_t p0 = poff[i], np = poff[i + 1] - p0;
+            const uint32_t c0 = coff[i], nc = coff[i + 1] - c0;
+            const uint32_t o0 = eop[i], o1 = eop[i + 1];
+            const uint2 q = cs[i];
+            const bool h0 = np > 0, h1 = np > 1;
+            PREP_ASSERT(p0 + np <= npar && c0 + nc <= npar && o0 <= o1 && o1 <= nops, PREP_T_ERECP);
+            if (CHECK && oob) {   // no reads through a bad index (the document fails with PREP_BOUNDS)
+                for (int k = 0; k < 5; k++) r[k] = make_uint4(0, 0, 0, 0);
+            } else {
+            r[0] = make_uint4(e.x, e.y, p0, np);
+            r[1] = make_uint4(o0, o1 - o0, q.x, q.y + e.x);
+            r[2] = make_uint4(c0, nc, h0 ? par[p0] : 0xFFFFFFFFu, h0 ? pent[p0] : 0xFFFFFFFFu);
+            r[3] = make_uint4(h0 ? pch[p0] : 0u, h0 ? pcnt[p0] : 0u, h1 ? pent[p0 + 1] : 0xFFFFFFFFu,
+                              h1 ? pch[p0 + 1] : 0u);
+            r[4] = make_uint4(h1 ? pcnt[p0 + 1] : 0u, nc ? child[c0 + nc - 1] : 0xFFFFFFFFu, nc ? child[c0] : 0xFFFFFFFFu, 0u);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const uint32_t nw = 5 * min(32u, ne - i0);
+        uint4 *dst = reinterpret_cast<uint4 *>(erec + size_t(i0) * EREC_WORDS);
+        for (uint32_t w = l; w < nw; w += 64) dst[w] = stage[w];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
     // op runs: apply commands and the dense chain tables (LV | is_del per chain seq), one op run
     // per lane -- per entry, a history of few long entries (node_nodecc: 91 entries, 53k runs)
@@ -539,8 +558,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
         const uint32_t v = P.d_ver[D.d_ver + t];
         const uint32_t e = entry_of(ent, ne, v);
         if (e >= ne || v < ent[e].x || v >= ent[e].y) tip_miss = true;   // host path: ErrCheckout
-        P.tip[2 * (D.o_tip + t)] = v;
-        P.tip[2 * (D.o_tip + t) + 1] = e;
+        *reinterpret_cast<uint2 *>(P.tip + 2 * (D.o_tip + t)) = make_uint2(v, e);
     }
     if (ballot(tip_miss)) {
         if (l == 0) { R.status = PREP_BAD; P.results[doc] = R; }
@@ -571,8 +589,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
         wave_fence();
         for (uint32_t k = l; k < D.n_aruns; k += 64) {
             const uint4 a = ar[k];   // lv, len, agent, seq
-            uint32_t *q = P.aruns + 4 * (D.o_arun + k);
-            q[0] = a.x; q[1] = owner[a.z]; q[2] = a.w; q[3] = a.z;
+            *reinterpret_cast<uint4 *>(P.aruns + 4 * (D.o_arun + k)) = make_uint4(a.x, owner[a.z], a.w, a.z);
         }
     } else {
         for (uint32_t k = l; k < D.n_aruns; k += 64) {
@@ -590,8 +607,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
                 if (!cmp) cmp = o.y < me.y ? -1 : o.y > me.y ? 1 : 0;
                 rank += cmp < 0 ? 1u : 0u;
             }
-            uint32_t *q = P.aruns + 4 * (D.o_arun + k);
-            q[0] = a.x; q[1] = rank; q[2] = a.w; q[3] = a.z;
+            *reinterpret_cast<uint4 *>(P.aruns + 4 * (D.o_arun + k)) = make_uint4(a.x, rank, a.w, a.z);
         }
     }
     for (int d = 32; d >= 1; d >>= 1) n_ins += uint32_t(__shfl_xor(int(n_ins), d));
@@ -735,7 +751,7 @@ __global__ __launch_bounds__(64) void chain_kernel(PrepParams P) {
 int launch_prep_stage(const PrepParams &p, void *stream, int stage) {
     if (!p.n_docs) return 0;
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    const size_t cw = (size_t(p.max_entries) + 1) / 2, rw = 8 * 64 + 24;
+    const size_t cw = (size_t(p.max_entries) + 1) / 2, rw = 32 * EREC_WORDS;   // >= the ring (8 x 64 + 24)
     const size_t lds = (cw > rw ? cw : rw) * 4;
     PrepParams q = p;
     if (stage == 2) {
@@ -751,7 +767,7 @@ int launch_prep_stage(const PrepParams &p, void *stream, int stage) {
 int launch_prep(const PrepParams &p, void *stream) {
     if (!p.n_docs) return 0;
     // LDS: the child counts (u16 per entry), later the chain decomposition's ring (8 rows + meta)
-    const size_t cw = (size_t(p.max_entries) + 1) / 2, rw = 8 * 64 + 24;
+    const size_t cw = (size_t(p.max_entries) + 1) / 2, rw = 32 * EREC_WORDS;   // >= the ring (8 x 64 + 24)
     const size_t lds = (cw > rw ? cw : rw) * 4;
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     PrepParams q = p;
