@@ -155,3 +155,35 @@ def test_document_past_the_block_limit():
     b = dt_amd.Batch(oplogs=[o])
     res, texts = _texts(b)
     assert res[0]["status"] == 65   # DTGPU_ERR_CAPACITY
+
+
+@pytest.mark.gpu
+def test_large_batch_chain_and_walk_kernels():
+    """A device-staged batch of 300 documents takes the batch paths: prep as three launches with
+    the chain decomposition four documents per wave (chain_kernel), the walk orders four per wave
+    (walk_kernel, CSR mode on its own stream beside prep's second half) and the planner's
+    lane-parallel phase B.  The pool mixes friendsforever (golden, 4 causal chains),
+    pairwise-merge documents of 4-16 agents (9-33 chains: past chain_kernel's 16, prep's second
+    half redoes the decomposition) and 40-agent ones (64-69 chains: 64 plans on the device, the
+    wider ones go through the host-staged retry).  Every text equals the golden / oracle text,
+    with the walk overlapped and serialised."""
+    import os
+    pool = [G.dt_bytes("friendsforever")]
+    pool += [dt_amd.synth_merge_oplog(d, 1200 + 60 * d).encode() for d in range(12)]
+    pool += [dt_amd.synth_merge_oplog(100 + d, 2000, 40).encode() for d in range(4)]
+    want = [G.trace("friendsforever_flat")["endContent"].encode()]
+    want += [OracleOpLog.load_from(x).checkout_tip_bytes() for x in pool[1:]]
+    docs = [pool[i % len(pool)] for i in range(300)]
+    b = dt_amd.Batch(docs=docs, staging="device")
+    for overlap in (True, False):
+        if not overlap:
+            os.environ["DTGPU_NO_WALK_OVERLAP"] = "1"
+        try:
+            b.run()
+            b.sync()
+        finally:
+            os.environ.pop("DTGPU_NO_WALK_OVERLAP", None)
+        res = b.results()
+        assert all(r["status"] == 0 for r in res)
+        bad = [i for i in range(len(docs)) if b.text(i) != want[i % len(pool)]]
+        assert not bad, (overlap, bad[:10])
