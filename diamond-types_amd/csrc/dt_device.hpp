@@ -108,7 +108,7 @@ struct PlanDesc {       // per document; offsets index the concatenated PlanInpu
     uint64_t prow_off;    // parent version vectors (per entry, row_stride words, chains < n_agents)
     uint32_t ne, n_agents, n_aruns, ntip, n_lv, ccap, tcap, skip;
     uint32_t row_stride, pad;
-    uint64_t coff_off, poff_off;   // device staging: children CSR offsets (prep scratch), parent offsets (decoder)
+    uint64_t coff_off, poff_off;   // device staging: per entry children (prep scratch), parent offsets (decoder)
 };
 struct PlanResult {
     uint32_t status, ncmd, ntlist, n_tip;

@@ -1253,10 +1253,9 @@ __global__ __launch_bounds__(64) void walk_kernel(PlanParams Q) {
             ns++;
             // the entry's children (first / last from the record; a longer list from the CSR)
             uint32_t nch, ch0, firstch = 0, lastch = 0;
-            if (CSR) {   // the CSR offsets, then (below) the list itself
-                const uint32_t rv = coff[idx + (c & 1u)];
-                ch0 = wsh(rv, base);
-                nch = wsh(rv, base + 1) - ch0;
+            if (CSR) {   // prep's first half: {children, first slot, first child, last child}
+                const uint32_t rv = coff[4 * size_t(idx) + (c & 3u)];
+                nch = wsh(rv, base); ch0 = wsh(rv, base + 1); firstch = wsh(rv, base + 2); lastch = wsh(rv, base + 3);
             } else {
                 const uint32_t wsel = c == 0 ? R_NCH : c == 1 ? R_CH0 : c == 2 ? R_FIRSTCH : R_LASTCH;
                 const uint32_t rv = erec[size_t(idx) * EREC_WORDS + wsel];
@@ -1265,7 +1264,7 @@ __global__ __launch_bounds__(64) void walk_kernel(PlanParams Q) {
             for (uint32_t cc = 0; cc < nch; cc += WG) {
                 const bool has = cc + c < nch;
                 uint32_t chv = 0;
-                if (has) chv = !CSR && nch <= 2 ? (c == 0 ? firstch : lastch) : child[ch0 + cc + c];
+                if (has) chv = nch <= 2 ? (c == 0 ? firstch : lastch) : child[ch0 + cc + c];
                 bool ready = false;
                 if (has) {
                     const uint8_t pdv = uint8_t(pend[chv] - 1);

@@ -662,7 +662,7 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
         q.erec_off = r.o_erec; q.doff_off = r.o_doff; q.dense_off = r.o_dense;
         q.base_off = base_total;
         q.prow_off = r.o_rows;   // device-staged: the prep kernel's parent vectors
-        q.coff_off = r.o_scr + ((uint64_t(r.n_par) + 1) & ~1ull) + 2ull * r.ne;   // dt_prep.hpp scratch layout
+        q.coff_off = r.o_scr + prep_kids_offset(r.n_par, r.ne);   // walk kernel: children per entry
         q.poff_off = r.d_poff;
         q.row_stride = PREP_MAX_CHAINS;
         q.ne = r.ne; q.n_agents = prr[i].n_chains; q.n_aruns = r.n_aruns; q.ntip = r.n_ver; q.n_lv = r.n_lv;
