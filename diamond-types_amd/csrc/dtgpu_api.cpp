@@ -58,21 +58,19 @@ uint32_t plan_split_setting() {
 }
 // The walk orders four documents per wave (walk_kernel) before the plan kernel, unless
 // DTGPU_PLAN_WALK=0 lets the plan kernel walk each document itself (A/B).
-// Small batches (a walk kernel launch costs a single document more than it saves) walk in the
-// plan kernel.
-uint32_t walk_setting(size_t n_docs) {
+// (Also for a single document: its walk then runs beside prep's second half, single
+// friendsforever pass 12.9 -> 12.0 ms.)
+uint32_t walk_setting(size_t) {
     const char *e = getenv("DTGPU_PLAN_WALK");
-    if (e && *e) return *e == '0' ? 0u : 1u;
-    return n_docs >= 256 ? 1u : 0u;
+    return e && *e == '0' ? 0u : 1u;
 }
 // Prep as three launches with the chain decomposition four documents per wave, unless
 // DTGPU_PREP_CHAINS=0 selects the single launch (A/B).
-// (Small batches keep the single launch: a document's chain walk on a 16-lane group is slower
-// than on a whole wave, and the launch saves nothing when the CU is not shared.)
-uint32_t prep_chains_setting(size_t n_docs) {
+// (Also for small batches: a document's chain walk on a 16-lane group is slower than on a whole
+// wave, but the split lets the planner's walk run beside it.)
+uint32_t prep_chains_setting(size_t) {
     const char *e = getenv("DTGPU_PREP_CHAINS");
-    if (e && *e) return *e == '0' ? 0u : 1u;
-    return n_docs >= 256 ? 1u : 0u;
+    return e && *e == '0' ? 0u : 1u;
 }
 // Per-document replay layout: block capacity, HBM index bytes, LDS tier.
 struct Layout { uint32_t max_blocks; uint64_t gidx; int tier; uint32_t tier_blocks; };
