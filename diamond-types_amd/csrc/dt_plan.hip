@@ -765,7 +765,7 @@ DEV void plan_doc1(P &p, PlanResult *res) {
 //     commands written by its own lane.
 // Same output as plan_doc1 (tested against the host walk).
 constexpr uint32_t kSplitLaneTl = 24, kSplitLaneOps = 8;   // per-lane step writes up to these sizes
-constexpr uint32_t kSplitRegChains = 4;   // up to this many chains: output-parallel chunk writes
+constexpr uint32_t kSplitRegChains = 4;   // up to this many moving chains per step: output-parallel chunk writes
 constexpr uint32_t kSplitSegChunk = 4096;
 constexpr uint32_t kSplitCopyDepth = 8;   // big steps: 8 x 64 dense-table loads per round trip   // ... for chunks writing up to this many entries / commands
 DEV void plan_doc_split(P &p, PlanResult *res) {
@@ -867,12 +867,12 @@ DEV void plan_doc_split(P &p, PlanResult *res) {
         if (valid && p.prow[size_t(e) * rs + min(chain, rs - 1)] != seq0 && !code) code = PLAN_NOT_CHAIN;
         // the frontier before the step (the previous entry folded) against the step's parents
         uint32_t total = 0, nadv = 0;
-        uint32_t sn[kSplitRegChains], ss[kSplitRegChains], sadv = 0;   // A <= 4: the step's ranges
+        // the step's first kSplitRegChains moving chains (ascending): range length, dense source,
+        // advance bit; more moving chains than that send the chunk to the per-step writes
+        uint32_t sn[kSplitRegChains], ss[kSplitRegChains], sadv = 0, nmov = 0;
 #pragma unroll
         for (uint32_t a = 0; a < kSplitRegChains; a++) sn[a] = ss[a] = 0;
-        for (uint32_t a = 0; a < A; a++) {
-            const uint32_t to = valid ? p.prow[size_t(e) * rs + a] : 0;
-            uint32_t from = hp ? p.prow[size_t(ep) * rs + a] : 0;
+        auto chain_diff = [&](uint32_t a, uint32_t to, uint32_t from) {
             if (hp && a == p_chain) from = p_seq0 + (p_end - p_start);
             const bool adv = to > from;
             const uint32_t n = adv ? to - from : from - to;
@@ -880,10 +880,28 @@ DEV void plan_doc_split(P &p, PlanResult *res) {
             if (n && sdoff[a] + s0 + n > sdoff[a + 1] && !code) code = PLAN_ERR_INTERNAL;
             total += n;
             nadv += adv ? n : 0;
+            if (n) {
 #pragma unroll
-            for (uint32_t q = 0; q < kSplitRegChains; q++)
-                if (a == q) { sn[q] = n; ss[q] = sdoff[a] + s0; }
-            if (adv && a < kSplitRegChains) sadv |= 1u << a;
+                for (uint32_t q = 0; q < kSplitRegChains; q++)
+                    if (nmov == q) { sn[q] = n; ss[q] = sdoff[a] + s0; }
+                if (adv && nmov < kSplitRegChains) sadv |= 1u << nmov;
+                nmov++;
+            }
+        };
+        if ((rs & 3u) == 0) {   // rows 16-byte aligned (device staging): four chains per load
+            const uint4 *r4e = reinterpret_cast<const uint4 *>(p.prow + size_t(e) * rs);
+            const uint4 *r4p = reinterpret_cast<const uint4 *>(p.prow + size_t(ep) * rs);
+            for (uint32_t a = 0; a < A; a += 4) {
+                const uint4 t4 = valid ? r4e[a / 4] : make_uint4(0, 0, 0, 0);
+                const uint4 f4 = hp ? r4p[a / 4] : make_uint4(0, 0, 0, 0);
+                chain_diff(a, t4.x, f4.x);
+                if (a + 1 < A) chain_diff(a + 1, t4.y, f4.y);
+                if (a + 2 < A) chain_diff(a + 2, t4.z, f4.z);
+                if (a + 3 < A) chain_diff(a + 3, t4.w, f4.w);
+            }
+        } else {
+            for (uint32_t a = 0; a < A; a++)
+                chain_diff(a, valid ? p.prow[size_t(e) * rs + a] : 0u, hp ? p.prow[size_t(ep) * rs + a] : 0u);
         }
         if (!valid) total = nadv = 0;
         const uint32_t ncmd = valid ? (total ? 1u : 0u) + nop : 0u;
@@ -908,8 +926,8 @@ DEV void plan_doc_split(P &p, PlanResult *res) {
         // steps retreat / advance thousands of entries each): then step by step, each step's
         // ranges copied contiguously by the whole wave
         const bool seg_chunk = sum_t > kSplitSegChunk || sum_c > kSplitSegChunk;
-        const bool outpar = A <= kSplitRegChains && !seg_chunk;
-        const bool big = valid && (A > kSplitRegChains ? (total > kSplitLaneTl || nop > kSplitLaneOps) : seg_chunk);
+        const bool outpar = !__ballot(valid && nmov > kSplitRegChains) && !seg_chunk;
+        const bool big = valid && (!outpar ? (seg_chunk || total > kSplitLaneTl || nop > kSplitLaneOps) : false);
         if (!p.count_only && outpar) {
             // output-parallel: output u of the chunk belongs to the first step whose inclusive
             // prefix exceeds it (a binary search over the lanes), inside it to the chain range
@@ -973,7 +991,7 @@ DEV void plan_doc_split(P &p, PlanResult *res) {
             }
             if (bad) { err_step = i; err_code = PLAN_ERR_INTERNAL; }
         }
-        if (!p.count_only && valid && !big && A > kSplitRegChains) {
+        if (!p.count_only && valid && !big && !outpar) {
             uint32_t cw = co;
             bool bad = false;
             if (total) {
