@@ -781,7 +781,7 @@ class Batch:
         _check(lib().dtgpu_batch_doc_stats(self._h, i, out))
         keys = ["n_items", "n_blocks", "fail_cmd", "fail_site", "n_cmds", "max_blocks",
                 "cyc_ins", "cyc_del", "cyc_tog", "cyc_mat", "cyc_yjs", "cyc_split", "cyc_find", "cyc_bload",
-                "cyc_orr", "cyc_run", "n_hit", "n_runs", "n_relink", "n_yjs", "n_split", "cyc_total",
+                "cyc_orr", "cyc_run", "cyc_r1", "cyc_r2", "cyc_r3", "n_yjs", "n_split", "cyc_total",
                 "n_sb", "lds_index", "cyc_t1", "cyc_t2", "cyc_t3", "n_dirty", "n_load"]
         return dict(zip(keys, list(out)))
 
