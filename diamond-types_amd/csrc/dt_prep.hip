@@ -450,12 +450,31 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
     }
 
     // ---- 4. lane-parallel outputs -----------------------------------------------------------------
-    for (uint32_t k = l; k < npar; k += 64) {   // parent slots: chain and ops of that chain up to it
-        const uint32_t pe = pent[k];
-        PREP_ASSERT(pe < ne, PREP_T_PAIRS);
-        const uint2 q = (!CHECK || pe < ne) ? cs[pe] : make_uint2(0, 0);
-        pch[k] = q.x;
-        pcnt[k] = q.y + par[k] + 1;
+    // parent slots: chain and ops of that chain up to it; four 64-slot rounds per iteration so
+    // their dependent loads (slot -> entry -> chain pair) are in flight together
+    for (uint32_t k0 = 0; k0 < npar; k0 += 256) {
+        uint32_t pe[4], pv[4];
+        uint2 q[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const uint32_t k = k0 + 64 * uint32_t(r) + l;
+            pe[r] = k < npar ? pent[k] : 0u;
+            pv[r] = k < npar ? par[k] : 0u;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const uint32_t k = k0 + 64 * uint32_t(r) + l;
+            PREP_ASSERT(k >= npar || pe[r] < ne, PREP_T_PAIRS);
+            q[r] = k < npar && (!CHECK || pe[r] < ne) ? cs[pe[r]] : make_uint2(0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const uint32_t k = k0 + 64 * uint32_t(r) + l;
+            if (k < npar) {
+                pch[k] = q[r].x;
+                pcnt[k] = q[r].y + pv[r] + 1;
+            }
+        }
     }
     wave_fence();
     // entry records (dt_host.hpp PlanInput::erec), 32 at a time: each lane builds its record in
