@@ -18,8 +18,17 @@ struct DocDesc {
     uint64_t tlist_off;     // into tlist (uint32 units)
     uint32_t ncmd, n_lv, n_aruns, max_blocks, out_cap, content_len;
     uint32_t ascii;         // every inserted char is one byte
+    // Cut replay (a long document replayed as segments on several waves, see dt_replay.hip
+    // "segments"): this replay applies the commands of the LV range [seg_lo, seg_hi) on top of
+    // seg_u placeholder items standing for the text at seg_lo, and writes its visible items as a
+    // source list (src_off, src_cap entries) instead of text.  Plain documents: seg_lo = seg_u =
+    // 0, seg_hi = ~0, src_off = ~0.
+    uint32_t seg_lo, seg_hi, seg_u, src_cap;
+    uint64_t pc_off;        // into pos / ao: lv_off, or a segment's own region (n_lv + seg_u words)
+    uint64_t src_off;       // into src (uint32 units), or ~0
     uint32_t pad;
 };
+constexpr uint32_t SEG_PHANTOM = 0x80000000u;   // source-list entry: placeholder item index
 
 struct DocResult {
     uint32_t status, out_len;
@@ -63,7 +72,24 @@ struct BatchParams {
     unsigned long long *mup;
     uint32_t *tup;
     uint32_t *xf;
+    uint32_t *src;   // cut replay: the segments' source lists (DocDesc::src_off)
 };
+
+// Cut replay: after the replay, one workgroup per cut document resolves its segments' source
+// lists in order (each placeholder to the previous segment's entry) and writes the text.
+struct SegGroup { uint32_t first, count; };   // into seg_docs: the document's segments in LV order
+struct CombineParams {
+    const SegGroup *groups;
+    const uint32_t *seg_docs;
+    uint32_t n_groups;
+    const DocDesc *docs;
+    DocResult *results;
+    uint32_t *src;
+    const uint32_t *cbyte;
+    const uint8_t *content;
+    uint8_t *out;
+};
+int launch_combine(const CombineParams &p, void *stream);
 
 // Superblock capacity for an index of `mb` blocks: every superblock but the first holds >= 32
 // blocks (they split 64 -> 32 + 32).

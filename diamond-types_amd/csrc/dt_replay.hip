@@ -163,7 +163,7 @@ enum ProfSlot { P_INS = 0, P_DEL, P_TOG, P_MAT, P_YJS, P_SPLIT, P_FIND, P_BLOAD,
 struct Doc {
     // inputs
     const Cmd *cmds;
-    uint32_t ncmd, n_lv;
+    uint32_t ncmd, n_lv;   // n_lv: item ids (the LVs, then a segment's placeholders)
     const uint32_t *tlist;
     const DocDesc *desc;   // cold fields (content, agent runs, output) are read from it when used
     // per-LV state (HBM)
@@ -1057,12 +1057,150 @@ DEV void materialise(Doc &D, GLOBAL_AS uint8_t *out, uint32_t cap, uint32_t &len
     items_out = items;
 }
 
+// ---- segments (cut replay) -------------------------------------------------------------------
+// A long document whose causal graph has cut points -- LVs v such that every op below v is in
+// the history of every op at or above v, so the text at v is a plain string that the later ops
+// address only by position (the reference's fast-forward boundary, merge.rs:811-840, taken at
+// any such v instead of only before the first concurrent entry) -- replays as segments on
+// separate waves.  The segment [lo, hi) starts from seg_u placeholder items (ids n_lv + p)
+// standing for the text at lo.  seg_u is an upper bound on that text's length (the host takes
+// inserts - deletes + concurrent deletes below lo: only a concurrent delete can hit an item
+// that is already deleted).  Placeholders past the true length are never addressed by a
+// position (every later op addresses the true text), and an insert at the true end lands in
+// front of them: its origin_right is the first placeholder instead of END, which sorts after
+// every real item in YjsMod's keys as END does.  A placeholder is always live, so it is never
+// a YjsMod candidate; only its document-order key and pc[] word are read.  launch_combine
+// resolves the segments' source lists into the text.
+
+// LV of the first apply command at or after i (NONE past the last one).
+DEV uint32_t first_apply_lv(const Cmd *cmds, uint32_t ncmd, uint32_t i) {
+    for (; i < ncmd; i++) {
+        const Cmd c = cmds[i];
+        if ((c.op & 15u) != CMD_TOG) return c.lv;
+    }
+    return NONE;
+}
+// First command of the segment that starts at LV v: the walk visits ancestors first, so every
+// command of an entry below the cut precedes every command of an entry above it, and "the first
+// apply command at or after i has lv >= v" is monotone in i (64-ary search).
+DEV uint32_t seg_cmd(const Cmd *cmds, uint32_t ncmd, uint32_t v) {
+    const uint32_t l = lane_id();
+    uint32_t lo = 0, hi = ncmd;   // answer in [lo, hi]
+    while (lo < hi) {
+        const uint32_t step = max(1u, (hi - lo + 63) / 64), b = lo;
+        const uint32_t i = b + l * step;
+        const bool in = i < hi;
+        const u64 m = __ballot(in && first_apply_lv(cmds, ncmd, i) >= v);
+        if (m) {
+            const uint32_t f = first_lane(m);
+            hi = b + f * step;
+            lo = f ? b + (f - 1) * step + 1 : b;
+        } else {
+            lo = b + last_lane(__ballot(in)) * step + 1;
+        }
+        lo = U(lo);
+        hi = U(hi);
+    }
+    return lo;
+}
+// True when the last apply command before c runs past LV v (the cut is not a command boundary).
+DEV bool seg_straddles(const Cmd *cmds, uint32_t c, uint32_t v) {
+    if (v == NONE || c == 0) return false;
+    bool bad = false;
+    if (lane_id() == 0) {
+        for (uint32_t j = c; j-- > 0;) {
+            const Cmd x = cmds[j];
+            if ((x.op & 15u) != CMD_TOG) { bad = x.lv + x.len > v; break; }
+        }
+    }
+    return __ballot(bad) != 0;
+}
+constexpr uint32_t PH_FILL = 48;   // placeholder items per block (the HBM tier keeps >= 32)
+constexpr uint32_t PH_SB = 40;     // placeholder blocks per superblock
+// The tracker a segment starts from: u visible placeholder items in document order.
+template <bool L>
+DEV bool init_phantoms(Doc &D, uint32_t u) {
+    const uint32_t l = lane_id();
+    const uint32_t base = U(vld(&D.desc->n_lv));   // placeholder ids follow the LVs
+    const uint32_t nbp = (u + PH_FILL - 1) / PH_FILL, nsb = (nbp + PH_SB - 1) / PH_SB;
+    if (nbp + 1 > D.max_blocks || nsb + 1 > D.max_sb) { fail(D, ErrCapacity, 12); return false; }
+    for (uint32_t b = l; b < nbp; b += 64) {
+        const uint32_t k = min(PH_FILL, u - b * PH_FILL);
+        const uint32_t S = b / PH_SB, i = b % PH_SB;
+        D.cnt[b] = k * (C_VIS + C_LIVE + C_ITEMS);
+        set_opos<L>(D, b, (S << 6) | i);
+        D.sbl[size_t(S) * SBC + i] = uint16_t(b);
+        st(D.m2 + 2 * size_t(b), lanes_below(k));
+        st(D.m2 + 2 * size_t(b) + 1, lanes_below(k));
+    }
+    for (uint32_t S = l; S < nsb; S += 64) {
+        const uint32_t nb = min(PH_SB, nbp - S * PH_SB);
+        const uint32_t nv = min(nb * PH_FILL, u - S * PH_SB * PH_FILL);
+        D.sbn[S] = nb;
+        D.sbpos[S] = S;
+        D.top[S] = (S << 16) | nv;
+        D.tlive[S] = nv;
+    }
+    for (uint32_t b = 0; b < nbp; b++) {   // rows: one wave store per block
+        const uint32_t k = min(PH_FILL, u - b * PH_FILL);
+        D.items[size_t(b) * BLK + l] = l < k ? base + b * PH_FILL + l : 0u;
+    }
+    for (uint32_t p = l; p < u; p += 64) st(D.pc + base + p, pc_of(p / PH_FILL, 1u));
+    wave_fence();
+    D.nb = nbp;
+    D.nsb = nsb;
+    return true;
+}
+// A segment's visible items in document order as a source list (an LV, or SEG_PHANTOM | the
+// placeholder's index), gathered G blocks per round as materialise() does.
+template <bool L>
+DEV void materialise_src(Doc &D, GLOBAL_AS uint32_t *src, uint32_t cap, uint32_t &len_out, uint32_t &items_out) {
+    constexpr uint32_t G = 8;
+    const uint32_t l = lane_id();
+    const uint32_t n_lv = U(vld(&D.desc->n_lv));   // D.n_lv also counts the placeholders
+    uint32_t total = 0, items = 0;
+    for (uint32_t p = 0; p < D.nsb; p++) {
+        const uint32_t S = U(ix<L>(D.top + p)) >> 16;
+        const uint32_t n = U(ix<L>(D.sbn + S));
+        for (uint32_t i = 0; i < n; i += G) {
+            const bool gl = l < G && i + l < n;
+            const uint32_t b0 = ix16<L>(D.sbl + size_t(S) * SBC + min(i + (l & (G - 1)), SBC - 1));
+            const uint32_t bl = gl ? b0 : 0;
+            const uint32_t n0 = c_items(ix<L>(D.cnt + bl));
+            const uint32_t nl = gl ? n0 : 0;
+            items += wave_sum(nl);
+            uint32_t it[G];
+            bool vis[G];
+#pragma unroll
+            for (uint32_t g = 0; g < G; g++) {
+                const uint32_t b = bcast(bl, g);
+                vis[g] = l < bcast(nl, g);
+                const uint32_t i0 = D.items[size_t(b) * BLK + l];
+                it[g] = vis[g] ? i0 : 0;
+            }
+#pragma unroll
+            for (uint32_t g = 0; g < G; g++) vis[g] = vis[g] && pc_cnt(ld(D.pc + it[g])) == 1u;
+#pragma unroll
+            for (uint32_t g = 0; g < G; g++) {
+                const uint32_t c = vis[g] ? 1u : 0u;
+                const uint32_t inc = wave_scan(c);
+                const uint32_t at = total + inc - c;
+                if (c && at < cap) src[at] = it[g] < n_lv ? it[g] : (SEG_PHANTOM | (it[g] - n_lv));
+                total += bcast(inc, 63);
+            }
+        }
+    }
+    len_out = total;
+    items_out = items;
+}
+
 // Debug-mode consistency check of the whole structure (DTGPU_DEBUG=1): returns 0 or a code.
 // Checks every block's counts against its masks (clean blocks) or against cv[] (DIRTY blocks),
 // and that pos[] names each item's block.
 template <bool L, bool XF>
 DEV uint32_t check_invariants(Doc &D, DocResult *res) {
     const uint32_t l = lane_id();
+    const uint32_t n_ids = D.n_lv;   // LVs, then a segment's placeholders
     uint32_t blocks = 0;
     for (uint32_t p = 0; p < D.nsb; p++) {
         const uint32_t S = U(ix<L>(D.top + p)) >> 16;
@@ -1079,7 +1217,7 @@ DEV uint32_t check_invariants(Doc &D, DocResult *res) {
             u64 mv = U64(ld(D.m2 + 2 * size_t(b))), ml = U64(ld(D.m2 + 2 * size_t(b) + 1));
             if (dirty) {   // stale masks: check the counts against cv[] instead
                 const uint32_t i2 = l < cnt ? D.items[size_t(b) * BLK + l] : 0;
-                const uint32_t k = l < cnt && i2 < D.n_lv ? pc_cnt(ld(D.pc + i2)) : 0u;
+                const uint32_t k = l < cnt && i2 < n_ids ? pc_cnt(ld(D.pc + i2)) : 0u;
                 mv = __ballot(l < cnt && k == 1u);
                 ml = __ballot(l < cnt && k != 0u);
             }
@@ -1092,7 +1230,7 @@ DEV uint32_t check_invariants(Doc &D, DocResult *res) {
             uint32_t w = 0, it = 0xFFFFFFFFu;
             if (l < cnt) {
                 it = D.items[size_t(b) * BLK + l];
-                if (it >= D.n_lv) bad = true;
+                if (it >= n_ids) bad = true;
                 else {
                     w = pc_blk(ld(D.pc + it));
                     const uint32_t k = pc_cnt(ld(D.pc + it));
@@ -1123,21 +1261,34 @@ DEV uint32_t check_invariants(Doc &D, DocResult *res) {
 template <bool L, bool PROF, bool XF>
 DEV void run_doc(Doc &D) {
     const uint32_t l = lane_id();
-    // fresh tracker: one empty block in one superblock (per-LV words are written when their
-    // item is inserted)
-    if (l == 0) {
-        D.cnt[0] = 0; set_opos<L>(D, 0, 0);
-        D.sbl[0] = 0; D.sbn[0] = 1; D.sbpos[0] = 0; D.top[0] = 0; D.tlive[0] = 0;
-        if (XF) { D.tup[0] = 0; st(D.mup, 0ull); }
-    }
-    if (l < 2) st(D.m2 + l, 0ull);
-    wave_fence();
     D.nb = 1;
     D.nsb = 1;
     D.err = 0;
     D.steps = 0;
-    D.step_limit = uint32_t(min<uint64_t>(64ull * (uint64_t(D.ncmd) + D.n_lv) + 4096, 0xFFFFFFF0ull));
     D.site = 0;
+    // a segment (cut replay) applies its LV range's commands only
+    const uint32_t seg_lo = U(vld(&D.desc->seg_lo)), seg_hi = U(vld(&D.desc->seg_hi));
+    if (!XF && (seg_lo != 0 || seg_hi != NONE)) {
+        const uint32_t c0 = seg_lo ? U(seg_cmd(D.cmds, D.ncmd, seg_lo)) : 0u;
+        const uint32_t c1 = seg_hi != NONE ? U(seg_cmd(D.cmds, D.ncmd, seg_hi)) : D.ncmd;
+        if (c1 < c0 || seg_straddles(D.cmds, c0, seg_lo) || seg_straddles(D.cmds, c1, seg_hi)) fail(D, ErrCheckout, 30);
+        else { D.cmds += c0; D.ncmd = c1 - c0; }
+    }
+    D.step_limit = uint32_t(min<uint64_t>(64ull * (uint64_t(D.ncmd) + D.n_lv) + 4096, 0xFFFFFFF0ull));
+    const uint32_t seg_u = XF ? 0u : U(vld(&D.desc->seg_u));
+    if (seg_u) {
+        if (!D.err) init_phantoms<L>(D, seg_u);
+    } else {
+        // fresh tracker: one empty block in one superblock (per-LV words are written when their
+        // item is inserted)
+        if (l == 0) {
+            D.cnt[0] = 0; set_opos<L>(D, 0, 0);
+            D.sbl[0] = 0; D.sbn[0] = 1; D.sbpos[0] = 0; D.top[0] = 0; D.tlive[0] = 0;
+            if (XF) { D.tup[0] = 0; st(D.mup, 0ull); }
+        }
+        if (l < 2) st(D.m2 + l, 0ull);
+        wave_fence();
+    }
     D.cb = NONE;
     D.cit = 0;
     D.cmv = D.cml = 0;
@@ -1223,8 +1374,13 @@ DEV void run_doc(Doc &D) {
     u64 h = 0;
     const uint64_t t_mat = tick<PROF>();
     if (!D.err) {
-        GLOBAL_AS uint8_t *out = gp(vld(&KP().out)) + vld(&D.desc->out_off);
-        materialise<L>(D, out, U(vld(&D.desc->out_cap)), len, h, n_items);
+        const uint64_t so = vld(&D.desc->src_off);
+        if (!XF && so != ~0ull) {   // a segment: its source list, resolved by launch_combine
+            materialise_src<L>(D, gp(vld(&KP().src)) + so, U(vld(&D.desc->src_cap)), len, n_items);
+        } else {
+            GLOBAL_AS uint8_t *out = gp(vld(&KP().out)) + vld(&D.desc->out_off);
+            materialise<L>(D, out, U(vld(&D.desc->out_cap)), len, h, n_items);
+        }
     }
     GLOBAL_AS DocResult *res = gp(vld(&KP().results)) + D.doc;
     if (l == 0) {
@@ -1287,10 +1443,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_REPLAY
     D.debug = P.debug & 1u;
     D.cmds = P.cmds + dd.cmd_off;
     D.ncmd = U(dd.ncmd);
-    D.n_lv = U(dd.n_lv);
+    // item ids: the LVs, then a segment's placeholders (cut replay)
+    D.n_lv = U(dd.n_lv) + (XF ? 0u : U(dd.seg_u));
     D.tlist = P.tlist + dd.tlist_off;
-    D.pc = P.pos + dd.lv_off;
-    D.ao = P.ao + dd.lv_off;
+    D.pc = P.pos + dd.pc_off;   // lv_off, or a segment's own region
+    D.ao = P.ao + dd.pc_off;
     D.items = P.items + dd.blk_off * BLK;
     D.m2 = P.m2 + 2 * dd.blk_off;
     D.max_blocks = U(dd.max_blocks);
@@ -1308,6 +1465,101 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_REPLAY
         D.xf = P.xf + dd.lv_off;
     }
     run_doc<LDS_INDEX, PROF, XF>(D);
+}
+
+
+// Cut replay: one workgroup per cut document resolves its segments' source lists in LV order --
+// a placeholder of segment k is entry p of segment k-1's resolved list; segment k's entries
+// from the first placeholder past that list's length on are the surplus placeholders (a
+// suffix, checked) -- and writes the text with materialise()'s bytes and hash.  The document's
+// own result slot (its first segment) gets the length and hash, or the first failing
+// segment's status.
+constexpr uint32_t COMBINE_THREADS = 1024;
+__global__ __launch_bounds__(COMBINE_THREADS) void combine_kernel(CombineParams P) {
+    __shared__ uint32_t s_cut, s_bad, s_wsum[COMBINE_THREADS / 64];
+    __shared__ u64 s_h[COMBINE_THREADS / 64];
+    const SegGroup g = P.groups[blockIdx.x];
+    const uint32_t t = threadIdx.x, w = t / 64, nw = COMBINE_THREADS / 64;
+    const uint32_t d0 = P.seg_docs[g.first];
+    DocResult *res0 = P.results + d0;
+    uint32_t status = 0, site = 0, fcmd = 0;
+    for (uint32_t k = 0; k < g.count && !status; k++) {
+        const DocResult &r = P.results[P.seg_docs[g.first + k]];
+        status = r.status; site = r.fail_site; fcmd = r.fail_cmd;
+    }
+    if (status) {
+        __syncthreads();
+        if (t == 0) { res0->status = status; res0->fail_site = site; res0->fail_cmd = fcmd; res0->out_len = 0; res0->hash = 0; }
+        return;
+    }
+    const uint32_t *R = P.src + P.docs[d0].src_off;
+    uint32_t nR = P.results[d0].out_len;
+    if (t == 0) s_bad = 0;
+    for (uint32_t k = 1; k < g.count; k++) {
+        const uint32_t dk = P.seg_docs[g.first + k];
+        uint32_t *S = P.src + P.docs[dk].src_off;
+        const uint32_t nS = P.results[dk].out_len;
+        if (t == 0) {   // "a surplus placeholder" is monotone along the list: binary search
+            uint32_t lo = 0, hi = nS;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) / 2, e = S[mid];
+                if ((e & SEG_PHANTOM) && (e & ~SEG_PHANTOM) >= nR) hi = mid;
+                else lo = mid + 1;
+            }
+            s_cut = lo;
+            // surplus placeholders are the last ones, in order: the suffix is exactly them
+            if (lo < nS && S[nS - 1] != (SEG_PHANTOM | (S[lo] & ~SEG_PHANTOM) + (nS - 1 - lo))) s_bad = 1;
+        }
+        __syncthreads();
+        const uint32_t cut = s_cut;
+        for (uint32_t i = t; i < cut; i += COMBINE_THREADS) {
+            const uint32_t e = S[i];
+            if (e & SEG_PHANTOM) S[i] = R[e & ~SEG_PHANTOM];
+        }
+        __syncthreads();
+        R = S;
+        nR = cut;
+    }
+    const DocDesc &dd = P.docs[d0];
+    const uint32_t *cbyte = P.cbyte + dd.lv_off;
+    const uint8_t *content = P.content + dd.content_off;
+    uint8_t *out = P.out + dd.out_off;
+    const uint32_t cap = dd.out_cap, n_lv = dd.n_lv, clen = dd.content_len;
+    const bool ascii = dd.ascii != 0;
+    u64 h = 0;
+    uint32_t base = 0;
+    for (uint32_t i0 = 0; i0 < nR; i0 += COMBINE_THREADS) {
+        const uint32_t i = i0 + t;
+        uint32_t cb = 0, len = 0;
+        if (i < nR) {
+            const uint32_t e = R[i];
+            const uint32_t c = e < n_lv ? cbyte[e] : NONE;
+            if (c < clen) { cb = c; len = ascii ? 1u : utf8_len(content[c]); }
+            else s_bad = 1;
+        }
+        const uint32_t inc = wave_scan(len);
+        if ((t & 63) == 63) s_wsum[w] = inc;
+        __syncthreads();
+        uint32_t before = 0, round = 0;
+        for (uint32_t j = 0; j < nw; j++) { const uint32_t x = s_wsum[j]; if (j < w) before += x; round += x; }
+        const uint32_t at = base + before + inc - len;
+        for (uint32_t k = 0; k < len; k++) {
+            const uint8_t by = content[cb + k];
+            if (at + k < cap) out[at + k] = by;
+            h += splitmix((u64(at + k) << 8) | by);
+        }
+        base += round;
+        __syncthreads();   // s_wsum reused next round
+    }
+    h = wave_sum64(h);
+    if ((t & 63) == 0) s_h[w] = h;
+    __syncthreads();
+    if (t == 0) {
+        u64 H = 0;
+        for (uint32_t j = 0; j < nw; j++) H += s_h[j];
+        if (s_bad) { res0->status = ErrCheckout; res0->fail_site = 31; res0->out_len = 0; res0->hash = 0; }
+        else { res0->out_len = base; res0->hash = H; }
+    }
 }
 
 }  // namespace dev
@@ -1393,6 +1645,13 @@ int launch_replay_xf(const BatchParams &large, void *stream) {
     if (!large.n_list) return OK;
     if (!large.xf || !large.mup || !large.tup) return ErrArg;
     hipLaunchKernelGGL((dev::replay_kernel<false, false, true>), dim3(large.n_list), dim3(64), 0, s, large);
+    return hipGetLastError() == hipSuccess ? OK : ErrHip;
+}
+
+int launch_combine(const CombineParams &p, void *stream) {
+    if (!p.n_groups) return OK;
+    hipLaunchKernelGGL(dev::combine_kernel, dim3(p.n_groups), dim3(dev::COMBINE_THREADS), 0,
+                       reinterpret_cast<hipStream_t>(stream), p);
     return hipGetLastError() == hipSuccess ? OK : ErrHip;
 }
 

@@ -4,12 +4,14 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <queue>
+#include <set>
 #include <thread>
 #include <tuple>
 #include <vector>
@@ -84,6 +86,104 @@ Layout replay_layout(uint64_t n_ins, uint64_t lds_fill, bool hbm_only) {
     return L;
 }
 
+// ---- cut replay (dt_replay.hip "segments") ------------------------------------------------------
+// A long document replays as segments on several waves, cut at LVs v where the prefix [0, v)
+// is one version ({v-1}) and every later entry has it in its history: the reference fast-forwards
+// exactly there (merge.rs:811-840) because the text at v is then a plain string.  Cuts go at op
+// run starts (every command boundary is one), spread so that the segments hold about equal op
+// runs.  A segment's placeholders bound the text at its start: inserts - deletes + the deletes
+// that are concurrent with some other op (a delete can hit an already deleted item only then).
+struct SegCut { uint32_t lo, hi, u; uint64_t ins; };   // LV range, placeholders, inserted chars in range
+struct SegInput {
+    uint64_t n_lv = 0;
+    std::vector<std::pair<uint64_t, uint64_t>> ent;   // entries [start, end) in LV order
+    std::vector<uint32_t> poff;                       // parents CSR (ent.size() + 1)
+    std::vector<uint64_t> par;
+    std::vector<std::array<uint64_t, 3>> ops;         // op runs (lv, len, kind: 0 ins, 1 del) in LV order
+};
+struct SegSettings { bool on; uint64_t ops_per_seg; uint32_t max_seg; };
+SegSettings seg_settings() {
+    SegSettings s{true, 3000, 16};
+    if (const char *e = getenv("DTGPU_SEG")) s.on = *e != '0';
+    if (const char *e = getenv("DTGPU_SEG_OPS")) s.ops_per_seg = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
+    if (const char *e = getenv("DTGPU_SEG_MAX")) s.max_seg = uint32_t(std::max<uint64_t>(1, strtoull(e, nullptr, 10)));
+    return s;
+}
+std::vector<SegCut> plan_segments(const SegInput &in, const SegSettings &cfg) {
+    std::vector<SegCut> out;
+    const size_t ne = in.ent.size(), nop = in.ops.size();
+    const uint32_t S = uint32_t(std::min<uint64_t>(cfg.max_seg, nop / cfg.ops_per_seg));
+    if (S < 2 || ne == 0 || in.n_lv >= 0x7FFFFFFFull) return out;
+    // cut ranges [a, b]: every v in them is a cut
+    std::vector<int64_t> sufmin(ne + 1, INT64_MAX);
+    for (size_t k = ne; k-- > 0;) {
+        int64_t mp = -1;   // ROOT
+        if (in.poff[k + 1] > in.poff[k]) {
+            mp = INT64_MAX;
+            for (uint32_t j = in.poff[k]; j < in.poff[k + 1]; j++) mp = std::min<int64_t>(mp, int64_t(in.par[j]));
+        }
+        sufmin[k] = std::min(sufmin[k + 1], mp);
+    }
+    std::vector<std::pair<uint64_t, uint64_t>> cuts;
+    std::set<uint64_t> F;   // frontier of the prefix
+    for (size_t k = 0; k < ne; k++) {
+        const uint64_t s = in.ent[k].first, t = in.ent[k].second;
+        for (uint32_t j = in.poff[k]; j < in.poff[k + 1]; j++) F.erase(in.par[j]);
+        if (F.empty()) {
+            const int64_t lim = sufmin[k + 1] == INT64_MAX ? int64_t(t) : std::min<int64_t>(int64_t(t), sufmin[k + 1] + 1);
+            if (lim >= int64_t(s) + 1) cuts.push_back({s + 1, uint64_t(lim)});
+        }
+        F.insert(t - 1);
+    }
+    if (cuts.empty()) return out;
+    auto in_cut = [&](uint64_t v) {
+        auto it = std::upper_bound(cuts.begin(), cuts.end(), std::make_pair(v, UINT64_MAX));
+        return it != cuts.begin() && v <= std::prev(it)->second;
+    };
+    auto linear = [&](uint64_t lv, uint64_t len) {   // every op in [lv, lv+len) is concurrent with nothing
+        auto it = std::upper_bound(cuts.begin(), cuts.end(), std::make_pair(lv, UINT64_MAX));
+        return it != cuts.begin() && lv + len <= std::prev(it)->second;
+    };
+    // op-run starts that are cuts, nearest to the equal-op targets
+    std::vector<size_t> pick;
+    for (uint32_t k = 1; k < S; k++) {
+        const size_t target = size_t(uint64_t(k) * nop / S);
+        size_t best = SIZE_MAX;
+        for (size_t d = 0; d < nop && best == SIZE_MAX; d++) {
+            for (size_t j : {target - std::min(target, d), target + d}) {
+                if (j > 0 && j < nop && in_cut(in.ops[j][0])) { best = j; break; }
+            }
+            if (d > nop / (2 * S)) break;   // no cut near this target
+        }
+        if (best != SIZE_MAX && (pick.empty() || best > pick.back() + cfg.ops_per_seg / 4)) pick.push_back(best);
+    }
+    while (!pick.empty() && nop - pick.back() < cfg.ops_per_seg / 4) pick.pop_back();
+    if (pick.empty()) return out;
+    // prefix counts at the picked op runs
+    int64_t ins = 0, del = 0, dconc = 0;
+    size_t pi = 0;
+    std::vector<std::array<int64_t, 3>> at(pick.size());
+    uint64_t seg_ins = 0;
+    std::vector<uint64_t> seg_ins_v;
+    for (size_t j = 0; j <= nop; j++) {
+        if (pi < pick.size() && j == pick[pi]) { at[pi++] = {ins, del, dconc}; seg_ins_v.push_back(seg_ins); seg_ins = 0; }
+        if (j == nop) break;
+        const auto &o = in.ops[j];
+        if (o[2] == 0) { ins += int64_t(o[1]); seg_ins += o[1]; }
+        else { del += int64_t(o[1]); if (!linear(o[0], o[1])) dconc += int64_t(o[1]); }
+    }
+    seg_ins_v.push_back(seg_ins);
+    for (size_t k = 0; k <= pick.size(); k++) {
+        SegCut c{};
+        c.lo = k ? uint32_t(in.ops[pick[k - 1]][0]) : 0u;
+        c.hi = k < pick.size() ? uint32_t(in.ops[pick[k]][0]) : 0xFFFFFFFFu;
+        c.u = k ? uint32_t(std::max<int64_t>(0, std::min(at[k - 1][0], at[k - 1][0] - at[k - 1][1] + at[k - 1][2]))) : 0u;
+        c.ins = seg_ins_v[k];
+        out.push_back(c);
+    }
+    return out;
+}
+
 }  // namespace
 
 struct dtgpu_batch {
@@ -133,6 +233,16 @@ struct dtgpu_batch {
     DevBuf<DocDesc> d_docs;
     DevBuf<DocResult> d_results;
     BatchParams tier[kLdsTiers]{}, large{};
+    // cut replay: segment documents (docs[n..]: a long document's later LV ranges, replayed
+    // beside its first one) and the combine step that joins their source lists into its text
+    std::vector<uint64_t> seg_cost;
+    std::vector<SegGroup> seg_groups;
+    std::vector<uint32_t> seg_docs;
+    DevBuf<SegGroup> d_groups;
+    DevBuf<uint32_t> d_segdocs, d_src;
+    CombineParams comb{};
+    hipEvent_t ev_splan = nullptr;   // split pass: the big tier's plans are done (segments may
+                                     // replay in another tier, on the main stream)
 
     // device-staged batches (dtgpu_batch_create_device): the decoded oplogs stay in the
     // decoder's arenas (content and per-LV offsets are read there by the replay) and the
@@ -143,7 +253,10 @@ struct dtgpu_batch {
     DevBuf<PrepResult> pr_res;
     PrepParams prep{};
     hipEvent_t ev_dec = nullptr, ev_prep = nullptr;
-    hipStream_t wstream = nullptr;               // the planner's walk beside prep's second half
+    // the planner's walk beside prep's second half: a side stream (idle until the replay), since
+    // a process gets GPU_MAX_HW_QUEUES = 4 hardware queues and a fifth stream would share one --
+    // serialising two replay tiers that should run side by side
+    hipStream_t wstream = nullptr;
     hipEvent_t ev_w0 = nullptr, ev_w1 = nullptr;
     float last_decode_ms = 0, last_prep_ms = 0;
 
@@ -157,9 +270,9 @@ struct dtgpu_batch {
     EncParams enc{};
 
     ~dtgpu_batch() {
+        if (ev_splan) (void)hipEventDestroy(ev_splan);
         if (ev_w0) (void)hipEventDestroy(ev_w0);
         if (ev_w1) (void)hipEventDestroy(ev_w1);
-        if (wstream) (void)hipStreamDestroy(wstream);
         if (ev_dec) (void)hipEventDestroy(ev_dec);
         if (ev_prep) (void)hipEventDestroy(ev_prep);
         if (ev0) (void)hipEventDestroy(ev0);
@@ -226,7 +339,8 @@ size_t n_lds_docs(const dtgpu_batch &B) {
 std::vector<uint32_t> tier_lists(dtgpu_batch &B) {
     std::vector<uint32_t> all;
     auto by_cost = [&](std::vector<uint32_t> &v) {
-        std::stable_sort(v.begin(), v.end(), [&](uint32_t a, uint32_t b) { return B.n_lv[a] > B.n_lv[b]; });
+        auto cost = [&](uint32_t d) { return d < B.n ? B.n_lv[d] : B.seg_cost[d - B.n]; };
+        std::stable_sort(v.begin(), v.end(), [&](uint32_t a, uint32_t b) { return cost(a) > cost(b); });
         append(all, v);
     };
     for (int t = 0; t < kLdsTiers; t++) by_cost(B.tier_list[t]);
@@ -256,6 +370,7 @@ dtgpu_status set_tier_params(dtgpu_batch &B, const BatchParams &base) {
     }
     B.debug = base.debug;
     if (!B.ev_fork && hipEventCreateWithFlags(&B.ev_fork, hipEventDisableTiming) != hipSuccess) return DTGPU_ERR_HIP;
+    if (!B.ev_splan && hipEventCreateWithFlags(&B.ev_splan, hipEventDisableTiming) != hipSuccess) return DTGPU_ERR_HIP;
     for (int k = 0; k < kSideStreams; k++) {
         if (!B.side[k] && hipStreamCreateWithFlags(&B.side[k], hipStreamNonBlocking) != hipSuccess) return DTGPU_ERR_HIP;
         if (!B.ev_join[k] && hipEventCreateWithFlags(&B.ev_join[k], hipEventDisableTiming) != hipSuccess) return DTGPU_ERR_HIP;
@@ -277,7 +392,127 @@ int replay_all(dtgpu_batch *B, hipStream_t s, int skip_tier = -1) {
     r.stream = s;
     for (int k = 0; k < kSideStreams; k++) { r.side[k] = B->side[k]; r.ev_join[k] = B->ev_join[k]; }
     r.ev_fork = B->ev_fork;
-    return launch_replay(r);
+    // split pass: a segment of a big-tier document may sit in a tier replayed from s
+    if (skip_tier >= 0 && !B->seg_groups.empty() && hipStreamWaitEvent(s, B->ev_splan, 0) != hipSuccess) return ErrHip;
+    const int e = launch_replay(r);
+    return e ? e : launch_combine(B->comb, s);   // cut documents: their segments' texts joined
+}
+
+// Cut replay inputs from a host oplog / from the decoder's device arrays (one long document).
+void seg_input_from_log(const HostOpLog &o, SegInput &si) {
+    si.n_lv = o.n_lv;
+    si.poff.push_back(0);
+    for (const GraphEntry &g : o.graph.entries) {
+        si.ent.push_back({g.start, g.end});
+        for (uint64_t p : g.parents) si.par.push_back(p);
+        si.poff.push_back(uint32_t(si.par.size()));
+    }
+    for (const OpRun &r : o.ops) si.ops.push_back({r.lv, r.len, uint64_t(r.kind)});
+}
+bool seg_input_from_device(const dtgpu_decoded &Dd, size_t i, SegInput &si, hipStream_t s) {
+    const DecodeResult &r = Dd.res[i];
+    const DecodeDesc &d = Dd.desc[i];
+    std::vector<uint32_t> ent(2 * size_t(r.n_entries)), poff(size_t(r.n_entries) + 1), par(r.n_parents), ops(4 * size_t(r.n_ops));
+    if ((!ent.empty() && hipMemcpyAsync(ent.data(), Dd.ent.p + 2 * d.ent_off, ent.size() * 4, hipMemcpyDeviceToHost, s) != hipSuccess) ||
+        hipMemcpyAsync(poff.data(), Dd.poff.p + d.poff_off, poff.size() * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        (!par.empty() && hipMemcpyAsync(par.data(), Dd.par.p + d.par_off, par.size() * 4, hipMemcpyDeviceToHost, s) != hipSuccess) ||
+        (!ops.empty() && hipMemcpyAsync(ops.data(), Dd.ops.p + 4 * d.op_off, ops.size() * 4, hipMemcpyDeviceToHost, s) != hipSuccess) ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return false;
+    si.n_lv = r.n_lv;
+    for (size_t k = 0; k < r.n_entries; k++) si.ent.push_back({ent[2 * k], ent[2 * k + 1]});
+    si.poff = poff;
+    si.par.assign(par.begin(), par.end());
+    for (size_t k = 0; k < r.n_ops; k++) si.ops.push_back({ops[4 * k], ops[4 * k + 1], uint64_t(ops[4 * k + 3] & 1u)});
+    return true;
+}
+// Add document i's later segments (cuts[1..]) as documents of its replay tier (or the HBM
+// tier) and make document i the first segment.  pc_total / blk_total / gidx_total / src_total
+// are the arenas' running sizes.
+bool add_segments(dtgpu_batch &B, uint32_t i, const std::vector<SegCut> &cuts, int tier, uint32_t,
+                  uint64_t lds_fill, uint64_t &pc_total, uint64_t &blk_total, uint64_t &gidx_total, uint64_t &src_total) {
+    std::vector<uint32_t> mb(cuts.size(), 0);
+    for (size_t k = 1; k < cuts.size(); k++) {   // placeholders 48 per block, then the inserts
+        const uint64_t m = (uint64_t(cuts[k].u) + 47) / 48 + cuts[k].ins / 32 + 3;
+        if (m > std::min<uint64_t>(LOC_MAX_BLOCKS, MAX_DOC_BLOCKS)) return false;
+        mb[k] = uint32_t(m);
+    }
+    const SegGroup g{uint32_t(B.seg_docs.size()), uint32_t(cuts.size())};
+    {
+        DocDesc &d0 = B.docs[i];
+        d0.seg_hi = cuts[0].hi;
+        d0.src_off = src_total;
+        d0.src_cap = uint32_t(cuts[0].ins);
+        src_total += cuts[0].ins;
+    }
+    B.seg_docs.push_back(i);
+    const uint64_t n_lv = B.docs[i].n_lv;
+    for (size_t k = 1; k < cuts.size(); k++) {
+        DocDesc e = B.docs[i];
+        e.seg_lo = cuts[k].lo;
+        e.seg_hi = cuts[k].hi;
+        e.seg_u = cuts[k].u;
+        e.pc_off = pc_total;
+        pc_total += n_lv + cuts[k].u;
+        e.max_blocks = mb[k];
+        e.blk_off = blk_total;
+        blk_total += mb[k];
+        e.gidx_off = gidx_total;
+        gidx_total += index_bytes(mb[k]);
+        e.src_off = src_total;
+        e.src_cap = uint32_t(cuts[k].u + cuts[k].ins);
+        src_total += e.src_cap;
+        const uint32_t idx = uint32_t(B.docs.size());
+        B.docs.push_back(e);
+        B.seg_cost.push_back(cuts[k].hi == 0xFFFFFFFFu ? n_lv - cuts[k].lo : cuts[k].hi - cuts[k].lo);
+        B.seg_docs.push_back(idx);
+        // its own replay tier, sized for its placeholders and inserts (a split pass's main
+        // stream waits for the big tier's plans before replaying: see replay_all)
+        const Layout lay = replay_layout(cuts[k].u + cuts[k].ins, lds_fill, false);
+        if (tier >= -1 && lay.tier >= 0) {
+            const uint32_t est = std::max<uint32_t>(lay.tier_blocks, uint32_t((uint64_t(cuts[k].u) + 47) / 48 + 8));
+            B.tier_list[lay.tier].push_back(idx);
+            B.tier_blocks[lay.tier] = std::max(B.tier_blocks[lay.tier], std::min(est, mb[k]));
+        } else {
+            B.large_list.push_back(idx);
+        }
+    }
+    B.seg_groups.push_back(g);
+    return true;
+}
+// Which documents of a batch replay as segments, and how long a segment is: a document is cut
+// when it holds at least two segments' worth of op runs, where a segment is DTGPU_SEG_OPS op
+// runs or the batch's fair share per wave slot (all op runs over 8 waves per CU), whichever is
+// more -- a batch of many equal documents already fills the GPU and is left alone.
+template <typename NOps>
+std::vector<uint32_t> seg_candidates(size_t n, SegSettings &sc, int n_cu, NOps n_ops) {
+    std::vector<uint32_t> c;
+    if (!sc.on) return c;
+    uint64_t total = 0;
+    for (size_t i = 0; i < n; i++) total += n_ops(i);
+    sc.ops_per_seg = std::max<uint64_t>(sc.ops_per_seg, total / (uint64_t(std::max(n_cu, 1)) * 8));
+    for (size_t i = 0; i < n; i++)
+        if (n_ops(i) >= 2 * sc.ops_per_seg) c.push_back(uint32_t(i));
+    return c;
+}
+// The batch's combine step and source-list arena (after every add_segments).
+hipError_t finish_segments(dtgpu_batch &B, uint64_t src_total, const uint32_t *cbyte, const uint8_t *content, hipStream_t s) {
+    hipError_t e = hipSuccess;
+    if ((e = B.d_src.alloc(std::max<uint64_t>(src_total, 1))) != hipSuccess) return e;
+    if (!B.seg_groups.empty()) {
+        if ((e = B.d_groups.upload(B.seg_groups, s)) != hipSuccess || (e = B.d_segdocs.upload(B.seg_docs, s)) != hipSuccess) return e;
+    }
+    CombineParams &c = B.comb;
+    c.groups = B.d_groups.p;
+    c.seg_docs = B.d_segdocs.p;
+    c.n_groups = uint32_t(B.seg_groups.size());
+    c.docs = B.d_docs.p;
+    c.results = B.d_results.p;
+    c.src = B.d_src.p;
+    c.cbyte = cbyte;
+    c.content = content;
+    c.out = B.d_out.p;
+    return hipSuccess;
 }
 
 // xf: a transformed-ops batch (iter_xf_operations): host plans in TransformedOpsIter order
@@ -405,6 +640,8 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     // expected inserted chars per block in the LDS tier (per tracker); DTGPU_LDS_FILL overrides it
     // for experiments (a document that outgrows its LDS index replays on the HBM tier)
     const uint64_t lds_fill = lds_fill_setting();
+    std::vector<int> seg_tier(n, -2);          // replay tier per document (-2: not replayed)
+    std::vector<uint32_t> seg_est(n, 0);
     for (size_t i = 0; i < n; i++) {
         Prepared &p = prep[i];
         B->host_status[i] = p.status;
@@ -412,6 +649,8 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         B->total_lv += p.log.n_lv;
         DocDesc &d = B->docs[i];
         std::memset(&d, 0, sizeof d);
+        d.seg_hi = 0xFFFFFFFFu;   // not a segment (cut replay)
+        d.src_off = ~0ull;
         const uint64_t aq = p.pi.aruns.size() / 4;
         d.arun_off = pdesc[i].arun_off * 4;
         if (p.status != OK) { pdesc[i].skip = 1; continue; }
@@ -442,6 +681,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         }
         d.ascii = p.log.ins_content.size() == n_ins ? 1u : 0u;
         d.lv_off = lv_total;
+        d.pc_off = lv_total;
         d.n_lv = uint32_t(p.log.n_lv);
         d.content_off = content.size();
         d.content_len = uint32_t(p.log.ins_content.size());
@@ -468,6 +708,8 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         d.gidx_off = gidx_total;
         gidx_total += lay.gidx;
         const int t = lay.tier;
+        seg_tier[i] = t;
+        seg_est[i] = lay.tier_blocks;
         if (t >= 0) {
             B->tier_list[t].push_back(uint32_t(i));
             B->tier_blocks[t] = std::max(B->tier_blocks[t], lay.tier_blocks);
@@ -497,6 +739,18 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
             B->plan.aruns = B->d_aruns.p;
         }
     }
+    // cut replay: long documents' later LV ranges as documents of their own
+    uint64_t pc_total = lv_total, src_total = 0;
+    if (!xf) {
+        SegSettings sc = seg_settings();
+        for (uint32_t i : seg_candidates(n, sc, B->n_cu, [&](size_t k) { return seg_tier[k] != -2 ? prep[k].log.ops.size() : 0; })) {
+            SegInput si;
+            seg_input_from_log(prep[i].log, si);
+            const std::vector<SegCut> cuts = plan_segments(si, sc);
+            if (cuts.size() >= 2)
+                add_segments(*B, i, cuts, seg_tier[i], seg_est[i], lds_fill, pc_total, blk_total, gidx_total, src_total);
+        }
+    }
     hcmds.resize(cmd_total);
     htlist.resize(tlist_total);
     CK(B->d_cmds.upload(hcmds, s));
@@ -509,16 +763,17 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     CK(B->d_content.upload(content, s));
     CK(B->d_docs.upload(B->docs, s));
     CK(B->d_lists.upload(tier_lists(*B), s));
-    CK(B->d_pos.alloc(lv_total));
-    CK(B->d_ao.alloc(lv_total));
+    CK(B->d_pos.alloc(pc_total));
+    CK(B->d_ao.alloc(pc_total));
     CK(B->d_items.alloc(blk_total * 64));
     CK(B->d_m2.alloc(2 * blk_total));
     CK(B->d_out.alloc(out_total));
     CK(B->d_gidx.alloc(gidx_total));
     CK(B->d_fb.alloc(n_lds_docs(*B) + 1));
     CK(B->d_counter.alloc(2));
-    CK(B->d_results.alloc(n));
-    CK(hipMemsetAsync(B->d_results.p, 0, std::max<size_t>(n, 1) * sizeof(DocResult), s));
+    CK(B->d_results.alloc(B->docs.size()));
+    CK(hipMemsetAsync(B->d_results.p, 0, std::max<size_t>(B->docs.size(), 1) * sizeof(DocResult), s));
+    CK(finish_segments(*B, src_total, B->d_cbyte.p, B->d_content.p, s));
     if (xf) {
         CK(B->d_mup.alloc(blk_total));
         CK(B->d_tup.alloc(blk_total + 2 * n));
@@ -545,6 +800,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     base.gidx = B->d_gidx.p;
     base.docs = B->d_docs.p;
     base.results = B->d_results.p;
+    base.src = B->d_src.p;
     if (set_tier_params(*B, base) != DTGPU_OK) return DTGPU_ERR_HIP;
     *out = B.release();
     return DTGPU_OK;
@@ -569,7 +825,6 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
 #define CK(x) do { if ((x) != hipSuccess) return DTGPU_ERR_HIP; } while (0)
     CK(hipEventCreate(&B->ev0)); CK(hipEventCreate(&B->ev_mid)); CK(hipEventCreate(&B->ev1));
     CK(hipEventCreate(&B->ev_dec)); CK(hipEventCreate(&B->ev_prep));
-    CK(hipStreamCreateWithFlags(&B->wstream, hipStreamNonBlocking));
     CK(hipEventCreateWithFlags(&B->ev_w0, hipEventDisableTiming));
     CK(hipEventCreateWithFlags(&B->ev_w1, hipEventDisableTiming));
     hipStream_t s = B->stream;
@@ -696,9 +951,13 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     // ---- replay layout ---------------------------------------------------------------------------
     uint64_t cmd_total = 0, tlist_total = 0, blk_total = 0, out_total = 0, gidx_total = 0;
     const uint64_t lds_fill = lds_fill_setting();
+    std::vector<int> seg_tier(n, -2);          // replay tier per document (-2: not replayed)
+    std::vector<uint32_t> seg_est(n, 0);
     for (size_t i = 0; i < n; i++) {
         DocDesc &d = B->docs[i];
         std::memset(&d, 0, sizeof d);
+        d.seg_hi = 0xFFFFFFFFu;   // not a segment (cut replay)
+        d.src_off = ~0ull;
         if (B->host_status[i] != OK) { pdesc[i].skip = 1; continue; }
         if (pres[i].status != PLAN_OK) { B->host_status[i] = DECODE_DEFER; pdesc[i].skip = 1; continue; }
         const DecodeResult &r = Dd.res[i];
@@ -713,6 +972,7 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
         B->n_gpu_planned++;
         d.ascii = r.n_content == n_ins ? 1u : 0u;
         d.lv_off = dd.lv_off;                 // per-LV arenas share the decoder's LV numbering
+        d.pc_off = dd.lv_off;
         d.n_lv = uint32_t(r.n_lv);
         d.content_off = dd.content_off;       // inserted text read in place
         d.content_len = r.n_content;
@@ -731,6 +991,8 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
         d.gidx_off = gidx_total;
         gidx_total += lay.gidx;
         const int t = lay.tier;
+        seg_tier[i] = t;
+        seg_est[i] = lay.tier_blocks;
         if (t >= 0) {
             B->tier_list[t].push_back(uint32_t(i));
             B->tier_blocks[t] = std::max(B->tier_blocks[t], lay.tier_blocks);
@@ -739,6 +1001,18 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
         }
     }
     const uint64_t lv_total = Dd.cbyte.n;
+    // cut replay: long documents' later LV ranges as documents of their own
+    uint64_t pc_total = lv_total, src_total = 0;
+    {
+        SegSettings sc = seg_settings();
+        for (uint32_t i : seg_candidates(n, sc, B->n_cu, [&](size_t k) { return seg_tier[k] != -2 ? Dd.res[k].n_ops : 0u; })) {
+            SegInput si;
+            if (!seg_input_from_device(Dd, i, si, s)) return DTGPU_ERR_HIP;
+            const std::vector<SegCut> cuts = plan_segments(si, sc);
+            if (cuts.size() >= 2)
+                add_segments(*B, i, cuts, seg_tier[i], seg_est[i], lds_fill, pc_total, blk_total, gidx_total, src_total);
+        }
+    }
     CK(B->d_cmds.alloc(cmd_total));
     CK(B->d_tlist.alloc(tlist_total));
     CK(B->p_docs.upload(pdesc, s));
@@ -747,16 +1021,17 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     B->plan.tlist = B->d_tlist.p;
     CK(B->d_docs.upload(B->docs, s));
     CK(B->d_lists.upload(tier_lists(*B), s));
-    CK(B->d_pos.alloc(lv_total));
-    CK(B->d_ao.alloc(lv_total));
+    CK(B->d_pos.alloc(pc_total));
+    CK(B->d_ao.alloc(pc_total));
     CK(B->d_items.alloc(blk_total * 64));
     CK(B->d_m2.alloc(2 * blk_total));
     CK(B->d_out.alloc(out_total));
     CK(B->d_gidx.alloc(gidx_total));
     CK(B->d_fb.alloc(n_lds_docs(*B) + 1));
     CK(B->d_counter.alloc(2));
-    CK(B->d_results.alloc(n));
-    CK(hipMemsetAsync(B->d_results.p, 0, std::max<size_t>(n, 1) * sizeof(DocResult), s));
+    CK(B->d_results.alloc(B->docs.size()));
+    CK(hipMemsetAsync(B->d_results.p, 0, std::max<size_t>(B->docs.size(), 1) * sizeof(DocResult), s));
+    CK(finish_segments(*B, src_total, Dd.cbyte.p, Dd.content.p, s));
     CK(hipStreamSynchronize(s));
 #undef CK
     BatchParams base{};
@@ -774,7 +1049,9 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     base.gidx = B->d_gidx.p;
     base.docs = B->d_docs.p;
     base.results = B->d_results.p;
+    base.src = B->d_src.p;
     if (set_tier_params(*B, base) != DTGPU_OK) return DTGPU_ERR_HIP;
+    B->wstream = B->side[kSideStreams - 1];   // the smallest side tier's stream (see wstream)
     // split pass: when the biggest non-empty LDS tier rides a side stream and other documents
     // exist, its documents' prep and plan do not wait for everyone else's (a skewed batch's
     // longest replays start as soon as their own plans are done)
@@ -783,7 +1060,8 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
         for (int t = kLdsTiers - 1; t >= 1; t--)
             if (!B->tier_list[t].empty()) { tb = t; break; }
         if (tb >= 1) {
-            std::vector<uint32_t> lst = B->tier_list[tb];
+            std::vector<uint32_t> lst;   // the tier's documents, without segment documents
+            for (uint32_t d : B->tier_list[tb]) if (d < n) lst.push_back(d);
             std::vector<uint8_t> big(n, 0);
             for (uint32_t d : lst) big[d] = 1;
             const size_t nb = lst.size();
@@ -820,6 +1098,7 @@ int launch_split_side(dtgpu_batch *B, hipStream_t s) {
     qq.doc_list = B->d_split.p;
     qq.n_docs = B->n_big;
     if (B->n_gpu_planned && launch_plan(qq, sb) != OK) return ErrHip;
+    if (hipEventRecord(B->ev_splan, sb) != hipSuccess) return ErrHip;
     BatchParams tiers[kLdsTiers];
     for (int t = 0; t < kLdsTiers; t++) {
         tiers[t] = B->tier[t];
@@ -1447,6 +1726,28 @@ dtgpu_status dtgpu_batch_last_times(const dtgpu_batch *B, float out[3]) {
     out[1] = B->last_replay_ms;
     out[2] = B->last_prep_ms;
     return DTGPU_OK;
+}
+size_t dtgpu_batch_segments(dtgpu_batch *B, size_t doc, uint32_t *out, size_t cap) {
+    if (!B || doc >= B->n) return 0;
+    for (const SegGroup &g : B->seg_groups) {
+        if (B->seg_docs[g.first] != doc) continue;
+        if (hipSetDevice(B->device) != hipSuccess) return 0;
+        for (uint32_t k = 0; k < g.count && k < cap; k++) {
+            const uint32_t d = B->seg_docs[g.first + k];
+            const DocDesc &e = B->docs[d];
+            DocResult r{};
+            if (hipMemcpyAsync(&r, B->d_results.p + d, sizeof r, hipMemcpyDeviceToHost, B->stream) != hipSuccess ||
+                hipStreamSynchronize(B->stream) != hipSuccess)
+                return 0;
+            uint32_t *w = out + 8 * size_t(k);
+            w[0] = e.seg_lo; w[1] = e.seg_hi; w[2] = e.seg_u;
+            // the first segment's result slot is the document's: the combine step rewrote it
+            w[3] = k ? r.status : 0u; w[4] = k ? r.out_len : 0u; w[5] = r.dbg[15];
+            w[6] = r.lds; w[7] = r.n_blocks;
+        }
+        return g.count;
+    }
+    return 0;
 }
 size_t dtgpu_batch_host_planned(const dtgpu_batch *B, uint8_t *flags, size_t cap) {
     if (!B) return 0;

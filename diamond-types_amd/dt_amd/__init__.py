@@ -143,6 +143,8 @@ def lib():
     L.dtgpu_batch_algorithmic_bytes.argtypes = [vp]
     L.dtgpu_batch_algorithmic_bytes.restype = u64
     L.dtgpu_batch_doc_stats.argtypes = [vp, sz, ctypes.POINTER(ctypes.c_uint32)]
+    L.dtgpu_batch_segments.argtypes = [vp, sz, ctypes.POINTER(ctypes.c_uint32), sz]
+    L.dtgpu_batch_segments.restype = sz
     L.dtgpu_batch_plan_profile.argtypes = [vp, sz, ctypes.POINTER(ctypes.c_uint64)]
     L.dtgpu_batch_total_lv.argtypes = [vp]
     L.dtgpu_batch_total_lv.restype = u64
@@ -784,6 +786,14 @@ class Batch:
                 "cyc_orr", "cyc_run", "cyc_r1", "cyc_r2", "cyc_r3", "n_yjs", "n_split", "cyc_total",
                 "n_sb", "lds_index", "cyc_t1", "cyc_t2", "cyc_t3", "n_dirty", "n_load"]
         return dict(zip(keys, list(out)))
+
+    def segments(self, i):
+        """Cut replay: the LV segments document i replayed as (see dtgpu_batch_segments), as
+        dicts; [] when it replayed whole."""
+        out = (ctypes.c_uint32 * (8 * 64))()
+        n = lib().dtgpu_batch_segments(self._h, i, out, 64)
+        keys = ["lo", "hi", "placeholders", "status", "items_visible", "cyc_total", "lds_index", "n_blocks"]
+        return [dict(zip(keys, list(out[8 * k:8 * k + 8]))) for k in range(min(n, 64))]
 
     @property
     def algorithmic_bytes(self):

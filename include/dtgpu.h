@@ -281,6 +281,17 @@ uint64_t dtgpu_batch_algorithmic_bytes(dtgpu_batch *batch);
  * counts; total cycles/16), [22] superblocks, [23] 1 if the index was in LDS, [24..26] the
  * retreat/advance pass split, [27] block loads that rebuilt stale masks, [28] block loads. */
 dtgpu_status dtgpu_batch_doc_stats(dtgpu_batch *batch, size_t doc, uint32_t out[29]);
+/* Cut replay: the LV segments document `doc` replays as, each on its own wave -- cut where the
+ * whole history below the cut is one version that every later op has seen, the boundary the
+ * reference fast-forwards across (src/listmerge/merge.rs:811-840), each later segment starting
+ * from placeholders for the text at its cut.  Returns the segment count (0 for a document
+ * replayed whole) and writes up to `cap` records of 8 words: {first LV, end LV (~0: the end),
+ * placeholders, status, visible items, cycles/16 (DTGPU_DEBUG=2), 1 if its index was in LDS,
+ * blocks used} from the last run.
+ * DTGPU_SEG=0 disables segmenting; DTGPU_SEG_OPS (op runs per segment, default 3000, raised
+ * to the batch's fair share per wave slot) and DTGPU_SEG_MAX (default 16) size it; read at
+ * batch creation. */
+size_t dtgpu_batch_segments(dtgpu_batch *batch, size_t doc, uint32_t *out, size_t cap);
 /* Device planner cycle profile of one document (DTGPU_PLAN_PROF set at batch creation):
  * out[0..5] cycles waiting for entry records, computing parent vectors, children + next pick,
  * emitting retreat/advance entries, copying op runs, initialising; out[6] commands, out[7]

@@ -1,0 +1,169 @@
+"""Cut replay (dt_replay.hip "segments"): a long document replays as LV segments on separate
+waves -- cut where everything below the cut is one version that every later op has seen, the
+boundary the reference fast-forwards across (src/listmerge/merge.rs:811-840) -- each later
+segment starting from placeholders for the text at its cut, and the combine step joins the
+segments' source lists into the text.  Every text must equal the golden / oracle text, with
+segmenting forced onto documents that would replay whole by default, through both staging
+paths, the timed pass, the debug invariant checks and the LDS -> HBM tier hand-back."""
+import hashlib
+import random
+
+import pytest
+
+import golden_data as G
+from oracle.oracle import OpLog as OracleOpLog
+
+pytestmark = pytest.mark.gpu
+
+import dt_amd  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if dt_amd.device_count() < 1:
+        pytest.fail("no HIP device visible: the engine has no CPU fallback")
+
+
+def _run(docs, staging, timed=False):
+    b = dt_amd.Batch(docs=docs, staging=staging)
+    if timed:
+        b.run_timed()
+    else:
+        b.run()
+        b.sync()
+    res = b.results()
+    return b, res, [b.text(i) if r["status"] == 0 else None for i, r in enumerate(res)]
+
+
+def _check_segments(segs, min_count=2):
+    assert len(segs) >= min_count, segs
+    assert segs[0]["lo"] == 0 and segs[-1]["hi"] == 0xFFFFFFFF
+    for a, b in zip(segs, segs[1:]):
+        assert a["hi"] == b["lo"] and a["lo"] < a["hi"]
+    assert all(s["status"] == 0 for s in segs), segs
+
+
+FF_WANT = None
+
+
+def _ff_want():
+    global FF_WANT
+    if FF_WANT is None:
+        FF_WANT = G.trace("friendsforever_flat")["endContent"].encode()
+    return FF_WANT
+
+
+@pytest.mark.parametrize("staging", ["device", "host"])
+def test_forced_segments_friendsforever(monkeypatch, staging):
+    monkeypatch.setenv("DTGPU_SEG_OPS", "300")
+    b, res, texts = _run([G.dt_bytes("friendsforever")] * 3, staging)
+    assert [r["status"] for r in res] == [0, 0, 0]
+    assert all(t == _ff_want() for t in texts)
+    for i in range(3):
+        _check_segments(b.segments(i), 4)
+
+
+def test_forced_segments_timed_and_rerun(monkeypatch):
+    monkeypatch.setenv("DTGPU_SEG_OPS", "500")
+    b = dt_amd.Batch(docs=[G.dt_bytes("friendsforever")] * 2, staging="device")
+    for _ in range(2):   # a rerun replays every segment and combines again from scratch
+        b.run_timed()
+        res = b.results()
+        assert [r["status"] for r in res] == [0, 0]
+        assert all(b.text(i) == _ff_want() for i in range(2))
+    _check_segments(b.segments(0))
+
+
+def test_node_nodecc_segments_by_default():
+    data = G.dt_bytes("node_nodecc")
+    want = OracleOpLog.load_from(data).checkout_tip_bytes()
+    b, res, texts = _run([data], "device")
+    assert res[0]["status"] == 0
+    _check_segments(b.segments(0))
+    assert hashlib.sha256(texts[0]).hexdigest() == hashlib.sha256(want).hexdigest()
+
+
+def test_segmenting_off_replays_whole(monkeypatch):
+    monkeypatch.setenv("DTGPU_SEG", "0")
+    data = G.dt_bytes("node_nodecc")
+    b, res, texts = _run([data], "device")
+    assert res[0]["status"] == 0 and b.segments(0) == []
+    want = OracleOpLog.load_from(data).checkout_tip_bytes()
+    assert texts[0] == want
+
+
+def _phased_doc(seed, phases=14):
+    """Concurrent phases joined by linear stretches: each phase forks 2-3 branches off one
+    version (branch 0 inserts and deletes, the others only insert, so the merged length is
+    known), then a linear stretch continues from the merge -- cut points between phases,
+    concurrency right up to them."""
+    rng = random.Random(seed)
+    o = dt_amd.ListOpLog()
+    agents = [o.get_or_create_agent_id(n) for n in ("ann", "bob", "cyd")]
+    length = 0
+    alpha = "abcdefghijklmnopqrstuvwxyz"
+    for _ in range(phases):
+        fork = list(o.local_frontier())
+        added = 0
+        for j in range(rng.choice((2, 3))):
+            par, blen = fork, length
+            for _ in range(rng.randint(3, 9)):
+                if j == 0 and blen > 4 and rng.random() < 0.35:
+                    a = rng.randrange(blen - 1)
+                    b = min(blen, a + rng.randint(1, 4))
+                    lv = o.add_delete_at(agents[j], par, a, b)
+                    blen -= b - a
+                    added -= b - a
+                else:
+                    t = "".join(rng.choice(alpha) for _ in range(rng.randint(1, 6)))
+                    lv = o.add_insert_at(agents[j], par, rng.randint(0, blen), t)
+                    blen += len(t)
+                    added += len(t)
+                par = [lv]
+        length += added
+        for _ in range(rng.randint(2, 8)):   # linear stretch from the merge
+            a = rng.choice(agents)
+            if length > 4 and rng.random() < 0.3:
+                s0 = rng.randrange(length - 1)
+                e0 = min(length, s0 + rng.randint(1, 3))
+                o.add_delete_without_content(a, s0, e0)
+                length -= e0 - s0
+            else:
+                t = "".join(rng.choice(alpha) for _ in range(rng.randint(1, 8)))
+                o.add_insert(a, rng.randint(0, length), t)
+                length += len(t)
+    return o.encode()
+
+
+def test_forced_segments_synthetic(monkeypatch):
+    """Phased synthetic documents (concurrency up to every cut): the segmented texts equal
+    the oracle's."""
+    monkeypatch.setenv("DTGPU_SEG_OPS", "12")
+    docs = [_phased_doc(s) for s in range(6)]
+    b, res, texts = _run(docs, "device")
+    for i, d in enumerate(docs):
+        assert res[i]["status"] == 0, (i, res[i])
+        assert texts[i] == OracleOpLog.load_from(d).checkout_tip_bytes(), i
+        _check_segments(b.segments(i), 3)
+
+
+def test_forced_segments_debug_invariants(monkeypatch):
+    """DTGPU_DEBUG=1 checks the whole index after every command: the placeholder blocks a
+    segment starts from must be a consistent index."""
+    monkeypatch.setenv("DTGPU_SEG_OPS", "400")
+    monkeypatch.setenv("DTGPU_DEBUG", "1")
+    b, res, texts = _run([G.dt_bytes("friendsforever")], "device")
+    assert res[0]["status"] == 0, res[0]
+    assert texts[0] == _ff_want()
+    _check_segments(b.segments(0))
+
+
+def test_forced_segments_lds_handback(monkeypatch):
+    """An LDS index sized far too small: segments overflow it and replay again on the HBM
+    tier, placeholders included."""
+    monkeypatch.setenv("DTGPU_SEG_OPS", "300")
+    monkeypatch.setenv("DTGPU_LDS_FILL", "4000")
+    b, res, texts = _run([G.dt_bytes("friendsforever")] * 2, "device")
+    assert [r["status"] for r in res] == [0, 0]
+    assert all(t == _ff_want() for t in texts)
+    _check_segments(b.segments(0), 4)

@@ -34,6 +34,10 @@ def main():
               f"blocks={st['n_blocks']}/{st['max_blocks']} sb={st['n_sb']} lds={st['lds_index']} yjs={st['n_yjs']} splits={st['n_split']} "
               f"loads={st['n_load']} dirty={st['n_dirty']} {parts}",
               flush=True)
+        for k, s in enumerate(b.segments(0)):   # cut replay: one wave per segment
+            print(f"  segment {k}: lv [{s['lo']}, {s['hi'] if s['hi'] != 0xFFFFFFFF else 'end'}) "
+                  f"placeholders={s['placeholders']} visible={s['items_visible']} "
+                  f"cycles={s['cyc_total'] * 16 / 1e6:.2f}M lds={s['lds_index']} blocks={s['n_blocks']}", flush=True)
 
 
 
