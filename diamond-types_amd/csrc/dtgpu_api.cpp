@@ -103,7 +103,7 @@ struct SegInput {
 };
 struct SegSettings { bool on; uint64_t ops_per_seg; uint32_t max_seg; };
 SegSettings seg_settings() {
-    SegSettings s{true, 3000, 16};
+    SegSettings s{true, 500, 16};
     if (const char *e = getenv("DTGPU_SEG")) s.on = *e != '0';
     if (const char *e = getenv("DTGPU_SEG_OPS")) s.ops_per_seg = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
     if (const char *e = getenv("DTGPU_SEG_MAX")) s.max_seg = uint32_t(std::max<uint64_t>(1, strtoull(e, nullptr, 10)));
