@@ -980,6 +980,75 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
     wave_fence();
 }
 
+// Multi-wave retreat / advance pass (the big LDS tiers' workgroups have TOG_WAVES waves; the
+// first replays, the others wait at a barrier until a long pass is posted).  The counters make
+// the pass order-free (see toggle_pass), so the waves take 64-entry chunks round robin and
+// change each item's count with one returning atomic: its visibility / liveness transition is
+// read off the old and new count of that atomic, and the transitions of an item touched twice
+// telescope to its net change whatever the interleaving (a count may pass through "-1"
+// transiently; the block and superblock counts are modular sums and end exact).
+constexpr uint32_t TOG_WAVES = 4;
+constexpr uint32_t TOG_MW_MIN = 512;   // entries: shorter passes stay on the replay wave
+__shared__ uint32_t tog_job[4];        // {off, n, go (0: the document is done), error}
+template <bool L>
+DEV void toggle_chunks(Doc &D, uint32_t off, uint32_t n, uint32_t w0) {
+    const uint32_t l = lane_id();
+    uint32_t err = 0;
+    // the next chunk's entries and delete targets are fetched before this chunk's atomics
+    auto fetch = [&](uint32_t j, uint32_t &e, uint32_t &tgt) {
+        e = D.tlist[off + min(j + l, n - 1)];
+        const uint32_t lv = e & 0x3FFFFFFFu;
+        const bool del = j + l < n && ((e >> 30) & 1u) && lv < D.n_lv;
+        tgt = *reinterpret_cast<const uint32_t *>(D.ao + (del ? lv : 0u));
+    };
+    uint32_t e = 0, tgt = 0;
+    if (w0 * 64 < n) fetch(w0 * 64, e, tgt);
+    for (uint32_t j = w0 * 64; j < n; j += TOG_WAVES * 64) {
+        const bool valid = j + l < n;
+        const uint32_t lv = e & 0x3FFFFFFFu;
+        const bool del = valid && ((e >> 30) & 1u) && lv < D.n_lv;
+        const uint32_t item = del ? tgt : lv;
+        const bool act = valid && lv < D.n_lv && item < D.n_lv;
+        if (valid && !act) err = 1;
+        const uint32_t d = (e >> 31) ? 1u : 0xFFFFu;   // +1 / -1 in the 16-bit count field
+        if (j + TOG_WAVES * 64 < n) fetch(j + TOG_WAVES * 64, e, tgt);
+        uint32_t old = 0;
+        if (act) old = __hip_atomic_fetch_add(D.pc + item, d << 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint32_t oc = old >> 16, nc = (oc + d) & 0xFFFFu, b = old & 0xFFFFu;
+        const bool fv = act && ((oc == 1) != (nc == 1)), fl = act && ((oc != 0) != (nc != 0));
+        if (fv || fl) {
+            const uint32_t dv = fv ? (nc == 1 ? 1u : 0xFFFFFFFFu) : 0u, dl = fl ? (nc != 0 ? 1u : 0xFFFFFFFFu) : 0u;
+            const uint32_t tp = ix<L>(D.sbpos + (opos_of<L>(D, b) >> 6));
+            if (fv) at_add(D.top + tp, dv);
+            if (fl) at_add(D.tlive + tp, dl);
+            at_add(D.cnt + b, dv * C_VIS + dl * C_LIVE);
+            at_or(D.cnt + b, C_DIRTY);
+        }
+    }
+    if (__ballot(err)) at_or(&tog_job[3], 1u);
+}
+// The replay wave's side: post the pass, take its share, wait for the others.
+template <bool L>
+DEV void toggle_mw(Doc &D, uint32_t off, uint32_t n) {
+    if (lane_id() == 0) { tog_job[0] = off; tog_job[1] = n; tog_job[2] = 1; tog_job[3] = 0; }
+    __syncthreads();
+    toggle_chunks<L>(D, off, n, 0);
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // other waves' atomics: no stale L1 lines
+    if (U(tog_job[3])) fail(D, ErrCheckout, 16);
+    D.cb = NONE;
+}
+// The other waves: passes until the replay wave reports the document done.
+template <bool L>
+DEV void toggle_helper(Doc &D, uint32_t w) {
+    for (;;) {
+        __syncthreads();
+        if (!U(tog_job[2])) return;
+        toggle_chunks<L>(D, U(tog_job[0]), U(tog_job[1]), w);
+        __syncthreads();
+    }
+}
+
 // Stream-compact the visible items (the tip's content) in document order into out[]
 // (list/merge.rs:63-95).  G blocks per round keep that many dependent gathers in flight.
 // Visibility comes from the counts (the final advance to the tip leaves masks stale): the
@@ -1258,7 +1327,7 @@ DEV uint32_t check_invariants(Doc &D, DocResult *res) {
     return 0;
 }
 
-template <bool L, bool PROF, bool XF>
+template <bool L, bool PROF, bool XF, bool MW>
 DEV void run_doc(Doc &D) {
     const uint32_t l = lane_id();
     D.nb = 1;
@@ -1348,7 +1417,8 @@ DEV void run_doc(Doc &D) {
                     if (PROF) D.prof[P_DEL] += tick<PROF>() - t0;
                     break;
                 case CMD_TOG:
-                    toggle_pass<L, PROF>(D, a, n, pf, pf_ok);
+                    if (MW && n >= TOG_MW_MIN) toggle_mw<L>(D, a, n);
+                    else toggle_pass<L, PROF>(D, a, n, pf, pf_ok);
                     if (PROF) D.prof[P_TOG] += tick<PROF>() - t0;
                     break;
                 default: fail(D, ErrCheckout, 18); break;
@@ -1423,8 +1493,10 @@ DEV void bind_index(Doc &D, uint8_t *base, uint32_t mb, uint32_t ms, bool narrow
 #ifndef DTGPU_REPLAY_WAVES
 #define DTGPU_REPLAY_WAVES 1   // occupancy floor for the compiler's register budget (tuning knob)
 #endif
-template <bool LDS_INDEX, bool PROF, bool XF>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_REPLAY_WAVES))) void replay_kernel(BatchParams P) {
+// MW: TOG_WAVES waves per workgroup, the others helping with long retreat / advance passes
+// (the big LDS tiers: one or two documents per CU, so the extra waves cost no occupancy).
+template <bool LDS_INDEX, bool PROF, bool XF, bool MW = false>
+__global__ __launch_bounds__(MW ? 64 * TOG_WAVES : 64) __attribute__((amdgpu_waves_per_eu(DTGPU_REPLAY_WAVES))) void replay_kernel(BatchParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t di = U(blockIdx.x);
     uint32_t d;
@@ -1464,7 +1536,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_REPLAY
         D.tup = P.tup + dd.blk_off + 2ull * d;   // sb_capacity(mb) <= mb + 2 slots per document
         D.xf = P.xf + dd.lv_off;
     }
-    run_doc<LDS_INDEX, PROF, XF>(D);
+    if (MW) {
+        const uint32_t w = U(threadIdx.x / 64);
+        if (w) { toggle_helper<LDS_INDEX>(D, w); return; }
+    }
+    run_doc<LDS_INDEX, PROF, XF, MW>(D);
+    if (MW) {   // release the helper waves
+        if (lane_id() == 0) tog_job[2] = 0;
+        __syncthreads();
+    }
 }
 
 
@@ -1569,14 +1649,29 @@ static int launch_lds_tier(const BatchParams &q, hipStream_t s, bool prof) {
     size_t lds = size_t(index_bytes_ms(q.lds_blocks, q.lds_sb, true));
     if (const char *pad = getenv("DTGPU_LDS_PAD")) lds += size_t(strtoul(pad, nullptr, 10));   // occupancy experiments
     if (lds > 160 * 1024) return ErrArg;   // a tier cap above the CU's LDS
+    // documents whose index takes >= 32 KiB of LDS (at most four per CU) replay with helper
+    // waves for long retreat / advance passes (DTGPU_TOG_WAVES=1: one wave)
+    const char *tw = getenv("DTGPU_TOG_WAVES");
+    constexpr size_t kStatic = sizeof(uint32_t) * 4;   // tog_job: the multi-wave kernel's static LDS
+    const bool mw = lds >= 32 * 1024 && lds + kStatic <= 160 * 1024 && !(tw && *tw == '1');
     // allow dynamic LDS up to the CU's 160 KiB: a per-function, per-device attribute, set on
     // every launch (cheap) so it holds on whatever device the batch runs
-    const void *fn = prof ? reinterpret_cast<const void *>(&dev::replay_kernel<true, true, false>)
-                          : reinterpret_cast<const void *>(&dev::replay_kernel<true, false, false>);
-    if (lds > 64 * 1024 && hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+    const void *fn = mw ? (prof ? reinterpret_cast<const void *>(&dev::replay_kernel<true, true, false, true>)
+                                : reinterpret_cast<const void *>(&dev::replay_kernel<true, false, false, true>))
+                        : (prof ? reinterpret_cast<const void *>(&dev::replay_kernel<true, true, false>)
+                                : reinterpret_cast<const void *>(&dev::replay_kernel<true, false, false>));
+    if (lds > 64 * 1024 &&
+        hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024 - (mw ? kStatic : 0))) != hipSuccess)
         return ErrHip;
-    if (prof) hipLaunchKernelGGL((dev::replay_kernel<true, true, false>), dim3(q.n_list), dim3(64), lds, s, q);
-    else hipLaunchKernelGGL((dev::replay_kernel<true, false, false>), dim3(q.n_list), dim3(64), lds, s, q);
+    if (mw) {
+        const dim3 blk(64 * dev::TOG_WAVES);
+        if (prof) hipLaunchKernelGGL((dev::replay_kernel<true, true, false, true>), dim3(q.n_list), blk, lds, s, q);
+        else hipLaunchKernelGGL((dev::replay_kernel<true, false, false, true>), dim3(q.n_list), blk, lds, s, q);
+    } else if (prof) {
+        hipLaunchKernelGGL((dev::replay_kernel<true, true, false>), dim3(q.n_list), dim3(64), lds, s, q);
+    } else {
+        hipLaunchKernelGGL((dev::replay_kernel<true, false, false>), dim3(q.n_list), dim3(64), lds, s, q);
+    }
     return hipGetLastError() == hipSuccess ? OK : ErrHip;
 }
 

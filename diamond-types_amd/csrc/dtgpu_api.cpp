@@ -109,12 +109,11 @@ SegSettings seg_settings() {
     if (const char *e = getenv("DTGPU_SEG_MAX")) s.max_seg = uint32_t(std::max<uint64_t>(1, strtoull(e, nullptr, 10)));
     return s;
 }
-std::vector<SegCut> plan_segments(const SegInput &in, const SegSettings &cfg) {
-    std::vector<SegCut> out;
-    const size_t ne = in.ent.size(), nop = in.ops.size();
-    const uint32_t S = uint32_t(std::min<uint64_t>(cfg.max_seg, nop / cfg.ops_per_seg));
-    if (S < 2 || ne == 0 || in.n_lv >= 0x7FFFFFFFull) return out;
-    // cut ranges [a, b]: every v in them is a cut
+// Cut ranges [a, b] (every v in them is a cut), in LV order: at entry k ([s, t), parents P)
+// the prefix's frontier minus P must be empty (then [0, v) is the version {v-1} for s < v <= t),
+// and every later entry's parents must be >= v-1 (so each has v-1 in its history).
+std::vector<std::pair<uint64_t, uint64_t>> cut_ranges(const SegInput &in) {
+    const size_t ne = in.ent.size();
     std::vector<int64_t> sufmin(ne + 1, INT64_MAX);
     for (size_t k = ne; k-- > 0;) {
         int64_t mp = -1;   // ROOT
@@ -135,6 +134,14 @@ std::vector<SegCut> plan_segments(const SegInput &in, const SegSettings &cfg) {
         }
         F.insert(t - 1);
     }
+    return cuts;
+}
+std::vector<SegCut> plan_segments(const SegInput &in, const SegSettings &cfg) {
+    std::vector<SegCut> out;
+    const size_t ne = in.ent.size(), nop = in.ops.size();
+    const uint32_t S = uint32_t(std::min<uint64_t>(cfg.max_seg, nop / cfg.ops_per_seg));
+    if (S < 2 || ne == 0 || in.n_lv >= 0x7FFFFFFFull) return out;
+    const std::vector<std::pair<uint64_t, uint64_t>> cuts = cut_ranges(in);
     if (cuts.empty()) return out;
     auto in_cut = [&](uint64_t v) {
         auto it = std::upper_bound(cuts.begin(), cuts.end(), std::make_pair(v, UINT64_MAX));
@@ -1251,6 +1258,14 @@ int64_t dtgpu_oplog_add_delete_without_content(dtgpu_oplog *h, int32_t agent, ui
     return dtgpu_oplog_add_delete_at(h, agent, v.data(), v.size(), s, e);
 }
 size_t dtgpu_oplog_len(const dtgpu_oplog *h) { return h ? size_t(h->o.n_lv) : 0; }
+size_t dtgpu_oplog_cut_ranges(const dtgpu_oplog *h, uint64_t *out, size_t cap) {
+    if (!h) return 0;
+    SegInput si;
+    seg_input_from_log(h->o, si);
+    const auto cuts = cut_ranges(si);
+    for (size_t k = 0; k < cuts.size() && k < cap && out; k++) { out[2 * k] = cuts[k].first; out[2 * k + 1] = cuts[k].second; }
+    return cuts.size();
+}
 size_t dtgpu_oplog_local_frontier(const dtgpu_oplog *h, uint64_t *out, size_t cap) {
     if (!h) return 0;
     for (size_t i = 0; i < h->o.version.size() && i < cap; i++) out[i] = h->o.version[i];

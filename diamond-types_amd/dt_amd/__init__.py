@@ -145,6 +145,8 @@ def lib():
     L.dtgpu_batch_doc_stats.argtypes = [vp, sz, ctypes.POINTER(ctypes.c_uint32)]
     L.dtgpu_batch_segments.argtypes = [vp, sz, ctypes.POINTER(ctypes.c_uint32), sz]
     L.dtgpu_batch_segments.restype = sz
+    L.dtgpu_oplog_cut_ranges.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), sz]
+    L.dtgpu_oplog_cut_ranges.restype = sz
     L.dtgpu_batch_plan_profile.argtypes = [vp, sz, ctypes.POINTER(ctypes.c_uint64)]
     L.dtgpu_batch_total_lv.argtypes = [vp]
     L.dtgpu_batch_total_lv.restype = u64
@@ -413,6 +415,14 @@ class ListOpLog:
         "parent_offsets", "parents", "content", "char_offsets", "version", "agent_names"."""
         a = _export(lambda c, p, n: lib().dtgpu_oplog_export(self._h, c, p, n), what)
         return _names(a) if what == "agent_names" else a
+
+    def cut_ranges(self):
+        """Maximal [first, last] LV ranges of cut points (dtgpu_oplog_cut_ranges): v such that the
+        ops below v are the version {v-1} and every later op has v-1 in its history."""
+        n = lib().dtgpu_oplog_cut_ranges(self._h, None, 0)
+        buf = (ctypes.c_uint64 * max(2, 2 * n))()
+        lib().dtgpu_oplog_cut_ranges(self._h, buf, n)
+        return [(int(buf[2 * k]), int(buf[2 * k + 1])) for k in range(n)]
 
     def checkout_tip_bytes(self) -> bytes:
         n = ctypes.c_size_t()

@@ -120,6 +120,12 @@ dtgpu_status dtgpu_oplog_encode(const dtgpu_oplog *oplog, const uint64_t *from, 
 
 /* ListOpLog::len() (src/list/oplog.rs:89-91) */
 size_t dtgpu_oplog_len(const dtgpu_oplog *oplog);
+/* Cut points of the causal graph: LVs v such that the ops below v form the single version
+ * {v-1} and every later op has v-1 in its history -- where the reference's merge can
+ * fast-forward (src/listmerge/merge.rs:811-840) and where a batch's cut replay may split a
+ * document.  Returns the number of maximal ranges and writes up to `cap` of them as
+ * {first, last} pairs (both ends are cuts). */
+size_t dtgpu_oplog_cut_ranges(const dtgpu_oplog *oplog, uint64_t *out, size_t cap);
 /* ListOpLog::local_frontier() (src/list/oplog.rs:329-331).  Returns the frontier length;
  * writes min(len, cap) LVs. */
 size_t dtgpu_oplog_local_frontier(const dtgpu_oplog *oplog, uint64_t *out, size_t cap);

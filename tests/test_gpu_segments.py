@@ -6,11 +6,11 @@ segments' source lists into the text.  Every text must equal the golden / oracle
 segmenting forced onto documents that would replay whole by default, through both staging
 paths, the timed pass, the debug invariant checks and the LDS -> HBM tier hand-back."""
 import hashlib
-import random
 
 import pytest
 
 import golden_data as G
+from synth_docs import _phased_doc
 from oracle.oracle import OpLog as OracleOpLog
 
 pytestmark = pytest.mark.gpu
@@ -90,49 +90,6 @@ def test_segmenting_off_replays_whole(monkeypatch):
     assert res[0]["status"] == 0 and b.segments(0) == []
     want = OracleOpLog.load_from(data).checkout_tip_bytes()
     assert texts[0] == want
-
-
-def _phased_doc(seed, phases=14):
-    """Concurrent phases joined by linear stretches: each phase forks 2-3 branches off one
-    version (branch 0 inserts and deletes, the others only insert, so the merged length is
-    known), then a linear stretch continues from the merge -- cut points between phases,
-    concurrency right up to them."""
-    rng = random.Random(seed)
-    o = dt_amd.ListOpLog()
-    agents = [o.get_or_create_agent_id(n) for n in ("ann", "bob", "cyd")]
-    length = 0
-    alpha = "abcdefghijklmnopqrstuvwxyz"
-    for _ in range(phases):
-        fork = list(o.local_frontier())
-        added = 0
-        for j in range(rng.choice((2, 3))):
-            par, blen = fork, length
-            for _ in range(rng.randint(3, 9)):
-                if j == 0 and blen > 4 and rng.random() < 0.35:
-                    a = rng.randrange(blen - 1)
-                    b = min(blen, a + rng.randint(1, 4))
-                    lv = o.add_delete_at(agents[j], par, a, b)
-                    blen -= b - a
-                    added -= b - a
-                else:
-                    t = "".join(rng.choice(alpha) for _ in range(rng.randint(1, 6)))
-                    lv = o.add_insert_at(agents[j], par, rng.randint(0, blen), t)
-                    blen += len(t)
-                    added += len(t)
-                par = [lv]
-        length += added
-        for _ in range(rng.randint(2, 8)):   # linear stretch from the merge
-            a = rng.choice(agents)
-            if length > 4 and rng.random() < 0.3:
-                s0 = rng.randrange(length - 1)
-                e0 = min(length, s0 + rng.randint(1, 3))
-                o.add_delete_without_content(a, s0, e0)
-                length -= e0 - s0
-            else:
-                t = "".join(rng.choice(alpha) for _ in range(rng.randint(1, 8)))
-                o.add_insert(a, rng.randint(0, length), t)
-                length += len(t)
-    return o.encode()
 
 
 def test_forced_segments_synthetic(monkeypatch):
