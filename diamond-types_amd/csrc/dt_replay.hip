@@ -987,8 +987,14 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
 // read off the old and new count of that atomic, and the transitions of an item touched twice
 // telescope to its net change whatever the interleaving (a count may pass through "-1"
 // transiently; the block and superblock counts are modular sums and end exact).
-constexpr uint32_t TOG_WAVES = 4;
-constexpr uint32_t TOG_MW_MIN = 512;   // entries: shorter passes stay on the replay wave
+#ifndef DTGPU_TOG_WAVES
+#define DTGPU_TOG_WAVES 4
+#endif
+#ifndef DTGPU_TOG_MW_MIN
+#define DTGPU_TOG_MW_MIN 512
+#endif
+constexpr uint32_t TOG_WAVES = DTGPU_TOG_WAVES;
+constexpr uint32_t TOG_MW_MIN = DTGPU_TOG_MW_MIN;   // entries: shorter passes stay on the replay wave
 __shared__ uint32_t tog_job[4];        // {off, n, go (0: the document is done), error}
 template <bool L>
 DEV void toggle_chunks(Doc &D, uint32_t off, uint32_t n, uint32_t w0) {
