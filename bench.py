@@ -167,8 +167,8 @@ def cpu_config0():
 def single_doc_latency(data, gpu, staging):
     """One document alone (single-doc latency on one core, median of 5 after a
     warmup): the GPU checkout pass of a one-document batch next to the C oracle's checkout_tip()
-    on one host thread.  A single document is one sequential replay chain, so the GPU is not
-    expected to win here; the batch is what it is for."""
+    on one host thread.  A document's replay is a sequential chain between the cut points of its
+    history; the cut replay (dt_replay.hip "segments") runs the pieces on separate waves."""
     import dt_amd
     from oracle.oracle import OpLog as OracleOpLog
     b = dt_amd.Batch(docs=[data], device=gpu, staging=staging)
