@@ -73,3 +73,22 @@ def test_run_timed_on_host_and_device_staged_batches():
         assert ms > 0 and plan > 0 and replay > 0
         assert (prep > 0) == (staging == "device")   # walker inputs are a kernel only when device-staged
         assert all(r["status"] == 0 for r in b.results())
+
+
+def test_mixed_skewed_batch_forced_segments(mixed, monkeypatch):
+    """The same skewed batch with cut replay forced onto every document of 200+ op runs (the
+    linear JSON traces cut anywhere, node_nodecc and friendsforever where their histories allow):
+    segment documents in every LDS tier, the split pass's big tier among them, both staging
+    paths; every text still equals its golden / oracle text."""
+    monkeypatch.setenv("DTGPU_SEG_OPS", "100")
+    docs, want = mixed
+    for staging in ("device", "host"):
+        b = dt_amd.Batch(docs=docs, staging=staging)
+        b.run_timed()
+        res = b.results()
+        for i, (r, w) in enumerate(zip(res, want)):
+            assert r["status"] == 0, (staging, i, r)
+            assert b.text(i) == w, (staging, i)
+        segs = [b.segments(i) for i in range(len(docs))]
+        assert sum(1 for s in segs if len(s) >= 2) >= len(docs) // 2, staging
+        assert all(x["status"] == 0 for s in segs for x in s)
