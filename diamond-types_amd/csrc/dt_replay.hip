@@ -1659,7 +1659,9 @@ static int launch_lds_tier(const BatchParams &q, hipStream_t s, bool prof) {
     // waves for long retreat / advance passes (DTGPU_TOG_WAVES=1: one wave)
     const char *tw = getenv("DTGPU_TOG_WAVES");
     constexpr size_t kStatic = sizeof(uint32_t) * 4;   // tog_job: the multi-wave kernel's static LDS
-    const bool mw = lds >= 32 * 1024 && lds + kStatic <= 160 * 1024 && !(tw && *tw == '1');
+    size_t mw_min = 32 * 1024;   // DTGPU_TOG_MW_LDS: the LDS bytes from which a tier gets helper waves
+    if (const char *e = getenv("DTGPU_TOG_MW_LDS")) mw_min = size_t(strtoull(e, nullptr, 10));
+    const bool mw = lds >= mw_min && lds + kStatic <= 160 * 1024 && !(tw && *tw == '1');
     // allow dynamic LDS up to the CU's 160 KiB: a per-function, per-device attribute, set on
     // every launch (cheap) so it holds on whatever device the batch runs
     const void *fn = mw ? (prof ? reinterpret_cast<const void *>(&dev::replay_kernel<true, true, false, true>)
