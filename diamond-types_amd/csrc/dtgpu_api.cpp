@@ -473,10 +473,13 @@ bool add_segments(dtgpu_batch &B, uint32_t i, const std::vector<SegCut> &cuts, i
         B.docs.push_back(e);
         B.seg_cost.push_back(cuts[k].hi == 0xFFFFFFFFu ? n_lv - cuts[k].lo : cuts[k].hi - cuts[k].lo);
         B.seg_docs.push_back(idx);
-        // its own replay tier, sized for its placeholders and inserts (a split pass's main
-        // stream waits for the big tier's plans before replaying: see replay_all)
+        // its own replay tier, sized for its placeholders and inserts, never above its
+        // document's: a split pass replays the biggest tier beside the other documents' plans,
+        // so a segment may sit there only when its document is planned there too (the main
+        // stream waits for the big tier's plans before replaying any tier: see replay_all); a
+        // document on the HBM tier keeps its segments there
         const Layout lay = replay_layout(cuts[k].u + cuts[k].ins, lds_fill, false);
-        if (tier >= -1 && lay.tier >= 0) {
+        if (tier >= 0 && lay.tier >= 0 && lay.tier <= tier) {
             const uint32_t est = std::max<uint32_t>(lay.tier_blocks, uint32_t((uint64_t(cuts[k].u) + 47) / 48 + 8));
             B.tier_list[lay.tier].push_back(idx);
             B.tier_blocks[lay.tier] = std::max(B.tier_blocks[lay.tier], std::min(est, mb[k]));
