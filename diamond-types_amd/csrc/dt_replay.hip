@@ -1600,7 +1600,10 @@ __global__ __launch_bounds__(COMBINE_THREADS) void combine_kernel(CombineParams 
         const uint32_t cut = s_cut;
         for (uint32_t i = t; i < cut; i += COMBINE_THREADS) {
             const uint32_t e = S[i];
-            if (e & SEG_PHANTOM) S[i] = R[e & ~SEG_PHANTOM];
+            if (e & SEG_PHANTOM) {
+                if ((e & ~SEG_PHANTOM) < nR) S[i] = R[e & ~SEG_PHANTOM];
+                else s_bad = 1;   // (the suffix search makes this unreachable)
+            }
         }
         __syncthreads();
         R = S;
