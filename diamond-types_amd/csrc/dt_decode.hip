@@ -1167,6 +1167,53 @@ __device__ __forceinline__ bool batch_agents(VQ &q, uint32_t n_file, uint32_t *f
 
 struct FastOut { uint32_t status, n_aruns, n_pre, n_lv, ins_size; uint64_t t_mid; };
 
+// Non-ASCII insert text on the batched path: fast_runs numbers the inserted chars (cbyte = the
+// char's index), then this pass puts each char's byte offset in place, 64 LVs at a time: the
+// chunk's inserted chars are the next ones of the text, so their starts are the next char-start
+// bytes from a running byte cursor (one ballot per 64 text bytes, a rank into LDS).  Returns
+// false (the caller takes the exact path) when the numbering does not run 0, 1, 2, ... along
+// the LVs or the text ends early.
+__device__ __forceinline__ uint32_t count_char_starts(const uint8_t *t, uint32_t n) {
+    uint32_t c = 0;
+    for (uint32_t i = 0; i < n; i += 64) {
+        const uint32_t j = i + lane();
+        c += popc(ballot(j < n && (t[j] & 0xC0u) != 0x80u));
+    }
+    return c;
+}
+__device__ __forceinline__ bool utf8_offsets(const uint8_t *t, uint32_t n, uint32_t *cbyte, uint32_t n_lv, uint32_t n_chars) {
+    __shared__ uint32_t slot[64];
+    const uint32_t l = lane();
+    uint32_t cur = 0, kbase = 0;
+    for (uint32_t lv0 = 0; lv0 < n_lv; lv0 += 64) {
+        const uint32_t lv = lv0 + l;
+        const uint32_t k = lv < n_lv ? cbyte[lv] : 0xFFFFFFFFu;
+        const bool ins = k != 0xFFFFFFFFu;
+        const uint64_t m = ballot(ins);
+        if (!m) continue;
+        const uint32_t need = popc(m), r = popc(m & lt_mask());
+        if (ballot(ins && k != kbase + r)) return false;
+        uint32_t got = 0;
+        for (uint32_t w = cur; got < need; w += 64) {
+            if (w >= n) return false;
+            const uint32_t j = w + l;
+            const bool st = j < n && (t[j] & 0xC0u) != 0x80u;
+            const uint64_t sm = ballot(st);
+            const uint32_t rk = got + popc(sm & lt_mask());
+            if (st && rk < need) slot[rk] = j;
+            got += popc(sm);
+        }
+        __syncthreads();
+        if (ins) cbyte[lv] = slot[r];
+        const uint32_t lastb = slot[need - 1];
+        __syncthreads();
+        const uint8_t c0 = t[lastb];
+        cur = lastb + (c0 < 0x80 ? 1u : (c0 & 0xE0u) == 0xC0u ? 2u : (c0 & 0xF0u) == 0xE0u ? 3u : 4u);
+        kbase += need;
+    }
+    return kbase == n_chars;
+}
+
 __device__ __forceinline__ FastOut fast_runs(VQ qav, VQ qtp, VQ runs, uint32_t text_n, uint32_t n_file, uint32_t *fseq,
                                           const uint32_t *fmap, uint32_t *vs, uint4 *aruns_out, uint4 *pre_out,
                                           uint32_t *cbyte, uint32_t *bnd, uint32_t arun_cap, uint32_t pre_cap,
@@ -1541,10 +1588,21 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
         for (uint64_t i = lane(); i < k; i += 64) O.cbyte[lv0 + i] = v;
     };
 
-    if (ins.present && ins.ascii && !del.present) {
+    if (ins.present && !del.present) {
         const uint64_t t_runs = __builtin_amdgcn_s_memtime();
-        const FastOut fo = fast_runs(qav, qtp, ins.runs, ins.text.n, n_file, L.fseq, L.fmap, vs, O.aruns, O.pre,
-                                     O.cbyte, O.alist, D.arun_cap, D.pre_cap, D.lv_cap);
+        // a non-ASCII text: the batched path numbers chars, utf8_offsets then places their bytes
+        const uint8_t *txt = C.ptr(ins.text.s) + ins.text.p;
+        const uint32_t n_chars = ins.ascii ? ins.text.n : count_char_starts(txt, ins.text.n);
+        FastOut fo = fast_runs(qav, qtp, ins.runs, n_chars, n_file, L.fseq, L.fmap, vs, O.aruns, O.pre,
+                               O.cbyte, O.alist, D.arun_cap, D.pre_cap, D.lv_cap);
+        if (fo.status == 0 && !ins.ascii) {
+            if (utf8_offsets(txt, ins.text.n, O.cbyte, fo.n_lv, n_chars)) {
+                fo.ins_size = ins.text.n;   // bytes from here on
+                all_ascii = 0;
+            } else {
+                fo.status = 1;
+            }
+        }
         if (fo.status == 0) {
             R.prof[7] += uint32_t(fo.t_mid - t_runs);   // the agent-assignment half of the fast path
             qa.at = fo.n_aruns;

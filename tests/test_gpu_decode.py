@@ -186,3 +186,36 @@ def test_lz4_shapes_decode_identically():
     for i, d in enumerate(docs):
         assert dec.status(i)["status"] == 0, i
         _same_arrays(dec, i, d)
+
+
+def _utf8_docs():
+    """Non-ASCII insert text: the JSON traces whose content is not all ASCII, written as .dt the
+    way configs[4] writes them, and small documents with 2-, 3- and 4-byte chars between ASCII
+    ones, deletes and concurrent inserts."""
+    docs = []
+    for n in ("seph-blog1", "rustcode"):
+        docs.append(dt_amd.apply_edits_push_merge(G.trace(n)["txns"]).encode())
+    o = dt_amd.ListOpLog()
+    a, b = o.get_or_create_agent_id("a"), o.get_or_create_agent_id("b")
+    o.add_insert(a, 0, "héllo wörld — ✓ 😀 end")
+    o.add_delete_without_content(a, 3, 6)
+    o.add_insert(b, 2, "ßü€𝄞")
+    v = list(o.local_frontier())
+    o.add_insert_at(a, v, 1, "日本語")
+    o.add_insert_at(b, v, 4, "x😀y")
+    o.add_insert(a, 0, "plain ascii at the front ")
+    docs.append(o.encode())
+    return docs
+
+
+def test_utf8_text_takes_the_batched_path():
+    """Non-ASCII insert text decodes on the batched op-record path too (the char numbering, then
+    each char's byte offset placed from the text): arrays equal the host decoder's, and profile
+    slot 7 shows the batched path ran."""
+    docs = _utf8_docs()
+    dec = dt_amd.DecodeBatch(docs)
+    dec.run()
+    for i, d in enumerate(docs):
+        assert dec.status(i)["status"] == 0, i
+        _same_arrays(dec, i, d)
+        assert dec.profile(i)[7] > 0, i
