@@ -18,3 +18,11 @@ for name, data in docs:
     o = dt_amd.ListOpLog.load_from(data)
     print(f"{name}: {len(data)} B, {len(o)} LVs, {len(o.export('ops'))} op runs, decode {ms:.2f} ms; "
           f"phases {one.profile(0)}", flush=True)
+
+# device encoder, one document alone per trace (ENCODE_FULL; bytes checked against the host)
+if os.environ.get("DMIXED_ENCODE"):
+    for name, data in docs:
+        b = dt_amd.Batch(docs=[data], staging="device")
+        ms = min(b.encode() for _ in range(3))
+        ok = b.encoded(0) == dt_amd.ListOpLog.load_from(data).encode()
+        print(f"{name}: encode {ms:.2f} ms, bytes equal host: {ok}", flush=True)
