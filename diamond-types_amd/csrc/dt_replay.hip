@@ -1452,7 +1452,9 @@ DEV void run_doc(Doc &D) {
     if (!D.err) {
         const uint64_t so = vld(&D.desc->src_off);
         if (!XF && so != ~0ull) {   // a segment: its source list, resolved by launch_combine
-            materialise_src<L>(D, gp(vld(&KP().src)) + so, U(vld(&D.desc->src_cap)), len, n_items);
+            const uint32_t cap = U(vld(&D.desc->src_cap));
+            materialise_src<L>(D, gp(vld(&KP().src)) + so, cap, len, n_items);
+            if (len > cap) { fail(D, ErrCapacity, 32); len = 0; }   // (cap bounds the items: unreachable)
         } else {
             GLOBAL_AS uint8_t *out = gp(vld(&KP().out)) + vld(&D.desc->out_off);
             materialise<L>(D, out, U(vld(&D.desc->out_cap)), len, h, n_items);
