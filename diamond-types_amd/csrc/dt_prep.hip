@@ -167,6 +167,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
 
 #ifdef DTGPU_PREP_PROF
     const uint64_t T0 = wall_clock64();
+    uint64_t T1 = T0, T2 = T0;
 #endif
     if (P.mode != 2) {
     // ---- 1. parents: entry of each parent, child counts ------------------------------------------
@@ -211,7 +212,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
     wave_fence();
     // children in child-index order (slots are in (child, parent) order): a stable scatter,
 #ifdef DTGPU_PREP_PROF
-    const uint64_t T1 = wall_clock64();
+    T1 = wall_clock64();
 #endif
     // 64 slots at a time: each lane gathers its key's CSR offset and fill once, register-only
     // rounds (one key each) rank the lanes sharing a key, then one parallel store places them and
@@ -245,7 +246,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
     if (report_oob()) return;
 
 #ifdef DTGPU_PREP_PROF
-    const uint64_t T2 = wall_clock64();
+    T2 = wall_clock64();
 #endif
     // ---- 2. each entry's first op run (ops are split at entry boundaries) ------------------------
     // eop[i] = lower bound of the entry's first LV among the op runs' first LVs (strictly
