@@ -597,7 +597,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
     // one lookup per run; otherwise ranked per run
     const uint2 *names = reinterpret_cast<const uint2 *>(P.d_agents) + D.d_agent;
     const uint8_t *in = P.in + D.d_in;
-    if (D.n_agents <= ((npar + 1) & ~1u)) {
+    // (the LDS is free by now: the ranks go there when they fit -- it is at least the erec
+    // staging's 32 records -- else into the owner scratch)
+    const uint32_t lds_words = max((P.max_entries + 1) / 2, 32u * EREC_WORDS);
+    uint32_t *rk = D.n_agents <= lds_words ? lfw : owner;
+    if (D.n_agents <= lds_words || D.n_agents <= ((npar + 1) & ~1u)) {
         for (uint32_t a = l; a < D.n_agents; a += 64) {
             const uint2 me = names[a];
             uint32_t rank = 0;
@@ -612,12 +616,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
                 if (!cmp) cmp = o.y < me.y ? -1 : o.y > me.y ? 1 : 0;
                 rank += cmp < 0 ? 1u : 0u;
             }
-            owner[a] = rank;
+            rk[a] = rank;
         }
-        wave_fence();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         for (uint32_t k = l; k < D.n_aruns; k += 64) {
             const uint4 a = ar[k];   // lv, len, agent, seq
-            *reinterpret_cast<uint4 *>(P.aruns + 4 * (D.o_arun + k)) = make_uint4(a.x, owner[a.z], a.w, a.z);
+            *reinterpret_cast<uint4 *>(P.aruns + 4 * (D.o_arun + k)) = make_uint4(a.x, rk[a.z], a.w, a.z);
         }
     } else {
         for (uint32_t k = l; k < D.n_aruns; k += 64) {
