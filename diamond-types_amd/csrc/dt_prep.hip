@@ -528,15 +528,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
     // offset comes from a register (lane = chain), not a dependent load.
     uint32_t n_ins = 0;
     {
-        uint32_t ebase = 0;
+        // software-pipelined: chunk j0 + 64's window and runs are requested before chunk j0's
+        // stores (gfx9 counts stores in vmcnt: loads issued after them would wait for them)
+        auto fetch = [&](uint32_t j0, uint32_t eb, uint32_t &we, uint2 &wq, uint4 &o) {
+            const uint32_t wi = eb + l;
+            const bool wv = wi < ne;
+            we = wv ? eop[wi + 1] : 0xFFFFFFFFu;   // end of entry eb + l
+            wq = wv ? cs[wi] : make_uint2(0, 0);
+            o = j0 + l < nops ? ops[j0 + l] : make_uint4(0, 0, 0, 0);   // lv, len, pos, kind | fwd << 1
+        };
+        uint32_t ebase = 0, we = 0;
+        uint2 wq = make_uint2(0, 0);
+        uint4 o = make_uint4(0, 0, 0, 0);
+        if (nops) fetch(0, 0, we, wq, o);
         for (uint32_t j0 = 0; j0 < nops; j0 += 64) {
             const uint32_t j = j0 + l;
             const bool live = j < nops;
-            const uint32_t wi = ebase + l;
-            const bool wv = wi < ne;
-            const uint32_t we = wv ? eop[wi + 1] : 0xFFFFFFFFu;   // end of entry ebase + l
-            const uint2 wq = wv ? cs[wi] : make_uint2(0, 0);
-            const uint4 o = live ? ops[j] : make_uint4(0, 0, 0, 0);   // lv, len, pos, kind | fwd << 1
             uint32_t c = 0;
 #pragma unroll
             for (uint32_t st = 32; st >= 1; st >>= 1)
@@ -555,26 +562,28 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
                 qx = q.x; qy = q.y;
             }
             const uint32_t dch = uint32_t(__shfl(int(doff_l), int(qx & 63u)));
+            const uint4 oc = o;
+            ebase = rdl(i, min(nops - 1 - j0, 63u));
+            if (j0 + 64 < nops) fetch(j0 + 64, ebase, we, wq, o);
             // the run's dense slots [dch + qy + lv, + len) lie inside the chain tables
-            PREP_ASSERT(!live || (qx < nch && uint64_t(uint32_t(dch + qy + o.x)) + o.y <= D.n_lv), PREP_T_DENSE);
+            PREP_ASSERT(!live || (qx < nch && uint64_t(uint32_t(dch + qy + oc.x)) + oc.y <= D.n_lv), PREP_T_DENSE);
             if (live && (!CHECK || !oob)) {
-                const bool del = o.w & 1u;
-                opc[j] = Cmd{del ? (CMD_DEL | ((o.w & 2u) ? 16u : 0u)) : uint32_t(CMD_INS), o.x, o.y, o.z};
-                if (!del) n_ins += o.y;
+                const bool del = oc.w & 1u;
+                opc[j] = Cmd{del ? (CMD_DEL | ((oc.w & 2u) ? 16u : 0u)) : uint32_t(CMD_INS), oc.x, oc.y, oc.z};
+                if (!del) n_ins += oc.y;
                 // the run's dense slots (chain offset + seq0 - start + LV): 16-byte stores between
                 // a scalar head and tail.  (Filling the chunk LV by LV across the lanes instead
                 // measured no faster.)
                 const uint32_t flag = del ? TL_DEL : 0u;
-                uint32_t *dp = dense + uint32_t(dch + qy + o.x);
+                uint32_t *dp = dense + uint32_t(dch + qy + oc.x);
                 uint32_t v = 0;
-                for (; v < o.y && (reinterpret_cast<uintptr_t>(dp + v) & 15u); v++) dp[v] = (o.x + v) | flag;
-                for (; v + 4 <= o.y; v += 4) {
-                    const uint32_t b = o.x + v;
+                for (; v < oc.y && (reinterpret_cast<uintptr_t>(dp + v) & 15u); v++) dp[v] = (oc.x + v) | flag;
+                for (; v + 4 <= oc.y; v += 4) {
+                    const uint32_t b = oc.x + v;
                     *reinterpret_cast<uint4 *>(dp + v) = make_uint4(b | flag, (b + 1) | flag, (b + 2) | flag, (b + 3) | flag);
                 }
-                for (; v < o.y; v++) dp[v] = (o.x + v) | flag;
+                for (; v < oc.y; v++) dp[v] = (oc.x + v) | flag;
             }
-            ebase = rdl(i, min(nops - 1 - j0, 63u));
         }
     }
     if (report_oob()) return;
