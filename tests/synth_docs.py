@@ -4,7 +4,7 @@ import random
 import dt_amd
 
 
-def _phased_doc(seed, phases=14):
+def phased_doc(seed, phases=14):
     """Concurrent phases joined by linear stretches: each phase forks 2-3 branches off one
     version (branch 0 inserts and deletes, the others only insert, so the merged length is
     known), then a linear stretch continues from the merge -- cut points between phases,

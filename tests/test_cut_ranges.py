@@ -7,7 +7,7 @@ pinned on the benchmark files."""
 import pytest
 
 import golden_data as G
-from synth_docs import _phased_doc
+from synth_docs import phased_doc
 
 import dt_amd
 
@@ -57,7 +57,7 @@ def _merged(ranges):
 
 @pytest.mark.parametrize("seed", range(5))
 def test_cut_ranges_match_definition(seed):
-    o = dt_amd.ListOpLog.load_from(_phased_doc(seed, phases=6))
+    o = dt_amd.ListOpLog.load_from(phased_doc(seed, phases=6))
     assert len(o) < 1500
     got = _merged(o.cut_ranges())
     assert got == _brute_cuts(o)

@@ -10,7 +10,7 @@ import hashlib
 import pytest
 
 import golden_data as G
-from synth_docs import _phased_doc
+from synth_docs import phased_doc
 from oracle.oracle import OpLog as OracleOpLog
 
 pytestmark = pytest.mark.gpu
@@ -96,7 +96,7 @@ def test_forced_segments_synthetic(monkeypatch):
     """Phased synthetic documents (concurrency up to every cut): the segmented texts equal
     the oracle's."""
     monkeypatch.setenv("DTGPU_SEG_OPS", "12")
-    docs = [_phased_doc(s) for s in range(6)]
+    docs = [phased_doc(s) for s in range(6)]
     b, res, texts = _run(docs, "device")
     for i, d in enumerate(docs):
         assert res[i]["status"] == 0, (i, res[i])
