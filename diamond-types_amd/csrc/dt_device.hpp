@@ -73,6 +73,7 @@ struct BatchParams {
     uint32_t *tup;
     uint32_t *xf;
     uint32_t *src;   // cut replay: the segments' source lists (DocDesc::src_off)
+    uint32_t lds_flat;   // LDS tiers: 1 = the flat 2-level index (IX_FLAT), 0 = the 3-level one
 };
 
 // Cut replay: after the replay, one workgroup per cut document resolves its segments' source
@@ -114,6 +115,15 @@ __host__ __device__ inline uint32_t lds_sb_capacity(uint32_t mb, uint32_t fill =
     const uint32_t opt = mb / fill + 3;
     return opt < sb_capacity(mb) ? opt : sb_capacity(mb);
 }
+// The flat LDS index (dt_replay.hip IX_FLAT): per block the packed counts (u32), its position
+// and the block at each position (u16 each); per 64 positions the packed visible | live totals.
+__host__ __device__ inline uint32_t flat_chunks(uint32_t mb) { return (mb + 63) / 64; }
+__host__ __device__ inline uint64_t flat_index_bytes(uint64_t mb) {
+    return ((4 * mb + 8 * ((mb + 1) / 2) + 4 * uint64_t(flat_chunks(uint32_t(mb)))) + 15) & ~uint64_t(15);
+}
+// The flat index serves the smallest LDS tier; a split costs O(blocks / 64) lane rounds, so it is
+// kept to documents of at most this many blocks.
+constexpr uint32_t FLAT_MAX_BLOCKS = 2048;
 constexpr uint32_t MAX_DOC_BLOCKS = 65535;   // block ids are u16 in the superblock lists
 
 // ---- device planner (dt_plan.hip) -------------------------------------------------------------

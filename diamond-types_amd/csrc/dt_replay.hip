@@ -151,11 +151,11 @@ template <typename T> DEV void at_or(T *p, T v) { __hip_atomic_fetch_or(p, v, __
 
 // Index accessors.  LDS tier: plain LDS (one wave owns the workgroup).  HBM tier: words that
 // atomics touch are read L2-coherently.
-template <bool L> DEV uint32_t ix(const uint32_t *p) {
+template <int L> DEV uint32_t ix(const uint32_t *p) {
     if (L) return *p;
     return ld_sc(p);
 }
-template <bool L> DEV uint32_t ix16(const uint16_t *p) { return *p; }
+template <int L> DEV uint32_t ix16(const uint16_t *p) { return *p; }
 
 enum ProfSlot { P_INS = 0, P_DEL, P_TOG, P_MAT, P_YJS, P_SPLIT, P_FIND, P_BLOAD, P_ORR, P_RUN, P_R1, P_R2, P_R3, P_N_YJS, P_N_SPLIT,
                 P_T1, P_T2, P_T3, P_N_DIRTY, P_N_LOAD, P_N };   // P_T*: retreat/advance pass split (entries + merge, counts, index)
@@ -213,24 +213,41 @@ DEV bool charge(Doc &D) {
 }
 template <bool PROF> DEV uint64_t tick() { return PROF ? __builtin_amdgcn_s_memtime() : 0; }
 
-// Block -> (superblock << 6 | index in its list).  The LDS tier keeps it in 16 bits (its
-// superblock ids stay below 1024), which lets six documents share a SIMD instead of five.
-template <bool L> DEV uint32_t opos_of(const Doc &D, uint32_t b) {
+// Index kinds (the template parameter L of the navigation code; nonzero = the index is in LDS):
+//   IX_HBM   3-level index in HBM (big documents, LDS overflow, transformed-ops mode)
+//   IX_LDS   3-level index in LDS (the big LDS tiers)
+//   IX_FLAT  2-level index in LDS (the smallest tier: friendsforever-sized documents).  The
+//            blocks in document order are one array ord[] (block id by position), opos16[b] is
+//            block b's position, and ctot[c] (held in D.top) packs the visible | live << 16
+//            totals of positions [64c, 64c + 64).  A split shifts ord[] right of the new block
+//            (O(blocks / 64) lane rounds; ~550 splits per friendsforever document) and moves one
+//            block's totals across each chunk boundary it passes.  8 bytes per block and 4 per 64
+//            blocks instead of 6 per block + 144 per superblock: friendsforever's index takes
+//            4.9 KB instead of 6.2 KB, so 32 documents share a CU's 160 KiB instead of 25.
+constexpr int IX_HBM = 0, IX_LDS = 1, IX_FLAT = 2;
+// Block -> (superblock << 6 | index in its list); flat index: block -> position.  The LDS tiers
+// keep it in 16 bits (superblock ids below 1024; positions below 65536).
+template <int L> DEV uint32_t opos_of(const Doc &D, uint32_t b) {
     if (L) return D.opos16[b];
     return ix<L>(D.opos + b);
 }
-template <bool L> DEV void set_opos(Doc &D, uint32_t b, uint32_t v) {
+template <int L> DEV void set_opos(Doc &D, uint32_t b, uint32_t v) {
     if (L) D.opos16[b] = uint16_t(v);
     else D.opos[b] = v;
 }
 
 // ---- navigation ------------------------------------------------------------------------------
 
-template <bool L> DEV uint32_t first_block(const Doc &D) {
+template <int L> DEV uint32_t first_block(const Doc &D) {
+    if (L == IX_FLAT) return U(D.sbl[0]);
     return U(ix16<L>(D.sbl + size_t(U(ix<L>(D.top)) >> 16) * SBC));
 }
 // Next block in document order, or NONE.
-template <bool L> DEV uint32_t next_block(const Doc &D, uint32_t b) {
+template <int L> DEV uint32_t next_block(const Doc &D, uint32_t b) {
+    if (L == IX_FLAT) {
+        const uint32_t p = U(D.opos16[b]) + 1;
+        return p < D.nb ? U(D.sbl[p]) : NONE;
+    }
     const uint32_t o = U(opos_of<L>(D, b));
     const uint32_t S = o >> 6, i = o & 63u;
     if (i + 1 < U(ix<L>(D.sbn + S))) return U(ix16<L>(D.sbl + size_t(S) * SBC + i + 1));
@@ -239,7 +256,8 @@ template <bool L> DEV uint32_t next_block(const Doc &D, uint32_t b) {
     return U(ix16<L>(D.sbl + size_t(U(ix<L>(D.top + p)) >> 16) * SBC));
 }
 // Document-order key of (block, slot).
-template <bool L> DEV uint32_t key_at(const Doc &D, uint32_t b, uint32_t s) {
+template <int L> DEV uint32_t key_at(const Doc &D, uint32_t b, uint32_t s) {
+    if (L == IX_FLAT) return (uint32_t(D.opos16[b]) << 6) | s;
     const uint32_t o = opos_of<L>(D, b);
     return (ix<L>(D.sbpos + (o >> 6)) << 12) | ((o & 63u) << 6) | s;
 }
@@ -265,12 +283,12 @@ DEV uint32_t find_slot(const Doc &D, uint32_t b, uint32_t item) {
     return s;
 }
 // Document-order key of an inserted item, per lane.
-template <bool L> DEV uint32_t key_of(const Doc &D, uint32_t item) {
+template <int L> DEV uint32_t key_of(const Doc &D, uint32_t item) {
     const uint32_t b = pc_blk(ld(D.pc + item));
     return key_at<L>(D, b, find_slot(D, b, item));
 }
 // Same for a wave-uniform item: one row load and a ballot.
-template <bool L> DEV uint32_t ukey_of(const Doc &D, uint32_t item) {
+template <int L> DEV uint32_t ukey_of(const Doc &D, uint32_t item) {
     const uint32_t b = U(pc_blk(ld(D.pc + item)));
     const u64 m = __ballot(D.items[size_t(b) * BLK + lane_id()] == item);
     return U(key_at<L>(D, b, first_lane(m)));
@@ -283,10 +301,41 @@ struct Found {
     uint32_t b, k;     // block, rank of the item among the block's visible items
     uint32_t S, tp;    // its superblock and that superblock's top position
 };
-template <bool L>
+template <int L>
 DEV bool find_vis(Doc &D, uint32_t p, Found &f) {
     const uint32_t l = lane_id();
     uint32_t base = 0, S = NONE;
+    if (L == IX_FLAT) {   // chunk totals, then the chunk's blocks
+        const uint32_t nc = (D.nb + 63) >> 6;
+        for (uint32_t c = 0; c < nc; c += 64) {
+            const uint32_t i = c + l;
+            const uint32_t w0 = D.top[min(i, nc - 1)];
+            const uint32_t v = i < nc ? (w0 & 0xFFFFu) : 0u;
+            const uint32_t inc = wave_scan(v);
+            const u64 m = __ballot(base + inc > p);
+            if (m) {
+                const uint32_t fl = first_lane(m);
+                S = U(c + fl);
+                base += bcast(inc - v, fl);
+                break;
+            }
+            base += bcast(inc, 63);
+        }
+        if (S == NONE) return false;
+        f.S = f.tp = S;
+        const uint32_t q = (S << 6) + l;
+        const uint32_t b0 = D.sbl[min(q, D.nb - 1)];
+        const uint32_t b = q < D.nb ? b0 : 0;
+        const uint32_t v0 = c_vis(D.cnt[b]);
+        const uint32_t v = q < D.nb ? v0 : 0;
+        const uint32_t inc = wave_scan(v);
+        const u64 m = __ballot(base + inc > p);
+        if (!m) return false;
+        const uint32_t fl = first_lane(m);
+        f.b = U(bcast(b, fl));
+        f.k = U(p - base - bcast(inc - v, fl));
+        return true;
+    }
     for (uint32_t c = 0; c < D.nsb; c += 64) {
         const uint32_t i = c + l;
         const uint32_t w0 = ix<L>(D.top + min(i, D.nsb - 1));   // clamped, then masked: no exec branch
@@ -329,9 +378,38 @@ DEV uint32_t select_bit(u64 m, uint32_t k) {
 
 // First block after b (document order) with a live item, or NONE (origin_right search,
 // merge.rs:405-423).
-template <bool L>
+template <int L>
 DEV uint32_t next_live_block(Doc &D, uint32_t b) {
     const uint32_t l = lane_id();
+    if (L == IX_FLAT) {
+        const uint32_t p0 = U(D.opos16[b]) + 1, nc = (D.nb + 63) >> 6;
+        uint32_t c = p0 >> 6;
+        {   // rest of p0's chunk
+            const uint32_t q = (c << 6) + l;
+            const uint32_t b0 = D.sbl[min(q, D.nb - 1)];
+            const bool in = q >= p0 && q < D.nb;
+            const uint32_t bl = in ? b0 : 0;
+            const uint32_t cl = c_live(D.cnt[bl]);
+            const u64 m = __ballot(in && cl != 0);
+            if (m) return U(bcast(bl, first_lane(m)));
+        }
+        for (c = c + 1; c < nc; c += 64) {   // later chunks by their live totals
+            if (!charge(D)) return NONE;
+            const uint32_t i = c + l;
+            const uint32_t t = D.top[min(i, nc - 1)] >> 16;
+            const u64 m = __ballot(i < nc && t != 0);
+            if (m) {
+                const uint32_t q = ((c + first_lane(m)) << 6) + l;
+                const uint32_t b0 = D.sbl[min(q, D.nb - 1)];
+                const uint32_t bl = q < D.nb ? b0 : 0;
+                const uint32_t cl = c_live(D.cnt[bl]);
+                const u64 m2 = __ballot(q < D.nb && cl != 0);
+                if (!m2) { fail(D, ErrCheckout, 19); return NONE; }
+                return U(bcast(bl, first_lane(m2)));
+            }
+        }
+        return NONE;
+    }
     const uint32_t o = U(opos_of<L>(D, b));
     uint32_t S = o >> 6;
     {   // rest of b's superblock
@@ -365,7 +443,7 @@ DEV uint32_t next_live_block(Doc &D, uint32_t b) {
 
 // Split the full superblock S (64 blocks): its upper half becomes a new superblock right after
 // it in the top order.
-template <bool L, bool XF>
+template <int L, bool XF>
 DEV void split_sb(Doc &D, uint32_t S) {
     const uint32_t l = lane_id();
     if (D.nsb >= D.max_sb) { fail(D, ErrCapacity, 21); return; }
@@ -413,7 +491,7 @@ DEV void split_sb(Doc &D, uint32_t S) {
 
 // Split the full block b (items in `it` lane by lane, masks mv / ml) at slot c: items [c, 64)
 // move to a new block b2 placed right after b in its superblock.
-template <bool L, bool XF>
+template <int L, bool XF>
 DEV uint32_t split_block(Doc &D, uint32_t b, uint32_t c, uint32_t it, u64 mv, u64 ml) {
     const uint32_t l = lane_id();
     if (D.nb >= D.max_blocks) { fail(D, ErrCapacity, 12); return 0; }
@@ -433,6 +511,42 @@ DEV uint32_t split_block(Doc &D, uint32_t b, uint32_t c, uint32_t it, u64 mv, u6
     if (l < 4) {   // both blocks' mask pairs in one store
         const u64 v = l == 0 ? (mv & lo) : l == 1 ? (ml & lo) : l == 2 ? mv_hi : ml_hi;
         st(D.m2 + 2 * size_t(l < 2 ? b : b2) + (l & 1), v);
+    }
+    if (L == IX_FLAT) {   // b2 goes to position pos + 1: shift ord[pos + 1, nb) right by one
+        const uint32_t pos = U(D.opos16[b]);
+        for (int hi = int(D.nb) - 1; hi > int(pos); hi -= 64) {   // highest chunk first
+            const int q = hi - int(l);
+            const bool mvl = q > int(pos);
+            uint32_t v = 0;
+            if (mvl) v = D.sbl[q];
+            wave_fence();
+            if (mvl) {
+                D.sbl[q + 1] = uint16_t(v);
+                D.opos16[v] = uint16_t(q + 1);
+                if (((q + 1) & 63) == 0) {   // v crosses into the next chunk: move its totals
+                    const uint32_t cv = D.cnt[v];
+                    const uint32_t w = c_vis(cv) | (c_live(cv) << 16);
+                    at_add(D.top + (uint32_t(q) >> 6), 0u - w);
+                    at_add(D.top + (uint32_t(q + 1) >> 6), w);
+                }
+            }
+            wave_fence();
+        }
+        if (l == 0) {
+            const uint32_t v2 = uint32_t(__popcll(mv_hi)), l2 = uint32_t(__popcll(ml_hi));
+            D.cnt[b2] = v2 * C_VIS + l2 * C_LIVE + (BLK - c) * C_ITEMS;
+            D.cnt[b] = uint32_t(__popcll(mv & lo)) * C_VIS + uint32_t(__popcll(ml & lo)) * C_LIVE + c * C_ITEMS;
+            D.sbl[pos + 1] = uint16_t(b2);
+            D.opos16[b2] = uint16_t(pos + 1);
+            if (((pos + 1) & 63) == 0) {   // b2's items leave b's chunk
+                const uint32_t w = v2 | (l2 << 16);
+                at_add(D.top + (pos >> 6), 0u - w);
+                at_add(D.top + ((pos + 1) >> 6), w);
+            }
+        }
+        wave_fence();
+        D.nb++;
+        return b2;
     }
     const uint32_t o = U(opos_of<L>(D, b));
     const uint32_t S = o >> 6, i = o & 63u, n = U(ix<L>(D.sbn + S));
@@ -469,12 +583,12 @@ DEV uint32_t split_block(Doc &D, uint32_t b, uint32_t c, uint32_t it, u64 mv, u6
 // capacity is sized for that fill; a document that still outgrows it is handed to the HBM
 // tier, which always cuts at the midpoint so every block keeps >= 32 items and
 // n_ins / 32 + 2 blocks suffice.
-template <bool L> DEV uint32_t cut_point(uint32_t s) { return L ? min(max(s, 16u), 48u) : BLK / 2; }
+template <int L> DEV uint32_t cut_point(uint32_t s) { return L ? min(max(s, 16u), 48u) : BLK / 2; }
 
 // Transformed-ops mode: the upstream position of slot s of block b -- the never-deleted items
 // before it in document order (MarkerMetrics upstream_len, metrics.rs:18-66; the position
 // integrate() / apply() report as BaseMoved, merge.rs:154-278, 457-556).
-template <bool L>
+template <int L>
 DEV uint32_t up_rank(Doc &D, uint32_t b, uint32_t s) {
     const uint32_t l = lane_id();
     const uint32_t o = U(opos_of<L>(D, b));
@@ -489,7 +603,7 @@ DEV uint32_t up_rank(Doc &D, uint32_t b, uint32_t s) {
 
 // Insert the run [lv, lv+k) before slot s of block b (all new items visible).  `it` holds the
 // block's items lane by lane (lanes >= the block count are don't-care); mv / ml its masks.
-template <bool L, bool PROF, bool XF>
+template <int L, bool PROF, bool XF>
 DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml, uint32_t lv, uint32_t k,
                     uint32_t ol, uint32_t orr, uint32_t tph, uint32_t c_in) {
     D.cb = NONE;
@@ -547,12 +661,16 @@ DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml,
             mu = m == 64 ? ins : ((mu & low) | ((mu & ~low) << m) | ins);
             if (l == 0) st(D.mup + b, mu);
         }
-        if (tph == NONE) tph = U(ix<L>(D.sbpos + (opos_of<L>(D, b) >> 6)));
+        if (tph == NONE) tph = L == IX_FLAT ? U(uint32_t(D.opos16[b]) >> 6) : U(ix<L>(D.sbpos + (opos_of<L>(D, b) >> 6)));
         if (l == 0) {   // the superblock's totals by atomic add: no dependent read
             D.cnt[b] = c + m * (C_VIS + C_LIVE + C_ITEMS + (XF ? C_UP : 0u));
             const uint32_t tp = tph;
-            at_add(D.top + tp, m);
-            at_add(D.tlive + tp, m);
+            if (L == IX_FLAT) {
+                at_add(D.top + tp, m | (m << 16));
+            } else {
+                at_add(D.top + tp, m);
+                at_add(D.tlive + tp, m);
+            }
             if (XF) at_add(D.tup + tp, m);
         }
         wave_fence();
@@ -598,7 +716,7 @@ DEV void agent_of(Doc &D, uint32_t lv, uint32_t &rank, uint32_t &seq) {
 // Every candidate's keys come in lane-parallel; the sequential scan state machine is resolved
 // with ballots: the first stopping lane ends the scan, and `scanning` is the state after the
 // last event lane before it.  Returns the insertion point in (b, s).
-template <bool L>
+template <int L>
 DEV void yjs_scan(Doc &D, uint32_t &b, uint32_t &s, uint32_t rb, uint32_t rs, uint32_t my_l, uint32_t my_r,
                   uint32_t ol_new, uint32_t orr_new, uint32_t lv) {
     const uint32_t l = lane_id();
@@ -682,7 +800,7 @@ DEV void yjs_scan(Doc &D, uint32_t &b, uint32_t &s, uint32_t rb, uint32_t rs, ui
 // Items and masks of block b (packed count c) into registers: items lane by lane, masks
 // wave-uniform.  A block whose masks a retreat/advance pass invalidated (DIRTY) gets them
 // rebuilt from the items' counts and stored back clean.
-template <bool L, bool PROF = false>
+template <int L, bool PROF = false>
 DEV void load_block(Doc &D, uint32_t b, uint32_t c, uint32_t &it, u64 &mv, u64 &ml) {
     const uint32_t l = lane_id();
     const uint32_t bc = c_items(c);
@@ -705,7 +823,7 @@ DEV void load_block(Doc &D, uint32_t b, uint32_t c, uint32_t &it, u64 &mv, u64 &
 
 // Apply an insert run at visible position pos (M2Tracker::apply Ins + integrate,
 // merge.rs:154-278, 383-455).
-template <bool L, bool PROF, bool XF>
+template <int L, bool PROF, bool XF>
 DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
     uint64_t tp = tick<PROF>();
     uint32_t b, kk = 0, tph = 0;   // tph: top position of b's superblock (first block: 0)
@@ -786,7 +904,7 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
 
 // Apply a delete run: n visible items from position pos (merge.rs:457-556).  LV lv+j targets
 // the j-th item (fwd) or the (n-1-j)-th item (reversed / backspace runs, op_metrics.rs:184-202).
-template <bool L, bool PROF, bool XF>
+template <int L, bool PROF, bool XF>
 DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
     const uint32_t l = lane_id();
     uint32_t j0 = 0;
@@ -852,7 +970,7 @@ DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
 // same item -- only a deleted item can be touched twice (two deletes of it, or a delete and its
 // own insert) -- are merged first.  Blocks whose visibility / liveness changed are marked
 // DIRTY; their masks are rebuilt when a command next loads them.
-template <bool L, bool PROF>
+template <int L, bool PROF>
 DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_pre) {
     const uint32_t l = lane_id();
     uint64_t tq = tick<PROF>();
@@ -950,7 +1068,13 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
         const bool flip = fv || fl;
         if (__ballot(flip && b == D.cb)) D.cb = NONE;
         if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_T2] += t - tq; tq = t; }
-        if (L) {   // LDS index: per-lane LDS atomics
+        if (L == IX_FLAT) {   // flat LDS index: the chunk's packed totals in one atomic
+            if (flip) {
+                at_add(D.top + (uint32_t(D.opos16[b]) >> 6), uint32_t(dv) + (uint32_t(dl) << 16));
+                at_add(D.cnt + b, uint32_t(dv) * C_VIS + uint32_t(dl) * C_LIVE);
+                at_or(D.cnt + b, C_DIRTY);
+            }
+        } else if (L) {   // LDS index: per-lane LDS atomics
             if (flip) {
                 const uint32_t tp = ix<L>(D.sbpos + (opos_of<L>(D, b) >> 6));
                 if (fv) at_add(D.top + tp, uint32_t(dv));
@@ -996,7 +1120,7 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
 constexpr uint32_t TOG_WAVES = DTGPU_TOG_WAVES;
 constexpr uint32_t TOG_MW_MIN = DTGPU_TOG_MW_MIN;   // entries: shorter passes stay on the replay wave
 __shared__ uint32_t tog_job[4];        // {off, n, go (0: the document is done), error}
-template <bool L>
+template <int L>
 DEV void toggle_chunks(Doc &D, uint32_t off, uint32_t n, uint32_t w0) {
     const uint32_t l = lane_id();
     uint32_t err = 0;
@@ -1024,9 +1148,13 @@ DEV void toggle_chunks(Doc &D, uint32_t off, uint32_t n, uint32_t w0) {
         const bool fv = act && ((oc == 1) != (nc == 1)), fl = act && ((oc != 0) != (nc != 0));
         if (fv || fl) {
             const uint32_t dv = fv ? (nc == 1 ? 1u : 0xFFFFFFFFu) : 0u, dl = fl ? (nc != 0 ? 1u : 0xFFFFFFFFu) : 0u;
-            const uint32_t tp = ix<L>(D.sbpos + (opos_of<L>(D, b) >> 6));
-            if (fv) at_add(D.top + tp, dv);
-            if (fl) at_add(D.tlive + tp, dl);
+            if (L == IX_FLAT) {
+                at_add(D.top + (uint32_t(D.opos16[b]) >> 6), dv + (dl << 16));
+            } else {
+                const uint32_t tp = ix<L>(D.sbpos + (opos_of<L>(D, b) >> 6));
+                if (fv) at_add(D.top + tp, dv);
+                if (fl) at_add(D.tlive + tp, dl);
+            }
             at_add(D.cnt + b, dv * C_VIS + dl * C_LIVE);
             at_or(D.cnt + b, C_DIRTY);
         }
@@ -1034,7 +1162,7 @@ DEV void toggle_chunks(Doc &D, uint32_t off, uint32_t n, uint32_t w0) {
     if (__ballot(err)) at_or(&tog_job[3], 1u);
 }
 // The replay wave's side: post the pass, take its share, wait for the others.
-template <bool L>
+template <int L>
 DEV void toggle_mw(Doc &D, uint32_t off, uint32_t n) {
     if (lane_id() == 0) { tog_job[0] = off; tog_job[1] = n; tog_job[2] = 1; tog_job[3] = 0; }
     __syncthreads();
@@ -1045,7 +1173,7 @@ DEV void toggle_mw(Doc &D, uint32_t off, uint32_t n) {
     D.cb = NONE;
 }
 // The other waves: passes until the replay wave reports the document done.
-template <bool L>
+template <int L>
 DEV void toggle_helper(Doc &D, uint32_t w) {
     for (;;) {
         __syncthreads();
@@ -1059,7 +1187,7 @@ DEV void toggle_helper(Doc &D, uint32_t w) {
 // (list/merge.rs:63-95).  G blocks per round keep that many dependent gathers in flight.
 // Visibility comes from the counts (the final advance to the tip leaves masks stale): the
 // count and the byte offset of every item are gathered together, so this adds no round trip.
-template <bool L>
+template <int L>
 DEV void materialise(Doc &D, GLOBAL_AS uint8_t *out, uint32_t cap, uint32_t &len_out, u64 &hash_out, uint32_t &items_out) {
     constexpr uint32_t G = 8;
     const uint32_t l = lane_id();
@@ -1068,13 +1196,20 @@ DEV void materialise(Doc &D, GLOBAL_AS uint8_t *out, uint32_t cap, uint32_t &len
     const bool ascii = U(vld(&D.desc->ascii)) != 0;
     uint32_t total = 0, items = 0;
     u64 h = 0;
-    for (uint32_t p = 0; p < D.nsb; p++) {
-        const uint32_t S = U(ix<L>(D.top + p)) >> 16;
-        const uint32_t n = U(ix<L>(D.sbn + S));
+    const uint32_t nlists = L == IX_FLAT ? 1u : D.nsb;   // the flat index is one list
+    for (uint32_t p = 0; p < nlists; p++) {
+        const uint16_t *list = D.sbl;
+        uint32_t n = D.nb, ncap = D.nb;
+        if (L != IX_FLAT) {
+            const uint32_t S = U(ix<L>(D.top + p)) >> 16;
+            n = U(ix<L>(D.sbn + S));
+            list = D.sbl + size_t(S) * SBC;
+            ncap = SBC;
+        }
         for (uint32_t i = 0; i < n; i += G) {
             // lane g < G fetches block g's id and item count
             const bool gl = l < G && i + l < n;
-            const uint32_t b0 = ix16<L>(D.sbl + size_t(S) * SBC + min(i + (l & (G - 1)), SBC - 1));
+            const uint32_t b0 = ix16<L>(list + min(i + (l & (G - 1)), ncap - 1));
             const uint32_t bl = gl ? b0 : 0;
             const uint32_t n0 = c_items(ix<L>(D.cnt + bl));
             const uint32_t nl = gl ? n0 : 0;
@@ -1193,12 +1328,26 @@ DEV bool seg_straddles(const Cmd *cmds, uint32_t c, uint32_t v) {
 constexpr uint32_t PH_FILL = 48;   // placeholder items per block (the HBM tier keeps >= 32)
 constexpr uint32_t PH_SB = 40;     // placeholder blocks per superblock
 // The tracker a segment starts from: u visible placeholder items in document order.
-template <bool L>
+template <int L>
 DEV bool init_phantoms(Doc &D, uint32_t u) {
     const uint32_t l = lane_id();
     const uint32_t base = U(vld(&D.desc->n_lv));   // placeholder ids follow the LVs
     const uint32_t nbp = (u + PH_FILL - 1) / PH_FILL, nsb = (nbp + PH_SB - 1) / PH_SB;
-    if (nbp + 1 > D.max_blocks || nsb + 1 > D.max_sb) { fail(D, ErrCapacity, 12); return false; }
+    if (nbp + 1 > D.max_blocks || (L != IX_FLAT && nsb + 1 > D.max_sb)) { fail(D, ErrCapacity, 12); return false; }
+    if (L == IX_FLAT) {   // block b at position b; chunk totals of 64 blocks
+        for (uint32_t b = l; b < nbp; b += 64) {
+            const uint32_t k = min(PH_FILL, u - b * PH_FILL);
+            D.cnt[b] = k * (C_VIS + C_LIVE + C_ITEMS);
+            D.opos16[b] = uint16_t(b);
+            D.sbl[b] = uint16_t(b);
+            st(D.m2 + 2 * size_t(b), lanes_below(k));
+            st(D.m2 + 2 * size_t(b) + 1, lanes_below(k));
+        }
+        for (uint32_t c = l; c < D.max_sb; c += 64) {   // max_sb: the chunk capacity
+            const uint32_t lo = min(u, c * 64 * PH_FILL), hi = min(u, (c + 1) * 64 * PH_FILL);
+            D.top[c] = (hi - lo) | ((hi - lo) << 16);
+        }
+    } else {
     for (uint32_t b = l; b < nbp; b += 64) {
         const uint32_t k = min(PH_FILL, u - b * PH_FILL);
         const uint32_t S = b / PH_SB, i = b % PH_SB;
@@ -1216,6 +1365,7 @@ DEV bool init_phantoms(Doc &D, uint32_t u) {
         D.top[S] = (S << 16) | nv;
         D.tlive[S] = nv;
     }
+    }
     for (uint32_t b = 0; b < nbp; b++) {   // rows: one wave store per block
         const uint32_t k = min(PH_FILL, u - b * PH_FILL);
         D.items[size_t(b) * BLK + l] = l < k ? base + b * PH_FILL + l : 0u;
@@ -1228,18 +1378,25 @@ DEV bool init_phantoms(Doc &D, uint32_t u) {
 }
 // A segment's visible items in document order as a source list (an LV, or SEG_PHANTOM | the
 // placeholder's index), gathered G blocks per round as materialise() does.
-template <bool L>
+template <int L>
 DEV void materialise_src(Doc &D, GLOBAL_AS uint32_t *src, uint32_t cap, uint32_t &len_out, uint32_t &items_out) {
     constexpr uint32_t G = 8;
     const uint32_t l = lane_id();
     const uint32_t n_lv = U(vld(&D.desc->n_lv));   // D.n_lv also counts the placeholders
     uint32_t total = 0, items = 0;
-    for (uint32_t p = 0; p < D.nsb; p++) {
-        const uint32_t S = U(ix<L>(D.top + p)) >> 16;
-        const uint32_t n = U(ix<L>(D.sbn + S));
+    const uint32_t nlists = L == IX_FLAT ? 1u : D.nsb;   // the flat index is one list
+    for (uint32_t p = 0; p < nlists; p++) {
+        const uint16_t *list = D.sbl;
+        uint32_t n = D.nb, ncap = D.nb;
+        if (L != IX_FLAT) {
+            const uint32_t S = U(ix<L>(D.top + p)) >> 16;
+            n = U(ix<L>(D.sbn + S));
+            list = D.sbl + size_t(S) * SBC;
+            ncap = SBC;
+        }
         for (uint32_t i = 0; i < n; i += G) {
             const bool gl = l < G && i + l < n;
-            const uint32_t b0 = ix16<L>(D.sbl + size_t(S) * SBC + min(i + (l & (G - 1)), SBC - 1));
+            const uint32_t b0 = ix16<L>(list + min(i + (l & (G - 1)), ncap - 1));
             const uint32_t bl = gl ? b0 : 0;
             const uint32_t n0 = c_items(ix<L>(D.cnt + bl));
             const uint32_t nl = gl ? n0 : 0;
@@ -1272,20 +1429,26 @@ DEV void materialise_src(Doc &D, GLOBAL_AS uint32_t *src, uint32_t cap, uint32_t
 // Debug-mode consistency check of the whole structure (DTGPU_DEBUG=1): returns 0 or a code.
 // Checks every block's counts against its masks (clean blocks) or against cv[] (DIRTY blocks),
 // and that pos[] names each item's block.
-template <bool L, bool XF>
+template <int L, bool XF>
 DEV uint32_t check_invariants(Doc &D, DocResult *res) {
     const uint32_t l = lane_id();
     const uint32_t n_ids = D.n_lv;   // LVs, then a segment's placeholders
     uint32_t blocks = 0;
-    for (uint32_t p = 0; p < D.nsb; p++) {
-        const uint32_t S = U(ix<L>(D.top + p)) >> 16;
-        if (U(ix<L>(D.sbpos + S)) != p) return 205;
-        const uint32_t n = U(ix<L>(D.sbn + S));
-        if (n == 0 || n >= SBC) return 206;
+    const uint32_t nlists = L == IX_FLAT ? (D.nb + 63) >> 6 : D.nsb;   // flat: chunks of 64 positions
+    for (uint32_t p = 0; p < nlists; p++) {
+        uint32_t S = p, n;
+        if (L == IX_FLAT) {
+            n = min(64u, D.nb - 64 * p);
+        } else {
+            S = U(ix<L>(D.top + p)) >> 16;
+            if (U(ix<L>(D.sbpos + S)) != p) return 205;
+            n = U(ix<L>(D.sbn + S));
+            if (n == 0 || n >= SBC) return 206;
+        }
         uint32_t tv = 0, tl = 0, tu = 0;
         for (uint32_t i = 0; i < n; i++) {
-            const uint32_t b = U(ix16<L>(D.sbl + size_t(S) * SBC + i));
-            if (U(opos_of<L>(D, b)) != ((S << 6) | i)) return 201;
+            const uint32_t b = U(ix16<L>(D.sbl + size_t(S) * (L == IX_FLAT ? 64u : SBC) + i));
+            if (U(opos_of<L>(D, b)) != (L == IX_FLAT ? 64 * p + i : ((S << 6) | i))) return 201;
             const uint32_t c = U(ix<L>(D.cnt + b));
             const uint32_t cnt = c_items(c);
             const bool dirty = (c & C_DIRTY) != 0;
@@ -1326,14 +1489,18 @@ DEV uint32_t check_invariants(Doc &D, DocResult *res) {
             blocks++;
         }
         if (tv != (U(ix<L>(D.top + p)) & 0xFFFFu)) return 203;
-        if (tl != U(ix<L>(D.tlive + p))) return 204;
+        if (tl != (L == IX_FLAT ? U(ix<L>(D.top + p)) >> 16 : U(ix<L>(D.tlive + p)))) return 204;
         if (XF && tu != U(ix<L>(D.tup + p))) return 210;
     }
     if (blocks != D.nb) return 208;
+    if (L == IX_FLAT) {   // chunks past the last position hold nothing
+        for (uint32_t c = nlists + l; c < D.max_sb; c += 64)
+            if (__ballot(D.top[c] != 0)) return 211;
+    }
     return 0;
 }
 
-template <bool L, bool PROF, bool XF, bool MW>
+template <int L, bool PROF, bool XF, bool MW>
 DEV void run_doc(Doc &D) {
     const uint32_t l = lane_id();
     D.nb = 1;
@@ -1356,7 +1523,10 @@ DEV void run_doc(Doc &D) {
     } else {
         // fresh tracker: one empty block in one superblock (per-LV words are written when their
         // item is inserted)
-        if (l == 0) {
+        if (L == IX_FLAT) {   // every chunk total starts at zero (chunks fill as blocks split)
+            for (uint32_t c = l; c < D.max_sb; c += 64) D.top[c] = 0;
+            if (l == 0) { D.cnt[0] = 0; D.opos16[0] = 0; D.sbl[0] = 0; }
+        } else if (l == 0) {
             D.cnt[0] = 0; set_opos<L>(D, 0, 0);
             D.sbl[0] = 0; D.sbn[0] = 1; D.sbpos[0] = 0; D.top[0] = 0; D.tlive[0] = 0;
             if (XF) { D.tup[0] = 0; st(D.mup, 0ull); }
@@ -1429,7 +1599,7 @@ DEV void run_doc(Doc &D) {
                     break;
                 default: fail(D, ErrCheckout, 18); break;
             }
-            if (D.debug && !D.err) {
+            if (PROF && (D.debug & 1u) && !D.err) {   // invariant checks: instrumented builds only
                 const uint32_t code = check_invariants<L, XF>(D, vld(&KP().results) + D.doc);
                 if (code) fail(D, ErrCheckout, code);
             }
@@ -1471,7 +1641,7 @@ DEV void run_doc(Doc &D) {
         res->lds = L ? 1u : 0u;
         res->fail_cmd = D.err ? ci : 0;
         res->fail_site = D.err ? D.site : 0;
-        if (PROF) {
+        if (PROF && (D.debug & 2u)) {
             D.prof[P_MAT] = tick<PROF>() - t_mat;
             for (int i = 0; i < P_T1; i++) res->dbg[i] = uint32_t(D.prof[i] >> (i < P_N_YJS ? 4 : 0));
             res->dbg[15] = uint32_t((tick<PROF>() - t_start) >> 4);
@@ -1496,6 +1666,16 @@ DEV void bind_index(Doc &D, uint8_t *base, uint32_t mb, uint32_t ms, bool narrow
     D.sbl = reinterpret_cast<uint16_t *>(w);
 }
 
+// The flat index (IX_FLAT) for `mb` blocks; layout must match flat_index_bytes().
+DEV void bind_index_flat(Doc &D, uint8_t *base, uint32_t mb) {
+    uint32_t *w = reinterpret_cast<uint32_t *>(base);
+    D.cnt = w; w += mb;
+    D.opos16 = reinterpret_cast<uint16_t *>(w); w += (mb + 1) / 2;
+    D.sbl = reinterpret_cast<uint16_t *>(w); w += (mb + 1) / 2;   // ord[]: block by position
+    D.top = w;                                                     // ctot[]: per 64 positions
+    D.opos = D.tlive = D.sbn = D.sbpos = nullptr;
+}
+
 // One 64-lane workgroup per document of the list (the hardware dispatcher is the work queue;
 // LDS per workgroup bounds how many documents share a CU).
 #ifndef DTGPU_REPLAY_WAVES
@@ -1503,8 +1683,10 @@ DEV void bind_index(Doc &D, uint8_t *base, uint32_t mb, uint32_t ms, bool narrow
 #endif
 // MW: TOG_WAVES waves per workgroup, the others helping with long retreat / advance passes
 // (the big LDS tiers: one or two documents per CU, so the extra waves cost no occupancy).
-template <bool LDS_INDEX, bool PROF, bool XF, bool MW = false>
-__global__ __launch_bounds__(MW ? 64 * TOG_WAVES : 64) __attribute__((amdgpu_waves_per_eu(DTGPU_REPLAY_WAVES))) void replay_kernel(BatchParams P) {
+// WAVES: the occupancy the compiler budgets registers for (the flat tier's documents are small
+// enough for 32 per CU, i.e. 8 waves per SIMD if the kernel takes <= 80 SGPRs and <= 64 VGPRs).
+template <int LDS_INDEX, bool PROF, bool XF, bool MW = false, int WAVES = DTGPU_REPLAY_WAVES>
+__global__ __launch_bounds__(MW ? 64 * TOG_WAVES : 64) __attribute__((amdgpu_waves_per_eu(WAVES))) void replay_kernel(BatchParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t di = U(blockIdx.x);
     uint32_t d;
@@ -1520,7 +1702,7 @@ __global__ __launch_bounds__(MW ? 64 * TOG_WAVES : 64) __attribute__((amdgpu_wav
     Doc D;
     D.doc = d;
     D.desc = P.docs + d;
-    D.debug = P.debug & 1u;
+    D.debug = P.debug & 3u;
     D.cmds = P.cmds + dd.cmd_off;
     D.ncmd = U(dd.ncmd);
     // item ids: the LVs, then a segment's placeholders (cut replay)
@@ -1532,7 +1714,13 @@ __global__ __launch_bounds__(MW ? 64 * TOG_WAVES : 64) __attribute__((amdgpu_wav
     D.m2 = P.m2 + 2 * dd.blk_off;
     D.max_blocks = U(dd.max_blocks);
     D.max_sb = sb_capacity(D.max_blocks);
-    if (LDS_INDEX) {
+    static_assert(!(XF && LDS_INDEX), "transformed-ops mode replays on the HBM index");
+    static_assert(!(MW && LDS_INDEX != IX_LDS), "helper waves serve the 3-level LDS tiers");
+    if (LDS_INDEX == IX_FLAT) {
+        if (D.max_blocks > P.lds_blocks) D.max_blocks = P.lds_blocks;
+        D.max_sb = flat_chunks(P.lds_blocks);   // chunk capacity
+        bind_index_flat(D, smem, P.lds_blocks);
+    } else if (LDS_INDEX) {
         if (D.max_blocks > P.lds_blocks) D.max_blocks = P.lds_blocks;
         D.max_sb = P.lds_sb;
         bind_index(D, smem, P.lds_blocks, D.max_sb, true);
@@ -1657,6 +1845,20 @@ __global__ __launch_bounds__(COMBINE_THREADS) void combine_kernel(CombineParams 
 
 static int launch_lds_tier(const BatchParams &q, hipStream_t s, bool prof) {
     if (!q.n_list) return OK;
+    if (q.lds_flat) {   // the flat index: small documents, one wave each
+        if (q.lds_blocks > FLAT_MAX_BLOCKS) return ErrArg;
+        size_t lds = size_t(flat_index_bytes(q.lds_blocks));
+        if (const char *pad = getenv("DTGPU_LDS_PAD")) lds += size_t(strtoul(pad, nullptr, 10));   // occupancy experiments
+        if (lds > 64 * 1024) return ErrArg;
+        // DTGPU_FLAT_WAVES: the register budget's occupancy (A/B; 1 = the compiler's choice)
+        int w = 8;
+        if (const char *e = getenv("DTGPU_FLAT_WAVES")) w = atoi(e);
+        if (prof) hipLaunchKernelGGL((dev::replay_kernel<dev::IX_FLAT, true, false>), dim3(q.n_list), dim3(64), lds, s, q);
+        else if (w == 8) hipLaunchKernelGGL((dev::replay_kernel<dev::IX_FLAT, false, false, false, 8>), dim3(q.n_list), dim3(64), lds, s, q);
+        else if (w == 7) hipLaunchKernelGGL((dev::replay_kernel<dev::IX_FLAT, false, false, false, 7>), dim3(q.n_list), dim3(64), lds, s, q);
+        else hipLaunchKernelGGL((dev::replay_kernel<dev::IX_FLAT, false, false, false, 1>), dim3(q.n_list), dim3(64), lds, s, q);
+        return hipGetLastError() == hipSuccess ? OK : ErrHip;
+    }
     size_t lds = size_t(index_bytes_ms(q.lds_blocks, q.lds_sb, true));
     if (const char *pad = getenv("DTGPU_LDS_PAD")) lds += size_t(strtoul(pad, nullptr, 10));   // occupancy experiments
     if (lds > 160 * 1024) return ErrArg;   // a tier cap above the CU's LDS
@@ -1669,21 +1871,21 @@ static int launch_lds_tier(const BatchParams &q, hipStream_t s, bool prof) {
     const bool mw = lds >= mw_min && lds + kStatic <= 160 * 1024 && !(tw && *tw == '1');
     // allow dynamic LDS up to the CU's 160 KiB: a per-function, per-device attribute, set on
     // every launch (cheap) so it holds on whatever device the batch runs
-    const void *fn = mw ? (prof ? reinterpret_cast<const void *>(&dev::replay_kernel<true, true, false, true>)
-                                : reinterpret_cast<const void *>(&dev::replay_kernel<true, false, false, true>))
-                        : (prof ? reinterpret_cast<const void *>(&dev::replay_kernel<true, true, false>)
-                                : reinterpret_cast<const void *>(&dev::replay_kernel<true, false, false>));
+    const void *fn = mw ? (prof ? reinterpret_cast<const void *>(&dev::replay_kernel<dev::IX_LDS, true, false, true>)
+                                : reinterpret_cast<const void *>(&dev::replay_kernel<dev::IX_LDS, false, false, true>))
+                        : (prof ? reinterpret_cast<const void *>(&dev::replay_kernel<dev::IX_LDS, true, false>)
+                                : reinterpret_cast<const void *>(&dev::replay_kernel<dev::IX_LDS, false, false>));
     if (lds > 64 * 1024 &&
         hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024 - (mw ? kStatic : 0))) != hipSuccess)
         return ErrHip;
     if (mw) {
         const dim3 blk(64 * dev::TOG_WAVES);
-        if (prof) hipLaunchKernelGGL((dev::replay_kernel<true, true, false, true>), dim3(q.n_list), blk, lds, s, q);
-        else hipLaunchKernelGGL((dev::replay_kernel<true, false, false, true>), dim3(q.n_list), blk, lds, s, q);
+        if (prof) hipLaunchKernelGGL((dev::replay_kernel<dev::IX_LDS, true, false, true>), dim3(q.n_list), blk, lds, s, q);
+        else hipLaunchKernelGGL((dev::replay_kernel<dev::IX_LDS, false, false, true>), dim3(q.n_list), blk, lds, s, q);
     } else if (prof) {
-        hipLaunchKernelGGL((dev::replay_kernel<true, true, false>), dim3(q.n_list), dim3(64), lds, s, q);
+        hipLaunchKernelGGL((dev::replay_kernel<dev::IX_LDS, true, false>), dim3(q.n_list), dim3(64), lds, s, q);
     } else {
-        hipLaunchKernelGGL((dev::replay_kernel<true, false, false>), dim3(q.n_list), dim3(64), lds, s, q);
+        hipLaunchKernelGGL((dev::replay_kernel<dev::IX_LDS, false, false>), dim3(q.n_list), dim3(64), lds, s, q);
     }
     return hipGetLastError() == hipSuccess ? OK : ErrHip;
 }
@@ -1691,11 +1893,11 @@ static int launch_lds_tier(const BatchParams &q, hipStream_t s, bool prof) {
 int launch_replay(const ReplayLaunch &r) {
     hipStream_t s = reinterpret_cast<hipStream_t>(r.stream);
     const BatchParams &large = *r.large;
-    bool prof = large.debug & 2u;
+    bool prof = (large.debug & 3u) != 0;   // invariant checks and cycle profiles: the instrumented kernels
     uint32_t n_lds = 0;
     const uint32_t *fb_count = nullptr;
     for (int t = 0; t < r.n_lds; t++) {
-        prof |= (r.lds[t].debug & 2u) != 0;
+        prof |= (r.lds[t].debug & 3u) != 0;
         n_lds += r.lds[t].n_list;
         if (r.lds[t].fb_count) fb_count = r.lds[t].fb_count;
     }
@@ -1739,8 +1941,8 @@ int launch_replay(const ReplayLaunch &r) {
     // HBM tier: its own list plus a slot per LDS-tier document that may be handed back
     const uint32_t grid = large.n_list + (large.fb_list ? large.fb_slots : 0);
     if (grid) {
-        if (prof) hipLaunchKernelGGL((dev::replay_kernel<false, true, false>), dim3(grid), dim3(64), 0, s, large);
-        else hipLaunchKernelGGL((dev::replay_kernel<false, false, false>), dim3(grid), dim3(64), 0, s, large);
+        if (prof) hipLaunchKernelGGL((dev::replay_kernel<dev::IX_HBM, true, false>), dim3(grid), dim3(64), 0, s, large);
+        else hipLaunchKernelGGL((dev::replay_kernel<dev::IX_HBM, false, false>), dim3(grid), dim3(64), 0, s, large);
         if (hipGetLastError() != hipSuccess) return ErrHip;
     }
     return OK;
@@ -1752,7 +1954,8 @@ int launch_replay_xf(const BatchParams &large, void *stream) {
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (!large.n_list) return OK;
     if (!large.xf || !large.mup || !large.tup) return ErrArg;
-    hipLaunchKernelGGL((dev::replay_kernel<false, false, true>), dim3(large.n_list), dim3(64), 0, s, large);
+    if (large.debug & 3u) hipLaunchKernelGGL((dev::replay_kernel<dev::IX_HBM, true, true>), dim3(large.n_list), dim3(64), 0, s, large);
+    else hipLaunchKernelGGL((dev::replay_kernel<dev::IX_HBM, false, true>), dim3(large.n_list), dim3(64), 0, s, large);
     return hipGetLastError() == hipSuccess ? OK : ErrHip;
 }
 

@@ -52,6 +52,12 @@ uint64_t lds_fill_setting() {
     if (const char *e = getenv("DTGPU_LDS_FILL")) f = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
     return f;
 }
+// The smallest LDS tier replays on the flat 2-level index (dt_replay.hip IX_FLAT), unless
+// DTGPU_FLAT=0 selects the 3-level one (A/B).
+bool flat_setting() {
+    const char *e = getenv("DTGPU_FLAT");
+    return !(e && *e == '0');
+}
 // The <= 64-chain planner: two phases (walk order, then lane-parallel steps) unless
 // DTGPU_PLAN_SPLIT=0 selects the one-phase walk (A/B).
 uint32_t plan_split_setting() {
@@ -364,6 +370,7 @@ dtgpu_status set_tier_params(dtgpu_batch &B, const BatchParams &base) {
         q.n_list = uint32_t(B.tier_list[t].size());
         q.lds_blocks = B.tier_blocks[t];
         q.lds_sb = lds_sb_capacity(q.lds_blocks);
+        q.lds_flat = t == 0 && flat_setting() && q.lds_blocks <= FLAT_MAX_BLOCKS ? 1u : 0u;
         off += B.tier_list[t].size();
         if (fb) { q.fb_count = B.d_fb.p; q.fb_list = B.d_fb.p + 1; }
     }
@@ -500,7 +507,8 @@ std::vector<uint32_t> seg_candidates(size_t n, SegSettings &sc, int n_cu, NOps n
     if (!sc.on) return c;
     uint64_t total = 0;
     for (size_t i = 0; i < n; i++) total += n_ops(i);
-    sc.ops_per_seg = std::max<uint64_t>(sc.ops_per_seg, total / (uint64_t(std::max(n_cu, 1)) * 8));
+    const char *fair = getenv("DTGPU_SEG_FAIR");   // "0": no fair-share floor (experiments)
+    if (!(fair && *fair == '0')) sc.ops_per_seg = std::max<uint64_t>(sc.ops_per_seg, total / (uint64_t(std::max(n_cu, 1)) * 8));
     for (size_t i = 0; i < n; i++)
         if (n_ops(i) >= 2 * sc.ops_per_seg) c.push_back(uint32_t(i));
     return c;
