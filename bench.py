@@ -427,9 +427,9 @@ def main():
     if os.path.exists(tpath):   # HBM bytes per launch from rocprofv3 PMC runs of this command
         tj = json.load(open(tpath))
         pass_traffic = tj.get("hbm_bytes_per_pass")
-        rk = [v for k, v in tj.get("per_kernel", {}).items() if "replay_kernel<true" in k]
-        if rk:
-            traffic = (2 * rk[0]["fetch_kib"] + rk[0]["write_kib"]) * 1024
+        rk = [v for k, v in tj.get("per_kernel", {}).items() if k.startswith("replay_kernel")]
+        if rk:   # every replay tier's launch of the pass (tools/traffic.py)
+            traffic = sum(2 * v["fetch_kib"] + v["write_kib"] for v in rk) * 1024
 
     out = {
         "metric": "merged ops/sec (whole node) for batched checkout",
@@ -457,7 +457,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "replay_kernel (dominant kernel of the pass)", "kernel_ms": replay_ms,
-                     "pass": {"kernels": "prep_kernel + plan_kernel + replay_kernel", "ms": avg_kernel_ms,
+                     "pass": {"kernels": "prep_kernel x2 + chain_kernel + walk_kernel + plan_kernel + replay_kernel tiers (+ combine_kernel)", "ms": avg_kernel_ms,
                               "prep_ms": prep_ms, "plan_ms": plan_ms, "replay_ms": replay_ms,
                               "achieved": alg_bytes / (avg_kernel_ms / 1000.0) / 1e9,
                               "frac": alg_bytes / (avg_kernel_ms / 1000.0) / 1e9 / HBM_PEAK_GBS,

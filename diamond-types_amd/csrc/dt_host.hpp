@@ -7,6 +7,7 @@
 //   AgentRun  <- client_with_localtime (src/causalgraph/agent_assignment/mod.rs:29-45)
 //   GraphEntry<- GraphEntryInternal   (src/causalgraph/graph/mod.rs:25-53)
 #pragma once
+#include <cstddef>
 #include <cstdint>
 #include <functional>
 #include <string>

@@ -1312,6 +1312,11 @@ int launch_walk(const PlanParams &q, void *stream, bool csr) {
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const size_t wlds = size_t(pdev::WALK_DOCS) * 2 * (PLAN_TODO_CAP + (q.lds_entries + 1) / 2);
     const dim3 grid((q.n_docs + pdev::WALK_DOCS - 1) / pdev::WALK_DOCS);
+    if (wlds > 160 * 1024) return ErrArg;
+    if (wlds > 64 * 1024) {   // past the default dynamic-LDS limit (documents near PLAN_MAX_LDS_ENTRIES)
+        const void *fn = csr ? reinterpret_cast<const void *>(&pdev::walk_kernel<true>) : reinterpret_cast<const void *>(&pdev::walk_kernel<false>);
+        if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024)) != hipSuccess) return ErrHip;
+    }
     if (csr) hipLaunchKernelGGL(pdev::walk_kernel<true>, grid, dim3(64), wlds, s, q);
     else hipLaunchKernelGGL(pdev::walk_kernel<false>, grid, dim3(64), wlds, s, q);
     return hipGetLastError() == hipSuccess ? OK : ErrHip;

@@ -80,6 +80,21 @@ DEV uint32_t shfl(uint32_t v, uint32_t src) {
     return uint32_t(__builtin_amdgcn_ds_bpermute(int(src << 2), int(v)));
 }
 DEV u64 lanes_below(uint32_t l) { return l >= 64 ? ~0ull : ((1ull << l) - 1ull); }
+// Set bits of m below this lane (v_mbcnt: two VALU ops, no 64-bit shifts).
+DEV uint32_t bits_below(u64 m) {
+    return __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+}
+// The replay's scalar issue is its bottleneck (one SALU per SIMD per 4 cycles; +48 SALU per
+// command costs the full issue time, +48 VALU 40 % of it): per-lane flags are kept as 0/1
+// integers in VGPRs.  A bool per lane is a lane mask in SGPRs, and each &&, || or ! on it is a
+// 64-bit scalar op; the empty asm keeps the compiler from folding the integer back into one.
+DEV uint32_t vflag(bool c) {
+    uint32_t x = c ? 1u : 0u;
+    asm volatile("" : "+v"(x));
+    return x;
+}
+// __ballot with the mask straight from the compare (the HIP wrapper adds a select and a compare).
+#define BALLOT(c) __ballot(c)
 
 // Inclusive wave prefix sum over 64 lanes with DPP: Hillis-Steele inside each 16-lane row
 // (row_shr 1/2/4/8), then row_bcast:15 and row_bcast:31 carry the row totals forward.
@@ -193,6 +208,11 @@ struct Doc {
     // same state (every change is stored); a toggle touching the block drops it.
     uint32_t cb, cit;
     u64 cmv, cml;
+    // flat index: the chunk the last position lookup landed in and its block ids (lane = position
+    // in the chunk), so the next lookup gathers that chunk's counts beside the chunk totals --
+    // one LDS round trip instead of three while the edits stay in one chunk (64 blocks, ~2.7k
+    // chars of friendsforever).  A split that shifts those positions drops it.
+    uint32_t fc, ford;
     // transformed-ops mode (iter_xf_operations): per block the never-deleted mask, per top
     // position the never-deleted total, per LV the transformed position written out
     u64 *mup;
@@ -290,7 +310,7 @@ template <int L> DEV uint32_t key_of(const Doc &D, uint32_t item) {
 // Same for a wave-uniform item: one row load and a ballot.
 template <int L> DEV uint32_t ukey_of(const Doc &D, uint32_t item) {
     const uint32_t b = U(pc_blk(ld(D.pc + item)));
-    const u64 m = __ballot(D.items[size_t(b) * BLK + lane_id()] == item);
+    const u64 m = BALLOT(D.items[size_t(b) * BLK + lane_id()] == item);
     return U(key_at<L>(D, b, first_lane(m)));
 }
 
@@ -300,6 +320,7 @@ template <int L> DEV uint32_t ukey_of(const Doc &D, uint32_t item) {
 struct Found {
     uint32_t b, k;     // block, rank of the item among the block's visible items
     uint32_t S, tp;    // its superblock and that superblock's top position
+    uint32_t c;        // the block's packed counts (flat index), NONE: not gathered
 };
 template <int L>
 DEV bool find_vis(Doc &D, uint32_t p, Found &f) {
@@ -307,12 +328,15 @@ DEV bool find_vis(Doc &D, uint32_t p, Found &f) {
     uint32_t base = 0, S = NONE;
     if (L == IX_FLAT) {   // chunk totals, then the chunk's blocks
         const uint32_t nc = (D.nb + 63) >> 6;
+        // the cached chunk's counts, requested with the first 64 chunk totals
+        const uint32_t cc = D.fc;
+        const uint32_t cw = D.cnt[cc != NONE ? D.ford : 0u];
         for (uint32_t c = 0; c < nc; c += 64) {
             const uint32_t i = c + l;
             const uint32_t w0 = D.top[min(i, nc - 1)];
             const uint32_t v = i < nc ? (w0 & 0xFFFFu) : 0u;
             const uint32_t inc = wave_scan(v);
-            const u64 m = __ballot(base + inc > p);
+            const u64 m = BALLOT(base + inc > p);
             if (m) {
                 const uint32_t fl = first_lane(m);
                 S = U(c + fl);
@@ -324,16 +348,25 @@ DEV bool find_vis(Doc &D, uint32_t p, Found &f) {
         if (S == NONE) return false;
         f.S = f.tp = S;
         const uint32_t q = (S << 6) + l;
-        const uint32_t b0 = D.sbl[min(q, D.nb - 1)];
+        uint32_t b0, w;
+        if (S == cc) {   // the cached chunk: its counts are in
+            b0 = D.ford;
+            w = cw;
+        } else {
+            b0 = D.sbl[min(q, D.nb - 1)];
+            w = D.cnt[b0];
+            D.fc = S;
+            D.ford = b0;
+        }
         const uint32_t b = q < D.nb ? b0 : 0;
-        const uint32_t v0 = c_vis(D.cnt[b]);
-        const uint32_t v = q < D.nb ? v0 : 0;
+        const uint32_t v = q < D.nb ? c_vis(w) : 0;
         const uint32_t inc = wave_scan(v);
-        const u64 m = __ballot(base + inc > p);
+        const u64 m = BALLOT(base + inc > p);
         if (!m) return false;
         const uint32_t fl = first_lane(m);
         f.b = U(bcast(b, fl));
         f.k = U(p - base - bcast(inc - v, fl));
+        f.c = U(bcast(w, fl));
         return true;
     }
     for (uint32_t c = 0; c < D.nsb; c += 64) {
@@ -342,7 +375,7 @@ DEV bool find_vis(Doc &D, uint32_t p, Found &f) {
         const uint32_t w = i < D.nsb ? w0 : 0;
         const uint32_t v = w & 0xFFFFu;
         const uint32_t inc = wave_scan(v);
-        const u64 m = __ballot(base + inc > p);
+        const u64 m = BALLOT(base + inc > p);
         if (m) {
             const uint32_t fl = first_lane(m);
             S = U(bcast(w, fl) >> 16);
@@ -354,13 +387,14 @@ DEV bool find_vis(Doc &D, uint32_t p, Found &f) {
     }
     if (S == NONE) return false;
     f.S = S;
+    f.c = NONE;
     const uint32_t n = U(ix<L>(D.sbn + S));
     const uint32_t b0 = ix16<L>(D.sbl + size_t(S) * SBC + l);   // a list row holds SBC slots
     const uint32_t b = l < n ? b0 : 0;
     const uint32_t v0 = c_vis(ix<L>(D.cnt + b));
     const uint32_t v = l < n ? v0 : 0;
     const uint32_t inc = wave_scan(v);
-    const u64 m = __ballot(base + inc > p);
+    const u64 m = BALLOT(base + inc > p);
     if (!m) return false;
     const uint32_t fl = first_lane(m);
     f.b = U(bcast(b, fl));
@@ -373,7 +407,7 @@ DEV uint32_t select_bit(u64 m, uint32_t k) {
     const uint32_t l = lane_id();
     const bool set = (m >> l) & 1ull;
     const uint32_t before = uint32_t(__popcll(m & lanes_below(l)));
-    return first_lane(__ballot(set && before == k));
+    return first_lane(BALLOT(set && before == k));
 }
 
 // First block after b (document order) with a live item, or NONE (origin_right search,
@@ -390,20 +424,20 @@ DEV uint32_t next_live_block(Doc &D, uint32_t b) {
             const bool in = q >= p0 && q < D.nb;
             const uint32_t bl = in ? b0 : 0;
             const uint32_t cl = c_live(D.cnt[bl]);
-            const u64 m = __ballot(in && cl != 0);
+            const u64 m = BALLOT(in && cl != 0);
             if (m) return U(bcast(bl, first_lane(m)));
         }
         for (c = c + 1; c < nc; c += 64) {   // later chunks by their live totals
             if (!charge(D)) return NONE;
             const uint32_t i = c + l;
             const uint32_t t = D.top[min(i, nc - 1)] >> 16;
-            const u64 m = __ballot(i < nc && t != 0);
+            const u64 m = BALLOT(i < nc && t != 0);
             if (m) {
                 const uint32_t q = ((c + first_lane(m)) << 6) + l;
                 const uint32_t b0 = D.sbl[min(q, D.nb - 1)];
                 const uint32_t bl = q < D.nb ? b0 : 0;
                 const uint32_t cl = c_live(D.cnt[bl]);
-                const u64 m2 = __ballot(q < D.nb && cl != 0);
+                const u64 m2 = BALLOT(q < D.nb && cl != 0);
                 if (!m2) { fail(D, ErrCheckout, 19); return NONE; }
                 return U(bcast(bl, first_lane(m2)));
             }
@@ -417,21 +451,21 @@ DEV uint32_t next_live_block(Doc &D, uint32_t b) {
         const uint32_t b0 = ix16<L>(D.sbl + size_t(S) * SBC + l);
         const uint32_t bl = l < n ? b0 : 0;
         const uint32_t cl = c_live(ix<L>(D.cnt + bl));
-        const u64 m = __ballot(l >= i0 && l < n && cl != 0);
+        const u64 m = BALLOT(l >= i0 && l < n && cl != 0);
         if (m) return U(bcast(bl, first_lane(m)));
     }
     for (uint32_t p = U(ix<L>(D.sbpos + S)) + 1; p < D.nsb; p += 64) {
         if (!charge(D)) return NONE;
         const uint32_t i = p + l;
         const uint32_t tl = ix<L>(D.tlive + min(i, D.nsb - 1));
-        const u64 m = __ballot(i < D.nsb && tl != 0);
+        const u64 m = BALLOT(i < D.nsb && tl != 0);
         if (m) {
             S = U(ix<L>(D.top + p + first_lane(m)) >> 16);
             const uint32_t n = U(ix<L>(D.sbn + S));
             const uint32_t b0 = ix16<L>(D.sbl + size_t(S) * SBC + l);
             const uint32_t bl = l < n ? b0 : 0;
             const uint32_t cl = c_live(ix<L>(D.cnt + bl));
-            const u64 m2 = __ballot(l < n && cl != 0);
+            const u64 m2 = BALLOT(l < n && cl != 0);
             if (!m2) { fail(D, ErrCheckout, 19); return NONE; }
             return U(bcast(bl, first_lane(m2)));
         }
@@ -514,6 +548,7 @@ DEV uint32_t split_block(Doc &D, uint32_t b, uint32_t c, uint32_t it, u64 mv, u6
     }
     if (L == IX_FLAT) {   // b2 goes to position pos + 1: shift ord[pos + 1, nb) right by one
         const uint32_t pos = U(D.opos16[b]);
+        if (D.fc != NONE && pos + 1 < 64 * (D.fc + 1)) D.fc = NONE;   // the cached chunk's positions shift
         for (int hi = int(D.nb) - 1; hi > int(pos); hi -= 64) {   // highest chunk first
             const int q = hi - int(l);
             const bool mvl = q > int(pos);
@@ -644,11 +679,7 @@ DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml,
         // with one store; only the new items get a block in pos[] (shifted ones stay put)
         const uint32_t shifted = shfl(it, l >= m ? l - m : l);
         it = l < s ? it : (l < s + m ? lv + (l - s) : shifted);
-#ifdef DTGPU_ROW_MASKED   // experiment: store only the slots the insert changed
-        if (l >= s && l < bc + m) items[l] = it;
-#else
         items[l] = it;   // the whole row: slots past the count are don't-care
-#endif
         if (l >= s && l < s + m) st(D.pc + it, pc_of(b, 1u));
         if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_R1] += t - tr; tr = t; }
         const u64 low = lanes_below(s);
@@ -699,13 +730,13 @@ DEV void agent_of(Doc &D, uint32_t lv, uint32_t &rank, uint32_t &seq) {
         const uint32_t stride = (n + 63) / 64;
         const uint32_t idx = lo + l * stride;
         const bool ok = l * stride < n && aruns[4 * idx] <= lv;
-        const uint32_t k = uint32_t(__popcll(__ballot(ok)));
+        const uint32_t k = uint32_t(__popcll(BALLOT(ok)));
         const uint32_t nlo = lo + (k ? k - 1 : 0) * stride;
         n = min(stride, lo + n - nlo);
         lo = nlo;
     }
     const bool ok = l < n && aruns[4 * (lo + l)] <= lv;
-    const uint32_t k = uint32_t(__popcll(__ballot(ok)));
+    const uint32_t k = uint32_t(__popcll(BALLOT(ok)));
     const uint32_t j = U(lo + (k ? k - 1 : 0));
     rank = U(aruns[4 * j + 1]);
     seq = U(aruns[4 * j + 2]) + (lv - U(aruns[4 * j]));
@@ -753,18 +784,18 @@ DEV void yjs_scan(Doc &D, uint32_t &b, uint32_t &s, uint32_t rb, uint32_t rs, ui
         const bool l_eq = ol_o == ol_new, l_root = ol_o == ROOT_ID;
         const bool l_gt = !l_eq && !l_root && l > cs && ol_o == prev;
         uint32_t kl = l_eq ? my_l : (l_root ? 0u : (l_gt ? my_l + 1u : 0u));
-        if (__ballot(inr && !l_eq && !l_root && !l_gt)) {
+        if (BALLOT(inr && !l_eq && !l_root && !l_gt)) {
             if (inr && !l_eq && !l_root && !l_gt) kl = key_of<L>(D, ol_o) + 1u;
         }
         // kr = key(origin_right): only where the scan state machine reads it
         uint32_t kr = 0xFFFFFFFFu;
         const bool need_r = inr && kl == my_l && orr_o != orr_new && orr_o != END_ID;
-        if (__ballot(need_r)) {
+        if (BALLOT(need_r)) {
             if (need_r) kr = key_of<L>(D, orr_o);
         }
         const bool tie = inr && kl == my_l && orr_o == orr_new;
         bool new_lt = false;
-        for (u64 mt = __ballot(tie); mt; mt &= mt - 1) {
+        for (u64 mt = BALLOT(tie); mt; mt &= mt - 1) {
             const uint32_t f = first_lane(mt);
             uint32_t r2, s2;
             agent_of(D, U(bcast(o, f)), r2, s2);
@@ -774,10 +805,10 @@ DEV void yjs_scan(Doc &D, uint32_t &b, uint32_t &s, uint32_t rb, uint32_t rs, ui
         const bool stop = inr && (kl < my_l || (tie && new_lt));
         const bool setv = inr && kl == my_l && orr_o != orr_new && kr < my_r;
         const bool clr = inr && kl == my_l && !stop && !setv;
-        const u64 ms = __ballot(stop);
+        const u64 ms = BALLOT(stop);
         const uint32_t lim = ms ? first_lane(ms) : end;
         const u64 below = lanes_below(lim);
-        const u64 mset = __ballot(setv) & below, mclr = __ballot(clr) & below;
+        const u64 mset = BALLOT(setv) & below, mclr = BALLOT(clr) & below;
         if (mset | mclr) {
             const int lc = mclr ? int(last_lane(mclr)) : -1;
             const int ls = mset ? int(last_lane(mset)) : -1;
@@ -809,8 +840,8 @@ DEV void load_block(Doc &D, uint32_t b, uint32_t c, uint32_t &it, u64 &mv, u64 &
     it = l < bc ? it0 : 0;
     if (c & C_DIRTY) {
         const uint32_t k = pc_cnt(ld(D.pc + it));   // lanes past the count read item 0's word
-        mv = __ballot(l < bc && k == 1u);
-        ml = __ballot(l < bc && k != 0u);
+        mv = BALLOT(l < bc && k == 1u);
+        ml = BALLOT(l < bc && k != 0u);
         st(D.m2 + 2 * size_t(b) + (l & 1u), (l & 1u) ? ml : mv);
         if (l == 0) D.cnt[b] = c & ~C_DIRTY;
         wave_fence();
@@ -827,6 +858,7 @@ template <int L, bool PROF, bool XF>
 DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
     uint64_t tp = tick<PROF>();
     uint32_t b, kk = 0, tph = 0;   // tph: top position of b's superblock (first block: 0)
+    uint32_t fcnt = NONE;          // b's packed counts when the lookup gathered them
     if (pos == 0) {
         b = first_block<L>(D);
     } else {
@@ -835,9 +867,10 @@ DEV void do_insert(Doc &D, uint32_t lv, uint32_t k, uint32_t pos) {
         b = f.b;
         kk = f.k;
         tph = f.tp;
+        fcnt = f.c;
     }
     if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_FIND] += t - tp; tp = t; }
-    const uint32_t c0 = U(ix<L>(D.cnt + b));
+    const uint32_t c0 = L == IX_FLAT && fcnt != NONE ? fcnt : U(ix<L>(D.cnt + b));
     const uint32_t bc = c_items(c0);
     uint32_t cb = c0 & ~C_DIRTY;   // b's packed counts once its masks are current
     uint32_t it;
@@ -913,7 +946,7 @@ DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
         Found f;
         if (!find_vis<L>(D, pos, f)) { fail(D, ErrCheckout, 14); return; }
         const uint32_t b = f.b, kk = f.k, tpos = f.tp;
-        const uint32_t c0 = U(ix<L>(D.cnt + b));
+        const uint32_t c0 = L == IX_FLAT && f.c != NONE ? f.c : U(ix<L>(D.cnt + b));
         uint32_t it;
         u64 mv, ml;
         if (b == D.cb) { it = D.cit; mv = D.cmv; ml = D.cml; }
@@ -923,7 +956,7 @@ DEV void do_delete(Doc &D, uint32_t lv, uint32_t n, uint32_t pos, bool fwd) {
         const uint32_t take = min(avail, n - j0);
         const uint32_t r = uint32_t(__popcll(mv & lanes_below(l)));
         const bool sel = ((mv >> l) & 1ull) && r >= kk && r < kk + take;
-        const u64 selm = __ballot(sel);
+        const u64 selm = BALLOT(sel);
         if (uint32_t(__popcll(selm)) != take || take == 0) { fail(D, ErrCheckout, 15); return; }
         u64 mu = 0;
         uint32_t base = 0;
@@ -991,7 +1024,8 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
     if (n == 0) return;
     const uint32_t last = off + n - 1;
     uint32_t e_cur = have_pre ? pre : D.tlist[min(off + l, last)];
-    uint32_t e_nx = D.tlist[min(off + 64 + l, last)];
+    uint32_t e_nx = 0;
+    if (n > 64) e_nx = D.tlist[min(off + 64 + l, last)];
     uint32_t it_cur;
     bool del_cur, bad_cur;
     resolve(0, e_cur, it_cur, del_cur, bad_cur);
@@ -1013,12 +1047,12 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
             resolve(j + 64, e_cur, it_cur, del_cur, bad_cur);
             e_nx = D.tlist[min(off + j + 128 + l, last)];
         }
-        if (__ballot(bad)) { fail(D, ErrCheckout, 16); return; }
+        if (BALLOT(bad)) { fail(D, ErrCheckout, 16); return; }
         if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_T1] += t - tq; tq = t; }
         // lanes whose item another lane also touches: every lane's item against every other
         // lane's (63 lane rotations, four independent chains); only those go through the merge
         // (a few delete lanes: the merge loop over them is cheaper than the rotations)
-        const u64 dmask = __ballot(act && del);
+        const u64 dmask = BALLOT(act && del);
         bool dup = del;
         if (__popcll(dmask) > 4) {
             dup = false;
@@ -1034,9 +1068,9 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
                 dup |= (r0 == x) | (r1 == x) | (r2 == x) | (r3 == x);
             }
         }
-        for (u64 dm = __ballot(act && dup); dm;) {   // each round retires >= 1 lane
+        for (u64 dm = BALLOT(act && dup); dm;) {   // each round retires >= 1 lane
             const uint32_t t = bcast(item, first_lane(dm));
-            const u64 same = __ballot(act && item == t);
+            const u64 same = BALLOT(act && item == t);
             if (same & (same - 1)) {
                 const bool mine = (same >> l) & 1ull;
                 const int32_t sum = int32_t(wave_sum(mine ? uint32_t(d) : 0u));
@@ -1064,9 +1098,9 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
             dv = fv ? (nc == 1 ? 1 : -1) : 0;
             dl = fl ? (nc != 0 ? 1 : -1) : 0;
         }
-        if (__ballot(bad)) { fail(D, ErrCheckout, 16); return; }
+        if (BALLOT(bad)) { fail(D, ErrCheckout, 16); return; }
         const bool flip = fv || fl;
-        if (__ballot(flip && b == D.cb)) D.cb = NONE;
+        if (BALLOT(flip && b == D.cb)) D.cb = NONE;
         if (PROF) { const uint64_t t = tick<PROF>(); D.prof[P_T2] += t - tq; tq = t; }
         if (L == IX_FLAT) {   // flat LDS index: the chunk's packed totals in one atomic
             if (flip) {
@@ -1083,10 +1117,10 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
                 at_or(D.cnt + b, C_DIRTY);
             }
         } else {   // HBM index: one atomic per distinct block (a global atomic is a memory-side request)
-            for (u64 pend = __ballot(flip); pend;) {   // each round retires >= 1 lane
+            for (u64 pend = BALLOT(flip); pend;) {   // each round retires >= 1 lane
                 const uint32_t f = first_lane(pend);
                 const uint32_t bb = bcast(b, f);
-                const u64 same = __ballot(flip && b == bb);
+                const u64 same = BALLOT(flip && b == bb);
                 const bool mine = (same >> l) & 1ull;
                 const uint32_t sv = wave_sum(mine ? uint32_t(dv) : 0u), sl = wave_sum(mine ? uint32_t(dl) : 0u);
                 if (l == f) {
@@ -1159,7 +1193,7 @@ DEV void toggle_chunks(Doc &D, uint32_t off, uint32_t n, uint32_t w0) {
             at_or(D.cnt + b, C_DIRTY);
         }
     }
-    if (__ballot(err)) at_or(&tog_job[3], 1u);
+    if (BALLOT(err)) at_or(&tog_job[3], 1u);
 }
 // The replay wave's side: post the pass, take its share, wait for the others.
 template <int L>
@@ -1300,13 +1334,13 @@ DEV uint32_t seg_cmd(const Cmd *cmds, uint32_t ncmd, uint32_t v) {
         const uint32_t step = max(1u, (hi - lo + 63) / 64), b = lo;
         const uint32_t i = b + l * step;
         const bool in = i < hi;
-        const u64 m = __ballot(in && first_apply_lv(cmds, ncmd, i) >= v);
+        const u64 m = BALLOT(in && first_apply_lv(cmds, ncmd, i) >= v);
         if (m) {
             const uint32_t f = first_lane(m);
             hi = b + f * step;
             lo = f ? b + (f - 1) * step + 1 : b;
         } else {
-            lo = b + last_lane(__ballot(in)) * step + 1;
+            lo = b + last_lane(BALLOT(in)) * step + 1;
         }
         lo = U(lo);
         hi = U(hi);
@@ -1323,7 +1357,7 @@ DEV bool seg_straddles(const Cmd *cmds, uint32_t c, uint32_t v) {
             if ((x.op & 15u) != CMD_TOG) { bad = x.lv + x.len > v; break; }
         }
     }
-    return __ballot(bad) != 0;
+    return BALLOT(bad) != 0;
 }
 constexpr uint32_t PH_FILL = 48;   // placeholder items per block (the HBM tier keeps >= 32)
 constexpr uint32_t PH_SB = 40;     // placeholder blocks per superblock
@@ -1456,8 +1490,8 @@ DEV uint32_t check_invariants(Doc &D, DocResult *res) {
             if (dirty) {   // stale masks: check the counts against cv[] instead
                 const uint32_t i2 = l < cnt ? D.items[size_t(b) * BLK + l] : 0;
                 const uint32_t k = l < cnt && i2 < n_ids ? pc_cnt(ld(D.pc + i2)) : 0u;
-                mv = __ballot(l < cnt && k == 1u);
-                ml = __ballot(l < cnt && k != 0u);
+                mv = BALLOT(l < cnt && k == 1u);
+                ml = BALLOT(l < cnt && k != 0u);
             }
             if (uint32_t(__popcll(mv)) != c_vis(c) || uint32_t(__popcll(ml)) != c_live(c)) return 207;
             if (XF && uint32_t(__popcll(U64(ld(D.mup + b)))) != c_up(c)) return 209;
@@ -1477,7 +1511,7 @@ DEV uint32_t check_invariants(Doc &D, DocResult *res) {
                     if (w != b || find_slot(D, b, it) != l) bad = true;
                 }
             } else if (((mv | ml) >> l) & 1) bad = true;
-            const u64 bm = __ballot(bad);
+            const u64 bm = BALLOT(bad);
             if (bm) {
                 if (l == first_lane(bm)) {
                     res->dbg[0] = b; res->dbg[1] = l; res->dbg[2] = cnt; res->dbg[3] = it; res->dbg[4] = w;
@@ -1495,7 +1529,7 @@ DEV uint32_t check_invariants(Doc &D, DocResult *res) {
     if (blocks != D.nb) return 208;
     if (L == IX_FLAT) {   // chunks past the last position hold nothing
         for (uint32_t c = nlists + l; c < D.max_sb; c += 64)
-            if (__ballot(D.top[c] != 0)) return 211;
+            if (BALLOT(D.top[c] != 0)) return 211;
     }
     return 0;
 }
@@ -1537,6 +1571,8 @@ DEV void run_doc(Doc &D) {
     D.cb = NONE;
     D.cit = 0;
     D.cmv = D.cml = 0;
+    D.fc = NONE;
+    D.ford = 0;
     if (PROF) for (int i = 0; i < P_N; i++) D.prof[i] = 0;
     const uint64_t t_start = tick<PROF>();
     // commands are fetched 64 at a time (one per lane) and broadcast with readlane; the first
@@ -1548,56 +1584,38 @@ DEV void run_doc(Doc &D) {
         const uint32_t n_here = min(64u, D.ncmd - base);
         Cmd pre = {0, 0, 0, 0};
         pre = D.cmds[min(base + l, D.ncmd - 1)];   // lanes past n_here are never read
-        for (uint32_t j = 0; j < n_here && !D.err; j++) {
+        // The chunk's commands checked lane-parallel: a malformed one (an unknown op, an apply
+        // run outside the LVs) ends the replay at its index; the retreat / advance passes are a
+        // mask, so each command's look-ahead is one bit test.  (The scalar unit is what a
+        // batch's replay is bound by: per-command bookkeeping is kept off it.)
+        const uint32_t op_l = pre.op & 15u;
+        const bool apply_l = op_l == CMD_INS || op_l == CMD_DEL;
+        const u64 bad_cmds = BALLOT(l < n_here && (op_l > CMD_TOG || (apply_l && (pre.len == 0 || pre.lv >= D.n_lv ||
+                                                                               pre.len > D.n_lv - pre.lv))));
+        const u64 tog_cmds = BALLOT(l < n_here && op_l == CMD_TOG);
+        const uint32_t n_ok = bad_cmds ? first_lane(bad_cmds) : n_here;
+        for (uint32_t j = 0; j < n_ok && !D.err; j++) {
             ci = base + j;
             const uint32_t op = U(bcast(pre.op, j)), a = U(bcast(pre.lv, j)), n = U(bcast(pre.len, j)),
                            pos = U(bcast(pre.pos, j));
-            if (!charge(D)) break;
             uint32_t nx_pf = 0;
             bool nx_ok = false;
-            if (j + 1 < n_here && (U(bcast(pre.op, j + 1)) & 15u) == CMD_TOG) {
+            if ((tog_cmds >> j) & 2ull) {   // the next command is a pass: its first entries now
                 const uint32_t o2 = U(bcast(pre.lv, j + 1)), n2 = U(bcast(pre.len, j + 1));
                 if (n2) nx_pf = D.tlist[o2 + min(l, n2 - 1)];
                 nx_ok = true;
             }
             const uint64_t t0 = tick<PROF>();
-#ifdef DTGPU_SALU_PAD   // experiment: extra independent scalar adds per command (SALU issue-bound?)
-            {
-                uint32_t x0 = ci, x1 = x0 + 1, x2 = x0 + 2, x3 = x0 + 3;
-#pragma unroll
-                for (int q = 0; q < DTGPU_SALU_PAD; q++)
-                    asm volatile("s_add_u32 %0, %0, 1\n\ts_add_u32 %1, %1, 1\n\ts_add_u32 %2, %2, 1\n\ts_add_u32 %3, %3, 1"
-                                 : "+s"(x0), "+s"(x1), "+s"(x2), "+s"(x3));
-                D.site += (x0 + x1 + x2 + x3 == 0x12345u) ? 1u : 0u;
-            }
-#endif
-#ifdef DTGPU_VALU_PAD   // experiment: extra independent vector adds per command (VALU issue-bound?)
-            {
-                uint32_t x0 = l, x1 = l + 1, x2 = l + 2, x3 = l + 3;
-#pragma unroll
-                for (int q = 0; q < DTGPU_VALU_PAD; q++)
-                    asm volatile("v_add_u32 %0, %0, 1\n\tv_add_u32 %1, %1, 1\n\tv_add_u32 %2, %2, 1\n\tv_add_u32 %3, %3, 1"
-                                 : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
-                if (__ballot(x0 + x1 + x2 + x3 == 0x12345u)) D.site++;
-            }
-#endif
-            switch (op & 15u) {
-                case CMD_INS:
-                    if (n == 0 || a >= D.n_lv || n > D.n_lv - a) { fail(D, ErrCheckout, 17); break; }
-                    do_insert<L, PROF, XF>(D, a, n, pos);
-                    if (PROF) D.prof[P_INS] += tick<PROF>() - t0;
-                    break;
-                case CMD_DEL:
-                    if (n == 0 || a >= D.n_lv || n > D.n_lv - a) { fail(D, ErrCheckout, 17); break; }
-                    do_delete<L, PROF, XF>(D, a, n, pos, (op & 16u) != 0);
-                    if (PROF) D.prof[P_DEL] += tick<PROF>() - t0;
-                    break;
-                case CMD_TOG:
-                    if (MW && n >= TOG_MW_MIN) toggle_mw<L>(D, a, n);
-                    else toggle_pass<L, PROF>(D, a, n, pf, pf_ok);
-                    if (PROF) D.prof[P_TOG] += tick<PROF>() - t0;
-                    break;
-                default: fail(D, ErrCheckout, 18); break;
+            if ((op & 15u) == CMD_INS) {
+                do_insert<L, PROF, XF>(D, a, n, pos);
+                if (PROF) D.prof[P_INS] += tick<PROF>() - t0;
+            } else if ((op & 15u) == CMD_DEL) {
+                do_delete<L, PROF, XF>(D, a, n, pos, (op & 16u) != 0);
+                if (PROF) D.prof[P_DEL] += tick<PROF>() - t0;
+            } else {
+                if (MW && n >= TOG_MW_MIN) toggle_mw<L>(D, a, n);
+                else toggle_pass<L, PROF>(D, a, n, pf, pf_ok);
+                if (PROF) D.prof[P_TOG] += tick<PROF>() - t0;
             }
             if (PROF && (D.debug & 1u) && !D.err) {   // invariant checks: instrumented builds only
                 const uint32_t code = check_invariants<L, XF>(D, vld(&KP().results) + D.doc);
@@ -1605,6 +1623,10 @@ DEV void run_doc(Doc &D) {
             }
             pf = nx_pf;
             pf_ok = nx_ok;
+        }
+        if (bad_cmds && !D.err) {
+            ci = base + n_ok;
+            fail(D, ErrCheckout, (U(bcast(pre.op, n_ok)) & 15u) > CMD_TOG ? 18u : 17u);
         }
     }
     // an LDS-tier document that outgrew its optimistic block capacity is queued for the HBM
@@ -1875,7 +1897,7 @@ static int launch_lds_tier(const BatchParams &q, hipStream_t s, bool prof) {
                                 : reinterpret_cast<const void *>(&dev::replay_kernel<dev::IX_LDS, false, false, true>))
                         : (prof ? reinterpret_cast<const void *>(&dev::replay_kernel<dev::IX_LDS, true, false>)
                                 : reinterpret_cast<const void *>(&dev::replay_kernel<dev::IX_LDS, false, false>));
-    if (lds > 64 * 1024 &&
+    if (lds + (mw ? kStatic : 0) > 64 * 1024 &&
         hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024 - (mw ? kStatic : 0))) != hipSuccess)
         return ErrHip;
     if (mw) {

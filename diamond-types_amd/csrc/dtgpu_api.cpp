@@ -446,8 +446,12 @@ bool seg_input_from_device(const dtgpu_decoded &Dd, size_t i, SegInput &si, hipS
 bool add_segments(dtgpu_batch &B, uint32_t i, const std::vector<SegCut> &cuts, int tier, uint32_t,
                   uint64_t lds_fill, uint64_t &pc_total, uint64_t &blk_total, uint64_t &gidx_total, uint64_t &src_total) {
     std::vector<uint32_t> mb(cuts.size(), 0);
-    for (size_t k = 1; k < cuts.size(); k++) {   // placeholders 48 per block, then the inserts
-        const uint64_t m = (uint64_t(cuts[k].u) + 47) / 48 + cuts[k].ins / 32 + 3;
+    for (size_t k = 1; k < cuts.size(); k++) {
+        // placeholders 48 per block, then the inserts -- and at least what the HBM tier's
+        // midpoint splits guarantee (every block keeps >= 32 items, so (u + ins) / 32 + 2
+        // blocks hold any placement of the inserts among the placeholders)
+        const uint64_t m = std::max<uint64_t>((uint64_t(cuts[k].u) + 47) / 48 + cuts[k].ins / 32 + 3,
+                                              (uint64_t(cuts[k].u) + cuts[k].ins) / 32 + 3);
         if (m > std::min<uint64_t>(LOC_MAX_BLOCKS, MAX_DOC_BLOCKS)) return false;
         mb[k] = uint32_t(m);
     }

@@ -66,6 +66,8 @@ extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *h
     std::vector<int32_t> front;   // every query's versions, a then b
     const uint32_t out_cap = uint32_t(4 * std::max<size_t>(span_cap, 1));
     const uint32_t c_cap = uint32_t(std::min<size_t>(common_cap, 1u << 24));
+    // every query's common-frontier slots in one u32-indexed arena (as the frontier arena's 2^28 check)
+    if (uint64_t(nq) * c_cap > (uint64_t(1) << 28)) return DTGPU_ERR_ARG;
     auto npar_of = [&](uint32_t ent_off, uint32_t n_ent) -> uint64_t {
         return ents[4 * (size_t(ent_off) + n_ent) + 3] - ents[4 * size_t(ent_off) + 3];
     };

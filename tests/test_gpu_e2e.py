@@ -36,6 +36,30 @@ def test_friendsforever_device_staged():
     assert b.host_planned() == [0] * 64
 
 
+@pytest.mark.parametrize("copies", [2048, 10000])
+def test_headline_batch_matches_golden(copies):
+    """The bench's own path (bench.py defaults: friendsforever x 10,000 device-staged, timed
+    passes): every document's (length, hash) equals the golden endContent, on the flat LDS tier
+    at full occupancy.  2,048 copies are replayed whole (no cut replay: a batch that fills the
+    GPU is left uncut)."""
+    want = G.trace("friendsforever_flat")["endContent"].encode()
+    h = dt_amd.text_hash(want)
+    b = dt_amd.Batch(docs=[G.dt_bytes("friendsforever")] * copies, staging="device")
+    b.run()
+    b.sync()
+    for _ in range(2):
+        assert b.run_timed() > 0
+    res = b.results()
+    bad = [i for i, r in enumerate(res) if r["status"] != 0 or r["text_len"] != len(want) or r["text_hash"] != h]
+    assert not bad, f"{len(bad)} documents differ from the golden text, first {bad[:5]}"
+    assert b.text(copies - 1) == want
+    assert b.host_planned() == [0] * copies
+    st = b.doc_stats(copies // 2)
+    assert st["lds_index"] == 1 and st["fail_site"] == 0
+    if copies == 2048:
+        assert all(b.segments(i) == [] for i in range(0, copies, 97))
+
+
 @pytest.mark.parametrize("name", ["git-makefile", "node_nodecc"])
 def test_large_docs_device_staged(name):
     data = G.dt_bytes(name)

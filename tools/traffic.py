@@ -1,40 +1,80 @@
 """HBM traffic per checkout pass from rocprofv3 PMC runs (FETCH_SIZE and WRITE_SIZE in separate
-passes, MI355X_MICROARCH.md HBM section): for each checkout kernel the last dispatch of the run
-is taken (earlier ones are the staging sizing pass and warmups); bytes = 2 * FETCH_SIZE (gfx950
-reports half of a wide read) + WRITE_SIZE, both in KiB.
+passes, MI355X_MICROARCH.md HBM section).  Every dispatch of the LAST checkout pass of the run
+is summed: walking back from the last replay / combine dispatch through the pass kernels (prep
+stages, chain, walk, plan, replay tiers, combine, the fallback-counter fill) to the previous
+pass's last replay / combine dispatch -- run the profiled command with a warmup pass, so that
+the staging kernels (decode, the planner's sizing pass) are never counted.  bytes = 2 *
+FETCH_SIZE (gfx950 reports half of a wide read) + WRITE_SIZE, both in KiB.
 Usage: python tools/traffic.py FETCH_DIR WRITE_DIR OUT.json"""
 import csv
 import glob
 import json
 import os
+import re
 import sys
 
-KERNELS = ("prep_kernel", "plan_kernel", "replay_kernel")
+PASS = ("prep_kernel", "chain_kernel", "walk_kernel", "plan_kernel", "replay_kernel", "combine_kernel",
+        "fillBuffer")
+END = ("replay_kernel", "combine_kernel")
 
 
-def last_per_kernel(d, counter):
-    last = {}
+def short(name):
+    """Kernel name without the namespace and parameter list, template arguments kept."""
+    m = re.search(r"(\w+_kernel\w*(?:<[^()]*>)?)", name)
+    return m.group(1) if m else name.split("(")[0][-60:]
+
+
+def dispatches(d, counter):
+    """{dispatch id: (kernel name, summed counter value)} over every CSV in d."""
+    out = {}
     for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            if r["Counter_Name"] != counter or not any(k in r["Kernel_Name"] for k in KERNELS):
+            if r["Counter_Name"] != counter:
                 continue
-            key = r["Kernel_Name"]
             did = int(r["Dispatch_Id"])
-            prev = last.get(key)
-            if prev is None or did > prev[0]:
-                last[key] = (did, 0.0)
-            if last[key][0] == did:
-                last[key] = (did, last[key][1] + float(r["Counter_Value"]))
-    return {k: v[1] for k, v in last.items()}
+            name, v = out.get(did, (r["Kernel_Name"], 0.0))
+            out[did] = (name, v + float(r["Counter_Value"]))
+    return out
+
+
+def last_pass(disp):
+    """Dispatch ids of the last checkout pass (see the module docstring)."""
+    ids = sorted(disp)
+    i = len(ids) - 1
+    while i >= 0 and not any(k in disp[ids[i]][0] for k in END):
+        i -= 1
+    picked = []
+    seen_body = False
+    while i >= 0:
+        name = disp[ids[i]][0]
+        if not any(k in name for k in PASS):
+            break
+        is_end = any(k in name for k in END)
+        if is_end and seen_body:
+            break   # the previous pass's replay
+        if not is_end and "fillBuffer" not in name:
+            seen_body = True
+        picked.append(ids[i])
+        i -= 1
+    return sorted(picked)
 
 
 def main():
-    fetch = last_per_kernel(sys.argv[1], "FETCH_SIZE")
-    write = last_per_kernel(sys.argv[2], "WRITE_SIZE")
-    per = {k: {"fetch_kib": fetch.get(k, 0.0), "write_kib": write.get(k, 0.0)} for k in set(fetch) | set(write)}
+    fetch = dispatches(sys.argv[1], "FETCH_SIZE")
+    write = dispatches(sys.argv[2], "WRITE_SIZE")
+    fp, wp = last_pass(fetch), last_pass(write)
+    per = {}
+    for ids, src, key in ((fp, fetch, "fetch_kib"), (wp, write, "write_kib")):
+        for did in ids:
+            k = short(src[did][0])
+            e = per.setdefault(k, {"fetch_kib": 0.0, "write_kib": 0.0, "dispatches": 0})
+            e[key] += src[did][1]
+            if key == "fetch_kib":
+                e["dispatches"] += 1
     total = sum(2 * v["fetch_kib"] + v["write_kib"] for v in per.values()) * 1024
     out = {"hbm_bytes_per_pass": total, "per_kernel": per,
-           "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024, last dispatch of each kernel"}
+           "dispatches": {"fetch": [short(fetch[i][0]) for i in fp], "write": [short(write[i][0]) for i in wp]},
+           "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024, every dispatch of the last checkout pass"}
     json.dump(out, open(sys.argv[3], "w"), indent=1)
     print(json.dumps(out))
 
