@@ -185,6 +185,57 @@ def single_doc_latency(data, gpu, staging):
     return {"gpu_ms": g, "cpu_ms": sorted(ts)[2], "cpu_cores": 1, "doc": "first document of the workload"}
 
 
+def single_doc_table(gpu, staging):
+    """SURVEY.md 8(d) single-document latency for every benchmark_data trace (bench.sh:5-7 pins
+    one core): the GPU checkout pass of a one-document batch (median of 5 after a warmup) next
+    to the C oracle's checkout_tip on one host thread, fast-forwarding a linear history as the
+    reference does (dto_checkout_tip_ff, merge.rs:811-840; the tracker otherwise).  `cut_ms` is
+    the host's cut analysis for the document (dtgpu_oplog_cut_ranges: where the history is one
+    version, the boundary the reference fast-forwards across), which staging runs before the
+    pass when it replays the document as segments; `gpu_with_cut_ms` counts it in.  Every text
+    is checked: the .dt files against the oracle, the JSON traces against their endContent."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import golden_data as G
+    import dt_amd
+    from oracle.oracle import OpLog as OracleOpLog, oplog_from_trace
+    rows = []
+
+    def med(fn, k=5):
+        fn()
+        ts = []
+        for _ in range(k):
+            t0 = time.perf_counter()
+            out = fn()
+            ts.append((time.perf_counter() - t0) * 1e3)
+        return sorted(ts)[k // 2], out
+    for name in list(G.DT_FILES) + list(G.JSON_TRACES):
+        if name in G.DT_FILES:
+            data = G.dt_bytes(name)
+            o = OracleOpLog.load_from(data)
+            want = None
+        else:
+            t = G.trace(name)
+            data = dt_amd.apply_edits_push_merge(t["txns"]).encode()
+            o = oplog_from_trace(t["txns"])
+            want = t["endContent"].encode()
+        cpu_ms, (text, ff) = med(o.checkout_tip_ff_bytes)
+        if want is None:
+            want = text
+        assert text == want, f"{name}: oracle checkout differs"
+        b = dt_amd.Batch(docs=[data], device=gpu, staging=staging)
+        b.run()
+        b.sync()
+        g = sorted(b.run_timed() for _ in range(5))[2]
+        assert b.results()[0]["status"] == 0 and b.text(0) == want, f"{name}: GPU checkout differs"
+        h = dt_amd.ListOpLog.load_from(data)
+        cut_ms, _ = med(h.cut_ranges)
+        segs = len(b.segments(0))
+        rows.append({"trace": name, "merged_ops": len(o), "gpu_ms": g, "cut_ms": cut_ms,
+                     "gpu_with_cut_ms": g + (cut_ms if segs else 0.0), "segments": segs,
+                     "cpu_ms": cpu_ms, "cpu_path": "fast-forward" if ff else "tracker", "cpu_cores": 1})
+    return rows
+
+
 def e2e_leg(batch, docs, steps, expect, total_lv):
     """`.dt` bytes in HBM -> text: device decode (dt_decode.hip) + planner inputs (dt_prep.hip) +
     walk plan + replay, re-run `steps` times on the device-staged batch (HIP events per kernel).
@@ -477,6 +528,8 @@ def main():
     if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(pool, args.cpu_seconds, args.cpu_cores, args.workload)
         out["single_doc_latency"] = single_doc_latency(pool[0], gpu, staging)
+        if staging == "device":
+            out["single_doc_table"] = single_doc_table(gpu, staging)
         out["cpu_config0"] = cpu_config0()
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -108,6 +108,15 @@ DEV uint32_t wave_scan(uint32_t x) {
     x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x143, 0xC, 0xF, false));
     return x;
 }
+// The same over lanes 0..31 only (lanes 32..63 left partial): one DPP step fewer.
+DEV uint32_t wave_scan32(uint32_t x) {
+    x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x111, 0xF, 0xF, false));
+    x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x112, 0xF, 0xF, false));
+    x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x114, 0xF, 0xF, false));
+    x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x118, 0xF, 0xF, false));
+    x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x142, 0xA, 0xF, false));
+    return x;
+}
 DEV uint32_t wave_sum(uint32_t v) { return uint32_t(__builtin_amdgcn_readlane(int(wave_scan(v)), 63)); }
 DEV u64 wave_sum64(u64 v) {
 #pragma unroll
@@ -331,21 +340,15 @@ DEV bool find_vis(Doc &D, uint32_t p, Found &f) {
         // the cached chunk's counts, requested with the first 64 chunk totals
         const uint32_t cc = D.fc;
         const uint32_t cw = D.cnt[cc != NONE ? D.ford : 0u];
-        for (uint32_t c = 0; c < nc; c += 64) {
-            const uint32_t i = c + l;
-            const uint32_t w0 = D.top[min(i, nc - 1)];
-            const uint32_t v = i < nc ? (w0 & 0xFFFFu) : 0u;
-            const uint32_t inc = wave_scan(v);
-            const u64 m = BALLOT(base + inc > p);
-            if (m) {
-                const uint32_t fl = first_lane(m);
-                S = U(c + fl);
-                base += bcast(inc - v, fl);
-                break;
-            }
-            base += bcast(inc, 63);
+        {   // at most 32 chunks (FLAT_MAX_BLOCKS): one scan over lanes 0..31
+            const uint32_t w0 = D.top[min(l, nc - 1)];
+            const uint32_t v = l < nc ? (w0 & 0xFFFFu) : 0u;
+            const uint32_t inc = wave_scan32(v);
+            const u64 m = BALLOT(inc > p) & 0xFFFFFFFFull;
+            if (!m) return false;
+            S = first_lane(m);
+            base = bcast(inc - v, S);
         }
-        if (S == NONE) return false;
         f.S = f.tp = S;
         const uint32_t q = (S << 6) + l;
         uint32_t b0, w;
