@@ -651,6 +651,32 @@ DEV void insert_run(Doc &D, uint32_t b, uint32_t s, uint32_t it, u64 mv, u64 ml,
         const uint32_t r0 = up_rank<L>(D, b, s);
         for (uint32_t j = l; j < k0; j += 64) D.xf[lv0 + j] = r0 + j;
     }
+    if (!XF && c_in != NONE && c_items(c_in) + k <= BLK) {
+        // the common case as straight-line code: the run fits the block (no split, one round)
+        const uint32_t shifted = shfl(it, l >= k ? l - k : l);
+        it = l < s ? it : (l < s + k ? lv + (l - s) : shifted);
+        D.items[size_t(b) * BLK + l] = it;
+        if (l >= s && l < s + k) st(D.pc + it, pc_of(b, 1u));
+        const u64 low = lanes_below(s);
+        const u64 ins = lanes_below(k) << s;
+        mv = k == 64 ? ins : ((mv & low) | ((mv & ~low) << k) | ins);
+        ml = k == 64 ? ins : ((ml & low) | ((ml & ~low) << k) | ins);
+        st(D.m2 + 2 * size_t(b) + (l & 1u), (l & 1u) ? ml : mv);
+        if (tph == NONE) tph = L == IX_FLAT ? U(uint32_t(D.opos16[b]) >> 6) : U(ix<L>(D.sbpos + (opos_of<L>(D, b) >> 6)));
+        if (l == 0) {
+            D.cnt[b] = c_in + k * (C_VIS + C_LIVE + C_ITEMS);
+            if (L == IX_FLAT) {
+                at_add(D.top + tph, k | (k << 16));
+            } else {
+                at_add(D.top + tph, k);
+                at_add(D.tlive + tph, k);
+            }
+        }
+        if (l < k) D.ao[lv + l] = u64(l == 0 ? ol : lv + l - 1) | (u64(orr) << 32);
+        wave_fence();
+        D.cb = b; D.cit = it; D.cmv = mv; D.cml = ml;
+        return;
+    }
     while (k > 0) {   // each round inserts >= 1 item or splits (bounded by max_blocks)
         // b's packed counts: the caller's clean copy on the first round, reloaded after a split
         const uint32_t c = c_in != NONE ? c_in : U(ix<L>(D.cnt + b));
@@ -1059,22 +1085,24 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
         bool dup = del;
         if (__popcll(dmask) > 4) {
             dup = false;
+            // (a running min of xors: equality tests OR-ed as lane masks would each be a scalar op)
             const uint32_t x = act ? item : (0x80000000u | l);   // inactive lanes never match
             uint32_t r0 = x, r1 = shfl(x, (l + 16) & 63u), r2 = shfl(x, (l + 32) & 63u), r3 = shfl(x, (l + 48) & 63u);
-            dup = (r1 == x) | (r2 == x) | (r3 == x);
+            uint32_t mn = min(min(r1 ^ x, r2 ^ x), r3 ^ x);
 #pragma unroll
             for (int k = 1; k < 16; k++) {
                 r0 = uint32_t(__builtin_amdgcn_mov_dpp(int(r0), 0x13C, 0xF, 0xF, false));   // wave_ror:1
                 r1 = uint32_t(__builtin_amdgcn_mov_dpp(int(r1), 0x13C, 0xF, 0xF, false));
                 r2 = uint32_t(__builtin_amdgcn_mov_dpp(int(r2), 0x13C, 0xF, 0xF, false));
                 r3 = uint32_t(__builtin_amdgcn_mov_dpp(int(r3), 0x13C, 0xF, 0xF, false));
-                dup |= (r0 == x) | (r1 == x) | (r2 == x) | (r3 == x);
+                mn = min(mn, min(min(r0 ^ x, r1 ^ x), min(r2 ^ x, r3 ^ x)));
             }
+            dup = mn == 0u;
         }
         for (u64 dm = BALLOT(act && dup); dm;) {   // each round retires >= 1 lane
             const uint32_t t = bcast(item, first_lane(dm));
             const u64 same = BALLOT(act && item == t);
-            if (same & (same - 1)) {
+            if (__popcll(same) > 1) {
                 const bool mine = (same >> l) & 1ull;
                 const int32_t sum = int32_t(wave_sum(mine ? uint32_t(d) : 0u));
                 const int32_t neg = int32_t(wave_sum(mine ? uint32_t(dneg) : 0u));
