@@ -1059,17 +1059,14 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
     bool del_cur, bad_cur;
     resolve(0, e_cur, it_cur, del_cur, bad_cur);
     for (uint32_t j = 0; j < n; j += 64) {
-        bool bad = bad_cur, act = false;
+        // (an invalid lane's item is 0 < n_lv; the deltas are arithmetic on the advance bit, so
+        // no divergent block)
+        bool bad = bad_cur || it_cur >= D.n_lv;
+        bool act = j + l < n && !bad;
         const bool del = del_cur;
         const uint32_t item = it_cur;
-        int32_t d = 0, dneg = 0;   // net delta; sum of the retreats (applied first)
-        if (j + l < n) {
-            const bool adv = (e_cur >> 31) != 0;
-            if (!bad && item >= D.n_lv) bad = true;
-            act = !bad;
-            d = adv ? 1 : -1;
-            dneg = adv ? 0 : -1;
-        }
+        int32_t d = int32_t((e_cur >> 31) << 1) - 1;   // net delta (+1 advance, -1 retreat)
+        int32_t dneg = int32_t(e_cur >> 31) - 1;       // sum of the retreats (applied first)
         // the next chunk's targets and the one after's entries, in flight behind this chunk
         if (j + 64 < n) {
             e_cur = e_nx;
@@ -1119,7 +1116,8 @@ DEV void toggle_pass(Doc &D, uint32_t off, uint32_t n, uint32_t pre, bool have_p
         {   // every lane loads (inactive ones item 0's word); only the store is masked
             const uint32_t w = ld(D.pc + (act ? item : 0u));
             const uint32_t bw = pc_blk(w), oc = pc_cnt(w), nc = oc + uint32_t(d);
-            const bool badc = act && (int32_t(oc) + dneg < 0 || int32_t(oc) + d > 0xFFFF || bw >= D.nb);
+            // oc + dneg < 0, oc + d > 0xFFFF or a block past the count: one sign test
+            const bool badc = act && int32_t((oc + uint32_t(dneg)) | (0xFFFFu - nc) | (D.nb - 1u - bw)) < 0;
             const bool ok = act && !badc;
             bad = bad || badc;
             if (ok) st(D.pc + item, pc_of(bw, nc));

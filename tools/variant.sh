@@ -7,7 +7,7 @@ DIR=$1; SRC=$2; OBJ=$3; shift 3
 cd "$(dirname "$0")/../diamond-types_amd"
 mkdir -p "$DIR"
 for o in lib/*.o; do [[ $(basename $o .o) == $OBJ ]] || cp "$o" "$DIR/"; done
-/opt/rocm/bin/hipcc -O3 -g -fPIC -std=c++17 -Wall -Wno-unused-function --offload-arch=gfx950 -munsafe-fp-atomics -mllvm -structurizecfg-skip-uniform-regions=true \
+/opt/rocm/bin/hipcc -O3 -g -fPIC -std=c++17 -Wall -Wno-unused-function --offload-arch=gfx950 -munsafe-fp-atomics -mllvm -structurizecfg-skip-uniform-regions=true -mllvm -amdgpu-atomic-optimizer-strategy=None \
   -Icsrc "$@" -c "$SRC" -o "$DIR/$OBJ.o"
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$DIR/libdtgpu.so" "$DIR"/*.o -lpthread
 rm -f "$DIR"/*.o
