@@ -208,7 +208,7 @@ struct Doc {
     uint32_t err;
     uint32_t debug;
     uint32_t site;
-    uint32_t steps, step_limit;   // watchdog: every loop iteration is charged; a bound
+    uint32_t steps;               // watchdog: loop iterations left; every loop iteration is charged; a bound
                                   // violation ends the document with ErrCapacity
     uint64_t prof[P_N];
     uint32_t doc;
@@ -217,11 +217,6 @@ struct Doc {
     // same state (every change is stored); a toggle touching the block drops it.
     uint32_t cb, cit;
     u64 cmv, cml;
-    // flat index: the chunk the last position lookup landed in and its block ids (lane = position
-    // in the chunk), so the next lookup gathers that chunk's counts beside the chunk totals --
-    // one LDS round trip instead of three while the edits stay in one chunk (64 blocks, ~2.7k
-    // chars of friendsforever).  A split that shifts those positions drops it.
-    uint32_t fc, ford;
     // transformed-ops mode (iter_xf_operations): per block the never-deleted mask, per top
     // position the never-deleted total, per LV the transformed position written out
     u64 *mup;
@@ -237,7 +232,8 @@ DEV void fail(Doc &D, uint32_t code, uint32_t site) {
 // search), whose termination rests on the index being consistent; every other loop retires at
 // least one item, lane or block per round.
 DEV bool charge(Doc &D) {
-    if (++D.steps > D.step_limit) { fail(D, ErrCapacity, 1); return false; }
+    if (D.steps == 0) { fail(D, ErrCapacity, 1); return false; }
+    D.steps--;
     return true;
 }
 template <bool PROF> DEV uint64_t tick() { return PROF ? __builtin_amdgcn_s_memtime() : 0; }
@@ -337,9 +333,6 @@ DEV bool find_vis(Doc &D, uint32_t p, Found &f) {
     uint32_t base = 0, S = NONE;
     if (L == IX_FLAT) {   // chunk totals, then the chunk's blocks
         const uint32_t nc = (D.nb + 63) >> 6;
-        // the cached chunk's counts, requested with the first 64 chunk totals
-        const uint32_t cc = D.fc;
-        const uint32_t cw = D.cnt[cc != NONE ? D.ford : 0u];
         {   // at most 32 chunks (FLAT_MAX_BLOCKS): one scan over lanes 0..31
             const uint32_t w0 = D.top[min(l, nc - 1)];
             const uint32_t v = l < nc ? (w0 & 0xFFFFu) : 0u;
@@ -351,16 +344,8 @@ DEV bool find_vis(Doc &D, uint32_t p, Found &f) {
         }
         f.S = f.tp = S;
         const uint32_t q = (S << 6) + l;
-        uint32_t b0, w;
-        if (S == cc) {   // the cached chunk: its counts are in
-            b0 = D.ford;
-            w = cw;
-        } else {
-            b0 = D.sbl[min(q, D.nb - 1)];
-            w = D.cnt[b0];
-            D.fc = S;
-            D.ford = b0;
-        }
+        const uint32_t b0 = D.sbl[min(q, D.nb - 1)];
+        const uint32_t w = D.cnt[b0];
         const uint32_t b = q < D.nb ? b0 : 0;
         const uint32_t v = q < D.nb ? c_vis(w) : 0;
         const uint32_t inc = wave_scan(v);
@@ -551,7 +536,6 @@ DEV uint32_t split_block(Doc &D, uint32_t b, uint32_t c, uint32_t it, u64 mv, u6
     }
     if (L == IX_FLAT) {   // b2 goes to position pos + 1: shift ord[pos + 1, nb) right by one
         const uint32_t pos = U(D.opos16[b]);
-        if (D.fc != NONE && pos + 1 < 64 * (D.fc + 1)) D.fc = NONE;   // the cached chunk's positions shift
         for (int hi = int(D.nb) - 1; hi > int(pos); hi -= 64) {   // highest chunk first
             const int q = hi - int(l);
             const bool mvl = q > int(pos);
@@ -1569,7 +1553,6 @@ DEV void run_doc(Doc &D) {
     D.nb = 1;
     D.nsb = 1;
     D.err = 0;
-    D.steps = 0;
     D.site = 0;
     // a segment (cut replay) applies its LV range's commands only
     const uint32_t seg_lo = U(vld(&D.desc->seg_lo)), seg_hi = U(vld(&D.desc->seg_hi));
@@ -1579,7 +1562,7 @@ DEV void run_doc(Doc &D) {
         if (c1 < c0 || seg_straddles(D.cmds, c0, seg_lo) || seg_straddles(D.cmds, c1, seg_hi)) fail(D, ErrCheckout, 30);
         else { D.cmds += c0; D.ncmd = c1 - c0; }
     }
-    D.step_limit = uint32_t(min<uint64_t>(64ull * (uint64_t(D.ncmd) + D.n_lv) + 4096, 0xFFFFFFF0ull));
+    D.steps = uint32_t(min<uint64_t>(64ull * (uint64_t(D.ncmd) + D.n_lv) + 4096, 0xFFFFFFF0ull));
     const uint32_t seg_u = XF ? 0u : U(vld(&D.desc->seg_u));
     if (seg_u) {
         if (!D.err) init_phantoms<L>(D, seg_u);
@@ -1600,8 +1583,6 @@ DEV void run_doc(Doc &D) {
     D.cb = NONE;
     D.cit = 0;
     D.cmv = D.cml = 0;
-    D.fc = NONE;
-    D.ford = 0;
     if (PROF) for (int i = 0; i < P_N; i++) D.prof[i] = 0;
     const uint64_t t_start = tick<PROF>();
     // commands are fetched 64 at a time (one per lane) and broadcast with readlane; the first
