@@ -74,6 +74,8 @@ struct BatchParams {
     uint32_t *xf;
     uint32_t *src;   // cut replay: the segments' source lists (DocDesc::src_off)
     uint32_t lds_flat;   // LDS tiers: 1 = the flat 2-level index (IX_FLAT), 0 = the 3-level one
+    uint32_t prio_from;  // LDS tiers: workgroups from this index on (dispatched after the first
+                         // resident set) raise their wave priority (0: off)
 };
 
 // Cut replay: after the replay, one workgroup per cut document resolves its segments' source

@@ -49,6 +49,7 @@
 // YjsMod compares those keys directly (merge.rs:154-278) instead of counting items.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <stdint.h>
 
@@ -1710,17 +1711,19 @@ DEV void bind_index_flat(Doc &D, uint8_t *base, uint32_t mb) {
 
 // One 64-lane workgroup per document of the list (the hardware dispatcher is the work queue;
 // LDS per workgroup bounds how many documents share a CU).
-#ifndef DTGPU_REPLAY_WAVES
-#define DTGPU_REPLAY_WAVES 1   // occupancy floor for the compiler's register budget (tuning knob)
-#endif
 // MW: TOG_WAVES waves per workgroup, the others helping with long retreat / advance passes
 // (the big LDS tiers: one or two documents per CU, so the extra waves cost no occupancy).
 // WAVES: the occupancy the compiler budgets registers for (the flat tier's documents are small
 // enough for 32 per CU, i.e. 8 waves per SIMD if the kernel takes <= 80 SGPRs and <= 64 VGPRs).
-template <int LDS_INDEX, bool PROF, bool XF, bool MW = false, int WAVES = DTGPU_REPLAY_WAVES>
+template <int LDS_INDEX, bool PROF, bool XF, bool MW = false, int WAVES = 1>
 __global__ __launch_bounds__(MW ? 64 * TOG_WAVES : 64) __attribute__((amdgpu_waves_per_eu(WAVES))) void replay_kernel(BatchParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t di = U(blockIdx.x);
+    // A workgroup dispatched into a slot an earlier document freed starts as the youngest wave
+    // on its SIMD, and the arbiter serves older waves first: such a late document would run to
+    // the end of the batch at the back of the queue.  It takes the higher priority instead, so
+    // the batch's last documents finish beside the first round's slowest ones.
+    if (P.prio_from && di >= P.prio_from) __builtin_amdgcn_s_setprio(3);
     uint32_t d;
     if (di < P.n_list) {
         d = U(P.doc_list[di]);
@@ -1880,15 +1883,21 @@ static int launch_lds_tier(const BatchParams &q, hipStream_t s, bool prof) {
     if (q.lds_flat) {   // the flat index: small documents, one wave each
         if (q.lds_blocks > FLAT_MAX_BLOCKS) return ErrArg;
         size_t lds = size_t(flat_index_bytes(q.lds_blocks));
-        if (const char *pad = getenv("DTGPU_LDS_PAD")) lds += size_t(strtoul(pad, nullptr, 10));   // occupancy experiments
         if (lds > 64 * 1024) return ErrArg;
-        // DTGPU_FLAT_WAVES: the register budget's occupancy (A/B; 1 = the compiler's choice)
-        int w = 8;
-        if (const char *e = getenv("DTGPU_FLAT_WAVES")) w = atoi(e);
-        if (prof) hipLaunchKernelGGL((dev::replay_kernel<dev::IX_FLAT, true, false>), dim3(q.n_list), dim3(64), lds, s, q);
-        else if (w == 8) hipLaunchKernelGGL((dev::replay_kernel<dev::IX_FLAT, false, false, false, 8>), dim3(q.n_list), dim3(64), lds, s, q);
-        else if (w == 7) hipLaunchKernelGGL((dev::replay_kernel<dev::IX_FLAT, false, false, false, 7>), dim3(q.n_list), dim3(64), lds, s, q);
-        else hipLaunchKernelGGL((dev::replay_kernel<dev::IX_FLAT, false, false, false, 1>), dim3(q.n_list), dim3(64), lds, s, q);
+        // resident documents per CU: 8 waves per SIMD (the kernel's register budget) or what the
+        // LDS allows (allocated in 1280-byte granules; tools/occ_probe.hip measured both)
+        BatchParams qp = q;
+        qp.prio_from = 0;
+        const char *pe = getenv("DTGPU_PRIO");
+        if (!(pe && *pe == '0')) {
+            static int n_cu = 0;
+            if (!n_cu && hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) n_cu = 0;
+            const size_t gran = (lds + 1279) / 1280 * 1280;
+            const size_t per_cu = std::min<size_t>(32, 163840 / std::max<size_t>(gran, 1280));
+            qp.prio_from = uint32_t(per_cu * size_t(std::max(n_cu, 1)));
+        }
+        if (prof) hipLaunchKernelGGL((dev::replay_kernel<dev::IX_FLAT, true, false>), dim3(q.n_list), dim3(64), lds, s, qp);
+        else hipLaunchKernelGGL((dev::replay_kernel<dev::IX_FLAT, false, false, false, 8>), dim3(q.n_list), dim3(64), lds, s, qp);
         return hipGetLastError() == hipSuccess ? OK : ErrHip;
     }
     size_t lds = size_t(index_bytes_ms(q.lds_blocks, q.lds_sb, true));

@@ -1,6 +1,6 @@
 set -o pipefail
 O=gpurun_out/r5m; mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 > $O/t.log 2>&1; rc=$?; tail -2 $O/t.log; [ $rc = 0 ] || exit 1
-for v in lib_base lib lib_base lib; do
-  echo "-- $v"; DTGPU_LIB_DIR=$v timeout -k 10 200 python -u tools/kbench.py friendsforever 10000 3 || exit 1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/t.log 2>&1; rc=$?; tail -3 $O/t.log; [ $rc = 0 ] || exit 1
+for v in 0 1; do
+  echo "-- DTGPU_PRIO=$v"; DTGPU_PRIO=$v timeout -k 10 200 python -u tools/kbench.py friendsforever 10000 3 || exit 1
 done 2>&1 | tee $O/ab.log
