@@ -1241,6 +1241,8 @@ __global__ __launch_bounds__(64) void walk_kernel(PlanParams Q) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     uint32_t ns = 0, ordv = 0;
+    uint32_t wb = 0xFFFFFFFFu;   // CSR: the entries whose records the group holds (wb + lane)
+    uint4 wk = make_uint4(0, 0, 0, 0);
     bool act = on && !err && top > 0;
     while (__ballot(act)) {
         if (act) {
@@ -1272,8 +1274,16 @@ __global__ __launch_bounds__(64) void walk_kernel(PlanParams Q) {
             // the entry's children (first / last from the record; a longer list from the CSR)
             uint32_t nch, ch0, firstch = 0, lastch = 0;
             if (CSR) {   // prep's first half: {children, first slot, first child, last child}
-                const uint32_t rv = coff[4 * size_t(idx) + (c & 3u)];
-                nch = wsh(rv, base); ch0 = wsh(rv, base + 1); firstch = wsh(rv, base + 2); lastch = wsh(rv, base + 3);
+                // the records of 16 consecutive entries stay in the group's lanes (lane c: entry
+                // wb + c): a walk mostly steps to the next entry, so most steps need no load
+                if ((idx & ~(WG - 1)) != wb) {
+                    wb = idx & ~(WG - 1);
+                    const uint2 *k2 = reinterpret_cast<const uint2 *>(coff + 4 * size_t(min(wb + c, ne - 1)));
+                    const uint2 a = k2[0], b = k2[1];
+                    wk = make_uint4(a.x, a.y, b.x, b.y);
+                }
+                const uint32_t src = base + (idx & (WG - 1));
+                nch = wsh(wk.x, src); ch0 = wsh(wk.y, src); firstch = wsh(wk.z, src); lastch = wsh(wk.w, src);
             } else {
                 const uint32_t wsel = c == 0 ? R_NCH : c == 1 ? R_CH0 : c == 2 ? R_FIRSTCH : R_LASTCH;
                 const uint32_t rv = erec[size_t(idx) * EREC_WORDS + wsel];

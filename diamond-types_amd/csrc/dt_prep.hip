@@ -141,6 +141,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
     uint32_t *doff = P.doff + D.o_doff;
     uint32_t *dense = P.dense + D.o_dense;
     uint32_t *rows = P.rows + D.o_rows;
+    const uint32_t rs = D.row_stride;   // <= PREP_MAX_CHAINS
     uint32_t *owner = P.scr + D.o_scr;
     // per entry {chain, seq0 - start (mod 2^32)}: one 8-byte load gives a parent's chain and the
     // offset that turns its parent LV into a chain length (dt_prep.hpp prep_scratch_words)
@@ -362,7 +363,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
                     if (hit) { prow = ring_row[slot * 64 + l]; pc = ring_meta[3 * slot + 1]; psd = ring_meta[3 * slot + 2]; }
                     if (!hit) {
                         PREP_ASSERT(pe < i, PREP_T_ROWS);
-                        prow = (!CHECK || pe < i) ? rows[size_t(pe) * PREP_MAX_CHAINS + l] : 0u;
+                        prow = l < rs && (!CHECK || pe < i) ? rows[size_t(pe) * rs + l] : 0u;
                         if (pe >= (i & ~63u)) {   // not flushed yet: from the registers
                             pc = rdl(bch, pe & 63u); psd = rdl(bsd, pe & 63u);
                         } else {
@@ -389,7 +390,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
                 if (m) c = ctz(m);
             }
             if (c == 0xFFFFFFFFu) {
-                if (nch == PREP_MAX_CHAINS) {
+                if (nch == rs) {   // (rs = PREP_MAX_CHAINS until staging counted the chains)
                     if (l == 0) { R.status = PREP_WIDE; R.n_chains = nch + 1; P.results[doc] = R; }
                     return;
                 }
@@ -416,9 +417,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
                 if (slot == RING - 1 || i + 1 == ne) {
                     for (uint32_t r = i & ~(RING - 1); r <= i; r++) {
                         // a row a child more than RING entries on reads back is stored whole
-                        // (chains opened later read as zero); the planner reads chains < nch
-                        if (l < nch || ((keep >> (r & 63u)) & 1u))
-                            rows[size_t(r) * PREP_MAX_CHAINS + l] = ring_row[(r & (RING - 1)) * 64 + l];
+                        // (chains opened later read as zero); the planner reads chains < nch.
+                        // A compact stride stores every row whole (one short contiguous piece)
+                        if (l < rs && (rs < PREP_MAX_CHAINS || l < nch || ((keep >> (r & 63u)) & 1u)))
+                            rows[size_t(r) * rs + l] = ring_row[(r & (RING - 1)) * 64 + l];
                     }
                 }
             }
@@ -675,7 +677,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
 // of steps; four documents now share every instruction.  Group-uniform values live in VGPRs,
 // reads across a group's lanes are permutes within the group.  A document that opens a 17th
 // chain is left to the second half of prep_kernel (its flag stays 1).  Rows are stored whole
-// (CHAIN_GROUP words: the planner reads chains < its count), so no keep-list is needed.
+// (min(CHAIN_GROUP, row stride) words: the planner reads chains < its count), so no keep-list is needed.
 __device__ __forceinline__ uint32_t gsh(uint32_t v, uint32_t src) { return uint32_t(__shfl(int(v), int(src))); }
 
 __global__ __launch_bounds__(64) void chain_kernel(PrepParams P) {
@@ -694,6 +696,7 @@ __global__ __launch_bounds__(64) void chain_kernel(PrepParams P) {
     const uint32_t *par_in = P.d_par + D.d_par;
     const uint32_t *pent = P.pent + D.o_par;
     uint32_t *rows = P.rows + D.o_rows;
+    const uint32_t rs = D.row_stride;
     uint32_t *doff = P.doff + D.o_doff;
     uint2 *cs = reinterpret_cast<uint2 *>(P.scr + D.o_scr + ((npar + 1) & ~1u));
     if (c < RING) rm[3 * c] = 0xFFFFFFFFu;
@@ -736,7 +739,7 @@ __global__ __launch_bounds__(64) void chain_kernel(PrepParams P) {
                     if (rm[3 * slot] == pe) {
                         prow = rr[slot * G + c]; pc = rm[3 * slot + 1]; psd = rm[3 * slot + 2];
                     } else {
-                        prow = rows[size_t(pe) * PREP_MAX_CHAINS + c];
+                        prow = c < rs ? rows[size_t(pe) * rs + c] : 0u;
                         if (pe >= (i & ~(G - 1))) { pc = gsh(bch, base + (pe & (G - 1))); psd = gsh(bsd, base + (pe & (G - 1))); }
                         else { const uint2 q = cs[pe]; pc = q.x; psd = q.y; }
                     }
@@ -752,7 +755,7 @@ __global__ __launch_bounds__(64) void chain_kernel(PrepParams P) {
                 if (m) ch = uint32_t(__ffs(int(m)) - 1);
             }
             if (ch == 0xFFFFFFFFu) {
-                if (nch == G) ok = false;   // a 17th chain: prep_kernel's second half redoes it
+                if (nch == G || nch == rs) ok = false;   // a 17th chain: prep_kernel's second half redoes it
                 else ch = nch++;
             }
             if (ok) {
@@ -768,7 +771,8 @@ __global__ __launch_bounds__(64) void chain_kernel(PrepParams P) {
                 // the block's rows and chain pairs go out together (one wait per 16 entries)
                 if (ib == G - 1 || i + 1 == ne) {
                     const uint32_t at = i & ~(G - 1);
-                    for (uint32_t r = at; r <= i; r++) rows[size_t(r) * PREP_MAX_CHAINS + c] = rr[(r & (RING - 1)) * G + c];
+                    if (c < rs)
+                        for (uint32_t r = at; r <= i; r++) rows[size_t(r) * rs + c] = rr[(r & (RING - 1)) * G + c];
                     if (at + c <= i) cs[at + c] = make_uint2(bch, bsd);
                     wave_fence();   // later entries read these back
                 }

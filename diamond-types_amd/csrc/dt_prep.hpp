@@ -18,6 +18,10 @@ struct PrepDesc {
     // decoder arenas (offsets in the decoder's units: quads / pairs / words / bytes)
     uint64_t d_op, d_arun, d_ent, d_poff, d_par, d_ver, d_agent, d_in;
     uint32_t n_ops, n_aruns, ne, n_par, n_ver, n_agents, n_lv, skip;
+    // words per parent-vector row: PREP_MAX_CHAINS until the staging pass has counted the
+    // document's chains, then that count rounded up to a multiple of four (a decomposition that
+    // would open a chain past it reports PREP_WIDE); the planner reads rows with the same stride
+    uint32_t row_stride, pad;
     // planner arenas (offsets in PlanDesc units)
     uint64_t o_par;     // par / pent / pch / pcnt slots
     uint64_t o_child;   // child slots
@@ -27,7 +31,7 @@ struct PrepDesc {
     uint64_t o_erec;    // words (EREC_WORDS per entry)
     uint64_t o_doff;    // words (PREP_MAX_CHAINS + 1)
     uint64_t o_dense;   // words (n_lv)
-    uint64_t o_rows;    // words (PREP_MAX_CHAINS per entry): parent vectors of the decomposition
+    uint64_t o_rows;    // words (PREP_MAX_CHAINS per entry reserved): parent vectors of the decomposition
     uint64_t o_scr;     // words (even): owner (n_par, padded), {chain, seq0 - start} (2 ne), coff, eop (ne + 1 each)
 };
 

@@ -1901,7 +1901,6 @@ static int launch_lds_tier(const BatchParams &q, hipStream_t s, bool prof) {
         return hipGetLastError() == hipSuccess ? OK : ErrHip;
     }
     size_t lds = size_t(index_bytes_ms(q.lds_blocks, q.lds_sb, true));
-    if (const char *pad = getenv("DTGPU_LDS_PAD")) lds += size_t(strtoul(pad, nullptr, 10));   // occupancy experiments
     if (lds > 160 * 1024) return ErrArg;   // a tier cap above the CU's LDS
     // documents whose index takes >= 32 KiB of LDS (at most four per CU) replay with helper
     // waves for long retreat / advance passes (DTGPU_TOG_WAVES=1: one wave)

@@ -891,6 +891,7 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
         q.o_doff = o_doff; o_doff += PREP_MAX_CHAINS + 1;
         q.o_dense = o_dense; o_dense += r.n_lv;
         q.o_rows = o_rows; o_rows += uint64_t(PREP_MAX_CHAINS) * r.n_entries;
+        q.row_stride = PREP_MAX_CHAINS;
         q.o_scr = o_scr; o_scr += prep_scratch_words(r.n_parents, r.n_entries);
         max_e = std::max<uint32_t>(max_e, r.n_entries);
     }
@@ -1035,6 +1036,17 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
                 add_segments(*B, i, cuts, seg_tier[i], seg_est[i], lds_fill, pc_total, blk_total, gidx_total, src_total);
         }
     }
+    // every later pass: parent-vector rows as wide as the document's chains (staging counted
+    // them), four-word aligned for the planner's 16-byte row loads -- a 64-word row per entry
+    // spread two live words over a cache line of their own (prep's stores, the planner's loads)
+    for (size_t i = 0; i < n; i++) {
+        if (pd[i].skip || prr[i].status != PREP_OK) continue;
+        const uint32_t rs = std::min<uint32_t>((std::max<uint32_t>(prr[i].n_chains, 1) + 3) & ~3u, PREP_MAX_CHAINS);
+        pd[i].row_stride = rs;
+        pdesc[i].row_stride = rs;
+    }
+    CK(B->pr_docs.upload(pd, s));
+    B->prep.docs = B->pr_docs.p;
     CK(B->d_cmds.alloc(cmd_total));
     CK(B->d_tlist.alloc(tlist_total));
     CK(B->p_docs.upload(pdesc, s));
