@@ -1282,7 +1282,7 @@ Status build_plan_input(const HostOpLog &o, PlanInput &pi) {
     // entry records
     pi.erec.assign(ne * EREC_WORDS, 0);
     for (size_t i = 0; i < ne; i++) {
-        uint32_t *r = &pi.erec[i * EREC_WORDS];
+        uint32_t r[EREC_WORDS] = {};
         r[0] = uint32_t(E[i].start);
         r[1] = uint32_t(E[i].end);
         r[2] = pi.poff[i];
@@ -1303,6 +1303,7 @@ Status build_plan_input(const HostOpLog &o, PlanInput &pi) {
         }
         r[17] = r[9] ? pi.child[pi.coff[i + 1] - 1] : 0xFFFFFFFFu;
         r[18] = r[9] ? pi.child[pi.coff[i]] : 0xFFFFFFFFu;
+        for (uint32_t k = 0; k < EREC_WORDS; k++) pi.erec[erec_word(ne, i, k)] = r[k];
     }
     // dense chain seq -> LV | is_del tables (the planner copies retreat/advance ranges out)
     pi.doff.assign(pi.n_chains + 1, 0);

@@ -147,9 +147,11 @@ struct PlanInput {
     std::vector<uint32_t> isdel;    // bit per LV: 1 = delete op
     std::vector<uint32_t> tip;      // pairs (LV, entry) of cg.version
     // per entry, EREC_WORDS words: start, end, parents offset, parent count, first op run, op
-    // runs, chain, first seq in the chain, children offset, child count, first parent LV, then
-    // for the first two parents (entry, chain, ops of that chain up to the parent), last child,
-    // first child
+    // runs, chain, first seq in the chain (the head: EREC_HEAD words), then children offset,
+    // child count, first parent LV, for the first two parents (entry, chain, ops of that chain up
+    // to the parent), last child, first child (the tail).  Stored split: every entry's head
+    // (entry e at e * EREC_HEAD), then every entry's tail (at ne * EREC_HEAD + e * EREC_TAIL) --
+    // the planner's per-step loads and the checkout pass's prep touch only the heads
     std::vector<uint32_t> erec;
     std::vector<uint32_t> pch, pcnt;  // per parent slot: its chain and that chain's ops up to it
     uint32_t n_chains = 0;          // causal chains the entries are partitioned into
@@ -158,7 +160,11 @@ struct PlanInput {
     std::vector<uint32_t> dense;    // per chain, by seq: LV | is_del << 30
     bool device_ok = true;
 };
-constexpr uint32_t EREC_WORDS = 20;
+constexpr uint32_t EREC_WORDS = 20, EREC_HEAD = 8, EREC_TAIL = EREC_WORDS - EREC_HEAD;
+// word k of entry e's record among ne entries
+constexpr size_t erec_word(size_t ne, size_t e, uint32_t k) {
+    return k < EREC_HEAD ? e * EREC_HEAD + k : ne * EREC_HEAD + e * EREC_TAIL + (k - EREC_HEAD);
+}
 constexpr uint32_t PLAN_CHAIN_LIMIT = 512;   // = PLAN_MAX_AGENTS of the device planner
 Status build_plan_input(const HostOpLog &o, PlanInput &pi);
 

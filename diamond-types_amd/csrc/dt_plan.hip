@@ -95,7 +95,7 @@ enum {
 };
 DEV uint32_t load_rec(const P &p, uint32_t e) {
     const uint32_t l = lane_id();
-    return l < EREC_WORDS ? p.erec[size_t(e) * EREC_WORDS + l] : 0;
+    return l < EREC_WORDS ? p.erec[erec_word(p.ne, e, l)] : 0;
 }
 DEV uint32_t R(uint32_t rw, int k) { return U(bcast(rw, uint32_t(k))); }
 
@@ -327,7 +327,7 @@ DEV void plan_doc(P &p, PlanResult *res) {
     for (uint32_t c = 0; c < p.ne; c += 64) {
         const uint32_t e = c + l;
         if (e < p.ne) {
-            const uint32_t np = p.erec[size_t(e) * EREC_WORDS + R_NP];
+            const uint32_t np = p.erec[size_t(e) * EREC_HEAD + R_NP];
             if (np > 0x7Fu) bad_np = true;
             p.pending[e] = uint8_t(min(np, 0x7Fu) | (np >= 2 ? MERGE_BIT : 0));
         }
@@ -335,7 +335,7 @@ DEV void plan_doc(P &p, PlanResult *res) {
     for (int c = int((p.ne + 63) / 64) - 1; c >= 0; c--) {
         if (!charge(p)) break;
         const uint32_t e = uint32_t(c) * 64 + (63 - l);   // descending entry index across lanes
-        const bool root = e < p.ne && p.erec[size_t(e) * EREC_WORDS + R_NP] == 0;
+        const bool root = e < p.ne && p.erec[size_t(e) * EREC_HEAD + R_NP] == 0;
         const u64 m = __ballot(root);
         const uint32_t rank = uint32_t(__popcll(m & ((1ull << l) - 1ull)));
         if (top + uint32_t(__popcll(m)) > PLAN_TODO_CAP) { fail(p, PLAN_TODO_FULL); break; }
@@ -611,7 +611,7 @@ DEV void plan_doc1(P &p, PlanResult *res) {
     for (uint32_t c = 0; c < p.ne; c += 64) {
         const uint32_t e = c + l;
         if (e < p.ne) {
-            const uint32_t np = p.erec[size_t(e) * EREC_WORDS + R_NP];
+            const uint32_t np = p.erec[size_t(e) * EREC_HEAD + R_NP];
             if (np > 0x7Fu) bad_np = true;
             p.pending[e] = uint8_t(min(np, 0x7Fu) | (np >= 2 ? MERGE_BIT : 0));
         }
@@ -619,7 +619,7 @@ DEV void plan_doc1(P &p, PlanResult *res) {
     for (int c = int((p.ne + 63) / 64) - 1; c >= 0; c--) {
         if (!charge(p)) break;
         const uint32_t e = uint32_t(c) * 64 + (63 - l);
-        const bool root = e < p.ne && p.erec[size_t(e) * EREC_WORDS + R_NP] == 0;
+        const bool root = e < p.ne && p.erec[size_t(e) * EREC_HEAD + R_NP] == 0;
         const u64 m = __ballot(root);
         const uint32_t rank = uint32_t(__popcll(m & ((1ull << l) - 1ull)));
         if (top + uint32_t(__popcll(m)) > PLAN_TODO_CAP) { fail(p, PLAN_TODO_FULL); break; }
@@ -775,7 +775,7 @@ DEV void plan_doc_split(P &p, PlanResult *res) {
     for (uint32_t c = 0; c < p.ne && !p.walk; c += 64) {
         const uint32_t e = c + l;
         if (e < p.ne) {
-            const uint32_t np = p.erec[size_t(e) * EREC_WORDS + R_NP];
+            const uint32_t np = p.erec[size_t(e) * EREC_HEAD + R_NP];
             if (np > 0x7Fu) bad_np = true;
             p.pending[e] = uint8_t(min(np, 0x7Fu) | (np >= 2 ? MERGE_BIT : 0));
         }
@@ -783,7 +783,7 @@ DEV void plan_doc_split(P &p, PlanResult *res) {
     for (int c = p.walk ? -1 : int((p.ne + 63) / 64) - 1; c >= 0; c--) {
         if (!charge(p)) break;
         const uint32_t e = uint32_t(c) * 64 + (63 - l);
-        const bool root = e < p.ne && p.erec[size_t(e) * EREC_WORDS + R_NP] == 0;
+        const bool root = e < p.ne && p.erec[size_t(e) * EREC_HEAD + R_NP] == 0;
         const u64 m = __ballot(root);
         const uint32_t rank = uint32_t(__popcll(m & ((1ull << l) - 1ull)));
         if (top + uint32_t(__popcll(m)) > PLAN_TODO_CAP) { fail(p, PLAN_TODO_FULL); break; }
@@ -856,10 +856,10 @@ DEV void plan_doc_split(P &p, PlanResult *res) {
         const uint32_t e = valid ? order[i] : 0;
         const bool hp = valid && i > 0;
         const uint32_t ep = hp ? order[i - 1] : 0;
-        const uint4 *r4 = reinterpret_cast<const uint4 *>(p.erec);
-        const uint4 a0 = r4[size_t(e) * (EREC_WORDS / 4)], a1 = r4[size_t(e) * (EREC_WORDS / 4) + 1];
+        const uint4 *r4 = reinterpret_cast<const uint4 *>(p.erec);   // the heads (32 bytes each)
+        const uint4 a0 = r4[size_t(e) * (EREC_HEAD / 4)], a1 = r4[size_t(e) * (EREC_HEAD / 4) + 1];
         uint4 b0 = make_uint4(0, 0, 0, 0), b1 = make_uint4(0, 0, 0, 0);
-        if (hp) { b0 = r4[size_t(ep) * (EREC_WORDS / 4)]; b1 = r4[size_t(ep) * (EREC_WORDS / 4) + 1]; }
+        if (hp) { b0 = r4[size_t(ep) * (EREC_HEAD / 4)]; b1 = r4[size_t(ep) * (EREC_HEAD / 4) + 1]; }
         const uint32_t e_start = a0.x, e_end = a0.y, op0 = a1.x, nop = a1.y, chain = a1.z, seq0 = a1.w;
         const uint32_t p_start = b0.x, p_end = b0.y, p_chain = b1.z, p_seq0 = b1.w;
         uint32_t code = 0;
@@ -1224,7 +1224,7 @@ __global__ __launch_bounds__(64) void walk_kernel(PlanParams Q) {
     const uint32_t below = (1u << c) - 1u;
     bool bad_np = false;
     for (uint32_t e = c; e < ne; e += WG) {
-        const uint32_t np = CSR ? poff[e + 1] - poff[e] : erec[size_t(e) * EREC_WORDS + R_NP];
+        const uint32_t np = CSR ? poff[e + 1] - poff[e] : erec[size_t(e) * EREC_HEAD + R_NP];
         if (np > 0x7Fu) bad_np = true;
         pend[e] = uint8_t(min(np, 0x7Fu) | (np >= 2 ? MERGE_BIT : 0));
     }
@@ -1232,7 +1232,7 @@ __global__ __launch_bounds__(64) void walk_kernel(PlanParams Q) {
     // roots, highest index first, so the lowest root ends on the top
     for (int cb = int((ne + WG - 1) / WG) - 1; cb >= 0 && !err; cb--) {
         const uint32_t e = uint32_t(cb) * WG + (WG - 1 - c);
-        const bool root = e < ne && (CSR ? poff[e + 1] == poff[e] : erec[size_t(e) * EREC_WORDS + R_NP] == 0);
+        const bool root = e < ne && (CSR ? poff[e + 1] == poff[e] : erec[size_t(e) * EREC_HEAD + R_NP] == 0);
         const uint32_t m = uint32_t(__ballot(root) >> base) & 0xFFFFu;
         if (top + uint32_t(__popc(m)) > PLAN_TODO_CAP) { err = PLAN_TODO_FULL; break; }
         if (root) todo[top + uint32_t(__popc(m & below))] = uint16_t(e);
@@ -1286,7 +1286,7 @@ __global__ __launch_bounds__(64) void walk_kernel(PlanParams Q) {
                 nch = wsh(wk.x, src); ch0 = wsh(wk.y, src); firstch = wsh(wk.z, src); lastch = wsh(wk.w, src);
             } else {
                 const uint32_t wsel = c == 0 ? R_NCH : c == 1 ? R_CH0 : c == 2 ? R_FIRSTCH : R_LASTCH;
-                const uint32_t rv = erec[size_t(idx) * EREC_WORDS + wsel];
+                const uint32_t rv = erec[erec_word(ne, idx, wsel)];
                 nch = wsh(rv, base); ch0 = wsh(rv, base + 1); firstch = wsh(rv, base + 2); lastch = wsh(rv, base + 3);
             }
             for (uint32_t cc = 0; cc < nch; cc += WG) {

@@ -54,6 +54,8 @@ struct PrepParams {
     // document into chains, the second half decomposes the rest itself; null: one launch
     uint32_t *chain_flag;
     uint32_t mode;                  // set by launch_prep: 0 whole kernel, 1 first half, 2 second half
+    uint32_t short_rec;             // entry records: heads only (a pass whose walk reads the CSR and
+                                    // whose planner reads heads: dt_host.hpp PlanInput::erec)
 };
 // chain_kernel: documents per wave, lanes (= chains) per document
 constexpr uint32_t CHAIN_GROUP = 16, CHAIN_DOCS = 64 / CHAIN_GROUP;

@@ -1178,11 +1178,14 @@ int prep_and_plan(dtgpu_batch *B, hipStream_t s, hipEvent_t mid) {
         if (mid && hipEventRecord(mid, s) != hipSuccess) return ErrHip;
         return B->n_gpu_planned ? launch_plan(B->plan, s) : OK;
     }
-    if (launch_prep_stage(B->prep, s, 1)) return ErrHip;
+    // the walk reads prep's CSR and, split, the planner only the entry records' heads
+    PrepParams pp = B->prep;
+    pp.short_rec = B->plan.split ? 1u : 0u;
+    if (launch_prep_stage(pp, s, 1)) return ErrHip;
     if (hipEventRecord(B->ev_w0, s) != hipSuccess || hipStreamWaitEvent(B->wstream, B->ev_w0, 0) != hipSuccess) return ErrHip;
     if (launch_walk(B->plan, B->wstream, true) != OK) return ErrHip;
     if (hipEventRecord(B->ev_w1, B->wstream) != hipSuccess) return ErrHip;
-    if (launch_prep_stage(B->prep, s, 2) || launch_prep_stage(B->prep, s, 3)) return ErrHip;
+    if (launch_prep_stage(pp, s, 2) || launch_prep_stage(pp, s, 3)) return ErrHip;
     if (mid && hipEventRecord(mid, s) != hipSuccess) return ErrHip;
     if (hipStreamWaitEvent(s, B->ev_w1, 0) != hipSuccess) return ErrHip;
     return launch_plan(B->plan, s, false);
