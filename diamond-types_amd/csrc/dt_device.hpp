@@ -166,6 +166,8 @@ struct PlanParams {
     uint32_t *walk;         // nullable: per document {status, steps} of walk_kernel (the orders
                             // four documents per wave); null: the planner walks itself
     const uint32_t *coff, *poff;   // walk_kernel's CSR mode: children offsets, parent offsets
+    uint32_t todo_cap;             // walk_kernel: stack slots per document (0: PLAN_TODO_CAP) -- the
+                                   // staging walk's deepest stack, so more walks share a CU's LDS
     Cmd *cmds;
     uint32_t *tlist;
     const PlanDesc *docs;

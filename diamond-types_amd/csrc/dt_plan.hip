@@ -804,7 +804,7 @@ DEV void plan_doc_split(P &p, PlanResult *res) {
     uint32_t ns = 0;
     uint32_t ordv = 0;   // lane j: order[64 * (ns / 64) + j] until its 64 are stored together
     if (p.walk) {
-        const uint32_t wst = U(p.walk[0]);
+        const uint32_t wst = U(p.walk[0]) & 0xFFFFu;   // (high 16 bits: the walk's stack depth)
         ns = U(p.walk[1]);
         if (wst) fail(p, wst);
     }
@@ -1201,13 +1201,18 @@ __global__ __launch_bounds__(64) void plan_kernel_wide(PlanParams Q) { plan_entr
 // kernel then runs phase B from the stored order (PlanParams.walk: status, steps).
 constexpr uint32_t WG = 16, WALK_DOCS = 64 / WG;
 DEV uint32_t wsh(uint32_t v, uint32_t src) { return uint32_t(__shfl(int(v), int(src))); }
+// s_waitcnt vmcnt(0) alone, inside the branch that loads: where the paths meet the compiler then
+// sees nothing pending and places no wait of its own -- a wait there would also wait for the
+// order store of the step before (vmcnt counts stores), a full memory round trip per 16 steps
+DEV void walk_wait_vm() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 template <bool CSR>
 __global__ __launch_bounds__(64) void walk_kernel(PlanParams Q) {
     extern __shared__ __attribute__((aligned(16))) uint16_t wl16[];
     const uint32_t l = lane_id(), g = l / WG, c = l % WG, base = g * WG;
-    const uint32_t stride = PLAN_TODO_CAP + (Q.lds_entries + 1) / 2;   // u16 per group: stack, pending bytes
+    const uint32_t cap = Q.todo_cap ? Q.todo_cap : PLAN_TODO_CAP;   // stack slots (even)
+    const uint32_t stride = cap + (Q.lds_entries + 1) / 2;   // u16 per group: stack, pending bytes
     uint16_t *todo = wl16 + g * stride;
-    uint8_t *pend = reinterpret_cast<uint8_t *>(todo + PLAN_TODO_CAP);
+    uint8_t *pend = reinterpret_cast<uint8_t *>(todo + cap);
     const uint32_t li = blockIdx.x * WALK_DOCS + g;
     bool on = li < Q.n_docs;
     const uint32_t d = on ? (Q.doc_list ? Q.doc_list[li] : li) : 0u;
@@ -1218,7 +1223,7 @@ __global__ __launch_bounds__(64) void walk_kernel(PlanParams Q) {
     const uint32_t *child = Q.child + pd.child_off;
     const uint32_t *coff = CSR ? Q.coff + pd.coff_off : nullptr, *poff = CSR ? Q.poff + pd.poff_off : nullptr;
     uint32_t *order = Q.order + pd.erec_off / EREC_WORDS;
-    uint32_t err = 0, top = 0;
+    uint32_t err = 0, top = 0, hw = 0;   // hw: the stack's high-water mark
     const uint32_t limit = uint32_t(min<uint64_t>(1024ull * (uint64_t(ne) + 16) + 4ull * pd.n_lv + (1u << 20), 0xFFFFFFF0ull));
     uint32_t steps = 0;
     const uint32_t below = (1u << c) - 1u;
@@ -1234,15 +1239,16 @@ __global__ __launch_bounds__(64) void walk_kernel(PlanParams Q) {
         const uint32_t e = uint32_t(cb) * WG + (WG - 1 - c);
         const bool root = e < ne && (CSR ? poff[e + 1] == poff[e] : erec[size_t(e) * EREC_HEAD + R_NP] == 0);
         const uint32_t m = uint32_t(__ballot(root) >> base) & 0xFFFFu;
-        if (top + uint32_t(__popc(m)) > PLAN_TODO_CAP) { err = PLAN_TODO_FULL; break; }
+        if (top + uint32_t(__popc(m)) > cap) { err = PLAN_TODO_FULL; break; }
         if (root) todo[top + uint32_t(__popc(m & below))] = uint16_t(e);
         top += uint32_t(__popc(m));
+        hw = max(hw, top);
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     uint32_t ns = 0, ordv = 0;
-    uint32_t wb = 0xFFFFFFFFu;   // CSR: the entries whose records the group holds (wb + lane)
-    uint4 wk = make_uint4(0, 0, 0, 0);
+    uint32_t wb = 0xFFFFFFFFu;   // CSR: the 64 entries whose records the group holds
+    uint2 wk[4] = {};
     bool act = on && !err && top > 0;
     while (__ballot(act)) {
         if (act) {
@@ -1273,17 +1279,23 @@ __global__ __launch_bounds__(64) void walk_kernel(PlanParams Q) {
             ns++;
             // the entry's children (first / last from the record; a longer list from the CSR)
             uint32_t nch, ch0, firstch = 0, lastch = 0;
-            if (CSR) {   // prep's first half: {children, first slot, first child, last child}
-                // the records of 16 consecutive entries stay in the group's lanes (lane c: entry
-                // wb + c): a walk mostly steps to the next entry, so most steps need no load
-                if ((idx & ~(WG - 1)) != wb) {
-                    wb = idx & ~(WG - 1);
-                    const uint2 *k2 = reinterpret_cast<const uint2 *>(coff + 4 * size_t(min(wb + c, ne - 1)));
-                    const uint2 a = k2[0], b = k2[1];
-                    wk = make_uint4(a.x, a.y, b.x, b.y);
+            if (CSR) {   // prep's first half: {children | first slot << 16, first | last child << 16}
+                // the records of 64 consecutive entries stay in the group's lanes (lane c, word j:
+                // entry wb + 16 j + c): a walk mostly steps to a nearby later entry, so few steps
+                // load (friendsforever: 5 % of steps miss a 64-entry window, 19 % a 16-entry one,
+                // and four documents share each wave's stall)
+                if ((idx & ~63u) != wb) {
+                    wb = idx & ~63u;
+                    const uint2 *k2 = reinterpret_cast<const uint2 *>(coff);
+#pragma unroll
+                    for (uint32_t j = 0; j < 4; j++) wk[j] = k2[min(wb + WG * j + c, ne - 1)];
+                    walk_wait_vm();
                 }
-                const uint32_t src = base + (idx & (WG - 1));
-                nch = wsh(wk.x, src); ch0 = wsh(wk.y, src); firstch = wsh(wk.z, src); lastch = wsh(wk.w, src);
+                const uint32_t o = idx - wb, j = o / WG;   // group-uniform: each lane picks the word
+                const uint2 v = j == 0 ? wk[0] : j == 1 ? wk[1] : j == 2 ? wk[2] : wk[3];
+                const uint32_t src = base + (o & (WG - 1));
+                const uint32_t w0 = wsh(v.x, src), w1 = wsh(v.y, src);
+                nch = w0 & 0xFFFFu; ch0 = w0 >> 16; firstch = w1 & 0xFFFFu; lastch = w1 >> 16;
             } else {
                 const uint32_t wsel = c == 0 ? R_NCH : c == 1 ? R_CH0 : c == 2 ? R_FIRSTCH : R_LASTCH;
                 const uint32_t rv = erec[erec_word(ne, idx, wsel)];
@@ -1291,8 +1303,11 @@ __global__ __launch_bounds__(64) void walk_kernel(PlanParams Q) {
             }
             for (uint32_t cc = 0; cc < nch; cc += WG) {
                 const bool has = cc + c < nch;
-                uint32_t chv = 0;
-                if (has) chv = nch <= 2 ? (c == 0 ? firstch : lastch) : child[ch0 + cc + c];
+                uint32_t chv = nch <= 2 ? (c == 0 ? firstch : lastch) : 0u;
+                if (has && nch > 2) {
+                    chv = child[ch0 + cc + c];
+                    walk_wait_vm();
+                }
                 bool ready = false;
                 if (has) {
                     const uint8_t pdv = uint8_t(pend[chv] - 1);
@@ -1300,9 +1315,10 @@ __global__ __launch_bounds__(64) void walk_kernel(PlanParams Q) {
                     ready = (pdv & 0x7F) == 0;
                 }
                 const uint32_t m = uint32_t(__ballot(ready) >> base) & 0xFFFFu;
-                if (top + uint32_t(__popc(m)) > PLAN_TODO_CAP) { err = PLAN_TODO_FULL; break; }
+                if (top + uint32_t(__popc(m)) > cap) { err = PLAN_TODO_FULL; break; }
                 if (ready) todo[top + uint32_t(__popc(m & below))] = uint16_t(chv);
                 top += uint32_t(__popc(m));
+                hw = max(hw, top);
             }
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             act = !err && top > 0;
@@ -1310,7 +1326,7 @@ __global__ __launch_bounds__(64) void walk_kernel(PlanParams Q) {
     }
     if (on && (ns & (WG - 1)) && c < (ns & (WG - 1))) order[(ns & ~(WG - 1)) + c] = ordv;
     if (on && c == 0) {
-        Q.walk[2 * size_t(d)] = err;
+        Q.walk[2 * size_t(d)] = err | (hw << 16);   // status | stack high-water mark << 16
         Q.walk[2 * size_t(d) + 1] = ns;
     }
 }
@@ -1320,7 +1336,9 @@ __global__ __launch_bounds__(64) void walk_kernel(PlanParams Q) {
 int launch_walk(const PlanParams &q, void *stream, bool csr) {
     if (!q.n_docs || !q.split || !q.walk) return OK;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    const size_t wlds = size_t(pdev::WALK_DOCS) * 2 * (PLAN_TODO_CAP + (q.lds_entries + 1) / 2);
+    const size_t cap = q.todo_cap ? q.todo_cap : PLAN_TODO_CAP;
+    if (cap > PLAN_TODO_CAP || (cap & 1u)) return ErrArg;
+    const size_t wlds = size_t(pdev::WALK_DOCS) * 2 * (cap + (q.lds_entries + 1) / 2);
     const dim3 grid((q.n_docs + pdev::WALK_DOCS - 1) / pdev::WALK_DOCS);
     if (wlds > 160 * 1024) return ErrArg;
     if (wlds > 64 * 1024) {   // past the default dynamic-LDS limit (documents near PLAN_MAX_LDS_ENTRIES)

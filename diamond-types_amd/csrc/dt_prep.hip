@@ -147,7 +147,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
     // offset that turns its parent LV into a chain length (dt_prep.hpp prep_scratch_words)
     uint2 *cs = reinterpret_cast<uint2 *>(owner + ((npar + 1) & ~1u));
     uint32_t *coff = reinterpret_cast<uint32_t *>(cs + ne), *eop = coff + ne + 1;
-    uint32_t *kids = eop + ne + 1;   // walk kernel: per entry {children, first slot, first, last child}
+    uint32_t *kids = eop + ne + 1;   // walk kernel: per entry {children | first slot, first | last child}
     Cmd *opc = P.opc + D.o_op;
     if (ne > P.max_entries || D.n_lv >= (1u << 30)) {
         if (l == 0) { R.status = PREP_BAD; P.results[doc] = R; }
@@ -280,12 +280,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
     wave_fence();
     }   // P.mode != 2
     if (P.mode == 1) {   // first half done: chain_kernel (or the second half) goes on from HBM
-        // each entry's children for the walk kernel, which starts now (one record load a step)
+        // each entry's children for the walk kernel, which starts now: {children | first slot
+        // << 16, first child | last child << 16} (slots < n_par < 0xFFFF; the walk takes documents
+        // of at most PLAN_MAX_LDS_ENTRIES entries)
+        uint2 *k2 = reinterpret_cast<uint2 *>(kids);
         for (uint32_t i = l; i < ne; i += 64) {
             const uint32_t c0 = coff[i], nc = coff[i + 1] - c0;
-            uint2 *k2 = reinterpret_cast<uint2 *>(kids + 4 * size_t(i));
-            k2[0] = make_uint2(nc, c0);
-            k2[1] = make_uint2(nc ? child[c0] : 0xFFFFFFFFu, nc ? child[c0 + nc - 1] : 0xFFFFFFFFu);
+            k2[i] = make_uint2(nc | (c0 << 16), nc ? (child[c0] & 0xFFFFu) | (child[c0 + nc - 1] << 16) : 0u);
         }
         if (l == 0) P.chain_flag[doc] = 1;
         return;

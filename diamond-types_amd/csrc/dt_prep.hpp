@@ -61,7 +61,8 @@ struct PrepParams {
 constexpr uint32_t CHAIN_GROUP = 16, CHAIN_DOCS = 64 / CHAIN_GROUP;
 
 // owner (n_par, padded to even), {chain, seq0 - start} pairs (2 ne), coff, eop (ne + 1 each), then
-// per entry {children, first child slot, first child, last child} (4 ne, the walk kernel's): even,
+// per entry {children | first child slot << 16, first child | last child << 16} (2 ne used of 4 ne,
+// the walk kernel's): even,
 // so every document's pair array is 8-byte aligned
 inline uint64_t prep_scratch_words(uint32_t n_par, uint32_t ne) { return (uint64_t(n_par) + 1) / 2 * 2 + 8ull * ne + 2; }
 inline uint64_t prep_kids_offset(uint32_t n_par, uint32_t ne) { return (uint64_t(n_par) + 1) / 2 * 2 + 4ull * ne + 2; }

@@ -965,11 +965,27 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     q.prof = getenv("DTGPU_PLAN_PROF") ? 1u : 0u;
     q.docs = B->p_docs.p; q.results = B->p_results.p; q.n_docs = uint32_t(n);
     q.count_only = 1;
+    q.todo_cap = 0;
     if (launch_plan(q, s) != OK) return DTGPU_ERR_HIP;
     q.count_only = 0;
     std::vector<PlanResult> pres(n);
     CK(hipMemcpyAsync(pres.data(), B->p_results.p, std::max<size_t>(n, 1) * sizeof(PlanResult), hipMemcpyDeviceToHost, s));
+    std::vector<uint32_t> wres;
+    if (q.walk) {
+        wres.resize(2 * n);
+        CK(hipMemcpyAsync(wres.data(), q.walk, 2 * n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    }
     CK(hipStreamSynchronize(s));
+    // the walks of every later pass are the same walks: their stacks get the deepest one seen
+    // here (plus slack), not PLAN_TODO_CAP -- the walk kernel's LDS then leaves room for the
+    // chain decomposition's waves beside it.  (A deeper walk would fail its document visibly,
+    // PLAN_TODO_FULL; the walk is deterministic, so none does.)
+    if (q.walk && q.split) {
+        uint32_t deep = 0;
+        for (size_t i = 0; i < n; i++)
+            if (!pdesc[i].skip && pres[i].status == PLAN_OK) deep = std::max(deep, wres[2 * i] >> 16);
+        q.todo_cap = std::min<uint32_t>(PLAN_TODO_CAP, (deep + 16 + 1) & ~1u);
+    }
 
     // ---- replay layout ---------------------------------------------------------------------------
     uint64_t cmd_total = 0, tlist_total = 0, blk_total = 0, out_total = 0, gidx_total = 0;
