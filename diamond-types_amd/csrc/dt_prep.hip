@@ -691,10 +691,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
 __device__ __forceinline__ uint32_t gsh(uint32_t v, uint32_t src) { return uint32_t(__shfl(int(v), int(src))); }
 
 __global__ __launch_bounds__(64) void chain_kernel(PrepParams P) {
-    constexpr uint32_t G = CHAIN_GROUP, RING = G;
-    extern __shared__ uint32_t csh[];   // per group: RING rows x G words, RING x {entry, chain, sd}
+    // RING: the last 2 G entries' rows and {entry, chain, sd} in LDS.  A block of G entries goes
+    // out to HBM (rows, chain pairs) in the middle of the next block, and the fence that makes it
+    // readable waits at the start of the block after that: by then the stores are done, so
+    // neither the fence nor the next block's loads (vmcnt counts stores) wait on a store in
+    // flight.  Parents up to 2 G entries back come from the ring and the block registers.
+    constexpr uint32_t G = CHAIN_GROUP, RING = 2 * G, FLUSH_AT = G / 2 - 1;
+    // per group: RING rows x W words, RING x {entry, chain, sd}.  W: the batch's widest row
+    // stride up to G (every document here has fewer chains than its stride, so a row's words
+    // past W are zero)
+    extern __shared__ uint32_t csh[];
+    const uint32_t W = chain_ring_width(P.chain_w);
     const uint32_t l = lane(), g = l / G, c = l % G, base = g * G;
-    uint32_t *rr = csh + g * (RING * G + 3 * RING), *rm = rr + RING * G;
+    uint32_t *rr = csh + g * (RING * W + 3 * RING), *rm = rr + RING * W;
     const uint32_t li = blockIdx.x * CHAIN_DOCS + g;
     bool live = li < P.n_docs;
     const uint32_t doc = live ? (P.doc_list ? P.doc_list[li] : li) : 0u;
@@ -709,26 +718,38 @@ __global__ __launch_bounds__(64) void chain_kernel(PrepParams P) {
     const uint32_t rs = D.row_stride;
     uint32_t *doff = P.doff + D.o_doff;
     uint2 *cs = reinterpret_cast<uint2 *>(P.scr + D.o_scr + ((npar + 1) & ~1u));
-    if (c < RING) rm[3 * c] = 0xFFFFFFFFu;
+    for (uint32_t r = c; r < RING; r += G) rm[3 * r] = 0xFFFFFFFFu;
     __builtin_amdgcn_wave_barrier();
     uint32_t maxne = ne;
     for (int d = 32; d >= 1; d >>= 1) maxne = max(maxne, uint32_t(__shfl_xor(int(maxne), d)));
     uint32_t clen = 0, nch = 0, prev_row = 0, prev_chain = 0, prev_sd = 0;
     uint32_t bk0 = 0, bk1 = 0, bs = 0, be = 0, bch = 0, bsd = 0;   // lane c: entry (i & ~15) + c
+    uint32_t pbch = 0, pbsd = 0;                                   // lane c: entry (i & ~15) - 16 + c
     uint32_t pblk = 0xFFFFFFFFu, ppa = 0, ppe = 0;                 // lane c: parent slot pblk + c
     bool ok = live;
+    // entries [at, at + G) out: rows from the ring, chain pairs from lane registers
+    auto flush = [&](uint32_t at, uint32_t end, uint32_t ch_l, uint32_t sd_l) {
+        if (c < rs)
+            for (uint32_t r = at; r < end; r++) rows[size_t(r) * rs + c] = c < W ? rr[(r & (RING - 1)) * W + c] : 0u;
+        if (at + c < end) cs[at + c] = make_uint2(ch_l, sd_l);
+    };
     for (uint32_t i = 0; i < maxne; i++) {
         const bool on = ok && i < ne;
-        const uint32_t ib = i & (G - 1);
-        if (ib == 0 && on) {
-            const uint32_t j = min(i + c, ne - 1);
-            bk0 = poff[j];
-            bk1 = poff[j + 1];
-            const uint2 se = ent[j];
-            bs = se.x;
-            be = se.y;
-            wait_vm();
+        const uint32_t ib = i & (G - 1), at = i & ~(G - 1);
+        if (ib == 0) {
+            wave_fence();   // the block flushed in the middle of the last one is readable
+            if (i < ne) { pbch = bch; pbsd = bsd; }
+            if (on) {
+                const uint32_t j = min(i + c, ne - 1);
+                bk0 = poff[j];
+                bk1 = poff[j + 1];
+                const uint2 se = ent[j];
+                bs = se.x;
+                be = se.y;
+                wait_vm();
+            }
         }
+        if (on && ib == FLUSH_AT && at) flush(at - G, at, pbch, pbsd);
         if (on) {
             const uint32_t k0 = gsh(bk0, base + ib), k1 = gsh(bk1, base + ib);
             uint32_t row = 0, first_chain = 0xFFFFFFFFu;
@@ -747,11 +768,12 @@ __global__ __launch_bounds__(64) void chain_kernel(PrepParams P) {
                 } else {
                     const uint32_t slot = pe & (RING - 1);
                     if (rm[3 * slot] == pe) {
-                        prow = rr[slot * G + c]; pc = rm[3 * slot + 1]; psd = rm[3 * slot + 2];
-                    } else {
+                        prow = c < W ? rr[slot * W + c] : 0u; pc = rm[3 * slot + 1]; psd = rm[3 * slot + 2];
+                    } else {   // more than RING entries back: flushed and fenced
                         prow = c < rs ? rows[size_t(pe) * rs + c] : 0u;
-                        if (pe >= (i & ~(G - 1))) { pc = gsh(bch, base + (pe & (G - 1))); psd = gsh(bsd, base + (pe & (G - 1))); }
-                        else { const uint2 q = cs[pe]; pc = q.x; psd = q.y; }
+                        const uint2 q = cs[pe];
+                        wait_vm();
+                        pc = q.x; psd = q.y;
                     }
                 }
                 row = max(row, prow);
@@ -776,18 +798,16 @@ __global__ __launch_bounds__(64) void chain_kernel(PrepParams P) {
                 bsd = ib == c ? s0 - s : bsd;
                 prev_row = row; prev_chain = ch; prev_sd = s0 - s;
                 const uint32_t slot = i & (RING - 1);
-                rr[slot * G + c] = row;
+                if (c < W) rr[slot * W + c] = row;
                 if (c == 0) { rm[3 * slot] = i; rm[3 * slot + 1] = ch; rm[3 * slot + 2] = s0 - s; }
-                // the block's rows and chain pairs go out together (one wait per 16 entries)
-                if (ib == G - 1 || i + 1 == ne) {
-                    const uint32_t at = i & ~(G - 1);
-                    if (c < rs)
-                        for (uint32_t r = at; r <= i; r++) rows[size_t(r) * rs + c] = rr[(r & (RING - 1)) * G + c];
-                    if (at + c <= i) cs[at + c] = make_uint2(bch, bsd);
-                    wave_fence();   // later entries read these back
-                }
             }
         }
+    }
+    if (ok && ne) {   // the blocks not out yet: the last one, and the one before unless flushed
+        const uint32_t at = (ne - 1) & ~(G - 1);
+        if (at && ((ne - 1) & (G - 1)) < FLUSH_AT) flush(at - G, at, pbch, pbsd);
+        flush(at, ne, bch, bsd);
+        wave_fence();
     }
     if (ok) {   // the chain tables' offsets: exclusive prefix of the chain lengths
         uint32_t v = c < nch ? clen : 0u;
@@ -812,7 +832,7 @@ int launch_prep_stage(const PrepParams &p, void *stream, int stage) {
     const size_t lds = (cw > rw ? cw : rw) * 4;
     PrepParams q = p;
     if (stage == 2) {
-        const size_t clds = size_t(CHAIN_DOCS) * (CHAIN_GROUP * CHAIN_GROUP + 3 * CHAIN_GROUP) * 4;
+        const size_t clds = size_t(CHAIN_DOCS) * chain_lds_words(p.chain_w) * 4;
         hipLaunchKernelGGL(prep::chain_kernel, dim3((p.n_docs + CHAIN_DOCS - 1) / CHAIN_DOCS), dim3(64), clds, st, q);
     } else {
         q.mode = stage == 1 ? 1u : 2u;
@@ -837,7 +857,7 @@ int launch_prep(const PrepParams &p, void *stream) {
     // first half, the chain decomposition four documents per wave, second half
     q.mode = 1;
     hipLaunchKernelGGL(prep::prep_kernel<false>, dim3(p.n_docs), dim3(64), lds, st, q);
-    const size_t clds = size_t(CHAIN_DOCS) * (CHAIN_GROUP * CHAIN_GROUP + 3 * CHAIN_GROUP) * 4;
+    const size_t clds = size_t(CHAIN_DOCS) * chain_lds_words(p.chain_w) * 4;
     hipLaunchKernelGGL(prep::chain_kernel, dim3((p.n_docs + CHAIN_DOCS - 1) / CHAIN_DOCS), dim3(64), clds, st, q);
     q.mode = 2;
     hipLaunchKernelGGL(prep::prep_kernel<false>, dim3(p.n_docs), dim3(64), lds, st, q);

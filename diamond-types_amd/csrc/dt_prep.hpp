@@ -54,11 +54,15 @@ struct PrepParams {
     // document into chains, the second half decomposes the rest itself; null: one launch
     uint32_t *chain_flag;
     uint32_t mode;                  // set by launch_prep: 0 whole kernel, 1 first half, 2 second half
+    uint32_t chain_w;               // chain_kernel: the widest row stride of the batch (0: unknown)
     uint32_t short_rec;             // entry records: heads only (a pass whose walk reads the CSR and
                                     // whose planner reads heads: dt_host.hpp PlanInput::erec)
 };
-// chain_kernel: documents per wave, lanes (= chains) per document
+// chain_kernel: documents per wave, lanes (= chains) per document; per document a ring of the
+// last 2 CHAIN_GROUP entries' rows (chain_w words each, 0: CHAIN_GROUP) and {entry, chain, sd}
 constexpr uint32_t CHAIN_GROUP = 16, CHAIN_DOCS = 64 / CHAIN_GROUP;
+constexpr uint32_t chain_ring_width(uint32_t w) { return w && w < CHAIN_GROUP ? w : CHAIN_GROUP; }
+constexpr uint32_t chain_lds_words(uint32_t w) { return 2 * CHAIN_GROUP * (chain_ring_width(w) + 3); }
 
 // owner (n_par, padded to even), {chain, seq0 - start} pairs (2 ne), coff, eop (ne + 1 each), then
 // per entry {children | first child slot << 16, first child | last child << 16} (2 ne used of 4 ne,

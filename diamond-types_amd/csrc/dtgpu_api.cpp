@@ -1055,12 +1055,15 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     // every later pass: parent-vector rows as wide as the document's chains (staging counted
     // them), four-word aligned for the planner's 16-byte row loads -- a 64-word row per entry
     // spread two live words over a cache line of their own (prep's stores, the planner's loads)
+    uint32_t widest = 0;
     for (size_t i = 0; i < n; i++) {
         if (pd[i].skip || prr[i].status != PREP_OK) continue;
         const uint32_t rs = std::min<uint32_t>((std::max<uint32_t>(prr[i].n_chains, 1) + 3) & ~3u, PREP_MAX_CHAINS);
         pd[i].row_stride = rs;
         pdesc[i].row_stride = rs;
+        widest = std::max(widest, rs);
     }
+    B->prep.chain_w = widest;   // the chain decomposition's LDS ring rows, as wide as needed
     CK(B->pr_docs.upload(pd, s));
     B->prep.docs = B->pr_docs.p;
     CK(B->d_cmds.alloc(cmd_total));
