@@ -185,7 +185,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
                 if (pe == 0xFFFFFFFFu) { bad = true; break; }
                 PREP_ASSERT(pe < i, PREP_T_ENTRY);
                 owner[k] = i;
-                par[k] = p;
+                if (!P.short_rec) par[k] = p;   // (read by the records' tails and the one-phase planner)
                 pent[k] = pe;
                 atomicAdd(&lfw[pe >> 1], 1u << (16 * (pe & 1u)));
             }
@@ -455,8 +455,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
 
     // ---- 4. lane-parallel outputs -----------------------------------------------------------------
     // parent slots: chain and ops of that chain up to it; four 64-slot rounds per iteration so
-    // their dependent loads (slot -> entry -> chain pair) are in flight together
-    for (uint32_t k0 = 0; k0 < npar; k0 += 256) {
+    // their dependent loads (slot -> entry -> chain pair) are in flight together.  (Read by the
+    // records' tails and the one-phase planner only: a heads-only pass skips them.)
+    for (uint32_t k0 = 0; k0 < npar && !P.short_rec; k0 += 256) {
         uint32_t pe[4], pv[4];
         uint2 q[4];
 #pragma unroll
