@@ -61,13 +61,38 @@ class GraphAnswer(ctypes.Structure):
 _lib = None
 
 
+def _check_build_record():
+    """The library's build record (lib/build_info.json, tools/build_info.py) names the hash of every
+    source it was built from: a library built from other sources than the ones beside it (a stale
+    prebuilt binary) is refused.  Experiment builds without a record (DTGPU_LIB_DIR) load as they are."""
+    import hashlib
+    import json
+    info = os.path.join(os.path.dirname(LIB_PATH), "build_info.json")
+    if not os.path.exists(info):
+        return
+    with open(info) as f:
+        rec = json.load(f)
+    pkg = os.path.dirname(os.path.dirname(LIB_PATH))
+    stale = []
+    for rel, h in rec.get("sources", {}).items():
+        path = os.path.join(pkg, rel)
+        if os.path.exists(path):
+            with open(path, "rb") as f:
+                if hashlib.sha256(f.read()).hexdigest() != h:
+                    stale.append(rel)
+    if stale:
+        raise RuntimeError(f"{LIB_PATH} was built from other sources than {', '.join(stale[:4])}"
+                           f"{' ...' if len(stale) > 4 else ''}; rebuild with `make -C diamond-types_amd`")
+
+
 def lib():
-    """Load libdtgpu.so (fails loudly when it has not been built)."""
+    """Load libdtgpu.so (fails loudly when it has not been built, or was built from other sources)."""
     global _lib
     if _lib is not None:
         return _lib
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"libdtgpu.so not built at {LIB_PATH}; run `make -C diamond-types_amd`")
+    _check_build_record()
     L = ctypes.CDLL(LIB_PATH)
     vp, sz, u64, i64, c = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int
     pu64 = ctypes.POINTER(ctypes.c_uint64)
