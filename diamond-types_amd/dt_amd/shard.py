@@ -22,26 +22,28 @@ def lpt_assign(costs, world):
     return [sorted(x) for x in out]
 
 
-COST_ALPHA = 1.0    # per op run x log2(op runs): positional lookups in the content index
-COST_BETA = 0.25    # per retreated / advanced LV of the walk plan: lane-parallel toggle passes
+COST_GAMMA = 2.05   # per LV^2 / 1e6: a long document holds a big LDS tier (few per CU) and a long
+                    # uncuttable stretch, so its batch cost grows faster than its LVs
+COST_BETA = 0.35    # per retreated / advanced LV of the walk plan: lane-parallel toggle passes
 
 
 def doc_cost(data: bytes) -> float:
-    """SURVEY.md 8(e) cost estimate of one document's checkout, from its host decode and host
-    walk plan (native, no GPU): c = LVs + alpha * runs * log2(runs) + beta * walk, with runs =
-    op runs and walk = LVs retreated + advanced by the SpanningTreeWalker plan.  alpha = 1 and
-    beta = 0.25 fit the single-document replay times of the three benchmark .dt files (kprof,
-    profiles/r2_calib: git-makefile / friendsforever 9.5-10x, node_nodecc / friendsforever
-    ~22x; the model gives 9.2x and 22x).  A document that does not decode costs its size."""
-    import math
+    """SURVEY.md 8(e) cost estimate of one document's checkout in a batch, from its host decode
+    and host walk plan (native, no GPU): c = LVs + gamma * LVs^2 / 1e6 + beta * walk, walk = LVs
+    retreated + advanced by the SpanningTreeWalker plan.  gamma = 2.05 and beta = 0.35 fit the
+    per-document batch cost of the eight benchmark traces at round 5 (1,024 device-staged copies
+    each, pass ms / 1,024; friendsforever from its 10k pass: profiles/r5_cost/cost_1024.jsonl) to
+    within 0.66-1.39x (log least squares); round 2's alpha * runs * log2(runs) term fitted to zero
+    and its model was off by up to 4.8x now that cut replay spreads long linear documents over
+    waves.  A document that does not decode costs its size."""
     import dt_amd
     try:
         o = dt_amd.ListOpLog.load_from(data)
     except dt_amd.ParseError:   # only an undecodable document; any other error is a bug and raises
         return float(len(data))
-    runs = max(1, len(o.export("ops")))
     ps = o.plan_stats()
-    return len(o) + COST_ALPHA * runs * math.log2(runs + 1) + COST_BETA * (ps["retreat"] + ps["advance"])
+    n = float(len(o))
+    return n + COST_GAMMA * n * n / 1e6 + COST_BETA * (ps["retreat"] + ps["advance"])
 
 
 def gather_results(records, n_total, dist, device=None):
