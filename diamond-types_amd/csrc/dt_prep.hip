@@ -782,7 +782,8 @@ __global__ __launch_bounds__(64) void chain_kernel(PrepParams P) {
                 if (k == k0) first_chain = pc;
             }
             uint32_t ch = 0xFFFFFFFFu;
-            if (first_chain != 0xFFFFFFFFu && gsh(row, base + first_chain) == gsh(clen, base + first_chain)) ch = first_chain;
+            const uint64_t eqm = ballot(row == clen);   // (a ballot, not two lane permutes)
+            if (first_chain != 0xFFFFFFFFu && ((eqm >> (base + first_chain)) & 1ull)) ch = first_chain;
             if (ch == 0xFFFFFFFFu) {
                 const uint32_t m = uint32_t(ballot(c < nch && row == clen) >> base) & 0xFFFFu;
                 if (m) ch = uint32_t(__ffs(int(m)) - 1);
