@@ -723,23 +723,27 @@ __global__ __launch_bounds__(64) void chain_kernel(PrepParams P) {
     __builtin_amdgcn_wave_barrier();
     uint32_t maxne = ne;
     for (int d = 32; d >= 1; d >>= 1) maxne = max(maxne, uint32_t(__shfl_xor(int(maxne), d)));
+    // prev_sd: seq0 - start of entry i - 1, held by the lane of its chain (the one lane that
+    // reads it); the ring's {entry, chain, sd} are written by that lane too, so no lane of the
+    // group waits for a permute of the chain's length
     uint32_t clen = 0, nch = 0, prev_row = 0, prev_chain = 0, prev_sd = 0;
-    uint32_t bk0 = 0, bk1 = 0, bs = 0, be = 0, bch = 0, bsd = 0;   // lane c: entry (i & ~15) + c
-    uint32_t pbch = 0, pbsd = 0;                                   // lane c: entry (i & ~15) - 16 + c
+    uint32_t bk0 = 0, bk1 = 0, bs = 0, be = 0;                     // lane c: entry (i & ~15) + c
     uint32_t pblk = 0xFFFFFFFFu, ppa = 0, ppe = 0;                 // lane c: parent slot pblk + c
     bool ok = live;
-    // entries [at, at + G) out: rows from the ring, chain pairs from lane registers
-    auto flush = [&](uint32_t at, uint32_t end, uint32_t ch_l, uint32_t sd_l) {
+    // entries [at, end) out: rows and chain pairs from the ring
+    auto flush = [&](uint32_t at, uint32_t end) {
         if (c < rs)
             for (uint32_t r = at; r < end; r++) rows[size_t(r) * rs + c] = c < W ? rr[(r & (RING - 1)) * W + c] : 0u;
-        if (at + c < end) cs[at + c] = make_uint2(ch_l, sd_l);
+        if (at + c < end) {
+            const uint32_t sl = (at + c) & (RING - 1);
+            cs[at + c] = make_uint2(rm[3 * sl + 1], rm[3 * sl + 2]);
+        }
     };
     for (uint32_t i = 0; i < maxne; i++) {
         const bool on = ok && i < ne;
         const uint32_t ib = i & (G - 1), at = i & ~(G - 1);
         if (ib == 0) {
             wave_fence();   // the block flushed in the middle of the last one is readable
-            if (i < ne) { pbch = bch; pbsd = bsd; }
             if (on) {
                 const uint32_t j = min(i + c, ne - 1);
                 bk0 = poff[j];
@@ -750,7 +754,7 @@ __global__ __launch_bounds__(64) void chain_kernel(PrepParams P) {
                 wait_vm();
             }
         }
-        if (on && ib == FLUSH_AT && at) flush(at - G, at, pbch, pbsd);
+        if (on && ib == FLUSH_AT && at) flush(at - G, at);
         if (on) {
             const uint32_t k0 = gsh(bk0, base + ib), k1 = gsh(bk1, base + ib);
             uint32_t row = 0, first_chain = 0xFFFFFFFFu;
@@ -794,21 +798,21 @@ __global__ __launch_bounds__(64) void chain_kernel(PrepParams P) {
             }
             if (ok) {
                 const uint32_t s = gsh(bs, base + ib), e = gsh(be, base + ib);
-                const uint32_t s0 = gsh(clen, base + ch);
-                if (c == ch) clen += e - s;
-                bch = ib == c ? ch : bch;
-                bsd = ib == c ? s0 - s : bsd;
-                prev_row = row; prev_chain = ch; prev_sd = s0 - s;
                 const uint32_t slot = i & (RING - 1);
+                if (c == ch) {   // seq0 - start = the chain's length so far - start
+                    prev_sd = clen - s;
+                    rm[3 * slot] = i; rm[3 * slot + 1] = ch; rm[3 * slot + 2] = clen - s;
+                    clen += e - s;
+                }
+                prev_row = row; prev_chain = ch;
                 if (c < W) rr[slot * W + c] = row;
-                if (c == 0) { rm[3 * slot] = i; rm[3 * slot + 1] = ch; rm[3 * slot + 2] = s0 - s; }
             }
         }
     }
     if (ok && ne) {   // the blocks not out yet: the last one, and the one before unless flushed
         const uint32_t at = (ne - 1) & ~(G - 1);
-        if (at && ((ne - 1) & (G - 1)) < FLUSH_AT) flush(at - G, at, pbch, pbsd);
-        flush(at, ne, bch, bsd);
+        if (at && ((ne - 1) & (G - 1)) < FLUSH_AT) flush(at - G, at);
+        flush(at, ne);
         wave_fence();
     }
     if (ok) {   // the chain tables' offsets: exclusive prefix of the chain lengths
