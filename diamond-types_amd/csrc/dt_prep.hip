@@ -829,7 +829,217 @@ __global__ __launch_bounds__(64) void chain_kernel(PrepParams P) {
     }
 }
 
+
+// ---- cut_kernel: the cut planning of one cut document per wave (dt_prep.hpp CutParams) -----------
+// The same decisions as dtgpu_api.cpp cut_ranges / plan_segments, lane-parallel:
+//   entry k is a cut range's entry when the prefix's frontier is empty there -- every earlier
+//   entry's last LV is named as a parent by some entry up to k: max over j < k of nxt(j) <= k,
+//   nxt(j) = the first entry naming j's last LV -- and the range is [start + 1, min(end, 1 + the
+//   smallest parent of every later entry)];
+//   the cuts are the op-run starts inside a range nearest to the equal-share targets (nearest
+//   first, the earlier of two at the same distance), a later one only past the previous one plus
+//   a quarter share, none a quarter share from the end;
+//   a segment's placeholders bound the text at its start: min(inserts, inserts - deletes + the
+//   deletes not inside one range).
+// (the cut kernel's scratch is written by stores and memory-side atomics and read back by other
+// lanes: an agent-scope fence also drops the CU's L1 lines, so no read meets a stale one)
+__device__ __forceinline__ void agent_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent"); }
+__device__ __forceinline__ uint32_t scan_max_excl(uint32_t v) {   // exclusive prefix max
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = uint32_t(__shfl_up(int(v), d));
+        if (lane() >= uint32_t(d)) v = max(v, o);
+    }
+    const uint32_t e = uint32_t(__shfl_up(int(v), 1));
+    return lane() ? e : 0u;
+}
+__device__ __forceinline__ int32_t scan_min_suffix(int32_t v) {   // inclusive suffix min
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int32_t o = __shfl_down(v, d);
+        if (lane() + uint32_t(d) < 64u) v = min(v, o);
+    }
+    return v;
+}
+// the last range whose first cut is <= v (ranges ascending), or nr
+__device__ __forceinline__ uint32_t range_of(const uint2 *rng, uint32_t nr, uint32_t v) {
+    uint32_t lo = 0, hi = nr;   // first range with .x > v
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (rng[mid].x <= v) lo = mid + 1; else hi = mid;
+    }
+    return lo ? lo - 1 : nr;
+}
+
+__global__ __launch_bounds__(64) void cut_kernel(CutParams P) {
+    if (blockIdx.x >= P.n_groups) return;
+    const uint32_t l = lane();
+    const SegGroup G = P.groups[blockIdx.x];
+    const SegPlan SP = P.plans[blockIdx.x];
+    const uint32_t d = P.seg_docs[G.first];
+    const PrepDesc D = P.pdocs[d];
+    const uint32_t ne = D.ne, nop = D.n_ops, S = G.count, T = SP.n_targets;   // segments; equal-share targets
+    if (S < 2 || S > 64 || T < S || ne == 0 || nop == 0) return;   // (staging makes none such; the poisoned ranges then fail)
+    const uint2 *ent = reinterpret_cast<const uint2 *>(P.d_ent) + D.d_ent;
+    const uint32_t *poff = P.d_poff + D.d_poff, *par = P.d_par + D.d_par;
+    const uint4 *ops = reinterpret_cast<const uint4 *>(P.d_ops) + D.d_op;   // lv, len, pos, kind (bit 0: delete)
+    uint32_t *nxt = P.scr + SP.scr_off;                                      // ne
+    int32_t *suf = reinterpret_cast<int32_t *>(nxt + ne);                    // ne + 1
+    uint2 *rng = reinterpret_cast<uint2 *>(P.scr + SP.scr_off + ((2ull * ne + 2) & ~1ull));   // <= ne ranges
+
+    // 1. nxt(j) and each entry's smallest parent (-1: ROOT)
+    for (uint32_t j = l; j < ne; j += 64) nxt[j] = 0xFFFFFFFFu;
+    agent_fence();
+    for (uint32_t e = l; e < ne; e += 64) {
+        const uint32_t k0 = poff[e], k1 = poff[e + 1];
+        int32_t mp = k0 == k1 ? -1 : 0x7FFFFFFF;
+        for (uint32_t k = k0; k < k1; k++) {
+            const uint32_t p = par[k];
+            mp = min(mp, int32_t(p));
+            const uint32_t j = entry_of(ent, e, p);
+            if (j != 0xFFFFFFFFu && p + 1 == ent[j].y) atomicMin(&nxt[j], e);
+        }
+        suf[e] = mp;
+    }
+    agent_fence();
+    // 2. suffix minima of the smallest parents (suf[k] = over entries >= k; suf[ne] = none)
+    {
+        int32_t carry = 0x7FFFFFFF;
+        for (int32_t c0 = int32_t((ne - 1) & ~63u); c0 >= 0; c0 -= 64) {
+            const uint32_t k = uint32_t(c0) + l;
+            const int32_t v = scan_min_suffix(k < ne ? suf[k] : 0x7FFFFFFF);
+            if (k < ne) suf[k] = min(v, carry);
+            carry = min(carry, __shfl(v, 0));
+        }
+        if (l == 0) suf[ne] = 0x7FFFFFFF;
+    }
+    agent_fence();
+    // 3. the cut ranges, compacted in entry order
+    uint32_t nr = 0;
+    {
+        uint32_t carry = 0;   // max nxt over the entries before the chunk
+        for (uint32_t c0 = 0; c0 < ne; c0 += 64) {
+            const uint32_t k = c0 + l;
+            const bool live = k < ne;
+            const uint32_t v = live ? __hip_atomic_load(nxt + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+            const uint32_t before = max(carry, scan_max_excl(v));
+            bool ok = false;
+            uint2 r = make_uint2(0, 0);
+            if (live && before <= k) {
+                const uint2 se = ent[k];
+                const int32_t sn = suf[k + 1];
+                const int64_t lim = sn == 0x7FFFFFFF ? int64_t(se.y) : min(int64_t(se.y), int64_t(sn) + 1);
+                ok = lim >= int64_t(se.x) + 1;
+                r = make_uint2(se.x + 1, uint32_t(lim));
+            }
+            const uint64_t m = ballot(ok);
+            if (ok) rng[nr + popc(m & lt_mask())] = r;
+            nr += popc(m);
+            uint32_t cm = live ? v : 0u;
+#pragma unroll
+            for (int dd = 32; dd >= 1; dd >>= 1) cm = max(cm, uint32_t(__shfl_xor(int(cm), dd)));
+            carry = max(carry, cm);
+        }
+    }
+    agent_fence();
+    if (nr == 0) return;
+    auto in_cut = [&](uint32_t v) {
+        const uint32_t i = range_of(rng, nr, v);
+        return i < nr && v <= rng[i].y;
+    };
+    // 4. the cuts: op-run starts in a range, nearest to k * nop / S
+    const uint32_t q4 = SP.ops_per_seg / 4;
+    uint32_t picks = 0, npick = 0, last = 0;   // lane i of picks: the i-th cut's op run
+    for (uint32_t k = 1; k < T; k++) {
+        const uint32_t target = uint32_t(uint64_t(k) * nop / T);
+        const uint32_t dmax = nop / (2 * T) + 1;
+        uint32_t best = 0xFFFFFFFFu;
+        for (uint32_t d0 = 0; d0 <= dmax && d0 < nop && best == 0xFFFFFFFFu; d0 += 32) {
+            const uint32_t dd = d0 + (l >> 1);
+            const uint32_t j = (l & 1u) ? target + dd : target - min(target, dd);
+            const bool ok = dd <= dmax && dd < nop && j > 0 && j < nop && in_cut(ops[j].x);
+            const uint64_t m = ballot(ok);
+            if (m) best = rdl(j, ctz(m));
+        }
+        if (best != 0xFFFFFFFFu && (npick == 0 || best > last + q4)) {
+            picks = l == npick ? best : picks;
+            npick++;
+            last = best;
+        }
+    }
+    while (npick && nop - rdl(picks, npick - 1) < q4) npick--;
+    if (npick + 1 != S) return;   // not the staged segments (the poisoned ranges then fail the document)
+    // 5. inserts, deletes and concurrent deletes before each cut (exclusive prefix sums)
+    uint32_t at_ins = 0, at_del = 0, at_dc = 0;   // lane i: before the i-th cut
+    uint32_t tot_ins = 0;
+    {
+        uint32_t ci = 0, cd = 0, cc = 0, pi = 0;
+        for (uint32_t c0 = 0; c0 < nop; c0 += 64) {
+            const uint32_t j = c0 + l;
+            uint32_t vi = 0, vd = 0, vc = 0;
+            if (j < nop) {
+                const uint4 o = ops[j];
+                if (o.w & 1u) {
+                    vd = o.y;
+                    const uint32_t i = range_of(rng, nr, o.x);
+                    if (!(i < nr && uint64_t(o.x) + o.y <= rng[i].y)) vc = o.y;
+                } else {
+                    vi = o.y;
+                }
+            }
+            const uint32_t si = scan_incl(vi), sd = scan_incl(vd), sc = scan_incl(vc);
+            while (pi < npick) {
+                const uint32_t pj = rdl(picks, pi);
+                if (pj >= c0 + 64) break;
+                const uint32_t t = pj - c0;   // exclusive prefix at lane t
+                const uint32_t ei = ci + rdl(si, t) - rdl(vi, t), ed = cd + rdl(sd, t) - rdl(vd, t), ec = cc + rdl(sc, t) - rdl(vc, t);
+                at_ins = l == pi ? ei : at_ins;
+                at_del = l == pi ? ed : at_del;
+                at_dc = l == pi ? ec : at_dc;
+                pi++;
+            }
+            ci += rdl(si, 63); cd += rdl(sd, 63); cc += rdl(sc, 63);
+        }
+        tot_ins = ci;
+    }
+    // 6. each segment's range and placeholder bound, against what staging reserved
+    bool fits = true;
+    for (uint32_t k = 0; k < S; k++) {
+        const uint32_t ins_lo = k ? rdl(at_ins, k - 1) : 0u;
+        const uint32_t ins_hi = k + 1 < S ? rdl(at_ins, k) : tot_ins;
+        const int64_t ai = k ? int64_t(rdl(at_ins, k - 1)) : 0, ad = k ? int64_t(rdl(at_del, k - 1)) : 0,
+                      ac = k ? int64_t(rdl(at_dc, k - 1)) : 0;
+        const uint32_t u = k ? uint32_t(max<int64_t>(0, min(ai, ai - ad + ac))) : 0u;
+        const SegCap cap = P.caps[G.first + k];
+        fits = fits && u <= cap.u && ins_hi - ins_lo <= cap.ins;
+    }
+    if (!fits) return;
+    {   // lane k writes segment k's descriptor fields
+        const uint32_t k = l;
+        const uint32_t pprev = uint32_t(__shfl(int(picks), int(k ? k - 1 : 0)));   // cut before segment k
+        const uint32_t ai = uint32_t(__shfl(int(at_ins), int(k ? k - 1 : 0)));
+        const uint32_t ad = uint32_t(__shfl(int(at_del), int(k ? k - 1 : 0)));
+        const uint32_t ac = uint32_t(__shfl(int(at_dc), int(k ? k - 1 : 0)));
+        if (k < S) {
+            const uint32_t lo = k ? ops[pprev].x : 0u;
+            const uint32_t hi = k + 1 < S ? ops[picks].x : 0xFFFFFFFFu;
+            const uint32_t u = k ? uint32_t(max<int64_t>(0, min(int64_t(ai), int64_t(ai) - int64_t(ad) + int64_t(ac)))) : 0u;
+            DocDesc *dd = P.docs + P.seg_docs[G.first + k];
+            dd->seg_lo = lo;
+            dd->seg_hi = hi;
+            dd->seg_u = u;
+        }
+    }
+}
+
+
 }  // namespace prep
+
+int launch_cut(const CutParams &p, void *stream) {
+    if (!p.n_groups) return 0;
+    hipLaunchKernelGGL(prep::cut_kernel, dim3(p.n_groups), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), p);
+    return hipGetLastError() == hipSuccess ? 0 : 66;
+}
 
 int launch_prep_stage(const PrepParams &p, void *stream, int stage) {
     if (!p.n_docs) return 0;

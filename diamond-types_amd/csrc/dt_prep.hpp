@@ -3,6 +3,7 @@
 #pragma once
 #include <stdint.h>
 
+#include "dt_device.hpp"
 #include "dt_host.hpp"
 
 namespace dtgpu {
@@ -72,6 +73,28 @@ inline uint64_t prep_scratch_words(uint32_t n_par, uint32_t ne) { return (uint64
 inline uint64_t prep_kids_offset(uint32_t n_par, uint32_t ne) { return (uint64_t(n_par) + 1) / 2 * 2 + 4ull * ne + 2; }
 
 int launch_prep(const PrepParams &p, void *stream);
+
+// Cut planning inside the checkout pass (cut_kernel): for every cut document (SegGroup), from the
+// decoded oplog, the cut ranges (dtgpu_api.cpp cut_ranges), the cuts nearest to equal op-run
+// shares (plan_segments) and each segment's LV range and placeholder bound, written into its
+// DocDesc.  Staging only reserves each segment's arenas (SegCap: the placeholders and inserts
+// its arenas hold) and poisons the descriptors' ranges, so a pass without this kernel fails.
+struct SegPlan { uint32_t ops_per_seg, n_targets; uint64_t scr_off; };   // per group: the planner's
+                                                                          // share, its target count, scratch (words)
+struct SegCap { uint32_t u, ins; };                                 // per seg_docs slot
+struct CutParams {
+    const uint32_t *d_ops, *d_ent, *d_poff, *d_par;   // decoder arenas (as PrepParams)
+    const PrepDesc *pdocs;                            // per document
+    const SegGroup *groups;
+    const uint32_t *seg_docs;
+    const SegPlan *plans;
+    const SegCap *caps;
+    DocDesc *docs;
+    uint32_t *scr;      // per group 4 ne + 4 words (SegPlan::scr_off)
+    uint32_t n_groups, pad;
+};
+inline uint64_t cut_scratch_words(uint32_t ne) { return 4ull * ne + 4; }
+int launch_cut(const CutParams &p, void *stream);
 // The three-launch pass one stage at a time (1: first half, 2: chains, 3: second half), so a
 // caller can start work that needs only the first half (the planner's walk) beside the rest.
 // Requires p.chain_flag and !p.check.

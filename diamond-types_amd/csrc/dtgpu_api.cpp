@@ -254,6 +254,15 @@ struct dtgpu_batch {
     DevBuf<SegGroup> d_groups;
     DevBuf<uint32_t> d_segdocs, d_src;
     CombineParams comb{};
+    // device-staged batches: the cut planning runs in every pass (cut_kernel, dt_prep.hpp); staging
+    // only reserves each segment's arenas and uploads its descriptor with a poisoned LV range
+    std::vector<SegPlan> seg_plans;
+    std::vector<SegCap> seg_caps;
+    DevBuf<SegPlan> d_plans;
+    DevBuf<SegCap> d_caps;
+    DevBuf<uint32_t> d_cutscr;
+    CutParams cut{};
+    hipEvent_t ev_cut = nullptr;
     hipEvent_t ev_splan = nullptr;   // split pass: the big tier's plans are done (segments may
                                      // replay in another tier, on the main stream)
 
@@ -284,6 +293,7 @@ struct dtgpu_batch {
 
     ~dtgpu_batch() {
         if (ev_splan) (void)hipEventDestroy(ev_splan);
+        if (ev_cut) (void)hipEventDestroy(ev_cut);
         if (ev_w0) (void)hipEventDestroy(ev_w0);
         if (ev_w1) (void)hipEventDestroy(ev_w1);
         if (ev_dec) (void)hipEventDestroy(ev_dec);
@@ -516,6 +526,25 @@ std::vector<uint32_t> seg_candidates(size_t n, SegSettings &sc, int n_cu, NOps n
     for (size_t i = 0; i < n; i++)
         if (n_ops(i) >= 2 * sc.ops_per_seg) c.push_back(uint32_t(i));
     return c;
+}
+// The documents the smallest LDS tier dispatches after its first resident round (its list runs
+// longest first, so these are its shortest): they start when the first round's documents begin
+// to finish and would run to the end of the batch at low occupancy; each is cut once where its
+// history allows, so its two halves finish earlier beside each other.  (Device-staged batches:
+// the pass itself plans the cut, cut_kernel.)
+template <typename NOps>
+std::vector<uint8_t> late_documents(const dtgpu_batch &B, const SegSettings &sc, NOps n_ops) {
+    std::vector<uint8_t> late(B.n, 0);
+    const char *e = getenv("DTGPU_SEG_LATE");   // "0": no late cuts
+    if (!sc.on || (e && *e == '0') || B.tier_list[0].empty() || !flat_setting() || B.tier_blocks[0] > FLAT_MAX_BLOCKS) return late;
+    const size_t lds = size_t(flat_index_bytes(B.tier_blocks[0]));
+    const size_t gran = (lds + 1279) / 1280 * 1280;
+    const size_t resident = std::min<size_t>(32, 163840 / std::max<size_t>(gran, 1280)) * size_t(std::max(B.n_cu, 1));
+    std::vector<uint32_t> order(B.tier_list[0].begin(), B.tier_list[0].end());
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return B.n_lv[a] > B.n_lv[b]; });
+    for (size_t k = resident; k < order.size(); k++)
+        if (order[k] < B.n && n_ops(order[k]) >= 128) late[order[k]] = 1;
+    return late;
 }
 // The batch's combine step and source-list arena (after every add_segments).
 hipError_t finish_segments(dtgpu_batch &B, uint64_t src_total, const uint32_t *cbyte, const uint8_t *content, hipStream_t s) {
@@ -1044,13 +1073,28 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     uint64_t pc_total = lv_total, src_total = 0;
     {
         SegSettings sc = seg_settings();
-        for (uint32_t i : seg_candidates(n, sc, B->n_cu, [&](size_t k) { return seg_tier[k] != -2 ? Dd.res[k].n_ops : 0u; })) {
+        const std::vector<uint32_t> cand = seg_candidates(n, sc, B->n_cu, [&](size_t k) { return seg_tier[k] != -2 ? Dd.res[k].n_ops : 0u; });
+        std::vector<uint8_t> late = late_documents(*B, sc, [&](size_t k) { return Dd.res[k].n_ops; });
+        for (uint32_t i : cand) late[i] = 0;
+        std::vector<uint32_t> all = cand;
+        for (size_t i = 0; i < n; i++) if (late[i]) all.push_back(uint32_t(i));
+        std::sort(all.begin(), all.end());
+        uint64_t scr = 0;
+        for (uint32_t i : all) {
             SegInput si;
             if (!seg_input_from_device(Dd, i, si, s)) return DTGPU_ERR_HIP;
-            const std::vector<SegCut> cuts = plan_segments(si, sc);
-            if (cuts.size() >= 2)
-                add_segments(*B, i, cuts, seg_tier[i], seg_est[i], lds_fill, pc_total, blk_total, gidx_total, src_total);
+            SegSettings c = sc;
+            if (late[i]) { c.max_seg = 2; c.ops_per_seg = std::max<uint64_t>(1, si.ops.size() / 2); }
+            const std::vector<SegCut> cuts = plan_segments(si, c);
+            if (cuts.size() < 2 ||
+                !add_segments(*B, i, cuts, seg_tier[i], seg_est[i], lds_fill, pc_total, blk_total, gidx_total, src_total))
+                continue;
+            const uint32_t targets = uint32_t(std::min<uint64_t>(c.max_seg, si.ops.size() / c.ops_per_seg));
+            B->seg_plans.push_back(SegPlan{uint32_t(c.ops_per_seg), targets, scr});
+            for (const SegCut &k : cuts) B->seg_caps.push_back(SegCap{k.u, uint32_t(k.ins)});
+            scr += cut_scratch_words(Dd.res[i].n_entries);
         }
+        CK(B->d_cutscr.alloc(std::max<uint64_t>(scr, 1)));
     }
     // every later pass: parent-vector rows as wide as the document's chains (staging counted
     // them), four-word aligned for the planner's 16-byte row loads -- a 64-word row per entry
@@ -1072,7 +1116,12 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     B->plan.docs = B->p_docs.p;
     B->plan.cmds = B->d_cmds.p;
     B->plan.tlist = B->d_tlist.p;
-    CK(B->d_docs.upload(B->docs, s));
+    {   // every segment's LV range is the pass's cut planning's to write (poisoned here: a replay
+        // without it fails, ErrCheckout site 30)
+        std::vector<DocDesc> up = B->docs;
+        for (uint32_t d : B->seg_docs) { up[d].seg_lo = 0xFFFFFFFFu; up[d].seg_hi = 0; }
+        CK(B->d_docs.upload(up, s));
+    }
     CK(B->d_lists.upload(tier_lists(*B), s));
     CK(B->d_pos.alloc(pc_total));
     CK(B->d_ao.alloc(pc_total));
@@ -1085,6 +1134,21 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     CK(B->d_results.alloc(B->docs.size()));
     CK(hipMemsetAsync(B->d_results.p, 0, std::max<size_t>(B->docs.size(), 1) * sizeof(DocResult), s));
     CK(finish_segments(*B, src_total, Dd.cbyte.p, Dd.content.p, s));
+    if (!B->seg_groups.empty()) {
+        CK(B->d_plans.upload(B->seg_plans, s));
+        CK(B->d_caps.upload(B->seg_caps, s));
+        CutParams &c = B->cut;
+        c.d_ops = Dd.ops.p; c.d_ent = Dd.ent.p; c.d_poff = Dd.poff.p; c.d_par = Dd.par.p;
+        c.pdocs = B->pr_docs.p;
+        c.groups = B->d_groups.p;
+        c.seg_docs = B->d_segdocs.p;
+        c.plans = B->d_plans.p;
+        c.caps = B->d_caps.p;
+        c.docs = B->d_docs.p;
+        c.scr = B->d_cutscr.p;
+        c.n_groups = uint32_t(B->seg_groups.size());
+        if (!B->ev_cut) CK(hipEventCreateWithFlags(&B->ev_cut, hipEventDisableTiming));
+    }
     CK(hipStreamSynchronize(s));
 #undef CK
     BatchParams base{};
@@ -1193,6 +1257,7 @@ int prep_and_plan(dtgpu_batch *B, hipStream_t s, hipEvent_t mid) {
     const bool overlap = prep && B->n_gpu_planned && B->prep.chain_flag && !B->prep.check && B->plan.walk &&
                          B->plan.coff && B->wstream && !getenv("DTGPU_NO_WALK_OVERLAP");
     if (!overlap) {
+        if (launch_cut(B->cut, s)) return ErrHip;
         if (prep && launch_prep(B->prep, s)) return ErrHip;
         if (mid && hipEventRecord(mid, s) != hipSuccess) return ErrHip;
         return B->n_gpu_planned ? launch_plan(B->plan, s) : OK;
@@ -1200,6 +1265,11 @@ int prep_and_plan(dtgpu_batch *B, hipStream_t s, hipEvent_t mid) {
     // the walk reads prep's CSR and, split, the planner only the entry records' heads
     PrepParams pp = B->prep;
     pp.short_rec = B->plan.split ? 1u : 0u;
+    if (B->cut.n_groups) {   // the cut planning beside prep's first half, on the walk's stream
+        if (hipEventRecord(B->ev_cut, s) != hipSuccess || hipStreamWaitEvent(B->wstream, B->ev_cut, 0) != hipSuccess ||
+            launch_cut(B->cut, B->wstream))
+            return ErrHip;
+    }
     if (launch_prep_stage(pp, s, 1)) return ErrHip;
     if (hipEventRecord(B->ev_w0, s) != hipSuccess || hipStreamWaitEvent(B->wstream, B->ev_w0, 0) != hipSuccess) return ErrHip;
     if (launch_walk(B->plan, B->wstream, true) != OK) return ErrHip;
@@ -1213,6 +1283,7 @@ int prep_and_plan(dtgpu_batch *B, hipStream_t s, hipEvent_t mid) {
 int launch_all(dtgpu_batch *B, hipStream_t s) {
     if (B->xf_mode) return launch_replay_xf(B->large, s);
     if (B->split) {
+        if (launch_cut(B->cut, s)) return ErrHip;
         int e = launch_split_side(B, s);
         if (!e) e = launch_split_prep(B, s);
         if (!e) e = launch_split_plan(B, s);
@@ -1754,7 +1825,7 @@ dtgpu_status dtgpu_batch_run_timed(dtgpu_batch *B, float *ms) {
     const bool prep = B->dec && !B->xf_mode;
     const bool split = prep && B->split;   // split pass: prep / plan times are the main pipeline's
     if (hipEventRecord(B->ev_prep, s) != hipSuccess) return DTGPU_ERR_HIP;
-    if (split && launch_split_side(B, s)) return DTGPU_ERR_HIP;
+    if (split && (launch_cut(B->cut, s) || launch_split_side(B, s))) return DTGPU_ERR_HIP;
     if (split) {
         if (launch_split_prep(B, s) != OK || hipEventRecord(B->ev0, s) != hipSuccess || launch_split_plan(B, s) != OK)
             return DTGPU_ERR_HIP;

@@ -13,7 +13,7 @@ import os
 import re
 import sys
 
-PASS = ("prep_kernel", "chain_kernel", "walk_kernel", "plan_kernel", "replay_kernel", "combine_kernel",
+PASS = ("prep_kernel", "chain_kernel", "walk_kernel", "plan_kernel", "replay_kernel", "combine_kernel", "cut_kernel",
         "fillBuffer")
 END = ("replay_kernel", "combine_kernel")
 
