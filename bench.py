@@ -498,8 +498,8 @@ def main():
         "config": {"workload": f"{args.workload} x {args.docs} docs per GPU (checkout_tip)",
                    "docs_per_gpu": args.docs, "merged_ops_per_doc": lv_per_doc,
                    "distinct_docs": len(pool),
-                   "timed": "device walker inputs (prep) + walk planning + replay + materialisation of the "
-                            "whole batch (decoded oplogs resident in HBM)",
+                   "timed": "device walker inputs (prep) + cut planning + walk planning + replay + materialisation "
+                            "of the whole batch (decoded oplogs resident in HBM)",
                    "parallelism": f"dp{world} (documents sharded, no data-path collective)"},
         "docs_per_sec": n_total * args.steps / elapsed,
         "total_merged_ops": total_lv,
@@ -508,7 +508,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "replay_kernel (dominant kernel of the pass)", "kernel_ms": replay_ms,
-                     "pass": {"kernels": "prep_kernel x2 + chain_kernel + walk_kernel + plan_kernel + replay_kernel tiers (+ combine_kernel)", "ms": avg_kernel_ms,
+                     "pass": {"kernels": "prep_kernel x2 + chain_kernel + walk_kernel + cut_kernel + plan_kernel + replay_kernel tiers + combine_kernel", "ms": avg_kernel_ms,
                               "prep_ms": prep_ms, "plan_ms": plan_ms, "replay_ms": replay_ms,
                               "achieved": alg_bytes / (avg_kernel_ms / 1000.0) / 1e9,
                               "frac": alg_bytes / (avg_kernel_ms / 1000.0) / 1e9 / HBM_PEAK_GBS,

@@ -883,24 +883,26 @@ __global__ __launch_bounds__(64) void cut_kernel(CutParams P) {
     const uint2 *ent = reinterpret_cast<const uint2 *>(P.d_ent) + D.d_ent;
     const uint32_t *poff = P.d_poff + D.d_poff, *par = P.d_par + D.d_par;
     const uint4 *ops = reinterpret_cast<const uint4 *>(P.d_ops) + D.d_op;   // lv, len, pos, kind (bit 0: delete)
-    uint32_t *nxt = P.scr + SP.scr_off;                                      // ne
-    int32_t *suf = reinterpret_cast<int32_t *>(nxt + ne);                    // ne + 1
-    uint2 *rng = reinterpret_cast<uint2 *>(P.scr + SP.scr_off + ((2ull * ne + 2) & ~1ull));   // <= ne ranges
+    if (ne > P.max_ne) return;
+    extern __shared__ uint32_t nxt[];   // per entry: the first entry naming its last LV as a parent
+    const uint32_t *pent = P.pent ? P.pent + D.o_par : nullptr;   // prep's first half: each parent's entry (or searched)
+    int32_t *suf = reinterpret_cast<int32_t *>(P.scr + SP.scr_off);        // ne + 1
+    uint2 *rng = reinterpret_cast<uint2 *>(P.scr + SP.scr_off + ((uint64_t(ne) + 2) & ~1ull));   // <= ne ranges
 
-    // 1. nxt(j) and each entry's smallest parent (-1: ROOT)
+    // 1. nxt (LDS atomics) and each entry's smallest parent (-1: ROOT)
     for (uint32_t j = l; j < ne; j += 64) nxt[j] = 0xFFFFFFFFu;
-    agent_fence();
+    __syncthreads();
     for (uint32_t e = l; e < ne; e += 64) {
         const uint32_t k0 = poff[e], k1 = poff[e + 1];
         int32_t mp = k0 == k1 ? -1 : 0x7FFFFFFF;
         for (uint32_t k = k0; k < k1; k++) {
-            const uint32_t p = par[k];
+            const uint32_t p = par[k], j = pent ? pent[k] : entry_of(ent, e, p);
             mp = min(mp, int32_t(p));
-            const uint32_t j = entry_of(ent, e, p);
-            if (j != 0xFFFFFFFFu && p + 1 == ent[j].y) atomicMin(&nxt[j], e);
+            if (j < e && p + 1 == ent[j].y) atomicMin(&nxt[j], e);
         }
         suf[e] = mp;
     }
+    __syncthreads();
     agent_fence();
     // 2. suffix minima of the smallest parents (suf[k] = over entries >= k; suf[ne] = none)
     {
@@ -921,12 +923,12 @@ __global__ __launch_bounds__(64) void cut_kernel(CutParams P) {
         for (uint32_t c0 = 0; c0 < ne; c0 += 64) {
             const uint32_t k = c0 + l;
             const bool live = k < ne;
-            const uint32_t v = live ? __hip_atomic_load(nxt + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+            const uint2 se = live ? ent[k] : make_uint2(0, 1);
+            const uint32_t v = live ? nxt[k] : 0u;
             const uint32_t before = max(carry, scan_max_excl(v));
             bool ok = false;
             uint2 r = make_uint2(0, 0);
             if (live && before <= k) {
-                const uint2 se = ent[k];
                 const int32_t sn = suf[k + 1];
                 const int64_t lim = sn == 0x7FFFFFFF ? int64_t(se.y) : min(int64_t(se.y), int64_t(sn) + 1);
                 ok = lim >= int64_t(se.x) + 1;
@@ -973,20 +975,38 @@ __global__ __launch_bounds__(64) void cut_kernel(CutParams P) {
     uint32_t at_ins = 0, at_del = 0, at_dc = 0;   // lane i: before the i-th cut
     uint32_t tot_ins = 0;
     {
+        // a delete run is inside one range or concurrent: the runs' LVs ascend, so each chunk
+        // looks its runs up among the 64 ranges from the previous chunk's last one (one load,
+        // a search by lane permutes), a global bisection only past that window
         uint32_t ci = 0, cd = 0, cc = 0, pi = 0;
+        uint32_t rc = 0;   // range of the previous chunk's last run (ranges ascend with LVs)
+        const uint32_t last_pick = rdl(picks, npick - 1);   // past it only the inserts are summed
         for (uint32_t c0 = 0; c0 < nop; c0 += 64) {
             const uint32_t j = c0 + l;
+            const uint4 o = j < nop ? ops[j] : make_uint4(0xFFFFFFFFu, 0, 0, 0);
+            const bool look = c0 <= last_pick;
+            const uint2 wr = look && rc + l < nr ? rng[rc + l] : make_uint2(0xFFFFFFFFu, 0);
+            uint32_t c = 0;   // window ranges whose first cut is <= the run's LV
+#pragma unroll
+            for (uint32_t st = 32; st >= 1; st >>= 1)
+                if (uint32_t(__shfl(int(wr.x), int(c + st - 1))) <= o.x) c += st;
+            if (c == 63 && rdl(wr.x, 63) <= o.x) c = 64;
+            uint32_t ri = c ? rc + c - 1 : nr, rhi = uint32_t(__shfl(int(wr.y), int(c ? c - 1 : 0)));
+            if (look && j < nop && c == 64 && rc + 64 < nr) {   // past the window
+                ri = range_of(rng, nr, o.x);
+                rhi = ri < nr ? rng[ri].y : 0u;
+            }
             uint32_t vi = 0, vd = 0, vc = 0;
             if (j < nop) {
-                const uint4 o = ops[j];
                 if (o.w & 1u) {
                     vd = o.y;
-                    const uint32_t i = range_of(rng, nr, o.x);
-                    if (!(i < nr && uint64_t(o.x) + o.y <= rng[i].y)) vc = o.y;
+                    if (!(ri < nr && uint64_t(o.x) + o.y <= rhi)) vc = o.y;
                 } else {
                     vi = o.y;
                 }
             }
+            const uint32_t rl = rdl(ri, min(nop - 1 - c0, 63u));
+            if (rl < nr) rc = rl;
             const uint32_t si = scan_incl(vi), sd = scan_incl(vd), sc = scan_incl(vc);
             while (pi < npick) {
                 const uint32_t pj = rdl(picks, pi);
@@ -1037,7 +1057,9 @@ __global__ __launch_bounds__(64) void cut_kernel(CutParams P) {
 
 int launch_cut(const CutParams &p, void *stream) {
     if (!p.n_groups) return 0;
-    hipLaunchKernelGGL(prep::cut_kernel, dim3(p.n_groups), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), p);
+    const size_t lds = size_t(p.max_ne) * 4;
+    if (lds > 64 * 1024) return 66;   // (staging cuts documents of at most PLAN_MAX_LDS_ENTRIES entries)
+    hipLaunchKernelGGL(prep::cut_kernel, dim3(p.n_groups), dim3(64), lds, reinterpret_cast<hipStream_t>(stream), p);
     return hipGetLastError() == hipSuccess ? 0 : 66;
 }
 

@@ -90,10 +90,13 @@ struct CutParams {
     const SegPlan *plans;
     const SegCap *caps;
     DocDesc *docs;
-    uint32_t *scr;      // per group 4 ne + 4 words (SegPlan::scr_off)
-    uint32_t n_groups, pad;
+    const uint32_t *pent;   // prep's first half: each parent slot's entry (the kernel then runs after
+                            // it); null: the kernel searches the entries itself
+    uint32_t *scr;      // per group cut_scratch_words (SegPlan::scr_off)
+    uint32_t n_groups, max_ne;   // max_ne: the LDS table's entries (the groups' largest document)
 };
-inline uint64_t cut_scratch_words(uint32_t ne) { return 4ull * ne + 4; }
+// suffix minima (ne + 1), cut ranges (2 ne), alignment
+inline uint64_t cut_scratch_words(uint32_t ne) { return 3ull * ne + 4; }
 int launch_cut(const CutParams &p, void *stream);
 // The three-launch pass one stage at a time (1: first half, 2: chains, 3: second half), so a
 // caller can start work that needs only the first half (the planner's walk) beside the rest.

@@ -1092,7 +1092,8 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
             const uint32_t targets = uint32_t(std::min<uint64_t>(c.max_seg, si.ops.size() / c.ops_per_seg));
             B->seg_plans.push_back(SegPlan{uint32_t(c.ops_per_seg), targets, scr});
             for (const SegCut &k : cuts) B->seg_caps.push_back(SegCap{k.u, uint32_t(k.ins)});
-            scr += cut_scratch_words(Dd.res[i].n_entries);
+            scr += (cut_scratch_words(Dd.res[i].n_entries) + 1) & ~1ull;
+            B->cut.max_ne = std::max<uint32_t>(B->cut.max_ne, Dd.res[i].n_entries);
         }
         CK(B->d_cutscr.alloc(std::max<uint64_t>(scr, 1)));
     }
@@ -1146,6 +1147,7 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
         c.caps = B->d_caps.p;
         c.docs = B->d_docs.p;
         c.scr = B->d_cutscr.p;
+        c.pent = B->p_pent.p;
         c.n_groups = uint32_t(B->seg_groups.size());
         if (!B->ev_cut) CK(hipEventCreateWithFlags(&B->ev_cut, hipEventDisableTiming));
     }
@@ -1232,6 +1234,13 @@ int launch_split_side(dtgpu_batch *B, hipStream_t s) {
     r.keep_fb = true;
     return launch_replay(r);
 }
+// A split pass plans its cuts before either pipeline's prep: the cut kernel then finds each
+// parent's entry itself.
+CutParams cut_before_prep(const dtgpu_batch *B) {
+    CutParams c = B->cut;
+    c.pent = nullptr;
+    return c;
+}
 // The main pipeline's prep and plan of a split pass (the documents outside the big tier).
 int launch_split_prep(dtgpu_batch *B, hipStream_t s) {
     PrepParams pp = B->prep;
@@ -1257,33 +1266,34 @@ int prep_and_plan(dtgpu_batch *B, hipStream_t s, hipEvent_t mid) {
     const bool overlap = prep && B->n_gpu_planned && B->prep.chain_flag && !B->prep.check && B->plan.walk &&
                          B->plan.coff && B->wstream && !getenv("DTGPU_NO_WALK_OVERLAP");
     if (!overlap) {
-        if (launch_cut(B->cut, s)) return ErrHip;
         if (prep && launch_prep(B->prep, s)) return ErrHip;
+        if (launch_cut(B->cut, s)) return ErrHip;   // (after prep: it reads the parents' entries)
         if (mid && hipEventRecord(mid, s) != hipSuccess) return ErrHip;
         return B->n_gpu_planned ? launch_plan(B->plan, s) : OK;
     }
     // the walk reads prep's CSR and, split, the planner only the entry records' heads
     PrepParams pp = B->prep;
     pp.short_rec = B->plan.split ? 1u : 0u;
-    if (B->cut.n_groups) {   // the cut planning beside prep's first half, on the walk's stream
-        if (hipEventRecord(B->ev_cut, s) != hipSuccess || hipStreamWaitEvent(B->wstream, B->ev_cut, 0) != hipSuccess ||
-            launch_cut(B->cut, B->wstream))
-            return ErrHip;
-    }
     if (launch_prep_stage(pp, s, 1)) return ErrHip;
     if (hipEventRecord(B->ev_w0, s) != hipSuccess || hipStreamWaitEvent(B->wstream, B->ev_w0, 0) != hipSuccess) return ErrHip;
     if (launch_walk(B->plan, B->wstream, true) != OK) return ErrHip;
     if (hipEventRecord(B->ev_w1, B->wstream) != hipSuccess) return ErrHip;
+    // the cut planning after the walk (it reads prep's parent entries), beside prep's second half
+    // and the planner (only the replay needs it)
+    if (B->cut.n_groups && (launch_cut(B->cut, B->wstream) || hipEventRecord(B->ev_cut, B->wstream) != hipSuccess))
+        return ErrHip;
     if (launch_prep_stage(pp, s, 2) || launch_prep_stage(pp, s, 3)) return ErrHip;
     if (mid && hipEventRecord(mid, s) != hipSuccess) return ErrHip;
     if (hipStreamWaitEvent(s, B->ev_w1, 0) != hipSuccess) return ErrHip;
-    return launch_plan(B->plan, s, false);
+    if (launch_plan(B->plan, s, false) != OK) return ErrHip;
+    if (B->cut.n_groups && hipStreamWaitEvent(s, B->ev_cut, 0) != hipSuccess) return ErrHip;
+    return OK;
 }
 
 int launch_all(dtgpu_batch *B, hipStream_t s) {
     if (B->xf_mode) return launch_replay_xf(B->large, s);
     if (B->split) {
-        if (launch_cut(B->cut, s)) return ErrHip;
+        if (launch_cut(cut_before_prep(B), s)) return ErrHip;
         int e = launch_split_side(B, s);
         if (!e) e = launch_split_prep(B, s);
         if (!e) e = launch_split_plan(B, s);
@@ -1825,7 +1835,7 @@ dtgpu_status dtgpu_batch_run_timed(dtgpu_batch *B, float *ms) {
     const bool prep = B->dec && !B->xf_mode;
     const bool split = prep && B->split;   // split pass: prep / plan times are the main pipeline's
     if (hipEventRecord(B->ev_prep, s) != hipSuccess) return DTGPU_ERR_HIP;
-    if (split && (launch_cut(B->cut, s) || launch_split_side(B, s))) return DTGPU_ERR_HIP;
+    if (split && (launch_cut(cut_before_prep(B), s) || launch_split_side(B, s))) return DTGPU_ERR_HIP;
     if (split) {
         if (launch_split_prep(B, s) != OK || hipEventRecord(B->ev0, s) != hipSuccess || launch_split_plan(B, s) != OK)
             return DTGPU_ERR_HIP;
