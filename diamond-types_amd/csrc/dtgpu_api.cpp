@@ -1946,7 +1946,7 @@ dtgpu_status dtgpu_batch_plan_profile(dtgpu_batch *B, size_t i, uint64_t out[8])
     return DTGPU_OK;
 }
 dtgpu_status dtgpu_batch_doc_stats(dtgpu_batch *B, size_t i, uint32_t out[29]) {
-    if (!B || i >= B->n || !out) return DTGPU_ERR_ARG;
+    if (!B || i >= B->docs.size() || !out) return DTGPU_ERR_ARG;   // (past n: the segment documents)
     DocResult r;
     if (hipMemcpyAsync(&r, B->d_results.p + i, sizeof r, hipMemcpyDeviceToHost, B->stream) != hipSuccess ||
         hipStreamSynchronize(B->stream) != hipSuccess)

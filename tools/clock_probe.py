@@ -19,6 +19,12 @@ def main():
     for _ in range(3):
         ms = b.run_timed()
     st = [b.doc_stats(i) for i in range(n)]
+    while True:   # the segment documents after them
+        try:
+            st.append(b.doc_stats(len(st)))
+        except Exception:
+            break
+    n = len(st)
     mt = np.array([s["cyc_ins"] for s in st], dtype=np.float64)
     rt = np.array([s["cyc_del"] for s in st], dtype=np.float64)
     t0 = np.array([s["cyc_tog"] for s in st], dtype=np.int64)
@@ -49,6 +55,12 @@ def by_unit(name="friendsforever", n=10000):
     b.run(); b.sync()
     b.run_timed()
     st = [b.doc_stats(i) for i in range(n)]
+    while True:   # the segment documents after them
+        try:
+            st.append(b.doc_stats(len(st)))
+        except Exception:
+            break
+    n = len(st)
     rt = np.array([s["cyc_del"] for s in st], dtype=np.float64) / 1e5
     t0 = np.array([s["cyc_tog"] for s in st], dtype=np.int64)
     hw = np.array([s["cyc_yjs"] for s in st], dtype=np.int64)
