@@ -1785,7 +1785,7 @@ __global__ __launch_bounds__(MW ? 64 * TOG_WAVES : 64) __attribute__((amdgpu_wav
 // suffix, checked) -- and writes the text with materialise()'s bytes and hash.  The document's
 // own result slot (its first segment) gets the length and hash, or the first failing
 // segment's status.
-constexpr uint32_t COMBINE_THREADS = 1024;
+constexpr uint32_t COMBINE_THREADS = 256;   // (1024: a few workgroups per CU, the cut batch in rounds)
 __global__ __launch_bounds__(COMBINE_THREADS) void combine_kernel(CombineParams P) {
     __shared__ uint32_t s_cut, s_bad, s_wsum[COMBINE_THREADS / 64];
     __shared__ u64 s_h[COMBINE_THREADS / 64];
