@@ -482,55 +482,37 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
         }
     }
     wave_fence();
-    // entry records (dt_host.hpp PlanInput::erec), 32 at a time: each lane builds its record in
-    // LDS (the ring's space), then the wave stores the 32 heads (1,024 contiguous bytes) and the
-    // 32 tails (1,536) with 16-byte lanes side by side -- a lane storing its own record leaves
-    // 16-byte pieces a record apart, each its own partial write request.  P.short_rec: the pass's
-    // walk reads the CSR and its planner only the heads, so the tails are neither built nor
-    // stored (their gathers of parent and child slots skipped with them)
-    for (uint32_t i0 = 0; i0 < ne; i0 += 32) {
-        // head: 0-3 start, end, parents offset / count; 4-7 first op run, op runs, chain, seq0.
-        // tail: 8-10 children offset / count, first parent LV; 11-13 and 14-16 the first two
-        // parents' entry, chain, count; 17 last child, 18 first child
+    // entry records (dt_host.hpp PlanInput::erec), one per lane: a lane's head (32 bytes) and
+    // tail (48) are contiguous and next to its neighbours', so the stores coalesce as they are
+    // (the 80-byte records of round 4 went through LDS, with a fence per 32 records).
+    // P.short_rec: the pass's walk reads the CSR and its planner only the heads, so the tails are
+    // neither built nor stored (their gathers of parent and child slots skipped with them)
+    {
         static_assert(EREC_WORDS == 20 && EREC_HEAD == 8, "erec layout");
-        uint4 *sh = reinterpret_cast<uint4 *>(lfw), *stl = sh + 64;   // 32 x 2, then 32 x 3 uint4
-        const uint32_t i = i0 + l;
-        if (l < 32 && i < ne) {
-            uint4 *h = sh + 2 * l, *t = stl + 3 * l;
+        uint4 *eh = reinterpret_cast<uint4 *>(erec);
+        uint4 *et = reinterpret_cast<uint4 *>(erec + size_t(ne) * EREC_HEAD);
+        for (uint32_t i = l; i < ne; i += 64) {
+            // head: 0-3 start, end, parents offset / count; 4-7 first op run, op runs, chain, seq0.
+            // tail: 8-10 children offset / count, first parent LV; 11-13 and 14-16 the first two
+            // parents' entry, chain, count; 17 last child, 18 first child
             const uint2 e = ent[i];
             const uint32_t p0 = poff[i], np = poff[i + 1] - p0;
             const uint32_t c0 = coff[i], nc = coff[i + 1] - c0;
             const uint32_t o0 = eop[i], o1 = eop[i + 1];
             const uint2 q = cs[i];
-            const bool h0 = np > 0, h1 = np > 1;
             PREP_ASSERT(p0 + np <= npar && c0 + nc <= npar && o0 <= o1 && o1 <= nops, PREP_T_ERECP);
-            if (CHECK && oob) {   // no reads through a bad index (the document fails with PREP_BOUNDS)
-                for (int k = 0; k < 2; k++) h[k] = make_uint4(0, 0, 0, 0);
-                for (int k = 0; k < 3; k++) t[k] = make_uint4(0, 0, 0, 0);
-            } else {
-                h[0] = make_uint4(e.x, e.y, p0, np);
-                h[1] = make_uint4(o0, o1 - o0, q.x, q.y + e.x);
-                if (!P.short_rec) {
-                    t[0] = make_uint4(c0, nc, h0 ? par[p0] : 0xFFFFFFFFu, h0 ? pent[p0] : 0xFFFFFFFFu);
-                    t[1] = make_uint4(h0 ? pch[p0] : 0u, h0 ? pcnt[p0] : 0u, h1 ? pent[p0 + 1] : 0xFFFFFFFFu,
-                                      h1 ? pch[p0 + 1] : 0u);
-                    t[2] = make_uint4(h1 ? pcnt[p0 + 1] : 0u, nc ? child[c0 + nc - 1] : 0xFFFFFFFFu, nc ? child[c0] : 0xFFFFFFFFu, 0u);
-                }
+            if (CHECK && oob) continue;   // no reads through a bad index (the document fails with PREP_BOUNDS)
+            eh[2 * size_t(i)] = make_uint4(e.x, e.y, p0, np);
+            eh[2 * size_t(i) + 1] = make_uint4(o0, o1 - o0, q.x, q.y + e.x);
+            if (!P.short_rec) {
+                const bool h0 = np > 0, h1 = np > 1;
+                et[3 * size_t(i)] = make_uint4(c0, nc, h0 ? par[p0] : 0xFFFFFFFFu, h0 ? pent[p0] : 0xFFFFFFFFu);
+                et[3 * size_t(i) + 1] = make_uint4(h0 ? pch[p0] : 0u, h0 ? pcnt[p0] : 0u, h1 ? pent[p0 + 1] : 0xFFFFFFFFu,
+                                                   h1 ? pch[p0 + 1] : 0u);
+                et[3 * size_t(i) + 2] = make_uint4(h1 ? pcnt[p0 + 1] : 0u, nc ? child[c0 + nc - 1] : 0xFFFFFFFFu,
+                                                   nc ? child[c0] : 0xFFFFFFFFu, 0u);
             }
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        const uint32_t cnt = min(32u, ne - i0);
-        uint4 *dh = reinterpret_cast<uint4 *>(erec + size_t(i0) * EREC_HEAD);
-        if (l < 2 * cnt) dh[l] = sh[l];
-        if (!P.short_rec) {
-            uint4 *dt = reinterpret_cast<uint4 *>(erec + size_t(ne) * EREC_HEAD + size_t(i0) * EREC_TAIL);
-            for (uint32_t w = l; w < 3 * cnt; w += 64) dt[w] = stl[w];
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
     // op runs: apply commands and the dense chain tables (LV | is_del per chain seq), one op run
     // per lane -- per entry, a history of few long entries (node_nodecc: 91 entries, 53k runs)
