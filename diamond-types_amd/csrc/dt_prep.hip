@@ -853,9 +853,11 @@ __device__ __forceinline__ uint32_t range_of(const uint2 *rng, uint32_t nr, uint
     return lo ? lo - 1 : nr;
 }
 
-__global__ __launch_bounds__(64) void cut_kernel(CutParams P) {
+constexpr uint32_t CUT_WAVES = 4;   // the op-run pass (step 5) on four waves: a long document's 53k runs
+__global__ __launch_bounds__(64 * CUT_WAVES) void cut_kernel(CutParams P) {
     if (blockIdx.x >= P.n_groups) return;
-    const uint32_t l = lane();
+    const uint32_t l = lane(), w = threadIdx.x / 64;
+    __shared__ uint32_t s_pick[64], s_np, s_nr, s_at[3][64], s_tot[CUT_WAVES][3], s_ok;
     const SegGroup G = P.groups[blockIdx.x];
     const SegPlan SP = P.plans[blockIdx.x];
     const uint32_t d = P.seg_docs[G.first];
@@ -871,9 +873,12 @@ __global__ __launch_bounds__(64) void cut_kernel(CutParams P) {
     int32_t *suf = reinterpret_cast<int32_t *>(P.scr + SP.scr_off);        // ne + 1
     uint2 *rng = reinterpret_cast<uint2 *>(P.scr + SP.scr_off + ((uint64_t(ne) + 2) & ~1ull));   // <= ne ranges
 
+    if (threadIdx.x == 0) s_ok = 0;
+    __syncthreads();
+    if (w == 0) {
     // 1. nxt (LDS atomics) and each entry's smallest parent (-1: ROOT)
     for (uint32_t j = l; j < ne; j += 64) nxt[j] = 0xFFFFFFFFu;
-    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     for (uint32_t e = l; e < ne; e += 64) {
         const uint32_t k0 = poff[e], k1 = poff[e + 1];
         int32_t mp = k0 == k1 ? -1 : 0x7FFFFFFF;
@@ -884,7 +889,7 @@ __global__ __launch_bounds__(64) void cut_kernel(CutParams P) {
         }
         suf[e] = mp;
     }
-    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     agent_fence();
     // 2. suffix minima of the smallest parents (suf[k] = over entries >= k; suf[ne] = none)
     {
@@ -926,7 +931,7 @@ __global__ __launch_bounds__(64) void cut_kernel(CutParams P) {
         }
     }
     agent_fence();
-    if (nr == 0) return;
+    if (nr != 0) {
     auto in_cut = [&](uint32_t v) {
         const uint32_t i = range_of(rng, nr, v);
         return i < nr && v <= rng[i].y;
@@ -952,20 +957,35 @@ __global__ __launch_bounds__(64) void cut_kernel(CutParams P) {
         }
     }
     while (npick && nop - rdl(picks, npick - 1) < q4) npick--;
-    if (npick + 1 != S) return;   // not the staged segments (the poisoned ranges then fail the document)
-    // 5. inserts, deletes and concurrent deletes before each cut (exclusive prefix sums)
+    if (npick + 1 == S) {   // else not the staged segments (the poisoned ranges then fail the document)
+        if (l < npick) s_pick[l] = picks;
+        if (l == 0) { s_np = npick; s_nr = nr; s_ok = 1; }
+    }
+    }   // nr != 0
+    }
+    __syncthreads();
+    if (!s_ok) return;
+    // 5. inserts, deletes and concurrent deletes before each cut (exclusive prefix sums), the op
+    //    runs split in four contiguous parts, one per wave; each part's sums are offset by the
+    //    parts before it afterwards
+    const uint32_t npick = s_np, nr = s_nr;
+    const uint32_t picks = l < npick ? s_pick[l] : 0u;
     uint32_t at_ins = 0, at_del = 0, at_dc = 0;   // lane i: before the i-th cut
     uint32_t tot_ins = 0;
     {
         // a delete run is inside one range or concurrent: the runs' LVs ascend, so each chunk
         // looks its runs up among the 64 ranges from the previous chunk's last one (one load,
         // a search by lane permutes), a global bisection only past that window
+        const uint32_t part = ((nop + CUT_WAVES - 1) / CUT_WAVES + 63) & ~63u;
+        const uint32_t b0 = min(nop, w * part), b1 = min(nop, b0 + part);
         uint32_t ci = 0, cd = 0, cc = 0, pi = 0;
-        uint32_t rc = 0;   // range of the previous chunk's last run (ranges ascend with LVs)
         const uint32_t last_pick = rdl(picks, npick - 1);   // past it only the inserts are summed
-        for (uint32_t c0 = 0; c0 < nop; c0 += 64) {
+        uint32_t rc = b0 < b1 ? range_of(rng, nr, ops[b0].x) : 0u;
+        if (rc >= nr) rc = 0;
+        while (pi < npick && rdl(picks, pi) < b0) pi++;
+        for (uint32_t c0 = b0; c0 < b1; c0 += 64) {
             const uint32_t j = c0 + l;
-            const uint4 o = j < nop ? ops[j] : make_uint4(0xFFFFFFFFu, 0, 0, 0);
+            const uint4 o = j < b1 ? ops[j] : make_uint4(0xFFFFFFFFu, 0, 0, 0);
             const bool look = c0 <= last_pick;
             const uint2 wr = look && rc + l < nr ? rng[rc + l] : make_uint2(0xFFFFFFFFu, 0);
             uint32_t c = 0;   // window ranges whose first cut is <= the run's LV
@@ -974,12 +994,12 @@ __global__ __launch_bounds__(64) void cut_kernel(CutParams P) {
                 if (uint32_t(__shfl(int(wr.x), int(c + st - 1))) <= o.x) c += st;
             if (c == 63 && rdl(wr.x, 63) <= o.x) c = 64;
             uint32_t ri = c ? rc + c - 1 : nr, rhi = uint32_t(__shfl(int(wr.y), int(c ? c - 1 : 0)));
-            if (look && j < nop && c == 64 && rc + 64 < nr) {   // past the window
+            if (look && j < b1 && ((c == 64 && rc + 64 < nr) || (c == 0 && rc > 0))) {   // outside the window
                 ri = range_of(rng, nr, o.x);
                 rhi = ri < nr ? rng[ri].y : 0u;
             }
             uint32_t vi = 0, vd = 0, vc = 0;
-            if (j < nop) {
+            if (j < b1) {
                 if (o.w & 1u) {
                     vd = o.y;
                     if (!(ri < nr && uint64_t(o.x) + o.y <= rhi)) vc = o.y;
@@ -987,22 +1007,35 @@ __global__ __launch_bounds__(64) void cut_kernel(CutParams P) {
                     vi = o.y;
                 }
             }
-            const uint32_t rl = rdl(ri, min(nop - 1 - c0, 63u));
+            const uint32_t rl = rdl(ri, min(b1 - 1 - c0, 63u));
             if (rl < nr) rc = rl;
             const uint32_t si = scan_incl(vi), sd = scan_incl(vd), sc = scan_incl(vc);
             while (pi < npick) {
                 const uint32_t pj = rdl(picks, pi);
-                if (pj >= c0 + 64) break;
-                const uint32_t t = pj - c0;   // exclusive prefix at lane t
-                const uint32_t ei = ci + rdl(si, t) - rdl(vi, t), ed = cd + rdl(sd, t) - rdl(vd, t), ec = cc + rdl(sc, t) - rdl(vc, t);
-                at_ins = l == pi ? ei : at_ins;
-                at_del = l == pi ? ed : at_del;
-                at_dc = l == pi ? ec : at_dc;
+                if (pj >= c0 + 64 || pj >= b1) break;
+                const uint32_t t = pj - c0;   // exclusive prefix (within the part) at lane t
+                if (l == 0) {
+                    s_at[0][pi] = ci + rdl(si, t) - rdl(vi, t);
+                    s_at[1][pi] = cd + rdl(sd, t) - rdl(vd, t);
+                    s_at[2][pi] = cc + rdl(sc, t) - rdl(vc, t);
+                }
                 pi++;
             }
             ci += rdl(si, 63); cd += rdl(sd, 63); cc += rdl(sc, 63);
         }
-        tot_ins = ci;
+        if (l == 0) { s_tot[w][0] = ci; s_tot[w][1] = cd; s_tot[w][2] = cc; }
+        __syncthreads();
+        if (w) return;
+        // offsets: every part before the cut's own
+        uint32_t oi = 0, od = 0, oc = 0, pw = 0;
+        const uint32_t pk = picks;
+        for (uint32_t v = 0; v < CUT_WAVES; v++) {
+            const uint32_t vb0 = min(nop, v * part);
+            if (l < npick && pk >= vb0 + part) { oi += s_tot[v][0]; od += s_tot[v][1]; oc += s_tot[v][2]; }
+            (void)pw;
+        }
+        if (l < npick) { at_ins = oi + s_at[0][l]; at_del = od + s_at[1][l]; at_dc = oc + s_at[2][l]; }
+        for (uint32_t v = 0; v < CUT_WAVES; v++) tot_ins += s_tot[v][0];
     }
     // 6. each segment's range and placeholder bound, against what staging reserved
     bool fits = true;
@@ -1041,7 +1074,7 @@ int launch_cut(const CutParams &p, void *stream) {
     if (!p.n_groups) return 0;
     const size_t lds = size_t(p.max_ne) * 4;
     if (lds > 64 * 1024) return 66;   // (staging cuts documents of at most PLAN_MAX_LDS_ENTRIES entries)
-    hipLaunchKernelGGL(prep::cut_kernel, dim3(p.n_groups), dim3(64), lds, reinterpret_cast<hipStream_t>(stream), p);
+    hipLaunchKernelGGL(prep::cut_kernel, dim3(p.n_groups), dim3(64 * prep::CUT_WAVES), lds, reinterpret_cast<hipStream_t>(stream), p);
     return hipGetLastError() == hipSuccess ? 0 : 66;
 }
 

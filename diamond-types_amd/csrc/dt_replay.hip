@@ -1785,7 +1785,9 @@ __global__ __launch_bounds__(MW ? 64 * TOG_WAVES : 64) __attribute__((amdgpu_wav
 // suffix, checked) -- and writes the text with materialise()'s bytes and hash.  The document's
 // own result slot (its first segment) gets the length and hash, or the first failing
 // segment's status.
-constexpr uint32_t COMBINE_THREADS = 256;   // (1024: a few workgroups per CU, the cut batch in rounds)
+// COMBINE_THREADS: 1024 threads for a few cut documents (long texts: node_nodecc's 13 segments
+// combine in ~0.9 ms), 256 for many (a batch's cut documents in one round of workgroups, not four)
+template <uint32_t COMBINE_THREADS>
 __global__ __launch_bounds__(COMBINE_THREADS) void combine_kernel(CombineParams P) {
     __shared__ uint32_t s_cut, s_bad, s_wsum[COMBINE_THREADS / 64];
     __shared__ u64 s_h[COMBINE_THREADS / 64];
@@ -2001,8 +2003,11 @@ int launch_replay_xf(const BatchParams &large, void *stream) {
 
 int launch_combine(const CombineParams &p, void *stream) {
     if (!p.n_groups) return OK;
-    hipLaunchKernelGGL(dev::combine_kernel, dim3(p.n_groups), dim3(dev::COMBINE_THREADS), 0,
-                       reinterpret_cast<hipStream_t>(stream), p);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    static int n_cu = 0;
+    if (!n_cu && hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) n_cu = 256;
+    if (p.n_groups >= uint32_t(2 * std::max(n_cu, 1))) hipLaunchKernelGGL(dev::combine_kernel<256>, dim3(p.n_groups), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL(dev::combine_kernel<1024>, dim3(p.n_groups), dim3(1024), 0, s, p);
     return hipGetLastError() == hipSuccess ? OK : ErrHip;
 }
 
