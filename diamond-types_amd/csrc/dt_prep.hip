@@ -562,15 +562,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
             if (j0 + 64 < nops) fetch(j0 + 64, ebase, we, wq, o);
             // the run's dense slots [dch + qy + lv, + len) lie inside the chain tables
             PREP_ASSERT(!live || (qx < nch && uint64_t(uint32_t(dch + qy + oc.x)) + oc.y <= D.n_lv), PREP_T_DENSE);
-            if (live && (!CHECK || !oob)) {
+            const bool ok = live && (!CHECK || !oob);
+            const uint32_t flag = (oc.w & 1u) ? TL_DEL : 0u;
+            const uint32_t dst = dch + qy + oc.x;   // the run's first dense slot
+            constexpr uint32_t LONG_RUN = 64;      // longer runs are filled by the whole wave
+            if (ok) {
                 const bool del = oc.w & 1u;
                 opc[j] = Cmd{del ? (CMD_DEL | ((oc.w & 2u) ? 16u : 0u)) : uint32_t(CMD_INS), oc.x, oc.y, oc.z};
                 if (!del) n_ins += oc.y;
+            }
+            if (ok && oc.y <= LONG_RUN) {
                 // the run's dense slots (chain offset + seq0 - start + LV): 16-byte stores between
                 // a scalar head and tail.  (Filling the chunk LV by LV across the lanes instead
                 // measured no faster.)
-                const uint32_t flag = del ? TL_DEL : 0u;
-                uint32_t *dp = dense + uint32_t(dch + qy + oc.x);
+                uint32_t *dp = dense + dst;
                 uint32_t v = 0;
                 for (; v < oc.y && (reinterpret_cast<uintptr_t>(dp + v) & 15u); v++) dp[v] = (oc.x + v) | flag;
                 for (; v + 4 <= oc.y; v += 4) {
@@ -578,6 +583,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_PREP_W
                     *reinterpret_cast<uint4 *>(dp + v) = make_uint4(b | flag, (b + 1) | flag, (b + 2) | flag, (b + 3) | flag);
                 }
                 for (; v < oc.y; v++) dp[v] = (oc.x + v) | flag;
+            }
+            // a long run (node_nodecc's pastes: thousands of LVs) by every lane, 256 bytes per
+            // store instead of one lane's serial stores setting the chunk's time
+            for (uint64_t m = ballot(ok && oc.y > LONG_RUN); m; m &= m - 1) {
+                const uint32_t k = ctz(m);
+                const uint32_t d0 = rdl(dst, k), lv0 = rdl(oc.x, k), len = rdl(oc.y, k), fl = rdl(flag, k);
+                for (uint32_t v = l; v < len; v += 64) dense[d0 + v] = (lv0 + v) | fl;
             }
         }
     }
