@@ -1193,22 +1193,27 @@ __device__ __forceinline__ bool utf8_offsets(const uint8_t *t, uint32_t n, uint3
         if (!m) continue;
         const uint32_t need = popc(m), r = popc(m & lt_mask());
         if (ballot(ins && k != kbase + r)) return false;
-        uint32_t got = 0;
+        uint32_t got = 0, lastb = 0, lastc = 0;
         for (uint32_t w = cur; got < need; w += 64) {
             if (w >= n) return false;
             const uint32_t j = w + l;
-            const bool st = j < n && (t[j] & 0xC0u) != 0x80u;
+            const uint32_t c = j < n ? t[j] : 0x80u;
+            const bool st = (c & 0xC0u) != 0x80u;
             const uint64_t sm = ballot(st);
             const uint32_t rk = got + popc(sm & lt_mask());
             if (st && rk < need) slot[rk] = j;
+            // the chunk's last char start and its lead byte, straight from the window's lanes
+            // (no read back of the slot and no dependent byte load before the next chunk)
+            const uint64_t lm = ballot(st && rk == need - 1);
+            if (lm) { lastb = rdl(j, ctz(lm)); lastc = rdl(c, ctz(lm)); }
             got += popc(sm);
         }
-        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         if (ins) cbyte[lv] = slot[r];
-        const uint32_t lastb = slot[need - 1];
-        __syncthreads();
-        const uint8_t c0 = t[lastb];
-        cur = lastb + (c0 < 0x80 ? 1u : (c0 & 0xE0u) == 0xC0u ? 2u : (c0 & 0xF0u) == 0xE0u ? 3u : 4u);
+        __builtin_amdgcn_wave_barrier();   // (slot is rewritten by the next chunk: reads first, in order within the wave)
+        cur = lastb + (lastc < 0x80 ? 1u : (lastc & 0xE0u) == 0xC0u ? 2u : (lastc & 0xF0u) == 0xE0u ? 3u : 4u);
         kbase += need;
     }
     return kbase == n_chars;
