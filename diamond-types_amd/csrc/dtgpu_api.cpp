@@ -542,7 +542,9 @@ std::vector<uint8_t> late_documents(const dtgpu_batch &B, const SegSettings &sc,
     const size_t resident = std::min<size_t>(32, 163840 / std::max<size_t>(gran, 1280)) * size_t(std::max(B.n_cu, 1));
     std::vector<uint32_t> order(B.tier_list[0].begin(), B.tier_list[0].end());
     std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return B.n_lv[a] > B.n_lv[b]; });
-    for (size_t k = resident; k < order.size(); k++)
+    // (a batch of many rounds: its last round's worth, the documents that end the batch)
+    const size_t from = std::max(resident, order.size() > resident ? order.size() - resident : size_t(0));
+    for (size_t k = from; k < order.size(); k++)
         if (order[k] < B.n && n_ops(order[k]) >= 128) late[order[k]] = 1;
     return late;
 }
