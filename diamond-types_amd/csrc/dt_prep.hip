@@ -876,6 +876,10 @@ __global__ __launch_bounds__(64 * CUT_WAVES) void cut_kernel(CutParams P) {
     const PrepDesc D = P.pdocs[d];
     const uint32_t ne = D.ne, nop = D.n_ops, S = G.count, T = SP.n_targets;   // segments; equal-share targets
     if (S < 2 || S > 64 || T < S || ne == 0 || nop == 0) return;   // (staging makes none such; the poisoned ranges then fail)
+    // short documents: one wave (the others leave before any barrier; a barrier waits only for
+    // the waves still running)
+    const uint32_t NW = nop >= 4096 ? CUT_WAVES : 1u;
+    if (w >= NW) return;
     const uint2 *ent = reinterpret_cast<const uint2 *>(P.d_ent) + D.d_ent;
     const uint32_t *poff = P.d_poff + D.d_poff, *par = P.d_par + D.d_par;
     const uint4 *ops = reinterpret_cast<const uint4 *>(P.d_ops) + D.d_op;   // lv, len, pos, kind (bit 0: delete)
@@ -988,7 +992,7 @@ __global__ __launch_bounds__(64 * CUT_WAVES) void cut_kernel(CutParams P) {
         // a delete run is inside one range or concurrent: the runs' LVs ascend, so each chunk
         // looks its runs up among the 64 ranges from the previous chunk's last one (one load,
         // a search by lane permutes), a global bisection only past that window
-        const uint32_t part = ((nop + CUT_WAVES - 1) / CUT_WAVES + 63) & ~63u;
+        const uint32_t part = ((nop + NW - 1) / NW + 63) & ~63u;
         const uint32_t b0 = min(nop, w * part), b1 = min(nop, b0 + part);
         uint32_t ci = 0, cd = 0, cc = 0, pi = 0;
         const uint32_t last_pick = rdl(picks, npick - 1);   // past it only the inserts are summed
@@ -1041,13 +1045,13 @@ __global__ __launch_bounds__(64 * CUT_WAVES) void cut_kernel(CutParams P) {
         // offsets: every part before the cut's own
         uint32_t oi = 0, od = 0, oc = 0, pw = 0;
         const uint32_t pk = picks;
-        for (uint32_t v = 0; v < CUT_WAVES; v++) {
+        for (uint32_t v = 0; v < NW; v++) {
             const uint32_t vb0 = min(nop, v * part);
             if (l < npick && pk >= vb0 + part) { oi += s_tot[v][0]; od += s_tot[v][1]; oc += s_tot[v][2]; }
             (void)pw;
         }
         if (l < npick) { at_ins = oi + s_at[0][l]; at_del = od + s_at[1][l]; at_dc = oc + s_at[2][l]; }
-        for (uint32_t v = 0; v < CUT_WAVES; v++) tot_ins += s_tot[v][0];
+        for (uint32_t v = 0; v < NW; v++) tot_ins += s_tot[v][0];
     }
     // 6. each segment's range and placeholder bound, against what staging reserved
     bool fits = true;

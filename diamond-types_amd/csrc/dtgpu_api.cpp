@@ -113,6 +113,7 @@ SegSettings seg_settings() {
     if (const char *e = getenv("DTGPU_SEG")) s.on = *e != '0';
     if (const char *e = getenv("DTGPU_SEG_OPS")) s.ops_per_seg = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
     if (const char *e = getenv("DTGPU_SEG_MAX")) s.max_seg = uint32_t(std::max<uint64_t>(1, strtoull(e, nullptr, 10)));
+    s.max_seg = std::min<uint32_t>(s.max_seg, 64);   // the device cut planning's lane-per-segment bound
     return s;
 }
 // Cut ranges [a, b] (every v in them is a cut), in LV order: at entry k ([s, t), parents P)
