@@ -285,7 +285,10 @@ uint64_t dtgpu_batch_algorithmic_bytes(dtgpu_batch *batch);
  * (DTGPU_DEBUG=2: cycles/16 in insert, delete, retreat+advance, materialise, YjsMod scans,
  * splits, and the insert phases find / block load / origin_right / run; scan and split
  * counts; total cycles/16), [22] superblocks, [23] 1 if the index was in LDS, [24..26] the
- * retreat/advance pass split, [27] block loads that rebuilt stale masks, [28] block loads. */
+ * retreat/advance pass split, [27] block loads that rebuilt stale masks, [28] block loads.
+ * doc < the batch size addresses a document (its first segment when it was cut); past it, the
+ * cut documents' later segments in staging order, up to the first index that returns
+ * DTGPU_ERR_ARG. */
 dtgpu_status dtgpu_batch_doc_stats(dtgpu_batch *batch, size_t doc, uint32_t out[29]);
 /* Cut replay: the LV segments document `doc` replays as, each on its own wave -- cut where the
  * whole history below the cut is one version that every later op has seen, the boundary the
