@@ -830,9 +830,10 @@ __global__ __launch_bounds__(64) void chain_kernel(PrepParams P) {
 //   entry's last LV is named as a parent by some entry up to k: max over j < k of nxt(j) <= k,
 //   nxt(j) = the first entry naming j's last LV -- and the range is [start + 1, min(end, 1 + the
 //   smallest parent of every later entry)];
-//   the cuts are the op-run starts inside a range nearest to the equal-share targets (nearest
-//   first, the earlier of two at the same distance), a later one only past the previous one plus
-//   a quarter share, none a quarter share from the end;
+//   the cuts are the op-run starts inside a range nearest to the op runs where the cost (SegPlan::w_op,
+//   dt_prep.hpp) reaches each equal share (nearest first, the earlier of two at the same
+//   distance), a later one only a quarter share of the cost past the previous one, none a
+//   quarter share from the end;
 //   a segment's placeholders bound the text at its start: min(inserts, inserts - deletes + the
 //   deletes not inside one range).
 // (the cut kernel's scratch is written by stores and memory-side atomics and read back by other
@@ -952,11 +953,24 @@ __global__ __launch_bounds__(64 * CUT_WAVES) void cut_kernel(CutParams P) {
         const uint32_t i = range_of(rng, nr, v);
         return i < nr && v <= rng[i].y;
     };
-    // 4. the cuts: op-run starts in a range, nearest to k * nop / S
-    const uint32_t q4 = SP.ops_per_seg / 4;
-    uint32_t picks = 0, npick = 0, last = 0;   // lane i of picks: the i-th cut's op run
+    // 4. the cuts: op-run starts in a range, nearest to where the cost reaches k / T of the total
+    const uint4 lastop = ops[nop - 1];
+    const uint64_t total = uint64_t(SP.w_op) * nop + lastop.x + lastop.y, q4c = total / (4ull * T);
+    auto cost = [&](uint32_t j) { return uint64_t(SP.w_op) * j + ops[j].x; };
+    uint32_t tj = 0;   // lane k: the first op run whose cost reaches k * total / T (a bisection each)
+    if (l >= 1 && l < T) {
+        const uint64_t tc = uint64_t(l) * total / T;
+        uint32_t lo = 0, hi = nop;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (cost(mid) < tc) lo = mid + 1; else hi = mid;
+        }
+        tj = lo;
+    }
+    uint32_t picks = 0, npick = 0;   // lane i of picks: the i-th cut's op run
+    uint64_t lastc = 0;
     for (uint32_t k = 1; k < T; k++) {
-        const uint32_t target = uint32_t(uint64_t(k) * nop / T);
+        const uint32_t target = rdl(tj, k);
         const uint32_t dmax = nop / (2 * T) + 1;
         uint32_t best = 0xFFFFFFFFu;
         for (uint32_t d0 = 0; d0 <= dmax && d0 < nop && best == 0xFFFFFFFFu; d0 += 32) {
@@ -966,13 +980,16 @@ __global__ __launch_bounds__(64 * CUT_WAVES) void cut_kernel(CutParams P) {
             const uint64_t m = ballot(ok);
             if (m) best = rdl(j, ctz(m));
         }
-        if (best != 0xFFFFFFFFu && (npick == 0 || best > last + q4)) {
-            picks = l == npick ? best : picks;
-            npick++;
-            last = best;
+        if (best != 0xFFFFFFFFu) {
+            const uint64_t bc = cost(best);
+            if (npick == 0 || bc > lastc + q4c) {
+                picks = l == npick ? best : picks;
+                npick++;
+                lastc = bc;
+            }
         }
     }
-    while (npick && nop - rdl(picks, npick - 1) < q4) npick--;
+    while (npick && total - cost(rdl(picks, npick - 1)) < q4c) npick--;
     if (npick + 1 == S) {   // else not the staged segments (the poisoned ranges then fail the document)
         if (l < npick) s_pick[l] = picks;
         if (l == 0) { s_np = npick; s_nr = nr; s_ok = 1; }

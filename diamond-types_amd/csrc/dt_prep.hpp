@@ -75,12 +75,18 @@ inline uint64_t prep_kids_offset(uint32_t n_par, uint32_t ne) { return (uint64_t
 int launch_prep(const PrepParams &p, void *stream);
 
 // Cut planning inside the checkout pass (cut_kernel): for every cut document (SegGroup), from the
-// decoded oplog, the cut ranges (dtgpu_api.cpp cut_ranges), the cuts nearest to equal op-run
+// decoded oplog, the cut ranges (dtgpu_api.cpp cut_ranges), the cuts nearest to equal cost
 // shares (plan_segments) and each segment's LV range and placeholder bound, written into its
 // DocDesc.  Staging only reserves each segment's arenas (SegCap: the placeholders and inserts
 // its arenas hold) and poisons the descriptors' ranges, so a pass without this kernel fails.
-struct SegPlan { uint32_t ops_per_seg, n_targets; uint64_t scr_off; };   // per group: the planner's
-                                                                          // share, its target count, scratch (words)
+// A segment's replay cost in LVs: the replay holds one item per LV, so an op run costs its
+// length (inserted items, deleted items toggled) plus a fixed share per run (the position lookup
+// and the block loads): the cuts share out w_op * runs + LVs, not the runs alone (rustcode's
+// pastes of 50k characters put 4x the work in 1/16th of the runs).  cost(j) = w_op * j + the LV
+// of op run j; the total is w_op * runs + the last run's end.
+constexpr uint32_t SEG_W_OP = 48;   // default w_op (DTGPU_SEG_W)
+struct SegPlan { uint32_t w_op, n_targets; uint64_t scr_off; };   // per group: the cost weight of an
+                                                                  // op run, the target count, scratch (words)
 struct SegCap { uint32_t u, ins; };                                 // per seg_docs slot
 struct CutParams {
     const uint32_t *d_ops, *d_ent, *d_poff, *d_par;   // decoder arenas (as PrepParams)

@@ -107,9 +107,10 @@ struct SegInput {
     std::vector<uint64_t> par;
     std::vector<std::array<uint64_t, 3>> ops;         // op runs (lv, len, kind: 0 ins, 1 del) in LV order
 };
-struct SegSettings { bool on; uint64_t ops_per_seg; uint32_t max_seg; };
+struct SegSettings { bool on; uint64_t ops_per_seg; uint32_t max_seg, w_op; };
 SegSettings seg_settings() {
-    SegSettings s{true, 500, 16};
+    SegSettings s{true, 500, 16, SEG_W_OP};
+    if (const char *e = getenv("DTGPU_SEG_W")) s.w_op = uint32_t(std::min<uint64_t>(strtoull(e, nullptr, 10), 1u << 20));
     if (const char *e = getenv("DTGPU_SEG")) s.on = *e != '0';
     if (const char *e = getenv("DTGPU_SEG_OPS")) s.ops_per_seg = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
     if (const char *e = getenv("DTGPU_SEG_MAX")) s.max_seg = uint32_t(std::max<uint64_t>(1, strtoull(e, nullptr, 10)));
@@ -158,10 +159,19 @@ std::vector<SegCut> plan_segments(const SegInput &in, const SegSettings &cfg) {
         auto it = std::upper_bound(cuts.begin(), cuts.end(), std::make_pair(lv, UINT64_MAX));
         return it != cuts.begin() && lv + len <= std::prev(it)->second;
     };
-    // op-run starts that are cuts, nearest to the equal-op targets
+    // op-run starts that are cuts, nearest to the op runs where the cost reaches each equal share
+    // (SegPlan::w_op, dt_prep.hpp); later cuts a quarter share of the cost past the previous one
+    auto cost = [&](size_t j) { return uint64_t(cfg.w_op) * j + in.ops[j][0]; };
+    const uint64_t total = uint64_t(cfg.w_op) * nop + in.ops[nop - 1][0] + in.ops[nop - 1][1], q4c = total / (4ull * S);
     std::vector<size_t> pick;
     for (uint32_t k = 1; k < S; k++) {
-        const size_t target = size_t(uint64_t(k) * nop / S);
+        const uint64_t tc = uint64_t(k) * total / S;
+        size_t lo = 0, hi = nop;   // the first op run whose cost reaches tc
+        while (lo < hi) {
+            const size_t mid = (lo + hi) / 2;
+            if (cost(mid) < tc) lo = mid + 1; else hi = mid;
+        }
+        const size_t target = lo;
         size_t best = SIZE_MAX;
         for (size_t d = 0; d < nop && best == SIZE_MAX; d++) {
             for (size_t j : {target - std::min(target, d), target + d}) {
@@ -169,9 +179,9 @@ std::vector<SegCut> plan_segments(const SegInput &in, const SegSettings &cfg) {
             }
             if (d > nop / (2 * S)) break;   // no cut near this target
         }
-        if (best != SIZE_MAX && (pick.empty() || best > pick.back() + cfg.ops_per_seg / 4)) pick.push_back(best);
+        if (best != SIZE_MAX && (pick.empty() || cost(best) > cost(pick.back()) + q4c)) pick.push_back(best);
     }
-    while (!pick.empty() && nop - pick.back() < cfg.ops_per_seg / 4) pick.pop_back();
+    while (!pick.empty() && total - cost(pick.back()) < q4c) pick.pop_back();
     if (pick.empty()) return out;
     // prefix counts at the picked op runs
     int64_t ins = 0, del = 0, dconc = 0;
@@ -1093,7 +1103,7 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
                 !add_segments(*B, i, cuts, seg_tier[i], seg_est[i], lds_fill, pc_total, blk_total, gidx_total, src_total))
                 continue;
             const uint32_t targets = uint32_t(std::min<uint64_t>(c.max_seg, si.ops.size() / c.ops_per_seg));
-            B->seg_plans.push_back(SegPlan{uint32_t(c.ops_per_seg), targets, scr});
+            B->seg_plans.push_back(SegPlan{c.w_op, targets, scr});
             for (const SegCut &k : cuts) B->seg_caps.push_back(SegCap{k.u, uint32_t(k.ins)});
             scr += (cut_scratch_words(Dd.res[i].n_entries) + 1) & ~1ull;
             B->cut.max_ne = std::max<uint32_t>(B->cut.max_ne, Dd.res[i].n_entries);
