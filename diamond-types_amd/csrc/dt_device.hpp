@@ -26,9 +26,13 @@ struct DocDesc {
     uint32_t seg_lo, seg_hi, seg_u, src_cap;
     uint64_t pc_off;        // into pos / ao: lv_off, or a segment's own region (n_lv + seg_u words)
     uint64_t src_off;       // into src (uint32 units), or ~0
-    uint32_t pad;
+    uint32_t flags;         // DOC_CRITICAL
 };
 constexpr uint32_t SEG_PHANTOM = 0x80000000u;   // source-list entry: placeholder item index
+// The batch's critical path (dtgpu_api.cpp mark_critical): a replay several times longer than the
+// batch's typical one, which the waves beside it would otherwise slow down by sharing the SIMD's
+// issue; its waves take the top priority.
+constexpr uint32_t DOC_CRITICAL = 1u;
 
 struct DocResult {
     uint32_t status, out_len;

@@ -1734,6 +1734,7 @@ __global__ __launch_bounds__(MW ? 64 * TOG_WAVES : 64) __attribute__((amdgpu_wav
         d = U(P.fb_list[j]);
     }
     const DocDesc dd = P.docs[d];
+    if (dd.flags & DOC_CRITICAL) __builtin_amdgcn_s_setprio(3);
     Doc D;
     D.doc = d;
     D.desc = P.docs + d;

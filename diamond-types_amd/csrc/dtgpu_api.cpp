@@ -260,6 +260,8 @@ struct dtgpu_batch {
     // cut replay: segment documents (docs[n..]: a long document's later LV ranges, replayed
     // beside its first one) and the combine step that joins their source lists into its text
     std::vector<uint64_t> seg_cost;
+    std::vector<uint64_t> first_cost;   // per document: its first segment's LVs when cut (else 0)
+    std::vector<uint64_t> n_runs;       // per document: its op runs (mark_critical)
     std::vector<SegGroup> seg_groups;
     std::vector<uint32_t> seg_docs;
     DevBuf<SegGroup> d_groups;
@@ -368,12 +370,17 @@ size_t n_lds_docs(const dtgpu_batch &B) {
     return k;
 }
 // Launch order of the documents: the LDS tiers, then the HBM tier; inside a list the documents
-// go by descending LVs, so the hardware dispatcher starts the longest replays first (LPT inside
-// the GPU: the short ones fill in behind them).
+// go by descending LVs (a cut document's first segment by its own), so the hardware dispatcher
+// starts the longest replays first (LPT inside the GPU: the short ones fill in behind them), the
+// critical ones (DOC_CRITICAL) before all.
 std::vector<uint32_t> tier_lists(dtgpu_batch &B) {
     std::vector<uint32_t> all;
     auto by_cost = [&](std::vector<uint32_t> &v) {
-        auto cost = [&](uint32_t d) { return d < B.n ? B.n_lv[d] : B.seg_cost[d - B.n]; };
+        auto cost = [&](uint32_t d) -> uint64_t {
+            if (B.docs[d].flags & DOC_CRITICAL) return UINT64_MAX;   // the critical path first
+            if (d >= B.n) return B.seg_cost[d - B.n];
+            return d < B.first_cost.size() && B.first_cost[d] ? B.first_cost[d] : B.n_lv[d];
+        };
         std::stable_sort(v.begin(), v.end(), [&](uint32_t a, uint32_t b) { return cost(a) > cost(b); });
         append(all, v);
     };
@@ -485,6 +492,8 @@ bool add_segments(dtgpu_batch &B, uint32_t i, const std::vector<SegCut> &cuts, i
         src_total += cuts[0].ins;
     }
     B.seg_docs.push_back(i);
+    if (B.first_cost.size() < B.n) B.first_cost.resize(B.n, 0);
+    B.first_cost[i] = std::max<uint64_t>(1, cuts[0].hi);
     const uint64_t n_lv = B.docs[i].n_lv;
     for (size_t k = 1; k < cuts.size(); k++) {
         DocDesc e = B.docs[i];
@@ -559,6 +568,39 @@ std::vector<uint8_t> late_documents(const dtgpu_batch &B, const SegSettings &sc,
         if (order[k] < B.n && n_ops(order[k]) >= 128) late[order[k]] = 1;
     return late;
 }
+// The batch's critical replays (DOC_CRITICAL): a batch whose longest replay unit -- a document
+// replayed whole, by the cut planner's cost (SEG_W_OP per op run + LVs); a segment, by its
+// document's cost over its segment count -- is at
+// least 3x the median gives the units within half of it the top wave priority, as long as they are
+// at most an eighth of the units (mixed batches: git-makefile's 50 uncut documents among 1,500
+// segments and documents; a batch of equal documents marks none).  DTGPU_CRITICAL=0: off.
+void mark_critical(dtgpu_batch &B) {
+    for (DocDesc &d : B.docs) d.flags &= ~DOC_CRITICAL;
+    const char *e = getenv("DTGPU_CRITICAL");
+    if ((e && *e == '0') || B.docs.size() < 2) return;
+    std::vector<uint32_t> per(B.docs.size(), 1);   // segments of each unit's document
+    for (const SegGroup &g : B.seg_groups)
+        for (uint32_t k = 0; k < g.count; k++) per[B.seg_docs[g.first + k]] = g.count;
+    std::vector<uint32_t> owner(B.docs.size());   // a segment document's document
+    for (size_t d = 0; d < B.docs.size(); d++) owner[d] = uint32_t(d);
+    for (const SegGroup &g : B.seg_groups)
+        for (uint32_t k = 1; k < g.count; k++) owner[B.seg_docs[g.first + k]] = B.seg_docs[g.first];
+    std::vector<double> cost(B.docs.size());
+    for (size_t i = 0; i < B.docs.size(); i++) {
+        const size_t o = owner[i];
+        const double runs = o < B.n_runs.size() ? double(B.n_runs[o]) : 0.0;
+        cost[i] = (double(SEG_W_OP) * runs + double(B.docs[i].n_lv)) / per[i];
+    }
+    std::vector<double> srt = cost;
+    std::nth_element(srt.begin(), srt.begin() + srt.size() / 2, srt.end());
+    const double med = srt[srt.size() / 2], mx = *std::max_element(cost.begin(), cost.end());
+    if (mx < 3.0 * med) return;
+    size_t n = 0;
+    for (double c : cost) n += c >= mx / 2;
+    if (8 * n > B.docs.size()) return;
+    for (size_t i = 0; i < B.docs.size(); i++)
+        if (cost[i] >= mx / 2) B.docs[i].flags |= DOC_CRITICAL;
+}
 // The batch's combine step and source-list arena (after every add_segments).
 hipError_t finish_segments(dtgpu_batch &B, uint64_t src_total, const uint32_t *cbyte, const uint8_t *content, hipStream_t s) {
     hipError_t e = hipSuccess;
@@ -602,6 +644,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     B->n = n;
     B->host_status.resize(n);
     B->n_lv.resize(n);
+    B->n_runs.assign(n, 0);
     B->docs.resize(n);
     B->host_planned.assign(n, 0);
     const bool force_host = xf || getenv("DTGPU_HOST_PLAN") != nullptr;
@@ -710,6 +753,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         Prepared &p = prep[i];
         B->host_status[i] = p.status;
         B->n_lv[i] = p.log.n_lv;
+        B->n_runs[i] = p.log.ops.size();
         B->total_lv += p.log.n_lv;
         DocDesc &d = B->docs[i];
         std::memset(&d, 0, sizeof d);
@@ -825,6 +869,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     B->plan.tlist = B->d_tlist.p;
     CK(B->d_cbyte.upload(cbyte, s));
     CK(B->d_content.upload(content, s));
+    mark_critical(*B);
     CK(B->d_docs.upload(B->docs, s));
     CK(B->d_lists.upload(tier_lists(*B), s));
     CK(B->d_pos.alloc(pc_total));
@@ -900,6 +945,7 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     B->n = n;
     B->host_status.assign(n, OK);
     B->n_lv.assign(n, 0);
+    B->n_runs.assign(n, 0);
     B->docs.assign(n, DocDesc{});
     B->host_planned.assign(n, 0);
 
@@ -918,6 +964,7 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
         if (st == OK && (r.n_lv >= MAX_PLAN_LV || r.n_entries > PLAN_MAX_LDS_ENTRIES)) st = DECODE_DEFER;
         B->host_status[i] = st;
         B->n_lv[i] = r.n_lv;
+        B->n_runs[i] = r.n_ops;
         if (st != OK) continue;
         q.skip = 0;
         q.d_op = d.op_off; q.d_arun = d.arun_off; q.d_ent = d.ent_off; q.d_poff = d.poff_off; q.d_par = d.par_off;
@@ -1132,6 +1179,7 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     B->plan.tlist = B->d_tlist.p;
     {   // every segment's LV range is the pass's cut planning's to write (poisoned here: a replay
         // without it fails, ErrCheckout site 30)
+        mark_critical(*B);
         std::vector<DocDesc> up = B->docs;
         for (uint32_t d : B->seg_docs) { up[d].seg_lo = 0xFFFFFFFFu; up[d].seg_hi = 0; }
         CK(B->d_docs.upload(up, s));
@@ -1184,18 +1232,27 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     base.src = B->d_src.p;
     if (set_tier_params(*B, base) != DTGPU_OK) return DTGPU_ERR_HIP;
     B->wstream = B->side[kSideStreams - 1];   // the smallest side tier's stream (see wstream)
-    // split pass: when the biggest non-empty LDS tier rides a side stream and other documents
-    // exist, its documents' prep and plan do not wait for everyone else's (a skewed batch's
-    // longest replays start as soon as their own plans are done)
+    // split pass: when an LDS tier rides a side stream and other documents exist, its
+    // documents' prep and plan do not wait for everyone else's (a skewed batch's longest replays
+    // start as soon as their own plans are done).  The tier: the critical documents' (DOC_CRITICAL,
+    // the batch's longest replays), else the biggest non-empty one.  Its segment documents'
+    // documents are planned there too (the main pipeline's replay waits for those plans).
     if (!getenv("DTGPU_NO_SPLIT")) {
         int tb = -1;
-        for (int t = kLdsTiers - 1; t >= 1; t--)
-            if (!B->tier_list[t].empty()) { tb = t; break; }
+        for (int t = kLdsTiers - 1; t >= 1 && tb < 0; t--)
+            for (uint32_t d : B->tier_list[t])
+                if (B->docs[d].flags & DOC_CRITICAL) { tb = t; break; }
+        for (int t = kLdsTiers - 1; t >= 1 && tb < 0; t--)
+            if (!B->tier_list[t].empty()) tb = t;
         if (tb >= 1) {
-            std::vector<uint32_t> lst;   // the tier's documents, without segment documents
-            for (uint32_t d : B->tier_list[tb]) if (d < n) lst.push_back(d);
+            std::vector<uint32_t> owner(B->docs.size());   // a segment document's document
+            for (size_t d = 0; d < B->docs.size(); d++) owner[d] = uint32_t(d);
+            for (const SegGroup &g : B->seg_groups)
+                for (uint32_t k = 1; k < g.count; k++) owner[B->seg_docs[g.first + k]] = B->seg_docs[g.first];
             std::vector<uint8_t> big(n, 0);
-            for (uint32_t d : lst) big[d] = 1;
+            std::vector<uint32_t> lst;   // in the tier's order
+            for (uint32_t d : B->tier_list[tb])
+                if (owner[d] < n && !big[owner[d]]) { big[owner[d]] = 1; lst.push_back(owner[d]); }
             const size_t nb = lst.size();
             for (size_t i = 0; i < n; i++)
                 if (!big[i]) lst.push_back(uint32_t(i));
@@ -1212,6 +1269,13 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     return DTGPU_OK;
 }
 
+// A split pass plans its cuts beside the side pipeline's prep, before the main pipeline's: the cut
+// kernel then finds each parent's entry itself.
+CutParams cut_before_prep(const dtgpu_batch *B) {
+    CutParams c = B->cut;
+    c.pent = nullptr;
+    return c;
+}
 // The split pass's side pipeline (see stage_device): after a fork from s, the big tier's
 // prep, plan and replay on its side stream.  The fallback counter is reset first, on s, since
 // both pipelines' LDS tiers append to it; the main pipeline's replay_all(skip_tier) joins the
@@ -1231,6 +1295,11 @@ int launch_split_side(dtgpu_batch *B, hipStream_t s) {
     qq.n_docs = B->n_big;
     if (B->n_gpu_planned && launch_plan(qq, sb) != OK) return ErrHip;
     if (hipEventRecord(B->ev_splan, sb) != hipSuccess) return ErrHip;
+    // the cut planning on s, beside the side pipeline's prep and plan (the main pipeline's prep
+    // follows it there); the side replay waits for it
+    if (B->cut.n_groups && (launch_cut(cut_before_prep(B), s) || hipEventRecord(B->ev_cut, s) != hipSuccess ||
+                            hipStreamWaitEvent(sb, B->ev_cut, 0) != hipSuccess))
+        return ErrHip;
     BatchParams tiers[kLdsTiers];
     for (int t = 0; t < kLdsTiers; t++) {
         tiers[t] = B->tier[t];
@@ -1246,13 +1315,6 @@ int launch_split_side(dtgpu_batch *B, hipStream_t s) {
     r.stream = sb;
     r.keep_fb = true;
     return launch_replay(r);
-}
-// A split pass plans its cuts before either pipeline's prep: the cut kernel then finds each
-// parent's entry itself.
-CutParams cut_before_prep(const dtgpu_batch *B) {
-    CutParams c = B->cut;
-    c.pent = nullptr;
-    return c;
 }
 // The main pipeline's prep and plan of a split pass (the documents outside the big tier).
 int launch_split_prep(dtgpu_batch *B, hipStream_t s) {
@@ -1306,8 +1368,7 @@ int prep_and_plan(dtgpu_batch *B, hipStream_t s, hipEvent_t mid) {
 int launch_all(dtgpu_batch *B, hipStream_t s) {
     if (B->xf_mode) return launch_replay_xf(B->large, s);
     if (B->split) {
-        if (launch_cut(cut_before_prep(B), s)) return ErrHip;
-        int e = launch_split_side(B, s);
+        int e = launch_split_side(B, s);   // (it plans the cuts too)
         if (!e) e = launch_split_prep(B, s);
         if (!e) e = launch_split_plan(B, s);
         return e ? e : replay_all(B, s, B->split_tier);
@@ -1829,6 +1890,12 @@ dtgpu_status dtgpu_batch_run(dtgpu_batch *B, void *stream) {
         fprintf(stderr, "[dtgpu] launch lds tiers %u/%u/%u/%u (blocks %u/%u/%u/%u) hbm %u\n", B->tier[0].n_list,
                 B->tier[1].n_list, B->tier[2].n_list, B->tier[3].n_list, B->tier[0].lds_blocks, B->tier[1].lds_blocks,
                 B->tier[2].lds_blocks, B->tier[3].lds_blocks, B->large.n_list);
+    if (B->debug) {
+        size_t nc = 0;
+        for (const DocDesc &d : B->docs) nc += (d.flags & DOC_CRITICAL) != 0;
+        fprintf(stderr, "[dtgpu] critical %zu of %zu replays; split tier %d (%u + %u documents)\n", nc, B->docs.size(),
+                B->split ? B->split_tier : -1, B->n_big, B->n_rest);
+    }
     dtgpu_status st = dtgpu_status(launch_all(B, reinterpret_cast<hipStream_t>(s)));
     if (B->debug) {
         fprintf(stderr, "[dtgpu] launched status %d\n", int(st));
@@ -1848,7 +1915,7 @@ dtgpu_status dtgpu_batch_run_timed(dtgpu_batch *B, float *ms) {
     const bool prep = B->dec && !B->xf_mode;
     const bool split = prep && B->split;   // split pass: prep / plan times are the main pipeline's
     if (hipEventRecord(B->ev_prep, s) != hipSuccess) return DTGPU_ERR_HIP;
-    if (split && (launch_cut(cut_before_prep(B), s) || launch_split_side(B, s))) return DTGPU_ERR_HIP;
+    if (split && launch_split_side(B, s)) return DTGPU_ERR_HIP;   // (it plans the cuts too)
     if (split) {
         if (launch_split_prep(B, s) != OK || hipEventRecord(B->ev0, s) != hipSuccess || launch_split_plan(B, s) != OK)
             return DTGPU_ERR_HIP;

@@ -3,21 +3,10 @@
 set -o pipefail
 O=gpurun_out/r5s; mkdir -p $O
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
-cat > /tmp/one.py <<'PY'
-import sys, os
-sys.path.insert(0, "diamond-types_amd"); sys.path.insert(0, "tests")
-import dt_amd, golden_data as G
-out = []
-for name in ["friendsforever", "node_nodecc", "automerge-paper", "rustcode", "seph-blog1", "sveltecomponent"]:
-    data = G.dt_bytes(name) if name in G.DT_FILES else dt_amd.apply_edits_push_merge(G.trace(name)["txns"]).encode()
-    b = dt_amd.Batch(docs=[data], staging="device"); b.run(); b.sync()
-    ts = sorted(b.run_timed() for _ in range(5))
-    out.append(f"{name} {ts[2]:.2f}/{len(b.segments(0))}")
-print("W", os.environ.get("DTGPU_SEG_W"), " ".join(out), flush=True)
-PY
-for w in 24 32 48 96 128 256; do
-DTGPU_SEG_W=$w timeout -k 10 200 python -u /tmp/one.py || exit 1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_segments.py tests/test_gpu_mixed.py -x -q --timeout 200 --timeout-method thread > $O/segtests.log 2>&1
+rc=$?; tail -3 $O/segtests.log; [ $rc -eq 0 ] || exit 1
+for c in 0 1 0 1; do
+DTGPU_CRIT_APART=$c timeout -k 10 300 python -u bench.py --workload mixed --docs 400 --steps 3 --warmup 1 --no-cpu-baseline --no-decode --no-encode > $O/mx$c.json 2> $O/mx.err || { tail $O/mx.err; exit 1; }
+echo "apart=$c $(grep -o '"ms_per_step": [0-9.]*' $O/mx$c.json)"
 done
-for w in 64; do
-DTGPU_SEG_W=$w timeout -k 10 200 python -u tools/kbench.py friendsforever 10000 3 || exit 1
-done
+timeout -k 10 200 python -u tools/kbench.py friendsforever 10000 3 || exit 1
