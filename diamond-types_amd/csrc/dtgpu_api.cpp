@@ -293,6 +293,8 @@ struct dtgpu_batch {
     // serialising two replay tiers that should run side by side
     hipStream_t wstream = nullptr;
     hipEvent_t ev_w0 = nullptr, ev_w1 = nullptr;
+    hipStream_t ws_side = nullptr;                    // split pass: the side pipeline's walk
+    hipEvent_t ev_sw0 = nullptr, ev_sw1 = nullptr;
     float last_decode_ms = 0, last_prep_ms = 0;
 
     // batched encoder (dtgpu_batch_encode): per-document descriptors, scratch, output
@@ -307,6 +309,9 @@ struct dtgpu_batch {
     ~dtgpu_batch() {
         if (ev_splan) (void)hipEventDestroy(ev_splan);
         if (ev_cut) (void)hipEventDestroy(ev_cut);
+        if (ev_sw0) (void)hipEventDestroy(ev_sw0);
+        if (ev_sw1) (void)hipEventDestroy(ev_sw1);
+        if (ws_side) (void)hipStreamDestroy(ws_side);
         if (ev_w0) (void)hipEventDestroy(ev_w0);
         if (ev_w1) (void)hipEventDestroy(ev_w1);
         if (ev_dec) (void)hipEventDestroy(ev_dec);
@@ -1260,6 +1265,9 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
                 if (B->d_split.upload(lst, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) return DTGPU_ERR_HIP;
                 B->split = true;
                 B->split_tier = tb;
+                if (!B->ws_side && hipStreamCreateWithFlags(&B->ws_side, hipStreamNonBlocking) != hipSuccess) return DTGPU_ERR_HIP;
+                if (!B->ev_sw0 && hipEventCreateWithFlags(&B->ev_sw0, hipEventDisableTiming) != hipSuccess) return DTGPU_ERR_HIP;
+                if (!B->ev_sw1 && hipEventCreateWithFlags(&B->ev_sw1, hipEventDisableTiming) != hipSuccess) return DTGPU_ERR_HIP;
                 B->n_big = uint32_t(nb);
                 B->n_rest = uint32_t(lst.size() - nb);
             }
@@ -1289,11 +1297,24 @@ int launch_split_side(dtgpu_batch *B, hipStream_t s) {
     PrepParams pp = B->prep;
     pp.doc_list = B->d_split.p;
     pp.n_docs = B->n_big;
-    if (launch_prep(pp, sb)) return ErrHip;
     PlanParams qq = B->plan;
     qq.doc_list = B->d_split.p;
     qq.n_docs = B->n_big;
-    if (B->n_gpu_planned && launch_plan(qq, sb) != OK) return ErrHip;
+    // as prep_and_plan: the walk (CSR mode, after prep's first half) on a stream of its own,
+    // beside the chain decomposition and prep's second half
+    const bool overlap = B->n_gpu_planned && B->prep.chain_flag && !B->prep.check && B->plan.walk && B->plan.coff &&
+                         B->ws_side && !getenv("DTGPU_NO_WALK_OVERLAP");
+    if (overlap) {
+        pp.short_rec = B->plan.split ? 1u : 0u;
+        if (launch_prep_stage(pp, sb, 1)) return ErrHip;
+        if (hipEventRecord(B->ev_sw0, sb) != hipSuccess || hipStreamWaitEvent(B->ws_side, B->ev_sw0, 0) != hipSuccess) return ErrHip;
+        if (launch_walk(qq, B->ws_side, true) != OK || hipEventRecord(B->ev_sw1, B->ws_side) != hipSuccess) return ErrHip;
+        if (launch_prep_stage(pp, sb, 2) || launch_prep_stage(pp, sb, 3)) return ErrHip;
+        if (hipStreamWaitEvent(sb, B->ev_sw1, 0) != hipSuccess || launch_plan(qq, sb, false) != OK) return ErrHip;
+    } else {
+        if (launch_prep(pp, sb)) return ErrHip;
+        if (B->n_gpu_planned && launch_plan(qq, sb) != OK) return ErrHip;
+    }
     if (hipEventRecord(B->ev_splan, sb) != hipSuccess) return ErrHip;
     // the cut planning on s, beside the side pipeline's prep and plan (the main pipeline's prep
     // follows it there); the side replay waits for it

@@ -3,10 +3,10 @@
 set -o pipefail
 O=gpurun_out/r5s; mkdir -p $O
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
-timeout -k 10 300 python -u -m pytest tests/test_gpu_segments.py tests/test_gpu_mixed.py -x -q --timeout 200 --timeout-method thread > $O/segtests.log 2>&1
-rc=$?; tail -3 $O/segtests.log; [ $rc -eq 0 ] || exit 1
-for c in 0 1 0 1; do
-DTGPU_CRIT_APART=$c timeout -k 10 300 python -u bench.py --workload mixed --docs 400 --steps 3 --warmup 1 --no-cpu-baseline --no-decode --no-encode > $O/mx$c.json 2> $O/mx.err || { tail $O/mx.err; exit 1; }
-echo "apart=$c $(grep -o '"ms_per_step": [0-9.]*' $O/mx$c.json)"
+mx() { timeout -k 10 300 python -u bench.py --workload mixed --docs 400 --steps 3 --warmup 1 --no-cpu-baseline --no-decode --no-encode > $O/mx.json 2> $O/mx.err || { tail $O/mx.err; return 1; }; grep -o '"ms_per_step": [0-9.]*' $O/mx.json; }
+for k in 1 2; do
+echo "overlap: $(mx)" || exit 1
+echo "no overlap: $(DTGPU_NO_WALK_OVERLAP=1 mx)" || exit 1
 done
-timeout -k 10 200 python -u tools/kbench.py friendsforever 10000 3 || exit 1
+rm -rf $O/mx
+timeout -k 10 300 rocprofv3 --kernel-trace -d $O/mx -o run -f csv -- python -u bench.py --workload mixed --docs 400 --steps 3 --warmup 1 --no-cpu-baseline --no-decode --no-encode > $O/mx.log 2>&1 || { tail $O/mx.log; exit 1; }
