@@ -92,3 +92,30 @@ def test_mixed_skewed_batch_forced_segments(mixed, monkeypatch):
         segs = [b.segments(i) for i in range(len(docs))]
         assert sum(1 for s in segs if len(s) >= 2) >= len(docs) // 2, staging
         assert all(x["status"] == 0 for s in segs for x in s)
+
+
+@pytest.mark.parametrize("critical", ["1", "0"])
+def test_configs4_batch_critical_documents(mixed, monkeypatch, critical):
+    """configs[4] as bench.py runs it (all 8 traces x 50, round-robin): git-makefile's uncut
+    documents are the batch's critical replays (dtgpu_api.cpp mark_critical: first in their
+    tier, top wave priority, their tier in the split pipeline with its overlapped walk); with
+    DTGPU_CRITICAL=0 none are.  Every text either way equals the golden / oracle text."""
+    docs, want = mixed
+    uniq = {}
+    for d, w in zip(docs, want):
+        uniq[d] = w
+    names = list(uniq)
+    assert len(names) == 8
+    monkeypatch.setenv("DTGPU_CRITICAL", critical)
+    batch = [names[i % 8] for i in range(400)]
+    b = dt_amd.Batch(docs=batch, staging="device")
+    b.run()
+    b.sync()
+    res = b.results()
+    for i, r in enumerate(res):
+        w = uniq[batch[i]]
+        assert r["status"] == 0, (i, r)
+        assert (r["text_len"], r["text_hash"]) == (len(w), dt_amd.text_hash(w)), i
+    b.run_timed()
+    res2 = b.results()
+    assert [(r["text_len"], r["text_hash"]) for r in res2] == [(r["text_len"], r["text_hash"]) for r in res]
