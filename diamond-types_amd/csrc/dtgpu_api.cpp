@@ -109,7 +109,7 @@ struct SegInput {
 };
 struct SegSettings { bool on; uint64_t ops_per_seg; uint32_t max_seg, w_op; };
 SegSettings seg_settings() {
-    SegSettings s{true, 500, 16, SEG_W_OP};
+    SegSettings s{true, 500, 32, SEG_W_OP};   // 32 segments: measured against 16-64 on the six cut traces
     if (const char *e = getenv("DTGPU_SEG_W")) s.w_op = uint32_t(std::min<uint64_t>(strtoull(e, nullptr, 10), 1u << 20));
     if (const char *e = getenv("DTGPU_SEG")) s.on = *e != '0';
     if (const char *e = getenv("DTGPU_SEG_OPS")) s.ops_per_seg = std::max<uint64_t>(1, strtoull(e, nullptr, 10));

@@ -298,7 +298,7 @@ dtgpu_status dtgpu_batch_doc_stats(dtgpu_batch *batch, size_t doc, uint32_t out[
  * placeholders, status, visible items, cycles/16 (DTGPU_DEBUG=2), 1 if its index was in LDS,
  * blocks used} from the last run.
  * DTGPU_SEG=0 disables segmenting; DTGPU_SEG_OPS (op runs per segment, default 500, raised
- * to the batch's fair share per wave slot) and DTGPU_SEG_MAX (default 16) size it; read at
+ * to the batch's fair share per wave slot) and DTGPU_SEG_MAX (default 32) size it; read at
  * batch creation. */
 size_t dtgpu_batch_segments(dtgpu_batch *batch, size_t doc, uint32_t *out, size_t cap);
 /* Device planner cycle profile of one document (DTGPU_PLAN_PROF set at batch creation):
