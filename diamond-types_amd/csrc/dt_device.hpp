@@ -33,6 +33,11 @@ constexpr uint32_t SEG_PHANTOM = 0x80000000u;   // source-list entry: placeholde
 // batch's typical one, which the waves beside it would otherwise slow down by sharing the SIMD's
 // issue; its waves take the top priority.
 constexpr uint32_t DOC_CRITICAL = 1u;
+// A linear history checked out on the fast-forward piece table (dt_ff.hip), not replayed.
+constexpr uint32_t DOC_FF = 2u;
+// A cut document whose segments' ranges came from the host plan because cut_kernel declined it
+// (dt_prep.hip; tests assert the device plan is the one used).
+constexpr uint32_t DOC_CUT_HOST = 4u;
 
 struct DocResult {
     uint32_t status, out_len;
@@ -80,6 +85,7 @@ struct BatchParams {
     uint32_t lds_flat;   // LDS tiers: 1 = the flat 2-level index (IX_FLAT), 0 = the 3-level one
     uint32_t prio_from;  // LDS tiers: workgroups from this index on (dispatched after the first
                          // resident set) raise their wave priority (0: off)
+    uint32_t n_cu;       // compute units of the batch's device (resident-set sizes)
 };
 
 // Cut replay: after the replay, one workgroup per cut document resolves its segments' source
@@ -95,6 +101,7 @@ struct CombineParams {
     const uint32_t *cbyte;
     const uint8_t *content;
     uint8_t *out;
+    uint32_t n_cu;   // compute units of the batch's device
 };
 int launch_combine(const CombineParams &p, void *stream);
 

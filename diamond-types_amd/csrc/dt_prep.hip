@@ -876,15 +876,23 @@ __global__ __launch_bounds__(64 * CUT_WAVES) void cut_kernel(CutParams P) {
     const uint32_t d = P.seg_docs[G.first];
     const PrepDesc D = P.pdocs[d];
     const uint32_t ne = D.ne, nop = D.n_ops, S = G.count, T = SP.n_targets;   // segments; equal-share targets
-    if (S < 2 || S > 64 || T < S || ne == 0 || nop == 0) return;   // (staging makes none such; the poisoned ranges then fail)
-    // short documents: one wave (the others leave before any barrier; a barrier waits only for
-    // the waves still running)
+    // declined: the host plan's ranges (staging reserved the arenas from it; DOC_CUT_HOST marks it)
+    auto host_ranges = [&]() {
+        if (w != 0 || l >= S || l >= 64) return;
+        const SegCap cap = P.caps[G.first + l];
+        DocDesc *dd = P.docs + P.seg_docs[G.first + l];
+        dd->seg_lo = cap.lo;
+        dd->seg_hi = cap.hi;
+        dd->seg_u = cap.u;
+        dd->flags |= DOC_CUT_HOST;
+    };
+    if (S < 2 || S > 64 || T < S || ne == 0 || nop == 0 || ne > P.max_ne) { host_ranges(); return; }   // (staging makes none such)
+    // short documents: the op-run pass on one wave (the other waves take empty parts: every wave
+    // stays to the workgroup's barriers)
     const uint32_t NW = nop >= 4096 ? CUT_WAVES : 1u;
-    if (w >= NW) return;
     const uint2 *ent = reinterpret_cast<const uint2 *>(P.d_ent) + D.d_ent;
     const uint32_t *poff = P.d_poff + D.d_poff, *par = P.d_par + D.d_par;
     const uint4 *ops = reinterpret_cast<const uint4 *>(P.d_ops) + D.d_op;   // lv, len, pos, kind (bit 0: delete)
-    if (ne > P.max_ne) return;
     extern __shared__ uint32_t nxt[];   // per entry: the first entry naming its last LV as a parent
     const uint32_t *pent = P.pent ? P.pent + D.o_par : nullptr;   // prep's first half: each parent's entry (or searched)
     int32_t *suf = reinterpret_cast<int32_t *>(P.scr + SP.scr_off);        // ne + 1
@@ -997,7 +1005,7 @@ __global__ __launch_bounds__(64 * CUT_WAVES) void cut_kernel(CutParams P) {
     }   // nr != 0
     }
     __syncthreads();
-    if (!s_ok) return;
+    if (!s_ok) { host_ranges(); return; }
     // 5. inserts, deletes and concurrent deletes before each cut (exclusive prefix sums), the op
     //    runs split in four contiguous parts, one per wave; each part's sums are offset by the
     //    parts before it afterwards
@@ -1010,7 +1018,7 @@ __global__ __launch_bounds__(64 * CUT_WAVES) void cut_kernel(CutParams P) {
         // looks its runs up among the 64 ranges from the previous chunk's last one (one load,
         // a search by lane permutes), a global bisection only past that window
         const uint32_t part = ((nop + NW - 1) / NW + 63) & ~63u;
-        const uint32_t b0 = min(nop, w * part), b1 = min(nop, b0 + part);
+        const uint32_t b0 = w < NW ? min(nop, w * part) : nop, b1 = min(nop, b0 + part);
         uint32_t ci = 0, cd = 0, cc = 0, pi = 0;
         const uint32_t last_pick = rdl(picks, npick - 1);   // past it only the inserts are summed
         uint32_t rc = b0 < b1 ? range_of(rng, nr, ops[b0].x) : 0u;
@@ -1081,7 +1089,7 @@ __global__ __launch_bounds__(64 * CUT_WAVES) void cut_kernel(CutParams P) {
         const SegCap cap = P.caps[G.first + k];
         fits = fits && u <= cap.u && ins_hi - ins_lo <= cap.ins;
     }
-    if (!fits) return;
+    if (!fits) { host_ranges(); return; }
     {   // lane k writes segment k's descriptor fields
         const uint32_t k = l;
         const uint32_t pprev = uint32_t(__shfl(int(picks), int(k ? k - 1 : 0)));   // cut before segment k
@@ -1096,6 +1104,7 @@ __global__ __launch_bounds__(64 * CUT_WAVES) void cut_kernel(CutParams P) {
             dd->seg_lo = lo;
             dd->seg_hi = hi;
             dd->seg_u = u;
+            dd->flags &= ~DOC_CUT_HOST;
         }
     }
 }
@@ -1106,7 +1115,13 @@ __global__ __launch_bounds__(64 * CUT_WAVES) void cut_kernel(CutParams P) {
 int launch_cut(const CutParams &p, void *stream) {
     if (!p.n_groups) return 0;
     const size_t lds = size_t(p.max_ne) * 4;
-    if (lds > 64 * 1024) return 66;   // (staging cuts documents of at most PLAN_MAX_LDS_ENTRIES entries)
+    // the entry table beside ~1.1 KB of static LDS: past the default 64 KiB of dynamic LDS the
+    // per-function limit is raised (staging cuts documents of at most PLAN_MAX_LDS_ENTRIES entries)
+    if (lds + 2048 > 160 * 1024) return 66;
+    if (lds + 2048 > 64 * 1024 &&
+        hipFuncSetAttribute(reinterpret_cast<const void *>(&prep::cut_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            int(lds)) != hipSuccess)
+        return 66;
     hipLaunchKernelGGL(prep::cut_kernel, dim3(p.n_groups), dim3(64 * prep::CUT_WAVES), lds, reinterpret_cast<hipStream_t>(stream), p);
     return hipGetLastError() == hipSuccess ? 0 : 66;
 }

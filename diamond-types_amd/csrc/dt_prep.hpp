@@ -87,7 +87,10 @@ int launch_prep(const PrepParams &p, void *stream);
 constexpr uint32_t SEG_W_OP = 48;   // default w_op (DTGPU_SEG_W)
 struct SegPlan { uint32_t w_op, n_targets; uint64_t scr_off; };   // per group: the cost weight of an
                                                                   // op run, the target count, scratch (words)
-struct SegCap { uint32_t u, ins; };                                 // per seg_docs slot
+// per seg_docs slot: the reserved placeholders and inserts, and the host plan's LV range, which
+// the kernel writes instead of its own when it declines the document (its cuts differ from the
+// reserved segments, or a bound exceeds what was reserved; DOC_CUT_HOST marks it)
+struct SegCap { uint32_t u, ins, lo, hi; };
 struct CutParams {
     const uint32_t *d_ops, *d_ent, *d_poff, *d_par;   // decoder arenas (as PrepParams)
     const PrepDesc *pdocs;                            // per document

@@ -1893,11 +1893,10 @@ static int launch_lds_tier(const BatchParams &q, hipStream_t s, bool prof) {
         qp.prio_from = 0;
         const char *pe = getenv("DTGPU_PRIO");
         if (!(pe && *pe == '0')) {
-            static int n_cu = 0;
-            if (!n_cu && hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) n_cu = 0;
+            // (the batch's own device: late_documents sizes the same resident set from it)
             const size_t gran = (lds + 1279) / 1280 * 1280;
             const size_t per_cu = std::min<size_t>(32, 163840 / std::max<size_t>(gran, 1280));
-            qp.prio_from = uint32_t(per_cu * size_t(std::max(n_cu, 1)));
+            qp.prio_from = uint32_t(per_cu * size_t(std::max<uint32_t>(q.n_cu, 1)));
         }
         if (prof) hipLaunchKernelGGL((dev::replay_kernel<dev::IX_FLAT, true, false>), dim3(q.n_list), dim3(64), lds, s, qp);
         else hipLaunchKernelGGL((dev::replay_kernel<dev::IX_FLAT, false, false, false, 8>), dim3(q.n_list), dim3(64), lds, s, qp);
@@ -2005,9 +2004,8 @@ int launch_replay_xf(const BatchParams &large, void *stream) {
 int launch_combine(const CombineParams &p, void *stream) {
     if (!p.n_groups) return OK;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    static int n_cu = 0;
-    if (!n_cu && hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) n_cu = 256;
-    if (p.n_groups >= uint32_t(2 * std::max(n_cu, 1))) hipLaunchKernelGGL(dev::combine_kernel<256>, dim3(p.n_groups), dim3(256), 0, s, p);
+    const uint32_t n_cu = p.n_cu ? p.n_cu : 256u;   // the batch's device
+    if (p.n_groups >= 2 * n_cu) hipLaunchKernelGGL(dev::combine_kernel<256>, dim3(p.n_groups), dim3(256), 0, s, p);
     else hipLaunchKernelGGL(dev::combine_kernel<1024>, dim3(p.n_groups), dim3(1024), 0, s, p);
     return hipGetLastError() == hipSuccess ? OK : ErrHip;
 }

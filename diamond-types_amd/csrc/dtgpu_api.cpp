@@ -23,6 +23,7 @@
 #include "dt_host.hpp"
 #include "dt_prep.hpp"
 #include "dt_encoder.hpp"
+#include "dt_ff.hpp"
 
 using namespace dtgpu;
 
@@ -297,6 +298,21 @@ struct dtgpu_batch {
     hipEvent_t ev_sw0 = nullptr, ev_sw1 = nullptr;
     float last_decode_ms = 0, last_prep_ms = 0;
 
+    // linear histories (dt_ff.hip): a document whose history is one graph entry checks out on the
+    // fast-forward piece table instead of prep -> plan -> replay (staging still prepares and plans
+    // it, for the batched encoder); the pass's prep / plan lists hold the other documents
+    std::vector<uint8_t> ff_doc;          // per document: 1 = fast-forward path
+    uint32_t n_ff = 0, n_track = 0;       // documents on each path
+    DevBuf<uint32_t> d_track;             // the tracker's documents (prep / plan doc_list)
+    DevBuf<uint32_t> f_ops;               // host-staged batches: op runs as the decoder's quads
+    DevBuf<FFDoc> f_docs;
+    DevBuf<FFSeg> f_segs;
+    DevBuf<FFPair> f_pairs;
+    DevBuf<FFChunk> f_chunks;
+    DevBuf<int32_t> f_delta;
+    DevBuf<uint32_t> f_bad, f_pa, f_pb, f_ca, f_cb, f_boff;
+    FFParams ff{};
+
     // batched encoder (dtgpu_batch_encode): per-document descriptors, scratch, output
     std::vector<EncDesc> e_desc;
     std::vector<EncResult> e_res;
@@ -415,6 +431,8 @@ dtgpu_status set_tier_params(dtgpu_batch &B, const BatchParams &base) {
         B.large.fb_list = B.d_fb.p + 1;
         B.large.fb_slots = uint32_t(off);   // every LDS-tier document may be handed back
     }
+    for (int t = 0; t < kLdsTiers; t++) B.tier[t].n_cu = uint32_t(B.n_cu);
+    B.large.n_cu = uint32_t(B.n_cu);
     B.debug = base.debug;
     if (!B.ev_fork && hipEventCreateWithFlags(&B.ev_fork, hipEventDisableTiming) != hipSuccess) return DTGPU_ERR_HIP;
     if (!B.ev_splan && hipEventCreateWithFlags(&B.ev_splan, hipEventDisableTiming) != hipSuccess) return DTGPU_ERR_HIP;
@@ -590,21 +608,25 @@ void mark_critical(dtgpu_batch &B) {
     for (size_t d = 0; d < B.docs.size(); d++) owner[d] = uint32_t(d);
     for (const SegGroup &g : B.seg_groups)
         for (uint32_t k = 1; k < g.count; k++) owner[B.seg_docs[g.first + k]] = B.seg_docs[g.first];
-    std::vector<double> cost(B.docs.size());
+    std::vector<double> cost;   // replay units (fast-forwarded documents do not replay)
+    std::vector<uint32_t> unit;
     for (size_t i = 0; i < B.docs.size(); i++) {
+        if (B.docs[i].flags & DOC_FF) continue;
         const size_t o = owner[i];
         const double runs = o < B.n_runs.size() ? double(B.n_runs[o]) : 0.0;
-        cost[i] = (double(SEG_W_OP) * runs + double(B.docs[i].n_lv)) / per[i];
+        cost.push_back((double(SEG_W_OP) * runs + double(B.docs[i].n_lv)) / per[i]);
+        unit.push_back(uint32_t(i));
     }
+    if (cost.size() < 2) return;
     std::vector<double> srt = cost;
     std::nth_element(srt.begin(), srt.begin() + srt.size() / 2, srt.end());
     const double med = srt[srt.size() / 2], mx = *std::max_element(cost.begin(), cost.end());
     if (mx < 3.0 * med) return;
     size_t n = 0;
     for (double c : cost) n += c >= mx / 2;
-    if (8 * n > B.docs.size()) return;
-    for (size_t i = 0; i < B.docs.size(); i++)
-        if (cost[i] >= mx / 2) B.docs[i].flags |= DOC_CRITICAL;
+    if (8 * n > cost.size()) return;
+    for (size_t k = 0; k < cost.size(); k++)
+        if (cost[k] >= mx / 2) B.docs[unit[k]].flags |= DOC_CRITICAL;
 }
 // The batch's combine step and source-list arena (after every add_segments).
 hipError_t finish_segments(dtgpu_batch &B, uint64_t src_total, const uint32_t *cbyte, const uint8_t *content, hipStream_t s) {
@@ -623,6 +645,102 @@ hipError_t finish_segments(dtgpu_batch &B, uint64_t src_total, const uint32_t *c
     c.cbyte = cbyte;
     c.content = content;
     c.out = B.d_out.p;
+    c.n_cu = uint32_t(B.n_cu);
+    return hipSuccess;
+}
+
+// ---- linear histories (dt_ff.hip) ---------------------------------------------------------------
+// A document checks out on the fast-forward path when its whole history is one graph entry: the
+// reference's merge then fast-forwards through every op (merge.rs:811-840; Graph::push extends
+// the last entry whenever a span continues it, so one entry <=> a linear history).
+bool ff_setting() {
+    const char *e = getenv("DTGPU_FF");   // "0": every document on the tracker (A/B, tests)
+    return !(e && *e == '0');
+}
+struct FFIn { uint64_t op_off; uint32_t n_ops; uint32_t doc; };   // op runs: quads into `ops`
+// The fast-forward layout of the batch's linear documents: segments of FF_RUNS op runs, the
+// composition pairs of every level, the copy chunks.  out_off / out_cap / lv_off / content_off /
+// ascii come from B.docs (the documents' normal layout); the tracker documents become the
+// pass's prep / plan list.
+hipError_t stage_ff(dtgpu_batch &B, const std::vector<FFIn> &in, const uint32_t *ops, const uint32_t *cbyte,
+                    const uint8_t *content, hipStream_t s) {
+    hipError_t e = hipSuccess;
+    std::vector<uint32_t> track;
+    for (size_t i = 0; i < B.n; i++)
+        if (!B.ff_doc[i]) track.push_back(uint32_t(i));
+    B.n_track = uint32_t(track.size());
+    B.n_ff = uint32_t(in.size());
+    if ((e = B.d_track.upload(track, s)) != hipSuccess) return e;
+    B.prep.doc_list = B.d_track.p;
+    B.prep.n_docs = B.n_track;
+    B.plan.doc_list = B.d_track.p;
+    B.plan.n_docs = B.n_track;
+    if (in.empty()) return hipSuccess;
+    std::vector<FFDoc> docs;
+    std::vector<FFSeg> segs;
+    std::vector<std::vector<FFPair>> lv;
+    std::vector<FFChunk> chunks;
+    for (const FFIn &f : in) {
+        const DocDesc &d = B.docs[f.doc];
+        FFDoc q{};
+        q.op_off = f.op_off;
+        q.lv_off = d.lv_off;
+        q.content_off = d.content_off;
+        q.out_off = d.out_off;
+        q.n_ops = f.n_ops;
+        q.first_seg = uint32_t(segs.size());
+        q.n_seg = (f.n_ops + FF_RUNS - 1) / FF_RUNS;
+        q.piece_off = uint64_t(FF_PIECES) * q.first_seg;
+        q.out_cap = d.out_cap;
+        q.result = f.doc;
+        q.ascii = d.ascii;
+        while ((1u << q.levels) < q.n_seg) q.levels++;
+        const uint32_t di = uint32_t(docs.size());
+        for (uint32_t k = 0; k < q.n_seg; k++)
+            segs.push_back(FFSeg{di, k * FF_RUNS, std::min<uint32_t>(FF_RUNS, f.n_ops - k * FF_RUNS), 0});
+        if (lv.size() < q.levels) lv.resize(q.levels);
+        for (uint32_t k = 0; k < q.levels; k++) {
+            const uint32_t g = 1u << k;
+            for (uint32_t a = 0; a < q.n_seg; a += 2 * g) lv[k].push_back(FFPair{di, a, a + g < q.n_seg ? a + g : FF_NONE, 0});
+        }
+        for (uint64_t c = 0; c < d.out_cap; c += FF_CHUNK) chunks.push_back(FFChunk{di, uint32_t(c)});
+        docs.push_back(q);
+    }
+    if (lv.size() > 32) return hipErrorInvalidValue;
+    FFParams &p = B.ff;
+    p = FFParams{};
+    std::vector<FFPair> pairs;
+    for (size_t k = 0; k < lv.size(); k++) {
+        p.level_off[k] = uint32_t(pairs.size());
+        append(pairs, lv[k]);
+    }
+    p.level_off[lv.size()] = uint32_t(pairs.size());
+    const size_t slots = size_t(FF_PIECES) * segs.size();
+    if ((e = B.f_docs.upload(docs, s)) != hipSuccess || (e = B.f_segs.upload(segs, s)) != hipSuccess ||
+        (e = B.f_pairs.upload(pairs, s)) != hipSuccess || (e = B.f_chunks.upload(chunks, s)) != hipSuccess ||
+        (e = B.f_delta.alloc(segs.size())) != hipSuccess || (e = B.f_bad.alloc(docs.size())) != hipSuccess ||
+        (e = B.f_pa.alloc(4 * slots)) != hipSuccess || (e = B.f_pb.alloc(4 * slots)) != hipSuccess ||
+        (e = B.f_ca.alloc(segs.size())) != hipSuccess || (e = B.f_cb.alloc(segs.size())) != hipSuccess ||
+        (e = B.f_boff.alloc(slots)) != hipSuccess)
+        return e;
+    p.ops = ops;
+    p.cbyte = cbyte;
+    p.content = content;
+    p.out = B.d_out.p;
+    p.results = B.d_results.p;
+    p.docs = B.f_docs.p;
+    p.segs = B.f_segs.p;
+    p.pairs = B.f_pairs.p;
+    p.chunks = B.f_chunks.p;
+    p.n_docs = uint32_t(docs.size());
+    p.n_segs = uint32_t(segs.size());
+    p.n_chunks = uint32_t(chunks.size());
+    p.n_levels = uint32_t(lv.size());
+    p.delta = B.f_delta.p;
+    p.bad = B.f_bad.p;
+    p.pa = B.f_pa.p; p.pb = B.f_pb.p;
+    p.ca = B.f_ca.p; p.cb = B.f_cb.p;
+    p.boff = B.f_boff.p;
     return hipSuccess;
 }
 
@@ -652,6 +770,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     B->n_runs.assign(n, 0);
     B->docs.resize(n);
     B->host_planned.assign(n, 0);
+    B->ff_doc.assign(n, 0);
     const bool force_host = xf || getenv("DTGPU_HOST_PLAN") != nullptr;
 
     // ---- 1. device planner inputs; a sizing pass of the planner gives exact stream sizes ----
@@ -799,6 +918,23 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         d.content_off = content.size();
         d.content_len = uint32_t(p.log.ins_content.size());
         d.n_aruns = uint32_t(aq);
+        if (!xf && ff_setting() && p.log.graph.entries.size() == 1 && !p.log.ops.empty() && p.log.content_complete) {
+            // a linear history: the fast-forward path (dt_ff.hip), out arena only
+            B->ff_doc[i] = 1;
+            d.flags |= DOC_FF;
+            out_total = (out_total + 15) & ~15ull;
+            d.out_off = out_total;
+            d.out_cap = uint32_t(p.log.ins_content.size());
+            out_total += (uint64_t(d.out_cap) + 15) & ~15ull;
+            cbyte.insert(cbyte.end(), p.log.ins_cbyte.begin(), p.log.ins_cbyte.end());
+            content.insert(content.end(), p.log.ins_content.begin(), p.log.ins_content.end());
+            lv_total += p.log.n_lv;
+            uint64_t parents = 0;
+            for (const GraphEntry &g : p.log.graph.entries) parents += g.parents.size();
+            B->alg_in_bytes += 16ull * p.log.ops.size() + 8ull * p.log.graph.entries.size() + 4ull * parents +
+                               12ull * p.log.agent_runs.size() + d.content_len;
+            continue;
+        }
         const Layout lay = replay_layout(n_ins, lds_fill, xf);
         d.max_blocks = lay.max_blocks;
         d.blk_off = blk_total;
@@ -888,6 +1024,18 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     CK(B->d_results.alloc(B->docs.size()));
     CK(hipMemsetAsync(B->d_results.p, 0, std::max<size_t>(B->docs.size(), 1) * sizeof(DocResult), s));
     CK(finish_segments(*B, src_total, B->d_cbyte.p, B->d_content.p, s));
+    {   // linear documents: their op runs as the decoder's quads (lv, len, pos, kind | fwd << 1)
+        std::vector<FFIn> ffin;
+        std::vector<uint32_t> quads;
+        for (size_t i = 0; i < n; i++) {
+            if (!B->ff_doc[i]) continue;
+            ffin.push_back(FFIn{quads.size() / 4, uint32_t(prep[i].log.ops.size()), uint32_t(i)});
+            for (const OpRun &r : prep[i].log.ops)
+                quads.insert(quads.end(), {uint32_t(r.lv), uint32_t(r.len), uint32_t(r.pos), uint32_t(r.kind) | (uint32_t(r.fwd) << 1)});
+        }
+        CK(B->f_ops.upload(quads, s));
+        CK(stage_ff(*B, ffin, B->f_ops.p, B->d_cbyte.p, B->d_content.p, s));
+    }
     if (xf) {
         CK(B->d_mup.alloc(blk_total));
         CK(B->d_tup.alloc(blk_total + 2 * n));
@@ -953,6 +1101,8 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     B->n_runs.assign(n, 0);
     B->docs.assign(n, DocDesc{});
     B->host_planned.assign(n, 0);
+    B->ff_doc.assign(n, 0);
+    const bool ff_on = ff_setting();
 
     // ---- prep layout ----------------------------------------------------------------------------
     std::vector<PrepDesc> pd(n);
@@ -971,6 +1121,7 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
         B->n_lv[i] = r.n_lv;
         B->n_runs[i] = r.n_ops;
         if (st != OK) continue;
+        if (ff_on && r.n_entries == 1 && r.n_ops > 0) B->ff_doc[i] = 1;   // linear history (dt_ff.hip)
         q.skip = 0;
         q.d_op = d.op_off; q.d_arun = d.arun_off; q.d_ent = d.ent_off; q.d_poff = d.poff_off; q.d_par = d.par_off;
         q.d_ver = d.ver_off; q.d_agent = d.agent_off; q.d_in = d.in_off;
@@ -1111,6 +1262,16 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
         d.content_len = r.n_content;
         d.arun_off = pd[i].o_arun * 4;
         d.n_aruns = r.n_aruns;
+        if (B->ff_doc[i]) {   // the fast-forward path: out arena only (dt_ff.hip)
+            d.flags |= DOC_FF;
+            out_total = (out_total + 15) & ~15ull;
+            d.out_off = out_total;
+            d.out_cap = r.n_content;
+            out_total += (uint64_t(d.out_cap) + 15) & ~15ull;
+            B->total_lv += r.n_lv;
+            B->alg_in_bytes += 16ull * r.n_ops + 8ull * r.n_entries + 4ull * r.n_parents + 12ull * r.n_aruns + r.n_content;
+            continue;
+        }
         if (n_ins / 32 + 2 > std::min<uint64_t>(LOC_MAX_BLOCKS, MAX_DOC_BLOCKS)) { B->host_status[i] = ErrCapacity; pdesc[i].skip = 1; continue; }
         const Layout lay = replay_layout(n_ins, lds_fill, false);
         d.max_blocks = lay.max_blocks;
@@ -1156,7 +1317,7 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
                 continue;
             const uint32_t targets = uint32_t(std::min<uint64_t>(c.max_seg, si.ops.size() / c.ops_per_seg));
             B->seg_plans.push_back(SegPlan{c.w_op, targets, scr});
-            for (const SegCut &k : cuts) B->seg_caps.push_back(SegCap{k.u, uint32_t(k.ins)});
+            for (const SegCut &k : cuts) B->seg_caps.push_back(SegCap{k.u, uint32_t(k.ins), k.lo, k.hi});
             scr += (cut_scratch_words(Dd.res[i].n_entries) + 1) & ~1ull;
             B->cut.max_ne = std::max<uint32_t>(B->cut.max_ne, Dd.res[i].n_entries);
         }
@@ -1201,6 +1362,13 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     CK(B->d_results.alloc(B->docs.size()));
     CK(hipMemsetAsync(B->d_results.p, 0, std::max<size_t>(B->docs.size(), 1) * sizeof(DocResult), s));
     CK(finish_segments(*B, src_total, Dd.cbyte.p, Dd.content.p, s));
+    {   // linear documents: the fast-forward layout over the decoder's op runs, in place
+        std::vector<FFIn> ffin;
+        for (size_t i = 0; i < n; i++)
+            if (B->ff_doc[i] && B->host_status[i] == OK) ffin.push_back(FFIn{Dd.desc[i].op_off, Dd.res[i].n_ops, uint32_t(i)});
+            else B->ff_doc[i] = 0;
+        CK(stage_ff(*B, ffin, Dd.ops.p, Dd.cbyte.p, Dd.content.p, s));
+    }
     if (!B->seg_groups.empty()) {
         CK(B->d_plans.upload(B->seg_plans, s));
         CK(B->d_caps.upload(B->seg_caps, s));
@@ -1260,7 +1428,7 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
                 if (owner[d] < n && !big[owner[d]]) { big[owner[d]] = 1; lst.push_back(owner[d]); }
             const size_t nb = lst.size();
             for (size_t i = 0; i < n; i++)
-                if (!big[i]) lst.push_back(uint32_t(i));
+                if (!big[i] && !B->ff_doc[i]) lst.push_back(uint32_t(i));
             if (lst.size() > nb) {
                 if (B->d_split.upload(lst, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) return DTGPU_ERR_HIP;
                 B->split = true;
@@ -1386,15 +1554,24 @@ int prep_and_plan(dtgpu_batch *B, hipStream_t s, hipEvent_t mid) {
     return OK;
 }
 
+// The linear documents' checkout (dt_ff.hip) on s: first in a pass, or, in a split pass, right
+// after the side pipeline's fork (beside it, before the main pipeline's prep).
+int launch_ff_pass(dtgpu_batch *B, hipStream_t s) { return B->n_ff ? launch_ff(B->ff, s) : OK; }
+// The tracker part of a pass (prep -> plan -> replay), unless every document fast-forwards.
+bool tracker_pass(const dtgpu_batch *B) { return B->n_track != 0 || B->ff_doc.empty(); }
+
 int launch_all(dtgpu_batch *B, hipStream_t s) {
     if (B->xf_mode) return launch_replay_xf(B->large, s);
     if (B->split) {
         int e = launch_split_side(B, s);   // (it plans the cuts too)
+        if (!e) e = launch_ff_pass(B, s);
         if (!e) e = launch_split_prep(B, s);
         if (!e) e = launch_split_plan(B, s);
         return e ? e : replay_all(B, s, B->split_tier);
     }
-    const int e = prep_and_plan(B, s, nullptr);   // device-staged: walker inputs first
+    int e = launch_ff_pass(B, s);
+    if (e || !tracker_pass(B)) return e;
+    e = prep_and_plan(B, s, nullptr);   // device-staged: walker inputs first
     return e ? e : replay_all(B, s);
 }
 
@@ -1779,9 +1956,10 @@ dtgpu_status dtgpu_batch_run_e2e_timed(dtgpu_batch *B, float ms[4]) {
     if (hipEventRecord(B->ev_dec, s) != hipSuccess) return DTGPU_ERR_HIP;
     if (launch_decode(B->dec->P, s)) return DTGPU_ERR_HIP;
     if (hipEventRecord(B->ev_prep, s) != hipSuccess) return DTGPU_ERR_HIP;
-    if (prep_and_plan(B, s, B->ev0) != OK) return DTGPU_ERR_HIP;
+    if (launch_ff_pass(B, s)) return DTGPU_ERR_HIP;   // linear documents (dt_ff.hip)
+    if (tracker_pass(B) ? prep_and_plan(B, s, B->ev0) != OK : hipEventRecord(B->ev0, s) != hipSuccess) return DTGPU_ERR_HIP;
     if (hipEventRecord(B->ev_mid, s) != hipSuccess) return DTGPU_ERR_HIP;
-    int st = replay_all(B, s);
+    int st = tracker_pass(B) ? replay_all(B, s) : OK;
     if (st) return dtgpu_status(st);
     if (hipEventRecord(B->ev1, s) != hipSuccess) return DTGPU_ERR_HIP;
     if (hipEventSynchronize(B->ev1) != hipSuccess) return DTGPU_ERR_HIP;
@@ -1852,9 +2030,16 @@ dtgpu_status dtgpu_batch_encode(dtgpu_batch *B, uint32_t flags, float *kernel_ms
         q.prof = getenv("DTGPU_ENC_PROF") ? 1u : 0u;
         for (int k = 0; k < 32; k++) q.x2n[k] = Dd.P.x2n[k];
     }
-    // the walk order: the planner's commands (prep + plan, as a checkout pass runs them)
-    if (launch_prep(B->prep, s)) return DTGPU_ERR_HIP;
-    if (B->n_gpu_planned && launch_plan(B->plan, s) != OK) return DTGPU_ERR_HIP;
+    // the walk order: the planner's commands (prep + plan, as a checkout pass runs them), for
+    // every document (a checkout pass skips the fast-forwarded ones: their lists cover the rest)
+    {
+        PrepParams pp = B->prep;
+        PlanParams qq = B->plan;
+        pp.doc_list = nullptr; pp.n_docs = uint32_t(B->n);
+        qq.doc_list = nullptr; qq.n_docs = uint32_t(B->n);
+        if (launch_prep(pp, s)) return DTGPU_ERR_HIP;
+        if (B->n_gpu_planned && launch_plan(qq, s) != OK) return DTGPU_ERR_HIP;
+    }
     B->enc.flags = flags;
     CK(hipMemsetAsync(B->e_dres.p, 0, std::max<size_t>(B->n, 1) * sizeof(EncResult), s));
     CK(hipEventRecord(B->ev0, s));
@@ -1937,7 +2122,13 @@ dtgpu_status dtgpu_batch_run_timed(dtgpu_batch *B, float *ms) {
     const bool split = prep && B->split;   // split pass: prep / plan times are the main pipeline's
     if (hipEventRecord(B->ev_prep, s) != hipSuccess) return DTGPU_ERR_HIP;
     if (split && launch_split_side(B, s)) return DTGPU_ERR_HIP;   // (it plans the cuts too)
-    if (split) {
+    // linear documents (dt_ff.hip): a batch of only those reports their pass as its replay time
+    if (!B->xf_mode && !tracker_pass(B)) {
+        if (hipEventRecord(B->ev0, s) != hipSuccess || hipEventRecord(B->ev_mid, s) != hipSuccess) return DTGPU_ERR_HIP;
+    }
+    if (!B->xf_mode && launch_ff_pass(B, s)) return DTGPU_ERR_HIP;
+    if (!B->xf_mode && !tracker_pass(B)) {
+    } else if (split) {
         if (launch_split_prep(B, s) != OK || hipEventRecord(B->ev0, s) != hipSuccess || launch_split_plan(B, s) != OK)
             return DTGPU_ERR_HIP;
     } else if (B->xf_mode) {
@@ -1946,8 +2137,8 @@ dtgpu_status dtgpu_batch_run_timed(dtgpu_batch *B, float *ms) {
     } else if (prep_and_plan(B, s, B->ev0) != OK) {
         return DTGPU_ERR_HIP;
     }
-    if (hipEventRecord(B->ev_mid, s) != hipSuccess) return DTGPU_ERR_HIP;
-    int st = B->xf_mode ? launch_replay_xf(B->large, s) : replay_all(B, s, split ? B->split_tier : -1);
+    if (tracker_pass(B) && hipEventRecord(B->ev_mid, s) != hipSuccess) return DTGPU_ERR_HIP;
+    int st = B->xf_mode ? launch_replay_xf(B->large, s) : tracker_pass(B) ? replay_all(B, s, split ? B->split_tier : -1) : OK;
     if (st) return dtgpu_status(st);
     if (hipEventRecord(B->ev1, s) != hipSuccess) return DTGPU_ERR_HIP;
     if (hipEventSynchronize(B->ev1) != hipSuccess) return DTGPU_ERR_HIP;
@@ -1980,12 +2171,19 @@ size_t dtgpu_batch_segments(dtgpu_batch *B, size_t doc, uint32_t *out, size_t ca
         if (hipSetDevice(B->device) != hipSuccess) return 0;
         for (uint32_t k = 0; k < g.count && k < cap; k++) {
             const uint32_t d = B->seg_docs[g.first + k];
-            const DocDesc &e = B->docs[d];
+            DocDesc e{};   // the device descriptor: the pass's cut planning wrote the range
             DocResult r{};
             if (hipMemcpyAsync(&r, B->d_results.p + d, sizeof r, hipMemcpyDeviceToHost, B->stream) != hipSuccess ||
+                hipMemcpyAsync(&e, B->d_docs.p + d, sizeof e, hipMemcpyDeviceToHost, B->stream) != hipSuccess ||
                 hipStreamSynchronize(B->stream) != hipSuccess)
                 return 0;
-            uint32_t *w = out + 8 * size_t(k);
+            uint32_t *w = out + 12 * size_t(k);
+            const size_t slot = size_t(g.first) + k;
+            const bool dev_cut = slot < B->seg_caps.size();   // device-staged: the pass plans the cuts
+            w[8] = dev_cut && (e.flags & DOC_CUT_HOST) ? 1u : 0u;
+            w[9] = dev_cut ? B->seg_caps[slot].lo : e.seg_lo;
+            w[10] = dev_cut ? B->seg_caps[slot].hi : e.seg_hi;
+            w[11] = dev_cut ? B->seg_caps[slot].u : e.seg_u;
             w[0] = e.seg_lo; w[1] = e.seg_hi; w[2] = e.seg_u;
             // the first segment's result slot is the document's: the combine step rewrote it
             w[3] = k ? r.status : 0u; w[4] = k ? r.out_len : 0u; w[5] = r.dbg[15];
@@ -2001,6 +2199,11 @@ size_t dtgpu_batch_host_planned(const dtgpu_batch *B, uint8_t *flags, size_t cap
     size_t k = 0;
     for (uint8_t f : B->host_planned) k += f != 0;
     return k;
+}
+size_t dtgpu_batch_fast_forwarded(const dtgpu_batch *B, uint8_t *flags, size_t cap) {
+    if (!B) return 0;
+    if (flags) for (size_t i = 0; i < B->n && i < cap; i++) flags[i] = i < B->ff_doc.size() ? B->ff_doc[i] : 0;
+    return B->n_ff;
 }
 dtgpu_status dtgpu_batch_plan(dtgpu_batch *B, size_t i, uint32_t *cmds, size_t cmd_cap, uint32_t *tlist,
                               size_t tlist_cap, size_t *n_cmds, size_t *n_tlist) {

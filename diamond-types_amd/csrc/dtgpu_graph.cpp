@@ -64,7 +64,10 @@ extern "C" dtgpu_status dtgpu_graph_queries(const int64_t *hist, const size_t *h
     }
     std::vector<GraphQuery> q(nq);
     std::vector<int32_t> front;   // every query's versions, a then b
+    // every query's output spans in one u32-indexed arena: out_off = i * out_cap must not wrap
+    if (span_cap > (size_t(1) << 28)) return DTGPU_ERR_ARG;
     const uint32_t out_cap = uint32_t(4 * std::max<size_t>(span_cap, 1));
+    if (uint64_t(nq) * out_cap > (uint64_t(1) << 31)) return DTGPU_ERR_ARG;
     const uint32_t c_cap = uint32_t(std::min<size_t>(common_cap, 1u << 24));
     // every query's common-frontier slots in one u32-indexed arena (as the frontier arena's 2^28 check)
     if (uint64_t(nq) * c_cap > (uint64_t(1) << 28)) return DTGPU_ERR_ARG;

@@ -121,6 +121,8 @@ def lib():
     L.dtgpu_batch_last_times.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
     L.dtgpu_batch_host_planned.argtypes = [vp, ctypes.POINTER(ctypes.c_uint8), sz]
     L.dtgpu_batch_host_planned.restype = sz
+    L.dtgpu_batch_fast_forwarded.argtypes = [vp, ctypes.POINTER(ctypes.c_uint8), sz]
+    L.dtgpu_batch_fast_forwarded.restype = sz
     pu32 = ctypes.POINTER(ctypes.c_uint32)
     L.dtgpu_batch_plan.argtypes = [vp, sz, pu32, sz, pu32, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
     L.dtgpu_oplog_ins_content.argtypes = [vp, ctypes.c_char_p, sz]
@@ -797,6 +799,14 @@ class Batch:
         lib().dtgpu_batch_host_planned(self._h, buf, n)
         return [int(x) for x in buf[:n]]
 
+    def fast_forwarded(self):
+        """Per document: 1 when it checked out on the fast-forward path (dt_ff.hip: a linear
+        history, merge.rs:811-840), else 0."""
+        n = len(self)
+        buf = (ctypes.c_uint8 * max(1, n))()
+        lib().dtgpu_batch_fast_forwarded(self._h, buf, n)
+        return [int(x) for x in buf[:n]]
+
     def plan(self, i):
         """Command stream (op, lv, len, pos) and retreat/advance entries of document i."""
         nc, nt = ctypes.c_size_t(), ctypes.c_size_t()
@@ -825,10 +835,11 @@ class Batch:
     def segments(self, i):
         """Cut replay: the LV segments document i replayed as (see dtgpu_batch_segments), as
         dicts; [] when it replayed whole."""
-        out = (ctypes.c_uint32 * (8 * 64))()
+        out = (ctypes.c_uint32 * (12 * 64))()
         n = lib().dtgpu_batch_segments(self._h, i, out, 64)
-        keys = ["lo", "hi", "placeholders", "status", "items_visible", "cyc_total", "lds_index", "n_blocks"]
-        return [dict(zip(keys, list(out[8 * k:8 * k + 8]))) for k in range(min(n, 64))]
+        keys = ["lo", "hi", "placeholders", "status", "items_visible", "cyc_total", "lds_index", "n_blocks",
+                "host_fallback", "host_lo", "host_hi", "host_placeholders"]
+        return [dict(zip(keys, list(out[12 * k:12 * k + 12]))) for k in range(min(n, 64))]
 
     @property
     def algorithmic_bytes(self):

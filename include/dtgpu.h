@@ -267,6 +267,11 @@ dtgpu_status dtgpu_batch_last_times(const dtgpu_batch *batch, float out[3]);
  * numbering), 16 + k the device planner stopped with status k (17: an agent whose ops are not
  * one causal chain, e.g. one author committing on concurrent branches). */
 size_t dtgpu_batch_host_planned(const dtgpu_batch *batch, uint8_t *flags, size_t cap);
+/* Documents checked out on the fast-forward path (dt_ff.hip): a history of one graph entry, which
+ * the reference's merge fast-forwards through op by op (src/listmerge/merge.rs:811-840) -- on
+ * the device a piece table of segment replays composed pairwise, not the per-item tracker.
+ * flags[i] = 1 for those documents (up to cap); returns how many there are. */
+size_t dtgpu_batch_fast_forwarded(const dtgpu_batch *batch, uint8_t *flags, size_t cap);
 /* The command stream of document `doc` as last planned (16-byte commands as uint32 quads
  * {op, lv, len, pos}; TOG commands index the retreat/advance entries copied to tlist).
  * NULL buffers query the sizes. */
@@ -294,9 +299,11 @@ dtgpu_status dtgpu_batch_doc_stats(dtgpu_batch *batch, size_t doc, uint32_t out[
  * whole history below the cut is one version that every later op has seen, the boundary the
  * reference fast-forwards across (src/listmerge/merge.rs:811-840), each later segment starting
  * from placeholders for the text at its cut.  Returns the segment count (0 for a document
- * replayed whole) and writes up to `cap` records of 8 words: {first LV, end LV (~0: the end),
- * placeholders, status, visible items, cycles/16 (DTGPU_DEBUG=2), 1 if its index was in LDS,
- * blocks used} from the last run.
+ * replayed whole) and writes up to `cap` records of 12 words: {first LV, end LV (~0: the end),
+ * placeholders -- as the last pass's cut planning (cut_kernel) wrote them on the device --,
+ * status, visible items, cycles/16 (DTGPU_DEBUG=2), 1 if its index was in LDS, blocks used,
+ * 1 if the device planning declined and the host plan's ranges were used, then the host
+ * plan's first LV, end LV and placeholders} from the last run.
  * DTGPU_SEG=0 disables segmenting; DTGPU_SEG_OPS (op runs per segment, default 500, raised
  * to the batch's fair share per wave slot) and DTGPU_SEG_MAX (default 32) size it; read at
  * batch creation. */

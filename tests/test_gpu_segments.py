@@ -41,6 +41,11 @@ def _check_segments(segs, min_count=2):
     for a, b in zip(segs, segs[1:]):
         assert a["hi"] == b["lo"] and a["lo"] < a["hi"]
     assert all(s["status"] == 0 for s in segs), segs
+    # the ranges the pass used are the device cut planning's own (cut_kernel), equal to the host
+    # plan staging reserved the arenas from; the host-plan fallback never engaged
+    for s in segs:
+        assert s["host_fallback"] == 0, segs
+        assert (s["lo"], s["hi"], s["placeholders"]) == (s["host_lo"], s["host_hi"], s["host_placeholders"]), segs
 
 
 FF_WANT = None
@@ -124,3 +129,71 @@ def test_forced_segments_lds_handback(monkeypatch):
     assert [r["status"] for r in res] == [0, 0]
     assert all(t == _ff_want() for t in texts)
     _check_segments(b.segments(0), 4)
+
+
+def _scattered_inserts_doc(seed, n_ins=400):
+    """A concurrent prefix (two agents, then a merge: the history has cut points only after it),
+    then long inserts (16-48 chars) scattered over the whole text and a few deletes: with small
+    segments each later segment's inserts land across many placeholder blocks, the case the
+    block reservation of add_segments (dtgpu_api.cpp) bounds."""
+    import random
+    rng = random.Random(seed)
+    o = dt_amd.ListOpLog()
+    a = o.get_or_create_agent_id("a")
+    b = o.get_or_create_agent_id("b")
+    for k in range(60):
+        o.add_insert(a, 0, "".join(rng.choice("abcdefgh") for _ in range(100)))
+    v = o.local_frontier()
+    x = o.add_insert_at(a, v, 10, "AAAA")
+    y = o.add_insert_at(b, v, 20, "BBBB")
+    o.add_insert_at(a, [x, y], 0, "merge")
+    n = 6000 + 13
+    for k in range(n_ins):
+        if k % 10 == 9 and n > 100:
+            p = rng.randrange(n - 30)
+            o.add_delete_without_content(a if k % 20 else b, p, p + 20)
+            n -= 20
+        else:
+            s = "".join(rng.choice("ijklmnop") for _ in range(rng.randint(16, 48)))
+            o.add_insert(b if k % 3 else a, rng.randint(0, n), s)
+            n += len(s)
+    return o.encode()
+
+
+def test_segments_with_scattered_long_inserts(monkeypatch):
+    monkeypatch.setenv("DTGPU_SEG_OPS", "24")
+    docs = [_scattered_inserts_doc(s) for s in range(3)]
+    b, res, texts = _run(docs, "device")
+    for i, d in enumerate(docs):
+        assert res[i]["status"] == 0, (i, res[i])
+        assert texts[i] == OracleOpLog.load_from(d).checkout_tip_bytes(), i
+        _check_segments(b.segments(i), 4)
+
+
+def _many_entries_doc(rounds):
+    """2 * rounds + 1 graph entries: each round two agents insert at the same version, the next
+    round merges them."""
+    o = dt_amd.ListOpLog()
+    a = o.get_or_create_agent_id("a")
+    b = o.get_or_create_agent_id("b")
+    v = [o.add_insert(a, 0, "start")]
+    n = 5
+    for r in range(rounds):
+        x = o.add_insert_at(a, v, r % n, "x")
+        y = o.add_insert_at(b, v, (r * 7) % n, "y")
+        v = [x, y]
+        n += 2
+    return o.encode()
+
+
+def test_walk_kernel_past_64k_lds():
+    """~16k graph entries (near PLAN_MAX_LDS_ENTRIES): the walk kernel's stack and pending counts
+    take more than the default 64 KiB of dynamic LDS (dt_plan.hip launch_walk raises the
+    limit); device-planned, text equal to the oracle's."""
+    d = _many_entries_doc(8000)
+    o = dt_amd.ListOpLog.load_from(d)
+    assert 16000 <= len(o.export("entries")) <= 16384
+    b, res, texts = _run([d], "device")
+    assert res[0]["status"] == 0, res[0]
+    assert b.host_planned() == [0]
+    assert texts[0] == OracleOpLog.load_from(d).checkout_tip_bytes()

@@ -74,8 +74,9 @@ def test_gpu_device_staged_synth_merge_docs_match_oracle():
             continue
         assert res[i]["status"] == 0, (i, res[i])
         assert b.text(i) == want, i
-    assert set(range(len(docs), len(allv))) <= set(deferred), "wide documents must be handed back"
-    assert len(deferred) <= len(wide) + 4
+    # only the wide documents (96 agents: past the device prep's 64 causal chains) are handed
+    # back; every ordinary 4-16-agent document checks out on the device path
+    assert set(deferred) == set(range(len(docs), len(allv))), deferred
     # the documented retry: the host-staged batch checks the deferred ones out on the device
     h = dt_amd.Batch(docs=[allv[i] for i in deferred], staging="host")
     h.run()

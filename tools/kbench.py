@@ -18,6 +18,8 @@ def main():
     if name.startswith("synth"):   # synth[:distinct] -- synthetic concurrent docs (dt_synth.cpp)
         distinct = int(name.split(":")[1]) if ":" in name else 256
         pool = [dt_amd.synth_merge_oplog(i, 5000) for i in range(distinct)]
+    elif name in G.JSON_TRACES:   # a linear trace, built as crates/bench builds it, written as .dt
+        data = dt_amd.apply_edits_push_merge(G.trace(name)["txns"]).encode()
     else:
         data = G.dt_bytes(name)
     for n in counts:
@@ -38,7 +40,8 @@ def main():
         best = min(ms)
         print(f"{name} docs={n} stage={stage:.2f}s kernel_ms={best:.2f} (all {['%.2f' % m for m in ms]}) "
               f"ok={ok} Mops/s={lv / best / 1e3:.1f} alg_GB/s={b.algorithmic_bytes / best / 1e6:.1f} "
-              f"plan/replay_ms={split[ms.index(best)][0]:.2f}/{split[ms.index(best)][1]:.2f} host_planned={sum(b.host_planned())}",
+              f"plan/replay_ms={split[ms.index(best)][0]:.2f}/{split[ms.index(best)][1]:.2f} host_planned={sum(b.host_planned())} "
+              f"ff={sum(b.fast_forwarded())}",
               flush=True)
 
 
