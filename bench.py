@@ -41,7 +41,8 @@ def parse():
     p.add_argument("--workload", default="friendsforever",
                    help="friendsforever | git-makefile | node_nodecc (benchmark_data copies), synth "
                         "(BASELINE configs[3]: synthetic concurrent documents, dt_synth.cpp, written as .dt) or "
-                        "mixed (configs[4]: all 8 benchmark_data traces)")
+                        "mixed (configs[4]: all 8 benchmark_data traces) or linear (the five linear JSON traces, "
+                        "checked out on the fast-forward path, dt_ff.hip)")
     p.add_argument("--distinct", type=int, default=256, help="synth: distinct documents, replicated to --docs")
     p.add_argument("--synth-family", default="merge", choices=["merge", "epoch"],
                    help="synth: SURVEY 8(d)4 pairwise-merge generator (default) or the epoch generator")
@@ -93,26 +94,28 @@ def cpu_baseline(pool, budget_s, cores, workload="friendsforever"):
     """The CPU oracle (C restatement of the reference algorithm, one document per thread)
     timed on a bounded sample of the same workload: checkout_tip() on an already-decoded
     oplog, as the reference's `complex/merge` bench times it.  `pool`: the distinct documents.
-    The oracle replays every LV through a per-item tracker; the reference fast-forwards linear
-    prefixes (src/listmerge/merge.rs:811-840) and uses RLE spans, so on concurrent histories
-    the real Rust path is likely faster than this restatement."""
+    A linear history takes the oracle's fast-forward path (dto_checkout_tip_ff, as the
+    reference's merge.rs:811-840); a concurrent one replays every LV through a per-item tracker
+    where the reference uses RLE spans, so on concurrent histories the real Rust path is likely
+    faster than this restatement."""
     from oracle.oracle import OpLog as OracleOpLog
     why = "--cpu-cores"
     if cores <= 0:
         cores, why = host_threads()
     o = OracleOpLog.load_from(pool[0])
     t0 = time.perf_counter()
-    o.checkout_tip_bytes()
+    o.checkout_tip_ff_bytes()
     one = time.perf_counter() - t0
     per_core = max(1, int(budget_s / max(one, 1e-4) / cores))
     done = [0] * cores
     lvs = [0] * cores
+    ff = [False] * cores
     logs = [[OracleOpLog.load_from(pool[(k + j) % len(pool)]) for j in range(min(len(pool), 4))] for k in range(cores)]
 
     def work(k):
         for i in range(per_core):
             lg = logs[k][i % len(logs[k])]
-            lg.checkout_tip_bytes()
+            ff[k] |= lg.checkout_tip_ff_bytes()[1]
             done[k] += 1
             lvs[k] += len(lg)
 
@@ -127,8 +130,11 @@ def cpu_baseline(pool, budget_s, cores, workload="friendsforever"):
     return {"value": sum(lvs) / wall, "unit": "merged ops/s", "cores": cores, "kind": "port",
             "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(), "threads_from": why,
             "sample": f"{docs} x {workload} checkout_tip (decoded oplog) on {cores} host threads, {wall:.2f} s: "
-                      f"C per-item restatement of the reference algorithm (oracle/dt_oracle.c), no fast-forward "
-                      f"path (the reference fast-forwards linear prefixes, merge.rs:811-840)"}
+                      f"C restatement of the reference algorithm (oracle/dt_oracle.c): "
+                      + ("the fast-forward path for the linear histories (dto_checkout_tip_ff, merge.rs:811-840)"
+                         + (", the per-item tracker for the others" if len(pool) > 5 else "") if any(ff) else
+                         "per-item tracker (no linear history in the sample; the reference fast-forwards only a "
+                         "linear prefix, merge.rs:811-840)")}
 
 
 def cpu_config0():
@@ -339,6 +345,14 @@ def workload_pool(args):
         return pool, ("all 8 benchmark_data traces (3 .dt files + 5 JSON traces built the way "
                       "crates/bench/src/utils.rs:25-44 builds their oplogs and written as .dt by "
                       "dtgpu_oplog_encode), replicated round-robin")
+    if args.workload == "linear":   # the five linear traces: one graph entry each (fast-forward path)
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import golden_data as G
+        import dt_amd
+        pool = [dt_amd.apply_edits_push_merge(G.trace(n)["txns"]).encode() for n in G.JSON_TRACES]
+        return pool, ("the 5 linear benchmark_data JSON traces (automerge-paper, rustcode, seph-blog1, "
+                      "sveltecomponent, friendsforever_flat) built as crates/bench/src/utils.rs:25-44 builds "
+                      "them, written as .dt by dtgpu_oplog_encode, replicated round-robin")
     path = os.path.join(ROOT, "tests", "golden", "benchmark_data", args.workload + ".dt")
     return [open(path, "rb").read()], f"benchmark_data/{args.workload}.dt replicated (byte-identical copies in distinct buffers)"
 
@@ -356,7 +370,7 @@ def expected_texts(args, pool):
     from concurrent.futures import ThreadPoolExecutor
 
     def one(d):
-        t = OracleOpLog.load_from(d).checkout_tip_bytes()
+        t = OracleOpLog.load_from(d).checkout_tip_ff_bytes()[0]   # (the tracker unless linear)
         return (len(t), dt_amd.text_hash(t))
     with ThreadPoolExecutor(max(1, args.gen_threads)) as ex:
         return list(ex.map(one, pool))
@@ -470,6 +484,8 @@ def main():
     replay_ms = statistics.mean(x[1] for x in split)
     prep_ms = statistics.mean(x[2] for x in split)
     alg_bytes = batch.algorithmic_bytes
+    n_ff = sum(batch.fast_forwarded())
+    all_ff = n_ff == len(docs)
     # roofline of the dominant kernel (replay_kernel): the pass's algorithmic bytes over the
     # replay launch's own HIP-event time on the batch's stream
     achieved = alg_bytes / (replay_ms / 1000.0) / 1e9
@@ -478,7 +494,7 @@ def main():
     if os.path.exists(tpath):   # HBM bytes per launch from rocprofv3 PMC runs of this command
         tj = json.load(open(tpath))
         pass_traffic = tj.get("hbm_bytes_per_pass")
-        rk = [v for k, v in tj.get("per_kernel", {}).items() if k.startswith("replay_kernel")]
+        rk = [v for k, v in tj.get("per_kernel", {}).items() if k.startswith("ff_" if all_ff else "replay_kernel")]
         if rk:   # every replay tier's launch of the pass (tools/traffic.py)
             traffic = sum(2 * v["fetch_kib"] + v["write_kib"] for v in rk) * 1024
 
@@ -498,8 +514,11 @@ def main():
         "config": {"workload": f"{args.workload} x {args.docs} docs per GPU (checkout_tip)",
                    "docs_per_gpu": args.docs, "merged_ops_per_doc": lv_per_doc,
                    "distinct_docs": len(pool),
-                   "timed": "device walker inputs (prep) + cut planning + walk planning + replay + materialisation "
-                            "of the whole batch (decoded oplogs resident in HBM)",
+                   "timed": ("fast-forward checkout (dt_ff.hip: segment replays on piece tables, pairwise "
+                             "composition, text) of the whole batch (decoded oplogs resident in HBM)" if all_ff else
+                             "device walker inputs (prep) + cut planning + walk planning + replay + materialisation "
+                             "of the whole batch (decoded oplogs resident in HBM)"
+                             + (f"; {n_ff} linear documents on the fast-forward path (dt_ff.hip)" if n_ff else "")),
                    "parallelism": f"dp{world} (documents sharded, no data-path collective)"},
         "docs_per_sec": n_total * args.steps / elapsed,
         "total_merged_ops": total_lv,
@@ -507,8 +526,12 @@ def main():
         "staging": staging,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "replay_kernel (dominant kernel of the pass)", "kernel_ms": replay_ms,
-                     "pass": {"kernels": "prep_kernel x2 + chain_kernel + walk_kernel + cut_kernel + plan_kernel + replay_kernel tiers + combine_kernel", "ms": avg_kernel_ms,
+                     "kernel": ("ff kernels (dt_ff.hip: delta, segment replay, composition levels, text, copy)"
+                                if all_ff else "replay_kernel (dominant kernel of the pass)"), "kernel_ms": replay_ms,
+                     "pass": {"kernels": ("ff_delta + ff_seg + ff_compose x levels + ff_text + ff_copy" if all_ff else
+                                          "prep_kernel x2 + chain_kernel + walk_kernel + cut_kernel + plan_kernel + "
+                                          "replay_kernel tiers + combine_kernel"
+                                          + (" + the ff kernels" if n_ff else "")), "ms": avg_kernel_ms,
                               "prep_ms": prep_ms, "plan_ms": plan_ms, "replay_ms": replay_ms,
                               "achieved": alg_bytes / (avg_kernel_ms / 1000.0) / 1e9,
                               "frac": alg_bytes / (avg_kernel_ms / 1000.0) / 1e9 / HBM_PEAK_GBS,

@@ -1126,6 +1126,14 @@ int launch_cut(const CutParams &p, void *stream) {
     return hipGetLastError() == hipSuccess ? 0 : 66;
 }
 
+namespace prep {
+__global__ void pass_mark_kernel() {}
+}  // namespace prep
+int launch_pass_mark(void *stream) {
+    hipLaunchKernelGGL(prep::pass_mark_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream));
+    return hipGetLastError() == hipSuccess ? 0 : 66;
+}
+
 int launch_prep_stage(const PrepParams &p, void *stream, int stage) {
     if (!p.n_docs) return 0;
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);

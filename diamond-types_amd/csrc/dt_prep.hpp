@@ -111,5 +111,9 @@ int launch_cut(const CutParams &p, void *stream);
 // caller can start work that needs only the first half (the planner's walk) beside the rest.
 // Requires p.chain_flag and !p.check.
 int launch_prep_stage(const PrepParams &p, void *stream, int stage);
+// An empty one-wave kernel that opens a checkout pass when DTGPU_PASS_MARK is set at staging:
+// the PMC traffic tool (tools/traffic.py) sums the dispatches after the last marker, whatever
+// mix of streams and pipelines the pass uses.
+int launch_pass_mark(void *stream);
 
 }  // namespace dtgpu

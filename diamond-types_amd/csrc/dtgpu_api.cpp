@@ -312,6 +312,7 @@ struct dtgpu_batch {
     DevBuf<int32_t> f_delta;
     DevBuf<uint32_t> f_bad, f_pa, f_pb, f_ca, f_cb, f_boff;
     FFParams ff{};
+    bool pass_mark = false;   // DTGPU_PASS_MARK at staging: every pass opens with pass_mark_kernel
 
     // batched encoder (dtgpu_batch_encode): per-document descriptors, scratch, output
     std::vector<EncDesc> e_desc;
@@ -665,6 +666,7 @@ struct FFIn { uint64_t op_off; uint32_t n_ops; uint32_t doc; };   // op runs: qu
 hipError_t stage_ff(dtgpu_batch &B, const std::vector<FFIn> &in, const uint32_t *ops, const uint32_t *cbyte,
                     const uint8_t *content, hipStream_t s) {
     hipError_t e = hipSuccess;
+    B.pass_mark = getenv("DTGPU_PASS_MARK") != nullptr;   // (profiling runs: tools/traffic.py)
     std::vector<uint32_t> track;
     for (size_t i = 0; i < B.n; i++)
         if (!B.ff_doc[i]) track.push_back(uint32_t(i));
@@ -1561,6 +1563,7 @@ int launch_ff_pass(dtgpu_batch *B, hipStream_t s) { return B->n_ff ? launch_ff(B
 bool tracker_pass(const dtgpu_batch *B) { return B->n_track != 0 || B->ff_doc.empty(); }
 
 int launch_all(dtgpu_batch *B, hipStream_t s) {
+    if (B->pass_mark && launch_pass_mark(s)) return ErrHip;
     if (B->xf_mode) return launch_replay_xf(B->large, s);
     if (B->split) {
         int e = launch_split_side(B, s);   // (it plans the cuts too)
@@ -2120,6 +2123,7 @@ dtgpu_status dtgpu_batch_run_timed(dtgpu_batch *B, float *ms) {
     hipStream_t s = B->stream;
     const bool prep = B->dec && !B->xf_mode;
     const bool split = prep && B->split;   // split pass: prep / plan times are the main pipeline's
+    if (B->pass_mark && launch_pass_mark(s)) return DTGPU_ERR_HIP;
     if (hipEventRecord(B->ev_prep, s) != hipSuccess) return DTGPU_ERR_HIP;
     if (split && launch_split_side(B, s)) return DTGPU_ERR_HIP;   // (it plans the cuts too)
     // linear documents (dt_ff.hip): a batch of only those reports their pass as its replay time

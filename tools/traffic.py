@@ -38,8 +38,14 @@ def dispatches(d, counter):
 
 
 def last_pass(disp):
-    """Dispatch ids of the last checkout pass (see the module docstring)."""
+    """Dispatch ids of the last checkout pass (see the module docstring).  A run staged with
+    DTGPU_PASS_MARK=1 opens every pass with pass_mark_kernel: then the pass is every dispatch
+    after the last marker (split pipelines, fast-forward kernels and all); run the profiled
+    bench with --no-decode --no-encode so that nothing follows the timed pass."""
     ids = sorted(disp)
+    marks = [i for i in ids if "pass_mark_kernel" in disp[i][0]]
+    if marks:
+        return [i for i in ids if i > marks[-1]]
     i = len(ids) - 1
     while i >= 0 and not any(k in disp[ids[i]][0] for k in END):
         i -= 1
