@@ -109,7 +109,14 @@ extern "C" {
                                    n_frontier: *mut usize) -> dtgpu_status;
     pub fn dtgpu_batch_create_decoded(dec: *mut dtgpu_decoded, out: *mut *mut dtgpu_batch) -> dtgpu_status;
     pub fn dtgpu_device_count() -> c_int;
+    // the decoded oplog's arrays (op runs, inserted content, per-LV byte offsets, ...)
+    pub fn dtgpu_oplog_export(oplog: *const dtgpu_oplog, what: c_int, out: *mut c_void, cap: usize) -> usize;
+    // which documents of a batch took the fast-forward path (linear histories, merge.rs:811-840)
+    pub fn dtgpu_batch_fast_forwarded(batch: *const dtgpu_batch, flags: *mut u8, cap: usize) -> usize;
 }
+pub const DTGPU_EXPORT_OPS: c_int = 0;
+pub const DTGPU_EXPORT_CONTENT: c_int = 5;
+pub const DTGPU_EXPORT_CHAR_OFFSETS: c_int = 6;
 
 /// A decoded oplog (`ListOpLog`), owned.
 pub struct ListOpLog {
@@ -195,8 +202,110 @@ impl ListOpLog {
     }
 }
 
+impl ListOpLog {
+    /// `ListOpLog::checkout_tip()` (src/list/oplog.rs:38-42): the branch at the oplog's version.
+    pub fn checkout_tip(&self) -> Result<ListBranch, i32> {
+        Ok(ListBranch { content: self.checkout_tip_text()?, version: self.local_frontier() })
+    }
+    /// `ListOpLog::checkout(version)` (src/list/oplog.rs:32-36).
+    pub fn checkout(&self, version: &[u64]) -> Result<ListBranch, i32> {
+        let mut v = version.to_vec();
+        v.sort_unstable();
+        Ok(ListBranch { content: self.checkout_text(&v)?, version: v })
+    }
+    /// `find_dominators_2(a, b)` (src/causalgraph/graph/tools.rs:545-578): the frontier of a and b together.
+    pub fn dominators(&self, a: &[u64], b: &[u64]) -> Result<Vec<u64>, i32> {
+        unsafe {
+            let n = dtgpu_oplog_dominators(self.h, a.as_ptr(), a.len(), b.as_ptr(), b.len(), std::ptr::null_mut(), 0);
+            if n < 0 { return Err(-1); }
+            let mut v = vec![0u64; n as usize];
+            dtgpu_oplog_dominators(self.h, a.as_ptr(), a.len(), b.as_ptr(), b.len(), v.as_mut_ptr(), v.len());
+            Ok(v)
+        }
+    }
+    fn export_u32(&self, what: c_int) -> Vec<u32> {
+        unsafe {
+            let n = dtgpu_oplog_export(self.h, what, std::ptr::null_mut(), 0);
+            let mut v = vec![0u32; n / 4];
+            dtgpu_oplog_export(self.h, what, v.as_mut_ptr() as *mut c_void, n);
+            v
+        }
+    }
+    fn export_bytes(&self, what: c_int) -> Vec<u8> {
+        unsafe {
+            let n = dtgpu_oplog_export(self.h, what, std::ptr::null_mut(), 0);
+            let mut v = vec![0u8; n];
+            dtgpu_oplog_export(self.h, what, v.as_mut_ptr() as *mut c_void, n);
+            v
+        }
+    }
+}
+
 impl Drop for ListOpLog {
     fn drop(&mut self) { unsafe { dtgpu_oplog_free(self.h) } }
+}
+
+/// `ListBranch` (src/list/mod.rs:65-76, src/list/branch.rs): a document's text at a version.
+/// Checkouts and the transformed ops a merge applies are computed on the GPU.
+#[derive(Clone, Debug, Default, PartialEq, Eq)]
+pub struct ListBranch {
+    content: String,
+    version: Vec<u64>,
+}
+
+impl ListBranch {
+    /// `ListBranch::new()` (src/list/branch.rs:12-20): empty, at ROOT.
+    pub fn new() -> Self { ListBranch::default() }
+    /// `ListBranch::new_at_tip(oplog)` (src/list/branch.rs:30-32).
+    pub fn new_at_tip(oplog: &ListOpLog) -> Result<Self, i32> { oplog.checkout_tip() }
+    /// `ListBranch::new_at_local_version(oplog, version)` (src/list/branch.rs:22-26).
+    pub fn new_at_local_version(oplog: &ListOpLog, version: &[u64]) -> Result<Self, i32> { oplog.checkout(version) }
+    /// `ListBranch::content()` (src/list/branch.rs:38-41).
+    pub fn content(&self) -> &str { &self.content }
+    /// `ListBranch::len()` (src/list/branch.rs:49-52): characters, not bytes.
+    pub fn len(&self) -> usize { self.content.chars().count() }
+    pub fn is_empty(&self) -> bool { self.content.is_empty() }
+    /// `ListBranch::local_frontier()` (src/list/branch.rs:43-46).
+    pub fn local_frontier(&self) -> Vec<u64> { self.version.clone() }
+    pub fn local_frontier_ref(&self) -> &[u64] { &self.version }
+    /// `ListBranch::merge(&oplog, merge_frontier)` (src/list/merge.rs:63-95): apply the
+    /// transformed operations between the branch's version and `merge_frontier`
+    /// (iter_xf_operations_from, replayed on the GPU) to the content, then move to the dominators
+    /// of both versions.
+    pub fn merge(&mut self, oplog: &ListOpLog, merge_frontier: &[u64]) -> Result<(), i32> {
+        let target = oplog.dominators(&self.version, merge_frontier)?;
+        if target == self.version { return Ok(()); }
+        let xf = oplog.xf_operations_from(&self.version, merge_frontier)?;
+        let ops = oplog.export_u32(DTGPU_EXPORT_OPS);          // lv, len, pos, kind | fwd << 1
+        let content = oplog.export_bytes(DTGPU_EXPORT_CONTENT);
+        let cbyte = oplog.export_u32(DTGPU_EXPORT_CHAR_OFFSETS);
+        let mut text: Vec<char> = self.content.chars().collect();
+        for (lv, pos) in xf {
+            let pos = match pos { Some(p) => p as usize, None => continue };   // DeleteAlreadyHappened
+            // the op run holding lv (runs are in LV order)
+            let runs = ops.len() / 4;
+            let (mut lo, mut hi) = (0usize, runs);
+            while hi - lo > 1 {
+                let mid = (lo + hi) / 2;
+                if ops[4 * mid] <= lv { lo = mid; } else { hi = mid; }
+            }
+            if runs == 0 || lv < ops[4 * lo] || lv >= ops[4 * lo] + ops[4 * lo + 1] || pos > text.len() {
+                return Err(64);   // DTGPU_ERR_CHECKOUT
+            }
+            if ops[4 * lo + 3] & 1 == 0 {
+                let at = cbyte[lv as usize] as usize;
+                if at >= content.len() { return Err(64); }
+                let ch = std::str::from_utf8(&content[at..]).ok().and_then(|t| t.chars().next()).ok_or(64)?;
+                text.insert(pos, ch);
+            } else {
+                if pos >= text.len() { return Err(64); }
+                text.remove(pos);
+            }
+        }
+        self.content = text.into_iter().collect();
+        self.version = target;
+        Ok(())
+    }
 }
 
 /// Many `ListOpLog::load_from(doc)?.checkout_tip()` at once on one GPU: per document its status,

@@ -1561,6 +1561,7 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
         }
         R.raw_aruns = runs;
         R.n_lv = lv;
+        prof_mark(2);
         return S_OK;
     }
 

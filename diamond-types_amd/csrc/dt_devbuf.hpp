@@ -3,6 +3,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 namespace dtgpu {
@@ -26,5 +29,16 @@ struct DevBuf {
         return hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s);
     }
 };
+
+// Staging phase clock (DTGPU_STAGE_PROF=1): stage_prof("name") prints the wall milliseconds since
+// the previous call on this thread to stderr; stage_prof(nullptr) restarts the clock.
+inline void stage_prof(const char *phase) {
+    static const bool on = getenv("DTGPU_STAGE_PROF") != nullptr;
+    thread_local std::chrono::steady_clock::time_point last = std::chrono::steady_clock::now();
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    if (phase) fprintf(stderr, "[stage] %-28s %9.2f ms\n", phase, std::chrono::duration<double, std::milli>(now - last).count());
+    last = now;
+}
 
 }  // namespace dtgpu

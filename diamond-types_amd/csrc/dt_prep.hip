@@ -877,7 +877,9 @@ __global__ __launch_bounds__(64 * CUT_WAVES) void cut_kernel(CutParams P) {
     const PrepDesc D = P.pdocs[d];
     const uint32_t ne = D.ne, nop = D.n_ops, S = G.count, T = SP.n_targets;   // segments; equal-share targets
     // declined: the host plan's ranges (staging reserved the arenas from it; DOC_CUT_HOST marks it)
+    uint32_t *sized = P.sized ? P.sized + size_t(blockIdx.x) * CUT_SIZED_WORDS : nullptr;
     auto host_ranges = [&]() {
+        if (sized) { if (threadIdx.x == 0) sized[0] = 0; return; }   // sizing: not cut
         if (w != 0 || l >= S || l >= 64) return;
         const SegCap cap = P.caps[G.first + l];
         DocDesc *dd = P.docs + P.seg_docs[G.first + l];
@@ -998,7 +1000,7 @@ __global__ __launch_bounds__(64 * CUT_WAVES) void cut_kernel(CutParams P) {
         }
     }
     while (npick && total - cost(rdl(picks, npick - 1)) < q4c) npick--;
-    if (npick + 1 == S) {   // else not the staged segments (the poisoned ranges then fail the document)
+    if (sized ? npick >= 1 : npick + 1 == S) {   // else not the staged segments (the host plan's ranges then)
         if (l < npick) s_pick[l] = picks;
         if (l == 0) { s_np = npick; s_nr = nr; s_ok = 1; }
     }
@@ -1078,7 +1080,25 @@ __global__ __launch_bounds__(64 * CUT_WAVES) void cut_kernel(CutParams P) {
         if (l < npick) { at_ins = oi + s_at[0][l]; at_del = od + s_at[1][l]; at_dc = oc + s_at[2][l]; }
         for (uint32_t v = 0; v < NW; v++) tot_ins += s_tot[v][0];
     }
-    // 6. each segment's range and placeholder bound, against what staging reserved
+    // 6. each segment's range and placeholder bound, against what staging reserved (sizing:
+    //    written out for staging to reserve)
+    if (sized) {
+        const uint32_t Sr = npick + 1, k = l;
+        const uint32_t pprev = uint32_t(__shfl(int(picks), int(k ? k - 1 : 0)));
+        const uint32_t ai = uint32_t(__shfl(int(at_ins), int(k ? k - 1 : 0)));
+        const uint32_t ad = uint32_t(__shfl(int(at_del), int(k ? k - 1 : 0)));
+        const uint32_t ac = uint32_t(__shfl(int(at_dc), int(k ? k - 1 : 0)));
+        const uint32_t ins_lo = k ? ai : 0u;
+        const uint32_t ins_hi = k + 1 < Sr ? at_ins : tot_ins;
+        if (k < Sr) {
+            sized[1 + 4 * k] = k ? ops[pprev].x : 0u;
+            sized[2 + 4 * k] = k + 1 < Sr ? ops[picks].x : 0xFFFFFFFFu;
+            sized[3 + 4 * k] = k ? uint32_t(max<int64_t>(0, min(int64_t(ai), int64_t(ai) - int64_t(ad) + int64_t(ac)))) : 0u;
+            sized[4 + 4 * k] = ins_hi - ins_lo;
+        }
+        if (l == 0) sized[0] = Sr;
+        return;
+    }
     bool fits = true;
     for (uint32_t k = 0; k < S; k++) {
         const uint32_t ins_lo = k ? rdl(at_ins, k - 1) : 0u;

@@ -103,7 +103,12 @@ struct CutParams {
                             // it); null: the kernel searches the entries itself
     uint32_t *scr;      // per group cut_scratch_words (SegPlan::scr_off)
     uint32_t n_groups, max_ne;   // max_ne: the LDS table's entries (the groups' largest document)
+    // staging (sizing mode): groups hold one document each with count = the target count; the
+    // kernel writes per group CUT_SIZED_WORDS words -- the segment count (0: not cut), then per
+    // segment {first LV, end LV, placeholders, inserted chars} -- instead of descriptors
+    uint32_t *sized;
 };
+constexpr uint32_t CUT_SIZED_WORDS = 1 + 4 * 64;
 // suffix minima (ne + 1), cut ranges (2 ne), alignment
 inline uint64_t cut_scratch_words(uint32_t ne) { return 3ull * ne + 4; }
 int launch_cut(const CutParams &p, void *stream);

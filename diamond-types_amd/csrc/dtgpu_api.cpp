@@ -464,7 +464,7 @@ int replay_all(dtgpu_batch *B, hipStream_t s, int skip_tier = -1) {
     return e ? e : launch_combine(B->comb, s);   // cut documents: their segments' texts joined
 }
 
-// Cut replay inputs from a host oplog / from the decoder's device arrays (one long document).
+// Cut replay inputs from a host oplog (one long document).
 void seg_input_from_log(const HostOpLog &o, SegInput &si) {
     si.n_lv = o.n_lv;
     si.poff.push_back(0);
@@ -474,23 +474,6 @@ void seg_input_from_log(const HostOpLog &o, SegInput &si) {
         si.poff.push_back(uint32_t(si.par.size()));
     }
     for (const OpRun &r : o.ops) si.ops.push_back({r.lv, r.len, uint64_t(r.kind)});
-}
-bool seg_input_from_device(const dtgpu_decoded &Dd, size_t i, SegInput &si, hipStream_t s) {
-    const DecodeResult &r = Dd.res[i];
-    const DecodeDesc &d = Dd.desc[i];
-    std::vector<uint32_t> ent(2 * size_t(r.n_entries)), poff(size_t(r.n_entries) + 1), par(r.n_parents), ops(4 * size_t(r.n_ops));
-    if ((!ent.empty() && hipMemcpyAsync(ent.data(), Dd.ent.p + 2 * d.ent_off, ent.size() * 4, hipMemcpyDeviceToHost, s) != hipSuccess) ||
-        hipMemcpyAsync(poff.data(), Dd.poff.p + d.poff_off, poff.size() * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        (!par.empty() && hipMemcpyAsync(par.data(), Dd.par.p + d.par_off, par.size() * 4, hipMemcpyDeviceToHost, s) != hipSuccess) ||
-        (!ops.empty() && hipMemcpyAsync(ops.data(), Dd.ops.p + 4 * d.op_off, ops.size() * 4, hipMemcpyDeviceToHost, s) != hipSuccess) ||
-        hipStreamSynchronize(s) != hipSuccess)
-        return false;
-    si.n_lv = r.n_lv;
-    for (size_t k = 0; k < r.n_entries; k++) si.ent.push_back({ent[2 * k], ent[2 * k + 1]});
-    si.poff = poff;
-    si.par.assign(par.begin(), par.end());
-    for (size_t k = 0; k < r.n_ops; k++) si.ops.push_back({ops[4 * k], ops[4 * k + 1], uint64_t(ops[4 * k + 3] & 1u)});
-    return true;
 }
 // Add document i's later segments (cuts[1..]) as documents of its replay tier (or the HBM
 // tier) and make document i the first segment.  pc_total / blk_total / gidx_total / src_total
@@ -1097,6 +1080,7 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
         CK(hipMemcpyAsync(Dd.res.data(), Dd.d_res.p, n * sizeof(DecodeResult), hipMemcpyDeviceToHost, s));
         CK(hipStreamSynchronize(s));
     }
+    stage_prof("stage: decode pass");
     B->n = n;
     B->host_status.assign(n, OK);
     B->n_lv.assign(n, 0);
@@ -1168,6 +1152,7 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     std::vector<PrepResult> prr(n);
     CK(hipMemcpyAsync(prr.data(), B->pr_res.p, n * sizeof(PrepResult), hipMemcpyDeviceToHost, s));
     CK(hipStreamSynchronize(s));
+    stage_prof("stage: prep layout + pass");
 
     // ---- planner sizing pass ----------------------------------------------------------------------
     std::vector<PlanDesc> pdesc(n);
@@ -1234,6 +1219,7 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
         q.todo_cap = std::min<uint32_t>(PLAN_TODO_CAP, (deep + 16 + 1) & ~1u);
     }
 
+    stage_prof("stage: planner sizing pass");
     // ---- replay layout ---------------------------------------------------------------------------
     uint64_t cmd_total = 0, tlist_total = 0, blk_total = 0, out_total = 0, gidx_total = 0;
     const uint64_t lds_fill = lds_fill_setting();
@@ -1307,24 +1293,62 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
         std::vector<uint32_t> all = cand;
         for (size_t i = 0; i < n; i++) if (late[i]) all.push_back(uint32_t(i));
         std::sort(all.begin(), all.end());
-        uint64_t scr = 0;
+        // the cut planning itself (cut_kernel in sizing mode), one launch over every candidate
+        // and one copy back: the same deterministic kernel every pass then runs against the
+        // arenas reserved here (a host plan would need each document's decoded arrays back)
+        std::vector<SegGroup> sg;
+        std::vector<SegPlan> sp;
+        std::vector<uint32_t> sdocs;
+        uint64_t sscr = 0;
+        uint32_t smax_ne = 0;
         for (uint32_t i : all) {
-            SegInput si;
-            if (!seg_input_from_device(Dd, i, si, s)) return DTGPU_ERR_HIP;
+            const DecodeResult &r = Dd.res[i];
             SegSettings c = sc;
-            if (late[i]) { c.max_seg = 2; c.ops_per_seg = std::max<uint64_t>(1, si.ops.size() / 2); }
-            const std::vector<SegCut> cuts = plan_segments(si, c);
+            if (late[i]) { c.max_seg = 2; c.ops_per_seg = std::max<uint64_t>(1, r.n_ops / 2); }
+            const uint32_t T = uint32_t(std::min<uint64_t>(c.max_seg, r.n_ops / c.ops_per_seg));
+            if (T < 2 || r.n_entries == 0 || r.n_lv >= 0x7FFFFFFFull || r.n_entries > PLAN_MAX_LDS_ENTRIES) continue;
+            sg.push_back(SegGroup{uint32_t(sdocs.size()), T});
+            sdocs.push_back(i);
+            sp.push_back(SegPlan{c.w_op, T, sscr});
+            sscr += (cut_scratch_words(r.n_entries) + 1) & ~1ull;
+            smax_ne = std::max<uint32_t>(smax_ne, r.n_entries);
+        }
+        std::vector<uint32_t> sized(sg.size() * CUT_SIZED_WORDS);
+        if (!sg.empty()) {
+            DevBuf<SegGroup> dg;
+            DevBuf<SegPlan> dp;
+            DevBuf<uint32_t> dd, dscr, dout;
+            CK(dg.upload(sg, s)); CK(dp.upload(sp, s)); CK(dd.upload(sdocs, s));
+            CK(dscr.alloc(std::max<uint64_t>(sscr, 1))); CK(dout.alloc(sized.size()));
+            CutParams c{};
+            c.d_ops = Dd.ops.p; c.d_ent = Dd.ent.p; c.d_poff = Dd.poff.p; c.d_par = Dd.par.p;
+            c.pdocs = B->pr_docs.p;
+            c.groups = dg.p; c.seg_docs = dd.p; c.plans = dp.p;
+            c.scr = dscr.p;
+            c.n_groups = uint32_t(sg.size());
+            c.max_ne = smax_ne;
+            c.sized = dout.p;
+            if (launch_cut(c, s)) return DTGPU_ERR_HIP;
+            CK(hipMemcpyAsync(sized.data(), dout.p, sized.size() * 4, hipMemcpyDeviceToHost, s));
+            CK(hipStreamSynchronize(s));
+        }
+        uint64_t scr = 0;
+        for (size_t g = 0; g < sg.size(); g++) {
+            const uint32_t i = sdocs[g];
+            const uint32_t *z = sized.data() + g * CUT_SIZED_WORDS;
+            std::vector<SegCut> cuts(std::min<uint32_t>(z[0], 64));
+            for (size_t k = 0; k < cuts.size(); k++) cuts[k] = SegCut{z[1 + 4 * k], z[2 + 4 * k], z[3 + 4 * k], z[4 + 4 * k]};
             if (cuts.size() < 2 ||
                 !add_segments(*B, i, cuts, seg_tier[i], seg_est[i], lds_fill, pc_total, blk_total, gidx_total, src_total))
                 continue;
-            const uint32_t targets = uint32_t(std::min<uint64_t>(c.max_seg, si.ops.size() / c.ops_per_seg));
-            B->seg_plans.push_back(SegPlan{c.w_op, targets, scr});
+            B->seg_plans.push_back(SegPlan{sp[g].w_op, sp[g].n_targets, scr});
             for (const SegCut &k : cuts) B->seg_caps.push_back(SegCap{k.u, uint32_t(k.ins), k.lo, k.hi});
             scr += (cut_scratch_words(Dd.res[i].n_entries) + 1) & ~1ull;
             B->cut.max_ne = std::max<uint32_t>(B->cut.max_ne, Dd.res[i].n_entries);
         }
         CK(B->d_cutscr.alloc(std::max<uint64_t>(scr, 1)));
     }
+    stage_prof("stage: layout + cut plans");
     // every later pass: parent-vector rows as wide as the document's chains (staging counted
     // them), four-word aligned for the planner's 16-byte row loads -- a 64-word row per entry
     // spread two live words over a cache line of their own (prep's stores, the planner's loads)
@@ -1388,6 +1412,7 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
         if (!B->ev_cut) CK(hipEventCreateWithFlags(&B->ev_cut, hipEventDisableTiming));
     }
     CK(hipStreamSynchronize(s));
+    stage_prof("stage: arenas + uploads");
 #undef CK
     BatchParams base{};
     if (const char *dbg = getenv("DTGPU_DEBUG")) base.debug = uint32_t(atoi(dbg) ? atoi(dbg) : 1);
@@ -1443,6 +1468,7 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
             }
         }
     }
+    stage_prof("stage: split setup");
     *out = B.release();
     return DTGPU_OK;
 }

@@ -8,7 +8,10 @@
 
 #include <algorithm>
 #include <cstring>
+#include <atomic>
 #include <memory>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/dtgpu.h"
@@ -35,6 +38,81 @@ uint32_t multmodp_host(uint32_t a, uint32_t b) {
 
 uint64_t align256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
 
+// Process-wide pinned staging chunks for document uploads (allocated once, reused by every batch).
+struct Staging {
+    std::mutex mu;
+    uint8_t *buf[2] = {nullptr, nullptr};
+    hipEvent_t done[2] = {nullptr, nullptr};
+    int device = -1;
+};
+Staging &staging() {
+    static Staging *st = new Staging();   // (never destroyed: pinned memory outlives static teardown)
+    return *st;
+}
+constexpr uint64_t kStageChunk = 64ull << 20;
+
+// The documents into dst (their DecodeDesc offsets, zero padding up to the next document) on
+// stream s: packed on nt host threads into a pinned chunk, one async copy per chunk, two chunks
+// alternating.  A document larger than a chunk is copied from the caller's buffer directly.
+Status upload_packed(uint8_t *dst, uint64_t total, const uint8_t *const *docs, const size_t *lens, size_t n,
+                     const std::vector<DecodeDesc> &desc, int nt, hipStream_t s) {
+    if (!total) return OK;
+    Staging &st = staging();
+    std::lock_guard<std::mutex> lock(st.mu);
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return ErrHip;
+    if (st.device != dev) {   // (a different device: pinned chunks are portable, events are per device)
+        for (int k = 0; k < 2; k++) {
+            if (st.done[k]) (void)hipEventDestroy(st.done[k]);
+            st.done[k] = nullptr;
+        }
+        st.device = dev;
+    }
+    for (int k = 0; k < 2; k++) {
+        if (!st.buf[k] && hipHostMalloc(reinterpret_cast<void **>(&st.buf[k]), kStageChunk, hipHostMallocPortable) != hipSuccess)
+            return ErrHip;
+        if (!st.done[k] && hipEventCreateWithFlags(&st.done[k], hipEventDisableTiming) != hipSuccess) return ErrHip;
+        if (hipEventSynchronize(st.done[k]) != hipSuccess) return ErrHip;   // (an earlier batch's copy)
+    }
+    auto end_of = [&](size_t i) { return i + 1 < n ? desc[i + 1].in_off : total; };
+    size_t i = 0;
+    int k = 0;
+    while (i < n) {
+        const uint64_t base = desc[i].in_off;
+        size_t j = i;
+        while (j < n && end_of(j) - base <= kStageChunk) j++;
+        if (j == i) {   // one document larger than a chunk: straight from the caller's memory
+            if ((lens[i] && hipMemcpyAsync(dst + base, docs[i], lens[i], hipMemcpyHostToDevice, s) != hipSuccess) ||
+                hipMemsetAsync(dst + base + lens[i], 0, end_of(i) - base - lens[i], s) != hipSuccess ||
+                hipStreamSynchronize(s) != hipSuccess)
+                return ErrHip;
+            i++;
+            continue;
+        }
+        if (hipEventSynchronize(st.done[k]) != hipSuccess) return ErrHip;   // the chunk's last copy is done
+        uint8_t *chunk = st.buf[k];
+        std::atomic<size_t> next{i};
+        auto work = [&] {
+            for (size_t q; (q = next.fetch_add(1)) < j;) {
+                uint8_t *p = chunk + (desc[q].in_off - base);
+                if (lens[q]) std::memcpy(p, docs[q], lens[q]);
+                std::memset(p + lens[q], 0, end_of(q) - desc[q].in_off - lens[q]);
+            }
+        };
+        const int w = int(std::min<size_t>(size_t(nt), (j - i) / 16 + 1));
+        std::vector<std::thread> pool;
+        for (int t = 1; t < w; t++) pool.emplace_back(work);
+        work();
+        for (auto &th : pool) th.join();
+        if (hipMemcpyAsync(dst + base, chunk, end_of(j - 1) - base, hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipEventRecord(st.done[k], s) != hipSuccess)
+            return ErrHip;
+        k ^= 1;
+        i = j;
+    }
+    return hipStreamSynchronize(s) == hipSuccess ? OK : ErrHip;
+}
+
 }  // namespace
 
 extern "C" {
@@ -44,6 +122,7 @@ dtgpu_status dtgpu_decode_create(const uint8_t *const *docs, const size_t *lens,
     if (!out || (n && (!docs || !lens))) return DTGPU_ERR_ARG;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return DTGPU_ERR_NO_DEVICE;
+    stage_prof(nullptr);
     auto D = new dtgpu_decoded();
     std::unique_ptr<dtgpu_decoded> guard(D);
     D->device = opts ? opts->device : 0;
@@ -66,11 +145,15 @@ dtgpu_status dtgpu_decode_create(const uint8_t *const *docs, const size_t *lens,
         total = align256(total + lens[i] + 256);
         D->in_bytes += lens[i];
     }
-    {
-        std::vector<uint8_t> host(total, 0);
-        for (size_t i = 0; i < n; i++)
-            if (lens[i]) std::memcpy(host.data() + D->desc[i].in_off, docs[i], lens[i]);
-        CK(D->in.upload(host, s));
+    {   // one device arena: the documents are packed into pinned staging chunks on host threads
+        // (only each document's padding is zeroed) and each chunk is copied while the next one is
+        // packed -- no transient host copy of the whole batch (at 10k friendsforever documents a
+        // 360 MB buffer spent ~100 ms in page faults and unmapping alone)
+        CK(D->in.alloc(total));
+        int nt = opts && opts->host_threads > 0 ? opts->host_threads : int(std::thread::hardware_concurrency());
+        nt = int(std::max<size_t>(1, std::min<size_t>({size_t(std::max(nt, 1)), size_t(16), n / 64 + 1})));
+        if (Status e = upload_packed(D->in.p, total, docs, lens, n, D->desc, nt, s)) return dtgpu_status(e);
+        stage_prof("decode: upload documents");
     }
     CK(D->d_desc.upload(D->desc, s));
     CK(D->d_res.alloc(n));
@@ -87,6 +170,13 @@ dtgpu_status dtgpu_decode_create(const uint8_t *const *docs, const size_t *lens,
     if (launch_decode(P, s)) return DTGPU_ERR_HIP;
     CK(hipMemcpyAsync(D->res.data(), D->d_res.p, n * sizeof(DecodeResult), hipMemcpyDeviceToHost, s));
     CK(hipStreamSynchronize(s));
+    stage_prof("decode: sizing pass");
+    if (getenv("DTGPU_STAGE_PROF") && n) {   // core cycles per sizing phase: header + LZ4 claim, chunks, OpVersions
+        double a[3] = {0, 0, 0}, m[3] = {0, 0, 0};
+        for (size_t i = 0; i < n; i++)
+            for (int k = 0; k < 3; k++) { a[k] += D->res[i].prof[k]; m[k] = std::max<double>(m[k], D->res[i].prof[k]); }
+        fprintf(stderr, "[stage] sizing cycles/doc avg %.0f %.0f %.0f max %.0f %.0f %.0f\n", a[0] / n, a[1] / n, a[2] / n, m[0], m[1], m[2]);
+    }
     // arenas from the sizing pass
     uint64_t lz = 0, ar = 0, pre = 0, ops = 0, ent = 0, poff = 0, par = 0, content = 0, lv = 0, ag = 0, ver = 0;
     uint32_t max_f = 0;
@@ -148,6 +238,7 @@ dtgpu_status dtgpu_decode_create(const uint8_t *const *docs, const size_t *lens,
     P.size_only = 0;
     P.max_file_agents = std::max<uint32_t>(max_f, 1);
     CK(hipStreamSynchronize(s));
+    stage_prof("decode: arenas");
 #undef CK
     *out = guard.release();
     return DTGPU_OK;

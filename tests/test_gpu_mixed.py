@@ -76,13 +76,14 @@ def test_run_timed_on_host_and_device_staged_batches():
 
 
 def test_mixed_skewed_batch_forced_segments(mixed, monkeypatch):
-    """The same skewed batch with cut replay forced onto every document of 200+ op runs (the
-    linear JSON traces cut anywhere, node_nodecc and friendsforever where their histories allow):
-    segment documents in every LDS tier, the split pass's big tier among them, both staging
-    paths; every text still equals its golden / oracle text."""
+    """The same skewed batch with cut replay forced onto every tracker document of 200+ op runs
+    (node_nodecc and friendsforever where their histories allow; with DTGPU_FF=0 the linear
+    JSON traces too, cut anywhere): segment documents in every LDS tier, the split pass's big
+    tier among them, both staging paths; every text still equals its golden / oracle text."""
     monkeypatch.setenv("DTGPU_SEG_OPS", "100")
     docs, want = mixed
-    for staging in ("device", "host"):
+    for staging, ff in (("device", "1"), ("host", "1"), ("device", "0")):
+        monkeypatch.setenv("DTGPU_FF", ff)
         b = dt_amd.Batch(docs=docs, staging=staging)
         b.run_timed()
         res = b.results()
@@ -90,7 +91,11 @@ def test_mixed_skewed_batch_forced_segments(mixed, monkeypatch):
             assert r["status"] == 0, (staging, i, r)
             assert b.text(i) == w, (staging, i)
         segs = [b.segments(i) for i in range(len(docs))]
-        assert sum(1 for s in segs if len(s) >= 2) >= len(docs) // 2, staging
+        fast = b.fast_forwarded()
+        assert (sum(fast) > 0) == (ff == "1")
+        tracked = [i for i in range(len(docs)) if not fast[i]]
+        assert sum(1 for i in tracked if len(segs[i]) >= 2) >= len(tracked) // 2, staging
+        assert all(segs[i] == [] for i in range(len(docs)) if fast[i])
         assert all(x["status"] == 0 for s in segs for x in s)
 
 
