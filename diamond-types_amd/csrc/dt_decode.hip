@@ -31,6 +31,7 @@
 #include <stdint.h>
 
 #include "dt_decode.hpp"
+#include "dt_device.hpp"
 
 namespace dtgpu {
 namespace ddec {
@@ -2828,7 +2829,7 @@ int launch_decode(const DecodeParams &p, void *stream) {
         hipLaunchKernelGGL(ddec::decode_kernel<true>, dim3(p.n_docs), dim3(64), lds, s, p);
     else
         hipLaunchKernelGGL(ddec::decode_kernel<false>, dim3(p.n_docs), dim3(64), lds, s, p);
-    return hipGetLastError() == hipSuccess ? 0 : 66;
+    return launch_error() == hipSuccess ? 0 : 66;
 }
 
 int launch_decode_add(const AddParams &p, void *stream) {
@@ -2840,7 +2841,7 @@ int launch_decode_add(const AddParams &p, void *stream) {
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
         return 66;
     hipLaunchKernelGGL(ddec::decode_add_kernel, dim3(p.n_docs), dim3(64), lds, reinterpret_cast<hipStream_t>(stream), p);
-    return hipGetLastError() == hipSuccess ? 0 : 66;
+    return launch_error() == hipSuccess ? 0 : 66;
 }
 
 }  // namespace dtgpu

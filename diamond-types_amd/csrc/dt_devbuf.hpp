@@ -30,6 +30,15 @@ struct DevBuf {
     }
 };
 
+// A failed HIP call on a staging path: named on stderr (file:line and the runtime's message)
+// before the caller returns DTGPU_ERR_HIP, so a failure is never anonymous.
+inline bool hip_failed(hipError_t e, const char *file, int line) {
+    if (e == hipSuccess) return false;
+    fprintf(stderr, "[dtgpu] HIP error at %s:%d: %s\n", file, line, hipGetErrorString(e));
+    return true;
+}
+#define DTGPU_HIP_FAILED(x) ::dtgpu::hip_failed((x), __FILE__, __LINE__)
+
 // Staging phase clock (DTGPU_STAGE_PROF=1): stage_prof("name") prints the wall milliseconds since
 // the previous call on this thread to stderr; stage_prof(nullptr) restarts the clock.
 inline void stage_prof(const char *phase) {

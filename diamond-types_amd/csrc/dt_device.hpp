@@ -1,10 +1,20 @@
 // dt_device.hpp -- host/device shared layout of a staged batch (see dt_replay.hip).
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstdio>
 
 #include "dt_host.hpp"
 
 namespace dtgpu {
+
+// The last launch's error (hipGetLastError, which also clears it), named on stderr with the
+// launching file and line when set: a failed launch is never anonymous.
+inline hipError_t launch_error(const char *file = __builtin_FILE(), int line = __builtin_LINE()) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) fprintf(stderr, "[dtgpu] launch error at %s:%d: %s\n", file, line, hipGetErrorString(e));
+    return e;
+}
 
 // Per-document descriptor (device resident).  Offsets index the batch arenas.
 struct DocDesc {

@@ -25,6 +25,7 @@
 #include <stdint.h>
 
 #include "dt_encoder.hpp"
+#include "dt_device.hpp"
 
 namespace dtgpu {
 namespace enc {
@@ -1175,9 +1176,9 @@ int launch_encode(const EncParams &p, void *stream) {
     if (!p.n_docs) return OK;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(enc::encode_records_kernel, dim3(p.n_docs), dim3(64), (2 * size_t(p.max_agents) + 3 * 256) * 4, s, p);
-    if (hipGetLastError() != hipSuccess) return ErrHip;
+    if (launch_error() != hipSuccess) return ErrHip;
     hipLaunchKernelGGL(enc::encode_write_kernel, dim3(p.n_docs), dim3(64), 4096 * 4 + enc::LZ_RING + size_t(p.lds_text + 15) / 16 * 16, s, p);
-    return hipGetLastError() == hipSuccess ? OK : ErrHip;
+    return launch_error() == hipSuccess ? OK : ErrHip;
 }
 
 }  // namespace dtgpu

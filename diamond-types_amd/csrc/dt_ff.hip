@@ -403,7 +403,7 @@ int launch_ff(const FFParams &p, void *stream) {
     }
     hipLaunchKernelGGL(ff::ff_text_kernel, dim3(p.n_docs), dim3(ff::TT), 0, s, p);
     if (p.n_chunks) hipLaunchKernelGGL(ff::ff_copy_kernel, dim3(p.n_chunks), dim3(ff::XT), 0, s, p);
-    return hipGetLastError() == hipSuccess ? 0 : int(ErrHip);
+    return launch_error() == hipSuccess ? 0 : int(ErrHip);
 }
 
 }  // namespace dtgpu

@@ -21,6 +21,7 @@
 #include <stdint.h>
 
 #include "dt_graph.hpp"
+#include "dt_device.hpp"
 
 namespace dtgpu {
 namespace gdev {
@@ -493,7 +494,7 @@ int launch_graph_queries(const GraphParams &p, void *stream, bool big) {
     if (!p.n_queries) return 0;
     if (big) hipLaunchKernelGGL(gdev::graph_query_kernel<true>, dim3(p.n_queries), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), p);
     else hipLaunchKernelGGL(gdev::graph_query_kernel<false>, dim3(p.n_queries), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), p);
-    return hipGetLastError() == hipSuccess ? 0 : 66;
+    return launch_error() == hipSuccess ? 0 : 66;
 }
 
 }  // namespace dtgpu

@@ -38,6 +38,7 @@
 #include <stdint.h>
 
 #include "dt_graph.hpp"
+#include "dt_device.hpp"
 
 namespace dtgpu {
 namespace ldev {
@@ -559,7 +560,7 @@ int launch_levels(const LevelParams &p, void *stream) {
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (p.lvl_lds) hipLaunchKernelGGL(ldev::level_kernel<true>, dim3(p.n_graphs), dim3(ldev::NT), level_lds_bytes(p.lvl_lds), st, p);
     else hipLaunchKernelGGL(ldev::level_kernel<false>, dim3(p.n_graphs), dim3(ldev::NT), 0, st, p);
-    return hipGetLastError() == hipSuccess ? 0 : 66;
+    return launch_error() == hipSuccess ? 0 : 66;
 }
 
 int launch_level_diff(const LevelParams &p, const GraphParams &q, void *stream) {
@@ -567,7 +568,7 @@ int launch_level_diff(const LevelParams &p, const GraphParams &q, void *stream) 
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (p.lds_ent) hipLaunchKernelGGL(ldev::level_diff_kernel<true>, dim3(q.n_queries), dim3(ldev::NT), 8 * size_t(p.lds_ent), st, p, q);
     else hipLaunchKernelGGL(ldev::level_diff_kernel<false>, dim3(q.n_queries), dim3(ldev::NT), 0, st, p, q);
-    return hipGetLastError() == hipSuccess ? 0 : 66;
+    return launch_error() == hipSuccess ? 0 : 66;
 }
 
 int launch_level_conflict(const LevelParams &p, const GraphParams &q, void *stream, bool big) {
@@ -581,7 +582,7 @@ int launch_level_conflict(const LevelParams &p, const GraphParams &q, void *stre
         if (big) hipLaunchKernelGGL((ldev::level_conflict_kernel<false, false>), dim3(q.n_queries), dim3(ldev::NT), lp, st, p, q);
         else hipLaunchKernelGGL((ldev::level_conflict_kernel<false, true>), dim3(q.n_queries), dim3(ldev::NT), lp, st, p, q);
     }
-    return hipGetLastError() == hipSuccess ? 0 : 66;
+    return launch_error() == hipSuccess ? 0 : 66;
 }
 
 }  // namespace dtgpu

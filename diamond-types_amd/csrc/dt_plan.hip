@@ -1347,7 +1347,7 @@ int launch_walk(const PlanParams &q, void *stream, bool csr) {
     }
     if (csr) hipLaunchKernelGGL(pdev::walk_kernel<true>, grid, dim3(64), wlds, s, q);
     else hipLaunchKernelGGL(pdev::walk_kernel<false>, grid, dim3(64), wlds, s, q);
-    return hipGetLastError() == hipSuccess ? OK : ErrHip;
+    return launch_error() == hipSuccess ? OK : ErrHip;
 }
 
 int launch_plan(const PlanParams &q, void *stream, bool walk) {
@@ -1357,10 +1357,10 @@ int launch_plan(const PlanParams &q, void *stream, bool walk) {
     if (walk && q.split && q.walk && launch_walk(q, stream, false)) return ErrHip;
     if (q.split) hipLaunchKernelGGL(pdev::plan_kernel_1<true>, dim3(q.n_docs), dim3(64), lds, s, q);
     else hipLaunchKernelGGL(pdev::plan_kernel_1<false>, dim3(q.n_docs), dim3(64), lds, s, q);
-    if (hipGetLastError() != hipSuccess) return ErrHip;
+    if (launch_error() != hipSuccess) return ErrHip;
     if (q.max_agents > 64) {
         hipLaunchKernelGGL(pdev::plan_kernel_wide, dim3(q.n_docs), dim3(64), lds, s, q);
-        if (hipGetLastError() != hipSuccess) return ErrHip;
+        if (launch_error() != hipSuccess) return ErrHip;
     }
     return OK;
 }

@@ -1143,7 +1143,7 @@ int launch_cut(const CutParams &p, void *stream) {
                             int(lds)) != hipSuccess)
         return 66;
     hipLaunchKernelGGL(prep::cut_kernel, dim3(p.n_groups), dim3(64 * prep::CUT_WAVES), lds, reinterpret_cast<hipStream_t>(stream), p);
-    return hipGetLastError() == hipSuccess ? 0 : 66;
+    return launch_error() == hipSuccess ? 0 : 66;
 }
 
 namespace prep {
@@ -1151,7 +1151,7 @@ __global__ void pass_mark_kernel() {}
 }  // namespace prep
 int launch_pass_mark(void *stream) {
     hipLaunchKernelGGL(prep::pass_mark_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream));
-    return hipGetLastError() == hipSuccess ? 0 : 66;
+    return launch_error() == hipSuccess ? 0 : 66;
 }
 
 int launch_prep_stage(const PrepParams &p, void *stream, int stage) {
@@ -1167,7 +1167,7 @@ int launch_prep_stage(const PrepParams &p, void *stream, int stage) {
         q.mode = stage == 1 ? 1u : 2u;
         hipLaunchKernelGGL(prep::prep_kernel<false>, dim3(p.n_docs), dim3(64), lds, st, q);
     }
-    return hipGetLastError() == hipSuccess ? 0 : 66;
+    return launch_error() == hipSuccess ? 0 : 66;
 }
 
 int launch_prep(const PrepParams &p, void *stream) {
@@ -1181,7 +1181,7 @@ int launch_prep(const PrepParams &p, void *stream) {
         q.mode = 0;
         if (p.check) hipLaunchKernelGGL(prep::prep_kernel<true>, dim3(p.n_docs), dim3(64), lds, st, q);
         else hipLaunchKernelGGL(prep::prep_kernel<false>, dim3(p.n_docs), dim3(64), lds, st, q);
-        return hipGetLastError() == hipSuccess ? 0 : 66;
+        return launch_error() == hipSuccess ? 0 : 66;
     }
     // first half, the chain decomposition four documents per wave, second half
     q.mode = 1;
@@ -1190,7 +1190,7 @@ int launch_prep(const PrepParams &p, void *stream) {
     hipLaunchKernelGGL(prep::chain_kernel, dim3((p.n_docs + CHAIN_DOCS - 1) / CHAIN_DOCS), dim3(64), clds, st, q);
     q.mode = 2;
     hipLaunchKernelGGL(prep::prep_kernel<false>, dim3(p.n_docs), dim3(64), lds, st, q);
-    return hipGetLastError() == hipSuccess ? 0 : 66;
+    return launch_error() == hipSuccess ? 0 : 66;
 }
 
 }  // namespace dtgpu

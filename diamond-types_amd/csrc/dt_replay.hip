@@ -1900,7 +1900,7 @@ static int launch_lds_tier(const BatchParams &q, hipStream_t s, bool prof) {
         }
         if (prof) hipLaunchKernelGGL((dev::replay_kernel<dev::IX_FLAT, true, false>), dim3(q.n_list), dim3(64), lds, s, qp);
         else hipLaunchKernelGGL((dev::replay_kernel<dev::IX_FLAT, false, false, false, 8>), dim3(q.n_list), dim3(64), lds, s, qp);
-        return hipGetLastError() == hipSuccess ? OK : ErrHip;
+        return launch_error() == hipSuccess ? OK : ErrHip;
     }
     size_t lds = size_t(index_bytes_ms(q.lds_blocks, q.lds_sb, true));
     if (lds > 160 * 1024) return ErrArg;   // a tier cap above the CU's LDS
@@ -1929,7 +1929,7 @@ static int launch_lds_tier(const BatchParams &q, hipStream_t s, bool prof) {
     } else {
         hipLaunchKernelGGL((dev::replay_kernel<dev::IX_LDS, false, false>), dim3(q.n_list), dim3(64), lds, s, q);
     }
-    return hipGetLastError() == hipSuccess ? OK : ErrHip;
+    return launch_error() == hipSuccess ? OK : ErrHip;
 }
 
 int launch_replay(const ReplayLaunch &r) {
@@ -1985,7 +1985,7 @@ int launch_replay(const ReplayLaunch &r) {
     if (grid) {
         if (prof) hipLaunchKernelGGL((dev::replay_kernel<dev::IX_HBM, true, false>), dim3(grid), dim3(64), 0, s, large);
         else hipLaunchKernelGGL((dev::replay_kernel<dev::IX_HBM, false, false>), dim3(grid), dim3(64), 0, s, large);
-        if (hipGetLastError() != hipSuccess) return ErrHip;
+        if (launch_error() != hipSuccess) return ErrHip;
     }
     return OK;
 }
@@ -1998,7 +1998,7 @@ int launch_replay_xf(const BatchParams &large, void *stream) {
     if (!large.xf || !large.mup || !large.tup) return ErrArg;
     if (large.debug & 3u) hipLaunchKernelGGL((dev::replay_kernel<dev::IX_HBM, true, true>), dim3(large.n_list), dim3(64), 0, s, large);
     else hipLaunchKernelGGL((dev::replay_kernel<dev::IX_HBM, false, true>), dim3(large.n_list), dim3(64), 0, s, large);
-    return hipGetLastError() == hipSuccess ? OK : ErrHip;
+    return launch_error() == hipSuccess ? OK : ErrHip;
 }
 
 int launch_combine(const CombineParams &p, void *stream) {
@@ -2007,7 +2007,7 @@ int launch_combine(const CombineParams &p, void *stream) {
     const uint32_t n_cu = p.n_cu ? p.n_cu : 256u;   // the batch's device
     if (p.n_groups >= 2 * n_cu) hipLaunchKernelGGL(dev::combine_kernel<256>, dim3(p.n_groups), dim3(256), 0, s, p);
     else hipLaunchKernelGGL(dev::combine_kernel<1024>, dim3(p.n_groups), dim3(1024), 0, s, p);
-    return hipGetLastError() == hipSuccess ? OK : ErrHip;
+    return launch_error() == hipSuccess ? OK : ErrHip;
 }
 
 }  // namespace dtgpu

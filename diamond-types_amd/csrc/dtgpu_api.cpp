@@ -435,11 +435,11 @@ dtgpu_status set_tier_params(dtgpu_batch &B, const BatchParams &base) {
     for (int t = 0; t < kLdsTiers; t++) B.tier[t].n_cu = uint32_t(B.n_cu);
     B.large.n_cu = uint32_t(B.n_cu);
     B.debug = base.debug;
-    if (!B.ev_fork && hipEventCreateWithFlags(&B.ev_fork, hipEventDisableTiming) != hipSuccess) return DTGPU_ERR_HIP;
-    if (!B.ev_splan && hipEventCreateWithFlags(&B.ev_splan, hipEventDisableTiming) != hipSuccess) return DTGPU_ERR_HIP;
+    if (!B.ev_fork && DTGPU_HIP_FAILED(hipEventCreateWithFlags(&B.ev_fork, hipEventDisableTiming))) return DTGPU_ERR_HIP;
+    if (!B.ev_splan && DTGPU_HIP_FAILED(hipEventCreateWithFlags(&B.ev_splan, hipEventDisableTiming))) return DTGPU_ERR_HIP;
     for (int k = 0; k < kSideStreams; k++) {
-        if (!B.side[k] && hipStreamCreateWithFlags(&B.side[k], hipStreamNonBlocking) != hipSuccess) return DTGPU_ERR_HIP;
-        if (!B.ev_join[k] && hipEventCreateWithFlags(&B.ev_join[k], hipEventDisableTiming) != hipSuccess) return DTGPU_ERR_HIP;
+        if (!B.side[k] && DTGPU_HIP_FAILED(hipStreamCreateWithFlags(&B.side[k], hipStreamNonBlocking))) return DTGPU_ERR_HIP;
+        if (!B.ev_join[k] && DTGPU_HIP_FAILED(hipEventCreateWithFlags(&B.ev_join[k], hipEventDisableTiming))) return DTGPU_ERR_HIP;
     }
     return DTGPU_OK;
 }
@@ -737,16 +737,14 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return DTGPU_ERR_NO_DEVICE;
     auto B = std::make_unique<dtgpu_batch>();
     B->device = opts ? opts->device : 0;
-    if (hipSetDevice(B->device) != hipSuccess) return DTGPU_ERR_HIP;
+#define CK(x) do { if (DTGPU_HIP_FAILED(x)) return DTGPU_ERR_HIP; } while (0)
+    CK(hipSetDevice(B->device));
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, B->device) == hipSuccess && prop.multiProcessorCount > 0)
         B->n_cu = prop.multiProcessorCount;
-    if (hipStreamCreateWithFlags(&B->stream, hipStreamNonBlocking) != hipSuccess) return DTGPU_ERR_HIP;
-    if (hipEventCreate(&B->ev0) != hipSuccess || hipEventCreate(&B->ev_mid) != hipSuccess ||
-        hipEventCreate(&B->ev1) != hipSuccess || hipEventCreate(&B->ev_prep) != hipSuccess)
-        return DTGPU_ERR_HIP;
+    CK(hipStreamCreateWithFlags(&B->stream, hipStreamNonBlocking));
+    CK(hipEventCreate(&B->ev0)); CK(hipEventCreate(&B->ev_mid)); CK(hipEventCreate(&B->ev1)); CK(hipEventCreate(&B->ev_prep));
     hipStream_t s = B->stream;
-#define CK(x) do { if ((x) != hipSuccess) return DTGPU_ERR_HIP; } while (0)
     const size_t n = prep.size();
     const int threads = threads_for(opts, n);
     B->n = n;
@@ -828,7 +826,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         q.prof = getenv("DTGPU_PLAN_PROF") ? 1u : 0u;
         q.docs = B->p_docs.p; q.results = B->p_results.p; q.n_docs = uint32_t(n);
         q.count_only = 1;
-        if (launch_plan(q, s) != OK) return DTGPU_ERR_HIP;
+        if (launch_plan(q, s) != OK) { DTGPU_HIP_FAILED(hipErrorLaunchFailure); return DTGPU_ERR_HIP; }
         q.count_only = 0;
     }
     std::vector<PlanResult> pres(n);
@@ -1048,7 +1046,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     base.docs = B->d_docs.p;
     base.results = B->d_results.p;
     base.src = B->d_src.p;
-    if (set_tier_params(*B, base) != DTGPU_OK) return DTGPU_ERR_HIP;
+    if (set_tier_params(*B, base) != DTGPU_OK) { DTGPU_HIP_FAILED(hipErrorUnknown); return DTGPU_ERR_HIP; }
     *out = B.release();
     return DTGPU_OK;
 }
@@ -1069,7 +1067,7 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
         B->n_cu = prop.multiProcessorCount;
     B->stream = Dd.stream;   // one stream for decode, prep, plan and replay
     Dd.stream = nullptr;     // owned by the batch from here on
-#define CK(x) do { if ((x) != hipSuccess) return DTGPU_ERR_HIP; } while (0)
+#define CK(x) do { if (DTGPU_HIP_FAILED(x)) return DTGPU_ERR_HIP; } while (0)
     CK(hipEventCreate(&B->ev0)); CK(hipEventCreate(&B->ev_mid)); CK(hipEventCreate(&B->ev1));
     CK(hipEventCreate(&B->ev_dec)); CK(hipEventCreate(&B->ev_prep));
     CK(hipEventCreateWithFlags(&B->ev_w0, hipEventDisableTiming));
@@ -1198,7 +1196,7 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     q.docs = B->p_docs.p; q.results = B->p_results.p; q.n_docs = uint32_t(n);
     q.count_only = 1;
     q.todo_cap = 0;
-    if (launch_plan(q, s) != OK) return DTGPU_ERR_HIP;
+    if (launch_plan(q, s) != OK) { DTGPU_HIP_FAILED(hipErrorLaunchFailure); return DTGPU_ERR_HIP; }
     q.count_only = 0;
     std::vector<PlanResult> pres(n);
     CK(hipMemcpyAsync(pres.data(), B->p_results.p, std::max<size_t>(n, 1) * sizeof(PlanResult), hipMemcpyDeviceToHost, s));
@@ -1430,7 +1428,7 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     base.docs = B->d_docs.p;
     base.results = B->d_results.p;
     base.src = B->d_src.p;
-    if (set_tier_params(*B, base) != DTGPU_OK) return DTGPU_ERR_HIP;
+    if (set_tier_params(*B, base) != DTGPU_OK) { DTGPU_HIP_FAILED(hipErrorUnknown); return DTGPU_ERR_HIP; }
     B->wstream = B->side[kSideStreams - 1];   // the smallest side tier's stream (see wstream)
     // split pass: when an LDS tier rides a side stream and other documents exist, its
     // documents' prep and plan do not wait for everyone else's (a skewed batch's longest replays
@@ -1457,12 +1455,12 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
             for (size_t i = 0; i < n; i++)
                 if (!big[i] && !B->ff_doc[i]) lst.push_back(uint32_t(i));
             if (lst.size() > nb) {
-                if (B->d_split.upload(lst, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) return DTGPU_ERR_HIP;
+                if (DTGPU_HIP_FAILED(B->d_split.upload(lst, s)) || DTGPU_HIP_FAILED(hipStreamSynchronize(s))) return DTGPU_ERR_HIP;
                 B->split = true;
                 B->split_tier = tb;
-                if (!B->ws_side && hipStreamCreateWithFlags(&B->ws_side, hipStreamNonBlocking) != hipSuccess) return DTGPU_ERR_HIP;
-                if (!B->ev_sw0 && hipEventCreateWithFlags(&B->ev_sw0, hipEventDisableTiming) != hipSuccess) return DTGPU_ERR_HIP;
-                if (!B->ev_sw1 && hipEventCreateWithFlags(&B->ev_sw1, hipEventDisableTiming) != hipSuccess) return DTGPU_ERR_HIP;
+                if (!B->ws_side && DTGPU_HIP_FAILED(hipStreamCreateWithFlags(&B->ws_side, hipStreamNonBlocking))) return DTGPU_ERR_HIP;
+                if (!B->ev_sw0 && DTGPU_HIP_FAILED(hipEventCreateWithFlags(&B->ev_sw0, hipEventDisableTiming))) return DTGPU_ERR_HIP;
+                if (!B->ev_sw1 && DTGPU_HIP_FAILED(hipEventCreateWithFlags(&B->ev_sw1, hipEventDisableTiming))) return DTGPU_ERR_HIP;
                 B->n_big = uint32_t(nb);
                 B->n_rest = uint32_t(lst.size() - nb);
             }
@@ -2005,7 +2003,7 @@ dtgpu_status dtgpu_batch_encode(dtgpu_batch *B, uint32_t flags, float *kernel_ms
     if (flags & ~uint32_t(DTGPU_ENCODE_FULL)) return DTGPU_ERR_ARG;
     if (hipSetDevice(B->device) != hipSuccess) return DTGPU_ERR_HIP;
     hipStream_t s = B->stream;
-#define CK(x) do { if ((x) != hipSuccess) return DTGPU_ERR_HIP; } while (0)
+#define CK(x) do { if (DTGPU_HIP_FAILED(x)) return DTGPU_ERR_HIP; } while (0)
     if (B->e_desc.empty() && B->n) {   // layout once per batch
         const dtgpu_decoded &Dd = *B->dec;
         B->e_desc.assign(B->n, EncDesc{});

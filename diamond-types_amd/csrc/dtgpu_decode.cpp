@@ -38,12 +38,11 @@ uint32_t multmodp_host(uint32_t a, uint32_t b) {
 
 uint64_t align256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
 
-// Process-wide pinned staging chunks for document uploads (allocated once, reused by every batch).
+// Process-wide pinned staging chunks for document uploads (allocated once, reused by every batch;
+// each upload ends with its stream synchronised, so the next one finds both chunks idle).
 struct Staging {
     std::mutex mu;
     uint8_t *buf[2] = {nullptr, nullptr};
-    hipEvent_t done[2] = {nullptr, nullptr};
-    int device = -1;
 };
 Staging &staging() {
     static Staging *st = new Staging();   // (never destroyed: pinned memory outlives static teardown)
@@ -59,21 +58,16 @@ Status upload_packed(uint8_t *dst, uint64_t total, const uint8_t *const *docs, c
     if (!total) return OK;
     Staging &st = staging();
     std::lock_guard<std::mutex> lock(st.mu);
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return ErrHip;
-    if (st.device != dev) {   // (a different device: pinned chunks are portable, events are per device)
-        for (int k = 0; k < 2; k++) {
-            if (st.done[k]) (void)hipEventDestroy(st.done[k]);
-            st.done[k] = nullptr;
-        }
-        st.device = dev;
-    }
-    for (int k = 0; k < 2; k++) {
-        if (!st.buf[k] && hipHostMalloc(reinterpret_cast<void **>(&st.buf[k]), kStageChunk, hipHostMallocPortable) != hipSuccess)
+    for (int k = 0; k < 2; k++)
+        if (!st.buf[k] && DTGPU_HIP_FAILED(hipHostMalloc(reinterpret_cast<void **>(&st.buf[k]), kStageChunk, hipHostMallocPortable)))
             return ErrHip;
-        if (!st.done[k] && hipEventCreateWithFlags(&st.done[k], hipEventDisableTiming) != hipSuccess) return ErrHip;
-        if (hipEventSynchronize(st.done[k]) != hipSuccess) return ErrHip;   // (an earlier batch's copy)
-    }
+    struct Ev {   // this upload's copy-done events, one per chunk
+        hipEvent_t e[2] = {nullptr, nullptr};
+        bool rec[2] = {false, false};
+        ~Ev() { for (hipEvent_t x : e) if (x) (void)hipEventDestroy(x); }
+    } ev;
+    for (int k = 0; k < 2; k++)
+        if (DTGPU_HIP_FAILED(hipEventCreateWithFlags(&ev.e[k], hipEventDisableTiming))) return ErrHip;
     auto end_of = [&](size_t i) { return i + 1 < n ? desc[i + 1].in_off : total; };
     size_t i = 0;
     int k = 0;
@@ -82,14 +76,14 @@ Status upload_packed(uint8_t *dst, uint64_t total, const uint8_t *const *docs, c
         size_t j = i;
         while (j < n && end_of(j) - base <= kStageChunk) j++;
         if (j == i) {   // one document larger than a chunk: straight from the caller's memory
-            if ((lens[i] && hipMemcpyAsync(dst + base, docs[i], lens[i], hipMemcpyHostToDevice, s) != hipSuccess) ||
-                hipMemsetAsync(dst + base + lens[i], 0, end_of(i) - base - lens[i], s) != hipSuccess ||
-                hipStreamSynchronize(s) != hipSuccess)
+            if ((lens[i] && DTGPU_HIP_FAILED(hipMemcpyAsync(dst + base, docs[i], lens[i], hipMemcpyHostToDevice, s))) ||
+                DTGPU_HIP_FAILED(hipMemsetAsync(dst + base + lens[i], 0, end_of(i) - base - lens[i], s)) ||
+                DTGPU_HIP_FAILED(hipStreamSynchronize(s)))
                 return ErrHip;
             i++;
             continue;
         }
-        if (hipEventSynchronize(st.done[k]) != hipSuccess) return ErrHip;   // the chunk's last copy is done
+        if (ev.rec[k] && DTGPU_HIP_FAILED(hipEventSynchronize(ev.e[k]))) return ErrHip;   // the chunk's last copy is done
         uint8_t *chunk = st.buf[k];
         std::atomic<size_t> next{i};
         auto work = [&] {
@@ -104,13 +98,14 @@ Status upload_packed(uint8_t *dst, uint64_t total, const uint8_t *const *docs, c
         for (int t = 1; t < w; t++) pool.emplace_back(work);
         work();
         for (auto &th : pool) th.join();
-        if (hipMemcpyAsync(dst + base, chunk, end_of(j - 1) - base, hipMemcpyHostToDevice, s) != hipSuccess ||
-            hipEventRecord(st.done[k], s) != hipSuccess)
+        if (DTGPU_HIP_FAILED(hipMemcpyAsync(dst + base, chunk, end_of(j - 1) - base, hipMemcpyHostToDevice, s)) ||
+            DTGPU_HIP_FAILED(hipEventRecord(ev.e[k], s)))
             return ErrHip;
+        ev.rec[k] = true;
         k ^= 1;
         i = j;
     }
-    return hipStreamSynchronize(s) == hipSuccess ? OK : ErrHip;
+    return DTGPU_HIP_FAILED(hipStreamSynchronize(s)) ? ErrHip : OK;
 }
 
 }  // namespace
@@ -126,7 +121,7 @@ dtgpu_status dtgpu_decode_create(const uint8_t *const *docs, const size_t *lens,
     auto D = new dtgpu_decoded();
     std::unique_ptr<dtgpu_decoded> guard(D);
     D->device = opts ? opts->device : 0;
-#define CK(x) do { if ((x) != hipSuccess) return DTGPU_ERR_HIP; } while (0)
+#define CK(x) do { if (DTGPU_HIP_FAILED(x)) return DTGPU_ERR_HIP; } while (0)
     CK(hipSetDevice(D->device));
     CK(hipStreamCreateWithFlags(&D->stream, hipStreamNonBlocking));
     CK(hipEventCreate(&D->ev0));
@@ -272,7 +267,7 @@ dtgpu_status dtgpu_decode_add(const dtgpu_decoded *B, const uint8_t *const *patc
     std::unique_ptr<dtgpu_decoded> guard(M);
     M->device = B->device;
     M->merged = true;
-#define CK(x) do { if ((x) != hipSuccess) return DTGPU_ERR_HIP; } while (0)
+#define CK(x) do { if (DTGPU_HIP_FAILED(x)) return DTGPU_ERR_HIP; } while (0)
     CK(hipSetDevice(M->device));
     CK(hipStreamCreateWithFlags(&M->stream, hipStreamNonBlocking));
     CK(hipEventCreate(&M->ev0));

@@ -199,7 +199,10 @@ def test_device_planner_on_traces_and_kats():
     g.add_delete_at(c, [t], 0, 2)
     g.add_insert_at(a, [2, 5], 0, "ccc")
     oplogs.append(g)
-    b = dt_amd.Batch(oplogs=oplogs)
+    # the linear traces check out on the fast-forward path by default (dt_ff.hip, no walk plan);
+    # the planner is compared on them with that path off
+    assert dt_amd.Batch(oplogs=oplogs).fast_forwarded() == [1, 1, 0]
+    b = _with_env({"DTGPU_FF": "0"}, lambda: dt_amd.Batch(oplogs=oplogs))
     assert b.host_planned() == [0] * 3
     b.run()
     b.sync()
