@@ -32,7 +32,18 @@ pub struct dtgpu_batch_opts {
     pub ignore_crc: c_int,
     pub host_threads: c_int,
     pub device: c_int,
+    pub flags: u32,      // DTGPU_OPT_*
+    pub seg_ops: u32,    // 0: default
+    pub seg_max: u32,    // 0: default
+    pub lds_fill: u32,   // 0: default
 }
+pub const DTGPU_OPT_NO_FAST_FORWARD: u32 = 1;
+pub const DTGPU_OPT_NO_SEGMENTS: u32 = 2;
+pub const DTGPU_OPT_HOST_PLAN: u32 = 4;
+pub const DTGPU_OPT_NO_SPLIT: u32 = 8;
+pub const DTGPU_OPT_NO_CRITICAL: u32 = 16;
+pub const DTGPU_OPT_DEBUG: u32 = 32;
+pub const DTGPU_OPT_PASS_MARK: u32 = 64;
 pub type dtgpu_status = c_int;
 pub const DTGPU_OK: dtgpu_status = 0;
 // EncodeOptions (src/list/encoding/encode_oplog.rs:88-130) as dtgpu_oplog_encode flags
@@ -313,7 +324,7 @@ impl ListBranch {
 pub fn batch_checkout(docs: &[&[u8]], device: i32) -> Result<Vec<dtgpu_doc_result>, i32> {
     let ptrs: Vec<*const u8> = docs.iter().map(|d| d.as_ptr()).collect();
     let lens: Vec<usize> = docs.iter().map(|d| d.len()).collect();
-    let opts = dtgpu_batch_opts { ignore_crc: 0, host_threads: 0, device };
+    let opts = dtgpu_batch_opts { device, ..Default::default() };
     let mut res = vec![dtgpu_doc_result::default(); docs.len()];
     let s = unsafe { dtgpu_batch_checkout(ptrs.as_ptr(), lens.as_ptr(), docs.len(), &opts, res.as_mut_ptr()) };
     if s != DTGPU_OK { Err(s) } else { Ok(res) }
@@ -330,7 +341,7 @@ impl DecodedBatch {
     pub fn load(docs: &[&[u8]], device: i32) -> Result<DecodedBatch, i32> {
         let ptrs: Vec<*const u8> = docs.iter().map(|d| d.as_ptr()).collect();
         let lens: Vec<usize> = docs.iter().map(|d| d.len()).collect();
-        let opts = dtgpu_batch_opts { ignore_crc: 0, host_threads: 0, device };
+        let opts = dtgpu_batch_opts { device, ..Default::default() };
         let mut h = std::ptr::null_mut();
         let s = unsafe { dtgpu_decode_create(ptrs.as_ptr(), lens.as_ptr(), docs.len(), &opts, &mut h) };
         if s != DTGPU_OK { return Err(s); }

@@ -96,6 +96,9 @@ struct BatchParams {
     uint32_t prio_from;  // LDS tiers: workgroups from this index on (dispatched after the first
                          // resident set) raise their wave priority (0: off)
     uint32_t n_cu;       // compute units of the batch's device (resident-set sizes)
+    uint32_t prio_on;    // LDS tiers: late workgroups raise their priority (prio_from computed at launch)
+    uint32_t tog_waves;  // 1: retreat / advance passes on one wave; else helper waves on the big tiers
+    uint32_t tog_mw_lds; // LDS index bytes from which a tier gets helper waves
 };
 
 // Cut replay: after the replay, one workgroup per cut document resolves its segments' source

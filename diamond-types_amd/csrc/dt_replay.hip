@@ -1891,8 +1891,7 @@ static int launch_lds_tier(const BatchParams &q, hipStream_t s, bool prof) {
         // LDS allows (allocated in 1280-byte granules; tools/occ_probe.hip measured both)
         BatchParams qp = q;
         qp.prio_from = 0;
-        const char *pe = getenv("DTGPU_PRIO");
-        if (!(pe && *pe == '0')) {
+        if (q.prio_on) {
             // (the batch's own device: late_documents sizes the same resident set from it)
             const size_t gran = (lds + 1279) / 1280 * 1280;
             const size_t per_cu = std::min<size_t>(32, 163840 / std::max<size_t>(gran, 1280));
@@ -1906,11 +1905,9 @@ static int launch_lds_tier(const BatchParams &q, hipStream_t s, bool prof) {
     if (lds > 160 * 1024) return ErrArg;   // a tier cap above the CU's LDS
     // documents whose index takes >= 32 KiB of LDS (at most four per CU) replay with helper
     // waves for long retreat / advance passes (DTGPU_TOG_WAVES=1: one wave)
-    const char *tw = getenv("DTGPU_TOG_WAVES");
     constexpr size_t kStatic = sizeof(uint32_t) * 4;   // tog_job: the multi-wave kernel's static LDS
-    size_t mw_min = 32 * 1024;   // DTGPU_TOG_MW_LDS: the LDS bytes from which a tier gets helper waves
-    if (const char *e = getenv("DTGPU_TOG_MW_LDS")) mw_min = size_t(strtoull(e, nullptr, 10));
-    const bool mw = lds >= mw_min && lds + kStatic <= 160 * 1024 && !(tw && *tw == '1');
+    const size_t mw_min = q.tog_mw_lds;   // the LDS bytes from which a tier gets helper waves
+    const bool mw = lds >= mw_min && lds + kStatic <= 160 * 1024 && q.tog_waves != 1;
     // allow dynamic LDS up to the CU's 160 KiB: a per-function, per-device attribute, set on
     // every launch (cheap) so it holds on whatever device the batch runs
     const void *fn = mw ? (prof ? reinterpret_cast<const void *>(&dev::replay_kernel<dev::IX_LDS, true, false, true>)

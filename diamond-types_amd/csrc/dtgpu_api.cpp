@@ -45,41 +45,86 @@ int item_tier(uint32_t est) {
     for (int t = 0; t < kLdsTiers; t++) if (bytes <= kItemTierCap[t]) return t;
     return -1;
 }
-// Expected inserted chars per block when sizing a document's LDS index: blocks end up ~43 items
-// full on the benchmark traces (cut_point, dt_replay.hip), sized at 40.  DTGPU_LDS_FILL
-// overrides it (tests force the LDS overflow -> HBM tier hand-back with it).
-uint64_t lds_fill_setting() {
-    uint64_t f = 40;
-    if (const char *e = getenv("DTGPU_LDS_FILL")) f = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
-    return f;
-}
-// The smallest LDS tier replays on the flat 2-level index (dt_replay.hip IX_FLAT), unless
-// DTGPU_FLAT=0 selects the 3-level one (A/B).
-bool flat_setting() {
-    const char *e = getenv("DTGPU_FLAT");
-    return !(e && *e == '0');
-}
-// The <= 64-chain planner: two phases (walk order, then lane-parallel steps) unless
-// DTGPU_PLAN_SPLIT=0 selects the one-phase walk (A/B).
-uint32_t plan_split_setting() {
-    const char *e = getenv("DTGPU_PLAN_SPLIT");
-    return e && *e == '0' ? 0u : 1u;
-}
-// The walk orders four documents per wave (walk_kernel) before the plan kernel, unless
-// DTGPU_PLAN_WALK=0 lets the plan kernel walk each document itself (A/B).
-// (Also for a single document: its walk then runs beside prep's second half, single
-// friendsforever pass 12.9 -> 12.0 ms.)
-uint32_t walk_setting(size_t) {
-    const char *e = getenv("DTGPU_PLAN_WALK");
-    return e && *e == '0' ? 0u : 1u;
-}
-// Prep as three launches with the chain decomposition four documents per wave, unless
-// DTGPU_PREP_CHAINS=0 selects the single launch (A/B).
-// (Also for small batches: a document's chain walk on a 16-lane group is slower than on a whole
-// wave, but the split lets the planner's walk run beside it.)
-uint32_t prep_chains_setting(size_t) {
-    const char *e = getenv("DTGPU_PREP_CHAINS");
-    return e && *e == '0' ? 0u : 1u;
+// How a batch checks out: the defaults, then dtgpu_batch_opts (the API's knobs), then the DTGPU_*
+// environment overrides (experiments, A/B runs, tests), read once when the batch is created.
+struct Settings {
+    bool ff = true;            // linear histories on the fast-forward path (dt_ff.hip)
+    bool seg = true;           // cut replay (long documents as LV segments on several waves)
+    uint64_t seg_ops = 500;    // op runs per segment (raised to the batch's fair share per wave slot)
+    uint32_t seg_max = 32;     // segments per document: measured against 16-64 on the six cut traces
+    uint32_t seg_w = SEG_W_OP; // the cut planner's cost weight of an op run
+    bool seg_fair = true;      // the fair-share floor on seg_ops
+    bool seg_late = true;      // late documents of the smallest tier cut once
+    // expected inserted chars per block when sizing a document's LDS index: blocks end up ~43
+    // items full on the benchmark traces (cut_point, dt_replay.hip), sized at 40 (tests force the
+    // LDS overflow -> HBM tier hand-back with a large value)
+    uint64_t lds_fill = 40;
+    bool flat = true;          // the smallest LDS tier on the flat 2-level index (IX_FLAT)
+    bool plan_split = true;    // the <= 64-chain planner in two phases (walk order, then lane-parallel steps)
+    // the walk four documents per wave (walk_kernel) before the plan kernel (also for a single
+    // document: its walk then runs beside prep's second half, 12.9 -> 12.0 ms)
+    bool plan_walk = true;
+    bool prep_chains = true;   // prep as three launches, the chain decomposition four documents per wave
+    bool walk_overlap = true;  // the walk on its own stream beside prep's second half
+    bool host_plan = false;    // walk plans built on the host
+    bool split = true;         // split pass for skewed batches
+    bool critical = true;      // critical replays first, at top wave priority
+    bool fallback = true;      // LDS-tier documents that outgrow their index replay on the HBM tier
+    bool prio = true;          // late workgroups of the flat tier raise their wave priority
+    uint32_t tog_waves = 0;    // 1: retreat / advance passes on one wave (else DTGPU_TOG_WAVES helpers)
+    uint32_t tog_mw_lds = 32 * 1024;   // LDS index bytes from which a tier gets helper waves
+    uint32_t debug = 0;        // bit 0 invariant checks, bit 1 cycle profile (the instrumented kernels)
+    bool prep_check = false;   // the bounds-checked prep kernel
+    bool pass_mark = false;    // every pass opens with pass_mark_kernel (tools/traffic.py)
+    bool plan_prof = false, enc_prof = false;
+    uint32_t enc_lds_text = 0;
+};
+Settings settings_for(const dtgpu_batch_opts *o) {
+    Settings c;
+    if (o) {
+        c.ff = !(o->flags & DTGPU_OPT_NO_FAST_FORWARD);
+        c.seg = !(o->flags & DTGPU_OPT_NO_SEGMENTS);
+        c.host_plan = (o->flags & DTGPU_OPT_HOST_PLAN) != 0;
+        c.split = !(o->flags & DTGPU_OPT_NO_SPLIT);
+        c.critical = !(o->flags & DTGPU_OPT_NO_CRITICAL);
+        c.debug = (o->flags & DTGPU_OPT_DEBUG) ? 1u : 0u;
+        c.pass_mark = (o->flags & DTGPU_OPT_PASS_MARK) != 0;
+        if (o->seg_ops) c.seg_ops = o->seg_ops;
+        if (o->seg_max) c.seg_max = o->seg_max;
+        if (o->lds_fill) c.lds_fill = o->lds_fill;
+    }
+    auto on = [](const char *name, bool &v) { if (const char *e = getenv(name)) v = *e != '0'; };
+    auto set = [](const char *name) { return getenv(name) != nullptr; };
+    auto num = [](const char *name, uint64_t lo, uint64_t hi, uint64_t &v) {
+        if (const char *e = getenv(name)) v = std::min<uint64_t>(std::max<uint64_t>(lo, strtoull(e, nullptr, 10)), hi);
+    };
+    on("DTGPU_FF", c.ff);
+    on("DTGPU_SEG", c.seg);
+    num("DTGPU_SEG_OPS", 1, UINT64_MAX, c.seg_ops);
+    uint64_t x = c.seg_max; num("DTGPU_SEG_MAX", 1, 64, x); c.seg_max = uint32_t(std::min<uint64_t>(x, 64));
+    x = c.seg_w; num("DTGPU_SEG_W", 0, 1u << 20, x); c.seg_w = uint32_t(x);
+    on("DTGPU_SEG_FAIR", c.seg_fair);
+    on("DTGPU_SEG_LATE", c.seg_late);
+    num("DTGPU_LDS_FILL", 1, UINT64_MAX, c.lds_fill);
+    on("DTGPU_FLAT", c.flat);
+    on("DTGPU_PLAN_SPLIT", c.plan_split);
+    on("DTGPU_PLAN_WALK", c.plan_walk);
+    on("DTGPU_PREP_CHAINS", c.prep_chains);
+    on("DTGPU_CRITICAL", c.critical);
+    on("DTGPU_PRIO", c.prio);
+    if (set("DTGPU_HOST_PLAN")) c.host_plan = true;
+    if (set("DTGPU_NO_SPLIT")) c.split = false;
+    if (set("DTGPU_NO_FALLBACK")) c.fallback = false;
+    if (set("DTGPU_NO_WALK_OVERLAP")) c.walk_overlap = false;
+    if (const char *e = getenv("DTGPU_DEBUG")) c.debug = uint32_t(atoi(e) ? atoi(e) : 1);
+    c.prep_check = c.debug != 0 || set("DTGPU_PREP_CHECK");
+    if (set("DTGPU_PASS_MARK")) c.pass_mark = true;
+    c.plan_prof = set("DTGPU_PLAN_PROF");
+    c.enc_prof = set("DTGPU_ENC_PROF");
+    x = c.tog_waves; num("DTGPU_TOG_WAVES", 0, 64, x); c.tog_waves = uint32_t(x);
+    x = c.tog_mw_lds; num("DTGPU_TOG_MW_LDS", 0, UINT64_MAX, x); c.tog_mw_lds = uint32_t(std::min<uint64_t>(x, UINT32_MAX));
+    x = 0; num("DTGPU_ENC_LDS_TEXT", 0, 24064, x); c.enc_lds_text = uint32_t(x);
+    return c;
 }
 // Per-document replay layout: block capacity, HBM index bytes, LDS tier.
 struct Layout { uint32_t max_blocks; uint64_t gidx; int tier; uint32_t tier_blocks; };
@@ -109,14 +154,8 @@ struct SegInput {
     std::vector<std::array<uint64_t, 3>> ops;         // op runs (lv, len, kind: 0 ins, 1 del) in LV order
 };
 struct SegSettings { bool on; uint64_t ops_per_seg; uint32_t max_seg, w_op; };
-SegSettings seg_settings() {
-    SegSettings s{true, 500, 32, SEG_W_OP};   // 32 segments: measured against 16-64 on the six cut traces
-    if (const char *e = getenv("DTGPU_SEG_W")) s.w_op = uint32_t(std::min<uint64_t>(strtoull(e, nullptr, 10), 1u << 20));
-    if (const char *e = getenv("DTGPU_SEG")) s.on = *e != '0';
-    if (const char *e = getenv("DTGPU_SEG_OPS")) s.ops_per_seg = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
-    if (const char *e = getenv("DTGPU_SEG_MAX")) s.max_seg = uint32_t(std::max<uint64_t>(1, strtoull(e, nullptr, 10)));
-    s.max_seg = std::min<uint32_t>(s.max_seg, 64);   // the device cut planning's lane-per-segment bound
-    return s;
+SegSettings seg_settings(const Settings &c) {
+    return SegSettings{c.seg, c.seg_ops, std::min<uint32_t>(c.seg_max, 64), c.seg_w};   // (<= 64: the device cut planning's lane per segment)
 }
 // Cut ranges [a, b] (every v in them is a cut), in LV order: at entry k ([s, t), parents P)
 // the prefix's frontier minus P must be empty (then [0, v) is the version {v-1} for s < v <= t),
@@ -214,6 +253,7 @@ std::vector<SegCut> plan_segments(const SegInput &in, const SegSettings &cfg) {
 struct dtgpu_batch {
     int device = 0;
     int n_cu = 256;
+    Settings cfg;   // opts + DTGPU_* overrides, fixed at creation
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev_mid = nullptr, ev1 = nullptr;
     size_t n = 0;
@@ -411,7 +451,7 @@ std::vector<uint32_t> tier_lists(dtgpu_batch &B) {
     return all;
 }
 dtgpu_status set_tier_params(dtgpu_batch &B, const BatchParams &base) {
-    const bool fb = n_lds_docs(B) && !getenv("DTGPU_NO_FALLBACK");
+    const bool fb = n_lds_docs(B) && B.cfg.fallback;
     size_t off = 0;
     for (int t = 0; t < kLdsTiers; t++) {
         BatchParams &q = B.tier[t];
@@ -420,7 +460,10 @@ dtgpu_status set_tier_params(dtgpu_batch &B, const BatchParams &base) {
         q.n_list = uint32_t(B.tier_list[t].size());
         q.lds_blocks = B.tier_blocks[t];
         q.lds_sb = lds_sb_capacity(q.lds_blocks);
-        q.lds_flat = t == 0 && flat_setting() && q.lds_blocks <= FLAT_MAX_BLOCKS ? 1u : 0u;
+        q.lds_flat = t == 0 && B.cfg.flat && q.lds_blocks <= FLAT_MAX_BLOCKS ? 1u : 0u;
+        q.prio_on = B.cfg.prio ? 1u : 0u;
+        q.tog_waves = B.cfg.tog_waves;
+        q.tog_mw_lds = B.cfg.tog_mw_lds;
         off += B.tier_list[t].size();
         if (fb) { q.fb_count = B.d_fb.p; q.fb_list = B.d_fb.p + 1; }
     }
@@ -543,13 +586,12 @@ bool add_segments(dtgpu_batch &B, uint32_t i, const std::vector<SegCut> &cuts, i
 // runs or the batch's fair share per wave slot (all op runs over 8 waves per CU), whichever is
 // more -- a batch of many equal documents already fills the GPU and is left alone.
 template <typename NOps>
-std::vector<uint32_t> seg_candidates(size_t n, SegSettings &sc, int n_cu, NOps n_ops) {
+std::vector<uint32_t> seg_candidates(size_t n, SegSettings &sc, int n_cu, bool fair, NOps n_ops) {
     std::vector<uint32_t> c;
     if (!sc.on) return c;
     uint64_t total = 0;
     for (size_t i = 0; i < n; i++) total += n_ops(i);
-    const char *fair = getenv("DTGPU_SEG_FAIR");   // "0": no fair-share floor (experiments)
-    if (!(fair && *fair == '0')) sc.ops_per_seg = std::max<uint64_t>(sc.ops_per_seg, total / (uint64_t(std::max(n_cu, 1)) * 8));
+    if (fair) sc.ops_per_seg = std::max<uint64_t>(sc.ops_per_seg, total / (uint64_t(std::max(n_cu, 1)) * 8));
     for (size_t i = 0; i < n; i++)
         if (n_ops(i) >= 2 * sc.ops_per_seg) c.push_back(uint32_t(i));
     return c;
@@ -562,8 +604,7 @@ std::vector<uint32_t> seg_candidates(size_t n, SegSettings &sc, int n_cu, NOps n
 template <typename NOps>
 std::vector<uint8_t> late_documents(const dtgpu_batch &B, const SegSettings &sc, NOps n_ops) {
     std::vector<uint8_t> late(B.n, 0);
-    const char *e = getenv("DTGPU_SEG_LATE");   // "0": no late cuts
-    if (!sc.on || (e && *e == '0') || B.tier_list[0].empty() || !flat_setting() || B.tier_blocks[0] > FLAT_MAX_BLOCKS) return late;
+    if (!sc.on || !B.cfg.seg_late || B.tier_list[0].empty() || !B.cfg.flat || B.tier_blocks[0] > FLAT_MAX_BLOCKS) return late;
     const size_t lds = size_t(flat_index_bytes(B.tier_blocks[0]));
     const size_t gran = (lds + 1279) / 1280 * 1280;
     const size_t resident = std::min<size_t>(32, 163840 / std::max<size_t>(gran, 1280)) * size_t(std::max(B.n_cu, 1));
@@ -583,8 +624,7 @@ std::vector<uint8_t> late_documents(const dtgpu_batch &B, const SegSettings &sc,
 // segments and documents; a batch of equal documents marks none).  DTGPU_CRITICAL=0: off.
 void mark_critical(dtgpu_batch &B) {
     for (DocDesc &d : B.docs) d.flags &= ~DOC_CRITICAL;
-    const char *e = getenv("DTGPU_CRITICAL");
-    if ((e && *e == '0') || B.docs.size() < 2) return;
+    if (!B.cfg.critical || B.docs.size() < 2) return;
     std::vector<uint32_t> per(B.docs.size(), 1);   // segments of each unit's document
     for (const SegGroup &g : B.seg_groups)
         for (uint32_t k = 0; k < g.count; k++) per[B.seg_docs[g.first + k]] = g.count;
@@ -637,10 +677,6 @@ hipError_t finish_segments(dtgpu_batch &B, uint64_t src_total, const uint32_t *c
 // A document checks out on the fast-forward path when its whole history is one graph entry: the
 // reference's merge then fast-forwards through every op (merge.rs:811-840; Graph::push extends
 // the last entry whenever a span continues it, so one entry <=> a linear history).
-bool ff_setting() {
-    const char *e = getenv("DTGPU_FF");   // "0": every document on the tracker (A/B, tests)
-    return !(e && *e == '0');
-}
 struct FFIn { uint64_t op_off; uint32_t n_ops; uint32_t doc; };   // op runs: quads into `ops`
 // The fast-forward layout of the batch's linear documents: segments of FF_RUNS op runs, the
 // composition pairs of every level, the copy chunks.  out_off / out_cap / lv_off / content_off /
@@ -649,7 +685,7 @@ struct FFIn { uint64_t op_off; uint32_t n_ops; uint32_t doc; };   // op runs: qu
 hipError_t stage_ff(dtgpu_batch &B, const std::vector<FFIn> &in, const uint32_t *ops, const uint32_t *cbyte,
                     const uint8_t *content, hipStream_t s) {
     hipError_t e = hipSuccess;
-    B.pass_mark = getenv("DTGPU_PASS_MARK") != nullptr;   // (profiling runs: tools/traffic.py)
+    B.pass_mark = B.cfg.pass_mark;   // (profiling runs: tools/traffic.py)
     std::vector<uint32_t> track;
     for (size_t i = 0; i < B.n; i++)
         if (!B.ff_doc[i]) track.push_back(uint32_t(i));
@@ -736,6 +772,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return DTGPU_ERR_NO_DEVICE;
     auto B = std::make_unique<dtgpu_batch>();
+    B->cfg = settings_for(opts);
     B->device = opts ? opts->device : 0;
 #define CK(x) do { if (DTGPU_HIP_FAILED(x)) return DTGPU_ERR_HIP; } while (0)
     CK(hipSetDevice(B->device));
@@ -754,7 +791,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     B->docs.resize(n);
     B->host_planned.assign(n, 0);
     B->ff_doc.assign(n, 0);
-    const bool force_host = xf || getenv("DTGPU_HOST_PLAN") != nullptr;
+    const bool force_host = xf || B->cfg.host_plan;
 
     // ---- 1. device planner inputs; a sizing pass of the planner gives exact stream sizes ----
     std::vector<PlanDesc> pdesc(n);
@@ -819,11 +856,11 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         q.child = B->p_child.p; q.opc = B->p_opc.p;
         q.aruns = B->d_aruns.p; q.tip = B->p_tip.p; q.erec = B->p_erec.p; q.doff = B->p_doff.p;
         q.dense = B->p_dense.p; q.base = B->p_base.p; q.prow = B->p_base.p; q.order = B->p_order.p;
-        q.walk = walk_setting(n) ? B->p_walk.p : nullptr;
-        q.split = plan_split_setting();
+        q.walk = B->cfg.plan_walk ? B->p_walk.p : nullptr;
+        q.split = B->cfg.plan_split ? 1u : 0u;
         q.lds_entries = (lds_entries + 7) & ~7u;
         q.max_agents = max_agents;
-        q.prof = getenv("DTGPU_PLAN_PROF") ? 1u : 0u;
+        q.prof = B->cfg.plan_prof ? 1u : 0u;
         q.docs = B->p_docs.p; q.results = B->p_results.p; q.n_docs = uint32_t(n);
         q.count_only = 1;
         if (launch_plan(q, s) != OK) { DTGPU_HIP_FAILED(hipErrorLaunchFailure); return DTGPU_ERR_HIP; }
@@ -853,7 +890,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     uint64_t lv_total = 0, blk_total = 0, out_total = 0, gidx_total = 0;
     // expected inserted chars per block in the LDS tier (per tracker); DTGPU_LDS_FILL overrides it
     // for experiments (a document that outgrows its LDS index replays on the HBM tier)
-    const uint64_t lds_fill = lds_fill_setting();
+    const uint64_t lds_fill = B->cfg.lds_fill;
     std::vector<int> seg_tier(n, -2);          // replay tier per document (-2: not replayed)
     std::vector<uint32_t> seg_est(n, 0);
     for (size_t i = 0; i < n; i++) {
@@ -901,7 +938,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
         d.content_off = content.size();
         d.content_len = uint32_t(p.log.ins_content.size());
         d.n_aruns = uint32_t(aq);
-        if (!xf && ff_setting() && p.log.graph.entries.size() == 1 && !p.log.ops.empty() && p.log.content_complete) {
+        if (!xf && B->cfg.ff && p.log.graph.entries.size() == 1 && !p.log.ops.empty() && p.log.content_complete) {
             // a linear history: the fast-forward path (dt_ff.hip), out arena only
             B->ff_doc[i] = 1;
             d.flags |= DOC_FF;
@@ -974,8 +1011,8 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     // cut replay: long documents' later LV ranges as documents of their own
     uint64_t pc_total = lv_total, src_total = 0;
     if (!xf) {
-        SegSettings sc = seg_settings();
-        for (uint32_t i : seg_candidates(n, sc, B->n_cu, [&](size_t k) { return seg_tier[k] != -2 ? prep[k].log.ops.size() : 0; })) {
+        SegSettings sc = seg_settings(B->cfg);
+        for (uint32_t i : seg_candidates(n, sc, B->n_cu, B->cfg.seg_fair, [&](size_t k) { return seg_tier[k] != -2 ? prep[k].log.ops.size() : 0; })) {
             SegInput si;
             seg_input_from_log(prep[i].log, si);
             const std::vector<SegCut> cuts = plan_segments(si, sc);
@@ -1031,7 +1068,7 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
     base.mup = B->d_mup.p;
     base.tup = B->d_tup.p;
     base.xf = B->d_xf.p;
-    if (const char *dbg = getenv("DTGPU_DEBUG")) base.debug = uint32_t(atoi(dbg) ? atoi(dbg) : 1);
+    base.debug = B->cfg.debug;
     base.cmds = B->d_cmds.p;
     base.tlist = B->d_tlist.p;
     base.cbyte = B->d_cbyte.p;
@@ -1055,8 +1092,9 @@ dtgpu_status stage(std::vector<Prepared> &prep, const dtgpu_batch_opts *opts, dt
 // replay layout.  The host only reads back per-document counts to size the arenas.  Documents
 // the device path hands back (decoder or prep limits) get status DTGPU_DECODE_DEFER.
 // `dec` is a decoded handle (dtgpu_decode_create: decoded here; dtgpu_decode_add: already merged).
-dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
+dtgpu_status stage_device(dtgpu_decoded *dec, const dtgpu_batch_opts *opts, dtgpu_batch **out) {
     auto B = std::make_unique<dtgpu_batch>();
+    B->cfg = settings_for(opts);
     B->device = dec->device;
     B->dec.reset(dec);
     dtgpu_decoded &Dd = *B->dec;
@@ -1086,7 +1124,7 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     B->docs.assign(n, DocDesc{});
     B->host_planned.assign(n, 0);
     B->ff_doc.assign(n, 0);
-    const bool ff_on = ff_setting();
+    const bool ff_on = B->cfg.ff;
 
     // ---- prep layout ----------------------------------------------------------------------------
     std::vector<PrepDesc> pd(n);
@@ -1139,13 +1177,13 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     pp.par = B->p_par.p; pp.pent = B->p_pent.p; pp.pch = B->p_pch.p; pp.pcnt = B->p_pcnt.p; pp.child = B->p_child.p;
     pp.aruns = B->d_aruns.p; pp.tip = B->p_tip.p; pp.erec = B->p_erec.p; pp.doff = B->p_doff.p; pp.dense = B->p_dense.p;
     pp.rows = B->pr_rows.p; pp.scr = B->pr_scr.p; pp.opc = B->p_opc.p;
-    if (prep_chains_setting(n)) {
+    if (B->cfg.prep_chains) {
         CK(B->pr_chain.alloc(std::max<size_t>(n, 1)));
         pp.chain_flag = B->pr_chain.p;
     }
     pp.docs = B->pr_docs.p; pp.results = B->pr_res.p; pp.n_docs = uint32_t(n); pp.max_entries = max_e;
     // debug mode (DTGPU_DEBUG, or DTGPU_PREP_CHECK alone): the bounds-checked prep kernel
-    pp.check = (getenv("DTGPU_DEBUG") || getenv("DTGPU_PREP_CHECK")) ? 1u : 0u;
+    pp.check = B->cfg.prep_check ? 1u : 0u;
     if (launch_prep(pp, s)) return DTGPU_ERR_HIP;
     std::vector<PrepResult> prr(n);
     CK(hipMemcpyAsync(prr.data(), B->pr_res.p, n * sizeof(PrepResult), hipMemcpyDeviceToHost, s));
@@ -1186,13 +1224,13 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     q.par = B->p_par.p; q.pent = B->p_pent.p; q.pch = B->p_pch.p; q.pcnt = B->p_pcnt.p; q.child = B->p_child.p;
     q.opc = B->p_opc.p; q.aruns = B->d_aruns.p; q.tip = B->p_tip.p; q.erec = B->p_erec.p; q.doff = B->p_doff.p;
     q.dense = B->p_dense.p; q.base = B->p_base.p; q.prow = B->pr_rows.p; q.order = B->p_order.p;
-    q.walk = walk_setting(n) ? B->p_walk.p : nullptr;
+    q.walk = B->cfg.plan_walk ? B->p_walk.p : nullptr;
     q.coff = B->pr_scr.p;
     q.poff = Dd.poff.p;
-    q.split = plan_split_setting();
+    q.split = B->cfg.plan_split ? 1u : 0u;
     q.lds_entries = (lds_entries + 7) & ~7u;
     q.max_agents = max_agents;
-    q.prof = getenv("DTGPU_PLAN_PROF") ? 1u : 0u;
+    q.prof = B->cfg.plan_prof ? 1u : 0u;
     q.docs = B->p_docs.p; q.results = B->p_results.p; q.n_docs = uint32_t(n);
     q.count_only = 1;
     q.todo_cap = 0;
@@ -1220,7 +1258,7 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     stage_prof("stage: planner sizing pass");
     // ---- replay layout ---------------------------------------------------------------------------
     uint64_t cmd_total = 0, tlist_total = 0, blk_total = 0, out_total = 0, gidx_total = 0;
-    const uint64_t lds_fill = lds_fill_setting();
+    const uint64_t lds_fill = B->cfg.lds_fill;
     std::vector<int> seg_tier(n, -2);          // replay tier per document (-2: not replayed)
     std::vector<uint32_t> seg_est(n, 0);
     for (size_t i = 0; i < n; i++) {
@@ -1284,8 +1322,8 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     // cut replay: long documents' later LV ranges as documents of their own
     uint64_t pc_total = lv_total, src_total = 0;
     {
-        SegSettings sc = seg_settings();
-        const std::vector<uint32_t> cand = seg_candidates(n, sc, B->n_cu, [&](size_t k) { return seg_tier[k] != -2 ? Dd.res[k].n_ops : 0u; });
+        SegSettings sc = seg_settings(B->cfg);
+        const std::vector<uint32_t> cand = seg_candidates(n, sc, B->n_cu, B->cfg.seg_fair, [&](size_t k) { return seg_tier[k] != -2 ? Dd.res[k].n_ops : 0u; });
         std::vector<uint8_t> late = late_documents(*B, sc, [&](size_t k) { return Dd.res[k].n_ops; });
         for (uint32_t i : cand) late[i] = 0;
         std::vector<uint32_t> all = cand;
@@ -1413,7 +1451,7 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     stage_prof("stage: arenas + uploads");
 #undef CK
     BatchParams base{};
-    if (const char *dbg = getenv("DTGPU_DEBUG")) base.debug = uint32_t(atoi(dbg) ? atoi(dbg) : 1);
+    base.debug = B->cfg.debug;
     base.cmds = B->d_cmds.p;
     base.tlist = B->d_tlist.p;
     base.cbyte = Dd.cbyte.p;
@@ -1435,7 +1473,7 @@ dtgpu_status stage_device(dtgpu_decoded *dec, dtgpu_batch **out) {
     // start as soon as their own plans are done).  The tier: the critical documents' (DOC_CRITICAL,
     // the batch's longest replays), else the biggest non-empty one.  Its segment documents'
     // documents are planned there too (the main pipeline's replay waits for those plans).
-    if (!getenv("DTGPU_NO_SPLIT")) {
+    if (B->cfg.split) {
         int tb = -1;
         for (int t = kLdsTiers - 1; t >= 1 && tb < 0; t--)
             for (uint32_t d : B->tier_list[t])
@@ -1497,7 +1535,7 @@ int launch_split_side(dtgpu_batch *B, hipStream_t s) {
     // as prep_and_plan: the walk (CSR mode, after prep's first half) on a stream of its own,
     // beside the chain decomposition and prep's second half
     const bool overlap = B->n_gpu_planned && B->prep.chain_flag && !B->prep.check && B->plan.walk && B->plan.coff &&
-                         B->ws_side && !getenv("DTGPU_NO_WALK_OVERLAP");
+                         B->ws_side && B->cfg.walk_overlap;
     if (overlap) {
         pp.short_rec = B->plan.split ? 1u : 0u;
         if (launch_prep_stage(pp, sb, 1)) return ErrHip;
@@ -1554,7 +1592,7 @@ int launch_split_plan(dtgpu_batch *B, hipStream_t s) {
 int prep_and_plan(dtgpu_batch *B, hipStream_t s, hipEvent_t mid) {
     const bool prep = B->dec != nullptr;
     const bool overlap = prep && B->n_gpu_planned && B->prep.chain_flag && !B->prep.check && B->plan.walk &&
-                         B->plan.coff && B->wstream && !getenv("DTGPU_NO_WALK_OVERLAP");
+                         B->plan.coff && B->wstream && B->cfg.walk_overlap;
     if (!overlap) {
         if (prep && launch_prep(B->prep, s)) return ErrHip;
         if (launch_cut(B->cut, s)) return ErrHip;   // (after prep: it reads the parents' entries)
@@ -1964,7 +2002,7 @@ dtgpu_status dtgpu_batch_create_device(const uint8_t *const *docs, const size_t 
     dtgpu_decoded *dh = nullptr;
     const dtgpu_status st = dtgpu_decode_create(docs, lens, n, opts, &dh);
     if (st != DTGPU_OK) return st;
-    return stage_device(dh, out);
+    return stage_device(dh, opts, out);
 }
 
 dtgpu_status dtgpu_batch_create_decoded(dtgpu_decoded *dec, dtgpu_batch **out) {
@@ -1973,7 +2011,7 @@ dtgpu_status dtgpu_batch_create_decoded(dtgpu_decoded *dec, dtgpu_batch **out) {
         dtgpu_decode_free(dec);   // consumed on failure too (dtgpu.h)
         return DTGPU_ERR_HIP;
     }
-    return stage_device(dec, out);
+    return stage_device(dec, nullptr, out);
 }
 dtgpu_status dtgpu_batch_run_e2e_timed(dtgpu_batch *B, float ms[4]) {
     if (!B || !B->dec || B->dec->merged) return DTGPU_ERR_ARG;
@@ -2053,8 +2091,8 @@ dtgpu_status dtgpu_batch_encode(dtgpu_batch *B, uint32_t flags, float *kernel_ms
         // it read from HBM at 9 waves per CU -- occupancy wins in a batch, so staging is opt-in
         q.lds_text = 0;
         (void)max_text;
-        if (const char *e = getenv("DTGPU_ENC_LDS_TEXT")) q.lds_text = std::min<uint32_t>(uint32_t(strtoul(e, nullptr, 10)), 24064);
-        q.prof = getenv("DTGPU_ENC_PROF") ? 1u : 0u;
+        q.lds_text = B->cfg.enc_lds_text;
+        q.prof = B->cfg.enc_prof ? 1u : 0u;
         for (int k = 0; k < 32; k++) q.x2n[k] = Dd.P.x2n[k];
     }
     // the walk order: the planner's commands (prep + plan, as a checkout pass runs them), for

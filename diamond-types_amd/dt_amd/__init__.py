@@ -44,7 +44,15 @@ class DocResult(ctypes.Structure):
 
 
 class BatchOpts(ctypes.Structure):
-    _fields_ = [("ignore_crc", ctypes.c_int), ("host_threads", ctypes.c_int), ("device", ctypes.c_int)]
+    """dtgpu_batch_opts (include/dtgpu.h): flags = DTGPU_OPT_* (OPT_* below); seg_ops / seg_max /
+    lds_fill 0 = defaults.  DTGPU_* environment variables override them at batch creation."""
+    _fields_ = [("ignore_crc", ctypes.c_int), ("host_threads", ctypes.c_int), ("device", ctypes.c_int),
+                ("flags", ctypes.c_uint32), ("seg_ops", ctypes.c_uint32), ("seg_max", ctypes.c_uint32),
+                ("lds_fill", ctypes.c_uint32)]
+
+
+OPT_NO_FAST_FORWARD, OPT_NO_SEGMENTS, OPT_HOST_PLAN, OPT_NO_SPLIT, OPT_NO_CRITICAL, OPT_DEBUG, OPT_PASS_MARK = \
+    1, 2, 4, 8, 16, 32, 64
 
 
 class GraphQuery(ctypes.Structure):
@@ -692,11 +700,13 @@ class Batch:
     (dt_replay.hip) always run on the GPU."""
 
     def __init__(self, docs=None, oplogs=None, ignore_crc=False, host_threads=0, device=0, staging="host",
-                 xf=False):
+                 xf=False, flags=0, seg_ops=0, seg_max=0, lds_fill=0):
         """xf=True (with oplogs): a transformed-ops batch, every document's iter_xf_operations()
-        computed by the replay (dtgpu_batch_create_xf); read it with xf_positions(i)."""
+        computed by the replay (dtgpu_batch_create_xf); read it with xf_positions(i).  flags
+        (OPT_*), seg_ops, seg_max, lds_fill: dtgpu_batch_opts."""
         L = lib()
-        opts = BatchOpts(int(ignore_crc), int(host_threads), int(device))
+        opts = BatchOpts(int(ignore_crc), int(host_threads), int(device), int(flags), int(seg_ops), int(seg_max),
+                         int(lds_fill))
         out = ctypes.c_void_p()
         if oplogs is not None:
             arr = (ctypes.c_void_p * max(1, len(oplogs)))(*[o._h for o in oplogs])

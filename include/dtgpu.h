@@ -226,7 +226,20 @@ typedef struct dtgpu_batch_opts {
     int ignore_crc;          /* DecodeOptions::ignore_crc */
     int host_threads;        /* decode/plan worker threads, 0 = hardware concurrency */
     int device;              /* HIP device ordinal */
+    /* How the batch checks out (0 everywhere = the defaults).  The DTGPU_* environment variables
+     * of the same names override these at batch creation, for experiments and A/B runs only. */
+    uint32_t flags;          /* DTGPU_OPT_* below */
+    uint32_t seg_ops;        /* cut replay: op runs per segment (0: 500, raised to the batch's fair share) */
+    uint32_t seg_max;        /* cut replay: segments per document, <= 64 (0: 32) */
+    uint32_t lds_fill;       /* expected chars per 64-slot block when sizing LDS indexes (0: 40) */
 } dtgpu_batch_opts;
+#define DTGPU_OPT_NO_FAST_FORWARD 1u   /* linear histories on the tracker, not dt_ff.hip (DTGPU_FF=0) */
+#define DTGPU_OPT_NO_SEGMENTS 2u       /* no cut replay: long documents on one wave (DTGPU_SEG=0) */
+#define DTGPU_OPT_HOST_PLAN 4u         /* walk plans built on the host (DTGPU_HOST_PLAN) */
+#define DTGPU_OPT_NO_SPLIT 8u          /* no split pass for skewed batches (DTGPU_NO_SPLIT) */
+#define DTGPU_OPT_NO_CRITICAL 16u      /* no critical-replay priority (DTGPU_CRITICAL=0) */
+#define DTGPU_OPT_DEBUG 32u            /* invariant checks after every replay command (DTGPU_DEBUG=1) */
+#define DTGPU_OPT_PASS_MARK 64u        /* every pass opens with a marker kernel (DTGPU_PASS_MARK) */
 
 typedef struct dtgpu_doc_result {
     uint32_t status;         /* dtgpu_status of this document */

@@ -173,3 +173,19 @@ def test_host_staged_and_checkout_tip(traces):
     check(b, want)
     for d, w in zip(docs, want):
         assert dt_amd.ListOpLog.load_from(d).checkout_tip_bytes() == w
+
+
+def test_batch_opts_select_the_path(traces):
+    """dtgpu_batch_opts carries the knobs (DTGPU_OPT_*): the same as the environment overrides."""
+    docs = [d for _, d, _ in traces]
+    want = [w for _, _, w in traces]
+    b = dt_amd.Batch(docs=docs, staging="device", flags=dt_amd.OPT_NO_FAST_FORWARD)
+    assert b.fast_forwarded() == [0] * len(docs)
+    b.run()
+    b.sync()
+    check(b, want)
+    b = dt_amd.Batch(docs=docs, staging="device", flags=dt_amd.OPT_NO_FAST_FORWARD | dt_amd.OPT_NO_SEGMENTS)
+    b.run()
+    b.sync()
+    check(b, want)
+    assert all(b.segments(i) == [] for i in range(len(docs)))
