@@ -193,7 +193,9 @@ DEV uint32_t last_at_or_before(const uint4 *A, uint32_t n, uint32_t x) {
     return lo;
 }
 
-constexpr uint32_t CT = 256;   // compose threads
+// CT threads per pair: one wave for the low levels (a pair of <= 4 segments' pieces is one or
+// a few rounds), four for the rest
+template <uint32_t CT>
 __global__ __launch_bounds__(CT) void ff_compose_kernel(FFParams P, uint32_t level, const uint4 *in, uint4 *out,
                                                         const uint32_t *cin, uint32_t *cout) {
     __shared__ uint32_t s_ex[CT + 1], s_i0[CT], s_w[CT / 64 + 1];
@@ -397,7 +399,8 @@ int launch_ff(const FFParams &p, void *stream) {
     uint32_t *ca = p.ca, *cb = p.cb;
     for (uint32_t k = 0; k < p.n_levels; k++) {
         const uint32_t np = p.level_off[k + 1] - p.level_off[k];
-        if (np) hipLaunchKernelGGL(ff::ff_compose_kernel, dim3(np), dim3(ff::CT), 0, s, p, k, a, b, ca, cb);
+        if (np && k < 2) hipLaunchKernelGGL(ff::ff_compose_kernel<64>, dim3(np), dim3(64), 0, s, p, k, a, b, ca, cb);
+        else if (np) hipLaunchKernelGGL(ff::ff_compose_kernel<256>, dim3(np), dim3(256), 0, s, p, k, a, b, ca, cb);
         std::swap(a, b);
         std::swap(ca, cb);
     }

@@ -22,6 +22,10 @@ done > "$OUT/kbench.log" 2>&1
 cat "$OUT/kbench.log"
 timeout -k 10 300 python -u bench.py --workload mixed --docs 400 --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/mixed.json" 2> "$OUT/mixed.err" || exit 1
 head -c 400 "$OUT/mixed.json"; echo
+bash tools/bench_profile.sh "$OUT/lin" --workload linear --docs 2000 --steps 10 --warmup 2 || exit 1
+head -c 400 "$OUT/lin/bench.json"; echo
+DTGPU_STAGE_PROF=1 timeout -k 10 200 python -u tools/stage_probe.py friendsforever 10000 > "$OUT/stage_probe.log" 2>&1 || exit 1
+tail -1 "$OUT/stage_probe.log"
 timeout -k 10 500 python -u bench.py --workload synth --distinct 65536 --docs 125000 --steps 3 --warmup 1 --no-cpu-baseline --no-decode --no-encode > "$OUT/synth_125k.json" 2> "$OUT/synth_125k.err" || exit 1
 head -c 400 "$OUT/synth_125k.json"; echo
 echo done
