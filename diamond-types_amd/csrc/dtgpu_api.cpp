@@ -2275,6 +2275,11 @@ dtgpu_status dtgpu_batch_plan(dtgpu_batch *B, size_t i, uint32_t *cmds, size_t c
                               size_t tlist_cap, size_t *n_cmds, size_t *n_tlist) {
     if (!B || i >= B->n) return DTGPU_ERR_ARG;
     if (B->host_status[i] != OK) return dtgpu_status(B->host_status[i]);
+    if (i < B->ff_doc.size() && B->ff_doc[i]) {   // fast-forwarded: a checkout pass plans no walk for it
+        if (n_cmds) *n_cmds = 0;
+        if (n_tlist) *n_tlist = 0;
+        return DTGPU_OK;
+    }
     const DocDesc &d = B->docs[i];
     std::vector<Cmd> c(d.ncmd);
     if (d.ncmd && hipMemcpyAsync(c.data(), B->d_cmds.p + d.cmd_off, d.ncmd * sizeof(Cmd), hipMemcpyDeviceToHost, B->stream) != hipSuccess)

@@ -287,7 +287,8 @@ size_t dtgpu_batch_host_planned(const dtgpu_batch *batch, uint8_t *flags, size_t
 size_t dtgpu_batch_fast_forwarded(const dtgpu_batch *batch, uint8_t *flags, size_t cap);
 /* The command stream of document `doc` as last planned (16-byte commands as uint32 quads
  * {op, lv, len, pos}; TOG commands index the retreat/advance entries copied to tlist).
- * NULL buffers query the sizes. */
+ * NULL buffers query the sizes.  A fast-forwarded document (dtgpu_batch_fast_forwarded) has no
+ * walk plan in a checkout pass: 0 commands. */
 dtgpu_status dtgpu_batch_plan(dtgpu_batch *batch, size_t doc, uint32_t *cmds, size_t cmd_cap, uint32_t *tlist,
                               size_t tlist_cap, size_t *n_cmds, size_t *n_tlist);
 /* Copy per-document results (n_docs entries) to host. */
