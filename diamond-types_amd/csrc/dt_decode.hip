@@ -56,6 +56,21 @@ __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 __device__ __forceinline__ uint64_t lt_mask() { return (1ull << lane()) - 1ull; }
 __device__ __forceinline__ uint32_t popc(uint64_t m) { return uint32_t(__popcll(m)); }
 __device__ __forceinline__ uint32_t ctz(uint64_t m) { return uint32_t(__ffsll((unsigned long long)m) - 1); }
+// Inclusive prefix sum over the wave (all lanes active): row_shr 1, 2, 4, 8 scan each row of 16
+// lanes, row_bcast 15 adds row 0's total to row 1 and row 2's to row 3, row_bcast 31 adds rows
+// 0-1's total to rows 2 and 3 -- six DPP adds instead of six dependent LDS permutes.
+__device__ __forceinline__ uint32_t scan_incl(uint32_t v) {
+    v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x111, 0xf, 0xf, false));   // row_shr:1
+    v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x112, 0xf, 0xf, false));   // row_shr:2
+    v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x114, 0xf, 0xf, false));   // row_shr:4
+    v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x118, 0xf, 0xf, false));   // row_shr:8
+    v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x142, 0xa, 0xf, false));   // row_bcast:15
+    v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x143, 0xc, 0xf, false));   // row_bcast:31
+    return v;
+}
+// LDS stores of this wave become visible to its lanes' later LDS loads (a wave's LDS operations
+// complete in order; this only keeps the compiler from reordering them).
+__device__ __forceinline__ void wave_lds_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 // Stores of this wave become visible to its later loads (same CU; workgroup scope).
 __device__ __forceinline__ void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
 
@@ -390,42 +405,94 @@ __device__ __forceinline__ uint32_t crc32c_par(const uint8_t *s, uint32_t n, con
 // its byte k repeats byte k mod offset, so one hop leaves the match; every hop lands in an
 // earlier sequence, so at most 64 hops), and the bytes are copied wave-wide, one gather load and
 // one store per lane per 64 bytes, instead of a dependent load round trip per sequence.
-__device__ __forceinline__ bool lz4_block(Ctx &C, const Rd &src, uint8_t *dst, uint32_t out_len) {
+__device__ __forceinline__ bool lz4_block(Ctx &C, const Rd &src, uint8_t *dst, uint32_t out_len, uint4 *lzm,
+                                          uint32_t *parse_cycles = nullptr) {
     const uint8_t *sp = C.in + src.p;
     const uint32_t n = src.n;
     uint32_t ip = 0, op = 0;
+    uint32_t steps = 0, step_at = 1u;   // the token-step table and the window it was built for
     bool end = n == 0;
     while (!end) {
         // ---- parse up to 64 sequences (uniform) ----
         uint32_t so = 0xFFFFFFFFu, slit = 0, ssrc = 0, soff = 0, sml = 0;   // lane j: sequence j
         const uint32_t bs = op;
         uint32_t ns = 0;
+#ifdef DT_LZPROF
+        const uint64_t t_parse = __builtin_amdgcn_s_memtime();
+#endif
         while (ns < 64 && !end) {
-            {   // the common sequence: no length bytes, a match follows the literals (one-byte
-                // length extensions measured slower: more issue per sequence than they save)
+            {   // sequences whose lengths take at most one extension byte each, found by walking
+                // a per-window table of token steps: lane l holds, for the window's bytes
+                // 4l .. 4l+3 read as tokens, the distance to the next token (0 where that sequence
+                // would have a longer length, no match, or cross the window or the block end).
+                // The walk records each token's window offset in the next free lane; those lanes
+                // then decode their sequences at once, and the reader's checks cut the run at the
+                // first sequence failing one (the exact path below re-reads it).
                 const uint32_t pos = src.p + ip;
                 Win &W = C.w0;
-                if (pos - W.wpos + 20u > 256u) {   // one window covers the token, literals and offset
+                if (pos - W.wpos + 20u > 256u) {
                     W.wpos = pos & ~3u;
                     W.w = *reinterpret_cast<const uint32_t *>(W.base + W.wpos + 4u * lane());
                 }
-                const uint32_t d = pos - W.wpos;
-                const uint32_t tok = (rdl(W.w, d >> 2) >> ((d & 3u) << 3)) & 0xFFu;
-                const uint32_t lit = tok >> 4, ml = (tok & 15u) + 4u;
-                const uint32_t e = d + 1u + lit;   // the offset's two bytes (e + 2 <= d + 18 <= 254)
-                const uint64_t pr = uint64_t(rdl(W.w, e >> 2)) | (uint64_t(rdl(W.w, min((e >> 2) + 1u, 63u))) << 32);
-                const uint32_t off = uint32_t(pr >> ((e & 3u) << 3)) & 0xFFFFu;
-                const uint32_t ms = op + lit;   // the match's output start
-                if (lit < 15u && ml < 19u && ip + 3u + lit <= n && off != 0 && off <= ms &&
-                    uint64_t(ms) + ml <= out_len) {
-                    const bool me = lane() == ns;
-                    so = me ? op : so; slit = me ? lit : slit; ssrc = me ? ip + 1u : ssrc;
-                    soff = me ? off : soff; sml = me ? ml : sml;
-                    ns++;
-                    ip += 3u + lit;
-                    op = ms + ml;
-                    end = ip >= n;
-                    continue;
+                if (step_at != W.wpos) {
+                    step_at = W.wpos;
+                    const uint32_t lim = src.p + n - W.wpos;   // the block end, window-relative
+                    const uint32_t wn = uint32_t(__shfl(int(W.w), int(min(lane() + 1u, 63u))));
+                    const uint64_t w2 = uint64_t(W.w) | (uint64_t(wn) << 32);
+                    steps = 0;
+#pragma unroll
+                    for (uint32_t j = 0; j < 4; j++) {
+                        const uint32_t c = 4u * lane() + j;
+                        const uint32_t tok = uint32_t(w2 >> (8u * j)) & 0xFFu, b1 = uint32_t(w2 >> (8u * j + 8u)) & 0xFFu;
+                        const uint32_t le = (tok >> 4) == 15u, me = (tok & 15u) == 15u;
+                        const uint32_t lit = le ? 15u + b1 : tok >> 4;
+                        const uint32_t mp = c + 3u + le + lit;   // the match length's extension byte
+                        const uint32_t b2 = (uint32_t(__shfl(int(W.w), int(min(mp >> 2, 63u)))) >> ((mp & 3u) << 3)) & 0xFFu;
+                        const uint32_t st = 3u + le + lit + me;
+                        const bool ok = (!le || b1 < 255u) && (!me || b2 < 255u) && c + st <= 255u && c + st <= lim;
+                        steps |= (ok ? st : 0u) << (8u * j);
+                    }
+                }
+                uint32_t d = pos - W.wpos, cnt = 0, at = 0;
+                const uint32_t cap = 64u - ns;
+                while (cnt < cap) {   // uniform
+                    const uint32_t st = (rdl(steps, d >> 2) >> ((d & 3u) << 3)) & 0xFFu;
+                    if (!st) break;
+                    at = lane() == ns + cnt ? d : at;
+                    cnt++;
+                    d += st;
+                }
+                if (cnt) {
+                    const bool mine = lane() - ns < cnt;   // lanes ns .. ns + cnt - 1
+                    const uint32_t t0 = uint32_t(__shfl(int(W.w), int(at >> 2)));
+                    const uint32_t t1 = uint32_t(__shfl(int(W.w), int(min((at >> 2) + 1u, 63u))));
+                    const uint32_t x = uint32_t((uint64_t(t0) | (uint64_t(t1) << 32)) >> ((at & 3u) << 3));
+                    const uint32_t tok = x & 0xFFu;
+                    const uint32_t le = (tok >> 4) == 15u, me = (tok & 15u) == 15u;
+                    const uint32_t lit = le ? 15u + ((x >> 8) & 0xFFu) : tok >> 4;
+                    const uint32_t e = at + 1u + le + lit;   // the offset's two bytes, then the extension
+                    const uint32_t e0 = uint32_t(__shfl(int(W.w), int(e >> 2)));
+                    const uint32_t e1 = uint32_t(__shfl(int(W.w), int(min((e >> 2) + 1u, 63u))));
+                    const uint32_t y = uint32_t((uint64_t(e0) | (uint64_t(e1) << 32)) >> ((e & 3u) << 3));
+                    const uint32_t off = y & 0xFFFFu;
+                    const uint32_t ml = me ? 19u + ((y >> 16) & 0xFFu) : (tok & 15u) + 4u;
+                    const uint32_t len = mine ? lit + ml : 0u;
+                    const uint32_t incl = scan_incl(len);
+                    const uint32_t o0 = op + incl - len, ms = o0 + lit;   // output start, match start
+                    const uint64_t bm = ballot(mine && (off == 0 || off > ms || uint64_t(ms) + ml > out_len));
+                    if (bm) cnt = ctz(bm) - ns;
+                    if (cnt) {
+                        const bool take = lane() - ns < cnt;
+                        so = take ? o0 : so; slit = take ? lit : slit;
+                        ssrc = take ? W.wpos + at - src.p + 1u + le : ssrc;
+                        soff = take ? off : soff; sml = take ? ml : sml;
+                        const uint32_t last = ns + cnt - 1u;
+                        ip = W.wpos + rdl(e, last) - src.p + 2u + rdl(me, last);
+                        op += rdl(incl, last);
+                        ns += cnt;
+                        end = ip >= n;
+                        continue;
+                    }
                 }
             }
             const uint32_t tok = C.byte(0, src.p + ip++);
@@ -469,31 +536,74 @@ __device__ __forceinline__ bool lz4_block(Ctx &C, const Rd &src, uint8_t *dst, u
             soff = me ? off : soff; sml = me ? ml : sml;
             ns++;
         }
-        // ---- resolve and copy the batch's output bytes [bs, op) ----
-        for (uint32_t g = bs; g < op; g += 64) {   // uniform
-            const uint32_t p = g + lane();
-            uint32_t cur = p, from = 0;
-            bool inp = false, done = p >= op;
-            while (ballot(!done)) {
-                uint32_t r = 0;
+#ifdef DT_LZPROF
+        if (parse_cycles) *parse_cycles += uint32_t(__builtin_amdgcn_s_memtime() - t_parse);
+#endif
+        // ---- resolve and copy the batch's output bytes [bs, op), CU rounds of 64 at a time ----
+        // (every source lies in the input or before bs, so a group's loads all issue before its
+        // stores: one memory round trip per group, not per round).  A batch of at most 4 KB of
+        // output finds the sequence holding a byte in one LDS read: word w of lzm holds the
+        // sequence starts among bytes bs + 64w .. + 63 as a bit mask and the starts before them;
+        // a larger batch bisects the lanes' starts.
+        const uint32_t nw = (op - bs + 63u) >> 6;
+        const bool mapped = nw <= 64u;   // uniform
+        if (mapped) {
+            if (lane() < nw) lzm[lane()] = make_uint4(0u, 0u, 0u, 0u);
+            wave_lds_fence();
+            const uint32_t rel = so - bs;
+            if (lane() < ns && rel < op - bs)
+                atomicOr(reinterpret_cast<uint32_t *>(&lzm[rel >> 6]) + ((rel >> 5) & 1u), 1u << (rel & 31u));
+            wave_lds_fence();
+            const uint4 wv = lzm[lane()];
+            const uint32_t c = lane() < nw ? uint32_t(__popc(wv.x) + __popc(wv.y)) : 0u;
+            const uint32_t inc = scan_incl(c);
+            if (lane() < nw) lzm[lane()].z = inc - c;
+            wave_lds_fence();
+        }
+        constexpr uint32_t CU = 8;
+        for (uint32_t g0 = bs; g0 < op; g0 += 64u * CU) {   // uniform
+            uint32_t fr[CU], inm = 0;   // per round: the source offset; bit u: it is an input byte
 #pragma unroll
-                for (uint32_t st = 32; st >= 1; st >>= 1)
-                    if (uint32_t(__shfl(int(so), int(r + st))) <= cur) r += st;
-                const uint32_t o0 = uint32_t(__shfl(int(so), int(r))), lit = uint32_t(__shfl(int(slit), int(r)));
-                const uint32_t ls = uint32_t(__shfl(int(ssrc), int(r))), off = uint32_t(__shfl(int(soff), int(r)));
-                const uint32_t ml = uint32_t(__shfl(int(sml), int(r)));
-                if (!done) {
-                    const uint32_t k = cur - o0;
-                    if (k < lit) {
-                        from = ls + k; inp = true; done = true;
+            for (uint32_t u = 0; u < CU; u++) {
+                const uint32_t p = g0 + 64u * u + lane();
+                uint32_t cur = p, from = 0;
+                bool inp = false, done = p >= op;
+                while (ballot(!done)) {
+                    uint32_t r = 0;
+                    if (mapped) {
+                        const uint32_t rl = cur - bs;
+                        const uint4 m = lzm[min(rl >> 6, 63u)];
+                        const uint64_t bits = ((uint64_t(m.y) << 32) | m.x) & (~0ull >> (63u - (rl & 63u)));
+                        r = m.z + popc(bits) - 1u;
                     } else {
-                        const uint32_t m = k - lit;
-                        const uint32_t q = o0 + lit - off + (off < ml ? m % off : m);
-                        if (q < bs) { from = q; done = true; } else cur = q;
+#pragma unroll
+                        for (uint32_t st = 32; st >= 1; st >>= 1)
+                            if (uint32_t(__shfl(int(so), int(r + st))) <= cur) r += st;
+                    }
+                    const uint32_t o0 = uint32_t(__shfl(int(so), int(r))), lit = uint32_t(__shfl(int(slit), int(r)));
+                    const uint32_t ls = uint32_t(__shfl(int(ssrc), int(r))), off = uint32_t(__shfl(int(soff), int(r)));
+                    const uint32_t ml = uint32_t(__shfl(int(sml), int(r)));
+                    if (!done) {
+                        const uint32_t k = cur - o0;
+                        if (k < lit) {
+                            from = ls + k; inp = true; done = true;
+                        } else {
+                            const uint32_t m = k - lit;
+                            const uint32_t q = o0 + lit - off + (off < ml ? m % off : m);
+                            if (q < bs) { from = q; done = true; } else cur = q;
+                        }
                     }
                 }
+                fr[u] = from;
+                inm |= uint32_t(inp) << u;
             }
-            if (p < op) dst[p] = inp ? sp[from] : dst[from];
+            uint32_t v[CU];
+#pragma unroll
+            for (uint32_t u = 0; u < CU; u++)
+                v[u] = g0 + 64u * u + lane() >= op ? 0u : ((inm >> u) & 1u) ? sp[fr[u]] : dst[fr[u]];
+#pragma unroll
+            for (uint32_t u = 0; u < CU; u++)
+                if (g0 + 64u * u + lane() < op) dst[g0 + 64u * u + lane()] = uint8_t(v[u]);
         }
         wave_fence();   // the next batch reads these bytes
     }
@@ -512,7 +622,7 @@ struct Lds {                 // per-wave tables, F = max file agents of the batc
     uint32_t *amono;         // agent id -> 1 if its runs' seq ranges increase in LV order
     uint32_t *crc;           // CRC-32C table (256)
     uint32_t *fr;            // frontier compaction scratch (64)
-    uint32_t *vq;            // varint queue compaction scratch (192)
+    uint32_t *vq;            // varint queue compaction scratch (192); fr + vq: the LZ4 byte map (1 KB)
 };
 
 struct CRuns {               // ContentIsKnown run iterator (ReadPatchContentIter)
@@ -690,15 +800,6 @@ __device__ __forceinline__ int64_t lookup_lv(const Out &O, const Lds &L, uint32_
 // per-LV offsets.
 // Anything unusual -- including any error -- returns status 1 and decode_doc re-decodes along the
 // exact piecewise path, which yields the reference's status.
-
-__device__ __forceinline__ uint32_t scan_incl(uint32_t v) {   // inclusive prefix sum over the wave
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = uint32_t(__shfl_up(int(v), d));
-        if (lane() >= uint32_t(d)) v += o;
-    }
-    return v;
-}
 
 // Up to 64 OpTypeAndPosition records at once (the fast path's common case): the queued varints'
 // roles (record head or a head's diff) by a prefix composition, each record's cursor and LV by
@@ -1428,7 +1529,12 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
                 R.lz_len = uint32_t(ulen);
             } else {
                 if (ulen > D.lz_cap) return ErrCapacity;
-                if (!lz4_block(C, c, C.lz, uint32_t(ulen))) return LZ4DecompressionError;
+#ifdef DT_LZPROF
+                if (!lz4_block(C, c, C.lz, uint32_t(ulen), reinterpret_cast<uint4 *>(L.fr), &R.prof[7]))
+                    return LZ4DecompressionError;
+#else
+                if (!lz4_block(C, c, C.lz, uint32_t(ulen), reinterpret_cast<uint4 *>(L.fr))) return LZ4DecompressionError;
+#endif
             }
             comp.n = uint32_t(ulen);
             has_comp = true;
@@ -1611,7 +1717,9 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
             }
         }
         if (fo.status == 0) {
+#ifndef DT_LZPROF
             R.prof[7] += uint32_t(fo.t_mid - t_runs);   // the agent-assignment half of the fast path
+#endif
             qa.at = fo.n_aruns;
             qp.at = fo.n_pre;
             n_lv = next_assign = fo.n_lv;
@@ -2262,7 +2370,7 @@ __device__ __forceinline__ int add_doc(const AddParams &P, const AddDesc &D, Dec
             if (ulen > (uint64_t(1) << 34)) return LZ4DecompressionError;
             if (ulen > 255ull * c.n + 64) return LZ4DecompressionError;
             if (ulen > D.lz_cap) return ErrCapacity;
-            if (!lz4_block(C, c, C.lz, uint32_t(ulen))) return LZ4DecompressionError;
+            if (!lz4_block(C, c, C.lz, uint32_t(ulen), reinterpret_cast<uint4 *>(L.fr))) return LZ4DecompressionError;
             comp.n = uint32_t(ulen);
             has_comp = true;
         }
