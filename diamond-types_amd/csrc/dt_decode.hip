@@ -792,6 +792,70 @@ __device__ __forceinline__ int64_t lookup_lv(const Out &O, const Lds &L, uint32_
     return int64_t(fl) + int64_t(seq - fs);
 }
 
+// ---- UTF-8 insert text with few multi-byte chars ------------------------------------------------
+// The byte offset of char k of a text is k plus the continuation bytes before the char's start.
+// With at most 64 continuation bytes in the text they fit one register: lane e holds, for the e-th
+// continuation byte (at byte p, e of them before it), t_e = p - e, the index of the first char
+// starting after it -- so char k's offset is k + |{e : t_e <= k}|.  The fast path writes byte
+// offsets straight away with it (no per-LV pass afterwards); a text with more continuation bytes
+// takes utf8_offsets below.
+struct Utf8Tab { uint32_t t, n; };   // lane e: t_e (n <= 64 entries, uniform)
+
+// One pass over the text, 16 B per lane (aligned blocks: each holds a text byte, so the load
+// stays inside the text's page).  Returns false with more than 64 continuation bytes.
+__device__ __forceinline__ bool utf8_table(const uint8_t *txt, uint32_t n, Utf8Tab &tab, uint32_t &n_chars) {
+    __shared__ uint32_t ent[64];
+    const uintptr_t a0 = reinterpret_cast<uintptr_t>(txt) & ~uintptr_t(15);
+    const uint32_t head = uint32_t(reinterpret_cast<uintptr_t>(txt) - a0), span = head + n;
+    uint32_t conts = 0;   // uniform: continuation bytes before the current stride
+    for (uint32_t b = 0; b < span; b += 1024) {
+        const uint32_t o = b + 16u * lane();   // block offset from a0
+        uint4 w = make_uint4(0u, 0u, 0u, 0u);
+        if (o < span) w = *reinterpret_cast<const uint4 *>(a0 + o);
+        uint32_t cm[4];
+        uint32_t nc = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) {
+            const uint32_t x = q == 0 ? w.x : q == 1 ? w.y : q == 2 ? w.z : w.w;
+            uint32_t m = x & ~(x << 1) & 0x80808080u;   // bytes 10xxxxxx
+#pragma unroll
+            for (uint32_t k = 0; k < 4; k++) {   // keep the text's own bytes only
+                const uint32_t off = o + 4u * q + k;
+                if (off < head || off >= span) m &= ~(0x80u << (8u * k));
+            }
+            cm[q] = m;
+            nc += uint32_t(__popc(m));
+        }
+        const uint32_t incl = scan_incl(nc);
+        const uint32_t tot = rdl(incl, 63);
+        if (conts + tot > 64u) return false;
+        if (nc) {   // rare: record this block's continuation bytes at their ranks
+            uint32_t e = conts + incl - nc;
+            for (uint32_t q = 0; q < 4; q++)
+                for (uint32_t m = cm[q]; m; m &= m - 1) {
+                    const uint32_t p = o + 4u * q + (uint32_t(__ffs(int(m)) - 1) >> 3) - head;
+                    ent[e] = p - e;
+                    e++;
+                }
+        }
+        conts += tot;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    tab.n = conts;
+    tab.t = lane() < conts ? ent[lane()] : 0xFFFFFFFFu;
+    n_chars = n - conts;
+    return true;
+}
+// byte offsets of the lanes' char indices k, all within [kmin, kmax] (uniform; all lanes active)
+__device__ __forceinline__ uint32_t utf8_xlat(const Utf8Tab &tab, uint32_t k, uint32_t kmin, uint32_t kmax) {
+    uint32_t v = k + popc(ballot(lane() < tab.n && tab.t <= kmin));
+    for (uint64_t m = ballot(lane() < tab.n && tab.t > kmin && tab.t <= kmax); m; m &= m - 1)
+        if (k >= rdl(tab.t, ctz(m))) v++;
+    return v;
+}
+
 // ---- decode fast path ---------------------------------------------------------------------------
 // The common case: the insert text is ASCII and covered by known runs, there is no deleted
 // content (every benchmark file).  Pieces are then the op records split at agent-run boundaries
@@ -813,7 +877,7 @@ __device__ __forceinline__ bool batch_records(VQ &q, const uint32_t *bnd, uint32
                                               uint32_t total, uint32_t &ins_size, int64_t &last_cursor,
                                               uint32_t &cr_valid, uint32_t &cr_lv, uint32_t &cr_len, uint32_t &cr_pos,
                                               uint32_t &cr_kind, uint32_t &cr_fwd, Quads &qp, uint4 *pre_out,
-                                              uint32_t pre_cap, uint32_t *cbyte) {
+                                              uint32_t pre_cap, uint32_t *cbyte, const Utf8Tab &tab) {
     const uint32_t l = lane();
     const uint32_t h0 = q.head, cnt = q.cnt;
     const bool inq = l >= h0 && l < cnt;
@@ -891,15 +955,33 @@ __device__ __forceinline__ bool batch_records(VQ &q, const uint32_t *bnd, uint32
         const uint32_t tot = rdl(lincl, 63);
         const uint32_t vk = ins_size + iincl - ilen - (lincl - L);   // content byte = vk + LV offset
         const bool dk = rec && is_del;
-        for (uint32_t b = 0; b < tot; b += 64) {   // uniform: every lane runs the shuffles
+        if (tot >= 16u * popc(hm)) {   // long records: one wave-wide fill per record
+            for (uint64_t m = hm; m; m &= m - 1) {   // uniform
+                const uint32_t i = ctz(m);
+                const uint32_t li = rdl(L, i), j0 = rdl(lincl, i) - li, vi = rdl(vk, i) + j0;
+                const bool di = rdl(uint32_t(dk), i) != 0;
+                if (di || !tab.n) {
+                    for (uint32_t k = l; k < li; k += 64) cbyte[lv + j0 + k] = di ? 0xFFFFFFFFu : vi + k;
+                } else {
+                    for (uint32_t k0 = 0; k0 < li; k0 += 64) {   // uniform
+                        const uint32_t v = utf8_xlat(tab, vi + k0 + l, vi + k0, vi + min(k0 + 63u, li - 1u));
+                        if (k0 + l < li) cbyte[lv + j0 + k0 + l] = v;
+                    }
+                }
+            }
+        } else for (uint32_t b = 0; b < tot; b += 64) {   // uniform: every lane runs the shuffles
             const uint32_t j = b + l;
             uint32_t r = 0;
 #pragma unroll
             for (uint32_t s = 32; s >= 1; s >>= 1)
                 if (uint32_t(__shfl(int(lincl), int(r + s - 1))) <= j) r += s;
-            const uint32_t v = uint32_t(__shfl(int(vk), int(r)));
+            uint32_t v = uint32_t(__shfl(int(vk), int(r))) + j;
             const bool d = __shfl(int(dk), int(r)) != 0;
-            if (j < tot) cbyte[lv + j] = d ? 0xFFFFFFFFu : v + j;
+            if (tab.n) {   // the inserted chars of these LVs are numbered consecutively
+                const uint64_t im = ballot(j < tot && !d);
+                if (im) v = utf8_xlat(tab, v, rdl(v, ctz(im)), rdl(v, 63u - uint32_t(__clzll((long long)im))));
+            }
+            if (j < tot) cbyte[lv + j] = d ? 0xFFFFFFFFu : v;
         }
     }
     // RLE merge of the records into op runs
@@ -1324,7 +1406,7 @@ __device__ __forceinline__ bool utf8_offsets(const uint8_t *t, uint32_t n, uint3
 __device__ __forceinline__ FastOut fast_runs(VQ qav, VQ qtp, VQ runs, uint32_t text_n, uint32_t n_file, uint32_t *fseq,
                                           const uint32_t *fmap, uint32_t *vs, uint4 *aruns_out, uint4 *pre_out,
                                           uint32_t *cbyte, uint32_t *bnd, uint32_t arun_cap, uint32_t pre_cap,
-                                          uint32_t lv_cap) {
+                                          uint32_t lv_cap, const Utf8Tab &tab) {
     FastOut fo{1, 0, 0, 0, 0, 0};
     uint64_t ins_total = 0;
     while (runs.left()) {
@@ -1387,7 +1469,7 @@ __device__ __forceinline__ FastOut fast_runs(VQ qav, VQ qtp, VQ runs, uint32_t t
         if (!qtp.left()) return fo;
         if (qtp.head == qtp.cnt) vq_refill(qtp, vs);
         if (qtp.cnt - qtp.head >= 8 && batch_records(qtp, bnd, nb, bi, lv, total, ins_size, last_cursor, cr_valid, cr_lv,
-                                                     cr_len, cr_pos, cr_kind, cr_fwd, qp, pre_out, pre_cap, cbyte)) {
+                                                     cr_len, cr_pos, cr_kind, cr_fwd, qp, pre_out, pre_cap, cbyte, tab)) {
             bblk = 0xFFFFFFFFu;   // bi moved: the cached boundary window is stale
             continue;
         }
@@ -1431,7 +1513,15 @@ __device__ __forceinline__ FastOut fast_runs(VQ qav, VQ qtp, VQ runs, uint32_t t
             const uint32_t pos = uint32_t(ppos);
             bool merged = false;
             if (!is_del) {
-                for (uint32_t i = lane(); i < take; i += 64) cbyte[lv + i] = ins_size + i;
+                if (!tab.n) {
+                    for (uint32_t i = lane(); i < take; i += 64) cbyte[lv + i] = ins_size + i;
+                } else {
+                    for (uint32_t i0 = 0; i0 < take; i0 += 64) {   // uniform
+                        const uint32_t v = utf8_xlat(tab, ins_size + i0 + lane(), ins_size + i0,
+                                                     ins_size + min(i0 + 63u, take - 1u));
+                        if (i0 + lane() < take) cbyte[lv + i0 + lane()] = v;
+                    }
+                }
                 ins_size += take;
                 if (cr_valid && cr_kind == 0 && cr_lv + cr_len == lv && cr_pos + cr_len == pos) { cr_len += take; merged = true; }
                 st += int64_t(take);
@@ -1703,12 +1793,22 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
 
     if (ins.present && !del.present) {
         const uint64_t t_runs = __builtin_amdgcn_s_memtime();
-        // a non-ASCII text: the batched path numbers chars, utf8_offsets then places their bytes
+        // a non-ASCII text: with at most 64 continuation bytes the batched path writes byte offsets
+        // through utf8_table; otherwise it numbers chars and utf8_offsets then places their bytes
         const uint8_t *txt = C.ptr(ins.text.s) + ins.text.p;
-        const uint32_t n_chars = ins.ascii ? ins.text.n : count_char_starts(txt, ins.text.n);
+        Utf8Tab tab{0xFFFFFFFFu, 0u};
+        uint32_t n_chars = ins.text.n;
+        const bool tabled = !ins.ascii && ins.text.n && utf8_table(txt, ins.text.n, tab, n_chars);
+        if (!ins.ascii && !tabled) {
+            tab.n = 0;
+            n_chars = count_char_starts(txt, ins.text.n);
+        }
         FastOut fo = fast_runs(qav, qtp, ins.runs, n_chars, n_file, L.fseq, L.fmap, vs, O.aruns, O.pre,
-                               O.cbyte, O.alist, D.arun_cap, D.pre_cap, D.lv_cap);
-        if (fo.status == 0 && !ins.ascii) {
+                               O.cbyte, O.alist, D.arun_cap, D.pre_cap, D.lv_cap, tab);
+        if (fo.status == 0 && tabled) {   // the offsets are bytes already
+            fo.ins_size = ins.text.n;
+            all_ascii = 0;
+        } else if (fo.status == 0 && !ins.ascii) {
             if (utf8_offsets(txt, ins.text.n, O.cbyte, fo.n_lv, n_chars)) {
                 fo.ins_size = ins.text.n;   // bytes from here on
                 all_ascii = 0;

@@ -39,19 +39,17 @@ DEV uint64_t lt_mask() { return (1ull << lane()) - 1ull; }
 DEV uint32_t popc(uint64_t m) { return uint32_t(__popcll(m)); }
 DEV uint32_t ctz(uint64_t m) { return uint32_t(__ffsll((unsigned long long)m) - 1); }
 DEV void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+// inclusive prefix sum over the wave (all lanes active): DPP row scans, then row_bcast 15 / 31
 DEV uint32_t scan_incl(uint32_t v) {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = uint32_t(__shfl_up(int(v), d));
-        if (lane() >= uint32_t(d)) v += o;
-    }
+    v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x111, 0xf, 0xf, false));   // row_shr:1
+    v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x112, 0xf, 0xf, false));   // row_shr:2
+    v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x114, 0xf, 0xf, false));   // row_shr:4
+    v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x118, 0xf, 0xf, false));   // row_shr:8
+    v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x142, 0xa, 0xf, false));   // row_bcast:15
+    v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x143, 0xc, 0xf, false));   // row_bcast:31
     return v;
 }
-DEV uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += uint32_t(__shfl_xor(int(v), d));
-    return v;
-}
+DEV uint32_t wave_sum(uint32_t v) { return uint32_t(__builtin_amdgcn_readlane(int(scan_incl(v)), 63)); }
 
 // wave-wide byte copy, eight loads in flight per lane before their stores
 DEV void copy_bytes(uint8_t *dst, const uint8_t *src, uint32_t n) {

@@ -205,6 +205,15 @@ def _utf8_docs():
     o.add_insert_at(b, v, 4, "x😀y")
     o.add_insert(a, 0, "plain ascii at the front ")
     docs.append(o.encode())
+    # continuation-byte counts around the 64 a register table holds (more take the char-numbering
+    # pass), and multi-byte chars straddling the table pass's 1 KB strides
+    for text in ("é" * 64, "é" * 65, "日本語テキスト" * 10, "a" * 1021 + "€" + "b" * 500 + "😀" + "c" * 2000):
+        o = dt_amd.ListOpLog()
+        a = o.get_or_create_agent_id("a")
+        o.add_insert(a, 0, text)
+        o.add_delete_without_content(a, 5, 3)
+        o.add_insert(a, 7, "ü")
+        docs.append(o.encode())
     return docs
 
 
