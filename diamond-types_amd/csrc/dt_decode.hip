@@ -68,6 +68,24 @@ __device__ __forceinline__ uint32_t scan_incl(uint32_t v) {
     v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x143, 0xc, 0xf, false));   // row_bcast:31
     return v;
 }
+// Prefix composition of boolean functions f_l: {0,1} -> {0,1} along the wave (all lanes
+// active), each packed as f(0) | !f(1) << 1 so that the identity is 0 (what a DPP lane without a
+// source reads): lane l gets f_l o ... o f_0, by the same row scan and row broadcasts as scan_incl.
+__device__ __forceinline__ uint32_t fn_pack(bool f0, bool f1) { return uint32_t(f0) | (uint32_t(!f1) << 1); }
+__device__ __forceinline__ uint32_t compose_scan(uint32_t v) {
+    auto step = [&](uint32_t p) {   // v := v o p
+        const uint32_t m0 = v & 1u, m1 = ((v >> 1) & 1u) ^ 1u;
+        const uint32_t p0 = p & 1u, p1 = ((p >> 1) & 1u) ^ 1u;
+        v = (p0 ? m1 : m0) | (((p1 ? m1 : m0) ^ 1u) << 1);
+    };
+    step(uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x111, 0xf, 0xf, false)));   // row_shr:1
+    step(uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x112, 0xf, 0xf, false)));   // row_shr:2
+    step(uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x114, 0xf, 0xf, false)));   // row_shr:4
+    step(uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x118, 0xf, 0xf, false)));   // row_shr:8
+    step(uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x142, 0xa, 0xf, false)));   // row_bcast:15
+    step(uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x143, 0xc, 0xf, false)));   // row_bcast:31
+    return v;
+}
 // LDS stores of this wave become visible to its lanes' later LDS loads (a wave's LDS operations
 // complete in order; this only keeps the compiler from reordering them).
 __device__ __forceinline__ void wave_lds_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
@@ -885,17 +903,9 @@ __device__ __forceinline__ bool batch_records(VQ &q, const uint32_t *bnd, uint32
     const uint64_t x = uint64_t(q.lo) | (uint64_t(q.hi) << 32);
     // roles: a head with has_length and diff_nz is followed by its diff varint
     const bool needs = (x & 1) && ((x >> 1) & 1);
-    bool g0 = inq ? needs : false, g1 = false;      // successor's role given mine (head 0 / diff 1)
-    if (!inq) { g0 = false; g1 = true; }            // identity outside the queue
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const bool b0 = __shfl_up(int(g0), d) != 0, b1 = __shfl_up(int(g1), d) != 0;
-        if (l >= uint32_t(d)) {
-            const bool n0 = b0 ? g1 : g0, n1 = b1 ? g1 : g0;
-            g0 = n0; g1 = n1;
-        }
-    }
-    const bool role_after = g0;                      // role of lane l + 1 (the head lane starts as a head)
+    // successor's role given mine (head 0 / diff 1): (needs, false) in the queue, identity outside
+    const uint32_t gf = compose_scan(inq ? fn_pack(needs, false) : fn_pack(false, true));
+    const bool role_after = gf & 1u;                 // role of lane l + 1 (the head lane starts as a head)
     const bool role_here = __shfl_up(int(role_after), 1) != 0;   // (every lane runs the permute)
     const bool is_diff = l > h0 && role_here;
     const bool head = inq && !is_diff;
@@ -927,14 +937,13 @@ __device__ __forceinline__ bool batch_records(VQ &q, const uint32_t *bnd, uint32
     const uint32_t lincl = scan_incl(L);
     const uint32_t lv_r = lv + lincl - L;
     const int64_t adj = !is_del ? int64_t(len) : (fwd ? 0 : -int64_t(len));
-    int64_t step = rec ? diff + adj : 0;
-    int64_t cincl = step;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int64_t o = __shfl_up(cincl, d);
-        if (l >= uint32_t(d)) cincl += o;
-    }
-    const int64_t raw = last_cursor + (cincl - step) + diff;
+    const int64_t step = rec ? diff + adj : 0;
+    // the cursor prefix in 32-bit wrapping arithmetic: record k's prefix is the previous record's
+    // end cursor minus last_cursor, exact as an int32 while every earlier record's cursors lie in
+    // [0, 2^31) -- which the checks below demand of each record (any failure rejects the batch)
+    if (ballot(rec && (step != int64_t(int32_t(step)) || diff != int64_t(int32_t(diff))))) return false;
+    const uint32_t cincl = scan_incl(uint32_t(step));
+    const int64_t raw = last_cursor + int64_t(int32_t(cincl - uint32_t(step))) + diff;
     const int64_t st = (is_del && !fwd) ? raw - int64_t(len) : raw;
     bad = bad || (rec && (raw < 0 || st < 0 || uint64_t(st) + len >= LIM31 || uint64_t(raw) >= LIM31));
     bad = bad || (rec && uint64_t(lv_r) + len > total);
@@ -1078,7 +1087,7 @@ __device__ __forceinline__ bool batch_records(VQ &q, const uint32_t *bnd, uint32
     q.head = vlast + 1;
     lv += rdl(lincl, t);
     ins_size += rdl(iincl, t);
-    last_cursor += int64_t(uint64_t(rdl(uint32_t(uint64_t(cincl)), t)) | (uint64_t(rdl(uint32_t(uint64_t(cincl) >> 32), t)) << 32));
+    last_cursor += int64_t(int32_t(rdl(cincl, t)));
     bi += rdl(c, t);
     return true;
 }
