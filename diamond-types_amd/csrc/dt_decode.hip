@@ -424,7 +424,7 @@ __device__ __forceinline__ uint32_t crc32c_par(const uint8_t *s, uint32_t n, con
 // earlier sequence, so at most 64 hops), and the bytes are copied wave-wide, one gather load and
 // one store per lane per 64 bytes, instead of a dependent load round trip per sequence.
 __device__ __forceinline__ bool lz4_block(Ctx &C, const Rd &src, uint8_t *dst, uint32_t out_len, uint4 *lzm,
-                                          uint32_t *parse_cycles = nullptr) {
+                                          uint32_t *parse_cycles = nullptr) {   // DT_LZPROF: the DecodeResult::prof slots
     const uint8_t *sp = C.in + src.p;
     const uint32_t n = src.n;
     uint32_t ip = 0, op = 0;
@@ -555,7 +555,15 @@ __device__ __forceinline__ bool lz4_block(Ctx &C, const Rd &src, uint8_t *dst, u
             ns++;
         }
 #ifdef DT_LZPROF
-        if (parse_cycles) *parse_cycles += uint32_t(__builtin_amdgcn_s_memtime() - t_parse);
+        uint64_t t_lz = __builtin_amdgcn_s_memtime();
+        if (parse_cycles) parse_cycles[7] += uint32_t(t_lz - t_parse);
+        auto lz_mark = [&](int k) {   // DT_LZPROF: cycles of the copy's stages in prof[3..5]
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            if (parse_cycles) parse_cycles[k] += uint32_t(t - t_lz);
+            t_lz = t;
+        };
+#else
+        auto lz_mark = [](int) {};
 #endif
         // ---- resolve and copy the batch's output bytes [bs, op), CU rounds of 64 at a time ----
         // (every source lies in the input or before bs, so a group's loads all issue before its
@@ -580,6 +588,7 @@ __device__ __forceinline__ bool lz4_block(Ctx &C, const Rd &src, uint8_t *dst, u
         }
         constexpr uint32_t CU = 8;
         for (uint32_t g0 = bs; g0 < op; g0 += 64u * CU) {   // uniform
+            lz_mark(5);
             uint32_t fr[CU], inm = 0;   // per round: the source offset; bit u: it is an input byte
 #pragma unroll
             for (uint32_t u = 0; u < CU; u++) {
@@ -615,6 +624,7 @@ __device__ __forceinline__ bool lz4_block(Ctx &C, const Rd &src, uint8_t *dst, u
                 fr[u] = from;
                 inm |= uint32_t(inp) << u;
             }
+            lz_mark(3);
             uint32_t v[CU];
 #pragma unroll
             for (uint32_t u = 0; u < CU; u++)
@@ -622,8 +632,10 @@ __device__ __forceinline__ bool lz4_block(Ctx &C, const Rd &src, uint8_t *dst, u
 #pragma unroll
             for (uint32_t u = 0; u < CU; u++)
                 if (g0 + 64u * u + lane() < op) dst[g0 + 64u * u + lane()] = uint8_t(v[u]);
+            lz_mark(4);
         }
         wave_fence();   // the next batch reads these bytes
+        lz_mark(5);
     }
     return op == out_len;
 }
@@ -891,6 +903,9 @@ __device__ __forceinline__ uint32_t utf8_xlat(const Utf8Tab &tab, uint32_t k, ui
 // false without consuming anything when the batch is not the plain case (an error entry, a
 // record crossing an agent-run boundary or the end of the assigned LVs, an incomplete record
 // at the queue's end, a position out of range): the caller then takes one record the exact way.
+#ifndef DTGPU_REC_FILL
+#define DTGPU_REC_FILL 16u   // mean LVs per record from which the per-LV offsets are filled record by record
+#endif
 __device__ __forceinline__ bool batch_records(VQ &q, const uint32_t *bnd, uint32_t nb, uint32_t &bi, uint32_t &lv,
                                               uint32_t total, uint32_t &ins_size, int64_t &last_cursor,
                                               uint32_t &cr_valid, uint32_t &cr_lv, uint32_t &cr_len, uint32_t &cr_pos,
@@ -964,7 +979,7 @@ __device__ __forceinline__ bool batch_records(VQ &q, const uint32_t *bnd, uint32
         const uint32_t tot = rdl(lincl, 63);
         const uint32_t vk = ins_size + iincl - ilen - (lincl - L);   // content byte = vk + LV offset
         const bool dk = rec && is_del;
-        if (tot >= 16u * popc(hm)) {   // long records: one wave-wide fill per record
+        if (tot >= DTGPU_REC_FILL * popc(hm)) {   // long records: one wave-wide fill per record
             for (uint64_t m = hm; m; m &= m - 1) {   // uniform
                 const uint32_t i = ctz(m);
                 const uint32_t li = rdl(L, i), j0 = rdl(lincl, i) - li, vi = rdl(vk, i) + j0;
@@ -1629,7 +1644,7 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
             } else {
                 if (ulen > D.lz_cap) return ErrCapacity;
 #ifdef DT_LZPROF
-                if (!lz4_block(C, c, C.lz, uint32_t(ulen), reinterpret_cast<uint4 *>(L.fr), &R.prof[7]))
+                if (!lz4_block(C, c, C.lz, uint32_t(ulen), reinterpret_cast<uint4 *>(L.fr), R.prof))
                     return LZ4DecompressionError;
 #else
                 if (!lz4_block(C, c, C.lz, uint32_t(ulen), reinterpret_cast<uint4 *>(L.fr))) return LZ4DecompressionError;
