@@ -424,6 +424,7 @@ __device__ __forceinline__ uint32_t crc32c_par(const uint8_t *s, uint32_t n, con
 // earlier sequence, so at most 64 hops), and the bytes are copied wave-wide, one gather load and
 // one store per lane per 64 bytes, instead of a dependent load round trip per sequence.
 __device__ __forceinline__ bool lz4_block(Ctx &C, const Rd &src, uint8_t *dst, uint32_t out_len, uint4 *lzm,
+                                          uint32_t *lzr, uint32_t ring_n,
                                           uint32_t *parse_cycles = nullptr) {   // DT_LZPROF: the DecodeResult::prof slots
     const uint8_t *sp = C.in + src.p;
     const uint32_t n = src.n;
@@ -587,12 +588,16 @@ __device__ __forceinline__ bool lz4_block(Ctx &C, const Rd &src, uint8_t *dst, u
             wave_lds_fence();
         }
         constexpr uint32_t CU = 8;
+        // Resolved sources of this batch's bytes, round by round, in an LDS ring (bit 31: an input
+        // byte): a match byte whose source lies in an earlier round of the batch takes that
+        // byte's source from the ring instead of hopping on (about half the resolution steps).
+        const bool ring = ring_n && out_len < 0x80000000u;   // offsets leave bit 31 free (input too)
         for (uint32_t g0 = bs; g0 < op; g0 += 64u * CU) {   // uniform
             lz_mark(5);
             uint32_t fr[CU], inm = 0;   // per round: the source offset; bit u: it is an input byte
 #pragma unroll
             for (uint32_t u = 0; u < CU; u++) {
-                const uint32_t p = g0 + 64u * u + lane();
+                const uint32_t gu = g0 + 64u * u, p = gu + lane();
                 uint32_t cur = p, from = 0;
                 bool inp = false, done = p >= op;
                 while (ballot(!done)) {
@@ -617,12 +622,21 @@ __device__ __forceinline__ bool lz4_block(Ctx &C, const Rd &src, uint8_t *dst, u
                         } else {
                             const uint32_t m = k - lit;
                             const uint32_t q = o0 + lit - off + (off < ml ? m % off : m);
-                            if (q < bs) { from = q; done = true; } else cur = q;
+                            if (q < bs) {
+                                from = q; done = true;
+                            } else if (ring && q < gu && q + ring_n >= gu) {
+                                const uint32_t x = lzr[q & (ring_n - 1u)];
+                                from = x & 0x7FFFFFFFu; inp = x >> 31; done = true;
+                            } else {
+                                cur = q;
+                            }
                         }
                     }
                 }
                 fr[u] = from;
                 inm |= uint32_t(inp) << u;
+                if (ring && p < op) lzr[p & (ring_n - 1u)] = from | (uint32_t(inp) << 31);
+                wave_lds_fence();
             }
             lz_mark(3);
             uint32_t v[CU];
@@ -653,6 +667,7 @@ struct Lds {                 // per-wave tables, F = max file agents of the batc
     uint32_t *crc;           // CRC-32C table (256)
     uint32_t *fr;            // frontier compaction scratch (64)
     uint32_t *vq;            // varint queue compaction scratch (192); fr + vq: the LZ4 byte map (1 KB)
+    uint32_t *lzr;           // the LZ4 copy's resolved-source ring (DecodeParams::lz_ring entries)
 };
 
 struct CRuns {               // ContentIsKnown run iterator (ReadPatchContentIter)
@@ -1644,10 +1659,11 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
             } else {
                 if (ulen > D.lz_cap) return ErrCapacity;
 #ifdef DT_LZPROF
-                if (!lz4_block(C, c, C.lz, uint32_t(ulen), reinterpret_cast<uint4 *>(L.fr), R.prof))
+                if (!lz4_block(C, c, C.lz, uint32_t(ulen), reinterpret_cast<uint4 *>(L.fr), L.lzr, P.lz_ring, R.prof))
                     return LZ4DecompressionError;
 #else
-                if (!lz4_block(C, c, C.lz, uint32_t(ulen), reinterpret_cast<uint4 *>(L.fr))) return LZ4DecompressionError;
+                if (!lz4_block(C, c, C.lz, uint32_t(ulen), reinterpret_cast<uint4 *>(L.fr), L.lzr, P.lz_ring))
+                    return LZ4DecompressionError;
 #endif
             }
             comp.n = uint32_t(ulen);
@@ -2233,6 +2249,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_DECODE
     L.aoff = L.acnt + F;
     L.acur = L.aoff + F;
     L.amono = L.acur + F;
+    L.lzr = L.amono + F;
     if (!SIZE) {
         for (uint32_t i = lane(); i < 256; i += 64) {
             uint32_t c = i;
@@ -2494,7 +2511,7 @@ __device__ __forceinline__ int add_doc(const AddParams &P, const AddDesc &D, Dec
             if (ulen > (uint64_t(1) << 34)) return LZ4DecompressionError;
             if (ulen > 255ull * c.n + 64) return LZ4DecompressionError;
             if (ulen > D.lz_cap) return ErrCapacity;
-            if (!lz4_block(C, c, C.lz, uint32_t(ulen), reinterpret_cast<uint4 *>(L.fr))) return LZ4DecompressionError;
+            if (!lz4_block(C, c, C.lz, uint32_t(ulen), reinterpret_cast<uint4 *>(L.fr), nullptr, 0u)) return LZ4DecompressionError;
             comp.n = uint32_t(ulen);
             has_comp = true;
         }
@@ -3055,7 +3072,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_ADD_WA
 
 int launch_decode(const DecodeParams &p, void *stream) {
     if (!p.n_docs) return 0;
-    const size_t lds = (512 + 8 * size_t(p.max_file_agents)) * 4;
+    const size_t lds = (512 + 8 * size_t(p.max_file_agents) + (p.size_only ? 0u : p.lz_ring)) * 4;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (p.size_only)
         hipLaunchKernelGGL(ddec::decode_kernel<true>, dim3(p.n_docs), dim3(64), lds, s, p);

@@ -54,7 +54,8 @@ struct DecodeParams {
     uint8_t *content;
     const DecodeDesc *docs;
     DecodeResult *results;
-    uint32_t n_docs, size_only, max_file_agents, pad;
+    uint32_t n_docs, size_only, max_file_agents;
+    uint32_t lz_ring;       // entries of the LZ4 copy's resolved-source ring in dynamic LDS (0: none)
     uint32_t x2n[32];       // x^(2^k) mod the CRC-32C polynomial (crc32 combine tables)
 };
 
