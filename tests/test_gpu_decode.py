@@ -153,7 +153,8 @@ def _lz4_shape_docs():
     """Documents whose LZ4-compressed insert content covers the decompressor's cases: runs with
     match offsets 1-3 (overlapping, periodic copies) and length-extension chains past 255, long
     literal runs (extension bytes, 255 chains), matches reaching back more than one 64-sequence
-    batch and more than one 256-byte window, and short texts that stay uncompressed."""
+    batch and more than one 256-byte window, and short texts that stay uncompressed; with blocks
+    past 64 KB in the batch, the copy's resolved-source ring is on."""
     import random
     rng = random.Random(7)
     vocab = ["".join(rng.choice("abcdefghij ") for _ in range(rng.randint(2, 9))) for _ in range(40)]
@@ -165,6 +166,11 @@ def _lz4_shape_docs():
         " ".join(rng.choice(vocab) for _ in range(20000)),
         "q" * 20 + "".join(chr(33 + rng.randrange(90)) for _ in range(17)) + "q" * 300,
         "short",
+        # blocks past 64 KB (the batch then runs the copy's resolved-source ring): one run longer
+        # than a 4 KB mapped batch, a period of 37 across rounds, matches reaching past the ring
+        "a" * 70000,
+        "0123456789abcdefghijklmnopqrstuvwxyz!" * 3000,
+        "".join(chr(33 + rng.randrange(90)) for _ in range(3000)) * 25,
     ]
     docs = []
     for t in texts:
