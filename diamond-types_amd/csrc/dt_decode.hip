@@ -423,22 +423,21 @@ __device__ __forceinline__ uint32_t crc32c_par(const uint8_t *s, uint32_t n, con
 // its byte k repeats byte k mod offset, so one hop leaves the match; every hop lands in an
 // earlier sequence, so at most 64 hops), and the bytes are copied wave-wide, one gather load and
 // one store per lane per 64 bytes, instead of a dependent load round trip per sequence.
+template <bool TWO = false>
 __device__ __forceinline__ bool lz4_block(Ctx &C, const Rd &src, uint8_t *dst, uint32_t out_len, uint4 *lzm,
                                           uint32_t *lzr, uint32_t ring_n,
-                                          uint32_t *parse_cycles = nullptr) {   // DT_LZPROF: the DecodeResult::prof slots
+                                          uint32_t *parse_cycles = nullptr,   // DT_LZPROF: DecodeResult::prof
+                                          uint32_t *xb = nullptr) {            // TWO: the batch exchange (LDS)
     const uint8_t *sp = C.in + src.p;
     const uint32_t n = src.n;
     uint32_t ip = 0, op = 0;
     uint32_t steps = 0, step_at = 1u;   // the token-step table and the window it was built for
     bool end = n == 0;
-    while (!end) {
-        // ---- parse up to 64 sequences (uniform) ----
-        uint32_t so = 0xFFFFFFFFu, slit = 0, ssrc = 0, soff = 0, sml = 0;   // lane j: sequence j
-        const uint32_t bs = op;
-        uint32_t ns = 0;
-#ifdef DT_LZPROF
-        const uint64_t t_parse = __builtin_amdgcn_s_memtime();
-#endif
+    // ---- parse up to 64 sequences into lanes (uniform); false: a malformed block ----
+    auto parse_batch = [&](uint32_t &so, uint32_t &slit, uint32_t &ssrc, uint32_t &soff, uint32_t &sml,
+                           uint32_t &ns) -> bool {
+        so = 0xFFFFFFFFu; slit = 0; ssrc = 0; soff = 0; sml = 0;   // lane j: sequence j
+        ns = 0;
         while (ns < 64 && !end) {
             {   // sequences whose lengths take at most one extension byte each, found by walking
                 // a per-window table of token steps: lane l holds, for the window's bytes
@@ -555,17 +554,10 @@ __device__ __forceinline__ bool lz4_block(Ctx &C, const Rd &src, uint8_t *dst, u
             soff = me ? off : soff; sml = me ? ml : sml;
             ns++;
         }
-#ifdef DT_LZPROF
-        uint64_t t_lz = __builtin_amdgcn_s_memtime();
-        if (parse_cycles) parse_cycles[7] += uint32_t(t_lz - t_parse);
-        auto lz_mark = [&](int k) {   // DT_LZPROF: cycles of the copy's stages in prof[3..5]
-            const uint64_t t = __builtin_amdgcn_s_memtime();
-            if (parse_cycles) parse_cycles[k] += uint32_t(t - t_lz);
-            t_lz = t;
-        };
-#else
-        auto lz_mark = [](int) {};
-#endif
+        return true;
+    };
+    auto copy_batch = [&](const uint32_t bs, const uint32_t op, const uint32_t ns, const uint32_t so,
+                          const uint32_t slit, const uint32_t ssrc, const uint32_t soff, const uint32_t sml) {
         // ---- resolve and copy the batch's output bytes [bs, op), CU rounds of 64 at a time ----
         // (every source lies in the input or before bs, so a group's loads all issue before its
         // stores: one memory round trip per group, not per round).  A batch of at most 4 KB of
@@ -593,7 +585,6 @@ __device__ __forceinline__ bool lz4_block(Ctx &C, const Rd &src, uint8_t *dst, u
         // byte's source from the ring instead of hopping on (about half the resolution steps).
         const bool ring = ring_n && out_len < 0x80000000u;   // offsets leave bit 31 free (input too)
         for (uint32_t g0 = bs; g0 < op; g0 += 64u * CU) {   // uniform
-            lz_mark(5);
             uint32_t fr[CU], inm = 0;   // per round: the source offset; bit u: it is an input byte
 #pragma unroll
             for (uint32_t u = 0; u < CU; u++) {
@@ -638,7 +629,6 @@ __device__ __forceinline__ bool lz4_block(Ctx &C, const Rd &src, uint8_t *dst, u
                 if (ring && p < op) lzr[p & (ring_n - 1u)] = from | (uint32_t(inp) << 31);
                 wave_lds_fence();
             }
-            lz_mark(3);
             uint32_t v[CU];
 #pragma unroll
             for (uint32_t u = 0; u < CU; u++)
@@ -646,12 +636,57 @@ __device__ __forceinline__ bool lz4_block(Ctx &C, const Rd &src, uint8_t *dst, u
 #pragma unroll
             for (uint32_t u = 0; u < CU; u++)
                 if (g0 + 64u * u + lane() < op) dst[g0 + 64u * u + lane()] = uint8_t(v[u]);
-            lz_mark(4);
         }
         wave_fence();   // the next batch reads these bytes
-        lz_mark(5);
+    };
+    if (!TWO) {
+        while (!end) {
+            uint32_t so, slit, ssrc, soff, sml, ns;
+            const uint32_t bs = op;
+#ifdef DT_LZPROF
+            const uint64_t t_parse = __builtin_amdgcn_s_memtime();
+#endif
+            if (!parse_batch(so, slit, ssrc, soff, sml, ns)) return false;
+#ifdef DT_LZPROF
+            if (parse_cycles) parse_cycles[7] += uint32_t(__builtin_amdgcn_s_memtime() - t_parse);
+#endif
+            copy_batch(bs, op, ns, so, slit, ssrc, soff, sml);
+        }
+        return op == out_len;
     }
-    return op == out_len;
+    // Two waves (lz4_kernel): wave 0 parses batch k + 1 while wave 1 copies batch k.  A batch passes
+    // through one of two slots of xb: the five lane arrays, then bs, the batch's end, its sequence
+    // count and flags (bit 0: the block's last batch, bit 1: malformed); both waves read the same
+    // flags after each barrier, so they leave together.
+    constexpr uint32_t XS = 5 * 64 + 4;
+    const bool parser = threadIdx.x < 64;
+    auto parse_into = [&](uint32_t slot) {
+        uint32_t so, slit, ssrc, soff, sml, ns;
+        const uint32_t bs = op;
+        const bool good = parse_batch(so, slit, ssrc, soff, sml, ns);
+        uint32_t *b = xb + slot * XS;
+        b[lane()] = so; b[64 + lane()] = slit; b[128 + lane()] = ssrc; b[192 + lane()] = soff; b[256 + lane()] = sml;
+        const bool last = good && end;
+        if (lane() == 0) {
+            b[320] = bs; b[321] = op; b[322] = ns;
+            b[323] = (last ? 1u : 0u) | ((!good || (last && op != out_len)) ? 2u : 0u);
+        }
+    };
+    if (parser) parse_into(0);
+    __syncthreads();
+    for (uint32_t k = 0;; k++) {
+        const uint32_t *cur = xb + (k & 1u) * XS;
+        const uint32_t fl = cur[323];
+        if (fl & 2u) return false;
+        if (parser) {
+            if (!(fl & 1u)) parse_into((k + 1u) & 1u);
+        } else {
+            copy_batch(cur[320], cur[321], cur[322], cur[lane()], cur[64 + lane()], cur[128 + lane()],
+                       cur[192 + lane()], cur[256 + lane()]);
+        }
+        __syncthreads();
+        if (fl & 1u) return true;
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1658,13 +1693,17 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
                 R.lz_len = uint32_t(ulen);
             } else {
                 if (ulen > D.lz_cap) return ErrCapacity;
+                const uint32_t pre = P.lz_pre ? P.lz_pre[blockIdx.x] : 0u;   // lz4_kernel's verdict
+                if (pre == 2u) return LZ4DecompressionError;
+                if (pre != 1u) {
 #ifdef DT_LZPROF
-                if (!lz4_block(C, c, C.lz, uint32_t(ulen), reinterpret_cast<uint4 *>(L.fr), L.lzr, P.lz_ring, R.prof))
-                    return LZ4DecompressionError;
+                    if (!lz4_block(C, c, C.lz, uint32_t(ulen), reinterpret_cast<uint4 *>(L.fr), L.lzr, P.lz_ring, R.prof))
+                        return LZ4DecompressionError;
 #else
-                if (!lz4_block(C, c, C.lz, uint32_t(ulen), reinterpret_cast<uint4 *>(L.fr), L.lzr, P.lz_ring))
-                    return LZ4DecompressionError;
+                    if (!lz4_block(C, c, C.lz, uint32_t(ulen), reinterpret_cast<uint4 *>(L.fr), L.lzr, P.lz_ring))
+                        return LZ4DecompressionError;
 #endif
+                }
             }
             comp.n = uint32_t(ulen);
             has_comp = true;
@@ -2225,6 +2264,44 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
     R.ascii = all_ascii;
     R.n_lv = n_lv;
     return S_OK;
+}
+
+// The LZ4 block of a document in P.lz_big, before decode_kernel: its header read as decode_doc
+// reads it (anything unusual leaves the document to decode_kernel, which then reports it), the
+// block decompressed by two waves (lz4_block<true>), the verdict in P.lz_pre.
+constexpr uint32_t LZ_PRE_RING = 1024;
+constexpr size_t LZ_PRE_LDS = (256 + LZ_PRE_RING + 2 * (5 * 64 + 4)) * 4;
+__global__ __launch_bounds__(128) void lz4_kernel(DecodeParams P) {
+    extern __shared__ uint32_t lds[];
+    const uint32_t doc = P.lz_big[blockIdx.x];
+    const DecodeDesc D = P.docs[doc];
+    Ctx C;
+    C.in = P.in + D.in_off;
+    C.lz = P.lz + D.lz_off;
+    C.w0 = Win{C.in, 0x80000000u, 0};
+    C.w1 = Win{C.lz, 0x80000000u, 0};
+    const uint32_t len = D.in_len;
+    uint32_t verdict = 0;
+    do {   // both waves read the header alike (wave-uniform), so they agree on what follows
+        if (len < 8) break;
+        bool bad = false;
+        const char *magic = "DMNDTYPS";
+        for (uint32_t i = 0; i < 8; i++)
+            if (C.byte(0, i) != uint32_t(uint8_t(magic[i]))) bad = true;
+        if (bad) break;
+        Rd r{0, 8, len - 8};
+        uint64_t pv;
+        if (C.u64v(r, pv) || pv != 0) break;
+        bool found;
+        Rd c;
+        if (C.chunk_if(r, 5, found, c) || !found) break;
+        uint64_t ulen;
+        if (C.u64v(c, ulen)) break;
+        if (ulen > (uint64_t(1) << 34) || ulen > 255ull * c.n + 64 || ulen > D.lz_cap) break;
+        verdict = lz4_block<true>(C, c, C.lz, uint32_t(ulen), reinterpret_cast<uint4 *>(lds), lds + 256,
+                                  LZ_PRE_RING, nullptr, lds + 256 + LZ_PRE_RING) ? 1u : 2u;
+    } while (false);
+    if (threadIdx.x == 0) P.lz_pre[doc] = verdict;
 }
 
 template <bool SIZE>
@@ -3074,6 +3151,8 @@ int launch_decode(const DecodeParams &p, void *stream) {
     if (!p.n_docs) return 0;
     const size_t lds = (512 + 8 * size_t(p.max_file_agents) + (p.size_only ? 0u : p.lz_ring)) * 4;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (!p.size_only && p.n_big)
+        hipLaunchKernelGGL(ddec::lz4_kernel, dim3(p.n_big), dim3(128), ddec::LZ_PRE_LDS, s, p);
     if (p.size_only)
         hipLaunchKernelGGL(ddec::decode_kernel<true>, dim3(p.n_docs), dim3(64), lds, s, p);
     else

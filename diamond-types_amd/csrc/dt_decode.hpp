@@ -56,6 +56,12 @@ struct DecodeParams {
     DecodeResult *results;
     uint32_t n_docs, size_only, max_file_agents;
     uint32_t lz_ring;       // entries of the LZ4 copy's resolved-source ring in dynamic LDS (0: none)
+    // documents with a long LZ4 block, decompressed first by lz4_kernel (two waves each: one
+    // parses the next 64 sequences while the other copies the current ones); lz_pre[doc]:
+    // 1 decompressed, 2 malformed (LZ4DecompressionError), 0 left to decode_kernel
+    const uint32_t *lz_big;
+    uint32_t *lz_pre;
+    uint32_t n_big, pad2;
     uint32_t x2n[32];       // x^(2^k) mod the CRC-32C polynomial (crc32 combine tables)
 };
 

@@ -25,6 +25,7 @@ struct dtgpu_decoded {
     std::vector<DecodeResult> res;
     DevBuf<uint8_t> in, lz, content;
     DevBuf<uint32_t> aruns, alist, pre, ops, ent, poff, par, cbyte, agents, ver;
+    DevBuf<uint32_t> lz_big, lz_pre;   // documents whose LZ4 block lz4_kernel decompresses, its verdicts
     // dtgpu_decode_add results: the merged oplogs (not re-decodable), each merge's status and the
     // patch's version
     bool merged = false;

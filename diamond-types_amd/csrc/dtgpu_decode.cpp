@@ -235,9 +235,26 @@ dtgpu_status dtgpu_decode_create(const uint8_t *const *docs, const size_t *lens,
     P.agents = D->agents.p; P.ver = D->ver.p; P.content = D->content.p;
     P.size_only = 0;
     P.max_file_agents = std::max<uint32_t>(max_f, 1);
-    // the ring pays where a long LZ4 block bounds the batch; its 4 KB of LDS per wave would cost
-    // a batch of small documents occupancy (friendsforever x 10,000: 8.3 -> 9.0 ms)
-    P.lz_ring = max_lz >= 65536 ? 1024u : 0u;
+    // a long LZ4 block bounds the batch's decode: lz4_kernel decompresses those first, two waves
+    // per document (its resolved-source ring included); decode_kernel then needs no ring, whose
+    // 4 KB of LDS per wave would cost the small documents occupancy
+    P.lz_ring = 0;
+    P.n_big = 0;
+    P.lz_big = nullptr;
+    P.lz_pre = nullptr;
+    constexpr uint64_t LZ_BIG = 65536;   // a block this long gets lz4_kernel (DTGPU_NO_LZ_PRE: never)
+    if (max_lz >= LZ_BIG && !getenv("DTGPU_NO_LZ_PRE")) {
+        std::vector<uint32_t> big;
+        for (size_t i = 0; i < n; i++)
+            if (!D->desc[i].skip && D->res[i].lz_len >= LZ_BIG) big.push_back(uint32_t(i));
+        CK(D->lz_big.alloc(big.size()));
+        CK(hipMemcpyAsync(D->lz_big.p, big.data(), big.size() * 4, hipMemcpyHostToDevice, s));
+        CK(D->lz_pre.alloc(n));
+        CK(hipMemsetAsync(D->lz_pre.p, 0, n * 4, s));
+        P.lz_big = D->lz_big.p;
+        P.lz_pre = D->lz_pre.p;
+        P.n_big = uint32_t(big.size());
+    }
     CK(hipStreamSynchronize(s));
     stage_prof("decode: arenas");
 #undef CK

@@ -194,6 +194,45 @@ def test_lz4_shapes_decode_identically():
         _same_arrays(dec, i, d)
 
 
+def test_lz4_shapes_single_wave(monkeypatch):
+    """The same documents with the two-wave LZ4 kernel off (DTGPU_NO_LZ_PRE): every block is
+    decompressed inside decode_kernel by one wave."""
+    monkeypatch.setenv("DTGPU_NO_LZ_PRE", "1")
+    docs = _lz4_shape_docs()
+    dec = dt_amd.DecodeBatch(docs)
+    dec.run()
+    for i, d in enumerate(docs):
+        assert dec.status(i)["status"] == 0, i
+        _same_arrays(dec, i, d)
+
+
+def test_lz4_corrupt_long_blocks():
+    """Corruptions of documents whose LZ4 block goes through the two-wave kernel: the verdict
+    (status and, when it decodes, the arrays) equals the host decoder's."""
+    import random
+    rng = random.Random(11)
+    base = _lz4_shape_docs()[-3:]
+    docs = []
+    for d in base:
+        for _ in range(6):
+            b = bytearray(d)
+            for _ in range(rng.randint(1, 4)):
+                k = rng.randrange(16, len(b))
+                b[k] = rng.randrange(256)
+            docs.append(bytes(b))
+    for crc in (False, True):   # with the CRC check off, the LZ4 verdicts themselves are compared
+        dec = dt_amd.DecodeBatch(docs, ignore_crc=not crc)
+        dec.run()
+        for i, d in enumerate(docs):
+            got = dec.status(i)["status"]
+            if got == dt_amd.DECODE_DEFER:
+                continue
+            want = _host_code(d, ignore_crc=not crc)
+            assert got == want, (crc, i, got, want)
+            if want == 0:
+                _same_arrays(dec, i, d, ignore_crc=not crc)
+
+
 def _utf8_docs():
     """Non-ASCII insert text: the JSON traces whose content is not all ASCII, written as .dt the
     way configs[4] writes them, and small documents with 2-, 3- and 4-byte chars between ASCII
