@@ -956,11 +956,49 @@ __device__ __forceinline__ uint32_t utf8_xlat(const Utf8Tab &tab, uint32_t k, ui
 #ifndef DTGPU_REC_FILL
 #define DTGPU_REC_FILL 16u   // mean LVs per record from which the per-LV offsets are filled record by record
 #endif
+constexpr uint32_t FILL_JOB = 132;   // words of a deferred fill job: lv, tot, lincl[64], vk[64], dk mask
+constexpr uint32_t FILL_HDR = 68;    // words before a document's jobs: the UTF-8 table (n, t[64])
+// The per-LV content offsets of one batch of op records (batch_records, fill_kernel): LV j of
+// the batch (lv + j) holds its record's vk + j for an insert, ~0 for a delete; lane i holds record
+// i's inclusive LV prefix lincl, its length L (0: no record), vk and the delete flag dk.
+__device__ __forceinline__ void fill_lvs(uint32_t *cbyte, uint32_t lv, uint32_t tot, uint32_t lincl, uint32_t L,
+                                         uint32_t vk, bool dk, uint64_t hm, const Utf8Tab &tab) {
+    const uint32_t l = lane();
+    if (tot >= DTGPU_REC_FILL * popc(hm)) {   // long records: one wave-wide fill per record
+        for (uint64_t m = hm; m; m &= m - 1) {   // uniform
+            const uint32_t i = ctz(m);
+            const uint32_t li = rdl(L, i), j0 = rdl(lincl, i) - li, vi = rdl(vk, i) + j0;
+            const bool di = rdl(uint32_t(dk), i) != 0;
+            if (di || !tab.n) {
+                for (uint32_t k = l; k < li; k += 64) cbyte[lv + j0 + k] = di ? 0xFFFFFFFFu : vi + k;
+            } else {
+                for (uint32_t k0 = 0; k0 < li; k0 += 64) {   // uniform
+                    const uint32_t v = utf8_xlat(tab, vi + k0 + l, vi + k0, vi + min(k0 + 63u, li - 1u));
+                    if (k0 + l < li) cbyte[lv + j0 + k0 + l] = v;
+                }
+            }
+        }
+    } else for (uint32_t b = 0; b < tot; b += 64) {   // uniform: every lane runs the shuffles
+        const uint32_t j = b + l;
+        uint32_t r = 0;
+#pragma unroll
+        for (uint32_t s = 32; s >= 1; s >>= 1)
+            if (uint32_t(__shfl(int(lincl), int(r + s - 1))) <= j) r += s;
+        uint32_t v = uint32_t(__shfl(int(vk), int(r))) + j;
+        const bool d = __shfl(int(dk), int(r)) != 0;
+        if (tab.n) {   // the inserted chars of these LVs are numbered consecutively
+            const uint64_t im = ballot(j < tot && !d);
+            if (im) v = utf8_xlat(tab, v, rdl(v, ctz(im)), rdl(v, 63u - uint32_t(__clzll((long long)im))));
+        }
+        if (j < tot) cbyte[lv + j] = d ? 0xFFFFFFFFu : v;
+    }
+}
+
 __device__ __forceinline__ bool batch_records(VQ &q, const uint32_t *bnd, uint32_t nb, uint32_t &bi, uint32_t &lv,
                                               uint32_t total, uint32_t &ins_size, int64_t &last_cursor,
                                               uint32_t &cr_valid, uint32_t &cr_lv, uint32_t &cr_len, uint32_t &cr_pos,
                                               uint32_t &cr_kind, uint32_t &cr_fwd, Quads &qp, uint4 *pre_out,
-                                              uint32_t pre_cap, uint32_t *cbyte, const Utf8Tab &tab) {
+                                              uint32_t pre_cap, uint32_t *cbyte, const Utf8Tab &tab, uint32_t *job) {
     const uint32_t l = lane();
     const uint32_t h0 = q.head, cnt = q.cnt;
     const bool inq = l >= h0 && l < cnt;
@@ -1029,33 +1067,13 @@ __device__ __forceinline__ bool batch_records(VQ &q, const uint32_t *bnd, uint32
         const uint32_t tot = rdl(lincl, 63);
         const uint32_t vk = ins_size + iincl - ilen - (lincl - L);   // content byte = vk + LV offset
         const bool dk = rec && is_del;
-        if (tot >= DTGPU_REC_FILL * popc(hm)) {   // long records: one wave-wide fill per record
-            for (uint64_t m = hm; m; m &= m - 1) {   // uniform
-                const uint32_t i = ctz(m);
-                const uint32_t li = rdl(L, i), j0 = rdl(lincl, i) - li, vi = rdl(vk, i) + j0;
-                const bool di = rdl(uint32_t(dk), i) != 0;
-                if (di || !tab.n) {
-                    for (uint32_t k = l; k < li; k += 64) cbyte[lv + j0 + k] = di ? 0xFFFFFFFFu : vi + k;
-                } else {
-                    for (uint32_t k0 = 0; k0 < li; k0 += 64) {   // uniform
-                        const uint32_t v = utf8_xlat(tab, vi + k0 + l, vi + k0, vi + min(k0 + 63u, li - 1u));
-                        if (k0 + l < li) cbyte[lv + j0 + k0 + l] = v;
-                    }
-                }
-            }
-        } else for (uint32_t b = 0; b < tot; b += 64) {   // uniform: every lane runs the shuffles
-            const uint32_t j = b + l;
-            uint32_t r = 0;
-#pragma unroll
-            for (uint32_t s = 32; s >= 1; s >>= 1)
-                if (uint32_t(__shfl(int(lincl), int(r + s - 1))) <= j) r += s;
-            uint32_t v = uint32_t(__shfl(int(vk), int(r))) + j;
-            const bool d = __shfl(int(dk), int(r)) != 0;
-            if (tab.n) {   // the inserted chars of these LVs are numbered consecutively
-                const uint64_t im = ballot(j < tot && !d);
-                if (im) v = utf8_xlat(tab, v, rdl(v, ctz(im)), rdl(v, 63u - uint32_t(__clzll((long long)im))));
-            }
-            if (j < tot) cbyte[lv + j] = d ? 0xFFFFFFFFu : v;
+        if (job) {   // deferred: fill_kernel writes them once the document is decoded
+            job[2 + l] = lincl;
+            job[66 + l] = vk;
+            const uint64_t dm = ballot(dk);
+            if (l == 0) { job[0] = lv; job[1] = tot; job[130] = uint32_t(dm); job[131] = uint32_t(dm >> 32); }
+        } else {
+            fill_lvs(cbyte, lv, tot, lincl, L, vk, dk, hm, tab);
         }
     }
     // RLE merge of the records into op runs
@@ -1423,7 +1441,7 @@ __device__ __forceinline__ bool batch_agents(VQ &q, uint32_t n_file, uint32_t *f
     return true;
 }
 
-struct FastOut { uint32_t status, n_aruns, n_pre, n_lv, ins_size; uint64_t t_mid; };
+struct FastOut { uint32_t status, n_aruns, n_pre, n_lv, ins_size, n_jobs; uint64_t t_mid; };
 
 // Non-ASCII insert text on the batched path: fast_runs numbers the inserted chars (cbyte = the
 // char's index), then this pass puts each char's byte offset in place, 64 LVs at a time: the
@@ -1480,8 +1498,9 @@ __device__ __forceinline__ bool utf8_offsets(const uint8_t *t, uint32_t n, uint3
 __device__ __forceinline__ FastOut fast_runs(VQ qav, VQ qtp, VQ runs, uint32_t text_n, uint32_t n_file, uint32_t *fseq,
                                           const uint32_t *fmap, uint32_t *vs, uint4 *aruns_out, uint4 *pre_out,
                                           uint32_t *cbyte, uint32_t *bnd, uint32_t arun_cap, uint32_t pre_cap,
-                                          uint32_t lv_cap, const Utf8Tab &tab) {
-    FastOut fo{1, 0, 0, 0, 0, 0};
+                                          uint32_t lv_cap, const Utf8Tab &tab, uint32_t *jobs, uint32_t job_cap) {
+    FastOut fo{1, 0, 0, 0, 0, 0, 0};
+    uint32_t nj = 0;   // deferred fill jobs written (jobs: DecodeParams::fill slots, job_cap of them)
     uint64_t ins_total = 0;
     while (runs.left()) {
         uint64_t x;
@@ -1542,8 +1561,10 @@ __device__ __forceinline__ FastOut fast_runs(VQ qav, VQ qtp, VQ runs, uint32_t t
     while (lv < total) {
         if (!qtp.left()) return fo;
         if (qtp.head == qtp.cnt) vq_refill(qtp, vs);
+        uint32_t *job = jobs && nj < job_cap ? jobs + nj * FILL_JOB : nullptr;
         if (qtp.cnt - qtp.head >= 8 && batch_records(qtp, bnd, nb, bi, lv, total, ins_size, last_cursor, cr_valid, cr_lv,
-                                                     cr_len, cr_pos, cr_kind, cr_fwd, qp, pre_out, pre_cap, cbyte, tab)) {
+                                                     cr_len, cr_pos, cr_kind, cr_fwd, qp, pre_out, pre_cap, cbyte, tab, job)) {
+            if (job) nj++;
             bblk = 0xFFFFFFFFu;   // bi moved: the cached boundary window is stale
             continue;
         }
@@ -1633,6 +1654,7 @@ __device__ __forceinline__ FastOut fast_runs(VQ qav, VQ qtp, VQ runs, uint32_t t
     qa.flush(aruns_out);
     qp.flush(pre_out);
     fo.status = 0;
+    fo.n_jobs = nj;
     fo.n_aruns = uint32_t(qa.at);
     fo.n_pre = uint32_t(qp.at);
     fo.n_lv = lv;
@@ -1882,8 +1904,16 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
             tab.n = 0;
             n_chars = count_char_starts(txt, ins.text.n);
         }
+        uint32_t *jobs = nullptr;   // a long document defers its per-LV offsets to fill_kernel
+        if (P.fill && D.fill_cap && (ins.ascii || tabled)) {
+            uint32_t *hdr = P.fill + D.fill_off;
+            hdr[1 + lane()] = tab.t;
+            if (lane() == 0) hdr[0] = tab.n;
+            jobs = hdr + FILL_HDR;
+        }
         FastOut fo = fast_runs(qav, qtp, ins.runs, n_chars, n_file, L.fseq, L.fmap, vs, O.aruns, O.pre,
-                               O.cbyte, O.alist, D.arun_cap, D.pre_cap, D.lv_cap, tab);
+                               O.cbyte, O.alist, D.arun_cap, D.pre_cap, D.lv_cap, tab, jobs, D.fill_cap);
+        if (fo.status == 0 && jobs && lane() == 0) P.fill_n[blockIdx.x] = fo.n_jobs;
         if (fo.status == 0 && tabled) {   // the offsets are bytes already
             fo.ins_size = ins.text.n;
             all_ascii = 0;
@@ -2302,6 +2332,26 @@ __global__ __launch_bounds__(128) void lz4_kernel(DecodeParams P) {
                                   LZ_PRE_RING, nullptr, lds + 256 + LZ_PRE_RING) ? 1u : 2u;
     } while (false);
     if (threadIdx.x == 0) P.lz_pre[doc] = verdict;
+}
+
+// The per-LV content offsets that long documents deferred (fill_lvs on each job): one wave per
+// job slot; slots past the document's job count (its fast path failed: 0) leave at once.
+__global__ __launch_bounds__(64) void fill_kernel(DecodeParams P) {
+    const uint32_t b = blockIdx.x;
+    const uint32_t doc = P.fill_doc[b];
+    const DecodeDesc D = P.docs[doc];
+    const uint32_t j = b - D.fill_job0;
+    if (j >= P.fill_n[doc]) return;
+    const uint32_t *hdr = P.fill + D.fill_off;
+    const uint32_t *job = hdr + FILL_HDR + size_t(j) * FILL_JOB;
+    Utf8Tab tab;
+    tab.n = hdr[0];
+    tab.t = hdr[1 + lane()];
+    const uint32_t lincl = job[2 + lane()], vk = job[66 + lane()];
+    const uint64_t dm = uint64_t(job[130]) | (uint64_t(job[131]) << 32);
+    const uint32_t prev = uint32_t(__shfl_up(int(lincl), 1));
+    const uint32_t L = lincl - (lane() ? prev : 0u);
+    fill_lvs(P.cbyte + D.lv_off, job[0], job[1], lincl, L, vk, (dm >> lane()) & 1u, ballot(L > 0), tab);
 }
 
 template <bool SIZE>
@@ -3153,10 +3203,13 @@ int launch_decode(const DecodeParams &p, void *stream) {
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (!p.size_only && p.n_big)
         hipLaunchKernelGGL(ddec::lz4_kernel, dim3(p.n_big), dim3(128), ddec::LZ_PRE_LDS, s, p);
+    if (!p.size_only && p.fill_blocks && hipMemsetAsync(p.fill_n, 0, size_t(p.n_docs) * 4, s) != hipSuccess) return 66;
     if (p.size_only)
         hipLaunchKernelGGL(ddec::decode_kernel<true>, dim3(p.n_docs), dim3(64), lds, s, p);
     else
         hipLaunchKernelGGL(ddec::decode_kernel<false>, dim3(p.n_docs), dim3(64), lds, s, p);
+    if (!p.size_only && p.fill_blocks)
+        hipLaunchKernelGGL(ddec::fill_kernel, dim3(p.fill_blocks), dim3(64), 0, s, p);
     return launch_error() == hipSuccess ? 0 : 66;
 }
 

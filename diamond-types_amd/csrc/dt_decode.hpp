@@ -28,6 +28,10 @@ struct DecodeDesc {
     uint32_t in_len, lz_cap, arun_cap, pre_cap, op_cap, ent_cap, par_cap, content_cap, lv_cap, agent_cap;
     uint32_t ignore_crc, skip;
     uint32_t patch, pad;    // sizing a patch for decode_and_add: a StartBranch version is not an error
+    // a long document's deferred per-LV offsets (fill_kernel): its area in DecodeParams::fill
+    // (words), its first job slot in the fill grid and its job capacity (0: filled inline)
+    uint64_t fill_off;
+    uint32_t fill_job0, fill_cap;
 };
 
 struct DecodeResult {
@@ -62,6 +66,12 @@ struct DecodeParams {
     const uint32_t *lz_big;
     uint32_t *lz_pre;
     uint32_t n_big, pad2;
+    // deferred per-LV offsets of long documents: job arena, each document's job count (written by
+    // decode_kernel when its fast path succeeds), the document of each fill-grid slot, grid size
+    uint32_t *fill;
+    uint32_t *fill_n;
+    const uint32_t *fill_doc;
+    uint32_t fill_blocks, pad3;
     uint32_t x2n[32];       // x^(2^k) mod the CRC-32C polynomial (crc32 combine tables)
 };
 

@@ -177,6 +177,9 @@ dtgpu_status dtgpu_decode_create(const uint8_t *const *docs, const size_t *lens,
     uint64_t lz = 0, ar = 0, pre = 0, ops = 0, ent = 0, poff = 0, par = 0, content = 0, lv = 0, ag = 0, ver = 0;
     uint32_t max_f = 0;
     uint64_t max_lz = 0;
+    constexpr uint64_t FILL_BIG = 131072;   // LVs from which a document defers its per-LV offsets
+    uint64_t fill_words = 0;
+    std::vector<uint32_t> fill_doc;
     for (size_t i = 0; i < n; i++) {
         DecodeDesc &d = D->desc[i];
         const DecodeResult &r = D->res[i];
@@ -214,6 +217,22 @@ dtgpu_status dtgpu_decode_create(const uint8_t *const *docs, const size_t *lens,
         ver += DECODE_MAX_FRONTIER;
         if (!d.skip) max_f = std::max(max_f, r.n_file_agents);
         if (!d.skip) max_lz = std::max<uint64_t>(max_lz, r.lz_len);
+        // a long document hands its per-LV offsets to fill_kernel: about one job per 64-varint
+        // batch of op records (a document that needs more fills the rest inline)
+        d.fill_off = 0; d.fill_job0 = 0; d.fill_cap = 0;
+        if (!d.skip && r.n_lv >= FILL_BIG && !getenv("DTGPU_NO_FILL_DEFER")) {
+            d.fill_off = fill_words;
+            d.fill_job0 = uint32_t(fill_doc.size());
+            d.fill_cap = r.tp_bytes / 32 + 64;
+            fill_words += 68 + uint64_t(d.fill_cap) * 132;
+            fill_doc.insert(fill_doc.end(), d.fill_cap, uint32_t(i));
+        }
+    }
+    if (!fill_doc.empty()) {
+        CK(D->fill.alloc(fill_words));
+        CK(D->fill_n.alloc(n));
+        CK(D->fill_doc.alloc(fill_doc.size()));
+        CK(hipMemcpyAsync(D->fill_doc.p, fill_doc.data(), fill_doc.size() * 4, hipMemcpyHostToDevice, s));
     }
     CK(D->lz.alloc(lz));
     CK(D->aruns.alloc(4 * ar));
@@ -238,6 +257,10 @@ dtgpu_status dtgpu_decode_create(const uint8_t *const *docs, const size_t *lens,
     // a long LZ4 block bounds the batch's decode: lz4_kernel decompresses those first, two waves
     // per document (its resolved-source ring included); decode_kernel then needs no ring, whose
     // 4 KB of LDS per wave would cost the small documents occupancy
+    P.fill = fill_doc.empty() ? nullptr : D->fill.p;
+    P.fill_n = fill_doc.empty() ? nullptr : D->fill_n.p;
+    P.fill_doc = fill_doc.empty() ? nullptr : D->fill_doc.p;
+    P.fill_blocks = uint32_t(fill_doc.size());
     P.lz_ring = 0;
     P.n_big = 0;
     P.lz_big = nullptr;
