@@ -1892,6 +1892,7 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
         for (uint64_t i = lane(); i < k; i += 64) O.cbyte[lv0 + i] = v;
     };
 
+    uint32_t fill_jobs = 0;   // deferred fill jobs of a long document (fill_kernel)
     if (ins.present && !del.present) {
         const uint64_t t_runs = __builtin_amdgcn_s_memtime();
         // a non-ASCII text: with at most 64 continuation bytes the batched path writes byte offsets
@@ -1913,7 +1914,10 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
         }
         FastOut fo = fast_runs(qav, qtp, ins.runs, n_chars, n_file, L.fseq, L.fmap, vs, O.aruns, O.pre,
                                O.cbyte, O.alist, D.arun_cap, D.pre_cap, D.lv_cap, tab, jobs, D.fill_cap);
-        if (fo.status == 0 && jobs && lane() == 0) P.fill_n[blockIdx.x] = fo.n_jobs;
+        if (fo.status == 0 && jobs) {
+            fill_jobs = fo.n_jobs;
+            if (lane() == 0) P.fill_n[blockIdx.x] = fill_jobs;   // (bit 31 set with the text copy below)
+        }
         if (fo.status == 0 && tabled) {   // the offsets are bytes already
             fo.ins_size = ins.text.n;
             all_ascii = 0;
@@ -2209,7 +2213,16 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
     prof_mark(5);
 
     // ---- the insert text (every known piece, in order) ------------------------------------------
-    if (ins.present && ins_size) {
+    if (ins.present && ins_size && P.fill && D.fill_cap) {   // a long document: fill_kernel copies it
+        if (ins_size > D.content_cap) return ErrCapacity;
+        uint32_t *hdr = P.fill + D.fill_off;
+        if (lane() == 0) {
+            hdr[65] = ins.text.s;
+            hdr[66] = ins.t0;
+            hdr[67] = ins_size;
+            P.fill_n[blockIdx.x] = fill_jobs | 0x80000000u;
+        }
+    } else if (ins.present && ins_size) {
         if (ins_size > D.content_cap) return ErrCapacity;
         const uint8_t *src = C.ptr(ins.text.s) + ins.t0;
         for (uint32_t i = 0; i < ins_size; i += 256) {
@@ -2341,8 +2354,29 @@ __global__ __launch_bounds__(64) void fill_kernel(DecodeParams P) {
     const uint32_t doc = P.fill_doc[b];
     const DecodeDesc D = P.docs[doc];
     const uint32_t j = b - D.fill_job0;
-    if (j >= P.fill_n[doc]) return;
+    const uint32_t fn = P.fill_n[doc];
     const uint32_t *hdr = P.fill + D.fill_off;
+    if (j >= D.fill_cap) {   // 4 KB of the insert text (bit 31 of fill_n: decode_kernel left it here)
+        if (!(fn >> 31)) return;
+        const uint8_t *src = (hdr[65] == SRC_LZ ? P.lz + D.lz_off : P.in + D.in_off) + hdr[66];
+        uint8_t *dst = P.content + D.content_off;
+        const uint32_t n = hdr[67], k0 = (j - D.fill_cap) * 4096u;
+        uint8_t v[16];
+        for (uint32_t q = 0; q < 4; q++) {   // 16 loads in flight per lane, then their stores
+#pragma unroll
+            for (uint32_t u = 0; u < 16; u++) {
+                const uint32_t i = k0 + 1024u * q + 64u * u + lane();
+                v[u] = i < n ? src[i] : 0;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < 16; u++) {
+                const uint32_t i = k0 + 1024u * q + 64u * u + lane();
+                if (i < n) dst[i] = v[u];
+            }
+        }
+        return;
+    }
+    if (j >= (fn & 0x7FFFFFFFu)) return;
     const uint32_t *job = hdr + FILL_HDR + size_t(j) * FILL_JOB;
     Utf8Tab tab;
     tab.n = hdr[0];

@@ -32,6 +32,7 @@ struct DecodeDesc {
     // (words), its first job slot in the fill grid and its job capacity (0: filled inline)
     uint64_t fill_off;
     uint32_t fill_job0, fill_cap;
+    uint32_t fill_copy, pad4;   // its fill-grid slots after the jobs: the insert text copied 4 KB each
 };
 
 struct DecodeResult {

@@ -219,13 +219,14 @@ dtgpu_status dtgpu_decode_create(const uint8_t *const *docs, const size_t *lens,
         if (!d.skip) max_lz = std::max<uint64_t>(max_lz, r.lz_len);
         // a long document hands its per-LV offsets to fill_kernel: about one job per 64-varint
         // batch of op records (a document that needs more fills the rest inline)
-        d.fill_off = 0; d.fill_job0 = 0; d.fill_cap = 0;
+        d.fill_off = 0; d.fill_job0 = 0; d.fill_cap = 0; d.fill_copy = 0;
         if (!d.skip && r.n_lv >= FILL_BIG && !getenv("DTGPU_NO_FILL_DEFER")) {
             d.fill_off = fill_words;
             d.fill_job0 = uint32_t(fill_doc.size());
             d.fill_cap = r.tp_bytes / 32 + 64;
+            d.fill_copy = d.content_cap / 4096 + 1;   // the insert text, 4 KB per slot
             fill_words += 68 + uint64_t(d.fill_cap) * 132;
-            fill_doc.insert(fill_doc.end(), d.fill_cap, uint32_t(i));
+            fill_doc.insert(fill_doc.end(), size_t(d.fill_cap) + d.fill_copy, uint32_t(i));
         }
     }
     if (!fill_doc.empty()) {
