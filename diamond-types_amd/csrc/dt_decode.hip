@@ -275,12 +275,42 @@ __device__ __forceinline__ int vq_zigzag(VQ &q, int64_t &v, uint32_t *scratch) {
 // ---------------------------------------------------------------------------------------------
 // lane-parallel helpers
 // ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool utf8_ok_bytes(const uint8_t *s, uint32_t n, uint32_t t0, uint32_t t1, bool &ascii);
 // UTF-8 validity (std::str::from_utf8): every lead byte carries exactly its continuation bytes,
 // no overlong forms, no surrogates, <= U+10FFFF; every continuation byte lies inside the span
 // of the nearest preceding lead.  ASCII windows are cleared by one ballot.
 __device__ __forceinline__ bool utf8_ok(const uint8_t *s, uint32_t n, bool &ascii) {
     ascii = true;
-    for (uint32_t i = 0; i < n; i += 64) {
+    // 1 KB at a time, 16 bytes per lane from aligned blocks (each holds a text byte, so the load
+    // stays inside the text's page): a kilobyte without a byte >= 0x80 is cleared by one ballot,
+    // one with some takes the byte-wise check below
+    const uintptr_t a0 = reinterpret_cast<uintptr_t>(s) & ~uintptr_t(15);
+    const uint32_t head = uint32_t(reinterpret_cast<uintptr_t>(s) - a0), span = head + n;
+    for (uint32_t b = 0; b < span; b += 1024) {
+        const uint32_t o = b + 16u * lane();
+        uint4 w = make_uint4(0u, 0u, 0u, 0u);
+        if (o < span) w = *reinterpret_cast<const uint4 *>(a0 + o);
+        uint32_t hi = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) {
+            uint32_t m = (q == 0 ? w.x : q == 1 ? w.y : q == 2 ? w.z : w.w) & 0x80808080u;
+#pragma unroll
+            for (uint32_t k = 0; k < 4; k++) {
+                const uint32_t off = o + 4u * q + k;
+                if (off < head || off >= span) m &= ~(0x80u << (8u * k));
+            }
+            hi |= m;
+        }
+        if (!ballot(hi != 0)) continue;
+        const uint32_t t0 = b > head ? b - head : 0u, t1 = min(b + 1024u, span) - head;
+        if (!utf8_ok_bytes(s, n, t0, t1, ascii)) return false;
+    }
+    return true;
+}
+// the byte-wise check of text bytes [t0, t1) (continuations look back, leads forward, over the
+// whole text)
+__device__ __forceinline__ bool utf8_ok_bytes(const uint8_t *s, uint32_t n, uint32_t t0, uint32_t t1, bool &ascii) {
+    for (uint32_t i = t0; i < t1; i += 64) {
         const uint32_t j = i + lane();
         const uint32_t c = j < n ? s[j] : 0u;
         if (!ballot(c >= 0x80u)) continue;
