@@ -1063,7 +1063,7 @@ __device__ __forceinline__ bool batch_records(VQ &q, const uint32_t *bnd, uint32
         len = 1;
         diff = int64_t(rest >> 1) * ((rest & 1) ? -1 : 1);
     }
-    const bool rec = (hm >> l) & 1;
+    bool rec = (hm >> l) & 1;
     bool bad = rec && (len == 0 || len >= LIM31);
     const uint32_t L = rec && !bad ? uint32_t(len) : 0u;
     // LVs and cursors (64-bit cursor prefix over the records)
@@ -1089,16 +1089,20 @@ __device__ __forceinline__ bool batch_records(VQ &q, const uint32_t *bnd, uint32
     if (c == 63 && rdl(bw, 63) <= lv_r) c = 64;
     const uint32_t be = uint32_t(__shfl(int(bw), int(min(c, 63u))));
     bad = bad || (rec && (c >= 64 || uint64_t(lv_r) + len > be));
-    if (ballot(bad)) return false;
+    if (const uint64_t bm = ballot(bad)) {   // the records before the first bad one still go as a batch
+        hm &= (1ull << ctz(bm)) - 1ull;      // (every value below is a prefix over the records)
+        if (!hm) return false;               // the first record itself: the caller takes it exactly
+        rec = (hm >> l) & 1;
+    }
     // content offsets per LV
     const uint32_t ilen = rec && !is_del ? L : 0u;
     const uint32_t iincl = scan_incl(ilen);
     {   // every LV of the batch, wave-strided: its record is the first lane whose lincl exceeds it
-        const uint32_t tot = rdl(lincl, 63);
+        const uint32_t tot = rdl(lincl, 63u - uint32_t(__clzll((long long)hm)));
         const uint32_t vk = ins_size + iincl - ilen - (lincl - L);   // content byte = vk + LV offset
         const bool dk = rec && is_del;
         if (job) {   // deferred: fill_kernel writes them once the document is decoded
-            job[2 + l] = lincl;
+            job[2 + l] = (hm >> l) ? lincl : tot;   // (no records past the batch's last one)
             job[66 + l] = vk;
             const uint64_t dm = ballot(dk);
             if (l == 0) { job[0] = lv; job[1] = tot; job[130] = uint32_t(dm); job[131] = uint32_t(dm >> 32); }
