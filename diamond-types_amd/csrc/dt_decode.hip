@@ -255,6 +255,48 @@ __device__ __forceinline__ void vq_refill(VQ &q, uint32_t *scratch) {
 }
 
 // Reader::u64v on a queue
+// Top a queue up before it runs dry: the r < 64 entries left move to lanes 0 .. r-1 and the
+// varints of the next window follow, as many as fit (the batched record loop then never sees a
+// queue of a few varints, which it would take one record at a time).  A window without a
+// terminator leaves the queue as it is; the refill once it is empty reports it.
+__device__ __forceinline__ void vq_topup(VQ &q, uint32_t *scratch) {
+    const uint32_t i = lane();
+    const uint32_t r = q.cnt - q.head;
+    const uint32_t olo = uint32_t(__shfl(int(q.lo), int(min(q.head + i, 63u))));
+    const uint32_t ohi = uint32_t(__shfl(int(q.hi), int(min(q.head + i, 63u))));
+    const uint32_t oend = uint32_t(__shfl(int(q.end), int(min(q.head + i, 63u))));
+    const uint32_t rem = q.len - q.wpos;
+    const uint32_t b = i < rem ? q.base[q.wpos + i] : 0x80u;
+    const uint64_t T = ballot(i < rem && b < 0x80u);
+    if (!T) return;
+    const bool term = (T >> i) & 1;
+    const uint64_t below = T & lt_mask();
+    const uint32_t start = below ? uint32_t(64 - __clzll((long long)below)) : 0u;
+    const uint32_t L = i - start + 1;
+    uint64_t v = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 10; j++) {
+        const uint32_t bj = uint32_t(__shfl(int(b), int(i >= j ? i - j : 0)));
+        if (j < L) v |= uint64_t(bj & 0x7fu) << (7 * (L - 1 - j));
+    }
+    const bool err = L > 10 || (L == 10 && (b & 0x7fu) > 1u);
+    const uint32_t nk = min(popc(T), 64u - r);   // new entries that fit
+    const uint32_t k = popc(below);
+    if (i < r) { scratch[3 * i] = olo; scratch[3 * i + 1] = ohi; scratch[3 * i + 2] = oend; }
+    if (term && k < nk) {
+        scratch[3 * (r + k)] = err ? uint32_t(InvalidVarInt) : uint32_t(v);
+        scratch[3 * (r + k) + 1] = uint32_t(v >> 32);
+        scratch[3 * (r + k) + 2] = err ? 0xFFFFFFFFu : q.wpos + i + 1;
+    }
+    const uint32_t lastk = ctz(ballot(term && k == nk - 1u));   // the window lane of the last kept one
+    __syncthreads();
+    q.cnt = r + nk;
+    q.head = 0;
+    if (i < q.cnt) { q.lo = scratch[3 * i]; q.hi = scratch[3 * i + 1]; q.end = scratch[3 * i + 2]; }
+    __syncthreads();
+    q.wpos += lastk + 1u;
+}
+
 __device__ __forceinline__ int vq_pop(VQ &q, uint64_t &v, uint32_t *scratch) {
     if (q.at >= q.len) return UnexpectedEOF;
     if (q.head == q.cnt) vq_refill(q, scratch);
@@ -1595,6 +1637,7 @@ __device__ __forceinline__ FastOut fast_runs(VQ qav, VQ qtp, VQ runs, uint32_t t
     while (lv < total) {
         if (!qtp.left()) return fo;
         if (qtp.head == qtp.cnt) vq_refill(qtp, vs);
+        else if (qtp.cnt - qtp.head < 8 && qtp.wpos < qtp.len) vq_topup(qtp, vs);
         uint32_t *job = jobs && nj < job_cap ? jobs + nj * FILL_JOB : nullptr;
         if (qtp.cnt - qtp.head >= 8 && batch_records(qtp, bnd, nb, bi, lv, total, ins_size, last_cursor, cr_valid, cr_lv,
                                                      cr_len, cr_pos, cr_kind, cr_fwd, qp, pre_out, pre_cap, cbyte, tab, job)) {
