@@ -1592,6 +1592,7 @@ __device__ __forceinline__ FastOut fast_runs(VQ qav, VQ qtp, VQ runs, uint32_t t
     uint32_t nb = 0, bbuf = 0;
     while (qav.left()) {
         if (qav.head == qav.cnt) vq_refill(qav, vs);
+        else if (qav.cnt - qav.head < 6 && qav.wpos < qav.len) vq_topup(qav, vs);
         if (qav.cnt - qav.head >= 6 && batch_agents(qav, n_file, fseq, fmap, next_assign, ca_valid, ca_lv, ca_len, ca_agent,
                                                     ca_seq, qa, aruns_out, arun_cap, nb, bbuf, bnd))
             continue;
@@ -2183,6 +2184,7 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
     uint32_t fr = 0, fn = 0;   // frontier: lane k holds element k (sorted)
     while (qhist.left()) {
         if (qhist.head == qhist.cnt) vq_refill(qhist, vs);
+        else if (qhist.cnt - qhist.head < 4 && qhist.wpos < qhist.len) vq_topup(qhist, vs);
         if (qhist.cnt - qhist.head >= 4) {   // next_assign < 2^31 (checked with the agent runs)
             uint32_t nf = uint32_t(next_file);
             if (batch_parents(qhist, nf, uint32_t(next_assign), pe_valid, pe_start, pe_end, pe_poff, n_ent, n_par,
