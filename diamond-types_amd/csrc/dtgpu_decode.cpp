@@ -4,6 +4,7 @@
 // the decoder's register windows never read past the allocation), a sizing pass of the decode
 // kernel reads the chunk directory and the OpVersions stream, and the output arenas are
 // allocated from its counts.  dtgpu_decode_run is then the full decode, entirely on the device.
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -177,7 +178,8 @@ dtgpu_status dtgpu_decode_create(const uint8_t *const *docs, const size_t *lens,
     uint64_t lz = 0, ar = 0, pre = 0, ops = 0, ent = 0, poff = 0, par = 0, content = 0, lv = 0, ag = 0, ver = 0;
     uint32_t max_f = 0;
     uint64_t max_lz = 0;
-    constexpr uint64_t FILL_BIG = 131072;   // LVs from which a document defers its per-LV offsets
+    // LVs from which a document defers its per-LV offsets (DTGPU_FILL_MIN overrides)
+    const uint64_t FILL_BIG = getenv("DTGPU_FILL_MIN") ? strtoull(getenv("DTGPU_FILL_MIN"), nullptr, 10) : 131072;
     uint64_t fill_words = 0;
     std::vector<uint32_t> fill_doc;
     for (size_t i = 0; i < n; i++) {
@@ -266,7 +268,8 @@ dtgpu_status dtgpu_decode_create(const uint8_t *const *docs, const size_t *lens,
     P.n_big = 0;
     P.lz_big = nullptr;
     P.lz_pre = nullptr;
-    constexpr uint64_t LZ_BIG = 65536;   // a block this long gets lz4_kernel (DTGPU_NO_LZ_PRE: never)
+    // a block this long gets lz4_kernel (DTGPU_LZ_PRE_MIN overrides; DTGPU_NO_LZ_PRE: never)
+    const uint64_t LZ_BIG = getenv("DTGPU_LZ_PRE_MIN") ? strtoull(getenv("DTGPU_LZ_PRE_MIN"), nullptr, 10) : 65536;
     if (max_lz >= LZ_BIG && !getenv("DTGPU_NO_LZ_PRE")) {
         std::vector<uint32_t> big;
         for (size_t i = 0; i < n; i++)
