@@ -206,6 +206,19 @@ def test_lz4_shapes_single_wave(monkeypatch):
         _same_arrays(dec, i, d)
 
 
+def test_long_documents_uncompressed():
+    """Documents past the deferred-fill threshold (131,072 LVs) written without LZ4: fill_kernel
+    copies their insert text from the document bytes instead of the LZ4 buffer (and their per-LV
+    offsets, ASCII and non-ASCII, from the deferred jobs)."""
+    opts = dt_amd.EncodeOptions(True, False, True)
+    docs = [dt_amd.apply_edits_push_merge(G.trace(n)["txns"]).encode(opts) for n in ("automerge-paper", "rustcode")]
+    dec = dt_amd.DecodeBatch(docs)
+    dec.run()
+    for i, d in enumerate(docs):
+        assert dec.status(i)["status"] == 0, i
+        _same_arrays(dec, i, d)
+
+
 def test_lz4_corrupt_long_blocks():
     """Corruptions of documents whose LZ4 block goes through the two-wave kernel: the verdict
     (status and, when it decodes, the arrays) equals the host decoder's."""
