@@ -495,7 +495,7 @@ __device__ __forceinline__ uint32_t crc32c_par(const uint8_t *s, uint32_t n, con
 // its byte k repeats byte k mod offset, so one hop leaves the match; every hop lands in an
 // earlier sequence, so at most 64 hops), and the bytes are copied wave-wide, one gather load and
 // one store per lane per 64 bytes, instead of a dependent load round trip per sequence.
-template <bool TWO = false>
+template <bool TWO = false, bool THREE = false>
 __device__ __forceinline__ bool lz4_block(Ctx &C, const Rd &src, uint8_t *dst, uint32_t out_len, uint4 *lzm,
                                           uint32_t *lzr, uint32_t ring_n,
                                           uint32_t *parse_cycles = nullptr,   // DT_LZPROF: DecodeResult::prof
@@ -628,8 +628,10 @@ __device__ __forceinline__ bool lz4_block(Ctx &C, const Rd &src, uint8_t *dst, u
         }
         return true;
     };
+    bool waited_out = false;   // THREE: a wait for the other copier gave up (the caller redoes the block)
     auto copy_batch = [&](const uint32_t bs, const uint32_t op, const uint32_t ns, const uint32_t so,
-                          const uint32_t slit, const uint32_t ssrc, const uint32_t soff, const uint32_t sml) {
+                          const uint32_t slit, const uint32_t ssrc, const uint32_t soff, const uint32_t sml,
+                          uint4 *lzm, uint32_t *lzr, const volatile uint32_t *wflag, uint32_t wval) {
         // ---- resolve and copy the batch's output bytes [bs, op), CU rounds of 64 at a time ----
         // (every source lies in the input or before bs, so a group's loads all issue before its
         // stores: one memory round trip per group, not per round).  A batch of at most 4 KB of
@@ -651,7 +653,8 @@ __device__ __forceinline__ bool lz4_block(Ctx &C, const Rd &src, uint8_t *dst, u
             if (lane() < nw) lzm[lane()].z = inc - c;
             wave_lds_fence();
         }
-        constexpr uint32_t CU = 8;
+        constexpr uint32_t CU = THREE ? 16 : 8;
+        bool waited = wflag == nullptr;   // THREE, odd batches: wait for the even batch's stores
         // Resolved sources of this batch's bytes, round by round, in an LDS ring (bit 31: an input
         // byte): a match byte whose source lies in an earlier round of the batch takes that
         // byte's source from the ring instead of hopping on (about half the resolution steps).
@@ -701,6 +704,14 @@ __device__ __forceinline__ bool lz4_block(Ctx &C, const Rd &src, uint8_t *dst, u
                 if (ring && p < op) lzr[p & (ring_n - 1u)] = from | (uint32_t(inp) << 31);
                 wave_lds_fence();
             }
+            if (!waited) {   // (the first group's sources are resolved while the other copier works)
+                for (uint32_t it = 0; *wflag < wval; it++) {
+                    if (it > (1u << 22)) { waited_out = true; break; }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                waited = true;
+            }
             uint32_t v[CU];
 #pragma unroll
             for (uint32_t u = 0; u < CU; u++)
@@ -722,15 +733,69 @@ __device__ __forceinline__ bool lz4_block(Ctx &C, const Rd &src, uint8_t *dst, u
 #ifdef DT_LZPROF
             if (parse_cycles) parse_cycles[7] += uint32_t(__builtin_amdgcn_s_memtime() - t_parse);
 #endif
-            copy_batch(bs, op, ns, so, slit, ssrc, soff, sml);
+            copy_batch(bs, op, ns, so, slit, ssrc, soff, sml, lzm, lzr, nullptr, 0u);
         }
         return op == out_len;
+    }
+    constexpr uint32_t XS = 5 * 64 + 4;
+    if (THREE) {
+        // Three waves: wave 0 parses batches 2t + 2 and 2t + 3 while wave 1 copies batch 2t and
+        // wave 2 batch 2t + 1; wave 2 resolves its sources at once and waits for wave 1's stores
+        // (a count in LDS) before its loads.  Four slots; flags bit 2: no such batch.  Each copier
+        // has its own start map and ring (lzm, lzr: 256 + ring_n words each).
+        const uint32_t w = threadIdx.x >> 6;
+        volatile uint32_t *done = xb + 4 * XS;
+        auto parse_slot = [&](uint32_t slot) {
+            uint32_t so, slit, ssrc, soff, sml, ns;
+            const uint32_t bs = op;
+            const bool good = parse_batch(so, slit, ssrc, soff, sml, ns);
+            uint32_t *b = xb + slot * XS;
+            b[lane()] = so; b[64 + lane()] = slit; b[128 + lane()] = ssrc; b[192 + lane()] = soff; b[256 + lane()] = sml;
+            const bool last = good && end;
+            if (lane() == 0) {
+                b[320] = bs; b[321] = op; b[322] = ns;
+                b[323] = (last ? 1u : 0u) | ((!good || (last && op != out_len)) ? 2u : 0u);
+            }
+            return good && !last;
+        };
+        auto none_slot = [&](uint32_t slot) { if (lane() == 0) xb[slot * XS + 323] = 4u; };
+        if (w == 0) {
+            if (lane() == 0) { done[0] = 0; done[1] = 0; done[2] = 0; }
+            if (parse_slot(0)) parse_slot(1); else none_slot(1);
+        }
+        __syncthreads();
+        uint4 *mz = reinterpret_cast<uint4 *>(reinterpret_cast<uint32_t *>(lzm) + (w == 2 ? 256u + ring_n : 0u));
+        uint32_t *rz = lzr + (w == 2 ? 256u + ring_n : 0u);
+        for (uint32_t t = 0;; t++) {
+            const uint32_t *c0 = xb + ((2u * t) & 3u) * XS, *c1 = xb + ((2u * t + 1u) & 3u) * XS;
+            const uint32_t f0 = c0[323], f1 = c1[323];
+            if ((f0 | f1) & 2u) return false;
+            const bool fin = (f0 & 1u) || (f1 & 5u);
+            if (w == 0) {
+                if (!fin) {
+                    if (parse_slot((2u * t + 2u) & 3u)) parse_slot((2u * t + 3u) & 3u);
+                    else none_slot((2u * t + 3u) & 3u);
+                }
+            } else if (w == 1) {
+                copy_batch(c0[320], c0[321], c0[322], c0[lane()], c0[64 + lane()], c0[128 + lane()],
+                           c0[192 + lane()], c0[256 + lane()], mz, rz, nullptr, 0u);
+                if (lane() == 0) done[0] = t + 1u;
+            } else if (!(f1 & 4u)) {
+                copy_batch(c1[320], c1[321], c1[322], c1[lane()], c1[64 + lane()], c1[128 + lane()],
+                           c1[192 + lane()], c1[256 + lane()], mz, rz, done, t + 1u);
+            }
+            __syncthreads();
+            if (fin) {
+                done[1 + (w == 2 ? 1u : 0u)] = waited_out ? 1u : 0u;   // (lane writes; read after the barrier)
+                __syncthreads();
+                return !(done[1] | done[2]);
+            }
+        }
     }
     // Two waves (lz4_kernel): wave 0 parses batch k + 1 while wave 1 copies batch k.  A batch passes
     // through one of two slots of xb: the five lane arrays, then bs, the batch's end, its sequence
     // count and flags (bit 0: the block's last batch, bit 1: malformed); both waves read the same
     // flags after each barrier, so they leave together.
-    constexpr uint32_t XS = 5 * 64 + 4;
     const bool parser = threadIdx.x < 64;
     auto parse_into = [&](uint32_t slot) {
         uint32_t so, slit, ssrc, soff, sml, ns;
@@ -754,7 +819,7 @@ __device__ __forceinline__ bool lz4_block(Ctx &C, const Rd &src, uint8_t *dst, u
             if (!(fl & 1u)) parse_into((k + 1u) & 1u);
         } else {
             copy_batch(cur[320], cur[321], cur[322], cur[lane()], cur[64 + lane()], cur[128 + lane()],
-                       cur[192 + lane()], cur[256 + lane()]);
+                       cur[192 + lane()], cur[256 + lane()], lzm, lzr, nullptr, 0u);
         }
         __syncthreads();
         if (fl & 1u) return true;
@@ -2392,8 +2457,13 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
 // reads it (anything unusual leaves the document to decode_kernel, which then reports it), the
 // block decompressed by two waves (lz4_block<true>), the verdict in P.lz_pre.
 constexpr uint32_t LZ_PRE_RING = 1024;
-constexpr size_t LZ_PRE_LDS = (256 + LZ_PRE_RING + 2 * (5 * 64 + 4)) * 4;
-__global__ __launch_bounds__(128) void lz4_kernel(DecodeParams P) {
+// waves per long block: 2 (parse | copy) or 3 (parse | copy even batches | copy odd batches)
+template <int W>
+constexpr size_t lz_pre_lds() {
+    return W == 3 ? (2 * (256 + LZ_PRE_RING) + 4 * (5 * 64 + 4) + 4) * 4 : (256 + LZ_PRE_RING + 2 * (5 * 64 + 4)) * 4;
+}
+template <int DTGPU_LZ_WAVES>
+__global__ __launch_bounds__(64 * DTGPU_LZ_WAVES) void lz4_kernel(DecodeParams P) {
     extern __shared__ uint32_t lds[];
     const uint32_t doc = P.lz_big[blockIdx.x];
     const DecodeDesc D = P.docs[doc];
@@ -2420,8 +2490,16 @@ __global__ __launch_bounds__(128) void lz4_kernel(DecodeParams P) {
         uint64_t ulen;
         if (C.u64v(c, ulen)) break;
         if (ulen > (uint64_t(1) << 34) || ulen > 255ull * c.n + 64 || ulen > D.lz_cap) break;
-        verdict = lz4_block<true>(C, c, C.lz, uint32_t(ulen), reinterpret_cast<uint4 *>(lds), lds + 256,
-                                  LZ_PRE_RING, nullptr, lds + 256 + LZ_PRE_RING) ? 1u : 2u;
+        if (DTGPU_LZ_WAVES == 3) {   // waves 1 and 2 each: start map (256) + ring; then the slots
+            const bool ok = lz4_block<true, true>(C, c, C.lz, uint32_t(ulen), reinterpret_cast<uint4 *>(lds),
+                                                  lds + 256, LZ_PRE_RING, nullptr, lds + 2 * (256 + LZ_PRE_RING));
+            // a copier that gave up waiting leaves the block to decode_kernel (verdict 0)
+            const volatile uint32_t *done = lds + 2 * (256 + LZ_PRE_RING) + 4 * (5 * 64 + 4);
+            verdict = ok ? 1u : (done[1] | done[2]) ? 0u : 2u;
+        } else {
+            verdict = lz4_block<true>(C, c, C.lz, uint32_t(ulen), reinterpret_cast<uint4 *>(lds), lds + 256,
+                                      LZ_PRE_RING, nullptr, lds + 256 + LZ_PRE_RING) ? 1u : 2u;
+        }
     } while (false);
     if (threadIdx.x == 0) P.lz_pre[doc] = verdict;
 }
@@ -3315,7 +3393,14 @@ int launch_decode(const DecodeParams &p, void *stream) {
     const size_t lds = (512 + 8 * size_t(p.max_file_agents) + (p.size_only ? 0u : p.lz_ring)) * 4;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (!p.size_only && p.n_big)
-        hipLaunchKernelGGL(ddec::lz4_kernel, dim3(p.n_big), dim3(128), ddec::LZ_PRE_LDS, s, p);
+    {   // three waves while the long blocks are few enough to have the GPU to themselves (the
+        // mixed batch's 300: node_nodecc 13.6 -> 13.0 ms); a batch of many runs two per block
+        // (2,000 linear documents: 15.0 vs 18.0 ms, git-makefile x 10,000: 48 vs 57 ms)
+        if (p.n_big <= 512)
+            hipLaunchKernelGGL(ddec::lz4_kernel<3>, dim3(p.n_big), dim3(192), ddec::lz_pre_lds<3>(), s, p);
+        else
+            hipLaunchKernelGGL(ddec::lz4_kernel<2>, dim3(p.n_big), dim3(128), ddec::lz_pre_lds<2>(), s, p);
+    }
     if (!p.size_only && p.fill_blocks && hipMemsetAsync(p.fill_n, 0, size_t(p.n_docs) * 4, s) != hipSuccess) return 66;
     if (p.size_only)
         hipLaunchKernelGGL(ddec::decode_kernel<true>, dim3(p.n_docs), dim3(64), lds, s, p);

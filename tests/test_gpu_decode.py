@@ -206,6 +206,19 @@ def test_lz4_shapes_single_wave(monkeypatch):
         _same_arrays(dec, i, d)
 
 
+def test_lz4_many_long_blocks():
+    """More than 512 documents with a long LZ4 block take the two-wave kernel (fewer take three):
+    every copy decodes like the host decoder."""
+    shapes = _lz4_shape_docs()[-3:]
+    docs = [shapes[i % 3] for i in range(540)]
+    dec = dt_amd.DecodeBatch(docs)
+    dec.run()
+    for i, d in enumerate(docs):
+        assert dec.status(i)["status"] == 0, i
+    for i in (0, 1, 2, 271, 539):
+        _same_arrays(dec, i, docs[i])
+
+
 def test_long_documents_uncompressed():
     """Documents past the deferred-fill threshold (131,072 LVs) written without LZ4: fill_kernel
     copies their insert text from the document bytes instead of the LZ4 buffer (and their per-LV
