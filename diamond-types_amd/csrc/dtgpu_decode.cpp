@@ -274,6 +274,8 @@ dtgpu_status dtgpu_decode_create(const uint8_t *const *docs, const size_t *lens,
         std::vector<uint32_t> big;
         for (size_t i = 0; i < n; i++)
             if (!D->desc[i].skip && D->res[i].lz_len >= LZ_BIG) big.push_back(uint32_t(i));
+        // longest blocks first: they are dispatched first, each to a CU of its own
+        std::stable_sort(big.begin(), big.end(), [&](uint32_t a, uint32_t b) { return D->res[a].lz_len > D->res[b].lz_len; });
         CK(D->lz_big.alloc(big.size()));
         CK(hipMemcpyAsync(D->lz_big.p, big.data(), big.size() * 4, hipMemcpyHostToDevice, s));
         CK(D->lz_pre.alloc(n));
