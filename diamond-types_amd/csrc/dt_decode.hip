@@ -1819,7 +1819,8 @@ __device__ __forceinline__ FastOut fast_runs(VQ qav, VQ qtp, VQ runs, uint32_t t
 }
 
 template <bool SIZE>
-__device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDesc &D, DecodeResult &R, const Lds &L) {
+__device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDesc &D, DecodeResult &R, const Lds &L,
+                                          uint32_t doc) {
     Ctx C;
     C.in = P.in + D.in_off;
     C.lz = P.lz + D.lz_off;
@@ -1871,7 +1872,7 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
                 R.lz_len = uint32_t(ulen);
             } else {
                 if (ulen > D.lz_cap) return ErrCapacity;
-                const uint32_t pre = P.lz_pre ? P.lz_pre[blockIdx.x] : 0u;   // lz4_kernel's verdict
+                const uint32_t pre = P.lz_pre ? P.lz_pre[doc] : 0u;   // lz4_kernel's verdict
                 if (pre == 2u) return LZ4DecompressionError;
                 if (pre != 1u) {
 #ifdef DT_LZPROF
@@ -2072,7 +2073,7 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
                                O.cbyte, O.alist, D.arun_cap, D.pre_cap, D.lv_cap, tab, jobs, D.fill_cap);
         if (fo.status == 0 && jobs) {
             fill_jobs = fo.n_jobs;
-            if (lane() == 0) P.fill_n[blockIdx.x] = fill_jobs;   // (bit 31 set with the text copy below)
+            if (lane() == 0) P.fill_n[doc] = fill_jobs;   // (bit 31 set with the text copy below)
         }
         if (fo.status == 0 && tabled) {   // the offsets are bytes already
             fo.ins_size = ins.text.n;
@@ -2377,7 +2378,7 @@ __device__ __forceinline__ int decode_doc(const DecodeParams &P, const DecodeDes
             hdr[65] = ins.text.s;
             hdr[66] = ins.t0;
             hdr[67] = ins_size;
-            P.fill_n[blockIdx.x] = fill_jobs | 0x80000000u;
+            P.fill_n[doc] = fill_jobs | 0x80000000u;
         }
     } else if (ins.present && ins_size) {
         if (ins_size > D.content_cap) return ErrCapacity;
@@ -2564,8 +2565,8 @@ template <bool SIZE>
 #endif
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_DECODE_WAVES))) void decode_kernel(DecodeParams P) {
     extern __shared__ uint32_t lds[];
-    const uint32_t doc = blockIdx.x;
-    if (doc >= P.n_docs) return;
+    if (blockIdx.x >= P.n_docs) return;
+    const uint32_t doc = !SIZE && P.order ? P.order[blockIdx.x] : blockIdx.x;   // longest documents first
     const DecodeDesc D = P.docs[doc];
     Lds L;
     const uint32_t F = P.max_file_agents;
@@ -2592,7 +2593,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_DECODE
     DecodeResult R{};
     int st = S_OK;
     if (D.skip) st = Defer;
-    else st = decode_doc<SIZE>(P, D, R, L);
+    else st = decode_doc<SIZE>(P, D, R, L, doc);
     R.status = uint32_t(st);
     if (lane() == 0) P.results[doc] = R;
 }

@@ -73,6 +73,7 @@ struct DecodeParams {
     uint32_t *fill_n;
     const uint32_t *fill_doc;
     uint32_t fill_blocks, pad3;
+    const uint32_t *order;  // decode_kernel's block -> document (longest first), or null
     uint32_t x2n[32];       // x^(2^k) mod the CRC-32C polynomial (crc32 combine tables)
 };
 

@@ -27,6 +27,7 @@ struct dtgpu_decoded {
     DevBuf<uint32_t> aruns, alist, pre, ops, ent, poff, par, cbyte, agents, ver;
     DevBuf<uint32_t> lz_big, lz_pre;   // documents whose LZ4 block lz4_kernel decompresses, its verdicts
     DevBuf<uint32_t> fill, fill_n, fill_doc;   // deferred per-LV offsets (DecodeParams::fill)
+    DevBuf<uint32_t> order;                    // decode_kernel's dispatch order (DecodeParams::order)
     // dtgpu_decode_add results: the merged oplogs (not re-decodable), each merge's status and the
     // patch's version
     bool merged = false;

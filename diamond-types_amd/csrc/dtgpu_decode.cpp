@@ -260,6 +260,19 @@ dtgpu_status dtgpu_decode_create(const uint8_t *const *docs, const size_t *lens,
     // a long LZ4 block bounds the batch's decode: lz4_kernel decompresses those first, two waves
     // per document (its resolved-source ring included); decode_kernel then needs no ring, whose
     // 4 KB of LDS per wave would cost the small documents occupancy
+    // decode_kernel dispatches the longest documents first (a batch with long ones only: they
+    // bound it, and a late start would add to the tail)
+    P.order = nullptr;
+    if (n > 1 && (max_lz >= 65536 || !fill_doc.empty())) {
+        std::vector<uint32_t> ord(n);
+        for (size_t i = 0; i < n; i++) ord[i] = uint32_t(i);
+        std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) {
+            return uint64_t(D->desc[a].in_len) + D->res[a].lz_len > uint64_t(D->desc[b].in_len) + D->res[b].lz_len;
+        });
+        CK(D->order.alloc(n));
+        CK(hipMemcpyAsync(D->order.p, ord.data(), n * 4, hipMemcpyHostToDevice, s));
+        P.order = D->order.p;
+    }
     P.fill = fill_doc.empty() ? nullptr : D->fill.p;
     P.fill_n = fill_doc.empty() ? nullptr : D->fill_n.p;
     P.fill_doc = fill_doc.empty() ? nullptr : D->fill_doc.p;
