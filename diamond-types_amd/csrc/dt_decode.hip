@@ -3407,10 +3407,9 @@ int launch_decode(const DecodeParams &p, void *stream) {
     const size_t lds = (512 + 8 * size_t(p.max_file_agents) + (p.size_only ? 0u : p.lz_ring)) * 4;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (!p.size_only && p.n_big)
-    {   // three waves while the long blocks are few enough to have the GPU to themselves (the
-        // mixed batch's 300: node_nodecc 13.6 -> 13.0 ms); a batch of many runs two per block
-        // (2,000 linear documents: 15.0 vs 18.0 ms, git-makefile x 10,000: 48 vs 57 ms)
-        if (p.n_big <= 512)
+    {   // three waves while the long blocks are not too many (P.lz3_max; the mixed batch's 300:
+        // node_nodecc 13.6 -> 13.0 ms), two past that (git-makefile x 10,000: 47 vs 56 ms)
+        if (p.n_big <= p.lz3_max)
             hipLaunchKernelGGL(ddec::lz4_kernel<3>, dim3(p.n_big), dim3(192), ddec::lz_pre_lds<3>(), s, p);
         else
             hipLaunchKernelGGL(ddec::lz4_kernel<2>, dim3(p.n_big), dim3(128), ddec::lz_pre_lds<2>(), s, p);

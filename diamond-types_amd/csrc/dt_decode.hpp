@@ -66,7 +66,7 @@ struct DecodeParams {
     // 1 decompressed, 2 malformed (LZ4DecompressionError), 0 left to decode_kernel
     const uint32_t *lz_big;
     uint32_t *lz_pre;
-    uint32_t n_big, pad2;
+    uint32_t n_big, lz3_max;   // lz3_max: three waves per block while n_big <= lz3_max
     // deferred per-LV offsets of long documents: job arena, each document's job count (written by
     // decode_kernel when its fast path succeeds), the document of each fill-grid slot, grid size
     uint32_t *fill;

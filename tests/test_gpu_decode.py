@@ -206,9 +206,11 @@ def test_lz4_shapes_single_wave(monkeypatch):
         _same_arrays(dec, i, d)
 
 
-def test_lz4_many_long_blocks():
-    """More than 512 documents with a long LZ4 block take the two-wave kernel (fewer take three):
-    every copy decodes like the host decoder."""
+@pytest.mark.parametrize("lz3_max", ["4096", "0"])
+def test_lz4_many_long_blocks(monkeypatch, lz3_max):
+    """540 documents with a long LZ4 block, on the three-wave kernel (up to 4,096 blocks) and on
+    the two-wave one (DTGPU_LZ3_MAX=0, as past that): every copy decodes like the host decoder."""
+    monkeypatch.setenv("DTGPU_LZ3_MAX", lz3_max)
     shapes = _lz4_shape_docs()[-3:]
     docs = [shapes[i % 3] for i in range(540)]
     dec = dt_amd.DecodeBatch(docs)
