@@ -2561,7 +2561,8 @@ __global__ __launch_bounds__(64) void fill_kernel(DecodeParams P) {
 
 template <bool SIZE>
 #ifndef DTGPU_DECODE_WAVES
-#define DTGPU_DECODE_WAVES 6   // occupancy target (tuning knob; the register budget follows from it)
+#define DTGPU_DECODE_WAVES 5   // occupancy target (tuning knob; the register budget follows from it):
+                               // 5 (96 VGPRs) beat 6 (80, VGPR spills) once long documents moved work out (r6_w5)
 #endif
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DTGPU_DECODE_WAVES))) void decode_kernel(DecodeParams P) {
     extern __shared__ uint32_t lds[];
